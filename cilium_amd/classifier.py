@@ -1,0 +1,383 @@
+"""Classifier: the batched verdict interface over libciliumgpu.
+
+Mirrors the reference's entry points for the classification path:
+
+* ``PolicyMap``  — pkg/maps/policymap (Allow/AllowKey/Exists/Delete/DeleteKey/
+  DumpToSlice/Flush) + batched ``policy_can_access`` (bpf/lib/policy.h:46-163)
+* ``PreFilter``  — pkg/datapath/prefilter (Insert/Delete/Dump with revisions)
+  + batched XDP ``check_filters`` (bpf/bpf_xdp.c:88-184)
+* ``Classifier.update_http_policy`` / ``http_verdicts`` — Envoy
+  NetworkPolicyMap (onConfigUpdate / Allowed, envoy/cilium_network_policy.h)
+* ``Classifier.update_kafka_policy`` / ``kafka_verdicts`` — pkg/proxy/kafka.go
+  canAccess → pkg/kafka MatchesRule
+
+All verdicts are computed by the HIP kernels; the ``*_host`` calls copy
+inputs to the GPU and back, the ``*_dev`` calls take device pointers
+(torch tensors) and enqueue asynchronously on the handle's stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import ipaddress
+import json
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .policy import PolicyEntry, PolicyKey, PortRuleKafka, htons
+
+L4_TUPLE_DTYPE = np.dtype([("identity", "<u4"), ("dport", "<u2"), ("proto", "u1"), ("flags", "u1"),
+                           ("len", "<u4")])
+POLICY_KEY_DTYPE = np.dtype([("sec_label", "<u4"), ("dport", "<u2"), ("protocol", "u1"), ("egress", "u1")])
+CIDR_DTYPE = np.dtype([("family", "u1"), ("prefixlen", "u1"), ("pad", "u1", (2,)), ("addr", "u1", (16,))])
+KAFKA_REQ_DTYPE = np.dtype([("api_key", "<i2"), ("api_version", "<i2"), ("kind", "u1"), ("n_topics", "u1"),
+                            ("policy", "<u2"), ("remote", "<u4"), ("client_id", "<u4"),
+                            ("topic_ids", "<u4", (N.CG_KAFKA_MAX_TOPICS,))])
+assert L4_TUPLE_DTYPE.itemsize == 12 and KAFKA_REQ_DTYPE.itemsize == 64 and CIDR_DTYPE.itemsize == 20
+
+
+def _p(a):
+    return N.ptr(a)
+
+
+class Classifier:
+    """One engine handle bound to one GPU (``device=-1``: host-only handle that
+    can compile policies and pack requests but refuses every verdict call)."""
+
+    def __init__(self, device: int = 0, debug: bool = False):
+        kv = (N.KV * 1)(N.KV(b"device", str(device).encode()))
+        self.h = N.lib.cg_open(kv, 1, 1 if debug else 0)
+        if not self.h:
+            raise N.CiliumGPUError(N.CG_NO_DEVICE, N.lib.cg_last_error().decode())
+        self.device = device
+
+    def close(self) -> None:
+        if self.h:
+            N.lib.cg_close(self.h)
+            self.h = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self) -> None:
+        N.check(N.lib.cg_sync(self.h))
+
+    # ------------------------------------------------------------- L4 --
+    def policy_map(self, max_entries: int = 0) -> "PolicyMap":
+        return PolicyMap(self, max_entries)
+
+    # ------------------------------------------------------------ LPM --
+    def prefilter(self, dyn4: bool = False, dyn6: bool = False, fix4: bool = True, fix6: bool = True,
+                  max_lpm: int = 0, max_hash: int = 0) -> "PreFilter":
+        return PreFilter(self, dyn4, dyn6, fix4, fix6, max_lpm, max_hash)
+
+    # ----------------------------------------------------------- HTTP --
+    def update_http_policy(self, policies: list[dict] | bytes | str) -> None:
+        """Install NPDS NetworkPolicies (all-or-nothing)."""
+        blob = policies if isinstance(policies, (bytes, str)) else json.dumps(policies, separators=(",", ":"))
+        if isinstance(blob, str):
+            blob = blob.encode()
+        N.check(N.lib.cg_http_policy_update(self.h, blob, len(blob)))
+
+    def http_policy_index(self, name: str) -> int:
+        v = C.c_uint32()
+        rc = N.lib.cg_http_policy_index(self.h, name.encode(), C.byref(v))
+        if rc == N.CG_NOT_FOUND:
+            return 0xFFFFFFFF
+        N.check(rc)
+        return v.value
+
+    def http_policy_stats(self) -> dict:
+        out = (C.c_uint64 * 8)()
+        N.check(N.lib.cg_http_policy_stats(self.h, out, 8))
+        keys = ["programs", "parts", "states", "table_bytes", "fields", "rules", "policies", "remote_slots"]
+        return dict(zip(keys, list(out)))
+
+    def pack_http(self, policy: np.ndarray, ingress: np.ndarray, port: np.ndarray, remote: np.ndarray,
+                  hdr_blob: np.ndarray, hdr_off: np.ndarray):
+        """Pack requests into tile-transposed records (+ overflow arena)."""
+        n = len(policy)
+        policy = np.ascontiguousarray(policy, dtype=np.uint32)
+        ingress = np.ascontiguousarray(ingress, dtype=np.uint8)
+        port = np.ascontiguousarray(port, dtype=np.uint16)
+        remote = np.ascontiguousarray(remote, dtype=np.uint32)
+        hdr_blob = np.ascontiguousarray(hdr_blob, dtype=np.uint8)
+        hdr_off = np.ascontiguousarray(hdr_off, dtype=np.uint64)
+        if len(hdr_blob) == 0:
+            hdr_blob = np.zeros(1, np.uint8)
+        used = C.c_size_t()
+        N.check(N.lib.cg_http_pack(self.h, n, _p(policy), _p(ingress), _p(port), _p(remote), _p(hdr_blob),
+                                   _p(hdr_off), None, None, 0, C.byref(used)))
+        records = np.zeros(N.lib.cg_http_records_bytes(n), np.uint8)
+        arena = np.zeros(max(used.value, 16), np.uint8)
+        N.check(N.lib.cg_http_pack(self.h, n, _p(policy), _p(ingress), _p(port), _p(remote), _p(hdr_blob),
+                                   _p(hdr_off), _p(records), _p(arena), arena.nbytes, C.byref(used)))
+        return records, arena
+
+    def http_verdicts(self, records: np.ndarray, n: int, arena: Optional[np.ndarray] = None) -> np.ndarray:
+        out = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_http_verdicts_host(self.h, _p(records), n, _p(arena), 0 if arena is None else arena.nbytes,
+                                            _p(out)))
+        return out[:n]
+
+    def http_verdicts_dev(self, d_records, n: int, d_arena, d_out, stream=None) -> None:
+        N.check(N.lib.cg_http_verdicts_dev(self.h, _p(d_records), n, _p(d_arena), _p(d_out), stream))
+
+    def http_eval_host_diag(self, records: np.ndarray, n: int, arena: Optional[np.ndarray] = None) -> np.ndarray:
+        """Compiler diagnostics only: walk the compiled tables on the CPU."""
+        out = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_diag_http_eval_host(self.h, _p(records), n, _p(arena),
+                                             0 if arena is None else arena.nbytes, _p(out)))
+        return out[:n]
+
+    # ---------------------------------------------------------- Kafka --
+    def update_kafka_policy(self, redirects: list[dict]) -> None:
+        """Install Kafka redirect rule sets: [{"name", "selectors": [{"identities": [...]|None,
+        "rules": [PortRuleKafka|dict, ...]}]}]."""
+        def conv(r):
+            return r.to_json() if isinstance(r, PortRuleKafka) else r
+        doc = [{"name": rd["name"], "selectors": [
+            {"identities": s.get("identities"), "rules": [conv(r) for r in s.get("rules", [])]}
+            for s in rd.get("selectors", [])]} for rd in redirects]
+        blob = json.dumps(doc).encode()
+        N.check(N.lib.cg_kafka_policy_update(self.h, blob, len(blob)))
+
+    def kafka_redirect_index(self, name: str) -> int:
+        v = C.c_uint32()
+        rc = N.lib.cg_kafka_policy_index(self.h, name.encode(), C.byref(v))
+        if rc == N.CG_NOT_FOUND:
+            return 0xFFFF
+        N.check(rc)
+        return v.value
+
+    def kafka_intern(self, what: str, s: bytes) -> int:
+        v = C.c_uint32()
+        N.check(N.lib.cg_kafka_intern(self.h, 0 if what == "topic" else 1, s, len(s), C.byref(v)))
+        return v.value
+
+    def pack_kafka(self, redirect: Sequence[int], remote: Sequence[int], api_key: Sequence[int],
+                   api_version: Sequence[int], kind: Sequence[int], client_id: Sequence[bytes],
+                   topics: Sequence[Sequence[bytes]]):
+        """Intern strings against the installed snapshot and build 64-byte records."""
+        n = len(redirect)
+        reqs = np.zeros(n, KAFKA_REQ_DTYPE)
+        reqs["policy"] = np.asarray(redirect, np.uint16)
+        reqs["remote"] = np.asarray(remote, np.uint32)
+        reqs["api_key"] = np.asarray(api_key, np.int16)
+        reqs["api_version"] = np.asarray(api_version, np.int16)
+        reqs["kind"] = np.asarray(kind, np.uint8)
+        cache_t: dict = {}
+        cache_c: dict = {}
+        arena: list[int] = []
+        for i in range(n):
+            c = client_id[i]
+            if c not in cache_c:
+                cache_c[c] = self.kafka_intern("client", c)
+            reqs["client_id"][i] = cache_c[c]
+            ts = topics[i]
+            ids = []
+            for t in ts:
+                if t not in cache_t:
+                    cache_t[t] = self.kafka_intern("topic", t)
+                ids.append(cache_t[t])
+            if len(ids) > 255:
+                raise ValueError("more than 255 topics in one request")
+            reqs["n_topics"][i] = len(ids)
+            if len(ids) <= N.CG_KAFKA_MAX_TOPICS:
+                reqs["topic_ids"][i, :len(ids)] = ids
+            else:
+                reqs["topic_ids"][i, 0] = len(arena)
+                arena.extend(ids)
+        return reqs, np.asarray(arena if arena else [0], np.uint32)
+
+    def kafka_verdicts(self, reqs: np.ndarray, arena: Optional[np.ndarray] = None) -> np.ndarray:
+        n = len(reqs)
+        out = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_kafka_verdicts_host(self.h, _p(reqs), n, _p(arena), 0 if arena is None else len(arena),
+                                             _p(out)))
+        return out[:n]
+
+    def kafka_verdicts_dev(self, d_reqs, n: int, d_arena, d_out, stream=None) -> None:
+        N.check(N.lib.cg_kafka_verdicts_dev(self.h, _p(d_reqs), n, _p(d_arena), _p(d_out), stream))
+
+    def kafka_eval_host_diag(self, reqs: np.ndarray, arena: Optional[np.ndarray] = None) -> np.ndarray:
+        n = len(reqs)
+        out = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_diag_kafka_eval_host(self.h, _p(reqs), n, _p(arena), 0 if arena is None else len(arena),
+                                              _p(out)))
+        return out[:n]
+
+    # -------------------------------------------------------- counters --
+    def read_counters(self, what: int, ident: int = 0) -> np.ndarray:
+        n = C.c_size_t()
+        N.check(N.lib.cg_read_counters(self.h, what, ident, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.uint64)
+        N.check(N.lib.cg_read_counters(self.h, what, ident, _p(out), n.value, C.byref(n)))
+        return out[:n.value]
+
+    def counters_device_ptr(self, what: int, ident: int = 0) -> tuple[int, int]:
+        p = C.c_void_p()
+        n = C.c_size_t()
+        N.check(N.lib.cg_counters_device_ptr(self.h, what, ident, C.byref(p), C.byref(n)))
+        return p.value or 0, n.value
+
+    def reset_counters(self) -> None:
+        N.check(N.lib.cg_reset_counters(self.h))
+
+
+class PolicyMap:
+    """pkg/maps/policymap.PolicyMap on the device."""
+
+    def __init__(self, cl: Classifier, max_entries: int = 0):
+        self.cl = cl
+        v = C.c_uint32()
+        N.check(N.lib.cg_policymap_create(cl.h, max_entries, C.byref(v)))
+        self.id = v.value
+
+    @staticmethod
+    def _keys(keys: Iterable[PolicyKey]) -> np.ndarray:
+        ks = list(keys)
+        a = np.zeros(len(ks), POLICY_KEY_DTYPE)
+        for i, k in enumerate(ks):
+            a[i] = (k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection)
+        return a
+
+    def allow_key(self, k: PolicyKey, proxy_port_be: int) -> None:
+        """AllowKey: proxy_port already in network byte order (as PolicyEntry stores it)."""
+        self.allow_keys(self._keys([k]), np.asarray([proxy_port_be], np.uint16))
+
+    def allow(self, identity: int, dport: int, proto: int, direction: int, proxy_port: int) -> None:
+        """Allow (policymap.go:170-176): dport and proxy_port in host byte order."""
+        self.allow_key(PolicyKey(identity, htons(dport), proto, int(direction)), htons(proxy_port))
+
+    def allow_keys(self, keys: np.ndarray, ports_be: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, POLICY_KEY_DTYPE)
+        ports_be = np.ascontiguousarray(ports_be, np.uint16)
+        N.check(N.lib.cg_policymap_allow(self.cl.h, self.id, _p(keys), _p(ports_be), len(keys)))
+
+    def exists(self, identity: int, dport: int, proto: int, direction: int) -> bool:
+        return self.lookup(PolicyKey(identity, htons(dport), proto, int(direction))) is not None
+
+    def lookup(self, k: PolicyKey) -> Optional[PolicyEntry]:
+        key = self._keys([k])
+        e = N.PolicyEntryC()
+        rc = N.lib.cg_policymap_lookup(self.cl.h, self.id, _p(key), C.byref(e))
+        if rc == N.CG_NOT_FOUND:
+            return None
+        N.check(rc)
+        return PolicyEntry(e.proxy_port, e.packets, e.bytes)
+
+    def delete_key(self, k: PolicyKey) -> None:
+        key = self._keys([k])
+        N.check(N.lib.cg_policymap_delete(self.cl.h, self.id, _p(key), 1))
+
+    def delete(self, identity: int, dport: int, proto: int, direction: int) -> None:
+        self.delete_key(PolicyKey(identity, htons(dport), proto, int(direction)))
+
+    def dump_to_slice(self) -> list[tuple[PolicyKey, PolicyEntry]]:
+        n = C.c_size_t()
+        N.check(N.lib.cg_policymap_dump(self.cl.h, self.id, None, None, 0, C.byref(n)))
+        keys = np.zeros(max(n.value, 1), POLICY_KEY_DTYPE)
+        ents = (N.PolicyEntryC * max(n.value, 1))()
+        N.check(N.lib.cg_policymap_dump(self.cl.h, self.id, _p(keys), C.addressof(ents), n.value, C.byref(n)))
+        return [(PolicyKey(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"])),
+                 PolicyEntry(e.proxy_port, e.packets, e.bytes)) for k, e in zip(keys[:n.value], ents[:n.value])]
+
+    def flush(self) -> None:
+        N.check(N.lib.cg_policymap_flush(self.cl.h, self.id))
+
+    def verdicts(self, tuples: np.ndarray) -> np.ndarray:
+        tuples = np.ascontiguousarray(tuples, L4_TUPLE_DTYPE)
+        out = np.zeros(max(len(tuples), 1), np.int32)
+        N.check(N.lib.cg_l4_verdicts_host(self.cl.h, self.id, _p(tuples), len(tuples), _p(out)))
+        return out[:len(tuples)]
+
+    def verdicts_dev(self, d_tuples, n: int, d_out, stream=None) -> None:
+        N.check(N.lib.cg_l4_verdicts_dev(self.cl.h, self.id, _p(d_tuples), n, _p(d_out), stream))
+
+
+def parse_cidr(s: str) -> np.ndarray:
+    """net.ParseCIDR → (family, ones, network) in the cg_cidr layout."""
+    net = ipaddress.ip_network(s, strict=False)
+    a = np.zeros(1, CIDR_DTYPE)
+    a["family"] = 4 if net.version == 4 else 6
+    a["prefixlen"] = net.prefixlen
+    raw = net.network_address.packed
+    a["addr"][0, :len(raw)] = np.frombuffer(raw, np.uint8)
+    return a
+
+
+class PreFilter:
+    """pkg/datapath/prefilter.PreFilter on the device."""
+
+    def __init__(self, cl: Classifier, dyn4=False, dyn6=False, fix4=True, fix6=True, max_lpm=0, max_hash=0):
+        self.cl = cl
+        cfg = (N.CG_PF_DYN4 if dyn4 else 0) | (N.CG_PF_DYN6 if dyn6 else 0) | (N.CG_PF_FIX4 if fix4 else 0) | \
+              (N.CG_PF_FIX6 if fix6 else 0)
+        self.config = cfg
+        v = C.c_uint32()
+        N.check(N.lib.cg_prefilter_create(cl.h, cfg, max_lpm, max_hash, C.byref(v)))
+        self.id = v.value
+
+    @staticmethod
+    def cidrs(strs: Iterable[str]) -> np.ndarray:
+        lst = [parse_cidr(s) for s in strs]
+        return np.concatenate(lst) if lst else np.zeros(0, CIDR_DTYPE)
+
+    def insert(self, revision: int, cidrs) -> int:
+        arr = self.cidrs(cidrs) if not isinstance(cidrs, np.ndarray) else np.ascontiguousarray(cidrs, CIDR_DTYPE)
+        rev = C.c_int64()
+        N.check(N.lib.cg_prefilter_insert(self.cl.h, self.id, revision, _p(arr) if len(arr) else None, len(arr),
+                                          C.byref(rev)))
+        return rev.value
+
+    def delete(self, revision: int, cidrs) -> int:
+        arr = self.cidrs(cidrs) if not isinstance(cidrs, np.ndarray) else np.ascontiguousarray(cidrs, CIDR_DTYPE)
+        rev = C.c_int64()
+        N.check(N.lib.cg_prefilter_delete(self.cl.h, self.id, revision, _p(arr) if len(arr) else None, len(arr),
+                                          C.byref(rev)))
+        return rev.value
+
+    def dump(self) -> tuple[list[str], int]:
+        n = C.c_size_t()
+        rev = C.c_int64()
+        N.check(N.lib.cg_prefilter_dump(self.cl.h, self.id, None, 0, C.byref(n), C.byref(rev)))
+        arr = np.zeros(max(n.value, 1), CIDR_DTYPE)
+        N.check(N.lib.cg_prefilter_dump(self.cl.h, self.id, _p(arr), n.value, C.byref(n), C.byref(rev)))
+        out = []
+        for c in arr[:n.value]:
+            if c["family"] == 4:
+                out.append(str(ipaddress.ip_network((bytes(c["addr"][:4]), int(c["prefixlen"])))))
+            else:
+                out.append(str(ipaddress.ip_network((bytes(c["addr"]), int(c["prefixlen"])))))
+        return out, rev.value
+
+    def set_endpoints(self, v4_be: np.ndarray, v6: np.ndarray) -> None:
+        v4_be = np.ascontiguousarray(v4_be, np.uint32)
+        v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1)
+        N.check(N.lib.cg_prefilter_set_endpoints(self.cl.h, self.id, _p(v4_be) if len(v4_be) else None,
+                                                 len(v4_be), _p(v6) if len(v6) else None, len(v6) // 16))
+
+    def verdicts(self, v4: np.ndarray, v6: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """v4: (n4, 2) uint32 {saddr, daddr} as in the IP header; v6: (n6, 32) uint8."""
+        v4 = np.ascontiguousarray(v4, np.uint32).reshape(-1, 2)
+        v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1, 32)
+        o4 = np.zeros(max(len(v4), 1), np.uint8)
+        o6 = np.zeros(max(len(v6), 1), np.uint8)
+        N.check(N.lib.cg_prefilter_verdicts_host(self.cl.h, self.id, _p(v4), len(v4), _p(o4), _p(v6), len(v6),
+                                                 _p(o6)))
+        return o4[:len(v4)], o6[:len(v6)]
+
+    def verdicts_dev(self, d_v4, n4: int, d_o4, d_v6, n6: int, d_o6, stream=None) -> None:
+        N.check(N.lib.cg_prefilter_verdicts_dev(self.cl.h, self.id, _p(d_v4), n4, _p(d_o4), _p(d_v6), n6, _p(d_o6),
+                                                stream))

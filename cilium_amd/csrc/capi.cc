@@ -1,0 +1,779 @@
+// capi.cc — the extern "C" boundary (include/cilium_gpu.h).  Every entry
+// point catches internal errors and returns a cg_result code.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "engine.h"
+#include "http.h"
+#include "kafka.h"
+#include "kernels.h"
+#include "l4.h"
+#include "lpm.h"
+#include "regex.h"
+
+using namespace cg;
+
+namespace {
+
+std::mutex g_handles_mu;
+std::map<uint64_t, std::shared_ptr<Engine>> g_handles;
+uint64_t g_next_handle = 1;
+
+std::shared_ptr<Engine> get(uint64_t h) {
+  std::lock_guard<std::mutex> lk(g_handles_mu);
+  auto it = g_handles.find(h);
+  if (it == g_handles.end()) fail(CG_INVALID_INSTANCE, "unknown handle");
+  return it->second;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return CG_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("out of host memory");
+    return CG_UNKNOWN_ERROR;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return CG_UNKNOWN_ERROR;
+  } catch (...) {
+    set_error("unknown error");
+    return CG_UNKNOWN_ERROR;
+  }
+}
+
+PolicyMapState& get_map(Engine& e, uint32_t id) {
+  auto it = e.maps.find(id);
+  if (it == e.maps.end()) fail(CG_NOT_FOUND, "unknown policy map id");
+  return *it->second;
+}
+
+PrefilterState& get_pf(Engine& e, uint32_t id) {
+  auto it = e.prefilters.find(id);
+  if (it == e.prefilters.end()) fail(CG_NOT_FOUND, "unknown prefilter id");
+  return *it->second;
+}
+
+void* stream_of(Engine& e, void* s) { return s ? s : e.stream; }
+
+void check_launch(int err, const char* what) { hip_check(err, what); }
+
+struct HostDev {
+  DevMem m;
+  void* put(const void* src, size_t bytes) {
+    m.alloc(bytes);
+    if (bytes) hip_check(hipMemcpy(m.get(), src, bytes, hipMemcpyHostToDevice), "H2D");
+    return m.get();
+  }
+  void* reserve(size_t bytes) {
+    m.alloc(bytes);
+    return m.get();
+  }
+};
+
+CidrKey make_cidr(const cg_cidr& c) {
+  CidrKey k;
+  if (c.family != 4 && c.family != 6) fail(CG_INVALID_ADDRESS, "cidr family must be 4 or 6");
+  int bits = c.family == 4 ? 32 : 128;
+  if (c.prefixlen > bits) fail(CG_INVALID_ADDRESS, "prefix length out of range");
+  k.family = c.family;
+  k.plen = c.prefixlen;
+  k.net.fill(0);
+  int bytes = bits / 8;
+  for (int i = 0; i < bytes; ++i) {
+    int keep = std::max(0, std::min(8, (int)c.prefixlen - 8 * i));
+    uint8_t mask = keep == 0 ? 0 : (uint8_t)(0xFF << (8 - keep));
+    k.net[i] = c.addr[i] & mask;  // net.ParseCIDR returns the masked network
+  }
+  return k;
+}
+
+// selectMap (prefilter.go:108-122)
+int select_map(const CidrKey& k) {
+  if (k.family == 4) return k.plen == 32 ? 1 : 0;
+  return k.plen == 128 ? 3 : 2;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cg_last_error(void) { return get_error().c_str(); }
+
+const char* cg_version(void) { return "libciliumgpu gfx950 r1"; }
+
+uint64_t cg_open(const cg_kv* params, size_t n, uint8_t debug) {
+  uint64_t out = 0;
+  int rc = guarded([&] {
+    auto e = std::make_shared<Engine>();
+    e->debug = debug;
+    int dev = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (params[i].key && params[i].value && strcmp(params[i].key, "device") == 0) dev = atoi(params[i].value);
+    e->device = dev;
+    if (dev >= 0) {
+      int count = 0;
+      if (hipGetDeviceCount(&count) != hipSuccess || dev >= count)
+        fail(CG_NO_DEVICE, "no HIP device " + std::to_string(dev));
+      hipDeviceProp_t prop;
+      hip_check(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+      if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        fail(CG_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950 only");
+      e->cus = prop.multiProcessorCount;
+      hip_check(hipSetDevice(dev), "hipSetDevice");
+      hipStream_t s;
+      hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+      e->stream = s;
+    }
+    std::lock_guard<std::mutex> lk(g_handles_mu);
+    out = g_next_handle++;
+    g_handles[out] = e;
+  });
+  return rc == CG_OK ? out : 0;
+}
+
+void cg_close(uint64_t h) {
+  std::shared_ptr<Engine> e;
+  {
+    std::lock_guard<std::mutex> lk(g_handles_mu);
+    auto it = g_handles.find(h);
+    if (it == g_handles.end()) return;
+    e = it->second;
+    g_handles.erase(it);
+  }
+  if (e->has_gpu()) {
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize((hipStream_t)e->stream);
+    e->maps.clear();
+    e->prefilters.clear();
+    e->http.reset();
+    e->kafka.reset();
+    (void)hipStreamDestroy((hipStream_t)e->stream);
+  }
+}
+
+int cg_sync(uint64_t h) {
+  return guarded([&] {
+    auto e = get(h);
+    if (e->has_gpu()) dev_sync(*e, nullptr);
+  });
+}
+
+// ------------------------------------------------------------------ L4 ----
+int cg_policymap_create(uint64_t h, uint32_t max_entries, uint32_t* map_id) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!map_id) fail(CG_INVALID_ARGUMENT, "map_id is NULL");
+    if (max_entries == 0) max_entries = 16384;  // policymap.go:37 MaxEntries
+    if (max_entries > 65536) fail(CG_INVALID_ARGUMENT, "max_entries > 65536");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto m = std::make_unique<PolicyMapState>();
+    m->max_entries = max_entries;
+    uint32_t id = e->next_id++;
+    e->maps[id] = std::move(m);
+    *map_id = id;
+  });
+}
+
+int cg_policymap_destroy(uint64_t h, uint32_t map_id) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    get_map(*e, map_id);
+    if (e->has_gpu()) dev_sync(*e, nullptr);
+    e->maps.erase(map_id);
+  });
+}
+
+int cg_policymap_allow(uint64_t h, uint32_t map_id, const cg_policy_key* keys, const uint16_t* ports_be,
+                       size_t n) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PolicyMapState& m = get_map(*e, map_id);
+    if (n && (!keys || !ports_be)) fail(CG_INVALID_ARGUMENT, "NULL keys/ports");
+    size_t fresh = 0;
+    std::map<uint64_t, int> seen;
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t k = l4_key(keys[i]);
+      if (k == kL4EmptyKey) fail(CG_INVALID_ARGUMENT, "reserved all-ones policy key");
+      if (!m.entries.count(k) && seen.emplace(k, 1).second) ++fresh;
+    }
+    if (m.entries.size() + fresh > m.max_entries) fail(CG_MAP_FULL, "policy map full (E2BIG)");
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t k = l4_key(keys[i]);
+      auto it = m.entries.find(k);
+      if (it != m.entries.end()) {
+        it->second.proxy_port_be = ports_be[i];
+      } else {
+        uint32_t id;
+        if (!m.free_ids.empty()) {
+          id = m.free_ids.back();
+          m.free_ids.pop_back();
+        } else {
+          id = m.next_id++;
+        }
+        m.zero_counter(*e, id);
+        m.entries[k] = {ports_be[i], id};
+        m.order.push_back(k);
+      }
+    }
+    m.dirty = true;
+  });
+}
+
+int cg_policymap_delete(uint64_t h, uint32_t map_id, const cg_policy_key* keys, size_t n) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PolicyMapState& m = get_map(*e, map_id);
+    for (size_t i = 0; i < n; ++i)
+      if (!m.entries.count(l4_key(keys[i]))) fail(CG_NOT_FOUND, "policy key not found (ENOENT)");
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t k = l4_key(keys[i]);
+      auto it = m.entries.find(k);
+      if (it == m.entries.end()) continue;  // duplicate in the batch
+      m.free_ids.push_back(it->second.id);
+      m.entries.erase(it);
+      m.order.erase(std::find(m.order.begin(), m.order.end(), k));
+    }
+    m.dirty = true;
+  });
+}
+
+int cg_policymap_lookup(uint64_t h, uint32_t map_id, const cg_policy_key* key, cg_policy_entry* entry) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PolicyMapState& m = get_map(*e, map_id);
+    auto it = m.entries.find(l4_key(*key));
+    if (it == m.entries.end()) fail(CG_NOT_FOUND, "policy key not found");
+    if (entry) {
+      memset(entry, 0, sizeof(*entry));
+      entry->proxy_port = it->second.proxy_port_be;
+      if (e->has_gpu()) dev_sync(*e, nullptr);
+      m.read_counters(*e, it->second.id, &entry->packets, &entry->bytes);
+    }
+  });
+}
+
+int cg_policymap_dump(uint64_t h, uint32_t map_id, cg_policy_key* keys, cg_policy_entry* entries, size_t cap,
+                      size_t* n) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PolicyMapState& m = get_map(*e, map_id);
+    if (n) *n = m.order.size();
+    std::vector<uint64_t> ctr;
+    if (e->has_gpu() && m.d_counters.size()) {
+      dev_sync(*e, nullptr);
+      ctr.resize((size_t)m.max_entries * 2);
+      hip_check(hipMemcpy(ctr.data(), m.d_counters.get(), ctr.size() * 8, hipMemcpyDeviceToHost), "D2H counters");
+    }
+    size_t i = 0;
+    for (uint64_t k : m.order) {
+      if (i >= cap) break;
+      if (keys) keys[i] = l4_unkey(k);
+      if (entries) {
+        memset(&entries[i], 0, sizeof(cg_policy_entry));
+        const auto& en = m.entries[k];
+        entries[i].proxy_port = en.proxy_port_be;
+        if (!ctr.empty()) {
+          entries[i].packets = ctr[(size_t)en.id * 2];
+          entries[i].bytes = ctr[(size_t)en.id * 2 + 1];
+        }
+      }
+      ++i;
+    }
+  });
+}
+
+int cg_policymap_flush(uint64_t h, uint32_t map_id) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PolicyMapState& m = get_map(*e, map_id);
+    for (auto& [k, en] : m.entries) m.free_ids.push_back(en.id);
+    m.entries.clear();
+    m.order.clear();
+    m.dirty = true;
+  });
+}
+
+static void l4_run(Engine& e, uint32_t map_id, const cg_l4_tuple* d_t, size_t n, int32_t* d_out, void* s) {
+  e.require_gpu();
+  PolicyMapState* mp;
+  {
+    std::lock_guard<std::mutex> lk(e.mu);
+    mp = &get_map(e, map_id);
+    if (mp->dirty) mp->rebuild(e);
+  }
+  e.set_device();
+  check_launch(launch_l4(mp->dev, d_t, n, d_out, stream_of(e, s), e.cus), "l4 kernel launch");
+}
+
+int cg_l4_verdicts_dev(uint64_t h, uint32_t map_id, const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts,
+                       void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    l4_run(*e, map_id, d_tuples, n, d_verdicts, stream);
+  });
+}
+
+int cg_l4_verdicts_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, size_t n, int32_t* verdicts) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    e->set_device();
+    HostDev in, out;
+    void* din = in.put(tuples, n * sizeof(cg_l4_tuple));
+    void* dout = out.reserve(n * sizeof(int32_t));
+    l4_run(*e, map_id, (const cg_l4_tuple*)din, n, (int32_t*)dout, nullptr);
+    dev_sync(*e, nullptr);
+    if (n) hip_check(hipMemcpy(verdicts, dout, n * sizeof(int32_t), hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
+// ----------------------------------------------------------------- LPM ----
+int cg_prefilter_create(uint64_t h, uint32_t config, uint32_t max_lpm, uint32_t max_hash, uint32_t* pf_id) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!pf_id) fail(CG_INVALID_ARGUMENT, "pf_id is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto p = std::make_unique<PrefilterState>();
+    p->config = config;
+    if (max_lpm) p->max_lpm = max_lpm;
+    if (max_hash) p->max_hash = max_hash;
+    uint32_t id = e->next_id++;
+    e->prefilters[id] = std::move(p);
+    *pf_id = id;
+  });
+}
+
+int cg_prefilter_destroy(uint64_t h, uint32_t pf_id) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    get_pf(*e, pf_id);
+    if (e->has_gpu()) dev_sync(*e, nullptr);
+    e->prefilters.erase(pf_id);
+  });
+}
+
+int cg_prefilter_insert(uint64_t h, uint32_t pf_id, int64_t revision, const cg_cidr* cidrs, size_t n,
+                        int64_t* revision_out) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PrefilterState& p = get_pf(*e, pf_id);
+    if (revision != 0 && p.revision != revision)
+      fail(CG_REVISION_MISMATCH,
+           "Latest revision is " + std::to_string(p.revision) + " not " + std::to_string(revision));
+    std::vector<std::pair<int, CidrKey>> undo;
+    int err = 0;
+    std::string msg;
+    for (size_t i = 0; i < n && !err; ++i) {
+      CidrKey k = make_cidr(cidrs[i]);
+      int which = select_map(k);
+      if (!p.enabled(which)) {
+        err = CG_NO_MAP;
+        msg = "No map enabled for CIDR string";
+        break;
+      }
+      uint32_t cap = (which == 0 || which == 2) ? p.max_lpm : p.max_hash;
+      if (p.maps[which].count(k)) continue;  // BPF_ANY update of an existing key
+      if (p.maps[which].size() >= cap) {
+        err = CG_MAP_FULL;
+        msg = "Error inserting CIDR string: map full";
+        break;
+      }
+      p.maps[which].insert(k);
+      undo.push_back({which, k});
+    }
+    if (err) {
+      for (auto& [w, k] : undo) p.maps[w].erase(k);
+      fail(err, msg);
+    }
+    p.revision++;
+    p.dirty = true;
+    if (revision_out) *revision_out = p.revision;
+  });
+}
+
+int cg_prefilter_delete(uint64_t h, uint32_t pf_id, int64_t revision, const cg_cidr* cidrs, size_t n,
+                        int64_t* revision_out) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PrefilterState& p = get_pf(*e, pf_id);
+    if (revision != 0 && p.revision != revision)
+      fail(CG_REVISION_MISMATCH,
+           "Latest revision is " + std::to_string(p.revision) + " not " + std::to_string(revision));
+    std::vector<CidrKey> ks;
+    for (size_t i = 0; i < n; ++i) {
+      CidrKey k = make_cidr(cidrs[i]);
+      int which = select_map(k);
+      if (!p.enabled(which)) fail(CG_NO_MAP, "No map enabled for CIDR string");
+      if (!p.maps[which].count(k)) fail(CG_NOT_FOUND, "No map entry for CIDR string");
+      ks.push_back(k);
+    }
+    for (auto& k : ks) p.maps[select_map(k)].erase(k);
+    p.revision++;
+    p.dirty = true;
+    if (revision_out) *revision_out = p.revision;
+  });
+}
+
+int cg_prefilter_dump(uint64_t h, uint32_t pf_id, cg_cidr* out, size_t cap, size_t* n, int64_t* revision) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PrefilterState& p = get_pf(*e, pf_id);
+    size_t i = 0, total = 0;
+    for (int w = 0; w < 4; ++w) {  // prefixesV4Dyn .. prefixesV6Fix order (prefilter.go:102)
+      for (const auto& k : p.maps[w]) {
+        if (out && i < cap) {
+          memset(&out[i], 0, sizeof(cg_cidr));
+          out[i].family = k.family;
+          out[i].prefixlen = k.plen;
+          memcpy(out[i].addr, k.net.data(), 16);
+          ++i;
+        }
+        ++total;
+      }
+    }
+    if (n) *n = total;
+    if (revision) *revision = p.revision;
+  });
+}
+
+int cg_prefilter_set_endpoints(uint64_t h, uint32_t pf_id, const uint32_t* v4, size_t n4, const uint8_t* v6,
+                               size_t n6) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PrefilterState& p = get_pf(*e, pf_id);
+    p.ep4.assign(v4, v4 + n4);
+    p.ep6.resize(n6);
+    for (size_t i = 0; i < n6; ++i) memcpy(p.ep6[i].data(), v6 + 16 * i, 16);
+    p.dirty = true;
+  });
+}
+
+static void lpm_run(Engine& e, uint32_t pf_id, const uint32_t* d_v4, size_t n4, uint8_t* d_o4, const uint8_t* d_v6,
+                    size_t n6, uint8_t* d_o6, void* s) {
+  e.require_gpu();
+  PrefilterState* p;
+  {
+    std::lock_guard<std::mutex> lk(e.mu);
+    p = &get_pf(e, pf_id);
+    if (p->dirty) p->rebuild(e);
+  }
+  e.set_device();
+  check_launch(launch_lpm(p->dev, p->v4_filter, p->v6_filter, d_v4, n4, d_o4, d_v6, n6, d_o6, stream_of(e, s), e.cus),
+               "lpm kernel launch");
+}
+
+int cg_prefilter_verdicts_dev(uint64_t h, uint32_t pf_id, const uint32_t* d_v4, size_t n4, uint8_t* d_out4,
+                              const uint8_t* d_v6, size_t n6, uint8_t* d_out6, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    lpm_run(*e, pf_id, d_v4, n4, d_out4, d_v6, n6, d_out6, stream);
+  });
+}
+
+int cg_prefilter_verdicts_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, size_t n4, uint8_t* out4,
+                               const uint8_t* v6, size_t n6, uint8_t* out6) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    e->set_device();
+    HostDev a, b, c, d;
+    void* d4 = a.put(v4, n4 * 8);
+    void* d6 = b.put(v6, n6 * 32);
+    void* o4 = c.reserve(n4 + 1);
+    void* o6 = d.reserve(n6 + 1);
+    lpm_run(*e, pf_id, (const uint32_t*)d4, n4, (uint8_t*)o4, (const uint8_t*)d6, n6, (uint8_t*)o6, nullptr);
+    dev_sync(*e, nullptr);
+    if (n4) hip_check(hipMemcpy(out4, o4, n4, hipMemcpyDeviceToHost), "D2H");
+    if (n6) hip_check(hipMemcpy(out6, o6, n6, hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
+// ---------------------------------------------------------------- HTTP ----
+int cg_http_policy_update(uint64_t h, const char* json, size_t len) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!json) fail(CG_INVALID_ARGUMENT, "NULL policy");
+    std::shared_ptr<HttpSnapshot> snap = http_compile(json, len);
+    if (e->has_gpu()) {
+      e->set_device();
+      snap->upload(*e);
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->http = snap;  // publish
+  });
+}
+
+static std::shared_ptr<HttpSnapshot> http_snap(Engine& e) {
+  std::lock_guard<std::mutex> lk(e.mu);
+  if (!e.http) fail(CG_NOT_FOUND, "no HTTP policy installed");
+  return e.http;
+}
+
+int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = http_snap(*e);
+    auto it = s->policy_index.find(name ? name : "");
+    if (it == s->policy_index.end()) fail(CG_NOT_FOUND, "no policy named " + std::string(name ? name : ""));
+    *index = it->second;
+  });
+}
+
+int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = http_snap(*e);
+    uint64_t v[8] = {s->progs.size(),
+                     s->parts.size(),
+                     s->total_states,
+                     s->trans.size() * 2 + s->acc.size() * 4 + s->masks.size() * 8 + s->clsmap.size(),
+                     s->fields.size(),
+                     s->total_rules,
+                     s->npolicies,
+                     s->rhash_keys.size()};
+    for (size_t i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  });
+}
+
+size_t cg_http_records_bytes(size_t n) {
+  return ((n + CG_HTTP_TILE - 1) / CG_HTTP_TILE) * (size_t)CG_HTTP_TILE * CG_HTTP_UNITS * 16;
+}
+
+int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                 const uint32_t* remote, const uint8_t* hdr_blob, const uint64_t* hdr_off, void* records,
+                 uint8_t* arena, size_t arena_cap, size_t* arena_used) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = http_snap(*e);
+    http_pack(*s, n, policy, ingress, port, remote, hdr_blob, hdr_off, records, arena, arena_cap, arena_used);
+  });
+}
+
+int cg_http_verdicts_dev(uint64_t h, const void* d_records, size_t n, const uint8_t* d_arena, uint8_t* d_out,
+                         void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = http_snap(*e);
+    e->set_device();
+    check_launch(launch_http(s->dev, d_records, n, d_arena, d_out, stream_of(*e, stream), e->cus),
+                 "http kernel launch");
+  });
+}
+
+int cg_http_verdicts_host(uint64_t h, const void* records, size_t n, const uint8_t* arena, size_t arena_len,
+                          uint8_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = http_snap(*e);
+    e->set_device();
+    HostDev r, a, o;
+    void* dr = r.put(records, cg_http_records_bytes(n));
+    void* da = a.put(arena, arena ? arena_len : 0);
+    void* dout = o.reserve(n + 1);
+    check_launch(launch_http(s->dev, dr, n, (const uint8_t*)da, (uint8_t*)dout, e->stream, e->cus),
+                 "http kernel launch");
+    dev_sync(*e, nullptr);
+    if (n) hip_check(hipMemcpy(out, dout, n, hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
+// --------------------------------------------------------------- Kafka ----
+int cg_kafka_policy_update(uint64_t h, const char* json, size_t len) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!json) fail(CG_INVALID_ARGUMENT, "NULL policy");
+    auto snap = kafka_compile(json, len);
+    if (e->has_gpu()) {
+      e->set_device();
+      snap->upload(*e);
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->kafka = snap;
+  });
+}
+
+static std::shared_ptr<KafkaSnapshot> kafka_snap(Engine& e) {
+  std::lock_guard<std::mutex> lk(e.mu);
+  if (!e.kafka) fail(CG_NOT_FOUND, "no Kafka policy installed");
+  return e.kafka;
+}
+
+int cg_kafka_policy_index(uint64_t h, const char* name, uint32_t* index) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = kafka_snap(*e);
+    auto it = s->redirect_index.find(name ? name : "");
+    if (it == s->redirect_index.end()) fail(CG_NOT_FOUND, "no Kafka redirect named " + std::string(name ? name : ""));
+    *index = it->second;
+  });
+}
+
+int cg_kafka_intern(uint64_t h, uint32_t what, const char* str, size_t len, uint32_t* id) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = kafka_snap(*e);
+    const auto& m = what == 0 ? s->topic_ids : s->client_ids;
+    auto it = m.find(std::string(str ? str : "", len));
+    *id = it == m.end() ? CG_KAFKA_UNKNOWN_STR : it->second;
+  });
+}
+
+int cg_kafka_verdicts_dev(uint64_t h, const cg_kafka_request* d_reqs, size_t n, const uint32_t* d_arena,
+                          uint8_t* d_out, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = kafka_snap(*e);
+    e->set_device();
+    check_launch(launch_kafka(s->dev, d_reqs, n, d_arena, d_out, stream_of(*e, stream), e->cus),
+                 "kafka kernel launch");
+  });
+}
+
+int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n, const uint32_t* arena,
+                           size_t arena_len, uint8_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = kafka_snap(*e);
+    e->set_device();
+    HostDev r, a, o;
+    void* dr = r.put(reqs, n * sizeof(cg_kafka_request));
+    void* da = a.put(arena, arena ? arena_len * 4 : 0);
+    void* dout = o.reserve(n + 1);
+    check_launch(launch_kafka(s->dev, dr, n, (const uint32_t*)da, (uint8_t*)dout, e->stream, e->cus),
+                 "kafka kernel launch");
+    dev_sync(*e, nullptr);
+    if (n) hip_check(hipMemcpy(out, dout, n, hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
+// ------------------------------------------------------------ counters ----
+static void counters_loc(Engine& e, uint32_t what, uint32_t id, void** p, size_t* n) {
+  *p = nullptr;
+  *n = 0;
+  if (what == 0) {
+    auto s = http_snap(e);
+    *p = s->d_counters.get();
+    *n = s->progs.size() * 2;
+  } else if (what == 1) {
+    auto s = kafka_snap(e);
+    *p = s->d_counters.get();
+    *n = s->dflt_group.size() * 2;
+  } else if (what == 2) {
+    std::lock_guard<std::mutex> lk(e.mu);
+    PrefilterState& pf = get_pf(e, id);
+    *p = pf.d_counters.get();
+    *n = pf.d_counters.get() ? 2 : 0;
+  } else {
+    fail(CG_INVALID_ARGUMENT, "unknown counter set");
+  }
+}
+
+int cg_read_counters(uint64_t h, uint32_t what, uint32_t id, uint64_t* out, size_t cap, size_t* n) {
+  return guarded([&] {
+    auto e = get(h);
+    void* p;
+    size_t cnt;
+    counters_loc(*e, what, id, &p, &cnt);
+    if (n) *n = cnt;
+    size_t k = std::min(cap, cnt);
+    if (k && p && e->has_gpu()) {
+      dev_sync(*e, nullptr);
+      hip_check(hipMemcpy(out, p, k * 8, hipMemcpyDeviceToHost), "D2H counters");
+    } else if (k) {
+      memset(out, 0, k * 8);
+    }
+  });
+}
+
+int cg_counters_device_ptr(uint64_t h, uint32_t what, uint32_t id, void** d_ptr, size_t* n) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    counters_loc(*e, what, id, d_ptr, n);
+  });
+}
+
+int cg_counters_copy_dev(uint64_t h, uint32_t what, uint32_t id, void* d_dst, size_t n, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    void* p;
+    size_t cnt;
+    counters_loc(*e, what, id, &p, &cnt);
+    size_t k = std::min(n, cnt);
+    e->set_device();
+    if (k)
+      hip_check(hipMemcpyAsync(d_dst, p, k * 8, hipMemcpyDeviceToDevice, (hipStream_t)stream_of(*e, stream)),
+                "D2D counters");
+  });
+}
+
+int cg_reset_counters(uint64_t h) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!e->has_gpu()) return;
+    dev_sync(*e, nullptr);
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->http) e->http->d_counters.zero();
+    if (e->kafka) e->kafka->d_counters.zero();
+    for (auto& [id, p] : e->prefilters) p->d_counters.zero();
+    for (auto& [id, m] : e->maps) m->d_counters.zero();
+  });
+}
+
+// ------------------------------------------------------- diagnostics ----
+// Host-side walkers of the compiled tables and the regex compiler, for the
+// CPU test-suite only.  No verdict entry point calls them.
+int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t len, uint32_t search,
+                        uint8_t* result) {
+  return guarded([&] {
+    ByteDfa d = compile_regex(std::string(re, re_len), ByteSet::all(), search ? MatchMode::Search : MatchMode::Full);
+    *result = dfa_run(d, std::string((const char*)s, len)) ? 1 : 0;
+  });
+}
+
+int cg_diag_http_eval_host(uint64_t h, const void* records, size_t n, const uint8_t* arena, size_t arena_len,
+                           uint8_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = http_snap(*e);
+    for (size_t i = 0; i < n; ++i) out[i] = http_eval_host(*s, (const uint8_t*)records, i, arena, arena_len);
+  });
+}
+
+int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n, const uint32_t* arena,
+                            size_t arena_len, uint8_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = kafka_snap(*e);
+    for (size_t i = 0; i < n; ++i) out[i] = kafka_eval_host(*s, reqs[i], arena, arena_len);
+  });
+}
+
+}  // extern "C"

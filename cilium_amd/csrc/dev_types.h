@@ -1,0 +1,173 @@
+// dev_types.h — table layouts shared by the host builders (.cc) and the HIP
+// kernels (kernels.hip).  Plain structs passed to kernels by value.
+#pragma once
+
+#include <cstdint>
+
+#if defined(__HIP__) || defined(__HIPCC__)
+#define CG_HD __host__ __device__
+#else
+#define CG_HD
+#endif
+
+namespace cg {
+
+// ------------------------------------------------------------------ L4 ----
+// Cuckoo hash of policy keys (2 choices × 64-B buckets of 4 slots).
+// slot = {u64 key, u32 val, u32 pad}; key = sec_label | dport<<32 | proto<<48 |
+// egress_byte<<56 (the 8-byte struct policy_key read little-endian);
+// val = entry id (bits 0..15) | proxy_port_be (bits 16..31).
+// Empty slot: key == kL4EmptyKey (an all-ones key, rejected on insert).
+constexpr uint64_t kL4EmptyKey = ~0ULL;
+struct L4Slot {
+  uint64_t key;
+  uint32_t val;
+  uint32_t pad;
+};
+struct L4Dev {
+  const L4Slot* slots;   // nbuckets * 4
+  uint32_t bucket_mask;  // nbuckets - 1
+  uint32_t max_entries;  // counter ids < max_entries
+  unsigned long long* counters;  // [id*2] packets, [id*2+1] bytes
+};
+
+CG_HD inline uint64_t l4_hash1(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+CG_HD inline uint64_t l4_hash2(uint64_t k) {
+  k += 0x9e3779b97f4a7c15ULL;
+  k ^= k >> 30;
+  k *= 0xbf58476d1ce4e5b9ULL;
+  k ^= k >> 27;
+  k *= 0x94d049bb133111ebULL;
+  k ^= k >> 31;
+  return k;
+}
+
+// ----------------------------------------------------------------- LPM ----
+// IPv4: DIR-24-8.  dir24[a >> 8]: 0 = not covered, 1 = covered,
+// v >= 2 → leaf v-2: 256-bit bitmap (4 × u64) over the last octet.
+// IPv6: disjoint covered intervals [lo, hi] sorted by lo (hi/lo as two u64,
+// big-endian word order), indexed by the top 16 address bits:
+// v6_idx[t] = first interval whose hi >= t<<112, v6_idx[65536] = count.
+// Local endpoints (cilium_lxc): open addressing, linear probing.
+struct LpmDev {
+  const uint32_t* dir24;     // 1<<24 entries (nullptr: no v4 filter)
+  const uint64_t* leaves;    // 4 u64 per leaf
+  const uint32_t* v6_idx;    // 65537 entries (nullptr: no v6 filter)
+  const uint64_t* v6_lo;     // 2 u64 per interval (hi word, lo word)
+  const uint64_t* v6_hi;
+  const uint32_t* ep4_keys;  // v4 endpoint table (cap4 entries)
+  const uint8_t* ep4_occ;
+  uint32_t ep4_mask;
+  const uint64_t* ep6_keys;  // 2 u64 per entry
+  const uint8_t* ep6_occ;
+  uint32_t ep6_mask;
+  unsigned long long* counters;  // [0] drop, [1] pass
+};
+
+CG_HD inline uint32_t ep_hash32(uint32_t a) {
+  uint64_t k = a * 0x9e3779b97f4a7c15ULL;
+  return (uint32_t)(k >> 32) ^ (uint32_t)k;
+}
+CG_HD inline uint32_t ep_hash128(uint64_t hi, uint64_t lo) {
+  uint64_t k = l4_hash1(hi ^ l4_hash2(lo));
+  return (uint32_t)(k >> 32) ^ (uint32_t)k;
+}
+
+// ---------------------------------------------------------------- HTTP ----
+// Program = one (policy, direction, port) evaluation: Envoy's exact-port
+// PortNetworkPolicyRules merged with the port-0 ones (cilium_network_policy.h:169-192).
+constexpr uint32_t kProgAllowAll = 1;  // some scope has no HTTP rules / no rules
+constexpr uint32_t kNoAcc = 0xFFFFFFFFu;
+struct HttpProg {
+  uint32_t part_begin;
+  uint32_t part_count;
+  uint32_t flags;
+  uint32_t mask_words;      // W
+  uint32_t always_off;      // u64 word offset of the "no HTTP rules" PNPR mask
+  uint32_t default_remote;  // u64 word offset of the mask for unlisted remotes
+  uint32_t pad0, pad1;
+};
+struct HttpPart {
+  uint32_t trans_off;  // u16 entries
+  uint32_t ncls;
+  uint32_t cls_off;    // bytes into clsmap (256 per part)
+  uint32_t acc_off;    // u32 entries: per state, word offset of accept mask or kNoAcc
+  uint32_t nstates;
+  uint32_t pad0, pad1, pad2;
+};
+// Special program ids in the program lookup.
+constexpr uint32_t kProgAllow = 0xFFFFFFFEu;  // no policy for the port → allow
+constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
+struct HttpDev {
+  const HttpProg* progs;
+  const HttpPart* parts;
+  const uint8_t* clsmap;
+  const uint16_t* trans;
+  const uint32_t* acc;
+  const unsigned long long* masks;
+  // program lookup: key = policy<<17 | ingress<<16 | port
+  const uint32_t* phash_keys;  // empty = 0xFFFFFFFF
+  const uint32_t* phash_vals;
+  uint32_t phash_mask;
+  const uint32_t* dflt;        // [policy*2 + ingress] → program id or kProg*
+  uint32_t npolicies;
+  // remote lookup: key = prog<<32 | remote → u64 word offset of the mask
+  const unsigned long long* rhash_keys;  // empty = ~0
+  const uint32_t* rhash_vals;
+  uint32_t rhash_mask;
+  uint32_t nprogs;
+  uint32_t nparts;
+  uint32_t cls_lds_bytes;  // bytes of clsmap staged in LDS (0 = read global)
+  unsigned long long* counters;  // [prog*2] allowed, [prog*2+1] denied
+};
+
+CG_HD inline uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+CG_HD inline uint32_t hash64to32(uint64_t k) {
+  k = l4_hash1(k);
+  return (uint32_t)k;
+}
+
+// --------------------------------------------------------------- Kafka ----
+// Per (redirect, identity group): compiled rule sets; see kafka.cc.
+struct KafkaRuleDev {
+  unsigned long long keys;  // bit k: apiKey k allowed (k < 64)
+  uint32_t flags;           // bit0: apiKey wildcard, bit1: version wildcard, bit2: has clientID
+  int32_t version;
+  uint32_t client_id;
+  uint32_t pad;
+};
+constexpr uint32_t kKfKeyWild = 1, kKfVerWild = 2, kKfHasClient = 4;
+struct KafkaGroupDev {
+  uint32_t wild_off, wild_cnt;    // topic-less rules (KafkaRuleDev index range)
+  uint32_t tr_off, tr_cnt;        // topic rules, sorted by topic id
+  uint32_t any_rules;             // 1 if the group has any Kafka rule (else deny)
+  uint32_t pad0, pad1, pad2;
+};
+struct KafkaDev {
+  const KafkaRuleDev* rules;
+  const uint32_t* topic_of;       // topic id per rule in the tr range (sorted)
+  const KafkaGroupDev* groups;
+  // (redirect, identity) → group: key = redirect<<32 | identity
+  const unsigned long long* ghash_keys;
+  const uint32_t* ghash_vals;
+  uint32_t ghash_mask;
+  const uint32_t* dflt_group;     // per redirect: group for unlisted identities
+  uint32_t nredirects;
+  unsigned long long* counters;   // [redirect*2] allowed, [+1] denied
+};
+
+}  // namespace cg

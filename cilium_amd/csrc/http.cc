@@ -1,0 +1,800 @@
+// http.cc — compile Envoy cilium.NetworkPolicy (NPDS) HTTP rules into
+// per-program union DFAs, pack requests, and a host walker for diagnostics.
+//
+// Reference semantics restated (envoy/cilium_network_policy.h):
+//   PolicyInstance::Allowed(ingress, port, remote, headers)          :198-203
+//   PortNetworkPolicy::Matches — exact port, then port 0, else allow  :169-192
+//     (only TCP port policies are installed, :157-165; duplicate port
+//      → EnvoyException rejects the update, :160-162)
+//   PortNetworkPolicyRules::Matches — no HTTP rules → allow; empty → allow;
+//     else OR over rules                                             :128-146
+//   PortNetworkPolicyRule::Matches — remote set (empty = all), then OR over
+//     HTTP rules (none = allow)                                      :90-108
+//   HttpNetworkPolicyRule::Matches — AND over header matchers        :68-71
+//
+// Compilation: the header fields referenced by any matcher form a fixed
+// field order F (":method", ":path", ":authority", then other names sorted).
+// A request becomes the string  v_1 SEP v_2 SEP ... v_F SEP  with SEP = 0x00
+// and an absent header encoded as the single byte 0x01 (neither byte can
+// occur in a header value Envoy's codec accepts).  Each HTTP rule becomes a
+// layered DFA (one deterministic automaton per field, chained by SEP); all
+// rules of a program are unioned by subset construction over (rule, state)
+// pairs, accepting states labelled with the set of PortNetworkPolicyRules
+// (PNPRs) whose HTTP rule matched.  The kernel walks the string once and
+// ANDs that label with the remote-identity mask.
+#include "http.h"
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <set>
+#include <unordered_map>
+
+#include "clsdfa.h"
+#include "json.h"
+#include "regex.h"
+
+namespace cg {
+
+namespace {
+
+constexpr uint8_t kSep = 0x00;
+constexpr uint8_t kAbsent = 0x01;
+constexpr int kMaxUnionStates = 400000;  // before minimization, per part
+constexpr int kMaxPartStates = 65535;    // u16 transition entries
+
+enum class MKind { Exact, Regex, Present };
+struct MatcherSpec {
+  std::string name;  // lowercase
+  MKind kind;
+  std::string value;
+};
+struct PnprSpec {
+  bool has_remotes = false;
+  std::vector<uint64_t> remotes;
+  bool has_http = false;
+  std::vector<std::vector<MatcherSpec>> http;  // each: AND of matchers
+};
+struct ScopeSpec {
+  std::vector<PnprSpec> rules;
+};
+struct PolicySpec {
+  std::string name;
+  std::map<uint32_t, ScopeSpec> dir[2];  // [0] egress, [1] ingress
+};
+
+std::string lower(const std::string& s) {
+  std::string o = s;
+  for (auto& c : o)
+    if (c >= 'A' && c <= 'Z') c = c - 'A' + 'a';
+  return o;
+}
+
+MatcherSpec parse_matcher(const Json& h) {
+  if (h.type != Json::OBJ) fail(CG_POLICY_REJECTED, "header matcher must be an object");
+  MatcherSpec m;
+  const Json* name = h.get("name");
+  if (!name) fail(CG_POLICY_REJECTED, "header matcher without name");
+  m.name = lower(name->as_str("name"));
+  const Json* ex = h.get("exact_match");
+  const Json* rx = h.get("regex_match");
+  const Json* pr = h.get("present_match");
+  const Json* val = h.get("value");
+  const Json* inv = h.get("invert_match");
+  if (inv && inv->type == Json::BOOL && inv->b) fail(CG_UNSUPPORTED, "invert_match");
+  for (const char* k : {"range_match", "prefix_match", "suffix_match"})
+    if (h.get(k)) fail(CG_UNSUPPORTED, std::string("header matcher ") + k);
+  if (ex) {
+    m.kind = MKind::Exact;
+    m.value = ex->as_str("exact_match");
+  } else if (rx) {
+    m.kind = MKind::Regex;
+    m.value = rx->as_str("regex_match");
+  } else if (pr) {
+    m.kind = MKind::Present;
+  } else if (val) {
+    // deprecated {value, regex} form: empty value = presence check
+    m.value = val->as_str("value");
+    const Json* isre = h.get("regex");
+    bool re = false;
+    if (isre) {
+      if (isre->type == Json::BOOL) re = isre->b;
+      else if (isre->type == Json::OBJ && isre->get("value")) re = isre->get("value")->b;
+    }
+    m.kind = m.value.empty() ? MKind::Present : (re ? MKind::Regex : MKind::Exact);
+  } else {
+    m.kind = MKind::Present;
+  }
+  return m;
+}
+
+std::vector<PolicySpec> parse_npds(const char* json, size_t len) {
+  Json root = JsonParser(json, len).parse();
+  const Json* list = &root;
+  if (root.type == Json::OBJ) {
+    list = root.get("resources");
+    if (!list) fail(CG_POLICY_REJECTED, "expected a list of NetworkPolicy or {resources: [...]}");
+  }
+  if (list->type != Json::ARR) fail(CG_POLICY_REJECTED, "expected a list of NetworkPolicy");
+  std::vector<PolicySpec> out;
+  std::set<std::string> names;
+  for (const Json& p : list->arr) {
+    if (p.type != Json::OBJ) fail(CG_POLICY_REJECTED, "NetworkPolicy must be an object");
+    PolicySpec ps;
+    const Json* nm = p.get("name");
+    if (!nm) fail(CG_POLICY_REJECTED, "NetworkPolicy without name");
+    ps.name = nm->as_str("name");
+    if (!names.insert(ps.name).second) fail(CG_POLICY_REJECTED, "duplicate NetworkPolicy name " + ps.name);
+    for (int d = 0; d < 2; ++d) {
+      const Json* ports = p.get(d ? "ingress_per_port_policies" : "egress_per_port_policies");
+      if (!ports) continue;
+      if (ports->type != Json::ARR) fail(CG_POLICY_REJECTED, "per_port_policies must be a list");
+      for (const Json& pp : ports->arr) {
+        uint32_t port = 0;
+        if (const Json* j = pp.get("port")) port = (uint32_t)j->as_u64("port");
+        bool tcp = true;
+        if (const Json* j = pp.get("protocol")) {
+          if (j->type == Json::STR) tcp = j->s == "TCP";
+          else tcp = j->as_u64("protocol") == 0;
+        }
+        if (!tcp) continue;  // "NOT installing non-TCP policy" (cilium_network_policy.h:163-165)
+        ScopeSpec sc;
+        if (const Json* rules = pp.get("rules")) {
+          if (rules->type != Json::ARR) fail(CG_POLICY_REJECTED, "rules must be a list");
+          for (const Json& r : rules->arr) {
+            PnprSpec pr;
+            if (const Json* rp = r.get("remote_policies")) {
+              if (rp->type != Json::ARR) fail(CG_POLICY_REJECTED, "remote_policies must be a list");
+              for (const Json& id : rp->arr) pr.remotes.push_back(id.as_u64("remote_policies"));
+              pr.has_remotes = !pr.remotes.empty();
+            }
+            if (const Json* hr = r.get("http_rules")) {
+              if (hr->type != Json::NUL) {
+                pr.has_http = true;
+                if (const Json* lst = hr->get("http_rules")) {
+                  if (lst->type != Json::ARR) fail(CG_POLICY_REJECTED, "http_rules must be a list");
+                  for (const Json& rule : lst->arr) {
+                    std::vector<MatcherSpec> ms;
+                    if (const Json* hs = rule.get("headers")) {
+                      if (hs->type != Json::ARR) fail(CG_POLICY_REJECTED, "headers must be a list");
+                      for (const Json& h : hs->arr) ms.push_back(parse_matcher(h));
+                    }
+                    pr.http.push_back(std::move(ms));
+                  }
+                }
+              }
+            }
+            sc.rules.push_back(std::move(pr));
+          }
+        }
+        if (!ps.dir[d].emplace(port, std::move(sc)).second)
+          fail(CG_POLICY_REJECTED, "PortNetworkPolicy: Duplicate port number");
+      }
+    }
+    out.push_back(std::move(ps));
+  }
+  return out;
+}
+
+// Field-value alphabet: any byte except SEP and the absent marker.
+ByteSet value_alphabet() {
+  ByteSet s = ByteSet::all();
+  s.w[0] &= ~3ULL;
+  return s;
+}
+
+// One deterministic automaton per (field, conjunction of matchers).
+struct FieldDfaCache {
+  std::vector<ByteDfa> dfas;
+  std::map<std::string, int> by_key;
+  int any_id = -1;
+
+  int add(ByteDfa d, const std::string& key) {
+    auto it = by_key.find(key);
+    if (it != by_key.end()) return it->second;
+    dfas.push_back(std::move(d));
+    by_key[key] = (int)dfas.size() - 1;
+    return (int)dfas.size() - 1;
+  }
+  int any() {
+    if (any_id < 0) {
+      ByteSet a = ByteSet::all();
+      a.w[0] &= ~1ULL;  // everything but SEP (the absent marker included)
+      any_id = add(dfa_star(a), "ANY");
+    }
+    return any_id;
+  }
+  int single(const MatcherSpec& m) {
+    std::string key = std::string(1, "ERP"[(int)m.kind]) + ":" + m.value;
+    auto it = by_key.find(key);
+    if (it != by_key.end()) return it->second;
+    ByteSet va = value_alphabet();
+    ByteDfa d;
+    switch (m.kind) {
+      case MKind::Exact: d = dfa_literal(m.value, va); break;
+      case MKind::Regex: d = compile_regex(m.value, va, MatchMode::Full); break;
+      case MKind::Present: d = dfa_star(va); break;
+    }
+    return add(std::move(d), key);
+  }
+  int conj(const std::vector<const MatcherSpec*>& ms) {
+    if (ms.empty()) return any();
+    std::vector<int> ids;
+    for (auto* m : ms) ids.push_back(single(*m));
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    if (ids.size() == 1) return ids[0];
+    std::string key = "AND";
+    for (int i : ids) key += ":" + std::to_string(i);
+    auto it = by_key.find(key);
+    if (it != by_key.end()) return it->second;
+    ByteDfa d = dfas[ids[0]];
+    for (size_t i = 1; i < ids.size(); ++i) d = dfa_intersect(d, dfas[ids[i]]);
+    return add(std::move(d), key);
+  }
+  bool empty_lang(int id) const {
+    const ByteDfa& d = dfas[id];
+    if (d.accept[d.start]) return false;
+    for (int b = 0; b < 256; ++b)
+      if (d.next(d.start, b)) return false;
+    return true;
+  }
+};
+
+struct URule {
+  std::vector<int> fd;            // field dfa per field
+  std::vector<uint32_t> tags;     // PNPR indices
+};
+
+struct VecHash64 {
+  size_t operator()(const std::vector<uint64_t>& v) const {
+    uint64_t h = 0x243f6a8885a308d3ULL ^ v.size();
+    for (uint64_t x : v) h = mix64(h ^ x);
+    return (size_t)h;
+  }
+};
+
+struct TooBig {};
+
+// Layered union construction over `rules` (indices into all_rules).
+ClsDfa build_union(const FieldDfaCache& fc, const std::vector<URule>& all_rules,
+                   const std::vector<int>& rules, int F, uint32_t W,
+                   std::vector<std::vector<uint64_t>>& label_masks) {
+  // global byte classes: SEP alone, refined by every field DFA's columns
+  std::vector<int> cls(256, 1);
+  cls[kSep] = 0;
+  {
+    std::set<int> used;
+    for (int r : rules)
+      for (int id : all_rules[r].fd) used.insert(id);
+    for (int id : used) {
+      const ByteDfa& d = fc.dfas[id];
+      // column signature per byte
+      std::map<std::vector<int32_t>, int> colid;
+      std::vector<int> dc(256);
+      std::vector<int32_t> col(d.size());
+      for (int b = 0; b < 256; ++b) {
+        for (int s = 0; s < d.size(); ++s) col[s] = d.trans[(size_t)s * 256 + b];
+        dc[b] = colid.emplace(col, (int)colid.size()).first->second;
+      }
+      std::map<std::pair<int, int>, int> nid;
+      for (int b = 0; b < 256; ++b) cls[b] = nid.emplace(std::make_pair(cls[b], dc[b]), (int)nid.size()).first->second;
+    }
+  }
+  int ncls = 0;
+  for (int b = 0; b < 256; ++b) ncls = std::max(ncls, cls[b] + 1);
+  std::vector<int> rep(ncls, -1);
+  for (int b = 0; b < 256; ++b)
+    if (rep[cls[b]] < 0) rep[cls[b]] = b;
+
+  ClsDfa d;
+  d.ncls = ncls;
+  for (int b = 0; b < 256; ++b) d.clsmap[b] = (uint8_t)cls[b];
+  std::unordered_map<std::vector<uint64_t>, int, VecHash64> ids;
+  std::vector<std::vector<uint64_t>> states;  // [0] = layer, then rule<<32|q
+  std::map<std::vector<uint64_t>, uint32_t> mask_ids;
+  label_masks.clear();
+
+  auto label_of = [&](const std::vector<uint64_t>& st) -> uint32_t {
+    if ((int)st[0] != F) return 0;
+    std::vector<uint64_t> m(W, 0);
+    for (size_t i = 1; i < st.size(); ++i)
+      for (uint32_t t : all_rules[(size_t)(st[i] >> 32)].tags) m[t >> 6] |= 1ULL << (t & 63);
+    auto it = mask_ids.emplace(m, (uint32_t)mask_ids.size() + 1);
+    if (it.second) label_masks.push_back(m);
+    return it.first->second;
+  };
+  auto intern = [&](std::vector<uint64_t>&& st) -> int {
+    if (st.size() == 1) return 0;  // no live rule
+    auto it = ids.find(st);
+    if (it != ids.end()) return it->second;
+    int id = (int)states.size();
+    if (id >= kMaxUnionStates) throw TooBig{};
+    ids.emplace(st, id);
+    d.label.push_back(label_of(st));
+    states.push_back(std::move(st));
+    d.trans.resize((size_t)(id + 1) * ncls, 0);
+    return id;
+  };
+  // dead
+  states.push_back({(uint64_t)-1});
+  d.label.push_back(0);
+  d.trans.assign(ncls, 0);
+  // start
+  {
+    std::vector<uint64_t> st{0};
+    for (int r : rules) {
+      if (F == 0) {
+        st.push_back((uint64_t)r << 32 | 1);
+      } else {
+        st.push_back((uint64_t)r << 32 | (uint32_t)fc.dfas[all_rules[r].fd[0]].start);
+      }
+    }
+    if (F == 0) st[0] = 0;  // layer 0 == F
+    if (st.size() == 1) {
+      // no rules: start is a copy of dead
+      states.push_back({(uint64_t)-2});
+      d.label.push_back(0);
+      d.trans.resize(2 * ncls, 0);
+    } else {
+      int id = (int)states.size();
+      ids.emplace(st, id);
+      d.label.push_back(label_of(st));
+      states.push_back(st);
+      d.trans.resize((size_t)(id + 1) * ncls, 0);
+    }
+  }
+  std::vector<uint64_t> nx;
+  for (size_t si = 1; si < states.size(); ++si) {
+    if (states[si][0] == (uint64_t)-2) break;
+    const int f = (int)states[si][0];
+    for (int c = 0; c < ncls; ++c) {
+      int b = rep[c];
+      int target = 0;
+      if (f < F) {
+        const std::vector<uint64_t>& cur = states[si];
+        nx.clear();
+        if (b == kSep) {
+          nx.push_back((uint64_t)(f + 1));
+          for (size_t i = 1; i < cur.size(); ++i) {
+            uint32_t r = (uint32_t)(cur[i] >> 32), q = (uint32_t)cur[i];
+            const ByteDfa& fd = fc.dfas[all_rules[r].fd[f]];
+            if (!fd.accept[q]) continue;
+            uint32_t nq = (f + 1 < F) ? (uint32_t)fc.dfas[all_rules[r].fd[f + 1]].start : 1u;
+            nx.push_back((uint64_t)r << 32 | nq);
+          }
+        } else {
+          nx.push_back((uint64_t)f);
+          for (size_t i = 1; i < cur.size(); ++i) {
+            uint32_t r = (uint32_t)(cur[i] >> 32), q = (uint32_t)cur[i];
+            int nq = fc.dfas[all_rules[r].fd[f]].next((int)q, b);
+            if (nq) nx.push_back((uint64_t)r << 32 | (uint32_t)nq);
+          }
+        }
+        target = intern(std::vector<uint64_t>(nx));
+      }
+      d.trans[si * ncls + c] = target;
+    }
+  }
+  return d;
+}
+
+struct PartOut {
+  ClsDfa dfa;
+  std::vector<std::vector<uint64_t>> label_masks;
+};
+
+void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, std::vector<int> rules,
+                 int F, uint32_t W, std::vector<PartOut>& out) {
+  if (rules.empty()) return;
+  PartOut p;
+  bool ok = true;
+  try {
+    ClsDfa raw = build_union(fc, all_rules, rules, F, W, p.label_masks);
+    p.dfa = minimize_cls(raw);
+    if (p.dfa.size() > kMaxPartStates) ok = false;
+  } catch (const TooBig&) {
+    ok = false;
+  }
+  if (ok) {
+    out.push_back(std::move(p));
+    return;
+  }
+  if (rules.size() == 1) fail(CG_UNSUPPORTED, "a single HTTP rule exceeds the DFA state budget");
+  std::vector<int> a(rules.begin(), rules.begin() + rules.size() / 2);
+  std::vector<int> b(rules.begin() + rules.size() / 2, rules.end());
+  build_parts(fc, all_rules, a, F, W, out);
+  build_parts(fc, all_rules, b, F, W, out);
+}
+
+}  // namespace
+
+std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
+  std::vector<PolicySpec> pols = parse_npds(json, len);
+  auto snap = std::make_shared<HttpSnapshot>();
+  HttpSnapshot& S = *snap;
+  if (pols.size() >= 0x7FFF) fail(CG_POLICY_REJECTED, "too many policies");
+
+  // ---- field order
+  std::set<std::string> names;
+  for (const auto& p : pols)
+    for (int d = 0; d < 2; ++d)
+      for (const auto& [port, sc] : p.dir[d])
+        for (const auto& pr : sc.rules)
+          for (const auto& hr : pr.http)
+            for (const auto& m : hr) names.insert(m.name);
+  for (const char* pseudo : {":method", ":path", ":authority"})
+    if (names.count(pseudo)) {
+      S.fields.push_back(pseudo);
+      names.erase(pseudo);
+    }
+  for (const auto& n : names) S.fields.push_back(n);
+  const int F = (int)S.fields.size();
+  std::map<std::string, int> field_idx;
+  for (int i = 0; i < F; ++i) field_idx[S.fields[i]] = i;
+
+  FieldDfaCache fc;
+  S.npolicies = (uint32_t)pols.size();
+  S.dflt.assign((size_t)S.npolicies * 2, kProgAllow);
+  std::vector<std::pair<uint32_t, uint32_t>> phash;  // key → prog
+  std::vector<std::pair<uint64_t, uint32_t>> rhash;  // (prog<<32|remote) → mask word off
+
+  auto add_mask = [&](const std::vector<uint64_t>& m) -> uint32_t {
+    uint32_t off = (uint32_t)S.masks.size();
+    S.masks.insert(S.masks.end(), m.begin(), m.end());
+    return off;
+  };
+
+  // Build one program from the merged PNPR list; returns program id.
+  auto build_prog = [&](const std::vector<const ScopeSpec*>& scopes, uint32_t key) -> uint32_t {
+    HttpProg pg{};
+    uint32_t pid = (uint32_t)S.progs.size();
+    bool allow_all = false;
+    std::vector<const PnprSpec*> pnprs;
+    for (const ScopeSpec* sc : scopes) {
+      bool have_http = false;
+      for (const auto& r : sc->rules) have_http |= r.has_http;
+      if (!have_http || sc->rules.empty()) allow_all = true;  // :129-138
+      for (const auto& r : sc->rules) pnprs.push_back(&r);
+    }
+    if (allow_all) {
+      pg.flags = kProgAllowAll;
+      S.progs.push_back(pg);
+      S.prog_key.push_back(key);
+      return pid;
+    }
+    const uint32_t R = (uint32_t)pnprs.size();
+    const uint32_t W = (R + 63) / 64;
+    pg.mask_words = W;
+    // always: PNPRs with no HTTP rules match any payload (:98-107)
+    std::vector<uint64_t> always(W, 0), open(W, 0);
+    std::map<uint32_t, std::vector<uint64_t>> by_remote;
+    for (uint32_t j = 0; j < R; ++j) {
+      if (pnprs[j]->http.empty()) always[j >> 6] |= 1ULL << (j & 63);
+      if (!pnprs[j]->has_remotes) open[j >> 6] |= 1ULL << (j & 63);
+    }
+    for (uint32_t j = 0; j < R; ++j) {
+      if (!pnprs[j]->has_remotes) continue;
+      for (uint64_t rid : pnprs[j]->remotes) {
+        if (rid > 0xFFFFFFFFULL) continue;  // can never equal a u32 identity
+        auto it = by_remote.find((uint32_t)rid);
+        if (it == by_remote.end()) it = by_remote.emplace((uint32_t)rid, open).first;
+        it->second[j >> 6] |= 1ULL << (j & 63);
+      }
+    }
+    pg.always_off = add_mask(always);
+    pg.default_remote = add_mask(open);
+    for (auto& [rid, m] : by_remote) rhash.push_back({((uint64_t)pid << 32) | rid, add_mask(m)});
+    // union rules
+    std::vector<URule> urules;
+    std::map<std::vector<int>, size_t> dedupe;
+    for (uint32_t j = 0; j < R; ++j) {
+      for (const auto& hr : pnprs[j]->http) {
+        std::vector<std::vector<const MatcherSpec*>> per_field(F);
+        for (const auto& m : hr) per_field[field_idx[m.name]].push_back(&m);
+        std::vector<int> fd(F);
+        bool empty = false;
+        for (int f = 0; f < F; ++f) {
+          fd[f] = fc.conj(per_field[f]);
+          if (fc.empty_lang(fd[f])) empty = true;
+        }
+        if (empty) continue;
+        auto it = dedupe.find(fd);
+        if (it == dedupe.end()) {
+          dedupe[fd] = urules.size();
+          urules.push_back({fd, {j}});
+        } else {
+          urules[it->second].tags.push_back(j);
+        }
+      }
+    }
+    S.total_rules += urules.size();
+    std::vector<int> idx(urules.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
+    std::vector<PartOut> parts;
+    build_parts(fc, urules, idx, F, W, parts);
+    pg.part_begin = (uint32_t)S.parts.size();
+    pg.part_count = (uint32_t)parts.size();
+    for (auto& po : parts) {
+      HttpPart hp{};
+      const ClsDfa& d = po.dfa;
+      hp.ncls = (uint32_t)d.ncls;
+      hp.nstates = (uint32_t)d.size();
+      hp.cls_off = (uint32_t)S.clsmap.size();
+      S.clsmap.insert(S.clsmap.end(), d.clsmap, d.clsmap + 256);
+      hp.trans_off = (uint32_t)S.trans.size();
+      for (int32_t t : d.trans) S.trans.push_back((uint16_t)t);
+      hp.acc_off = (uint32_t)S.acc.size();
+      std::vector<uint32_t> lab_off(po.label_masks.size());
+      for (size_t l = 0; l < po.label_masks.size(); ++l) lab_off[l] = add_mask(po.label_masks[l]);
+      for (int s = 0; s < d.size(); ++s) S.acc.push_back(d.label[s] ? lab_off[d.label[s] - 1] : kNoAcc);
+      S.total_states += d.size();
+      S.parts.push_back(hp);
+    }
+    S.progs.push_back(pg);
+    S.prog_key.push_back(key);
+    return pid;
+  };
+
+  for (uint32_t pi = 0; pi < pols.size(); ++pi) {
+    const PolicySpec& p = pols[pi];
+    S.policy_index[p.name] = pi;
+    for (int d = 0; d < 2; ++d) {
+      const auto& ports = p.dir[d];
+      const ScopeSpec* wild = nullptr;
+      auto w = ports.find(0);
+      if (w != ports.end()) wild = &w->second;
+      if (wild) S.dflt[pi * 2 + d] = build_prog({wild}, (pi << 17) | ((uint32_t)d << 16));
+      for (const auto& [port, sc] : ports) {
+        if (port == 0) continue;
+        if (port > 0xFFFF) continue;  // can never equal a 16-bit destination port
+        std::vector<const ScopeSpec*> scs{&sc};
+        if (wild) scs.push_back(wild);
+        uint32_t key = (pi << 17) | ((uint32_t)d << 16) | port;
+        phash.push_back({key, build_prog(scs, key)});
+      }
+    }
+  }
+
+  // ---- hash tables
+  {
+    uint32_t cap = next_pow2(std::max<size_t>(2 * phash.size(), 16));
+    S.phash_keys.assign(cap, 0xFFFFFFFFu);
+    S.phash_vals.assign(cap, 0);
+    S.phash_mask = cap - 1;
+    for (auto [k, v] : phash) {
+      uint32_t h = hash32(k) & S.phash_mask;
+      while (S.phash_keys[h] != 0xFFFFFFFFu) h = (h + 1) & S.phash_mask;
+      S.phash_keys[h] = k;
+      S.phash_vals[h] = v;
+    }
+  }
+  {
+    uint32_t cap = next_pow2(std::max<size_t>(2 * rhash.size(), 16));
+    S.rhash_keys.assign(cap, ~0ULL);
+    S.rhash_vals.assign(cap, 0);
+    S.rhash_mask = cap - 1;
+    for (auto [k, v] : rhash) {
+      uint32_t h = hash64to32(k) & S.rhash_mask;
+      while (S.rhash_keys[h] != ~0ULL) h = (h + 1) & S.rhash_mask;
+      S.rhash_keys[h] = k;
+      S.rhash_vals[h] = v;
+    }
+  }
+  if (S.masks.empty()) S.masks.push_back(0);
+  if (S.trans.empty()) S.trans.push_back(0);
+  if (S.acc.empty()) S.acc.push_back(kNoAcc);
+  if (S.clsmap.empty()) S.clsmap.assign(256, 0);
+  if (S.progs.empty()) S.progs.push_back(HttpProg{});
+  if (S.parts.empty()) S.parts.push_back(HttpPart{});
+  if (S.dflt.empty()) S.dflt.push_back(kProgDeny);
+  return snap;
+}
+
+uint32_t HttpSnapshot::lookup_prog(uint32_t policy, bool ingress, uint32_t port) const {
+  if (policy >= npolicies) return kProgDeny;
+  uint32_t key = (policy << 17) | ((uint32_t)ingress << 16) | (port & 0xFFFF);
+  uint32_t h = hash32(key) & phash_mask;
+  while (phash_keys[h] != 0xFFFFFFFFu) {
+    if (phash_keys[h] == key) return phash_vals[h];
+    h = (h + 1) & phash_mask;
+  }
+  return dflt[policy * 2 + (ingress ? 1 : 0)];
+}
+
+// ------------------------------------------------------------- packing ----
+namespace {
+
+inline uint8_t* unit_ptr(void* records, size_t i, int u) {
+  size_t tile = i / CG_HTTP_TILE, lane = i % CG_HTTP_TILE;
+  return (uint8_t*)records + tile * (CG_HTTP_UNITS * CG_HTTP_TILE * 16) + (size_t)u * CG_HTTP_TILE * 16 +
+         lane * 16;
+}
+
+bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
+  if (an != lower_b.size()) return false;
+  for (size_t i = 0; i < an; ++i) {
+    uint8_t c = a[i];
+    if (c >= 'A' && c <= 'Z') c = c - 'A' + 'a';
+    if (c != (uint8_t)lower_b[i]) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const uint8_t* ingress,
+               const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
+               const uint64_t* hdr_off, void* records, uint8_t* arena, size_t arena_cap,
+               size_t* arena_used) {
+  const size_t F = s.fields.size();
+  size_t used = 0;
+  std::vector<const uint8_t*> vp(F);
+  std::vector<size_t> vl(F);
+  std::string str;
+  size_t ntiles = (n + CG_HTTP_TILE - 1) / CG_HTTP_TILE;
+  // pad lanes of the last tile
+  for (size_t i = n; records && i < ntiles * CG_HTTP_TILE; ++i) {
+    uint8_t* m = unit_ptr(records, i, 0);
+    memset(m, 0, 16);
+    m[15] = CG_HTTP_F_PAD;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    std::fill(vp.begin(), vp.end(), nullptr);
+    const uint8_t* p = hdr_blob + hdr_off[i];
+    const uint8_t* e = hdr_blob + hdr_off[i + 1];
+    while (p < e) {
+      const uint8_t* nm = p;
+      while (p < e && *p) ++p;
+      size_t nl = p - nm;
+      if (p < e) ++p;
+      const uint8_t* v = p;
+      while (p < e && *p) ++p;
+      size_t vlen = p - v;
+      if (p < e) ++p;
+      for (size_t f = 0; f < F; ++f)
+        if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
+          vp[f] = v;
+          vl[f] = vlen;
+        }
+    }
+    str.clear();
+    bool malformed = false;
+    for (size_t f = 0; f < F; ++f) {
+      if (!vp[f]) {
+        str.push_back((char)kAbsent);
+      } else {
+        for (size_t k = 0; k < vl[f]; ++k) {
+          if (vp[f][k] == kAbsent || vp[f][k] == kSep) malformed = true;
+          str.push_back((char)vp[f][k]);
+        }
+      }
+      str.push_back((char)kSep);
+    }
+    // meta: [0..3] remote, [4..5] port, [6..7] policy (0xFFFF unknown),
+    // [8..11] string length, [12..14] arena offset / 16, [15] flags
+    uint8_t meta[16] = {0};
+    memcpy(meta, &remote[i], 4);
+    memcpy(meta + 4, &port[i], 2);
+    uint16_t pol16 = policy[i] >= s.npolicies ? 0xFFFF : (uint16_t)policy[i];
+    memcpy(meta + 6, &pol16, 2);
+    uint8_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0;
+    if (malformed) flags |= CG_HTTP_F_MALFORMED;
+    uint32_t len = (uint32_t)str.size();
+    memcpy(meta + 8, &len, 4);
+    uint8_t slot[CG_HTTP_SLOT_BYTES] = {0};
+    if (len <= CG_HTTP_SLOT_BYTES) {
+      memcpy(slot, str.data(), len);
+    } else {
+      flags |= CG_HTTP_F_OVERFLOW;
+      if (used / 16 >= (1u << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
+      uint32_t off16 = (uint32_t)(used / 16);
+      if (arena && used + len <= arena_cap) memcpy(arena + used, str.data(), len);
+      used += (len + 15) & ~(size_t)15;
+      meta[12] = off16 & 0xFF;
+      meta[13] = (off16 >> 8) & 0xFF;
+      meta[14] = (off16 >> 16) & 0xFF;
+    }
+    meta[15] = flags;
+    if (records) {
+      memcpy(unit_ptr(records, i, 0), meta, 16);
+      for (int u = 0; u < 8; ++u) memcpy(unit_ptr(records, i, u + 1), slot + u * 16, 16);
+    }
+  }
+  if (arena_used) *arena_used = used;
+  if (arena && used > arena_cap) fail(CG_INVALID_ARGUMENT, "overflow arena too small");
+}
+
+uint8_t http_eval_host(const HttpSnapshot& s, const uint8_t* records, size_t i, const uint8_t* arena,
+                       size_t arena_len) {
+  uint8_t meta[16];
+  memcpy(meta, unit_ptr((void*)records, i, 0), 16);
+  uint32_t remote, len;
+  uint16_t port, pol;
+  memcpy(&remote, meta, 4);
+  memcpy(&port, meta + 4, 2);
+  memcpy(&pol, meta + 6, 2);
+  memcpy(&len, meta + 8, 4);
+  uint32_t off = ((uint32_t)meta[12] | ((uint32_t)meta[13] << 8) | ((uint32_t)meta[14] << 16)) * 16u;
+  uint8_t flags = meta[15];
+  if (flags & CG_HTTP_F_PAD) return 0;
+  if (flags & CG_HTTP_F_MALFORMED) return 0;
+  uint32_t prog = pol == 0xFFFF ? kProgDeny : s.lookup_prog(pol, flags & CG_HTTP_F_INGRESS, port);
+  if (prog == kProgDeny) return 0;
+  if (prog == kProgAllow) return 1;
+  const HttpProg& pg = s.progs[prog];
+  if (pg.flags & kProgAllowAll) return 1;
+  std::string str;
+  if (flags & CG_HTTP_F_OVERFLOW) {
+    if ((size_t)off + len > arena_len) return 0;
+    str.assign((const char*)arena + off, len);
+  } else {
+    uint8_t slot[128];
+    for (int u = 0; u < 8; ++u) memcpy(slot + u * 16, unit_ptr((void*)records, i, u + 1), 16);
+    str.assign((const char*)slot, std::min<uint32_t>(len, 128));
+  }
+  // remote mask
+  uint32_t roff = pg.default_remote;
+  uint64_t key = ((uint64_t)prog << 32) | remote;
+  uint32_t h = hash64to32(key) & s.rhash_mask;
+  while (s.rhash_keys[h] != ~0ULL) {
+    if (s.rhash_keys[h] == key) {
+      roff = s.rhash_vals[h];
+      break;
+    }
+    h = (h + 1) & s.rhash_mask;
+  }
+  for (uint32_t w = 0; w < pg.mask_words; ++w)
+    if (s.masks[pg.always_off + w] & s.masks[roff + w]) return 1;
+  for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
+    const HttpPart& pt = s.parts[pg.part_begin + pi];
+    uint32_t st = 1;
+    for (unsigned char c : str) {
+      st = s.trans[pt.trans_off + st * pt.ncls + s.clsmap[pt.cls_off + c]];
+      if (!st) break;
+    }
+    uint32_t a = s.acc[pt.acc_off + st];
+    if (a == kNoAcc) continue;
+    for (uint32_t w = 0; w < pg.mask_words; ++w)
+      if (s.masks[a + w] & s.masks[roff + w]) return 1;
+  }
+  return 0;
+}
+
+void HttpSnapshot::upload(Engine& e) {
+  if (!e.has_gpu()) return;
+  d_progs.upload_vec(progs);
+  d_parts.upload_vec(parts);
+  d_clsmap.upload_vec(clsmap);
+  d_trans.upload_vec(trans);
+  d_acc.upload_vec(acc);
+  d_masks.upload_vec(masks);
+  d_phk.upload_vec(phash_keys);
+  d_phv.upload_vec(phash_vals);
+  d_dflt.upload_vec(dflt);
+  d_rhk.upload_vec(rhash_keys);
+  d_rhv.upload_vec(rhash_vals);
+  d_counters.alloc(std::max<size_t>(progs.size(), 1) * 2 * sizeof(uint64_t));
+  d_counters.zero();
+  dev.progs = d_progs.as<HttpProg>();
+  dev.parts = d_parts.as<HttpPart>();
+  dev.clsmap = d_clsmap.as<uint8_t>();
+  dev.trans = d_trans.as<uint16_t>();
+  dev.acc = d_acc.as<uint32_t>();
+  dev.masks = d_masks.as<unsigned long long>();
+  dev.phash_keys = d_phk.as<uint32_t>();
+  dev.phash_vals = d_phv.as<uint32_t>();
+  dev.phash_mask = phash_mask;
+  dev.dflt = d_dflt.as<uint32_t>();
+  dev.npolicies = npolicies;
+  dev.rhash_keys = d_rhk.as<unsigned long long>();
+  dev.rhash_vals = d_rhv.as<uint32_t>();
+  dev.rhash_mask = rhash_mask;
+  dev.nprogs = (uint32_t)progs.size();
+  dev.nparts = (uint32_t)parts.size();
+  dev.cls_lds_bytes = clsmap.size() <= 32768 ? (uint32_t)clsmap.size() : 0;
+  dev.counters = d_counters.as<unsigned long long>();
+}
+
+}  // namespace cg

@@ -1,0 +1,58 @@
+// http.h — HTTP L7 policy snapshot: NPDS JSON → programs of union DFAs.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dev_types.h"
+#include "engine.h"
+
+namespace cg {
+
+struct HttpSnapshot {
+  std::vector<std::string> fields;  // walked fields, canonical order, lowercase
+  std::map<std::string, uint32_t> policy_index;
+  uint32_t npolicies = 0;
+
+  std::vector<HttpProg> progs;
+  std::vector<HttpPart> parts;
+  std::vector<uint8_t> clsmap;
+  std::vector<uint16_t> trans;
+  std::vector<uint32_t> acc;
+  std::vector<uint64_t> masks;
+  std::vector<uint32_t> phash_keys, phash_vals;
+  uint32_t phash_mask = 0;
+  std::vector<uint32_t> dflt;
+  std::vector<uint64_t> rhash_keys;
+  std::vector<uint32_t> rhash_vals;
+  uint32_t rhash_mask = 0;
+  // (policy, ingress, port) of each program, for counter attribution
+  std::vector<uint32_t> prog_key;
+
+  uint64_t total_states = 0;
+  uint64_t total_rules = 0;
+
+  DevMem d_progs, d_parts, d_clsmap, d_trans, d_acc, d_masks, d_phk, d_phv, d_dflt, d_rhk, d_rhv,
+      d_counters;
+  HttpDev dev{};
+
+  void upload(Engine& e);
+  uint32_t lookup_prog(uint32_t policy, bool ingress, uint32_t port) const;
+};
+
+std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len);
+
+// Pack requests into tile-transposed records (see include/cilium_gpu.h).
+void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const uint8_t* ingress,
+               const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
+               const uint64_t* hdr_off, void* records, uint8_t* arena, size_t arena_cap,
+               size_t* arena_used);
+
+// Walk the snapshot's tables on the host exactly as the kernel does
+// (diagnostics / compiler tests only; the verdict API never calls this).
+uint8_t http_eval_host(const HttpSnapshot& s, const uint8_t* records, size_t i, const uint8_t* arena,
+                       size_t arena_len);
+
+}  // namespace cg

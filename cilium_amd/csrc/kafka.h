@@ -1,0 +1,35 @@
+// kafka.h — Kafka L7 policy snapshot (per-redirect L7DataMap rule sets).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "dev_types.h"
+#include "engine.h"
+
+namespace cg {
+
+struct KafkaSnapshot {
+  std::map<std::string, uint32_t> redirect_index;
+  std::unordered_map<std::string, uint32_t> topic_ids, client_ids;
+  std::vector<KafkaRuleDev> rules;
+  std::vector<uint32_t> topic_of;
+  std::vector<KafkaGroupDev> groups;
+  std::vector<uint64_t> ghash_keys;
+  std::vector<uint32_t> ghash_vals;
+  uint32_t ghash_mask = 0;
+  std::vector<uint32_t> dflt_group;
+
+  DevMem d_rules, d_topic_of, d_groups, d_ghk, d_ghv, d_dflt, d_counters;
+  KafkaDev dev{};
+  void upload(Engine& e);
+};
+
+std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len);
+uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& r, const uint32_t* arena,
+                        size_t arena_len);
+
+}  // namespace cg

@@ -1,0 +1,21 @@
+// kernels.h — host-callable launchers of the gfx950 kernels (kernels.hip).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "dev_types.h"
+
+namespace cg {
+
+// All launchers enqueue on `stream` (hipStream_t) and return the hipError_t
+// of the launch.  n == 0 launches nothing.
+int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus);
+int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* v4, size_t n4,
+               uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus);
+int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
+                void* stream, int cus);
+int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
+                 void* stream, int cus);
+
+}  // namespace cg

@@ -1,0 +1,520 @@
+// kernels.hip — gfx950 verdict kernels.
+//
+// All four kernels are byte/integer work bound by HBM streaming plus table
+// probes (no MFMA): one lane per item, 64-lane wavefronts, vector loads of the
+// packed input, counters privatized in LDS and flushed once per block.
+#include <hip/hip_runtime.h>
+
+#include "../../include/cilium_gpu.h"
+#include "dev_types.h"
+#include "kernels.h"
+
+namespace cg {
+
+namespace {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// =============================================================== L4 ======
+// __policy_can_access (bpf/lib/policy.h:46-110) per tuple.
+
+__device__ __forceinline__ bool l4_probe_bucket(const L4Slot* slots, uint32_t b, uint64_t key,
+                                                uint32_t* val, uint32_t* slot_out) {
+  const uint4* p = reinterpret_cast<const uint4*>(slots + (size_t)b * 4);
+  bool hit = false;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint4 v = p[s];
+    uint64_t k = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    if (k == key) {
+      hit = true;
+      *val = v.z;
+    }
+  }
+  return hit;
+}
+
+__device__ __forceinline__ bool l4_lookup(const L4Dev& t, uint64_t key, uint32_t* val) {
+  uint32_t dummy;
+  if (l4_probe_bucket(t.slots, (uint32_t)l4_hash1(key) & t.bucket_mask, key, val, &dummy)) return true;
+  return l4_probe_bucket(t.slots, (uint32_t)l4_hash2(key) & t.bucket_mask, key, val, &dummy);
+}
+
+template <bool kLdsCounters>
+__global__ __launch_bounds__(1024) void l4_kernel(L4Dev t, const uint32_t* __restrict__ tuples, size_t n,
+                                                  int32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* lpk = lds;
+  uint32_t* lby = lds + t.max_entries;
+  if (kLdsCounters) {
+    for (uint32_t i = threadIdx.x; i < 2 * t.max_entries; i += blockDim.x) lds[i] = 0;
+    __syncthreads();
+  }
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t per_chunk = (size_t)65536;  // tuples per thread-block between flushes ≤ 64K
+  size_t done_in_chunk = 0;
+  for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+    size_t i = base + threadIdx.x;
+    if (i < n) {
+      const uint32_t w0 = tuples[i * 3 + 0];
+      const uint32_t w1 = tuples[i * 3 + 1];
+      const uint32_t len = tuples[i * 3 + 2];
+      const uint32_t identity = w0;
+      const uint32_t dport = w1 & 0xFFFF;
+      const uint32_t proto = (w1 >> 16) & 0xFF;
+      const uint32_t flags = w1 >> 24;
+      const bool frag = flags & CG_L4_F_FRAGMENT;
+      // key.egress = !dir with dir = CT_INGRESS(1) / CT_EGRESS(0)
+      const uint64_t eg = (flags & CG_L4_F_INGRESS) ? 0ULL : 1ULL;
+      uint32_t val = 0;
+      int32_t verdict;
+      int which = 0;  // 1: L4 hit, 2: L3 hit, 3: wildcard-identity L4 hit
+      if (!frag && l4_lookup(t, (uint64_t)identity | ((uint64_t)dport << 32) | ((uint64_t)proto << 48) | (eg << 56), &val))
+        which = 1;
+      else if (l4_lookup(t, (uint64_t)identity | (eg << 56), &val))
+        which = 2;
+      else if (!frag && l4_lookup(t, ((uint64_t)dport << 32) | ((uint64_t)proto << 48) | (eg << 56), &val))
+        which = 3;
+      if (which == 1 || which == 3) {
+        verdict = (int32_t)(val >> 16);  // return policy->proxy_port (be16 as stored)
+      } else if (which == 2) {
+        verdict = 0;  // TC_ACT_OK: the L3 entry's proxy_port is ignored
+      } else if (flags & CG_L4_F_CB_POLICY) {
+        verdict = 0;
+      } else {
+        verdict = frag ? CG_DROP_FRAG_NOSUPPORT : CG_DROP_POLICY;
+      }
+      out[i] = verdict;
+      if (which) {
+        const uint32_t id = val & 0xFFFF;
+        if (kLdsCounters) {
+          atomicAdd(&lpk[id], 1u);
+          if (len < 65536u)
+            atomicAdd(&lby[id], len);
+          else
+            atomicAdd(&t.counters[2 * id + 1], (unsigned long long)len);
+        } else {
+          atomicAdd(&t.counters[2 * id], 1ULL);
+          atomicAdd(&t.counters[2 * id + 1], (unsigned long long)len);
+        }
+      }
+    }
+    if (kLdsCounters) {
+      if (++done_in_chunk == per_chunk / 1024 || base + stride >= n) {
+        done_in_chunk = 0;
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < t.max_entries; e += blockDim.x) {
+          uint32_t p = lpk[e], b = lby[e];
+          if (p) {
+            atomicAdd(&t.counters[2 * e], (unsigned long long)p);
+            lpk[e] = 0;
+          }
+          if (b) {
+            atomicAdd(&t.counters[2 * e + 1], (unsigned long long)b);
+            lby[e] = 0;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// ============================================================== LPM ======
+// check_v4 / check_v6 (bpf/bpf_xdp.c:97-156).
+
+__device__ __forceinline__ bool ep4_has(const LpmDev& t, uint32_t a) {
+  uint32_t h = ep_hash32(a) & t.ep4_mask;
+  for (uint32_t probe = 0; probe <= t.ep4_mask; ++probe) {
+    if (!t.ep4_occ[h]) return false;
+    if (t.ep4_keys[h] == a) return true;
+    h = (h + 1) & t.ep4_mask;
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool ep6_has(const LpmDev& t, uint64_t hi, uint64_t lo) {
+  uint32_t h = ep_hash128(hi, lo) & t.ep6_mask;
+  for (uint32_t probe = 0; probe <= t.ep6_mask; ++probe) {
+    if (!t.ep6_occ[h]) return false;
+    if (t.ep6_keys[2 * h] == hi && t.ep6_keys[2 * h + 1] == lo) return true;
+    h = (h + 1) & t.ep6_mask;
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool v4_covered(const LpmDev& t, uint32_t a /* host order */) {
+  uint32_t e = t.dir24[a >> 8];
+  if (e < 2) return e == 1;
+  const uint64_t* l = t.leaves + (size_t)(e - 2) * 4;
+  uint32_t x = a & 0xFF;
+  return (l[x >> 6] >> (x & 63)) & 1;
+}
+
+__device__ __forceinline__ bool lt128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+  return ah < bh || (ah == bh && al < bl);
+}
+
+__device__ __forceinline__ bool v6_covered(const LpmDev& t, uint64_t hi, uint64_t lo) {
+  const uint32_t top = (uint32_t)(hi >> 48);
+  int64_t L = t.v6_idx[top];
+  int64_t cnt = t.v6_idx[65536];
+  int64_t R = t.v6_idx[top + 1];
+  if (R > cnt - 1) R = cnt - 1;
+  // last interval in [L, R] with lo_i <= addr
+  int64_t ans = -1;
+  while (L <= R) {
+    int64_t m = (L + R) >> 1;
+    uint64_t mh = t.v6_lo[2 * m], ml = t.v6_lo[2 * m + 1];
+    if (!lt128(hi, lo, mh, ml)) {
+      ans = m;
+      L = m + 1;
+    } else {
+      R = m - 1;
+    }
+  }
+  if (ans < 0) return false;
+  uint64_t eh = t.v6_hi[2 * ans], el = t.v6_hi[2 * ans + 1];
+  return !lt128(eh, el, hi, lo);
+}
+
+__global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, const uint2* __restrict__ v4,
+                                                  size_t n4, uint8_t* __restrict__ out4,
+                                                  const uint4* __restrict__ v6, size_t n6,
+                                                  uint8_t* __restrict__ out6) {
+  uint32_t drops = 0, passes = 0;
+  const size_t total = n4 + n6;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    uint8_t v;
+    if (i < n4) {
+      uint2 r = v4[i];
+      bool drop = v4f && v4_covered(t, bswap32(r.x));
+      if (!drop) drop = !ep4_has(t, r.y);
+      v = drop ? CG_XDP_DROP : CG_XDP_PASS;
+      out4[i] = v;
+    } else {
+      size_t j = i - n4;
+      uint4 s = v6[2 * j], d = v6[2 * j + 1];
+      uint64_t shi = bswap64((uint64_t)s.x | ((uint64_t)s.y << 32));
+      uint64_t slo = bswap64((uint64_t)s.z | ((uint64_t)s.w << 32));
+      bool drop = v6f && v6_covered(t, shi, slo);
+      if (!drop) {
+        uint64_t dhi = bswap64((uint64_t)d.x | ((uint64_t)d.y << 32));
+        uint64_t dlo = bswap64((uint64_t)d.z | ((uint64_t)d.w << 32));
+        drop = !ep6_has(t, dhi, dlo);
+      }
+      v = drop ? CG_XDP_DROP : CG_XDP_PASS;
+      out6[j] = v;
+    }
+    drops += v == CG_XDP_DROP;
+    passes += v == CG_XDP_PASS;
+  }
+  // wave reduce then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    drops += __shfl_down(drops, o, kWave);
+    passes += __shfl_down(passes, o, kWave);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (drops) atomicAdd(&t.counters[0], (unsigned long long)drops);
+    if (passes) atomicAdd(&t.counters[1], (unsigned long long)passes);
+  }
+}
+
+// ============================================================= HTTP ======
+// NetworkPolicyMap::Allowed (envoy/cilium_network_policy.h:223-237) per
+// record; one lane per request, records tile-transposed so every unit load of
+// a wavefront is one contiguous 1 KiB read.
+
+__device__ __forceinline__ uint32_t prog_lookup(const HttpDev& T, uint32_t pol, uint32_t ingress, uint32_t port) {
+  if (pol >= T.npolicies) return kProgDeny;
+  const uint32_t key = (pol << 17) | (ingress << 16) | port;
+  uint32_t h = hash32(key) & T.phash_mask;
+  for (uint32_t probe = 0; probe <= T.phash_mask; ++probe) {
+    uint32_t k = T.phash_keys[h];
+    if (k == key) return T.phash_vals[h];
+    if (k == 0xFFFFFFFFu) break;
+    h = (h + 1) & T.phash_mask;
+  }
+  return T.dflt[pol * 2 + ingress];
+}
+
+__device__ __forceinline__ uint32_t remote_row(const HttpDev& T, uint32_t prog, uint32_t remote, uint32_t dflt) {
+  const unsigned long long key = ((unsigned long long)prog << 32) | remote;
+  uint32_t h = hash64to32(key) & T.rhash_mask;
+  for (uint32_t probe = 0; probe <= T.rhash_mask; ++probe) {
+    unsigned long long k = T.rhash_keys[h];
+    if (k == key) return T.rhash_vals[h];
+    if (k == ~0ULL) break;
+    h = (h + 1) & T.rhash_mask;
+  }
+  return dflt;
+}
+
+__device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
+                                           uint32_t w) {
+  for (uint32_t i = 0; i < w; ++i)
+    if (m[a + i] & m[b + i]) return true;
+  return false;
+}
+
+__device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
+  const uint32_t word = (k < 4) ? w.x : (k < 8) ? w.y : (k < 12) ? w.z : w.w;
+  return (word >> ((k & 3) * 8)) & 0xFFu;
+}
+
+template <bool kClsLds>
+__global__ __launch_bounds__(256) void http_kernel(HttpDev T, const uint4* __restrict__ rec, size_t n,
+                                                   const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
+                                                   uint32_t lds_counters) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* cls_lds = smem;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + ((T.cls_lds_bytes + 15) & ~15u));
+  if (kClsLds)
+    for (uint32_t i = threadIdx.x; i < T.cls_lds_bytes / 16; i += blockDim.x)
+      reinterpret_cast<uint4*>(cls_lds)[i] = reinterpret_cast<const uint4*>(T.clsmap)[i];
+  if (lds_counters)
+    for (uint32_t i = threadIdx.x; i < 2 * T.nprogs; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  const uint8_t* __restrict__ cls = kClsLds ? cls_lds : T.clsmap;
+
+  const int lane = threadIdx.x & 63;
+  const size_t wave = threadIdx.x >> 6;
+  const size_t waves_per_block = blockDim.x >> 6;
+  const size_t ntiles = (n + kWave - 1) / kWave;
+  for (size_t tile = blockIdx.x * waves_per_block + wave; tile < ntiles; tile += gridDim.x * waves_per_block) {
+    const uint4* tb = rec + tile * (CG_HTTP_UNITS * kWave);
+    const uint4 meta = tb[lane];
+    uint4 s[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] = tb[(u + 1) * kWave + lane];
+    const size_t idx = tile * kWave + lane;
+    const uint32_t remote = meta.x;
+    const uint32_t port = meta.y & 0xFFFF;
+    const uint32_t pol = meta.y >> 16;
+    const uint32_t len = meta.z;
+    const uint32_t flags = meta.w >> 24;
+    const uint32_t aoff = (meta.w & 0xFFFFFF) * 16u;
+    const uint32_t ingress = flags & CG_HTTP_F_INGRESS;
+    uint32_t verdict = 0;
+    uint32_t prog = kProgDeny;
+    bool decided = true;
+    if (!(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED)) && pol != 0xFFFF) {
+      prog = prog_lookup(T, pol, ingress, port);
+      if (prog == kProgAllow) {
+        verdict = 1;
+      } else if (prog != kProgDeny) {
+        const HttpProg pg = T.progs[prog];
+        if (pg.flags & kProgAllowAll) {
+          verdict = 1;
+        } else {
+          const uint32_t rrow = remote_row(T, prog, remote, pg.default_remote);
+          if (masks_meet(T.masks, pg.always_off, rrow, pg.mask_words)) {
+            verdict = 1;
+          } else {
+            decided = false;
+            for (uint32_t pi = 0; pi < pg.part_count && !verdict; ++pi) {
+              const HttpPart pt = T.parts[pg.part_begin + pi];
+              const uint16_t* __restrict__ tr = T.trans + pt.trans_off;
+              const uint8_t* __restrict__ cm = cls + pt.cls_off;
+              const uint32_t ncls = pt.ncls;
+              uint32_t st = 1;
+              if (!(flags & CG_HTTP_F_OVERFLOW)) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+#pragma unroll
+                  for (int k = 0; k < 16; ++k) {
+                    const uint32_t p = u * 16 + k;
+                    if (p < len && st != 0) st = tr[st * ncls + cm[get_byte(s[u], k)]];
+                  }
+                }
+              } else {
+                for (uint32_t p = 0; p < len && st != 0; ++p) st = tr[st * ncls + cm[arena[aoff + p]]];
+              }
+              const uint32_t a = T.acc[pt.acc_off + st];
+              if (a != kNoAcc && masks_meet(T.masks, a, rrow, pg.mask_words)) verdict = 1;
+            }
+            decided = true;
+          }
+        }
+      }
+    }
+    (void)decided;
+    if (idx < n) {
+      out[idx] = (uint8_t)verdict;
+      if (prog < T.nprogs) {
+        if (lds_counters)
+          atomicAdd(&cnt[prog * 2 + (verdict ? 0 : 1)], 1u);
+        else
+          atomicAdd(&T.counters[prog * 2 + (verdict ? 0 : 1)], 1ULL);
+      }
+    }
+  }
+  if (lds_counters) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 2 * T.nprogs; i += blockDim.x)
+      if (cnt[i]) atomicAdd(&T.counters[i], (unsigned long long)cnt[i]);
+  }
+}
+
+// ============================================================ Kafka ======
+// kafkaRedirect.canAccess → RequestMessage.MatchesRule
+// (pkg/proxy/kafka.go:117-153, pkg/kafka/policy.go:144-225).
+
+__device__ __forceinline__ bool kf_is_topic_key(int k) {
+  // isTopicAPIKey (pkg/kafka/policy.go:27-52) as a bitmask over 0..37
+  const unsigned long long m = (1ULL << 0) | (1ULL << 1) | (1ULL << 2) | (1ULL << 3) | (1ULL << 4) |
+                               (1ULL << 5) | (1ULL << 6) | (1ULL << 8) | (1ULL << 9) | (1ULL << 19) |
+                               (1ULL << 20) | (1ULL << 21) | (1ULL << 23) | (1ULL << 24) | (1ULL << 27) |
+                               (1ULL << 28) | (1ULL << 34) | (1ULL << 35) | (1ULL << 37);
+  return k >= 0 && k < 64 && ((m >> k) & 1);
+}
+
+__device__ __forceinline__ bool kf_rule_matches(const KafkaRuleDev& r, bool has_topic, int key, int ver,
+                                                uint32_t kind, uint32_t client) {
+  if (!(r.flags & kKfKeyWild)) {
+    if (key < 0 || key >= 64 || !((r.keys >> key) & 1)) return false;
+  }
+  if (!(r.flags & kKfVerWild) && r.version != ver) return false;
+  const bool has_client = r.flags & kKfHasClient;
+  if (!has_topic && !has_client) return true;
+  if (kind == CG_KAFKA_K_TYPED) return !has_client || r.client_id == client;
+  if (kind == CG_KAFKA_K_CONSUMER_METADATA) return true;
+  return !(has_topic && kf_is_topic_key(key));
+}
+
+__global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __restrict__ reqs, size_t n,
+                                                    const uint32_t* __restrict__ arena, uint8_t* __restrict__ out) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint4* r = reqs + i * 4;
+    const uint4 h = r[0];
+    const int key = (int16_t)(h.x & 0xFFFF);
+    const int ver = (int16_t)(h.x >> 16);
+    const uint32_t kind = h.y & 0xFF;
+    const uint32_t nt = (h.y >> 8) & 0xFF;
+    const uint32_t red = h.y >> 16;
+    const uint32_t remote = h.z;
+    const uint32_t client = h.w;
+    uint32_t v = 0;
+    if (red < T.nredirects) {
+      uint32_t g = T.dflt_group[red];
+      if (remote != 0) {
+        const unsigned long long k = ((unsigned long long)red << 32) | remote;
+        uint32_t hh = hash64to32(k) & T.ghash_mask;
+        for (uint32_t probe = 0; probe <= T.ghash_mask; ++probe) {
+          unsigned long long kk = T.ghash_keys[hh];
+          if (kk == k) {
+            g = T.ghash_vals[hh];
+            break;
+          }
+          if (kk == ~0ULL) break;
+          hh = (hh + 1) & T.ghash_mask;
+        }
+      }
+      const KafkaGroupDev G = T.groups[g];
+      if (G.any_rules) {
+        for (uint32_t j = 0; j < G.wild_cnt && !v; ++j)
+          if (kf_rule_matches(T.rules[G.wild_off + j], false, key, ver, kind, client)) v = 1;
+        if (!v) {
+          if (nt == 0) {
+            for (uint32_t j = 0; j < G.tr_cnt && !v; ++j)
+              if (kf_rule_matches(T.rules[G.tr_off + j], true, key, ver, kind, client)) v = 1;
+          } else {
+            uint32_t tids[CG_KAFKA_MAX_TOPICS];
+            const uint4 t0 = r[1], t1 = r[2], t2 = r[3];
+            tids[0] = t0.x; tids[1] = t0.y; tids[2] = t0.z; tids[3] = t0.w;
+            tids[4] = t1.x; tids[5] = t1.y; tids[6] = t1.z; tids[7] = t1.w;
+            tids[8] = t2.x; tids[9] = t2.y; tids[10] = t2.z; tids[11] = t2.w;
+            const bool ovf = nt > CG_KAFKA_MAX_TOPICS;
+            bool all = true;
+            for (uint32_t t = 0; t < nt && all; ++t) {
+              const uint32_t tid = ovf ? arena[tids[0] + t] : tids[t];
+              // rules of this group sorted by topic id: binary search the first
+              uint32_t lo = 0, hi = G.tr_cnt;
+              while (lo < hi) {
+                uint32_t m = (lo + hi) >> 1;
+                if (T.topic_of[G.tr_off + m] < tid) lo = m + 1; else hi = m;
+              }
+              bool cov = false;
+              for (uint32_t j = lo; j < G.tr_cnt && T.topic_of[G.tr_off + j] == tid && !cov; ++j)
+                if (kf_rule_matches(T.rules[G.tr_off + j], true, key, ver, kind, client)) cov = true;
+              all = cov;
+            }
+            v = all ? 1 : 0;
+          }
+        }
+      }
+      atomicAdd(&T.counters[red * 2 + (v ? 0 : 1)], 1ULL);
+    }
+    out[i] = (uint8_t)v;
+  }
+}
+
+int grid_for(size_t items, int per_block, int cus, int blocks_per_cu) {
+  size_t need = (items + per_block - 1) / per_block;
+  size_t cap = (size_t)cus * blocks_per_cu;
+  if (need > cap) need = cap;
+  if (need < 1) need = 1;
+  return (int)need;
+}
+
+}  // namespace
+
+int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus) {
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (t.max_entries <= 16384) {
+    size_t lds = (size_t)t.max_entries * 2 * sizeof(uint32_t);
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute((const void*)l4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(l4_kernel<true>, dim3(grid_for(n, 1024, cus, 1)), dim3(1024), lds, s, t,
+                       (const uint32_t*)tuples, n, out);
+  } else {
+    hipLaunchKernelGGL(l4_kernel<false>, dim3(grid_for(n, 1024, cus, 2)), dim3(1024), 0, s, t,
+                       (const uint32_t*)tuples, n, out);
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n4, uint8_t* out4,
+               const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus) {
+  if (n4 + n6 == 0) return 0;
+  hipLaunchKernelGGL(lpm_kernel, dim3(grid_for(n4 + n6, 256, cus, 8)), dim3(256), 0, (hipStream_t)stream, t, v4f,
+                     v6f, (const uint2*)v4, n4, out4, (const uint4*)v6, n6, out6);
+  return (int)hipGetLastError();
+}
+
+int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
+                void* stream, int cus) {
+  if (n == 0) return 0;
+  const size_t ntiles = (n + kWave - 1) / kWave;
+  size_t cls_bytes = (t.cls_lds_bytes + 15) & ~(size_t)15;
+  size_t cnt_bytes = (size_t)t.nprogs * 2 * sizeof(uint32_t);
+  uint32_t lds_counters = (cls_bytes + cnt_bytes) <= 48 * 1024 ? 1 : 0;
+  size_t lds = cls_bytes + (lds_counters ? cnt_bytes : 0);
+  int grid = grid_for(ntiles, 4, cus, 8);
+  if (t.cls_lds_bytes)
+    hipLaunchKernelGGL(http_kernel<true>, dim3(grid), dim3(256), lds, (hipStream_t)stream, t, (const uint4*)records,
+                       n, arena, out, lds_counters);
+  else
+    hipLaunchKernelGGL(http_kernel<false>, dim3(grid), dim3(256), lds, (hipStream_t)stream, t,
+                       (const uint4*)records, n, arena, out, lds_counters);
+  return (int)hipGetLastError();
+}
+
+int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
+                 void* stream, int cus) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, (hipStream_t)stream, t,
+                     (const uint4*)reqs, n, arena, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace cg

@@ -1,0 +1,88 @@
+// l4.cc — cuckoo table build for policy maps.
+//
+// The reference keeps one BPF_MAP_TYPE_HASH per endpoint keyed by the 8-byte
+// struct policy_key (bpf/lib/common.h:180-186, pkg/maps/policymap).  The
+// device copy is a 2-choice cuckoo hash of 64-byte buckets (4 slots of
+// {key, entry id | proxy_port_be << 16}): a lookup touches at most two cache
+// lines.  Counters live in a separate per-entry-id array so a rebuild never
+// moves them.
+#include "l4.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <random>
+
+namespace cg {
+
+namespace {
+
+bool try_build(const std::unordered_map<uint64_t, PolicyMapState::Entry>& entries, uint32_t nbuckets,
+               std::vector<L4Slot>& slots) {
+  slots.assign((size_t)nbuckets * 4, L4Slot{kL4EmptyKey, 0, 0});
+  const uint32_t mask = nbuckets - 1;
+  std::mt19937_64 rng(0xC111A);
+  for (const auto& [key, ent] : entries) {
+    L4Slot cur{key, (uint32_t)ent.id | ((uint32_t)ent.proxy_port_be << 16), 0};
+    uint32_t b = (uint32_t)l4_hash1(cur.key) & mask;
+    bool placed = false;
+    for (int kick = 0; kick < 500 && !placed; ++kick) {
+      uint32_t b1 = (uint32_t)l4_hash1(cur.key) & mask, b2 = (uint32_t)l4_hash2(cur.key) & mask;
+      for (uint32_t bb : {b1, b2}) {
+        for (int s = 0; s < 4; ++s)
+          if (slots[(size_t)bb * 4 + s].key == kL4EmptyKey) {
+            slots[(size_t)bb * 4 + s] = cur;
+            placed = true;
+            break;
+          }
+        if (placed) break;
+      }
+      if (placed) break;
+      // evict a random slot of the alternate bucket
+      b = (b == b1) ? b2 : b1;
+      int victim = (int)(rng() & 3);
+      std::swap(cur, slots[(size_t)b * 4 + victim]);
+    }
+    if (!placed) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+void PolicyMapState::rebuild(Engine& e) {
+  uint32_t nb = next_pow2(std::max<size_t>((entries.size() * 10 / 4 + 3) / 4 + 1, 4));
+  while (!try_build(entries, nb, slots)) nb *= 2;
+  bucket_mask = nb - 1;
+  if (e.has_gpu()) {
+    e.set_device();
+    d_slots.upload_vec(slots);
+    if (d_counters.size() == 0) {
+      d_counters.alloc((size_t)max_entries * 2 * sizeof(uint64_t));
+      d_counters.zero();
+    }
+    dev.slots = d_slots.as<L4Slot>();
+    dev.bucket_mask = bucket_mask;
+    dev.max_entries = max_entries;
+    dev.counters = d_counters.as<unsigned long long>();
+  }
+  dirty = false;
+}
+
+void PolicyMapState::read_counters(Engine& e, uint32_t id, uint64_t* pk, uint64_t* by) {
+  *pk = *by = 0;
+  if (!e.has_gpu() || d_counters.size() == 0) return;
+  e.set_device();
+  uint64_t v[2];
+  hip_check(hipMemcpy(v, d_counters.as<uint64_t>() + (size_t)id * 2, 16, hipMemcpyDeviceToHost),
+            "read counters");
+  *pk = v[0];
+  *by = v[1];
+}
+
+void PolicyMapState::zero_counter(Engine& e, uint32_t id) {
+  if (!e.has_gpu() || d_counters.size() == 0) return;
+  e.set_device();
+  hip_check(hipMemset(d_counters.as<uint64_t>() + (size_t)id * 2, 0, 16), "zero counter");
+}
+
+}  // namespace cg

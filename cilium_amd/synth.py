@@ -1,0 +1,385 @@
+"""Synthetic workloads for the BASELINE.json configs (seeded, deterministic).
+
+Each generator follows SURVEY.md §8(d): star-wars HTTP (config 1), L4
+policymap (2), CIDR prefilter (3), Kafka (4) and the 10K-rule HTTP set (5).
+Requests are returned in the engine's input formats (header blobs for the
+HTTP packer, numpy records for L4/LPM, field lists for Kafka).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .policy import (PortRuleHTTP, PortRuleKafka, get_http_rule, htons, network_policy, port_network_policy,
+                     port_network_policy_rule)
+
+SEED = 0xC111A
+METHODS = [b"GET", b"POST", b"PUT", b"DELETE", b"HEAD", b"PATCH"]
+
+
+def _blob(reqs: list[list[tuple[bytes, bytes]]]) -> tuple[np.ndarray, np.ndarray]:
+    parts = []
+    off = [0]
+    for hs in reqs:
+        b = b"".join(k + b"\0" + v + b"\0" for k, v in hs)
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    return np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy(), np.asarray(off, np.uint64)
+
+
+# ------------------------------------------------------- config 1: star-wars
+SPACESHIP_ID = 257
+DEATHSTAR_ID = 258
+OTHER_ID = 300
+
+
+def starwars_rules() -> list[PortRuleHTTP]:
+    """examples/demo/sw_policy_http.real.json:13-31."""
+    return [PortRuleHTTP(Method="GET", Path="/v1/"),
+            PortRuleHTTP(Method="POST", Path="/v1/request-landing/"),
+            PortRuleHTTP(Method="PUT", Path="/v1/exhaust-port/", Headers=["X-Has-Force: true"])]
+
+
+def starwars_policy() -> list[dict]:
+    """Two endpoint policies: the spaceship's egress (toPorts without
+    toEndpoints → any destination) and the deathstar's ingress restricted to
+    the spaceship identity (the L3-dependent variant)."""
+    hs = [get_http_rule(r)[0] for r in starwars_rules()]
+    return [
+        network_policy("spaceship", SPACESHIP_ID,
+                       egress=[port_network_policy(80, [port_network_policy_rule([], hs)])]),
+        network_policy("deathstar", DEATHSTAR_ID,
+                       ingress=[port_network_policy(80, [port_network_policy_rule([SPACESHIP_ID], hs)])]),
+    ]
+
+
+def starwars_requests(n: int, seed: int = SEED):
+    rng = np.random.default_rng(seed)
+    paths = [b"/v1/", b"/v1/request-landing/", b"/v1/exhaust-port/"]
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8)
+    reqs = []
+    pol = rng.integers(0, 2, n).astype(np.uint32)
+    ingress = (pol == 1).astype(np.uint8)
+    remote = np.where(rng.random(n) < 0.5, SPACESHIP_ID, OTHER_ID).astype(np.uint32)
+    remote = np.where(pol == 0, DEATHSTAR_ID, remote).astype(np.uint32)
+    port = np.full(n, 80, np.uint16)
+    port[rng.random(n) < 0.05] = 8080
+    m = rng.integers(0, len(METHODS), n)
+    pk = rng.integers(0, 4, n)
+    hdr = rng.random(n) < 0.5
+    hv = rng.integers(0, 3, n)
+    for i in range(n):
+        if pk[i] < 3:
+            path = paths[pk[i]]
+        else:
+            L = int(rng.integers(1, 25))
+            path = b"/v1/" + letters[rng.integers(0, len(letters), L)].tobytes()
+        hs = [(b":method", METHODS[m[i]]), (b":path", path), (b":authority", b"deathstar.empire.svc")]
+        if hdr[i]:
+            hs.append((b"X-Has-Force", [b"true", b"True", b"false"][hv[i]]))
+        reqs.append(hs)
+    blob, off = _blob(reqs)
+    return dict(policy=pol, ingress=ingress, port=port, remote=remote, hdr_blob=blob, hdr_off=off)
+
+
+# -------------------------------------------------- config 5: 10K-rule HTTP
+HTTP10K_METHODS = ["GET", "POST", "PUT", "DELETE", "GET|HEAD", "P(UT|OST)"]
+WORDS = ["alpha", "bravo", "charlie", "delta", "echo", "foxtrot", "golf", "hotel", "india", "juliet", "kilo",
+         "lima", "mike", "november", "oscar", "papa"]
+
+
+def http10k_rules(n_rules: int = 10000, n_ports: int = 64, n_ids: int = 1000, n_selectors: int = 256,
+                  seed: int = SEED):
+    """Rules spread over ports and selectors (each selector = a set of
+    identities).  Returns (npds policies, rule metadata used by the request
+    generator)."""
+    rng = np.random.default_rng(seed)
+    ports = (8000 + np.arange(n_ports)).tolist()
+    ids = (1000 + np.arange(n_ids)).tolist()
+    sel_ids = [sorted(rng.choice(ids, size=int(rng.integers(4, 9)), replace=False).tolist())
+               for _ in range(n_selectors)]
+    meta = []
+    by_scope: dict[tuple[int, int], list] = {}
+    for k in range(n_rules):
+        port = ports[int(rng.integers(0, n_ports))]
+        sel = int(rng.integers(0, n_selectors))
+        method = HTTP10K_METHODS[int(rng.integers(0, len(HTTP10K_METHODS)))]
+        kind = int(rng.integers(0, 3))
+        word = WORDS[int(rng.integers(0, len(WORDS)))]
+        if kind == 0:
+            path = f"/api/v[0-9]+/svc{k}/.*"
+        elif kind == 1:
+            path = f"/static/{k}/[a-z]+\\.(js|css)"
+        else:
+            path = f"/svc{k}/{word}"
+        host = f"svc{k}\\.example\\.com" if rng.random() < 0.2 else ""
+        headers = [f"X-Tenant-{k % 7}: t{k % 13}"] if rng.random() < 0.1 else []
+        r = PortRuleHTTP(Method=method, Path=path, Host=host, Headers=headers)
+        meta.append(dict(k=k, port=port, sel=sel, kind=kind, word=word, rule=r))
+        by_scope.setdefault((port, sel), []).append(r)
+    per_port: dict[int, list] = {}
+    for (port, sel), rules in sorted(by_scope.items()):
+        per_port.setdefault(port, []).append(
+            port_network_policy_rule(sel_ids[sel], [get_http_rule(r)[0] for r in rules]))
+    policies = [network_policy("ep-10k", 4242,
+                               ingress=[port_network_policy(p, per_port[p]) for p in sorted(per_port)])]
+    return policies, dict(meta=meta, sel_ids=sel_ids, ports=ports, ids=ids)
+
+
+def _example(meta: dict, rng, hit: bool) -> list[tuple[bytes, bytes]]:
+    k, kind, word = meta["k"], meta["kind"], meta["word"]
+    method = meta["rule"].Method
+    mchoices = {"GET": ["GET"], "POST": ["POST"], "PUT": ["PUT"], "DELETE": ["DELETE"], "GET|HEAD": ["GET", "HEAD"],
+                "P(UT|OST)": ["PUT", "POST"]}[method]
+    m = mchoices[int(rng.integers(0, len(mchoices)))]
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    if kind == 0:
+        tail = "".join(letters[int(x)] for x in rng.integers(0, 26, int(rng.integers(0, 40))))
+        path = f"/api/v{int(rng.integers(1, 10))}/svc{k}/{tail}"
+    elif kind == 1:
+        stem = "".join(letters[int(x)] for x in rng.integers(0, 26, int(rng.integers(1, 24))))
+        path = f"/static/{k}/{stem}.{'js' if rng.random() < 0.5 else 'css'}"
+    else:
+        path = f"/svc{k}/{word}"
+    host = f"svc{k}.example.com" if meta["rule"].Host else f"h{int(rng.integers(0, 100))}.example.com"
+    hs = [(b":method", m.encode()), (b":path", path.encode()), (b":authority", host.encode())]
+    for h in meta["rule"].Headers:
+        name, val = h.split(" ", 1)
+        hs.append((name.rstrip(":").encode(), val.encode()))
+    if not hit:
+        # near miss: one field mutated
+        which = int(rng.integers(0, 4))
+        if which == 0:
+            hs[0] = (b":method", b"PATCH")
+        elif which == 1:
+            p = bytearray(hs[1][1])
+            pos = int(rng.integers(1, len(p)))
+            p[pos] = ord("~")
+            hs[1] = (b":path", bytes(p))
+        elif which == 2:
+            hs[1] = (b":path", hs[1][1] + b"/x")
+        else:
+            hs[2] = (b":authority", b"evil.example.com")
+    return hs
+
+
+def http10k_requests(n: int, info: dict, seed: int = SEED, distinct: int = 200_000):
+    """n requests: 50% crafted to hit a random rule, 50% near-miss mutations.
+    `distinct` unique header blocks are generated and tiled to n."""
+    rng = np.random.default_rng(seed ^ 0x5EED)
+    meta, sel_ids = info["meta"], info["sel_ids"]
+    d = min(n, distinct)
+    reqs = []
+    port = np.zeros(d, np.uint16)
+    remote = np.zeros(d, np.uint32)
+    rix = rng.integers(0, len(meta), d)
+    hit = rng.random(d) < 0.5
+    for i in range(d):
+        mt = meta[int(rix[i])]
+        reqs.append(_example(mt, rng, bool(hit[i])))
+        port[i] = mt["port"]
+        ids = sel_ids[mt["sel"]]
+        remote[i] = ids[int(rng.integers(0, len(ids)))]
+    blob, off = _blob(reqs)
+    rep = (n + d - 1) // d
+    if rep > 1:
+        lens = np.diff(off)
+        blob = np.tile(blob, rep)
+        off = np.concatenate([[0], np.cumsum(np.tile(lens, rep))]).astype(np.uint64)
+        port = np.tile(port, rep)
+        remote = np.tile(remote, rep)
+    off = off[:n + 1]
+    blob = blob[:int(off[-1])] if n else blob[:1]
+    return dict(policy=np.zeros(n, np.uint32), ingress=np.ones(n, np.uint8), port=port[:n], remote=remote[:n],
+                hdr_blob=blob, hdr_off=off)
+
+
+# ------------------------------------------------------ config 2: L4 table
+def l4_table(n_entries: int = 16384, n_ids: int = 16384, seed: int = SEED):
+    """70% {id,port,proto,dir}, 20% {id,0,0,dir}, 10% {0,port,proto,dir}."""
+    rng = np.random.default_rng(seed)
+    from .classifier import POLICY_KEY_DTYPE
+    ids = np.concatenate([np.arange(1, 6), 256 + np.arange(n_ids)]).astype(np.uint32)
+    keys = set()
+    out = []
+    while len(out) < n_entries:
+        r = rng.random()
+        d = int(rng.integers(0, 2))
+        if r < 0.7:
+            k = (int(rng.choice(ids)), htons(int(rng.integers(1, 65536))), int(rng.choice([6, 17])), d)
+        elif r < 0.9:
+            k = (int(rng.choice(ids)), 0, 0, d)
+        else:
+            k = (0, htons(int(rng.integers(1, 65536))), int(rng.choice([6, 17])), d)
+        if k in keys:
+            continue
+        keys.add(k)
+        out.append(k)
+    arr = np.zeros(len(out), POLICY_KEY_DTYPE)
+    arr["sec_label"] = [k[0] for k in out]
+    arr["dport"] = [k[1] for k in out]
+    arr["protocol"] = [k[2] for k in out]
+    arr["egress"] = [k[3] for k in out]
+    ports = np.where(rng.random(len(out)) < 0.8, 0, rng.integers(10000, 11000, len(out))).astype(np.uint16)
+    ports_be = ((ports & 0xFF) << 8 | ports >> 8).astype(np.uint16)
+    return arr, ports_be
+
+
+def l4_tuples(n: int, keys: np.ndarray, n_ids: int = 16384, seed: int = SEED):
+    """identity uniform over the table's ids + 10 unknown, dport 50% from table
+    ports (Zipf s=1.1) / 50% uniform, proto 50/50, dir 50/50, fragment 1%,
+    len 64-1500."""
+    rng = np.random.default_rng(seed ^ 0x7)
+    from .classifier import L4_TUPLE_DTYPE
+    t = np.zeros(n, L4_TUPLE_DTYPE)
+    ids = np.concatenate([np.arange(1, 6), 256 + np.arange(n_ids), 900000 + np.arange(10)]).astype(np.uint32)
+    t["identity"] = ids[rng.integers(0, len(ids), n)]
+    tports = keys["dport"][keys["dport"] != 0]
+    if len(tports) == 0:
+        tports = np.array([htons(80)], np.uint16)
+    z = np.minimum(rng.zipf(1.1, n) - 1, len(tports) - 1)
+    uni = rng.integers(1, 65536, n).astype(np.uint16)
+    uni_be = ((uni & 0xFF) << 8 | uni >> 8).astype(np.uint16)
+    t["dport"] = np.where(rng.random(n) < 0.5, tports[z], uni_be)
+    t["proto"] = np.where(rng.random(n) < 0.5, 6, 17)
+    flags = (rng.random(n) < 0.5).astype(np.uint8)  # ingress
+    flags |= ((rng.random(n) < 0.01).astype(np.uint8) << 1)  # fragment
+    flags |= ((rng.random(n) < 0.01).astype(np.uint8) << 2)  # cb_policy
+    t["flags"] = flags
+    t["len"] = rng.integers(64, 1501, n)
+    return t
+
+
+# ---------------------------------------------------- config 3: prefilter
+def lpm_prefixes(n_v4: int = 700_000, n_v6: int = 300_000, seed: int = SEED):
+    """Prefix-length mix of SURVEY §8(d) config 3; returns cg_cidr records."""
+    from .classifier import CIDR_DTYPE
+    rng = np.random.default_rng(seed)
+    out = np.zeros(n_v4 + n_v6, CIDR_DTYPE)
+    r = rng.random(n_v4)
+    plen4 = np.where(r < 0.55, 24, np.where(r < 0.85, rng.integers(16, 24, n_v4),
+                                            np.where(r < 0.90, rng.integers(8, 16, n_v4), 32)))
+    a4 = rng.integers(0, 2 ** 32, n_v4, dtype=np.uint64).astype(np.uint32)
+    mask = np.where(plen4 == 0, 0, (0xFFFFFFFF << (32 - plen4)) & 0xFFFFFFFF).astype(np.uint32)
+    a4 &= mask
+    out["family"][:n_v4] = 4
+    out["prefixlen"][:n_v4] = plen4
+    out["addr"][:n_v4, :4] = a4.astype(">u4").view(np.uint8).reshape(-1, 4)
+    r = rng.random(n_v6)
+    plen6 = np.where(r < 0.40, rng.integers(32, 49, n_v6), np.where(r < 0.85, rng.integers(49, 65, n_v6),
+                                                                   np.where(r < 0.90, rng.integers(65, 128, n_v6),
+                                                                            128)))
+    a6 = rng.integers(0, 256, (n_v6, 16), dtype=np.uint8)
+    for i in range(16):  # mask host bits
+        keep = np.clip(plen6 - 8 * i, 0, 8)
+        a6[:, i] &= ((0xFF << (8 - keep)) & 0xFF).astype(np.uint8)
+    out["family"][n_v4:] = 6
+    out["prefixlen"][n_v4:] = plen6
+    out["addr"][n_v4:] = a6
+    return out
+
+
+def lpm_addresses(n: int, prefixes: np.ndarray, n_eps: int = 65536, seed: int = SEED):
+    """70% v4 / 30% v6; 50% drawn inside a random prefix; destinations are
+    local endpoints 50% of the time.  Returns (v4 (n4,2) u32, v6 (n6,32) u8,
+    ep4 u32, ep6 (m,16) u8)."""
+    rng = np.random.default_rng(seed ^ 0x3)
+    p4 = prefixes[prefixes["family"] == 4]
+    p6 = prefixes[prefixes["family"] == 6]
+    n4 = int(n * 0.7)
+    n6 = n - n4
+    ep4 = rng.integers(0, 2 ** 32, n_eps // 2, dtype=np.uint64).astype(np.uint32)
+    ep6 = rng.integers(0, 256, (n_eps // 2, 16), dtype=np.uint8)
+    # v4
+    s4 = rng.integers(0, 2 ** 32, n4, dtype=np.uint64).astype(np.uint32)
+    inside = rng.random(n4) < 0.5
+    pick = p4[rng.integers(0, len(p4), n4)]
+    base = pick["addr"][:, :4].copy().view(">u4").reshape(-1).astype(np.uint32)
+    host_bits = (32 - pick["prefixlen"].astype(np.int64))
+    hm = np.where(host_bits >= 32, 0xFFFFFFFF, (1 << host_bits) - 1).astype(np.uint32)
+    s4 = np.where(inside, base | (s4 & hm), s4).astype(np.uint32)
+    d4 = np.where(rng.random(n4) < 0.5, ep4[rng.integers(0, len(ep4), n4)],
+                  rng.integers(0, 2 ** 32, n4, dtype=np.uint64).astype(np.uint32)).astype(np.uint32)
+    v4 = np.empty((n4, 2), np.uint32)
+    v4[:, 0] = s4.astype(">u4").view("<u4")  # network order as in iphdr
+    v4[:, 1] = d4.astype(">u4").view("<u4")
+    ep4_be = ep4.astype(">u4").view("<u4")
+    # v6
+    s6 = rng.integers(0, 256, (n6, 16), dtype=np.uint8)
+    inside = rng.random(n6) < 0.5
+    pick = p6[rng.integers(0, len(p6), n6)]
+    for i in range(16):
+        keep = np.clip(pick["prefixlen"].astype(np.int64) - 8 * i, 0, 8)
+        m = ((0xFF << (8 - keep)) & 0xFF).astype(np.uint8)
+        s6[:, i] = np.where(inside, (pick["addr"][:, i] & m) | (s6[:, i] & ~m), s6[:, i])
+    d6 = np.where((rng.random(n6) < 0.5)[:, None], ep6[rng.integers(0, len(ep6), n6)],
+                  rng.integers(0, 256, (n6, 16), dtype=np.uint8))
+    v6 = np.concatenate([s6, d6], axis=1).astype(np.uint8)
+    return v4, v6, ep4_be, ep6
+
+
+# -------------------------------------------------------- config 4: Kafka
+def kafka_policy(n_rules: int = 1000, n_topics: int = 1000, n_clients: int = 100, n_ids: int = 64,
+                 seed: int = SEED):
+    """Rules mixing {apiKey}, {role}, {apiKey,topic}, {role,topic},
+    {apiVersion}, {clientID} (examples/policies/l7/kafka/*.yaml patterns)."""
+    rng = np.random.default_rng(seed)
+    topics = [f"topic-{i}" for i in range(n_topics)]
+    clients = [f"client-{i}" for i in range(n_clients)]
+    keys = list(__import__("cilium_amd.policy", fromlist=["KAFKA_API_KEY_MAP"]).KAFKA_API_KEY_MAP)
+    sels = []
+    ids = (2000 + np.arange(n_ids)).tolist()
+    n_sel = 16
+    for s in range(n_sel + 1):
+        rules = []
+        for _ in range(n_rules // (n_sel + 1)):
+            kind = int(rng.integers(0, 6))
+            r = PortRuleKafka()
+            if kind == 0:
+                r.APIKey = keys[int(rng.integers(0, len(keys)))]
+            elif kind == 1:
+                r.Role = ["produce", "consume"][int(rng.integers(0, 2))]
+            elif kind == 2:
+                r.APIKey = ["produce", "fetch", "metadata"][int(rng.integers(0, 3))]
+                r.Topic = topics[int(rng.integers(0, n_topics))]
+            elif kind == 3:
+                r.Role = ["produce", "consume"][int(rng.integers(0, 2))]
+                r.Topic = topics[int(rng.integers(0, n_topics))]
+            elif kind == 4:
+                r.APIKey = keys[int(rng.integers(0, len(keys)))]
+                r.APIVersion = str(int(rng.integers(0, 6)))
+            else:
+                r.ClientID = clients[int(rng.integers(0, n_clients))]
+                r.APIKey = ["produce", "fetch"][int(rng.integers(0, 2))]
+            rules.append(r)
+        if s == n_sel:
+            sels.append({"identities": None, "rules": rules[: max(1, len(rules) // 8)]})
+        else:
+            sels.append({"identities": sorted(rng.choice(ids, 8, replace=False).tolist()), "rules": rules})
+    return [{"name": "kafka-redirect-9092", "selectors": sels}], dict(topics=topics, clients=clients, ids=ids)
+
+
+def kafka_requests(n: int, info: dict, seed: int = SEED):
+    """apiKey weighted (produce 35%, fetch 35%, metadata 15%, other 15% over the
+    34 keys), version 0-5, 1-4 topics, clientID from 100."""
+    rng = np.random.default_rng(seed ^ 0x9)
+    topics, clients, ids = info["topics"], info["clients"], info["ids"]
+    r = rng.random(n)
+    key = np.where(r < 0.35, 0, np.where(r < 0.70, 1, np.where(r < 0.85, 3, rng.integers(0, 38, n)))).astype(np.int16)
+    ver = rng.integers(0, 6, n).astype(np.int16)
+    typed = np.isin(key, [0, 1, 2, 3, 8, 9])
+    kind = np.where(typed, 1, np.where(key == 10, 2, 0)).astype(np.uint8)
+    remote = np.where(rng.random(n) < 0.9, np.asarray(ids)[rng.integers(0, len(ids), n)],
+                      rng.integers(0, 10, n)).astype(np.uint32)
+    nt = np.where(typed, rng.integers(1, 5, n), 0)
+    cl = rng.integers(0, len(clients), n)
+    client = [clients[int(c)].encode() for c in cl]
+    tix = rng.integers(0, len(topics) + 20, (n, 4))
+    tps = []
+    for i in range(n):
+        ts = []
+        for j in range(int(nt[i])):
+            t = int(tix[i, j])
+            ts.append(topics[t].encode() if t < len(topics) else f"unknown-{t}".encode())
+        tps.append(ts)
+    return dict(redirect=np.zeros(n, np.uint32), remote=remote, api_key=key, api_version=ver, kind=kind,
+                client_id=client, topics=tps)

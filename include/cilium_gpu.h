@@ -1,0 +1,354 @@
+/*
+ * cilium_gpu.h — C ABI of libciliumgpu.so, the MI355X (gfx950) batched
+ * policy-verdict engine.
+ *
+ * This is the drop-in boundary for Cilium's data-parallel classification path
+ * (SURVEY.md §8).  Every entry point is plain C: integers, pointers and sizes;
+ * no C++ or torch types cross it.  Conventions kept from the reference:
+ *
+ *  - Return codes reuse proxylib's FilterResult numbering for the shared
+ *    values (proxylib/proxylib/types.h:38-47); engine-specific codes start at
+ *    16.  Nothing throws across the ABI (proxylib/proxylib/connection.go:119-135
+ *    recovers panics into PARSER_ERROR; we return codes).
+ *  - Buffers are caller-owned; the library never retains a caller pointer
+ *    after a call returns (proxylib/proxylib.go:46-51 copies strings on entry).
+ *  - Policy updates are all-or-nothing: the new tables are compiled and
+ *    uploaded first, then published by a pointer swap, so a failed update
+ *    leaves the previous snapshot serving (proxylib/proxylib/instance.go:180-215,
+ *    envoy/cilium_network_policy.cc onConfigUpdate).
+ *  - "_dev" verdict calls take DEVICE pointers and a hipStream_t (passed as
+ *    void*, NULL = the handle's stream) and are asynchronous; the "_host"
+ *    variants take host pointers and return when the verdicts are written.
+ *
+ * Each declaration cites the reference interface it replaces.
+ */
+#ifndef CILIUM_GPU_H
+#define CILIUM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Result codes                                                              */
+/* ------------------------------------------------------------------------ */
+typedef enum {
+  CG_OK = 0,                  /* FILTER_OK                 types.h:39 */
+  CG_POLICY_DROP = 1,         /* FILTER_POLICY_DROP        types.h:40 */
+  CG_PARSER_ERROR = 2,        /* FILTER_PARSER_ERROR       types.h:41 */
+  CG_UNKNOWN_PARSER = 3,      /* FILTER_UNKNOWN_PARSER     types.h:42 */
+  CG_UNKNOWN_CONNECTION = 4,  /* FILTER_UNKNOWN_CONNECTION types.h:43 */
+  CG_INVALID_ADDRESS = 5,     /* FILTER_INVALID_ADDRESS    types.h:44 */
+  CG_INVALID_INSTANCE = 6,    /* FILTER_INVALID_INSTANCE   types.h:45 */
+  CG_UNKNOWN_ERROR = 7,       /* FILTER_UNKNOWN_ERROR      types.h:46 */
+  /* engine-specific */
+  CG_INVALID_ARGUMENT = 16,
+  CG_NO_DEVICE = 17,          /* no usable gfx950 device / HIP error at open */
+  CG_DEVICE_ERROR = 18,       /* a HIP call failed */
+  CG_POLICY_REJECTED = 19,    /* policy failed to parse/compile; old snapshot kept */
+  CG_REVISION_MISMATCH = 20,  /* prefilter.go:131-133 "Latest revision is %d not %d" */
+  CG_MAP_FULL = 21,           /* bpf map E2BIG: more keys than max_entries */
+  CG_NOT_FOUND = 22,          /* key/CIDR/policy not present (ENOENT) */
+  CG_NO_MAP = 23,             /* prefilter.go:137-139 "No map enabled for CIDR" */
+  CG_UNSUPPORTED = 24         /* regex construct outside the supported subset */
+} cg_result;
+
+typedef struct {
+  const char* key;
+  const char* value;
+} cg_kv;
+
+/* ------------------------------------------------------------------------ */
+/* Module lifetime — replaces proxylib OpenModule/CloseModule                */
+/* (proxylib/libcilium.h:107-115, proxylib/proxylib.go:118-155).             */
+/* params: "device" = HIP device ordinal (default "0").                      */
+/* Returns 0 on error (same convention as OpenModule).  Host-only work       */
+/* (policy compilation, table builds) works on a handle opened with          */
+/* "device" = "-1" (no GPU); verdict calls on such a handle return           */
+/* CG_NO_DEVICE — there is no CPU fallback.                                  */
+/* ------------------------------------------------------------------------ */
+uint64_t cg_open(const cg_kv* params, size_t n_params, uint8_t debug);
+void cg_close(uint64_t h);
+/* Last error message of the calling thread (static storage, never NULL). */
+const char* cg_last_error(void);
+/* Library/kernels build string, e.g. "libciliumgpu gfx950 r1". */
+const char* cg_version(void);
+
+/* ======================================================================== */
+/* L4: policymap verdicts — bpf/lib/policy.h:46-163                          */
+/* ======================================================================== */
+
+/* struct policy_key, bpf/lib/common.h:180-186; Go PolicyKey,
+ * pkg/maps/policymap/policymap.go:64-69.  dport in NETWORK byte order. */
+typedef struct {
+  uint32_t sec_label;
+  uint16_t dport;     /* network byte order */
+  uint8_t protocol;   /* u8proto: TCP=6, UDP=17 (pkg/u8proto/u8proto.go:27-28) */
+  uint8_t egress;     /* bit0: TrafficDirection Ingress=0/Egress=1 (trafficdirection.go:20-29) */
+} cg_policy_key;
+
+/* struct policy_entry, bpf/lib/common.h:188-193; Go PolicyEntry,
+ * policymap.go:73-80.  proxy_port in NETWORK byte order. */
+typedef struct {
+  uint16_t proxy_port; /* network byte order */
+  uint16_t pad[3];
+  uint64_t packets;
+  uint64_t bytes;
+} cg_policy_entry;
+
+/* One packet to classify: the arguments of __policy_can_access
+ * (bpf/lib/policy.h:46-49) that reach the verdict, packed to 12 bytes. */
+typedef struct {
+  uint32_t identity;   /* sec_label of the remote endpoint */
+  uint16_t dport;      /* network byte order (tuple.dport) */
+  uint8_t proto;       /* tuple.nexthdr */
+  uint8_t flags;       /* CG_L4_F_* */
+  uint32_t len;        /* skb->len, added to policy_entry.bytes on a hit */
+} cg_l4_tuple;
+
+#define CG_L4_F_INGRESS 0x01u   /* dir == CT_INGRESS (common.h:328); else CT_EGRESS */
+#define CG_L4_F_FRAGMENT 0x02u  /* is_fragment */
+#define CG_L4_F_CB_POLICY 0x04u /* skb->cb[CB_POLICY] set (policy.h:98) */
+
+/* Verdict values written per tuple (int32), identical to the return of
+ * __policy_can_access: >0 proxy_port as stored (network order, read as a
+ * host u16), 0 = TC_ACT_OK, DROP_POLICY = -133 (common.h:240),
+ * DROP_FRAG_NOSUPPORT = -157 (common.h:264). */
+#define CG_DROP_POLICY (-133)
+#define CG_DROP_FRAG_NOSUPPORT (-157)
+
+/* Policy maps — one per endpoint, like cilium_policy_<epid>.
+ * max_entries: 0 = PolicyMap MaxEntries 16384 (policymap.go:37). */
+int cg_policymap_create(uint64_t h, uint32_t max_entries, uint32_t* map_id);
+int cg_policymap_destroy(uint64_t h, uint32_t map_id);
+/* PolicyMap.AllowKey/Allow (policymap.go:162-176): insert or update
+ * proxy_port (network order) for each key.  Existing counters are kept.
+ * CG_MAP_FULL if a new key would exceed max_entries (nothing applied). */
+int cg_policymap_allow(uint64_t h, uint32_t map_id, const cg_policy_key* keys,
+                       const uint16_t* proxy_ports_be, size_t n);
+/* PolicyMap.DeleteKey/Delete (policymap.go:187-199); CG_NOT_FOUND if any key
+ * is absent (nothing applied). */
+int cg_policymap_delete(uint64_t h, uint32_t map_id, const cg_policy_key* keys, size_t n);
+/* PolicyMap.Exists + LookupElement (policymap.go:181-185). */
+int cg_policymap_lookup(uint64_t h, uint32_t map_id, const cg_policy_key* key,
+                        cg_policy_entry* entry);
+/* PolicyMap.DumpToSlice (policymap.go:224-255).  Writes up to cap entries,
+ * sets *n to the number of entries in the map. */
+int cg_policymap_dump(uint64_t h, uint32_t map_id, cg_policy_key* keys,
+                      cg_policy_entry* entries, size_t cap, size_t* n);
+/* PolicyMap.Flush (policymap.go:257-280). */
+int cg_policymap_flush(uint64_t h, uint32_t map_id);
+
+/* Batched policy_can_access over tuples (policy.h:46-110).  Counters of the
+ * matching entry advance exactly as the BPF code's __sync_fetch_and_add
+ * (policy.h:68-69,80-81,92-93).  Device pointers, async on stream. */
+int cg_l4_verdicts_dev(uint64_t h, uint32_t map_id, const cg_l4_tuple* d_tuples,
+                       size_t n, int32_t* d_verdicts, void* stream);
+int cg_l4_verdicts_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples,
+                        size_t n, int32_t* verdicts);
+
+/* ======================================================================== */
+/* LPM: XDP CIDR prefilter — bpf/bpf_xdp.c:88-184,                           */
+/* pkg/datapath/prefilter/prefilter.go:57-298                                */
+/* ======================================================================== */
+
+/* A CIDR as the agent holds it (net.IPNet; cidrKey cidrmap.go:52-64). */
+typedef struct {
+  uint8_t family;     /* 4 or 6 */
+  uint8_t prefixlen;  /* ones of the mask */
+  uint8_t pad[2];
+  uint8_t addr[16];   /* network byte order; v4 uses addr[0..3] */
+} cg_cidr;
+
+/* preFilterConfig (prefilter.go:49-54); NewPreFilter default is fix4|fix6
+ * with dyn maps disabled (prefilter.go:281-298). */
+#define CG_PF_DYN4 0x1u
+#define CG_PF_DYN6 0x2u
+#define CG_PF_FIX4 0x4u
+#define CG_PF_FIX6 0x8u
+
+/* XDP verdicts written per address (linux enum xdp_action). */
+#define CG_XDP_DROP 1
+#define CG_XDP_PASS 2
+
+/* NewPreFilter.  max_lpm/max_hash: 0 = maxLKeys 65536 / maxHKeys 20M
+ * (prefilter.go:43-44).  Revision starts at 1 (prefilter.go:291). */
+int cg_prefilter_create(uint64_t h, uint32_t config, uint32_t max_lpm, uint32_t max_hash,
+                        uint32_t* pf_id);
+int cg_prefilter_destroy(uint64_t h, uint32_t pf_id);
+/* PreFilter.Insert (prefilter.go:125-159): revision check (0 = any), per-CIDR
+ * map selection (selectMap :108-122), undo on failure.  *revision_out gets the
+ * new revision on success. */
+int cg_prefilter_insert(uint64_t h, uint32_t pf_id, int64_t revision, const cg_cidr* cidrs,
+                        size_t n, int64_t* revision_out);
+/* PreFilter.Delete (prefilter.go:162-203). */
+int cg_prefilter_delete(uint64_t h, uint32_t pf_id, int64_t revision, const cg_cidr* cidrs,
+                        size_t n, int64_t* revision_out);
+/* PreFilter.Dump (prefilter.go:99-106): entries of dyn4, fix4, dyn6, fix6
+ * in that map order; *n gets the total. */
+int cg_prefilter_dump(uint64_t h, uint32_t pf_id, cg_cidr* out, size_t cap, size_t* n,
+                      int64_t* revision);
+/* The local endpoint set cilium_lxc consulted by check_v{4,6}_endpoint
+ * (bpf_xdp.c:88-95,123-130 → bpf/lib/eps.h:26-46).  Replaces the set. */
+int cg_prefilter_set_endpoints(uint64_t h, uint32_t pf_id, const uint32_t* v4_be, size_t n4,
+                               const uint8_t* v6, size_t n6);
+/* check_v4 / check_v6 (bpf_xdp.c:97-156) over a batch.
+ * v4: n4 records of {saddr, daddr} (u32 each, network order as in iphdr);
+ * v6: n6 records of {saddr[16], daddr[16]}.  out: one CG_XDP_* byte each. */
+int cg_prefilter_verdicts_dev(uint64_t h, uint32_t pf_id, const uint32_t* d_v4, size_t n4,
+                              uint8_t* d_out4, const uint8_t* d_v6, size_t n6, uint8_t* d_out6,
+                              void* stream);
+int cg_prefilter_verdicts_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, size_t n4,
+                               uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6);
+
+/* ======================================================================== */
+/* HTTP L7: Envoy cilium.l7policy — envoy/cilium_network_policy.h:40-237,    */
+/* envoy/cilium_l7policy.cc:127-182                                          */
+/* ======================================================================== */
+
+/* Install the full set of endpoint NetworkPolicies (the NPDS resource list,
+ * envoy/cilium/npds.proto:31-182) given in protobuf-JSON form:
+ *   [{"name": "...", "policy": 3,
+ *     "ingress_per_port_policies": [{"port": 80, "protocol": "TCP",
+ *        "rules": [{"remote_policies": [1],
+ *                   "http_rules": {"http_rules": [{"headers": [
+ *                       {"name": ":path", "regex_match": "..."} |
+ *                       {"name": "...", "exact_match": "..."} |
+ *                       {"name": "...", "present_match": true}]}]}}]}],
+ *     "egress_per_port_policies": [...]}]
+ * Compiles every regex to a minimized union DFA per (policy, direction,
+ * port) and swaps the snapshot in; on any error (regex outside the
+ * supported ECMAScript subset, duplicate port → EnvoyException
+ * "PortNetworkPolicy: Duplicate port number", cilium_network_policy.h:160)
+ * the previous snapshot stays and CG_POLICY_REJECTED is returned. */
+int cg_http_policy_update(uint64_t h, const char* npds_json, size_t len);
+/* Index of a policy name in the installed snapshot (for the packer);
+ * CG_NOT_FOUND → requests naming it are denied (cilium_network_policy.h:232-235). */
+int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index);
+/* Snapshot statistics: programs, DFA parts, total states, table bytes. */
+int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n);
+
+/* Packed request records.  A record is 9 × 16 bytes (1 meta unit + a
+ * 128-byte field slot) stored tile-transposed: requests are grouped in tiles
+ * of 64, and unit u of lane l lives at tile*9216 + u*1024 + l*16, so a
+ * wavefront's 16-byte load of unit u is one contiguous 1 KiB read.
+ * Use cg_http_records_bytes(n) to size the buffer. */
+#define CG_HTTP_TILE 64
+#define CG_HTTP_UNITS 9
+#define CG_HTTP_SLOT_BYTES 128
+size_t cg_http_records_bytes(size_t n);
+
+/* Request flags (meta byte 15).  Meta unit: [0..3] remote identity, [4..5] port,
+ * [6..7] policy index (0xFFFF unknown), [8..11] string length, [12..14] overflow
+ * arena offset / 16, [15] flags. */
+#define CG_HTTP_F_INGRESS 0x01u
+#define CG_HTTP_F_OVERFLOW 0x02u  /* fields in the overflow arena */
+#define CG_HTTP_F_MALFORMED 0x04u /* field holds a byte Envoy's codec rejects */
+#define CG_HTTP_F_PAD 0x08u
+
+/* Pack n requests.  Request i: policy index policy[i] (UINT32_MAX unknown),
+ * direction ingress[i], destination port port[i], remote identity
+ * remote[i] (source identity on ingress, destination on egress,
+ * cilium_l7policy.cc:144-150), and its header list as NUL-separated
+ * "name\0value\0" pairs in hdr_blob[hdr_off[i] .. hdr_off[i+1]).  Header
+ * names compare case-insensitively and only the first value of a name is
+ * seen (Envoy HeaderMap::get).  Records whose slot string exceeds 128 bytes
+ * spill into the overflow arena: pass arena/arena_cap (may be NULL/0 to
+ * query), *arena_used gets the bytes needed. */
+int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* ingress,
+                 const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
+                 const uint64_t* hdr_off, void* records, uint8_t* arena, size_t arena_cap,
+                 size_t* arena_used);
+
+/* NetworkPolicyMap::Allowed per record (cilium_network_policy.h:223-237):
+ * out[i] = 1 allow, 0 deny (→ 403).  d_arena may be NULL when no record
+ * overflowed.  Per-(policy,direction,port) allowed/denied counters advance
+ * (metrics policy_l7_forwarded/denied_total, pkg/metrics/metrics.go:270-296). */
+int cg_http_verdicts_dev(uint64_t h, const void* d_records, size_t n, const uint8_t* d_arena,
+                         uint8_t* d_out, void* stream);
+int cg_http_verdicts_host(uint64_t h, const void* records, size_t n, const uint8_t* arena,
+                          size_t arena_len, uint8_t* out);
+
+/* ======================================================================== */
+/* Kafka L7: pkg/kafka/policy.go:144-225 via pkg/proxy/kafka.go:117-153      */
+/* ======================================================================== */
+
+/* Install Kafka redirect rule sets, JSON form of L7DataMap per redirect:
+ *   [{"name": "...", "selectors": [
+ *       {"identities": [1, 2] or null for the wildcard selector,
+ *        "rules": [{"role": "...", "apiKey": "...", "apiVersion": "...",
+ *                   "clientID": "...", "topic": "..."}]}]}]
+ * Each PortRuleKafka is Sanitize()d (pkg/policy/api/rule_validation.go:232-275);
+ * a failure rejects the whole update. */
+int cg_kafka_policy_update(uint64_t h, const char* json, size_t len);
+int cg_kafka_policy_index(uint64_t h, const char* name, uint32_t* index);
+
+/* Packed Kafka request: 64 bytes. */
+#define CG_KAFKA_MAX_TOPICS 12
+typedef struct {
+  int16_t api_key;      /* RequestMessage.kind */
+  int16_t api_version;  /* RequestMessage.version */
+  uint8_t kind;         /* CG_KAFKA_K_*: which typed request ReadRequest produced */
+  uint8_t n_topics;     /* topics in topic_ids (> CG_KAFKA_MAX_TOPICS: overflow) */
+  uint16_t policy;      /* redirect index (UINT16_MAX unknown → deny) */
+  uint32_t remote;      /* source identity (0 = unknown: wildcard rules only) */
+  uint32_t client_id;   /* interned ClientID (CG_KAFKA_UNKNOWN_STR if not a rule string) */
+  uint32_t topic_ids[CG_KAFKA_MAX_TOPICS]; /* interned topics; overflow: [0] = arena offset */
+} cg_kafka_request;
+
+#define CG_KAFKA_K_NIL 0      /* request == nil (unparsed kinds) */
+#define CG_KAFKA_K_TYPED 1    /* Produce/Fetch/Offset/Metadata/OffsetCommit/OffsetFetch */
+#define CG_KAFKA_K_CONSUMER_METADATA 2
+#define CG_KAFKA_UNKNOWN_STR 0xFFFFFFFFu
+
+/* Intern a string against the installed Kafka snapshot's topic / clientID
+ * dictionaries (what=0 topic, 1 clientID). */
+int cg_kafka_intern(uint64_t h, uint32_t what, const char* s, size_t len, uint32_t* id);
+
+/* kafkaRedirect.canAccess per request: out[i] = 1 allow, 0 deny. */
+int cg_kafka_verdicts_dev(uint64_t h, const cg_kafka_request* d_reqs, size_t n,
+                          const uint32_t* d_arena, uint8_t* d_out, void* stream);
+int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
+                           const uint32_t* arena, size_t arena_len, uint8_t* out);
+
+/* ======================================================================== */
+/* Counters                                                                  */
+/* ======================================================================== */
+/* what: 0 = HTTP per-program {allowed, denied} u64 pairs,
+ *       1 = Kafka per-redirect {allowed, denied} u64 pairs,
+ *       2 = prefilter {drop, pass} u64 pair for pf_or_map.
+ * Writes min(cap, available) u64 values, *n = available. */
+int cg_read_counters(uint64_t h, uint32_t what, uint32_t pf_or_map, uint64_t* out, size_t cap,
+                     size_t* n);
+/* Same, into a device buffer (for an RCCL all-reduce across GPUs). */
+int cg_counters_device_ptr(uint64_t h, uint32_t what, uint32_t pf_or_map, void** d_ptr,
+                           size_t* n);
+/* Async device-to-device copy of up to n counters into d_dst on stream. */
+int cg_counters_copy_dev(uint64_t h, uint32_t what, uint32_t pf_or_map, void* d_dst, size_t n,
+                         void* stream);
+int cg_reset_counters(uint64_t h);
+
+/* Synchronize the handle's stream. */
+int cg_sync(uint64_t h);
+
+/* ======================================================================== */
+/* Diagnostics (CPU test-suite only; no verdict entry point calls these)    */
+/* ======================================================================== */
+/* Compile `re` with the engine's regex compiler and run the DFA on s
+ * (search = 0: full match as std::regex_match; 1: unanchored). */
+int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t len,
+                        uint32_t search, uint8_t* result);
+/* Walk the compiled HTTP / Kafka tables on the host, exactly as the kernels
+ * do, to test the compilers without a GPU. */
+int cg_diag_http_eval_host(uint64_t h, const void* records, size_t n, const uint8_t* arena,
+                           size_t arena_len, uint8_t* out);
+int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
+                            const uint32_t* arena, size_t arena_len, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CILIUM_GPU_H */

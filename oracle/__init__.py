@@ -1,0 +1,201 @@
+"""CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Loaded only by tests/, ``__graft_entry__.smoke()`` and bench.py's
+``cpu_baseline`` leg, as the checker or the timed CPU baseline; never by the
+product (``cilium_amd``).  ``liboracle.so`` (oracle.cc) restates the
+reference algorithms in C++ with libstdc++ std::regex (Envoy's engine);
+``ref_py`` restates them in pure Python for small cases and fixture
+generation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liboracle.so"
+
+
+def build() -> Path:
+    import subprocess
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def _load():
+    if not LIB_PATH.exists():
+        build()
+    lib = C.CDLL(str(LIB_PATH))
+    p, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
+    lib.or_last_error.restype = C.c_char_p
+    lib.or_l4.argtypes = [p, p, sz, p, sz, p, p, p]
+    lib.or_prefilter.argtypes = [u32, p, sz, p, sz, p, sz, p, sz, p, p, sz, p, C.c_int]
+    lib.or_http_load.restype = p
+    lib.or_http_load.argtypes = [C.c_char_p, sz]
+    lib.or_http_free.argtypes = [p]
+    lib.or_http_eval.argtypes = [p, sz, p, p, p, p, p, p, p, C.c_int]
+    lib.or_regex_match.argtypes = [C.c_char_p, sz, p, sz, C.c_int]
+    lib.or_kafka_load.restype = p
+    lib.or_kafka_load.argtypes = [C.c_char_p, sz]
+    lib.or_kafka_free.argtypes = [p]
+    lib.or_kafka_eval.argtypes = [p, sz, p, p, p, p, p, p, p, p, p, C.c_int]
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+# ------------------------------------------------------------------ L4 ----
+def l4(keys: np.ndarray, ports_be: np.ndarray, tuples: np.ndarray):
+    """__policy_can_access over tuples; returns (verdicts, packets, bytes per key)."""
+    keys = np.ascontiguousarray(keys)
+    ports_be = np.ascontiguousarray(ports_be, np.uint16)
+    tuples = np.ascontiguousarray(tuples)
+    out = np.zeros(max(len(tuples), 1), np.int32)
+    pk = np.zeros(max(len(keys), 1), np.uint64)
+    by = np.zeros(max(len(keys), 1), np.uint64)
+    lib().or_l4(_ptr(keys), _ptr(ports_be), len(keys), _ptr(tuples), len(tuples), _ptr(out), _ptr(pk), _ptr(by))
+    return out[:len(tuples)], pk[:len(keys)], by[:len(keys)]
+
+
+# ----------------------------------------------------------------- LPM ----
+def prefilter(config: int, cidrs: np.ndarray, ep4: np.ndarray, ep6: np.ndarray, v4: np.ndarray, v6: np.ndarray,
+              nthreads: int = 1):
+    cidrs = np.ascontiguousarray(cidrs)
+    ep4 = np.ascontiguousarray(ep4, np.uint32)
+    ep6 = np.ascontiguousarray(ep6, np.uint8).reshape(-1)
+    v4 = np.ascontiguousarray(v4, np.uint32).reshape(-1)
+    v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1)
+    n4, n6 = len(v4) // 2, len(v6) // 32
+    o4 = np.zeros(max(n4, 1), np.uint8)
+    o6 = np.zeros(max(n6, 1), np.uint8)
+    lib().or_prefilter(config, _ptr(cidrs), len(cidrs), _ptr(ep4), len(ep4), _ptr(ep6), len(ep6) // 16,
+                       _ptr(v4), n4, _ptr(o4), _ptr(v6), n6, _ptr(o6), nthreads)
+    return o4[:n4], o6[:n6]
+
+
+# ---------------------------------------------------------------- HTTP ----
+def _blob(b: bytes) -> bytes:
+    return str(len(b)).encode() + b" " + b
+
+
+def http_policy_text(policies: list[dict]) -> bytes:
+    """NPDS dicts → the oracle's length-prefixed text format."""
+    from cilium_amd.policy import matcher_kind  # pure-Python helper, no native code
+    out = []
+    for p in policies:
+        out.append(b"policy " + _blob(p["name"].encode()))
+        for d, key in ((1, "ingress_per_port_policies"), (0, "egress_per_port_policies")):
+            out.append(b"dir %d" % d)
+            for pp in p.get(key) or []:
+                proto = pp.get("protocol", "TCP")
+                tcp = 1 if proto in ("TCP", 0) else 0
+                out.append(b"port %d %d" % (int(pp.get("port", 0)), tcp))
+                for r in pp.get("rules") or []:
+                    remotes = [int(x) for x in r.get("remote_policies") or []]
+                    hr = r.get("http_rules")
+                    has_http = 1 if hr is not None else 0
+                    out.append(b"rule %d %d" % (has_http, len(remotes)) +
+                               b"".join(b" %d" % x for x in remotes))
+                    for rule in (hr or {}).get("http_rules") or []:
+                        hs = rule.get("headers") or []
+                        out.append(b"http %d" % len(hs))
+                        for m in hs:
+                            kind, val = matcher_kind(m)
+                            out.append(b"hdr " + kind.encode() + b" " + _blob(m["name"].encode()) + b" " +
+                                       _blob(val.encode()))
+    return b"\n".join(out) + b"\n"
+
+
+class HttpOracle:
+    def __init__(self, policies: list[dict]):
+        txt = http_policy_text(policies)
+        self.h = lib().or_http_load(txt, len(txt))
+        if not self.h:
+            raise ValueError("oracle rejected policy: " + lib().or_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_http_free(self.h)
+
+    def eval(self, policy, ingress, port, remote, hdr_blob, hdr_off, nthreads: int = 1) -> np.ndarray:
+        n = len(policy)
+        policy = np.ascontiguousarray(policy, np.uint32)
+        ingress = np.ascontiguousarray(ingress, np.uint8)
+        port = np.ascontiguousarray(port, np.uint16)
+        remote = np.ascontiguousarray(remote, np.uint32)
+        hdr_blob = np.ascontiguousarray(hdr_blob, np.uint8)
+        if len(hdr_blob) == 0:
+            hdr_blob = np.zeros(1, np.uint8)
+        hdr_off = np.ascontiguousarray(hdr_off, np.uint64)
+        out = np.zeros(max(n, 1), np.uint8)
+        lib().or_http_eval(self.h, n, _ptr(policy), _ptr(ingress), _ptr(port), _ptr(remote), _ptr(hdr_blob),
+                           _ptr(hdr_off), _ptr(out), nthreads)
+        return out[:n]
+
+
+def regex_match(re: bytes, s: bytes, search: bool = False) -> int:
+    """std::regex_match / regex_search (ECMAScript): 1, 0, or -1 for an invalid regex."""
+    buf = np.frombuffer(s, np.uint8) if s else np.zeros(1, np.uint8)
+    return lib().or_regex_match(re, len(re), _ptr(buf), len(s), 1 if search else 0)
+
+
+# --------------------------------------------------------------- Kafka ----
+def kafka_policy_text(redirects: list[dict]) -> bytes:
+    out = []
+    for rd in redirects:
+        out.append(b"redirect " + _blob(rd["name"].encode()))
+        for s in rd.get("selectors", []):
+            ids = s.get("identities")
+            wild = ids is None
+            ids = ids or []
+            out.append(b"sel %d %d" % (1 if wild else 0, len(ids)) + b"".join(b" %d" % int(x) for x in ids))
+            for r in s.get("rules", []):
+                if hasattr(r, "to_json"):
+                    r = r.to_json()
+                out.append(b"krule " + b" ".join(_blob(r.get(k, "").encode())
+                                                for k in ("role", "apiKey", "apiVersion", "clientID", "topic")))
+    return b"\n".join(out) + b"\n"
+
+
+class KafkaOracle:
+    def __init__(self, redirects: list[dict]):
+        txt = kafka_policy_text(redirects)
+        self.h = lib().or_kafka_load(txt, len(txt))
+        if not self.h:
+            raise ValueError("oracle rejected Kafka policy: " + lib().or_last_error().decode())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_kafka_free(self.h)
+
+    def eval(self, redirect, remote, api_key, api_version, kind, client_id, topics, nthreads: int = 1):
+        n = len(redirect)
+        parts, off = [], [0]
+        for i in range(n):
+            b = client_id[i] + b"\0" + b"".join(t + b"\0" for t in topics[i])
+            parts.append(b)
+            off.append(off[-1] + len(b))
+        blob = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()
+        args = [np.ascontiguousarray(redirect, np.uint32), np.ascontiguousarray(remote, np.uint32),
+                np.ascontiguousarray(api_key, np.int16), np.ascontiguousarray(api_version, np.int16),
+                np.ascontiguousarray(kind, np.uint8)]
+        off = np.asarray(off, np.uint64)
+        nt = np.asarray([len(t) for t in topics], np.uint32)
+        out = np.zeros(max(n, 1), np.uint8)
+        lib().or_kafka_eval(self.h, n, *[_ptr(a) for a in args], _ptr(blob), _ptr(off), _ptr(nt), _ptr(out),
+                            nthreads)
+        return out[:n]

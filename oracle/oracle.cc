@@ -1,0 +1,760 @@
+// oracle.cc — CPU restatement of the reference's verdict algorithms.
+//
+// TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg load this library, and only as the checker /
+// the timed CPU baseline.  It shares no code with the product
+// (cilium_amd/csrc): it is written from the reference sources cited below and
+// uses libstdc++'s std::regex (ECMAScript), the engine Envoy's
+// HeaderUtility::matchHeaders used for `regex_match` at the pinned Envoy
+// revision (envoy/WORKSPACE:10-16).
+//
+//   L4    bpf/lib/policy.h:46-110 (__policy_can_access), common.h:180-193
+//   LPM   bpf/bpf_xdp.c:88-178 (check_v4/check_v6), bpf/lib/eps.h:26-46
+//   HTTP  envoy/cilium_network_policy.h:50-203, envoy/cilium_l7policy.cc:127-150
+//   Kafka pkg/kafka/policy.go:27-225, pkg/policy/api/kafka.go:153-293,
+//         pkg/policy/api/rule_validation.go:232-275, pkg/proxy/kafka.go:117-153,
+//         pkg/policy/l4.go:118-141
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <stdexcept>
+#include <map>
+#include <memory>
+#include <regex>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+void run_threads(size_t n, int nthreads, const std::function<void(size_t, size_t)>& f) {
+  if (nthreads <= 1 || n < 1024) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  size_t chunk = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t) {
+    size_t a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    th.emplace_back(f, a, b);
+  }
+  for (auto& t : th) t.join();
+}
+
+// ----------------------------------------------------------------- L4 ----
+// struct policy_key {u32 sec_label; u16 dport; u8 protocol; u8 egress:1,pad:7}
+struct PolicyKey {
+  uint32_t sec_label;
+  uint16_t dport;
+  uint8_t protocol;
+  uint8_t egress_byte;
+  bool operator==(const PolicyKey& o) const {
+    return sec_label == o.sec_label && dport == o.dport && protocol == o.protocol && egress_byte == o.egress_byte;
+  }
+};
+struct PolicyKeyHash {
+  size_t operator()(const PolicyKey& k) const {
+    return std::hash<uint64_t>()((uint64_t)k.sec_label << 32 ^ (uint64_t)k.dport << 16 ^ k.protocol << 8 ^ k.egress_byte);
+  }
+};
+
+constexpr int TC_ACT_OK = 0;
+constexpr int DROP_POLICY = -133;        // common.h:240
+constexpr int DROP_FRAG_NOSUPPORT = -157;  // common.h:264
+constexpr int CT_EGRESS = 0, CT_INGRESS = 1;  // common.h:327-328
+
+struct PolicyEntry {
+  uint16_t proxy_port;  // __be16 as stored
+  uint64_t packets = 0, bytes = 0;
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* or_last_error() { return g_err.c_str(); }
+
+// __policy_can_access for each tuple.  keys: n_keys × 8 bytes (struct
+// policy_key), ports_be: proxy_port as stored.  tuples: 12 bytes
+// {u32 identity, u16 dport(be), u8 proto, u8 flags(1 ingress, 2 frag, 4 cb_policy), u32 len}.
+int or_l4(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const uint8_t* tuples, size_t n,
+          int32_t* out, uint64_t* packets, uint64_t* bytes) {
+  std::unordered_map<PolicyKey, size_t, PolicyKeyHash> map;
+  std::vector<PolicyEntry> ent(n_keys);
+  for (size_t i = 0; i < n_keys; ++i) {
+    PolicyKey k;
+    memcpy(&k.sec_label, keys + 8 * i, 4);
+    memcpy(&k.dport, keys + 8 * i + 4, 2);
+    k.protocol = keys[8 * i + 6];
+    k.egress_byte = keys[8 * i + 7];
+    map[k] = i;  // later duplicates overwrite (BPF_ANY)
+    ent[i].proxy_port = ports_be[i];
+  }
+  auto lookup = [&](const PolicyKey& k) -> PolicyEntry* {
+    auto it = map.find(k);
+    return it == map.end() ? nullptr : &ent[it->second];
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* t = tuples + 12 * i;
+    uint32_t identity, len;
+    uint16_t dport;
+    memcpy(&identity, t, 4);
+    memcpy(&dport, t + 4, 2);
+    uint8_t proto = t[6], flags = t[7];
+    memcpy(&len, t + 8, 4);
+    int dir = (flags & 1) ? CT_INGRESS : CT_EGRESS;
+    bool is_fragment = flags & 2;
+    bool cb_policy = flags & 4;
+    // __policy_can_access, policy.h:46-110
+    PolicyKey key{identity, dport, proto, (uint8_t)(!dir)};
+    PolicyEntry* policy = nullptr;
+    int ret;
+    if (!is_fragment && (policy = lookup(key))) {
+      policy->packets += 1;
+      policy->bytes += len;
+      ret = policy->proxy_port;
+      goto done;
+    }
+    key.dport = 0;
+    key.protocol = 0;
+    if ((policy = lookup(key))) {
+      policy->packets += 1;
+      policy->bytes += len;
+      ret = TC_ACT_OK;
+      goto done;
+    }
+    if (!is_fragment) {
+      key.sec_label = 0;
+      key.dport = dport;
+      key.protocol = proto;
+      if ((policy = lookup(key))) {
+        policy->packets += 1;
+        policy->bytes += len;
+        ret = policy->proxy_port;
+        goto done;
+      }
+    }
+    if (cb_policy)
+      ret = TC_ACT_OK;
+    else if (is_fragment)
+      ret = DROP_FRAG_NOSUPPORT;
+    else
+      ret = DROP_POLICY;
+  done:
+    out[i] = ret;
+  }
+  if (packets)
+    for (size_t i = 0; i < n_keys; ++i) packets[i] = ent[i].packets;
+  if (bytes)
+    for (size_t i = 0; i < n_keys; ++i) bytes[i] = ent[i].bytes;
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- LPM ----
+namespace {
+
+struct AddrKey {
+  uint8_t a[16];
+  bool operator==(const AddrKey& o) const { return memcmp(a, o.a, 16) == 0; }
+};
+struct AddrKeyHash {
+  size_t operator()(const AddrKey& k) const {
+    uint64_t x, y;
+    memcpy(&x, k.a, 8);
+    memcpy(&y, k.a + 8, 8);
+    return std::hash<uint64_t>()(x * 0x9e3779b97f4a7c15ULL ^ y);
+  }
+};
+
+// BPF_MAP_TYPE_LPM_TRIE with a dummy value: lookup of a full-length key hits
+// iff some stored prefix covers it.  One hash set per stored prefix length.
+struct LpmTrie {
+  int bits;
+  std::map<int, std::unordered_set<AddrKey, AddrKeyHash>> by_len;
+  static AddrKey mask(const uint8_t* a, int nbytes, int plen) {
+    AddrKey k{};
+    for (int i = 0; i < nbytes; ++i) {
+      int keep = std::max(0, std::min(8, plen - 8 * i));
+      k.a[i] = keep ? (a[i] & (uint8_t)(0xFF << (8 - keep))) : 0;
+    }
+    return k;
+  }
+  void insert(const uint8_t* a, int plen) { by_len[plen].insert(mask(a, bits / 8, plen)); }
+  bool lookup(const uint8_t* a) const {
+    for (const auto& [plen, set] : by_len)
+      if (set.count(mask(a, bits / 8, plen))) return true;
+    return false;
+  }
+};
+
+constexpr uint8_t XDP_DROP = 1, XDP_PASS = 2;
+
+}  // namespace
+
+extern "C" {
+
+// config bits: 1 dyn4, 2 dyn6, 4 fix4, 8 fix6 (preFilterConfig).  cidrs are
+// 20-byte {family, prefixlen, pad[2], addr[16]} entries already accepted by
+// PreFilter.Insert (dyn: prefixlen < bits, fix: == bits).
+int or_prefilter(uint32_t config, const uint8_t* cidrs, size_t ncidr, const uint32_t* ep4, size_t nep4,
+                 const uint8_t* ep6, size_t nep6, const uint32_t* v4, size_t n4, uint8_t* out4, const uint8_t* v6,
+                 size_t n6, uint8_t* out6, int nthreads) {
+  const bool fix4 = config & 4, dyn4 = config & 1, fix6 = config & 8, dyn6 = config & 2;
+  // node_config: CIDR4_FILTER iff fix4; CIDR4_LPM_PREFILTER iff fix4 && dyn4 (prefilter.go:77-88)
+  const bool cidr4_filter = fix4, cidr4_lpm = fix4 && dyn4;
+  const bool cidr6_filter = fix6, cidr6_lpm = fix6 && dyn6;
+  LpmTrie lmap4{32}, lmap6{128};
+  std::unordered_set<AddrKey, AddrKeyHash> hmap4, hmap6;
+  for (size_t i = 0; i < ncidr; ++i) {
+    const uint8_t* c = cidrs + 20 * i;
+    int fam = c[0], plen = c[1];
+    const uint8_t* a = c + 4;
+    if (fam == 4) {
+      if (plen == 32) hmap4.insert(LpmTrie::mask(a, 4, 32));
+      else lmap4.insert(a, plen);
+    } else {
+      if (plen == 128) hmap6.insert(LpmTrie::mask(a, 16, 128));
+      else lmap6.insert(a, plen);
+    }
+  }
+  // cilium_lxc endpoint map (eps.h:26-46)
+  std::unordered_set<uint32_t> lxc4(ep4, ep4 + nep4);
+  std::unordered_set<AddrKey, AddrKeyHash> lxc6;
+  for (size_t i = 0; i < nep6; ++i) lxc6.insert(LpmTrie::mask(ep6 + 16 * i, 16, 128));
+  run_threads(n4, nthreads, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      uint32_t saddr = v4[2 * i], daddr = v4[2 * i + 1];
+      uint8_t sa[4];
+      memcpy(sa, &saddr, 4);
+      uint8_t v;
+      // check_v4 (bpf_xdp.c:97-121)
+      if (cidr4_filter) {
+        if (cidr4_lpm && lmap4.lookup(sa))
+          v = XDP_DROP;
+        else
+          v = hmap4.count(LpmTrie::mask(sa, 4, 32)) ? XDP_DROP : (lxc4.count(daddr) ? XDP_PASS : XDP_DROP);
+      } else {
+        v = lxc4.count(daddr) ? XDP_PASS : XDP_DROP;
+      }
+      out4[i] = v;
+    }
+  });
+  run_threads(n6, nthreads, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      const uint8_t* sa = v6 + 32 * i;
+      AddrKey da = LpmTrie::mask(v6 + 32 * i + 16, 16, 128);
+      uint8_t v;
+      // check_v6 (bpf_xdp.c:132-156)
+      if (cidr6_filter) {
+        if (cidr6_lpm && lmap6.lookup(sa))
+          v = XDP_DROP;
+        else
+          v = hmap6.count(LpmTrie::mask(sa, 16, 128)) ? XDP_DROP : (lxc6.count(da) ? XDP_PASS : XDP_DROP);
+      } else {
+        v = lxc6.count(da) ? XDP_PASS : XDP_DROP;
+      }
+      out6[i] = v;
+    }
+  });
+  return 0;
+}
+
+}  // extern "C"
+
+// --------------------------------------------------------------- HTTP ----
+namespace {
+
+// Length-prefixed text reader for the policy descriptions tests pass in.
+struct Reader {
+  const char* p;
+  const char* e;
+  bool eof() {
+    while (p < e && (*p == ' ' || *p == '\n')) ++p;
+    return p >= e;
+  }
+  std::string word() {
+    while (p < e && (*p == ' ' || *p == '\n')) ++p;
+    const char* s = p;
+    while (p < e && *p != ' ' && *p != '\n') ++p;
+    return std::string(s, p);
+  }
+  long long num() { return std::stoll(word()); }
+  unsigned long long unum() { return std::stoull(word()); }
+  std::string blob() {
+    size_t n = (size_t)num();
+    ++p;  // one separating space
+    std::string s(p, p + n);
+    p += n;
+    return s;
+  }
+};
+
+std::string lower(std::string s) {
+  for (auto& c : s)
+    if (c >= 'A' && c <= 'Z') c += 'a' - 'A';
+  return s;
+}
+
+// Envoy HeaderUtility::HeaderData (Value / Regex / Present match types).
+struct HeaderData {
+  std::string name;  // LowerCaseString
+  char type;         // 'E' exact, 'R' regex, 'P' present
+  std::string value;
+  std::regex re;
+};
+
+using Headers = std::vector<std::pair<std::string, std::string>>;
+
+const std::string* header_get(const Headers& h, const std::string& name) {
+  for (const auto& kv : h)
+    if (kv.first == name) return &kv.second;  // first entry with that name
+  return nullptr;
+}
+
+// HeaderUtility::matchHeaders: every configured header must match.
+bool match_headers(const Headers& req, const std::vector<HeaderData>& cfg) {
+  for (const HeaderData& d : cfg) {
+    const std::string* v = header_get(req, d.name);
+    if (!v) return false;
+    switch (d.type) {
+      case 'E':
+        if (*v != d.value) return false;
+        break;
+      case 'R':
+        if (!std::regex_match(*v, d.re)) return false;
+        break;
+      default: break;  // present
+    }
+  }
+  return true;
+}
+
+// PortNetworkPolicyRule (cilium_network_policy.h:76-112)
+struct PortRule {
+  std::unordered_set<uint64_t> allowed_remotes;
+  std::vector<std::vector<HeaderData>> http_rules;
+  bool matches(uint64_t remote, const Headers& h) const {
+    if (!allowed_remotes.empty() && !allowed_remotes.count(remote)) return false;
+    if (!http_rules.empty()) {
+      for (const auto& r : http_rules)
+        if (match_headers(h, r)) return true;
+      return false;
+    }
+    return true;
+  }
+};
+
+// PortNetworkPolicyRules (:114-150)
+struct PortRules {
+  std::vector<PortRule> rules;
+  bool have_http_rules = false;
+  bool matches(uint64_t remote, const Headers& h) const {
+    if (!have_http_rules) return true;
+    if (rules.empty()) return true;
+    for (const auto& r : rules)
+      if (r.matches(remote, h)) return true;
+    return false;
+  }
+};
+
+// PortNetworkPolicy (:152-195)
+struct PortPolicy {
+  std::unordered_map<uint32_t, PortRules> rules;
+  bool matches(uint32_t port, uint64_t remote, const Headers& h) const {
+    bool found = false;
+    auto it = rules.find(port);
+    if (it != rules.end()) {
+      if (it->second.matches(remote, h)) return true;
+      found = true;
+    }
+    it = rules.find(0);
+    if (it != rules.end()) {
+      if (it->second.matches(remote, h)) return true;
+      found = true;
+    }
+    return !found;
+  }
+};
+
+struct PolicyInstance {
+  std::string name;
+  PortPolicy dir[2];  // [0] egress, [1] ingress
+};
+
+struct HttpOracle {
+  std::vector<PolicyInstance> policies;
+};
+
+}  // namespace
+
+extern "C" {
+
+// Text format (tests build it from the same NPDS dicts they hand the engine):
+//   policy <len> <name>
+//   dir <0|1>                     (1 = ingress)
+//   port <port> <tcp 0|1>
+//   rule <has_http 0|1> <n> <remote>...
+//   http <nheaders>
+//   hdr <E|R|P> <len> <name> <len> <value>
+void* or_http_load(const char* text, size_t len) {
+  try {
+    auto o = std::make_unique<HttpOracle>();
+    Reader r{text, text + len};
+    PolicyInstance* pol = nullptr;
+    PortPolicy* pp = nullptr;
+    PortRules* prs = nullptr;
+    PortRule* pr = nullptr;
+    std::vector<HeaderData>* hr = nullptr;
+    bool skip_port = false;
+    while (!r.eof()) {
+      std::string w = r.word();
+      if (w == "policy") {
+        o->policies.push_back({});
+        pol = &o->policies.back();
+        pol->name = r.blob();
+      } else if (w == "dir") {
+        pp = &pol->dir[r.num() ? 1 : 0];
+      } else if (w == "port") {
+        uint32_t port = (uint32_t)r.unum();
+        bool tcp = r.num();
+        skip_port = !tcp;  // only TCP policies are installed (:157-165)
+        if (skip_port) {
+          static PortRules sink;
+          sink = PortRules{};
+          prs = &sink;
+          continue;
+        }
+        auto ins = pp->rules.emplace(port, PortRules{});
+        if (!ins.second) throw std::runtime_error("PortNetworkPolicy: Duplicate port number");
+        prs = &ins.first->second;
+      } else if (w == "rule") {
+        bool has_http = r.num();
+        size_t n = (size_t)r.num();
+        prs->rules.push_back({});
+        pr = &prs->rules.back();
+        for (size_t i = 0; i < n; ++i) pr->allowed_remotes.insert(r.unum());
+        if (has_http) prs->have_http_rules = true;
+      } else if (w == "http") {
+        r.num();
+        pr->http_rules.push_back({});
+        hr = &pr->http_rules.back();
+      } else if (w == "hdr") {
+        HeaderData d;
+        d.type = r.word()[0];
+        d.name = lower(r.blob());
+        d.value = r.blob();
+        if (d.type == 'R') d.re = std::regex(d.value, std::regex::optimize);  // may throw: update rejected
+        hr->push_back(std::move(d));
+      } else {
+        throw std::runtime_error("bad oracle policy token " + w);
+      }
+    }
+    return o.release();
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
+void or_http_free(void* h) { delete (HttpOracle*)h; }
+
+// NetworkPolicyMap::Allowed (:223-237) per request.  Headers arrive as
+// "name\0value\0..." pairs; names are lower-cased like Envoy's codec does.
+int or_http_eval(void* h, size_t n, const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                 const uint32_t* remote, const uint8_t* blob, const uint64_t* off, uint8_t* out, int nthreads) {
+  const HttpOracle* o = (const HttpOracle*)h;
+  std::atomic<int> err{0};
+  run_threads(n, nthreads, [&](size_t a, size_t b) {
+    Headers hs;
+    for (size_t i = a; i < b; ++i) {
+      hs.clear();
+      const char* p = (const char*)blob + off[i];
+      const char* e = (const char*)blob + off[i + 1];
+      while (p < e) {
+        const char* nm = p;
+        while (p < e && *p) ++p;
+        std::string name(nm, p);
+        if (p < e) ++p;
+        const char* v = p;
+        while (p < e && *p) ++p;
+        std::string val(v, p);
+        if (p < e) ++p;
+        hs.emplace_back(lower(name), val);
+      }
+      bool malformed = false;
+      for (const auto& kv : hs)
+        for (char c : kv.second)
+          if (c == '\x01') malformed = true;  // a control byte Envoy's codec rejects
+      if (policy[i] >= o->policies.size() || malformed) {
+        out[i] = 0;  // "No policy found for endpoint" → deny (:232-235)
+        continue;
+      }
+      const PolicyInstance& pi = o->policies[policy[i]];
+      out[i] = pi.dir[ingress[i] ? 1 : 0].matches(port[i], remote[i], hs) ? 1 : 0;
+    }
+  });
+  return err;
+}
+
+// std::regex_match (ECMAScript) of s against re: 1/0, or -1 if re is invalid.
+int or_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t len, int search) {
+  try {
+    std::regex rx(std::string(re, re_len));
+    std::string str((const char*)s, len);
+    return (search ? std::regex_search(str, rx) : std::regex_match(str, rx)) ? 1 : 0;
+  } catch (const std::regex_error& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+}  // extern "C"
+
+// -------------------------------------------------------------- Kafka ----
+namespace {
+
+// api/kafka.go:111-142 constants
+enum : int16_t {
+  ProduceKey = 0, FetchKey = 1, OffsetsKey = 2, MetadataKey = 3, LeaderAndIsr = 4, StopReplica = 5,
+  UpdateMetadata = 6, OffsetCommitKey = 8, OffsetFetchKey = 9, FindCoordinatorKey = 10, JoinGroupKey = 11,
+  HeartbeatKey = 12, LeaveGroupKey = 13, SyncgroupKey = 14, APIVersionsKey = 18, CreateTopicsKey = 19,
+  DeleteTopicsKey = 20, DeleteRecordsKey = 21, OffsetForLeaderEpochKey = 23, AddPartitionsToTxnKey = 24,
+  WriteTxnMarkersKey = 27, TxnOffsetCommitKey = 28, AlterReplicaLogDirsKey = 34, DescribeLogDirsKey = 35,
+  CreatePartitionsKey = 37
+};
+
+const std::map<std::string, int16_t>& api_key_map() {
+  static const std::map<std::string, int16_t> m = {
+      {"produce", 0}, {"fetch", 1}, {"offsets", 2}, {"metadata", 3}, {"leaderandisr", 4}, {"stopreplica", 5},
+      {"updatemetadata", 6}, {"controlledshutdown", 7}, {"offsetcommit", 8}, {"offsetfetch", 9},
+      {"findcoordinator", 10}, {"joingroup", 11}, {"heartbeat", 12}, {"leavegroup", 13}, {"syncgroup", 14},
+      {"describegroups", 15}, {"listgroups", 16}, {"saslhandshake", 17}, {"apiversions", 18},
+      {"createtopics", 19}, {"deletetopics", 20}, {"deleterecords", 21}, {"initproducerid", 22},
+      {"offsetforleaderepoch", 23}, {"addpartitionstotxn", 24}, {"addoffsetstotxn", 25}, {"endtxn", 26},
+      {"writetxnmarkers", 27}, {"txnoffsetcommit", 28}, {"describeacls", 29}, {"createacls", 30},
+      {"deleteacls", 31}, {"describeconfigs", 32}, {"alterconfigs", 33}};
+  return m;
+}
+
+struct KafkaRule {  // PortRuleKafka after Sanitize
+  std::string role, apikey, apiversion, clientid, topic;
+  std::vector<int16_t> api_key_int;
+  bool has_version = false;
+  int16_t api_version_int = 0;
+};
+
+bool sanitize(KafkaRule& r) {
+  if (!r.apikey.empty() && !r.role.empty()) return false;
+  if (!r.apikey.empty()) {
+    auto it = api_key_map().find(lower(r.apikey));
+    if (it == api_key_map().end()) return false;
+    r.api_key_int.push_back(it->second);
+  }
+  if (!r.role.empty()) {
+    std::string lr = lower(r.role);
+    if (lr == "produce")
+      r.api_key_int = {ProduceKey, MetadataKey, APIVersionsKey};
+    else if (lr == "consume")
+      r.api_key_int = {FetchKey, OffsetsKey, MetadataKey, OffsetCommitKey, OffsetFetchKey, FindCoordinatorKey,
+                       JoinGroupKey, HeartbeatKey, LeaveGroupKey, SyncgroupKey, APIVersionsKey};
+    else
+      return false;
+  }
+  if (!r.apiversion.empty()) {
+    // strconv.ParseInt(s, 10, 16)
+    const std::string& s = r.apiversion;
+    size_t i = (s[0] == '+' || s[0] == '-') ? 1 : 0;
+    if (i == s.size()) return false;
+    long long v = 0;
+    for (size_t j = i; j < s.size(); ++j) {
+      if (!isdigit((unsigned char)s[j])) return false;
+      v = v * 10 + (s[j] - '0');
+      if (v > 1000000) return false;
+    }
+    if (s[0] == '-') v = -v;
+    if (v < -32768 || v > 32767) return false;
+    r.has_version = true;
+    r.api_version_int = (int16_t)v;
+  }
+  if (!r.topic.empty()) {
+    if (r.topic.size() > 255) return false;
+    static const std::regex valid("^[a-zA-Z0-9\\\\._\\\\-]+$");  // api/kafka.go:244 (Go raw string)
+    if (!std::regex_match(r.topic, valid)) return false;
+  }
+  return true;
+}
+
+bool is_topic_api_key(int16_t kind) {
+  switch (kind) {
+    case ProduceKey: case FetchKey: case OffsetsKey: case MetadataKey: case LeaderAndIsr: case StopReplica:
+    case UpdateMetadata: case OffsetCommitKey: case OffsetFetchKey: case CreateTopicsKey: case DeleteTopicsKey:
+    case DeleteRecordsKey: case OffsetForLeaderEpochKey: case AddPartitionsToTxnKey: case WriteTxnMarkersKey:
+    case TxnOffsetCommitKey: case AlterReplicaLogDirsKey: case DescribeLogDirsKey: case CreatePartitionsKey:
+      return true;
+  }
+  return false;
+}
+
+// RequestMessage as the decoded request reaches MatchesRule.  kind_class:
+// 0 = request == nil, 1 = one of the six typed topic requests, 2 = ConsumerMetadataReq
+struct Request {
+  int16_t kind, version;
+  int kind_class;
+  std::string client_id;
+  std::vector<std::string> topics;
+};
+
+bool check_api_key_role(const KafkaRule& r, int16_t kind) {
+  if (r.api_key_int.empty()) return true;
+  for (int16_t k : r.api_key_int)
+    if (k == kind) return true;
+  return false;
+}
+
+bool rule_matches(const Request& req, const KafkaRule& rule) {
+  if (!check_api_key_role(rule, req.kind)) return false;
+  if (rule.has_version && rule.api_version_int != req.version) return false;
+  if (rule.topic.empty() && rule.clientid.empty()) return true;
+  switch (req.kind_class) {
+    case 1: return rule.clientid.empty() || rule.clientid == req.client_id;  // match*Req
+    case 2: return true;                                                     // ConsumerMetadataReq
+    default: return !(!rule.topic.empty() && is_topic_api_key(req.kind));    // matchNonTopicRequests
+  }
+}
+
+// RequestMessage.MatchesRule (policy.go:200-225), literally.
+bool matches_rule(const Request& req, const std::vector<const KafkaRule*>& rules) {
+  std::map<std::string, bool> topics;
+  for (const auto& t : req.topics) topics[t] = true;
+  for (const KafkaRule* rule : rules) {
+    if (rule->topic.empty() || req.topics.empty()) {
+      if (rule_matches(req, *rule)) return true;
+    } else if (topics.count(rule->topic)) {
+      if (rule_matches(req, *rule)) {
+        topics.erase(rule->topic);
+        if (topics.empty()) return true;
+      }
+    }
+  }
+  return false;
+}
+
+struct Selector {
+  bool wildcard;
+  std::set<uint32_t> ids;
+  std::vector<KafkaRule> rules;
+};
+struct Redirect {
+  std::vector<Selector> sels;
+};
+struct KafkaOracle {
+  std::vector<Redirect> redirects;
+};
+
+}  // namespace
+
+extern "C" {
+
+// Text format:  redirect <len> <name> | sel <wild 0|1> <n> <id>... |
+//               krule <len> <role> <len> <apiKey> <len> <apiVersion> <len> <clientID> <len> <topic>
+void* or_kafka_load(const char* text, size_t len) {
+  auto o = std::make_unique<KafkaOracle>();
+  Reader r{text, text + len};
+  while (!r.eof()) {
+    std::string w = r.word();
+    if (w == "redirect") {
+      r.blob();
+      o->redirects.push_back({});
+    } else if (w == "sel") {
+      Selector s;
+      s.wildcard = r.num();
+      size_t n = (size_t)r.num();
+      for (size_t i = 0; i < n; ++i) s.ids.insert((uint32_t)r.unum());
+      o->redirects.back().sels.push_back(std::move(s));
+    } else if (w == "krule") {
+      KafkaRule k;
+      k.role = r.blob();
+      k.apikey = r.blob();
+      k.apiversion = r.blob();
+      k.clientid = r.blob();
+      k.topic = r.blob();
+      if (!sanitize(k)) {
+        g_err = "Kafka rule failed Sanitize";
+        return nullptr;
+      }
+      o->redirects.back().sels.back().rules.push_back(std::move(k));
+    } else {
+      g_err = "bad kafka oracle token " + w;
+      return nullptr;
+    }
+  }
+  return o.release();
+}
+
+void or_kafka_free(void* h) { delete (KafkaOracle*)h; }
+
+// canAccess per request.  blob holds, per request, clientID\0topic\0topic\0...
+// (ntopics topics).
+int or_kafka_eval(void* h, size_t n, const uint32_t* redirect, const uint32_t* remote, const int16_t* key,
+                  const int16_t* ver, const uint8_t* kind_class, const uint8_t* blob, const uint64_t* off,
+                  const uint32_t* ntopics, uint8_t* out, int nthreads) {
+  const KafkaOracle* o = (const KafkaOracle*)h;
+  run_threads(n, nthreads, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      if (redirect[i] >= o->redirects.size()) {
+        out[i] = 0;
+        continue;
+      }
+      Request req;
+      req.kind = key[i];
+      req.version = ver[i];
+      req.kind_class = kind_class[i];
+      const char* p = (const char*)blob + off[i];
+      const char* e = (const char*)blob + off[i + 1];
+      auto next = [&]() {
+        const char* s = p;
+        while (p < e && *p) ++p;
+        std::string v(s, p);
+        if (p < e) ++p;
+        return v;
+      };
+      req.client_id = next();
+      for (uint32_t t = 0; t < ntopics[i]; ++t) req.topics.push_back(next());
+      // GetRelevantRules (l4.go:118-141): matching selectors, then the wildcard's
+      const Redirect& rd = o->redirects[redirect[i]];
+      std::vector<const KafkaRule*> rules;
+      bool any = false;
+      if (remote[i] != 0)
+        for (const auto& s : rd.sels)
+          if (!s.wildcard && s.ids.count(remote[i]))
+            for (const auto& k : s.rules) {
+              rules.push_back(&k);
+              any = true;
+            }
+      for (const auto& s : rd.sels)
+        if (s.wildcard)
+          for (const auto& k : s.rules) {
+            rules.push_back(&k);
+            any = true;
+          }
+      if (!any) {
+        out[i] = 0;  // "No Kafka rules matching identity, rejecting"
+        continue;
+      }
+      out[i] = matches_rule(req, rules) ? 1 : 0;
+    }
+  });
+  return 0;
+}
+
+}  // extern "C"
