@@ -98,9 +98,10 @@ class Classifier:
         return v.value
 
     def http_policy_stats(self) -> dict:
-        out = (C.c_uint64 * 8)()
-        N.check(N.lib.cg_http_policy_stats(self.h, out, 8))
-        keys = ["programs", "parts", "states", "table_bytes", "fields", "rules", "policies", "remote_slots"]
+        out = (C.c_uint64 * 10)()
+        N.check(N.lib.cg_http_policy_stats(self.h, out, 10))
+        keys = ["programs", "parts", "states", "table_bytes", "fields", "rules", "policies", "remote_slots",
+                "exceptions", "cells"]
         return dict(zip(keys, list(out)))
 
     def pack_http(self, policy: np.ndarray, ingress: np.ndarray, port: np.ndarray, remote: np.ndarray,

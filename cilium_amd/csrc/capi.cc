@@ -545,15 +545,17 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
   return guarded([&] {
     auto e = get(h);
     auto s = http_snap(*e);
-    uint64_t v[8] = {s->progs.size(),
+    uint64_t v[10] = {s->progs.size(),
                      s->parts.size(),
                      s->total_states,
-                     s->trans.size() * 2 + s->acc.size() * 4 + s->masks.size() * 8 + s->clsmap.size(),
+                     s->cells.size() * 4 + s->acc.size() * 4 + s->masks.size() * 8,
                      s->fields.size(),
                      s->total_rules,
                      s->npolicies,
-                     s->rhash_keys.size()};
-    for (size_t i = 0; i < n && i < 8; ++i) out[i] = v[i];
+                     s->rhash_keys.size(),
+                     s->total_exceptions,
+                     s->cells.size()};
+    for (size_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
   });
 }
 

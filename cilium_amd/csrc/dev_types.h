@@ -94,11 +94,13 @@ struct HttpProg {
   uint32_t default_remote;  // u64 word offset of the mask for unlisted remotes
   uint32_t pad0, pad1;
 };
+// One DFA of a program as a comb-packed table (comb.h): states are encoded
+// as base | kind << 14; acc is indexed by base.
 struct HttpPart {
-  uint32_t trans_off;  // u16 entries
-  uint32_t ncls;
-  uint32_t cls_off;    // bytes into clsmap (256 per part)
-  uint32_t acc_off;    // u32 entries: per state, word offset of accept mask or kNoAcc
+  uint32_t cell_off;  // into cells (u32)
+  uint32_t ncells;
+  uint32_t acc_off;   // into acc (u32), indexed by base: mask word offset or kNoAcc
+  uint32_t start;     // start state encoding
   uint32_t nstates;
   uint32_t pad0, pad1, pad2;
 };
@@ -108,8 +110,7 @@ constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
 struct HttpDev {
   const HttpProg* progs;
   const HttpPart* parts;
-  const uint8_t* clsmap;
-  const uint16_t* trans;
+  const uint32_t* cells;
   const uint32_t* acc;
   const unsigned long long* masks;
   // program lookup: key = policy<<17 | ingress<<16 | port
@@ -124,7 +125,6 @@ struct HttpDev {
   uint32_t rhash_mask;
   uint32_t nprogs;
   uint32_t nparts;
-  uint32_t cls_lds_bytes;  // bytes of clsmap staged in LDS (0 = read global)
   unsigned long long* counters;  // [prog*2] allowed, [prog*2+1] denied
 };
 

@@ -32,6 +32,7 @@
 #include <unordered_map>
 
 #include "clsdfa.h"
+#include "comb.h"
 #include "json.h"
 #include "regex.h"
 
@@ -382,6 +383,7 @@ ClsDfa build_union(const FieldDfaCache& fc, const std::vector<URule>& all_rules,
 
 struct PartOut {
   ClsDfa dfa;
+  CombTable comb;
   std::vector<std::vector<uint64_t>> label_masks;
 };
 
@@ -393,7 +395,7 @@ void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, s
   try {
     ClsDfa raw = build_union(fc, all_rules, rules, F, W, p.label_masks);
     p.dfa = minimize_cls(raw);
-    if (p.dfa.size() > kMaxPartStates) ok = false;
+    if (p.dfa.size() > kMaxPartStates || !build_comb(p.dfa, &p.comb)) ok = false;
   } catch (const TooBig&) {
     ok = false;
   }
@@ -519,17 +521,21 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     for (auto& po : parts) {
       HttpPart hp{};
       const ClsDfa& d = po.dfa;
-      hp.ncls = (uint32_t)d.ncls;
+      const CombTable& cb = po.comb;
       hp.nstates = (uint32_t)d.size();
-      hp.cls_off = (uint32_t)S.clsmap.size();
-      S.clsmap.insert(S.clsmap.end(), d.clsmap, d.clsmap + 256);
-      hp.trans_off = (uint32_t)S.trans.size();
-      for (int32_t t : d.trans) S.trans.push_back((uint16_t)t);
+      hp.start = cb.start;
+      hp.cell_off = (uint32_t)S.cells.size();
+      hp.ncells = (uint32_t)cb.cells.size();
+      S.cells.insert(S.cells.end(), cb.cells.begin(), cb.cells.end());
       hp.acc_off = (uint32_t)S.acc.size();
       std::vector<uint32_t> lab_off(po.label_masks.size());
       for (size_t l = 0; l < po.label_masks.size(); ++l) lab_off[l] = add_mask(po.label_masks[l]);
-      for (int s = 0; s < d.size(); ++s) S.acc.push_back(d.label[s] ? lab_off[d.label[s] - 1] : kNoAcc);
+      std::vector<uint32_t> acc_by_base(cb.cells.size(), kNoAcc);
+      for (int s = 1; s < d.size(); ++s)
+        if (d.label[s]) acc_by_base[cb.state_enc[s] & kCombMaxBase] = lab_off[d.label[s] - 1];
+      S.acc.insert(S.acc.end(), acc_by_base.begin(), acc_by_base.end());
       S.total_states += d.size();
+      S.total_exceptions += cb.exceptions;
       S.parts.push_back(hp);
     }
     S.progs.push_back(pg);
@@ -583,9 +589,8 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     }
   }
   if (S.masks.empty()) S.masks.push_back(0);
-  if (S.trans.empty()) S.trans.push_back(0);
+  if (S.cells.empty()) S.cells.push_back(kCombEmpty);
   if (S.acc.empty()) S.acc.push_back(kNoAcc);
-  if (S.clsmap.empty()) S.clsmap.assign(256, 0);
   if (S.progs.empty()) S.progs.push_back(HttpProg{});
   if (S.parts.empty()) S.parts.push_back(HttpPart{});
   if (S.dflt.empty()) S.dflt.push_back(kProgDeny);
@@ -749,12 +754,22 @@ uint8_t http_eval_host(const HttpSnapshot& s, const uint8_t* records, size_t i, 
     if (s.masks[pg.always_off + w] & s.masks[roff + w]) return 1;
   for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
     const HttpPart& pt = s.parts[pg.part_begin + pi];
-    uint32_t st = 1;
+    const uint32_t* cells = s.cells.data() + pt.cell_off;
+    uint32_t st = pt.start;
+    static const bool count_steps = getenv("CG_HTTP_COUNT_STEPS") != nullptr;
+    static uint64_t nsteps = 0, nbytes = 0, nreq = 0;
     for (unsigned char c : str) {
-      st = s.trans[pt.trans_off + st * pt.ncls + s.clsmap[pt.cls_off + c]];
+      if (count_steps) {
+        ++nbytes;
+        if (c == 0 || (st >> 14) != 3) ++nsteps;
+      }
+      st = comb_next(cells, st, c);
       if (!st) break;
     }
-    uint32_t a = s.acc[pt.acc_off + st];
+    if (count_steps && (++nreq % 10000) == 0)
+      fprintf(stderr, "req=%llu bytes/req=%.1f table-steps/req=%.1f\n", (unsigned long long)nreq,
+              (double)nbytes / nreq, (double)nsteps / nreq);
+    uint32_t a = s.acc[pt.acc_off + (st & kCombMaxBase)];
     if (a == kNoAcc) continue;
     for (uint32_t w = 0; w < pg.mask_words; ++w)
       if (s.masks[a + w] & s.masks[roff + w]) return 1;
@@ -766,8 +781,7 @@ void HttpSnapshot::upload(Engine& e) {
   if (!e.has_gpu()) return;
   d_progs.upload_vec(progs);
   d_parts.upload_vec(parts);
-  d_clsmap.upload_vec(clsmap);
-  d_trans.upload_vec(trans);
+  d_cells.upload_vec(cells);
   d_acc.upload_vec(acc);
   d_masks.upload_vec(masks);
   d_phk.upload_vec(phash_keys);
@@ -779,8 +793,7 @@ void HttpSnapshot::upload(Engine& e) {
   d_counters.zero();
   dev.progs = d_progs.as<HttpProg>();
   dev.parts = d_parts.as<HttpPart>();
-  dev.clsmap = d_clsmap.as<uint8_t>();
-  dev.trans = d_trans.as<uint16_t>();
+  dev.cells = d_cells.as<uint32_t>();
   dev.acc = d_acc.as<uint32_t>();
   dev.masks = d_masks.as<unsigned long long>();
   dev.phash_keys = d_phk.as<uint32_t>();
@@ -793,7 +806,6 @@ void HttpSnapshot::upload(Engine& e) {
   dev.rhash_mask = rhash_mask;
   dev.nprogs = (uint32_t)progs.size();
   dev.nparts = (uint32_t)parts.size();
-  dev.cls_lds_bytes = clsmap.size() <= 32768 ? (uint32_t)clsmap.size() : 0;
   dev.counters = d_counters.as<unsigned long long>();
 }
 

@@ -18,8 +18,7 @@ struct HttpSnapshot {
 
   std::vector<HttpProg> progs;
   std::vector<HttpPart> parts;
-  std::vector<uint8_t> clsmap;
-  std::vector<uint16_t> trans;
+  std::vector<uint32_t> cells;
   std::vector<uint32_t> acc;
   std::vector<uint64_t> masks;
   std::vector<uint32_t> phash_keys, phash_vals;
@@ -32,10 +31,10 @@ struct HttpSnapshot {
   std::vector<uint32_t> prog_key;
 
   uint64_t total_states = 0;
+  uint64_t total_exceptions = 0;
   uint64_t total_rules = 0;
 
-  DevMem d_progs, d_parts, d_clsmap, d_trans, d_acc, d_masks, d_phk, d_phv, d_dflt, d_rhk, d_rhv,
-      d_counters;
+  DevMem d_progs, d_parts, d_cells, d_acc, d_masks, d_phk, d_phv, d_dflt, d_rhk, d_rhv, d_counters;
   HttpDev dev{};
 
   void upload(Engine& e);

@@ -266,20 +266,25 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
   return (word >> ((k & 3) * 8)) & 0xFFu;
 }
 
-template <bool kClsLds>
+// One comb-table transition (comb.h): a single dependent 4-byte load, plus
+// a header load only for states whose default is another state.
+__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t st, uint32_t b) {
+  const uint32_t base = st & 0x3FFFu;
+  const uint32_t e = cells[base + b];
+  if ((e & 0xFFFFu) == base) return e >> 16;
+  const uint32_t kind = st >> 14;
+  if (kind == 0) return 0;
+  if (kind == 2) return cells[base - 1] >> 16;
+  return st;  // kind 1 (self default) or 3 (self on all but SEP)
+}
+
 __global__ __launch_bounds__(256) void http_kernel(HttpDev T, const uint4* __restrict__ rec, size_t n,
                                                    const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
                                                    uint32_t lds_counters) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* cls_lds = smem;
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + ((T.cls_lds_bytes + 15) & ~15u));
-  if (kClsLds)
-    for (uint32_t i = threadIdx.x; i < T.cls_lds_bytes / 16; i += blockDim.x)
-      reinterpret_cast<uint4*>(cls_lds)[i] = reinterpret_cast<const uint4*>(T.clsmap)[i];
+  extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   if (lds_counters)
     for (uint32_t i = threadIdx.x; i < 2 * T.nprogs; i += blockDim.x) cnt[i] = 0;
   __syncthreads();
-  const uint8_t* __restrict__ cls = kClsLds ? cls_lds : T.clsmap;
 
   const int lane = threadIdx.x & 63;
   const size_t wave = threadIdx.x >> 6;
@@ -318,23 +323,30 @@ __global__ __launch_bounds__(256) void http_kernel(HttpDev T, const uint4* __res
             decided = false;
             for (uint32_t pi = 0; pi < pg.part_count && !verdict; ++pi) {
               const HttpPart pt = T.parts[pg.part_begin + pi];
-              const uint16_t* __restrict__ tr = T.trans + pt.trans_off;
-              const uint8_t* __restrict__ cm = cls + pt.cls_off;
-              const uint32_t ncls = pt.ncls;
-              uint32_t st = 1;
+              const uint32_t* __restrict__ cells = T.cells + pt.cell_off;
+              uint32_t st = pt.start;
               if (!(flags & CG_HTTP_F_OVERFLOW)) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
+                  // Keep the byte extraction of unit u next to its use: without
+                  // this barrier hipcc hoists all 128 extractions (128 VGPRs).
+                  uint4 w = s[u];
+                  asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
 #pragma unroll
                   for (int k = 0; k < 16; ++k) {
                     const uint32_t p = u * 16 + k;
-                    if (p < len && st != 0) st = tr[st * ncls + cm[get_byte(s[u], k)]];
+                    const uint32_t b = get_byte(w, k);
+                    // kind-3 states loop on every byte but SEP: no table access
+                    if (p < len && st != 0 && (b == 0 || (st >> 14) != 3)) st = comb_step(cells, st, b);
                   }
                 }
               } else {
-                for (uint32_t p = 0; p < len && st != 0; ++p) st = tr[st * ncls + cm[arena[aoff + p]]];
+                for (uint32_t p = 0; p < len && st != 0; ++p) {
+                  const uint32_t b = arena[aoff + p];
+                  if (b == 0 || (st >> 14) != 3) st = comb_step(cells, st, b);
+                }
               }
-              const uint32_t a = T.acc[pt.acc_off + st];
+              const uint32_t a = T.acc[pt.acc_off + (st & 0x3FFFu)];
               if (a != kNoAcc && masks_meet(T.masks, a, rrow, pg.mask_words)) verdict = 1;
             }
             decided = true;
@@ -495,17 +507,12 @@ int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* 
                 void* stream, int cus) {
   if (n == 0) return 0;
   const size_t ntiles = (n + kWave - 1) / kWave;
-  size_t cls_bytes = (t.cls_lds_bytes + 15) & ~(size_t)15;
   size_t cnt_bytes = (size_t)t.nprogs * 2 * sizeof(uint32_t);
-  uint32_t lds_counters = (cls_bytes + cnt_bytes) <= 48 * 1024 ? 1 : 0;
-  size_t lds = cls_bytes + (lds_counters ? cnt_bytes : 0);
+  uint32_t lds_counters = cnt_bytes <= 32 * 1024 ? 1 : 0;
+  size_t lds = lds_counters ? cnt_bytes : 0;
   int grid = grid_for(ntiles, 4, cus, 8);
-  if (t.cls_lds_bytes)
-    hipLaunchKernelGGL(http_kernel<true>, dim3(grid), dim3(256), lds, (hipStream_t)stream, t, (const uint4*)records,
-                       n, arena, out, lds_counters);
-  else
-    hipLaunchKernelGGL(http_kernel<false>, dim3(grid), dim3(256), lds, (hipStream_t)stream, t,
-                       (const uint4*)records, n, arena, out, lds_counters);
+  hipLaunchKernelGGL(http_kernel, dim3(grid), dim3(256), lds, (hipStream_t)stream, t, (const uint4*)records, n,
+                     arena, out, lds_counters);
   return (int)hipGetLastError();
 }
 
