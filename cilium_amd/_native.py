@@ -101,10 +101,12 @@ SIGNATURES = {
     "cg_http_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_http_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_http_policy_stats": (C.c_int, [_u64, C.POINTER(_u64), _sz]),
-    "cg_http_records_bytes": (_sz, [_sz]),
-    "cg_http_pack": (C.c_int, [_u64, _sz, _p, _p, _p, _p, _p, _p, _p, _p, _sz, C.POINTER(_sz)]),
+    "cg_http_batch_bytes": (_sz, [_u64, _sz]),
+    "cg_http_batch_slots": (_sz, [_u64, _sz]),
+    "cg_http_pack": (C.c_int, [_u64, _sz, _p, _p, _p, _p, _p, _p, _p, _sz, _p, C.POINTER(_sz), _p, _sz,
+                               C.POINTER(_sz)]),
     "cg_http_verdicts_dev": (C.c_int, [_u64, _p, _sz, _p, _p, _p]),
-    "cg_http_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
+    "cg_http_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_kafka_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_kafka_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_kafka_intern": (C.c_int, [_u64, _u32, C.c_char_p, _sz, C.POINTER(_u32)]),
@@ -115,7 +117,7 @@ SIGNATURES = {
     "cg_counters_copy_dev": (C.c_int, [_u64, _u32, _u32, _p, _sz, _p]),
     "cg_reset_counters": (C.c_int, [_u64]),
     "cg_diag_regex_match": (C.c_int, [C.c_char_p, _sz, _p, _sz, _u32, C.POINTER(C.c_uint8)]),
-    "cg_diag_http_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
+    "cg_diag_http_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_diag_kafka_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
 }
 

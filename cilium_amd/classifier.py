@@ -41,6 +41,19 @@ def _p(a):
     return N.ptr(a)
 
 
+class HttpBatch:
+    """A packed HTTP batch: ``batch`` bytes (header + chunk table + tiles),
+    overflow ``arena``, ``order[slot]`` = request index (0xFFFFFFFF padding)."""
+
+    def __init__(self, batch: np.ndarray, arena: np.ndarray, order: np.ndarray, nslots: int, n: int):
+        self.batch, self.arena, self.order, self.nslots, self.n = batch, arena, order, nslots, n
+
+    def used_bytes(self) -> int:
+        hdr = self.batch[:64].view(np.uint64)
+        ntiles = int(self.batch[12:16].view(np.uint32)[0])
+        return int(hdr[2]) + ntiles * 64 * N.CG_HTTP_UNITS * 16
+
+
 class Classifier:
     """One engine handle bound to one GPU (``device=-1``: host-only handle that
     can compile policies and pack requests but refuses every verdict call)."""
@@ -117,29 +130,34 @@ class Classifier:
         if len(hdr_blob) == 0:
             hdr_blob = np.zeros(1, np.uint8)
         used = C.c_size_t()
+        nslots = C.c_size_t()
         N.check(N.lib.cg_http_pack(self.h, n, _p(policy), _p(ingress), _p(port), _p(remote), _p(hdr_blob),
-                                   _p(hdr_off), None, None, 0, C.byref(used)))
-        records = np.zeros(N.lib.cg_http_records_bytes(n), np.uint8)
+                                   _p(hdr_off), None, 0, None, C.byref(nslots), None, 0, C.byref(used)))
+        batch = np.zeros(N.lib.cg_http_batch_bytes(self.h, n), np.uint8)
+        order = np.zeros(max(N.lib.cg_http_batch_slots(self.h, n), 1), np.uint32)
         arena = np.zeros(max(used.value, 16), np.uint8)
         N.check(N.lib.cg_http_pack(self.h, n, _p(policy), _p(ingress), _p(port), _p(remote), _p(hdr_blob),
-                                   _p(hdr_off), _p(records), _p(arena), arena.nbytes, C.byref(used)))
-        return records, arena
+                                   _p(hdr_off), _p(batch), batch.nbytes, _p(order), C.byref(nslots), _p(arena),
+                                   arena.nbytes, C.byref(used)))
+        return HttpBatch(batch, arena, order[:nslots.value], nslots.value, n)
 
-    def http_verdicts(self, records: np.ndarray, n: int, arena: Optional[np.ndarray] = None) -> np.ndarray:
-        out = np.zeros(max(n, 1), np.uint8)
-        N.check(N.lib.cg_http_verdicts_host(self.h, _p(records), n, _p(arena), 0 if arena is None else arena.nbytes,
-                                            _p(out)))
-        return out[:n]
+    def http_verdicts(self, b: "HttpBatch") -> np.ndarray:
+        """Verdicts (1 allow / 0 deny) in request order, computed on the GPU."""
+        out = np.zeros(max(b.n, 1), np.uint8)
+        N.check(N.lib.cg_http_verdicts_host(self.h, _p(b.batch), b.nslots, _p(b.order), b.n, _p(b.arena),
+                                            b.arena.nbytes, _p(out)))
+        return out[:b.n]
 
-    def http_verdicts_dev(self, d_records, n: int, d_arena, d_out, stream=None) -> None:
-        N.check(N.lib.cg_http_verdicts_dev(self.h, _p(d_records), n, _p(d_arena), _p(d_out), stream))
+    def http_verdicts_dev(self, d_batch, nslots: int, d_arena, d_out, stream=None) -> None:
+        """Enqueue the verdict kernel on device buffers; d_out is in slot order."""
+        N.check(N.lib.cg_http_verdicts_dev(self.h, _p(d_batch), nslots, _p(d_arena), _p(d_out), stream))
 
-    def http_eval_host_diag(self, records: np.ndarray, n: int, arena: Optional[np.ndarray] = None) -> np.ndarray:
+    def http_eval_host_diag(self, b: "HttpBatch") -> np.ndarray:
         """Compiler diagnostics only: walk the compiled tables on the CPU."""
-        out = np.zeros(max(n, 1), np.uint8)
-        N.check(N.lib.cg_diag_http_eval_host(self.h, _p(records), n, _p(arena),
-                                             0 if arena is None else arena.nbytes, _p(out)))
-        return out[:n]
+        out = np.zeros(max(b.n, 1), np.uint8)
+        N.check(N.lib.cg_diag_http_eval_host(self.h, _p(b.batch), b.nslots, _p(b.order), b.n, _p(b.arena),
+                                             b.arena.nbytes, _p(out)))
+        return out[:b.n]
 
     # ---------------------------------------------------------- Kafka --
     def update_kafka_policy(self, redirects: list[dict]) -> None:

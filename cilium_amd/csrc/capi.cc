@@ -8,6 +8,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "engine.h"
 #include "http.h"
@@ -559,47 +560,77 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
   });
 }
 
-size_t cg_http_records_bytes(size_t n) {
-  return ((n + CG_HTTP_TILE - 1) / CG_HTTP_TILE) * (size_t)CG_HTTP_TILE * CG_HTTP_UNITS * 16;
+size_t cg_http_batch_bytes(uint64_t h, size_t n) {
+  size_t v = 0;
+  guarded([&] {
+    auto e = get(h);
+    v = http_batch_bytes(*http_snap(*e), n);
+  });
+  return v;
+}
+
+size_t cg_http_batch_slots(uint64_t h, size_t n) {
+  size_t v = 0;
+  guarded([&] {
+    auto e = get(h);
+    v = http_batch_slots(*http_snap(*e), n);
+  });
+  return v;
 }
 
 int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
-                 const uint32_t* remote, const uint8_t* hdr_blob, const uint64_t* hdr_off, void* records,
-                 uint8_t* arena, size_t arena_cap, size_t* arena_used) {
+                 const uint32_t* remote, const uint8_t* hdr_blob, const uint64_t* hdr_off, void* batch,
+                 size_t batch_cap, uint32_t* order, size_t* nslots, uint8_t* arena, size_t arena_cap,
+                 size_t* arena_used) {
   return guarded([&] {
     auto e = get(h);
     auto s = http_snap(*e);
-    http_pack(*s, n, policy, ingress, port, remote, hdr_blob, hdr_off, records, arena, arena_cap, arena_used);
+    http_pack(*s, n, policy, ingress, port, remote, hdr_blob, hdr_off, batch, batch_cap, order, nslots, arena,
+              arena_cap, arena_used);
   });
 }
 
-int cg_http_verdicts_dev(uint64_t h, const void* d_records, size_t n, const uint8_t* d_arena, uint8_t* d_out,
+static size_t batch_used_bytes(const void* batch) {
+  HttpBatchHeader hdr;
+  memcpy(&hdr, batch, sizeof(hdr));
+  if (hdr.magic != kBatchMagic) fail(CG_INVALID_ARGUMENT, "not a packed HTTP batch");
+  return hdr.tiles_off + (size_t)hdr.ntiles * CG_HTTP_TILE * CG_HTTP_UNITS * 16;
+}
+
+int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const uint8_t* d_arena, uint8_t* d_out,
                          void* stream) {
   return guarded([&] {
     auto e = get(h);
     e->require_gpu();
     auto s = http_snap(*e);
     e->set_device();
-    check_launch(launch_http(s->dev, d_records, n, d_arena, d_out, stream_of(*e, stream), e->cus),
+    check_launch(launch_http(s->dev, d_batch, nslots, d_arena, d_out, stream_of(*e, stream), e->cus),
                  "http kernel launch");
   });
 }
 
-int cg_http_verdicts_host(uint64_t h, const void* records, size_t n, const uint8_t* arena, size_t arena_len,
-                          uint8_t* out) {
+int cg_http_verdicts_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order, size_t n,
+                          const uint8_t* arena, size_t arena_len, uint8_t* out) {
   return guarded([&] {
     auto e = get(h);
     e->require_gpu();
     auto s = http_snap(*e);
+    HttpBatchHeader hdr;
+    memcpy(&hdr, batch, sizeof(hdr));
+    if (hdr.magic != kBatchMagic || hdr.epoch != s->epoch)
+      fail(CG_INVALID_ARGUMENT, "batch was packed against another policy snapshot");
     e->set_device();
     HostDev r, a, o;
-    void* dr = r.put(records, cg_http_records_bytes(n));
+    void* dr = r.put(batch, batch_used_bytes(batch));
     void* da = a.put(arena, arena ? arena_len : 0);
-    void* dout = o.reserve(n + 1);
-    check_launch(launch_http(s->dev, dr, n, (const uint8_t*)da, (uint8_t*)dout, e->stream, e->cus),
+    void* dout = o.reserve(nslots + 1);
+    check_launch(launch_http(s->dev, dr, nslots, (const uint8_t*)da, (uint8_t*)dout, e->stream, e->cus),
                  "http kernel launch");
     dev_sync(*e, nullptr);
-    if (n) hip_check(hipMemcpy(out, dout, n, hipMemcpyDeviceToHost), "D2H");
+    std::vector<uint8_t> slots(nslots);
+    if (nslots) hip_check(hipMemcpy(slots.data(), dout, nslots, hipMemcpyDeviceToHost), "D2H");
+    for (size_t i = 0; i < nslots; ++i)
+      if (order[i] < n) out[order[i]] = slots[i];
   });
 }
 
@@ -760,12 +791,15 @@ int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t 
   });
 }
 
-int cg_diag_http_eval_host(uint64_t h, const void* records, size_t n, const uint8_t* arena, size_t arena_len,
-                           uint8_t* out) {
+int cg_diag_http_eval_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order, size_t n,
+                           const uint8_t* arena, size_t arena_len, uint8_t* out) {
   return guarded([&] {
     auto e = get(h);
     auto s = http_snap(*e);
-    for (size_t i = 0; i < n; ++i) out[i] = http_eval_host(*s, (const uint8_t*)records, i, arena, arena_len);
+    std::vector<uint8_t> slots(nslots);
+    http_eval_host(*s, (const uint8_t*)batch, arena, arena_len, slots.data());
+    for (size_t i = 0; i < nslots; ++i)
+      if (order[i] < n) out[order[i]] = slots[i];
   });
 }
 

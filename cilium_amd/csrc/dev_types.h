@@ -92,7 +92,8 @@ struct HttpProg {
   uint32_t mask_words;      // W
   uint32_t always_off;      // u64 word offset of the "no HTTP rules" PNPR mask
   uint32_t default_remote;  // u64 word offset of the mask for unlisted remotes
-  uint32_t pad0, pad1;
+  uint32_t cell_begin;      // the program's parts are contiguous in cells[]:
+  uint32_t cell_count;      // staged into LDS as one block
 };
 // One DFA of a program as a comb-packed table (comb.h): states are encoded
 // as base | kind << 14; acc is indexed by base.
@@ -107,6 +108,29 @@ struct HttpPart {
 // Special program ids in the program lookup.
 constexpr uint32_t kProgAllow = 0xFFFFFFFEu;  // no policy for the port → allow
 constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
+
+// Packed HTTP batch (cg_http_pack): a 64-byte header, the chunk table, then
+// tiles of 64 request records (9 × 16-byte units each, unit-major).  The
+// packer groups requests by program so every chunk (≤ kChunkTiles tiles)
+// belongs to one program and a workgroup can stage that program's table in
+// LDS.  Slot order is returned to the caller (order[]).
+constexpr uint32_t kBatchMagic = 0x42484743u;  // "CGHB"
+constexpr uint32_t kChunkTiles = 64;
+struct HttpBatchHeader {
+  uint32_t magic;
+  uint32_t epoch;      // snapshot the batch was packed against
+  uint32_t nchunks;
+  uint32_t ntiles;
+  uint64_t tiles_off;  // byte offset of tile 0 (multiple of 1024)
+  uint64_t nslots;
+  uint32_t pad[8];
+};
+struct HttpChunk {
+  uint32_t prog;
+  uint32_t first_tile;
+  uint32_t ntiles;
+  uint32_t pad;
+};
 struct HttpDev {
   const HttpProg* progs;
   const HttpPart* parts;
@@ -125,7 +149,9 @@ struct HttpDev {
   uint32_t rhash_mask;
   uint32_t nprogs;
   uint32_t nparts;
-  unsigned long long* counters;  // [prog*2] allowed, [prog*2+1] denied
+  uint32_t epoch;
+  uint32_t lds_cells;            // max cells a workgroup stages in LDS
+  unsigned long long* counters;  // [prog*2] allowed, [prog*2+1] denied, [2*nprogs] stale batches
 };
 
 CG_HD inline uint32_t hash32(uint32_t x) {

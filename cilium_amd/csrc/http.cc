@@ -25,6 +25,7 @@
 #include "http.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -416,6 +417,8 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
   std::vector<PolicySpec> pols = parse_npds(json, len);
   auto snap = std::make_shared<HttpSnapshot>();
   HttpSnapshot& S = *snap;
+  static std::atomic<uint32_t> g_epoch{0};
+  S.epoch = ++g_epoch;
   if (pols.size() >= 0x7FFF) fail(CG_POLICY_REJECTED, "too many policies");
 
   // ---- field order
@@ -518,6 +521,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     build_parts(fc, urules, idx, F, W, parts);
     pg.part_begin = (uint32_t)S.parts.size();
     pg.part_count = (uint32_t)parts.size();
+    pg.cell_begin = (uint32_t)S.cells.size();
     for (auto& po : parts) {
       HttpPart hp{};
       const ClsDfa& d = po.dfa;
@@ -538,6 +542,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       S.total_exceptions += cb.exceptions;
       S.parts.push_back(hp);
     }
+    pg.cell_count = (uint32_t)S.cells.size() - pg.cell_begin;
     S.progs.push_back(pg);
     S.prog_key.push_back(key);
     return pid;
@@ -608,175 +613,6 @@ uint32_t HttpSnapshot::lookup_prog(uint32_t policy, bool ingress, uint32_t port)
   return dflt[policy * 2 + (ingress ? 1 : 0)];
 }
 
-// ------------------------------------------------------------- packing ----
-namespace {
-
-inline uint8_t* unit_ptr(void* records, size_t i, int u) {
-  size_t tile = i / CG_HTTP_TILE, lane = i % CG_HTTP_TILE;
-  return (uint8_t*)records + tile * (CG_HTTP_UNITS * CG_HTTP_TILE * 16) + (size_t)u * CG_HTTP_TILE * 16 +
-         lane * 16;
-}
-
-bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
-  if (an != lower_b.size()) return false;
-  for (size_t i = 0; i < an; ++i) {
-    uint8_t c = a[i];
-    if (c >= 'A' && c <= 'Z') c = c - 'A' + 'a';
-    if (c != (uint8_t)lower_b[i]) return false;
-  }
-  return true;
-}
-
-}  // namespace
-
-void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const uint8_t* ingress,
-               const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
-               const uint64_t* hdr_off, void* records, uint8_t* arena, size_t arena_cap,
-               size_t* arena_used) {
-  const size_t F = s.fields.size();
-  size_t used = 0;
-  std::vector<const uint8_t*> vp(F);
-  std::vector<size_t> vl(F);
-  std::string str;
-  size_t ntiles = (n + CG_HTTP_TILE - 1) / CG_HTTP_TILE;
-  // pad lanes of the last tile
-  for (size_t i = n; records && i < ntiles * CG_HTTP_TILE; ++i) {
-    uint8_t* m = unit_ptr(records, i, 0);
-    memset(m, 0, 16);
-    m[15] = CG_HTTP_F_PAD;
-  }
-  for (size_t i = 0; i < n; ++i) {
-    std::fill(vp.begin(), vp.end(), nullptr);
-    const uint8_t* p = hdr_blob + hdr_off[i];
-    const uint8_t* e = hdr_blob + hdr_off[i + 1];
-    while (p < e) {
-      const uint8_t* nm = p;
-      while (p < e && *p) ++p;
-      size_t nl = p - nm;
-      if (p < e) ++p;
-      const uint8_t* v = p;
-      while (p < e && *p) ++p;
-      size_t vlen = p - v;
-      if (p < e) ++p;
-      for (size_t f = 0; f < F; ++f)
-        if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
-          vp[f] = v;
-          vl[f] = vlen;
-        }
-    }
-    str.clear();
-    bool malformed = false;
-    for (size_t f = 0; f < F; ++f) {
-      if (!vp[f]) {
-        str.push_back((char)kAbsent);
-      } else {
-        for (size_t k = 0; k < vl[f]; ++k) {
-          if (vp[f][k] == kAbsent || vp[f][k] == kSep) malformed = true;
-          str.push_back((char)vp[f][k]);
-        }
-      }
-      str.push_back((char)kSep);
-    }
-    // meta: [0..3] remote, [4..5] port, [6..7] policy (0xFFFF unknown),
-    // [8..11] string length, [12..14] arena offset / 16, [15] flags
-    uint8_t meta[16] = {0};
-    memcpy(meta, &remote[i], 4);
-    memcpy(meta + 4, &port[i], 2);
-    uint16_t pol16 = policy[i] >= s.npolicies ? 0xFFFF : (uint16_t)policy[i];
-    memcpy(meta + 6, &pol16, 2);
-    uint8_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0;
-    if (malformed) flags |= CG_HTTP_F_MALFORMED;
-    uint32_t len = (uint32_t)str.size();
-    memcpy(meta + 8, &len, 4);
-    uint8_t slot[CG_HTTP_SLOT_BYTES] = {0};
-    if (len <= CG_HTTP_SLOT_BYTES) {
-      memcpy(slot, str.data(), len);
-    } else {
-      flags |= CG_HTTP_F_OVERFLOW;
-      if (used / 16 >= (1u << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
-      uint32_t off16 = (uint32_t)(used / 16);
-      if (arena && used + len <= arena_cap) memcpy(arena + used, str.data(), len);
-      used += (len + 15) & ~(size_t)15;
-      meta[12] = off16 & 0xFF;
-      meta[13] = (off16 >> 8) & 0xFF;
-      meta[14] = (off16 >> 16) & 0xFF;
-    }
-    meta[15] = flags;
-    if (records) {
-      memcpy(unit_ptr(records, i, 0), meta, 16);
-      for (int u = 0; u < 8; ++u) memcpy(unit_ptr(records, i, u + 1), slot + u * 16, 16);
-    }
-  }
-  if (arena_used) *arena_used = used;
-  if (arena && used > arena_cap) fail(CG_INVALID_ARGUMENT, "overflow arena too small");
-}
-
-uint8_t http_eval_host(const HttpSnapshot& s, const uint8_t* records, size_t i, const uint8_t* arena,
-                       size_t arena_len) {
-  uint8_t meta[16];
-  memcpy(meta, unit_ptr((void*)records, i, 0), 16);
-  uint32_t remote, len;
-  uint16_t port, pol;
-  memcpy(&remote, meta, 4);
-  memcpy(&port, meta + 4, 2);
-  memcpy(&pol, meta + 6, 2);
-  memcpy(&len, meta + 8, 4);
-  uint32_t off = ((uint32_t)meta[12] | ((uint32_t)meta[13] << 8) | ((uint32_t)meta[14] << 16)) * 16u;
-  uint8_t flags = meta[15];
-  if (flags & CG_HTTP_F_PAD) return 0;
-  if (flags & CG_HTTP_F_MALFORMED) return 0;
-  uint32_t prog = pol == 0xFFFF ? kProgDeny : s.lookup_prog(pol, flags & CG_HTTP_F_INGRESS, port);
-  if (prog == kProgDeny) return 0;
-  if (prog == kProgAllow) return 1;
-  const HttpProg& pg = s.progs[prog];
-  if (pg.flags & kProgAllowAll) return 1;
-  std::string str;
-  if (flags & CG_HTTP_F_OVERFLOW) {
-    if ((size_t)off + len > arena_len) return 0;
-    str.assign((const char*)arena + off, len);
-  } else {
-    uint8_t slot[128];
-    for (int u = 0; u < 8; ++u) memcpy(slot + u * 16, unit_ptr((void*)records, i, u + 1), 16);
-    str.assign((const char*)slot, std::min<uint32_t>(len, 128));
-  }
-  // remote mask
-  uint32_t roff = pg.default_remote;
-  uint64_t key = ((uint64_t)prog << 32) | remote;
-  uint32_t h = hash64to32(key) & s.rhash_mask;
-  while (s.rhash_keys[h] != ~0ULL) {
-    if (s.rhash_keys[h] == key) {
-      roff = s.rhash_vals[h];
-      break;
-    }
-    h = (h + 1) & s.rhash_mask;
-  }
-  for (uint32_t w = 0; w < pg.mask_words; ++w)
-    if (s.masks[pg.always_off + w] & s.masks[roff + w]) return 1;
-  for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
-    const HttpPart& pt = s.parts[pg.part_begin + pi];
-    const uint32_t* cells = s.cells.data() + pt.cell_off;
-    uint32_t st = pt.start;
-    static const bool count_steps = getenv("CG_HTTP_COUNT_STEPS") != nullptr;
-    static uint64_t nsteps = 0, nbytes = 0, nreq = 0;
-    for (unsigned char c : str) {
-      if (count_steps) {
-        ++nbytes;
-        if (c == 0 || (st >> 14) != 3) ++nsteps;
-      }
-      st = comb_next(cells, st, c);
-      if (!st) break;
-    }
-    if (count_steps && (++nreq % 10000) == 0)
-      fprintf(stderr, "req=%llu bytes/req=%.1f table-steps/req=%.1f\n", (unsigned long long)nreq,
-              (double)nbytes / nreq, (double)nsteps / nreq);
-    uint32_t a = s.acc[pt.acc_off + (st & kCombMaxBase)];
-    if (a == kNoAcc) continue;
-    for (uint32_t w = 0; w < pg.mask_words; ++w)
-      if (s.masks[a + w] & s.masks[roff + w]) return 1;
-  }
-  return 0;
-}
-
 void HttpSnapshot::upload(Engine& e) {
   if (!e.has_gpu()) return;
   d_progs.upload_vec(progs);
@@ -789,7 +625,7 @@ void HttpSnapshot::upload(Engine& e) {
   d_dflt.upload_vec(dflt);
   d_rhk.upload_vec(rhash_keys);
   d_rhv.upload_vec(rhash_vals);
-  d_counters.alloc(std::max<size_t>(progs.size(), 1) * 2 * sizeof(uint64_t));
+  d_counters.alloc((std::max<size_t>(progs.size(), 1) * 2 + 1) * sizeof(uint64_t));
   d_counters.zero();
   dev.progs = d_progs.as<HttpProg>();
   dev.parts = d_parts.as<HttpPart>();
@@ -806,6 +642,8 @@ void HttpSnapshot::upload(Engine& e) {
   dev.rhash_mask = rhash_mask;
   dev.nprogs = (uint32_t)progs.size();
   dev.nparts = (uint32_t)parts.size();
+  dev.epoch = epoch;
+  dev.lds_cells = 16384;  // 64 KiB of LDS per workgroup
   dev.counters = d_counters.as<unsigned long long>();
 }
 

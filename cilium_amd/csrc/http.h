@@ -30,6 +30,7 @@ struct HttpSnapshot {
   // (policy, ingress, port) of each program, for counter attribution
   std::vector<uint32_t> prog_key;
 
+  uint32_t epoch = 0;
   uint64_t total_states = 0;
   uint64_t total_exceptions = 0;
   uint64_t total_rules = 0;
@@ -43,15 +44,21 @@ struct HttpSnapshot {
 
 std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len);
 
-// Pack requests into tile-transposed records (see include/cilium_gpu.h).
+// Upper bounds of a packed batch of n requests (slots, bytes).
+size_t http_batch_slots(const HttpSnapshot& s, size_t n);
+size_t http_batch_bytes(const HttpSnapshot& s, size_t n);
+
+// Pack requests into a program-grouped batch (dev_types.h HttpBatchHeader).
+// order[slot] = request index, or UINT32_MAX for a padding slot.
 void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const uint8_t* ingress,
                const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
-               const uint64_t* hdr_off, void* records, uint8_t* arena, size_t arena_cap,
-               size_t* arena_used);
+               const uint64_t* hdr_off, void* batch, size_t batch_cap, uint32_t* order, size_t* nslots,
+               uint8_t* arena, size_t arena_cap, size_t* arena_used);
 
-// Walk the snapshot's tables on the host exactly as the kernel does
-// (diagnostics / compiler tests only; the verdict API never calls this).
-uint8_t http_eval_host(const HttpSnapshot& s, const uint8_t* records, size_t i, const uint8_t* arena,
-                       size_t arena_len);
+// Walk the snapshot's tables on the host exactly as the kernel does, for
+// every slot of a batch (diagnostics / compiler tests only; the verdict API
+// never calls this).  out has one byte per slot.
+void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* arena, size_t arena_len,
+                    uint8_t* out);
 
 }  // namespace cg

@@ -1,0 +1,252 @@
+// http_pack.cc — program-grouped request batches and the host table walker.
+//
+// The packer resolves each request's program on the host (the lookup the
+// reference does per request in PortNetworkPolicy::Matches,
+// envoy/cilium_network_policy.h:169-192), groups requests by program and
+// pads every group to whole 64-request tiles, so each chunk of tiles has one
+// program whose comb table a workgroup stages in LDS.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+
+#include "comb.h"
+#include "http.h"
+
+namespace cg {
+
+namespace {
+
+constexpr uint8_t kSep = 0x00;
+constexpr uint8_t kAbsent = 0x01;
+constexpr size_t kTileBytes = (size_t)CG_HTTP_UNITS * CG_HTTP_TILE * 16;
+
+inline uint8_t* unit_ptr(uint8_t* tiles, size_t slot, int u) {
+  size_t tile = slot / CG_HTTP_TILE, lane = slot % CG_HTTP_TILE;
+  return tiles + tile * kTileBytes + (size_t)u * CG_HTTP_TILE * 16 + lane * 16;
+}
+
+bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
+  if (an != lower_b.size()) return false;
+  for (size_t i = 0; i < an; ++i) {
+    uint8_t c = a[i];
+    if (c >= 'A' && c <= 'Z') c = c - 'A' + 'a';
+    if (c != (uint8_t)lower_b[i]) return false;
+  }
+  return true;
+}
+
+size_t max_groups(const HttpSnapshot& s, size_t n) { return std::min(n, s.progs.size() + 2); }
+
+size_t header_bytes(size_t max_tiles) {
+  size_t b = sizeof(HttpBatchHeader) + sizeof(HttpChunk) * max_tiles;
+  return (b + 1023) & ~(size_t)1023;
+}
+
+}  // namespace
+
+size_t http_batch_slots(const HttpSnapshot& s, size_t n) {
+  return ((n + CG_HTTP_TILE - 1) / CG_HTTP_TILE + max_groups(s, n)) * CG_HTTP_TILE;
+}
+
+size_t http_batch_bytes(const HttpSnapshot& s, size_t n) {
+  size_t tiles = http_batch_slots(s, n) / CG_HTTP_TILE;
+  return header_bytes(tiles) + tiles * kTileBytes;
+}
+
+void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const uint8_t* ingress,
+               const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
+               const uint64_t* hdr_off, void* batch, size_t batch_cap, uint32_t* order, size_t* nslots_out,
+               uint8_t* arena, size_t arena_cap, size_t* arena_used) {
+  // ---- program of every request, groups in ascending program id
+  std::vector<uint32_t> prog(n);
+  std::map<uint32_t, size_t> count;
+  for (size_t i = 0; i < n; ++i) {
+    prog[i] = policy[i] >= s.npolicies ? kProgDeny : s.lookup_prog(policy[i], ingress[i] != 0, port[i]);
+    count[prog[i]]++;
+  }
+  std::map<uint32_t, size_t> first_slot;
+  std::vector<HttpChunk> chunks;
+  size_t tiles = 0;
+  for (auto& [p, c] : count) {
+    first_slot[p] = tiles * CG_HTTP_TILE;
+    size_t t = (c + CG_HTTP_TILE - 1) / CG_HTTP_TILE;
+    for (size_t k = 0; k < t; k += kChunkTiles)
+      chunks.push_back({p, (uint32_t)(tiles + k), (uint32_t)std::min<size_t>(kChunkTiles, t - k), 0});
+    tiles += t;
+  }
+  const size_t nslots = tiles * CG_HTTP_TILE;
+  if (nslots_out) *nslots_out = nslots;
+  const size_t hdr = header_bytes(http_batch_slots(s, n) / CG_HTTP_TILE);
+  const size_t need = hdr + tiles * kTileBytes;
+  if (batch && need > batch_cap) fail(CG_INVALID_ARGUMENT, "batch buffer too small");
+  uint8_t* tb = batch ? (uint8_t*)batch + hdr : nullptr;
+  if (batch) {
+    HttpBatchHeader h{};
+    h.magic = kBatchMagic;
+    h.epoch = s.epoch;
+    h.nchunks = (uint32_t)chunks.size();
+    h.ntiles = (uint32_t)tiles;
+    h.tiles_off = hdr;
+    h.nslots = nslots;
+    memcpy(batch, &h, sizeof(h));
+    memcpy((uint8_t*)batch + sizeof(h), chunks.data(), chunks.size() * sizeof(HttpChunk));
+    // padding slots of every group
+    for (auto& [p, c] : count) {
+      size_t s0 = first_slot[p];
+      size_t end = s0 + ((c + CG_HTTP_TILE - 1) / CG_HTTP_TILE) * CG_HTTP_TILE;
+      for (size_t sl = s0 + c; sl < end; ++sl) {
+        uint8_t* m = unit_ptr(tb, sl, 0);
+        memset(m, 0, 16);
+        m[15] = CG_HTTP_F_PAD;
+        for (int u = 1; u < CG_HTTP_UNITS; ++u) memset(unit_ptr(tb, sl, u), 0, 16);
+        if (order) order[sl] = 0xFFFFFFFFu;
+      }
+    }
+  }
+  std::map<uint32_t, size_t> next = first_slot;
+  const size_t F = s.fields.size();
+  size_t used = 0;
+  std::vector<const uint8_t*> vp(F);
+  std::vector<size_t> vl(F);
+  std::string str;
+  for (size_t i = 0; i < n; ++i) {
+    size_t sl = next[prog[i]]++;
+    if (order) order[sl] = (uint32_t)i;
+    if (!batch && !arena_used) continue;
+    std::fill(vp.begin(), vp.end(), nullptr);
+    const uint8_t* p = hdr_blob + hdr_off[i];
+    const uint8_t* e = hdr_blob + hdr_off[i + 1];
+    while (p < e) {
+      const uint8_t* nm = p;
+      while (p < e && *p) ++p;
+      size_t nl = p - nm;
+      if (p < e) ++p;
+      const uint8_t* v = p;
+      while (p < e && *p) ++p;
+      size_t vlen = p - v;
+      if (p < e) ++p;
+      for (size_t f = 0; f < F; ++f)
+        if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
+          vp[f] = v;
+          vl[f] = vlen;
+        }
+    }
+    str.clear();
+    bool malformed = false;
+    for (size_t f = 0; f < F; ++f) {
+      if (!vp[f]) {
+        str.push_back((char)kAbsent);
+      } else {
+        for (size_t k = 0; k < vl[f]; ++k) {
+          if (vp[f][k] == kAbsent || vp[f][k] == kSep) malformed = true;
+          str.push_back((char)vp[f][k]);
+        }
+      }
+      str.push_back((char)kSep);
+    }
+    // meta: [0..3] remote, [4..5] port, [6..7] policy (0xFFFF unknown),
+    // [8..11] string length, [12..14] arena offset / 16, [15] flags
+    uint8_t meta[16] = {0};
+    memcpy(meta, &remote[i], 4);
+    memcpy(meta + 4, &port[i], 2);
+    uint16_t pol16 = policy[i] >= s.npolicies ? 0xFFFF : (uint16_t)policy[i];
+    memcpy(meta + 6, &pol16, 2);
+    uint8_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0;
+    if (malformed) flags |= CG_HTTP_F_MALFORMED;
+    uint32_t len = (uint32_t)str.size();
+    memcpy(meta + 8, &len, 4);
+    uint8_t slot[CG_HTTP_SLOT_BYTES] = {0};
+    if (len <= CG_HTTP_SLOT_BYTES) {
+      memcpy(slot, str.data(), len);
+    } else {
+      flags |= CG_HTTP_F_OVERFLOW;
+      if (used / 16 >= (1u << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
+      uint32_t off16 = (uint32_t)(used / 16);
+      if (arena && used + len <= arena_cap) memcpy(arena + used, str.data(), len);
+      used += (len + 15) & ~(size_t)15;
+      meta[12] = off16 & 0xFF;
+      meta[13] = (off16 >> 8) & 0xFF;
+      meta[14] = (off16 >> 16) & 0xFF;
+    }
+    meta[15] = flags;
+    if (batch) {
+      memcpy(unit_ptr(tb, sl, 0), meta, 16);
+      for (int u = 0; u < 8; ++u) memcpy(unit_ptr(tb, sl, u + 1), slot + u * 16, 16);
+    }
+  }
+  if (arena_used) *arena_used = used;
+  if (arena && used > arena_cap) fail(CG_INVALID_ARGUMENT, "overflow arena too small");
+}
+
+void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* arena, size_t arena_len,
+                    uint8_t* out) {
+  HttpBatchHeader h;
+  memcpy(&h, batch, sizeof(h));
+  if (h.magic != kBatchMagic || h.epoch != s.epoch) fail(CG_INVALID_ARGUMENT, "batch packed for another snapshot");
+  const HttpChunk* chunks = (const HttpChunk*)(batch + sizeof(h));
+  uint8_t* tb = (uint8_t*)batch + h.tiles_off;
+  for (uint32_t c = 0; c < h.nchunks; ++c) {
+    const uint32_t prog = chunks[c].prog;
+    for (size_t sl = (size_t)chunks[c].first_tile * CG_HTTP_TILE;
+         sl < (size_t)(chunks[c].first_tile + chunks[c].ntiles) * CG_HTTP_TILE; ++sl) {
+      uint8_t meta[16];
+      memcpy(meta, unit_ptr(tb, sl, 0), 16);
+      uint32_t remote, len;
+      memcpy(&remote, meta, 4);
+      memcpy(&len, meta + 8, 4);
+      uint32_t off = ((uint32_t)meta[12] | ((uint32_t)meta[13] << 8) | ((uint32_t)meta[14] << 16)) * 16u;
+      const uint8_t flags = meta[15];
+      uint8_t v = 0;
+      out[sl] = 0;
+      if (flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED)) continue;
+      if (prog == kProgDeny) continue;
+      if (prog == kProgAllow) {
+        out[sl] = 1;
+        continue;
+      }
+      const HttpProg& pg = s.progs[prog];
+      if (pg.flags & kProgAllowAll) {
+        out[sl] = 1;
+        continue;
+      }
+      std::string str;
+      if (flags & CG_HTTP_F_OVERFLOW) {
+        if ((size_t)off + len > arena_len) continue;
+        str.assign((const char*)arena + off, len);
+      } else {
+        uint8_t slot[128];
+        for (int u = 0; u < 8; ++u) memcpy(slot + u * 16, unit_ptr(tb, sl, u + 1), 16);
+        str.assign((const char*)slot, std::min<uint32_t>(len, 128));
+      }
+      uint32_t roff = pg.default_remote;
+      uint64_t key = ((uint64_t)prog << 32) | remote;
+      uint32_t hh = hash64to32(key) & s.rhash_mask;
+      while (s.rhash_keys[hh] != ~0ULL) {
+        if (s.rhash_keys[hh] == key) {
+          roff = s.rhash_vals[hh];
+          break;
+        }
+        hh = (hh + 1) & s.rhash_mask;
+      }
+      for (uint32_t w = 0; w < pg.mask_words; ++w)
+        if (s.masks[pg.always_off + w] & s.masks[roff + w]) v = 1;
+      for (uint32_t pi = 0; pi < pg.part_count && !v; ++pi) {
+        const HttpPart& pt = s.parts[pg.part_begin + pi];
+        const uint32_t* cells = s.cells.data() + pt.cell_off;
+        uint32_t st = pt.start;
+        for (unsigned char ch : str) {
+          st = comb_next(cells, st, ch);
+          if (!st) break;
+        }
+        uint32_t a = s.acc[pt.acc_off + (st & kCombMaxBase)];
+        if (a == kNoAcc) continue;
+        for (uint32_t w = 0; w < pg.mask_words; ++w)
+          if (s.masks[a + w] & s.masks[roff + w]) v = 1;
+      }
+      out[sl] = v;
+    }
+  }
+}
+
+}  // namespace cg

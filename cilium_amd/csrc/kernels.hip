@@ -224,154 +224,6 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
   }
 }
 
-// ============================================================= HTTP ======
-// NetworkPolicyMap::Allowed (envoy/cilium_network_policy.h:223-237) per
-// record; one lane per request, records tile-transposed so every unit load of
-// a wavefront is one contiguous 1 KiB read.
-
-__device__ __forceinline__ uint32_t prog_lookup(const HttpDev& T, uint32_t pol, uint32_t ingress, uint32_t port) {
-  if (pol >= T.npolicies) return kProgDeny;
-  const uint32_t key = (pol << 17) | (ingress << 16) | port;
-  uint32_t h = hash32(key) & T.phash_mask;
-  for (uint32_t probe = 0; probe <= T.phash_mask; ++probe) {
-    uint32_t k = T.phash_keys[h];
-    if (k == key) return T.phash_vals[h];
-    if (k == 0xFFFFFFFFu) break;
-    h = (h + 1) & T.phash_mask;
-  }
-  return T.dflt[pol * 2 + ingress];
-}
-
-__device__ __forceinline__ uint32_t remote_row(const HttpDev& T, uint32_t prog, uint32_t remote, uint32_t dflt) {
-  const unsigned long long key = ((unsigned long long)prog << 32) | remote;
-  uint32_t h = hash64to32(key) & T.rhash_mask;
-  for (uint32_t probe = 0; probe <= T.rhash_mask; ++probe) {
-    unsigned long long k = T.rhash_keys[h];
-    if (k == key) return T.rhash_vals[h];
-    if (k == ~0ULL) break;
-    h = (h + 1) & T.rhash_mask;
-  }
-  return dflt;
-}
-
-__device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
-                                           uint32_t w) {
-  for (uint32_t i = 0; i < w; ++i)
-    if (m[a + i] & m[b + i]) return true;
-  return false;
-}
-
-__device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
-  const uint32_t word = (k < 4) ? w.x : (k < 8) ? w.y : (k < 12) ? w.z : w.w;
-  return (word >> ((k & 3) * 8)) & 0xFFu;
-}
-
-// One comb-table transition (comb.h): a single dependent 4-byte load, plus
-// a header load only for states whose default is another state.
-__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t st, uint32_t b) {
-  const uint32_t base = st & 0x3FFFu;
-  const uint32_t e = cells[base + b];
-  if ((e & 0xFFFFu) == base) return e >> 16;
-  const uint32_t kind = st >> 14;
-  if (kind == 0) return 0;
-  if (kind == 2) return cells[base - 1] >> 16;
-  return st;  // kind 1 (self default) or 3 (self on all but SEP)
-}
-
-__global__ __launch_bounds__(256) void http_kernel(HttpDev T, const uint4* __restrict__ rec, size_t n,
-                                                   const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                                   uint32_t lds_counters) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
-  if (lds_counters)
-    for (uint32_t i = threadIdx.x; i < 2 * T.nprogs; i += blockDim.x) cnt[i] = 0;
-  __syncthreads();
-
-  const int lane = threadIdx.x & 63;
-  const size_t wave = threadIdx.x >> 6;
-  const size_t waves_per_block = blockDim.x >> 6;
-  const size_t ntiles = (n + kWave - 1) / kWave;
-  for (size_t tile = blockIdx.x * waves_per_block + wave; tile < ntiles; tile += gridDim.x * waves_per_block) {
-    const uint4* tb = rec + tile * (CG_HTTP_UNITS * kWave);
-    const uint4 meta = tb[lane];
-    uint4 s[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] = tb[(u + 1) * kWave + lane];
-    const size_t idx = tile * kWave + lane;
-    const uint32_t remote = meta.x;
-    const uint32_t port = meta.y & 0xFFFF;
-    const uint32_t pol = meta.y >> 16;
-    const uint32_t len = meta.z;
-    const uint32_t flags = meta.w >> 24;
-    const uint32_t aoff = (meta.w & 0xFFFFFF) * 16u;
-    const uint32_t ingress = flags & CG_HTTP_F_INGRESS;
-    uint32_t verdict = 0;
-    uint32_t prog = kProgDeny;
-    bool decided = true;
-    if (!(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED)) && pol != 0xFFFF) {
-      prog = prog_lookup(T, pol, ingress, port);
-      if (prog == kProgAllow) {
-        verdict = 1;
-      } else if (prog != kProgDeny) {
-        const HttpProg pg = T.progs[prog];
-        if (pg.flags & kProgAllowAll) {
-          verdict = 1;
-        } else {
-          const uint32_t rrow = remote_row(T, prog, remote, pg.default_remote);
-          if (masks_meet(T.masks, pg.always_off, rrow, pg.mask_words)) {
-            verdict = 1;
-          } else {
-            decided = false;
-            for (uint32_t pi = 0; pi < pg.part_count && !verdict; ++pi) {
-              const HttpPart pt = T.parts[pg.part_begin + pi];
-              const uint32_t* __restrict__ cells = T.cells + pt.cell_off;
-              uint32_t st = pt.start;
-              if (!(flags & CG_HTTP_F_OVERFLOW)) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                  // Keep the byte extraction of unit u next to its use: without
-                  // this barrier hipcc hoists all 128 extractions (128 VGPRs).
-                  uint4 w = s[u];
-                  asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
-#pragma unroll
-                  for (int k = 0; k < 16; ++k) {
-                    const uint32_t p = u * 16 + k;
-                    const uint32_t b = get_byte(w, k);
-                    // kind-3 states loop on every byte but SEP: no table access
-                    if (p < len && st != 0 && (b == 0 || (st >> 14) != 3)) st = comb_step(cells, st, b);
-                  }
-                }
-              } else {
-                for (uint32_t p = 0; p < len && st != 0; ++p) {
-                  const uint32_t b = arena[aoff + p];
-                  if (b == 0 || (st >> 14) != 3) st = comb_step(cells, st, b);
-                }
-              }
-              const uint32_t a = T.acc[pt.acc_off + (st & 0x3FFFu)];
-              if (a != kNoAcc && masks_meet(T.masks, a, rrow, pg.mask_words)) verdict = 1;
-            }
-            decided = true;
-          }
-        }
-      }
-    }
-    (void)decided;
-    if (idx < n) {
-      out[idx] = (uint8_t)verdict;
-      if (prog < T.nprogs) {
-        if (lds_counters)
-          atomicAdd(&cnt[prog * 2 + (verdict ? 0 : 1)], 1u);
-        else
-          atomicAdd(&T.counters[prog * 2 + (verdict ? 0 : 1)], 1ULL);
-      }
-    }
-  }
-  if (lds_counters) {
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 2 * T.nprogs; i += blockDim.x)
-      if (cnt[i]) atomicAdd(&T.counters[i], (unsigned long long)cnt[i]);
-  }
-}
-
 // ============================================================ Kafka ======
 // kafkaRedirect.canAccess → RequestMessage.MatchesRule
 // (pkg/proxy/kafka.go:117-153, pkg/kafka/policy.go:144-225).
@@ -500,19 +352,6 @@ int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n
   if (n4 + n6 == 0) return 0;
   hipLaunchKernelGGL(lpm_kernel, dim3(grid_for(n4 + n6, 256, cus, 8)), dim3(256), 0, (hipStream_t)stream, t, v4f,
                      v6f, (const uint2*)v4, n4, out4, (const uint4*)v6, n6, out6);
-  return (int)hipGetLastError();
-}
-
-int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
-                void* stream, int cus) {
-  if (n == 0) return 0;
-  const size_t ntiles = (n + kWave - 1) / kWave;
-  size_t cnt_bytes = (size_t)t.nprogs * 2 * sizeof(uint32_t);
-  uint32_t lds_counters = cnt_bytes <= 32 * 1024 ? 1 : 0;
-  size_t lds = lds_counters ? cnt_bytes : 0;
-  int grid = grid_for(ntiles, 4, cus, 8);
-  hipLaunchKernelGGL(http_kernel, dim3(grid), dim3(256), lds, (hipStream_t)stream, t, (const uint4*)records, n,
-                     arena, out, lds_counters);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,199 @@
+// kernels_http.hip — HTTP L7 verdict kernel (gfx950).
+//
+// NetworkPolicyMap::Allowed (envoy/cilium_network_policy.h:223-237) for every
+// slot of a program-grouped batch (http_pack.cc).  One workgroup takes one
+// chunk of ≤ kChunkTiles tiles of a single program: it stages the program's
+// comb-packed DFA (comb.h) into LDS once, then each wavefront walks 64
+// requests at a time, one lane per request.  Records are tile-transposed, so
+// each of a wave's nine 16-byte unit loads is one contiguous 1 KiB read; the
+// DFA walk itself touches only LDS (one ds_read_b32 per byte, none inside
+// fields whose automaton is a self loop).
+#include <hip/hip_runtime.h>
+
+#include "../../include/cilium_gpu.h"
+#include "dev_types.h"
+#include "kernels.h"
+
+namespace cg {
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kHttpThreads = 512;
+
+__device__ __forceinline__ uint32_t remote_row(const HttpDev& T, uint32_t prog, uint32_t remote, uint32_t dflt) {
+  const unsigned long long key = ((unsigned long long)prog << 32) | remote;
+  uint32_t h = hash64to32(key) & T.rhash_mask;
+  for (uint32_t probe = 0; probe <= T.rhash_mask; ++probe) {
+    const unsigned long long k = T.rhash_keys[h];
+    if (k == key) return T.rhash_vals[h];
+    if (k == ~0ULL) break;
+    h = (h + 1) & T.rhash_mask;
+  }
+  return dflt;
+}
+
+__device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
+                                           uint32_t w) {
+  for (uint32_t i = 0; i < w; ++i)
+    if (m[a + i] & m[b + i]) return true;
+  return false;
+}
+
+__device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
+  const uint32_t word = (k < 4) ? w.x : (k < 8) ? w.y : (k < 12) ? w.z : w.w;
+  return (word >> ((k & 3) * 8)) & 0xFFu;
+}
+
+// One comb transition (comb.h).  kind 3 states are never stepped on a non-SEP
+// byte (the caller skips them).
+__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t st, uint32_t b) {
+  const uint32_t base = st & 0x3FFFu;
+  const uint32_t e = cells[base + b];
+  if ((e & 0xFFFFu) == base) return e >> 16;
+  const uint32_t kind = st >> 14;
+  if (kind == 0) return 0;
+  if (kind == 2) return cells[base - 1] >> 16;
+  return st;
+}
+
+// Walk the record string through one part's table; returns the final state.
+__device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ cells, uint32_t st, const uint4 (&s)[8],
+                                        uint32_t len, bool overflow, const uint8_t* __restrict__ arena,
+                                        uint32_t aoff) {
+  if (!overflow) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      // keep unit u's byte extraction next to its use (else hipcc hoists all
+      // 128 extractions into 128 VGPRs)
+      uint4 w = s[u];
+      asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t p = u * 16 + k;
+        const uint32_t b = get_byte(w, k);
+        if (p < len && st != 0 && (b == 0 || (st >> 14) != 3)) st = comb_step(cells, st, b);
+      }
+      if (!__any((u + 1) * 16 < (int)len && st != 0)) break;
+    }
+  } else {
+    for (uint32_t p = 0; p < len && st != 0; ++p) {
+      const uint32_t b = arena[aoff + p];
+      if (b == 0 || (st >> 14) != 3) st = comb_step(cells, st, b);
+    }
+  }
+  return st;
+}
+
+// One tile of 64 requests of program `prog` (a real, non-trivial program).
+template <bool kLds>
+__device__ __forceinline__ void http_tile(const HttpDev& T, const HttpProg& pg, uint32_t prog,
+                                          const uint32_t* __restrict__ pcells, const uint4* __restrict__ tb,
+                                          const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
+                                          size_t slot, uint32_t lane, uint32_t* n_allow, uint32_t* n_deny) {
+  const uint4 meta = tb[lane];
+  uint4 s[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s[u] = tb[(u + 1) * kWave + lane];
+  const uint32_t remote = meta.x;
+  const uint32_t len = meta.z;
+  const uint32_t flags = meta.w >> 24;
+  const uint32_t aoff = (meta.w & 0xFFFFFFu) * 16u;
+  const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+  uint32_t verdict = 0;
+  if (counted) {
+    const uint32_t rrow = remote_row(T, prog, remote, pg.default_remote);
+    if (masks_meet(T.masks, pg.always_off, rrow, pg.mask_words)) verdict = 1;
+    for (uint32_t pi = 0; pi < pg.part_count && !verdict; ++pi) {
+      const HttpPart pt = T.parts[pg.part_begin + pi];
+      const uint32_t* __restrict__ cells = pcells + (pt.cell_off - pg.cell_begin);
+      const uint32_t st = walk(cells, pt.start, s, len, flags & CG_HTTP_F_OVERFLOW, arena, aoff);
+      const uint32_t a = T.acc[pt.acc_off + (st & 0x3FFFu)];
+      if (a != kNoAcc && masks_meet(T.masks, a, rrow, pg.mask_words)) verdict = 1;
+    }
+  }
+  out[slot] = (uint8_t)verdict;
+  *n_allow += counted && verdict;
+  *n_deny += counted && !verdict;
+}
+
+__global__ __launch_bounds__(kHttpThreads) void http_kernel(HttpDev T, const uint8_t* __restrict__ batch,
+                                                            size_t nslots, const uint8_t* __restrict__ arena,
+                                                            uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
+  const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
+  const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
+  const uint64_t toff = H->tiles_off;
+  if (magic != kBatchMagic || epoch != T.epoch || (size_t)ntiles * kWave > nslots) {
+    // packed against another snapshot (or not a batch): deny every slot
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (size_t)gridDim.x * blockDim.x)
+      out[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&T.counters[2 * T.nprogs], 1ULL);
+    return;
+  }
+  const HttpChunk* chunks = reinterpret_cast<const HttpChunk*>(batch + sizeof(HttpBatchHeader));
+  const uint4* tiles = reinterpret_cast<const uint4*>(batch + toff);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const HttpChunk ch = chunks[c];
+    if (ch.first_tile + ch.ntiles > ntiles || ch.ntiles > kChunkTiles) continue;  // malformed chunk
+    const uint32_t prog = ch.prog;
+    const bool real = prog < T.nprogs;
+    HttpProg pg{};
+    if (real) pg = T.progs[prog];
+    const bool walkp = real && !(pg.flags & kProgAllowAll);
+    const bool lds = walkp && pg.cell_count <= T.lds_cells;
+    uint32_t n_allow = 0, n_deny = 0;
+    __syncthreads();  // the previous chunk is done with lcells
+    if (lds)
+      for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
+    __syncthreads();
+    for (uint32_t t = ch.first_tile + wave; t < ch.first_tile + ch.ntiles; t += nw) {
+      const uint4* tb = tiles + (size_t)t * (CG_HTTP_UNITS * kWave);
+      const size_t slot = (size_t)t * kWave + lane;
+      if (!walkp) {
+        // no policy for the port → allow; unknown policy → deny; a scope
+        // without HTTP rules → allow (cilium_network_policy.h:129-138,187-191)
+        const uint32_t flags = tb[lane].w >> 24;
+        const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+        const uint32_t v = counted && (prog == kProgAllow || real) ? 1u : 0u;
+        out[slot] = (uint8_t)v;
+        n_allow += real && counted;
+      } else if (lds) {
+        http_tile<true>(T, pg, prog, lcells, tb, arena, out, slot, lane, &n_allow, &n_deny);
+      } else {
+        http_tile<false>(T, pg, prog, T.cells + pg.cell_begin, tb, arena, out, slot, lane, &n_allow, &n_deny);
+      }
+    }
+    if (real) {
+      // wave totals → two atomics per wave per chunk
+      for (int o = 32; o > 0; o >>= 1) {
+        n_allow += __shfl_down(n_allow, o, kWave);
+        n_deny += __shfl_down(n_deny, o, kWave);
+      }
+      if (lane == 0) {
+        if (n_allow) atomicAdd(&T.counters[2 * prog], (unsigned long long)n_allow);
+        if (n_deny) atomicAdd(&T.counters[2 * prog + 1], (unsigned long long)n_deny);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_t* arena, uint8_t* out, void* stream,
+                int cus) {
+  if (nslots == 0) return 0;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    attr = true;
+  }
+  size_t tiles = nslots / kWave;
+  size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
+  hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), (size_t)t.lds_cells * 4,
+                     (hipStream_t)stream, t, (const uint8_t*)batch, nslots, arena, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace cg

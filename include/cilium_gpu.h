@@ -231,15 +231,24 @@ int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index);
 /* Snapshot statistics: programs, DFA parts, total states, table bytes. */
 int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n);
 
-/* Packed request records.  A record is 9 × 16 bytes (1 meta unit + a
- * 128-byte field slot) stored tile-transposed: requests are grouped in tiles
- * of 64, and unit u of lane l lives at tile*9216 + u*1024 + l*16, so a
- * wavefront's 16-byte load of unit u is one contiguous 1 KiB read.
- * Use cg_http_records_bytes(n) to size the buffer. */
+/* Packed request batches.  A record is 9 × 16 bytes (1 meta unit + a
+ * 128-byte field slot); records are stored tile-transposed in tiles of 64
+ * (unit u of lane l at tile*9216 + u*1024 + l*16), so a wavefront's 16-byte
+ * load of unit u is one contiguous 1 KiB read.  The packer resolves each
+ * request's (policy, direction, port) evaluation program on the host and
+ * groups requests by program (padding each group to whole tiles), so a
+ * workgroup stages one program's DFA in LDS.  A batch is a 64-byte header,
+ * a chunk table, then the tiles; slots are in grouped order and order[slot]
+ * gives the request index (UINT32_MAX for padding).  Size the buffers with
+ * cg_http_batch_bytes / cg_http_batch_slots (upper bounds for n requests
+ * under the installed policy; a batch is tied to the snapshot it was
+ * packed against — after a policy update it is rejected and every slot is
+ * denied). */
 #define CG_HTTP_TILE 64
 #define CG_HTTP_UNITS 9
 #define CG_HTTP_SLOT_BYTES 128
-size_t cg_http_records_bytes(size_t n);
+size_t cg_http_batch_bytes(uint64_t h, size_t n);
+size_t cg_http_batch_slots(uint64_t h, size_t n);
 
 /* Request flags (meta byte 15).  Meta unit: [0..3] remote identity, [4..5] port,
  * [6..7] policy index (0xFFFF unknown), [8..11] string length, [12..14] overflow
@@ -257,20 +266,24 @@ size_t cg_http_records_bytes(size_t n);
  * names compare case-insensitively and only the first value of a name is
  * seen (Envoy HeaderMap::get).  Records whose slot string exceeds 128 bytes
  * spill into the overflow arena: pass arena/arena_cap (may be NULL/0 to
- * query), *arena_used gets the bytes needed. */
+ * query), *arena_used gets the bytes needed.  *nslots gets the batch's slot
+ * count; order must hold cg_http_batch_slots(h, n) entries. */
 int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* ingress,
                  const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
-                 const uint64_t* hdr_off, void* records, uint8_t* arena, size_t arena_cap,
-                 size_t* arena_used);
+                 const uint64_t* hdr_off, void* batch, size_t batch_cap, uint32_t* order,
+                 size_t* nslots, uint8_t* arena, size_t arena_cap, size_t* arena_used);
 
-/* NetworkPolicyMap::Allowed per record (cilium_network_policy.h:223-237):
- * out[i] = 1 allow, 0 deny (→ 403).  d_arena may be NULL when no record
- * overflowed.  Per-(policy,direction,port) allowed/denied counters advance
- * (metrics policy_l7_forwarded/denied_total, pkg/metrics/metrics.go:270-296). */
-int cg_http_verdicts_dev(uint64_t h, const void* d_records, size_t n, const uint8_t* d_arena,
+/* NetworkPolicyMap::Allowed per slot (cilium_network_policy.h:223-237):
+ * d_out[slot] = 1 allow, 0 deny (→ 403), in batch slot order.  d_arena may
+ * be NULL when no record overflowed.  Per-(policy,direction,port) allowed/
+ * denied counters advance (metrics policy_l7_forwarded/denied_total,
+ * pkg/metrics/metrics.go:270-296). */
+int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const uint8_t* d_arena,
                          uint8_t* d_out, void* stream);
-int cg_http_verdicts_host(uint64_t h, const void* records, size_t n, const uint8_t* arena,
-                          size_t arena_len, uint8_t* out);
+/* Host convenience: uploads the batch, runs the kernel and writes out[i]
+ * for request i (un-permuting through order). */
+int cg_http_verdicts_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
+                          size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out);
 
 /* ======================================================================== */
 /* Kafka L7: pkg/kafka/policy.go:144-225 via pkg/proxy/kafka.go:117-153      */
@@ -343,8 +356,8 @@ int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t 
                         uint32_t search, uint8_t* result);
 /* Walk the compiled HTTP / Kafka tables on the host, exactly as the kernels
  * do, to test the compilers without a GPU. */
-int cg_diag_http_eval_host(uint64_t h, const void* records, size_t n, const uint8_t* arena,
-                           size_t arena_len, uint8_t* out);
+int cg_diag_http_eval_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
+                           size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out);
 int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
                             const uint32_t* arena, size_t arena_len, uint8_t* out);
 

@@ -133,9 +133,9 @@ def test_prefilter_edges(gpu):
 # ---------------------------------------------------------------- HTTP ----
 def _http_check(cl, pols, rq):
     cl.update_http_policy(pols)
-    rec, arena = cl.pack_http(**rq)
+    b = cl.pack_http(**rq)
     n = len(rq["policy"])
-    got = cl.http_verdicts(rec, n, arena)
+    got = cl.http_verdicts(b)
     exp = oracle.HttpOracle(pols).eval(**rq, nthreads=8)
     assert np.array_equal(got, exp)
     return got
@@ -172,8 +172,8 @@ def test_http_counters(gpu):
     pols = synth.starwars_policy()
     rq = synth.starwars_requests(10_000, seed=5)
     gpu.update_http_policy(pols)
-    rec, arena = gpu.pack_http(**rq)
-    got = gpu.http_verdicts(rec, len(rq["policy"]), arena)
+    b = gpu.pack_http(**rq)
+    got = gpu.http_verdicts(b)
     c = gpu.read_counters(0)
     # every request maps to a program (port 80) or to "no policy for port" (8080)
     on80 = rq["port"] == 80
