@@ -119,6 +119,8 @@ SIGNATURES = {
     "cg_diag_regex_match": (C.c_int, [C.c_char_p, _sz, _p, _sz, _u32, C.POINTER(C.c_uint8)]),
     "cg_diag_http_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_diag_kafka_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
+    "cg_diag_l4_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p]),
+    "cg_diag_prefilter_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
 }
 
 

@@ -324,6 +324,13 @@ class PolicyMap:
     def verdicts_dev(self, d_tuples, n: int, d_out, stream=None) -> None:
         N.check(N.lib.cg_l4_verdicts_dev(self.cl.h, self.id, _p(d_tuples), n, _p(d_out), stream))
 
+    def eval_host_diag(self, tuples: np.ndarray) -> np.ndarray:
+        """Table-builder diagnostics only: walk the cuckoo table on the CPU."""
+        tuples = np.ascontiguousarray(tuples, L4_TUPLE_DTYPE)
+        out = np.zeros(max(len(tuples), 1), np.int32)
+        N.check(N.lib.cg_diag_l4_eval_host(self.cl.h, self.id, _p(tuples), len(tuples), _p(out)))
+        return out[:len(tuples)]
+
 
 def parse_cidr(s: str) -> np.ndarray:
     """net.ParseCIDR → (family, ones, network) in the cg_cidr layout."""
@@ -395,6 +402,16 @@ class PreFilter:
         o6 = np.zeros(max(len(v6), 1), np.uint8)
         N.check(N.lib.cg_prefilter_verdicts_host(self.cl.h, self.id, _p(v4), len(v4), _p(o4), _p(v6), len(v6),
                                                  _p(o6)))
+        return o4[:len(v4)], o6[:len(v6)]
+
+    def eval_host_diag(self, v4: np.ndarray, v6: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """Table-builder diagnostics only: walk the LPM tables on the CPU."""
+        v4 = np.ascontiguousarray(v4, np.uint32).reshape(-1, 2)
+        v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1, 32)
+        o4 = np.zeros(max(len(v4), 1), np.uint8)
+        o6 = np.zeros(max(len(v6), 1), np.uint8)
+        N.check(N.lib.cg_diag_prefilter_eval_host(self.cl.h, self.id, _p(v4), len(v4), _p(o4), _p(v6), len(v6),
+                                                  _p(o6)))
         return o4[:len(v4)], o6[:len(v6)]
 
     def verdicts_dev(self, d_v4, n4: int, d_o4, d_v6, n6: int, d_o6, stream=None) -> None:

@@ -803,6 +803,104 @@ int cg_diag_http_eval_host(uint64_t h, const void* batch, size_t nslots, const u
   });
 }
 
+// Cuckoo lookup exactly as l4_kernel does it.
+static bool l4_lookup_host(const PolicyMapState& m, uint64_t key, uint32_t* val) {
+  for (uint64_t h : {l4_hash1(key), l4_hash2(key)}) {
+    const L4Slot* b = m.slots.data() + (size_t)((uint32_t)h & m.bucket_mask) * 4;
+    for (int s = 0; s < 4; ++s)
+      if (b[s].key == key) {
+        *val = b[s].val;
+        return true;
+      }
+  }
+  return false;
+}
+
+int cg_diag_l4_eval_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* t, size_t n, int32_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PolicyMapState& m = get_map(*e, map_id);
+    if (m.dirty) m.rebuild(*e);
+    for (size_t i = 0; i < n; ++i) {
+      const bool frag = t[i].flags & CG_L4_F_FRAGMENT;
+      const uint64_t eg = (t[i].flags & CG_L4_F_INGRESS) ? 0 : 1;
+      uint32_t val = 0;
+      int which = 0;
+      if (!frag && l4_lookup_host(m, (uint64_t)t[i].identity | ((uint64_t)t[i].dport << 32) |
+                                         ((uint64_t)t[i].proto << 48) | (eg << 56), &val))
+        which = 1;
+      else if (l4_lookup_host(m, (uint64_t)t[i].identity | (eg << 56), &val))
+        which = 2;
+      else if (!frag && l4_lookup_host(m, ((uint64_t)t[i].dport << 32) | ((uint64_t)t[i].proto << 48) | (eg << 56),
+                                       &val))
+        which = 3;
+      if (which == 1 || which == 3) out[i] = (int32_t)(val >> 16);
+      else if (which == 2 || (t[i].flags & CG_L4_F_CB_POLICY)) out[i] = 0;
+      else out[i] = frag ? CG_DROP_FRAG_NOSUPPORT : CG_DROP_POLICY;
+    }
+  });
+}
+
+// The prefilter tables walked exactly as lpm_kernel does.
+int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, size_t n4, uint8_t* out4,
+                                const uint8_t* v6, size_t n6, uint8_t* out6) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    PrefilterState& p = get_pf(*e, pf_id);
+    if (p.dirty) p.rebuild(*e);
+    auto ep4 = [&](uint32_t a) {
+      uint32_t mask = (uint32_t)p.ep4_occ.size() - 1, hh = ep_hash32(a) & mask;
+      for (uint32_t k = 0; k <= mask; ++k, hh = (hh + 1) & mask) {
+        if (!p.ep4_occ[hh]) return false;
+        if (p.ep4_keys[hh] == a) return true;
+      }
+      return false;
+    };
+    auto ep6 = [&](uint64_t hi, uint64_t lo) {
+      uint32_t mask = (uint32_t)p.ep6_occ.size() - 1, hh = ep_hash128(hi, lo) & mask;
+      for (uint32_t k = 0; k <= mask; ++k, hh = (hh + 1) & mask) {
+        if (!p.ep6_occ[hh]) return false;
+        if (p.ep6_keys[2 * hh] == hi && p.ep6_keys[2 * hh + 1] == lo) return true;
+      }
+      return false;
+    };
+    auto be64 = [](const uint8_t* a) {
+      uint64_t x = 0;
+      for (int i = 0; i < 8; ++i) x = x << 8 | a[i];
+      return x;
+    };
+    for (size_t i = 0; i < n4; ++i) {
+      uint32_t s = __builtin_bswap32(v4[2 * i]);
+      bool drop = false;
+      if (p.v4_filter) {
+        uint32_t en = p.dir24[s >> 8];
+        drop = en < 2 ? en == 1 : ((p.leaves[(size_t)(en - 2) * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1);
+      }
+      if (!drop) drop = !ep4(v4[2 * i + 1]);
+      out4[i] = drop ? CG_XDP_DROP : CG_XDP_PASS;
+    }
+    for (size_t i = 0; i < n6; ++i) {
+      uint64_t hi = be64(v6 + 32 * i), lo = be64(v6 + 32 * i + 8);
+      bool drop = false;
+      if (p.v6_filter) {
+        int64_t L = p.v6_idx[hi >> 48], cnt = p.v6_idx[65536], R = std::min<int64_t>(p.v6_idx[(hi >> 48) + 1], cnt - 1);
+        int64_t ans = -1;
+        while (L <= R) {
+          int64_t mid = (L + R) >> 1;
+          std::pair<uint64_t, uint64_t> lo_m{p.v6_lo[2 * mid], p.v6_lo[2 * mid + 1]};
+          if (!(std::make_pair(hi, lo) < lo_m)) ans = mid, L = mid + 1;
+          else R = mid - 1;
+        }
+        drop = ans >= 0 && !(std::make_pair(p.v6_hi[2 * ans], p.v6_hi[2 * ans + 1]) < std::make_pair(hi, lo));
+      }
+      if (!drop) drop = !ep6(be64(v6 + 32 * i + 16), be64(v6 + 32 * i + 24));
+      out6[i] = drop ? CG_XDP_DROP : CG_XDP_PASS;
+    }
+  });
+}
+
 int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n, const uint32_t* arena,
                             size_t arena_len, uint8_t* out) {
   return guarded([&] {

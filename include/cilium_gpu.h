@@ -360,6 +360,10 @@ int cg_diag_http_eval_host(uint64_t h, const void* batch, size_t nslots, const u
                            size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out);
 int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
                             const uint32_t* arena, size_t arena_len, uint8_t* out);
+int cg_diag_l4_eval_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, size_t n,
+                         int32_t* verdicts);
+int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, size_t n4,
+                                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6);
 
 #ifdef __cplusplus
 }
