@@ -392,7 +392,12 @@ int cg_prefilter_insert(uint64_t h, uint32_t pf_id, int64_t revision, const cg_c
         break;
       }
       uint32_t cap = (which == 0 || which == 2) ? p.max_lpm : p.max_hash;
-      if (p.maps[which].count(k)) continue;  // BPF_ANY update of an existing key
+      if (p.maps[which].count(k)) {
+        // BPF_ANY update of an existing key succeeds, and Insert still queues
+        // it for undo: a later failure deletes it (prefilter.go:141-158).
+        undo.push_back({which, k});
+        continue;
+      }
       if (p.maps[which].size() >= cap) {
         err = CG_MAP_FULL;
         msg = "Error inserting CIDR string: map full";

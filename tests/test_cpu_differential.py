@@ -1,0 +1,222 @@
+"""Randomized differential tests on the CPU: the engine's compilers (regex →
+DFA, NPDS → union DFAs, Kafka rule compiler, L4/LPM table builders), walked
+by the host diagnostic walkers, against the oracle on seeded random inputs.
+The GPU kernels are checked against the same oracle in test_gpu_parity.py."""
+import ctypes as C
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from cilium_amd import _native as N
+from cilium_amd import synth
+
+# ------------------------------------------------------------------ regex ---
+ATOMS = ["a", "b", "c", "x", "/", ".", "[a-c]", "[^ab]", "[^]", "[]", "\\d", "\\w", "\\s", "\\W", "\\D", "\\S",
+         "(a|b)", "(?:ab|c|)", "[0-9x-z]", "\\.", "\\/", "\\x41", "[\\d\\s]", "()", "(a*)", "\\t", "\\-", "[-a]",
+         "[a-]", "\\r", "\\n", "]", "}", "\\u0062"]
+QUANTS = ["", "", "", "*", "+", "?", "{0,1}", "{1,3}", "{2}", "{2,}", "*?", "+?", "??", "{1,2}?"]
+ALPHA = ["a", "b", "c", "x", "y", "/", ".", "1", "9", " ", "\t", "\n", "\r", "-", "_", "A", "B", "]", "}", "\x80",
+         "\xff", "\x00", "\x01"]
+
+
+def _rand_regex(rng, depth=0):
+    k = rng.randint(1, 4)
+    parts = []
+    for _ in range(k):
+        if depth < 2 and rng.random() < 0.15:
+            parts.append("(" + _rand_regex(rng, depth + 1) + ")" + rng.choice(QUANTS))
+        else:
+            parts.append(rng.choice(ATOMS) + rng.choice(QUANTS))
+    r = "".join(parts)
+    if rng.random() < 0.2:
+        r = r + "|" + _rand_regex(rng, depth + 1) if depth < 2 else r
+    if rng.random() < 0.1:
+        r = "^" + r
+    if rng.random() < 0.1:
+        r = r + "$"
+    return r
+
+
+def _engine_match(p: bytes, s: bytes, search: bool):
+    res = C.c_uint8()
+    buf = np.frombuffer(s, np.uint8) if s else np.zeros(1, np.uint8)
+    rc = N.lib.cg_diag_regex_match(p, len(p), buf.ctypes.data, len(s), 1 if search else 0, C.byref(res))
+    return -1 if rc != 0 else res.value
+
+
+@pytest.mark.parametrize("search", [False, True])
+def test_regex_random_vs_std_regex(search):
+    rng = random.Random(1234 + search)
+    checked = 0
+    for _ in range(400):
+        p = _rand_regex(rng).encode("latin-1")
+        valid = oracle.regex_match(p, b"") != -1
+        e = _engine_match(p, b"", search)
+        assert (e != -1) == valid, p
+        if not valid:
+            continue
+        for _ in range(30):
+            s = "".join(rng.choice(ALPHA) for _ in range(rng.randint(0, 8))).encode("latin-1")
+            assert _engine_match(p, s, search) == oracle.regex_match(p, s, search), (p, s)
+            checked += 1
+    assert checked > 5000
+
+
+# ------------------------------------------------------------------- HTTP ---
+HDR_NAMES = [":path", ":method", ":authority", "x-a", "X-B", "x-c"]
+VALUES = ["/", "/a", "/ab", "/public", "/x/y", "GET", "PUT", "POST", "h1", "h2.example.com", "true", "True", "", "zz"]
+
+
+def _rand_matcher(rng):
+    name = rng.choice(HDR_NAMES)
+    kind = rng.random()
+    if kind < 0.4:
+        return {"name": name, "exact_match": rng.choice(VALUES)}
+    if kind < 0.8:
+        return {"name": name, "regex_match": rng.choice(["/a.*", ".*b", "G.T", "P(UT|OST)", "[a-z]+", "h[0-9]",
+                                                         "/[a-z]*/?y?", ".*", "", "x|/", "T?r.e"])}
+    if kind < 0.9:
+        return {"name": name, "present_match": True}
+    return {"name": name, "value": rng.choice(VALUES), "regex": rng.random() < 0.5}
+
+
+def _rand_policy(rng, n_pol=3):
+    pols = []
+    for pi in range(n_pol):
+        p = {"name": f"p{pi}", "policy": pi}
+        for key in ("ingress_per_port_policies", "egress_per_port_policies"):
+            if rng.random() < 0.2:
+                continue
+            ports = rng.sample([0, 80, 81, 8080], rng.randint(0, 3))
+            lst = []
+            for port in ports:
+                rules = []
+                for _ in range(rng.randint(0, 3)):
+                    r = {"remote_policies": sorted(rng.sample([1, 2, 3, 4], rng.randint(0, 2)))}
+                    if rng.random() < 0.85:
+                        r["http_rules"] = {"http_rules": [
+                            {"headers": [_rand_matcher(rng) for _ in range(rng.randint(0, 3))]}
+                            for _ in range(rng.randint(0, 3))]}
+                    rules.append(r)
+                lst.append({"port": port, "protocol": "UDP" if rng.random() < 0.1 else "TCP", "rules": rules})
+            p[key] = lst
+        pols.append(p)
+    return pols
+
+
+def _rand_requests(rng, n, n_pol):
+    reqs = []
+    for _ in range(n):
+        hs = []
+        for name in HDR_NAMES:
+            if rng.random() < 0.7:
+                hs.append((name.upper() if rng.random() < 0.2 else name, rng.choice(VALUES)))
+        if rng.random() < 0.1 and hs:
+            hs.append((hs[0][0], "dup"))  # repeated header: the first value wins
+        reqs.append(hs)
+    parts, off = [], [0]
+    for hs in reqs:
+        b = b"".join(k.encode() + b"\0" + v.encode() + b"\0" for k, v in hs)
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    return dict(policy=np.array([rng.randint(0, n_pol) for _ in range(n)], np.uint32),  # n_pol = unknown
+                ingress=np.array([rng.randint(0, 1) for _ in range(n)], np.uint8),
+                port=np.array([rng.choice([80, 81, 8080, 9]) for _ in range(n)], np.uint16),
+                remote=np.array([rng.randint(0, 5) for _ in range(n)], np.uint32),
+                hdr_blob=np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy(),
+                hdr_off=np.array(off, np.uint64))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_http_random_policies(host, seed):
+    rng = random.Random(seed)
+    pols = _rand_policy(rng)
+    rq = _rand_requests(rng, 600, len(pols))
+    try:
+        orc = oracle.HttpOracle(pols)
+    except ValueError:
+        with pytest.raises(N.CiliumGPUError):
+            host.update_http_policy(pols)
+        return
+    host.update_http_policy(pols)
+    b = host.pack_http(**rq)
+    assert np.array_equal(host.http_eval_host_diag(b), orc.eval(**rq))
+
+
+def test_http_10k_compile_and_overflow(host):
+    pols, info = synth.http10k_rules()
+    rq = synth.http10k_requests(20_000, info)
+    host.update_http_policy(pols)
+    st = host.http_policy_stats()
+    assert st["rules"] == 10_000 and st["programs"] == 64
+    b = host.pack_http(**rq)
+    assert np.array_equal(host.http_eval_host_diag(b), oracle.HttpOracle(pols).eval(**rq, nthreads=4))
+
+
+def test_http_long_fields_overflow(host):
+    pols = synth.starwars_policy()
+    host.update_http_policy(pols)
+    rq = synth.starwars_requests(500, seed=3)
+    blob, off = rq["hdr_blob"].tobytes(), rq["hdr_off"]
+    parts = []
+    for i in range(len(off) - 1):
+        b = blob[off[i]:off[i + 1]]
+        if i % 2:
+            b = b.replace(b"/v1/", b"/v1/" + b"q" * (100 + i), 1)
+        parts.append(b)
+    rq["hdr_blob"] = np.frombuffer(b"".join(parts), np.uint8).copy()
+    rq["hdr_off"] = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.uint64)
+    b = host.pack_http(**rq)
+    assert b.arena.nbytes > 16
+    assert np.array_equal(host.http_eval_host_diag(b), oracle.HttpOracle(pols).eval(**rq))
+
+
+# ------------------------------------------------------------------ Kafka ---
+@pytest.mark.parametrize("seed", range(4))
+def test_kafka_random(host, seed):
+    pols, info = synth.kafka_policy(n_rules=300, n_topics=50, n_clients=10, seed=seed)
+    rq = synth.kafka_requests(20_000, info, seed=seed)
+    host.update_kafka_policy(pols)
+    reqs, arena = host.pack_kafka(**rq)
+    assert np.array_equal(host.kafka_eval_host_diag(reqs, arena), oracle.KafkaOracle(pols).eval(**rq))
+
+
+def test_kafka_many_topics_overflow(host):
+    pols, info = synth.kafka_policy(n_rules=200, n_topics=20, n_clients=4)
+    host.update_kafka_policy(pols)
+    rng = random.Random(5)
+    n = 300
+    rq = dict(redirect=[0] * n, remote=[rng.choice(info["ids"] + [0]) for _ in range(n)],
+              api_key=[rng.choice([0, 1, 3]) for _ in range(n)], api_version=[0] * n, kind=[1] * n,
+              client_id=[b"client-1"] * n,
+              topics=[[info["topics"][rng.randrange(20)].encode() for _ in range(rng.randint(0, 30))]
+                      for _ in range(n)])
+    reqs, arena = host.pack_kafka(**rq)
+    assert np.array_equal(host.kafka_eval_host_diag(reqs, arena), oracle.KafkaOracle(pols).eval(**rq))
+
+
+# ---------------------------------------------------------------- L4, LPM ---
+def test_l4_table_builder(host):
+    keys, ports = synth.l4_table(n_entries=16384)
+    pm = host.policy_map()
+    pm.allow_keys(keys, ports)
+    t = synth.l4_tuples(200_000, keys)
+    assert np.array_equal(pm.eval_host_diag(t), oracle.l4(keys, ports, t)[0])
+
+
+@pytest.mark.parametrize("cfg", [(True, True), (False, False), (True, False)])
+def test_prefilter_table_builder(host, cfg):
+    dyn4, dyn6 = cfg
+    pfx = synth.lpm_prefixes(40_000, 20_000, seed=11)
+    keep = ((pfx["family"] == 4) & ((pfx["prefixlen"] == 32) | dyn4)) | \
+           ((pfx["family"] == 6) & ((pfx["prefixlen"] == 128) | dyn6))
+    pfx = pfx[keep]
+    pf = host.prefilter(dyn4=dyn4, dyn6=dyn6, max_lpm=1 << 20)
+    pf.insert(0, pfx)
+    v4, v6, ep4, ep6 = synth.lpm_addresses(100_000, synth.lpm_prefixes(40_000, 20_000, seed=11), seed=5)
+    pf.set_endpoints(ep4, ep6)
+    g4, g6 = pf.eval_host_diag(v4, v6)
+    o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)

@@ -1,0 +1,80 @@
+"""The N>1 path on CPU: two ranks over gloo (127.0.0.1), each classifying
+its own shard of the 10K-rule workload (per-rank seed as in bench.py),
+then all-reducing the per-program allowed/denied counters — the only
+collective on this path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _per_program_counts(cl, b, verdicts_by_slot, nprog):
+    """allowed/denied per program from slot verdicts (what the kernel counts)."""
+    hdr = b.batch[:64]
+    nchunks = int(hdr[8:12].view(np.uint32)[0])
+    chunks = b.batch[64:64 + 16 * nchunks].view(np.uint32).reshape(nchunks, 4)
+    c = np.zeros(2 * nprog, np.int64)
+    for prog, first, nt, _ in chunks:
+        if prog >= nprog:
+            continue
+        sl = slice(int(first) * 64, int(first + nt) * 64)
+        real = b.order[sl] != 0xFFFFFFFF
+        v = verdicts_by_slot[sl][real]
+        c[2 * prog] += int(v.sum())
+        c[2 * prog + 1] += int((1 - v).sum())
+    return c
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from cilium_amd import synth
+        from cilium_amd.classifier import Classifier
+        cl = Classifier(device=-1)
+        pols, info = synth.http10k_rules(n_rules=2000, n_ports=16)
+        cl.update_http_policy(pols)
+        rq = synth.http10k_requests(4096, info, seed=synth.SEED ^ (rank * 7919))  # bench.py's shard seed
+        b = cl.pack_http(**rq)
+        exp = oracle.HttpOracle(pols).eval(**rq)
+        slot_v = np.zeros(b.nslots, np.int64)
+        real = b.order != 0xFFFFFFFF
+        slot_v[real] = exp[b.order[real]]
+        nprog = cl.http_policy_stats()["programs"]
+        mine = _per_program_counts(cl, b, slot_v, nprog)
+        t = torch.from_numpy(mine.copy())
+        dist.all_reduce(t)
+        gathered = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(gathered, torch.from_numpy(mine.copy()))
+        ok = bool(torch.equal(t, sum(gathered))) and int(t.sum()) == 4096 * world
+        q.put((rank, ok, int(t.sum())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_counter_allreduce():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(total == 8192 for _, _, total in res)
