@@ -6,59 +6,29 @@
 
 namespace cg {
 
-bool build_comb(const ClsDfa& d, CombTable* out) {
+bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable* out) {
   const int n = d.size();
   struct Row {
-    int state;
-    uint32_t kind;
-    int dflt;
+    bool self = false, skip = false;
     std::vector<uint8_t> exc;  // exception bytes
   };
   std::vector<Row> rows(n);
-  std::vector<int> cnt(n);
   for (int s = 1; s < n; ++s) {
-    // per-class targets, then pick the default that minimizes exception bytes
-    std::vector<int> cls_bytes(d.ncls, 0);
-    for (int b = 0; b < 256; ++b) cls_bytes[d.clsmap[b]]++;
-    int dead_n = 0, self_n = 0;
-    std::vector<std::pair<int, int>> other;  // (target, bytes)
-    for (int c = 0; c < d.ncls; ++c) {
-      int t = d.trans[(size_t)s * d.ncls + c];
-      if (t == 0) dead_n += cls_bytes[c];
-      else if (t == s) self_n += cls_bytes[c];
-      else {
-        bool found = false;
-        for (auto& o : other)
-          if (o.first == t) {
-            o.second += cls_bytes[c];
-            found = true;
-          }
-        if (!found) other.push_back({t, cls_bytes[c]});
-      }
+    int self_n = 0, dead_n = 0;
+    for (int b = 0; b < 256; ++b) {
+      int t = d.trans[(size_t)s * d.ncls + d.clsmap[b]];
+      self_n += t == s;
+      dead_n += t == 0;
     }
-    Row r;
-    r.state = s;
-    int best_other = -1, best_other_n = -1;
-    for (auto& o : other)
-      if (o.second > best_other_n) best_other = o.first, best_other_n = o.second;
-    if (self_n >= dead_n && self_n >= best_other_n) {
-      r.kind = 1;
-      r.dflt = s;
-    } else if (dead_n >= best_other_n) {
-      r.kind = 0;
-      r.dflt = 0;
-    } else {
-      r.kind = 2;
-      r.dflt = best_other;
-    }
+    Row& r = rows[s];
+    r.self = self_n > dead_n;
+    const int dflt = r.self ? s : 0;
     for (int b = 0; b < 256; ++b)
-      if (d.trans[(size_t)s * d.ncls + d.clsmap[b]] != r.dflt) r.exc.push_back((uint8_t)b);
-    // a self-loop on every byte but the field separator: the kernel skips to
-    // the next SEP without touching the table
-    if (r.kind == 1 && r.exc.size() == 1 && r.exc[0] == 0) r.kind = 3;
-    rows[s] = std::move(r);
+      if (d.trans[(size_t)s * d.ncls + d.clsmap[b]] != dflt) r.exc.push_back((uint8_t)b);
+    r.skip = r.self && r.exc.size() == 1 && r.exc[0] == 0;
   }
-  // placement: most exceptions first
+  // placement: most exceptions first, first fit; a state also owns the
+  // header cell base-1, so bases are unique
   std::vector<int> order(n > 0 ? n - 1 : 0);
   std::iota(order.begin(), order.end(), 1);
   std::stable_sort(order.begin(), order.end(),
@@ -88,16 +58,16 @@ bool build_comb(const ClsDfa& d, CombTable* out) {
     for (uint8_t x : r.exc) used[b0 + x] = 1;
     excs += r.exc.size();
   }
-  uint32_t ncells = 0;
+  uint32_t ncells = 257;
   for (int s = 1; s < n; ++s) ncells = std::max(ncells, base[s] + 256);
-  out->cells.assign(std::max<uint32_t>(ncells, 257), kCombEmpty);
+  out->cells.assign(ncells, kCombEmpty);
   out->state_enc.assign(n, 0);
-  for (int s = 1; s < n; ++s) out->state_enc[s] = base[s] | (rows[s].kind << 14);
+  for (int s = 1; s < n; ++s)
+    out->state_enc[s] = base[s] | (rows[s].self ? kCombSelf : 0) | (rows[s].skip ? kCombSkip : 0);
   for (int s = 1; s < n; ++s) {
-    const Row& r = rows[s];
-    uint32_t b0 = base[s];
-    out->cells[b0 - 1] = 0xFFFFu | (out->state_enc[r.dflt] << 16);
-    for (uint8_t x : r.exc) {
+    const uint32_t b0 = base[s];
+    out->cells[b0 - 1] = 0xFFFFu | ((labels[s] & 0xFFFFu) << 16);
+    for (uint8_t x : rows[s].exc) {
       int t = d.trans[(size_t)s * d.ncls + d.clsmap[x]];
       out->cells[b0 + x] = b0 | (out->state_enc[t] << 16);
     }

@@ -84,6 +84,7 @@ CG_HD inline uint32_t ep_hash128(uint64_t hi, uint64_t lo) {
 // Program = one (policy, direction, port) evaluation: Envoy's exact-port
 // PortNetworkPolicyRules merged with the port-0 ones (cilium_network_policy.h:169-192).
 constexpr uint32_t kProgAllowAll = 1;  // some scope has no HTTP rules / no rules
+constexpr uint32_t kProgHasAlways = 2;  // some PNPR has an empty HTTP rule list
 constexpr uint32_t kNoAcc = 0xFFFFFFFFu;
 struct HttpProg {
   uint32_t part_begin;
@@ -96,11 +97,12 @@ struct HttpProg {
   uint32_t cell_count;      // staged into LDS as one block
 };
 // One DFA of a program as a comb-packed table (comb.h): states are encoded
-// as base | kind << 14; acc is indexed by base.
+// as base | self << 14 | skip << 15; an accepting state's header cell holds
+// its accept label, acc[acc_off + label] the u64 word offset of its mask.
 struct HttpPart {
   uint32_t cell_off;  // into cells (u32)
   uint32_t ncells;
-  uint32_t acc_off;   // into acc (u32), indexed by base: mask word offset or kNoAcc
+  uint32_t acc_off;   // into acc (u32), indexed by accept label
   uint32_t start;     // start state encoding
   uint32_t nstates;
   uint32_t pad0, pad1, pad2;

@@ -396,7 +396,12 @@ void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, s
   try {
     ClsDfa raw = build_union(fc, all_rules, rules, F, W, p.label_masks);
     p.dfa = minimize_cls(raw);
-    if (p.dfa.size() > kMaxPartStates || !build_comb(p.dfa, &p.comb)) ok = false;
+    std::vector<uint32_t> labels(p.dfa.size(), kCombNoLabel);
+    for (int s = 0; s < p.dfa.size(); ++s)
+      if (p.dfa.label[s]) labels[s] = p.dfa.label[s] - 1;
+    if (p.dfa.size() > kMaxPartStates || p.label_masks.size() >= kCombNoLabel ||
+        !build_comb(p.dfa, labels, &p.comb))
+      ok = false;
   } catch (const TooBig&) {
     ok = false;
   }
@@ -489,6 +494,8 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       }
     }
     pg.always_off = add_mask(always);
+    for (uint64_t w : always)
+      if (w) pg.flags |= kProgHasAlways;
     pg.default_remote = add_mask(open);
     for (auto& [rid, m] : by_remote) rhash.push_back({((uint64_t)pid << 32) | rid, add_mask(m)});
     // union rules
@@ -531,13 +538,9 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       hp.cell_off = (uint32_t)S.cells.size();
       hp.ncells = (uint32_t)cb.cells.size();
       S.cells.insert(S.cells.end(), cb.cells.begin(), cb.cells.end());
+      // accept label l of this part → u64 word offset of its PNPR mask
       hp.acc_off = (uint32_t)S.acc.size();
-      std::vector<uint32_t> lab_off(po.label_masks.size());
-      for (size_t l = 0; l < po.label_masks.size(); ++l) lab_off[l] = add_mask(po.label_masks[l]);
-      std::vector<uint32_t> acc_by_base(cb.cells.size(), kNoAcc);
-      for (int s = 1; s < d.size(); ++s)
-        if (d.label[s]) acc_by_base[cb.state_enc[s] & kCombMaxBase] = lab_off[d.label[s] - 1];
-      S.acc.insert(S.acc.end(), acc_by_base.begin(), acc_by_base.end());
+      for (size_t l = 0; l < po.label_masks.size(); ++l) S.acc.push_back(add_mask(po.label_masks[l]));
       S.total_states += d.size();
       S.total_exceptions += cb.exceptions;
       S.parts.push_back(hp);
@@ -643,7 +646,12 @@ void HttpSnapshot::upload(Engine& e) {
   dev.nprogs = (uint32_t)progs.size();
   dev.nparts = (uint32_t)parts.size();
   dev.epoch = epoch;
-  dev.lds_cells = 16384;  // 64 KiB of LDS per workgroup
+  // LDS per workgroup = the largest program table (so 160 KiB / that many
+  // workgroups share a CU); programs above 40K cells walk from global memory
+  uint32_t max_cells = 0;
+  for (const auto& pg : progs)
+    if (!(pg.flags & kProgAllowAll) && pg.cell_count <= 40960) max_cells = std::max(max_cells, pg.cell_count);
+  dev.lds_cells = (max_cells + 255) & ~255u;
   dev.counters = d_counters.as<unsigned long long>();
 }
 

@@ -239,8 +239,9 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
           st = comb_next(cells, st, ch);
           if (!st) break;
         }
-        uint32_t a = s.acc[pt.acc_off + (st & kCombMaxBase)];
-        if (a == kNoAcc) continue;
+        const uint32_t lab = comb_label(cells, st);
+        if (lab == kCombNoLabel) continue;
+        const uint32_t a = s.acc[pt.acc_off + lab];
         for (uint32_t w = 0; w < pg.mask_words; ++w)
           if (s.masks[a + w] & s.masks[roff + w]) v = 1;
       }

@@ -21,18 +21,6 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kHttpThreads = 512;
 
-__device__ __forceinline__ uint32_t remote_row(const HttpDev& T, uint32_t prog, uint32_t remote, uint32_t dflt) {
-  const unsigned long long key = ((unsigned long long)prog << 32) | remote;
-  uint32_t h = hash64to32(key) & T.rhash_mask;
-  for (uint32_t probe = 0; probe <= T.rhash_mask; ++probe) {
-    const unsigned long long k = T.rhash_keys[h];
-    if (k == key) return T.rhash_vals[h];
-    if (k == ~0ULL) break;
-    h = (h + 1) & T.rhash_mask;
-  }
-  return dflt;
-}
-
 __device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
                                            uint32_t w) {
   for (uint32_t i = 0; i < w; ++i)
@@ -45,19 +33,11 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
   return (word >> ((k & 3) * 8)) & 0xFFu;
 }
 
-// One comb transition (comb.h).  kind 3 states are never stepped on a non-SEP
-// byte (the caller skips them).
-__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t st, uint32_t b) {
-  const uint32_t base = st & 0x3FFFu;
-  const uint32_t e = cells[base + b];
-  if ((e & 0xFFFFu) == base) return e >> 16;
-  const uint32_t kind = st >> 14;
-  if (kind == 0) return 0;
-  if (kind == 2) return cells[base - 1] >> 16;
-  return st;
-}
-
-// Walk the record string through one part's table; returns the final state.
+// Walk the record string through one part's comb table (comb.h); returns the
+// final state.  Branch-free per byte: every position reads the table and a
+// select keeps the state past the end of the string, so the wavefront runs no
+// exec-mask bookkeeping per byte; it leaves a 16-byte unit only when no lane
+// has work left.  A dead lane reads cells[b] (base 0), which never matches.
 __device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ cells, uint32_t st, const uint4 (&s)[8],
                                         uint32_t len, bool overflow, const uint8_t* __restrict__ arena,
                                         uint32_t aoff) {
@@ -70,19 +50,37 @@ __device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ cells, uin
       asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const uint32_t p = u * 16 + k;
         const uint32_t b = get_byte(w, k);
-        if (p < len && st != 0 && (b == 0 || (st >> 14) != 3)) st = comb_step(cells, st, b);
+        const uint32_t base = st & 0x3FFFu;
+        const uint32_t e = cells[base + b];
+        const uint32_t dflt = (st & 0x4000u) ? st : 0u;
+        const uint32_t nx = ((e & 0xFFFFu) == base) ? (e >> 16) : dflt;
+        st = ((uint32_t)(u * 16 + k) < len) ? nx : st;
       }
-      if (!__any((u + 1) * 16 < (int)len && st != 0)) break;
+      if (!__any((uint32_t)((u + 1) * 16) < len && st != 0)) break;
     }
   } else {
     for (uint32_t p = 0; p < len && st != 0; ++p) {
       const uint32_t b = arena[aoff + p];
-      if (b == 0 || (st >> 14) != 3) st = comb_step(cells, st, b);
+      const uint32_t base = st & 0x3FFFu;
+      const uint32_t e = cells[base + b];
+      st = ((e & 0xFFFFu) == base) ? (e >> 16) : ((st & 0x4000u) ? st : 0u);
     }
   }
   return st;
+}
+
+__device__ __forceinline__ uint32_t remote_row_from(const HttpDev& T, unsigned long long key, uint32_t h,
+                                                    unsigned long long k0, uint32_t v0, uint32_t dflt) {
+  if (k0 == key) return v0;
+  if (k0 == ~0ULL) return dflt;
+  for (uint32_t probe = 1; probe <= T.rhash_mask; ++probe) {
+    h = (h + 1) & T.rhash_mask;
+    const unsigned long long k = T.rhash_keys[h];
+    if (k == key) return T.rhash_vals[h];
+    if (k == ~0ULL) break;
+  }
+  return dflt;
 }
 
 // One tile of 64 requests of program `prog` (a real, non-trivial program).
@@ -100,17 +98,32 @@ __device__ __forceinline__ void http_tile(const HttpDev& T, const HttpProg& pg, 
   const uint32_t flags = meta.w >> 24;
   const uint32_t aoff = (meta.w & 0xFFFFFFu) * 16u;
   const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+  // first probe of the remote-identity mask, issued before the walk so its
+  // latency hides behind it
+  const unsigned long long rkey = ((unsigned long long)prog << 32) | remote;
+  const uint32_t rh = hash64to32(rkey) & T.rhash_mask;
+  const unsigned long long rk0 = T.rhash_keys[rh];
+  const uint32_t rv0 = T.rhash_vals[rh];
   uint32_t verdict = 0;
-  if (counted) {
-    const uint32_t rrow = remote_row(T, prog, remote, pg.default_remote);
-    if (masks_meet(T.masks, pg.always_off, rrow, pg.mask_words)) verdict = 1;
-    for (uint32_t pi = 0; pi < pg.part_count && !verdict; ++pi) {
-      const HttpPart pt = T.parts[pg.part_begin + pi];
-      const uint32_t* __restrict__ cells = pcells + (pt.cell_off - pg.cell_begin);
-      const uint32_t st = walk(cells, pt.start, s, len, flags & CG_HTTP_F_OVERFLOW, arena, aoff);
-      const uint32_t a = T.acc[pt.acc_off + (st & 0x3FFFu)];
-      if (a != kNoAcc && masks_meet(T.masks, a, rrow, pg.mask_words)) verdict = 1;
+  uint32_t rrow = 0;
+  bool have_rrow = false;
+  for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
+    const HttpPart pt = T.parts[pg.part_begin + pi];
+    const uint32_t* __restrict__ cells = pcells + (pt.cell_off - pg.cell_begin);
+    uint32_t st = walk(cells, pt.start, s, counted ? len : 0u, flags & CG_HTTP_F_OVERFLOW, arena, aoff);
+    if (!counted) st = 0;
+    const uint32_t lab = st ? (cells[(st & 0x3FFFu) - 1] >> 16) : 0xFFFFu;
+    if (lab != 0xFFFFu && !verdict) {
+      if (!have_rrow) {
+        rrow = remote_row_from(T, rkey, rh, rk0, rv0, pg.default_remote);
+        have_rrow = true;
+      }
+      if (masks_meet(T.masks, T.acc[pt.acc_off + lab], rrow, pg.mask_words)) verdict = 1;
     }
+  }
+  if (counted && !verdict && (pg.flags & kProgHasAlways)) {
+    if (!have_rrow) rrow = remote_row_from(T, rkey, rh, rk0, rv0, pg.default_remote);
+    if (masks_meet(T.masks, pg.always_off, rrow, pg.mask_words)) verdict = 1;
   }
   out[slot] = (uint8_t)verdict;
   *n_allow += counted && verdict;
@@ -186,12 +199,25 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   if (nslots == 0) return 0;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
+  // one resident wave of workgroups: as many per CU as LDS and registers
+  // allow (the program table size sets the LDS share), then grid-stride
+  const size_t lds = (size_t)t.lds_cells * 4;
+  static size_t occ_lds = ~(size_t)0;
+  static int occ = 1;
+  if (occ_lds != lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)http_kernel, kHttpThreads, lds) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+    occ = nb;
+    occ_lds = lds;
+  }
   size_t tiles = nslots / kWave;
-  size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
-  hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), (size_t)t.lds_cells * 4,
+  size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);
+  hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds,
                      (hipStream_t)stream, t, (const uint8_t*)batch, nslots, arena, out);
   return (int)hipGetLastError();
 }
