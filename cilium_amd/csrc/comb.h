@@ -6,22 +6,26 @@
 // (literal path prefixes).  Each state therefore keeps a default target —
 // dead or itself — and only its exception bytes are stored, packed first-fit
 // into one array of 32-bit cells indexed by byte value (row displacement,
-// Tarjan–Yao), so the kernel needs no byte-class lookup:
+// Tarjan–Yao), so the kernel needs no byte-class lookup.  A state IS its base
+// (a 16-bit cell index); rows whose default is the state itself get the
+// bases at or above a per-table threshold `self_lo`:
 //
-//   state encoding  S = base | self << 14 | skip << 15
-//       self: the default target is S itself (else dead)
-//       skip: self on every byte but SEP (0x00): the kernel does not even
-//             read the table inside such a field
-//   cell[base + b]  = base | next(S, b) << 16    when b is an exception
-//   cell[base - 1]  = 0xFFFF | label << 16       (header; 0xFFFF is never a
-//                                                 base; label = accept-set
-//                                                 index or 0xFFFF)
+//   cell[S + b]  = S | next(S, b) << 16      when b is an exception of S
+//   cell[S - 1]  = 0xFFFF | label << 16      (header; 0xFFFF is never a base;
+//                                             label = accept-set index or 0xFFFF)
 //
-//   next(S, b) = cell[base+b].lo == base ? cell[base+b].hi : (self ? S : 0)
+//   next(S, b) = cell[S+b].lo == S ? cell[S+b].hi : (S >= self_lo ? S : 0)
 //
-// The dead state is S = 0 (base 0 is never given to a state).  Bases are
-// limited to 14 bits; a program whose table does not fit is split into more
-// parts by the caller.
+// The dead state is S = 0 (base 0 is never given to a state, so no check
+// half-word is ever 0).  Accepting states are made absorbing (self, no
+// exceptions): the request strings these tables read end with the last
+// field's separator, after which every accepting row is dead anyway, so the
+// kernel may keep stepping through the zero padding of a record without
+// checking the string length per byte.
+//
+// Bases are table-local; `rebase_comb` shifts them by the table's offset
+// inside a program's cell block so that all parts of a program share one
+// pointer (the LDS block) — possible while the block stays below 0xFFFF cells.
 #pragma once
 
 #include <cstdint>
@@ -31,32 +35,33 @@
 
 namespace cg {
 
-constexpr uint32_t kCombMaxBase = 0x3FFF;
-constexpr uint32_t kCombSelf = 1u << 14;
-constexpr uint32_t kCombSkip = 1u << 15;
+constexpr uint32_t kCombMaxBase = 0xFEFF;  // base + 255 stays below 0xFFFF
 constexpr uint32_t kCombEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kCombNoLabel = 0xFFFF;
 
 struct CombTable {
   std::vector<uint32_t> cells;
-  std::vector<uint32_t> state_enc;  // encoding of each DFA state (0 for dead)
+  std::vector<uint32_t> state_enc;  // base of each DFA state (0 for dead)
   uint32_t start = 0;
+  uint32_t self_lo = 0;             // states >= self_lo default to themselves
   uint64_t exceptions = 0;
 };
 
-// labels[s]: accept-set index of DFA state s (kCombNoLabel if none).
-// Returns false if the table needs a base beyond kCombMaxBase.
-bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable* out);
+// labels[s]: accept-set index of DFA state s (kCombNoLabel if none).  An
+// accepting state must have no live transition (throws Error otherwise).
+// Returns false if the table needs a base beyond `max_base`.
+bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable* out,
+                uint32_t max_base = kCombMaxBase);
 
-inline uint32_t comb_next(const uint32_t* cells, uint32_t s, uint32_t b) {
-  const uint32_t base = s & kCombMaxBase;
-  const uint32_t e = cells[base + b];
-  if ((e & 0xFFFF) == base) return e >> 16;
-  return (s & kCombSelf) ? s : 0;
+// Shift every base of `t` by `off` (its position inside a program block).
+void rebase_comb(CombTable* t, uint32_t off);
+
+inline uint32_t comb_next(const uint32_t* cells, uint32_t self_lo, uint32_t s, uint32_t b) {
+  const uint32_t e = cells[s + b];
+  if ((e & 0xFFFF) == s) return e >> 16;
+  return s >= self_lo ? s : 0;
 }
 
-inline uint32_t comb_label(const uint32_t* cells, uint32_t s) {
-  return s ? cells[(s & kCombMaxBase) - 1] >> 16 : kCombNoLabel;
-}
+inline uint32_t comb_label(const uint32_t* cells, uint32_t s) { return s ? cells[s - 1] >> 16 : kCombNoLabel; }
 
 }  // namespace cg

@@ -96,16 +96,23 @@ struct HttpProg {
   uint32_t cell_begin;      // the program's parts are contiguous in cells[]:
   uint32_t cell_count;      // staged into LDS as one block
 };
-// One DFA of a program as a comb-packed table (comb.h): states are encoded
-// as base | self << 14 | skip << 15; an accepting state's header cell holds
-// its accept label, acc[acc_off + label] the u64 word offset of its mask.
+// One DFA of a program as a comb-packed table (comb.h).  A state is its base
+// cell index relative to `walk_off`; states >= self_lo default to themselves.
+// An accepting state's header cell holds its accept label and
+// acc[acc_off + label] the u64 word offset of its PNPR mask.  When a
+// program's block stays below 0xFFFF cells its parts are rebased onto the
+// block (walk_off = cell_begin for every part), so the kernel walks all parts
+// through one pointer — the LDS copy.
+constexpr uint32_t kProgRebased = 4;
 struct HttpPart {
-  uint32_t cell_off;  // into cells (u32)
+  uint32_t cell_off;  // first cell of this part in cells[]
   uint32_t ncells;
   uint32_t acc_off;   // into acc (u32), indexed by accept label
-  uint32_t start;     // start state encoding
+  uint32_t start;     // start state
   uint32_t nstates;
-  uint32_t pad0, pad1, pad2;
+  uint32_t self_lo;
+  uint32_t walk_off;  // cells[] offset the states are relative to
+  uint32_t pad;
 };
 // Special program ids in the program lookup.
 constexpr uint32_t kProgAllow = 0xFFFFFFFEu;  // no policy for the port → allow

@@ -45,6 +45,7 @@ constexpr uint8_t kSep = 0x00;
 constexpr uint8_t kAbsent = 0x01;
 constexpr int kMaxUnionStates = 400000;  // before minimization, per part
 constexpr int kMaxPartStates = 65535;    // u16 transition entries
+constexpr uint32_t kMaxLdsCells = 40960;  // 160 KiB: one program table per workgroup
 
 enum class MKind { Exact, Regex, Present };
 struct MatcherSpec {
@@ -529,13 +530,20 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     pg.part_begin = (uint32_t)S.parts.size();
     pg.part_count = (uint32_t)parts.size();
     pg.cell_begin = (uint32_t)S.cells.size();
+    size_t block = 0;
+    for (const auto& po : parts) block += po.comb.cells.size();
+    const bool rebase = block <= kCombMaxBase;
+    if (rebase) pg.flags |= kProgRebased;
     for (auto& po : parts) {
       HttpPart hp{};
       const ClsDfa& d = po.dfa;
-      const CombTable& cb = po.comb;
+      CombTable& cb = po.comb;
+      hp.cell_off = (uint32_t)S.cells.size();
+      if (rebase) rebase_comb(&cb, hp.cell_off - pg.cell_begin);
+      hp.walk_off = rebase ? pg.cell_begin : hp.cell_off;
       hp.nstates = (uint32_t)d.size();
       hp.start = cb.start;
-      hp.cell_off = (uint32_t)S.cells.size();
+      hp.self_lo = cb.self_lo;
       hp.ncells = (uint32_t)cb.cells.size();
       S.cells.insert(S.cells.end(), cb.cells.begin(), cb.cells.end());
       // accept label l of this part → u64 word offset of its PNPR mask
@@ -646,11 +654,12 @@ void HttpSnapshot::upload(Engine& e) {
   dev.nprogs = (uint32_t)progs.size();
   dev.nparts = (uint32_t)parts.size();
   dev.epoch = epoch;
-  // LDS per workgroup = the largest program table (so 160 KiB / that many
-  // workgroups share a CU); programs above 40K cells walk from global memory
+  // LDS per workgroup = the largest rebased program table (so 160 KiB / that
+  // many workgroups share a CU); larger programs walk from global memory
   uint32_t max_cells = 0;
   for (const auto& pg : progs)
-    if (!(pg.flags & kProgAllowAll) && pg.cell_count <= 40960) max_cells = std::max(max_cells, pg.cell_count);
+    if (!(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= kMaxLdsCells)
+      max_cells = std::max(max_cells, pg.cell_count);
   dev.lds_cells = (max_cells + 255) & ~255u;
   dev.counters = d_counters.as<unsigned long long>();
 }

@@ -233,10 +233,10 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         if (s.masks[pg.always_off + w] & s.masks[roff + w]) v = 1;
       for (uint32_t pi = 0; pi < pg.part_count && !v; ++pi) {
         const HttpPart& pt = s.parts[pg.part_begin + pi];
-        const uint32_t* cells = s.cells.data() + pt.cell_off;
+        const uint32_t* cells = s.cells.data() + pt.walk_off;
         uint32_t st = pt.start;
         for (unsigned char ch : str) {
-          st = comb_next(cells, st, ch);
+          st = comb_next(cells, pt.self_lo, st, ch);
           if (!st) break;
         }
         const uint32_t lab = comb_label(cells, st);

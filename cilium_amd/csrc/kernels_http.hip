@@ -6,8 +6,7 @@
 // comb-packed DFA (comb.h) into LDS once, then each wavefront walks 64
 // requests at a time, one lane per request.  Records are tile-transposed, so
 // each of a wave's nine 16-byte unit loads is one contiguous 1 KiB read; the
-// DFA walk itself touches only LDS (one ds_read_b32 per byte, none inside
-// fields whose automaton is a self loop).
+// DFA walk itself touches only LDS (one ds_read_b32 per byte).
 #include <hip/hip_runtime.h>
 
 #include "../../include/cilium_gpu.h"
@@ -19,7 +18,7 @@ namespace cg {
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kHttpThreads = 512;
+constexpr int kHttpThreads = 1024;
 
 __device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
                                            uint32_t w) {
@@ -33,40 +32,39 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
   return (word >> ((k & 3) * 8)) & 0xFFu;
 }
 
-// Walk the record string through one part's comb table (comb.h); returns the
-// final state.  Branch-free per byte: every position reads the table and a
-// select keeps the state past the end of the string, so the wavefront runs no
-// exec-mask bookkeeping per byte; it leaves a 16-byte unit only when no lane
-// has work left.  A dead lane reads cells[b] (base 0), which never matches.
-__device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ cells, uint32_t st, const uint4 (&s)[8],
-                                        uint32_t len, bool overflow, const uint8_t* __restrict__ arena,
-                                        uint32_t aoff) {
-  if (!overflow) {
+// One comb transition (comb.h), branch-free: every lane reads the table and
+// selects.  A dead lane (S = 0) reads cells[b], whose check half is never 0.
+__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+                                             uint32_t b) {
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + ((st << 2) + (b << 2)));
+  const uint32_t dflt = st >= self_lo ? st : 0u;
+  return (e & 0xFFFFu) == st ? (e >> 16) : dflt;
+}
+
+// Walk the in-record string of a tile's lanes (units 1..8 of the tile).
+// Accepting states absorb (comb.h) and the record is zero-padded, so lanes
+// step through all 16 bytes of a unit with no per-byte length test; units are
+// loaded one ahead and the walk ends once no lane is alive inside its string.
+__device__ __forceinline__ uint32_t walk_tile(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+                                             const uint4* __restrict__ tb, uint32_t lane, uint32_t len) {
+  if (!__any(len != 0 && st != 0)) return st;
+  uint4 cur = tb[1 * kWave + lane];
+  for (uint32_t u = 0; u < 8; ++u) {
+    const bool more = __any((u + 1) * 16 < len);
+    uint4 nxt = cur;
+    if (more && u < 7) nxt = tb[(u + 2) * kWave + lane];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      // keep unit u's byte extraction next to its use (else hipcc hoists all
-      // 128 extractions into 128 VGPRs)
-      uint4 w = s[u];
-      asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t b = get_byte(w, k);
-        const uint32_t base = st & 0x3FFFu;
-        const uint32_t e = cells[base + b];
-        const uint32_t dflt = (st & 0x4000u) ? st : 0u;
-        const uint32_t nx = ((e & 0xFFFFu) == base) ? (e >> 16) : dflt;
-        st = ((uint32_t)(u * 16 + k) < len) ? nx : st;
-      }
-      if (!__any((uint32_t)((u + 1) * 16) < len && st != 0)) break;
-    }
-  } else {
-    for (uint32_t p = 0; p < len && st != 0; ++p) {
-      const uint32_t b = arena[aoff + p];
-      const uint32_t base = st & 0x3FFFu;
-      const uint32_t e = cells[base + b];
-      st = ((e & 0xFFFFu) == base) ? (e >> 16) : ((st & 0x4000u) ? st : 0u);
-    }
+    for (int k = 0; k < 16; ++k) st = comb_step(cells, self_lo, st, get_byte(cur, k));
+    if (!more || !__any(st != 0 && (u + 1) * 16 < len)) break;
+    cur = nxt;
   }
+  return st;
+}
+
+// Records longer than a slot live in the overflow arena: byte loop.
+__device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+                                              const uint8_t* __restrict__ arena, uint32_t aoff, uint32_t len) {
+  for (uint32_t p = 0; p < len && st != 0; ++p) st = comb_step(cells, self_lo, st, arena[aoff + p]);
   return st;
 }
 
@@ -84,20 +82,20 @@ __device__ __forceinline__ uint32_t remote_row_from(const HttpDev& T, unsigned l
 }
 
 // One tile of 64 requests of program `prog` (a real, non-trivial program).
-template <bool kLds>
+// `pcells`: the program's cell block when it is rebased (LDS copy or global),
+// else the global table (parts walk from their own offsets).
 __device__ __forceinline__ void http_tile(const HttpDev& T, const HttpProg& pg, uint32_t prog,
-                                          const uint32_t* __restrict__ pcells, const uint4* __restrict__ tb,
-                                          const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                          size_t slot, uint32_t lane, uint32_t* n_allow, uint32_t* n_deny) {
+                                          const uint32_t* __restrict__ pcells, bool rebased,
+                                          const uint4* __restrict__ tb, const uint8_t* __restrict__ arena,
+                                          uint8_t* __restrict__ out, size_t slot, uint32_t lane, uint32_t* n_allow,
+                                          uint32_t* n_deny) {
   const uint4 meta = tb[lane];
-  uint4 s[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) s[u] = tb[(u + 1) * kWave + lane];
   const uint32_t remote = meta.x;
-  const uint32_t len = meta.z;
   const uint32_t flags = meta.w >> 24;
   const uint32_t aoff = (meta.w & 0xFFFFFFu) * 16u;
   const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+  const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
+  const uint32_t len = counted && !overflow ? meta.z : 0u;
   // first probe of the remote-identity mask, issued before the walk so its
   // latency hides behind it
   const unsigned long long rkey = ((unsigned long long)prog << 32) | remote;
@@ -109,10 +107,14 @@ __device__ __forceinline__ void http_tile(const HttpDev& T, const HttpProg& pg, 
   bool have_rrow = false;
   for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
     const HttpPart pt = T.parts[pg.part_begin + pi];
-    const uint32_t* __restrict__ cells = pcells + (pt.cell_off - pg.cell_begin);
-    uint32_t st = walk(cells, pt.start, s, counted ? len : 0u, flags & CG_HTTP_F_OVERFLOW, arena, aoff);
+    const uint32_t* __restrict__ cells = rebased ? pcells : pcells + pt.walk_off;
+    uint32_t st = walk_tile(cells, pt.self_lo, pt.start, tb, lane, len);
+    if (__any(overflow)) {
+      const uint32_t sa = walk_arena(cells, pt.self_lo, pt.start, arena, aoff, overflow ? meta.z : 0u);
+      if (overflow) st = sa;
+    }
     if (!counted) st = 0;
-    const uint32_t lab = st ? (cells[(st & 0x3FFFu) - 1] >> 16) : 0xFFFFu;
+    const uint32_t lab = st ? (cells[st - 1] >> 16) : 0xFFFFu;
     if (lab != 0xFFFFu && !verdict) {
       if (!have_rrow) {
         rrow = remote_row_from(T, rkey, rh, rk0, rv0, pg.default_remote);
@@ -130,7 +132,7 @@ __device__ __forceinline__ void http_tile(const HttpDev& T, const HttpProg& pg, 
   *n_deny += counted && !verdict;
 }
 
-__global__ __launch_bounds__(kHttpThreads) void http_kernel(HttpDev T, const uint8_t* __restrict__ batch,
+__global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(HttpDev T, const uint8_t* __restrict__ batch,
                                                             size_t nslots, const uint8_t* __restrict__ arena,
                                                             uint8_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(kHttpThreads) void http_kernel(HttpDev T, const uin
     HttpProg pg{};
     if (real) pg = T.progs[prog];
     const bool walkp = real && !(pg.flags & kProgAllowAll);
-    const bool lds = walkp && pg.cell_count <= T.lds_cells;
+    const bool lds = walkp && (pg.flags & kProgRebased) && pg.cell_count <= T.lds_cells;
     uint32_t n_allow = 0, n_deny = 0;
     __syncthreads();  // the previous chunk is done with lcells
     if (lds)
@@ -173,9 +175,11 @@ __global__ __launch_bounds__(kHttpThreads) void http_kernel(HttpDev T, const uin
         out[slot] = (uint8_t)v;
         n_allow += real && counted;
       } else if (lds) {
-        http_tile<true>(T, pg, prog, lcells, tb, arena, out, slot, lane, &n_allow, &n_deny);
+        http_tile(T, pg, prog, lcells, true, tb, arena, out, slot, lane, &n_allow, &n_deny);
+      } else if (pg.flags & kProgRebased) {
+        http_tile(T, pg, prog, T.cells + pg.cell_begin, true, tb, arena, out, slot, lane, &n_allow, &n_deny);
       } else {
-        http_tile<false>(T, pg, prog, T.cells + pg.cell_begin, tb, arena, out, slot, lane, &n_allow, &n_deny);
+        http_tile(T, pg, prog, T.cells, false, tb, arena, out, slot, lane, &n_allow, &n_deny);
       }
     }
     if (real) {
