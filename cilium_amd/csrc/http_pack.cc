@@ -6,6 +6,7 @@
 // pads every group to whole 64-request tiles, so each chunk of tiles has one
 // program whose comb table a workgroup stages in LDS.
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <map>
 #include <string>
@@ -104,47 +105,77 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
       }
     }
   }
-  std::map<uint32_t, size_t> next = first_slot;
+  // ---- request strings (field values in field order, SEP-terminated)
   const size_t F = s.fields.size();
-  size_t used = 0;
-  std::vector<const uint8_t*> vp(F);
-  std::vector<size_t> vl(F);
-  std::string str;
-  for (size_t i = 0; i < n; ++i) {
-    size_t sl = next[prog[i]]++;
-    if (order) order[sl] = (uint32_t)i;
-    if (!batch && !arena_used) continue;
-    std::fill(vp.begin(), vp.end(), nullptr);
-    const uint8_t* p = hdr_blob + hdr_off[i];
-    const uint8_t* e = hdr_blob + hdr_off[i + 1];
-    while (p < e) {
-      const uint8_t* nm = p;
-      while (p < e && *p) ++p;
-      size_t nl = p - nm;
-      if (p < e) ++p;
-      const uint8_t* v = p;
-      while (p < e && *p) ++p;
-      size_t vlen = p - v;
-      if (p < e) ++p;
-      for (size_t f = 0; f < F; ++f)
-        if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
-          vp[f] = v;
-          vl[f] = vlen;
-        }
-    }
-    str.clear();
-    bool malformed = false;
-    for (size_t f = 0; f < F; ++f) {
-      if (!vp[f]) {
-        str.push_back((char)kAbsent);
-      } else {
-        for (size_t k = 0; k < vl[f]; ++k) {
-          if (vp[f][k] == kAbsent || vp[f][k] == kSep) malformed = true;
-          str.push_back((char)vp[f][k]);
-        }
+  std::vector<uint8_t> strs;
+  std::vector<uint64_t> soff(n + 1, 0);
+  std::vector<uint8_t> malformed(n, 0);
+  const bool build = batch || arena_used;
+  if (build) {
+    strs.reserve(n * 64);
+    std::vector<const uint8_t*> vp(F);
+    std::vector<size_t> vl(F);
+    for (size_t i = 0; i < n; ++i) {
+      std::fill(vp.begin(), vp.end(), nullptr);
+      const uint8_t* p = hdr_blob + hdr_off[i];
+      const uint8_t* e = hdr_blob + hdr_off[i + 1];
+      while (p < e) {
+        const uint8_t* nm = p;
+        while (p < e && *p) ++p;
+        size_t nl = p - nm;
+        if (p < e) ++p;
+        const uint8_t* v = p;
+        while (p < e && *p) ++p;
+        size_t vlen = p - v;
+        if (p < e) ++p;
+        for (size_t f = 0; f < F; ++f)
+          if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
+            vp[f] = v;
+            vl[f] = vlen;
+          }
       }
-      str.push_back((char)kSep);
+      for (size_t f = 0; f < F; ++f) {
+        if (!vp[f]) {
+          strs.push_back(kAbsent);
+        } else {
+          for (size_t k = 0; k < vl[f]; ++k) {
+            if (vp[f][k] == kAbsent || vp[f][k] == kSep) malformed[i] = 1;
+            strs.push_back(vp[f][k]);
+          }
+        }
+        strs.push_back(kSep);
+      }
+      soff[i + 1] = strs.size();
     }
+  }
+  // ---- slot assignment: within a program group, requests ordered by the
+  // number of 16-byte units their string spans (stable), so the lanes of a
+  // tile end their walks together
+  std::vector<uint32_t> slot_of(n);
+  {
+    constexpr int kKeys = CG_HTTP_UNITS + 1;  // 0..8 units, 9 = overflow arena
+    std::map<uint32_t, std::array<size_t, kKeys + 1>> start;
+    std::vector<uint8_t> key(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+      const size_t len = build ? soff[i + 1] - soff[i] : 0;
+      key[i] = len > CG_HTTP_SLOT_BYTES ? kKeys - 1 : (uint8_t)((len + 15) / 16);
+      auto it = start.find(prog[i]);
+      if (it == start.end()) it = start.emplace(prog[i], std::array<size_t, kKeys + 1>{}).first;
+      it->second[key[i] + 1]++;
+    }
+    for (auto& [p, st] : start) {
+      st[0] = first_slot[p];
+      for (int k = 1; k <= kKeys; ++k) st[k] += st[k - 1];
+    }
+    for (size_t i = 0; i < n; ++i) slot_of[i] = (uint32_t)start[prog[i]][key[i]]++;
+  }
+  size_t used = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const size_t sl = slot_of[i];
+    if (order) order[sl] = (uint32_t)i;
+    if (!build) continue;
+    const uint8_t* str = strs.data() + soff[i];
+    const uint32_t len = (uint32_t)(soff[i + 1] - soff[i]);
     // meta: [0..3] remote, [4..5] port, [6..7] policy (0xFFFF unknown),
     // [8..11] string length, [12..14] arena offset / 16, [15] flags
     uint8_t meta[16] = {0};
@@ -153,17 +184,16 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     uint16_t pol16 = policy[i] >= s.npolicies ? 0xFFFF : (uint16_t)policy[i];
     memcpy(meta + 6, &pol16, 2);
     uint8_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0;
-    if (malformed) flags |= CG_HTTP_F_MALFORMED;
-    uint32_t len = (uint32_t)str.size();
+    if (malformed[i]) flags |= CG_HTTP_F_MALFORMED;
     memcpy(meta + 8, &len, 4);
     uint8_t slot[CG_HTTP_SLOT_BYTES] = {0};
     if (len <= CG_HTTP_SLOT_BYTES) {
-      memcpy(slot, str.data(), len);
+      memcpy(slot, str, len);
     } else {
       flags |= CG_HTTP_F_OVERFLOW;
       if (used / 16 >= (1u << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
       uint32_t off16 = (uint32_t)(used / 16);
-      if (arena && used + len <= arena_cap) memcpy(arena + used, str.data(), len);
+      if (arena && used + len <= arena_cap) memcpy(arena + used, str, len);
       used += (len + 15) & ~(size_t)15;
       meta[12] = off16 & 0xFF;
       meta[13] = (off16 >> 8) & 0xFF;
