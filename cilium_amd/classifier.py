@@ -111,10 +111,10 @@ class Classifier:
         return v.value
 
     def http_policy_stats(self) -> dict:
-        out = (C.c_uint64 * 10)()
-        N.check(N.lib.cg_http_policy_stats(self.h, out, 10))
+        out = (C.c_uint64 * 12)()
+        N.check(N.lib.cg_http_policy_stats(self.h, out, 12))
         keys = ["programs", "parts", "states", "table_bytes", "fields", "rules", "policies", "remote_slots",
-                "exceptions", "cells"]
+                "exceptions", "cells", "max_program_cells", "lds_programs"]
         return dict(zip(keys, list(out)))
 
     def pack_http(self, policy: np.ndarray, ingress: np.ndarray, port: np.ndarray, remote: np.ndarray,

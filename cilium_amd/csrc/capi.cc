@@ -551,7 +551,13 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
   return guarded([&] {
     auto e = get(h);
     auto s = http_snap(*e);
-    uint64_t v[10] = {s->progs.size(),
+    uint64_t max_prog_cells = 0, lds_progs = 0;
+    for (const auto& pg : s->progs) {
+      if (pg.flags & kProgAllowAll) continue;
+      max_prog_cells = std::max<uint64_t>(max_prog_cells, pg.cell_count);
+      lds_progs += (pg.flags & kProgRebased) && pg.cell_count <= 40960;
+    }
+    uint64_t v[12] = {s->progs.size(),
                      s->parts.size(),
                      s->total_states,
                      s->cells.size() * 4 + s->acc.size() * 4 + s->masks.size() * 8,
@@ -560,8 +566,10 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
                      s->npolicies,
                      s->rhash_keys.size(),
                      s->total_exceptions,
-                     s->cells.size()};
-    for (size_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
+                     s->cells.size(),
+                     max_prog_cells,
+                     lds_progs};
+    for (size_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
   });
 }
 

@@ -160,6 +160,7 @@ struct HttpDev {
   uint32_t nparts;
   uint32_t epoch;
   uint32_t lds_cells;            // max cells a workgroup stages in LDS
+  uint32_t n_global_progs;       // walked programs too large for LDS
   unsigned long long* counters;  // [prog*2] allowed, [prog*2+1] denied, [2*nprogs] stale batches
 };
 

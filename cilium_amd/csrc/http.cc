@@ -661,6 +661,10 @@ void HttpSnapshot::upload(Engine& e) {
     if (!(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= kMaxLdsCells)
       max_cells = std::max(max_cells, pg.cell_count);
   dev.lds_cells = (max_cells + 255) & ~255u;
+  dev.n_global_progs = 0;
+  for (const auto& pg : progs)
+    if (!(pg.flags & kProgAllowAll) && !((pg.flags & kProgRebased) && pg.cell_count <= dev.lds_cells))
+      dev.n_global_progs++;
   dev.counters = d_counters.as<unsigned long long>();
 }
 

@@ -19,6 +19,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kHttpThreads = 1024;
+constexpr int kTilesPerWave = 2;  // independent DFA chains per lane
 
 __device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
                                            uint32_t w) {
@@ -38,27 +39,56 @@ __device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells
                                              uint32_t b) {
   const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + ((st << 2) + (b << 2)));
   const uint32_t dflt = st >= self_lo ? st : 0u;
-  return (e & 0xFFFFu) == st ? (e >> 16) : dflt;
+  // nx = e.lo == st ? e.hi : dflt — SDWA word selects fold the shift
+  uint32_t nx;
+  asm("v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_sdwa %0, %3, %1, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+      : "=v"(nx)
+      : "v"(e), "v"(st), "v"(dflt)
+      : "vcc");
+  return nx;
 }
 
-// Walk the in-record string of a tile's lanes (units 1..8 of the tile).
-// Accepting states absorb (comb.h) and the record is zero-padded, so lanes
-// step through all 16 bytes of a unit with no per-byte length test; units are
+// Walk the in-record strings of K tiles per wave (units 1..8 of each tile):
+// K independent DFA chains per lane hide each other's LDS latency.
+// Accepting states absorb (comb.h) and records are zero-padded, so lanes step
+// through all 16 bytes of a unit with no per-byte length test; units are
 // loaded one ahead and the walk ends once no lane is alive inside its string.
-__device__ __forceinline__ uint32_t walk_tile(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
-                                             const uint4* __restrict__ tb, uint32_t lane, uint32_t len) {
-  if (!__any(len != 0 && st != 0)) return st;
-  uint4 cur = tb[1 * kWave + lane];
-  for (uint32_t u = 0; u < 8; ++u) {
-    const bool more = __any((u + 1) * 16 < len);
-    uint4 nxt = cur;
-    if (more && u < 7) nxt = tb[(u + 2) * kWave + lane];
+template <int K>
+__device__ __forceinline__ void walk_tiles(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t (&st)[K],
+                                           const uint4* const (&tb)[K], uint32_t lane, const uint32_t (&len)[K]) {
+  bool live = false;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) st = comb_step(cells, self_lo, st, get_byte(cur, k));
-    if (!more || !__any(st != 0 && (u + 1) * 16 < len)) break;
-    cur = nxt;
+  for (int j = 0; j < K; ++j) live |= len[j] != 0 && st[j] != 0;
+  if (!__any(live)) return;
+  uint4 cur[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) cur[j] = tb[j][1 * kWave + lane];
+  for (uint32_t u = 0; u < 8; ++u) {
+    bool longer = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) longer |= (u + 1) * 16 < len[j];
+    const bool more = __any(longer);
+    uint4 nxt[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) nxt[j] = cur[j];
+    if (more && u < 7) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) nxt[j] = tb[j][(u + 2) * kWave + lane];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) st[j] = comb_step(cells, self_lo, st[j], get_byte(cur[j], k));
+    }
+    bool alive = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) alive |= st[j] != 0 && (u + 1) * 16 < len[j];
+    if (!more || !__any(alive)) break;
+#pragma unroll
+    for (int j = 0; j < K; ++j) cur[j] = nxt[j];
   }
-  return st;
 }
 
 // Records longer than a slot live in the overflow arena: byte loop.
@@ -68,79 +98,119 @@ __device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cell
   return st;
 }
 
-__device__ __forceinline__ uint32_t remote_row_from(const HttpDev& T, unsigned long long key, uint32_t h,
-                                                    unsigned long long k0, uint32_t v0, uint32_t dflt) {
-  if (k0 == key) return v0;
-  if (k0 == ~0ULL) return dflt;
-  for (uint32_t probe = 1; probe <= T.rhash_mask; ++probe) {
-    h = (h + 1) & T.rhash_mask;
+// Remote-identity mask row of (prog, remote): linear probing from slot h.
+__device__ __forceinline__ uint32_t remote_row(const HttpDev& T, unsigned long long key, uint32_t h,
+                                               uint32_t dflt) {
+  for (uint32_t probe = 0; probe <= T.rhash_mask; ++probe) {
     const unsigned long long k = T.rhash_keys[h];
     if (k == key) return T.rhash_vals[h];
     if (k == ~0ULL) break;
+    h = (h + 1) & T.rhash_mask;
   }
   return dflt;
 }
 
-// One tile of 64 requests of program `prog` (a real, non-trivial program).
-// `pcells`: the program's cell block when it is rebased (LDS copy or global),
-// else the global table (parts walk from their own offsets).
-__device__ __forceinline__ void http_tile(const HttpDev& T, const HttpProg& pg, uint32_t prog,
-                                          const uint32_t* __restrict__ pcells, bool rebased,
-                                          const uint4* __restrict__ tb, const uint8_t* __restrict__ arena,
-                                          uint8_t* __restrict__ out, size_t slot, uint32_t lane, uint32_t* n_allow,
-                                          uint32_t* n_deny) {
-  const uint4 meta = tb[lane];
-  const uint32_t remote = meta.x;
-  const uint32_t flags = meta.w >> 24;
-  const uint32_t aoff = (meta.w & 0xFFFFFFu) * 16u;
-  const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
-  const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
-  const uint32_t len = counted && !overflow ? meta.z : 0u;
-  // first probe of the remote-identity mask, issued before the walk so its
-  // latency hides behind it
-  const unsigned long long rkey = ((unsigned long long)prog << 32) | remote;
-  const uint32_t rh = hash64to32(rkey) & T.rhash_mask;
-  const unsigned long long rk0 = T.rhash_keys[rh];
-  const uint32_t rv0 = T.rhash_vals[rh];
-  uint32_t verdict = 0;
-  uint32_t rrow = 0;
-  bool have_rrow = false;
+// K tiles of 64 requests of program `prog` (a real, non-trivial program);
+// tile j takes part only if valid[j].  `pcells`: the program's cell block
+// when it is rebased (LDS copy or global), else the global table (parts walk
+// from their own offsets).
+template <int K>
+__device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg, uint32_t prog,
+                                           const uint32_t* __restrict__ pcells, bool rebased,
+                                           const uint4* __restrict__ tiles, const uint32_t (&tile)[K],
+                                           const bool (&valid)[K], const uint8_t* __restrict__ arena,
+                                           uint8_t* __restrict__ out, uint32_t lane, uint32_t* n_allow,
+                                           uint32_t* n_deny) {
+  const uint4* tb[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) tb[j] = tiles + (size_t)tile[j] * (CG_HTTP_UNITS * kWave);
+  // only the string lengths stay live across the walk; the rest of the meta
+  // unit is re-read (an L2 hit) afterwards
+  uint32_t len[K];
+  bool any_overflow = false;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint4 meta = tb[j][lane];
+    const uint32_t flags = meta.w >> 24;
+    const bool counted = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+    const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
+    len[j] = counted && !overflow ? meta.z : 0u;
+    any_overflow |= overflow;
+  }
+  any_overflow = __any(any_overflow);
+  uint32_t verdict[K], rrow[K];
+  bool counted[K], have_rrow[K];
+  unsigned long long rkey[K];
+  uint32_t rh[K];
   for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
     const HttpPart pt = T.parts[pg.part_begin + pi];
     const uint32_t* __restrict__ cells = rebased ? pcells : pcells + pt.walk_off;
-    uint32_t st = walk_tile(cells, pt.self_lo, pt.start, tb, lane, len);
-    if (__any(overflow)) {
-      const uint32_t sa = walk_arena(cells, pt.self_lo, pt.start, arena, aoff, overflow ? meta.z : 0u);
-      if (overflow) st = sa;
-    }
-    if (!counted) st = 0;
-    const uint32_t lab = st ? (cells[st - 1] >> 16) : 0xFFFFu;
-    if (lab != 0xFFFFu && !verdict) {
-      if (!have_rrow) {
-        rrow = remote_row_from(T, rkey, rh, rk0, rv0, pg.default_remote);
-        have_rrow = true;
+    uint32_t st[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) st[j] = pt.start;
+    walk_tiles<K>(cells, pt.self_lo, st, tb, lane, len);
+    if (pi == 0) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint4 meta = tb[j][lane];
+        const uint32_t flags = meta.w >> 24;
+        counted[j] = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+        rkey[j] = ((unsigned long long)prog << 32) | meta.x;
+        rh[j] = hash64to32(rkey[j]) & T.rhash_mask;
+        verdict[j] = 0;
+        rrow[j] = 0;
+        have_rrow[j] = false;
       }
-      if (masks_meet(T.masks, T.acc[pt.acc_off + lab], rrow, pg.mask_words)) verdict = 1;
+    }
+    if (any_overflow) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint4 meta = tb[j][lane];
+        const bool ov = counted[j] && ((meta.w >> 24) & CG_HTTP_F_OVERFLOW);
+        const uint32_t sa = walk_arena(cells, pt.self_lo, pt.start, arena, (meta.w & 0xFFFFFFu) * 16u, ov ? meta.z : 0u);
+        if (ov) st[j] = sa;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t sj = counted[j] ? st[j] : 0u;
+      const uint32_t lab = sj ? (cells[sj - 1] >> 16) : 0xFFFFu;
+      if (lab != 0xFFFFu && !verdict[j]) {
+        if (!have_rrow[j]) {
+          rrow[j] = remote_row(T, rkey[j], rh[j], pg.default_remote);
+          have_rrow[j] = true;
+        }
+        if (masks_meet(T.masks, T.acc[pt.acc_off + lab], rrow[j], pg.mask_words)) verdict[j] = 1;
+      }
     }
   }
-  if (counted && !verdict && (pg.flags & kProgHasAlways)) {
-    if (!have_rrow) rrow = remote_row_from(T, rkey, rh, rk0, rv0, pg.default_remote);
-    if (masks_meet(T.masks, pg.always_off, rrow, pg.mask_words)) verdict = 1;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (counted[j] && !verdict[j] && (pg.flags & kProgHasAlways)) {
+      if (!have_rrow[j]) rrow[j] = remote_row(T, rkey[j], rh[j], pg.default_remote);
+      if (masks_meet(T.masks, pg.always_off, rrow[j], pg.mask_words)) verdict[j] = 1;
+    }
+    if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict[j];
+    *n_allow += counted[j] && verdict[j];
+    *n_deny += counted[j] && !verdict[j];
   }
-  out[slot] = (uint8_t)verdict;
-  *n_allow += counted && verdict;
-  *n_deny += counted && !verdict;
 }
 
-__global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(HttpDev T, const uint8_t* __restrict__ batch,
-                                                            size_t nslots, const uint8_t* __restrict__ arena,
-                                                            uint8_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
+// One workgroup per chunk (grid-stride).  kGlobal = false: chunks of trivial
+// programs and of programs whose table fits the workgroup's LDS share, which
+// is staged once per chunk; kGlobal = true: the remaining chunks (programs
+// too large for LDS), walked from global memory — a separate kernel so the
+// rare path does not set the common one's register budget.
+template <bool kGlobal>
+__device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
+                                            const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
+                                            uint32_t* lcells) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
   const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
   const uint64_t toff = H->tiles_off;
   if (magic != kBatchMagic || epoch != T.epoch || (size_t)ntiles * kWave > nslots) {
     // packed against another snapshot (or not a batch): deny every slot
+    if (kGlobal) return;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (size_t)gridDim.x * blockDim.x)
       out[i] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&T.counters[2 * T.nprogs], 1ULL);
@@ -158,28 +228,42 @@ __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8,
     if (real) pg = T.progs[prog];
     const bool walkp = real && !(pg.flags & kProgAllowAll);
     const bool lds = walkp && (pg.flags & kProgRebased) && pg.cell_count <= T.lds_cells;
+    if (kGlobal != (walkp && !lds)) continue;  // the other kernel's chunk
     uint32_t n_allow = 0, n_deny = 0;
-    __syncthreads();  // the previous chunk is done with lcells
-    if (lds)
-      for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
-    __syncthreads();
-    for (uint32_t t = ch.first_tile + wave; t < ch.first_tile + ch.ntiles; t += nw) {
-      const uint4* tb = tiles + (size_t)t * (CG_HTTP_UNITS * kWave);
-      const size_t slot = (size_t)t * kWave + lane;
-      if (!walkp) {
+    const uint32_t tend = ch.first_tile + ch.ntiles;
+    if (!walkp) {
+      for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         // no policy for the port → allow; unknown policy → deny; a scope
         // without HTTP rules → allow (cilium_network_policy.h:129-138,187-191)
-        const uint32_t flags = tb[lane].w >> 24;
+        const uint32_t flags = tiles[(size_t)t * (CG_HTTP_UNITS * kWave) + lane].w >> 24;
         const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
-        const uint32_t v = counted && (prog == kProgAllow || real) ? 1u : 0u;
-        out[slot] = (uint8_t)v;
+        out[(size_t)t * kWave + lane] = (uint8_t)(counted && (prog == kProgAllow || real) ? 1u : 0u);
         n_allow += real && counted;
-      } else if (lds) {
-        http_tile(T, pg, prog, lcells, true, tb, arena, out, slot, lane, &n_allow, &n_deny);
-      } else if (pg.flags & kProgRebased) {
-        http_tile(T, pg, prog, T.cells + pg.cell_begin, true, tb, arena, out, slot, lane, &n_allow, &n_deny);
-      } else {
-        http_tile(T, pg, prog, T.cells, false, tb, arena, out, slot, lane, &n_allow, &n_deny);
+      }
+    } else if (kGlobal) {
+      const bool rebased = pg.flags & kProgRebased;
+      const uint32_t* pcells = rebased ? T.cells + pg.cell_begin : T.cells;
+      for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
+        const uint32_t tile[1] = {t};
+        const bool valid[1] = {true};
+        http_tiles<1>(T, pg, prog, pcells, rebased, tiles, tile, valid, arena, out, lane, &n_allow, &n_deny);
+      }
+    } else {
+      __syncthreads();  // the previous chunk is done with lcells
+      for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
+      __syncthreads();
+      // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)
+      for (uint32_t t0 = ch.first_tile + wave; t0 < tend; t0 += kTilesPerWave * nw) {
+        uint32_t tile[kTilesPerWave];
+        bool valid[kTilesPerWave];
+#pragma unroll
+        for (int j = 0; j < kTilesPerWave; ++j) {
+          const uint32_t t = t0 + j * nw;
+          valid[j] = t < tend;
+          tile[j] = valid[j] ? t : t0;
+        }
+        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, tile, valid, arena, out, lane, &n_allow,
+                                  &n_deny);
       }
     }
     if (real) {
@@ -194,6 +278,19 @@ __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8,
       }
     }
   }
+}
+
+__global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
+    HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
+    uint8_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
+  http_chunks<false>(T, batch, nslots, arena, out, lcells);
+}
+
+__global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
+                                                                   size_t nslots, const uint8_t* __restrict__ arena,
+                                                                   uint8_t* __restrict__ out) {
+  http_chunks<true>(T, batch, nslots, arena, out, nullptr);
 }
 
 }  // namespace
@@ -219,10 +316,15 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
     occ = nb;
     occ_lds = lds;
   }
-  size_t tiles = nslots / kWave;
+  const size_t tiles = nslots / kWave;
   size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);
-  hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds,
-                     (hipStream_t)stream, t, (const uint8_t*)batch, nslots, arena, out);
+  hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
+                     (const uint8_t*)batch, nslots, arena, out);
+  if (t.n_global_progs) {
+    grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
+    hipLaunchKernelGGL(http_kernel_global, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream, t,
+                       (const uint8_t*)batch, nslots, arena, out);
+  }
   return (int)hipGetLastError();
 }
 
