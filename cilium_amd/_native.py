@@ -10,7 +10,8 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libciliumgpu.so"
+# CILIUM_AMD_LIB: load another build of the same library (kernel experiments)
+LIB_PATH = Path(os.environ.get("CILIUM_AMD_LIB") or Path(__file__).resolve().parent / "libciliumgpu.so")
 
 # cg_result (include/cilium_gpu.h)
 CG_OK = 0

@@ -149,25 +149,36 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     }
   }
   // ---- slot assignment: within a program group, requests ordered by the
-  // number of 16-byte units their string spans (stable), so the lanes of a
-  // tile end their walks together
+  // number of 16-byte units their string spans, so the lanes of a tile end
+  // their walks together, then by the string itself, so neighbouring lanes
+  // share DFA states for as long as their strings share a prefix (their LDS
+  // reads then broadcast instead of conflicting)
   std::vector<uint32_t> slot_of(n);
   {
-    constexpr int kKeys = CG_HTTP_UNITS + 1;  // 0..8 units, 9 = overflow arena
-    std::map<uint32_t, std::array<size_t, kKeys + 1>> start;
     std::vector<uint8_t> key(n, 0);
     for (size_t i = 0; i < n; ++i) {
       const size_t len = build ? soff[i + 1] - soff[i] : 0;
-      key[i] = len > CG_HTTP_SLOT_BYTES ? kKeys - 1 : (uint8_t)((len + 15) / 16);
-      auto it = start.find(prog[i]);
-      if (it == start.end()) it = start.emplace(prog[i], std::array<size_t, kKeys + 1>{}).first;
-      it->second[key[i] + 1]++;
+      key[i] = len > CG_HTTP_SLOT_BYTES ? CG_HTTP_UNITS + 1 : (uint8_t)((len + 15) / 16);
     }
-    for (auto& [p, st] : start) {
-      st[0] = first_slot[p];
-      for (int k = 1; k <= kKeys; ++k) st[k] += st[k - 1];
+    std::vector<uint32_t> idx(n);
+    for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+      if (prog[a] != prog[b]) return prog[a] < prog[b];
+      if (key[a] != key[b]) return key[a] < key[b];
+      if (build) {
+        const size_t la = soff[a + 1] - soff[a], lb = soff[b + 1] - soff[b];
+        const int c = memcmp(strs.data() + soff[a], strs.data() + soff[b], std::min(la, lb));
+        if (c != 0) return c < 0;
+        if (la != lb) return la < lb;
+      }
+      return a < b;
+    });
+    size_t pos = 0;
+    for (size_t r = 0; r < n; ++r) {
+      const uint32_t i = idx[r];
+      if (r == 0 || prog[i] != prog[idx[r - 1]]) pos = first_slot[prog[i]];
+      slot_of[i] = (uint32_t)pos++;
     }
-    for (size_t i = 0; i < n; ++i) slot_of[i] = (uint32_t)start[prog[i]][key[i]]++;
   }
   size_t used = 0;
   for (size_t i = 0; i < n; ++i) {

@@ -1,0 +1,57 @@
+"""Kernel experiments: build variants of kernels_http.hip (text substitutions
+applied to a copy) into tools/_exp/lib_<name>.so, linked with the library's
+other objects.  Run on the GPU box with tools/exp_http.sh; each variant is
+timed by tools/prof_http.py through CILIUM_AMD_LIB.  Variants are measuring
+devices only (e.g. "no LDS read") — their verdicts are meaningless.
+
+    python tools/exp_http.py build
+"""
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from cilium_amd import build as B  # noqa: E402
+
+OUT = ROOT / "tools" / "_exp"
+LDS_READ = ("  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + "
+            "((st << 2) + (b << 2)));")
+# keeps the walk's result live but never lets a meaningless state index the
+# accept tables (variants that break the DFA must stay memory-safe)
+SAFE_LABEL = ("      const uint32_t sj = counted[j] ? st[j] : 0u;",
+              "      const uint32_t sj = (st[j] == 0xFFFFFFFFu) ? 1u : 0u;")
+VARIANTS = {
+    "base": [],
+    # dependency chain kept on VALU, no LDS access
+    "nolds": [SAFE_LABEL, (LDS_READ, "  const uint32_t e = (st * 2654435761u) ^ (b << 16) ^ b ^ (uint32_t)(size_t)cells;")],
+    # no DFA steps: stream the units only
+    "nowalk": [SAFE_LABEL, ("      for (int j = 0; j < K; ++j) st[j] = comb_step(cells, self_lo, st[j], get_byte(cur[j], k));",
+                "      for (int j = 0; j < K; ++j) st[j] ^= get_byte(cur[j], k);")],
+    "k1": [("constexpr int kTilesPerWave = 2;", "constexpr int kTilesPerWave = 1;")],
+}
+
+
+def build_variant(name, subs):
+    src = (B.CSRC / "kernels_http.hip").read_text()
+    for a, b in subs:
+        assert a in src, (name, a)
+        src = src.replace(a, b)
+    OUT.mkdir(exist_ok=True)
+    f = OUT / f"kernels_http_{name}.hip"
+    f.write_text(src.replace('"../../include/cilium_gpu.h"', f'"{ROOT}/include/cilium_gpu.h"'))
+    obj = OUT / f"kernels_http_{name}.o"
+    cmd = [B.HIPCC, *B._flags("x.hip"), "-I", str(B.CSRC), "-c", str(f), "-o", str(obj)]
+    subprocess.run(cmd, check=True)
+    others = [B.BUILD / (s + ".o") for s in B.SOURCES if s != "kernels_http.hip"]
+    lib = OUT / f"lib_{name}.so"
+    subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *map(str, others), str(obj), "-o",
+                    str(lib)], check=True)
+    print("built", lib)
+
+
+if __name__ == "__main__":
+    B.build(verbose=False)
+    names = sys.argv[2:] or list(VARIANTS)
+    for n in names:
+        build_variant(n, VARIANTS[n])
