@@ -30,6 +30,7 @@ METRIC = "policy verdicts/sec (whole node) + request GB/s, 10K-rule L7 HTTP set"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 RECORD_BYTES = 144      # 16-byte meta unit + 128-byte field slot (include/cilium_gpu.h)
 OUT_BYTES = 1
+CHUNK_TILES = 64        # kChunkTiles (csrc/dev_types.h)
 
 
 def parse():
@@ -74,9 +75,10 @@ def main():
     D = min(args.distinct - args.distinct % 64, args.requests_per_gpu)
     rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
     b = cl.pack_http(**rq)
+    field_bytes = mean_field_bytes(b)
     reps = max(1, args.requests_per_gpu // D)
     B = reps * D                                  # requests per GPU per step
-    d_batch, nslots = replicate_batch(b, reps, dev, torch)
+    d_batch, nslots, tile_map = replicate_batch(b, reps, dev, torch)
     d_arena = torch.from_numpy(b.arena).to(dev)
     d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
     nprog_ctr = int(cl.read_counters(0).size)
@@ -105,7 +107,8 @@ def main():
         step()
         torch.cuda.synchronize()
         import oracle
-        slots = d_out[:b.nslots].cpu().numpy()
+        out_tiles = d_out.view(-1, 64)[torch.from_numpy(tile_map).to(dev)]
+        slots = out_tiles.reshape(-1).cpu().numpy()  # the first copy, in b's slot order
         got = np.zeros(D, np.uint8)
         real = b.order < D
         got[b.order[real]] = slots[real]
@@ -138,8 +141,11 @@ def main():
     ms_per_step = wall / args.steps * 1e3
     per_launch_bytes = B * (RECORD_BYTES + OUT_BYTES)
     achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
-    allow_frac = float(d_out[:b.nslots].float().sum().item()) / D
+    allow_frac = float(d_out.float().sum().item()) / B
 
+    traffic_bytes, traffic_src = pmc_traffic(B)
+    # same unit as `achieved`: HBM bytes per launch over the measured launch time
+    traffic = traffic_bytes / (kernel_ms * 1e-3) / 1e9 if traffic_bytes else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pols, info, args.cpu_seconds)
@@ -165,12 +171,15 @@ def main():
                        "dfa_states": int(stats["states"]), "table_bytes": int(stats["table_bytes"]),
                        "compile_s": round(compile_s, 3), "record_bytes": RECORD_BYTES, "parallelism": f"dp{world}"},
             "request_gbps": value * (RECORD_BYTES + OUT_BYTES) / 1e9,
+            "field_bytes_per_request": field_bytes,
+            "field_gbps": value * field_bytes / 1e9,
             "allow_fraction": allow_frac,
             "parity_check": check,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                          "kernel": "http_kernel", "kernel_ms": kernel_ms,
-                         "bytes_per_launch": per_launch_bytes},
+                         "bytes_per_launch": per_launch_bytes, "traffic_bytes_per_launch": traffic_bytes,
+                         "traffic_source": traffic_src},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -180,34 +189,83 @@ def main():
 
 
 def replicate_batch(b, reps: int, dev, torch):
-    """Device batch holding `reps` copies of packed batch b: the chunk table is
-    repeated with tile offsets shifted, the tiles are copied on the device."""
+    """Device batch of `reps` copies of packed batch b, laid out as the packer
+    lays out a batch of reps x D requests: each program's tiles (its `reps`
+    copies) are contiguous and cut into chunks of CHUNK_TILES
+    (http_pack.cc).  Returns (device batch, nslots, tile_map) where
+    tile_map[t] is the tile of the first copy of b's tile t."""
     hdr = b.batch[:64].copy()
     nchunks = int(hdr[8:12].view(np.uint32)[0])
     ntiles = int(hdr[12:16].view(np.uint32)[0])
     toff = int(hdr[16:24].view(np.uint64)[0])
     tile_bytes = 64 * RECORD_BYTES
     chunks = b.batch[64:64 + 16 * nchunks].view(np.uint32).reshape(nchunks, 4)
-    big = np.tile(chunks, (reps, 1))
-    big[:, 1] += np.repeat(np.arange(reps, dtype=np.uint32) * ntiles, nchunks)
-    hbytes = (64 + 16 * nchunks * reps + 1023) // 1024 * 1024
-    hdr[8:12] = np.array([nchunks * reps], np.uint32).view(np.uint8)
-    hdr[12:16] = np.array([ntiles * reps], np.uint32).view(np.uint8)
+    groups = []  # (prog, first tile, ntiles) of each program group of b
+    for prog, first, nt, _ in chunks:
+        if groups and groups[-1][0] == prog and groups[-1][1] + groups[-1][2] == first:
+            groups[-1][2] += int(nt)
+        else:
+            groups.append([int(prog), int(first), int(nt)])
+    big, placed, pos = [], [], 0
+    for prog, first, nt in groups:
+        run = nt * reps
+        for k in range(0, run, CHUNK_TILES):
+            big.append((prog, pos + k, min(CHUNK_TILES, run - k), 0))
+        placed.append((first, nt, pos))
+        pos += run
+    big = np.asarray(big, np.uint32)
+    hbytes = (64 + 16 * len(big) + 1023) // 1024 * 1024
+    hdr[8:12] = np.array([len(big)], np.uint32).view(np.uint8)
+    hdr[12:16] = np.array([pos], np.uint32).view(np.uint8)
     hdr[16:24] = np.array([hbytes], np.uint64).view(np.uint8)
-    hdr[24:32] = np.array([ntiles * reps * 64], np.uint64).view(np.uint8)
+    hdr[24:32] = np.array([pos * 64], np.uint64).view(np.uint8)
     head = np.zeros(hbytes, np.uint8)
     head[:64] = hdr
     head[64:64 + big.nbytes] = big.reshape(-1).view(np.uint8)
-    region = ntiles * tile_bytes
-    d = torch.empty(hbytes + reps * region, dtype=torch.uint8, device=dev)
+    d = torch.empty(hbytes + pos * tile_bytes, dtype=torch.uint8, device=dev)
     d[:hbytes].copy_(torch.from_numpy(head))
-    d[hbytes:hbytes + region].copy_(torch.from_numpy(b.batch[toff:toff + region]))
-    done = 1
-    while done < reps:  # doubling copies on the device
-        k = min(done, reps - done)
-        d[hbytes + done * region:hbytes + (done + k) * region].copy_(d[hbytes:hbytes + k * region])
-        done += k
-    return d, ntiles * reps * 64
+    src = torch.from_numpy(b.batch[toff:toff + ntiles * tile_bytes]).to(dev)
+    tile_map = np.zeros(ntiles, np.int64)
+    for first, nt, at in placed:
+        g0 = hbytes + at * tile_bytes
+        gb = nt * tile_bytes
+        d[g0:g0 + gb].copy_(src[first * tile_bytes:(first + nt) * tile_bytes])
+        done = 1
+        while done < reps:  # doubling copies on the device
+            k = min(done, reps - done)
+            d[g0 + done * gb:g0 + (done + k) * gb].copy_(d[g0:g0 + k * gb])
+            done += k
+        tile_map[first:first + nt] = np.arange(at, at + nt)
+    return d, pos * 64, tile_map
+
+
+def mean_field_bytes(b) -> float:
+    """Mean length of the requests' field strings (header values joined by
+    the packer's separators, http_pack.cc) over the real slots of batch b."""
+    ntiles = int(b.batch[12:16].view(np.uint32)[0])
+    toff = int(b.batch[16:24].view(np.uint64)[0])
+    meta = b.batch[toff:toff + ntiles * 64 * RECORD_BYTES].reshape(ntiles, 9, 64, 16)[:, 0]
+    ln = meta.reshape(-1, 16)[:, 8:12].copy().view(np.uint32).reshape(-1)
+    real = b.order != 0xFFFFFFFF
+    return float(ln[real].mean()) if real.any() else 0.0
+
+
+def pmc_traffic(requests_per_launch: int):
+    """HBM bytes per launch of the verdict kernel from the newest committed
+    PMC summary (profiles/r*_http_pmc.json, written by tools/pmc_summary.py
+    from separate rocprofv3 --pmc passes of the same workload: FETCH_SIZE ×2
+    gfx950 correction + WRITE_SIZE), scaled to this launch's request count.
+    rocprofv3 cannot run inside the timed process, hence a committed file."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_http_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        s = json.load(f)
+    per_item = s.get("hbm_bytes_per_item")
+    if not per_item:
+        return None, None
+    return per_item * requests_per_launch, os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(pols, info, seconds: float) -> dict:

@@ -271,15 +271,19 @@ class PolicyMap:
             a[i] = (k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection)
         return a
 
-    def allow_key(self, k: PolicyKey, proxy_port_be: int) -> None:
-        """AllowKey: proxy_port already in network byte order (as PolicyEntry stores it)."""
-        self.allow_keys(self._keys([k]), np.asarray([proxy_port_be], np.uint16))
+    def allow_key(self, k: PolicyKey, proxy_port: int) -> None:
+        """AllowKey (policymap.go:164-166): key and proxy_port in host byte
+        order, converted to network order on insert as Allow does."""
+        self.allow(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection, proxy_port)
 
     def allow(self, identity: int, dport: int, proto: int, direction: int, proxy_port: int) -> None:
         """Allow (policymap.go:170-176): dport and proxy_port in host byte order."""
-        self.allow_key(PolicyKey(identity, htons(dport), proto, int(direction)), htons(proxy_port))
+        self.allow_keys(self._keys([PolicyKey(identity, htons(dport), proto, int(direction))]),
+                        np.asarray([htons(proxy_port)], np.uint16))
 
     def allow_keys(self, keys: np.ndarray, ports_be: np.ndarray) -> None:
+        """Batched insert of raw map keys/values (network byte order, as the
+        BPF map stores them)."""
         keys = np.ascontiguousarray(keys, POLICY_KEY_DTYPE)
         ports_be = np.ascontiguousarray(ports_be, np.uint16)
         N.check(N.lib.cg_policymap_allow(self.cl.h, self.id, _p(keys), _p(ports_be), len(keys)))
@@ -297,11 +301,13 @@ class PolicyMap:
         return PolicyEntry(e.proxy_port, e.packets, e.bytes)
 
     def delete_key(self, k: PolicyKey) -> None:
-        key = self._keys([k])
-        N.check(N.lib.cg_policymap_delete(self.cl.h, self.id, _p(key), 1))
+        """DeleteKey (policymap.go:188-190): key in host byte order."""
+        self.delete(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection)
 
     def delete(self, identity: int, dport: int, proto: int, direction: int) -> None:
-        self.delete_key(PolicyKey(identity, htons(dport), proto, int(direction)))
+        """Delete (policymap.go:196-199): dport in host byte order."""
+        key = self._keys([PolicyKey(identity, htons(dport), proto, int(direction))])
+        N.check(N.lib.cg_policymap_delete(self.cl.h, self.id, _p(key), 1))
 
     def dump_to_slice(self) -> list[tuple[PolicyKey, PolicyEntry]]:
         n = C.c_size_t()

@@ -45,7 +45,7 @@ constexpr uint8_t kSep = 0x00;
 constexpr uint8_t kAbsent = 0x01;
 constexpr int kMaxUnionStates = 400000;  // before minimization, per part
 constexpr int kMaxPartStates = 65535;    // u16 transition entries
-constexpr uint32_t kMaxLdsCells = 40960;  // 160 KiB: one program table per workgroup
+constexpr uint32_t kMaxLdsCells = 40944;  // 160 KiB less 64 B of static LDS (counters): one program table per workgroup
 
 enum class MKind { Exact, Regex, Present };
 struct MatcherSpec {
@@ -660,7 +660,7 @@ void HttpSnapshot::upload(Engine& e) {
   for (const auto& pg : progs)
     if (!(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= kMaxLdsCells)
       max_cells = std::max(max_cells, pg.cell_count);
-  dev.lds_cells = (max_cells + 255) & ~255u;
+  dev.lds_cells = std::min((max_cells + 255) & ~255u, kMaxLdsCells);
   dev.n_global_progs = 0;
   for (const auto& pg : progs)
     if (!(pg.flags & kProgAllowAll) && !((pg.flags & kProgRebased) && pg.cell_count <= dev.lds_cells))

@@ -19,7 +19,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kHttpThreads = 1024;
-constexpr int kTilesPerWave = 2;  // independent DFA chains per lane
+constexpr int kTilesPerWave = 1;  // DFA chains per lane (2 measured slower: the chains share VCC in comb_step)
 
 __device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
                                            uint32_t w) {
@@ -196,6 +196,31 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   }
 }
 
+// End of a workgroup's run of chunks of program `prog`: wave totals are
+// summed in LDS, then one thread adds them to the global counters.  Ends
+// with every wave past a barrier, so the caller may restage lcells.
+__device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, uint32_t& n_allow, uint32_t& n_deny,
+                                             uint32_t lane, uint32_t* s_cnt) {
+  const bool real = prog < T.nprogs;  // uniform
+  if (real) {
+    for (int o = 32; o > 0; o >>= 1) {
+      n_allow += __shfl_down(n_allow, o, kWave);
+      n_deny += __shfl_down(n_deny, o, kWave);
+    }
+    if (lane == 0) {
+      atomicAdd(&s_cnt[0], n_allow);
+      atomicAdd(&s_cnt[1], n_deny);
+    }
+  }
+  n_allow = n_deny = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (real && s_cnt[0]) atomicAdd(&T.counters[2 * prog], (unsigned long long)s_cnt[0]);
+    if (real && s_cnt[1]) atomicAdd(&T.counters[2 * prog + 1], (unsigned long long)s_cnt[1]);
+    s_cnt[0] = s_cnt[1] = 0;
+  }
+}
+
 // One workgroup per chunk (grid-stride).  kGlobal = false: chunks of trivial
 // programs and of programs whose table fits the workgroup's LDS share, which
 // is staged once per chunk; kGlobal = true: the remaining chunks (programs
@@ -204,7 +229,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 template <bool kGlobal>
 __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
                                             const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                            uint32_t* lcells) {
+                                            uint32_t* lcells, uint32_t* s_cnt) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
   const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
   const uint64_t toff = H->tiles_off;
@@ -219,6 +244,14 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
   const HttpChunk* chunks = reinterpret_cast<const HttpChunk*>(batch + sizeof(HttpBatchHeader));
   const uint4* tiles = reinterpret_cast<const uint4*>(batch + toff);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // Chunks are dealt round-robin: a contiguous run per workgroup would pin
+  // each workgroup to one program and the costliest program sets the tail.
+  // Allowed/denied counts stay in registers while consecutive chunks share a
+  // program and go to the global counters once per run (one atomic pair per
+  // workgroup): concurrent workgroups work on the same program, so per-wave
+  // atomics would all hit the same two addresses.
+  uint32_t cur = kProgDeny;  // program of the current run (its table is in LDS if walked there)
+  uint32_t n_allow = 0, n_deny = 0;
   for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const HttpChunk ch = chunks[c];
     if (ch.first_tile + ch.ntiles > ntiles || ch.ntiles > kChunkTiles) continue;  // malformed chunk
@@ -229,7 +262,13 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
     const bool walkp = real && !(pg.flags & kProgAllowAll);
     const bool lds = walkp && (pg.flags & kProgRebased) && pg.cell_count <= T.lds_cells;
     if (kGlobal != (walkp && !lds)) continue;  // the other kernel's chunk
-    uint32_t n_allow = 0, n_deny = 0;
+    if (prog != cur) {  // uniform across the workgroup: same chunk sequence
+      flush_counts(T, cur, n_allow, n_deny, lane, s_cnt);
+      if (lds)
+        for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
+      __syncthreads();
+      cur = prog;
+    }
     const uint32_t tend = ch.first_tile + ch.ntiles;
     if (!walkp) {
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
@@ -249,9 +288,6 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         http_tiles<1>(T, pg, prog, pcells, rebased, tiles, tile, valid, arena, out, lane, &n_allow, &n_deny);
       }
     } else {
-      __syncthreads();  // the previous chunk is done with lcells
-      for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
-      __syncthreads();
       // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)
       for (uint32_t t0 = ch.first_tile + wave; t0 < tend; t0 += kTilesPerWave * nw) {
         uint32_t tile[kTilesPerWave];
@@ -266,31 +302,23 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
                                   &n_deny);
       }
     }
-    if (real) {
-      // wave totals → two atomics per wave per chunk
-      for (int o = 32; o > 0; o >>= 1) {
-        n_allow += __shfl_down(n_allow, o, kWave);
-        n_deny += __shfl_down(n_deny, o, kWave);
-      }
-      if (lane == 0) {
-        if (n_allow) atomicAdd(&T.counters[2 * prog], (unsigned long long)n_allow);
-        if (n_deny) atomicAdd(&T.counters[2 * prog + 1], (unsigned long long)n_deny);
-      }
-    }
   }
+  flush_counts(T, cur, n_allow, n_deny, lane, s_cnt);
 }
 
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
     uint8_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
-  http_chunks<false>(T, batch, nslots, arena, out, lcells);
+  __shared__ uint32_t s_cnt[2];
+  http_chunks<false>(T, batch, nslots, arena, out, lcells, s_cnt);
 }
 
 __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
                                                                    size_t nslots, const uint8_t* __restrict__ arena,
                                                                    uint8_t* __restrict__ out) {
-  http_chunks<true>(T, batch, nslots, arena, out, nullptr);
+  __shared__ uint32_t s_cnt[2];
+  http_chunks<true>(T, batch, nslots, arena, out, nullptr, s_cnt);
 }
 
 }  // namespace
@@ -300,7 +328,7 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   if (nslots == 0) return 0;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
     attr = true;
   }
   // one resident wave of workgroups: as many per CU as LDS and registers
