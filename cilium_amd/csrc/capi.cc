@@ -560,7 +560,7 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
     uint64_t v[12] = {s->progs.size(),
                      s->parts.size(),
                      s->total_states,
-                     s->cells.size() * 4 + s->acc.size() * 4 + s->masks.size() * 8,
+                     s->cells.size() * 4 + s->masks.size() * 8,
                      s->fields.size(),
                      s->total_rules,
                      s->npolicies,

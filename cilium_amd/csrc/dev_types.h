@@ -91,23 +91,24 @@ struct HttpProg {
   uint32_t part_count;
   uint32_t flags;
   uint32_t mask_words;      // W
-  uint32_t always_off;      // u64 word offset of the "no HTTP rules" PNPR mask
-  uint32_t default_remote;  // u64 word offset of the mask for unlisted remotes
-  uint32_t cell_begin;      // the program's parts are contiguous in cells[]:
-  uint32_t cell_count;      // staged into LDS as one block
+  uint32_t always_off;      // block offset (u32 units) of the "no HTTP rules" PNPR mask
+  uint32_t default_remote;  // masks[] u64 word offset of the mask for unlisted remotes
+  uint32_t cell_begin;      // the program's block in cells[], staged into LDS
+  uint32_t cell_count;      // as one piece: parts' comb cells, label tables, masks
 };
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; states >= self_lo default to themselves.
-// An accepting state's header cell holds its accept label and
-// acc[acc_off + label] the u64 word offset of its PNPR mask.  When a
-// program's block stays below 0xFFFF cells its parts are rebased onto the
-// block (walk_off = cell_begin for every part), so the kernel walks all parts
-// through one pointer — the LDS copy.
+// An accepting state's header cell holds its accept label; block[acc_off +
+// label] is the block offset of its PNPR mask (u64 words stored as u32
+// pairs, 8-byte aligned), block = cells + cell_begin.  When a program's DFA
+// cells stay below 0xFFFF its parts are rebased onto the block (walk_off =
+// cell_begin for every part), so the kernel walks all parts through one
+// pointer — the LDS copy.
 constexpr uint32_t kProgRebased = 4;
 struct HttpPart {
   uint32_t cell_off;  // first cell of this part in cells[]
   uint32_t ncells;
-  uint32_t acc_off;   // into acc (u32), indexed by accept label
+  uint32_t acc_off;   // block offset of the label table (u32 per accept label)
   uint32_t start;     // start state
   uint32_t nstates;
   uint32_t self_lo;
@@ -144,8 +145,7 @@ struct HttpDev {
   const HttpProg* progs;
   const HttpPart* parts;
   const uint32_t* cells;
-  const uint32_t* acc;
-  const unsigned long long* masks;
+  const unsigned long long* masks;  // remote-identity rows (rhash_vals → u64 word offset)
   // program lookup: key = policy<<17 | ingress<<16 | port
   const uint32_t* phash_keys;  // empty = 0xFFFFFFFF
   const uint32_t* phash_vals;

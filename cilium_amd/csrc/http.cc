@@ -15,8 +15,12 @@
 // Compilation: the header fields referenced by any matcher form a fixed
 // field order F (":method", ":path", ":authority", then other names sorted).
 // A request becomes the string  v_1 SEP v_2 SEP ... v_F SEP  with SEP = 0x00
-// and an absent header encoded as the single byte 0x01 (neither byte can
-// occur in a header value Envoy's codec accepts).  Each HTTP rule becomes a
+// and an absent header encoded as the single byte 0x01; when every field from
+// some point on is absent, that tail is the single byte REST = 0x02 instead
+// (headers are mostly absent, so strings shrink by ~20%).  None of these
+// bytes can occur in a header value Envoy's codec accepts (http_parser
+// rejects control bytes other than HTAB), and the packer denies requests
+// carrying one as malformed.  Each HTTP rule becomes a
 // layered DFA (one deterministic automaton per field, chained by SEP); all
 // rules of a program are unioned by subset construction over (rule, state)
 // pairs, accepting states labelled with the set of PortNetworkPolicyRules
@@ -43,6 +47,7 @@ namespace {
 
 constexpr uint8_t kSep = 0x00;
 constexpr uint8_t kAbsent = 0x01;
+constexpr uint8_t kRestAbsent = 0x02;  // every remaining field absent (ends the string)
 constexpr int kMaxUnionStates = 400000;  // before minimization, per part
 constexpr int kMaxPartStates = 65535;    // u16 transition entries
 constexpr uint32_t kMaxLdsCells = 40944;  // 160 KiB less 64 B of static LDS (counters): one program table per workgroup
@@ -180,10 +185,10 @@ std::vector<PolicySpec> parse_npds(const char* json, size_t len) {
   return out;
 }
 
-// Field-value alphabet: any byte except SEP and the absent marker.
+// Field-value alphabet: any byte except SEP and the absent markers.
 ByteSet value_alphabet() {
   ByteSet s = ByteSet::all();
-  s.w[0] &= ~3ULL;
+  s.w[0] &= ~7ULL;
   return s;
 }
 
@@ -203,7 +208,7 @@ struct FieldDfaCache {
   int any() {
     if (any_id < 0) {
       ByteSet a = ByteSet::all();
-      a.w[0] &= ~1ULL;  // everything but SEP (the absent marker included)
+      a.w[0] &= ~5ULL;  // everything but SEP and REST (the absent marker included)
       any_id = add(dfa_star(a), "ANY");
     }
     return any_id;
@@ -267,6 +272,7 @@ ClsDfa build_union(const FieldDfaCache& fc, const std::vector<URule>& all_rules,
   // global byte classes: SEP alone, refined by every field DFA's columns
   std::vector<int> cls(256, 1);
   cls[kSep] = 0;
+  cls[kRestAbsent] = 2;
   {
     std::set<int> used;
     for (int r : rules)
@@ -358,7 +364,23 @@ ClsDfa build_union(const FieldDfaCache& fc, const std::vector<URule>& all_rules,
       if (f < F) {
         const std::vector<uint64_t>& cur = states[si];
         nx.clear();
-        if (b == kSep) {
+        if (b == kRestAbsent) {
+          // fields f..F-1 all absent: a rule survives iff each of its
+          // remaining field automata accepts the absent marker (from its
+          // current state for field f, which the packer only leaves at the
+          // field's start)
+          nx.push_back((uint64_t)F);
+          for (size_t i = 1; i < cur.size(); ++i) {
+            uint32_t r = (uint32_t)(cur[i] >> 32), q = (uint32_t)cur[i];
+            bool ok = true;
+            for (int g = f; g < F && ok; ++g) {
+              const ByteDfa& fd = fc.dfas[all_rules[r].fd[g]];
+              const int s1 = fd.next(g == f ? (int)q : fd.start, kAbsent);
+              ok = s1 != 0 && fd.accept[s1];
+            }
+            if (ok) nx.push_back((uint64_t)r << 32 | 1u);
+          }
+        } else if (b == kSep) {
           nx.push_back((uint64_t)(f + 1));
           for (size_t i = 1; i < cur.size(); ++i) {
             uint32_t r = (uint32_t)(cur[i] >> 32), q = (uint32_t)cur[i];
@@ -494,7 +516,6 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
         it->second[j >> 6] |= 1ULL << (j & 63);
       }
     }
-    pg.always_off = add_mask(always);
     for (uint64_t w : always)
       if (w) pg.flags |= kProgHasAlways;
     pg.default_remote = add_mask(open);
@@ -529,6 +550,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     build_parts(fc, urules, idx, F, W, parts);
     pg.part_begin = (uint32_t)S.parts.size();
     pg.part_count = (uint32_t)parts.size();
+    if (S.cells.size() & 1) S.cells.push_back(kCombEmpty);  // blocks start 8-byte aligned
     pg.cell_begin = (uint32_t)S.cells.size();
     size_t block = 0;
     for (const auto& po : parts) block += po.comb.cells.size();
@@ -546,13 +568,36 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       hp.self_lo = cb.self_lo;
       hp.ncells = (uint32_t)cb.cells.size();
       S.cells.insert(S.cells.end(), cb.cells.begin(), cb.cells.end());
-      // accept label l of this part → u64 word offset of its PNPR mask
-      hp.acc_off = (uint32_t)S.acc.size();
-      for (size_t l = 0; l < po.label_masks.size(); ++l) S.acc.push_back(add_mask(po.label_masks[l]));
       S.total_states += d.size();
       S.total_exceptions += cb.exceptions;
       S.parts.push_back(hp);
     }
+    // The block continues with each part's label table (accept label l →
+    // block offset of its PNPR mask), the label masks and the "always" mask,
+    // all block-relative u32 offsets, masks as 8-byte-aligned u64 pairs: the
+    // kernel stages the whole block into LDS with the DFA.
+    auto put_mask = [&](const std::vector<uint64_t>& m) -> uint32_t {
+      if (S.cells.size() & 1) S.cells.push_back(0);
+      const uint32_t off = (uint32_t)S.cells.size() - pg.cell_begin;
+      for (uint64_t w : m) {
+        S.cells.push_back((uint32_t)w);
+        S.cells.push_back((uint32_t)(w >> 32));
+      }
+      return off;
+    };
+    for (size_t i = 0; i < parts.size(); ++i) {
+      HttpPart& hp = S.parts[pg.part_begin + i];
+      hp.acc_off = (uint32_t)S.cells.size() - pg.cell_begin;
+      S.cells.resize(S.cells.size() + parts[i].label_masks.size(), kNoAcc);
+    }
+    for (size_t i = 0; i < parts.size(); ++i) {
+      const uint32_t acc_at = pg.cell_begin + S.parts[pg.part_begin + i].acc_off;
+      for (size_t l = 0; l < parts[i].label_masks.size(); ++l) {
+        const uint32_t off = put_mask(parts[i].label_masks[l]);
+        S.cells[acc_at + l] = off;
+      }
+    }
+    pg.always_off = put_mask(always);
     pg.cell_count = (uint32_t)S.cells.size() - pg.cell_begin;
     S.progs.push_back(pg);
     S.prog_key.push_back(key);
@@ -604,9 +649,10 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       S.rhash_vals[h] = v;
     }
   }
-  if (S.masks.empty()) S.masks.push_back(0);
+  // two spare words: the kernel reads row words 0 and 1 whatever the width
+  S.masks.push_back(0);
+  S.masks.push_back(0);
   if (S.cells.empty()) S.cells.push_back(kCombEmpty);
-  if (S.acc.empty()) S.acc.push_back(kNoAcc);
   if (S.progs.empty()) S.progs.push_back(HttpProg{});
   if (S.parts.empty()) S.parts.push_back(HttpPart{});
   if (S.dflt.empty()) S.dflt.push_back(kProgDeny);
@@ -629,7 +675,6 @@ void HttpSnapshot::upload(Engine& e) {
   d_progs.upload_vec(progs);
   d_parts.upload_vec(parts);
   d_cells.upload_vec(cells);
-  d_acc.upload_vec(acc);
   d_masks.upload_vec(masks);
   d_phk.upload_vec(phash_keys);
   d_phv.upload_vec(phash_vals);
@@ -641,7 +686,6 @@ void HttpSnapshot::upload(Engine& e) {
   dev.progs = d_progs.as<HttpProg>();
   dev.parts = d_parts.as<HttpPart>();
   dev.cells = d_cells.as<uint32_t>();
-  dev.acc = d_acc.as<uint32_t>();
   dev.masks = d_masks.as<unsigned long long>();
   dev.phash_keys = d_phk.as<uint32_t>();
   dev.phash_vals = d_phv.as<uint32_t>();

@@ -19,7 +19,6 @@ struct HttpSnapshot {
   std::vector<HttpProg> progs;
   std::vector<HttpPart> parts;
   std::vector<uint32_t> cells;
-  std::vector<uint32_t> acc;
   std::vector<uint64_t> masks;
   std::vector<uint32_t> phash_keys, phash_vals;
   uint32_t phash_mask = 0;
@@ -35,7 +34,7 @@ struct HttpSnapshot {
   uint64_t total_exceptions = 0;
   uint64_t total_rules = 0;
 
-  DevMem d_progs, d_parts, d_cells, d_acc, d_masks, d_phk, d_phv, d_dflt, d_rhk, d_rhv, d_counters;
+  DevMem d_progs, d_parts, d_cells, d_masks, d_phk, d_phv, d_dflt, d_rhk, d_rhv, d_counters;
   HttpDev dev{};
 
   void upload(Engine& e);

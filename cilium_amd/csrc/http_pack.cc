@@ -20,6 +20,12 @@ namespace {
 
 constexpr uint8_t kSep = 0x00;
 constexpr uint8_t kAbsent = 0x01;
+constexpr uint8_t kRestAbsent = 0x02;  // every remaining field absent (http.cc)
+
+// A header value byte Envoy's HTTP/1 codec rejects (http_parser's
+// IS_HEADER_CHAR: control bytes other than HTAB, and DEL); the request never
+// reaches the L7 filter.
+inline bool codec_rejects(uint8_t c) { return (c < 0x20 && c != 0x09) || c == 0x7F; }
 constexpr size_t kTileBytes = (size_t)CG_HTTP_UNITS * CG_HTTP_TILE * 16;
 
 inline uint8_t* unit_ptr(uint8_t* tiles, size_t slot, int u) {
@@ -128,23 +134,23 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
         while (p < e && *p) ++p;
         size_t vlen = p - v;
         if (p < e) ++p;
+        for (size_t k = 0; k < vlen; ++k)
+          if (codec_rejects(v[k])) malformed[i] = 1;
         for (size_t f = 0; f < F; ++f)
           if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
             vp[f] = v;
             vl[f] = vlen;
           }
       }
-      for (size_t f = 0; f < F; ++f) {
-        if (!vp[f]) {
-          strs.push_back(kAbsent);
-        } else {
-          for (size_t k = 0; k < vl[f]; ++k) {
-            if (vp[f][k] == kAbsent || vp[f][k] == kSep) malformed[i] = 1;
-            strs.push_back(vp[f][k]);
-          }
-        }
+      size_t last = 0;  // fields [last, F) are all absent
+      for (size_t f = 0; f < F; ++f)
+        if (vp[f]) last = f + 1;
+      for (size_t f = 0; f < last; ++f) {
+        if (!vp[f]) strs.push_back(kAbsent);
+        else strs.insert(strs.end(), vp[f], vp[f] + vl[f]);
         strs.push_back(kSep);
       }
+      if (last < F) strs.push_back(kRestAbsent);
       soff[i + 1] = strs.size();
     }
   }
@@ -270,8 +276,10 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         }
         hh = (hh + 1) & s.rhash_mask;
       }
+      const uint32_t* blk = s.cells.data() + pg.cell_begin;
+      auto bmask = [&](uint32_t off, uint32_t w) { return (uint64_t)blk[off + 2 * w] | (uint64_t)blk[off + 2 * w + 1] << 32; };
       for (uint32_t w = 0; w < pg.mask_words; ++w)
-        if (s.masks[pg.always_off + w] & s.masks[roff + w]) v = 1;
+        if (bmask(pg.always_off, w) & s.masks[roff + w]) v = 1;
       for (uint32_t pi = 0; pi < pg.part_count && !v; ++pi) {
         const HttpPart& pt = s.parts[pg.part_begin + pi];
         const uint32_t* cells = s.cells.data() + pt.walk_off;
@@ -282,9 +290,9 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         }
         const uint32_t lab = comb_label(cells, st);
         if (lab == kCombNoLabel) continue;
-        const uint32_t a = s.acc[pt.acc_off + lab];
+        const uint32_t a = blk[pt.acc_off + lab];
         for (uint32_t w = 0; w < pg.mask_words; ++w)
-          if (s.masks[a + w] & s.masks[roff + w]) v = 1;
+          if (bmask(a, w) & s.masks[roff + w]) v = 1;
       }
       out[sl] = v;
     }

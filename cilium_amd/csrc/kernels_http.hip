@@ -3,10 +3,13 @@
 // NetworkPolicyMap::Allowed (envoy/cilium_network_policy.h:223-237) for every
 // slot of a program-grouped batch (http_pack.cc).  One workgroup takes one
 // chunk of ≤ kChunkTiles tiles of a single program: it stages the program's
-// comb-packed DFA (comb.h) into LDS once, then each wavefront walks 64
-// requests at a time, one lane per request.  Records are tile-transposed, so
-// each of a wave's nine 16-byte unit loads is one contiguous 1 KiB read; the
-// DFA walk itself touches only LDS (one ds_read_b32 per byte).
+// block — comb-packed DFA (comb.h), accept-label table and PNPR masks — into
+// LDS, then each wavefront walks 64 requests at a time, one lane per request.
+// Records are tile-transposed, so each of a wave's 16-byte unit loads is one
+// contiguous 1 KiB read; the DFA walk touches only LDS (one ds_read_b32 per
+// byte).  The walk is latency-bound (a dependent LDS read per byte), so the
+// common path streams a wave's tiles: the next tile's first units load while
+// the current tile walks, and units within a tile load two ahead.
 #include <hip/hip_runtime.h>
 
 #include "../../include/cilium_gpu.h"
@@ -19,14 +22,9 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kHttpThreads = 1024;
-constexpr int kTilesPerWave = 1;  // DFA chains per lane (2 measured slower: the chains share VCC in comb_step)
-
-__device__ __forceinline__ bool masks_meet(const unsigned long long* __restrict__ m, uint32_t a, uint32_t b,
-                                           uint32_t w) {
-  for (uint32_t i = 0; i < w; ++i)
-    if (m[a + i] & m[b + i]) return true;
-  return false;
-}
+constexpr uint32_t kTileVecs = CG_HTTP_UNITS * kWave;  // uint4 per tile
+constexpr int kTilesPerWave = 1;  // strings walked per lane at a time
+constexpr uint32_t kDealRun = 4;  // consecutive chunks per workgroup turn
 
 __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
   const uint32_t word = (k < 4) ? w.x : (k < 8) ? w.y : (k < 12) ? w.z : w.w;
@@ -35,11 +33,15 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
 
 // One comb transition (comb.h), branch-free: every lane reads the table and
 // selects.  A dead lane (S = 0) reads cells[b], whose check half is never 0.
+// The walk is VALU-issue bound (PMC: ~60% of SIMD cycles issue VALU), so the
+// select uses SDWA word selects: compare the check half and pick the next
+// half in two instructions.  It goes through VCC, which serializes several
+// chains per lane — one chain per lane (kTilesPerWave = 1) measured fastest.
 __device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
                                              uint32_t b) {
   const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + ((st << 2) + (b << 2)));
   const uint32_t dflt = st >= self_lo ? st : 0u;
-  // nx = e.lo == st ? e.hi : dflt — SDWA word selects fold the shift
+  // nx = e.lo == st ? e.hi : dflt
   uint32_t nx;
   asm("v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
       "s_nop 1\n\t"
@@ -48,47 +50,6 @@ __device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells
       : "v"(e), "v"(st), "v"(dflt)
       : "vcc");
   return nx;
-}
-
-// Walk the in-record strings of K tiles per wave (units 1..8 of each tile):
-// K independent DFA chains per lane hide each other's LDS latency.
-// Accepting states absorb (comb.h) and records are zero-padded, so lanes step
-// through all 16 bytes of a unit with no per-byte length test; units are
-// loaded one ahead and the walk ends once no lane is alive inside its string.
-template <int K>
-__device__ __forceinline__ void walk_tiles(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t (&st)[K],
-                                           const uint4* const (&tb)[K], uint32_t lane, const uint32_t (&len)[K]) {
-  bool live = false;
-#pragma unroll
-  for (int j = 0; j < K; ++j) live |= len[j] != 0 && st[j] != 0;
-  if (!__any(live)) return;
-  uint4 cur[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) cur[j] = tb[j][1 * kWave + lane];
-  for (uint32_t u = 0; u < 8; ++u) {
-    bool longer = false;
-#pragma unroll
-    for (int j = 0; j < K; ++j) longer |= (u + 1) * 16 < len[j];
-    const bool more = __any(longer);
-    uint4 nxt[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) nxt[j] = cur[j];
-    if (more && u < 7) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) nxt[j] = tb[j][(u + 2) * kWave + lane];
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) st[j] = comb_step(cells, self_lo, st[j], get_byte(cur[j], k));
-    }
-    bool alive = false;
-#pragma unroll
-    for (int j = 0; j < K; ++j) alive |= st[j] != 0 && (u + 1) * 16 < len[j];
-    if (!more || !__any(alive)) break;
-#pragma unroll
-    for (int j = 0; j < K; ++j) cur[j] = nxt[j];
-  }
 }
 
 // Records longer than a slot live in the overflow arena: byte loop.
@@ -110,89 +71,118 @@ __device__ __forceinline__ uint32_t remote_row(const HttpDev& T, unsigned long l
   return dflt;
 }
 
-// K tiles of 64 requests of program `prog` (a real, non-trivial program);
-// tile j takes part only if valid[j].  `pcells`: the program's cell block
-// when it is rebased (LDS copy or global), else the global table (parts walk
-// from their own offsets).
+// u64 word w of the block mask at block offset a (u32 units, 8-byte aligned).
+__device__ __forceinline__ unsigned long long blk_word(const uint32_t* __restrict__ blk, uint32_t a, uint32_t w) {
+  return *reinterpret_cast<const unsigned long long*>(blk + a + 2 * w);
+}
+
+// Does the block mask at `a` meet the remote row?  Words 0 and 1 of the row
+// come preloaded (r0, r1), the rest from T.masks.
+__device__ __forceinline__ bool meets(const uint32_t* __restrict__ blk, uint32_t a, const HttpDev& T, uint32_t row,
+                                      uint32_t W, unsigned long long r0, unsigned long long r1) {
+  if (W > 0 && (blk_word(blk, a, 0) & r0)) return true;
+  if (W > 1 && (blk_word(blk, a, 1) & r1)) return true;
+  for (uint32_t w = 2; w < W; ++w)
+    if (blk_word(blk, a, w) & T.masks[row + w]) return true;
+  return false;
+}
+
+// K tiles of a program (tile j takes part only if valid[j]): walk every
+// part, OR the verdicts.  blk = the program's block (LDS copy or global);
+// parts walk blk when rebased, else their own cells in T.cells.  Each lane
+// walks K independent strings, interleaved byte by byte, so one lane's LDS
+// reads overlap; units load one ahead and the walk ends once no lane is
+// alive inside its string.
 template <int K>
 __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg, uint32_t prog,
-                                           const uint32_t* __restrict__ pcells, bool rebased,
+                                           const uint32_t* __restrict__ blk, bool rebased,
                                            const uint4* __restrict__ tiles, const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
-                                           uint8_t* __restrict__ out, uint32_t lane, uint32_t* n_allow,
-                                           uint32_t* n_deny) {
+                                           uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
+                                           uint32_t& n_deny) {
   const uint4* tb[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) tb[j] = tiles + (size_t)tile[j] * (CG_HTTP_UNITS * kWave);
-  // only the string lengths stay live across the walk; the rest of the meta
-  // unit is re-read (an L2 hit) afterwards
-  uint32_t len[K];
+  uint32_t len[K], row[K];
+  bool counted[K], overflow[K], verdict[K];
+  unsigned long long r0[K], r1[K];
   bool any_overflow = false;
+  const uint32_t W = pg.mask_words;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
+    tb[j] = tiles + (size_t)tile[j] * kTileVecs;
     const uint4 meta = tb[j][lane];
     const uint32_t flags = meta.w >> 24;
-    const bool counted = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
-    const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
-    len[j] = counted && !overflow ? meta.z : 0u;
-    any_overflow |= overflow;
+    counted[j] = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+    overflow[j] = counted[j] && (flags & CG_HTTP_F_OVERFLOW);
+    len[j] = counted[j] && !overflow[j] ? meta.z : 0u;
+    any_overflow |= overflow[j];
+    const unsigned long long rkey = ((unsigned long long)prog << 32) | meta.x;
+    row[j] = remote_row(T, rkey, hash64to32(rkey) & T.rhash_mask, pg.default_remote);
+    r0[j] = T.masks[row[j]];
+    r1[j] = T.masks[row[j] + 1];
+    verdict[j] = false;
   }
   any_overflow = __any(any_overflow);
-  uint32_t verdict[K], rrow[K];
-  bool counted[K], have_rrow[K];
-  unsigned long long rkey[K];
-  uint32_t rh[K];
   for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
     const HttpPart pt = T.parts[pg.part_begin + pi];
-    const uint32_t* __restrict__ cells = rebased ? pcells : pcells + pt.walk_off;
+    const uint32_t* __restrict__ cells = rebased ? blk : T.cells + pt.walk_off;
     uint32_t st[K];
+    bool live = false;
 #pragma unroll
-    for (int j = 0; j < K; ++j) st[j] = pt.start;
-    walk_tiles<K>(cells, pt.self_lo, st, tb, lane, len);
-    if (pi == 0) {
+    for (int j = 0; j < K; ++j) {
+      st[j] = pt.start;
+      live |= len[j] != 0;
+    }
+    if (__any(live)) {
+      uint4 cur[K];
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint4 meta = tb[j][lane];
-        const uint32_t flags = meta.w >> 24;
-        counted[j] = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
-        rkey[j] = ((unsigned long long)prog << 32) | meta.x;
-        rh[j] = hash64to32(rkey[j]) & T.rhash_mask;
-        verdict[j] = 0;
-        rrow[j] = 0;
-        have_rrow[j] = false;
+      for (int j = 0; j < K; ++j) cur[j] = tb[j][kWave + lane];
+      for (uint32_t u = 0; u < 8; ++u) {
+        bool longer = false;
+#pragma unroll
+        for (int j = 0; j < K; ++j) longer |= (u + 1) * 16 < len[j];
+        const bool more = __any(longer);
+        uint4 nxt[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) nxt[j] = cur[j];
+        if (more && u < 7) {
+#pragma unroll
+          for (int j = 0; j < K; ++j) nxt[j] = tb[j][(u + 2) * kWave + lane];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+#pragma unroll
+          for (int j = 0; j < K; ++j) st[j] = comb_step(cells, pt.self_lo, st[j], get_byte(cur[j], k));
+        }
+        bool alive = false;
+#pragma unroll
+        for (int j = 0; j < K; ++j) alive |= st[j] != 0 && (u + 1) * 16 < len[j];
+        if (!more || !__any(alive)) break;
+#pragma unroll
+        for (int j = 0; j < K; ++j) cur[j] = nxt[j];
       }
     }
     if (any_overflow) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         const uint4 meta = tb[j][lane];
-        const bool ov = counted[j] && ((meta.w >> 24) & CG_HTTP_F_OVERFLOW);
-        const uint32_t sa = walk_arena(cells, pt.self_lo, pt.start, arena, (meta.w & 0xFFFFFFu) * 16u, ov ? meta.z : 0u);
-        if (ov) st[j] = sa;
+        const uint32_t sa =
+            walk_arena(cells, pt.self_lo, pt.start, arena, (meta.w & 0xFFFFFFu) * 16u, overflow[j] ? meta.z : 0u);
+        if (overflow[j]) st[j] = sa;
       }
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t sj = counted[j] ? st[j] : 0u;
-      const uint32_t lab = sj ? (cells[sj - 1] >> 16) : 0xFFFFu;
-      if (lab != 0xFFFFu && !verdict[j]) {
-        if (!have_rrow[j]) {
-          rrow[j] = remote_row(T, rkey[j], rh[j], pg.default_remote);
-          have_rrow[j] = true;
-        }
-        if (masks_meet(T.masks, T.acc[pt.acc_off + lab], rrow[j], pg.mask_words)) verdict[j] = 1;
-      }
+      const uint32_t lab = counted[j] && st[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
+      if (lab != 0xFFFFu && !verdict[j]) verdict[j] = meets(blk, blk[pt.acc_off + lab], T, row[j], W, r0[j], r1[j]);
     }
   }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    if (counted[j] && !verdict[j] && (pg.flags & kProgHasAlways)) {
-      if (!have_rrow[j]) rrow[j] = remote_row(T, rkey[j], rh[j], pg.default_remote);
-      if (masks_meet(T.masks, pg.always_off, rrow[j], pg.mask_words)) verdict[j] = 1;
-    }
+    if (counted[j] && !verdict[j] && (pg.flags & kProgHasAlways))
+      verdict[j] = meets(blk, pg.always_off, T, row[j], W, r0[j], r1[j]);
     if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict[j];
-    *n_allow += counted[j] && verdict[j];
-    *n_deny += counted[j] && !verdict[j];
+    n_allow += counted[j] && verdict[j];
+    n_deny += counted[j] && !verdict[j];
   }
 }
 
@@ -221,11 +211,11 @@ __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, ui
   }
 }
 
-// One workgroup per chunk (grid-stride).  kGlobal = false: chunks of trivial
-// programs and of programs whose table fits the workgroup's LDS share, which
-// is staged once per chunk; kGlobal = true: the remaining chunks (programs
-// too large for LDS), walked from global memory — a separate kernel so the
-// rare path does not set the common one's register budget.
+// Workgroups take chunks round-robin.  kGlobal = false: chunks of trivial
+// programs and of programs whose block fits the workgroup's LDS share, which
+// is staged when the program changes; kGlobal = true: the remaining chunks
+// (programs too large for LDS), walked from global memory — a separate kernel
+// so the rare path does not set the common one's register budget.
 template <bool kGlobal>
 __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
                                             const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
@@ -243,16 +233,22 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
   }
   const HttpChunk* chunks = reinterpret_cast<const HttpChunk*>(batch + sizeof(HttpBatchHeader));
   const uint4* tiles = reinterpret_cast<const uint4*>(batch + toff);
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // wave index made wave-uniform (SGPR): tile addresses then live in scalar
+  // registers and each load needs only its lane offset in a VGPR
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                 nw = blockDim.x >> 6;
   // Chunks are dealt round-robin: a contiguous run per workgroup would pin
   // each workgroup to one program and the costliest program sets the tail.
   // Allowed/denied counts stay in registers while consecutive chunks share a
   // program and go to the global counters once per run (one atomic pair per
   // workgroup): concurrent workgroups work on the same program, so per-wave
   // atomics would all hit the same two addresses.
-  uint32_t cur = kProgDeny;  // program of the current run (its table is in LDS if walked there)
+  uint32_t cur = kProgDeny;  // program of the current run (its block is in LDS if walked there)
   uint32_t n_allow = 0, n_deny = 0;
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+  // dealt in runs of kDealRun consecutive chunks (same program, mostly), so
+  // the block is restaged once per run
+  for (uint32_t cr = blockIdx.x * kDealRun; cr < nchunks; cr += gridDim.x * kDealRun)
+  for (uint32_t c = cr; c < min(nchunks, cr + kDealRun); ++c) {
     const HttpChunk ch = chunks[c];
     if (ch.first_tile + ch.ntiles > ntiles || ch.ntiles > kChunkTiles) continue;  // malformed chunk
     const uint32_t prog = ch.prog;
@@ -274,18 +270,18 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         // no policy for the port → allow; unknown policy → deny; a scope
         // without HTTP rules → allow (cilium_network_policy.h:129-138,187-191)
-        const uint32_t flags = tiles[(size_t)t * (CG_HTTP_UNITS * kWave) + lane].w >> 24;
+        const uint32_t flags = tiles[(size_t)t * kTileVecs + lane].w >> 24;
         const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
         out[(size_t)t * kWave + lane] = (uint8_t)(counted && (prog == kProgAllow || real) ? 1u : 0u);
         n_allow += real && counted;
       }
     } else if (kGlobal) {
       const bool rebased = pg.flags & kProgRebased;
-      const uint32_t* pcells = rebased ? T.cells + pg.cell_begin : T.cells;
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         const uint32_t tile[1] = {t};
         const bool valid[1] = {true};
-        http_tiles<1>(T, pg, prog, pcells, rebased, tiles, tile, valid, arena, out, lane, &n_allow, &n_deny);
+        http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, tile, valid, arena, out, lane, n_allow,
+                      n_deny);
       }
     } else {
       // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)
@@ -298,8 +294,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
           valid[j] = t < tend;
           tile[j] = valid[j] ? t : t0;
         }
-        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, tile, valid, arena, out, lane, &n_allow,
-                                  &n_deny);
+        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, tile, valid, arena, out, lane, n_allow, n_deny);
       }
     }
   }
@@ -328,11 +323,12 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   if (nslots == 0) return 0;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
+    (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
     attr = true;
   }
   // one resident wave of workgroups: as many per CU as LDS and registers
-  // allow (the program table size sets the LDS share), then grid-stride
+  // allow (the largest staged program block sets the LDS share), then the
+  // workgroups deal the chunks among themselves
   const size_t lds = (size_t)t.lds_cells * 4;
   static size_t occ_lds = ~(size_t)0;
   static int occ = 1;

@@ -491,10 +491,15 @@ int or_http_eval(void* h, size_t n, const uint32_t* policy, const uint8_t* ingre
         if (p < e) ++p;
         hs.emplace_back(lower(name), val);
       }
+      // Envoy's HTTP/1 codec (http_parser IS_HEADER_CHAR) rejects a header
+      // value holding a control byte other than HTAB, or DEL: such a request
+      // never reaches the filter
       bool malformed = false;
       for (const auto& kv : hs)
-        for (char c : kv.second)
-          if (c == '\x01') malformed = true;  // a control byte Envoy's codec rejects
+        for (char ch : kv.second) {
+          const unsigned char c = (unsigned char)ch;
+          if ((c < 0x20 && c != 0x09) || c == 0x7F) malformed = true;
+        }
       if (policy[i] >= o->policies.size() || malformed) {
         out[i] = 0;  // "No policy found for endpoint" → deny (:232-235)
         continue;

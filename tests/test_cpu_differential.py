@@ -115,6 +115,13 @@ def _rand_requests(rng, n, n_pol):
                 hs.append((name.upper() if rng.random() < 0.2 else name, rng.choice(VALUES)))
         if rng.random() < 0.1 and hs:
             hs.append((hs[0][0], "dup"))  # repeated header: the first value wins
+        if rng.random() < 0.2:  # a header no rule references
+            hs.append(("x-unref", rng.choice(VALUES)))
+        if rng.random() < 0.05 and hs:
+            # a control byte the codec rejects (any header) → denied; HTAB is fine
+            k = rng.randrange(len(hs))
+            c = rng.choice(["\x01", "\x02", "\x07", "\x1f", "\x7f", "\t", "\r"])
+            hs[k] = (hs[k][0], hs[k][1] + c)
         reqs.append(hs)
     parts, off = [], [0]
     for hs in reqs:

@@ -19,8 +19,6 @@ LDS_READ = ("  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret
             "((st << 2) + (b << 2)));")
 # keeps the walk's result live but never lets a meaningless state index the
 # accept tables (variants that break the DFA must stay memory-safe)
-SAFE_LABEL = ("      const uint32_t sj = counted[j] ? st[j] : 0u;",
-              "      const uint32_t sj = (st[j] == 0xFFFFFFFFu) ? 1u : 0u;")
 C_STEP = ("""  uint32_t nx;
   asm("v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\\n\\t"
       "s_nop 1\\n\\t"
@@ -29,21 +27,9 @@ C_STEP = ("""  uint32_t nx;
       : "v"(e), "v"(st), "v"(dflt)
       : "vcc");
   return nx;""", """  return (uint16_t)e == (uint16_t)st ? (e >> 16) : dflt;""")
+K = "constexpr int kTilesPerWave = 1;"
 VARIANTS = {
     "base": [],
-    # dependency chain kept on VALU, no LDS access
-    "nolds": [SAFE_LABEL, (LDS_READ, "  const uint32_t e = (st * 2654435761u) ^ (b << 16) ^ b ^ (uint32_t)(size_t)cells;")],
-    # no DFA steps: stream the units only
-    "nowalk": [SAFE_LABEL, ("      for (int j = 0; j < K; ++j) st[j] = comb_step(cells, self_lo, st[j], get_byte(cur[j], k));",
-                "      for (int j = 0; j < K; ++j) st[j] ^= get_byte(cur[j], k);")],
-    "k1": [("constexpr int kTilesPerWave = 2;", "constexpr int kTilesPerWave = 1;")],
-    # no per-program counter atomics (measures their contention)
-    "noctr": [("      if (lane == 0) {\n        if (n_allow)", "      if (lane == 0 && n_allow == 0xFFFFFFFFu) {\n        if (n_allow)")],
-    # plain C select: no shared-VCC inline asm, so the K chains can interleave
-    "cstep": [C_STEP],
-    "cstep_k1": [C_STEP, ("constexpr int kTilesPerWave = 2;", "constexpr int kTilesPerWave = 1;")],
-    "cstep_k3": [C_STEP, ("constexpr int kTilesPerWave = 2;", "constexpr int kTilesPerWave = 3;")],
-    "cstep_w4": [C_STEP, ("amdgpu_waves_per_eu(8, 8)", "amdgpu_waves_per_eu(4, 4)")],
 }
 
 
