@@ -28,7 +28,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "policy verdicts/sec (whole node) + request GB/s, 10K-rule L7 HTTP set"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-RECORD_BYTES = 144      # 16-byte meta unit + 128-byte field slot (include/cilium_gpu.h)
 OUT_BYTES = 1
 CHUNK_TILES = 64        # kChunkTiles (csrc/dev_types.h)
 
@@ -78,7 +77,7 @@ def main():
     field_bytes = mean_field_bytes(b)
     reps = max(1, args.requests_per_gpu // D)
     B = reps * D                                  # requests per GPU per step
-    d_batch, nslots, tile_map = replicate_batch(b, reps, dev, torch)
+    d_batch, nslots, tile_map, data_bytes = replicate_batch(b, reps, dev, torch)
     d_arena = torch.from_numpy(b.arena).to(dev)
     d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
     nprog_ctr = int(cl.read_counters(0).size)
@@ -139,7 +138,10 @@ def main():
     total_req = B * world * args.steps
     value = total_req / wall
     ms_per_step = wall / args.steps * 1e3
-    per_launch_bytes = B * (RECORD_BYTES + OUT_BYTES)
+    # algorithmic bytes: the packed input the launch consumes (tile data +
+    # chunk/tile tables; a tile stores its meta unit and the string units of
+    # its longest string) + one verdict byte per request
+    per_launch_bytes = data_bytes + B * OUT_BYTES
     achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
     allow_frac = float(d_out.float().sum().item()) / B
 
@@ -169,8 +171,9 @@ def main():
                                    "DFA), requests sharded across GPUs",
                        "requests_per_gpu": B, "rules": int(stats["rules"]), "programs": int(stats["programs"]),
                        "dfa_states": int(stats["states"]), "table_bytes": int(stats["table_bytes"]),
-                       "compile_s": round(compile_s, 3), "record_bytes": RECORD_BYTES, "parallelism": f"dp{world}"},
-            "request_gbps": value * (RECORD_BYTES + OUT_BYTES) / 1e9,
+                       "compile_s": round(compile_s, 3), "packed_bytes_per_request": per_launch_bytes / B,
+                       "parallelism": f"dp{world}"},
+            "request_gbps": value * per_launch_bytes / B / 1e9,
             "field_bytes_per_request": field_bytes,
             "field_gbps": value * field_bytes / 1e9,
             "allow_fraction": allow_frac,
@@ -188,64 +191,82 @@ def main():
     cl.close()
 
 
+def batch_parts(batch: np.ndarray):
+    """Header fields, chunk table and tile table of a packed batch
+    (HttpBatchHeader / HttpChunk / HttpTile, csrc/dev_types.h)."""
+    h = batch[:64]
+    nchunks = int(h[8:12].view(np.uint32)[0])
+    ntiles = int(h[12:16].view(np.uint32)[0])
+    toff, ttoff = int(h[16:24].view(np.uint64)[0]), int(h[32:40].view(np.uint64)[0])
+    chunks = batch[64:64 + 16 * nchunks].view(np.uint32).reshape(nchunks, 4)
+    ttab = batch[ttoff:ttoff + 8 * ntiles].view(np.uint32).reshape(ntiles, 2)
+    return ntiles, toff, chunks, ttab
+
+
 def replicate_batch(b, reps: int, dev, torch):
     """Device batch of `reps` copies of packed batch b, laid out as the packer
     lays out a batch of reps x D requests: each program's tiles (its `reps`
     copies) are contiguous and cut into chunks of CHUNK_TILES
-    (http_pack.cc).  Returns (device batch, nslots, tile_map) where
-    tile_map[t] is the tile of the first copy of b's tile t."""
-    hdr = b.batch[:64].copy()
-    nchunks = int(hdr[8:12].view(np.uint32)[0])
-    ntiles = int(hdr[12:16].view(np.uint32)[0])
-    toff = int(hdr[16:24].view(np.uint64)[0])
-    tile_bytes = 64 * RECORD_BYTES
-    chunks = b.batch[64:64 + 16 * nchunks].view(np.uint32).reshape(nchunks, 4)
+    (http_pack.cc).  Returns (device batch, nslots, tile_map, data_bytes)
+    where tile_map[t] is the tile of the first copy of b's tile t and
+    data_bytes the bytes of the packed input (tables + tiles)."""
+    ntiles, toff, chunks, ttab = batch_parts(b.batch)
     groups = []  # (prog, first tile, ntiles) of each program group of b
     for prog, first, nt, _ in chunks:
         if groups and groups[-1][0] == prog and groups[-1][1] + groups[-1][2] == first:
             groups[-1][2] += int(nt)
         else:
             groups.append([int(prog), int(first), int(nt)])
-    big, placed, pos = [], [], 0
+    kib = ttab[:, 0].astype(np.int64)
+    units = ttab[:, 1].astype(np.int64)
+    big, new_tt, placed, pos, kpos = [], [], [], 0, 0
     for prog, first, nt in groups:
         run = nt * reps
         for k in range(0, run, CHUNK_TILES):
             big.append((prog, pos + k, min(CHUNK_TILES, run - k), 0))
-        placed.append((first, nt, pos))
+        g_kib = int(kib[first + nt - 1] + 1 + units[first + nt - 1] - kib[first])
+        rel = kib[first:first + nt] - kib[first]
+        for r in range(reps):
+            new_tt.append(np.stack([kpos + r * g_kib + rel, units[first:first + nt]], axis=1))
+        placed.append((first, nt, pos, int(kib[first]), g_kib, kpos))
         pos += run
+        kpos += reps * g_kib
     big = np.asarray(big, np.uint32)
-    hbytes = (64 + 16 * len(big) + 1023) // 1024 * 1024
+    new_tt = np.concatenate(new_tt).astype(np.uint32)
+    ttoff = 64 + 16 * len(big)
+    hbytes = (ttoff + 8 * pos + 1023) // 1024 * 1024
+    total = hbytes + kpos * 1024
+    hdr = b.batch[:64].copy()
     hdr[8:12] = np.array([len(big)], np.uint32).view(np.uint8)
     hdr[12:16] = np.array([pos], np.uint32).view(np.uint8)
-    hdr[16:24] = np.array([hbytes], np.uint64).view(np.uint8)
-    hdr[24:32] = np.array([pos * 64], np.uint64).view(np.uint8)
+    hdr[16:48] = np.array([hbytes, pos * 64, ttoff, total], np.uint64).view(np.uint8)
     head = np.zeros(hbytes, np.uint8)
     head[:64] = hdr
     head[64:64 + big.nbytes] = big.reshape(-1).view(np.uint8)
-    d = torch.empty(hbytes + pos * tile_bytes, dtype=torch.uint8, device=dev)
+    head[ttoff:ttoff + new_tt.nbytes] = new_tt.reshape(-1).view(np.uint8)
+    d = torch.empty(total, dtype=torch.uint8, device=dev)
     d[:hbytes].copy_(torch.from_numpy(head))
-    src = torch.from_numpy(b.batch[toff:toff + ntiles * tile_bytes]).to(dev)
+    data_end = int(kib[-1] + 1 + units[-1]) * 1024 if ntiles else 0
+    src = torch.from_numpy(b.batch[toff:toff + data_end]).to(dev)
     tile_map = np.zeros(ntiles, np.int64)
-    for first, nt, at in placed:
-        g0 = hbytes + at * tile_bytes
-        gb = nt * tile_bytes
-        d[g0:g0 + gb].copy_(src[first * tile_bytes:(first + nt) * tile_bytes])
+    for first, nt, at, k0, g_kib, kp in placed:
+        g0, gb = hbytes + kp * 1024, g_kib * 1024
+        d[g0:g0 + gb].copy_(src[k0 * 1024:k0 * 1024 + gb])
         done = 1
         while done < reps:  # doubling copies on the device
             k = min(done, reps - done)
             d[g0 + done * gb:g0 + (done + k) * gb].copy_(d[g0:g0 + k * gb])
             done += k
         tile_map[first:first + nt] = np.arange(at, at + nt)
-    return d, pos * 64, tile_map
+    return d, pos * 64, tile_map, total - 64
 
 
 def mean_field_bytes(b) -> float:
     """Mean length of the requests' field strings (header values joined by
     the packer's separators, http_pack.cc) over the real slots of batch b."""
-    ntiles = int(b.batch[12:16].view(np.uint32)[0])
-    toff = int(b.batch[16:24].view(np.uint64)[0])
-    meta = b.batch[toff:toff + ntiles * 64 * RECORD_BYTES].reshape(ntiles, 9, 64, 16)[:, 0]
-    ln = meta.reshape(-1, 16)[:, 8:12].copy().view(np.uint32).reshape(-1)
+    ntiles, toff, _, ttab = batch_parts(b.batch)
+    metas = np.stack([b.batch[toff + int(k) * 1024:toff + int(k) * 1024 + 1024] for k in ttab[:, 0]])
+    ln = metas.reshape(-1, 16)[:, 8:12].copy().view(np.uint32).reshape(-1)
     real = b.order != 0xFFFFFFFF
     return float(ln[real].mean()) if real.any() else 0.0
 

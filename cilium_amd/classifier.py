@@ -49,9 +49,8 @@ class HttpBatch:
         self.batch, self.arena, self.order, self.nslots, self.n = batch, arena, order, nslots, n
 
     def used_bytes(self) -> int:
-        hdr = self.batch[:64].view(np.uint64)
-        ntiles = int(self.batch[12:16].view(np.uint32)[0])
-        return int(hdr[2]) + ntiles * 64 * N.CG_HTTP_UNITS * 16
+        """Size of the packed batch (HttpBatchHeader.total_bytes)."""
+        return int(self.batch[:64].view(np.uint64)[5])
 
 
 class Classifier:

@@ -607,7 +607,7 @@ static size_t batch_used_bytes(const void* batch) {
   HttpBatchHeader hdr;
   memcpy(&hdr, batch, sizeof(hdr));
   if (hdr.magic != kBatchMagic) fail(CG_INVALID_ARGUMENT, "not a packed HTTP batch");
-  return hdr.tiles_off + (size_t)hdr.ntiles * CG_HTTP_TILE * CG_HTTP_UNITS * 16;
+  return hdr.total_bytes;
 }
 
 int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const uint8_t* d_arena, uint8_t* d_out,

@@ -119,21 +119,29 @@ struct HttpPart {
 constexpr uint32_t kProgAllow = 0xFFFFFFFEu;  // no policy for the port → allow
 constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
 
-// Packed HTTP batch (cg_http_pack): a 64-byte header, the chunk table, then
-// tiles of 64 request records (9 × 16-byte units each, unit-major).  The
+// Packed HTTP batch (cg_http_pack): a 64-byte header, the chunk table, the
+// tile table, then the tiles (1 KiB aligned).  A tile is 64 request records
+// stored unit-major: its meta unit, then `units` 16-byte string units, each
+// unit one contiguous 1 KiB (unit u of lane l at tile + u*1024 + l*16).  The
 // packer groups requests by program so every chunk (≤ kChunkTiles tiles)
 // belongs to one program and a workgroup can stage that program's table in
 // LDS.  Slot order is returned to the caller (order[]).
-constexpr uint32_t kBatchMagic = 0x42484743u;  // "CGHB"
+constexpr uint32_t kBatchMagic = 0x32484743u;  // "CGH2"
 constexpr uint32_t kChunkTiles = 64;
 struct HttpBatchHeader {
   uint32_t magic;
   uint32_t epoch;      // snapshot the batch was packed against
   uint32_t nchunks;
   uint32_t ntiles;
-  uint64_t tiles_off;  // byte offset of tile 0 (multiple of 1024)
+  uint64_t tiles_off;  // byte offset of the tile data (multiple of 1024)
   uint64_t nslots;
-  uint32_t pad[8];
+  uint64_t ttab_off;   // byte offset of the tile table (ntiles HttpTile)
+  uint64_t total_bytes;
+  uint32_t pad[4];
+};
+struct HttpTile {
+  uint32_t kib;    // tile data at tiles_off + kib * 1024
+  uint32_t units;  // string units stored after the meta unit (0..8)
 };
 struct HttpChunk {
   uint32_t prog;

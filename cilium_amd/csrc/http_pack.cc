@@ -4,7 +4,10 @@
 // reference does per request in PortNetworkPolicy::Matches,
 // envoy/cilium_network_policy.h:169-192), groups requests by program and
 // pads every group to whole 64-request tiles, so each chunk of tiles has one
-// program whose comb table a workgroup stages in LDS.
+// program whose comb table a workgroup stages in LDS.  A tile holds the meta
+// unit and only as many 16-byte string units as its longest string needs
+// (the tile table gives each tile's offset and unit count), so the batch is
+// as large as its strings, not as the 128-byte slot.
 #include <algorithm>
 #include <array>
 #include <cstring>
@@ -26,12 +29,8 @@ constexpr uint8_t kRestAbsent = 0x02;  // every remaining field absent (http.cc)
 // IS_HEADER_CHAR: control bytes other than HTAB, and DEL); the request never
 // reaches the L7 filter.
 inline bool codec_rejects(uint8_t c) { return (c < 0x20 && c != 0x09) || c == 0x7F; }
-constexpr size_t kTileBytes = (size_t)CG_HTTP_UNITS * CG_HTTP_TILE * 16;
-
-inline uint8_t* unit_ptr(uint8_t* tiles, size_t slot, int u) {
-  size_t tile = slot / CG_HTTP_TILE, lane = slot % CG_HTTP_TILE;
-  return tiles + tile * kTileBytes + (size_t)u * CG_HTTP_TILE * 16 + lane * 16;
-}
+constexpr size_t kUnitBytes = (size_t)CG_HTTP_TILE * 16;  // one unit of a tile: 1 KiB
+constexpr size_t kMaxTileBytes = (size_t)CG_HTTP_UNITS * kUnitBytes;
 
 bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
   if (an != lower_b.size()) return false;
@@ -45,8 +44,10 @@ bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
 
 size_t max_groups(const HttpSnapshot& s, size_t n) { return std::min(n, s.progs.size() + 2); }
 
+// chunk table, then the tile table, then (1 KiB aligned) the tile data
+size_t ttab_off(size_t max_tiles) { return sizeof(HttpBatchHeader) + sizeof(HttpChunk) * max_tiles; }
 size_t header_bytes(size_t max_tiles) {
-  size_t b = sizeof(HttpBatchHeader) + sizeof(HttpChunk) * max_tiles;
+  size_t b = ttab_off(max_tiles) + sizeof(HttpTile) * max_tiles;
   return (b + 1023) & ~(size_t)1023;
 }
 
@@ -58,7 +59,7 @@ size_t http_batch_slots(const HttpSnapshot& s, size_t n) {
 
 size_t http_batch_bytes(const HttpSnapshot& s, size_t n) {
   size_t tiles = http_batch_slots(s, n) / CG_HTTP_TILE;
-  return header_bytes(tiles) + tiles * kTileBytes;
+  return header_bytes(tiles) + tiles * kMaxTileBytes;
 }
 
 void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const uint8_t* ingress,
@@ -84,33 +85,6 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   }
   const size_t nslots = tiles * CG_HTTP_TILE;
   if (nslots_out) *nslots_out = nslots;
-  const size_t hdr = header_bytes(http_batch_slots(s, n) / CG_HTTP_TILE);
-  const size_t need = hdr + tiles * kTileBytes;
-  if (batch && need > batch_cap) fail(CG_INVALID_ARGUMENT, "batch buffer too small");
-  uint8_t* tb = batch ? (uint8_t*)batch + hdr : nullptr;
-  if (batch) {
-    HttpBatchHeader h{};
-    h.magic = kBatchMagic;
-    h.epoch = s.epoch;
-    h.nchunks = (uint32_t)chunks.size();
-    h.ntiles = (uint32_t)tiles;
-    h.tiles_off = hdr;
-    h.nslots = nslots;
-    memcpy(batch, &h, sizeof(h));
-    memcpy((uint8_t*)batch + sizeof(h), chunks.data(), chunks.size() * sizeof(HttpChunk));
-    // padding slots of every group
-    for (auto& [p, c] : count) {
-      size_t s0 = first_slot[p];
-      size_t end = s0 + ((c + CG_HTTP_TILE - 1) / CG_HTTP_TILE) * CG_HTTP_TILE;
-      for (size_t sl = s0 + c; sl < end; ++sl) {
-        uint8_t* m = unit_ptr(tb, sl, 0);
-        memset(m, 0, 16);
-        m[15] = CG_HTTP_F_PAD;
-        for (int u = 1; u < CG_HTTP_UNITS; ++u) memset(unit_ptr(tb, sl, u), 0, 16);
-        if (order) order[sl] = 0xFFFFFFFFu;
-      }
-    }
-  }
   // ---- request strings (field values in field order, SEP-terminated)
   const size_t F = s.fields.size();
   std::vector<uint8_t> strs;
@@ -154,6 +128,14 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
       soff[i + 1] = strs.size();
     }
   }
+  auto str_len = [&](size_t i) -> size_t { return build ? soff[i + 1] - soff[i] : 0; };
+  // string units a request needs in its tile: 0 when the kernel does not
+  // walk the slot string (malformed, or spilled to the overflow arena)
+  auto walked_units = [&](size_t i) -> uint32_t {
+    const size_t len = str_len(i);
+    if (malformed[i] || len > CG_HTTP_SLOT_BYTES) return 0;
+    return (uint32_t)((len + 15) / 16);
+  };
   // ---- slot assignment: within a program group, requests ordered by the
   // number of 16-byte units their string spans, so the lanes of a tile end
   // their walks together, then by the string itself, so neighbouring lanes
@@ -163,7 +145,7 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   {
     std::vector<uint8_t> key(n, 0);
     for (size_t i = 0; i < n; ++i) {
-      const size_t len = build ? soff[i + 1] - soff[i] : 0;
+      const size_t len = str_len(i);
       key[i] = len > CG_HTTP_SLOT_BYTES ? CG_HTTP_UNITS + 1 : (uint8_t)((len + 15) / 16);
     }
     std::vector<uint32_t> idx(n);
@@ -186,6 +168,51 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
       slot_of[i] = (uint32_t)pos++;
     }
   }
+  // ---- tile table: each tile's string units = its longest walked string
+  std::vector<HttpTile> ttab(tiles);
+  for (size_t i = 0; i < n; ++i) {
+    HttpTile& t = ttab[slot_of[i] / CG_HTTP_TILE];
+    t.units = std::max(t.units, walked_units(i));
+  }
+  uint64_t kib = 0;
+  for (auto& t : ttab) {
+    if (kib > 0xFFFFFFFFull) fail(CG_INVALID_ARGUMENT, "batch beyond 4 TiB");
+    t.kib = (uint32_t)kib;
+    kib += 1 + t.units;
+  }
+  const size_t max_tiles = http_batch_slots(s, n) / CG_HTTP_TILE;
+  const size_t hdr = header_bytes(max_tiles);
+  const size_t need = hdr + kib * kUnitBytes;
+  if (batch && need > batch_cap) fail(CG_INVALID_ARGUMENT, "batch buffer too small");
+  uint8_t* data = batch ? (uint8_t*)batch + hdr : nullptr;
+  auto unit_ptr = [&](size_t slot, uint32_t u) {
+    const HttpTile& t = ttab[slot / CG_HTTP_TILE];
+    return data + (size_t)t.kib * kUnitBytes + (size_t)u * kUnitBytes + (slot % CG_HTTP_TILE) * 16;
+  };
+  if (batch) {
+    HttpBatchHeader h{};
+    h.magic = kBatchMagic;
+    h.epoch = s.epoch;
+    h.nchunks = (uint32_t)chunks.size();
+    h.ntiles = (uint32_t)tiles;
+    h.tiles_off = hdr;
+    h.nslots = nslots;
+    h.ttab_off = ttab_off(max_tiles);
+    h.total_bytes = need;
+    memcpy(batch, &h, sizeof(h));
+    memcpy((uint8_t*)batch + sizeof(h), chunks.data(), chunks.size() * sizeof(HttpChunk));
+    memcpy((uint8_t*)batch + h.ttab_off, ttab.data(), ttab.size() * sizeof(HttpTile));
+    memset(data, 0, kib * kUnitBytes);
+    // padding slots of every group
+    for (auto& [p, c] : count) {
+      size_t s0 = first_slot[p];
+      size_t end = s0 + ((c + CG_HTTP_TILE - 1) / CG_HTTP_TILE) * CG_HTTP_TILE;
+      for (size_t sl = s0 + c; sl < end; ++sl) {
+        unit_ptr(sl, 0)[15] = CG_HTTP_F_PAD;
+        if (order) order[sl] = 0xFFFFFFFFu;
+      }
+    }
+  }
   size_t used = 0;
   for (size_t i = 0; i < n; ++i) {
     const size_t sl = slot_of[i];
@@ -203,10 +230,7 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     uint8_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0;
     if (malformed[i]) flags |= CG_HTTP_F_MALFORMED;
     memcpy(meta + 8, &len, 4);
-    uint8_t slot[CG_HTTP_SLOT_BYTES] = {0};
-    if (len <= CG_HTTP_SLOT_BYTES) {
-      memcpy(slot, str, len);
-    } else {
+    if (len > CG_HTTP_SLOT_BYTES) {
       flags |= CG_HTTP_F_OVERFLOW;
       if (used / 16 >= (1u << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
       uint32_t off16 = (uint32_t)(used / 16);
@@ -218,8 +242,10 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     }
     meta[15] = flags;
     if (batch) {
-      memcpy(unit_ptr(tb, sl, 0), meta, 16);
-      for (int u = 0; u < 8; ++u) memcpy(unit_ptr(tb, sl, u + 1), slot + u * 16, 16);
+      memcpy(unit_ptr(sl, 0), meta, 16);
+      const uint32_t wu = walked_units(i);
+      for (uint32_t u = 0; u < wu; ++u)
+        memcpy(unit_ptr(sl, u + 1), str + u * 16, std::min<size_t>(16, len - u * 16));
     }
   }
   if (arena_used) *arena_used = used;
@@ -232,13 +258,18 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
   memcpy(&h, batch, sizeof(h));
   if (h.magic != kBatchMagic || h.epoch != s.epoch) fail(CG_INVALID_ARGUMENT, "batch packed for another snapshot");
   const HttpChunk* chunks = (const HttpChunk*)(batch + sizeof(h));
-  uint8_t* tb = (uint8_t*)batch + h.tiles_off;
+  const HttpTile* ttab = (const HttpTile*)(batch + h.ttab_off);
+  const uint8_t* data = batch + h.tiles_off;
+  auto unit_ptr = [&](size_t slot, uint32_t u) {
+    return data + (size_t)ttab[slot / CG_HTTP_TILE].kib * kUnitBytes + (size_t)u * kUnitBytes +
+           (slot % CG_HTTP_TILE) * 16;
+  };
   for (uint32_t c = 0; c < h.nchunks; ++c) {
     const uint32_t prog = chunks[c].prog;
     for (size_t sl = (size_t)chunks[c].first_tile * CG_HTTP_TILE;
          sl < (size_t)(chunks[c].first_tile + chunks[c].ntiles) * CG_HTTP_TILE; ++sl) {
       uint8_t meta[16];
-      memcpy(meta, unit_ptr(tb, sl, 0), 16);
+      memcpy(meta, unit_ptr(sl, 0), 16);
       uint32_t remote, len;
       memcpy(&remote, meta, 4);
       memcpy(&len, meta + 8, 4);
@@ -262,9 +293,10 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         if ((size_t)off + len > arena_len) continue;
         str.assign((const char*)arena + off, len);
       } else {
-        uint8_t slot[128];
-        for (int u = 0; u < 8; ++u) memcpy(slot + u * 16, unit_ptr(tb, sl, u + 1), 16);
-        str.assign((const char*)slot, std::min<uint32_t>(len, 128));
+        const uint32_t units = ttab[sl / CG_HTTP_TILE].units;
+        if ((len + 15) / 16 > units) fail(CG_UNKNOWN_ERROR, "internal: string longer than its tile");
+        for (uint32_t u = 0; u < (len + 15) / 16; ++u)
+          str.append((const char*)unit_ptr(sl, u + 1), std::min<size_t>(16, len - u * 16));
       }
       uint32_t roff = pg.default_remote;
       uint64_t key = ((uint64_t)prog << 32) | remote;
@@ -277,7 +309,7 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         hh = (hh + 1) & s.rhash_mask;
       }
       const uint32_t* blk = s.cells.data() + pg.cell_begin;
-      auto bmask = [&](uint32_t off, uint32_t w) { return (uint64_t)blk[off + 2 * w] | (uint64_t)blk[off + 2 * w + 1] << 32; };
+      auto bmask = [&](uint32_t o, uint32_t w) { return (uint64_t)blk[o + 2 * w] | (uint64_t)blk[o + 2 * w + 1] << 32; };
       for (uint32_t w = 0; w < pg.mask_words; ++w)
         if (bmask(pg.always_off, w) & s.masks[roff + w]) v = 1;
       for (uint32_t pi = 0; pi < pg.part_count && !v; ++pi) {

@@ -22,7 +22,6 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kHttpThreads = 1024;
-constexpr uint32_t kTileVecs = CG_HTTP_UNITS * kWave;  // uint4 per tile
 constexpr int kTilesPerWave = 1;  // strings walked per lane at a time
 constexpr uint32_t kDealRun = 4;  // consecutive chunks per workgroup turn
 
@@ -96,19 +95,24 @@ __device__ __forceinline__ bool meets(const uint32_t* __restrict__ blk, uint32_t
 template <int K>
 __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg, uint32_t prog,
                                            const uint32_t* __restrict__ blk, bool rebased,
-                                           const uint4* __restrict__ tiles, const uint32_t (&tile)[K],
+                                           const uint4* __restrict__ tiles, const HttpTile* __restrict__ ttab,
+                                           const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
                                            uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
                                            uint32_t& n_deny) {
   const uint4* tb[K];
   uint32_t len[K], row[K];
+  uint32_t units = 0, tu[K];  // string units: of the K tiles (the longest, wave-uniform), of each
   bool counted[K], overflow[K], verdict[K];
   unsigned long long r0[K], r1[K];
   bool any_overflow = false;
   const uint32_t W = pg.mask_words;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    tb[j] = tiles + (size_t)tile[j] * kTileVecs;
+    const HttpTile tt = ttab[tile[j]];
+    tb[j] = tiles + (size_t)tt.kib * kWave;
+    tu[j] = valid[j] ? tt.units : 0u;
+    units = max(units, tu[j]);
     const uint4 meta = tb[j][lane];
     const uint32_t flags = meta.w >> 24;
     counted[j] = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
@@ -132,21 +136,20 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
       st[j] = pt.start;
       live |= len[j] != 0;
     }
-    if (__any(live)) {
+    if (units && __any(live)) {
+      // a tile stores tu[j] string units; past them (K > 1) a lane re-reads
+      // its tile's last unit, bytes it never reaches within its string
       uint4 cur[K];
 #pragma unroll
-      for (int j = 0; j < K; ++j) cur[j] = tb[j][kWave + lane];
-      for (uint32_t u = 0; u < 8; ++u) {
-        bool longer = false;
-#pragma unroll
-        for (int j = 0; j < K; ++j) longer |= (u + 1) * 16 < len[j];
-        const bool more = __any(longer);
+      for (int j = 0; j < K; ++j) cur[j] = tb[j][min(1u, tu[j]) * kWave + lane];
+      for (uint32_t u = 0; u < units; ++u) {
+        const bool more = u + 1 < units;
         uint4 nxt[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) nxt[j] = cur[j];
-        if (more && u < 7) {
+        if (more) {
 #pragma unroll
-          for (int j = 0; j < K; ++j) nxt[j] = tb[j][(u + 2) * kWave + lane];
+          for (int j = 0; j < K; ++j) nxt[j] = tb[j][min(u + 2, tu[j]) * kWave + lane];
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
@@ -232,6 +235,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
     return;
   }
   const HttpChunk* chunks = reinterpret_cast<const HttpChunk*>(batch + sizeof(HttpBatchHeader));
+  const HttpTile* ttab = reinterpret_cast<const HttpTile*>(batch + H->ttab_off);
   const uint4* tiles = reinterpret_cast<const uint4*>(batch + toff);
   // wave index made wave-uniform (SGPR): tile addresses then live in scalar
   // registers and each load needs only its lane offset in a VGPR
@@ -270,7 +274,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         // no policy for the port → allow; unknown policy → deny; a scope
         // without HTTP rules → allow (cilium_network_policy.h:129-138,187-191)
-        const uint32_t flags = tiles[(size_t)t * kTileVecs + lane].w >> 24;
+        const uint32_t flags = tiles[(size_t)ttab[t].kib * kWave + lane].w >> 24;
         const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
         out[(size_t)t * kWave + lane] = (uint8_t)(counted && (prog == kProgAllow || real) ? 1u : 0u);
         n_allow += real && counted;
@@ -280,8 +284,8 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         const uint32_t tile[1] = {t};
         const bool valid[1] = {true};
-        http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, tile, valid, arena, out, lane, n_allow,
-                      n_deny);
+        http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, ttab, tile, valid, arena, out, lane,
+                      n_allow, n_deny);
       }
     } else {
       // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)
@@ -294,7 +298,8 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
           valid[j] = t < tend;
           tile[j] = valid[j] ? t : t0;
         }
-        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, tile, valid, arena, out, lane, n_allow, n_deny);
+        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, ttab, tile, valid, arena, out, lane, n_allow,
+                                  n_deny);
       }
     }
   }

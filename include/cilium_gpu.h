@@ -231,19 +231,22 @@ int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index);
 /* Snapshot statistics: programs, DFA parts, total states, table bytes. */
 int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n);
 
-/* Packed request batches.  A record is 9 × 16 bytes (1 meta unit + a
- * 128-byte field slot); records are stored tile-transposed in tiles of 64
- * (unit u of lane l at tile*9216 + u*1024 + l*16), so a wavefront's 16-byte
- * load of unit u is one contiguous 1 KiB read.  The packer resolves each
- * request's (policy, direction, port) evaluation program on the host and
- * groups requests by program (padding each group to whole tiles), so a
- * workgroup stages one program's DFA in LDS.  A batch is a 64-byte header,
- * a chunk table, then the tiles; slots are in grouped order and order[slot]
- * gives the request index (UINT32_MAX for padding).  Size the buffers with
- * cg_http_batch_bytes / cg_http_batch_slots (upper bounds for n requests
- * under the installed policy; a batch is tied to the snapshot it was
- * packed against — after a policy update it is rejected and every slot is
- * denied). */
+/* Packed request batches.  A record is a 16-byte meta unit plus its field
+ * string in 16-byte units (at most CG_HTTP_SLOT_BYTES in the record; longer
+ * strings go to the overflow arena).  Records are stored tile-transposed in
+ * tiles of 64: a tile is its meta unit then as many string units as its
+ * longest string needs (unit u of lane l at tile + u*1024 + l*16), so a
+ * wavefront's 16-byte load of unit u is one contiguous 1 KiB read.  The
+ * packer resolves each request's (policy, direction, port) evaluation
+ * program on the host and groups requests by program (padding each group to
+ * whole tiles), so a workgroup stages one program's DFA in LDS.  A batch is
+ * a 64-byte header (its total_bytes field = the batch's size), a chunk
+ * table, a tile table ({offset in KiB, units} per tile), then the tiles;
+ * slots are in grouped order and order[slot] gives the request index
+ * (UINT32_MAX for padding).  Size the buffers with cg_http_batch_bytes /
+ * cg_http_batch_slots (upper bounds for n requests under the installed
+ * policy; a batch is tied to the snapshot it was packed against — after a
+ * policy update it is rejected and every slot is denied). */
 #define CG_HTTP_TILE 64
 #define CG_HTTP_UNITS 9
 #define CG_HTTP_SLOT_BYTES 128

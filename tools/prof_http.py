@@ -36,7 +36,7 @@ def main():
         rq = synth.starwars_requests(args.distinct)
     b = cl.pack_http(**rq)
     reps = max(1, args.requests // args.distinct)
-    d_batch, nslots, _ = bench.replicate_batch(b, reps, dev, torch)
+    d_batch, nslots, _, _ = bench.replicate_batch(b, reps, dev, torch)
     d_arena = torch.from_numpy(b.arena).to(dev)
     d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
