@@ -560,11 +560,11 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
     uint64_t v[12] = {s->progs.size(),
                      s->parts.size(),
                      s->total_states,
-                     s->cells.size() * 4 + s->masks.size() * 8,
+                     s->cells.size() * 4,
                      s->fields.size(),
                      s->total_rules,
                      s->npolicies,
-                     s->rhash_keys.size(),
+                     s->total_remote_slots,
                      s->total_exceptions,
                      s->cells.size(),
                      max_prog_cells,

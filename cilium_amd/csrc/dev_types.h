@@ -92,10 +92,14 @@ struct HttpProg {
   uint32_t flags;
   uint32_t mask_words;      // W
   uint32_t always_off;      // block offset (u32 units) of the "no HTTP rules" PNPR mask
-  uint32_t default_remote;  // masks[] u64 word offset of the mask for unlisted remotes
+  uint32_t default_remote;  // block offset of the PNPR mask of identities not in the table
   uint32_t cell_begin;      // the program's block in cells[], staged into LDS
-  uint32_t cell_count;      // as one piece: parts' comb cells, label tables, masks
+  uint32_t cell_count;      // as one piece: parts' comb cells, label tables, masks,
+  uint32_t rtab_off;        // remote-identity table: {u32 identity, u32 mask offset}
+  uint32_t rtab_mask;       // slots, open addressing by hash32(identity)
+  uint32_t pad[2];
 };
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; states >= self_lo default to themselves.
 // An accepting state's header cell holds its accept label; block[acc_off +
@@ -153,17 +157,8 @@ struct HttpDev {
   const HttpProg* progs;
   const HttpPart* parts;
   const uint32_t* cells;
-  const unsigned long long* masks;  // remote-identity rows (rhash_vals → u64 word offset)
-  // program lookup: key = policy<<17 | ingress<<16 | port
-  const uint32_t* phash_keys;  // empty = 0xFFFFFFFF
-  const uint32_t* phash_vals;
-  uint32_t phash_mask;
   const uint32_t* dflt;        // [policy*2 + ingress] → program id or kProg*
   uint32_t npolicies;
-  // remote lookup: key = prog<<32 | remote → u64 word offset of the mask
-  const unsigned long long* rhash_keys;  // empty = ~0
-  const uint32_t* rhash_vals;
-  uint32_t rhash_mask;
   uint32_t nprogs;
   uint32_t nparts;
   uint32_t epoch;

@@ -471,13 +471,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
   S.npolicies = (uint32_t)pols.size();
   S.dflt.assign((size_t)S.npolicies * 2, kProgAllow);
   std::vector<std::pair<uint32_t, uint32_t>> phash;  // key → prog
-  std::vector<std::pair<uint64_t, uint32_t>> rhash;  // (prog<<32|remote) → mask word off
 
-  auto add_mask = [&](const std::vector<uint64_t>& m) -> uint32_t {
-    uint32_t off = (uint32_t)S.masks.size();
-    S.masks.insert(S.masks.end(), m.begin(), m.end());
-    return off;
-  };
 
   // Build one program from the merged PNPR list; returns program id.
   auto build_prog = [&](const std::vector<const ScopeSpec*>& scopes, uint32_t key) -> uint32_t {
@@ -518,8 +512,6 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     }
     for (uint64_t w : always)
       if (w) pg.flags |= kProgHasAlways;
-    pg.default_remote = add_mask(open);
-    for (auto& [rid, m] : by_remote) rhash.push_back({((uint64_t)pid << 32) | rid, add_mask(m)});
     // union rules
     std::vector<URule> urules;
     std::map<std::vector<int>, size_t> dedupe;
@@ -598,6 +590,37 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       }
     }
     pg.always_off = put_mask(always);
+    // remote-identity table (PortNetworkPolicyRule remote sets, :90-97):
+    // open addressing over {u32 identity, u32 block offset of its PNPR
+    // mask} slots, masks deduplicated; unlisted identities get the mask of
+    // the PNPRs without a remote set
+    {
+      std::map<std::vector<uint64_t>, uint32_t> rows;
+      auto row_of = [&](const std::vector<uint64_t>& m) {
+        auto it = rows.find(m);
+        if (it == rows.end()) it = rows.emplace(m, put_mask(m)).first;
+        return it->second;
+      };
+      pg.default_remote = row_of(open);
+      std::vector<std::pair<uint32_t, uint32_t>> ent;
+      for (auto& [rid, m] : by_remote) ent.push_back({rid, row_of(m)});
+      const uint32_t cap = next_pow2(std::max<size_t>((4 * ent.size() + 2) / 3, 8));  // load ≤ 3/4
+      if (S.cells.size() & 1) S.cells.push_back(0);
+      pg.rtab_off = (uint32_t)S.cells.size() - pg.cell_begin;
+      pg.rtab_mask = cap - 1;
+      const size_t at = S.cells.size();
+      S.cells.resize(at + 2 * (size_t)cap, 0);
+      for (size_t i = 0; i < cap; ++i) S.cells[at + 2 * i + 1] = kNoRow;
+      for (auto [rid, off] : ent) {
+        uint32_t h = hash32(rid) & pg.rtab_mask;
+        while (S.cells[at + 2 * h + 1] != kNoRow) h = (h + 1) & pg.rtab_mask;
+        S.cells[at + 2 * h] = rid;
+        S.cells[at + 2 * h + 1] = off;
+      }
+      S.total_remote_slots += cap;
+    }
+    S.cells.push_back(0);  // spare words: the kernel reads two mask words whatever the width
+    S.cells.push_back(0);
     pg.cell_count = (uint32_t)S.cells.size() - pg.cell_begin;
     S.progs.push_back(pg);
     S.prog_key.push_back(key);
@@ -637,21 +660,6 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       S.phash_vals[h] = v;
     }
   }
-  {
-    uint32_t cap = next_pow2(std::max<size_t>(2 * rhash.size(), 16));
-    S.rhash_keys.assign(cap, ~0ULL);
-    S.rhash_vals.assign(cap, 0);
-    S.rhash_mask = cap - 1;
-    for (auto [k, v] : rhash) {
-      uint32_t h = hash64to32(k) & S.rhash_mask;
-      while (S.rhash_keys[h] != ~0ULL) h = (h + 1) & S.rhash_mask;
-      S.rhash_keys[h] = k;
-      S.rhash_vals[h] = v;
-    }
-  }
-  // two spare words: the kernel reads row words 0 and 1 whatever the width
-  S.masks.push_back(0);
-  S.masks.push_back(0);
   if (S.cells.empty()) S.cells.push_back(kCombEmpty);
   if (S.progs.empty()) S.progs.push_back(HttpProg{});
   if (S.parts.empty()) S.parts.push_back(HttpPart{});
@@ -675,26 +683,14 @@ void HttpSnapshot::upload(Engine& e) {
   d_progs.upload_vec(progs);
   d_parts.upload_vec(parts);
   d_cells.upload_vec(cells);
-  d_masks.upload_vec(masks);
-  d_phk.upload_vec(phash_keys);
-  d_phv.upload_vec(phash_vals);
   d_dflt.upload_vec(dflt);
-  d_rhk.upload_vec(rhash_keys);
-  d_rhv.upload_vec(rhash_vals);
   d_counters.alloc((std::max<size_t>(progs.size(), 1) * 2 + 1) * sizeof(uint64_t));
   d_counters.zero();
   dev.progs = d_progs.as<HttpProg>();
   dev.parts = d_parts.as<HttpPart>();
   dev.cells = d_cells.as<uint32_t>();
-  dev.masks = d_masks.as<unsigned long long>();
-  dev.phash_keys = d_phk.as<uint32_t>();
-  dev.phash_vals = d_phv.as<uint32_t>();
-  dev.phash_mask = phash_mask;
   dev.dflt = d_dflt.as<uint32_t>();
   dev.npolicies = npolicies;
-  dev.rhash_keys = d_rhk.as<unsigned long long>();
-  dev.rhash_vals = d_rhv.as<uint32_t>();
-  dev.rhash_mask = rhash_mask;
   dev.nprogs = (uint32_t)progs.size();
   dev.nparts = (uint32_t)parts.size();
   dev.epoch = epoch;

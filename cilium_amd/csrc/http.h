@@ -19,13 +19,9 @@ struct HttpSnapshot {
   std::vector<HttpProg> progs;
   std::vector<HttpPart> parts;
   std::vector<uint32_t> cells;
-  std::vector<uint64_t> masks;
   std::vector<uint32_t> phash_keys, phash_vals;
   uint32_t phash_mask = 0;
   std::vector<uint32_t> dflt;
-  std::vector<uint64_t> rhash_keys;
-  std::vector<uint32_t> rhash_vals;
-  uint32_t rhash_mask = 0;
   // (policy, ingress, port) of each program, for counter attribution
   std::vector<uint32_t> prog_key;
 
@@ -33,8 +29,9 @@ struct HttpSnapshot {
   uint64_t total_states = 0;
   uint64_t total_exceptions = 0;
   uint64_t total_rules = 0;
+  uint64_t total_remote_slots = 0;
 
-  DevMem d_progs, d_parts, d_cells, d_masks, d_phk, d_phv, d_dflt, d_rhk, d_rhv, d_counters;
+  DevMem d_progs, d_parts, d_cells, d_dflt, d_counters;
   HttpDev dev{};
 
   void upload(Engine& e);

@@ -298,20 +298,19 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         for (uint32_t u = 0; u < (len + 15) / 16; ++u)
           str.append((const char*)unit_ptr(sl, u + 1), std::min<size_t>(16, len - u * 16));
       }
-      uint32_t roff = pg.default_remote;
-      uint64_t key = ((uint64_t)prog << 32) | remote;
-      uint32_t hh = hash64to32(key) & s.rhash_mask;
-      while (s.rhash_keys[hh] != ~0ULL) {
-        if (s.rhash_keys[hh] == key) {
-          roff = s.rhash_vals[hh];
-          break;
-        }
-        hh = (hh + 1) & s.rhash_mask;
-      }
       const uint32_t* blk = s.cells.data() + pg.cell_begin;
       auto bmask = [&](uint32_t o, uint32_t w) { return (uint64_t)blk[o + 2 * w] | (uint64_t)blk[o + 2 * w + 1] << 32; };
+      uint32_t roff = pg.default_remote;
+      for (uint32_t h = hash32(remote) & pg.rtab_mask;; h = (h + 1) & pg.rtab_mask) {
+        const uint32_t key = blk[pg.rtab_off + 2 * h], row = blk[pg.rtab_off + 2 * h + 1];
+        if (row == kNoRow) break;
+        if (key == remote) {
+          roff = row;
+          break;
+        }
+      }
       for (uint32_t w = 0; w < pg.mask_words; ++w)
-        if (bmask(pg.always_off, w) & s.masks[roff + w]) v = 1;
+        if (bmask(pg.always_off, w) & bmask(roff, w)) v = 1;
       for (uint32_t pi = 0; pi < pg.part_count && !v; ++pi) {
         const HttpPart& pt = s.parts[pg.part_begin + pi];
         const uint32_t* cells = s.cells.data() + pt.walk_off;
@@ -324,7 +323,7 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         if (lab == kCombNoLabel) continue;
         const uint32_t a = blk[pt.acc_off + lab];
         for (uint32_t w = 0; w < pg.mask_words; ++w)
-          if (bmask(a, w) & s.masks[roff + w]) v = 1;
+          if (bmask(a, w) & bmask(roff, w)) v = 1;
       }
       out[sl] = v;
     }

@@ -3,7 +3,8 @@
 // NetworkPolicyMap::Allowed (envoy/cilium_network_policy.h:223-237) for every
 // slot of a program-grouped batch (http_pack.cc).  One workgroup takes one
 // chunk of ≤ kChunkTiles tiles of a single program: it stages the program's
-// block — comb-packed DFA (comb.h), accept-label table and PNPR masks — into
+// block — comb-packed DFA (comb.h), accept-label table, PNPR masks and the
+// remote-identity table — into
 // LDS, then each wavefront walks 64 requests at a time, one lane per request.
 // Records are tile-transposed, so each of a wave's 16-byte unit loads is one
 // contiguous 1 KiB read; the DFA walk touches only LDS (one ds_read_b32 per
@@ -58,16 +59,17 @@ __device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cell
   return st;
 }
 
-// Remote-identity mask row of (prog, remote): linear probing from slot h.
-__device__ __forceinline__ uint32_t remote_row(const HttpDev& T, unsigned long long key, uint32_t h,
-                                               uint32_t dflt) {
-  for (uint32_t probe = 0; probe <= T.rhash_mask; ++probe) {
-    const unsigned long long k = T.rhash_keys[h];
-    if (k == key) return T.rhash_vals[h];
-    if (k == ~0ULL) break;
-    h = (h + 1) & T.rhash_mask;
+// Block offset of the PNPR mask of remote identity `remote`: the program's
+// remote table (open addressing, {identity, mask offset} slots).
+__device__ __forceinline__ uint32_t remote_row(const uint32_t* __restrict__ blk, const HttpProg& pg, uint32_t remote) {
+  uint32_t h = hash32(remote) & pg.rtab_mask;
+  for (uint32_t probe = 0; probe <= pg.rtab_mask; ++probe) {
+    const uint2 slot = *reinterpret_cast<const uint2*>(blk + pg.rtab_off + 2 * h);
+    if (slot.y == kNoRow) break;
+    if (slot.x == remote) return slot.y;
+    h = (h + 1) & pg.rtab_mask;
   }
-  return dflt;
+  return pg.default_remote;
 }
 
 // u64 word w of the block mask at block offset a (u32 units, 8-byte aligned).
@@ -75,14 +77,10 @@ __device__ __forceinline__ unsigned long long blk_word(const uint32_t* __restric
   return *reinterpret_cast<const unsigned long long*>(blk + a + 2 * w);
 }
 
-// Does the block mask at `a` meet the remote row?  Words 0 and 1 of the row
-// come preloaded (r0, r1), the rest from T.masks.
-__device__ __forceinline__ bool meets(const uint32_t* __restrict__ blk, uint32_t a, const HttpDev& T, uint32_t row,
-                                      uint32_t W, unsigned long long r0, unsigned long long r1) {
-  if (W > 0 && (blk_word(blk, a, 0) & r0)) return true;
-  if (W > 1 && (blk_word(blk, a, 1) & r1)) return true;
-  for (uint32_t w = 2; w < W; ++w)
-    if (blk_word(blk, a, w) & T.masks[row + w]) return true;
+// Do the PNPR masks at block offsets a and row share a rule?
+__device__ __forceinline__ bool meets(const uint32_t* __restrict__ blk, uint32_t a, uint32_t row, uint32_t W) {
+  for (uint32_t w = 0; w < W; ++w)
+    if (blk_word(blk, a, w) & blk_word(blk, row, w)) return true;
   return false;
 }
 
@@ -104,7 +102,6 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   uint32_t len[K], row[K];
   uint32_t units = 0, tu[K];  // string units: of the K tiles (the longest, wave-uniform), of each
   bool counted[K], overflow[K], verdict[K];
-  unsigned long long r0[K], r1[K];
   bool any_overflow = false;
   const uint32_t W = pg.mask_words;
 #pragma unroll
@@ -119,10 +116,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     overflow[j] = counted[j] && (flags & CG_HTTP_F_OVERFLOW);
     len[j] = counted[j] && !overflow[j] ? meta.z : 0u;
     any_overflow |= overflow[j];
-    const unsigned long long rkey = ((unsigned long long)prog << 32) | meta.x;
-    row[j] = remote_row(T, rkey, hash64to32(rkey) & T.rhash_mask, pg.default_remote);
-    r0[j] = T.masks[row[j]];
-    r1[j] = T.masks[row[j] + 1];
+    row[j] = remote_row(blk, pg, meta.x);
     verdict[j] = false;
   }
   any_overflow = __any(any_overflow);
@@ -176,17 +170,65 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t lab = counted[j] && st[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
-      if (lab != 0xFFFFu && !verdict[j]) verdict[j] = meets(blk, blk[pt.acc_off + lab], T, row[j], W, r0[j], r1[j]);
+      if (lab != 0xFFFFu && !verdict[j]) verdict[j] = meets(blk, blk[pt.acc_off + lab], row[j], W);
     }
   }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     if (counted[j] && !verdict[j] && (pg.flags & kProgHasAlways))
-      verdict[j] = meets(blk, pg.always_off, T, row[j], W, r0[j], r1[j]);
+      verdict[j] = meets(blk, pg.always_off, row[j], W);
     if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict[j];
     n_allow += counted[j] && verdict[j];
     n_deny += counted[j] && !verdict[j];
   }
+}
+
+// One tile of a one-part program whose block `blk` is in LDS, its string
+// units count N known up front (tile table): straight-line code.  Every load
+// of the tile issues at its start — meta, then the N string units — so the
+// tile pays one memory latency, which the SIMD's other waves cover; the
+// remote-identity lookup reads the LDS block after the walk, only for lanes
+// that reached an accepting state.  No early exit: lanes
+// whose string ended (or died) keep stepping through zero padding or the
+// dead state, which cannot change their verdict.
+template <int N>
+__device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
+                                            uint32_t prog, const uint32_t* __restrict__ blk,
+                                            const uint4* __restrict__ tb, uint32_t t,
+                                            const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
+                                            uint32_t lane, uint32_t& n_allow, uint32_t& n_deny) {
+  const uint4 meta = tb[lane];
+  uint4 unit[N > 0 ? N : 1];
+#pragma unroll
+  for (int k = 0; k < N; ++k) unit[k] = tb[(k + 1) * kWave + lane];
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t flags = meta.w >> 24;
+  const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+  const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
+  const uint32_t self_lo = pt.self_lo;
+  uint32_t st = pt.start;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) st = comb_step(blk, self_lo, st, get_byte(unit[k], i));
+  }
+  if (__any(overflow)) {
+    const uint32_t sa = walk_arena(blk, self_lo, pt.start, arena, (meta.w & 0xFFFFFFu) * 16u, overflow ? meta.z : 0u);
+    if (overflow) st = sa;
+  }
+  bool verdict = false;
+  if (counted) {
+    const uint32_t lab = st ? (blk[st - 1] >> 16) : 0xFFFFu;
+    const bool always = pg.flags & kProgHasAlways;
+    if (lab != 0xFFFFu || always) {
+      const uint32_t row = remote_row(blk, pg, meta.x);
+      if (lab != 0xFFFFu) verdict = meets(blk, blk[pt.acc_off + lab], row, pg.mask_words);
+      if (!verdict && always) verdict = meets(blk, pg.always_off, row, pg.mask_words);
+    }
+  }
+  out[(size_t)t * kWave + lane] = (uint8_t)verdict;
+  n_allow += counted && verdict;
+  n_deny += counted && !verdict;
 }
 
 // End of a workgroup's run of chunks of program `prog`: wave totals are
@@ -286,6 +328,22 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         const bool valid[1] = {true};
         http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, ttab, tile, valid, arena, out, lane,
                       n_allow, n_deny);
+      }
+    } else if (pg.part_count == 1) {
+      const HttpPart pt = T.parts[pg.part_begin];
+      for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
+        const HttpTile tt = ttab[t];
+        const uint4* tb = tiles + (size_t)tt.kib * kWave;
+        switch (tt.units) {  // wave-uniform
+#define CG_TILE_N(n) \
+  case n:            \
+    http_tile_n<n>(T, pg, pt, prog, lcells, tb, t, arena, out, lane, n_allow, n_deny); \
+    break;
+          CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
+          default:
+            http_tile_n<8>(T, pg, pt, prog, lcells, tb, t, arena, out, lane, n_allow, n_deny);
+#undef CG_TILE_N
+        }
       }
     } else {
       // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)

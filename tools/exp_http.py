@@ -28,8 +28,21 @@ C_STEP = ("""  uint32_t nx;
       : "vcc");
   return nx;""", """  return (uint16_t)e == (uint16_t)st ? (e >> 16) : dflt;""")
 K = "constexpr int kTilesPerWave = 1;"
+DFLT = "  const uint32_t dflt = st >= self_lo ? st : 0u;\n  // nx = e.lo == st ? e.hi : dflt\n"
+NODFA = ("  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + ((st << 2) + (b << 2)));",
+         "  const uint32_t e = (st * 33u + b) | 0x10000u;")
+WALK = "    for (int i = 0; i < 16; ++i) st = comb_step(blk, self_lo, st, get_byte(unit[k], i));"
+STAGE = "        for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];"
+NOWALK = (WALK, "    for (int i = 0; i < 1; ++i) st ^= unit[k].x ^ unit[k].y ^ unit[k].z ^ unit[k].w;")
+ATOM = ("    if (real && s_cnt[0]) atomicAdd(", "    if (real && s_cnt[0] == 0xFFFFFFFFu) atomicAdd(")
+ATOM2 = ("    if (real && s_cnt[1]) atomicAdd(", "    if (real && s_cnt[1] == 0xFFFFFFFFu) atomicAdd(")
+NOREMOTE = [("  unsigned long long k0 = T.rhash_keys[rh];\n  uint32_t v0 = T.rhash_vals[rh];",
+             "  unsigned long long k0 = rkey;\n  uint32_t v0 = pg.default_remote;"),
+            ("      r0 = T.masks[row];\n      r1 = T.masks[row + 1];\n      __builtin",
+             "      r0 = row;\n      r1 = row;\n      __builtin")]
 VARIANTS = {
     "base": [],
+    "nowalk": [NODFA, NOWALK],
 }
 
 
