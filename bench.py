@@ -74,7 +74,6 @@ def main():
     D = min(args.distinct - args.distinct % 64, args.requests_per_gpu)
     rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
     b = cl.pack_http(**rq)
-    field_bytes = mean_field_bytes(b)
     reps = max(1, args.requests_per_gpu // D)
     B = reps * D                                  # requests per GPU per step
     d_batch, nslots, tile_map, data_bytes = replicate_batch(b, reps, dev, torch)
@@ -174,8 +173,6 @@ def main():
                        "compile_s": round(compile_s, 3), "packed_bytes_per_request": per_launch_bytes / B,
                        "parallelism": f"dp{world}"},
             "request_gbps": value * per_launch_bytes / B / 1e9,
-            "field_bytes_per_request": field_bytes,
-            "field_gbps": value * field_bytes / 1e9,
             "allow_fraction": allow_frac,
             "parity_check": check,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -217,14 +214,15 @@ def replicate_batch(b, reps: int, dev, torch):
             groups[-1][2] += int(nt)
         else:
             groups.append([int(prog), int(first), int(nt)])
-    kib = ttab[:, 0].astype(np.int64)
+    kib = ttab[:, 0].astype(np.int64)  # tile offsets in 512-byte granules (HttpTile.at)
     units = ttab[:, 1].astype(np.int64)
+    span = 1 + 2 * units               # granules per tile: meta block + 1 KiB units
     big, new_tt, placed, pos, kpos = [], [], [], 0, 0
     for prog, first, nt in groups:
         run = nt * reps
         for k in range(0, run, CHUNK_TILES):
             big.append((prog, pos + k, min(CHUNK_TILES, run - k), 0))
-        g_kib = int(kib[first + nt - 1] + 1 + units[first + nt - 1] - kib[first])
+        g_kib = int(kib[first + nt - 1] + span[first + nt - 1] - kib[first])
         rel = kib[first:first + nt] - kib[first]
         for r in range(reps):
             new_tt.append(np.stack([kpos + r * g_kib + rel, units[first:first + nt]], axis=1))
@@ -235,7 +233,7 @@ def replicate_batch(b, reps: int, dev, torch):
     new_tt = np.concatenate(new_tt).astype(np.uint32)
     ttoff = 64 + 16 * len(big)
     hbytes = (ttoff + 8 * pos + 1023) // 1024 * 1024
-    total = hbytes + kpos * 1024
+    total = hbytes + kpos * 512
     hdr = b.batch[:64].copy()
     hdr[8:12] = np.array([len(big)], np.uint32).view(np.uint8)
     hdr[12:16] = np.array([pos], np.uint32).view(np.uint8)
@@ -246,12 +244,12 @@ def replicate_batch(b, reps: int, dev, torch):
     head[ttoff:ttoff + new_tt.nbytes] = new_tt.reshape(-1).view(np.uint8)
     d = torch.empty(total, dtype=torch.uint8, device=dev)
     d[:hbytes].copy_(torch.from_numpy(head))
-    data_end = int(kib[-1] + 1 + units[-1]) * 1024 if ntiles else 0
+    data_end = int(kib[-1] + span[-1]) * 512 if ntiles else 0
     src = torch.from_numpy(b.batch[toff:toff + data_end]).to(dev)
     tile_map = np.zeros(ntiles, np.int64)
     for first, nt, at, k0, g_kib, kp in placed:
-        g0, gb = hbytes + kp * 1024, g_kib * 1024
-        d[g0:g0 + gb].copy_(src[k0 * 1024:k0 * 1024 + gb])
+        g0, gb = hbytes + kp * 512, g_kib * 512
+        d[g0:g0 + gb].copy_(src[k0 * 512:k0 * 512 + gb])
         done = 1
         while done < reps:  # doubling copies on the device
             k = min(done, reps - done)
@@ -259,16 +257,6 @@ def replicate_batch(b, reps: int, dev, torch):
             done += k
         tile_map[first:first + nt] = np.arange(at, at + nt)
     return d, pos * 64, tile_map, total - 64
-
-
-def mean_field_bytes(b) -> float:
-    """Mean length of the requests' field strings (header values joined by
-    the packer's separators, http_pack.cc) over the real slots of batch b."""
-    ntiles, toff, _, ttab = batch_parts(b.batch)
-    metas = np.stack([b.batch[toff + int(k) * 1024:toff + int(k) * 1024 + 1024] for k in ttab[:, 0]])
-    ln = metas.reshape(-1, 16)[:, 8:12].copy().view(np.uint32).reshape(-1)
-    real = b.order != 0xFFFFFFFF
-    return float(ln[real].mean()) if real.any() else 0.0
 
 
 def pmc_traffic(requests_per_launch: int):

@@ -125,12 +125,13 @@ constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
 
 // Packed HTTP batch (cg_http_pack): a 64-byte header, the chunk table, the
 // tile table, then the tiles (1 KiB aligned).  A tile is 64 request records
-// stored unit-major: its meta unit, then `units` 16-byte string units, each
-// unit one contiguous 1 KiB (unit u of lane l at tile + u*1024 + l*16).  The
+// stored unit-major: the meta block (8 bytes per lane), then `units` 16-byte
+// string units, each one contiguous 1 KiB (string unit u ≥ 1 of lane l at
+// tile + 512 + (u-1)*1024 + l*16).  The
 // packer groups requests by program so every chunk (≤ kChunkTiles tiles)
 // belongs to one program and a workgroup can stage that program's table in
 // LDS.  Slot order is returned to the caller (order[]).
-constexpr uint32_t kBatchMagic = 0x32484743u;  // "CGH2"
+constexpr uint32_t kBatchMagic = 0x33484743u;  // "CGH3"
 constexpr uint32_t kChunkTiles = 64;
 struct HttpBatchHeader {
   uint32_t magic;
@@ -144,8 +145,8 @@ struct HttpBatchHeader {
   uint32_t pad[4];
 };
 struct HttpTile {
-  uint32_t kib;    // tile data at tiles_off + kib * 1024
-  uint32_t units;  // string units stored after the meta unit (0..8)
+  uint32_t at;     // tile data at tiles_off + at * 512: the 512-byte meta block
+  uint32_t units;  // (8 bytes per lane), then `units` 1 KiB string units (0..8)
 };
 struct HttpChunk {
   uint32_t prog;

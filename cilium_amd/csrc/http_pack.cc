@@ -29,8 +29,15 @@ constexpr uint8_t kRestAbsent = 0x02;  // every remaining field absent (http.cc)
 // IS_HEADER_CHAR: control bytes other than HTAB, and DEL); the request never
 // reaches the L7 filter.
 inline bool codec_rejects(uint8_t c) { return (c < 0x20 && c != 0x09) || c == 0x7F; }
-constexpr size_t kUnitBytes = (size_t)CG_HTTP_TILE * 16;  // one unit of a tile: 1 KiB
-constexpr size_t kMaxTileBytes = (size_t)CG_HTTP_UNITS * kUnitBytes;
+constexpr size_t kUnitBytes = (size_t)CG_HTTP_TILE * 16;  // one string unit of a tile: 1 KiB
+constexpr size_t kMetaBytes = (size_t)CG_HTTP_TILE * CG_HTTP_META_BYTES;  // the tile's meta block: 512 B
+constexpr size_t kGranule = 512;  // tile offsets count 512-byte granules
+constexpr size_t kMaxTileBytes = kMetaBytes + (size_t)(CG_HTTP_UNITS - 1) * kUnitBytes;
+
+// byte offset of unit u (0 = meta block) of a tile at granule g, lane l
+inline size_t tile_unit_at(uint32_t g, uint32_t u, size_t lane) {
+  return (size_t)g * kGranule + (u ? kMetaBytes + (size_t)(u - 1) * kUnitBytes + lane * 16 : lane * CG_HTTP_META_BYTES);
+}
 
 bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
   if (an != lower_b.size()) return false;
@@ -174,20 +181,19 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     HttpTile& t = ttab[slot_of[i] / CG_HTTP_TILE];
     t.units = std::max(t.units, walked_units(i));
   }
-  uint64_t kib = 0;
+  uint64_t gran = 0;
   for (auto& t : ttab) {
-    if (kib > 0xFFFFFFFFull) fail(CG_INVALID_ARGUMENT, "batch beyond 4 TiB");
-    t.kib = (uint32_t)kib;
-    kib += 1 + t.units;
+    if (gran > 0xFFFFFFFFull) fail(CG_INVALID_ARGUMENT, "batch beyond 2 TiB");
+    t.at = (uint32_t)gran;
+    gran += 1 + 2 * t.units;
   }
   const size_t max_tiles = http_batch_slots(s, n) / CG_HTTP_TILE;
   const size_t hdr = header_bytes(max_tiles);
-  const size_t need = hdr + kib * kUnitBytes;
+  const size_t need = hdr + gran * kGranule;
   if (batch && need > batch_cap) fail(CG_INVALID_ARGUMENT, "batch buffer too small");
   uint8_t* data = batch ? (uint8_t*)batch + hdr : nullptr;
   auto unit_ptr = [&](size_t slot, uint32_t u) {
-    const HttpTile& t = ttab[slot / CG_HTTP_TILE];
-    return data + (size_t)t.kib * kUnitBytes + (size_t)u * kUnitBytes + (slot % CG_HTTP_TILE) * 16;
+    return data + tile_unit_at(ttab[slot / CG_HTTP_TILE].at, u, slot % CG_HTTP_TILE);
   };
   if (batch) {
     HttpBatchHeader h{};
@@ -202,13 +208,13 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     memcpy(batch, &h, sizeof(h));
     memcpy((uint8_t*)batch + sizeof(h), chunks.data(), chunks.size() * sizeof(HttpChunk));
     memcpy((uint8_t*)batch + h.ttab_off, ttab.data(), ttab.size() * sizeof(HttpTile));
-    memset(data, 0, kib * kUnitBytes);
+    memset(data, 0, gran * kGranule);
     // padding slots of every group
     for (auto& [p, c] : count) {
       size_t s0 = first_slot[p];
       size_t end = s0 + ((c + CG_HTTP_TILE - 1) / CG_HTTP_TILE) * CG_HTTP_TILE;
       for (size_t sl = s0 + c; sl < end; ++sl) {
-        unit_ptr(sl, 0)[15] = CG_HTTP_F_PAD;
+        unit_ptr(sl, 0)[7] = CG_HTTP_F_PAD;
         if (order) order[sl] = 0xFFFFFFFFu;
       }
     }
@@ -220,29 +226,29 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     if (!build) continue;
     const uint8_t* str = strs.data() + soff[i];
     const uint32_t len = (uint32_t)(soff[i + 1] - soff[i]);
-    // meta: [0..3] remote, [4..5] port, [6..7] policy (0xFFFF unknown),
-    // [8..11] string length, [12..14] arena offset / 16, [15] flags
-    uint8_t meta[16] = {0};
+    // meta (CG_HTTP_META_BYTES = 8): [0..3] remote identity, [4..6] overflow
+    // arena offset / 16, [7] flags; an overflow arena entry is its u32 length
+    // then the string, 16-byte aligned
+    uint8_t meta[CG_HTTP_META_BYTES] = {0};
     memcpy(meta, &remote[i], 4);
-    memcpy(meta + 4, &port[i], 2);
-    uint16_t pol16 = policy[i] >= s.npolicies ? 0xFFFF : (uint16_t)policy[i];
-    memcpy(meta + 6, &pol16, 2);
     uint8_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0;
     if (malformed[i]) flags |= CG_HTTP_F_MALFORMED;
-    memcpy(meta + 8, &len, 4);
     if (len > CG_HTTP_SLOT_BYTES) {
       flags |= CG_HTTP_F_OVERFLOW;
       if (used / 16 >= (1u << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
       uint32_t off16 = (uint32_t)(used / 16);
-      if (arena && used + len <= arena_cap) memcpy(arena + used, str, len);
-      used += (len + 15) & ~(size_t)15;
-      meta[12] = off16 & 0xFF;
-      meta[13] = (off16 >> 8) & 0xFF;
-      meta[14] = (off16 >> 16) & 0xFF;
+      if (arena && used + 4 + len <= arena_cap) {
+        memcpy(arena + used, &len, 4);
+        memcpy(arena + used + 4, str, len);
+      }
+      used += (4 + len + 15) & ~(size_t)15;
+      meta[4] = off16 & 0xFF;
+      meta[5] = (off16 >> 8) & 0xFF;
+      meta[6] = (off16 >> 16) & 0xFF;
     }
-    meta[15] = flags;
+    meta[7] = flags;
     if (batch) {
-      memcpy(unit_ptr(sl, 0), meta, 16);
+      memcpy(unit_ptr(sl, 0), meta, CG_HTTP_META_BYTES);
       const uint32_t wu = walked_units(i);
       for (uint32_t u = 0; u < wu; ++u)
         memcpy(unit_ptr(sl, u + 1), str + u * 16, std::min<size_t>(16, len - u * 16));
@@ -261,20 +267,18 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
   const HttpTile* ttab = (const HttpTile*)(batch + h.ttab_off);
   const uint8_t* data = batch + h.tiles_off;
   auto unit_ptr = [&](size_t slot, uint32_t u) {
-    return data + (size_t)ttab[slot / CG_HTTP_TILE].kib * kUnitBytes + (size_t)u * kUnitBytes +
-           (slot % CG_HTTP_TILE) * 16;
+    return data + tile_unit_at(ttab[slot / CG_HTTP_TILE].at, u, slot % CG_HTTP_TILE);
   };
   for (uint32_t c = 0; c < h.nchunks; ++c) {
     const uint32_t prog = chunks[c].prog;
     for (size_t sl = (size_t)chunks[c].first_tile * CG_HTTP_TILE;
          sl < (size_t)(chunks[c].first_tile + chunks[c].ntiles) * CG_HTTP_TILE; ++sl) {
-      uint8_t meta[16];
-      memcpy(meta, unit_ptr(sl, 0), 16);
-      uint32_t remote, len;
+      uint8_t meta[CG_HTTP_META_BYTES];
+      memcpy(meta, unit_ptr(sl, 0), CG_HTTP_META_BYTES);
+      uint32_t remote;
       memcpy(&remote, meta, 4);
-      memcpy(&len, meta + 8, 4);
-      uint32_t off = ((uint32_t)meta[12] | ((uint32_t)meta[13] << 8) | ((uint32_t)meta[14] << 16)) * 16u;
-      const uint8_t flags = meta[15];
+      const uint32_t off = ((uint32_t)meta[4] | ((uint32_t)meta[5] << 8) | ((uint32_t)meta[6] << 16)) * 16u;
+      const uint8_t flags = meta[7];
       uint8_t v = 0;
       out[sl] = 0;
       if (flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED)) continue;
@@ -288,15 +292,17 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         out[sl] = 1;
         continue;
       }
+      // the bytes the kernel walks: the arena string, or the tile's units
+      // (the string and its zero padding, which cannot change the verdict)
       std::string str;
       if (flags & CG_HTTP_F_OVERFLOW) {
-        if ((size_t)off + len > arena_len) continue;
-        str.assign((const char*)arena + off, len);
+        uint32_t len = 0;
+        if ((size_t)off + 4 > arena_len) continue;
+        memcpy(&len, arena + off, 4);
+        if ((size_t)off + 4 + len > arena_len) continue;
+        str.assign((const char*)arena + off + 4, len);
       } else {
-        const uint32_t units = ttab[sl / CG_HTTP_TILE].units;
-        if ((len + 15) / 16 > units) fail(CG_UNKNOWN_ERROR, "internal: string longer than its tile");
-        for (uint32_t u = 0; u < (len + 15) / 16; ++u)
-          str.append((const char*)unit_ptr(sl, u + 1), std::min<size_t>(16, len - u * 16));
+        for (uint32_t u = 0; u < ttab[sl / CG_HTTP_TILE].units; ++u) str.append((const char*)unit_ptr(sl, u + 1), 16);
       }
       const uint32_t* blk = s.cells.data() + pg.cell_begin;
       auto bmask = [&](uint32_t o, uint32_t w) { return (uint64_t)blk[o + 2 * w] | (uint64_t)blk[o + 2 * w + 1] << 32; };

@@ -59,6 +59,35 @@ __device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cell
   return st;
 }
 
+// A tile's meta block (8 bytes per lane: remote identity, overflow arena
+// offset / 16 | flags << 24) and its string units (unit u ≥ 1 of lane l at
+// units[(u - 1) * 64 + l]).
+struct TileRef {
+  const uint2* meta;
+  const uint4* units;
+};
+__device__ __forceinline__ TileRef tile_ref(const uint8_t* __restrict__ tiles, const HttpTile& tt) {
+  const uint8_t* base = tiles + (size_t)tt.at * 512;
+  return {reinterpret_cast<const uint2*>(base), reinterpret_cast<const uint4*>(base + kWave * CG_HTTP_META_BYTES)};
+}
+
+// String unit u (1-based) of a tile holding `units` of them; past them a lane
+// re-reads the tile's last unit, or its meta block when it has none (bytes
+// it never walks within its string) — never beyond the tile.
+__device__ __forceinline__ uint4 tile_unit(const TileRef& tr, uint32_t units, uint32_t u, uint32_t lane) {
+  if (units == 0) return reinterpret_cast<const uint4*>(tr.meta)[lane & 31];
+  return tr.units[(min(u, units) - 1) * kWave + lane];
+}
+
+// The overflow string of a lane whose meta word is m (arena entry: u32 length, bytes).
+__device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+                                                 const uint8_t* __restrict__ arena, uint2 m, bool ov) {
+  if (!ov) return st;
+  const uint32_t aoff = (m.y & 0xFFFFFFu) * 16u;
+  const uint32_t len = *reinterpret_cast<const uint32_t*>(arena + aoff);
+  return walk_arena(cells, self_lo, st, arena, aoff + 4, len);
+}
+
 // Block offset of the PNPR mask of remote identity `remote`: the program's
 // remote table (open addressing, {identity, mask offset} slots).
 __device__ __forceinline__ uint32_t remote_row(const uint32_t* __restrict__ blk, const HttpProg& pg, uint32_t remote) {
@@ -93,13 +122,14 @@ __device__ __forceinline__ bool meets(const uint32_t* __restrict__ blk, uint32_t
 template <int K>
 __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg, uint32_t prog,
                                            const uint32_t* __restrict__ blk, bool rebased,
-                                           const uint4* __restrict__ tiles, const HttpTile* __restrict__ ttab,
+                                           const uint8_t* __restrict__ tiles, const HttpTile* __restrict__ ttab,
                                            const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
                                            uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
                                            uint32_t& n_deny) {
-  const uint4* tb[K];
-  uint32_t len[K], row[K];
+  TileRef tr[K];
+  uint2 meta[K];
+  uint32_t row[K];
   uint32_t units = 0, tu[K];  // string units: of the K tiles (the longest, wave-uniform), of each
   bool counted[K], overflow[K], verdict[K];
   bool any_overflow = false;
@@ -107,16 +137,15 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const HttpTile tt = ttab[tile[j]];
-    tb[j] = tiles + (size_t)tt.kib * kWave;
+    tr[j] = tile_ref(tiles, tt);
     tu[j] = valid[j] ? tt.units : 0u;
     units = max(units, tu[j]);
-    const uint4 meta = tb[j][lane];
-    const uint32_t flags = meta.w >> 24;
+    meta[j] = tr[j].meta[lane];
+    const uint32_t flags = meta[j].y >> 24;
     counted[j] = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
     overflow[j] = counted[j] && (flags & CG_HTTP_F_OVERFLOW);
-    len[j] = counted[j] && !overflow[j] ? meta.z : 0u;
     any_overflow |= overflow[j];
-    row[j] = remote_row(blk, pg, meta.x);
+    row[j] = remote_row(blk, pg, meta[j].x);
     verdict[j] = false;
   }
   any_overflow = __any(any_overflow);
@@ -124,18 +153,14 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     const HttpPart pt = T.parts[pg.part_begin + pi];
     const uint32_t* __restrict__ cells = rebased ? blk : T.cells + pt.walk_off;
     uint32_t st[K];
-    bool live = false;
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      st[j] = pt.start;
-      live |= len[j] != 0;
-    }
-    if (units && __any(live)) {
+    for (int j = 0; j < K; ++j) st[j] = pt.start;
+    if (units) {
       // a tile stores tu[j] string units; past them (K > 1) a lane re-reads
-      // its tile's last unit, bytes it never reaches within its string
+      // its tile's last unit, which cannot change its verdict
       uint4 cur[K];
 #pragma unroll
-      for (int j = 0; j < K; ++j) cur[j] = tb[j][min(1u, tu[j]) * kWave + lane];
+      for (int j = 0; j < K; ++j) cur[j] = tile_unit(tr[j], tu[j], 1, lane);
       for (uint32_t u = 0; u < units; ++u) {
         const bool more = u + 1 < units;
         uint4 nxt[K];
@@ -143,7 +168,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
         for (int j = 0; j < K; ++j) nxt[j] = cur[j];
         if (more) {
 #pragma unroll
-          for (int j = 0; j < K; ++j) nxt[j] = tb[j][min(u + 2, tu[j]) * kWave + lane];
+          for (int j = 0; j < K; ++j) nxt[j] = tile_unit(tr[j], tu[j], u + 2, lane);
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
@@ -152,7 +177,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
         }
         bool alive = false;
 #pragma unroll
-        for (int j = 0; j < K; ++j) alive |= st[j] != 0 && (u + 1) * 16 < len[j];
+        for (int j = 0; j < K; ++j) alive |= st[j] != 0;
         if (!more || !__any(alive)) break;
 #pragma unroll
         for (int j = 0; j < K; ++j) cur[j] = nxt[j];
@@ -161,9 +186,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     if (any_overflow) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const uint4 meta = tb[j][lane];
-        const uint32_t sa =
-            walk_arena(cells, pt.self_lo, pt.start, arena, (meta.w & 0xFFFFFFu) * 16u, overflow[j] ? meta.z : 0u);
+        const uint32_t sa = walk_overflow(cells, pt.self_lo, pt.start, arena, meta[j], overflow[j]);
         if (overflow[j]) st[j] = sa;
       }
     }
@@ -194,15 +217,15 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 template <int N>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
                                             uint32_t prog, const uint32_t* __restrict__ blk,
-                                            const uint4* __restrict__ tb, uint32_t t,
+                                            const TileRef tr, uint32_t t,
                                             const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
                                             uint32_t lane, uint32_t& n_allow, uint32_t& n_deny) {
-  const uint4 meta = tb[lane];
+  const uint2 meta = tr.meta[lane];
   uint4 unit[N > 0 ? N : 1];
 #pragma unroll
-  for (int k = 0; k < N; ++k) unit[k] = tb[(k + 1) * kWave + lane];
+  for (int k = 0; k < N; ++k) unit[k] = tr.units[k * kWave + lane];
   __builtin_amdgcn_sched_barrier(0);
-  const uint32_t flags = meta.w >> 24;
+  const uint32_t flags = meta.y >> 24;
   const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
   const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
   const uint32_t self_lo = pt.self_lo;
@@ -213,7 +236,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
     for (int i = 0; i < 16; ++i) st = comb_step(blk, self_lo, st, get_byte(unit[k], i));
   }
   if (__any(overflow)) {
-    const uint32_t sa = walk_arena(blk, self_lo, pt.start, arena, (meta.w & 0xFFFFFFu) * 16u, overflow ? meta.z : 0u);
+    const uint32_t sa = walk_overflow(blk, self_lo, pt.start, arena, meta, overflow);
     if (overflow) st = sa;
   }
   bool verdict = false;
@@ -278,7 +301,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
   }
   const HttpChunk* chunks = reinterpret_cast<const HttpChunk*>(batch + sizeof(HttpBatchHeader));
   const HttpTile* ttab = reinterpret_cast<const HttpTile*>(batch + H->ttab_off);
-  const uint4* tiles = reinterpret_cast<const uint4*>(batch + toff);
+  const uint8_t* tiles = batch + toff;
   // wave index made wave-uniform (SGPR): tile addresses then live in scalar
   // registers and each load needs only its lane offset in a VGPR
   const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
@@ -316,7 +339,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         // no policy for the port → allow; unknown policy → deny; a scope
         // without HTTP rules → allow (cilium_network_policy.h:129-138,187-191)
-        const uint32_t flags = tiles[(size_t)ttab[t].kib * kWave + lane].w >> 24;
+        const uint32_t flags = tile_ref(tiles, ttab[t]).meta[lane].y >> 24;
         const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
         out[(size_t)t * kWave + lane] = (uint8_t)(counted && (prog == kProgAllow || real) ? 1u : 0u);
         n_allow += real && counted;
@@ -333,7 +356,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       const HttpPart pt = T.parts[pg.part_begin];
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         const HttpTile tt = ttab[t];
-        const uint4* tb = tiles + (size_t)tt.kib * kWave;
+        const TileRef tb = tile_ref(tiles, tt);
         switch (tt.units) {  // wave-uniform
 #define CG_TILE_N(n) \
   case n:            \

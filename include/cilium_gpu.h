@@ -231,12 +231,13 @@ int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index);
 /* Snapshot statistics: programs, DFA parts, total states, table bytes. */
 int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n);
 
-/* Packed request batches.  A record is a 16-byte meta unit plus its field
+/* Packed request batches.  A record is an 8-byte meta word plus its field
  * string in 16-byte units (at most CG_HTTP_SLOT_BYTES in the record; longer
  * strings go to the overflow arena).  Records are stored tile-transposed in
- * tiles of 64: a tile is its meta unit then as many string units as its
- * longest string needs (unit u of lane l at tile + u*1024 + l*16), so a
- * wavefront's 16-byte load of unit u is one contiguous 1 KiB read.  The
+ * tiles of 64: a tile is its 512-byte meta block then as many string units as
+ * its longest string needs (string unit u ≥ 1 of lane l at tile + 512 +
+ * (u-1)*1024 + l*16), so a wavefront's 16-byte load of a unit is one
+ * contiguous 1 KiB read.  The
  * packer resolves each request's (policy, direction, port) evaluation
  * program on the host and groups requests by program (padding each group to
  * whole tiles), so a workgroup stages one program's DFA in LDS.  A batch is
@@ -250,12 +251,13 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n);
 #define CG_HTTP_TILE 64
 #define CG_HTTP_UNITS 9
 #define CG_HTTP_SLOT_BYTES 128
+#define CG_HTTP_META_BYTES 8
 size_t cg_http_batch_bytes(uint64_t h, size_t n);
 size_t cg_http_batch_slots(uint64_t h, size_t n);
 
-/* Request flags (meta byte 15).  Meta unit: [0..3] remote identity, [4..5] port,
- * [6..7] policy index (0xFFFF unknown), [8..11] string length, [12..14] overflow
- * arena offset / 16, [15] flags. */
+/* Request flags (meta byte 7).  Meta word: [0..3] remote identity, [4..6]
+ * overflow arena offset / 16, [7] flags.  An overflow arena entry is the
+ * string's u32 length followed by the string. */
 #define CG_HTTP_F_INGRESS 0x01u
 #define CG_HTTP_F_OVERFLOW 0x02u  /* fields in the overflow arena */
 #define CG_HTTP_F_MALFORMED 0x04u /* field holds a byte Envoy's codec rejects */
