@@ -1,0 +1,172 @@
+"""Throughput of the three non-north-star verdict kernels at their BASELINE
+configs, one JSON line each (bench.py covers config 5, the 10K-rule HTTP set):
+
+* L4 policymap (config 2): 16K-entry table, 100M tuples
+* CIDR prefilter (config 3): 1M mixed v4/v6 prefixes, 1B addresses
+* Kafka (config 4): 1K rules, 100M requests
+
+Inputs are resident in HBM before timing; kernels are timed with HIP events
+on their stream.  Each line carries the kernel's HBM roofline (algorithmic
+bytes: packed input + output per item) and the CPU oracle timed on a sample.
+Distinct synthetic items are generated on the host and tiled on the device
+to the config's count; verdicts of the first copy are checked against the
+oracle before timing.
+
+    python tools/bench_paths.py [--paths l4,lpm,kafka] [--steps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0
+
+
+def tile_dev(torch, host: np.ndarray, reps: int, dev):
+    """Device array of `reps` back-to-back copies of host (doubling copies)."""
+    raw = host.reshape(-1).view(np.uint8)
+    d = torch.empty(raw.nbytes * reps, dtype=torch.uint8, device=dev)
+    d[:raw.nbytes].copy_(torch.from_numpy(raw))
+    done = 1
+    while done < reps:
+        k = min(done, reps - done)
+        d[done * raw.nbytes:(done + k) * raw.nbytes].copy_(d[:k * raw.nbytes])
+        done += k
+    return d
+
+
+def timed(torch, stream, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = []
+    for _ in range(steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / steps * 1e-3
+
+
+def cpu_rate(fn, items, seconds):
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        n += items
+    return n / (time.perf_counter() - t0)
+
+
+def line(metric, n, sec, bytes_per_item, kernel, cpu, cpu_sample, threads, extra):
+    achieved = n * bytes_per_item / sec / 1e9
+    return {"metric": metric, "value": n / sec, "unit": "verdicts/s", "n_gpus": 1, "ms_per_launch": sec * 1e3,
+            "items_per_launch": n, "higher_is_better": True, "data": "synthetic",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "kernel": kernel, "bytes_per_item": bytes_per_item},
+            "cpu_baseline": {"value": cpu, "unit": "verdicts/s", "cores": threads, "kind": "port",
+                             "sample": cpu_sample}, **extra}
+
+
+def bench_l4(torch, dev, stream, cl, args, threads):
+    import oracle
+    from cilium_amd import synth
+    keys, ports = synth.l4_table()
+    pm = cl.policy_map()
+    pm.allow_keys(keys, ports)
+    D, reps = 10_000_000, 10
+    tup = synth.l4_tuples(D, keys)
+    got = pm.verdicts(tup[:2_000_000])
+    exp, _, _ = oracle.l4(keys, ports, tup[:2_000_000])
+    assert np.array_equal(got, exp), "L4 verdicts differ from the oracle"
+    d_t = tile_dev(torch, tup, reps, dev)
+    n = D * reps
+    d_o = torch.empty(n, dtype=torch.int32, device=dev)
+    sec = timed(torch, stream, lambda: pm.verdicts_dev(d_t, n, d_o, stream=stream.cuda_stream), args.steps, 2)
+    sample = tup[:2_000_000]
+    cpu = cpu_rate(lambda: oracle.l4(keys, ports, sample), len(sample), args.cpu_seconds)
+    return line("L4 policymap verdicts/s (__policy_can_access), config 2", n, sec, 16, "l4_kernel", cpu,
+                f"2M tuples of the same workload, 1 thread (oracle.l4 is single-threaded)", 1,
+                {"config": {"workload": "BASELINE config 2: 16,384-entry policy map, 100M tuples",
+                            "entries": int(len(keys)), "tuples": n}})
+
+
+def bench_lpm(torch, dev, stream, cl, args, threads):
+    import oracle
+    from cilium_amd import synth
+    pfx = synth.lpm_prefixes()
+    pf = cl.prefilter(dyn4=True, dyn6=True, max_lpm=1 << 21)
+    pf.insert(0, pfx)
+    D, reps = 100_000_000, 10
+    v4, v6, ep4, ep6 = synth.lpm_addresses(D, pfx)
+    pf.set_endpoints(ep4, ep6)
+    g4, g6 = pf.verdicts(v4[:1_000_000], v6[:400_000])
+    o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4[:1_000_000], v6[:400_000], nthreads=threads)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6), "prefilter verdicts differ from the oracle"
+    d4 = tile_dev(torch, v4, reps, dev)
+    d6 = tile_dev(torch, v6, reps, dev)
+    n4, n6 = len(v4) * reps, len(v6) * reps
+    o4d = torch.empty(n4, dtype=torch.uint8, device=dev)
+    o6d = torch.empty(n6, dtype=torch.uint8, device=dev)
+    sec = timed(torch, stream, lambda: pf.verdicts_dev(d4, n4, o4d, d6, n6, o6d, stream=stream.cuda_stream),
+                args.steps, 2)
+    bpi = (n4 * 9 + n6 * 33) / (n4 + n6)
+    s4, s6 = v4[:700_000], v6[:300_000]
+    cpu = cpu_rate(lambda: oracle.prefilter(pf.config, pfx, ep4, ep6, s4, s6, nthreads=threads), 1_000_000,
+                   args.cpu_seconds)
+    return line("XDP prefilter verdicts/s (check_v4/check_v6), config 3", n4 + n6, sec, bpi, "lpm_kernel", cpu,
+                f"1M addresses (70% v4) of the same workload, {threads} threads", threads,
+                {"config": {"workload": "BASELINE config 3: 1M mixed v4/v6 prefixes, 1B addresses",
+                            "prefixes": int(len(pfx)), "addresses": n4 + n6}})
+
+
+def bench_kafka(torch, dev, stream, cl, args, threads):
+    import oracle
+    from cilium_amd import synth
+    pols, info = synth.kafka_policy()
+    cl.update_kafka_policy(pols)
+    D, reps = 1_000_000, 100
+    rq = synth.kafka_requests(D, info)
+    reqs, arena = cl.pack_kafka(**rq)
+    got = cl.kafka_verdicts(reqs[:200_000], arena)
+    sub = {k: v[:200_000] for k, v in rq.items()}
+    orc = oracle.KafkaOracle(pols)
+    assert np.array_equal(got, orc.eval(**sub, nthreads=threads)), "Kafka verdicts differ from the oracle"
+    d_r = tile_dev(torch, reqs, reps, dev)
+    d_a = torch.from_numpy(arena).to(dev)
+    n = D * reps
+    d_o = torch.empty(n, dtype=torch.uint8, device=dev)
+    sec = timed(torch, stream, lambda: cl.kafka_verdicts_dev(d_r, n, d_a, d_o, stream=stream.cuda_stream),
+                args.steps, 2)
+    cpu = cpu_rate(lambda: orc.eval(**sub, nthreads=threads), 200_000, args.cpu_seconds)
+    return line("Kafka verdicts/s (kafkaRedirect.canAccess → MatchesRule), config 4", n, sec, 65, "kafka_kernel",
+                cpu, f"200K requests of the same workload, {threads} threads", threads,
+                {"config": {"workload": "BASELINE config 4: 1K Kafka rules, 100M requests", "requests": n}})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--paths", default="l4,lpm,kafka")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    args = ap.parse_args()
+    import torch
+    from cilium_amd.classifier import Classifier
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(device=dev)
+    cl = Classifier(device=0)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka}
+    for p in args.paths.split(","):
+        print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
+    cl.close()
+
+
+if __name__ == "__main__":
+    main()
