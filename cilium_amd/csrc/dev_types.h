@@ -182,25 +182,41 @@ CG_HD inline uint32_t hash64to32(uint64_t k) {
 }
 
 // --------------------------------------------------------------- Kafka ----
-// Per (redirect, identity group): compiled rule sets; see kafka.cc.
+// Per (redirect, identity group) the rule set is compiled into decision
+// summaries, one per (context, apiKey bucket): context 0 = the request has
+// topics (only topic-less rules apply unconditionally), 1 = it has none (every
+// rule applies); bucket = apiKey for 0..63, 64 for any other key (only
+// apiKey-wildcard rules reach it).  A summary answers ruleMatches for all its
+// rules at once per request class (typed / consumer-metadata / nil): `any`
+// bit c = some rule matches every version, vm[c] bit v = some rule matches
+// version v.  Rules the bits cannot express (a clientID that must be compared,
+// a version outside 0..63) are kept as exception rules, evaluated one by one.
+// Topic rules are reached per (group, topic) through a hash table.
 struct KafkaRuleDev {
   unsigned long long keys;  // bit k: apiKey k allowed (k < 64)
-  uint32_t flags;           // bit0: apiKey wildcard, bit1: version wildcard, bit2: has clientID
+  uint32_t flags;           // kKf* bits
   int32_t version;
   uint32_t client_id;
   uint32_t pad;
 };
-constexpr uint32_t kKfKeyWild = 1, kKfVerWild = 2, kKfHasClient = 4;
-struct KafkaGroupDev {
-  uint32_t wild_off, wild_cnt;    // topic-less rules (KafkaRuleDev index range)
-  uint32_t tr_off, tr_cnt;        // topic rules, sorted by topic id
-  uint32_t any_rules;             // 1 if the group has any Kafka rule (else deny)
-  uint32_t pad0, pad1, pad2;
+constexpr uint32_t kKfKeyWild = 1, kKfVerWild = 2, kKfHasClient = 4, kKfHasTopic = 8;
+constexpr uint32_t kKfBuckets = 65;                // apiKey 0..63 + "other"
+constexpr uint32_t kKfSumsPerGroup = 2 * kKfBuckets;
+struct KafkaSumDev {
+  unsigned long long vm[3];  // class 0 typed, 1 consumer-metadata, 2 nil: versions 0..63
+  uint32_t any;              // bit c: class c matches any version
+  uint32_t x_off, x_cnt;     // exception rules (KafkaRuleDev index range)
+  uint32_t pad;
+};
+struct KafkaTopicDev {
+  unsigned long long key;    // group<<32 | topic id; ~0 = empty
+  uint32_t off, cnt;         // KafkaRuleDev index range (rules with this Topic)
 };
 struct KafkaDev {
+  const KafkaSumDev* sums;        // [group * kKfSumsPerGroup + ctx * kKfBuckets + bucket]
   const KafkaRuleDev* rules;
-  const uint32_t* topic_of;       // topic id per rule in the tr range (sorted)
-  const KafkaGroupDev* groups;
+  const KafkaTopicDev* thash;
+  uint32_t thash_mask;
   // (redirect, identity) → group: key = redirect<<32 | identity
   const unsigned long long* ghash_keys;
   const uint32_t* ghash_vals;

@@ -10,7 +10,9 @@
 // MatchesRule is order-independent: it returns true iff some rule with an
 // empty Topic (or any rule, when the request has no topics) matches, or
 // every distinct request topic is the Topic of some matching rule.  The
-// device evaluation computes exactly that.
+// device evaluation computes exactly that, from per-group decision summaries
+// (dev_types.h KafkaSumDev): the topic-less half of the rule set becomes a few
+// bit tests per request instead of a loop over every rule of the group.
 #include "kafka.h"
 
 #include <algorithm>
@@ -111,6 +113,110 @@ RuleSpec sanitize(const Json& r) {
   return s;
 }
 
+// isTopicAPIKey, pkg/kafka/policy.go:27-52
+inline bool is_topic_api_key(int k) {
+  switch (k) {
+    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 8: case 9:
+    case 19: case 20: case 21: case 23: case 24: case 27: case 28: case 34: case 35: case 37:
+      return true;
+  }
+  return false;
+}
+
+inline bool rule_matches(const KafkaRuleDev& r, const cg_kafka_request& q) {
+  // ruleMatches, pkg/kafka/policy.go:144-195
+  const bool has_topic = r.flags & kKfHasTopic;
+  if (!(r.flags & kKfKeyWild)) {
+    if (q.api_key < 0 || q.api_key >= 64 || !((r.keys >> q.api_key) & 1)) return false;
+  }
+  if (!(r.flags & kKfVerWild) && r.version != q.api_version) return false;
+  bool has_client = r.flags & kKfHasClient;
+  if (!has_topic && !has_client) return true;
+  switch (q.kind) {
+    case CG_KAFKA_K_TYPED: return !has_client || r.client_id == q.client_id;
+    case CG_KAFKA_K_CONSUMER_METADATA: return true;
+    default: return !(has_topic && is_topic_api_key(q.api_key));  // matchNonTopicRequests
+  }
+}
+
+uint32_t intern(std::unordered_map<std::string, uint32_t>& m, const std::string& s) {
+  auto it = m.find(s);
+  if (it != m.end()) return it->second;
+  uint32_t id = (uint32_t)m.size();
+  m.emplace(s, id);
+  return id;
+}
+
+// Fold one rule into the summaries of one context (65 buckets).  `xs` collects
+// the exception rules per bucket.  Per request class the rule's ruleMatches
+// outcome (given key and version match) is fixed, except for a typed request
+// against a clientID rule, which needs the comparison.
+void fold_rule(KafkaSumDev* sums, std::vector<std::vector<KafkaRuleDev>>& xs, const KafkaRuleDev& d) {
+  const bool has_topic = d.flags & kKfHasTopic, has_client = d.flags & kKfHasClient;
+  for (uint32_t b = 0; b < kKfBuckets; ++b) {
+    if (!(d.flags & kKfKeyWild) && (b == 64 || !((d.keys >> b) & 1))) continue;
+    bool exception = false;
+    for (int c = 0; c < 3; ++c) {
+      // class 0 typed, 1 consumer-metadata, 2 nil (ruleMatches switch)
+      bool match = true, needs_client = false;
+      if (has_topic || has_client) {
+        if (c == 0) needs_client = has_client;
+        else if (c == 2) match = !(has_topic && b < 64 && is_topic_api_key((int)b));
+      }
+      if (!match) continue;
+      if (needs_client) {
+        exception = true;
+      } else if (d.flags & kKfVerWild) {
+        sums[b].any |= 1u << c;
+      } else if (d.version >= 0 && d.version < 64) {
+        sums[b].vm[c] |= 1ULL << d.version;
+      } else {
+        exception = true;
+      }
+    }
+    if (exception) xs[b].push_back(d);
+  }
+}
+
+KafkaRuleDev dev_rule(KafkaSnapshot& S, const RuleSpec& r) {
+  KafkaRuleDev d{};
+  d.keys = r.keys;
+  d.flags = (r.key_wild ? kKfKeyWild : 0) | (r.ver_wild ? kKfVerWild : 0) | (!r.client.empty() ? kKfHasClient : 0) |
+            (!r.topic.empty() ? kKfHasTopic : 0);
+  d.version = r.version;
+  d.client_id = r.client.empty() ? 0 : intern(S.client_ids, r.client);
+  return d;
+}
+
+// One identity group's rules (GetRelevantRules result) → its 130 summaries,
+// exception rules and (group, topic) rule lists.
+void add_group(KafkaSnapshot& S, uint32_t gid, const std::vector<RuleSpec>& rs,
+               std::vector<KafkaTopicDev>& tentries) {
+  S.sums.resize((size_t)(gid + 1) * kKfSumsPerGroup, KafkaSumDev{});
+  KafkaSumDev* sums = S.sums.data() + (size_t)gid * kKfSumsPerGroup;
+  std::vector<std::vector<KafkaRuleDev>> xs[2] = {std::vector<std::vector<KafkaRuleDev>>(kKfBuckets),
+                                                  std::vector<std::vector<KafkaRuleDev>>(kKfBuckets)};
+  std::map<uint32_t, std::vector<KafkaRuleDev>> by_topic;
+  for (const auto& r : rs) {
+    KafkaRuleDev d = dev_rule(S, r);
+    // request without topics: every rule is tried (MatchesRule, policy.go:211)
+    fold_rule(sums + kKfBuckets, xs[1], d);
+    if (r.topic.empty()) fold_rule(sums, xs[0], d);
+    else by_topic[intern(S.topic_ids, r.topic)].push_back(d);
+  }
+  for (int ctx = 0; ctx < 2; ++ctx)
+    for (uint32_t b = 0; b < kKfBuckets; ++b) {
+      KafkaSumDev& su = sums[ctx * kKfBuckets + b];
+      su.x_off = (uint32_t)S.rules.size();
+      su.x_cnt = (uint32_t)xs[ctx][b].size();
+      S.rules.insert(S.rules.end(), xs[ctx][b].begin(), xs[ctx][b].end());
+    }
+  for (auto& [t, v] : by_topic) {
+    tentries.push_back(KafkaTopicDev{((uint64_t)gid << 32) | t, (uint32_t)S.rules.size(), (uint32_t)v.size()});
+    S.rules.insert(S.rules.end(), v.begin(), v.end());
+  }
+}
+
 }  // namespace
 
 std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
@@ -118,15 +224,9 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
   if (root.type != Json::ARR) fail(CG_POLICY_REJECTED, "expected a list of Kafka redirects");
   auto snap = std::make_shared<KafkaSnapshot>();
   KafkaSnapshot& S = *snap;
-  auto intern = [](std::unordered_map<std::string, uint32_t>& m, const std::string& s) -> uint32_t {
-    auto it = m.find(s);
-    if (it != m.end()) return it->second;
-    uint32_t id = (uint32_t)m.size();
-    m.emplace(s, id);
-    return id;
-  };
   std::map<std::vector<int>, uint32_t> group_ids;  // selector set → group
   std::vector<std::pair<uint64_t, uint32_t>> gh;
+  std::vector<KafkaTopicDev> tentries;
   uint32_t ri = 0;
   for (const Json& red : root.arr) {
     const Json* nm = red.get("name");
@@ -168,38 +268,11 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
       // group ids are global; the selector indices are made global by
       // prefixing the redirect index
       if (it != group_ids.end()) return it->second;
-      KafkaGroupDev g{};
-      std::vector<RuleSpec> wr, tr;
+      std::vector<RuleSpec> rs;
       for (size_t i = 1; i < selset.size(); ++i)
-        for (const auto& r : sels[selset[i]].rules) (r.topic.empty() ? wr : tr).push_back(r);
-      g.any_rules = (wr.size() + tr.size()) > 0;
-      auto dev_rule = [&](const RuleSpec& r) {
-        KafkaRuleDev d{};
-        d.keys = r.keys;
-        d.flags = (r.key_wild ? kKfKeyWild : 0) | (r.ver_wild ? kKfVerWild : 0) |
-                  (!r.client.empty() ? kKfHasClient : 0);
-        d.version = r.version;
-        d.client_id = r.client.empty() ? 0 : intern(S.client_ids, r.client);
-        return d;
-      };
-      g.wild_off = (uint32_t)S.rules.size();
-      for (const auto& r : wr) {
-        S.rules.push_back(dev_rule(r));
-        S.topic_of.push_back(0xFFFFFFFFu);
-      }
-      g.wild_cnt = (uint32_t)wr.size();
-      std::vector<std::pair<uint32_t, KafkaRuleDev>> trd;
-      for (const auto& r : tr) trd.push_back({intern(S.topic_ids, r.topic), dev_rule(r)});
-      std::stable_sort(trd.begin(), trd.end(),
-                       [](const auto& a, const auto& b) { return a.first < b.first; });
-      g.tr_off = (uint32_t)S.rules.size();
-      for (auto& [t, d] : trd) {
-        S.rules.push_back(d);
-        S.topic_of.push_back(t);
-      }
-      g.tr_cnt = (uint32_t)trd.size();
-      uint32_t gid = (uint32_t)S.groups.size();
-      S.groups.push_back(g);
+        for (const auto& r : sels[selset[i]].rules) rs.push_back(r);
+      const uint32_t gid = S.ngroups++;
+      add_group(S, gid, rs, tentries);
       group_ids[selset] = gid;
       return gid;
     };
@@ -232,40 +305,25 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
     S.ghash_keys[h] = k;
     S.ghash_vals[h] = v;
   }
-  if (S.rules.empty()) {
-    S.rules.push_back(KafkaRuleDev{});
-    S.topic_of.push_back(0xFFFFFFFFu);
+  cap = next_pow2(std::max<size_t>(tentries.size() * 2, 16));
+  S.thash.assign(cap, KafkaTopicDev{~0ULL, 0, 0});
+  S.thash_mask = cap - 1;
+  for (const auto& t : tentries) {
+    uint32_t h = hash64to32(t.key) & S.thash_mask;
+    while (S.thash[h].key != ~0ULL) h = (h + 1) & S.thash_mask;
+    S.thash[h] = t;
   }
-  if (S.groups.empty()) S.groups.push_back(KafkaGroupDev{});
+  if (S.rules.empty()) S.rules.push_back(KafkaRuleDev{});
+  if (S.ngroups == 0) {
+    S.sums.assign(kKfSumsPerGroup, KafkaSumDev{});
+    S.ngroups = 1;
+  }
   if (S.dflt_group.empty()) S.dflt_group.push_back(0);
   return snap;
 }
 
-// isTopicAPIKey, pkg/kafka/policy.go:27-52
-static inline bool is_topic_api_key(int k) {
-  switch (k) {
-    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 8: case 9:
-    case 19: case 20: case 21: case 23: case 24: case 27: case 28: case 34: case 35: case 37:
-      return true;
-  }
-  return false;
-}
-
-static inline bool rule_matches(const KafkaRuleDev& r, bool has_topic, const cg_kafka_request& q) {
-  // ruleMatches, pkg/kafka/policy.go:144-195
-  if (!(r.flags & kKfKeyWild)) {
-    if (q.api_key < 0 || q.api_key >= 64 || !((r.keys >> q.api_key) & 1)) return false;
-  }
-  if (!(r.flags & kKfVerWild) && r.version != q.api_version) return false;
-  bool has_client = r.flags & kKfHasClient;
-  if (!has_topic && !has_client) return true;
-  switch (q.kind) {
-    case CG_KAFKA_K_TYPED: return !has_client || r.client_id == q.client_id;
-    case CG_KAFKA_K_CONSUMER_METADATA: return true;
-    default: return !(has_topic && is_topic_api_key(q.api_key));  // matchNonTopicRequests
-  }
-}
-
+// Mirrors kafka_kernel (kernels.hip) step for step, so the compiler can be
+// checked against the oracle without a GPU.
 uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const uint32_t* arena,
                         size_t arena_len) {
   if (q.policy >= s.dflt_group.size()) return 0;
@@ -281,26 +339,32 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
       h = (h + 1) & s.ghash_mask;
     }
   }
-  const KafkaGroupDev& G = s.groups[g];
-  if (!G.any_rules) return 0;  // "No Kafka rules matching identity, rejecting"
-  for (uint32_t i = 0; i < G.wild_cnt; ++i)
-    if (rule_matches(s.rules[G.wild_off + i], false, q)) return 1;
+  const uint32_t nt = q.n_topics;
+  const uint32_t b = (q.api_key >= 0 && q.api_key < 64) ? (uint32_t)q.api_key : 64;
+  const KafkaSumDev& su = s.sums[(size_t)g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b];
+  const int c = q.kind == CG_KAFKA_K_TYPED ? 0 : q.kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
+  if ((su.any >> c) & 1) return 1;
+  if (q.api_version >= 0 && q.api_version < 64 && ((su.vm[c] >> q.api_version) & 1)) return 1;
+  for (uint32_t i = 0; i < su.x_cnt; ++i)
+    if (rule_matches(s.rules[su.x_off + i], q)) return 1;
+  if (nt == 0) return 0;
   const uint32_t* topics = q.topic_ids;
-  uint32_t nt = q.n_topics;
   if (nt > CG_KAFKA_MAX_TOPICS) {
     if ((size_t)q.topic_ids[0] + nt > arena_len) return 0;
     topics = arena + q.topic_ids[0];
   }
-  if (nt == 0) {
-    for (uint32_t i = 0; i < G.tr_cnt; ++i)
-      if (rule_matches(s.rules[G.tr_off + i], true, q)) return 1;
-    return 0;
-  }
   for (uint32_t t = 0; t < nt; ++t) {
-    uint32_t tid = topics[t];
+    const uint64_t key = ((uint64_t)g << 32) | topics[t];
+    uint32_t h = hash64to32(key) & s.thash_mask;
     bool cov = false;
-    for (uint32_t i = 0; i < G.tr_cnt && !cov; ++i)
-      if (s.topic_of[G.tr_off + i] == tid && rule_matches(s.rules[G.tr_off + i], true, q)) cov = true;
+    while (s.thash[h].key != ~0ULL) {
+      if (s.thash[h].key == key) {
+        for (uint32_t i = 0; i < s.thash[h].cnt && !cov; ++i)
+          cov = rule_matches(s.rules[s.thash[h].off + i], q);
+        break;
+      }
+      h = (h + 1) & s.thash_mask;
+    }
     if (!cov) return 0;
   }
   return 1;
@@ -310,16 +374,17 @@ void KafkaSnapshot::upload(Engine& e) {
   if (!e.has_gpu()) return;
   e.set_device();
   d_rules.upload_vec(rules);
-  d_topic_of.upload_vec(topic_of);
-  d_groups.upload_vec(groups);
+  d_sums.upload_vec(sums);
+  d_thash.upload_vec(thash);
   d_ghk.upload_vec(ghash_keys);
   d_ghv.upload_vec(ghash_vals);
   d_dflt.upload_vec(dflt_group);
   d_counters.alloc(std::max<size_t>(dflt_group.size(), 1) * 2 * sizeof(uint64_t));
   d_counters.zero();
+  dev.sums = d_sums.as<KafkaSumDev>();
   dev.rules = d_rules.as<KafkaRuleDev>();
-  dev.topic_of = d_topic_of.as<uint32_t>();
-  dev.groups = d_groups.as<KafkaGroupDev>();
+  dev.thash = d_thash.as<KafkaTopicDev>();
+  dev.thash_mask = thash_mask;
   dev.ghash_keys = d_ghk.as<unsigned long long>();
   dev.ghash_vals = d_ghv.as<uint32_t>();
   dev.ghash_mask = ghash_mask;

@@ -15,15 +15,17 @@ namespace cg {
 struct KafkaSnapshot {
   std::map<std::string, uint32_t> redirect_index;
   std::unordered_map<std::string, uint32_t> topic_ids, client_ids;
-  std::vector<KafkaRuleDev> rules;
-  std::vector<uint32_t> topic_of;
-  std::vector<KafkaGroupDev> groups;
+  std::vector<KafkaRuleDev> rules;   // exception rules and topic rules
+  std::vector<KafkaSumDev> sums;     // kKfSumsPerGroup per group
+  std::vector<KafkaTopicDev> thash;
+  uint32_t thash_mask = 0;
+  uint32_t ngroups = 0;
   std::vector<uint64_t> ghash_keys;
   std::vector<uint32_t> ghash_vals;
   uint32_t ghash_mask = 0;
   std::vector<uint32_t> dflt_group;
 
-  DevMem d_rules, d_topic_of, d_groups, d_ghk, d_ghv, d_dflt, d_counters;
+  DevMem d_rules, d_sums, d_thash, d_ghk, d_ghv, d_dflt, d_counters;
   KafkaDev dev{};
   void upload(Engine& e);
 };

@@ -237,25 +237,39 @@ __device__ __forceinline__ bool kf_is_topic_key(int k) {
   return k >= 0 && k < 64 && ((m >> k) & 1);
 }
 
-__device__ __forceinline__ bool kf_rule_matches(const KafkaRuleDev& r, bool has_topic, int key, int ver,
-                                                uint32_t kind, uint32_t client) {
+__device__ __forceinline__ bool kf_rule_matches(const KafkaRuleDev& r, int key, int ver, uint32_t kind,
+                                                uint32_t client) {
   if (!(r.flags & kKfKeyWild)) {
     if (key < 0 || key >= 64 || !((r.keys >> key) & 1)) return false;
   }
   if (!(r.flags & kKfVerWild) && r.version != ver) return false;
   const bool has_client = r.flags & kKfHasClient;
+  const bool has_topic = r.flags & kKfHasTopic;
   if (!has_topic && !has_client) return true;
   if (kind == CG_KAFKA_K_TYPED) return !has_client || r.client_id == client;
   if (kind == CG_KAFKA_K_CONSUMER_METADATA) return true;
   return !(has_topic && kf_is_topic_key(key));
 }
 
+__device__ __forceinline__ void kf_flush(unsigned long long* counters, uint32_t red, uint32_t allow,
+                                         uint32_t deny) {
+  if (allow) atomicAdd(&counters[red * 2], (unsigned long long)allow);
+  if (deny) atomicAdd(&counters[red * 2 + 1], (unsigned long long)deny);
+}
+
+// One lane per request (64-B records, four 16-B loads).  The group lookup is
+// one hash probe; the summary for (group, topics?, apiKey) settles most
+// requests with two bit tests; the rest walk exception rules and, per topic,
+// the (group, topic) rule list.  Counters accumulate per lane while the
+// redirect stays the same and are wave-reduced at the end.
 __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __restrict__ reqs, size_t n,
                                                     const uint32_t* __restrict__ arena, uint8_t* __restrict__ out) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
+  uint32_t cred = ~0u, callow = 0, cdeny = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint4* r = reqs + i * 4;
     const uint4 h = r[0];
+    const uint4 t0 = r[1], t1 = r[2], t2 = r[3];
     const int key = (int16_t)(h.x & 0xFFFF);
     const int ver = (int16_t)(h.x >> 16);
     const uint32_t kind = h.y & 0xFF;
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
         const unsigned long long k = ((unsigned long long)red << 32) | remote;
         uint32_t hh = hash64to32(k) & T.ghash_mask;
         for (uint32_t probe = 0; probe <= T.ghash_mask; ++probe) {
-          unsigned long long kk = T.ghash_keys[hh];
+          const unsigned long long kk = T.ghash_keys[hh];
           if (kk == k) {
             g = T.ghash_vals[hh];
             break;
@@ -279,42 +293,58 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
           hh = (hh + 1) & T.ghash_mask;
         }
       }
-      const KafkaGroupDev G = T.groups[g];
-      if (G.any_rules) {
-        for (uint32_t j = 0; j < G.wild_cnt && !v; ++j)
-          if (kf_rule_matches(T.rules[G.wild_off + j], false, key, ver, kind, client)) v = 1;
-        if (!v) {
-          if (nt == 0) {
-            for (uint32_t j = 0; j < G.tr_cnt && !v; ++j)
-              if (kf_rule_matches(T.rules[G.tr_off + j], true, key, ver, kind, client)) v = 1;
-          } else {
-            uint32_t tids[CG_KAFKA_MAX_TOPICS];
-            const uint4 t0 = r[1], t1 = r[2], t2 = r[3];
-            tids[0] = t0.x; tids[1] = t0.y; tids[2] = t0.z; tids[3] = t0.w;
-            tids[4] = t1.x; tids[5] = t1.y; tids[6] = t1.z; tids[7] = t1.w;
-            tids[8] = t2.x; tids[9] = t2.y; tids[10] = t2.z; tids[11] = t2.w;
-            const bool ovf = nt > CG_KAFKA_MAX_TOPICS;
-            bool all = true;
-            for (uint32_t t = 0; t < nt && all; ++t) {
-              const uint32_t tid = ovf ? arena[tids[0] + t] : tids[t];
-              // rules of this group sorted by topic id: binary search the first
-              uint32_t lo = 0, hi = G.tr_cnt;
-              while (lo < hi) {
-                uint32_t m = (lo + hi) >> 1;
-                if (T.topic_of[G.tr_off + m] < tid) lo = m + 1; else hi = m;
-              }
-              bool cov = false;
-              for (uint32_t j = lo; j < G.tr_cnt && T.topic_of[G.tr_off + j] == tid && !cov; ++j)
-                if (kf_rule_matches(T.rules[G.tr_off + j], true, key, ver, kind, client)) cov = true;
-              all = cov;
+      const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
+      const KafkaSumDev* su = T.sums + (size_t)g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
+      const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
+      const uint4 tail = *reinterpret_cast<const uint4*>(&su->any);
+      const unsigned long long vm = su->vm[c];
+      v = ((tail.x >> c) & 1) | ((ver >= 0 && ver < 64) ? (uint32_t)((vm >> ver) & 1) : 0u);
+      for (uint32_t j = 0; j < tail.z && !v; ++j)
+        if (kf_rule_matches(T.rules[tail.y + j], key, ver, kind, client)) v = 1;
+      if (!v && nt != 0) {
+        const uint32_t tids[CG_KAFKA_MAX_TOPICS] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y,
+                                                    t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+        const bool ovf = nt > CG_KAFKA_MAX_TOPICS;
+        bool all = true;
+        for (uint32_t t = 0; t < nt && all; ++t) {
+          const uint32_t tid = ovf ? arena[tids[0] + t] : tids[t];
+          const unsigned long long k = ((unsigned long long)g << 32) | tid;
+          uint32_t hh = hash64to32(k) & T.thash_mask;
+          bool cov = false;
+          for (uint32_t probe = 0; probe <= T.thash_mask; ++probe) {
+            const KafkaTopicDev e = T.thash[hh];
+            if (e.key == k) {
+              for (uint32_t j = 0; j < e.cnt && !cov; ++j)
+                cov = kf_rule_matches(T.rules[e.off + j], key, ver, kind, client);
+              break;
             }
-            v = all ? 1 : 0;
+            if (e.key == ~0ULL) break;
+            hh = (hh + 1) & T.thash_mask;
           }
+          all = cov;
         }
+        v = all ? 1 : 0;
       }
-      atomicAdd(&T.counters[red * 2 + (v ? 0 : 1)], 1ULL);
+      if (red != cred) {
+        if (cred != ~0u) kf_flush(T.counters, cred, callow, cdeny);
+        cred = red;
+        callow = cdeny = 0;
+      }
+      callow += v;
+      cdeny += v ^ 1;
     }
     out[i] = (uint8_t)v;
+  }
+  // the common case: every lane of the wave counted for the same redirect
+  const uint32_t first = __builtin_amdgcn_readfirstlane(cred);
+  if (__all(cred == first)) {
+    for (int o = 32; o > 0; o >>= 1) {
+      callow += __shfl_down(callow, o, kWave);
+      cdeny += __shfl_down(cdeny, o, kWave);
+    }
+    if ((threadIdx.x & 63) == 0 && first != ~0u) kf_flush(T.counters, first, callow, cdeny);
+  } else if (cred != ~0u) {
+    kf_flush(T.counters, cred, callow, cdeny);
   }
 }
 

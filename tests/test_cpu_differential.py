@@ -204,6 +204,56 @@ def test_kafka_many_topics_overflow(host):
     assert np.array_equal(host.kafka_eval_host_diag(reqs, arena), oracle.KafkaOracle(pols).eval(**rq))
 
 
+def _kafka_edge_policy(rng):
+    from cilium_amd.policy import KAFKA_API_KEY_MAP, PortRuleKafka
+    keys = list(KAFKA_API_KEY_MAP)
+    topics = [f"t{i}" for i in range(6)]
+    clients = ["c0", "c1", "c2"]
+
+    def rule():
+        r = PortRuleKafka()
+        pick = rng.random()
+        if pick < 0.3:
+            r.APIKey = rng.choice(keys)
+        elif pick < 0.5:
+            r.Role = rng.choice(["produce", "consume"])
+        # else apiKey wildcard
+        if rng.random() < 0.4:
+            r.APIVersion = str(rng.choice([0, 1, 5, 63, 64, 100, -1, 32767, -32768]))
+        if rng.random() < 0.3:
+            r.ClientID = rng.choice(clients)
+        if rng.random() < 0.4:
+            r.Topic = rng.choice(topics)
+        return r
+
+    sels = [{"identities": [7, 8], "rules": [rule() for _ in range(rng.randint(0, 6))]},
+            {"identities": [8, 9], "rules": [rule() for _ in range(rng.randint(1, 6))]},
+            {"identities": [10], "rules": []},
+            {"identities": None, "rules": [rule() for _ in range(rng.randint(0, 2))]}]
+    return [{"name": "r0", "selectors": sels}, {"name": "r1", "selectors": sels[1:3]}], topics, clients
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_kafka_edge_rules(host, seed):
+    """Versions outside 0..63 and negative, apiKey-wildcard rules with topics
+    and clientIDs, unknown apiKeys (negative, > 63) and request kinds: the
+    summary bits, exception rules and topic lists against the oracle."""
+    rng = random.Random(seed)
+    pols, topics, clients = _kafka_edge_policy(rng)
+    host.update_kafka_policy(pols)
+    n = 3000
+    rq = dict(redirect=[rng.choice([0, 0, 1, 2]) for _ in range(n)],
+              remote=[rng.choice([0, 7, 8, 9, 10, 11]) for _ in range(n)],
+              api_key=[rng.choice([0, 1, 3, 10, 12, 18, 37, -1, 40, 63, 64, 1000]) for _ in range(n)],
+              api_version=[rng.choice([0, 1, 5, 63, 64, 100, -1, 32767, -32768]) for _ in range(n)],
+              kind=[rng.choice([0, 1, 2, 3]) for _ in range(n)],
+              client_id=[rng.choice(clients + ["zz"]).encode() for _ in range(n)],
+              topics=[[rng.choice(topics + ["nope"]).encode() for _ in range(rng.choice([0, 0, 1, 2, 3]))]
+                      for _ in range(n)])
+    reqs, arena = host.pack_kafka(**rq)
+    assert np.array_equal(host.kafka_eval_host_diag(reqs, arena), oracle.KafkaOracle(pols).eval(**rq))
+
+
 # ---------------------------------------------------------------- L4, LPM ---
 def test_l4_table_builder(host):
     keys, ports = synth.l4_table(n_entries=16384)

@@ -191,3 +191,30 @@ def test_kafka_parity(gpu):
     exp = oracle.KafkaOracle(pols).eval(**rq, nthreads=8)
     assert np.array_equal(got, exp)
     assert 0.05 < got.mean() < 0.99
+    # per-redirect counters: one redirect, every request counted once
+    c = gpu.read_counters(1)
+    assert int(c[0]) == int(got.sum()) and int(c[1]) == len(got) - int(got.sum())
+
+
+def test_kafka_edge_parity(gpu):
+    """Summary bits, exception rules, topic lists and unknown keys/kinds on
+    the device, against the oracle (cases of test_kafka_edge_rules)."""
+    import random
+
+    from test_cpu_differential import _kafka_edge_policy
+    for seed in range(6):
+        rng = random.Random(seed)
+        pols, topics, clients = _kafka_edge_policy(rng)
+        gpu.update_kafka_policy(pols)
+        n = 5000
+        rq = dict(redirect=[rng.choice([0, 0, 1, 2]) for _ in range(n)],
+                  remote=[rng.choice([0, 7, 8, 9, 10, 11]) for _ in range(n)],
+                  api_key=[rng.choice([0, 1, 3, 10, 12, 18, 37, -1, 40, 63, 64, 1000]) for _ in range(n)],
+                  api_version=[rng.choice([0, 1, 5, 63, 64, 100, -1, 32767, -32768]) for _ in range(n)],
+                  kind=[rng.choice([0, 1, 2, 3]) for _ in range(n)],
+                  client_id=[rng.choice(clients + ["zz"]).encode() for _ in range(n)],
+                  topics=[[rng.choice(topics + ["nope"]).encode() for _ in range(rng.choice([0, 0, 1, 2, 3, 14]))]
+                          for _ in range(n)])
+        reqs, arena = gpu.pack_kafka(**rq)
+        got = gpu.kafka_verdicts(reqs, arena)
+        assert np.array_equal(got, oracle.KafkaOracle(pols).eval(**rq)), f"seed {seed}"
