@@ -816,12 +816,14 @@ int cg_diag_http_eval_host(uint64_t h, const void* batch, size_t nslots, const u
   });
 }
 
-// Cuckoo lookup exactly as l4_kernel does it.
+// Cuckoo lookup as the L4 kernels do it: fingerprint screen, then the slot.
 static bool l4_lookup_host(const PolicyMapState& m, uint64_t key, uint32_t* val) {
-  for (uint64_t h : {l4_hash1(key), l4_hash2(key)}) {
-    const L4Slot* b = m.slots.data() + (size_t)((uint32_t)h & m.bucket_mask) * 4;
+  uint32_t b1, b2, fp;
+  l4_place(key, m.bucket_mask, &b1, &b2, &fp);
+  for (uint32_t bk : {b1, b2}) {
+    const L4Slot* b = m.slots.data() + (size_t)bk * 4;
     for (int s = 0; s < 4; ++s)
-      if (b[s].key == key) {
+      if (((m.fp[bk] >> (8 * s)) & 0xFF) == fp && b[s].key == key) {
         *val = b[s].val;
         return true;
       }

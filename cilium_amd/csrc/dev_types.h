@@ -26,6 +26,7 @@ struct L4Slot {
 };
 struct L4Dev {
   const L4Slot* slots;   // nbuckets * 4
+  const uint32_t* fp;    // nbuckets: the 4 slots' 8-bit fingerprints (0 = empty)
   uint32_t bucket_mask;  // nbuckets - 1
   uint32_t max_entries;  // counter ids < max_entries
   unsigned long long* counters;  // [id*2] packets, [id*2+1] bytes
@@ -39,6 +40,8 @@ CG_HD inline uint64_t l4_hash1(uint64_t k) {
   k ^= k >> 33;
   return k;
 }
+CG_HD inline uint32_t l4_alt(uint32_t fp) { return (fp * 0x5bd1e995u) | 1u; }
+
 CG_HD inline uint64_t l4_hash2(uint64_t k) {
   k += 0x9e3779b97f4a7c15ULL;
   k ^= k >> 30;
@@ -47,6 +50,18 @@ CG_HD inline uint64_t l4_hash2(uint64_t k) {
   k *= 0x94d049bb133111ebULL;
   k ^= k >> 31;
   return k;
+}
+
+// Partial-key cuckoo placement: one hash gives the first bucket and an 8-bit
+// fingerprint (1..255); the second bucket is the first XOR a function of the
+// fingerprint, so either bucket and the fingerprint recover the other.
+CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* b2, uint32_t* fp) {
+  const uint64_t h = l4_hash1(key);
+  uint32_t f = (uint32_t)(h >> 56);
+  f = f ? f : 1u;
+  *fp = f;
+  *b1 = (uint32_t)h & mask;
+  *b2 = *b1 ^ (l4_alt(f) & mask);
 }
 
 // ----------------------------------------------------------------- LPM ----
@@ -204,9 +219,21 @@ constexpr uint32_t kKfBuckets = 65;                // apiKey 0..63 + "other"
 constexpr uint32_t kKfSumsPerGroup = 2 * kKfBuckets;
 struct KafkaSumDev {
   unsigned long long vm[3];  // class 0 typed, 1 consumer-metadata, 2 nil: versions 0..63
-  uint32_t any;              // bit c: class c matches any version
+  uint32_t any;              // bit c: class c matches any version; bit 3: has clientID entries
   uint32_t x_off, x_cnt;     // exception rules (KafkaRuleDev index range)
   uint32_t pad;
+};
+constexpr uint32_t kKfSumHasClients = 8;
+// Typed requests against clientID rules: per (summary, clientID) the versions
+// those rules accept, so the comparison is one hash probe.
+struct KafkaClientDev {
+  unsigned long long key;    // summary index<<32 | client id; ~0 = empty
+  unsigned long long vm;     // versions 0..63
+  uint32_t any, pad[3];      // any: some rule accepts every version
+};
+struct KafkaGroupSlot {
+  unsigned long long key;    // redirect<<32 | identity; ~0 = empty
+  uint32_t group, pad;
 };
 struct KafkaTopicDev {
   unsigned long long key;    // group<<32 | topic id; ~0 = empty
@@ -217,9 +244,9 @@ struct KafkaDev {
   const KafkaRuleDev* rules;
   const KafkaTopicDev* thash;
   uint32_t thash_mask;
-  // (redirect, identity) → group: key = redirect<<32 | identity
-  const unsigned long long* ghash_keys;
-  const uint32_t* ghash_vals;
+  const KafkaClientDev* chash;
+  uint32_t chash_mask;
+  const KafkaGroupSlot* ghash;    // (redirect, identity) → group
   uint32_t ghash_mask;
   const uint32_t* dflt_group;     // per redirect: group for unlisted identities
   uint32_t nredirects;

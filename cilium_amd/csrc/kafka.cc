@@ -151,7 +151,10 @@ uint32_t intern(std::unordered_map<std::string, uint32_t>& m, const std::string&
 // the exception rules per bucket.  Per request class the rule's ruleMatches
 // outcome (given key and version match) is fixed, except for a typed request
 // against a clientID rule, which needs the comparison.
-void fold_rule(KafkaSumDev* sums, std::vector<std::vector<KafkaRuleDev>>& xs, const KafkaRuleDev& d) {
+using ClientMap = std::map<uint64_t, KafkaClientDev>;
+
+void fold_rule(KafkaSumDev* sums, uint32_t sum_base, std::vector<std::vector<KafkaRuleDev>>& xs, ClientMap& cm,
+               const KafkaRuleDev& d) {
   const bool has_topic = d.flags & kKfHasTopic, has_client = d.flags & kKfHasClient;
   for (uint32_t b = 0; b < kKfBuckets; ++b) {
     if (!(d.flags & kKfKeyWild) && (b == 64 || !((d.keys >> b) & 1))) continue;
@@ -165,7 +168,15 @@ void fold_rule(KafkaSumDev* sums, std::vector<std::vector<KafkaRuleDev>>& xs, co
       }
       if (!match) continue;
       if (needs_client) {
-        exception = true;
+        if (!(d.flags & kKfVerWild) && (d.version < 0 || d.version >= 64)) {
+          exception = true;
+          continue;
+        }
+        const uint64_t key = ((uint64_t)(sum_base + b) << 32) | d.client_id;
+        KafkaClientDev& e = cm.emplace(key, KafkaClientDev{key, 0, 0, {0, 0, 0}}).first->second;
+        if (d.flags & kKfVerWild) e.any = 1;
+        else e.vm |= 1ULL << d.version;
+        sums[b].any |= kKfSumHasClients;
       } else if (d.flags & kKfVerWild) {
         sums[b].any |= 1u << c;
       } else if (d.version >= 0 && d.version < 64) {
@@ -191,7 +202,7 @@ KafkaRuleDev dev_rule(KafkaSnapshot& S, const RuleSpec& r) {
 // One identity group's rules (GetRelevantRules result) → its 130 summaries,
 // exception rules and (group, topic) rule lists.
 void add_group(KafkaSnapshot& S, uint32_t gid, const std::vector<RuleSpec>& rs,
-               std::vector<KafkaTopicDev>& tentries) {
+               std::vector<KafkaTopicDev>& tentries, ClientMap& cm) {
   S.sums.resize((size_t)(gid + 1) * kKfSumsPerGroup, KafkaSumDev{});
   KafkaSumDev* sums = S.sums.data() + (size_t)gid * kKfSumsPerGroup;
   std::vector<std::vector<KafkaRuleDev>> xs[2] = {std::vector<std::vector<KafkaRuleDev>>(kKfBuckets),
@@ -200,8 +211,9 @@ void add_group(KafkaSnapshot& S, uint32_t gid, const std::vector<RuleSpec>& rs,
   for (const auto& r : rs) {
     KafkaRuleDev d = dev_rule(S, r);
     // request without topics: every rule is tried (MatchesRule, policy.go:211)
-    fold_rule(sums + kKfBuckets, xs[1], d);
-    if (r.topic.empty()) fold_rule(sums, xs[0], d);
+    const uint32_t base = gid * kKfSumsPerGroup;
+    fold_rule(sums + kKfBuckets, base + kKfBuckets, xs[1], cm, d);
+    if (r.topic.empty()) fold_rule(sums, base, xs[0], cm, d);
     else by_topic[intern(S.topic_ids, r.topic)].push_back(d);
   }
   for (int ctx = 0; ctx < 2; ++ctx)
@@ -227,6 +239,7 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
   std::map<std::vector<int>, uint32_t> group_ids;  // selector set → group
   std::vector<std::pair<uint64_t, uint32_t>> gh;
   std::vector<KafkaTopicDev> tentries;
+  ClientMap cmap;
   uint32_t ri = 0;
   for (const Json& red : root.arr) {
     const Json* nm = red.get("name");
@@ -272,7 +285,7 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
       for (size_t i = 1; i < selset.size(); ++i)
         for (const auto& r : sels[selset[i]].rules) rs.push_back(r);
       const uint32_t gid = S.ngroups++;
-      add_group(S, gid, rs, tentries);
+      add_group(S, gid, rs, tentries, cmap);
       group_ids[selset] = gid;
       return gid;
     };
@@ -296,14 +309,20 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
     ++ri;
   }
   uint32_t cap = next_pow2(std::max<size_t>(gh.size() * 2, 16));
-  S.ghash_keys.assign(cap, ~0ULL);
-  S.ghash_vals.assign(cap, 0);
+  S.ghash.assign(cap, KafkaGroupSlot{~0ULL, 0, 0});
   S.ghash_mask = cap - 1;
   for (auto [k, v] : gh) {
     uint32_t h = hash64to32(k) & S.ghash_mask;
-    while (S.ghash_keys[h] != ~0ULL) h = (h + 1) & S.ghash_mask;
-    S.ghash_keys[h] = k;
-    S.ghash_vals[h] = v;
+    while (S.ghash[h].key != ~0ULL) h = (h + 1) & S.ghash_mask;
+    S.ghash[h] = KafkaGroupSlot{k, v, 0};
+  }
+  cap = next_pow2(std::max<size_t>(cmap.size() * 2, 16));
+  S.chash.assign(cap, KafkaClientDev{~0ULL, 0, 0, {0, 0, 0}});
+  S.chash_mask = cap - 1;
+  for (const auto& [k, e] : cmap) {
+    uint32_t h = hash64to32(k) & S.chash_mask;
+    while (S.chash[h].key != ~0ULL) h = (h + 1) & S.chash_mask;
+    S.chash[h] = e;
   }
   cap = next_pow2(std::max<size_t>(tentries.size() * 2, 16));
   S.thash.assign(cap, KafkaTopicDev{~0ULL, 0, 0});
@@ -331,9 +350,9 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
   if (q.remote != 0) {
     uint64_t key = ((uint64_t)q.policy << 32) | q.remote;
     uint32_t h = hash64to32(key) & s.ghash_mask;
-    while (s.ghash_keys[h] != ~0ULL) {
-      if (s.ghash_keys[h] == key) {
-        g = s.ghash_vals[h];
+    while (s.ghash[h].key != ~0ULL) {
+      if (s.ghash[h].key == key) {
+        g = s.ghash[h].group;
         break;
       }
       h = (h + 1) & s.ghash_mask;
@@ -341,10 +360,23 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
   }
   const uint32_t nt = q.n_topics;
   const uint32_t b = (q.api_key >= 0 && q.api_key < 64) ? (uint32_t)q.api_key : 64;
-  const KafkaSumDev& su = s.sums[(size_t)g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b];
+  const uint32_t si = g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
+  const KafkaSumDev& su = s.sums[si];
   const int c = q.kind == CG_KAFKA_K_TYPED ? 0 : q.kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
+  const bool vin = q.api_version >= 0 && q.api_version < 64;
   if ((su.any >> c) & 1) return 1;
-  if (q.api_version >= 0 && q.api_version < 64 && ((su.vm[c] >> q.api_version) & 1)) return 1;
+  if (vin && ((su.vm[c] >> q.api_version) & 1)) return 1;
+  if (c == 0 && (su.any & kKfSumHasClients)) {
+    const uint64_t key = ((uint64_t)si << 32) | q.client_id;
+    uint32_t h = hash64to32(key) & s.chash_mask;
+    while (s.chash[h].key != ~0ULL) {
+      if (s.chash[h].key == key) {
+        if (s.chash[h].any || (vin && ((s.chash[h].vm >> q.api_version) & 1))) return 1;
+        break;
+      }
+      h = (h + 1) & s.chash_mask;
+    }
+  }
   for (uint32_t i = 0; i < su.x_cnt; ++i)
     if (rule_matches(s.rules[su.x_off + i], q)) return 1;
   if (nt == 0) return 0;
@@ -376,8 +408,8 @@ void KafkaSnapshot::upload(Engine& e) {
   d_rules.upload_vec(rules);
   d_sums.upload_vec(sums);
   d_thash.upload_vec(thash);
-  d_ghk.upload_vec(ghash_keys);
-  d_ghv.upload_vec(ghash_vals);
+  d_chash.upload_vec(chash);
+  d_ghash.upload_vec(ghash);
   d_dflt.upload_vec(dflt_group);
   d_counters.alloc(std::max<size_t>(dflt_group.size(), 1) * 2 * sizeof(uint64_t));
   d_counters.zero();
@@ -385,8 +417,9 @@ void KafkaSnapshot::upload(Engine& e) {
   dev.rules = d_rules.as<KafkaRuleDev>();
   dev.thash = d_thash.as<KafkaTopicDev>();
   dev.thash_mask = thash_mask;
-  dev.ghash_keys = d_ghk.as<unsigned long long>();
-  dev.ghash_vals = d_ghv.as<uint32_t>();
+  dev.chash = d_chash.as<KafkaClientDev>();
+  dev.chash_mask = chash_mask;
+  dev.ghash = d_ghash.as<KafkaGroupSlot>();
   dev.ghash_mask = ghash_mask;
   dev.dflt_group = d_dflt.as<uint32_t>();
   dev.nredirects = (uint32_t)dflt_group.size();

@@ -20,12 +20,13 @@ struct KafkaSnapshot {
   std::vector<KafkaTopicDev> thash;
   uint32_t thash_mask = 0;
   uint32_t ngroups = 0;
-  std::vector<uint64_t> ghash_keys;
-  std::vector<uint32_t> ghash_vals;
+  std::vector<KafkaClientDev> chash;
+  uint32_t chash_mask = 0;
+  std::vector<KafkaGroupSlot> ghash;
   uint32_t ghash_mask = 0;
   std::vector<uint32_t> dflt_group;
 
-  DevMem d_rules, d_sums, d_thash, d_ghk, d_ghv, d_dflt, d_counters;
+  DevMem d_rules, d_sums, d_thash, d_chash, d_ghash, d_dflt, d_counters;
   KafkaDev dev{};
   void upload(Engine& e);
 };

@@ -21,104 +21,167 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap
 // =============================================================== L4 ======
 // __policy_can_access (bpf/lib/policy.h:46-110) per tuple.
 
-__device__ __forceinline__ bool l4_probe_bucket(const L4Slot* slots, uint32_t b, uint64_t key,
-                                                uint32_t* val, uint32_t* slot_out) {
-  const uint4* p = reinterpret_cast<const uint4*>(slots + (size_t)b * 4);
-  bool hit = false;
+// Verdict for one tuple given which lookup hit (1: L4, 2: L3, 3: wildcard
+// identity L4, 0: none) and the slot value {entry id, proxy_port_be << 16}.
+__device__ __forceinline__ int32_t l4_verdict(int which, uint32_t val, uint32_t flags) {
+  if (which == 1 || which == 3) return (int32_t)(val >> 16);  // return policy->proxy_port
+  if (which == 2) return 0;  // TC_ACT_OK: the L3 entry's proxy_port is ignored
+  if (flags & CG_L4_F_CB_POLICY) return 0;
+  return (flags & CG_L4_F_FRAGMENT) ? CG_DROP_FRAG_NOSUPPORT : CG_DROP_POLICY;
+}
+
+// The three policy_key lookups of __policy_can_access in priority order:
+// {id, dport, proto, dir} (skipped for fragments), {id, 0, 0, dir},
+// {0, dport, proto, dir} (skipped for fragments).
+__device__ __forceinline__ void l4_keys(uint32_t w0, uint32_t w1, uint64_t k[3], bool* frag) {
+  const uint32_t flags = w1 >> 24;
+  *frag = flags & CG_L4_F_FRAGMENT;
+  // key.egress = !dir with dir = CT_INGRESS(1) / CT_EGRESS(0)
+  const uint64_t eg = (flags & CG_L4_F_INGRESS) ? 0ULL : (1ULL << 56);
+  const uint64_t pp = ((uint64_t)(w1 & 0xFFFF) << 32) | ((uint64_t)((w1 >> 16) & 0xFF) << 48);
+  k[0] = (uint64_t)w0 | pp | eg;
+  k[1] = (uint64_t)w0 | eg;
+  k[2] = pp | eg;
+}
+
+__device__ __forceinline__ uint32_t fp_match4(uint32_t word, uint32_t fp) {
+  // bit s set iff byte s of word == fp (fp != 0; empty slots hold 0)
+  const uint32_t x = word ^ (fp * 0x01010101u);
+  uint32_t m = 0;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    uint4 v = p[s];
-    uint64_t k = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    if (k == key) {
-      hit = true;
+  for (int s = 0; s < 4; ++s) m |= (((x >> (8 * s)) & 0xFF) == 0 ? 1u : 0u) << s;
+  return m;
+}
+
+// Candidates of the three keys (bit j*8 + c*4 + s: key j, bucket choice c,
+// slot s) from the fingerprint words; the lowest set bit is the highest
+// priority.  A real entry is present in exactly one slot, so walking the
+// candidates in bit order and stopping at the first key match gives the
+// reference's first-hit-wins order.
+template <typename FpWord>
+__device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, const uint64_t k[3], bool frag,
+                                          uint32_t* val) {
+  uint32_t bk[3][2], cand = 0;
+  const uint64_t k0 = k[0], k1 = k[1], k2 = k[2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    uint32_t fp;
+    l4_place(k[j], t.bucket_mask, &bk[j][0], &bk[j][1], &fp);
+    if (j != 1 && frag) continue;
+    cand |= (fp_match4(fpw(bk[j][0]), fp) | (fp_match4(fpw(bk[j][1]), fp) << 4)) << (8 * j);
+  }
+  while (cand) {
+    const int bit = __builtin_ctz(cand);
+    cand &= cand - 1;
+    const int j = bit >> 3;
+    const bool second = (bit >> 2) & 1;
+    // selects, not indexing: a dynamically indexed array would live in scratch
+    const uint32_t b = j == 0 ? (second ? bk[0][1] : bk[0][0])
+                     : j == 1 ? (second ? bk[1][1] : bk[1][0])
+                              : (second ? bk[2][1] : bk[2][0]);
+    const uint64_t kj = j == 0 ? k0 : j == 1 ? k1 : k2;
+    const uint4 v = *reinterpret_cast<const uint4*>(t.slots + (size_t)b * 4 + (bit & 3));
+    if (((uint64_t)v.x | ((uint64_t)v.y << 32)) == kj) {
       *val = v.z;
+      return j + 1;
     }
   }
-  return hit;
+  return 0;
 }
 
-__device__ __forceinline__ bool l4_lookup(const L4Dev& t, uint64_t key, uint32_t* val) {
-  uint32_t dummy;
-  if (l4_probe_bucket(t.slots, (uint32_t)l4_hash1(key) & t.bucket_mask, key, val, &dummy)) return true;
-  return l4_probe_bucket(t.slots, (uint32_t)l4_hash2(key) & t.bucket_mask, key, val, &dummy);
-}
+// Counter entry in LDS: one u64 per entry id, packets in bits 40..63, bytes in
+// bits 0..39 (lengths below 64 KiB; longer ones go straight to the global
+// byte counter).  A block flushes before 2^24 tuples, so neither field wraps.
+constexpr uint32_t kL4Tuples = 2;       // tuples per thread per iteration
+constexpr size_t kL4FlushTuples = (size_t)1 << 24;
 
-template <bool kLdsCounters>
-__global__ __launch_bounds__(1024) void l4_kernel(L4Dev t, const uint32_t* __restrict__ tuples, size_t n,
-                                                  int32_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* lpk = lds;
-  uint32_t* lby = lds + t.max_entries;
-  if (kLdsCounters) {
-    for (uint32_t i = threadIdx.x; i < 2 * t.max_entries; i += blockDim.x) lds[i] = 0;
-    __syncthreads();
+__device__ __forceinline__ void l4_count(const L4Dev& t, unsigned long long* lcnt, uint32_t id, uint32_t len) {
+  if (len < 65536u) {
+    atomicAdd(&lcnt[id], (1ULL << 40) | len);
+  } else {
+    atomicAdd(&lcnt[id], 1ULL << 40);
+    atomicAdd(&t.counters[2 * id + 1], (unsigned long long)len);
   }
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  const size_t per_chunk = (size_t)65536;  // tuples per thread-block between flushes ≤ 64K
-  size_t done_in_chunk = 0;
-  for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-    size_t i = base + threadIdx.x;
-    if (i < n) {
-      const uint32_t w0 = tuples[i * 3 + 0];
-      const uint32_t w1 = tuples[i * 3 + 1];
-      const uint32_t len = tuples[i * 3 + 2];
-      const uint32_t identity = w0;
-      const uint32_t dport = w1 & 0xFFFF;
-      const uint32_t proto = (w1 >> 16) & 0xFF;
-      const uint32_t flags = w1 >> 24;
-      const bool frag = flags & CG_L4_F_FRAGMENT;
-      // key.egress = !dir with dir = CT_INGRESS(1) / CT_EGRESS(0)
-      const uint64_t eg = (flags & CG_L4_F_INGRESS) ? 0ULL : 1ULL;
+}
+
+__device__ void l4_flush(const L4Dev& t, unsigned long long* lcnt) {
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < t.max_entries; e += blockDim.x) {
+    const unsigned long long c = lcnt[e];
+    if (c) {
+      atomicAdd(&t.counters[2 * e], c >> 40);
+      if (c & ((1ULL << 40) - 1)) atomicAdd(&t.counters[2 * e + 1], c & ((1ULL << 40) - 1));
+      lcnt[e] = 0;
+    }
+  }
+  __syncthreads();
+}
+
+// Tables whose fingerprints and counters fit LDS together (max_entries*8 +
+// nbuckets*4 <= 160 KiB; the 16,384-entry default): per tuple three key
+// hashes, six LDS fingerprint reads, and a slot read only on a fingerprint
+// match (hits, and ~1.6% false matches per key).
+__global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, const uint32_t* __restrict__ tuples, size_t n,
+                                                     int32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long l4_lds[];
+  unsigned long long* lcnt = l4_lds;
+  uint32_t* lfp = reinterpret_cast<uint32_t*>(l4_lds + t.max_entries);
+  const uint32_t nb = t.bucket_mask + 1;
+  for (uint32_t e = threadIdx.x; e < t.max_entries; e += blockDim.x) lcnt[e] = 0;
+  for (uint32_t e = threadIdx.x; e < nb; e += blockDim.x) lfp[e] = t.fp[e];
+  __syncthreads();
+  const size_t per_iter = (size_t)blockDim.x * kL4Tuples;
+  const size_t stride = (size_t)gridDim.x * per_iter;
+  size_t since_flush = 0;
+  for (size_t base = (size_t)blockIdx.x * per_iter; base < n; base += stride) {
+    uint32_t w[kL4Tuples][3];
+#pragma unroll
+    for (uint32_t u = 0; u < kL4Tuples; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i < n) {
+        w[u][0] = __builtin_nontemporal_load(tuples + i * 3 + 0);
+        w[u][1] = __builtin_nontemporal_load(tuples + i * 3 + 1);
+        w[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kL4Tuples; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i >= n) continue;
+      uint64_t k[3];
+      bool frag;
+      l4_keys(w[u][0], w[u][1], k, &frag);
       uint32_t val = 0;
-      int32_t verdict;
-      int which = 0;  // 1: L4 hit, 2: L3 hit, 3: wildcard-identity L4 hit
-      if (!frag && l4_lookup(t, (uint64_t)identity | ((uint64_t)dport << 32) | ((uint64_t)proto << 48) | (eg << 56), &val))
-        which = 1;
-      else if (l4_lookup(t, (uint64_t)identity | (eg << 56), &val))
-        which = 2;
-      else if (!frag && l4_lookup(t, ((uint64_t)dport << 32) | ((uint64_t)proto << 48) | (eg << 56), &val))
-        which = 3;
-      if (which == 1 || which == 3) {
-        verdict = (int32_t)(val >> 16);  // return policy->proxy_port (be16 as stored)
-      } else if (which == 2) {
-        verdict = 0;  // TC_ACT_OK: the L3 entry's proxy_port is ignored
-      } else if (flags & CG_L4_F_CB_POLICY) {
-        verdict = 0;
-      } else {
-        verdict = frag ? CG_DROP_FRAG_NOSUPPORT : CG_DROP_POLICY;
-      }
-      out[i] = verdict;
-      if (which) {
-        const uint32_t id = val & 0xFFFF;
-        if (kLdsCounters) {
-          atomicAdd(&lpk[id], 1u);
-          if (len < 65536u)
-            atomicAdd(&lby[id], len);
-          else
-            atomicAdd(&t.counters[2 * id + 1], (unsigned long long)len);
-        } else {
-          atomicAdd(&t.counters[2 * id], 1ULL);
-          atomicAdd(&t.counters[2 * id + 1], (unsigned long long)len);
-        }
-      }
+      const int which = l4_resolve(t, [&](uint32_t b) { return lfp[b]; }, k, frag, &val);
+      __builtin_nontemporal_store(l4_verdict(which, val, w[u][1] >> 24), out + i);
+      if (which) l4_count(t, lcnt, val & 0xFFFF, w[u][2]);
     }
-    if (kLdsCounters) {
-      if (++done_in_chunk == per_chunk / 1024 || base + stride >= n) {
-        done_in_chunk = 0;
-        __syncthreads();
-        for (uint32_t e = threadIdx.x; e < t.max_entries; e += blockDim.x) {
-          uint32_t p = lpk[e], b = lby[e];
-          if (p) {
-            atomicAdd(&t.counters[2 * e], (unsigned long long)p);
-            lpk[e] = 0;
-          }
-          if (b) {
-            atomicAdd(&t.counters[2 * e + 1], (unsigned long long)b);
-            lby[e] = 0;
-          }
-        }
-        __syncthreads();
-      }
+    since_flush += per_iter;
+    if (since_flush + per_iter > kL4FlushTuples && base + stride < n) {
+      l4_flush(t, lcnt);
+      since_flush = 0;
+    }
+  }
+  l4_flush(t, lcnt);
+}
+
+// Larger tables: fingerprints read from global memory (L2), counters as
+// global atomics.
+__global__ __launch_bounds__(256) void l4_kernel(L4Dev t, const uint32_t* __restrict__ tuples, size_t n,
+                                                 int32_t* __restrict__ out) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t w0 = tuples[i * 3 + 0], w1 = tuples[i * 3 + 1], len = tuples[i * 3 + 2];
+    uint64_t k[3];
+    bool frag;
+    l4_keys(w0, w1, k, &frag);
+    uint32_t val = 0;
+    const int which = l4_resolve(t, [&](uint32_t b) { return t.fp[b]; }, k, frag, &val);
+    out[i] = l4_verdict(which, val, w1 >> 24);
+    if (which) {
+      const uint32_t id = val & 0xFFFF;
+      atomicAdd(&t.counters[2 * id], 1ULL);
+      atomicAdd(&t.counters[2 * id + 1], (unsigned long long)len);
     }
   }
 }
@@ -269,7 +332,6 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint4* r = reqs + i * 4;
     const uint4 h = r[0];
-    const uint4 t0 = r[1], t1 = r[2], t2 = r[3];
     const int key = (int16_t)(h.x & 0xFFFF);
     const int ver = (int16_t)(h.x >> 16);
     const uint32_t kind = h.y & 0xFF;
@@ -284,9 +346,10 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
         const unsigned long long k = ((unsigned long long)red << 32) | remote;
         uint32_t hh = hash64to32(k) & T.ghash_mask;
         for (uint32_t probe = 0; probe <= T.ghash_mask; ++probe) {
-          const unsigned long long kk = T.ghash_keys[hh];
+          const uint4 e = *reinterpret_cast<const uint4*>(T.ghash + hh);
+          const unsigned long long kk = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
           if (kk == k) {
-            g = T.ghash_vals[hh];
+            g = e.z;
             break;
           }
           if (kk == ~0ULL) break;
@@ -294,20 +357,40 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
         }
       }
       const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
-      const KafkaSumDev* su = T.sums + (size_t)g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
+      const uint32_t si = g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
+      const KafkaSumDev* su = T.sums + si;
       const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
       const uint4 tail = *reinterpret_cast<const uint4*>(&su->any);
       const unsigned long long vm = su->vm[c];
-      v = ((tail.x >> c) & 1) | ((ver >= 0 && ver < 64) ? (uint32_t)((vm >> ver) & 1) : 0u);
+      const bool vin = ver >= 0 && ver < 64;
+      v = ((tail.x >> c) & 1) | (vin ? (uint32_t)((vm >> ver) & 1) : 0u);
+      if (!v && c == 0 && (tail.x & kKfSumHasClients)) {
+        const unsigned long long k = ((unsigned long long)si << 32) | client;
+        uint32_t hh = hash64to32(k) & T.chash_mask;
+        for (uint32_t probe = 0; probe <= T.chash_mask; ++probe) {
+          const KafkaClientDev* e = T.chash + hh;
+          const uint4 a = *reinterpret_cast<const uint4*>(e);
+          const unsigned long long kk = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
+          if (kk == k) {
+            const unsigned long long cvm = (unsigned long long)a.z | ((unsigned long long)a.w << 32);
+            v = (e->any != 0) | (vin ? (uint32_t)((cvm >> ver) & 1) : 0u);
+            break;
+          }
+          if (kk == ~0ULL) break;
+          hh = (hh + 1) & T.chash_mask;
+        }
+      }
       for (uint32_t j = 0; j < tail.z && !v; ++j)
         if (kf_rule_matches(T.rules[tail.y + j], key, ver, kind, client)) v = 1;
       if (!v && nt != 0) {
-        const uint32_t tids[CG_KAFKA_MAX_TOPICS] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y,
-                                                    t1.z, t1.w, t2.x, t2.y, t2.z, t2.w};
+        // topic ids re-read from the record (cached): a dynamically indexed
+        // register array would live in scratch
+        const uint32_t* tids = reinterpret_cast<const uint32_t*>(r + 1);
         const bool ovf = nt > CG_KAFKA_MAX_TOPICS;
+        const uint32_t* tsrc = ovf ? arena + tids[0] : tids;
         bool all = true;
         for (uint32_t t = 0; t < nt && all; ++t) {
-          const uint32_t tid = ovf ? arena[tids[0] + t] : tids[t];
+          const uint32_t tid = tsrc[t];
           const unsigned long long k = ((unsigned long long)g << 32) | tid;
           uint32_t hh = hash64to32(k) & T.thash_mask;
           bool cov = false;
@@ -361,18 +444,18 @@ int grid_for(size_t items, int per_block, int cus, int blocks_per_cu) {
 int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus) {
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  if (t.max_entries <= 16384) {
-    size_t lds = (size_t)t.max_entries * 2 * sizeof(uint32_t);
+  const size_t lds = (size_t)t.max_entries * 8 + (size_t)(t.bucket_mask + 1) * 4;
+  if (lds <= 160 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute((const void*)l4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void*)l4_fp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
-    hipLaunchKernelGGL(l4_kernel<true>, dim3(grid_for(n, 1024, cus, 1)), dim3(1024), lds, s, t,
+    hipLaunchKernelGGL(l4_fp_kernel, dim3(grid_for(n, 1024 * kL4Tuples, cus, 1)), dim3(1024), lds, s, t,
                        (const uint32_t*)tuples, n, out);
   } else {
-    hipLaunchKernelGGL(l4_kernel<false>, dim3(grid_for(n, 1024, cus, 2)), dim3(1024), 0, s, t,
-                       (const uint32_t*)tuples, n, out);
+    hipLaunchKernelGGL(l4_kernel, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, s, t, (const uint32_t*)tuples, n,
+                       out);
   }
   return (int)hipGetLastError();
 }

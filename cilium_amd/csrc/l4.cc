@@ -2,9 +2,10 @@
 //
 // The reference keeps one BPF_MAP_TYPE_HASH per endpoint keyed by the 8-byte
 // struct policy_key (bpf/lib/common.h:180-186, pkg/maps/policymap).  The
-// device copy is a 2-choice cuckoo hash of 64-byte buckets (4 slots of
-// {key, entry id | proxy_port_be << 16}): a lookup touches at most two cache
-// lines.  Counters live in a separate per-entry-id array so a rebuild never
+// device copy is a 2-choice (partial-key) cuckoo hash of 64-byte buckets (4
+// slots of {key, entry id | proxy_port_be << 16, fingerprint}) plus one u32 of
+// 8-bit fingerprints per bucket: the kernel screens a key against its two
+// buckets' fingerprints in LDS and reads a slot only on a fingerprint match.  Counters live in a separate per-entry-id array so a rebuild never
 // moves them.
 #include "l4.h"
 
@@ -23,24 +24,26 @@ bool try_build(const std::unordered_map<uint64_t, PolicyMapState::Entry>& entrie
   std::mt19937_64 rng(0xC111A);
   for (const auto& [key, ent] : entries) {
     L4Slot cur{key, (uint32_t)ent.id | ((uint32_t)ent.proxy_port_be << 16), 0};
-    uint32_t b = (uint32_t)l4_hash1(cur.key) & mask;
+    uint32_t b1, b2, fp;
+    l4_place(cur.key, mask, &b1, &b2, &fp);
+    cur.pad = fp;
+    uint32_t b = b1;
     bool placed = false;
     for (int kick = 0; kick < 500 && !placed; ++kick) {
-      uint32_t b1 = (uint32_t)l4_hash1(cur.key) & mask, b2 = (uint32_t)l4_hash2(cur.key) & mask;
-      for (uint32_t bb : {b1, b2}) {
-        for (int s = 0; s < 4; ++s)
+      const uint32_t alt = b ^ (l4_alt(cur.pad) & mask);
+      for (uint32_t bb : {b, alt}) {
+        for (int s = 0; s < 4 && !placed; ++s)
           if (slots[(size_t)bb * 4 + s].key == kL4EmptyKey) {
             slots[(size_t)bb * 4 + s] = cur;
             placed = true;
-            break;
           }
         if (placed) break;
       }
       if (placed) break;
-      // evict a random slot of the alternate bucket
-      b = (b == b1) ? b2 : b1;
-      int victim = (int)(rng() & 3);
-      std::swap(cur, slots[(size_t)b * 4 + victim]);
+      // evict a random slot of the alternate bucket; the victim moves on to
+      // its own alternate (partial-key cuckoo: bucket XOR alt(fingerprint))
+      b = alt;
+      std::swap(cur, slots[(size_t)b * 4 + (rng() & 3)]);
     }
     if (!placed) return false;
   }
@@ -50,17 +53,25 @@ bool try_build(const std::unordered_map<uint64_t, PolicyMapState::Entry>& entrie
 }  // namespace
 
 void PolicyMapState::rebuild(Engine& e) {
-  uint32_t nb = next_pow2(std::max<size_t>((entries.size() * 10 / 4 + 3) / 4 + 1, 4));
+  // load factor (0.25, 0.5]: 16,384 entries fit 8,192 buckets, whose 32 KiB
+  // fingerprint array sits in LDS next to the 128 KiB of counters
+  uint32_t nb = next_pow2(std::max<size_t>((entries.size() + 1) / 2, 4));
   while (!try_build(entries, nb, slots)) nb *= 2;
   bucket_mask = nb - 1;
+  fp.assign(nb, 0);
+  for (uint32_t bk = 0; bk < nb; ++bk)
+    for (int s = 0; s < 4; ++s)
+      if (slots[(size_t)bk * 4 + s].key != kL4EmptyKey) fp[bk] |= slots[(size_t)bk * 4 + s].pad << (8 * s);
   if (e.has_gpu()) {
     e.set_device();
     d_slots.upload_vec(slots);
+    d_fp.upload_vec(fp);
     if (d_counters.size() == 0) {
       d_counters.alloc((size_t)max_entries * 2 * sizeof(uint64_t));
       d_counters.zero();
     }
     dev.slots = d_slots.as<L4Slot>();
+    dev.fp = d_fp.as<uint32_t>();
     dev.bucket_mask = bucket_mask;
     dev.max_entries = max_entries;
     dev.counters = d_counters.as<unsigned long long>();

@@ -36,8 +36,9 @@ struct PolicyMapState {
 
   // device
   std::vector<L4Slot> slots;
+  std::vector<uint32_t> fp;  // per bucket: 4 x 8-bit slot fingerprints
   uint32_t bucket_mask = 0;
-  DevMem d_slots, d_counters;
+  DevMem d_slots, d_fp, d_counters;
   L4Dev dev{};
   std::vector<uint64_t> host_counters;  // for handles without a GPU (always 0)
 

@@ -86,6 +86,26 @@ def test_l4_empty_and_ragged(gpu):
         assert np.array_equal(got, exp), n
 
 
+def test_l4_large_map_and_long_lengths(gpu):
+    """A 65,536-entry map (fingerprints and counters no longer fit LDS: the
+    global-memory kernel) and packet lengths >= 64 KiB (the LDS counter's
+    byte field is bypassed), verdicts and counters against the oracle."""
+    keys, ports = synth.l4_table(n_entries=20000, n_ids=20000)
+    for max_entries in (65536, 20000):
+        pm = gpu.policy_map(max_entries=max_entries)
+        pm.allow_keys(keys, ports)
+        tuples = synth.l4_tuples(300_000, keys, n_ids=20000, seed=max_entries)
+        tuples["len"][::7] = 70000 + np.arange(len(tuples[::7])) % 1000
+        got = pm.verdicts(tuples)
+        exp, pk, by = oracle.l4(keys, ports, tuples)
+        assert np.array_equal(got, exp)
+        dump = {(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection): e for k, e in pm.dump_to_slice()}
+        for i in range(0, len(keys), 97):
+            k = keys[i]
+            e = dump[(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"]))]
+            assert (e.Packets, e.Bytes) == (int(pk[i]), int(by[i]))
+
+
 def test_l4_map_full(gpu):
     pm = gpu.policy_map(max_entries=4)
     for i in range(4):
