@@ -40,7 +40,21 @@ CG_HD inline uint64_t l4_hash1(uint64_t k) {
   k ^= k >> 33;
   return k;
 }
-CG_HD inline uint32_t l4_alt(uint32_t fp) { return (fp * 0x5bd1e995u) | 1u; }
+// Policy-key hash for the device table, 32-bit arithmetic only (three
+// quarter-rate multiplies per key and the first two shared between the three
+// keys of one tuple): key = identity | (dport | proto << 16 | egress << 24) << 32.
+CG_HD inline uint32_t l4_fin(uint32_t x) {
+  x ^= x >> 15;
+  x *= 0x2C1B3C6Du;
+  x ^= x >> 13;
+  return x;
+}
+constexpr uint32_t kL4MulLo = 0x9E3779B1u, kL4MulHi = 0x85EBCA77u;
+CG_HD inline uint32_t l4_h(uint64_t key) {
+  return l4_fin((uint32_t)key * kL4MulLo + (uint32_t)(key >> 32) * kL4MulHi);
+}
+// Second-bucket offset from the fingerprint (8-bit x 24-bit: a full-rate mul24).
+CG_HD inline uint32_t l4_alt(uint32_t fp) { return (fp * 0x9E3779u) | 1u; }
 
 CG_HD inline uint64_t l4_hash2(uint64_t k) {
   k += 0x9e3779b97f4a7c15ULL;
@@ -52,16 +66,19 @@ CG_HD inline uint64_t l4_hash2(uint64_t k) {
   return k;
 }
 
-// Partial-key cuckoo placement: one hash gives the first bucket and an 8-bit
-// fingerprint (1..255); the second bucket is the first XOR a function of the
-// fingerprint, so either bucket and the fingerprint recover the other.
-CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* b2, uint32_t* fp) {
-  const uint64_t h = l4_hash1(key);
-  uint32_t f = (uint32_t)(h >> 56);
+// Partial-key cuckoo placement: the hash gives the first bucket (low bits) and
+// an 8-bit fingerprint (top byte, 1..255); the second bucket is the first XOR
+// a function of the fingerprint, so either bucket and the fingerprint recover
+// the other.
+CG_HD inline void l4_place_h(uint32_t h, uint32_t mask, uint32_t* b1, uint32_t* b2, uint32_t* fp) {
+  uint32_t f = h >> 24;
   f = f ? f : 1u;
   *fp = f;
-  *b1 = (uint32_t)h & mask;
+  *b1 = h & mask;
   *b2 = *b1 ^ (l4_alt(f) & mask);
+}
+CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* b2, uint32_t* fp) {
+  l4_place_h(l4_h(key), mask, b1, b2, fp);
 }
 
 // ----------------------------------------------------------------- LPM ----

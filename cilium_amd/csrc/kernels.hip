@@ -14,6 +14,7 @@ namespace cg {
 namespace {
 
 constexpr int kWave = 64;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
@@ -30,69 +31,66 @@ __device__ __forceinline__ int32_t l4_verdict(int which, uint32_t val, uint32_t 
   return (flags & CG_L4_F_FRAGMENT) ? CG_DROP_FRAG_NOSUPPORT : CG_DROP_POLICY;
 }
 
-// The three policy_key lookups of __policy_can_access in priority order:
-// {id, dport, proto, dir} (skipped for fragments), {id, 0, 0, dir},
-// {0, dport, proto, dir} (skipped for fragments).
-__device__ __forceinline__ void l4_keys(uint32_t w0, uint32_t w1, uint64_t k[3], bool* frag) {
-  const uint32_t flags = w1 >> 24;
-  *frag = flags & CG_L4_F_FRAGMENT;
-  // key.egress = !dir with dir = CT_INGRESS(1) / CT_EGRESS(0)
-  const uint64_t eg = (flags & CG_L4_F_INGRESS) ? 0ULL : (1ULL << 56);
-  const uint64_t pp = ((uint64_t)(w1 & 0xFFFF) << 32) | ((uint64_t)((w1 >> 16) & 0xFF) << 48);
-  k[0] = (uint64_t)w0 | pp | eg;
-  k[1] = (uint64_t)w0 | eg;
-  k[2] = pp | eg;
-}
-
-__device__ __forceinline__ uint32_t fp_match4(uint32_t word, uint32_t fp) {
-  // bit s set iff byte s of word == fp (fp != 0; empty slots hold 0)
-  const uint32_t x = word ^ (fp * 0x01010101u);
-  uint32_t m = 0;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) m |= (((x >> (8 * s)) & 0xFF) == 0 ? 1u : 0u) << s;
-  return m;
-}
-
-// Candidates of the three keys (bit j*8 + c*4 + s: key j, bucket choice c,
-// slot s) from the fingerprint words; the lowest set bit is the highest
-// priority.  A real entry is present in exactly one slot, so walking the
-// candidates in bit order and stopping at the first key match gives the
-// reference's first-hit-wins order.
+// The three policy_key lookups of __policy_can_access (bpf/lib/policy.h:61-109)
+// in priority order: j=0 {id, dport, proto, dir} (skipped for fragments),
+// j=1 {id, 0, 0, dir}, j=2 {0, dport, proto, dir} (skipped for fragments).
+// The keys share their hash products: h_j = fin(lo_j*M1 + hi_j*M2) with
+// lo in {id, id, 0} and hi in {pp, eg, pp}.
+//
+// Candidates come from the fingerprint words: a zero-byte test on word^fp
+// (it can flag a byte next to a true match as well, which only costs a slot
+// read); bit p = slot*8 + j*2 + c for key j, bucket choice c.  A policy key
+// sits in one slot, so the lowest j whose slot key matches is the verdict;
+// candidates are walked in bit order and a j=0 match ends the walk.
 template <typename FpWord>
-__device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, const uint64_t k[3], bool frag,
+__device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, uint32_t w0, uint32_t w1, bool frag,
                                           uint32_t* val) {
-  uint32_t bk[3][2], cand = 0;
-  const uint64_t k0 = k[0], k1 = k[1], k2 = k[2];
+  const uint32_t flags = w1 >> 24;
+  // key.egress = !dir with dir = CT_INGRESS(1) / CT_EGRESS(0)
+  const uint32_t eg = (flags & CG_L4_F_INGRESS) ? 0u : (1u << 24);
+  const uint32_t pp = (w1 & 0xFFFFFF) | eg;  // dport | proto << 16 | egress << 24
+  const uint32_t P = w0 * kL4MulLo, Q = pp * kL4MulHi, E = eg * kL4MulHi;
+  const uint32_t hi[3] = {pp, eg, pp};
+  const uint32_t h[3] = {l4_fin(P + Q), l4_fin(P + E), l4_fin(Q)};
+  uint32_t bk[3][2];
+  uint64_t cand = 0;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     uint32_t fp;
-    l4_place(k[j], t.bucket_mask, &bk[j][0], &bk[j][1], &fp);
+    l4_place_h(h[j], t.bucket_mask, &bk[j][0], &bk[j][1], &fp);
     if (j != 1 && frag) continue;
-    cand |= (fp_match4(fpw(bk[j][0]), fp) | (fp_match4(fpw(bk[j][1]), fp) << 4)) << (8 * j);
-  }
-  while (cand) {
-    const int bit = __builtin_ctz(cand);
-    cand &= cand - 1;
-    const int j = bit >> 3;
-    const bool second = (bit >> 2) & 1;
-    // selects, not indexing: a dynamically indexed array would live in scratch
-    const uint32_t b = j == 0 ? (second ? bk[0][1] : bk[0][0])
-                     : j == 1 ? (second ? bk[1][1] : bk[1][0])
-                              : (second ? bk[2][1] : bk[2][0]);
-    const uint64_t kj = j == 0 ? k0 : j == 1 ? k1 : k2;
-    const uint4 v = *reinterpret_cast<const uint4*>(t.slots + (size_t)b * 4 + (bit & 3));
-    if (((uint64_t)v.x | ((uint64_t)v.y << 32)) == kj) {
-      *val = v.z;
-      return j + 1;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t x = fpw(bk[j][c]) ^ (fp * 0x01010101u);
+      const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;  // bit 8s+7: byte s zero
+      cand |= (uint64_t)(z >> 7) << (j * 2 + c);
     }
   }
-  return 0;
+  int best = 0;
+  while (cand) {
+    const int bit = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    const int jc = bit & 7, j = jc >> 1;
+    if (best && j + 1 >= best) continue;
+    // selects, not indexing: a dynamically indexed array would live in scratch
+    const uint32_t b = jc == 0 ? bk[0][0] : jc == 1 ? bk[0][1] : jc == 2 ? bk[1][0]
+                     : jc == 3 ? bk[1][1] : jc == 4 ? bk[2][0] : bk[2][1];
+    const uint32_t klo = j == 2 ? 0u : w0;
+    const uint32_t khi = j == 0 ? hi[0] : j == 1 ? hi[1] : hi[2];
+    const uint4 v = *reinterpret_cast<const uint4*>(t.slots + (size_t)b * 4 + (bit >> 3));
+    if (v.x == klo && v.y == khi) {
+      *val = v.z;
+      best = j + 1;
+      if (j == 0) break;
+    }
+  }
+  return best;
 }
 
 // Counter entry in LDS: one u64 per entry id, packets in bits 40..63, bytes in
 // bits 0..39 (lengths below 64 KiB; longer ones go straight to the global
 // byte counter).  A block flushes before 2^24 tuples, so neither field wraps.
-constexpr uint32_t kL4Tuples = 2;       // tuples per thread per iteration
+constexpr uint32_t kL4Tuples = 4;       // tuples per thread per iteration
 constexpr size_t kL4FlushTuples = (size_t)1 << 24;
 
 __device__ __forceinline__ void l4_count(const L4Dev& t, unsigned long long* lcnt, uint32_t id, uint32_t len) {
@@ -137,22 +135,19 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, const uint32_t* __
     uint32_t w[kL4Tuples][3];
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
-      const size_t i = base + u * blockDim.x + threadIdx.x;
-      if (i < n) {
-        w[u][0] = __builtin_nontemporal_load(tuples + i * 3 + 0);
-        w[u][1] = __builtin_nontemporal_load(tuples + i * 3 + 1);
-        w[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
-      }
+      size_t i = base + u * blockDim.x + threadIdx.x;
+      i = i < n ? i : n - 1;  // unconditional loads (see kafka_kernel)
+      w[u][0] = __builtin_nontemporal_load(tuples + i * 3 + 0);
+      w[u][1] = __builtin_nontemporal_load(tuples + i * 3 + 1);
+      w[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
     }
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
       const size_t i = base + u * blockDim.x + threadIdx.x;
       if (i >= n) continue;
-      uint64_t k[3];
-      bool frag;
-      l4_keys(w[u][0], w[u][1], k, &frag);
+      const bool frag = (w[u][1] >> 24) & CG_L4_F_FRAGMENT;
       uint32_t val = 0;
-      const int which = l4_resolve(t, [&](uint32_t b) { return lfp[b]; }, k, frag, &val);
+      const int which = l4_resolve(t, [&](uint32_t b) { return lfp[b]; }, w[u][0], w[u][1], frag, &val);
       __builtin_nontemporal_store(l4_verdict(which, val, w[u][1] >> 24), out + i);
       if (which) l4_count(t, lcnt, val & 0xFFFF, w[u][2]);
     }
@@ -172,11 +167,9 @@ __global__ __launch_bounds__(256) void l4_kernel(L4Dev t, const uint32_t* __rest
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t w0 = tuples[i * 3 + 0], w1 = tuples[i * 3 + 1], len = tuples[i * 3 + 2];
-    uint64_t k[3];
-    bool frag;
-    l4_keys(w0, w1, k, &frag);
+    const bool frag = (w1 >> 24) & CG_L4_F_FRAGMENT;
     uint32_t val = 0;
-    const int which = l4_resolve(t, [&](uint32_t b) { return t.fp[b]; }, k, frag, &val);
+    const int which = l4_resolve(t, [&](uint32_t b) { return t.fp[b]; }, w0, w1, frag, &val);
     out[i] = l4_verdict(which, val, w1 >> 24);
     if (which) {
       const uint32_t id = val & 0xFFFF;
@@ -320,103 +313,145 @@ __device__ __forceinline__ void kf_flush(unsigned long long* counters, uint32_t 
   if (deny) atomicAdd(&counters[red * 2 + 1], (unsigned long long)deny);
 }
 
-// One lane per request (64-B records, four 16-B loads).  The group lookup is
-// one hash probe; the summary for (group, topics?, apiKey) settles most
-// requests with two bit tests; the rest walk exception rules and, per topic,
-// the (group, topic) rule list.  Counters accumulate per lane while the
-// redirect stays the same and are wave-reduced at the end.
+// Slow part of one request: clientID table (typed requests against clientID
+// rules), exception rules, then per topic the (group, topic) rule list.
+__device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, const uint32_t* __restrict__ arena,
+                                         uint32_t g, uint32_t si, uint4 tail, int key, int ver, uint32_t kind,
+                                         uint32_t c, uint32_t nt, uint32_t client) {
+  const bool vin = ver >= 0 && ver < 64;
+  if (c == 0 && (tail.x & kKfSumHasClients)) {
+    const unsigned long long k = ((unsigned long long)si << 32) | client;
+    uint32_t hh = hash64to32(k) & T.chash_mask;
+    for (uint32_t probe = 0; probe <= T.chash_mask; ++probe) {
+      const KafkaClientDev* e = T.chash + hh;
+      const uint4 a = *reinterpret_cast<const uint4*>(e);
+      const unsigned long long kk = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
+      if (kk == k) {
+        const unsigned long long cvm = (unsigned long long)a.z | ((unsigned long long)a.w << 32);
+        if (e->any != 0 || (vin && ((cvm >> ver) & 1))) return 1;
+        break;
+      }
+      if (kk == ~0ULL) break;
+      hh = (hh + 1) & T.chash_mask;
+    }
+  }
+  for (uint32_t j = 0; j < tail.z; ++j)
+    if (kf_rule_matches(T.rules[tail.y + j], key, ver, kind, client)) return 1;
+  if (nt == 0) return 0;
+  // topic ids re-read from the record (cached)
+  const uint32_t* tids = reinterpret_cast<const uint32_t*>(r + 1);
+  const uint32_t* tsrc = nt > CG_KAFKA_MAX_TOPICS ? arena + tids[0] : tids;
+  for (uint32_t t = 0; t < nt; ++t) {
+    const unsigned long long k = ((unsigned long long)g << 32) | tsrc[t];
+    uint32_t hh = hash64to32(k) & T.thash_mask;
+    bool cov = false;
+    for (uint32_t probe = 0; probe <= T.thash_mask; ++probe) {
+      const KafkaTopicDev e = T.thash[hh];
+      if (e.key == k) {
+        for (uint32_t j = 0; j < e.cnt && !cov; ++j)
+          cov = kf_rule_matches(T.rules[e.off + j], key, ver, kind, client);
+        break;
+      }
+      if (e.key == ~0ULL) break;
+      hh = (hh + 1) & T.thash_mask;
+    }
+    if (!cov) return 0;
+  }
+  return 1;
+}
+
+// kKafkaReqs requests per lane per iteration, in phases so that each phase's
+// loads for all of them are in flight together: the 16-B record heads, the
+// (redirect, identity) group slots, the decision summaries.  The summary for
+// (group, topics?, apiKey) settles most requests with two bit tests; the rest
+// take kf_slow.  Counters accumulate per lane while the redirect stays the
+// same and are wave-reduced at the end.
+constexpr uint32_t kKafkaReqs = 4;
+
 __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __restrict__ reqs, size_t n,
                                                     const uint32_t* __restrict__ arena, uint8_t* __restrict__ out) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t per_iter = (size_t)blockDim.x * kKafkaReqs;
+  const size_t stride = (size_t)gridDim.x * per_iter;
   uint32_t cred = ~0u, callow = 0, cdeny = 0;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint4* r = reqs + i * 4;
-    const uint4 h = r[0];
-    const int key = (int16_t)(h.x & 0xFFFF);
-    const int ver = (int16_t)(h.x >> 16);
-    const uint32_t kind = h.y & 0xFF;
-    const uint32_t nt = (h.y >> 8) & 0xFF;
-    const uint32_t red = h.y >> 16;
-    const uint32_t remote = h.z;
-    const uint32_t client = h.w;
-    uint32_t v = 0;
-    if (red < T.nredirects) {
-      uint32_t g = T.dflt_group[red];
-      if (remote != 0) {
-        const unsigned long long k = ((unsigned long long)red << 32) | remote;
-        uint32_t hh = hash64to32(k) & T.ghash_mask;
-        for (uint32_t probe = 0; probe <= T.ghash_mask; ++probe) {
-          const uint4 e = *reinterpret_cast<const uint4*>(T.ghash + hh);
-          const unsigned long long kk = (unsigned long long)e.x | ((unsigned long long)e.y << 32);
-          if (kk == k) {
-            g = e.z;
-            break;
-          }
-          if (kk == ~0ULL) break;
-          hh = (hh + 1) & T.ghash_mask;
-        }
-      }
-      const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
-      const uint32_t si = g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
-      const KafkaSumDev* su = T.sums + si;
-      const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
-      const uint4 tail = *reinterpret_cast<const uint4*>(&su->any);
-      const unsigned long long vm = su->vm[c];
-      const bool vin = ver >= 0 && ver < 64;
-      v = ((tail.x >> c) & 1) | (vin ? (uint32_t)((vm >> ver) & 1) : 0u);
-      if (!v && c == 0 && (tail.x & kKfSumHasClients)) {
-        const unsigned long long k = ((unsigned long long)si << 32) | client;
-        uint32_t hh = hash64to32(k) & T.chash_mask;
-        for (uint32_t probe = 0; probe <= T.chash_mask; ++probe) {
-          const KafkaClientDev* e = T.chash + hh;
-          const uint4 a = *reinterpret_cast<const uint4*>(e);
-          const unsigned long long kk = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
-          if (kk == k) {
-            const unsigned long long cvm = (unsigned long long)a.z | ((unsigned long long)a.w << 32);
-            v = (e->any != 0) | (vin ? (uint32_t)((cvm >> ver) & 1) : 0u);
-            break;
-          }
-          if (kk == ~0ULL) break;
-          hh = (hh + 1) & T.chash_mask;
-        }
-      }
-      for (uint32_t j = 0; j < tail.z && !v; ++j)
-        if (kf_rule_matches(T.rules[tail.y + j], key, ver, kind, client)) v = 1;
-      if (!v && nt != 0) {
-        // topic ids re-read from the record (cached): a dynamically indexed
-        // register array would live in scratch
-        const uint32_t* tids = reinterpret_cast<const uint32_t*>(r + 1);
-        const bool ovf = nt > CG_KAFKA_MAX_TOPICS;
-        const uint32_t* tsrc = ovf ? arena + tids[0] : tids;
-        bool all = true;
-        for (uint32_t t = 0; t < nt && all; ++t) {
-          const uint32_t tid = tsrc[t];
-          const unsigned long long k = ((unsigned long long)g << 32) | tid;
-          uint32_t hh = hash64to32(k) & T.thash_mask;
-          bool cov = false;
-          for (uint32_t probe = 0; probe <= T.thash_mask; ++probe) {
-            const KafkaTopicDev e = T.thash[hh];
-            if (e.key == k) {
-              for (uint32_t j = 0; j < e.cnt && !cov; ++j)
-                cov = kf_rule_matches(T.rules[e.off + j], key, ver, kind, client);
-              break;
-            }
-            if (e.key == ~0ULL) break;
-            hh = (hh + 1) & T.thash_mask;
-          }
-          all = cov;
-        }
-        v = all ? 1 : 0;
-      }
-      if (red != cred) {
-        if (cred != ~0u) kf_flush(T.counters, cred, callow, cdeny);
-        cred = red;
-        callow = cdeny = 0;
-      }
-      callow += v;
-      cdeny += v ^ 1;
+  for (size_t base = (size_t)blockIdx.x * per_iter; base < n; base += stride) {
+    uint4 h[kKafkaReqs];
+#pragma unroll
+    for (uint32_t u = 0; u < kKafkaReqs; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      // unconditional (clamped) loads: a load under a branch gets its own
+      // vmcnt(0) at the join, which would serialize the four
+      const size_t ic = i < n ? i : n - 1;
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(reqs + ic * 4));
+      h[u] = make_uint4(v.x, v.y, v.z, v.w);
     }
-    out[i] = (uint8_t)v;
+    // group slot probes (first probe for every request; further ones rare)
+    uint32_t g[kKafkaReqs];
+    uint4 e[kKafkaReqs];
+    uint32_t hh[kKafkaReqs];
+#pragma unroll
+    for (uint32_t u = 0; u < kKafkaReqs; ++u) {
+      const uint32_t red = h[u].y >> 16;
+      const unsigned long long k = ((unsigned long long)red << 32) | h[u].z;
+      hh[u] = hash64to32(k) & T.ghash_mask;
+      e[u] = *reinterpret_cast<const uint4*>(T.ghash + hh[u]);
+      g[u] = T.dflt_group[red < T.nredirects ? red : 0];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kKafkaReqs; ++u) {
+      const uint32_t red = h[u].y >> 16;
+      if (h[u].z == 0) continue;
+      const unsigned long long k = ((unsigned long long)red << 32) | h[u].z;
+      uint4 x = e[u];
+      uint32_t slot = hh[u];
+      for (uint32_t probe = 0; probe <= T.ghash_mask; ++probe) {
+        const unsigned long long kk = (unsigned long long)x.x | ((unsigned long long)x.y << 32);
+        if (kk == k) {
+          g[u] = x.z;
+          break;
+        }
+        if (kk == ~0ULL) break;
+        slot = (slot + 1) & T.ghash_mask;
+        x = *reinterpret_cast<const uint4*>(T.ghash + slot);
+      }
+    }
+    // summaries
+    uint4 tail[kKafkaReqs];
+    unsigned long long vm[kKafkaReqs];
+    uint32_t si[kKafkaReqs];
+#pragma unroll
+    for (uint32_t u = 0; u < kKafkaReqs; ++u) {
+      const int key = (int16_t)(h[u].x & 0xFFFF);
+      const uint32_t kind = h[u].y & 0xFF, nt = (h[u].y >> 8) & 0xFF;
+      const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
+      const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
+      si[u] = g[u] * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
+      const KafkaSumDev* su = T.sums + si[u];
+      tail[u] = *reinterpret_cast<const uint4*>(&su->any);
+      vm[u] = su->vm[c];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kKafkaReqs; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i >= n) continue;
+      const int key = (int16_t)(h[u].x & 0xFFFF);
+      const int ver = (int16_t)(h[u].x >> 16);
+      const uint32_t kind = h[u].y & 0xFF, nt = (h[u].y >> 8) & 0xFF, red = h[u].y >> 16;
+      const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
+      uint32_t v = 0;
+      if (red < T.nredirects) {
+        v = ((tail[u].x >> c) & 1) | ((ver >= 0 && ver < 64) ? (uint32_t)((vm[u] >> ver) & 1) : 0u);
+        if (!v && ((c == 0 && (tail[u].x & kKfSumHasClients)) || tail[u].z || nt))
+          v = kf_slow(T, reqs + i * 4, arena, g[u], si[u], tail[u], key, ver, kind, c, nt, h[u].w);
+        if (red != cred) {
+          if (cred != ~0u) kf_flush(T.counters, cred, callow, cdeny);
+          cred = red;
+          callow = cdeny = 0;
+        }
+        callow += v;
+        cdeny += v ^ 1;
+      }
+      out[i] = (uint8_t)v;
+    }
   }
   // the common case: every lane of the wave counted for the same redirect
   const uint32_t first = __builtin_amdgcn_readfirstlane(cred);
@@ -429,6 +464,14 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
   } else if (cred != ~0u) {
     kf_flush(T.counters, cred, callow, cdeny);
   }
+}
+
+// Resident blocks per CU for a kernel (occupancy query, cached per kernel):
+// grid-stride kernels launch exactly what fits, so no block runs as a tail.
+int resident(const void* fn, int threads, size_t lds) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, lds) != hipSuccess || nb < 1) nb = 1;
+  return nb;
 }
 
 int grid_for(size_t items, int per_block, int cus, int blocks_per_cu) {
@@ -471,7 +514,8 @@ int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
                  void* stream, int cus) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, (hipStream_t)stream, t,
+  static const int occ = resident((const void*)kafka_kernel, 256, 0);
+  hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, 256 * kKafkaReqs, cus, occ)), dim3(256), 0, (hipStream_t)stream, t,
                      (const uint4*)reqs, n, arena, out);
   return (int)hipGetLastError();
 }

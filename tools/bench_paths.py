@@ -57,6 +57,8 @@ def timed(torch, stream, fn, steps, warmup):
 
 
 def cpu_rate(fn, items, seconds):
+    if seconds <= 0:
+        return None
     t0, n = time.perf_counter(), 0
     while time.perf_counter() - t0 < seconds:
         fn()

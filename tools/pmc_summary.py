@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--items", type=int, default=0, help="items (requests) per dispatch")
     ap.add_argument("--algo-bytes", type=float, default=0.0, help="algorithmic bytes per item")
     ap.add_argument("--out", default="")
+    ap.add_argument("--last", type=int, default=0, help="only the last N dispatches of the kernel")
     a = ap.parse_args()
     per = collections.defaultdict(list)
     resources = {}
@@ -32,6 +33,9 @@ def main():
             agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
             resources = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
                                            "VGPR_Count", "SGPR_Count")}
+        if a.last:
+            keep = set(sorted({int(d) for d, _ in agg}, key=int)[-a.last:])
+            agg = {k: v for k, v in agg.items() if int(k[0]) in keep}
         for (_, c), v in agg.items():
             per[c].append(v)
     avg = {c: sum(v) / len(v) for c, v in per.items()}
