@@ -232,6 +232,10 @@ struct KafkaRuleDev {
   uint32_t pad;
 };
 constexpr uint32_t kKfKeyWild = 1, kKfVerWild = 2, kKfHasClient = 4, kKfHasTopic = 8;
+// Kafka table hash over a (hi, lo) u32 key pair: 32-bit multiplies only.
+CG_HD inline uint32_t kf_hash(uint64_t k) {
+  return l4_fin((uint32_t)k * kL4MulLo + (uint32_t)(k >> 32) * kL4MulHi);
+}
 constexpr uint32_t kKfBuckets = 65;                // apiKey 0..63 + "other"
 constexpr uint32_t kKfSumsPerGroup = 2 * kKfBuckets;
 struct KafkaSumDev {

@@ -308,27 +308,27 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
     }
     ++ri;
   }
-  uint32_t cap = next_pow2(std::max<size_t>(gh.size() * 2, 16));
+  uint32_t cap = next_pow2(std::max<size_t>(gh.size() * 4, 16));  // load <= 1/4: ~1.1 probes
   S.ghash.assign(cap, KafkaGroupSlot{~0ULL, 0, 0});
   S.ghash_mask = cap - 1;
   for (auto [k, v] : gh) {
-    uint32_t h = hash64to32(k) & S.ghash_mask;
+    uint32_t h = kf_hash(k) & S.ghash_mask;
     while (S.ghash[h].key != ~0ULL) h = (h + 1) & S.ghash_mask;
     S.ghash[h] = KafkaGroupSlot{k, v, 0};
   }
-  cap = next_pow2(std::max<size_t>(cmap.size() * 2, 16));
+  cap = next_pow2(std::max<size_t>(cmap.size() * 4, 16));
   S.chash.assign(cap, KafkaClientDev{~0ULL, 0, 0, {0, 0, 0}});
   S.chash_mask = cap - 1;
   for (const auto& [k, e] : cmap) {
-    uint32_t h = hash64to32(k) & S.chash_mask;
+    uint32_t h = kf_hash(k) & S.chash_mask;
     while (S.chash[h].key != ~0ULL) h = (h + 1) & S.chash_mask;
     S.chash[h] = e;
   }
-  cap = next_pow2(std::max<size_t>(tentries.size() * 2, 16));
+  cap = next_pow2(std::max<size_t>(tentries.size() * 4, 16));
   S.thash.assign(cap, KafkaTopicDev{~0ULL, 0, 0});
   S.thash_mask = cap - 1;
   for (const auto& t : tentries) {
-    uint32_t h = hash64to32(t.key) & S.thash_mask;
+    uint32_t h = kf_hash(t.key) & S.thash_mask;
     while (S.thash[h].key != ~0ULL) h = (h + 1) & S.thash_mask;
     S.thash[h] = t;
   }
@@ -349,7 +349,7 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
   uint32_t g = s.dflt_group[q.policy];
   if (q.remote != 0) {
     uint64_t key = ((uint64_t)q.policy << 32) | q.remote;
-    uint32_t h = hash64to32(key) & s.ghash_mask;
+    uint32_t h = kf_hash(key) & s.ghash_mask;
     while (s.ghash[h].key != ~0ULL) {
       if (s.ghash[h].key == key) {
         g = s.ghash[h].group;
@@ -368,7 +368,7 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
   if (vin && ((su.vm[c] >> q.api_version) & 1)) return 1;
   if (c == 0 && (su.any & kKfSumHasClients)) {
     const uint64_t key = ((uint64_t)si << 32) | q.client_id;
-    uint32_t h = hash64to32(key) & s.chash_mask;
+    uint32_t h = kf_hash(key) & s.chash_mask;
     while (s.chash[h].key != ~0ULL) {
       if (s.chash[h].key == key) {
         if (s.chash[h].any || (vin && ((s.chash[h].vm >> q.api_version) & 1))) return 1;
@@ -387,7 +387,7 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
   }
   for (uint32_t t = 0; t < nt; ++t) {
     const uint64_t key = ((uint64_t)g << 32) | topics[t];
-    uint32_t h = hash64to32(key) & s.thash_mask;
+    uint32_t h = kf_hash(key) & s.thash_mask;
     bool cov = false;
     while (s.thash[h].key != ~0ULL) {
       if (s.thash[h].key == key) {

@@ -321,7 +321,7 @@ __device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, c
   const bool vin = ver >= 0 && ver < 64;
   if (c == 0 && (tail.x & kKfSumHasClients)) {
     const unsigned long long k = ((unsigned long long)si << 32) | client;
-    uint32_t hh = hash64to32(k) & T.chash_mask;
+    uint32_t hh = kf_hash(k) & T.chash_mask;
     for (uint32_t probe = 0; probe <= T.chash_mask; ++probe) {
       const KafkaClientDev* e = T.chash + hh;
       const uint4 a = *reinterpret_cast<const uint4*>(e);
@@ -343,7 +343,7 @@ __device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, c
   const uint32_t* tsrc = nt > CG_KAFKA_MAX_TOPICS ? arena + tids[0] : tids;
   for (uint32_t t = 0; t < nt; ++t) {
     const unsigned long long k = ((unsigned long long)g << 32) | tsrc[t];
-    uint32_t hh = hash64to32(k) & T.thash_mask;
+    uint32_t hh = kf_hash(k) & T.thash_mask;
     bool cov = false;
     for (uint32_t probe = 0; probe <= T.thash_mask; ++probe) {
       const KafkaTopicDev e = T.thash[hh];
@@ -363,21 +363,60 @@ __device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, c
 // kKafkaReqs requests per lane per iteration, in phases so that each phase's
 // loads for all of them are in flight together: the 16-B record heads, the
 // (redirect, identity) group slots, the decision summaries.  The summary for
-// (group, topics?, apiKey) settles most requests with two bit tests; the rest
-// take kf_slow.  Counters accumulate per lane while the redirect stays the
-// same and are wave-reduced at the end.
+// (group, topics?, apiKey) settles most requests with two bit tests.  The
+// rest (clientID comparisons, exception rules, topic lists) are queued in LDS
+// and evaluated 256 at a time by the whole block, so a few such requests do
+// not make every wave walk the slow path.  Counters accumulate per lane while
+// the redirect stays the same and are wave-reduced at the end.
 constexpr uint32_t kKafkaReqs = 4;
+constexpr uint32_t kKafkaThreads = 256;
+constexpr uint32_t kKafkaQueue = kKafkaThreads * (kKafkaReqs + 1);
 
-__global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __restrict__ reqs, size_t n,
-                                                    const uint32_t* __restrict__ arena, uint8_t* __restrict__ out) {
-  const size_t per_iter = (size_t)blockDim.x * kKafkaReqs;
+struct KfCount {
+  uint32_t red = ~0u, allow = 0, deny = 0;
+  __device__ __forceinline__ void add(const KafkaDev& T, uint32_t r, uint32_t v) {
+    if (r != red) {
+      if (red != ~0u) kf_flush(T.counters, red, allow, deny);
+      red = r;
+      allow = deny = 0;
+    }
+    allow += v;
+    deny += v ^ 1;
+  }
+};
+
+__device__ __forceinline__ void kf_slow_one(const KafkaDev& T, const uint4* __restrict__ reqs,
+                                            const uint32_t* __restrict__ arena, uint8_t* __restrict__ out,
+                                            uint32_t i, uint32_t g, KfCount& cnt) {
+  const uint4* r = reqs + (size_t)i * 4;
+  const uint4 h = r[0];
+  const int key = (int16_t)(h.x & 0xFFFF), ver = (int16_t)(h.x >> 16);
+  const uint32_t kind = h.y & 0xFF, nt = (h.y >> 8) & 0xFF, red = h.y >> 16;
+  const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
+  const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
+  const uint32_t si = g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
+  const uint4 tail = *reinterpret_cast<const uint4*>(&T.sums[si].any);
+  const uint32_t v = kf_slow(T, r, arena, g, si, tail, key, ver, kind, c, nt, h.w);
+  out[i] = (uint8_t)v;
+  cnt.add(T, red, v);
+}
+
+__global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, const uint4* __restrict__ reqs, size_t n,
+                                                              const uint32_t* __restrict__ arena,
+                                                              uint8_t* __restrict__ out) {
+  __shared__ uint32_t q_i[kKafkaQueue], q_g[kKafkaQueue];
+  __shared__ uint32_t q_n;
+  if (threadIdx.x == 0) q_n = 0;
+  __syncthreads();
+  const size_t per_iter = (size_t)kKafkaThreads * kKafkaReqs;
   const size_t stride = (size_t)gridDim.x * per_iter;
-  uint32_t cred = ~0u, callow = 0, cdeny = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  KfCount cnt;
   for (size_t base = (size_t)blockIdx.x * per_iter; base < n; base += stride) {
     uint4 h[kKafkaReqs];
 #pragma unroll
     for (uint32_t u = 0; u < kKafkaReqs; ++u) {
-      const size_t i = base + u * blockDim.x + threadIdx.x;
+      const size_t i = base + u * kKafkaThreads + threadIdx.x;
       // unconditional (clamped) loads: a load under a branch gets its own
       // vmcnt(0) at the join, which would serialize the four
       const size_t ic = i < n ? i : n - 1;
@@ -391,78 +430,98 @@ __global__ __launch_bounds__(256) void kafka_kernel(KafkaDev T, const uint4* __r
 #pragma unroll
     for (uint32_t u = 0; u < kKafkaReqs; ++u) {
       const uint32_t red = h[u].y >> 16;
-      const unsigned long long k = ((unsigned long long)red << 32) | h[u].z;
-      hh[u] = hash64to32(k) & T.ghash_mask;
+      hh[u] = kf_hash(((unsigned long long)red << 32) | h[u].z) & T.ghash_mask;
       e[u] = *reinterpret_cast<const uint4*>(T.ghash + hh[u]);
       g[u] = T.dflt_group[red < T.nredirects ? red : 0];
     }
 #pragma unroll
     for (uint32_t u = 0; u < kKafkaReqs; ++u) {
-      const uint32_t red = h[u].y >> 16;
       if (h[u].z == 0) continue;
-      const unsigned long long k = ((unsigned long long)red << 32) | h[u].z;
-      uint4 x = e[u];
+      const uint32_t red = h[u].y >> 16;
+      if (e[u].x == h[u].z && e[u].y == red) {
+        g[u] = e[u].z;
+        continue;
+      }
+      if (e[u].x == ~0u && e[u].y == ~0u) continue;
+      // collision: linear probing from the next slot (a separate loop, so the
+      // first probe's registers are not turned into a pointer phi)
       uint32_t slot = hh[u];
-      for (uint32_t probe = 0; probe <= T.ghash_mask; ++probe) {
-        const unsigned long long kk = (unsigned long long)x.x | ((unsigned long long)x.y << 32);
-        if (kk == k) {
+      for (uint32_t probe = 1; probe <= T.ghash_mask; ++probe) {
+        slot = (slot + 1) & T.ghash_mask;
+        const uint4 x = *reinterpret_cast<const uint4*>(T.ghash + slot);
+        if (x.x == h[u].z && x.y == red) {
           g[u] = x.z;
           break;
         }
-        if (kk == ~0ULL) break;
-        slot = (slot + 1) & T.ghash_mask;
-        x = *reinterpret_cast<const uint4*>(T.ghash + slot);
+        if (x.x == ~0u && x.y == ~0u) break;
       }
     }
     // summaries
     uint4 tail[kKafkaReqs];
     unsigned long long vm[kKafkaReqs];
-    uint32_t si[kKafkaReqs];
 #pragma unroll
     for (uint32_t u = 0; u < kKafkaReqs; ++u) {
       const int key = (int16_t)(h[u].x & 0xFFFF);
       const uint32_t kind = h[u].y & 0xFF, nt = (h[u].y >> 8) & 0xFF;
       const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
       const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
-      si[u] = g[u] * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
-      const KafkaSumDev* su = T.sums + si[u];
+      const KafkaSumDev* su = T.sums + g[u] * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
       tail[u] = *reinterpret_cast<const uint4*>(&su->any);
       vm[u] = su->vm[c];
     }
 #pragma unroll
     for (uint32_t u = 0; u < kKafkaReqs; ++u) {
-      const size_t i = base + u * blockDim.x + threadIdx.x;
-      if (i >= n) continue;
-      const int key = (int16_t)(h[u].x & 0xFFFF);
+      const size_t i = base + u * kKafkaThreads + threadIdx.x;
       const int ver = (int16_t)(h[u].x >> 16);
       const uint32_t kind = h[u].y & 0xFF, nt = (h[u].y >> 8) & 0xFF, red = h[u].y >> 16;
       const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
-      uint32_t v = 0;
-      if (red < T.nredirects) {
-        v = ((tail[u].x >> c) & 1) | ((ver >= 0 && ver < 64) ? (uint32_t)((vm[u] >> ver) & 1) : 0u);
-        if (!v && ((c == 0 && (tail[u].x & kKfSumHasClients)) || tail[u].z || nt))
-          v = kf_slow(T, reqs + i * 4, arena, g[u], si[u], tail[u], key, ver, kind, c, nt, h[u].w);
-        if (red != cred) {
-          if (cred != ~0u) kf_flush(T.counters, cred, callow, cdeny);
-          cred = red;
-          callow = cdeny = 0;
+      const bool live = i < n;
+      const bool known = red < T.nredirects;
+      uint32_t v = known ? (((tail[u].x >> c) & 1) | ((ver >= 0 && ver < 64) ? (uint32_t)((vm[u] >> ver) & 1) : 0u))
+                         : 0u;
+      const bool slow =
+          live && known && !v && ((c == 0 && (tail[u].x & kKfSumHasClients)) || tail[u].z != 0 || nt != 0);
+      // wave-aggregated append to the block's queue
+      const unsigned long long m = __ballot(slow);
+      if (m) {
+        uint32_t qb = 0;
+        if (lane == 0) qb = atomicAdd(&q_n, (uint32_t)__popcll(m));
+        qb = __shfl(qb, 0, kWave);
+        if (slow) {
+          const uint32_t p = qb + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
+          q_i[p] = (uint32_t)i;
+          q_g[p] = g[u];
         }
-        callow += v;
-        cdeny += v ^ 1;
       }
-      out[i] = (uint8_t)v;
+      if (live && !slow) {
+        __builtin_nontemporal_store((uint8_t)v, out + i);
+        if (known) cnt.add(T, red, v);
+      }
+    }
+    __syncthreads();
+    uint32_t nq = q_n;
+    while (nq >= kKafkaThreads) {
+      const uint32_t p = nq - kKafkaThreads + threadIdx.x;
+      kf_slow_one(T, reqs, arena, out, q_i[p], q_g[p], cnt);
+      nq -= kKafkaThreads;
+      __syncthreads();
+      if (threadIdx.x == 0) q_n = nq;
+      __syncthreads();
     }
   }
+  __syncthreads();
+  if (threadIdx.x < q_n) kf_slow_one(T, reqs, arena, out, q_i[threadIdx.x], q_g[threadIdx.x], cnt);
   // the common case: every lane of the wave counted for the same redirect
-  const uint32_t first = __builtin_amdgcn_readfirstlane(cred);
-  if (__all(cred == first)) {
+  const uint32_t first = __builtin_amdgcn_readfirstlane(cnt.red);
+  if (__all(cnt.red == first)) {
+    uint32_t callow = cnt.allow, cdeny = cnt.deny;
     for (int o = 32; o > 0; o >>= 1) {
       callow += __shfl_down(callow, o, kWave);
       cdeny += __shfl_down(cdeny, o, kWave);
     }
-    if ((threadIdx.x & 63) == 0 && first != ~0u) kf_flush(T.counters, first, callow, cdeny);
-  } else if (cred != ~0u) {
-    kf_flush(T.counters, cred, callow, cdeny);
+    if (lane == 0 && first != ~0u) kf_flush(T.counters, first, callow, cdeny);
+  } else if (cnt.red != ~0u) {
+    kf_flush(T.counters, cnt.red, cnt.allow, cnt.deny);
   }
 }
 
@@ -514,8 +573,9 @@ int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
                  void* stream, int cus) {
   if (n == 0) return 0;
-  static const int occ = resident((const void*)kafka_kernel, 256, 0);
-  hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, 256 * kKafkaReqs, cus, occ)), dim3(256), 0, (hipStream_t)stream, t,
+  static const int occ = resident((const void*)kafka_kernel, kKafkaThreads, 0);
+  hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, kKafkaThreads * kKafkaReqs, cus, occ)), dim3(kKafkaThreads), 0,
+                     (hipStream_t)stream, t,
                      (const uint4*)reqs, n, arena, out);
   return (int)hipGetLastError();
 }
