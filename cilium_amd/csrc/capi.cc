@@ -866,18 +866,20 @@ int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, 
     PrefilterState& p = get_pf(*e, pf_id);
     if (p.dirty) p.rebuild(*e);
     auto ep4 = [&](uint32_t a) {
-      uint32_t mask = (uint32_t)p.ep4_occ.size() - 1, hh = ep_hash32(a) & mask;
+      if (a == 0) return p.ep4_zero;
+      uint32_t mask = (uint32_t)p.ep4_keys.size() - 1, hh = ep_hash32(a) & mask;
       for (uint32_t k = 0; k <= mask; ++k, hh = (hh + 1) & mask) {
-        if (!p.ep4_occ[hh]) return false;
         if (p.ep4_keys[hh] == a) return true;
+        if (p.ep4_keys[hh] == 0) return false;
       }
       return false;
     };
     auto ep6 = [&](uint64_t hi, uint64_t lo) {
-      uint32_t mask = (uint32_t)p.ep6_occ.size() - 1, hh = ep_hash128(hi, lo) & mask;
+      if ((hi | lo) == 0) return p.ep6_zero;
+      uint32_t mask = (uint32_t)(p.ep6_keys.size() / 2) - 1, hh = ep_hash128(hi, lo) & mask;
       for (uint32_t k = 0; k <= mask; ++k, hh = (hh + 1) & mask) {
-        if (!p.ep6_occ[hh]) return false;
         if (p.ep6_keys[2 * hh] == hi && p.ep6_keys[2 * hh + 1] == lo) return true;
+        if ((p.ep6_keys[2 * hh] | p.ep6_keys[2 * hh + 1]) == 0) return false;
       }
       return false;
     };
@@ -890,8 +892,15 @@ int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, 
       uint32_t s = __builtin_bswap32(v4[2 * i]);
       bool drop = false;
       if (p.v4_filter) {
-        uint32_t en = p.dir24[s >> 8];
-        drop = en < 2 ? en == 1 : ((p.leaves[(size_t)(en - 2) * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1);
+        const uint32_t blk = s >> 8, w = p.codes[blk >> 4], c = (w >> (2 * (blk & 15))) & 3;
+        if (c == kLpmPartial) {
+          uint32_t rank = p.grp_rank[blk >> 6];
+          for (uint32_t j = (blk >> 6) * 4; j < (blk >> 4); ++j) rank += __builtin_popcount(lpm_partials(p.codes[j]));
+          rank += __builtin_popcount(lpm_partials(w) & ((1u << (2 * (blk & 15))) - 1));
+          drop = (p.leaves[(size_t)rank * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1;
+        } else {
+          drop = c == 1;
+        }
       }
       if (!drop) drop = !ep4(v4[2 * i + 1]);
       out4[i] = drop ? CG_XDP_DROP : CG_XDP_PASS;
@@ -900,15 +909,17 @@ int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, 
       uint64_t hi = be64(v6 + 32 * i), lo = be64(v6 + 32 * i + 8);
       bool drop = false;
       if (p.v6_filter) {
-        int64_t L = p.v6_idx[hi >> 48], cnt = p.v6_idx[65536], R = std::min<int64_t>(p.v6_idx[(hi >> 48) + 1], cnt - 1);
+        const uint64_t t = hi >> (64 - p.v6_bits);
+        const int64_t cnt = p.v6_idx[(size_t)1 << p.v6_bits];
+        int64_t L = p.v6_idx[t], R = std::min<int64_t>(p.v6_idx[t + 1], cnt - 1);
         int64_t ans = -1;
         while (L <= R) {
           int64_t mid = (L + R) >> 1;
-          std::pair<uint64_t, uint64_t> lo_m{p.v6_lo[2 * mid], p.v6_lo[2 * mid + 1]};
+          std::pair<uint64_t, uint64_t> lo_m{p.v6_iv[4 * mid], p.v6_iv[4 * mid + 1]};
           if (!(std::make_pair(hi, lo) < lo_m)) ans = mid, L = mid + 1;
           else R = mid - 1;
         }
-        drop = ans >= 0 && !(std::make_pair(p.v6_hi[2 * ans], p.v6_hi[2 * ans + 1]) < std::make_pair(hi, lo));
+        drop = ans >= 0 && !(std::make_pair(p.v6_iv[4 * ans + 2], p.v6_iv[4 * ans + 3]) < std::make_pair(hi, lo));
       }
       if (!drop) drop = !ep6(be64(v6 + 32 * i + 16), be64(v6 + 32 * i + 24));
       out6[i] = drop ? CG_XDP_DROP : CG_XDP_PASS;

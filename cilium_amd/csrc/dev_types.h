@@ -82,35 +82,41 @@ CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* 
 }
 
 // ----------------------------------------------------------------- LPM ----
-// IPv4: DIR-24-8.  dir24[a >> 8]: 0 = not covered, 1 = covered,
-// v >= 2 → leaf v-2: 256-bit bitmap (4 × u64) over the last octet.
-// IPv6: disjoint covered intervals [lo, hi] sorted by lo (hi/lo as two u64,
-// big-endian word order), indexed by the top 16 address bits:
-// v6_idx[t] = first interval whose hi >= t<<112, v6_idx[65536] = count.
-// Local endpoints (cilium_lxc): open addressing, linear probing.
+// IPv4: a 2-bit code per /24 block (0 not covered, 1 covered, 2 partial), 16
+// codes per u32 word (4 MiB for the whole space, L2/MALL resident); a partial
+// block's 256-bit leaf (4 x u64 over the last octet) is found by rank: the
+// partial blocks before its 64-block group (grp_rank) plus those before it
+// inside the group (popcount over the group's four code words, one 16-B load).
+// IPv6: disjoint covered intervals sorted by lo, 32-B records {lo hi-word,
+// lo lo-word, hi hi-word, hi lo-word}, indexed by the top v6_bits address bits
+// (sized so buckets hold ~1 interval): v6_idx[t] = first interval whose
+// hi >= t << (128 - v6_bits), v6_idx[1 << v6_bits] = count.
+// Local endpoints (cilium_lxc): open addressing, linear probing, 0 = empty
+// slot (the all-zero address is a flag of its own).
+constexpr uint32_t kLpmPartial = 2;
 struct LpmDev {
-  const uint32_t* dir24;     // 1<<24 entries (nullptr: no v4 filter)
-  const uint64_t* leaves;    // 4 u64 per leaf
-  const uint32_t* v6_idx;    // 65537 entries (nullptr: no v6 filter)
-  const uint64_t* v6_lo;     // 2 u64 per interval (hi word, lo word)
-  const uint64_t* v6_hi;
-  const uint32_t* ep4_keys;  // v4 endpoint table (cap4 entries)
-  const uint8_t* ep4_occ;
+  const uint32_t* codes;     // 1<<20 words (nullptr: no v4 filter)
+  const uint32_t* grp_rank;  // 1<<18 groups of 64 blocks
+  const uint64_t* leaves;    // 4 u64 per partial block, in block order
+  const uint32_t* v6_idx;    // (1 << v6_bits) + 1 entries (nullptr: no v6 filter)
+  const uint64_t* v6_iv;     // 4 u64 per interval
+  uint32_t v6_bits;
+  const uint32_t* ep4_keys;  // v4 endpoint table (network-order addresses)
   uint32_t ep4_mask;
-  const uint64_t* ep6_keys;  // 2 u64 per entry
-  const uint8_t* ep6_occ;
+  uint32_t ep4_zero;         // 0.0.0.0 is an endpoint
+  const uint64_t* ep6_keys;  // 2 u64 per slot (hi, lo)
   uint32_t ep6_mask;
+  uint32_t ep6_zero;
   unsigned long long* counters;  // [0] drop, [1] pass
 };
 
-CG_HD inline uint32_t ep_hash32(uint32_t a) {
-  uint64_t k = a * 0x9e3779b97f4a7c15ULL;
-  return (uint32_t)(k >> 32) ^ (uint32_t)k;
-}
+CG_HD inline uint32_t ep_hash32(uint32_t a) { return l4_fin(a * kL4MulLo); }
 CG_HD inline uint32_t ep_hash128(uint64_t hi, uint64_t lo) {
-  uint64_t k = l4_hash1(hi ^ l4_hash2(lo));
-  return (uint32_t)(k >> 32) ^ (uint32_t)k;
+  return l4_fin((uint32_t)hi * kL4MulLo + (uint32_t)(hi >> 32) * kL4MulHi + (uint32_t)lo * 0xC2B2AE3Du +
+                (uint32_t)(lo >> 32) * 0x27D4EB2Fu);
 }
+// Partial-block count among the 16 2-bit codes of a word (code 2 = binary 10).
+CG_HD inline uint32_t lpm_partials(uint32_t w) { return w & ~(w << 1) & 0xAAAAAAAAu; }
 
 // ---------------------------------------------------------------- HTTP ----
 // Program = one (policy, direction, port) evaluation: Envoy's exact-port

@@ -180,95 +180,205 @@ __global__ __launch_bounds__(256) void l4_kernel(L4Dev t, const uint32_t* __rest
 }
 
 // ============================================================== LPM ======
-// check_v4 / check_v6 (bpf/bpf_xdp.c:97-156).
+// check_v4 / check_v6 (bpf/bpf_xdp.c:97-156): drop when the source is covered
+// by the CIDR maps, else pass iff the destination is a local endpoint.
 
-__device__ __forceinline__ bool ep4_has(const LpmDev& t, uint32_t a) {
-  uint32_t h = ep_hash32(a) & t.ep4_mask;
-  for (uint32_t probe = 0; probe <= t.ep4_mask; ++probe) {
-    if (!t.ep4_occ[h]) return false;
-    if (t.ep4_keys[h] == a) return true;
+__device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+// Endpoint probes continue past the first slot (the first one is issued by
+// the caller together with the other requests' loads).
+__device__ __forceinline__ bool ep4_probe_more(const LpmDev& t, uint32_t a, uint32_t h) {
+  for (uint32_t probe = 1; probe <= t.ep4_mask; ++probe) {
     h = (h + 1) & t.ep4_mask;
+    const uint32_t k = t.ep4_keys[h];
+    if (k == a) return true;
+    if (k == 0) return false;
   }
   return false;
 }
 
-__device__ __forceinline__ bool ep6_has(const LpmDev& t, uint64_t hi, uint64_t lo) {
-  uint32_t h = ep_hash128(hi, lo) & t.ep6_mask;
-  for (uint32_t probe = 0; probe <= t.ep6_mask; ++probe) {
-    if (!t.ep6_occ[h]) return false;
-    if (t.ep6_keys[2 * h] == hi && t.ep6_keys[2 * h + 1] == lo) return true;
+__device__ __forceinline__ bool ep6_probe_more(const LpmDev& t, uint64_t hi, uint64_t lo, uint32_t h) {
+  for (uint32_t probe = 1; probe <= t.ep6_mask; ++probe) {
     h = (h + 1) & t.ep6_mask;
+    const uint4 k = *reinterpret_cast<const uint4*>(t.ep6_keys + 2 * (size_t)h);
+    if (u64_of(k.x, k.y) == hi && u64_of(k.z, k.w) == lo) return true;
+    if ((k.x | k.y | k.z | k.w) == 0) return false;
   }
   return false;
 }
 
-__device__ __forceinline__ bool v4_covered(const LpmDev& t, uint32_t a /* host order */) {
-  uint32_t e = t.dir24[a >> 8];
-  if (e < 2) return e == 1;
-  const uint64_t* l = t.leaves + (size_t)(e - 2) * 4;
-  uint32_t x = a & 0xFF;
-  return (l[x >> 6] >> (x & 63)) & 1;
+// A partial /24 block: its leaf by rank (partial blocks before it).
+__device__ __forceinline__ bool v4_leaf(const LpmDev& t, uint32_t s, uint32_t w) {
+  const uint32_t blk = s >> 8;
+  const uint4 grp = *reinterpret_cast<const uint4*>(t.codes + (blk >> 6) * 4);
+  uint32_t rank = t.grp_rank[blk >> 6];
+  const uint32_t wi = (blk >> 4) & 3;
+  rank += (wi > 0 ? __popc(lpm_partials(grp.x)) : 0) + (wi > 1 ? __popc(lpm_partials(grp.y)) : 0) +
+          (wi > 2 ? __popc(lpm_partials(grp.z)) : 0);
+  rank += __popc(lpm_partials(w) & ((1u << (2 * (blk & 15))) - 1));
+  return (t.leaves[(size_t)rank * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1;
 }
 
-__device__ __forceinline__ bool lt128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
-  return ah < bh || (ah == bh && al < bl);
+__device__ __forceinline__ bool le128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+  return ah < bh || (ah == bh && al <= bl);
 }
 
-__device__ __forceinline__ bool v6_covered(const LpmDev& t, uint64_t hi, uint64_t lo) {
-  const uint32_t top = (uint32_t)(hi >> 48);
-  int64_t L = t.v6_idx[top];
-  int64_t cnt = t.v6_idx[65536];
-  int64_t R = t.v6_idx[top + 1];
-  if (R > cnt - 1) R = cnt - 1;
-  // last interval in [L, R] with lo_i <= addr
+// Binary search over intervals [L, R] for the last lo <= addr (more than two
+// candidates in the bucket: rare with ~2 buckets per interval).
+__device__ __forceinline__ int64_t v6_search(const LpmDev& t, uint64_t hi, uint64_t lo, int64_t L, int64_t R) {
   int64_t ans = -1;
   while (L <= R) {
-    int64_t m = (L + R) >> 1;
-    uint64_t mh = t.v6_lo[2 * m], ml = t.v6_lo[2 * m + 1];
-    if (!lt128(hi, lo, mh, ml)) {
+    const int64_t m = (L + R) >> 1;
+    const uint4 x = *reinterpret_cast<const uint4*>(t.v6_iv + 4 * m);
+    if (le128(u64_of(x.x, x.y), u64_of(x.z, x.w), hi, lo)) {
       ans = m;
       L = m + 1;
     } else {
       R = m - 1;
     }
   }
-  if (ans < 0) return false;
-  uint64_t eh = t.v6_hi[2 * ans], el = t.v6_hi[2 * ans + 1];
-  return !lt128(eh, el, hi, lo);
+  return ans;
 }
+
+constexpr uint32_t kLpmV4 = 4, kLpmV6 = 2;  // addresses per lane per iteration
 
 __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, const uint2* __restrict__ v4,
                                                   size_t n4, uint8_t* __restrict__ out4,
                                                   const uint4* __restrict__ v6, size_t n6,
                                                   uint8_t* __restrict__ out6) {
   uint32_t drops = 0, passes = 0;
-  const size_t total = n4 + n6;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    uint8_t v;
-    if (i < n4) {
-      uint2 r = v4[i];
-      bool drop = v4f && v4_covered(t, bswap32(r.x));
-      if (!drop) drop = !ep4_has(t, r.y);
-      v = drop ? CG_XDP_DROP : CG_XDP_PASS;
-      out4[i] = v;
-    } else {
-      size_t j = i - n4;
-      uint4 s = v6[2 * j], d = v6[2 * j + 1];
-      uint64_t shi = bswap64((uint64_t)s.x | ((uint64_t)s.y << 32));
-      uint64_t slo = bswap64((uint64_t)s.z | ((uint64_t)s.w << 32));
-      bool drop = v6f && v6_covered(t, shi, slo);
-      if (!drop) {
-        uint64_t dhi = bswap64((uint64_t)d.x | ((uint64_t)d.y << 32));
-        uint64_t dlo = bswap64((uint64_t)d.z | ((uint64_t)d.w << 32));
-        drop = !ep6_has(t, dhi, dlo);
-      }
-      v = drop ? CG_XDP_DROP : CG_XDP_PASS;
-      out6[j] = v;
+  const size_t nthreads = (size_t)gridDim.x * blockDim.x;
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // ---- IPv4: {saddr, daddr} per packet
+  for (size_t base = (size_t)blockIdx.x * blockDim.x * kLpmV4; base < n4; base += nthreads * kLpmV4) {
+    uint2 r[kLpmV4];
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV4; ++u) {
+      size_t i = base + u * blockDim.x + threadIdx.x;
+      i = i < n4 ? i : n4 - 1;  // unconditional loads (see kafka_kernel)
+      const unsigned long long x =
+          __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(v4) + i);
+      r[u] = make_uint2((uint32_t)x, (uint32_t)(x >> 32));
     }
-    drops += v == CG_XDP_DROP;
-    passes += v == CG_XDP_PASS;
+    uint32_t w[kLpmV4], ek[kLpmV4], eh[kLpmV4];
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV4; ++u) {
+      const uint32_t s = bswap32(r[u].x);
+      w[u] = v4f ? t.codes[s >> 12] : 0u;
+      eh[u] = ep_hash32(r[u].y) & t.ep4_mask;
+      ek[u] = t.ep4_keys[eh[u]];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV4; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i >= n4) continue;
+      const uint32_t s = bswap32(r[u].x);
+      const uint32_t c = (w[u] >> (2 * ((s >> 8) & 15))) & 3;
+      bool drop = c == 1;
+      if (c == kLpmPartial) drop = v4_leaf(t, s, w[u]);
+      if (!drop) {
+        const uint32_t a = r[u].y;
+        bool has;
+        if (a == 0) has = t.ep4_zero;
+        else if (ek[u] == a) has = true;
+        else if (ek[u] == 0) has = false;
+        else has = ep4_probe_more(t, a, eh[u]);
+        drop = !has;
+      }
+      const uint8_t v = drop ? CG_XDP_DROP : CG_XDP_PASS;
+      __builtin_nontemporal_store(v, out4 + i);
+      drops += drop;
+      passes += !drop;
+    }
   }
+  // ---- IPv6: {saddr[16], daddr[16]} per packet
+  const int64_t icnt = v6f ? (int64_t)t.v6_idx[(size_t)1 << t.v6_bits] : 0;
+  for (size_t base = (size_t)blockIdx.x * blockDim.x * kLpmV6; base < n6; base += nthreads * kLpmV6) {
+    uint64_t sh[kLpmV6], sl[kLpmV6], dh[kLpmV6], dl[kLpmV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV6; ++u) {
+      size_t j = base + u * blockDim.x + threadIdx.x;
+      j = j < n6 ? j : n6 - 1;
+      const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v6 + 2 * j));
+      const u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v6 + 2 * j + 1));
+      sh[u] = bswap64(u64_of(a.x, a.y));
+      sl[u] = bswap64(u64_of(a.z, a.w));
+      dh[u] = bswap64(u64_of(b.x, b.y));
+      dl[u] = bswap64(u64_of(b.z, b.w));
+    }
+    int64_t L[kLpmV6], R[kLpmV6];
+    uint4 e[kLpmV6];
+    uint32_t eh[kLpmV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV6; ++u) {
+      if (v6f) {
+        const uint64_t tb = sh[u] >> (64 - t.v6_bits);
+        L[u] = t.v6_idx[tb];
+        R[u] = t.v6_idx[tb + 1];
+      } else {
+        L[u] = 0;
+        R[u] = -1;
+      }
+      eh[u] = ep_hash128(dh[u], dl[u]) & t.ep6_mask;
+      e[u] = *reinterpret_cast<const uint4*>(t.ep6_keys + 2 * (size_t)eh[u]);
+    }
+    // the top two candidates of each bucket, loaded together
+    uint4 c1lo[kLpmV6], c1hi[kLpmV6], c0lo[kLpmV6], c0hi[kLpmV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV6; ++u) {
+      R[u] = R[u] < icnt - 1 ? R[u] : icnt - 1;
+      const int64_t r1 = R[u] >= 0 ? R[u] : 0, r0 = R[u] >= 1 ? R[u] - 1 : 0;
+      const uint4* p1 = reinterpret_cast<const uint4*>(t.v6_iv + 4 * r1);
+      const uint4* p0 = reinterpret_cast<const uint4*>(t.v6_iv + 4 * r0);
+      c1lo[u] = p1[0];
+      c1hi[u] = p1[1];
+      c0lo[u] = p0[0];
+      c0hi[u] = p0[1];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV6; ++u) {
+      const size_t j = base + u * blockDim.x + threadIdx.x;
+      if (j >= n6) continue;
+      bool drop = false;
+      if (R[u] >= L[u]) {
+        uint64_t eh_ = 0, el_ = 0;
+        bool found = false;
+        if (le128(u64_of(c1lo[u].x, c1lo[u].y), u64_of(c1lo[u].z, c1lo[u].w), sh[u], sl[u])) {
+          eh_ = u64_of(c1hi[u].x, c1hi[u].y);
+          el_ = u64_of(c1hi[u].z, c1hi[u].w);
+          found = true;
+        } else if (R[u] - 1 >= L[u]) {
+          if (le128(u64_of(c0lo[u].x, c0lo[u].y), u64_of(c0lo[u].z, c0lo[u].w), sh[u], sl[u])) {
+            eh_ = u64_of(c0hi[u].x, c0hi[u].y);
+            el_ = u64_of(c0hi[u].z, c0hi[u].w);
+            found = true;
+          } else if (R[u] - 2 >= L[u]) {
+            const int64_t ans = v6_search(t, sh[u], sl[u], L[u], R[u] - 2);
+            if (ans >= 0) {
+              const uint4 x = reinterpret_cast<const uint4*>(t.v6_iv + 4 * ans)[1];
+              eh_ = u64_of(x.x, x.y);
+              el_ = u64_of(x.z, x.w);
+              found = true;
+            }
+          }
+        }
+        drop = found && le128(sh[u], sl[u], eh_, el_);
+      }
+      if (!drop) {
+        bool has;
+        if ((dh[u] | dl[u]) == 0) has = t.ep6_zero;
+        else if (u64_of(e[u].x, e[u].y) == dh[u] && u64_of(e[u].z, e[u].w) == dl[u]) has = true;
+        else if ((e[u].x | e[u].y | e[u].z | e[u].w) == 0) has = false;
+        else has = ep6_probe_more(t, dh[u], dl[u], eh[u]);
+        drop = !has;
+      }
+      const uint8_t v = drop ? CG_XDP_DROP : CG_XDP_PASS;
+      __builtin_nontemporal_store(v, out6 + j);
+      drops += drop;
+      passes += !drop;
+    }
+  }
+  (void)tid;
   // wave reduce then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) {
     drops += __shfl_down(drops, o, kWave);
@@ -565,7 +675,9 @@ int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* 
 int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n4, uint8_t* out4,
                const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus) {
   if (n4 + n6 == 0) return 0;
-  hipLaunchKernelGGL(lpm_kernel, dim3(grid_for(n4 + n6, 256, cus, 8)), dim3(256), 0, (hipStream_t)stream, t, v4f,
+  static const int occ = resident((const void*)lpm_kernel, 256, 0);
+  hipLaunchKernelGGL(lpm_kernel, dim3(grid_for(n4 / kLpmV4 + n6 / kLpmV6 + 1, 256, cus, occ)), dim3(256), 0,
+                     (hipStream_t)stream, t, v4f,
                      v6f, (const uint2*)v4, n4, out4, (const uint4*)v6, n6, out6);
   return (int)hipGetLastError();
 }

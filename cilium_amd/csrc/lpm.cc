@@ -6,12 +6,15 @@
 // prefilter.go:77-88) or equals a /32 (/128) of the fix hash map; otherwise
 // the packet passes iff its destination is a local endpoint (cilium_lxc,
 // bpf/lib/eps.h:26-46).  Both drop sources collapse into one "covered"
-// interval set per family, which is what the device structures encode.
+// interval set per family, which is what the device structures encode
+// (dev_types.h LpmDev: 2-bit /24 codes + ranked leaves for IPv4, a
+// top-bits-indexed sorted interval array for IPv6).
 #include "lpm.h"
 
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
 #include <map>
 
 namespace cg {
@@ -50,8 +53,9 @@ void PrefilterState::rebuild(Engine& e) {
   const bool lpm4 = v4_filter && (config & CG_PF_DYN4);
   const bool lpm6 = v6_filter && (config & CG_PF_DYN6);
 
-  // ---------------- IPv4 DIR-24-8
-  dir24.clear();
+  // ---------------- IPv4: 2-bit block codes + ranked leaves
+  codes.clear();
+  grp_rank.clear();
   leaves.clear();
   if (v4_filter) {
     std::vector<std::pair<uint32_t, uint32_t>> iv;
@@ -65,39 +69,40 @@ void PrefilterState::rebuild(Engine& e) {
       for (const auto& k : maps[0]) addv4(k);
     for (const auto& k : maps[1]) addv4(k);
     std::sort(iv.begin(), iv.end());
-    dir24.assign(1u << 24, 0);
-    std::map<uint32_t, uint32_t> leaf_of;
-    auto leaf = [&](uint32_t blk) -> uint64_t* {
-      auto it = leaf_of.find(blk);
-      if (it == leaf_of.end()) {
-        it = leaf_of.emplace(blk, (uint32_t)(leaves.size() / 4)).first;
-        leaves.resize(leaves.size() + 4, 0);
-      }
-      return &leaves[(size_t)it->second * 4];
-    };
+    std::vector<uint8_t> state(1u << 24, 0);
+    std::map<uint32_t, std::array<uint64_t, 4>> part;  // block → leaf bits
     for (auto [a, b] : iv) {
       uint32_t ba = a >> 8, bb = b >> 8;
       for (uint64_t blk = ba; blk <= bb; ++blk) {
         uint32_t lo = (blk == ba) ? (a & 0xFF) : 0;
         uint32_t hi = (blk == bb) ? (b & 0xFF) : 0xFF;
-        if (dir24[blk] == 1) continue;
+        if (state[blk] == 1) continue;
         if (lo == 0 && hi == 0xFF) {
-          dir24[blk] = 1;
+          state[blk] = 1;
+          part.erase((uint32_t)blk);
           continue;
         }
-        uint64_t* l = leaf((uint32_t)blk);
+        state[blk] = kLpmPartial;
+        auto& l = part[(uint32_t)blk];
         for (uint32_t x = lo; x <= hi; ++x) l[x >> 6] |= 1ULL << (x & 63);
       }
     }
-    for (auto [blk, li] : leaf_of)
-      if (dir24[blk] != 1) dir24[blk] = li + 2;
+    codes.assign(1u << 20, 0);
+    for (uint32_t blk = 0; blk < (1u << 24); ++blk) codes[blk >> 4] |= (uint32_t)state[blk] << (2 * (blk & 15));
+    grp_rank.assign(1u << 18, 0);
+    uint32_t rank = 0;
+    for (uint32_t g = 0; g < (1u << 18); ++g) {
+      grp_rank[g] = rank;
+      for (int w = 0; w < 4; ++w) rank += __builtin_popcount(lpm_partials(codes[g * 4 + w]));
+    }
+    leaves.reserve(part.size() * 4);
+    for (const auto& [blk, l] : part) leaves.insert(leaves.end(), l.begin(), l.end());
     if (leaves.empty()) leaves.assign(4, 0);
   }
 
-  // ---------------- IPv6 intervals + top-16 index
+  // ---------------- IPv6 intervals + top-bits index
   v6_idx.clear();
-  v6_lo.clear();
-  v6_hi.clear();
+  v6_iv.clear();
   if (v6_filter) {
     std::vector<std::pair<U128, U128>> iv;
     auto addv6 = [&](const CidrKey& k) {
@@ -129,49 +134,57 @@ void PrefilterState::rebuild(Engine& e) {
       mg.push_back(x);
     }
     for (auto& x : mg) {
-      v6_lo.push_back(x.first.first);
-      v6_lo.push_back(x.first.second);
-      v6_hi.push_back(x.second.first);
-      v6_hi.push_back(x.second.second);
+      v6_iv.push_back(x.first.first);
+      v6_iv.push_back(x.first.second);
+      v6_iv.push_back(x.second.first);
+      v6_iv.push_back(x.second.second);
     }
-    v6_idx.assign(65537, 0);
+    // index bits: about two buckets per interval, 16..22 bits
+    uint32_t bits = 16;
+    while (bits < 22 && (1ull << bits) < 2 * mg.size()) ++bits;
+    v6_bits = bits;
+    v6_idx.assign((1u << bits) + 1, 0);
     size_t i = 0;
-    for (uint32_t t = 0; t < 65536; ++t) {
-      uint64_t block_start = (uint64_t)t << 48;
+    for (uint32_t t = 0; t < (1u << bits); ++t) {
+      uint64_t block_start = (uint64_t)t << (64 - bits);
       while (i < mg.size() && mg[i].second.first < block_start) ++i;
       v6_idx[t] = (uint32_t)i;
     }
-    v6_idx[65536] = (uint32_t)mg.size();
-    if (v6_lo.empty()) {
-      v6_lo.assign(2, 0);
-      v6_hi.assign(2, 0);
-    }
+    v6_idx[1u << bits] = (uint32_t)mg.size();
+    if (v6_iv.empty()) v6_iv.assign(4, 0);
   }
 
-  // ---------------- endpoint tables
+  // ---------------- endpoint tables (0 = empty slot)
   {
     uint32_t cap = next_pow2(std::max<size_t>(ep4.size() * 2, 16));
     ep4_keys.assign(cap, 0);
-    ep4_occ.assign(cap, 0);
+    ep4_zero = false;
     for (uint32_t a : ep4) {
+      if (a == 0) {
+        ep4_zero = true;
+        continue;
+      }
       uint32_t h = ep_hash32(a) & (cap - 1);
-      while (ep4_occ[h] && ep4_keys[h] != a) h = (h + 1) & (cap - 1);
+      while (ep4_keys[h] != 0 && ep4_keys[h] != a) h = (h + 1) & (cap - 1);
       ep4_keys[h] = a;
-      ep4_occ[h] = 1;
     }
   }
   {
     uint32_t cap = next_pow2(std::max<size_t>(ep6.size() * 2, 16));
     ep6_keys.assign((size_t)cap * 2, 0);
-    ep6_occ.assign(cap, 0);
+    ep6_zero = false;
     for (const auto& a : ep6) {
       U128 k = load128(a.data());
+      if (k.first == 0 && k.second == 0) {
+        ep6_zero = true;
+        continue;
+      }
       uint32_t h = ep_hash128(k.first, k.second) & (cap - 1);
-      while (ep6_occ[h] && !(ep6_keys[2 * h] == k.first && ep6_keys[2 * h + 1] == k.second))
+      while ((ep6_keys[2 * h] | ep6_keys[2 * h + 1]) != 0 &&
+             !(ep6_keys[2 * h] == k.first && ep6_keys[2 * h + 1] == k.second))
         h = (h + 1) & (cap - 1);
       ep6_keys[2 * h] = k.first;
       ep6_keys[2 * h + 1] = k.second;
-      ep6_occ[h] = 1;
     }
   }
 
@@ -179,29 +192,28 @@ void PrefilterState::rebuild(Engine& e) {
     e.set_device();
     dev = LpmDev{};
     if (v4_filter) {
-      d_dir24.upload_vec(dir24);
+      d_codes.upload_vec(codes);
+      d_grp.upload_vec(grp_rank);
       d_leaves.upload_vec(leaves);
-      dev.dir24 = d_dir24.as<uint32_t>();
+      dev.codes = d_codes.as<uint32_t>();
+      dev.grp_rank = d_grp.as<uint32_t>();
       dev.leaves = d_leaves.as<uint64_t>();
     }
     if (v6_filter) {
       d_v6_idx.upload_vec(v6_idx);
-      d_v6_lo.upload_vec(v6_lo);
-      d_v6_hi.upload_vec(v6_hi);
+      d_v6_iv.upload_vec(v6_iv);
       dev.v6_idx = d_v6_idx.as<uint32_t>();
-      dev.v6_lo = d_v6_lo.as<uint64_t>();
-      dev.v6_hi = d_v6_hi.as<uint64_t>();
+      dev.v6_iv = d_v6_iv.as<uint64_t>();
+      dev.v6_bits = v6_bits;
     }
     d_ep4k.upload_vec(ep4_keys);
-    d_ep4o.upload_vec(ep4_occ);
     d_ep6k.upload_vec(ep6_keys);
-    d_ep6o.upload_vec(ep6_occ);
     dev.ep4_keys = d_ep4k.as<uint32_t>();
-    dev.ep4_occ = d_ep4o.as<uint8_t>();
-    dev.ep4_mask = (uint32_t)ep4_occ.size() - 1;
+    dev.ep4_mask = (uint32_t)ep4_keys.size() - 1;
+    dev.ep4_zero = ep4_zero;
     dev.ep6_keys = d_ep6k.as<uint64_t>();
-    dev.ep6_occ = d_ep6o.as<uint8_t>();
-    dev.ep6_mask = (uint32_t)ep6_occ.size() - 1;
+    dev.ep6_mask = (uint32_t)(ep6_keys.size() / 2) - 1;
+    dev.ep6_zero = ep6_zero;
     if (d_counters.size() == 0) {
       d_counters.alloc(2 * sizeof(uint64_t));
       d_counters.zero();

@@ -36,15 +36,15 @@ struct PrefilterState {
 
   bool enabled(int which) const;
   // device structures
-  std::vector<uint32_t> dir24;
+  std::vector<uint32_t> codes, grp_rank;
   std::vector<uint64_t> leaves;
   std::vector<uint32_t> v6_idx;
-  std::vector<uint64_t> v6_lo, v6_hi;
+  std::vector<uint64_t> v6_iv;
+  uint32_t v6_bits = 16;
   std::vector<uint32_t> ep4_keys;
-  std::vector<uint8_t> ep4_occ;
+  bool ep4_zero = false, ep6_zero = false;
   std::vector<uint64_t> ep6_keys;
-  std::vector<uint8_t> ep6_occ;
-  DevMem d_dir24, d_leaves, d_v6_idx, d_v6_lo, d_v6_hi, d_ep4k, d_ep4o, d_ep6k, d_ep6o, d_counters;
+  DevMem d_codes, d_grp, d_leaves, d_v6_idx, d_v6_iv, d_ep4k, d_ep6k, d_counters;
   LpmDev dev{};
   bool v4_filter = false, v6_filter = false;
 

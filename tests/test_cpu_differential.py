@@ -277,3 +277,56 @@ def test_prefilter_table_builder(host, cfg):
     g4, g6 = pf.eval_host_diag(v4, v6)
     o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6)
     assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
+
+
+def dense_prefilter_case(seed: int, n: int = 50_000):
+    """Dense partial /24 blocks (so group ranks add up over many partial
+    blocks), v6 buckets with many intervals (binary-search fallback), and the
+    all-zero addresses as endpoints (the probe tables' empty-slot flags)."""
+    from cilium_amd.classifier import CIDR_DTYPE
+    rng = np.random.default_rng(seed)
+    m4, m6 = 6000, 3000
+    pfx = np.zeros(m4 + m6, CIDR_DTYPE)
+    plen4 = rng.integers(25, 33, m4)
+    a4 = (0x0A000000 | rng.integers(0, 1 << 18, m4)).astype(np.uint32)  # 10.0.0.0/14
+    a4 &= ((0xFFFFFFFF << (32 - plen4)) & 0xFFFFFFFF).astype(np.uint32)
+    pfx["family"][:m4] = 4
+    pfx["prefixlen"][:m4] = plen4
+    pfx["addr"][:m4, :4] = a4.astype(">u4").view(np.uint8).reshape(-1, 4)
+    plen6 = rng.integers(40, 129, m6)
+    a6 = np.zeros((m6, 16), np.uint8)
+    a6[:, 0], a6[:, 1] = 0x20, 0x01  # everything under 2001::/16: one crowded top-bits bucket range
+    a6[:, 2:] = rng.integers(0, 256, (m6, 14), dtype=np.uint8)
+    a6[:, 2] &= 0x03
+    for i in range(16):
+        keep = np.clip(plen6 - 8 * i, 0, 8)
+        a6[:, i] &= ((0xFF << (8 - keep)) & 0xFF).astype(np.uint8)
+    pfx["family"][m4:] = 6
+    pfx["prefixlen"][m4:] = plen6
+    pfx["addr"][m4:] = a6
+    v4 = np.zeros((n, 2), np.uint32)
+    s4 = np.where(rng.random(n) < 0.8, 0x0A000000 | rng.integers(0, 1 << 18, n),
+                  rng.integers(0, 1 << 32, n, dtype=np.uint64)).astype(np.uint32)
+    v4[:, 0] = s4.astype(">u4").view("<u4")
+    ep4 = np.concatenate([[0], rng.integers(1, 1 << 32, 500, dtype=np.uint64)]).astype(np.uint32)
+    v4[:, 1] = np.where(rng.random(n) < 0.5, ep4[rng.integers(0, len(ep4), n)], 0)
+    v6 = np.zeros((n, 32), np.uint8)
+    v6[:, :16] = a6[rng.integers(0, m6, n)]
+    v6[:, 15] ^= rng.integers(0, 256, n, dtype=np.uint8)
+    v6[:, 8] ^= np.where(rng.random(n) < 0.3, rng.integers(0, 256, n), 0).astype(np.uint8)
+    ep6 = np.concatenate([np.zeros((1, 16), np.uint8), rng.integers(0, 256, (300, 16), dtype=np.uint8)])
+    pick = rng.integers(0, len(ep6), n)
+    v6[:, 16:] = np.where((rng.random(n) < 0.5)[:, None], ep6[pick], 0)
+    return pfx, v4, v6, ep4, ep6
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_prefilter_dense_partials(host, seed):
+    pfx, v4, v6, ep4, ep6 = dense_prefilter_case(seed)
+    pf = host.prefilter(dyn4=True, dyn6=True, max_lpm=1 << 20)
+    pf.insert(0, pfx)
+    pf.set_endpoints(ep4, ep6)
+    g4, g6 = pf.eval_host_diag(v4, v6)
+    o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
+    assert 0.05 < (o4 == 1).mean() < 0.95 and 0.05 < (o6 == 1).mean() < 0.95

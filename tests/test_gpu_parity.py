@@ -133,6 +133,20 @@ def test_prefilter_parity(gpu, dyn):
     assert (o4 == 1).any() and (o4 == 2).any() and (o6 == 1).any() and (o6 == 2).any()
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_prefilter_dense_partials(gpu, seed):
+    """Rank over many partial /24 blocks, crowded IPv6 buckets (binary
+    search), all-zero endpoint addresses (cases of the CPU differential)."""
+    from test_cpu_differential import dense_prefilter_case
+    pfx, v4, v6, ep4, ep6 = dense_prefilter_case(seed, n=400_000)
+    pf = gpu.prefilter(dyn4=True, dyn6=True, max_lpm=1 << 20)
+    pf.insert(0, pfx)
+    pf.set_endpoints(ep4, ep6)
+    g4, g6 = pf.verdicts(v4, v6)
+    o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6, nthreads=8)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
+
+
 def test_prefilter_edges(gpu):
     pf = gpu.prefilter(dyn4=True, dyn6=True)
     pf.insert(0, ["0.0.0.0/1", "10.0.0.0/8", "192.168.1.128/25", "::/1", "2001:db8::/32", "fe80::1/128"])
