@@ -892,14 +892,20 @@ int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, 
       uint32_t s = __builtin_bswap32(v4[2 * i]);
       bool drop = false;
       if (p.v4_filter) {
-        const uint32_t blk = s >> 8, w = p.codes[blk >> 4], c = (w >> (2 * (blk & 15))) & 3;
-        if (c == kLpmPartial) {
-          uint32_t rank = p.grp_rank[blk >> 6];
-          for (uint32_t j = (blk >> 6) * 4; j < (blk >> 4); ++j) rank += __builtin_popcount(lpm_partials(p.codes[j]));
-          rank += __builtin_popcount(lpm_partials(w) & ((1u << (2 * (blk & 15))) - 1));
-          drop = (p.leaves[(size_t)rank * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1;
+        const uint32_t q = s >> 16, tw = p.top[q >> 4], tc = (tw >> (2 * (q & 15))) & 3;
+        if (tc == kLpmPartial) {
+          const uint32_t m = p.top_rank[q >> 4] + __builtin_popcount(lpm_partials(tw) & ((1u << (2 * (q & 15))) - 1));
+          const uint32_t k = (s >> 8) & 255, w = p.mid[(size_t)m * 16 + (k >> 4)], c = (w >> (2 * (k & 15))) & 3;
+          if (c == kLpmPartial) {
+            uint32_t rank = p.leaf_base[m];
+            for (uint32_t j = 0; j < (k >> 4); ++j) rank += __builtin_popcount(lpm_partials(p.mid[(size_t)m * 16 + j]));
+            rank += __builtin_popcount(lpm_partials(w) & ((1u << (2 * (k & 15))) - 1));
+            drop = (p.leaves[(size_t)rank * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1;
+          } else {
+            drop = c == 1;
+          }
         } else {
-          drop = c == 1;
+          drop = tc == 1;
         }
       }
       if (!drop) drop = !ep4(v4[2 * i + 1]);

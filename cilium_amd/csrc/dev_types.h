@@ -82,11 +82,12 @@ CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* 
 }
 
 // ----------------------------------------------------------------- LPM ----
-// IPv4: a 2-bit code per /24 block (0 not covered, 1 covered, 2 partial), 16
-// codes per u32 word (4 MiB for the whole space, L2/MALL resident); a partial
-// block's 256-bit leaf (4 x u64 over the last octet) is found by rank: the
-// partial blocks before its 64-block group (grp_rank) plus those before it
-// inside the group (popcount over the group's four code words, one 16-B load).
+// IPv4: two levels of 2-bit codes (0 not covered, 1 covered, 2 mixed/partial),
+// 16 per u32 word.  Level 1: one code per /16 (16 KiB, cache resident).
+// Level 2, only for mixed /16s (ranked by popcount over level 1 plus
+// top_rank per word): the 256 /24 codes of the /16 in one 64-B chunk.  A
+// partial /24's 256-bit leaf (4 x u64 over the last octet) is leaf_base of its
+// /16 plus the partial /24s before it in the chunk.
 // IPv6: disjoint covered intervals sorted by lo, 32-B records {lo hi-word,
 // lo lo-word, hi hi-word, hi lo-word}, indexed by the top v6_bits address bits
 // (sized so buckets hold ~1 interval): v6_idx[t] = first interval whose
@@ -95,9 +96,11 @@ CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* 
 // slot (the all-zero address is a flag of its own).
 constexpr uint32_t kLpmPartial = 2;
 struct LpmDev {
-  const uint32_t* codes;     // 1<<20 words (nullptr: no v4 filter)
-  const uint32_t* grp_rank;  // 1<<18 groups of 64 blocks
-  const uint64_t* leaves;    // 4 u64 per partial block, in block order
+  const uint32_t* top;       // 4096 words: /16 codes (nullptr: no v4 filter)
+  const uint32_t* top_rank;  // 4096: mixed /16s before each word
+  const uint32_t* mid;       // 16 words per mixed /16: its /24 codes
+  const uint32_t* leaf_base; // per mixed /16: partial /24s before it
+  const uint64_t* leaves;    // 4 u64 per partial /24, in address order
   const uint32_t* v6_idx;    // (1 << v6_bits) + 1 entries (nullptr: no v6 filter)
   const uint64_t* v6_iv;     // 4 u64 per interval
   uint32_t v6_bits;

@@ -207,15 +207,26 @@ __device__ __forceinline__ bool ep6_probe_more(const LpmDev& t, uint64_t hi, uin
   return false;
 }
 
-// A partial /24 block: its leaf by rank (partial blocks before it).
-__device__ __forceinline__ bool v4_leaf(const LpmDev& t, uint32_t s, uint32_t w) {
-  const uint32_t blk = s >> 8;
-  const uint4 grp = *reinterpret_cast<const uint4*>(t.codes + (blk >> 6) * 4);
-  uint32_t rank = t.grp_rank[blk >> 6];
-  const uint32_t wi = (blk >> 4) & 3;
-  rank += (wi > 0 ? __popc(lpm_partials(grp.x)) : 0) + (wi > 1 ? __popc(lpm_partials(grp.y)) : 0) +
-          (wi > 2 ? __popc(lpm_partials(grp.z)) : 0);
-  rank += __popc(lpm_partials(w) & ((1u << (2 * (blk & 15))) - 1));
+// A mixed /16: its /24 code, then for a partial /24 the leaf by rank.
+__device__ __forceinline__ bool v4_mixed(const LpmDev& t, uint32_t s, uint32_t tw) {
+  const uint32_t q = s >> 16;
+  const uint32_t m = t.top_rank[q >> 4] + __popc(lpm_partials(tw) & ((1u << (2 * (q & 15))) - 1));
+  const uint32_t k = (s >> 8) & 255;
+  const uint4* chunk = reinterpret_cast<const uint4*>(t.mid + (size_t)m * 16);
+  const uint4 cw = chunk[k >> 6];
+  const uint32_t wi = (k >> 4) & 3;
+  const uint32_t w = wi == 0 ? cw.x : wi == 1 ? cw.y : wi == 2 ? cw.z : cw.w;
+  const uint32_t c = (w >> (2 * (k & 15))) & 3;
+  if (c != kLpmPartial) return c == 1;
+  uint32_t rank = t.leaf_base[m];
+  for (uint32_t j = 0; j < (k >> 6); ++j) {
+    const uint4 x = chunk[j];
+    rank += __popc(lpm_partials(x.x)) + __popc(lpm_partials(x.y)) + __popc(lpm_partials(x.z)) +
+            __popc(lpm_partials(x.w));
+  }
+  rank += (wi > 0 ? __popc(lpm_partials(cw.x)) : 0) + (wi > 1 ? __popc(lpm_partials(cw.y)) : 0) +
+          (wi > 2 ? __popc(lpm_partials(cw.z)) : 0);
+  rank += __popc(lpm_partials(w) & ((1u << (2 * (k & 15))) - 1));
   return (t.leaves[(size_t)rank * 4 + ((s & 0xFF) >> 6)] >> (s & 63)) & 1;
 }
 
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
 #pragma unroll
     for (uint32_t u = 0; u < kLpmV4; ++u) {
       const uint32_t s = bswap32(r[u].x);
-      w[u] = v4f ? t.codes[s >> 12] : 0u;
+      w[u] = v4f ? t.top[s >> 20] : 0u;
       eh[u] = ep_hash32(r[u].y) & t.ep4_mask;
       ek[u] = t.ep4_keys[eh[u]];
     }
@@ -273,9 +284,9 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
       const size_t i = base + u * blockDim.x + threadIdx.x;
       if (i >= n4) continue;
       const uint32_t s = bswap32(r[u].x);
-      const uint32_t c = (w[u] >> (2 * ((s >> 8) & 15))) & 3;
+      const uint32_t c = (w[u] >> (2 * ((s >> 16) & 15))) & 3;
       bool drop = c == 1;
-      if (c == kLpmPartial) drop = v4_leaf(t, s, w[u]);
+      if (c == kLpmPartial) drop = v4_mixed(t, s, w[u]);
       if (!drop) {
         const uint32_t a = r[u].y;
         bool has;
@@ -327,7 +338,10 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
 #pragma unroll
     for (uint32_t u = 0; u < kLpmV6; ++u) {
       R[u] = R[u] < icnt - 1 ? R[u] : icnt - 1;
-      const int64_t r1 = R[u] >= 0 ? R[u] : 0, r0 = R[u] >= 1 ? R[u] - 1 : 0;
+      // empty bucket (most random addresses): read record 0, a cache-resident
+      // line, instead of branching around the loads
+      const bool any = R[u] >= L[u];
+      const int64_t r1 = any ? R[u] : 0, r0 = any && R[u] - 1 >= L[u] ? R[u] - 1 : 0;
       const uint4* p1 = reinterpret_cast<const uint4*>(t.v6_iv + 4 * r1);
       const uint4* p0 = reinterpret_cast<const uint4*>(t.v6_iv + 4 * r0);
       c1lo[u] = p1[0];

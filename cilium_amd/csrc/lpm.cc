@@ -7,7 +7,7 @@
 // the packet passes iff its destination is a local endpoint (cilium_lxc,
 // bpf/lib/eps.h:26-46).  Both drop sources collapse into one "covered"
 // interval set per family, which is what the device structures encode
-// (dev_types.h LpmDev: 2-bit /24 codes + ranked leaves for IPv4, a
+// (dev_types.h LpmDev: two-level 2-bit /16 and /24 codes + ranked leaves for IPv4, a
 // top-bits-indexed sorted interval array for IPv6).
 #include "lpm.h"
 
@@ -54,8 +54,10 @@ void PrefilterState::rebuild(Engine& e) {
   const bool lpm6 = v6_filter && (config & CG_PF_DYN6);
 
   // ---------------- IPv4: 2-bit block codes + ranked leaves
-  codes.clear();
-  grp_rank.clear();
+  top.clear();
+  top_rank.clear();
+  mid.clear();
+  leaf_base.clear();
   leaves.clear();
   if (v4_filter) {
     std::vector<std::pair<uint32_t, uint32_t>> iv;
@@ -87,13 +89,34 @@ void PrefilterState::rebuild(Engine& e) {
         for (uint32_t x = lo; x <= hi; ++x) l[x >> 6] |= 1ULL << (x & 63);
       }
     }
-    codes.assign(1u << 20, 0);
-    for (uint32_t blk = 0; blk < (1u << 24); ++blk) codes[blk >> 4] |= (uint32_t)state[blk] << (2 * (blk & 15));
-    grp_rank.assign(1u << 18, 0);
-    uint32_t rank = 0;
-    for (uint32_t g = 0; g < (1u << 18); ++g) {
-      grp_rank[g] = rank;
-      for (int w = 0; w < 4; ++w) rank += __builtin_popcount(lpm_partials(codes[g * 4 + w]));
+    top.assign(4096, 0);
+    top_rank.assign(4096, 0);
+    mid.clear();
+    leaf_base.clear();
+    uint32_t nmixed = 0, nleaf = 0;
+    for (uint32_t q = 0; q < 65536; ++q) {
+      if ((q & 15) == 0) top_rank[q >> 4] = nmixed;
+      bool all1 = true, all0 = true;
+      for (uint32_t k = 0; k < 256; ++k) {
+        const uint8_t st = state[(q << 8) | k];
+        all1 &= st == 1;
+        all0 &= st == 0;
+      }
+      const uint32_t code = all1 ? 1 : all0 ? 0 : kLpmPartial;
+      top[q >> 4] |= code << (2 * (q & 15));
+      if (code != kLpmPartial) continue;
+      ++nmixed;
+      leaf_base.push_back(nleaf);
+      for (uint32_t w = 0; w < 16; ++w) {
+        uint32_t word = 0;
+        for (uint32_t k = 0; k < 16; ++k) word |= (uint32_t)state[(q << 8) | (w << 4) | k] << (2 * k);
+        mid.push_back(word);
+        nleaf += __builtin_popcount(lpm_partials(word));
+      }
+    }
+    if (mid.empty()) {
+      mid.assign(16, 0);
+      leaf_base.assign(1, 0);
     }
     leaves.reserve(part.size() * 4);
     for (const auto& [blk, l] : part) leaves.insert(leaves.end(), l.begin(), l.end());
@@ -192,11 +215,15 @@ void PrefilterState::rebuild(Engine& e) {
     e.set_device();
     dev = LpmDev{};
     if (v4_filter) {
-      d_codes.upload_vec(codes);
-      d_grp.upload_vec(grp_rank);
+      d_top.upload_vec(top);
+      d_top_rank.upload_vec(top_rank);
+      d_mid.upload_vec(mid);
+      d_leaf_base.upload_vec(leaf_base);
       d_leaves.upload_vec(leaves);
-      dev.codes = d_codes.as<uint32_t>();
-      dev.grp_rank = d_grp.as<uint32_t>();
+      dev.top = d_top.as<uint32_t>();
+      dev.top_rank = d_top_rank.as<uint32_t>();
+      dev.mid = d_mid.as<uint32_t>();
+      dev.leaf_base = d_leaf_base.as<uint32_t>();
       dev.leaves = d_leaves.as<uint64_t>();
     }
     if (v6_filter) {

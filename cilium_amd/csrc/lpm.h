@@ -36,7 +36,7 @@ struct PrefilterState {
 
   bool enabled(int which) const;
   // device structures
-  std::vector<uint32_t> codes, grp_rank;
+  std::vector<uint32_t> top, top_rank, mid, leaf_base;
   std::vector<uint64_t> leaves;
   std::vector<uint32_t> v6_idx;
   std::vector<uint64_t> v6_iv;
@@ -44,7 +44,7 @@ struct PrefilterState {
   std::vector<uint32_t> ep4_keys;
   bool ep4_zero = false, ep6_zero = false;
   std::vector<uint64_t> ep6_keys;
-  DevMem d_codes, d_grp, d_leaves, d_v6_idx, d_v6_iv, d_ep4k, d_ep6k, d_counters;
+  DevMem d_top, d_top_rank, d_mid, d_leaf_base, d_leaves, d_v6_idx, d_v6_iv, d_ep4k, d_ep6k, d_counters;
   LpmDev dev{};
   bool v4_filter = false, v6_filter = false;
 
