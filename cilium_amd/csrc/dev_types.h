@@ -143,9 +143,9 @@ struct HttpProg {
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; states >= self_lo default to themselves.
-// An accepting state's header cell holds its accept label; block[acc_off +
-// label] is the block offset of its PNPR mask (u64 words stored as u32
-// pairs, 8-byte aligned), block = cells + cell_begin.  When a program's DFA
+// An accepting state's header cell holds its accept label; the label's PNPR
+// mask (u64 words stored as u32 pairs, 8-byte aligned) is at block offset
+// acc_off + label * 2 * mask_words, block = cells + cell_begin.  When a program's DFA
 // cells stay below 0xFFFF its parts are rebased onto the block (walk_off =
 // cell_begin for every part), so the kernel walks all parts through one
 // pointer — the LDS copy.
@@ -153,7 +153,7 @@ constexpr uint32_t kProgRebased = 4;
 struct HttpPart {
   uint32_t cell_off;  // first cell of this part in cells[]
   uint32_t ncells;
-  uint32_t acc_off;   // block offset of the label table (u32 per accept label)
+  uint32_t acc_off;   // block offset of accept label 0's PNPR mask (label l: + l * 2 * mask_words)
   uint32_t start;     // start state
   uint32_t nstates;
   uint32_t self_lo;

@@ -564,10 +564,10 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       S.total_exceptions += cb.exceptions;
       S.parts.push_back(hp);
     }
-    // The block continues with each part's label table (accept label l →
-    // block offset of its PNPR mask), the label masks and the "always" mask,
-    // all block-relative u32 offsets, masks as 8-byte-aligned u64 pairs: the
-    // kernel stages the whole block into LDS with the DFA.
+    // The block continues with each part's label masks (indexed by accept
+    // label) and the "always" mask, masks as 8-byte-aligned u64 pairs at
+    // block-relative u32 offsets: the kernel stages the whole block into LDS
+    // with the DFA.
     auto put_mask = [&](const std::vector<uint64_t>& m) -> uint32_t {
       if (S.cells.size() & 1) S.cells.push_back(0);
       const uint32_t off = (uint32_t)S.cells.size() - pg.cell_begin;
@@ -577,17 +577,13 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       }
       return off;
     };
+    // each part's label masks back to back (stride 2W u32): accept label l of
+    // part i has its PNPR mask at block offset acc_off + l * 2W
     for (size_t i = 0; i < parts.size(); ++i) {
       HttpPart& hp = S.parts[pg.part_begin + i];
+      if (S.cells.size() & 1) S.cells.push_back(0);
       hp.acc_off = (uint32_t)S.cells.size() - pg.cell_begin;
-      S.cells.resize(S.cells.size() + parts[i].label_masks.size(), kNoAcc);
-    }
-    for (size_t i = 0; i < parts.size(); ++i) {
-      const uint32_t acc_at = pg.cell_begin + S.parts[pg.part_begin + i].acc_off;
-      for (size_t l = 0; l < parts[i].label_masks.size(); ++l) {
-        const uint32_t off = put_mask(parts[i].label_masks[l]);
-        S.cells[acc_at + l] = off;
-      }
+      for (size_t l = 0; l < parts[i].label_masks.size(); ++l) put_mask(parts[i].label_masks[l]);
     }
     pg.always_off = put_mask(always);
     // remote-identity table (PortNetworkPolicyRule remote sets, :90-97):

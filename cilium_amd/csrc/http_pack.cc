@@ -327,7 +327,7 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         }
         const uint32_t lab = comb_label(cells, st);
         if (lab == kCombNoLabel) continue;
-        const uint32_t a = blk[pt.acc_off + lab];
+        const uint32_t a = pt.acc_off + lab * 2 * pg.mask_words;
         for (uint32_t w = 0; w < pg.mask_words; ++w)
           if (bmask(a, w) & bmask(roff, w)) v = 1;
       }

@@ -193,7 +193,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t lab = counted[j] && st[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
-      if (lab != 0xFFFFu && !verdict[j]) verdict[j] = meets(blk, blk[pt.acc_off + lab], row[j], W);
+      if (lab != 0xFFFFu && !verdict[j]) verdict[j] = meets(blk, pt.acc_off + lab * 2 * W, row[j], W);
     }
   }
 #pragma unroll
@@ -245,7 +245,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
     const bool always = pg.flags & kProgHasAlways;
     if (lab != 0xFFFFu || always) {
       const uint32_t row = remote_row(blk, pg, meta.x);
-      if (lab != 0xFFFFu) verdict = meets(blk, blk[pt.acc_off + lab], row, pg.mask_words);
+      if (lab != 0xFFFFu) verdict = meets(blk, pt.acc_off + lab * 2 * pg.mask_words, row, pg.mask_words);
       if (!verdict && always) verdict = meets(blk, pg.always_off, row, pg.mask_words);
     }
   }
