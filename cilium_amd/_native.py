@@ -40,6 +40,7 @@ CG_DROP_FRAG_NOSUPPORT = -157
 
 CG_PF_DYN4, CG_PF_DYN6, CG_PF_FIX4, CG_PF_FIX6 = 1, 2, 4, 8
 CG_XDP_DROP, CG_XDP_PASS = 1, 2
+CG_WORLD_ID = 2
 
 CG_HTTP_TILE = 64
 CG_HTTP_UNITS = 9
@@ -99,6 +100,14 @@ SIGNATURES = {
     "cg_prefilter_set_endpoints": (C.c_int, [_u64, _u32, _p, _sz, _p, _sz]),
     "cg_prefilter_verdicts_dev": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p, _p]),
     "cg_prefilter_verdicts_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
+    "cg_ipcache_create": (C.c_int, [_u64, _u32, C.POINTER(_u32)]),
+    "cg_ipcache_destroy": (C.c_int, [_u64, _u32]),
+    "cg_ipcache_update": (C.c_int, [_u64, _u32, _p, _p, _sz]),
+    "cg_ipcache_delete": (C.c_int, [_u64, _u32, _p, _sz]),
+    "cg_ipcache_lookup": (C.c_int, [_u64, _u32, _p, _p]),
+    "cg_ipcache_dump": (C.c_int, [_u64, _u32, _p, _p, _sz, C.POINTER(_sz)]),
+    "cg_ipcache_resolve_dev": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p, _p]),
+    "cg_ipcache_resolve_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
     "cg_http_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_http_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_http_policy_stats": (C.c_int, [_u64, C.POINTER(_u64), _sz]),
@@ -121,6 +130,7 @@ SIGNATURES = {
     "cg_diag_http_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_diag_kafka_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
     "cg_diag_l4_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p]),
+    "cg_diag_ipcache_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
     "cg_diag_prefilter_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
 }
 

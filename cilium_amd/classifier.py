@@ -93,6 +93,10 @@ class Classifier:
                   max_lpm: int = 0, max_hash: int = 0) -> "PreFilter":
         return PreFilter(self, dyn4, dyn6, fix4, fix6, max_lpm, max_hash)
 
+    # -------------------------------------------------------- ipcache --
+    def ipcache(self, max_entries: int = 0) -> "IPCache":
+        return IPCache(self, max_entries)
+
     # ----------------------------------------------------------- HTTP --
     def update_http_policy(self, policies: list[dict] | bytes | str) -> None:
         """Install NPDS NetworkPolicies (all-or-nothing)."""
@@ -422,3 +426,84 @@ class PreFilter:
     def verdicts_dev(self, d_v4, n4: int, d_o4, d_v6, n6: int, d_o6, stream=None) -> None:
         N.check(N.lib.cg_prefilter_verdicts_dev(self.cl.h, self.id, _p(d_v4), n4, _p(d_o4), _p(d_v6), n6, _p(d_o6),
                                                 stream))
+
+
+class IPCache:
+    """pkg/maps/ipcache.Map (ipcache.go:36-130) on the device: Key {prefix,
+    family, IP} → RemoteEndpointInfo {SecurityIdentity, TunnelEndpoint}, and
+    the datapath's lookup_ip{4,6}_remote_endpoint (bpf/lib/eps.h:48-115)
+    resolved as bpf_lxc.c:509-518 (miss or identity 0 → WORLD_ID)."""
+
+    def __init__(self, cl: Classifier, max_entries: int = 0):
+        self.cl = cl
+        v = C.c_uint32()
+        N.check(N.lib.cg_ipcache_create(cl.h, max_entries, C.byref(v)))
+        self.id = v.value
+
+    @staticmethod
+    def _keys(keys) -> np.ndarray:
+        if isinstance(keys, np.ndarray):
+            return np.ascontiguousarray(keys, CIDR_DTYPE)
+        lst = [parse_cidr(k) for k in keys]
+        return np.concatenate(lst) if lst else np.zeros(0, CIDR_DTYPE)
+
+    def update(self, keys, values) -> None:
+        """Map.Update for each (Key, RemoteEndpointInfo); values: (n, 2) u32."""
+        k = self._keys(keys)
+        v = np.ascontiguousarray(values, np.uint32).reshape(-1, 2)
+        if len(k) != len(v):
+            raise ValueError("keys and values differ in length")
+        N.check(N.lib.cg_ipcache_update(self.cl.h, self.id, _p(k) if len(k) else None, _p(v) if len(v) else None,
+                                        len(k)))
+
+    def upsert(self, cidr: str, identity: int, tunnel_endpoint: int = 0) -> None:
+        self.update([cidr], [[identity, tunnel_endpoint]])
+
+    def delete(self, keys) -> None:
+        k = self._keys(keys)
+        N.check(N.lib.cg_ipcache_delete(self.cl.h, self.id, _p(k) if len(k) else None, len(k)))
+
+    def lookup(self, cidr: str) -> Optional[tuple[int, int]]:
+        k = parse_cidr(cidr)
+        v = np.zeros(2, np.uint32)
+        rc = N.lib.cg_ipcache_lookup(self.cl.h, self.id, _p(k), _p(v))
+        if rc == N.CG_NOT_FOUND:
+            return None
+        N.check(rc)
+        return int(v[0]), int(v[1])
+
+    def dump(self) -> list[tuple[str, int, int]]:
+        n = C.c_size_t()
+        N.check(N.lib.cg_ipcache_dump(self.cl.h, self.id, None, None, 0, C.byref(n)))
+        k = np.zeros(max(n.value, 1), CIDR_DTYPE)
+        v = np.zeros((max(n.value, 1), 2), np.uint32)
+        N.check(N.lib.cg_ipcache_dump(self.cl.h, self.id, _p(k), _p(v), n.value, C.byref(n)))
+        out = []
+        for c, x in zip(k[:n.value], v[:n.value]):
+            raw = bytes(c["addr"][:4]) if c["family"] == 4 else bytes(c["addr"])
+            out.append((str(ipaddress.ip_network((raw, int(c["prefixlen"])))), int(x[0]), int(x[1])))
+        return out
+
+    def resolve(self, v4: np.ndarray, v6: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """v4: u32 addresses in network order (iphdr.daddr); v6: (n6, 16) u8.
+        Returns (n4, 2) and (n6, 2) u32 {identity, tunnel_endpoint}."""
+        v4 = np.ascontiguousarray(v4, np.uint32).reshape(-1)
+        v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1, 16)
+        o4 = np.zeros((max(len(v4), 1), 2), np.uint32)
+        o6 = np.zeros((max(len(v6), 1), 2), np.uint32)
+        N.check(N.lib.cg_ipcache_resolve_host(self.cl.h, self.id, _p(v4), len(v4), _p(o4), _p(v6), len(v6), _p(o6)))
+        return o4[:len(v4)], o6[:len(v6)]
+
+    def resolve_dev(self, d_v4, n4: int, d_o4, d_v6, n6: int, d_o6, stream=None) -> None:
+        N.check(N.lib.cg_ipcache_resolve_dev(self.cl.h, self.id, _p(d_v4), n4, _p(d_o4), _p(d_v6), n6, _p(d_o6),
+                                             stream))
+
+    def eval_host_diag(self, v4: np.ndarray, v6: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """Table-builder diagnostics only: walk the ipcache tables on the CPU."""
+        v4 = np.ascontiguousarray(v4, np.uint32).reshape(-1)
+        v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1, 16)
+        o4 = np.zeros((max(len(v4), 1), 2), np.uint32)
+        o6 = np.zeros((max(len(v6), 1), 2), np.uint32)
+        N.check(N.lib.cg_diag_ipcache_eval_host(self.cl.h, self.id, _p(v4), len(v4), _p(o4), _p(v6), len(v6),
+                                                _p(o6)))
+        return o4[:len(v4)], o6[:len(v6)]

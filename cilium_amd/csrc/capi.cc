@@ -15,6 +15,7 @@
 #include "kafka.h"
 #include "kernels.h"
 #include "l4.h"
+#include "ipcache.h"
 #include "lpm.h"
 #include "regex.h"
 
@@ -56,6 +57,12 @@ int guarded(F&& f) {
 PolicyMapState& get_map(Engine& e, uint32_t id) {
   auto it = e.maps.find(id);
   if (it == e.maps.end()) fail(CG_NOT_FOUND, "unknown policy map id");
+  return *it->second;
+}
+
+IpcacheState& get_ipc(Engine& e, uint32_t id) {
+  auto it = e.ipcaches.find(id);
+  if (it == e.ipcaches.end()) fail(CG_NOT_FOUND, "unknown ipcache id");
   return *it->second;
 }
 
@@ -157,6 +164,7 @@ void cg_close(uint64_t h) {
     (void)hipStreamSynchronize((hipStream_t)e->stream);
     e->maps.clear();
     e->prefilters.clear();
+    e->ipcaches.clear();
     e->http.reset();
     e->kafka.reset();
     (void)hipStreamDestroy((hipStream_t)e->stream);
@@ -513,6 +521,168 @@ int cg_prefilter_verdicts_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, s
     dev_sync(*e, nullptr);
     if (n4) hip_check(hipMemcpy(out4, o4, n4, hipMemcpyDeviceToHost), "D2H");
     if (n6) hip_check(hipMemcpy(out6, o6, n6, hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
+// ------------------------------------------------------------- ipcache ----
+int cg_ipcache_create(uint64_t h, uint32_t max_entries, uint32_t* ipc_id) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!ipc_id) fail(CG_INVALID_ARGUMENT, "ipc_id is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto p = std::make_unique<IpcacheState>();
+    if (max_entries) p->max_entries = max_entries;
+    uint32_t id = e->next_id++;
+    e->ipcaches[id] = std::move(p);
+    *ipc_id = id;
+  });
+}
+
+int cg_ipcache_destroy(uint64_t h, uint32_t ipc_id) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    get_ipc(*e, ipc_id);
+    if (e->has_gpu()) dev_sync(*e, nullptr);
+    e->ipcaches.erase(ipc_id);
+  });
+}
+
+int cg_ipcache_update(uint64_t h, uint32_t ipc_id, const cg_cidr* keys, const cg_remote_endpoint_info* values,
+                      size_t n) {
+  return guarded([&] {
+    auto e = get(h);
+    if (n && (!keys || !values)) fail(CG_INVALID_ARGUMENT, "NULL keys/values");
+    std::lock_guard<std::mutex> lk(e->mu);
+    IpcacheState& p = get_ipc(*e, ipc_id);
+    std::map<CidrKey, IpcVal> batch;
+    for (size_t i = 0; i < n; ++i) batch[make_cidr(keys[i])] = IpcVal{values[i].sec_label, values[i].tunnel_endpoint};
+    size_t fresh = 0;
+    for (const auto& kv : batch) fresh += !p.entries.count(kv.first);
+    if (p.entries.size() + fresh > p.max_entries) fail(CG_MAP_FULL, "ipcache: map full (max_entries)");
+    // a key given twice in one batch keeps its last value, as sequential updates would
+    for (size_t i = 0; i < n; ++i) p.entries[make_cidr(keys[i])] = IpcVal{values[i].sec_label, values[i].tunnel_endpoint};
+    p.dirty = true;
+  });
+}
+
+int cg_ipcache_delete(uint64_t h, uint32_t ipc_id, const cg_cidr* keys, size_t n) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    IpcacheState& p = get_ipc(*e, ipc_id);
+    std::vector<CidrKey> ks;
+    for (size_t i = 0; i < n; ++i) {
+      CidrKey k = make_cidr(keys[i]);
+      if (!p.entries.count(k)) fail(CG_NOT_FOUND, "ipcache: no entry for key");
+      ks.push_back(k);
+    }
+    for (auto& k : ks) p.entries.erase(k);
+    p.dirty = true;
+  });
+}
+
+int cg_ipcache_lookup(uint64_t h, uint32_t ipc_id, const cg_cidr* key, cg_remote_endpoint_info* value) {
+  return guarded([&] {
+    auto e = get(h);
+    if (!key || !value) fail(CG_INVALID_ARGUMENT, "NULL key/value");
+    std::lock_guard<std::mutex> lk(e->mu);
+    IpcacheState& p = get_ipc(*e, ipc_id);
+    auto it = p.entries.find(make_cidr(*key));
+    if (it == p.entries.end()) fail(CG_NOT_FOUND, "ipcache: no entry for key");
+    value->sec_label = it->second.identity;
+    value->tunnel_endpoint = it->second.tunnel;
+  });
+}
+
+int cg_ipcache_dump(uint64_t h, uint32_t ipc_id, cg_cidr* keys, cg_remote_endpoint_info* values, size_t cap,
+                    size_t* n) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    IpcacheState& p = get_ipc(*e, ipc_id);
+    size_t i = 0;
+    for (const auto& [k, v] : p.entries) {
+      if (i >= cap) break;
+      if (keys) {
+        memset(&keys[i], 0, sizeof(cg_cidr));
+        keys[i].family = k.family;
+        keys[i].prefixlen = k.plen;
+        memcpy(keys[i].addr, k.net.data(), 16);
+      }
+      if (values) values[i] = cg_remote_endpoint_info{v.identity, v.tunnel};
+      ++i;
+    }
+    if (n) *n = p.entries.size();
+  });
+}
+
+static void ipcache_run(Engine& e, uint32_t ipc_id, const uint32_t* d_v4, size_t n4, cg_remote_endpoint_info* d_o4,
+                        const uint8_t* d_v6, size_t n6, cg_remote_endpoint_info* d_o6, void* s) {
+  e.require_gpu();
+  IpcacheState* p;
+  {
+    std::lock_guard<std::mutex> lk(e.mu);
+    p = &get_ipc(e, ipc_id);
+    if (p->dirty) p->rebuild(e);
+  }
+  e.set_device();
+  check_launch(launch_ipcache(p->dev, d_v4, n4, (IpcVal*)d_o4, d_v6, n6, (IpcVal*)d_o6, stream_of(e, s), e.cus),
+               "ipcache kernel launch");
+}
+
+int cg_ipcache_resolve_dev(uint64_t h, uint32_t ipc_id, const uint32_t* d_v4, size_t n4,
+                           cg_remote_endpoint_info* d_out4, const uint8_t* d_v6, size_t n6,
+                           cg_remote_endpoint_info* d_out6, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    ipcache_run(*e, ipc_id, d_v4, n4, d_out4, d_v6, n6, d_out6, stream);
+  });
+}
+
+int cg_ipcache_resolve_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, size_t n4,
+                            cg_remote_endpoint_info* out4, const uint8_t* v6, size_t n6,
+                            cg_remote_endpoint_info* out6) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    e->set_device();
+    HostDev a, b, c, d;
+    void* d4 = a.put(v4, n4 * 4);
+    void* d6 = b.put(v6, n6 * 16);
+    void* o4 = c.reserve(n4 * 8 + 8);
+    void* o6 = d.reserve(n6 * 8 + 8);
+    ipcache_run(*e, ipc_id, (const uint32_t*)d4, n4, (cg_remote_endpoint_info*)o4, (const uint8_t*)d6, n6,
+                (cg_remote_endpoint_info*)o6, nullptr);
+    dev_sync(*e, nullptr);
+    if (n4) hip_check(hipMemcpy(out4, o4, n4 * 8, hipMemcpyDeviceToHost), "D2H");
+    if (n6) hip_check(hipMemcpy(out6, o6, n6 * 8, hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
+// The ipcache tables walked on the host exactly as ipcache_kernel does.
+int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, size_t n4,
+                              cg_remote_endpoint_info* out4, const uint8_t* v6, size_t n6,
+                              cg_remote_endpoint_info* out6) {
+  return guarded([&] {
+    auto e = get(h);
+    std::lock_guard<std::mutex> lk(e->mu);
+    IpcacheState& p = get_ipc(*e, ipc_id);
+    if (p.dirty) p.rebuild(*e);
+    const IpcacheDev t = p.host_view();
+    for (size_t i = 0; i < n4; ++i) {
+      const IpcVal v = t.vals[ipc_v4_index(t, __builtin_bswap32(v4[i]))];
+      out4[i] = cg_remote_endpoint_info{v.identity, v.tunnel};
+    }
+    for (size_t i = 0; i < n6; ++i) {
+      uint64_t hi = 0, lo = 0;
+      for (int k = 0; k < 8; ++k) hi = hi << 8 | v6[16 * i + k];
+      for (int k = 8; k < 16; ++k) lo = lo << 8 | v6[16 * i + k];
+      const uint64_t tb = hi >> (64 - t.v6_bits);
+      const uint32_t run = ipc_v6_run(t, hi, lo, t.idx6[tb], t.idx6[tb + 1]);
+      const IpcVal v = t.vals[t.vidx6[run]];
+      out6[i] = cg_remote_endpoint_info{v.identity, v.tunnel};
+    }
   });
 }
 

@@ -47,6 +47,7 @@ class DevMem {
 
 struct PolicyMapState;
 struct PrefilterState;
+struct IpcacheState;
 struct HttpSnapshot;
 struct KafkaSnapshot;
 
@@ -60,6 +61,7 @@ struct Engine {
   uint32_t next_id = 1;
   std::map<uint32_t, std::unique_ptr<PolicyMapState>> maps;
   std::map<uint32_t, std::unique_ptr<PrefilterState>> prefilters;
+  std::map<uint32_t, std::unique_ptr<IpcacheState>> ipcaches;
   std::shared_ptr<HttpSnapshot> http;
   std::shared_ptr<KafkaSnapshot> kafka;
 

@@ -1,0 +1,181 @@
+// ipcache.cc — device structures for the IP → identity longest-prefix map.
+//
+// With HAVE_LPM_MAP_TYPE the datapath asks the kernel LPM trie for the
+// longest prefix covering the address (ipcache_lookup{4,6} with a full-length
+// key, bpf/lib/eps.h:111-114); without it, it probes the configured prefix
+// lengths from long to short (LPM_LOOKUP_FN, eps.h:86-108).  Both return the
+// entry of the longest covering prefix.  The callers then take sec_label and
+// tunnel_endpoint if the entry exists and sec_label != 0, else WORLD_ID
+// (bpf_lxc.c:509-518, :202-211).  The tables below store that resolved pair.
+#include "ipcache.h"
+
+#include <algorithm>
+#include <map>
+#include <tuple>
+
+namespace cg {
+
+namespace {
+
+using U128 = std::pair<uint64_t, uint64_t>;  // (high word, low word)
+
+U128 key128(const CidrKey& k) {
+  uint64_t hi = 0, lo = 0;
+  for (int i = 0; i < 8; ++i) hi = hi << 8 | k.net[i];
+  for (int i = 8; i < 16; ++i) lo = lo << 8 | k.net[i];
+  return {hi, lo};
+}
+
+U128 last128(U128 lo, int plen) {
+  const int host = 128 - plen;
+  if (host >= 64) {
+    lo.second = ~0ULL;
+    lo.first |= host == 128 ? ~0ULL : ((1ULL << (host - 64)) - 1);
+  } else if (host > 0) {
+    lo.second |= (1ULL << host) - 1;
+  }
+  return lo;
+}
+
+}  // namespace
+
+void IpcacheState::build_tables() {
+  // value table: index 0 = {WORLD_ID, 0} (no entry, or sec_label == 0)
+  vals.assign(1, IpcVal{kWorldId, 0});
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> vid;
+  auto value_index = [&](const IpcVal& v) -> uint32_t {
+    if (v.identity == 0) return 0;
+    auto [it, fresh] = vid.emplace(std::make_pair(v.identity, v.tunnel), (uint32_t)vals.size());
+    if (fresh) vals.push_back(v);
+    return it->second;
+  };
+
+  // ---- IPv4: paint prefixes in increasing length, so a range being painted
+  // never holds a pointer below the prefix's own level.
+  std::vector<std::tuple<int, uint32_t, uint32_t>> v4;  // plen, net (host order), value index
+  std::vector<std::tuple<U128, int, uint32_t>> v6;      // start, plen, value index
+  for (const auto& [k, v] : entries) {
+    const uint32_t vi = value_index(v);
+    if (k.family == 4)
+      v4.emplace_back(k.plen, (uint32_t)k.net[0] << 24 | k.net[1] << 16 | k.net[2] << 8 | k.net[3], vi);
+    else
+      v6.emplace_back(key128(k), k.plen, vi);
+  }
+  std::sort(v4.begin(), v4.end());
+  l16.assign(65536, 0);
+  chunks.clear();
+  auto child = [&](uint32_t& e) -> uint32_t {
+    if (!(e & kIpcPtr)) {
+      const uint32_t c = (uint32_t)(chunks.size() / 256);
+      if (c >= kIpcPtr) fail(CG_MAP_FULL, "ipcache: too many trie chunks");
+      chunks.insert(chunks.end(), 256, e);  // inherits the shorter prefix's value
+      e = kIpcPtr | c;
+    }
+    return e & ~kIpcPtr;
+  };
+  for (auto [plen, net, vi] : v4) {
+    if (plen <= 16) {
+      const uint32_t q = net >> 16, n = 1u << (16 - plen);
+      std::fill(l16.begin() + q, l16.begin() + q + n, vi);
+    } else if (plen <= 24) {
+      const uint32_t c = child(l16[net >> 16]);
+      const uint32_t k = (net >> 8) & 255, n = 1u << (24 - plen);
+      std::fill(chunks.begin() + (size_t)c * 256 + k, chunks.begin() + (size_t)c * 256 + k + n, vi);
+    } else {
+      const uint32_t c = child(l16[net >> 16]);
+      uint32_t e = chunks[(size_t)c * 256 + ((net >> 8) & 255)];
+      const uint32_t d = child(e);  // may grow chunks: write the entry back by index
+      chunks[(size_t)c * 256 + ((net >> 8) & 255)] = e;
+      const uint32_t k = net & 255, n = 1u << (32 - plen);
+      std::fill(chunks.begin() + (size_t)d * 256 + k, chunks.begin() + (size_t)d * 256 + k + n, vi);
+    }
+  }
+  if (chunks.empty()) chunks.assign(256, 0);
+
+  // ---- IPv6: sweep the nested prefix intervals into runs of one value.
+  std::sort(v6.begin(), v6.end(), [](const auto& a, const auto& b) {
+    return std::get<0>(a) != std::get<0>(b) ? std::get<0>(a) < std::get<0>(b) : std::get<1>(a) < std::get<1>(b);
+  });
+  std::vector<std::pair<U128, uint32_t>> runs{{U128{0, 0}, 0}};
+  auto emit = [&](U128 pos, uint32_t v) {
+    if (runs.back().first == pos) {
+      runs.back().second = v;
+      if (runs.size() > 1 && runs[runs.size() - 2].second == v) runs.pop_back();
+      return;
+    }
+    if (runs.back().second != v) runs.push_back({pos, v});
+  };
+  const U128 kMax{~0ULL, ~0ULL};
+  std::vector<std::pair<U128, uint32_t>> open;  // (last address, value)
+  auto close_one = [&] {
+    const U128 end = open.back().first;
+    open.pop_back();
+    if (end != kMax) {
+      U128 nx = end;
+      if (++nx.second == 0) ++nx.first;
+      emit(nx, open.empty() ? 0 : open.back().second);
+    }
+  };
+  for (const auto& [lo, plen, vi] : v6) {
+    while (!open.empty() && open.back().first < lo) close_one();
+    emit(lo, vi);
+    open.push_back({last128(lo, plen), vi});
+  }
+  while (!open.empty()) close_one();
+  keys6.clear();
+  vidx6.clear();
+  for (const auto& [pos, v] : runs) {
+    keys6.push_back(pos.first);
+    keys6.push_back(pos.second);
+    vidx6.push_back(v);
+  }
+  uint32_t bits = 16;
+  while (bits < 22 && (1ull << bits) < 2 * runs.size()) ++bits;
+  v6_bits = bits;
+  idx6.assign((1u << bits) + 1, 0);
+  size_t r = 0;
+  for (uint32_t t = 0; t < (1u << bits); ++t) {
+    const U128 start{(uint64_t)t << (64 - bits), 0};
+    while (r + 1 < runs.size() && runs[r + 1].first <= start) ++r;
+    idx6[t] = (uint32_t)r;
+  }
+  idx6[1u << bits] = (uint32_t)runs.size() - 1;
+}
+
+IpcacheDev IpcacheState::host_view() const {
+  IpcacheDev v{};
+  v.l16 = l16.data();
+  v.chunks = chunks.data();
+  v.vals = vals.data();
+  v.idx6 = idx6.data();
+  v.keys6 = keys6.data();
+  v.vidx6 = vidx6.data();
+  v.v6_bits = v6_bits;
+  v.nruns6 = (uint32_t)vidx6.size();
+  return v;
+}
+
+void IpcacheState::rebuild(Engine& e) {
+  build_tables();
+  if (e.has_gpu()) {
+    e.set_device();
+    d_l16.upload_vec(l16);
+    d_chunks.upload_vec(chunks);
+    d_vals.upload_vec(vals);
+    d_idx6.upload_vec(idx6);
+    d_keys6.upload_vec(keys6);
+    d_vidx6.upload_vec(vidx6);
+    dev = IpcacheDev{};
+    dev.l16 = d_l16.as<uint32_t>();
+    dev.chunks = d_chunks.as<uint32_t>();
+    dev.vals = d_vals.as<IpcVal>();
+    dev.idx6 = d_idx6.as<uint32_t>();
+    dev.keys6 = d_keys6.as<uint64_t>();
+    dev.vidx6 = d_vidx6.as<uint32_t>();
+    dev.v6_bits = v6_bits;
+    dev.nruns6 = (uint32_t)vidx6.size();
+  }
+  dirty = false;
+}
+
+}  // namespace cg

@@ -1,0 +1,34 @@
+// ipcache.h — the IP → security-identity map (cilium_ipcache,
+// bpf/lib/maps.h:135-159; Go side pkg/maps/ipcache/ipcache.go:36-130) and its
+// device longest-prefix structures (dev_types.h IpcacheDev).
+#pragma once
+
+#include <map>
+#include <vector>
+
+#include "dev_types.h"
+#include "engine.h"
+#include "lpm.h"
+
+namespace cg {
+
+struct IpcacheState {
+  uint32_t max_entries = 512000;  // ipcache.go:36 MaxEntries, node_config.h:61
+  // key {family, prefixlen, masked address} → RemoteEndpointInfo {sec_label, tunnel_endpoint}
+  std::map<CidrKey, IpcVal> entries;
+  bool dirty = true;
+
+  // host copies of the device tables (also walked by cg_diag_ipcache_eval_host)
+  std::vector<uint32_t> l16, chunks, idx6, vidx6;
+  std::vector<IpcVal> vals;
+  std::vector<uint64_t> keys6;
+  uint32_t v6_bits = 16;
+  DevMem d_l16, d_chunks, d_vals, d_idx6, d_keys6, d_vidx6;
+  IpcacheDev dev{};
+
+  void build_tables();
+  IpcacheDev host_view() const;
+  void rebuild(Engine& e);
+};
+
+}  // namespace cg

@@ -15,6 +15,8 @@ int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* 
                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus);
 int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
                 void* stream, int cus);
+int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
+                   IpcVal* out6, void* stream, int cus);
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
                  void* stream, int cus);
 

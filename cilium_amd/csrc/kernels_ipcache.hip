@@ -1,0 +1,115 @@
+// kernels_ipcache.hip — lookup_ip{4,6}_remote_endpoint over a batch
+// (bpf/lib/eps.h:48-115) with the callers' resolution (bpf_lxc.c:509-518):
+// address → {security identity, tunnel endpoint}.
+//
+// Integer work bound by the input/output stream plus dependent table loads
+// (IPv4: /16 entry, up to two 1-KiB chunks, the value; IPv6: two index words,
+// a short binary search over 16-B run keys, the value).  Each lane resolves
+// several addresses with every level's loads issued for all of them before
+// the next level, so a wave keeps 4 (v4) / 2 (v6) independent chains in
+// flight.
+#include <hip/hip_runtime.h>
+
+#include "dev_types.h"
+#include "kernels.h"
+
+namespace cg {
+
+namespace {
+
+constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;  // addresses per lane per iteration
+constexpr int kIpcThreads = 256;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+__device__ __forceinline__ void store_val(const IpcacheDev& t, uint32_t vi, IpcVal* out) {
+  const unsigned long long v = *reinterpret_cast<const unsigned long long*>(t.vals + vi);
+  __builtin_nontemporal_store(v, reinterpret_cast<unsigned long long*>(out));
+}
+
+__global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, const uint32_t* __restrict__ v4,
+                                                              size_t n4, IpcVal* __restrict__ out4,
+                                                              const uint4* __restrict__ v6, size_t n6,
+                                                              IpcVal* __restrict__ out6) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  // ---- IPv4 (daddr as in iphdr, network order)
+  for (size_t base = (size_t)blockIdx.x * blockDim.x * kIpcV4; base < n4; base += stride * kIpcV4) {
+    uint32_t a[kIpcV4], e[kIpcV4];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV4; ++u) {
+      size_t i = base + u * blockDim.x + threadIdx.x;
+      i = i < n4 ? i : n4 - 1;  // unconditional loads: no vmcnt(0) under a branch
+      a[u] = __builtin_bswap32(__builtin_nontemporal_load(v4 + i));
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV4; ++u) e[u] = t.l16[a[u] >> 16];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV4; ++u)
+      if (e[u] & kIpcPtr) e[u] = t.chunks[(size_t)(e[u] & ~kIpcPtr) * 256 + ((a[u] >> 8) & 255)];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV4; ++u)
+      if (e[u] & kIpcPtr) e[u] = t.chunks[(size_t)(e[u] & ~kIpcPtr) * 256 + (a[u] & 255)];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV4; ++u) {
+      const size_t i = base + u * blockDim.x + threadIdx.x;
+      if (i < n4) store_val(t, e[u], out4 + i);
+    }
+  }
+  // ---- IPv6 (16 address bytes, network order)
+  for (size_t base = (size_t)blockIdx.x * blockDim.x * kIpcV6; base < n6; base += stride * kIpcV6) {
+    uint64_t hi[kIpcV6], lo[kIpcV6];
+    uint32_t L[kIpcV6], R[kIpcV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV6; ++u) {
+      size_t j = base + u * blockDim.x + threadIdx.x;
+      j = j < n6 ? j : n6 - 1;
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v6 + j));
+      hi[u] = __builtin_bswap64(u64_of(x.x, x.y));
+      lo[u] = __builtin_bswap64(u64_of(x.z, x.w));
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV6; ++u) {
+      const uint64_t tb = hi[u] >> (64 - t.v6_bits);
+      L[u] = t.idx6[tb];
+      R[u] = t.idx6[tb + 1];
+    }
+    // the bucket's last run start, loaded for every lane at once: with ~2
+    // buckets per run it settles most addresses without a search
+    uint4 kr[kIpcV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV6; ++u) kr[u] = *reinterpret_cast<const uint4*>(t.keys6 + 2 * (size_t)R[u]);
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV6; ++u) {
+      const size_t j = base + u * blockDim.x + threadIdx.x;
+      if (j >= n6) continue;
+      uint32_t run;
+      if (ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u])) run = R[u];
+      else run = ipc_v6_run(t, hi[u], lo[u], L[u], R[u] - 1);
+      store_val(t, t.vidx6[run], out6 + j);
+    }
+  }
+}
+
+int resident_blocks(const void* fn, int threads) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, 0) != hipSuccess || nb < 1) nb = 1;
+  return nb;
+}
+
+}  // namespace
+
+int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
+                   IpcVal* out6, void* stream, int cus) {
+  if (n4 + n6 == 0) return 0;
+  static const int occ = resident_blocks((const void*)ipcache_kernel, kIpcThreads);
+  size_t need = (n4 / kIpcV4 + n6 / kIpcV6 + kIpcThreads) / kIpcThreads;
+  const size_t cap = (size_t)cus * occ;
+  need = need < cap ? need : cap;
+  need = need < 1 ? 1 : need;
+  hipLaunchKernelGGL(ipcache_kernel, dim3((unsigned)need), dim3(kIpcThreads), 0, (hipStream_t)stream, t, v4, n4,
+                     out4, (const uint4*)v6, n6, out6);
+  return (int)hipGetLastError();
+}
+
+}  // namespace cg

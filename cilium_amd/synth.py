@@ -317,6 +317,85 @@ def lpm_addresses(n: int, prefixes: np.ndarray, n_eps: int = 65536, seed: int = 
     return v4, v6, ep4_be, ep6
 
 
+# ------------------------------------------- ipcache
+def ipcache_entries(n: int = 512_000, n_nodes: int = 4096, seed: int = SEED):
+    """IP → identity entries shaped like a cluster's ipcache (MaxEntries
+    512000, pkg/maps/ipcache/ipcache.go:36): 70% IPv4 / 30% IPv6.  80% of
+    the v4 (70% of the v6) entries are pod /32 (/128) addresses inside one
+    of `n_nodes` per-node pod CIDRs (/24, /64) with the node's tunnel
+    endpoint; the rest are CIDR-policy prefixes (/8–/28, /32–/120) with
+    tunnel 0.  1% of the entries carry identity 0 (resolved to WORLD_ID).
+    Returns (cg_cidr records, (n, 2) u32 {sec_label, tunnel_endpoint}),
+    duplicate keys removed."""
+    from .classifier import CIDR_DTYPE
+    rng = np.random.default_rng(seed ^ 0x1CAC)
+    n4 = int(n * 0.7)
+    n6 = n - n4
+    keys = np.zeros(n4 + n6, CIDR_DTYPE)
+    vals = np.zeros((n4 + n6, 2), np.uint32)
+    node_tun = (np.uint32(0x0AFF0000) + np.arange(n_nodes, dtype=np.uint32)).astype(">u4").view("<u4")
+    # v4
+    pod = rng.random(n4) < 0.8
+    node = rng.integers(0, n_nodes, n4)
+    node24 = (0x0A000000 | (rng.permutation(1 << 16)[:n_nodes].astype(np.uint32) << 8)).astype(np.uint32)
+    a_pod = node24[node] | rng.integers(1, 255, n4).astype(np.uint32)
+    plen_c = rng.integers(16, 29, n4)
+    a_c = rng.integers(0, 2 ** 32, n4, dtype=np.uint64).astype(np.uint32)
+    a_c &= ((0xFFFFFFFF << (32 - plen_c)) & 0xFFFFFFFF).astype(np.uint32)
+    keys["family"][:n4] = 4
+    keys["prefixlen"][:n4] = np.where(pod, 32, plen_c)
+    keys["addr"][:n4, :4] = np.where(pod, a_pod, a_c).astype(">u4").view(np.uint8).reshape(-1, 4)
+    vals[:n4, 1] = np.where(pod, node_tun[node], 0)
+    # v6
+    pod = rng.random(n6) < 0.7
+    node = rng.integers(0, n_nodes, n6)
+    node64 = rng.integers(0, 256, (n_nodes, 8), dtype=np.uint8)
+    node64[:, 0] = 0xFD
+    a6 = rng.integers(0, 256, (n6, 16), dtype=np.uint8)
+    plen6 = np.where(pod, 128, rng.integers(32, 121, n6))
+    a6[:, :8] = np.where(pod[:, None], node64[node], a6[:, :8])
+    for i in range(16):
+        keep = np.clip(plen6 - 8 * i, 0, 8)
+        a6[:, i] &= ((0xFF << (8 - keep)) & 0xFF).astype(np.uint8)
+    keys["family"][n4:] = 6
+    keys["prefixlen"][n4:] = plen6
+    keys["addr"][n4:] = a6
+    vals[n4:, 1] = np.where(pod, node_tun[node], 0)
+    vals[:, 0] = rng.integers(256, 256 + 65536, n4 + n6).astype(np.uint32)
+    vals[rng.random(n4 + n6) < 0.01, 0] = 0
+    _, first = np.unique(keys.view(np.uint8).reshape(len(keys), -1), axis=0, return_index=True)
+    first.sort()
+    return keys[first], vals[first]
+
+
+def ipcache_addresses(n: int, keys: np.ndarray, seed: int = SEED):
+    """70% v4 / 30% v6 destination addresses; half drawn inside a random
+    entry (random host bits), half uniform.  Returns (v4 u32 network order,
+    v6 (n6, 16) u8)."""
+    rng = np.random.default_rng(seed ^ 0x1CAD)
+    k4 = keys[keys["family"] == 4]
+    k6 = keys[keys["family"] == 6]
+    n4 = int(n * 0.7)
+    n6 = n - n4
+    a4 = rng.integers(0, 2 ** 32, n4, dtype=np.uint64).astype(np.uint32)
+    if len(k4):
+        inside = rng.random(n4) < 0.5
+        pick = k4[rng.integers(0, len(k4), n4)]
+        base = pick["addr"][:, :4].copy().view(">u4").reshape(-1).astype(np.uint32)
+        host = 32 - pick["prefixlen"].astype(np.int64)
+        hm = np.where(host >= 32, 0xFFFFFFFF, (1 << host) - 1).astype(np.uint32)
+        a4 = np.where(inside, base | (a4 & hm), a4).astype(np.uint32)
+    a6 = rng.integers(0, 256, (n6, 16), dtype=np.uint8)
+    if len(k6):
+        inside = rng.random(n6) < 0.5
+        pick = k6[rng.integers(0, len(k6), n6)]
+        for i in range(16):
+            keep = np.clip(pick["prefixlen"].astype(np.int64) - 8 * i, 0, 8)
+            m = ((0xFF << (8 - keep)) & 0xFF).astype(np.uint8)
+            a6[:, i] = np.where(inside, (pick["addr"][:, i] & m) | (a6[:, i] & ~m), a6[:, i])
+    return a4.astype(">u4").view("<u4").copy(), a6
+
+
 # -------------------------------------------------------- config 4: Kafka
 def kafka_policy(n_rules: int = 1000, n_topics: int = 1000, n_clients: int = 100, n_ids: int = 64,
                  seed: int = SEED):

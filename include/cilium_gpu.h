@@ -205,6 +205,48 @@ int cg_prefilter_verdicts_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, s
                                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6);
 
 /* ======================================================================== */
+/* ipcache: IP -> security identity (cilium_ipcache, bpf/lib/maps.h:135-159; */
+/* pkg/maps/ipcache/ipcache.go:36-130; lookup bpf/lib/eps.h:48-115)         */
+/* ======================================================================== */
+
+/* RemoteEndpointInfo (bpf/lib/common.h:175-178, ipcache.go:127-130). */
+typedef struct {
+  uint32_t sec_label;
+  uint32_t tunnel_endpoint;  /* as stored: the node IPv4 address bytes */
+} cg_remote_endpoint_info;
+
+/* identity the callers fall back to (bpf/node_config.h:35) */
+#define CG_WORLD_ID 2
+
+/* A cilium_ipcache map.  max_entries 0 = MaxEntries 512000 (ipcache.go:36). */
+int cg_ipcache_create(uint64_t h, uint32_t max_entries, uint32_t* ipc_id);
+int cg_ipcache_destroy(uint64_t h, uint32_t ipc_id);
+/* Map.Update of {Key, RemoteEndpointInfo} pairs (ipcache.go NewKey: prefix
+ * from the mask, address masked to it, family 4/6).  BPF_ANY semantics: an
+ * existing key is overwritten.  All-or-nothing: CG_MAP_FULL when the batch
+ * would exceed max_entries, and nothing is applied. */
+int cg_ipcache_update(uint64_t h, uint32_t ipc_id, const cg_cidr* keys,
+                      const cg_remote_endpoint_info* values, size_t n);
+/* Map.Delete; CG_NOT_FOUND (nothing deleted) if any key is absent. */
+int cg_ipcache_delete(uint64_t h, uint32_t ipc_id, const cg_cidr* keys, size_t n);
+/* Exact-key lookup (bpf map lookup of a full key); CG_NOT_FOUND if absent. */
+int cg_ipcache_lookup(uint64_t h, uint32_t ipc_id, const cg_cidr* key, cg_remote_endpoint_info* value);
+/* Map.Dump: keys in (family, prefixlen, address) order; *n gets the total. */
+int cg_ipcache_dump(uint64_t h, uint32_t ipc_id, cg_cidr* keys, cg_remote_endpoint_info* values,
+                    size_t cap, size_t* n);
+/* lookup_ip4_remote_endpoint / lookup_ip6_remote_endpoint over a batch,
+ * resolved as bpf_lxc.c:509-518 does: the longest covering prefix's
+ * {sec_label, tunnel_endpoint} if it exists and sec_label != 0, else
+ * {CG_WORLD_ID, 0}.  v4: n4 u32 addresses (network order, as iphdr.daddr);
+ * v6: n6 16-byte addresses.  out: one cg_remote_endpoint_info each. */
+int cg_ipcache_resolve_dev(uint64_t h, uint32_t ipc_id, const uint32_t* d_v4, size_t n4,
+                           cg_remote_endpoint_info* d_out4, const uint8_t* d_v6, size_t n6,
+                           cg_remote_endpoint_info* d_out6, void* stream);
+int cg_ipcache_resolve_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, size_t n4,
+                            cg_remote_endpoint_info* out4, const uint8_t* v6, size_t n6,
+                            cg_remote_endpoint_info* out6);
+
+/* ======================================================================== */
 /* HTTP L7: Envoy cilium.l7policy — envoy/cilium_network_policy.h:40-237,    */
 /* envoy/cilium_l7policy.cc:127-182                                          */
 /* ======================================================================== */
@@ -367,6 +409,10 @@ int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
                             const uint32_t* arena, size_t arena_len, uint8_t* out);
 int cg_diag_l4_eval_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, size_t n,
                          int32_t* verdicts);
+/* The ipcache tables walked on the host exactly as ipcache_kernel does. */
+int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, size_t n4,
+                              cg_remote_endpoint_info* out4, const uint8_t* v6, size_t n6,
+                              cg_remote_endpoint_info* out6);
 int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, size_t n4,
                                 uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6);
 

@@ -32,6 +32,7 @@ def _load():
     lib.or_last_error.restype = C.c_char_p
     lib.or_l4.argtypes = [p, p, sz, p, sz, p, p, p]
     lib.or_prefilter.argtypes = [u32, p, sz, p, sz, p, sz, p, sz, p, p, sz, p, C.c_int]
+    lib.or_ipcache.argtypes = [p, p, sz, p, sz, p, p, sz, p, C.c_int]
     lib.or_http_load.restype = p
     lib.or_http_load.argtypes = [C.c_char_p, sz]
     lib.or_http_free.argtypes = [p]
@@ -84,6 +85,24 @@ def prefilter(config: int, cidrs: np.ndarray, ep4: np.ndarray, ep6: np.ndarray, 
     o6 = np.zeros(max(n6, 1), np.uint8)
     lib().or_prefilter(config, _ptr(cidrs), len(cidrs), _ptr(ep4), len(ep4), _ptr(ep6), len(ep6) // 16,
                        _ptr(v4), n4, _ptr(o4), _ptr(v6), n6, _ptr(o6), nthreads)
+    return o4[:n4], o6[:n6]
+
+
+# ------------------------------------------------------------- ipcache ----
+def ipcache(keys: np.ndarray, vals: np.ndarray, v4: np.ndarray, v6: np.ndarray, nthreads: int = 1):
+    """lookup_ip{4,6}_remote_endpoint + the bpf_lxc.c:509-518 resolution.
+
+    keys: CIDR_DTYPE records; vals: (n, 2) u32 {sec_label, tunnel_endpoint};
+    v4: u32 network-order addresses; v6: (n6, 16) u8.  Returns (n4, 2) and
+    (n6, 2) u32 {identity, tunnel_endpoint}."""
+    keys = np.ascontiguousarray(keys)
+    vals = np.ascontiguousarray(vals, np.uint32).reshape(-1, 2)
+    v4 = np.ascontiguousarray(v4, np.uint32).reshape(-1)
+    v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1)
+    n4, n6 = len(v4), len(v6) // 16
+    o4 = np.zeros((max(n4, 1), 2), np.uint32)
+    o6 = np.zeros((max(n6, 1), 2), np.uint32)
+    lib().or_ipcache(_ptr(keys), _ptr(vals), len(keys), _ptr(v4), n4, _ptr(o4), _ptr(v6), n6, _ptr(o6), nthreads)
     return o4[:n4], o6[:n6]
 
 

@@ -10,6 +10,7 @@
 //
 //   L4    bpf/lib/policy.h:46-110 (__policy_can_access), common.h:180-193
 //   LPM   bpf/bpf_xdp.c:88-178 (check_v4/check_v6), bpf/lib/eps.h:26-46
+//   ipcache bpf/lib/eps.h:48-115, bpf/lib/maps.h:135-159, bpf/bpf_lxc.c:509-518
 //   HTTP  envoy/cilium_network_policy.h:50-203, envoy/cilium_l7policy.cc:127-150
 //   Kafka pkg/kafka/policy.go:27-225, pkg/policy/api/kafka.go:153-293,
 //         pkg/policy/api/rule_validation.go:232-275, pkg/proxy/kafka.go:117-153,
@@ -757,6 +758,70 @@ int or_kafka_eval(void* h, size_t n, const uint32_t* redirect, const uint32_t* r
         continue;
       }
       out[i] = matches_rule(req, rules) ? 1 : 0;
+    }
+  });
+  return 0;
+}
+
+}  // extern "C"
+
+// ============================================================= ipcache ====
+// lookup_ip{4,6}_remote_endpoint as LPM_LOOKUP_FN spells it (bpf/lib/eps.h:
+// 86-108): probe the stored prefix lengths from long to short, each with the
+// address masked to that length (ipcache_lookup4 `key.ip4 &= GET_PREFIX`,
+// ipcache_lookup6 `ipv6_addr_clear_suffix`, eps.h:55-79); the first hit is the
+// entry.  The caller's resolution follows bpf_lxc.c:509-518: a hit with
+// sec_label != 0 gives {sec_label, tunnel_endpoint}, anything else
+// {WORLD_ID (node_config.h:35), 0}.
+namespace {
+
+struct IpcacheOracle {
+  // one exact-match table per prefix length, per family (the BPF map's key
+  // carries family and prefixlen, maps.h:135-148)
+  std::map<int, std::unordered_map<AddrKey, std::pair<uint32_t, uint32_t>, AddrKeyHash>, std::greater<int>> v4, v6;
+  std::pair<uint32_t, uint32_t> find(bool six, const uint8_t* a) const {
+    const auto& m = six ? v6 : v4;
+    for (const auto& [plen, tab] : m) {
+      auto it = tab.find(LpmTrie::mask(a, six ? 16 : 4, plen));
+      if (it != tab.end()) {
+        if (it->second.first) return it->second;  // info != NULL && info->sec_label
+        break;
+      }
+    }
+    return {2u, 0u};  // WORLD_ID
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+// entries: 20-byte cg_cidr {family, prefixlen, pad[2], addr[16]} + values
+// {u32 sec_label, u32 tunnel_endpoint}; later duplicates overwrite earlier ones.
+// v4: n4 u32 network-order addresses; v6: n6 x 16 bytes; out: {identity, tunnel}.
+int or_ipcache(const uint8_t* keys, const uint32_t* vals, size_t n, const uint32_t* v4, size_t n4, uint32_t* out4,
+               const uint8_t* v6, size_t n6, uint32_t* out6, int nthreads) {
+  IpcacheOracle o;
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* c = keys + 20 * i;
+    const bool six = c[0] == 6;
+    auto& m = six ? o.v6 : o.v4;
+    m[c[1]][LpmTrie::mask(c + 4, six ? 16 : 4, c[1])] = {vals[2 * i], vals[2 * i + 1]};
+  }
+  run_threads(n4, nthreads, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      uint8_t ad[4];
+      memcpy(ad, &v4[i], 4);
+      auto r = o.find(false, ad);
+      out4[2 * i] = r.first;
+      out4[2 * i + 1] = r.second;
+    }
+  });
+  run_threads(n6, nthreads, [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; ++i) {
+      auto r = o.find(true, v6 + 16 * i);
+      out6[2 * i] = r.first;
+      out6[2 * i + 1] = r.second;
     }
   });
   return 0;

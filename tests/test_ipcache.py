@@ -1,0 +1,213 @@
+"""ipcache: IP → security identity.
+
+Reference: cilium_ipcache (bpf/lib/maps.h:135-159), lookup_ip{4,6}_remote_endpoint
+(bpf/lib/eps.h:48-115) and the callers' resolution (bpf_lxc.c:509-518: a hit
+with sec_label != 0 gives {sec_label, tunnel_endpoint}, else WORLD_ID), map ops
+of pkg/maps/ipcache/ipcache.go:36-130.
+
+The reference has no unit test of this lookup (pkg/maps/ipcache has no
+_test.go); the KAT below is written from the branch structure of those lines
+— parity for it is pinned by that restatement only ("parity unpinned" at
+reference-test level).  The oracle is oracle.cc `or_ipcache` (the
+LPM_LOOKUP_FN probe order, eps.h:86-108); the product's tables are checked
+against it on the CPU (host walker of the same tables) and on the GPU.
+"""
+import ipaddress
+
+import numpy as np
+import pytest
+
+import oracle
+from cilium_amd import _native as N
+from cilium_amd import synth
+
+WORLD = N.CG_WORLD_ID
+TUN = 0x0101010A  # 10.1.1.1 stored as bytes
+
+KAT_ENTRIES = [
+    ("10.0.0.0/8", 100, 0),
+    ("10.1.0.0/16", 200, 0),
+    ("10.1.2.0/24", 0, 0),          # sec_label 0: shadows the /16, resolves to WORLD
+    ("10.1.2.3/32", 300, TUN),
+    ("192.168.0.0/31", 400, TUN),
+    ("255.255.255.255/32", 500, 0),
+    ("fd00::/8", 1100, 0),
+    ("fd00:1::/64", 1200, 0),
+    ("fd00:1::/96", 0, 0),
+    ("fd00:1::5/128", 1300, TUN),
+    ("::/0", 1400, 0),               # v6 default route
+    ("ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff/128", 1500, 0),
+]
+KAT_V4 = [
+    ("10.1.2.3", (300, TUN)), ("10.1.2.4", (WORLD, 0)), ("10.1.3.1", (200, 0)), ("10.2.0.0", (100, 0)),
+    ("10.255.255.255", (100, 0)), ("11.0.0.1", (WORLD, 0)), ("0.0.0.0", (WORLD, 0)),
+    ("192.168.0.1", (400, TUN)), ("192.168.0.2", (WORLD, 0)), ("255.255.255.255", (500, 0)),
+    ("255.255.255.254", (WORLD, 0)),
+]
+KAT_V6 = [
+    ("fd00:1::5", (1300, TUN)), ("fd00:1::6", (WORLD, 0)), ("fd00:1::1:0:0", (1200, 0)),
+    ("fd00:2::1", (1100, 0)), ("fe80::1", (1400, 0)), ("::", (1400, 0)),
+    ("ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff", (1500, 0)), ("ffff:ffff:ffff:ffff:ffff:ffff:ffff:fffe", (1400, 0)),
+]
+
+
+def _kat_arrays():
+    v4 = np.array([int.from_bytes(ipaddress.ip_address(a).packed, "little") for a, _ in KAT_V4], np.uint32)
+    v6 = np.array([list(ipaddress.ip_address(a).packed) for a, _ in KAT_V6], np.uint8)
+    e4 = np.array([x for _, x in KAT_V4], np.uint32)
+    e6 = np.array([x for _, x in KAT_V6], np.uint32)
+    return v4, v6, e4, e6
+
+
+def _kat_map(cl):
+    ic = cl.ipcache()
+    ic.update([c for c, _, _ in KAT_ENTRIES], [[i, t] for _, i, t in KAT_ENTRIES])
+    return ic
+
+
+def _kat_keys():
+    from cilium_amd.classifier import IPCache
+    k = IPCache._keys([c for c, _, _ in KAT_ENTRIES])
+    v = np.array([[i, t] for _, i, t in KAT_ENTRIES], np.uint32)
+    return k, v
+
+
+# ------------------------------------------------------------------ CPU ----
+def test_oracle_kat():
+    k, v = _kat_keys()
+    v4, v6, e4, e6 = _kat_arrays()
+    o4, o6 = oracle.ipcache(k, v, v4, v6)
+    assert np.array_equal(o4, e4)
+    assert np.array_equal(o6, e6)
+
+
+def test_tables_kat(host):
+    ic = _kat_map(host)
+    v4, v6, e4, e6 = _kat_arrays()
+    g4, g6 = ic.eval_host_diag(v4, v6)
+    assert np.array_equal(g4, e4)
+    assert np.array_equal(g6, e6)
+
+
+def test_map_ops(host):
+    ic = host.ipcache(max_entries=4)
+    ic.upsert("10.0.0.0/8", 7)
+    ic.upsert("10.0.0.1/8", 8)  # same key after masking: overwritten (BPF_ANY)
+    assert ic.lookup("10.0.0.0/8") == (8, 0)
+    assert ic.lookup("10.0.0.0/9") is None
+    ic.update(["1.2.3.4/32", "fd00::/8"], [[9, 1], [10, 0]])
+    with pytest.raises(N.CiliumGPUError) as ei:  # 3 + 2 new > 4: nothing applied
+        ic.update(["2.0.0.0/8", "3.0.0.0/8"], [[1, 0], [2, 0]])
+    assert ei.value.code == N.CG_MAP_FULL
+    assert len(ic.dump()) == 3
+    with pytest.raises(N.CiliumGPUError) as ei:  # one absent key: nothing deleted
+        ic.delete(["1.2.3.4/32", "9.9.9.9/32"])
+    assert ei.value.code == N.CG_NOT_FOUND
+    ic.delete(["1.2.3.4/32"])
+    assert ic.dump() == [("10.0.0.0/8", 8, 0), ("fd00::/8", 10, 0)]
+    # delete + re-resolve rebuilds the tables
+    g4, _ = ic.eval_host_diag(np.array([int.from_bytes(bytes([1, 2, 3, 4]), "little")], np.uint32),
+                              np.zeros((0, 16), np.uint8))
+    assert g4.tolist() == [[WORLD, 0]]
+
+
+def test_empty_map(host):
+    ic = host.ipcache()
+    v4 = np.arange(1000, dtype=np.uint32) * 4294967
+    v6 = np.random.default_rng(1).integers(0, 256, (100, 16), dtype=np.uint8)
+    g4, g6 = ic.eval_host_diag(v4, v6)
+    assert (g4 == [WORLD, 0]).all() and (g6 == [WORLD, 0]).all()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_tables_random_vs_oracle(host, seed):
+    rng = np.random.default_rng(seed)
+    k, v = synth.ipcache_entries(int(rng.integers(2000, 40000)), n_nodes=int(rng.integers(4, 300)), seed=seed)
+    a4, a6 = synth.ipcache_addresses(200_000, k, seed=seed)
+    ic = host.ipcache()
+    ic.update(k, v)
+    g4, g6 = ic.eval_host_diag(a4, a6)
+    o4, o6 = oracle.ipcache(k, v, a4, a6, nthreads=4)
+    assert np.array_equal(g4, o4)
+    assert np.array_equal(g6, o6)
+
+
+def test_tables_nested_dense(host):
+    """Deeply nested prefixes on one path (every length 0..32 / 0..128 over the
+    same address, alternating zero identities) plus their neighbours."""
+    from cilium_amd.classifier import CIDR_DTYPE
+    rng = np.random.default_rng(7)
+    base4 = bytes([172, 16, 99, 201])
+    base6 = bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    keys, vals = [], []
+    for plen in range(33):
+        keys.append(str(ipaddress.ip_network((base4, plen), strict=False)))
+        vals.append([0 if plen % 5 == 3 else 1000 + plen, plen])
+    for plen in range(129):
+        keys.append(str(ipaddress.ip_network((base6, plen), strict=False)))
+        vals.append([0 if plen % 7 == 2 else 5000 + plen, plen])
+    ic = host.ipcache()
+    ic.update(keys, vals)
+    from cilium_amd.classifier import IPCache
+    k = IPCache._keys(keys)
+    b4 = int.from_bytes(base4, "big")
+    a4 = np.array([(b4 ^ (1 << s)) for s in range(32)] + [b4], np.uint32).astype(">u4").view("<u4")
+    b6 = int.from_bytes(base6, "big")
+    a6 = np.array([list(((b6 ^ (1 << s)) % (1 << 128)).to_bytes(16, "big")) for s in range(128)] + [list(base6)],
+                  np.uint8)
+    g4, g6 = ic.eval_host_diag(a4, a6)
+    o4, o6 = oracle.ipcache(k, np.array(vals, np.uint32), a4, a6)
+    assert np.array_equal(g4, o4)
+    assert np.array_equal(g6, o6)
+    assert CIDR_DTYPE.itemsize == 20
+
+
+def test_host_handle_refuses_resolve(host):
+    ic = host.ipcache()
+    with pytest.raises(N.CiliumGPUError) as ei:
+        ic.resolve(np.zeros(4, np.uint32), np.zeros((0, 16), np.uint8))
+    assert ei.value.code == N.CG_NO_DEVICE
+
+
+# ------------------------------------------------------------------ GPU ----
+@pytest.mark.gpu
+def test_gpu_kat(gpu):
+    ic = _kat_map(gpu)
+    v4, v6, e4, e6 = _kat_arrays()
+    g4, g6 = ic.resolve(v4, v6)
+    assert np.array_equal(g4, e4)
+    assert np.array_equal(g6, e6)
+
+
+@pytest.mark.gpu
+def test_gpu_parity_full_map(gpu):
+    k, v = synth.ipcache_entries()
+    a4, a6 = synth.ipcache_addresses(2_000_000, k)
+    ic = gpu.ipcache()
+    ic.update(k, v)
+    g4, g6 = ic.resolve(a4, a6)
+    o4, o6 = oracle.ipcache(k, v, a4, a6, nthreads=16)
+    assert np.array_equal(g4, o4)
+    assert np.array_equal(g6, o6)
+
+
+@pytest.mark.gpu
+def test_gpu_empty_ragged_and_update(gpu):
+    k, v = synth.ipcache_entries(20_000, n_nodes=64, seed=5)
+    ic = gpu.ipcache()
+    g4, g6 = ic.resolve(np.zeros(0, np.uint32), np.zeros((0, 16), np.uint8))
+    assert g4.shape == (0, 2) and g6.shape == (0, 2)
+    g4, g6 = ic.resolve(np.arange(7, dtype=np.uint32), np.zeros((3, 16), np.uint8))  # empty map
+    assert (g4 == [WORLD, 0]).all() and (g6 == [WORLD, 0]).all()
+    ic.update(k, v)
+    for n in (1, 3, 255, 1025, 100_003):
+        a4, a6 = synth.ipcache_addresses(n, k, seed=n)
+        g4, g6 = ic.resolve(a4, a6)
+        o4, o6 = oracle.ipcache(k, v, a4, a6)
+        assert np.array_equal(g4, o4) and np.array_equal(g6, o6), n
+    # delete half the entries: the next resolve rebuilds the device tables
+    ic.delete(k[::2])
+    a4, a6 = synth.ipcache_addresses(100_000, k, seed=9)
+    g4, g6 = ic.resolve(a4, a6)
+    o4, o6 = oracle.ipcache(k[1::2], v[1::2], a4, a6)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)

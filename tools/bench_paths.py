@@ -4,6 +4,7 @@ configs, one JSON line each (bench.py covers config 5, the 10K-rule HTTP set):
 * L4 policymap (config 2): 16K-entry table, 100M tuples
 * CIDR prefilter (config 3): 1M mixed v4/v6 prefixes, 1B addresses
 * Kafka (config 4): 1K rules, 100M requests
+* ipcache: 512K-entry IP → identity map, 1B addresses
 
 Inputs are resident in HBM before timing; kernels are timed with HIP events
 on their stream.  Each line carries the kernel's HBM roofline (algorithmic
@@ -152,9 +153,37 @@ def bench_kafka(torch, dev, stream, cl, args, threads):
                 {"config": {"workload": "BASELINE config 4: 1K Kafka rules, 100M requests", "requests": n}})
 
 
+def bench_ipcache(torch, dev, stream, cl, args, threads):
+    import oracle
+    from cilium_amd import synth
+    k, v = synth.ipcache_entries()
+    ic = cl.ipcache()
+    ic.update(k, v)
+    D, reps = 100_000_000, 10
+    a4, a6 = synth.ipcache_addresses(D, k)
+    g4, g6 = ic.resolve(a4[:1_000_000], a6[:400_000])
+    o4, o6 = oracle.ipcache(k, v, a4[:1_000_000], a6[:400_000], nthreads=threads)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6), "ipcache results differ from the oracle"
+    d4 = tile_dev(torch, a4, reps, dev)
+    d6 = tile_dev(torch, a6, reps, dev)
+    n4, n6 = len(a4) * reps, len(a6) * reps
+    o4d = torch.empty(n4 * 2, dtype=torch.int32, device=dev)
+    o6d = torch.empty(n6 * 2, dtype=torch.int32, device=dev)
+    sec = timed(torch, stream, lambda: ic.resolve_dev(d4, n4, o4d, d6, n6, o6d, stream=stream.cuda_stream),
+                args.steps, 2)
+    bpi = (n4 * 12 + n6 * 24) / (n4 + n6)  # address in + {identity, tunnel} out
+    s4, s6 = a4[:700_000], a6[:300_000]
+    cpu = cpu_rate(lambda: oracle.ipcache(k, v, s4, s6, nthreads=threads), 1_000_000, args.cpu_seconds)
+    return line("ipcache lookups/s (lookup_ip{4,6}_remote_endpoint → identity, tunnel)", n4 + n6, sec, bpi,
+                "ipcache_kernel", cpu,
+                f"1M addresses (70% v4) of the same workload incl. the oracle's map build, {threads} threads",
+                threads, {"config": {"workload": "SURVEY 8(f) row 1: 512K-entry ipcache (MaxEntries), 1B addresses",
+                                     "entries": int(len(k)), "addresses": n4 + n6}})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--paths", default="l4,lpm,kafka")
+    ap.add_argument("--paths", default="l4,lpm,kafka,ipcache")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     args = ap.parse_args()
@@ -164,7 +193,7 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka}
+    fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()
