@@ -671,8 +671,8 @@ int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, s
     if (p.dirty) p.rebuild(*e);
     const IpcacheDev t = p.host_view();
     for (size_t i = 0; i < n4; ++i) {
-      const IpcVal v = t.vals[ipc_v4_index(t, __builtin_bswap32(v4[i]))];
-      out4[i] = cg_remote_endpoint_info{v.identity, v.tunnel};
+      const uint64_t v = ipc_v4_value(t, __builtin_bswap32(v4[i]));
+      out4[i] = cg_remote_endpoint_info{(uint32_t)v, (uint32_t)(v >> 32)};
     }
     for (size_t i = 0; i < n6; ++i) {
       uint64_t hi = 0, lo = 0;
@@ -680,8 +680,8 @@ int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, s
       for (int k = 8; k < 16; ++k) lo = lo << 8 | v6[16 * i + k];
       const uint64_t tb = hi >> (64 - t.v6_bits);
       const uint32_t run = ipc_v6_run(t, hi, lo, t.idx6[tb], t.idx6[tb + 1]);
-      const IpcVal v = t.vals[t.vidx6[run]];
-      out6[i] = cg_remote_endpoint_info{v.identity, v.tunnel};
+      const uint64_t v = t.runs6[4 * (size_t)run + 2];
+      out6[i] = cg_remote_endpoint_info{(uint32_t)v, (uint32_t)(v >> 32)};
     }
   });
 }

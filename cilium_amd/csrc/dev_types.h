@@ -290,35 +290,34 @@ struct KafkaDev {
 // callers do (bpf_lxc.c:509-518): hit with sec_label != 0 → {sec_label,
 // tunnel_endpoint}, else {WORLD_ID, 0}.
 //
-// Every table entry holds a value index into `vals`, already resolved that
-// way (vals[0] = {WORLD_ID, 0} is "no covering prefix").
-//  IPv4: 16-8-8 stride trie.  l16[a >> 16], then 256-entry chunks; an entry
-//        with bit 31 set is the index of the next level's chunk.
+// Table entries hold that resolved pair inline as a u64 (identity in the low
+// word, tunnel in the high word), so a lookup ends at its last table level.
+// A resolved identity is never 0, so identity 0 marks a pointer: the high
+// word is then the index of the next level's 256-entry chunk.
+//  IPv4: 16-8-8 stride trie.  l16[a >> 16], then 2-KiB chunks.
 //  IPv6: the prefixes partition the address space into runs with one
-//        longest-prefix value each; run starts are sorted 16-B keys (hi, lo)
-//        with a value index per run, and idx6[t] = the last run starting at or
+//        longest-prefix value each; runs are 32-B records {start hi, start lo,
+//        value, 0} sorted by start, and idx6[t] = the last run starting at or
 //        before the t-th (1 << v6_bits)-aligned block.
-constexpr uint32_t kIpcPtr = 0x80000000u;
 constexpr uint32_t kWorldId = 2;  // bpf/node_config.h:35
+constexpr uint64_t kIpcMiss = kWorldId;  // {WORLD_ID, 0}
 struct alignas(8) IpcVal {
   uint32_t identity;
   uint32_t tunnel;  // tunnel_endpoint as stored (network-order bytes)
 };
 struct IpcacheDev {
-  const uint32_t* l16;     // 65536 entries
-  const uint32_t* chunks;  // 256 entries per chunk
-  const IpcVal* vals;      // resolved {identity, tunnel_endpoint}
+  const uint64_t* l16;     // 65536 entries
+  const uint64_t* chunks;  // 256 entries per chunk
   const uint32_t* idx6;    // (1 << v6_bits) + 1
-  const uint64_t* keys6;   // 2 u64 per run (hi, lo)
-  const uint32_t* vidx6;   // value index per run
+  const uint64_t* runs6;   // 4 u64 per run
   uint32_t v6_bits;
   uint32_t nruns6;
 };
 
-CG_HD inline uint32_t ipc_v4_index(const IpcacheDev& t, uint32_t a) {  // a in host order
-  uint32_t e = t.l16[a >> 16];
-  if (e & kIpcPtr) e = t.chunks[(size_t)(e & ~kIpcPtr) * 256 + ((a >> 8) & 255)];
-  if (e & kIpcPtr) e = t.chunks[(size_t)(e & ~kIpcPtr) * 256 + (a & 255)];
+CG_HD inline uint64_t ipc_v4_value(const IpcacheDev& t, uint32_t a) {  // a in host order
+  uint64_t e = t.l16[a >> 16];
+  if ((uint32_t)e == 0) e = t.chunks[(size_t)(e >> 32) * 256 + ((a >> 8) & 255)];
+  if ((uint32_t)e == 0) e = t.chunks[(size_t)(e >> 32) * 256 + (a & 255)];
   return e;
 }
 
@@ -330,7 +329,7 @@ CG_HD inline bool ipc_le128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) 
 CG_HD inline uint32_t ipc_v6_run(const IpcacheDev& t, uint64_t hi, uint64_t lo, uint32_t L, uint32_t R) {
   while (L < R) {
     const uint32_t m = (L + R + 1) >> 1;
-    if (ipc_le128(t.keys6[2 * (size_t)m], t.keys6[2 * (size_t)m + 1], hi, lo)) L = m;
+    if (ipc_le128(t.runs6[4 * (size_t)m], t.runs6[4 * (size_t)m + 1], hi, lo)) L = m;
     else R = m - 1;
   }
   return L;

@@ -10,7 +10,6 @@
 #include "ipcache.h"
 
 #include <algorithm>
-#include <map>
 #include <tuple>
 
 namespace cg {
@@ -40,64 +39,58 @@ U128 last128(U128 lo, int plen) {
 }  // namespace
 
 void IpcacheState::build_tables() {
-  // value table: index 0 = {WORLD_ID, 0} (no entry, or sec_label == 0)
-  vals.assign(1, IpcVal{kWorldId, 0});
-  std::map<std::pair<uint32_t, uint32_t>, uint32_t> vid;
-  auto value_index = [&](const IpcVal& v) -> uint32_t {
-    if (v.identity == 0) return 0;
-    auto [it, fresh] = vid.emplace(std::make_pair(v.identity, v.tunnel), (uint32_t)vals.size());
-    if (fresh) vals.push_back(v);
-    return it->second;
+  // the resolved pair as a table entry: identity 0 (a pointer tag) never occurs
+  auto resolved = [](const IpcVal& v) -> uint64_t {
+    return v.identity == 0 ? kIpcMiss : ((uint64_t)v.tunnel << 32 | v.identity);
   };
 
   // ---- IPv4: paint prefixes in increasing length, so a range being painted
   // never holds a pointer below the prefix's own level.
-  std::vector<std::tuple<int, uint32_t, uint32_t>> v4;  // plen, net (host order), value index
-  std::vector<std::tuple<U128, int, uint32_t>> v6;      // start, plen, value index
+  std::vector<std::tuple<int, uint32_t, uint64_t>> v4;  // plen, net (host order), entry
+  std::vector<std::tuple<U128, int, uint64_t>> v6;      // start, plen, entry
   for (const auto& [k, v] : entries) {
-    const uint32_t vi = value_index(v);
     if (k.family == 4)
-      v4.emplace_back(k.plen, (uint32_t)k.net[0] << 24 | k.net[1] << 16 | k.net[2] << 8 | k.net[3], vi);
+      v4.emplace_back(k.plen, (uint32_t)k.net[0] << 24 | k.net[1] << 16 | k.net[2] << 8 | k.net[3], resolved(v));
     else
-      v6.emplace_back(key128(k), k.plen, vi);
+      v6.emplace_back(key128(k), k.plen, resolved(v));
   }
   std::sort(v4.begin(), v4.end());
-  l16.assign(65536, 0);
+  l16.assign(65536, kIpcMiss);
   chunks.clear();
-  auto child = [&](uint32_t& e) -> uint32_t {
-    if (!(e & kIpcPtr)) {
-      const uint32_t c = (uint32_t)(chunks.size() / 256);
-      if (c >= kIpcPtr) fail(CG_MAP_FULL, "ipcache: too many trie chunks");
+  auto child = [&](uint64_t& e) -> uint32_t {
+    if ((uint32_t)e != 0) {
+      const uint64_t c = chunks.size() / 256;
+      if (c > 0xFFFFFFFFull) fail(CG_MAP_FULL, "ipcache: too many trie chunks");
       chunks.insert(chunks.end(), 256, e);  // inherits the shorter prefix's value
-      e = kIpcPtr | c;
+      e = c << 32;
     }
-    return e & ~kIpcPtr;
+    return (uint32_t)(e >> 32);
   };
-  for (auto [plen, net, vi] : v4) {
+  for (auto [plen, net, val] : v4) {
     if (plen <= 16) {
       const uint32_t q = net >> 16, n = 1u << (16 - plen);
-      std::fill(l16.begin() + q, l16.begin() + q + n, vi);
+      std::fill(l16.begin() + q, l16.begin() + q + n, val);
     } else if (plen <= 24) {
       const uint32_t c = child(l16[net >> 16]);
       const uint32_t k = (net >> 8) & 255, n = 1u << (24 - plen);
-      std::fill(chunks.begin() + (size_t)c * 256 + k, chunks.begin() + (size_t)c * 256 + k + n, vi);
+      std::fill(chunks.begin() + (size_t)c * 256 + k, chunks.begin() + (size_t)c * 256 + k + n, val);
     } else {
       const uint32_t c = child(l16[net >> 16]);
-      uint32_t e = chunks[(size_t)c * 256 + ((net >> 8) & 255)];
+      uint64_t e = chunks[(size_t)c * 256 + ((net >> 8) & 255)];
       const uint32_t d = child(e);  // may grow chunks: write the entry back by index
       chunks[(size_t)c * 256 + ((net >> 8) & 255)] = e;
       const uint32_t k = net & 255, n = 1u << (32 - plen);
-      std::fill(chunks.begin() + (size_t)d * 256 + k, chunks.begin() + (size_t)d * 256 + k + n, vi);
+      std::fill(chunks.begin() + (size_t)d * 256 + k, chunks.begin() + (size_t)d * 256 + k + n, val);
     }
   }
-  if (chunks.empty()) chunks.assign(256, 0);
+  if (chunks.empty()) chunks.assign(256, kIpcMiss);
 
   // ---- IPv6: sweep the nested prefix intervals into runs of one value.
   std::sort(v6.begin(), v6.end(), [](const auto& a, const auto& b) {
     return std::get<0>(a) != std::get<0>(b) ? std::get<0>(a) < std::get<0>(b) : std::get<1>(a) < std::get<1>(b);
   });
-  std::vector<std::pair<U128, uint32_t>> runs{{U128{0, 0}, 0}};
-  auto emit = [&](U128 pos, uint32_t v) {
+  std::vector<std::pair<U128, uint64_t>> runs{{U128{0, 0}, kIpcMiss}};
+  auto emit = [&](U128 pos, uint64_t v) {
     if (runs.back().first == pos) {
       runs.back().second = v;
       if (runs.size() > 1 && runs[runs.size() - 2].second == v) runs.pop_back();
@@ -106,14 +99,14 @@ void IpcacheState::build_tables() {
     if (runs.back().second != v) runs.push_back({pos, v});
   };
   const U128 kMax{~0ULL, ~0ULL};
-  std::vector<std::pair<U128, uint32_t>> open;  // (last address, value)
+  std::vector<std::pair<U128, uint64_t>> open;  // (last address, value)
   auto close_one = [&] {
     const U128 end = open.back().first;
     open.pop_back();
     if (end != kMax) {
       U128 nx = end;
       if (++nx.second == 0) ++nx.first;
-      emit(nx, open.empty() ? 0 : open.back().second);
+      emit(nx, open.empty() ? kIpcMiss : open.back().second);
     }
   };
   for (const auto& [lo, plen, vi] : v6) {
@@ -122,12 +115,12 @@ void IpcacheState::build_tables() {
     open.push_back({last128(lo, plen), vi});
   }
   while (!open.empty()) close_one();
-  keys6.clear();
-  vidx6.clear();
+  runs6.clear();
   for (const auto& [pos, v] : runs) {
-    keys6.push_back(pos.first);
-    keys6.push_back(pos.second);
-    vidx6.push_back(v);
+    runs6.push_back(pos.first);
+    runs6.push_back(pos.second);
+    runs6.push_back(v);
+    runs6.push_back(0);
   }
   uint32_t bits = 16;
   while (bits < 22 && (1ull << bits) < 2 * runs.size()) ++bits;
@@ -146,12 +139,10 @@ IpcacheDev IpcacheState::host_view() const {
   IpcacheDev v{};
   v.l16 = l16.data();
   v.chunks = chunks.data();
-  v.vals = vals.data();
   v.idx6 = idx6.data();
-  v.keys6 = keys6.data();
-  v.vidx6 = vidx6.data();
+  v.runs6 = runs6.data();
   v.v6_bits = v6_bits;
-  v.nruns6 = (uint32_t)vidx6.size();
+  v.nruns6 = (uint32_t)(runs6.size() / 4);
   return v;
 }
 
@@ -161,19 +152,15 @@ void IpcacheState::rebuild(Engine& e) {
     e.set_device();
     d_l16.upload_vec(l16);
     d_chunks.upload_vec(chunks);
-    d_vals.upload_vec(vals);
     d_idx6.upload_vec(idx6);
-    d_keys6.upload_vec(keys6);
-    d_vidx6.upload_vec(vidx6);
+    d_runs6.upload_vec(runs6);
     dev = IpcacheDev{};
-    dev.l16 = d_l16.as<uint32_t>();
-    dev.chunks = d_chunks.as<uint32_t>();
-    dev.vals = d_vals.as<IpcVal>();
+    dev.l16 = d_l16.as<uint64_t>();
+    dev.chunks = d_chunks.as<uint64_t>();
     dev.idx6 = d_idx6.as<uint32_t>();
-    dev.keys6 = d_keys6.as<uint64_t>();
-    dev.vidx6 = d_vidx6.as<uint32_t>();
+    dev.runs6 = d_runs6.as<uint64_t>();
     dev.v6_bits = v6_bits;
-    dev.nruns6 = (uint32_t)vidx6.size();
+    dev.nruns6 = (uint32_t)(runs6.size() / 4);
   }
   dirty = false;
 }

@@ -19,11 +19,10 @@ struct IpcacheState {
   bool dirty = true;
 
   // host copies of the device tables (also walked by cg_diag_ipcache_eval_host)
-  std::vector<uint32_t> l16, chunks, idx6, vidx6;
-  std::vector<IpcVal> vals;
-  std::vector<uint64_t> keys6;
+  std::vector<uint64_t> l16, chunks, runs6;
+  std::vector<uint32_t> idx6;
   uint32_t v6_bits = 16;
-  DevMem d_l16, d_chunks, d_vals, d_idx6, d_keys6, d_vidx6;
+  DevMem d_l16, d_chunks, d_idx6, d_runs6;
   IpcacheDev dev{};
 
   void build_tables();

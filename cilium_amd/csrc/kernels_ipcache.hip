@@ -3,8 +3,10 @@
 // address → {security identity, tunnel endpoint}.
 //
 // Integer work bound by the input/output stream plus dependent table loads
-// (IPv4: /16 entry, up to two 1-KiB chunks, the value; IPv6: two index words,
-// a short binary search over 16-B run keys, the value).  Each lane resolves
+// (IPv4: the /16 entry, then up to two 2-KiB chunks; IPv6: two index words,
+// the bucket's last 32-B run record, a short binary search when that run
+// starts after the address).  Entries carry the resolved value inline, so
+// the last table load is the answer.  Each lane resolves
 // several addresses with every level's loads issued for all of them before
 // the next level, so a wave keeps 4 (v4) / 2 (v6) independent chains in
 // flight.
@@ -23,9 +25,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
 
-__device__ __forceinline__ void store_val(const IpcacheDev& t, uint32_t vi, IpcVal* out) {
-  const unsigned long long v = *reinterpret_cast<const unsigned long long*>(t.vals + vi);
-  __builtin_nontemporal_store(v, reinterpret_cast<unsigned long long*>(out));
+__device__ __forceinline__ void store_val(uint64_t v, IpcVal* out) {
+  __builtin_nontemporal_store((unsigned long long)v, reinterpret_cast<unsigned long long*>(out));
 }
 
 __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, const uint32_t* __restrict__ v4,
@@ -35,7 +36,8 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   // ---- IPv4 (daddr as in iphdr, network order)
   for (size_t base = (size_t)blockIdx.x * blockDim.x * kIpcV4; base < n4; base += stride * kIpcV4) {
-    uint32_t a[kIpcV4], e[kIpcV4];
+    uint32_t a[kIpcV4];
+    uint64_t e[kIpcV4];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV4; ++u) {
       size_t i = base + u * blockDim.x + threadIdx.x;
@@ -46,14 +48,14 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
     for (uint32_t u = 0; u < kIpcV4; ++u) e[u] = t.l16[a[u] >> 16];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV4; ++u)
-      if (e[u] & kIpcPtr) e[u] = t.chunks[(size_t)(e[u] & ~kIpcPtr) * 256 + ((a[u] >> 8) & 255)];
+      if ((uint32_t)e[u] == 0) e[u] = t.chunks[(size_t)(e[u] >> 32) * 256 + ((a[u] >> 8) & 255)];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV4; ++u)
-      if (e[u] & kIpcPtr) e[u] = t.chunks[(size_t)(e[u] & ~kIpcPtr) * 256 + (a[u] & 255)];
+      if ((uint32_t)e[u] == 0) e[u] = t.chunks[(size_t)(e[u] >> 32) * 256 + (a[u] & 255)];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV4; ++u) {
       const size_t i = base + u * blockDim.x + threadIdx.x;
-      if (i < n4) store_val(t, e[u], out4 + i);
+      if (i < n4) store_val(e[u], out4 + i);
     }
   }
   // ---- IPv6 (16 address bytes, network order)
@@ -74,19 +76,23 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       L[u] = t.idx6[tb];
       R[u] = t.idx6[tb + 1];
     }
-    // the bucket's last run start, loaded for every lane at once: with ~2
-    // buckets per run it settles most addresses without a search
-    uint4 kr[kIpcV6];
+    // the bucket's last run, loaded for every lane at once: with ~2 buckets
+    // per run it settles most addresses without a search
+    uint4 kr[kIpcV6], vr[kIpcV6];
 #pragma unroll
-    for (uint32_t u = 0; u < kIpcV6; ++u) kr[u] = *reinterpret_cast<const uint4*>(t.keys6 + 2 * (size_t)R[u]);
+    for (uint32_t u = 0; u < kIpcV6; ++u) {
+      const uint4* rec = reinterpret_cast<const uint4*>(t.runs6 + 4 * (size_t)R[u]);
+      kr[u] = rec[0];
+      vr[u] = rec[1];
+    }
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
       const size_t j = base + u * blockDim.x + threadIdx.x;
       if (j >= n6) continue;
-      uint32_t run;
-      if (ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u])) run = R[u];
-      else run = ipc_v6_run(t, hi[u], lo[u], L[u], R[u] - 1);
-      store_val(t, t.vidx6[run], out6 + j);
+      uint64_t v = u64_of(vr[u].x, vr[u].y);
+      if (!ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u]))
+        v = t.runs6[4 * (size_t)ipc_v6_run(t, hi[u], lo[u], L[u], R[u] - 1) + 2];
+      store_val(v, out6 + j);
     }
   }
 }

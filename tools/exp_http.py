@@ -43,6 +43,9 @@ NOREMOTE = [("  unsigned long long k0 = T.rhash_keys[rh];\n  uint32_t v0 = T.rha
 VARIANTS = {
     "base": [],
     "nowalk": [NODFA, NOWALK],
+    "deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
+    "deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
+    "deal16": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 16;")],
 }
 
 
