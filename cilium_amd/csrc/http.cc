@@ -52,7 +52,7 @@ constexpr int kMaxUnionStates = 400000;  // before minimization, per part
 constexpr int kMaxPartStates = 65535;    // u16 transition entries
 constexpr uint32_t kMaxLdsCells = 40944;  // 160 KiB less 64 B of static LDS (counters): one program table per workgroup
 
-enum class MKind { Exact, Regex, Present };
+enum class MKind { Exact, Regex, Present, Search };
 struct MatcherSpec {
   std::string name;  // lowercase
   MKind kind;
@@ -69,6 +69,9 @@ struct ScopeSpec {
 };
 struct PolicySpec {
   std::string name;
+  // proxylib verdict contract (proxylib/proxylib/policymap.go:208-236): a port
+  // with no policy (neither exact nor 0) is denied, where Envoy allows
+  bool deny_unlisted = false;
   std::map<uint32_t, ScopeSpec> dir[2];  // [0] egress, [1] ingress
 };
 
@@ -88,6 +91,9 @@ MatcherSpec parse_matcher(const Json& h) {
   const Json* ex = h.get("exact_match");
   const Json* rx = h.get("regex_match");
   const Json* pr = h.get("present_match");
+  // engine extension for proxylib parsers: an unanchored Go regexp.MatchString
+  // (proxylib/r2d2/r2d2parser.go:80), compiled in MatchMode::Search
+  const Json* rs = h.get("regex_search");
   const Json* val = h.get("value");
   const Json* inv = h.get("invert_match");
   if (inv && inv->type == Json::BOOL && inv->b) fail(CG_UNSUPPORTED, "invert_match");
@@ -99,6 +105,9 @@ MatcherSpec parse_matcher(const Json& h) {
   } else if (rx) {
     m.kind = MKind::Regex;
     m.value = rx->as_str("regex_match");
+  } else if (rs) {
+    m.kind = MKind::Search;
+    m.value = rs->as_str("regex_search");
   } else if (pr) {
     m.kind = MKind::Present;
   } else if (val) {
@@ -134,6 +143,7 @@ std::vector<PolicySpec> parse_npds(const char* json, size_t len) {
     if (!nm) fail(CG_POLICY_REJECTED, "NetworkPolicy without name");
     ps.name = nm->as_str("name");
     if (!names.insert(ps.name).second) fail(CG_POLICY_REJECTED, "duplicate NetworkPolicy name " + ps.name);
+    if (const Json* pl = p.get("proxylib")) ps.deny_unlisted = pl->type == Json::BOOL && pl->b;
     for (int d = 0; d < 2; ++d) {
       const Json* ports = p.get(d ? "ingress_per_port_policies" : "egress_per_port_policies");
       if (!ports) continue;
@@ -214,7 +224,7 @@ struct FieldDfaCache {
     return any_id;
   }
   int single(const MatcherSpec& m) {
-    std::string key = std::string(1, "ERP"[(int)m.kind]) + ":" + m.value;
+    std::string key = std::string(1, "ERPS"[(int)m.kind]) + ":" + m.value;
     auto it = by_key.find(key);
     if (it != by_key.end()) return it->second;
     ByteSet va = value_alphabet();
@@ -223,6 +233,7 @@ struct FieldDfaCache {
       case MKind::Exact: d = dfa_literal(m.value, va); break;
       case MKind::Regex: d = compile_regex(m.value, va, MatchMode::Full); break;
       case MKind::Present: d = dfa_star(va); break;
+      case MKind::Search: d = compile_regex(m.value, va, MatchMode::Search); break;
     }
     return add(std::move(d), key);
   }
@@ -631,6 +642,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       const ScopeSpec* wild = nullptr;
       auto w = ports.find(0);
       if (w != ports.end()) wild = &w->second;
+      if (p.deny_unlisted) S.dflt[pi * 2 + d] = kProgDeny;
       if (wild) S.dflt[pi * 2 + d] = build_prog({wild}, (pi << 17) | ((uint32_t)d << 16));
       for (const auto& [port, sc] : ports) {
         if (port == 0) continue;

@@ -1,0 +1,182 @@
+"""proxylib generic-L7 policy on the verdict engine.
+
+Mirrors the reference's proxylib policy layer:
+
+* ``RegisterL7RuleParser`` / the per-parser rule parsers
+  (proxylib/proxylib/policymap.go:28-45) — here a parser translates one NPDS
+  ``PortNetworkPolicyRule`` with ``l7_proto`` and ``l7_rules`` into header
+  matchers of the engine's HTTP union-DFA compiler;
+* ``newPortNetworkPolicies`` / ``newPortNetworkPolicyRules``
+  (policymap.go:118-206): UDP ports skipped, a duplicate port or a transport
+  other than TCP is a ParseError, a rule whose L7 parser is unknown drops the
+  whole port (the port is not installed), mismatching L7 types on one port
+  are a ParseError;
+* the verdict contract ``PolicyInstance.Matches`` (policymap.go:254-260,
+  :208-236): exact port, then port 0, and **no policy for the port → deny**
+  (the engine's ``"proxylib": true`` policy flag; Envoy would allow).
+
+The r2d2 parser (proxylib/r2d2/r2d2parser.go:61-123): a rule is an AND of
+``cmd`` exact equality (if non-empty) and an **unanchored** Go
+``regexp.MatchString`` on ``file`` (if non-empty), compiled by the engine in
+its search mode (``regex_search`` matcher).  A request is ``{cmd, file}`` as
+r2d2's OnData splits it (file is "" unless the line has exactly two fields).
+
+Verdicts run in the HIP ``http_kernel``: no CPU path.  Field bytes must be
+printable ASCII (0x21-0x7E: r2d2 splits on spaces) — the subset where Go
+RE2, ECMAScript and the engine agree; the packer flags control bytes as
+malformed, so such a request is denied (documented divergence).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+class ParseError(ValueError):
+    """proxylib.ParseError (policymap.go): the policy update is rejected."""
+
+
+# L7 rule parsers: name -> f(l7_rules list of {"rule": {k: v}}) -> list of matcher lists
+_L7_RULE_PARSERS: dict[str, Callable[[list], list[list[dict]]]] = {}
+
+
+def register_l7_rule_parser(name: str, fn: Callable[[list], list[list[dict]]]) -> None:
+    """RegisterL7RuleParser (policymap.go:42-45)."""
+    _L7_RULE_PARSERS[name] = fn
+
+
+R2D2_CMDS = ("READ", "WRITE", "HALT", "RESET")
+
+
+def r2d2_rule_parser(l7_rules: list) -> list[list[dict]]:
+    """ruleParser (r2d2parser.go:91-123): each L7 rule → an AND of matchers."""
+    out = []
+    for l7 in l7_rules:
+        rule = l7.get("rule") or {}
+        cmd, file_re = "", None
+        for k, v in rule.items():
+            if k == "cmd":
+                cmd = v
+            elif k == "file":
+                if v != "":
+                    file_re = v
+            else:
+                raise ParseError(f"Unsupported key: {k}")
+        if cmd and cmd not in R2D2_CMDS:
+            raise ParseError(f"Unable to parse L7 r2d2 rule with invalid cmd: '{cmd}'")
+        if file_re is not None and cmd not in ("", "READ", "WRITE"):
+            raise ParseError(f"Unable to parse L7 r2d2 rule, cmd '{cmd}' is not compatible with 'file'")
+        ms = []
+        if cmd:
+            ms.append({"name": "cmd", "exact_match": cmd})
+        if file_re is not None:
+            ms.append({"name": "file", "regex_search": file_re})
+        out.append(ms)
+    return out
+
+
+register_l7_rule_parser("r2d2", r2d2_rule_parser)
+
+
+def _translate_port(pp: dict) -> Optional[dict]:
+    """newPortNetworkPolicyRules (policymap.go:118-148) for one port; None =
+    the port is not installed (a rule with an unknown parser)."""
+    rules_out = []
+    first_type = ""
+    for r in pp.get("rules") or []:
+        l7_proto = r.get("l7_proto", "")
+        l7 = (r.get("l7_rules") or {}).get("l7_rules") or []
+        if l7_proto and l7_proto not in _L7_RULE_PARSERS:
+            return None  # newPortNetworkPolicyRule !ok → port skipped (:186-204)
+        if l7_proto:
+            if first_type == "":
+                first_type = l7_proto
+            elif l7_proto != first_type:
+                raise ParseError("Mismatching L7 types on the same port")
+        ms = _L7_RULE_PARSERS[l7_proto](l7) if l7_proto else []
+        out = {}
+        if r.get("remote_policies"):
+            out["remote_policies"] = [int(x) for x in r["remote_policies"]]
+        # a rule contributes L7 rules only when its parser produced some
+        # (HaveL7Rules, :132-134); otherwise it matches any payload
+        if ms:
+            out["http_rules"] = {"http_rules": [{"headers": m} for m in ms]}
+        rules_out.append(out)
+    return {"port": int(pp.get("port", 0)), "protocol": "TCP", "rules": rules_out}
+
+
+def translate_policies(policies: Sequence[dict]) -> list[dict]:
+    """NPDS NetworkPolicy dicts with proxylib L7 rules → the engine's NPDS form
+    (newPolicyInstance / newPortNetworkPolicies, policymap.go:177-252)."""
+    out = []
+    for p in policies:
+        q = {"name": p["name"], "proxylib": True}
+        if "policy" in p:
+            q["policy"] = p["policy"]
+        for key in ("ingress_per_port_policies", "egress_per_port_policies"):
+            ports, seen = [], set()
+            for pp in p.get(key) or []:
+                proto = pp.get("protocol", "TCP")
+                if proto in ("UDP", 1):
+                    continue
+                port = int(pp.get("port", 0))
+                if port in seen:
+                    raise ParseError(f"Duplicate port number {port}")
+                seen.add(port)
+                if proto not in ("TCP", 0):
+                    raise ParseError(f"Invalid transport protocol {proto}")
+                t = _translate_port(pp)
+                if t is not None:
+                    ports.append(t)
+            q[key] = ports
+        out.append(q)
+    return out
+
+
+def r2d2_request(line: bytes) -> tuple[bytes, bytes]:
+    """r2d2 OnData request split (r2d2parser.go:157-167): cmd, and the file
+    only when the line has exactly two space-separated fields."""
+    fields = line.split(b" ")
+    return fields[0], (fields[1] if len(fields) == 2 else b"")
+
+
+class ProxylibPolicy:
+    """A proxylib policy snapshot on a Classifier: ``update`` then batched
+    ``matches`` for r2d2 requests (Instance.PolicyMatches, instance.go:157-165)."""
+
+    def __init__(self, cl):
+        self.cl = cl
+        self.names: list[str] = []
+
+    def update(self, policies: Sequence[dict]) -> None:
+        eng = translate_policies(policies)
+        self.cl.update_http_policy(eng)
+        self.names = [p["name"] for p in eng]
+
+    def index(self, name: str) -> int:
+        try:
+            return self.cl.http_policy_index(name)
+        except N.CiliumGPUError:
+            return 0xFFFFFFFF  # unknown policy → deny
+
+    def pack(self, policy, ingress, port, remote, cmds: Sequence[bytes], files: Sequence[bytes]):
+        parts, off = [], [0]
+        for c, f in zip(cmds, files):
+            b = b"cmd\0" + c + b"\0file\0" + f + b"\0"
+            parts.append(b)
+            off.append(off[-1] + len(b))
+        blob = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()
+        return self.cl.pack_http(np.asarray(policy, np.uint32), np.asarray(ingress, np.uint8),
+                                 np.asarray(port, np.uint16), np.asarray(remote, np.uint32), blob,
+                                 np.asarray(off, np.uint64))
+
+    def matches(self, policy, ingress, port, remote, cmds, files) -> np.ndarray:
+        """One allow byte per request, from the GPU kernel."""
+        return self.cl.http_verdicts(self.pack(policy, ingress, port, remote, cmds, files))
+
+    def matches_host_diag(self, policy, ingress, port, remote, cmds, files) -> np.ndarray:
+        """Table-compiler diagnostics only (CPU walk of the same tables)."""
+        return self.cl.http_eval_host_diag(self.pack(policy, ingress, port, remote, cmds, files))

@@ -1,0 +1,121 @@
+"""CPU restatement of proxylib's generic-L7 policy evaluation with the r2d2
+rule parser.  TEST INFRASTRUCTURE ONLY (checker for tests/ and smoke()); it
+shares no code with cilium_amd and evaluates rules directly, rule by rule,
+the way the Go code does:
+
+  PolicyInstance.Matches         proxylib/proxylib/policymap.go:254-260
+  PortNetworkPolicies.Matches    :208-236 (exact port, port 0, else false)
+  newPortNetworkPolicies         :177-206 (UDP skipped, duplicate port error)
+  PortNetworkPolicyRules.Matches :150-171 (!HaveL7Rules → true)
+  newPortNetworkPolicyRules      :118-148 (unknown parser → port dropped)
+  PortNetworkPolicyRule.Matches  :91-111  (remote set, OR over L7 rules)
+  r2d2Rule.Matches / ruleParser  proxylib/r2d2/r2d2parser.go:61-123
+
+Go ``regexp.MatchString`` is restated with Python ``re.search`` on
+printable-ASCII inputs with the RE2/ECMAScript/Python common syntax subset
+(SURVEY §8(c)); pure-Python loops, so it is sized for small cases.
+"""
+from __future__ import annotations
+
+import re
+
+
+class ParseError(ValueError):
+    pass
+
+
+class _R2d2Rule:
+    def __init__(self, rule: dict):
+        self.cmd, self.file_re = "", None
+        for k, v in rule.items():
+            if k == "cmd":
+                self.cmd = v
+            elif k == "file":
+                if v != "":
+                    self.file_re = re.compile(v)
+            else:
+                raise ParseError("Unsupported key: " + k)
+        if self.cmd not in ("", "READ", "WRITE", "HALT", "RESET"):
+            raise ParseError("invalid cmd")
+        if self.file_re is not None and self.cmd not in ("", "READ", "WRITE"):
+            raise ParseError("cmd not compatible with file")
+
+    def matches(self, cmd: str, file: str) -> bool:
+        if self.cmd and self.cmd != cmd:
+            return False
+        if self.file_re is not None and not self.file_re.search(file):
+            return False
+        return True
+
+
+_PARSERS = {"r2d2": lambda l7: [_R2d2Rule(x.get("rule") or {}) for x in l7]}
+
+
+class _Rules:
+    def __init__(self, rules_cfg: list):
+        self.rules, self.have_l7, self.ok = [], False, True
+        first = ""
+        for r in rules_cfg:
+            proto = r.get("l7_proto", "")
+            if proto and proto not in _PARSERS:
+                self.ok = False
+                return
+            if proto:
+                if not first:
+                    first = proto
+                elif proto != first:
+                    raise ParseError("Mismatching L7 types on the same port")
+            l7 = _PARSERS[proto]((r.get("l7_rules") or {}).get("l7_rules") or []) if proto else []
+            if l7:
+                self.have_l7 = True
+            self.rules.append((set(int(x) for x in r.get("remote_policies") or []), l7))
+
+    def matches(self, remote: int, cmd: str, file: str) -> bool:
+        if not self.have_l7 or not self.rules:
+            return True
+        for remotes, l7 in self.rules:
+            if remotes and remote not in remotes:
+                continue
+            if not l7 or any(x.matches(cmd, file) for x in l7):
+                return True
+        return False
+
+
+class _Ports:
+    def __init__(self, cfg: list):
+        self.by_port = {}
+        for pp in cfg or []:
+            proto = pp.get("protocol", "TCP")
+            if proto in ("UDP", 1):
+                continue
+            port = int(pp.get("port", 0))
+            if port in self.by_port:
+                raise ParseError("Duplicate port number")
+            if proto not in ("TCP", 0):
+                raise ParseError("Invalid transport protocol")
+            r = _Rules(pp.get("rules") or [])
+            if r.ok:
+                self.by_port[port] = r
+
+    def matches(self, port: int, remote: int, cmd: str, file: str) -> bool:
+        r = self.by_port.get(port)
+        if r is not None and r.matches(remote, cmd, file):
+            return True
+        w = self.by_port.get(0)
+        if w is not None and w.matches(remote, cmd, file):
+            return True
+        return False
+
+
+class ProxylibOracle:
+    def __init__(self, policies: list[dict]):
+        self.pol = {}
+        for p in policies:
+            self.pol[p["name"]] = (_Ports(p.get("ingress_per_port_policies")),
+                                   _Ports(p.get("egress_per_port_policies")))
+
+    def matches(self, name: str, ingress: bool, port: int, remote: int, cmd: bytes, file: bytes) -> bool:
+        p = self.pol.get(name)
+        if p is None:
+            return False
+        return (p[0] if ingress else p[1]).matches(port, remote, cmd.decode("latin-1"), file.decode("latin-1"))
