@@ -15,6 +15,10 @@ Mirrors the reference's proxylib policy layer:
   :208-236): exact port, then port 0, and **no policy for the port → deny**
   (the engine's ``"proxylib": true`` policy flag; Envoy would allow).
 
+The cassandra parser (proxylib/cassandra/cassandraparser.go:58-131) works on
+the request path "/opcode/action/table"; each rule becomes an OR of engine
+rules over the path's shape, action and table (see cassandra_rule_parser).
+
 The r2d2 parser (proxylib/r2d2/r2d2parser.go:61-123): a rule is an AND of
 ``cmd`` exact equality (if non-empty) and an **unanchored** Go
 ``regexp.MatchString`` on ``file`` (if non-empty), compiled by the engine in
@@ -80,6 +84,57 @@ def r2d2_rule_parser(l7_rules: list) -> list[list[dict]]:
 
 register_l7_rule_parser("r2d2", r2d2_rule_parser)
 
+# queryActionMap (proxylib/cassandra/cassandraparser.go:315-366): 1 = takes a
+# table (query_table allowed), 2 = no table
+CASSANDRA_ACTIONS = dict(
+    [(a, 1) for a in ("select", "delete", "insert", "update", "create-table", "drop-table", "alter-table",
+                      "truncate-table", "use", "create-keyspace", "alter-keyspace", "drop-keyspace")] +
+    [(a, 2) for a in ("drop-index", "create-index", "create-materialized-view", "drop-materialized-view",
+                      "create-role", "alter-role", "drop-role", "grant-role", "revoke-role", "list-roles",
+                      "grant-permission", "revoke-permission", "list-permissions", "create-user", "alter-user",
+                      "drop-user", "list-users", "create-function", "drop-function", "create-aggregate",
+                      "drop-aggregate", "create-type", "alter-type", "drop-type", "create-trigger",
+                      "drop-trigger")])
+
+
+def cassandra_rule_parser(l7_rules: list) -> list[list[dict]]:
+    """CassandraRuleParser (cassandraparser.go:97-131).  A rule's Matches
+    (:58-90) is an OR of request shapes, split into engine rules (the L7
+    rules of a PNPR are OR-ed): a path of <= 2 parts matches any rule; one of
+    >= 4 parts needs the action and, if the table part is non-empty, the
+    unanchored table regex; a 3-part path matches none."""
+    out = []
+    for l7 in l7_rules:
+        rule = l7.get("rule") or {}
+        action, table_re = "", None
+        for k, v in rule.items():
+            if k == "query_action":
+                action = v
+            elif k == "query_table":
+                if v != "":
+                    table_re = v
+            else:
+                raise ParseError(f"Unsupported key: {k}")
+        if action:
+            kind = CASSANDRA_ACTIONS.get(action, 0)
+            if kind == 0:
+                raise ParseError(f"Unable to parse L7 cassandra rule with invalid query_action: '{action}'")
+            if kind == 2 and table_re is not None:
+                raise ParseError(f"query_action '{action}' is not compatible with a query_table match")
+        out.append([{"name": "cshape", "exact_match": "S"}])
+        long = [{"name": "cshape", "exact_match": "L"}]
+        if action:
+            long.append({"name": "action", "exact_match": action})
+        if table_re is None:
+            out.append(long)
+        else:
+            out.append(long + [{"name": "table", "exact_match": ""}])
+            out.append(long + [{"name": "table", "regex_search": table_re}])
+    return out
+
+
+register_l7_rule_parser("cassandra", cassandra_rule_parser)
+
 
 def _translate_port(pp: dict) -> Optional[dict]:
     """newPortNetworkPolicyRules (policymap.go:118-148) for one port; None =
@@ -136,6 +191,17 @@ def translate_policies(policies: Sequence[dict]) -> list[dict]:
     return out
 
 
+def cassandra_request(path: bytes) -> list[tuple[bytes, bytes]]:
+    """The fields of a cassandra request path ("/opcode[/action/table]",
+    cassandraparser.go:486-578) as CassandraRule.Matches splits it (:73-89)."""
+    parts = path.split(b"/")
+    if len(parts) <= 2:
+        return [(b"cshape", b"S")]
+    if len(parts) < 4:
+        return [(b"cshape", b"X")]
+    return [(b"cshape", b"L"), (b"action", parts[2]), (b"table", parts[3])]
+
+
 def r2d2_request(line: bytes) -> tuple[bytes, bytes]:
     """r2d2 OnData request split (r2d2parser.go:157-167): cmd, and the file
     only when the line has exactly two space-separated fields."""
@@ -162,16 +228,26 @@ class ProxylibPolicy:
         except N.CiliumGPUError:
             return 0xFFFFFFFF  # unknown policy → deny
 
-    def pack(self, policy, ingress, port, remote, cmds: Sequence[bytes], files: Sequence[bytes]):
+    def pack_fields(self, policy, ingress, port, remote, fields: Sequence[Sequence[tuple[bytes, bytes]]]):
+        """Requests given as their parser's (name, value) fields."""
         parts, off = [], [0]
-        for c, f in zip(cmds, files):
-            b = b"cmd\0" + c + b"\0file\0" + f + b"\0"
+        for fs in fields:
+            b = b"".join(k + b"\0" + v + b"\0" for k, v in fs)
             parts.append(b)
             off.append(off[-1] + len(b))
         blob = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()
         return self.cl.pack_http(np.asarray(policy, np.uint32), np.asarray(ingress, np.uint8),
                                  np.asarray(port, np.uint16), np.asarray(remote, np.uint32), blob,
                                  np.asarray(off, np.uint64))
+
+    def pack(self, policy, ingress, port, remote, cmds: Sequence[bytes], files: Sequence[bytes]):
+        """r2d2 requests: {cmd, file}."""
+        return self.pack_fields(policy, ingress, port, remote,
+                                [[(b"cmd", c), (b"file", f)] for c, f in zip(cmds, files)])
+
+    def matches_fields(self, policy, ingress, port, remote, fields, host_diag: bool = False) -> np.ndarray:
+        b = self.pack_fields(policy, ingress, port, remote, fields)
+        return self.cl.http_eval_host_diag(b) if host_diag else self.cl.http_verdicts(b)
 
     def matches(self, policy, ingress, port, remote, cmds, files) -> np.ndarray:
         """One allow byte per request, from the GPU kernel."""

@@ -10,6 +10,7 @@ the way the Go code does:
   newPortNetworkPolicyRules      :118-148 (unknown parser → port dropped)
   PortNetworkPolicyRule.Matches  :91-111  (remote set, OR over L7 rules)
   r2d2Rule.Matches / ruleParser  proxylib/r2d2/r2d2parser.go:61-123
+  CassandraRule.Matches / parser proxylib/cassandra/cassandraparser.go:40-131
 
 Go ``regexp.MatchString`` is restated with Python ``re.search`` on
 printable-ASCII inputs with the RE2/ECMAScript/Python common syntax subset
@@ -48,7 +49,50 @@ class _R2d2Rule:
         return True
 
 
-_PARSERS = {"r2d2": lambda l7: [_R2d2Rule(x.get("rule") or {}) for x in l7]}
+_CASS_NO_TABLE = {"drop-index", "create-index", "create-materialized-view", "drop-materialized-view",
+                  "create-role", "alter-role", "drop-role", "grant-role", "revoke-role", "list-roles",
+                  "grant-permission", "revoke-permission", "list-permissions", "create-user", "alter-user",
+                  "drop-user", "list-users", "create-function", "drop-function", "create-aggregate",
+                  "drop-aggregate", "create-type", "alter-type", "drop-type", "create-trigger", "drop-trigger"}
+_CASS_TABLE = {"select", "delete", "insert", "update", "create-table", "drop-table", "alter-table",
+               "truncate-table", "use", "create-keyspace", "alter-keyspace", "drop-keyspace"}
+
+
+class _CassandraRule:
+    """CassandraRule (proxylib/cassandra/cassandraparser.go:40-131); the
+    request is the path string its OnData builds."""
+
+    def __init__(self, rule: dict):
+        self.action, self.table_re = "", None
+        for k, v in rule.items():
+            if k == "query_action":
+                self.action = v
+            elif k == "query_table":
+                if v != "":
+                    self.table_re = re.compile(v)
+            else:
+                raise ParseError("Unsupported key: " + k)
+        if self.action:
+            if self.action not in _CASS_TABLE and self.action not in _CASS_NO_TABLE:
+                raise ParseError("invalid query_action")
+            if self.action in _CASS_NO_TABLE and self.table_re is not None:
+                raise ParseError("not compatible with a query_table match")
+
+    def matches(self, path: str, _unused: str = "") -> bool:
+        parts = path.split("/")
+        if len(parts) <= 2:
+            return True
+        if len(parts) < 4:
+            return False
+        if self.action and self.action != parts[2]:
+            return False
+        if len(parts[3]) > 0 and self.table_re is not None and not self.table_re.search(parts[3]):
+            return False
+        return True
+
+
+_PARSERS = {"r2d2": lambda l7: [_R2d2Rule(x.get("rule") or {}) for x in l7],
+            "cassandra": lambda l7: [_CassandraRule(x.get("rule") or {}) for x in l7]}
 
 
 class _Rules:
@@ -113,6 +157,13 @@ class ProxylibOracle:
         for p in policies:
             self.pol[p["name"]] = (_Ports(p.get("ingress_per_port_policies")),
                                    _Ports(p.get("egress_per_port_policies")))
+
+    def matches_path(self, name: str, ingress: bool, port: int, remote: int, path: bytes) -> bool:
+        """cassandra: the request is its path ("/opcode/action/table")."""
+        p = self.pol.get(name)
+        if p is None:
+            return False
+        return (p[0] if ingress else p[1]).matches(port, remote, path.decode("latin-1"), "")
 
     def matches(self, name: str, ingress: bool, port: int, remote: int, cmd: bytes, file: bytes) -> bool:
         p = self.pol.get(name)

@@ -1,8 +1,9 @@
-"""proxylib generic-L7 rules (r2d2) on the verdict engine.
+"""proxylib generic-L7 rules (r2d2, cassandra) on the verdict engine.
 
 KATs are the reference's own r2d2 tests (proxylib/r2d2/r2d2parser_test.go:
 70-190: TestR2d2OnDataBasicPass, ...AllowDenyCmd, ...AllowDenyRegex); the
-oracle is oracle/proxylib_ref.py (policymap.go + r2d2parser.go restated).
+oracle is oracle/proxylib_ref.py (policymap.go + r2d2parser.go + cassandraparser.go
+restated).  Cassandra KATs: cassandraparser_test.go:86-280 at the path level.
 """
 import numpy as np
 import pytest
@@ -172,3 +173,121 @@ def test_gpu_kat(gpu):
 @pytest.mark.parametrize("seed", range(4))
 def test_gpu_random_vs_oracle(gpu, seed):
     _check_random(gpu, 100 + seed, 20000, gpu=True)
+
+
+# ------------------------------------------------------------- cassandra ----
+# proxylib/cassandra/cassandraparser_test.go: cp6 (query_action select, remotes
+# 1,3,4) passes an OPTIONS frame ("/options", :86-115); cp4 (query_table ".*")
+# passes and cp1 (query_table "no-match") drops "SELECT ... FROM system.local"
+# ("/query/select/system.local", :145-172, :236-280).
+def _cass(name, rule):
+    return {"name": name, "policy": 2, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [1, 3, 4], "l7_proto": "cassandra", "l7_rules": {"l7_rules": [{"rule": rule}]}}]}]}
+
+
+CASS_POLS = [_cass("cp6", {"query_action": "select"}), _cass("cp4", {"query_table": ".*"}),
+             _cass("cp1", {"query_table": "no-match"})]
+CASS_KAT = [("cp6", b"/options", True), ("cp4", b"/query/select/system.local", True),
+            ("cp1", b"/query/select/system.local", False), ("cp1", b"/options", True),
+            ("cp6", b"/query/insert/system.local", False), ("cp6", b"/query/select", False)]
+
+
+def _cass_eval(pl, cases, host_diag):
+    n = len(cases)
+    return pl.matches_fields([pl.index(c[0]) for c in cases], [1] * n, [c[1] for c in cases], [c[2] for c in cases],
+                             [P.cassandra_request(c[3]) for c in cases], host_diag=host_diag)
+
+
+def test_cassandra_oracle_kat():
+    o = ProxylibOracle(CASS_POLS)
+    for name, path, exp in CASS_KAT:
+        assert o.matches_path(name, True, 80, 1, path) == exp, (name, path)
+    assert not o.matches_path("cp6", True, 80, 2, b"/options")  # remote 2 not in {1,3,4}
+
+
+def test_cassandra_tables_kat(host):
+    pl = P.ProxylibPolicy(host)
+    pl.update(CASS_POLS)
+    cases = [(n, 80, 1, p) for n, p, _ in CASS_KAT] + [("cp6", 80, 2, b"/options")]
+    assert _cass_eval(pl, cases, True).tolist() == [int(e) for _, _, e in CASS_KAT] + [0]
+
+
+@pytest.mark.parametrize("rule,msg", [
+    ({"query_action": "explode"}, "invalid query_action"),
+    ({"query_action": "create-role", "query_table": "t"}, "not compatible"),
+    ({"table": "x"}, "Unsupported key"),
+])
+def test_cassandra_parse_errors(rule, msg):
+    with pytest.raises(P.ParseError, match=msg):
+        P.translate_policies([_cass("e", rule)])
+
+
+CASS_TABLE_RES = ["^system\\.", "local$", "users", "db[0-9]", ".*", "^$", "a|b"]
+CASS_ACTIONS = ["select", "insert", "update", "delete", "use", "create-role", "drop-index"]
+
+
+def _cass_random(rng, n):
+    pols = []
+    for pi in range(3):
+        ports = []
+        for port in rng.choice([0, 9042, 80], size=int(rng.integers(1, 3)), replace=False):
+            rules = []
+            for _ in range(int(rng.integers(0, 3))):
+                r = {"l7_proto": "cassandra"}
+                if rng.random() < 0.4:
+                    r["remote_policies"] = [int(x) for x in rng.choice(6, size=2, replace=False)]
+                l7 = []
+                for _ in range(int(rng.integers(0, 3))):
+                    rule = {}
+                    a = str(rng.choice(CASS_ACTIONS + [""]))
+                    if a:
+                        rule["query_action"] = a
+                    if CASS_ACTIONS.index(a) < 5 if a else True:
+                        if rng.random() < 0.6:
+                            rule["query_table"] = str(rng.choice(CASS_TABLE_RES))
+                    l7.append({"rule": rule})
+                r["l7_rules"] = {"l7_rules": l7}
+                rules.append(r)
+            ports.append({"port": int(port), "rules": rules})
+        pols.append({"name": f"c{pi}", "ingress_per_port_policies": ports})
+    tables = ["system.local", "db1.users", "db2.t", "", "x.local", "ab", "users"]
+    reqs = []
+    for _ in range(n):
+        u = rng.random()
+        if u < 0.2:
+            path = b"/" + bytes(rng.choice([b"options", b"startup", b"register"]))
+        elif u < 0.3:
+            path = b"/query/" + bytes(rng.choice([b"select", b"use"]))
+        else:
+            path = b"/" + bytes(rng.choice([b"query", b"execute", b"batch"])) + b"/" + \
+                str(rng.choice(CASS_ACTIONS)).encode() + b"/" + str(rng.choice(tables)).encode()
+            if rng.random() < 0.1:
+                path += b"/extra"
+        reqs.append((f"c{int(rng.integers(0, 4))}", int(rng.choice([9042, 80, 7000])), int(rng.integers(0, 7)),
+                     path))
+    return pols, reqs
+
+
+def _check_cass(cl, seed, n, host_diag):
+    rng = np.random.default_rng(seed)
+    pols, reqs = _cass_random(rng, n)
+    o = ProxylibOracle(pols)
+    pl = P.ProxylibPolicy(cl)
+    pl.update(pols)
+    got = _cass_eval(pl, reqs, host_diag)
+    assert got.tolist() == [int(o.matches_path(r[0], True, r[1], r[2], r[3])) for r in reqs]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_cassandra_random_tables_vs_oracle(host, seed):
+    _check_cass(host, seed, 3000, True)
+
+
+@pytest.mark.gpu
+def test_gpu_cassandra_kat_and_random(gpu):
+    pl = P.ProxylibPolicy(gpu)
+    pl.update(CASS_POLS)
+    cases = [(n, 80, 1, p) for n, p, _ in CASS_KAT]
+    assert _cass_eval(pl, cases, False).tolist() == [int(e) for _, _, e in CASS_KAT]
+    for seed in range(3):
+        _check_cass(gpu, 200 + seed, 20000, False)
