@@ -5,6 +5,8 @@ configs, one JSON line each (bench.py covers config 5, the 10K-rule HTTP set):
 * CIDR prefilter (config 3): 1M mixed v4/v6 prefixes, 1B addresses
 * Kafka (config 4): 1K rules, 100M requests
 * ipcache: 512K-entry IP → identity map, 1B addresses
+* proxylib r2d2: 512 r2d2 rules over 64 ports, ~100M requests
+  on the HTTP kernel
 
 Inputs are resident in HBM before timing; kernels are timed with HIP events
 on their stream.  Each line carries the kernel's HBM roofline (algorithmic
@@ -181,9 +183,90 @@ def bench_ipcache(torch, dev, stream, cl, args, threads):
                                      "entries": int(len(k)), "addresses": n4 + n6}})
 
 
+def r2d2_workload(n: int, seed: int = 0xC111A):
+    """64 ports x 8 r2d2 rules (cmd and/or an unanchored file regex; a third
+    of the rules restricted to 4 of 64 remote identities); requests half
+    crafted to hit a random rule, half random."""
+    rng = np.random.default_rng(seed)
+    ports, rules_of = [], {}
+    for pi in range(64):
+        port = 7000 + pi
+        rules = []
+        for ri in range(8):
+            k = pi * 8 + ri
+            kind = ri % 4
+            rule = {}
+            if kind != 3:
+                rule["cmd"] = ["READ", "WRITE", "READ"][kind]
+            if kind == 0:
+                rule["file"] = f"^/svc{k}/[a-z]+"
+            elif kind == 1:
+                rule["file"] = f"data{k}\\.(csv|json)$"
+            elif kind == 3:
+                rule["file"] = f"tmp{k}"
+            r = {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": rule}]}}
+            if ri % 3 == 0:
+                r["remote_policies"] = [int(x) for x in rng.choice(64, 4, replace=False) + 256]
+            rules.append(r)
+            rules_of[(port, ri)] = (rule, r.get("remote_policies"))
+        ports.append({"port": port, "rules": rules})
+    pols = [{"name": "r2d2-bench", "ingress_per_port_policies": ports}]
+    reqs = []
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    for i in range(n):
+        pi, ri = int(rng.integers(0, 64)), int(rng.integers(0, 8))
+        port = 7000 + pi
+        rule, rem = rules_of[(port, ri)]
+        word = letters[rng.integers(0, 26, int(rng.integers(3, 12)))].tobytes()
+        k = pi * 8 + ri
+        if rng.random() < 0.5:
+            cmd = rule.get("cmd", "READ").encode()
+            f = {0: b"/svc%d/" % k + word, 1: b"x/data%d.json" % k, 2: word, 3: b"a/tmp%d/" % k + word}[ri % 4]
+            remote = rem[0] if rem else 256 + int(rng.integers(0, 64))
+        else:
+            cmd = [b"READ", b"WRITE", b"HALT", b"RESET"][int(rng.integers(0, 4))]
+            f = b"/svc%d/" % int(rng.integers(0, 512)) + word
+            remote = 256 + int(rng.integers(0, 64))
+        reqs.append((port, remote, cmd, f))
+    return pols, reqs
+
+
+def bench_proxylib(torch, dev, stream, cl, args, threads):
+    from bench import replicate_batch
+    from cilium_amd.proxylib import ProxylibPolicy
+    from oracle.proxylib_ref import ProxylibOracle
+    D, reps = 262_144, 400
+    pols, reqs = r2d2_workload(D)
+    pl = ProxylibPolicy(cl)
+    pl.update(pols)
+    pidx = pl.index("r2d2-bench")
+    args_ = ([pidx] * D, [1] * D, [r[0] for r in reqs], [r[1] for r in reqs], [r[2] for r in reqs],
+             [r[3] for r in reqs])
+    b = pl.pack(*args_)
+    o = ProxylibOracle(pols)
+    chk = 20_000
+    got = cl.http_verdicts(b)[:chk]
+    exp = [int(o.matches("r2d2-bench", True, r[0], r[1], r[2], r[3])) for r in reqs[:chk]]
+    assert got.tolist() == exp, "proxylib verdicts differ from the oracle"
+    d_batch, nslots, _, data_bytes = replicate_batch(b, reps, dev, torch)
+    d_arena = torch.from_numpy(b.arena).to(dev)
+    d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
+    n = D * reps
+    sec = timed(torch, stream, lambda: cl.http_verdicts_dev(d_batch, nslots, d_arena, d_out,
+                                                            stream=stream.cuda_stream), args.steps, 2)
+    bpi = data_bytes / n + 1
+    sample = reqs[:20_000]
+    cpu = cpu_rate(lambda: [o.matches("r2d2-bench", True, r[0], r[1], r[2], r[3]) for r in sample], len(sample),
+                   args.cpu_seconds)
+    return line("proxylib r2d2 verdicts/s (PolicyInstance.Matches + r2d2 rules) on http_kernel", n, sec, bpi,
+                "http_kernel", cpu, "20K requests of the same workload, 1 thread (pure-Python oracle)", 1,
+                {"config": {"workload": "SURVEY 8(f) row 4: 512 r2d2 rules over 64 ports, 104.9M requests",
+                            "requests": n, "allow_fraction": float(np.mean(exp))}})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--paths", default="l4,lpm,kafka,ipcache")
+    ap.add_argument("--paths", default="l4,lpm,kafka,ipcache,proxylib")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     args = ap.parse_args()
@@ -193,7 +276,8 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache}
+    fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
+           "proxylib": bench_proxylib}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()
