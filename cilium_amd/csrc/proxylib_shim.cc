@@ -1,0 +1,454 @@
+// proxylib_shim.cc — the proxylib C ABI (include/cilium_proxylib.h) over the
+// verdict engine, plus cg_proxylib_policy_update (include/cilium_gpu.h).
+//
+//   OpenModule / CloseModule     proxylib/proxylib.go:118-155
+//   OnNewConnection / Close      proxylib/proxylib.go:56-111, connection.go:60-100
+//   OnData                       connection.go:118-174 (op loop) +
+//                                r2d2/r2d2parser.go:148-199 (line framing)
+//   policy translation           proxylib/proxylib/policymap.go:118-206 with the
+//                                r2d2 (r2d2parser.go:91-123) and cassandra
+//                                (cassandraparser.go:97-131) rule parsers
+//
+// The policy verdicts of every request frame found in one OnData call are
+// evaluated as one batch by http_kernel (no CPU evaluation path).
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/cilium_gpu.h"
+#include "../../include/cilium_proxylib.h"
+#include "common.h"
+#include "json.h"
+
+using namespace cg;
+
+namespace {
+
+struct Instance {
+  uint64_t engine = 0;
+  std::string key;
+  std::mutex mu;  // serializes verdict batches on the engine stream
+};
+
+struct Conn {
+  std::shared_ptr<Instance> inst;
+  std::string parser, policy;
+  bool ingress = false;
+  uint32_t src_id = 0, dst_id = 0, port = 0;
+  GoSlice* orig_buf = nullptr;
+  GoSlice* reply_buf = nullptr;
+};
+
+std::mutex g_mu;
+std::map<uint64_t, std::shared_ptr<Instance>> g_instances;
+std::map<std::string, uint64_t> g_instance_by_key;
+std::map<uint64_t, std::shared_ptr<Conn>> g_conns;
+uint64_t g_next_instance = 1;
+
+std::string gostr(GoString s) { return s.p && s.n > 0 ? std::string(s.p, (size_t)s.n) : std::string(); }
+
+std::shared_ptr<Instance> find_instance(uint64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_instances.find(id);
+  return it == g_instances.end() ? nullptr : it->second;
+}
+
+// ------------------------------------------------------------ translation
+std::string jstr(const std::string& s) {
+  std::string o = "\"";
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += (char)c;
+    } else if (c < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", c);
+      o += b;
+    } else {
+      o += (char)c;
+    }
+  }
+  return o + "\"";
+}
+
+std::string m_exact(const char* name, const std::string& v) {
+  return std::string("{\"name\":\"") + name + "\",\"exact_match\":" + jstr(v) + "}";
+}
+std::string m_search(const char* name, const std::string& v) {
+  return std::string("{\"name\":\"") + name + "\",\"regex_search\":" + jstr(v) + "}";
+}
+std::string join(const std::vector<std::string>& xs) {
+  std::string o;
+  for (size_t i = 0; i < xs.size(); ++i) o += (i ? "," : "") + xs[i];
+  return o;
+}
+
+// each returned entry: one engine rule (an AND of matchers, JSON array body)
+std::vector<std::string> r2d2_rules(const Json* l7) {
+  std::vector<std::string> out;
+  for (const Json& e : l7->arr) {
+    std::string cmd, file;
+    bool has_file = false;
+    if (const Json* r = e.get("rule"))
+      for (const auto& [k, v] : r->obj) {
+        if (k == "cmd") cmd = v.as_str("cmd");
+        else if (k == "file") {
+          file = v.as_str("file");
+          has_file = !file.empty();
+        } else fail(CG_POLICY_REJECTED, "Unsupported key: " + k);
+      }
+    if (!cmd.empty() && cmd != "READ" && cmd != "WRITE" && cmd != "HALT" && cmd != "RESET")
+      fail(CG_POLICY_REJECTED, "Unable to parse L7 r2d2 rule with invalid cmd: '" + cmd + "'");
+    if (has_file && !(cmd.empty() || cmd == "READ" || cmd == "WRITE"))
+      fail(CG_POLICY_REJECTED, "Unable to parse L7 r2d2 rule, cmd '" + cmd + "' is not compatible with 'file'");
+    std::vector<std::string> ms;
+    if (!cmd.empty()) ms.push_back(m_exact("cmd", cmd));
+    if (has_file) ms.push_back(m_search("file", file));
+    out.push_back(join(ms));
+  }
+  return out;
+}
+
+int cassandra_action_kind(const std::string& a) {
+  static const std::set<std::string> table = {"select", "delete", "insert", "update", "create-table",
+                                              "drop-table", "alter-table", "truncate-table", "use",
+                                              "create-keyspace", "alter-keyspace", "drop-keyspace"};
+  static const std::set<std::string> notable = {
+      "drop-index", "create-index", "create-materialized-view", "drop-materialized-view", "create-role",
+      "alter-role", "drop-role", "grant-role", "revoke-role", "list-roles", "grant-permission",
+      "revoke-permission", "list-permissions", "create-user", "alter-user", "drop-user", "list-users",
+      "create-function", "drop-function", "create-aggregate", "drop-aggregate", "create-type", "alter-type",
+      "drop-type", "create-trigger", "drop-trigger"};
+  return table.count(a) ? 1 : notable.count(a) ? 2 : 0;
+}
+
+std::vector<std::string> cassandra_rules(const Json* l7) {
+  std::vector<std::string> out;
+  for (const Json& e : l7->arr) {
+    std::string action, table;
+    bool has_table = false;
+    if (const Json* r = e.get("rule"))
+      for (const auto& [k, v] : r->obj) {
+        if (k == "query_action") action = v.as_str("query_action");
+        else if (k == "query_table") {
+          table = v.as_str("query_table");
+          has_table = !table.empty();
+        } else fail(CG_POLICY_REJECTED, "Unsupported key: " + k);
+      }
+    if (!action.empty()) {
+      const int kind = cassandra_action_kind(action);
+      if (kind == 0) fail(CG_POLICY_REJECTED, "Unable to parse L7 cassandra rule with invalid query_action");
+      if (kind == 2 && has_table) fail(CG_POLICY_REJECTED, "query_action is not compatible with a query_table match");
+    }
+    out.push_back(m_exact("cshape", "S"));
+    std::vector<std::string> lng{m_exact("cshape", "L")};
+    if (!action.empty()) lng.push_back(m_exact("action", action));
+    if (!has_table) {
+      out.push_back(join(lng));
+    } else {
+      auto a = lng, b = lng;
+      a.push_back(m_exact("table", ""));
+      b.push_back(m_search("table", table));
+      out.push_back(join(a));
+      out.push_back(join(b));
+    }
+  }
+  return out;
+}
+
+bool known_parser(const std::string& p) { return p == "r2d2" || p == "cassandra"; }
+
+std::string translate(const char* json, size_t len) {
+  Json root = JsonParser(json, len).parse();
+  if (root.type != Json::ARR) fail(CG_POLICY_REJECTED, "expected a list of NetworkPolicy");
+  std::string out = "[";
+  bool firstp = true;
+  for (const Json& p : root.arr) {
+    const Json* nm = p.get("name");
+    if (!nm) fail(CG_POLICY_REJECTED, "NetworkPolicy without name");
+    out += std::string(firstp ? "" : ",") + "{\"name\":" + jstr(nm->as_str("name")) + ",\"proxylib\":true";
+    firstp = false;
+    for (const char* key : {"ingress_per_port_policies", "egress_per_port_policies"}) {
+      out += std::string(",\"") + key + "\":[";
+      std::set<uint64_t> seen;
+      bool firstport = true;
+      if (const Json* ports = p.get(key)) {
+        if (ports->type != Json::ARR) fail(CG_POLICY_REJECTED, "per_port_policies must be a list");
+        for (const Json& pp : ports->arr) {
+          std::string proto = "TCP";
+          if (const Json* j = pp.get("protocol"))
+            proto = j->type == Json::STR ? j->s : (j->as_u64("protocol") == 0 ? "TCP" : j->as_u64("protocol") == 1 ? "UDP" : "?");
+          if (proto == "UDP") continue;
+          const uint64_t port = pp.get("port") ? pp.get("port")->as_u64("port") : 0;
+          if (!seen.insert(port).second) fail(CG_POLICY_REJECTED, "Duplicate port number");
+          if (proto != "TCP") fail(CG_POLICY_REJECTED, "Invalid transport protocol");
+          std::string rules;
+          bool ok = true, firstr = true;
+          std::string first_type;
+          if (const Json* rs = pp.get("rules")) {
+            for (const Json& r : rs->arr) {
+              std::string l7p = r.get("l7_proto") ? r.get("l7_proto")->as_str("l7_proto") : "";
+              if (!l7p.empty() && !known_parser(l7p)) {
+                ok = false;  // newPortNetworkPolicyRule !ok: the port is not installed
+                break;
+              }
+              if (!l7p.empty()) {
+                if (first_type.empty()) first_type = l7p;
+                else if (l7p != first_type) fail(CG_POLICY_REJECTED, "Mismatching L7 types on the same port");
+              }
+              std::vector<std::string> ms;
+              const Json* l7 = nullptr;
+              if (const Json* lr = r.get("l7_rules")) l7 = lr->get("l7_rules");
+              if (!l7p.empty() && l7 && l7->type == Json::ARR)
+                ms = l7p == "r2d2" ? r2d2_rules(l7) : cassandra_rules(l7);
+              std::string rr = "{";
+              bool any = false;
+              if (const Json* rp = r.get("remote_policies")) {
+                std::vector<std::string> ids;
+                for (const Json& id : rp->arr) ids.push_back(std::to_string(id.as_u64("remote_policies")));
+                if (!ids.empty()) {
+                  rr += "\"remote_policies\":[" + join(ids) + "]";
+                  any = true;
+                }
+              }
+              if (!ms.empty()) {
+                std::vector<std::string> hr;
+                for (auto& m : ms) hr.push_back("{\"headers\":[" + m + "]}");
+                rr += std::string(any ? "," : "") + "\"http_rules\":{\"http_rules\":[" + join(hr) + "]}";
+              }
+              rules += std::string(firstr ? "" : ",") + rr + "}";
+              firstr = false;
+            }
+          }
+          if (!ok) continue;
+          out += std::string(firstport ? "" : ",") + "{\"port\":" + std::to_string(port) +
+                 ",\"protocol\":\"TCP\",\"rules\":[" + rules + "]}";
+          firstport = false;
+        }
+      }
+      out += "]";
+    }
+    out += "}";
+  }
+  return out + "]";
+}
+
+// --------------------------------------------------------------- framing
+struct Frame {
+  size_t len;  // bytes including "\r\n"
+  bool request;
+  std::string cmd, file;
+};
+
+size_t inject(GoSlice* buf, const char* data, size_t n) {  // connection.go:190-209
+  if (!buf || !buf->data) return 0;
+  const size_t off = (size_t)buf->len, room = (size_t)(buf->cap - buf->len);
+  const size_t k = n < room ? n : room;
+  memcpy((char*)buf->data + off, data, k);
+  buf->len += (int64_t)k;
+  return k;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len) {
+  auto inst = find_instance(instance);
+  if (!inst) return CG_INVALID_INSTANCE;
+  std::string eng;
+  try {
+    eng = translate(json, len);
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (...) {
+    set_error("proxylib policy translation failed");
+    return CG_UNKNOWN_ERROR;
+  }
+  std::lock_guard<std::mutex> lk(inst->mu);
+  return cg_http_policy_update(inst->engine, eng.data(), eng.size());
+}
+
+uint64_t OpenModule(GoSlice params, uint8_t debug) {
+  std::string key;
+  const GoString* kv = static_cast<const GoString*>(params.data);
+  for (int64_t i = 0; i < params.len; ++i) {
+    const std::string k = gostr(kv[2 * i]), v = gostr(kv[2 * i + 1]);
+    if (k != "access-log-path" && k != "xds-path" && k != "node-id") return 0;
+    key += k + "=" + v + ";";
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_instance_by_key.find(key);  // same parameters → same instance (libcilium.h:108)
+  if (it != g_instance_by_key.end()) return it->second;
+  const char* dv = getenv("CILIUM_GPU_DEVICE");
+  const std::string dev = dv ? dv : "0";
+  cg_kv p{"device", dev.c_str()};
+  const uint64_t h = cg_open(&p, 1, debug);
+  if (h == 0) return 0;
+  auto inst = std::make_shared<Instance>();
+  inst->engine = h;
+  inst->key = key;
+  const uint64_t id = g_next_instance++;
+  g_instances[id] = inst;
+  g_instance_by_key[key] = id;
+  return id;
+}
+
+void CloseModule(uint64_t id) {
+  std::shared_ptr<Instance> inst;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_instances.find(id);
+    if (it == g_instances.end()) return;
+    inst = it->second;
+    g_instances.erase(it);
+    g_instance_by_key.erase(inst->key);
+  }
+  cg_close(inst->engine);
+}
+
+FilterResult OnNewConnection(uint64_t instanceId, GoString proto, uint64_t connectionId, uint8_t ingress,
+                             uint32_t srcId, uint32_t dstId, GoString srcAddr, GoString dstAddr,
+                             GoString policyName, GoSlice* origBuf, GoSlice* replyBuf) {
+  auto inst = find_instance(instanceId);
+  if (!inst) return FILTER_INVALID_INSTANCE;
+  auto c = std::make_shared<Conn>();
+  c->parser = gostr(proto);
+  if (c->parser != "r2d2") return FILTER_UNKNOWN_PARSER;  // parser factories implemented here: r2d2
+  // net.SplitHostPort + ParseUint(port, 10, 32), port != 0 (connection.go:71-78)
+  const std::string da = gostr(dstAddr);
+  const size_t colon = da.rfind(':');
+  if (colon == std::string::npos || colon + 1 >= da.size()) return FILTER_INVALID_ADDRESS;
+  uint64_t port = 0;
+  for (size_t i = colon + 1; i < da.size(); ++i) {
+    if (da[i] < '0' || da[i] > '9') return FILTER_INVALID_ADDRESS;
+    port = port * 10 + (uint64_t)(da[i] - '0');
+    if (port > 0xFFFFFFFFull) return FILTER_INVALID_ADDRESS;
+  }
+  if (port == 0) return FILTER_INVALID_ADDRESS;
+  c->inst = inst;
+  c->ingress = ingress;
+  c->src_id = srcId;
+  c->dst_id = dstId;
+  c->port = (uint32_t)port;
+  c->policy = gostr(policyName);
+  c->orig_buf = origBuf;
+  c->reply_buf = replyBuf;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_conns[connectionId] = c;
+  return FILTER_OK;
+}
+
+void Close(uint64_t connectionId) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_conns.erase(connectionId);
+}
+
+FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoSlice* data, GoSlice* filterOps) {
+  (void)endStream;
+  std::shared_ptr<Conn> c;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_conns.find(connectionId);
+    if (it == g_conns.end()) return FILTER_UNKNOWN_CONNECTION;
+    c = it->second;
+  }
+  if (!data || !filterOps) return FILTER_UNKNOWN_ERROR;
+  // r2d2 reads bytes.Join(dataArray) (r2d2parser.go:151)
+  std::string in;
+  const GoSlice* parts = static_cast<const GoSlice*>(data->data);
+  for (int64_t i = 0; i < data->len; ++i) in.append(static_cast<const char*>(parts[i].data), (size_t)parts[i].len);
+  // frames this call will emit ops for (connection.go:141-172: until the ops
+  // slice is full or the parser asks for MORE)
+  std::vector<Frame> frames;
+  bool more = false;
+  size_t pos = 0;
+  const int64_t room = filterOps->cap - filterOps->len;
+  while ((int64_t)frames.size() < room) {
+    const size_t e = in.find("\r\n", pos);
+    if (e == std::string::npos) {
+      more = (int64_t)frames.size() < room;
+      break;
+    }
+    Frame f{e - pos + 2, !reply, "", ""};
+    if (f.request) {
+      const std::string msg = in.substr(pos, e - pos);
+      std::vector<std::string> fields;
+      size_t a = 0;
+      while (true) {  // strings.Split(msg, " ")
+        const size_t b = msg.find(' ', a);
+        fields.push_back(msg.substr(a, b == std::string::npos ? std::string::npos : b - a));
+        if (b == std::string::npos) break;
+        a = b + 1;
+      }
+      f.cmd = fields[0];
+      if (fields.size() == 2) f.file = fields[1];
+    }
+    frames.push_back(std::move(f));
+    pos = e + 2;
+  }
+  // one GPU batch for the request frames
+  std::vector<uint8_t> allow(frames.size(), 1);
+  std::vector<size_t> reqs;
+  for (size_t i = 0; i < frames.size(); ++i)
+    if (frames[i].request) reqs.push_back(i);
+  if (!reqs.empty()) {
+    Instance& inst = *c->inst;
+    std::lock_guard<std::mutex> lk(inst.mu);
+    const size_t n = reqs.size();
+    uint32_t pidx = 0xFFFFFFFFu;
+    if (cg_http_policy_index(inst.engine, c->policy.c_str(), &pidx) != CG_OK) {
+      // no such policy (or none installed): PolicyMatches is false → DROP
+      for (size_t i : reqs) allow[i] = 0;
+      reqs.clear();
+    }
+  }
+  if (!reqs.empty()) {
+    Instance& inst = *c->inst;
+    std::lock_guard<std::mutex> lk(inst.mu);
+    const size_t n = reqs.size();
+    uint32_t pidx = 0xFFFFFFFFu;
+    if (cg_http_policy_index(inst.engine, c->policy.c_str(), &pidx) != CG_OK) return FILTER_UNKNOWN_ERROR;
+    std::vector<uint32_t> pol(n, pidx), remote(n, c->src_id);  // Matches passes SrcId (connection.go:176-179)
+    std::vector<uint8_t> ing(n, c->ingress ? 1 : 0);
+    std::vector<uint16_t> port(n, (uint16_t)(c->port > 0xFFFF ? 0 : c->port));
+    std::string blob;
+    std::vector<uint64_t> off{0};
+    for (size_t i : reqs) {
+      blob += std::string("cmd") + '\0' + frames[i].cmd + '\0' + "file" + '\0' + frames[i].file + '\0';
+      off.push_back(blob.size());
+    }
+    if (blob.empty()) blob.push_back('\0');
+    size_t nslots = 0, used = 0;
+    int rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
+                          (const uint8_t*)blob.data(), off.data(), nullptr, 0, nullptr, &nslots, nullptr, 0, &used);
+    if (rc != CG_OK) return FILTER_UNKNOWN_ERROR;
+    std::vector<uint8_t> batch(cg_http_batch_bytes(inst.engine, n));
+    std::vector<uint32_t> order(cg_http_batch_slots(inst.engine, n) + 1);
+    std::vector<uint8_t> arena(used > 16 ? used : 16);
+    rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
+                      (const uint8_t*)blob.data(), off.data(), batch.data(), batch.size(), order.data(), &nslots,
+                      arena.data(), arena.size(), &used);
+    if (rc != CG_OK) return FILTER_UNKNOWN_ERROR;
+    std::vector<uint8_t> out(n);
+    rc = cg_http_verdicts_host(inst.engine, batch.data(), nslots, order.data(), n, arena.data(), arena.size(),
+                               out.data());
+    if (rc != CG_OK) return FILTER_UNKNOWN_ERROR;
+    for (size_t k = 0; k < n; ++k) allow[reqs[k]] = out[k];
+  }
+  FilterOp* ops = static_cast<FilterOp*>(filterOps->data);
+  for (size_t i = 0; i < frames.size(); ++i) {
+    if (!allow[i]) inject(c->reply_buf, "ERROR\r\n", 7);  // r2d2parser.go:197-199
+    ops[filterOps->len++] = FilterOp{(uint64_t)(allow[i] ? FILTEROP_PASS : FILTEROP_DROP), (int64_t)frames[i].len};
+  }
+  if (more) ops[filterOps->len++] = FilterOp{FILTEROP_MORE, 1};
+  return FILTER_OK;
+}
+
+}  // extern "C"

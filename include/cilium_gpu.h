@@ -247,6 +247,22 @@ int cg_ipcache_resolve_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, siz
                             cg_remote_endpoint_info* out6);
 
 /* ======================================================================== */
+/* proxylib generic L7 (proxylib/proxylib/policymap.go:118-260)              */
+/* ======================================================================== */
+
+/* Install the NetworkPolicy list of a proxylib instance (the id OpenModule
+ * returned, include/cilium_proxylib.h) — what the reference receives over
+ * NPDS (xds-path).  protobuf-JSON form with generic L7 rules:
+ *   [{"name": "cp1", "ingress_per_port_policies": [{"port": 80, "rules": [
+ *       {"remote_policies": [1], "l7_proto": "r2d2",
+ *        "l7_rules": {"l7_rules": [{"rule": {"cmd": "READ", "file": "s.*"}}]}}]}]}]
+ * Rule parsers: r2d2 (r2d2parser.go:91-123) and cassandra
+ * (cassandraparser.go:97-131); a rule with another l7_proto drops its port
+ * (policymap.go:186-204).  ParseError conditions → CG_POLICY_REJECTED and the
+ * previous snapshot stays.  Verdict contract: exact port, port 0, else deny. */
+int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len);
+
+/* ======================================================================== */
 /* HTTP L7: Envoy cilium.l7policy — envoy/cilium_network_policy.h:40-237,    */
 /* envoy/cilium_l7policy.cc:127-182                                          */
 /* ======================================================================== */

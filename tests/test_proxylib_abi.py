@@ -1,0 +1,163 @@
+"""The proxylib C ABI of libciliumgpu.so (include/cilium_proxylib.h): the
+symbols Envoy's proxylib filter dlopens (proxylib/libcilium.h:77-115), driven
+the way the reference's r2d2 tests drive them (proxylib/r2d2/
+r2d2parser_test.go:70-190: CheckInsertPolicyText → CheckNewConnectionOK →
+CheckOnDataOK with expected ops and injected reply bytes)."""
+import ctypes as C
+import json
+import os
+import re
+
+import pytest
+
+from cilium_amd import _native as N
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "cilium_proxylib.h")
+MORE, PASS, DROP = 0, 1, 2
+F_OK, F_UNKNOWN_PARSER, F_UNKNOWN_CONNECTION, F_INVALID_ADDRESS, F_INVALID_INSTANCE = 0, 3, 4, 5, 6
+
+
+class GoString(C.Structure):
+    _fields_ = [("p", C.c_char_p), ("n", C.c_ssize_t)]
+
+
+class GoSlice(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("len", C.c_int64), ("cap", C.c_int64)]
+
+
+class FilterOp(C.Structure):
+    _fields_ = [("op", C.c_uint64), ("n_bytes", C.c_int64)]
+
+
+def gs(b: bytes) -> GoString:
+    return GoString(b, len(b))
+
+
+_lib = C.CDLL(str(N.LIB_PATH))
+_lib.OpenModule.restype = C.c_uint64
+_lib.OpenModule.argtypes = [GoSlice, C.c_uint8]
+_lib.CloseModule.argtypes = [C.c_uint64]
+_lib.OnNewConnection.restype = C.c_int
+_lib.OnNewConnection.argtypes = [C.c_uint64, GoString, C.c_uint64, C.c_uint8, C.c_uint32, C.c_uint32, GoString,
+                                 GoString, GoString, C.POINTER(GoSlice), C.POINTER(GoSlice)]
+_lib.OnData.restype = C.c_int
+_lib.OnData.argtypes = [C.c_uint64, C.c_uint8, C.c_uint8, C.POINTER(GoSlice), C.POINTER(GoSlice)]
+_lib.Close.argtypes = [C.c_uint64]
+
+
+def open_module(params, device: str):
+    os.environ["CILIUM_GPU_DEVICE"] = device
+    arr = (GoString * (2 * max(len(params), 1)))()
+    for i, (k, v) in enumerate(params):
+        arr[2 * i], arr[2 * i + 1] = gs(k), gs(v)
+    return _lib.OpenModule(GoSlice(C.cast(arr, C.c_void_p), len(params), len(params)), 0)
+
+
+class Conn:
+    """A connection with caller-owned inject buffers (cap 1024 each)."""
+    _next = [1000]
+
+    def __init__(self, inst, proto=b"r2d2", ingress=True, src=1, dst=2, dst_addr=b"2.2.2.2:80", policy=b"cp1"):
+        self.orig_mem = C.create_string_buffer(1024)
+        self.reply_mem = C.create_string_buffer(1024)
+        self.orig = GoSlice(C.cast(self.orig_mem, C.c_void_p), 0, 1024)
+        self.reply = GoSlice(C.cast(self.reply_mem, C.c_void_p), 0, 1024)
+        Conn._next[0] += 1
+        self.id = Conn._next[0]
+        self.rc = _lib.OnNewConnection(inst, gs(proto), self.id, ingress, src, dst, gs(b"1.1.1.1:34567"),
+                                       gs(dst_addr), gs(policy), C.byref(self.orig), C.byref(self.reply))
+
+    def on_data(self, chunks, reply=False, cap=16):
+        bufs = [C.create_string_buffer(c, len(c)) for c in chunks]
+        arr = (GoSlice * max(len(chunks), 1))()
+        for i, (b, c) in enumerate(zip(bufs, chunks)):
+            arr[i] = GoSlice(C.cast(b, C.c_void_p), len(c), len(c))
+        data = GoSlice(C.cast(arr, C.c_void_p), len(chunks), len(chunks))
+        ops_mem = (FilterOp * cap)()
+        ops = GoSlice(C.cast(ops_mem, C.c_void_p), 0, cap)
+        rc = _lib.OnData(self.id, reply, 0, C.byref(data), C.byref(ops))
+        return rc, [(int(ops_mem[i].op), int(ops_mem[i].n_bytes)) for i in range(ops.len)]
+
+    def injected_reply(self) -> bytes:
+        return self.reply_mem.raw[:self.reply.len]
+
+    def close(self):
+        _lib.Close(self.id)
+
+
+def test_symbols_exported():
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    names = set(re.findall(r"\b(OnNewConnection|OnData|Close|OpenModule|CloseModule)\s*\(", text))
+    assert names == {"OnNewConnection", "OnData", "Close", "OpenModule", "CloseModule"}
+    for n in names:
+        assert hasattr(_lib, n)
+
+
+def test_module_and_connection_errors():
+    assert open_module([(b"bogus", b"x")], "-1") == 0  # unknown key → 0 (proxylib.go:129-131)
+    inst = open_module([(b"node-id", b"cpu-test"), (b"xds-path", b"/tmp/xds")], "-1")
+    assert inst != 0
+    assert open_module([(b"node-id", b"cpu-test"), (b"xds-path", b"/tmp/xds")], "-1") == inst  # same params
+    assert Conn(inst + 999).rc == F_INVALID_INSTANCE
+    assert Conn(inst, proto=b"nosuchparser").rc == F_UNKNOWN_PARSER
+    assert Conn(inst, dst_addr=b"2.2.2.2").rc == F_INVALID_ADDRESS
+    assert Conn(inst, dst_addr=b"2.2.2.2:0").rc == F_INVALID_ADDRESS
+    assert Conn(inst, dst_addr=b"2.2.2.2:http").rc == F_INVALID_ADDRESS
+    c = Conn(inst)
+    assert c.rc == F_OK
+    # reply direction: frames pass without a verdict (r2d2parser.go:160-162)
+    assert c.on_data([b"OK abc\r\nERR", b"OR\r\n"], reply=True) == (F_OK, [(PASS, 8), (PASS, 7), (MORE, 1)])
+    # partial request: MORE 1, no verdict needed
+    assert c.on_data([b"REA"]) == (F_OK, [(MORE, 1)])
+    # ops capacity bounds the frames handled in one call (connection.go:141)
+    assert c.on_data([b"OK\r\n" * 5], reply=True, cap=3) == (F_OK, [(PASS, 4)] * 3)
+    c.close()
+    rc, _ = c.on_data([b"READ x\r\n"])
+    assert rc == F_UNKNOWN_CONNECTION
+    bad = json.dumps([{"name": "e", "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"cmd": "JUMP"}}]}}]}]}]).encode()
+    assert N.lib.cg_proxylib_policy_update(inst, bad, len(bad)) == N.CG_POLICY_REJECTED
+    assert N.lib.cg_proxylib_policy_update(inst + 999, bad, len(bad)) == N.CG_INVALID_INSTANCE
+    _lib.CloseModule(inst)
+
+
+# the reference's r2d2 tests, end to end through the ABI
+R2D2_POLICIES = [
+    {"name": "cp1", "policy": 2, "ingress_per_port_policies": [{"port": 80, "rules": [{"l7_proto": "r2d2"}]}]},
+    {"name": "cp2", "policy": 2, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"cmd": "READ"}}]}}]}]},
+    {"name": "cp3", "policy": 2, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"file": "s.*"}}]}}]}]},
+]
+
+
+@pytest.mark.gpu
+def test_gpu_r2d2_reference_sequences():
+    inst = open_module([(b"node-id", b"gpu-test")], "0")
+    assert inst != 0
+    txt = json.dumps(R2D2_POLICIES).encode()
+    assert N.lib.cg_proxylib_policy_update(inst, txt, len(txt)) == N.CG_OK
+    # TestR2d2OnDataBasicPass (:70-95)
+    c = Conn(inst, policy=b"cp1")
+    msgs = [b"READ sssss\r\n", b"WRITE sssss\r\n", b"HALT\r\n", b"RESET\r\n"]
+    assert c.on_data([b"".join(msgs)]) == (F_OK, [(PASS, len(m)) for m in msgs] + [(MORE, 1)])
+    assert c.injected_reply() == b""
+    # TestR2d2OnDataMultipleReq (:97-117)
+    c = Conn(inst, policy=b"cp1")
+    assert c.on_data([b"RE", b"SET\r\n"]) == (F_OK, [(PASS, 7), (MORE, 1)])
+    # TestR2d2OnDataAllowDenyCmd (:119-146)
+    c = Conn(inst, policy=b"cp2")
+    m1, m2 = b"READ xssss\r\n", b"WRITE xssss\r\n"
+    assert c.on_data([m1 + m2]) == (F_OK, [(PASS, len(m1)), (DROP, len(m2)), (MORE, 1)])
+    assert c.injected_reply() == b"ERROR\r\n"
+    # TestR2d2OnDataAllowDenyRegex (:148-176)
+    c = Conn(inst, policy=b"cp3")
+    m1, m2 = b"READ ssss\r\n", b"WRITE yyyyy\r\n"
+    assert c.on_data([m1 + m2]) == (F_OK, [(PASS, len(m1)), (DROP, len(m2)), (MORE, 1)])
+    assert c.injected_reply() == b"ERROR\r\n"
+    # no policy for the port (81) and an unknown policy name: DROP
+    c = Conn(inst, policy=b"cp1", dst_addr=b"2.2.2.2:81")
+    assert c.on_data([b"READ a\r\n"]) == (F_OK, [(DROP, 8), (MORE, 1)])
+    c = Conn(inst, policy=b"nosuch")
+    assert c.on_data([b"READ a\r\n"]) == (F_OK, [(DROP, 8), (MORE, 1)])
+    _lib.CloseModule(inst)
