@@ -398,23 +398,16 @@ FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoS
   std::vector<size_t> reqs;
   for (size_t i = 0; i < frames.size(); ++i)
     if (frames[i].request) reqs.push_back(i);
-  if (!reqs.empty()) {
-    Instance& inst = *c->inst;
-    std::lock_guard<std::mutex> lk(inst.mu);
-    const size_t n = reqs.size();
-    uint32_t pidx = 0xFFFFFFFFu;
-    if (cg_http_policy_index(inst.engine, c->policy.c_str(), &pidx) != CG_OK) {
-      // no such policy (or none installed): PolicyMatches is false → DROP
-      for (size_t i : reqs) allow[i] = 0;
-      reqs.clear();
-    }
+  Instance& inst = *c->inst;
+  std::lock_guard<std::mutex> lk(inst.mu);
+  uint32_t pidx = 0xFFFFFFFFu;
+  if (!reqs.empty() && cg_http_policy_index(inst.engine, c->policy.c_str(), &pidx) != CG_OK) {
+    // no such policy (or none installed): PolicyMatches is false → DROP
+    for (size_t i : reqs) allow[i] = 0;
+    reqs.clear();
   }
   if (!reqs.empty()) {
-    Instance& inst = *c->inst;
-    std::lock_guard<std::mutex> lk(inst.mu);
     const size_t n = reqs.size();
-    uint32_t pidx = 0xFFFFFFFFu;
-    if (cg_http_policy_index(inst.engine, c->policy.c_str(), &pidx) != CG_OK) return FILTER_UNKNOWN_ERROR;
     std::vector<uint32_t> pol(n, pidx), remote(n, c->src_id);  // Matches passes SrcId (connection.go:176-179)
     std::vector<uint8_t> ing(n, c->ingress ? 1 : 0);
     std::vector<uint16_t> port(n, (uint16_t)(c->port > 0xFFFF ? 0 : c->port));
