@@ -116,6 +116,7 @@ SIGNATURES = {
     "cg_http_batch_slots": (_sz, [_u64, _sz]),
     "cg_http_pack": (C.c_int, [_u64, _sz, _p, _p, _p, _p, _p, _p, _p, _sz, _p, C.POINTER(_sz), _p, _sz,
                                C.POINTER(_sz)]),
+    "cg_http_parse_heads": (C.c_int, [_p, _p, _sz, _p, _sz, _p, C.POINTER(_sz), _p]),
     "cg_http_verdicts_dev": (C.c_int, [_u64, _p, _sz, _p, _p, _p]),
     "cg_http_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_kafka_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),

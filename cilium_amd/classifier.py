@@ -144,6 +144,30 @@ class Classifier:
                                    arena.nbytes, C.byref(used)))
         return HttpBatch(batch, arena, order[:nslots.value], nslots.value, n)
 
+    @staticmethod
+    def parse_http_heads(raw_blob: np.ndarray, raw_off: np.ndarray):
+        """cg_http_parse_heads: raw HTTP/1.x heads → (hdr_blob, hdr_off, ok)."""
+        raw_blob = np.ascontiguousarray(raw_blob, np.uint8)
+        raw_off = np.ascontiguousarray(raw_off, np.uint64)
+        n = len(raw_off) - 1
+        if len(raw_blob) == 0:
+            raw_blob = np.zeros(1, np.uint8)
+        used = C.c_size_t()
+        N.check(N.lib.cg_http_parse_heads(_p(raw_blob), _p(raw_off), n, None, 0, None, C.byref(used), None))
+        blob = np.zeros(max(used.value, 1), np.uint8)
+        off = np.zeros(n + 1, np.uint64)
+        ok = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_http_parse_heads(_p(raw_blob), _p(raw_off), n, _p(blob), blob.nbytes, _p(off),
+                                          C.byref(used), _p(ok)))
+        return blob, off, ok[:n]
+
+    def pack_http_raw(self, policy, ingress, port, remote, raw_blob: np.ndarray, raw_off: np.ndarray):
+        """Pack raw HTTP/1.x request heads: parsed by the library's codec step,
+        heads it rejects packed under an unknown policy (denied)."""
+        blob, off, ok = self.parse_http_heads(raw_blob, raw_off)
+        pol = np.where(ok.astype(bool), np.asarray(policy, np.uint32), np.uint32(0xFFFFFFFF)).astype(np.uint32)
+        return self.pack_http(pol, ingress, port, remote, blob, off)
+
     def http_verdicts(self, b: "HttpBatch") -> np.ndarray:
         """Verdicts (1 allow / 0 deny) in request order, computed on the GPU."""
         out = np.zeros(max(b.n, 1), np.uint8)

@@ -336,6 +336,18 @@ int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* in
                  const uint64_t* hdr_off, void* batch, size_t batch_cap, uint32_t* order,
                  size_t* nslots, uint8_t* arena, size_t arena_cap, size_t* arena_used);
 
+/* HTTP/1.x request heads from raw bytes (the Envoy codec
+ * step in front of AccessFilter::decodeHeaders, cilium_l7policy.cc:127-170).
+ * Request r is raw[raw_off[r] .. raw_off[r+1]): request-line, header fields,
+ * empty line.  Writes the cg_http_pack header lists (:method, :path with the
+ * query, :authority from Host, then the other headers as sent) into hdr_blob
+ * / hdr_off (n+1 entries) and ok[r] = 0 for a head the codec rejects
+ * (bad request-line, non-token name, control byte in a value, no final
+ * CRLF): pack those with policy UINT32_MAX so they are denied, as Envoy
+ * answers 400 before the filter.  hdr_blob NULL = size query (*blob_used). */
+int cg_http_parse_heads(const uint8_t* raw, const uint64_t* raw_off, size_t n, uint8_t* hdr_blob,
+                        size_t blob_cap, uint64_t* hdr_off, size_t* blob_used, uint8_t* ok);
+
 /* NetworkPolicyMap::Allowed per slot (cilium_network_policy.h:223-237):
  * d_out[slot] = 1 allow, 0 deny (→ 403), in batch slot order.  d_arena may
  * be NULL when no record overflowed.  Per-(policy,direction,port) allowed/
