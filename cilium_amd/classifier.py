@@ -354,6 +354,16 @@ class PolicyMap:
         N.check(N.lib.cg_l4_verdicts_host(self.cl.h, self.id, _p(tuples), len(tuples), _p(out)))
         return out[:len(tuples)]
 
+    def verdicts_via_ipcache(self, ipc: "IPCache", remote_v4: np.ndarray, tuples: np.ndarray) -> np.ndarray:
+        """Egress flow of bpf_lxc.c:509-527: identities from the ipcache
+        resolution of remote_v4 (network order), then __policy_can_access."""
+        tuples = np.ascontiguousarray(tuples, L4_TUPLE_DTYPE)
+        remote_v4 = np.ascontiguousarray(remote_v4, np.uint32)
+        out = np.zeros(max(len(tuples), 1), np.int32)
+        N.check(N.lib.cg_l4_verdicts_ipcache_host(self.cl.h, self.id, ipc.id, _p(remote_v4), _p(tuples), len(tuples),
+                                                  _p(out)))
+        return out[:len(tuples)]
+
     def verdicts_dev(self, d_tuples, n: int, d_out, stream=None) -> None:
         N.check(N.lib.cg_l4_verdicts_dev(self.cl.h, self.id, _p(d_tuples), n, _p(d_out), stream))
 

@@ -353,6 +353,48 @@ int cg_l4_verdicts_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, 
   });
 }
 
+// L4 verdicts with identities from the ipcache (bpf_lxc.c:509-527).
+static void l4_ipc_run(Engine& e, uint32_t map_id, uint32_t ipc_id, const uint32_t* d_addr, const cg_l4_tuple* d_t,
+                       size_t n, int32_t* d_out, void* s) {
+  e.require_gpu();
+  PolicyMapState* mp;
+  IpcacheState* ip;
+  {
+    std::lock_guard<std::mutex> lk(e.mu);
+    mp = &get_map(e, map_id);
+    ip = &get_ipc(e, ipc_id);
+    if (mp->dirty) mp->rebuild(e);
+    if (ip->dirty) ip->rebuild(e);
+  }
+  e.set_device();
+  check_launch(launch_l4_ipcache(mp->dev, ip->dev, d_addr, d_t, n, d_out, stream_of(e, s), e.cus),
+               "l4 (ipcache) kernel launch");
+}
+
+int cg_l4_verdicts_ipcache_dev(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* d_remote_v4,
+                               const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    l4_ipc_run(*e, map_id, ipc_id, d_remote_v4, d_tuples, n, d_verdicts, stream);
+  });
+}
+
+int cg_l4_verdicts_ipcache_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* remote_v4,
+                                const cg_l4_tuple* tuples, size_t n, int32_t* verdicts) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    e->set_device();
+    HostDev a, in, out;
+    void* da = a.put(remote_v4, n * 4);
+    void* din = in.put(tuples, n * sizeof(cg_l4_tuple));
+    void* dout = out.reserve(n * sizeof(int32_t));
+    l4_ipc_run(*e, map_id, ipc_id, (const uint32_t*)da, (const cg_l4_tuple*)din, n, (int32_t*)dout, nullptr);
+    dev_sync(*e, nullptr);
+    if (n) hip_check(hipMemcpy(verdicts, dout, n * sizeof(int32_t), hipMemcpyDeviceToHost), "D2H");
+  });
+}
+
 // ----------------------------------------------------------------- LPM ----
 int cg_prefilter_create(uint64_t h, uint32_t config, uint32_t max_lpm, uint32_t max_hash, uint32_t* pf_id) {
   return guarded([&] {

@@ -119,7 +119,12 @@ __device__ void l4_flush(const L4Dev& t, unsigned long long* lcnt) {
 // nbuckets*4 <= 160 KiB; the 16,384-entry default): per tuple three key
 // hashes, six LDS fingerprint reads, and a slot read only on a fingerprint
 // match (hits, and ~1.6% false matches per key).
-__global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, const uint32_t* __restrict__ tuples, size_t n,
+// kIpc: the tuple's identity is replaced by the ipcache resolution of its
+// remote IPv4 address (addrs[i], network order) — the egress flow of
+// bpf_lxc.c:509-527 (lookup_ip4_remote_endpoint → *dstID → policy_can_egress).
+template <bool kIpc>
+__global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, const uint32_t* __restrict__ addrs,
+                                                     const uint32_t* __restrict__ tuples, size_t n,
                                                      int32_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long l4_lds[];
   unsigned long long* lcnt = l4_lds;
@@ -137,9 +142,23 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, const uint32_t* __
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
       size_t i = base + u * blockDim.x + threadIdx.x;
       i = i < n ? i : n - 1;  // unconditional loads (see kafka_kernel)
-      w[u][0] = __builtin_nontemporal_load(tuples + i * 3 + 0);
+      w[u][0] = kIpc ? __builtin_bswap32(__builtin_nontemporal_load(addrs + i))
+                     : __builtin_nontemporal_load(tuples + i * 3 + 0);
       w[u][1] = __builtin_nontemporal_load(tuples + i * 3 + 1);
       w[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
+    }
+    if (kIpc) {  // the trie levels, each issued for all tuples of the lane
+      uint64_t e[kL4Tuples];
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) e[u] = ipc.l16[w[u][0] >> 16];
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u)
+        if ((uint32_t)e[u] == 0) e[u] = ipc.chunks[(size_t)(e[u] >> 32) * 256 + ((w[u][0] >> 8) & 255)];
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u)
+        if ((uint32_t)e[u] == 0) e[u] = ipc.chunks[(size_t)(e[u] >> 32) * 256 + (w[u][0] & 255)];
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = (uint32_t)e[u];
     }
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
@@ -162,11 +181,14 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, const uint32_t* __
 
 // Larger tables: fingerprints read from global memory (L2), counters as
 // global atomics.
-__global__ __launch_bounds__(256) void l4_kernel(L4Dev t, const uint32_t* __restrict__ tuples, size_t n,
+template <bool kIpc>
+__global__ __launch_bounds__(256) void l4_kernel(L4Dev t, IpcacheDev ipc, const uint32_t* __restrict__ addrs,
+                                                 const uint32_t* __restrict__ tuples, size_t n,
                                                  int32_t* __restrict__ out) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t w0 = tuples[i * 3 + 0], w1 = tuples[i * 3 + 1], len = tuples[i * 3 + 2];
+    const uint32_t w0 = kIpc ? (uint32_t)ipc_v4_value(ipc, __builtin_bswap32(addrs[i])) : tuples[i * 3 + 0];
+    const uint32_t w1 = tuples[i * 3 + 1], len = tuples[i * 3 + 2];
     const bool frag = (w1 >> 24) & CG_L4_F_FRAGMENT;
     uint32_t val = 0;
     const int which = l4_resolve(t, [&](uint32_t b) { return t.fp[b]; }, w0, w1, frag, &val);
@@ -667,23 +689,34 @@ int grid_for(size_t items, int per_block, int cus, int blocks_per_cu) {
 
 }  // namespace
 
-int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus) {
+template <bool kIpc>
+int launch_l4_t(const L4Dev& t, const IpcacheDev& ipc, const uint32_t* addrs, const void* tuples, size_t n,
+                int32_t* out, void* stream, int cus) {
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = (size_t)t.max_entries * 8 + (size_t)(t.bucket_mask + 1) * 4;
   if (lds <= 160 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute((const void*)l4_fp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void*)l4_fp_kernel<kIpc>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
-    hipLaunchKernelGGL(l4_fp_kernel, dim3(grid_for(n, 1024 * kL4Tuples, cus, 1)), dim3(1024), lds, s, t,
-                       (const uint32_t*)tuples, n, out);
+    hipLaunchKernelGGL(l4_fp_kernel<kIpc>, dim3(grid_for(n, 1024 * kL4Tuples, cus, 1)), dim3(1024), lds, s, t, ipc,
+                       addrs, (const uint32_t*)tuples, n, out);
   } else {
-    hipLaunchKernelGGL(l4_kernel, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, s, t, (const uint32_t*)tuples, n,
-                       out);
+    hipLaunchKernelGGL(l4_kernel<kIpc>, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, s, t, ipc, addrs,
+                       (const uint32_t*)tuples, n, out);
   }
   return (int)hipGetLastError();
+}
+
+int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus) {
+  return launch_l4_t<false>(t, IpcacheDev{}, nullptr, tuples, n, out, stream, cus);
+}
+
+int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, const uint32_t* addrs, const void* tuples, size_t n,
+                      int32_t* out, void* stream, int cus) {
+  return launch_l4_t<true>(t, ipc, addrs, tuples, n, out, stream, cus);
 }
 
 int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n4, uint8_t* out4,

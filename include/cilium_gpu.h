@@ -246,6 +246,17 @@ int cg_ipcache_resolve_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, siz
                             cg_remote_endpoint_info* out4, const uint8_t* v6, size_t n6,
                             cg_remote_endpoint_info* out6);
 
+/* The egress flow of bpf_lxc.c:509-527 over a batch: each tuple's remote
+ * identity is lookup_ip4_remote_endpoint(remote_v4[i]) resolved as the
+ * datapath does (WORLD_ID on a miss or sec_label 0), then
+ * __policy_can_access as cg_l4_verdicts_*; the tuples' identity fields are
+ * ignored.  remote_v4: network-order IPv4 addresses (iphdr.daddr).  Counters
+ * advance as in cg_l4_verdicts_*. */
+int cg_l4_verdicts_ipcache_dev(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* d_remote_v4,
+                               const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts, void* stream);
+int cg_l4_verdicts_ipcache_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* remote_v4,
+                                const cg_l4_tuple* tuples, size_t n, int32_t* verdicts);
+
 /* ======================================================================== */
 /* proxylib generic L7 (proxylib/proxylib/policymap.go:118-260)              */
 /* ======================================================================== */

@@ -211,3 +211,33 @@ def test_gpu_empty_ragged_and_update(gpu):
     g4, g6 = ic.resolve(a4, a6)
     o4, o6 = oracle.ipcache(k[1::2], v[1::2], a4, a6)
     assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
+
+
+# ------------------------------------------- ipcache → L4 (bpf_lxc.c:509-527)
+def _ipc_l4_case(n_entries: int, n: int, seed: int):
+    keys, ports = synth.l4_table(n_entries=n_entries, n_ids=1024, seed=seed)
+    ids = np.unique(keys["sec_label"])
+    ik, iv = synth.ipcache_entries(20_000, n_nodes=64, seed=seed)
+    rng = np.random.default_rng(seed)
+    iv = iv.copy()
+    iv[:, 0] = rng.choice(np.append(ids, [0, 2, 999_999]), len(iv))
+    a4, _ = synth.ipcache_addresses(n, ik, seed=seed)
+    tuples = synth.l4_tuples(len(a4), keys, n_ids=1024, seed=seed)
+    o4, _ = oracle.ipcache(ik, iv, a4, np.zeros((0, 16), np.uint8))
+    t2 = tuples.copy()
+    t2["identity"] = o4[:, 0]
+    exp, _, _ = oracle.l4(keys, ports, t2)
+    return keys, ports, ik, iv, a4, tuples, exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_entries", [2048, 65536])  # LDS-fingerprint kernel and the global one
+def test_gpu_l4_via_ipcache(gpu, n_entries):
+    keys, ports, ik, iv, a4, tuples, exp = _ipc_l4_case(n_entries, 300_000, 7)
+    pm = gpu.policy_map(max_entries=max(n_entries, 16384))
+    pm.allow_keys(keys, ports)
+    ic = gpu.ipcache()
+    ic.update(ik, iv)
+    got = pm.verdicts_via_ipcache(ic, a4, tuples)
+    assert np.array_equal(got, exp)
+    assert (exp == 0).any() and (exp < 0).any()
