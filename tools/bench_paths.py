@@ -5,6 +5,7 @@ configs, one JSON line each (bench.py covers config 5, the 10K-rule HTTP set):
 * CIDR prefilter (config 3): 1M mixed v4/v6 prefixes, 1B addresses
 * Kafka (config 4): 1K rules, 100M requests
 * ipcache: 512K-entry IP → identity map, 1B addresses
+* L4 with ipcache identities: config 2's map, identities resolved in-kernel
 * proxylib r2d2: 512 r2d2 rules over 64 ports, ~100M requests
   on the HTTP kernel
 
@@ -231,6 +232,46 @@ def r2d2_workload(n: int, seed: int = 0xC111A):
     return pols, reqs
 
 
+def bench_l4ipc(torch, dev, stream, cl, args, threads):
+    """Config 2's policy map with each tuple's identity resolved from its
+    remote IPv4 address through the 475K-entry ipcache in the same kernel."""
+    import oracle
+    from cilium_amd import synth
+    keys, ports = synth.l4_table()
+    pm = cl.policy_map()
+    pm.allow_keys(keys, ports)
+    ik, iv = synth.ipcache_entries()
+    rng = np.random.default_rng(5)
+    iv = iv.copy()
+    iv[:, 0] = rng.choice(np.append(np.unique(keys["sec_label"]), [0, 999_999]), len(iv))
+    ic = cl.ipcache()
+    ic.update(ik, iv)
+    D, reps = 10_000_000, 10
+    a4, _ = synth.ipcache_addresses(int(D / 0.7) + 1, ik)
+    a4 = a4[:D]
+    tup = synth.l4_tuples(D, keys)
+    got = pm.verdicts_via_ipcache(ic, a4[:1_000_000], tup[:1_000_000])
+    o4, _ = oracle.ipcache(ik, iv, a4[:1_000_000], np.zeros((0, 16), np.uint8), nthreads=threads)
+    t2 = tup[:1_000_000].copy()
+    t2["identity"] = o4[:, 0]
+    exp, _, _ = oracle.l4(keys, ports, t2)
+    assert np.array_equal(got, exp), "ipcache+L4 verdicts differ from the oracle"
+    d_t = tile_dev(torch, tup, reps, dev)
+    d_a = tile_dev(torch, a4, reps, dev)
+    n = D * reps
+    d_o = torch.empty(n, dtype=torch.int32, device=dev)
+    from cilium_amd import _native as N
+
+    def run():
+        N.check(N.lib.cg_l4_verdicts_ipcache_dev(cl.h, pm.id, ic.id, d_a.data_ptr(), d_t.data_ptr(), n,
+                                                 d_o.data_ptr(), stream.cuda_stream))
+    sec = timed(torch, stream, run, args.steps, 2)
+    return line("L4 verdicts/s with ipcache identities (bpf_lxc.c:509-527), config 2 map + 475K-entry ipcache", n,
+                sec, 20, "l4_fp_kernel<ipcache>", None, "not timed (composition of the l4 and ipcache lines)", 0,
+                {"config": {"workload": "BASELINE config 2 map, 100M tuples, identities from a 512K-draw ipcache",
+                            "tuples": n}})
+
+
 def bench_proxylib(torch, dev, stream, cl, args, threads):
     from bench import replicate_batch
     from cilium_amd.proxylib import ProxylibPolicy
@@ -266,7 +307,7 @@ def bench_proxylib(torch, dev, stream, cl, args, threads):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--paths", default="l4,lpm,kafka,ipcache,proxylib")
+    ap.add_argument("--paths", default="l4,lpm,kafka,ipcache,proxylib,l4ipc")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     args = ap.parse_args()
@@ -277,7 +318,7 @@ def main():
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
-           "proxylib": bench_proxylib}
+           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()
