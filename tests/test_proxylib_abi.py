@@ -161,3 +161,37 @@ def test_gpu_r2d2_reference_sequences():
     c = Conn(inst, policy=b"nosuch")
     assert c.on_data([b"READ a\r\n"]) == (F_OK, [(DROP, 8), (MORE, 1)])
     _lib.CloseModule(inst)
+
+
+def test_policy_update_translation_rules():
+    """cg_proxylib_policy_update applies the ParseError rules of both rule
+    parsers (r2d2parser.go:91-123, cassandraparser.go:97-131) and the port
+    rules of newPortNetworkPolicies (policymap.go:177-206)."""
+    inst = open_module([(b"node-id", b"cpu-translate")], "-1")
+    assert inst != 0
+
+    def upd(pols):
+        t = json.dumps(pols).encode()
+        return N.lib.cg_proxylib_policy_update(inst, t, len(t))
+
+    def pol(rules, port=80, proto="TCP"):
+        return [{"name": "p", "ingress_per_port_policies": [{"port": port, "protocol": proto, "rules": rules}]}]
+
+    def l7(parser, *rs):
+        return {"l7_proto": parser, "l7_rules": {"l7_rules": [{"rule": r} for r in rs]}}
+
+    assert upd(pol([l7("r2d2", {"cmd": "READ", "file": "^/a"})])) == N.CG_OK
+    assert upd(pol([l7("cassandra", {"query_action": "select", "query_table": "t$"})])) == N.CG_OK
+    assert upd(pol([l7("cassandra", {"query_action": "drop-role"})])) == N.CG_OK
+    assert upd(pol([l7("unknown-parser", {"x": "y"})])) == N.CG_OK  # the port is dropped, not an error
+    assert upd(pol([l7("r2d2"), {"l7_proto": "other"}])) == N.CG_OK  # unknown parser drops the port first
+    assert upd(pol([], proto="UDP")) == N.CG_OK
+    for bad in (pol([l7("cassandra", {"query_action": "explode"})]),
+                pol([l7("cassandra", {"query_action": "create-role", "query_table": "x"})]),
+                pol([l7("cassandra", {"table": "x"})]),
+                pol([l7("r2d2", {"cmd": "JUMP"})]),
+                pol([l7("r2d2", {"cmd": "RESET", "file": "x"})]),
+                pol([l7("r2d2"), l7("cassandra")]),
+                [{"name": "p", "ingress_per_port_policies": [{"port": 80}, {"port": 80}]}]):
+        assert upd(bad) == N.CG_POLICY_REJECTED, bad
+    _lib.CloseModule(inst)
