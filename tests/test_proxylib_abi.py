@@ -195,3 +195,36 @@ def test_policy_update_translation_rules():
                 [{"name": "p", "ingress_per_port_policies": [{"port": 80}, {"port": 80}]}]):
         assert upd(bad) == N.CG_POLICY_REJECTED, bad
     _lib.CloseModule(inst)
+
+
+@pytest.mark.gpu
+def test_gpu_shim_random_vs_oracle():
+    """Random r2d2 policies through the C++ translation and OnData framing,
+    one request frame per call, against oracle/proxylib_ref.py."""
+    import numpy as np
+
+    from oracle.proxylib_ref import ProxylibOracle
+    from test_proxylib import _rand_policies, _rand_requests
+    from cilium_amd import proxylib as P
+    inst = open_module([(b"node-id", b"gpu-random")], "0")
+    assert inst != 0
+    for seed in range(2):
+        rng = np.random.default_rng(300 + seed)
+        pols = _rand_policies(rng)
+        reqs = _rand_requests(rng, 1500, len(pols))
+        t = json.dumps(pols).encode()
+        assert N.lib.cg_proxylib_policy_update(inst, t, len(t)) == N.CG_OK
+        o = ProxylibOracle(pols)
+        conns = {}
+        for name, ingress, port, remote, line in reqs:
+            key = (name, ingress, port, remote)
+            if key not in conns:
+                conns[key] = Conn(inst, ingress=ingress, src=remote, dst=9, dst_addr=b"10.0.0.1:%d" % port,
+                                  policy=name.encode())
+                assert conns[key].rc == F_OK
+            rc, ops = conns[key].on_data([line + b"\r\n"])
+            exp = o.matches(name, ingress, port, remote, *P.r2d2_request(line))
+            assert rc == F_OK and ops == [(PASS if exp else DROP, len(line) + 2), (MORE, 1)], (key, line)
+        for c in conns.values():
+            c.close()
+    _lib.CloseModule(inst)
