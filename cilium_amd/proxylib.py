@@ -202,6 +202,78 @@ def cassandra_request(path: bytes) -> list[tuple[bytes, bytes]]:
     return [(b"cshape", b"L"), (b"action", parts[2]), (b"table", parts[3])]
 
 
+# NPDS protobuf text format (the form the reference's proxylib tests insert
+# policies in, CheckInsertPolicyText): repeated fields of
+# envoy/cilium/npds.proto:31-182 become lists, the L7 rule map entries
+# ("rule: < key: .. value: .. >") a dict.
+_REPEATED = {"ingress_per_port_policies", "egress_per_port_policies", "rules", "remote_policies", "l7_rules",
+             "http_rules", "headers", "kafka_rules"}
+_TOKEN_RE = None
+
+
+def parse_policy_text(text: str) -> dict:
+    """One NetworkPolicy in protobuf text format → the dict form used here."""
+    import re
+    global _TOKEN_RE
+    if _TOKEN_RE is None:
+        _TOKEN_RE = re.compile(r'\s*(?:(#[^\n]*)|([A-Za-z_][A-Za-z0-9_]*)|("(?:[^"\\]|\\.)*")|'
+                               r"('(?:[^'\\]|\\.)*')|(-?[0-9]+)|([:<>{}]))")
+    toks, pos = [], 0
+    while pos < len(text):
+        m = _TOKEN_RE.match(text, pos)
+        if not m or m.end() == pos:
+            if text[pos:].strip() == "":
+                break
+            raise ParseError(f"bad policy text at {pos}")
+        pos = m.end()
+        if m.group(1):
+            continue
+        toks.append(next(g for g in m.groups()[1:] if g is not None))
+    i = 0
+
+    def value(tok):
+        if tok[0] in "\"'":
+            return bytes(tok[1:-1], "utf-8").decode("unicode_escape")
+        if tok.lstrip("-").isdigit():
+            return int(tok)
+        return {"true": True, "false": False}.get(tok, tok)
+
+    def message(end):
+        nonlocal i
+        out: dict = {}
+        while i < len(toks) and toks[i] != end:
+            name = toks[i]
+            i += 1
+            if toks[i] == ":":
+                i += 1
+            if toks[i] in ("<", "{"):
+                close = ">" if toks[i] == "<" else "}"
+                i += 1
+                v = message(close)
+                i += 1
+                if name == "rule" and set(v) <= {"key", "value"}:  # map<string,string> entry
+                    out.setdefault("rule", {})[v.get("key", "")] = v.get("value", "")
+                    continue
+            else:
+                v = value(toks[i])
+                i += 1
+            if name in _REPEATED:
+                out.setdefault(name, []).append(v)
+            else:
+                out[name] = v
+        return out
+
+    pol = message(None)
+    # l7_rules is a message holding a repeated l7_rules: lift the inner list
+    for key in ("ingress_per_port_policies", "egress_per_port_policies"):
+        for pp in pol.get(key, []):
+            for r in pp.get("rules", []):
+                if "l7_rules" in r:
+                    inner = [x for wrapper in r["l7_rules"] for x in wrapper.get("l7_rules", [])]
+                    r["l7_rules"] = {"l7_rules": inner}
+    return pol
+
+
 def r2d2_request(line: bytes) -> tuple[bytes, bytes]:
     """r2d2 OnData request split (r2d2parser.go:157-167): cmd, and the file
     only when the line has exactly two space-separated fields."""

@@ -231,8 +231,54 @@ def regex_vectors(seed: int = 7, n_patterns: int = 160, n_strings: int = 24) -> 
     return {"generator": "tests/golden/make_golden.py regex_vectors(seed=7)", "cases": out}
 
 
+def _r2d2_policy(name: str, rule: str) -> str:
+    """The protobuf-text policy shape of r2d2parser_test.go (one ingress port 80
+    rule; `rule` is the l7_rules body, "" for the allow-all rule)."""
+    l7 = ("\n    l7_rules: <\n      l7_rules: <\n" + rule + "      >\n    >") if rule else ""
+    return (f'name: "{name}"\npolicy: 2\ningress_per_port_policies: <\n  port: 80\n  rules: <\n'
+            f'    l7_proto: "r2d2"{l7}\n  >\n>\n')
+
+
+def _cassandra_policy(name: str, key: str, value: str) -> str:
+    """cassandraparser_test.go's shape: remotes 1, 3, 4 and one l7 rule."""
+    return (f'name: "{name}"\npolicy: 2\ningress_per_port_policies: <\n  port: 80\n  rules: <\n'
+            '    remote_policies: 1\n    remote_policies: 3\n    remote_policies: 4\n'
+            '    l7_proto: "cassandra"\n    l7_rules: <\n      l7_rules: <\n'
+            f'        rule: <\n          key: "{key}"\n          value: "{value}"\n        >\n'
+            '      >\n    >\n  >\n>\n')
+
+
+def proxylib_kats() -> dict:
+    """proxylib policies in NPDS protobuf text (as the reference's tests insert
+    them) with the verdicts those tests assert, per request frame."""
+    r2d2 = [
+        {"src": "proxylib/r2d2/r2d2parser_test.go:70-95 TestR2d2OnDataBasicPass",
+         "policy": _r2d2_policy("cp1", ""),
+         "requests": [["READ sssss", True], ["WRITE sssss", True], ["HALT", True], ["RESET", True]]},
+        {"src": "proxylib/r2d2/r2d2parser_test.go:119-146 TestR2d2OnDataAllowDenyCmd",
+         "policy": _r2d2_policy("cp2", '        rule: <\n          key: "cmd"\n          value: "READ"\n        >\n'),
+         "requests": [["READ xssss", True], ["WRITE xssss", False]]},
+        {"src": "proxylib/r2d2/r2d2parser_test.go:148-176 TestR2d2OnDataAllowDenyRegex",
+         "policy": _r2d2_policy("cp3", '        rule: <\n          key: "file"\n          value: "s.*"\n        >\n'),
+         "requests": [["READ ssss", True], ["WRITE yyyyy", False]]},
+    ]
+    cass = [
+        {"src": "proxylib/cassandra/cassandraparser_test.go:86-115 TestCassandraOnDataOptionsReq (OPTIONS frame)",
+         "policy": _cassandra_policy("cp6", "query_action", "select"), "requests": [["/options", True]]},
+        {"src": "proxylib/cassandra/cassandraparser_test.go:145-172 TestCassandraOnDataQueryReq "
+                "(SELECT ... FROM system.local)",
+         "policy": _cassandra_policy("cp4", "query_table", ".*"),
+         "requests": [["/query/select/system.local", True]]},
+        {"src": "proxylib/cassandra/cassandraparser_test.go:236-280 TestSimpleCassandraPolicy",
+         "policy": _cassandra_policy("cp1", "query_table", "no-match"),
+         "requests": [["/options", True], ["/query/select/system.local", False]]},
+    ]
+    return {"generator": "tests/golden/make_golden.py proxylib_kats()", "remote": 1, "port": 80,
+            "r2d2": r2d2, "cassandra": cass}
+
+
 def main():
-    files = {"http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
+    files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
              "kafka_kat.json": kafka_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors()}
     for name, data in files.items():
         with open(os.path.join(HERE, name), "w") as f:

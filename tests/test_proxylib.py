@@ -291,3 +291,46 @@ def test_gpu_cassandra_kat_and_random(gpu):
     assert _cass_eval(pl, cases, False).tolist() == [int(e) for _, _, e in CASS_KAT]
     for seed in range(3):
         _check_cass(gpu, 200 + seed, 20000, False)
+
+
+# ------------------------------------------ golden: reference policy texts ----
+def _golden():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "proxylib_kat.json")))
+
+
+def _golden_eval(cl, matches_fn_name):
+    g = _golden()
+    pols, cases = [], []
+    for kind in ("r2d2", "cassandra"):
+        for c in g[kind]:
+            pol = P.parse_policy_text(c["policy"])
+            pol["name"] = f"{kind}-{pol['name']}"
+            pols.append(pol)
+            cases += [(kind, pol["name"], req.encode(), exp) for req, exp in c["requests"]]
+    o = ProxylibOracle(pols)
+    for kind, name, req, exp in cases:  # the oracle against the reference's assertions
+        if kind == "r2d2":
+            assert o.matches(name, True, g["port"], g["remote"], *P.r2d2_request(req)) == exp, (name, req)
+        else:
+            assert o.matches_path(name, True, g["port"], g["remote"], req) == exp, (name, req)
+    pl = P.ProxylibPolicy(cl)
+    pl.update(pols)
+    fields = [[(b"cmd", c), (b"file", f)] for c, f in [P.r2d2_request(r) for k, _, r, _ in cases if k == "r2d2"]]
+    fields += [P.cassandra_request(r) for k, _, r, _ in cases if k == "cassandra"]
+    ordered = [c for c in cases if c[0] == "r2d2"] + [c for c in cases if c[0] == "cassandra"]
+    n = len(ordered)
+    got = pl.matches_fields([pl.index(c[1]) for c in ordered], [1] * n, [g["port"]] * n, [g["remote"]] * n, fields,
+                            host_diag=(matches_fn_name == "host"))
+    assert got.tolist() == [int(c[3]) for c in ordered]
+
+
+def test_golden_policy_texts(host):
+    """The reference tests' protobuf-text policies (tests/golden/proxylib_kat.json)."""
+    _golden_eval(host, "host")
+
+
+@pytest.mark.gpu
+def test_gpu_golden_policy_texts(gpu):
+    _golden_eval(gpu, "gpu")
