@@ -334,3 +334,25 @@ def test_golden_policy_texts(host):
 @pytest.mark.gpu
 def test_gpu_golden_policy_texts(gpu):
     _golden_eval(gpu, "gpu")
+
+
+def test_policy_text_forms():
+    """Brace and angle-bracket message forms, comments, repeated fields."""
+    t = '''
+    # comment
+    name: "x" policy: 7
+    egress_per_port_policies { port: 9042 protocol: TCP rules {
+        remote_policies: 5 remote_policies: 6
+        l7_proto: "cassandra"
+        l7_rules { l7_rules { rule { key: "query_action" value: "select" }
+                              rule { key: "query_table" value: "^db\\\\." } } }
+    } }
+    egress_per_port_policies < port: 53 protocol: UDP >
+    '''
+    p = P.parse_policy_text(t)
+    assert p["name"] == "x" and p["policy"] == 7
+    pp = p["egress_per_port_policies"]
+    assert [x["port"] for x in pp] == [9042, 53] and pp[1]["protocol"] == "UDP"
+    r = pp[0]["rules"][0]
+    assert r["remote_policies"] == [5, 6]
+    assert r["l7_rules"] == {"l7_rules": [{"rule": {"query_action": "select", "query_table": "^db\\."}}]}
