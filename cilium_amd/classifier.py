@@ -345,6 +345,10 @@ class PolicyMap:
         return [(PolicyKey(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"])),
                  PolicyEntry(e.proxy_port, e.packets, e.bytes)) for k, e in zip(keys[:n.value], ents[:n.value])]
 
+    def destroy(self) -> None:
+        """Free the map's device tables (cg_policymap_destroy)."""
+        N.check(N.lib.cg_policymap_destroy(self.cl.h, self.id))
+
     def flush(self) -> None:
         N.check(N.lib.cg_policymap_flush(self.cl.h, self.id))
 
@@ -431,6 +435,10 @@ class PreFilter:
                 out.append(str(ipaddress.ip_network((bytes(c["addr"]), int(c["prefixlen"])))))
         return out, rev.value
 
+    def destroy(self) -> None:
+        """Free the prefilter's device tables (cg_prefilter_destroy)."""
+        N.check(N.lib.cg_prefilter_destroy(self.cl.h, self.id))
+
     def set_endpoints(self, v4_be: np.ndarray, v6: np.ndarray) -> None:
         v4_be = np.ascontiguousarray(v4_be, np.uint32)
         v6 = np.ascontiguousarray(v6, np.uint8).reshape(-1)
@@ -489,6 +497,10 @@ class IPCache:
             raise ValueError("keys and values differ in length")
         N.check(N.lib.cg_ipcache_update(self.cl.h, self.id, _p(k) if len(k) else None, _p(v) if len(v) else None,
                                         len(k)))
+
+    def destroy(self) -> None:
+        """Free the map's device tables (cg_ipcache_destroy)."""
+        N.check(N.lib.cg_ipcache_destroy(self.cl.h, self.id))
 
     def upsert(self, cidr: str, identity: int, tunnel_endpoint: int = 0) -> None:
         self.update([cidr], [[identity, tunnel_endpoint]])

@@ -241,3 +241,16 @@ def test_gpu_l4_via_ipcache(gpu, n_entries):
     got = pm.verdicts_via_ipcache(ic, a4, tuples)
     assert np.array_equal(got, exp)
     assert (exp == 0).any() and (exp < 0).any()
+
+
+def test_destroy(host):
+    ic = host.ipcache()
+    ic.upsert("10.0.0.0/8", 5)
+    ic.destroy()
+    with pytest.raises(N.CiliumGPUError) as ei:
+        ic.upsert("10.0.0.0/8", 5)
+    assert ei.value.code == N.CG_NOT_FOUND
+    pf = host.prefilter()
+    pf.destroy()
+    pm = host.policy_map()
+    pm.destroy()
