@@ -43,6 +43,13 @@ NOREMOTE = [("  unsigned long long k0 = T.rhash_keys[rh];\n  uint32_t v0 = T.rha
 VARIANTS = {
     "base": [],
     "nowalk": [NODFA, NOWALK],
+    "pftt": [("""      for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
+        const HttpTile tt = ttab[t];
+        const TileRef tb = tile_ref(tiles, tt);""", """      HttpTile nxt = ttab[min(ch.first_tile + wave, tend - 1)];
+      for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
+        const HttpTile tt = nxt;
+        nxt = ttab[min(t + nw, tend - 1)];  // next tile's entry loads under this tile's walk
+        const TileRef tb = tile_ref(tiles, tt);""")],
     "deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
     "deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "deal16": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 16;")],
