@@ -266,8 +266,18 @@ def bench_l4ipc(torch, dev, stream, cl, args, threads):
         N.check(N.lib.cg_l4_verdicts_ipcache_dev(cl.h, pm.id, ic.id, d_a.data_ptr(), d_t.data_ptr(), n,
                                                  d_o.data_ptr(), stream.cuda_stream))
     sec = timed(torch, stream, run, args.steps, 2)
+    sa, st = a4[:1_000_000], tup[:1_000_000]
+
+    def cpu_leg():
+        r4, _ = oracle.ipcache(ik, iv, sa, np.zeros((0, 16), np.uint8), nthreads=threads)
+        tt = st.copy()
+        tt["identity"] = r4[:, 0]
+        oracle.l4(keys, ports, tt)
+    cpu = cpu_rate(cpu_leg, len(st), args.cpu_seconds)
     return line("L4 verdicts/s with ipcache identities (bpf_lxc.c:509-527), config 2 map + 475K-entry ipcache", n,
-                sec, 20, "l4_fp_kernel<ipcache>", None, "not timed (composition of the l4 and ipcache lines)", 0,
+                sec, 20, "l4_fp_kernel<ipcache>", cpu,
+                f"1M tuples of the same workload: oracle ipcache ({threads} threads, incl. its map build) then "
+                "oracle.l4 (1 thread)", threads,
                 {"config": {"workload": "BASELINE config 2 map, 100M tuples, identities from a 512K-draw ipcache",
                             "tuples": n}})
 
