@@ -35,6 +35,7 @@ CG_UNSUPPORTED = 24
 CG_L4_F_INGRESS = 0x01
 CG_L4_F_FRAGMENT = 0x02
 CG_L4_F_CB_POLICY = 0x04
+CG_L4_CAN_ACCESS, CG_L4_INGRESS, CG_L4_EGRESS, CG_L4_IGNORE_DROP = 0, 1, 2, 0x100
 CG_DROP_POLICY = -133
 CG_DROP_FRAG_NOSUPPORT = -157
 
@@ -92,6 +93,8 @@ SIGNATURES = {
     "cg_policymap_flush": (C.c_int, [_u64, _u32]),
     "cg_l4_verdicts_dev": (C.c_int, [_u64, _u32, _p, _sz, _p, _p]),
     "cg_l4_verdicts_host": (C.c_int, [_u64, _u32, _p, _sz, _p]),
+    "cg_l4_policy_verdicts_dev": (C.c_int, [_u64, _u32, _u32, _p, _sz, _p, _p]),
+    "cg_l4_policy_verdicts_host": (C.c_int, [_u64, _u32, _u32, _p, _sz, _p]),
     "cg_prefilter_create": (C.c_int, [_u64, _u32, _u32, _u32, C.POINTER(_u32)]),
     "cg_prefilter_destroy": (C.c_int, [_u64, _u32]),
     "cg_prefilter_insert": (C.c_int, [_u64, _u32, _i64, _p, _sz, C.POINTER(_i64)]),
@@ -111,6 +114,8 @@ SIGNATURES = {
     "cg_proxylib_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_l4_verdicts_ipcache_dev": (C.c_int, [_u64, _u32, _u32, _p, _p, _sz, _p, _p]),
     "cg_l4_verdicts_ipcache_host": (C.c_int, [_u64, _u32, _u32, _p, _p, _sz, _p]),
+    "cg_l4_verdicts_ipcache6_dev": (C.c_int, [_u64, _u32, _u32, _p, _p, _sz, _p, _p]),
+    "cg_l4_verdicts_ipcache6_host": (C.c_int, [_u64, _u32, _u32, _p, _p, _sz, _p]),
     "cg_http_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_http_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_http_policy_stats": (C.c_int, [_u64, C.POINTER(_u64), _sz]),

@@ -352,24 +352,47 @@ class PolicyMap:
     def flush(self) -> None:
         N.check(N.lib.cg_policymap_flush(self.cl.h, self.id))
 
-    def verdicts(self, tuples: np.ndarray) -> np.ndarray:
+    def verdicts(self, tuples: np.ndarray, mode: int = N.CG_L4_CAN_ACCESS) -> np.ndarray:
+        """__policy_can_access per tuple (mode CG_L4_CAN_ACCESS), or the
+        wrappers policy_can_access_ingress (CG_L4_INGRESS) / policy_can_egress
+        (CG_L4_EGRESS), optionally | CG_L4_IGNORE_DROP (bpf/lib/policy.h:46-163)."""
         tuples = np.ascontiguousarray(tuples, L4_TUPLE_DTYPE)
         out = np.zeros(max(len(tuples), 1), np.int32)
-        N.check(N.lib.cg_l4_verdicts_host(self.cl.h, self.id, _p(tuples), len(tuples), _p(out)))
+        if mode == N.CG_L4_CAN_ACCESS:
+            N.check(N.lib.cg_l4_verdicts_host(self.cl.h, self.id, _p(tuples), len(tuples), _p(out)))
+        else:
+            N.check(N.lib.cg_l4_policy_verdicts_host(self.cl.h, self.id, mode, _p(tuples), len(tuples), _p(out)))
         return out[:len(tuples)]
 
-    def verdicts_via_ipcache(self, ipc: "IPCache", remote_v4: np.ndarray, tuples: np.ndarray) -> np.ndarray:
-        """Egress flow of bpf_lxc.c:509-527: identities from the ipcache
-        resolution of remote_v4 (network order), then __policy_can_access."""
+    def policy_can_access_ingress(self, tuples: np.ndarray) -> np.ndarray:
+        """policy_can_access_ingress (policy.h:126-146) per tuple."""
+        return self.verdicts(tuples, N.CG_L4_INGRESS)
+
+    def policy_can_egress(self, tuples: np.ndarray) -> np.ndarray:
+        """policy_can_egress (policy.h:150-163) per tuple."""
+        return self.verdicts(tuples, N.CG_L4_EGRESS)
+
+    def verdicts_via_ipcache(self, ipc: "IPCache", remote: np.ndarray, tuples: np.ndarray) -> np.ndarray:
+        """Egress flow of bpf_lxc.c:509-527 (IPv4: remote is u32 network-order
+        addresses) or :205-220 (IPv6: remote is (n, 16) u8): identities from
+        the ipcache resolution of the remote address, then policy_can_egress{4,6}."""
         tuples = np.ascontiguousarray(tuples, L4_TUPLE_DTYPE)
-        remote_v4 = np.ascontiguousarray(remote_v4, np.uint32)
         out = np.zeros(max(len(tuples), 1), np.int32)
-        N.check(N.lib.cg_l4_verdicts_ipcache_host(self.cl.h, self.id, ipc.id, _p(remote_v4), _p(tuples), len(tuples),
-                                                  _p(out)))
+        if remote.dtype == np.uint8:
+            remote = np.ascontiguousarray(remote, np.uint8).reshape(-1, 16)
+            N.check(N.lib.cg_l4_verdicts_ipcache6_host(self.cl.h, self.id, ipc.id, _p(remote), _p(tuples),
+                                                       len(tuples), _p(out)))
+        else:
+            remote = np.ascontiguousarray(remote, np.uint32)
+            N.check(N.lib.cg_l4_verdicts_ipcache_host(self.cl.h, self.id, ipc.id, _p(remote), _p(tuples),
+                                                      len(tuples), _p(out)))
         return out[:len(tuples)]
 
-    def verdicts_dev(self, d_tuples, n: int, d_out, stream=None) -> None:
-        N.check(N.lib.cg_l4_verdicts_dev(self.cl.h, self.id, _p(d_tuples), n, _p(d_out), stream))
+    def verdicts_dev(self, d_tuples, n: int, d_out, stream=None, mode: int = N.CG_L4_CAN_ACCESS) -> None:
+        if mode == N.CG_L4_CAN_ACCESS:
+            N.check(N.lib.cg_l4_verdicts_dev(self.cl.h, self.id, _p(d_tuples), n, _p(d_out), stream))
+        else:
+            N.check(N.lib.cg_l4_policy_verdicts_dev(self.cl.h, self.id, mode, _p(d_tuples), n, _p(d_out), stream))
 
     def eval_host_diag(self, tuples: np.ndarray) -> np.ndarray:
         """Table-builder diagnostics only: walk the cuckoo table on the CPU."""

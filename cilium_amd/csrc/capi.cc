@@ -76,19 +76,6 @@ void* stream_of(Engine& e, void* s) { return s ? s : e.stream; }
 
 void check_launch(int err, const char* what) { hip_check(err, what); }
 
-struct HostDev {
-  DevMem m;
-  void* put(const void* src, size_t bytes) {
-    m.alloc(bytes);
-    if (bytes) hip_check(hipMemcpy(m.get(), src, bytes, hipMemcpyHostToDevice), "H2D");
-    return m.get();
-  }
-  void* reserve(size_t bytes) {
-    m.alloc(bytes);
-    return m.get();
-  }
-};
-
 CidrKey make_cidr(const cg_cidr& c) {
   CidrKey k;
   if (c.family != 4 && c.family != 6) fail(CG_INVALID_ADDRESS, "cidr family must be 4 or 6");
@@ -270,7 +257,8 @@ int cg_policymap_lookup(uint64_t h, uint32_t map_id, const cg_policy_key* key, c
     if (entry) {
       memset(entry, 0, sizeof(*entry));
       entry->proxy_port = it->second.proxy_port_be;
-      if (e->has_gpu()) dev_sync(*e, nullptr);
+      // counters include every verdict call queued on this device so far
+      if (e->has_gpu()) hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
       m.read_counters(*e, it->second.id, &entry->packets, &entry->bytes);
     }
   });
@@ -284,10 +272,10 @@ int cg_policymap_dump(uint64_t h, uint32_t map_id, cg_policy_key* keys, cg_polic
     PolicyMapState& m = get_map(*e, map_id);
     if (n) *n = m.order.size();
     std::vector<uint64_t> ctr;
-    if (e->has_gpu() && m.d_counters.size()) {
-      dev_sync(*e, nullptr);
+    if (e->has_gpu() && m.d_counters) {
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
       ctr.resize((size_t)m.max_entries * 2);
-      hip_check(hipMemcpy(ctr.data(), m.d_counters.get(), ctr.size() * 8, hipMemcpyDeviceToHost), "D2H counters");
+      hip_check(hipMemcpy(ctr.data(), m.d_counters->get(), ctr.size() * 8, hipMemcpyDeviceToHost), "D2H counters");
     }
     size_t i = 0;
     for (uint64_t k : m.order) {
@@ -319,80 +307,115 @@ int cg_policymap_flush(uint64_t h, uint32_t map_id) {
   });
 }
 
-static void l4_run(Engine& e, uint32_t map_id, const cg_l4_tuple* d_t, size_t n, int32_t* d_out, void* s) {
+// A map's published tables, copied under the handle lock and held while the
+// launch is enqueued (engine.h DevTables).
+struct L4View {
+  std::shared_ptr<DevTables> keep;
+  L4Dev dev;
+};
+static L4View l4_view(Engine& e, uint32_t map_id) {
+  std::lock_guard<std::mutex> lk(e.mu);
+  PolicyMapState& m = get_map(e, map_id);
+  if (m.dirty) m.rebuild(e);
+  return {m.tab, m.dev};
+}
+struct IpcView {
+  std::shared_ptr<DevTables> keep;
+  IpcacheDev dev;
+};
+static IpcView ipc_view(Engine& e, uint32_t ipc_id) {
+  std::lock_guard<std::mutex> lk(e.mu);
+  IpcacheState& p = get_ipc(e, ipc_id);
+  if (p.dirty) p.rebuild(e);
+  return {p.tab, p.dev};
+}
+
+static uint32_t check_l4_mode(uint32_t mode) {
+  if ((mode & ~(3u | CG_L4_IGNORE_DROP)) || (mode & 3u) == 3u) fail(CG_INVALID_ARGUMENT, "unknown L4 verdict mode");
+  return mode;
+}
+
+static void l4_dev(Engine& e, uint32_t map_id, uint32_t mode, const cg_l4_tuple* d_t, size_t n, int32_t* d_out,
+                   void* s) {
   e.require_gpu();
-  PolicyMapState* mp;
-  {
-    std::lock_guard<std::mutex> lk(e.mu);
-    mp = &get_map(e, map_id);
-    if (mp->dirty) mp->rebuild(e);
-  }
+  const L4View v = l4_view(e, map_id);
   e.set_device();
-  check_launch(launch_l4(mp->dev, d_t, n, d_out, stream_of(e, s), e.cus), "l4 kernel launch");
+  check_launch(launch_l4(v.dev, d_t, n, d_out, mode, stream_of(e, s), e.cus), "l4 kernel launch");
+}
+
+static void l4_host(Engine& e, uint32_t map_id, uint32_t mode, const cg_l4_tuple* t, size_t n, int32_t* out) {
+  e.require_gpu();
+  if (n && (!t || !out)) fail(CG_INVALID_ARGUMENT, "NULL tuples/verdicts");
+  const L4View v = l4_view(e, map_id);
+  host_pipeline(e, n, {{t, sizeof(cg_l4_tuple)}}, {{out, sizeof(int32_t)}},
+                [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+                  check_launch(launch_l4(v.dev, din[0], cnt, (int32_t*)dout[0], mode, st, e.cus), "l4 kernel launch");
+                });
 }
 
 int cg_l4_verdicts_dev(uint64_t h, uint32_t map_id, const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts,
                        void* stream) {
-  return guarded([&] {
-    auto e = get(h);
-    l4_run(*e, map_id, d_tuples, n, d_verdicts, stream);
-  });
+  return guarded([&] { l4_dev(*get(h), map_id, CG_L4_CAN_ACCESS, d_tuples, n, d_verdicts, stream); });
 }
 
 int cg_l4_verdicts_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, size_t n, int32_t* verdicts) {
-  return guarded([&] {
-    auto e = get(h);
-    e->require_gpu();
-    e->set_device();
-    HostDev in, out;
-    void* din = in.put(tuples, n * sizeof(cg_l4_tuple));
-    void* dout = out.reserve(n * sizeof(int32_t));
-    l4_run(*e, map_id, (const cg_l4_tuple*)din, n, (int32_t*)dout, nullptr);
-    dev_sync(*e, nullptr);
-    if (n) hip_check(hipMemcpy(verdicts, dout, n * sizeof(int32_t), hipMemcpyDeviceToHost), "D2H");
-  });
+  return guarded([&] { l4_host(*get(h), map_id, CG_L4_CAN_ACCESS, tuples, n, verdicts); });
 }
 
-// L4 verdicts with identities from the ipcache (bpf_lxc.c:509-527).
-static void l4_ipc_run(Engine& e, uint32_t map_id, uint32_t ipc_id, const uint32_t* d_addr, const cg_l4_tuple* d_t,
-                       size_t n, int32_t* d_out, void* s) {
+int cg_l4_policy_verdicts_dev(uint64_t h, uint32_t map_id, uint32_t mode, const cg_l4_tuple* d_tuples, size_t n,
+                              int32_t* d_verdicts, void* stream) {
+  return guarded([&] { l4_dev(*get(h), map_id, check_l4_mode(mode), d_tuples, n, d_verdicts, stream); });
+}
+
+int cg_l4_policy_verdicts_host(uint64_t h, uint32_t map_id, uint32_t mode, const cg_l4_tuple* tuples, size_t n,
+                               int32_t* verdicts) {
+  return guarded([&] { l4_host(*get(h), map_id, check_l4_mode(mode), tuples, n, verdicts); });
+}
+
+// The egress flow with identities from the ipcache (bpf_lxc.c:509-527 v4,
+// :205-220 v6): policy_can_egress{4,6} semantics.
+static void l4_ipc_dev(Engine& e, uint32_t map_id, uint32_t ipc_id, int family, const void* d_addr,
+                       const cg_l4_tuple* d_t, size_t n, int32_t* d_out, void* s) {
   e.require_gpu();
-  PolicyMapState* mp;
-  IpcacheState* ip;
-  {
-    std::lock_guard<std::mutex> lk(e.mu);
-    mp = &get_map(e, map_id);
-    ip = &get_ipc(e, ipc_id);
-    if (mp->dirty) mp->rebuild(e);
-    if (ip->dirty) ip->rebuild(e);
-  }
+  const L4View v = l4_view(e, map_id);
+  const IpcView iv = ipc_view(e, ipc_id);
   e.set_device();
-  check_launch(launch_l4_ipcache(mp->dev, ip->dev, d_addr, d_t, n, d_out, stream_of(e, s), e.cus),
+  check_launch(launch_l4_ipcache(v.dev, iv.dev, family, d_addr, d_t, n, d_out, CG_L4_EGRESS, stream_of(e, s), e.cus),
                "l4 (ipcache) kernel launch");
+}
+
+static void l4_ipc_host(Engine& e, uint32_t map_id, uint32_t ipc_id, int family, const void* addr,
+                        const cg_l4_tuple* t, size_t n, int32_t* out) {
+  e.require_gpu();
+  if (n && (!addr || !t || !out)) fail(CG_INVALID_ARGUMENT, "NULL addresses/tuples/verdicts");
+  const L4View v = l4_view(e, map_id);
+  const IpcView iv = ipc_view(e, ipc_id);
+  host_pipeline(e, n, {{addr, family == 6 ? 16u : 4u}, {t, sizeof(cg_l4_tuple)}}, {{out, sizeof(int32_t)}},
+                [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+                  check_launch(launch_l4_ipcache(v.dev, iv.dev, family, din[0], din[1], cnt, (int32_t*)dout[0],
+                                                 CG_L4_EGRESS, st, e.cus),
+                               "l4 (ipcache) kernel launch");
+                });
 }
 
 int cg_l4_verdicts_ipcache_dev(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* d_remote_v4,
                                const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts, void* stream) {
-  return guarded([&] {
-    auto e = get(h);
-    l4_ipc_run(*e, map_id, ipc_id, d_remote_v4, d_tuples, n, d_verdicts, stream);
-  });
+  return guarded([&] { l4_ipc_dev(*get(h), map_id, ipc_id, 4, d_remote_v4, d_tuples, n, d_verdicts, stream); });
 }
 
 int cg_l4_verdicts_ipcache_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* remote_v4,
                                 const cg_l4_tuple* tuples, size_t n, int32_t* verdicts) {
-  return guarded([&] {
-    auto e = get(h);
-    e->require_gpu();
-    e->set_device();
-    HostDev a, in, out;
-    void* da = a.put(remote_v4, n * 4);
-    void* din = in.put(tuples, n * sizeof(cg_l4_tuple));
-    void* dout = out.reserve(n * sizeof(int32_t));
-    l4_ipc_run(*e, map_id, ipc_id, (const uint32_t*)da, (const cg_l4_tuple*)din, n, (int32_t*)dout, nullptr);
-    dev_sync(*e, nullptr);
-    if (n) hip_check(hipMemcpy(verdicts, dout, n * sizeof(int32_t), hipMemcpyDeviceToHost), "D2H");
-  });
+  return guarded([&] { l4_ipc_host(*get(h), map_id, ipc_id, 4, remote_v4, tuples, n, verdicts); });
+}
+
+int cg_l4_verdicts_ipcache6_dev(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint8_t* d_remote_v6,
+                                const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts, void* stream) {
+  return guarded([&] { l4_ipc_dev(*get(h), map_id, ipc_id, 6, d_remote_v6, d_tuples, n, d_verdicts, stream); });
+}
+
+int cg_l4_verdicts_ipcache6_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint8_t* remote_v6,
+                                 const cg_l4_tuple* tuples, size_t n, int32_t* verdicts) {
+  return guarded([&] { l4_ipc_host(*get(h), map_id, ipc_id, 6, remote_v6, tuples, n, verdicts); });
 }
 
 // ----------------------------------------------------------------- LPM ----
@@ -526,25 +549,27 @@ int cg_prefilter_set_endpoints(uint64_t h, uint32_t pf_id, const uint32_t* v4, s
   });
 }
 
-static void lpm_run(Engine& e, uint32_t pf_id, const uint32_t* d_v4, size_t n4, uint8_t* d_o4, const uint8_t* d_v6,
-                    size_t n6, uint8_t* d_o6, void* s) {
-  e.require_gpu();
-  PrefilterState* p;
-  {
-    std::lock_guard<std::mutex> lk(e.mu);
-    p = &get_pf(e, pf_id);
-    if (p->dirty) p->rebuild(e);
-  }
-  e.set_device();
-  check_launch(launch_lpm(p->dev, p->v4_filter, p->v6_filter, d_v4, n4, d_o4, d_v6, n6, d_o6, stream_of(e, s), e.cus),
-               "lpm kernel launch");
+struct LpmView {
+  std::shared_ptr<DevTables> keep;
+  LpmDev dev;
+  bool v4f, v6f;
+};
+static LpmView lpm_view(Engine& e, uint32_t pf_id) {
+  std::lock_guard<std::mutex> lk(e.mu);
+  PrefilterState& p = get_pf(e, pf_id);
+  if (p.dirty) p.rebuild(e);
+  return {p.tab, p.dev, p.v4_filter, p.v6_filter};
 }
 
 int cg_prefilter_verdicts_dev(uint64_t h, uint32_t pf_id, const uint32_t* d_v4, size_t n4, uint8_t* d_out4,
                               const uint8_t* d_v6, size_t n6, uint8_t* d_out6, void* stream) {
   return guarded([&] {
     auto e = get(h);
-    lpm_run(*e, pf_id, d_v4, n4, d_out4, d_v6, n6, d_out6, stream);
+    e->require_gpu();
+    const LpmView v = lpm_view(*e, pf_id);
+    e->set_device();
+    check_launch(launch_lpm(v.dev, v.v4f, v.v6f, d_v4, n4, d_out4, d_v6, n6, d_out6, stream_of(*e, stream), e->cus),
+                 "lpm kernel launch");
   });
 }
 
@@ -553,16 +578,18 @@ int cg_prefilter_verdicts_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, s
   return guarded([&] {
     auto e = get(h);
     e->require_gpu();
-    e->set_device();
-    HostDev a, b, c, d;
-    void* d4 = a.put(v4, n4 * 8);
-    void* d6 = b.put(v6, n6 * 32);
-    void* o4 = c.reserve(n4 + 1);
-    void* o6 = d.reserve(n6 + 1);
-    lpm_run(*e, pf_id, (const uint32_t*)d4, n4, (uint8_t*)o4, (const uint8_t*)d6, n6, (uint8_t*)o6, nullptr);
-    dev_sync(*e, nullptr);
-    if (n4) hip_check(hipMemcpy(out4, o4, n4, hipMemcpyDeviceToHost), "D2H");
-    if (n6) hip_check(hipMemcpy(out6, o6, n6, hipMemcpyDeviceToHost), "D2H");
+    if ((n4 && (!v4 || !out4)) || (n6 && (!v6 || !out6))) fail(CG_INVALID_ARGUMENT, "NULL address/verdict arrays");
+    const LpmView v = lpm_view(*e, pf_id);
+    host_pipeline(*e, n4, {{v4, 8}}, {{out4, 1}}, [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+      check_launch(launch_lpm(v.dev, v.v4f, v.v6f, (const uint32_t*)din[0], cnt, (uint8_t*)dout[0], nullptr, 0,
+                              nullptr, st, e->cus),
+                   "lpm kernel launch");
+    });
+    host_pipeline(*e, n6, {{v6, 32}}, {{out6, 1}}, [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+      check_launch(launch_lpm(v.dev, v.v4f, v.v6f, nullptr, 0, nullptr, (const uint8_t*)din[0], cnt,
+                              (uint8_t*)dout[0], st, e->cus),
+                   "lpm kernel launch");
+    });
   });
 }
 
@@ -659,26 +686,17 @@ int cg_ipcache_dump(uint64_t h, uint32_t ipc_id, cg_cidr* keys, cg_remote_endpoi
   });
 }
 
-static void ipcache_run(Engine& e, uint32_t ipc_id, const uint32_t* d_v4, size_t n4, cg_remote_endpoint_info* d_o4,
-                        const uint8_t* d_v6, size_t n6, cg_remote_endpoint_info* d_o6, void* s) {
-  e.require_gpu();
-  IpcacheState* p;
-  {
-    std::lock_guard<std::mutex> lk(e.mu);
-    p = &get_ipc(e, ipc_id);
-    if (p->dirty) p->rebuild(e);
-  }
-  e.set_device();
-  check_launch(launch_ipcache(p->dev, d_v4, n4, (IpcVal*)d_o4, d_v6, n6, (IpcVal*)d_o6, stream_of(e, s), e.cus),
-               "ipcache kernel launch");
-}
-
 int cg_ipcache_resolve_dev(uint64_t h, uint32_t ipc_id, const uint32_t* d_v4, size_t n4,
                            cg_remote_endpoint_info* d_out4, const uint8_t* d_v6, size_t n6,
                            cg_remote_endpoint_info* d_out6, void* stream) {
   return guarded([&] {
     auto e = get(h);
-    ipcache_run(*e, ipc_id, d_v4, n4, d_out4, d_v6, n6, d_out6, stream);
+    e->require_gpu();
+    const IpcView v = ipc_view(*e, ipc_id);
+    e->set_device();
+    check_launch(launch_ipcache(v.dev, d_v4, n4, (IpcVal*)d_out4, d_v6, n6, (IpcVal*)d_out6, stream_of(*e, stream),
+                                e->cus),
+                 "ipcache kernel launch");
   });
 }
 
@@ -688,17 +706,18 @@ int cg_ipcache_resolve_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, siz
   return guarded([&] {
     auto e = get(h);
     e->require_gpu();
-    e->set_device();
-    HostDev a, b, c, d;
-    void* d4 = a.put(v4, n4 * 4);
-    void* d6 = b.put(v6, n6 * 16);
-    void* o4 = c.reserve(n4 * 8 + 8);
-    void* o6 = d.reserve(n6 * 8 + 8);
-    ipcache_run(*e, ipc_id, (const uint32_t*)d4, n4, (cg_remote_endpoint_info*)o4, (const uint8_t*)d6, n6,
-                (cg_remote_endpoint_info*)o6, nullptr);
-    dev_sync(*e, nullptr);
-    if (n4) hip_check(hipMemcpy(out4, o4, n4 * 8, hipMemcpyDeviceToHost), "D2H");
-    if (n6) hip_check(hipMemcpy(out6, o6, n6 * 8, hipMemcpyDeviceToHost), "D2H");
+    if ((n4 && (!v4 || !out4)) || (n6 && (!v6 || !out6))) fail(CG_INVALID_ARGUMENT, "NULL address/result arrays");
+    const IpcView v = ipc_view(*e, ipc_id);
+    host_pipeline(*e, n4, {{v4, 4}}, {{out4, 8}}, [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+      check_launch(launch_ipcache(v.dev, (const uint32_t*)din[0], cnt, (IpcVal*)dout[0], nullptr, 0, nullptr, st,
+                                  e->cus),
+                   "ipcache kernel launch");
+    });
+    host_pipeline(*e, n6, {{v6, 16}}, {{out6, 8}}, [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+      check_launch(launch_ipcache(v.dev, nullptr, 0, nullptr, (const uint8_t*)din[0], cnt, (IpcVal*)dout[0], st,
+                                  e->cus),
+                   "ipcache kernel launch");
+    });
   });
 }
 
@@ -834,26 +853,42 @@ int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const u
   });
 }
 
+// Copy a host array into the lease's pinned buffer i and DMA it to its
+// device buffer i (async on the lease's stream).
+static void* stage_in(StagingSlot& sl, int i, const void* src, size_t bytes) {
+  void* d = sl.dev_buf(i, bytes);
+  if (!bytes) return d;
+  void* hb = sl.host_buf(i, bytes);
+  memcpy(hb, src, bytes);
+  hip_check(hipMemcpyAsync(d, hb, bytes, hipMemcpyHostToDevice, (hipStream_t)sl.stream), "H2D");
+  return d;
+}
+
 int cg_http_verdicts_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order, size_t n,
                           const uint8_t* arena, size_t arena_len, uint8_t* out) {
   return guarded([&] {
     auto e = get(h);
     e->require_gpu();
     auto s = http_snap(*e);
+    if (!batch || (n && (!order || !out))) fail(CG_INVALID_ARGUMENT, "NULL batch/order/out");
     HttpBatchHeader hdr;
     memcpy(&hdr, batch, sizeof(hdr));
     if (hdr.magic != kBatchMagic || hdr.epoch != s->epoch)
       fail(CG_INVALID_ARGUMENT, "batch was packed against another policy snapshot");
+    if (hdr.nslots != nslots) fail(CG_INVALID_ARGUMENT, "nslots differs from the packed batch");
+    if (hdr.arena_bytes && (!arena || arena_len < hdr.arena_bytes))
+      fail(CG_INVALID_ARGUMENT, "overflow arena shorter than the packed batch needs");
     e->set_device();
-    HostDev r, a, o;
-    void* dr = r.put(batch, batch_used_bytes(batch));
-    void* da = a.put(arena, arena ? arena_len : 0);
-    void* dout = o.reserve(nslots + 1);
-    check_launch(launch_http(s->dev, dr, nslots, (const uint8_t*)da, (uint8_t*)dout, e->stream, e->cus),
+    auto lease = e->staging.acquire(e->device);
+    void* dr = stage_in(*lease, 0, batch, batch_used_bytes(batch));
+    void* da = stage_in(*lease, 1, arena, hdr.arena_bytes);
+    void* dout = lease->dev_buf(2, nslots + 1);
+    check_launch(launch_http(s->dev, dr, nslots, (const uint8_t*)da, (uint8_t*)dout, lease->stream, e->cus),
                  "http kernel launch");
-    dev_sync(*e, nullptr);
-    std::vector<uint8_t> slots(nslots);
-    if (nslots) hip_check(hipMemcpy(slots.data(), dout, nslots, hipMemcpyDeviceToHost), "D2H");
+    uint8_t* slots = (uint8_t*)lease->host_buf(2, nslots + 1);
+    if (nslots)
+      hip_check(hipMemcpyAsync(slots, dout, nslots, hipMemcpyDeviceToHost, (hipStream_t)lease->stream), "D2H");
+    hip_check(hipStreamSynchronize((hipStream_t)lease->stream), "hipStreamSynchronize");
     for (size_t i = 0; i < nslots; ++i)
       if (order[i] < n) out[order[i]] = slots[i];
   });
@@ -918,15 +953,17 @@ int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n, c
     auto e = get(h);
     e->require_gpu();
     auto s = kafka_snap(*e);
+    if (n && (!reqs || !out)) fail(CG_INVALID_ARGUMENT, "NULL requests/out");
     e->set_device();
-    HostDev r, a, o;
-    void* dr = r.put(reqs, n * sizeof(cg_kafka_request));
-    void* da = a.put(arena, arena ? arena_len * 4 : 0);
-    void* dout = o.reserve(n + 1);
-    check_launch(launch_kafka(s->dev, dr, n, (const uint32_t*)da, (uint8_t*)dout, e->stream, e->cus),
-                 "kafka kernel launch");
-    dev_sync(*e, nullptr);
-    if (n) hip_check(hipMemcpy(out, dout, n, hipMemcpyDeviceToHost), "D2H");
+    // the topic arena is shared by every chunk: one copy on its own lease
+    auto lease = e->staging.acquire(e->device);
+    const uint32_t* da = (const uint32_t*)stage_in(*lease, 0, arena, arena ? arena_len * 4 : 0);
+    hip_check(hipStreamSynchronize((hipStream_t)lease->stream), "hipStreamSynchronize");
+    host_pipeline(*e, n, {{reqs, sizeof(cg_kafka_request)}}, {{out, 1}},
+                  [&](void* const* din, void* const* dout, size_t cnt, void* st) {
+                    check_launch(launch_kafka(s->dev, din[0], cnt, da, (uint8_t*)dout[0], st, e->cus),
+                                 "kafka kernel launch");
+                  });
   });
 }
 
@@ -945,8 +982,8 @@ static void counters_loc(Engine& e, uint32_t what, uint32_t id, void** p, size_t
   } else if (what == 2) {
     std::lock_guard<std::mutex> lk(e.mu);
     PrefilterState& pf = get_pf(e, id);
-    *p = pf.d_counters.get();
-    *n = pf.d_counters.get() ? 2 : 0;
+    *p = pf.d_counters ? pf.d_counters->get() : nullptr;
+    *n = pf.d_counters ? 2 : 0;
   } else {
     fail(CG_INVALID_ARGUMENT, "unknown counter set");
   }
@@ -961,7 +998,8 @@ int cg_read_counters(uint64_t h, uint32_t what, uint32_t id, uint64_t* out, size
     if (n) *n = cnt;
     size_t k = std::min(cap, cnt);
     if (k && p && e->has_gpu()) {
-      dev_sync(*e, nullptr);
+      e->set_device();
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
       hip_check(hipMemcpy(out, p, k * 8, hipMemcpyDeviceToHost), "D2H counters");
     } else if (k) {
       memset(out, 0, k * 8);
@@ -996,12 +1034,15 @@ int cg_reset_counters(uint64_t h) {
   return guarded([&] {
     auto e = get(h);
     if (!e->has_gpu()) return;
-    dev_sync(*e, nullptr);
+    e->set_device();
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     std::lock_guard<std::mutex> lk(e->mu);
     if (e->http) e->http->d_counters.zero();
     if (e->kafka) e->kafka->d_counters.zero();
-    for (auto& [id, p] : e->prefilters) p->d_counters.zero();
-    for (auto& [id, m] : e->maps) m->d_counters.zero();
+    for (auto& [id, p] : e->prefilters)
+      if (p->d_counters) p->d_counters->zero();
+    for (auto& [id, m] : e->maps)
+      if (m->d_counters) m->d_counters->zero();
   });
 }
 

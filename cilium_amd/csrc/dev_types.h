@@ -184,7 +184,8 @@ struct HttpBatchHeader {
   uint64_t nslots;
   uint64_t ttab_off;   // byte offset of the tile table (ntiles HttpTile)
   uint64_t total_bytes;
-  uint32_t pad[4];
+  uint64_t arena_bytes;  // overflow arena bytes the batch refers to (0: none)
+  uint32_t pad[2];
 };
 struct HttpTile {
   uint32_t at;     // tile data at tiles_off + at * 512: the 512-byte meta block

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -45,6 +46,78 @@ class DevMem {
   size_t n_ = 0;
 };
 
+// One published build of a map's device tables.  A rebuild uploads into a
+// fresh set and swaps the shared_ptr under the handle lock; a launch copies
+// the shared_ptr (and the table view) under that lock and holds it past the
+// enqueue.  So neither a rebuild nor a destroy overwrites or frees tables a
+// queued kernel reads: an old set is freed when its last holder lets go, and
+// hipFree waits for the device's queued work before it returns.
+struct DevTables {
+  std::vector<DevMem> bufs;
+  std::shared_ptr<DevMem> counters;  // survives rebuilds (per-entry counters)
+  template <class T>
+  T* add(const std::vector<T>& v) {
+    bufs.emplace_back();
+    bufs.back().upload_vec(v);
+    return bufs.back().as<T>();
+  }
+};
+
+// Page-locked host buffer (hipHostMalloc), grow-only.
+class PinnedMem {
+ public:
+  PinnedMem() = default;
+  ~PinnedMem();
+  PinnedMem(const PinnedMem&) = delete;
+  PinnedMem& operator=(const PinnedMem&) = delete;
+  void reserve(size_t bytes);
+  void* get() const { return p_; }
+  size_t size() const { return n_; }
+
+ private:
+  void* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// A staging slot for the "_host" entry points: its own stream, grow-only
+// device buffers and pinned host buffers, so host calls make no hipMalloc /
+// hipFree and copy with async DMA instead of pageable hipMemcpy.
+struct StagingSlot {
+  static constexpr int kBufs = 4;
+  void* stream = nullptr;  // hipStream_t
+  DevMem dev[kBufs];
+  PinnedMem host[kBufs];
+  void* dev_buf(int i, size_t bytes);  // grow-only device buffer i
+  void* host_buf(int i, size_t bytes); // grow-only pinned buffer i
+  ~StagingSlot();
+};
+
+// Slots are leased per call, so concurrent host calls on one handle (Envoy
+// workers, proxylib connections) proceed in parallel; a slot returns to the
+// pool when the lease ends.
+class StagingPool {
+ public:
+  class Lease {
+   public:
+    Lease(StagingPool* p, StagingSlot* s) : p_(p), s_(s) {}
+    Lease(Lease&& o) noexcept : p_(o.p_), s_(o.s_) { o.s_ = nullptr; }
+    ~Lease();
+    StagingSlot* operator->() const { return s_; }
+    StagingSlot& operator*() const { return *s_; }
+
+   private:
+    StagingPool* p_;
+    StagingSlot* s_;
+  };
+  Lease acquire(int device);
+  void clear();
+
+ private:
+  std::mutex mu_;
+  std::vector<std::unique_ptr<StagingSlot>> all_;
+  std::vector<StagingSlot*> free_;
+};
+
 struct PolicyMapState;
 struct PrefilterState;
 struct IpcacheState;
@@ -64,6 +137,7 @@ struct Engine {
   std::map<uint32_t, std::unique_ptr<IpcacheState>> ipcaches;
   std::shared_ptr<HttpSnapshot> http;
   std::shared_ptr<KafkaSnapshot> kafka;
+  StagingPool staging;  // the "_host" entry points' buffers and streams
 
   bool has_gpu() const { return device >= 0; }
   void require_gpu() const {
@@ -75,5 +149,24 @@ struct Engine {
 // HIP helpers (runtime.cc)
 void hip_check(int err, const char* what);
 void dev_sync(Engine& e, void* stream);
+
+// Element-wise host pipeline for the "_host" entry points: items [0, n) go
+// through in chunks; per chunk each input array is copied into a pinned
+// buffer, DMA'd to the device (async), `launch` runs on the slot's stream
+// over the chunk, and each output array comes back the same way.  Two
+// slots alternate, so the CPU copies of one chunk overlap the other's DMA
+// and kernel.  elem sizes are bytes per item; `launch` gets the device
+// pointers of the chunk's inputs and outputs, the item count and the stream.
+struct HostIn {
+  const void* src;
+  size_t elem;
+};
+struct HostOut {
+  void* dst;
+  size_t elem;
+};
+void host_pipeline(Engine& e, size_t n, const std::vector<HostIn>& ins, const std::vector<HostOut>& outs,
+                   const std::function<void(void* const* din, void* const* dout, size_t count, void* stream)>& launch,
+                   size_t chunk_items = 0);
 
 }  // namespace cg

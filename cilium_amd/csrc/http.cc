@@ -204,6 +204,7 @@ ByteSet value_alphabet() {
 
 // One deterministic automaton per (field, conjunction of matchers).
 struct FieldDfaCache {
+  bool raw = false;  // proxylib snapshot: matchers see arbitrary bytes, escaped (regex.h)
   std::vector<ByteDfa> dfas;
   std::map<std::string, int> by_key;
   int any_id = -1;
@@ -227,7 +228,10 @@ struct FieldDfaCache {
     std::string key = std::string(1, "ERPS"[(int)m.kind]) + ":" + m.value;
     auto it = by_key.find(key);
     if (it != by_key.end()) return it->second;
-    ByteSet va = value_alphabet();
+    // Envoy values never hold 0x00-0x02 (the codec rejects them); proxylib
+    // values may hold any byte and arrive escaped (packer), so their
+    // matchers are compiled over all bytes and then escaped
+    ByteSet va = raw ? ByteSet::all() : value_alphabet();
     ByteDfa d;
     switch (m.kind) {
       case MKind::Exact: d = dfa_literal(m.value, va); break;
@@ -235,6 +239,7 @@ struct FieldDfaCache {
       case MKind::Present: d = dfa_star(va); break;
       case MKind::Search: d = compile_regex(m.value, va, MatchMode::Search); break;
     }
+    if (raw) d = dfa_escape_low(d);
     return add(std::move(d), key);
   }
   int conj(const std::vector<const MatcherSpec*>& ms) {
@@ -479,6 +484,13 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
   for (int i = 0; i < F; ++i) field_idx[S.fields[i]] = i;
 
   FieldDfaCache fc;
+  {
+    size_t nraw = 0;
+    for (const auto& p : pols) nraw += p.deny_unlisted;
+    if (nraw && nraw != pols.size())
+      fail(CG_POLICY_REJECTED, "proxylib and Envoy HTTP policies cannot share one snapshot");
+    S.raw_values = fc.raw = nraw != 0;
+  }
   S.npolicies = (uint32_t)pols.size();
   S.dflt.assign((size_t)S.npolicies * 2, kProgAllow);
   std::vector<std::pair<uint32_t, uint32_t>> phash;  // key → prog

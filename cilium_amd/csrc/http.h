@@ -13,6 +13,9 @@ namespace cg {
 
 struct HttpSnapshot {
   std::vector<std::string> fields;  // walked fields, canonical order, lowercase
+  // proxylib snapshot: field values are arbitrary bytes, given escaped (bytes
+  // 0x00-0x03 as 0x03, 0x10 + b; regex.h kEscByte) and never codec-rejected
+  bool raw_values = false;
   std::map<std::string, uint32_t> policy_index;
   uint32_t npolicies = 0;
 

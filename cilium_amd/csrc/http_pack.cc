@@ -9,6 +9,7 @@
 // (the tile table gives each tile's offset and unit count), so the batch is
 // as large as its strings, not as the 128-byte slot.
 #include <algorithm>
+#include <cstddef>
 #include <array>
 #include <cstring>
 #include <map>
@@ -115,8 +116,20 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
         while (p < e && *p) ++p;
         size_t vlen = p - v;
         if (p < e) ++p;
-        for (size_t k = 0; k < vlen; ++k)
-          if (codec_rejects(v[k])) malformed[i] = 1;
+        if (s.raw_values) {
+          // escaped proxylib value: no raw byte <= 0x02, and 0x03 only as
+          // the first byte of an escape pair
+          for (size_t k = 0; k < vlen; ++k) {
+            if (v[k] <= 0x02) malformed[i] = 1;
+            if (v[k] == 0x03) {
+              if (k + 1 >= vlen || v[k + 1] < 0x10 || v[k + 1] > 0x13) malformed[i] = 1;
+              ++k;
+            }
+          }
+        } else {
+          for (size_t k = 0; k < vlen; ++k)
+            if (codec_rejects(v[k])) malformed[i] = 1;
+        }
         for (size_t f = 0; f < F; ++f)
           if (!vp[f] && name_eq_ci(nm, nl, s.fields[f])) {  // first value wins (HeaderMap::get)
             vp[f] = v;
@@ -256,6 +269,10 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   }
   if (arena_used) *arena_used = used;
   if (arena && used > arena_cap) fail(CG_INVALID_ARGUMENT, "overflow arena too small");
+  if (batch) {
+    uint64_t ab = used;
+    memcpy((uint8_t*)batch + offsetof(HttpBatchHeader, arena_bytes), &ab, sizeof(ab));
+  }
 }
 
 void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* arena, size_t arena_len,

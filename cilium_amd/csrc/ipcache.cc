@@ -150,17 +150,16 @@ void IpcacheState::rebuild(Engine& e) {
   build_tables();
   if (e.has_gpu()) {
     e.set_device();
-    d_l16.upload_vec(l16);
-    d_chunks.upload_vec(chunks);
-    d_idx6.upload_vec(idx6);
-    d_runs6.upload_vec(runs6);
-    dev = IpcacheDev{};
-    dev.l16 = d_l16.as<uint64_t>();
-    dev.chunks = d_chunks.as<uint64_t>();
-    dev.idx6 = d_idx6.as<uint32_t>();
-    dev.runs6 = d_runs6.as<uint64_t>();
-    dev.v6_bits = v6_bits;
-    dev.nruns6 = (uint32_t)(runs6.size() / 4);
+    auto t = std::make_shared<DevTables>();
+    IpcacheDev d{};
+    d.l16 = t->add(l16);
+    d.chunks = t->add(chunks);
+    d.idx6 = t->add(idx6);
+    d.runs6 = t->add(runs6);
+    d.v6_bits = v6_bits;
+    d.nruns6 = (uint32_t)(runs6.size() / 4);
+    tab = std::move(t);  // publish (the caller holds the handle lock)
+    dev = d;
   }
   dirty = false;
 }

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <map>
+#include <memory>
 #include <vector>
 
 #include "dev_types.h"
@@ -22,8 +23,8 @@ struct IpcacheState {
   std::vector<uint64_t> l16, chunks, runs6;
   std::vector<uint32_t> idx6;
   uint32_t v6_bits = 16;
-  DevMem d_l16, d_chunks, d_idx6, d_runs6;
-  IpcacheDev dev{};
+  std::shared_ptr<DevTables> tab;  // the published device tables (engine.h)
+  IpcacheDev dev{};                // view of tab; copy it together with tab
 
   void build_tables();
   IpcacheDev host_view() const;

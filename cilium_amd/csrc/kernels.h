@@ -10,11 +10,12 @@ namespace cg {
 
 // All launchers enqueue on `stream` (hipStream_t) and return the hipError_t
 // of the launch.  n == 0 launches nothing.
-int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus);
+// mode: CG_L4_CAN_ACCESS / CG_L4_INGRESS / CG_L4_EGRESS [| CG_L4_IGNORE_DROP].
+int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, uint32_t mode, void* stream, int cus);
 // launch_l4 with each tuple's identity taken from the ipcache resolution of
-// addrs[i] (remote IPv4 address, network order).
-int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, const uint32_t* addrs, const void* tuples, size_t n,
-                      int32_t* out, void* stream, int cus);
+// addrs[i] (remote address, network order: u32 for family 4, 16 bytes for 6).
+int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, int family, const void* addrs, const void* tuples,
+                      size_t n, int32_t* out, uint32_t mode, void* stream, int cus);
 int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* v4, size_t n4,
                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus);
 int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,

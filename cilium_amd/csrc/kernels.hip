@@ -5,6 +5,9 @@
 // packed input, counters privatized in LDS and flushed once per block.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include "../../include/cilium_gpu.h"
 #include "dev_types.h"
 #include "kernels.h"
@@ -29,6 +32,23 @@ __device__ __forceinline__ int32_t l4_verdict(int which, uint32_t val, uint32_t 
   if (which == 2) return 0;  // TC_ACT_OK: the L3 entry's proxy_port is ignored
   if (flags & CG_L4_F_CB_POLICY) return 0;
   return (flags & CG_L4_F_FRAGMENT) ? CG_DROP_FRAG_NOSUPPORT : CG_DROP_POLICY;
+}
+
+// The verdict wrappers (bpf/lib/policy.h:126-163).  mode & 3:
+// CG_L4_CAN_ACCESS = __policy_can_access with the tuple's own direction and
+// fragment flags; CG_L4_INGRESS = policy_can_access_ingress (dir CT_INGRESS,
+// the tuple's is_fragment); CG_L4_EGRESS = policy_can_egress (dir CT_EGRESS,
+// is_fragment false).  Both wrappers return DROP_POLICY for any negative
+// result, or TC_ACT_OK when built with IGNORE_DROP (mode & CG_L4_IGNORE_DROP).
+__device__ __forceinline__ uint32_t l4_mode_word(uint32_t w1, uint32_t mode) {
+  const uint32_t m = mode & 3u;
+  if (m == CG_L4_INGRESS) return w1 | (CG_L4_F_INGRESS << 24);
+  if (m == CG_L4_EGRESS) return w1 & ~((CG_L4_F_INGRESS | CG_L4_F_FRAGMENT) << 24);
+  return w1;
+}
+__device__ __forceinline__ int32_t l4_wrap(int32_t v, uint32_t mode) {
+  if ((mode & 3u) != CG_L4_CAN_ACCESS && v < 0) return (mode & CG_L4_IGNORE_DROP) ? 0 : CG_DROP_POLICY;
+  return v;
 }
 
 // The three policy_key lookups of __policy_can_access (bpf/lib/policy.h:61-109)
@@ -89,7 +109,8 @@ __device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, uint32_t w
 
 // Counter entry in LDS: one u64 per entry id, packets in bits 40..63, bytes in
 // bits 0..39 (lengths below 64 KiB; longer ones go straight to the global
-// byte counter).  A block flushes before 2^24 tuples, so neither field wraps.
+// byte counter).  A block flushes before it has counted 2^24 tuples, so
+// neither field wraps (2^24 - 1 packets; (2^24 - 1) x 65535 bytes < 2^40).
 constexpr uint32_t kL4Tuples = 4;       // tuples per thread per iteration
 constexpr size_t kL4FlushTuples = (size_t)1 << 24;
 
@@ -115,17 +136,27 @@ __device__ void l4_flush(const L4Dev& t, unsigned long long* lcnt) {
   __syncthreads();
 }
 
+// The remote identity of the egress flow (bpf_lxc.c:205-215 v6, :509-518 v4):
+// lookup_ip{4,6}_remote_endpoint resolved to sec_label, or WORLD_ID on a miss
+// or a zero sec_label (the tables store that resolution, dev_types.h).
+__device__ __forceinline__ uint32_t ipc_v6_identity(const IpcacheDev& ipc, uint64_t hi, uint64_t lo, uint32_t L,
+                                                    uint32_t R, uint4 kr, uint32_t v) {
+  if (!ipc_le128(((uint64_t)kr.y << 32) | kr.x, ((uint64_t)kr.w << 32) | kr.z, hi, lo))
+    v = (uint32_t)ipc.runs6[4 * (size_t)ipc_v6_run(ipc, hi, lo, L, R - 1) + 2];
+  return v;
+}
+
 // Tables whose fingerprints and counters fit LDS together (max_entries*8 +
 // nbuckets*4 <= 160 KiB; the 16,384-entry default): per tuple three key
 // hashes, six LDS fingerprint reads, and a slot read only on a fingerprint
 // match (hits, and ~1.6% false matches per key).
-// kIpc: the tuple's identity is replaced by the ipcache resolution of its
-// remote IPv4 address (addrs[i], network order) — the egress flow of
-// bpf_lxc.c:509-527 (lookup_ip4_remote_endpoint → *dstID → policy_can_egress).
-template <bool kIpc>
-__global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, const uint32_t* __restrict__ addrs,
+// kFam 4 / 6: the tuple's identity is replaced by the ipcache resolution of
+// its remote address (addrs: u32 IPv4 / 16-byte IPv6, network order) — the
+// egress flow of bpf_lxc.c:509-527 (v4) and :205-220 (v6).
+template <int kFam>
+__global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, const void* __restrict__ addrs,
                                                      const uint32_t* __restrict__ tuples, size_t n,
-                                                     int32_t* __restrict__ out) {
+                                                     int32_t* __restrict__ out, uint32_t mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long l4_lds[];
   unsigned long long* lcnt = l4_lds;
   uint32_t* lfp = reinterpret_cast<uint32_t*>(l4_lds + t.max_entries);
@@ -138,16 +169,23 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
   size_t since_flush = 0;
   for (size_t base = (size_t)blockIdx.x * per_iter; base < n; base += stride) {
     uint32_t w[kL4Tuples][3];
+    uint4 a6[kL4Tuples];
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
       size_t i = base + u * blockDim.x + threadIdx.x;
       i = i < n ? i : n - 1;  // unconditional loads (see kafka_kernel)
-      w[u][0] = kIpc ? __builtin_bswap32(__builtin_nontemporal_load(addrs + i))
-                     : __builtin_nontemporal_load(tuples + i * 3 + 0);
-      w[u][1] = __builtin_nontemporal_load(tuples + i * 3 + 1);
+      if (kFam == 6) {
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(addrs) + i);
+        a6[u] = make_uint4(x.x, x.y, x.z, x.w);
+        w[u][0] = 0;
+      } else {
+        w[u][0] = kFam == 4 ? __builtin_bswap32(__builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(addrs) + i))
+                            : __builtin_nontemporal_load(tuples + i * 3 + 0);
+      }
+      w[u][1] = l4_mode_word(__builtin_nontemporal_load(tuples + i * 3 + 1), mode);
       w[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
     }
-    if (kIpc) {  // the trie levels, each issued for all tuples of the lane
+    if (kFam == 4) {  // the trie levels, each issued for all tuples of the lane
       uint64_t e[kL4Tuples];
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) e[u] = ipc.l16[w[u][0] >> 16];
@@ -160,6 +198,27 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = (uint32_t)e[u];
     }
+    if (kFam == 6) {  // index words, then each bucket's last run, for all tuples of the lane
+      uint64_t hi[kL4Tuples], lo[kL4Tuples];
+      uint32_t L[kL4Tuples], R[kL4Tuples];
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) {
+        hi[u] = __builtin_bswap64(((uint64_t)a6[u].y << 32) | a6[u].x);
+        lo[u] = __builtin_bswap64(((uint64_t)a6[u].w << 32) | a6[u].z);
+        const uint64_t tb = hi[u] >> (64 - ipc.v6_bits);
+        L[u] = ipc.idx6[tb];
+        R[u] = ipc.idx6[tb + 1];
+      }
+      uint4 kr[kL4Tuples], vr[kL4Tuples];
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) {
+        const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R[u]);
+        kr[u] = rec[0];
+        vr[u] = rec[1];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], kr[u], vr[u].x);
+    }
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
       const size_t i = base + u * blockDim.x + threadIdx.x;
@@ -167,11 +226,12 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
       const bool frag = (w[u][1] >> 24) & CG_L4_F_FRAGMENT;
       uint32_t val = 0;
       const int which = l4_resolve(t, [&](uint32_t b) { return lfp[b]; }, w[u][0], w[u][1], frag, &val);
-      __builtin_nontemporal_store(l4_verdict(which, val, w[u][1] >> 24), out + i);
+      __builtin_nontemporal_store(l4_wrap(l4_verdict(which, val, w[u][1] >> 24), mode), out + i);
       if (which) l4_count(t, lcnt, val & 0xFFFF, w[u][2]);
     }
     since_flush += per_iter;
-    if (since_flush + per_iter > kL4FlushTuples && base + stride < n) {
+    // flush while the next iteration could bring the count to 2^24
+    if (since_flush + per_iter >= kL4FlushTuples && base + stride < n) {
       l4_flush(t, lcnt);
       since_flush = 0;
     }
@@ -181,18 +241,31 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
 
 // Larger tables: fingerprints read from global memory (L2), counters as
 // global atomics.
-template <bool kIpc>
-__global__ __launch_bounds__(256) void l4_kernel(L4Dev t, IpcacheDev ipc, const uint32_t* __restrict__ addrs,
+template <int kFam>
+__global__ __launch_bounds__(256) void l4_kernel(L4Dev t, IpcacheDev ipc, const void* __restrict__ addrs,
                                                  const uint32_t* __restrict__ tuples, size_t n,
-                                                 int32_t* __restrict__ out) {
+                                                 int32_t* __restrict__ out, uint32_t mode) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t w0 = kIpc ? (uint32_t)ipc_v4_value(ipc, __builtin_bswap32(addrs[i])) : tuples[i * 3 + 0];
-    const uint32_t w1 = tuples[i * 3 + 1], len = tuples[i * 3 + 2];
+    uint32_t w0;
+    if (kFam == 4) {
+      w0 = (uint32_t)ipc_v4_value(ipc, __builtin_bswap32(reinterpret_cast<const uint32_t*>(addrs)[i]));
+    } else if (kFam == 6) {
+      const uint4 x = reinterpret_cast<const uint4*>(addrs)[i];
+      const uint64_t hi = __builtin_bswap64(((uint64_t)x.y << 32) | x.x);
+      const uint64_t lo = __builtin_bswap64(((uint64_t)x.w << 32) | x.z);
+      const uint64_t tb = hi >> (64 - ipc.v6_bits);
+      const uint32_t L = ipc.idx6[tb], R = ipc.idx6[tb + 1];
+      const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R);
+      w0 = ipc_v6_identity(ipc, hi, lo, L, R, rec[0], rec[1].x);
+    } else {
+      w0 = tuples[i * 3 + 0];
+    }
+    const uint32_t w1 = l4_mode_word(tuples[i * 3 + 1], mode), len = tuples[i * 3 + 2];
     const bool frag = (w1 >> 24) & CG_L4_F_FRAGMENT;
     uint32_t val = 0;
     const int which = l4_resolve(t, [&](uint32_t b) { return t.fp[b]; }, w0, w1, frag, &val);
-    out[i] = l4_verdict(which, val, w1 >> 24);
+    out[i] = l4_wrap(l4_verdict(which, val, w1 >> 24), mode);
     if (which) {
       const uint32_t id = val & 0xFFFF;
       atomicAdd(&t.counters[2 * id], 1ULL);
@@ -679,6 +752,18 @@ int resident(const void* fn, int threads, size_t lds) {
   return nb;
 }
 
+// resident() per (kernel, device), cached under a lock.
+int resident_cached(const void* fn, int threads) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({fn, dev});
+  if (it == cache.end()) it = cache.emplace(std::make_pair(fn, dev), resident(fn, threads, 0)).first;
+  return it->second;
+}
+
 int grid_for(size_t items, int per_block, int cus, int blocks_per_cu) {
   size_t need = (items + per_block - 1) / per_block;
   size_t cap = (size_t)cus * blocks_per_cu;
@@ -689,40 +774,50 @@ int grid_for(size_t items, int per_block, int cus, int blocks_per_cu) {
 
 }  // namespace
 
-template <bool kIpc>
-int launch_l4_t(const L4Dev& t, const IpcacheDev& ipc, const uint32_t* addrs, const void* tuples, size_t n,
-                int32_t* out, void* stream, int cus) {
+// hipFuncSetAttribute per (kernel, device): the attribute is per device, and
+// handles on several GPUs may launch from several threads.
+template <class F>
+void set_max_lds_once(F fn, int dev_count_hint) {
+  static std::once_flag flags[64];
+  int d = 0;
+  (void)hipGetDevice(&d);
+  (void)dev_count_hint;
+  std::call_once(flags[d & 63], [&] {
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+}
+
+template <int kFam>
+int launch_l4_t(const L4Dev& t, const IpcacheDev& ipc, const void* addrs, const void* tuples, size_t n,
+                int32_t* out, uint32_t mode, void* stream, int cus) {
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = (size_t)t.max_entries * 8 + (size_t)(t.bucket_mask + 1) * 4;
   if (lds <= 160 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute((const void*)l4_fp_kernel<kIpc>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(l4_fp_kernel<kIpc>, dim3(grid_for(n, 1024 * kL4Tuples, cus, 1)), dim3(1024), lds, s, t, ipc,
-                       addrs, (const uint32_t*)tuples, n, out);
+    set_max_lds_once(l4_fp_kernel<kFam>, 0);
+    hipLaunchKernelGGL(l4_fp_kernel<kFam>, dim3(grid_for(n, 1024 * kL4Tuples, cus, 1)), dim3(1024), lds, s, t, ipc,
+                       addrs, (const uint32_t*)tuples, n, out, mode);
   } else {
-    hipLaunchKernelGGL(l4_kernel<kIpc>, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, s, t, ipc, addrs,
-                       (const uint32_t*)tuples, n, out);
+    hipLaunchKernelGGL(l4_kernel<kFam>, dim3(grid_for(n, 256, cus, 8)), dim3(256), 0, s, t, ipc, addrs,
+                       (const uint32_t*)tuples, n, out, mode);
   }
   return (int)hipGetLastError();
 }
 
-int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, void* stream, int cus) {
-  return launch_l4_t<false>(t, IpcacheDev{}, nullptr, tuples, n, out, stream, cus);
+int launch_l4(const L4Dev& t, const void* tuples, size_t n, int32_t* out, uint32_t mode, void* stream, int cus) {
+  return launch_l4_t<0>(t, IpcacheDev{}, nullptr, tuples, n, out, mode, stream, cus);
 }
 
-int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, const uint32_t* addrs, const void* tuples, size_t n,
-                      int32_t* out, void* stream, int cus) {
-  return launch_l4_t<true>(t, ipc, addrs, tuples, n, out, stream, cus);
+int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, int family, const void* addrs, const void* tuples,
+                      size_t n, int32_t* out, uint32_t mode, void* stream, int cus) {
+  if (family == 6) return launch_l4_t<6>(t, ipc, addrs, tuples, n, out, mode, stream, cus);
+  return launch_l4_t<4>(t, ipc, addrs, tuples, n, out, mode, stream, cus);
 }
 
 int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n4, uint8_t* out4,
                const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus) {
   if (n4 + n6 == 0) return 0;
-  static const int occ = resident((const void*)lpm_kernel, 256, 0);
+  const int occ = resident_cached((const void*)lpm_kernel, 256);
   hipLaunchKernelGGL(lpm_kernel, dim3(grid_for(n4 / kLpmV4 + n6 / kLpmV6 + 1, 256, cus, occ)), dim3(256), 0,
                      (hipStream_t)stream, t, v4f,
                      v6f, (const uint2*)v4, n4, out4, (const uint4*)v6, n6, out6);
@@ -732,7 +827,7 @@ int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
                  void* stream, int cus) {
   if (n == 0) return 0;
-  static const int occ = resident((const void*)kafka_kernel, kKafkaThreads, 0);
+  const int occ = resident_cached((const void*)kafka_kernel, kKafkaThreads);
   hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, kKafkaThreads * kKafkaReqs, cus, occ)), dim3(kKafkaThreads), 0,
                      (hipStream_t)stream, t,
                      (const uint4*)reqs, n, arena, out);

@@ -13,6 +13,10 @@
 // the current tile walks, and units within a tile load two ahead.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+#include <set>
+
 #include "../../include/cilium_gpu.h"
 #include "dev_types.h"
 #include "kernels.h"
@@ -79,13 +83,18 @@ __device__ __forceinline__ uint4 tile_unit(const TileRef& tr, uint32_t units, ui
   return tr.units[(min(u, units) - 1) * kWave + lane];
 }
 
-// The overflow string of a lane whose meta word is m (arena entry: u32 length, bytes).
+// The overflow string of a lane whose meta word is m (arena entry: u32 length,
+// bytes).  An entry reaching past the batch's arena (arena_bytes, from its
+// header) ends in the dead state: the request is denied.
 __device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
-                                                 const uint8_t* __restrict__ arena, uint2 m, bool ov) {
+                                                 const uint8_t* __restrict__ arena, uint64_t arena_bytes, uint2 m,
+                                                 bool ov) {
   if (!ov) return st;
-  const uint32_t aoff = (m.y & 0xFFFFFFu) * 16u;
+  const uint64_t aoff = (uint64_t)(m.y & 0xFFFFFFu) * 16u;
+  if (aoff + 4 > arena_bytes) return 0;
   const uint32_t len = *reinterpret_cast<const uint32_t*>(arena + aoff);
-  return walk_arena(cells, self_lo, st, arena, aoff + 4, len);
+  if (aoff + 4 + len > arena_bytes) return 0;
+  return walk_arena(cells, self_lo, st, arena, (uint32_t)aoff + 4, len);
 }
 
 // Block offset of the PNPR mask of remote identity `remote`: the program's
@@ -125,7 +134,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
                                            const uint8_t* __restrict__ tiles, const HttpTile* __restrict__ ttab,
                                            const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
-                                           uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
+                                           uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
                                            uint32_t& n_deny) {
   TileRef tr[K];
   uint2 meta[K];
@@ -186,7 +195,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     if (any_overflow) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const uint32_t sa = walk_overflow(cells, pt.self_lo, pt.start, arena, meta[j], overflow[j]);
+        const uint32_t sa = walk_overflow(cells, pt.self_lo, pt.start, arena, arena_bytes, meta[j], overflow[j]);
         if (overflow[j]) st[j] = sa;
       }
     }
@@ -218,8 +227,9 @@ template <int N>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
                                             uint32_t prog, const uint32_t* __restrict__ blk,
                                             const TileRef tr, uint32_t t,
-                                            const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                            uint32_t lane, uint32_t& n_allow, uint32_t& n_deny) {
+                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                            uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
+                                            uint32_t& n_deny) {
   const uint2 meta = tr.meta[lane];
   uint4 unit[N > 0 ? N : 1];
 #pragma unroll
@@ -236,7 +246,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
     for (int i = 0; i < 16; ++i) st = comb_step(blk, self_lo, st, get_byte(unit[k], i));
   }
   if (__any(overflow)) {
-    const uint32_t sa = walk_overflow(blk, self_lo, pt.start, arena, meta, overflow);
+    const uint32_t sa = walk_overflow(blk, self_lo, pt.start, arena, arena_bytes, meta, overflow);
     if (overflow) st = sa;
   }
   bool verdict = false;
@@ -290,7 +300,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
                                             uint32_t* lcells, uint32_t* s_cnt) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
   const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
-  const uint64_t toff = H->tiles_off;
+  const uint64_t toff = H->tiles_off, arena_bytes = H->arena_bytes;
   if (magic != kBatchMagic || epoch != T.epoch || (size_t)ntiles * kWave > nslots) {
     // packed against another snapshot (or not a batch): deny every slot
     if (kGlobal) return;
@@ -349,7 +359,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
         const uint32_t tile[1] = {t};
         const bool valid[1] = {true};
-        http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, ttab, tile, valid, arena, out, lane,
+        http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, ttab, tile, valid, arena, arena_bytes, out, lane,
                       n_allow, n_deny);
       }
     } else if (pg.part_count == 1) {
@@ -360,11 +370,11 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         switch (tt.units) {  // wave-uniform
 #define CG_TILE_N(n) \
   case n:            \
-    http_tile_n<n>(T, pg, pt, prog, lcells, tb, t, arena, out, lane, n_allow, n_deny); \
+    http_tile_n<n>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny); \
     break;
           CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
           default:
-            http_tile_n<8>(T, pg, pt, prog, lcells, tb, t, arena, out, lane, n_allow, n_deny);
+            http_tile_n<8>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny);
 #undef CG_TILE_N
         }
       }
@@ -379,8 +389,8 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
           valid[j] = t < tend;
           tile[j] = valid[j] ? t : t0;
         }
-        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, ttab, tile, valid, arena, out, lane, n_allow,
-                                  n_deny);
+        http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, ttab, tile, valid, arena, arena_bytes, out, lane,
+                                  n_allow, n_deny);
       }
     }
   }
@@ -407,24 +417,33 @@ __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, co
 int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_t* arena, uint8_t* out, void* stream,
                 int cus) {
   if (nslots == 0) return 0;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
-    attr = true;
-  }
-  // one resident wave of workgroups: as many per CU as LDS and registers
-  // allow (the largest staged program block sets the LDS share), then the
-  // workgroups deal the chunks among themselves
+  // hipFuncSetAttribute and the occupancy answer are per device: cached per
+  // device ordinal, set once under a lock (handles on several GPUs may launch
+  // from several threads)
+  int dev = 0;
+  (void)hipGetDevice(&dev);
   const size_t lds = (size_t)t.lds_cells * 4;
-  static size_t occ_lds = ~(size_t)0;
-  static int occ = 1;
-  if (occ_lds != lds) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)http_kernel, kHttpThreads, lds) != hipSuccess ||
-        nb < 1)
-      nb = 1;
-    occ = nb;
-    occ_lds = lds;
+  int occ = 1;
+  {
+    static std::mutex mu;
+    static std::map<std::pair<int, size_t>, int> occ_cache;
+    static std::set<int> attr_set;
+    std::lock_guard<std::mutex> lk(mu);
+    if (attr_set.insert(dev).second)
+      (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
+    auto it = occ_cache.find({dev, lds});
+    if (it == occ_cache.end()) {
+      // one resident wave of workgroups: as many per CU as LDS and registers
+      // allow (the largest staged program block sets the LDS share), then the
+      // workgroups deal the chunks among themselves
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)http_kernel, kHttpThreads, lds) !=
+              hipSuccess ||
+          nb < 1)
+        nb = 1;
+      it = occ_cache.emplace(std::make_pair(dev, lds), nb).first;
+    }
+    occ = it->second;
   }
   const size_t tiles = nslots / kWave;
   size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);

@@ -12,6 +12,9 @@
 // flight.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+
 #include "dev_types.h"
 #include "kernels.h"
 
@@ -108,7 +111,17 @@ int resident_blocks(const void* fn, int threads) {
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus) {
   if (n4 + n6 == 0) return 0;
-  static const int occ = resident_blocks((const void*)ipcache_kernel, kIpcThreads);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  static std::mutex mu;
+  static std::map<int, int> occ_by_dev;  // per device ordinal
+  int occ;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = occ_by_dev.find(dev);
+    if (it == occ_by_dev.end()) it = occ_by_dev.emplace(dev, resident_blocks((const void*)ipcache_kernel, kIpcThreads)).first;
+    occ = it->second;
+  }
   size_t need = (n4 / kIpcV4 + n6 / kIpcV6 + kIpcThreads) / kIpcThreads;
   const size_t cap = (size_t)cus * occ;
   need = need < cap ? need : cap;

@@ -64,36 +64,40 @@ void PolicyMapState::rebuild(Engine& e) {
       if (slots[(size_t)bk * 4 + s].key != kL4EmptyKey) fp[bk] |= slots[(size_t)bk * 4 + s].pad << (8 * s);
   if (e.has_gpu()) {
     e.set_device();
-    d_slots.upload_vec(slots);
-    d_fp.upload_vec(fp);
-    if (d_counters.size() == 0) {
-      d_counters.alloc((size_t)max_entries * 2 * sizeof(uint64_t));
-      d_counters.zero();
+    if (!d_counters) {
+      d_counters = std::make_shared<DevMem>();
+      d_counters->alloc((size_t)max_entries * 2 * sizeof(uint64_t));
+      d_counters->zero();
     }
-    dev.slots = d_slots.as<L4Slot>();
-    dev.fp = d_fp.as<uint32_t>();
-    dev.bucket_mask = bucket_mask;
-    dev.max_entries = max_entries;
-    dev.counters = d_counters.as<unsigned long long>();
+    auto t = std::make_shared<DevTables>();
+    L4Dev d{};
+    d.slots = t->add(slots);
+    d.fp = t->add(fp);
+    t->counters = d_counters;
+    d.bucket_mask = bucket_mask;
+    d.max_entries = max_entries;
+    d.counters = d_counters->as<unsigned long long>();
+    tab = std::move(t);  // publish (the caller holds the handle lock)
+    dev = d;
   }
   dirty = false;
 }
 
 void PolicyMapState::read_counters(Engine& e, uint32_t id, uint64_t* pk, uint64_t* by) {
   *pk = *by = 0;
-  if (!e.has_gpu() || d_counters.size() == 0) return;
+  if (!e.has_gpu() || !d_counters) return;
   e.set_device();
   uint64_t v[2];
-  hip_check(hipMemcpy(v, d_counters.as<uint64_t>() + (size_t)id * 2, 16, hipMemcpyDeviceToHost),
+  hip_check(hipMemcpy(v, d_counters->as<uint64_t>() + (size_t)id * 2, 16, hipMemcpyDeviceToHost),
             "read counters");
   *pk = v[0];
   *by = v[1];
 }
 
 void PolicyMapState::zero_counter(Engine& e, uint32_t id) {
-  if (!e.has_gpu() || d_counters.size() == 0) return;
+  if (!e.has_gpu() || !d_counters) return;
   e.set_device();
-  hip_check(hipMemset(d_counters.as<uint64_t>() + (size_t)id * 2, 0, 16), "zero counter");
+  hip_check(hipMemset(d_counters->as<uint64_t>() + (size_t)id * 2, 0, 16), "zero counter");
 }
 
 }  // namespace cg

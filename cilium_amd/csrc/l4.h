@@ -1,6 +1,7 @@
 // l4.h — policy map state (host mirror + device cuckoo table).
 #pragma once
 
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
@@ -38,8 +39,9 @@ struct PolicyMapState {
   std::vector<L4Slot> slots;
   std::vector<uint32_t> fp;  // per bucket: 4 x 8-bit slot fingerprints
   uint32_t bucket_mask = 0;
-  DevMem d_slots, d_fp, d_counters;
-  L4Dev dev{};
+  std::shared_ptr<DevMem> d_counters;  // [id] packets, bytes: kept across rebuilds
+  std::shared_ptr<DevTables> tab;      // the published device tables (engine.h)
+  L4Dev dev{};                         // view of tab; copy it together with tab
   std::vector<uint64_t> host_counters;  // for handles without a GPU (always 0)
 
   void rebuild(Engine& e);  // cuckoo build + upload (counters preserved by id)

@@ -213,39 +213,35 @@ void PrefilterState::rebuild(Engine& e) {
 
   if (e.has_gpu()) {
     e.set_device();
-    dev = LpmDev{};
+    if (!d_counters) {
+      d_counters = std::make_shared<DevMem>();
+      d_counters->alloc(2 * sizeof(uint64_t));
+      d_counters->zero();
+    }
+    auto t = std::make_shared<DevTables>();
+    LpmDev d{};
     if (v4_filter) {
-      d_top.upload_vec(top);
-      d_top_rank.upload_vec(top_rank);
-      d_mid.upload_vec(mid);
-      d_leaf_base.upload_vec(leaf_base);
-      d_leaves.upload_vec(leaves);
-      dev.top = d_top.as<uint32_t>();
-      dev.top_rank = d_top_rank.as<uint32_t>();
-      dev.mid = d_mid.as<uint32_t>();
-      dev.leaf_base = d_leaf_base.as<uint32_t>();
-      dev.leaves = d_leaves.as<uint64_t>();
+      d.top = t->add(top);
+      d.top_rank = t->add(top_rank);
+      d.mid = t->add(mid);
+      d.leaf_base = t->add(leaf_base);
+      d.leaves = t->add(leaves);
     }
     if (v6_filter) {
-      d_v6_idx.upload_vec(v6_idx);
-      d_v6_iv.upload_vec(v6_iv);
-      dev.v6_idx = d_v6_idx.as<uint32_t>();
-      dev.v6_iv = d_v6_iv.as<uint64_t>();
-      dev.v6_bits = v6_bits;
+      d.v6_idx = t->add(v6_idx);
+      d.v6_iv = t->add(v6_iv);
+      d.v6_bits = v6_bits;
     }
-    d_ep4k.upload_vec(ep4_keys);
-    d_ep6k.upload_vec(ep6_keys);
-    dev.ep4_keys = d_ep4k.as<uint32_t>();
-    dev.ep4_mask = (uint32_t)ep4_keys.size() - 1;
-    dev.ep4_zero = ep4_zero;
-    dev.ep6_keys = d_ep6k.as<uint64_t>();
-    dev.ep6_mask = (uint32_t)(ep6_keys.size() / 2) - 1;
-    dev.ep6_zero = ep6_zero;
-    if (d_counters.size() == 0) {
-      d_counters.alloc(2 * sizeof(uint64_t));
-      d_counters.zero();
-    }
-    dev.counters = d_counters.as<unsigned long long>();
+    d.ep4_keys = t->add(ep4_keys);
+    d.ep4_mask = (uint32_t)ep4_keys.size() - 1;
+    d.ep4_zero = ep4_zero;
+    d.ep6_keys = t->add(ep6_keys);
+    d.ep6_mask = (uint32_t)(ep6_keys.size() / 2) - 1;
+    d.ep6_zero = ep6_zero;
+    t->counters = d_counters;
+    d.counters = d_counters->as<unsigned long long>();
+    tab = std::move(t);  // publish (the caller holds the handle lock)
+    dev = d;
   }
   dirty = false;
 }

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <array>
+#include <memory>
 #include <set>
 #include <vector>
 
@@ -44,8 +45,9 @@ struct PrefilterState {
   std::vector<uint32_t> ep4_keys;
   bool ep4_zero = false, ep6_zero = false;
   std::vector<uint64_t> ep6_keys;
-  DevMem d_top, d_top_rank, d_mid, d_leaf_base, d_leaves, d_v6_idx, d_v6_iv, d_ep4k, d_ep6k, d_counters;
-  LpmDev dev{};
+  std::shared_ptr<DevMem> d_counters;  // {drop, pass}: kept across rebuilds
+  std::shared_ptr<DevTables> tab;      // the published device tables (engine.h)
+  LpmDev dev{};                        // view of tab; copy it together with tab
   bool v4_filter = false, v6_filter = false;
 
   void rebuild(Engine& e);

@@ -413,8 +413,23 @@ FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoS
     std::vector<uint16_t> port(n, (uint16_t)(c->port > 0xFFFF ? 0 : c->port));
     std::string blob;
     std::vector<uint64_t> off{0};
+    // values escaped for the proxylib snapshot (bytes 0x00-0x03 → 0x03,
+    // 0x10 + b): a NUL or control byte inside cmd/file stays part of the
+    // string the rules see, as in r2d2parser.go:157-183
+    auto esc = [](const std::string& v) {
+      std::string o;
+      for (unsigned char ch : v) {
+        if (ch <= 0x03) {
+          o += (char)0x03;
+          o += (char)(0x10 + ch);
+        } else {
+          o += (char)ch;
+        }
+      }
+      return o;
+    };
     for (size_t i : reqs) {
-      blob += std::string("cmd") + '\0' + frames[i].cmd + '\0' + "file" + '\0' + frames[i].file + '\0';
+      blob += std::string("cmd") + '\0' + esc(frames[i].cmd) + '\0' + "file" + '\0' + esc(frames[i].file) + '\0';
       off.push_back(blob.size());
     }
     if (blob.empty()) blob.push_back('\0');

@@ -35,17 +35,23 @@ ByteSet set_word() {
   s.set('_');
   return s;
 }
-ByteSet set_space() {
-  // libstdc++ ctype<char> "space" in the C locale.
+// Two flavours share the parser: Envoy's std::regex (ECMAScript, full
+// match) and Go's regexp (RE2 syntax, proxylib's MatchString search).  They
+// differ, on bytes, in '.' and '\s'.
+ByteSet set_space(bool go) {
+  // libstdc++ ctype<char> "space" in the C locale; Go RE2 \s is [\t\n\f\r ]
+  // (no \v: regexp/syntax perl_groups.go)
   ByteSet s;
-  for (int c : {' ', '\t', '\n', '\v', '\f', '\r'}) s.set(c);
+  for (int c : {' ', '\t', '\n', '\f', '\r'}) s.set(c);
+  if (!go) s.set('\v');
   return s;
 }
-ByteSet set_dot() {
-  // libstdc++ _AnyMatcher<ecma>: any char except '\n' and '\r'.
+ByteSet set_dot(bool go) {
+  // libstdc++ _AnyMatcher<ecma>: any char except '\n' and '\r'; Go RE2
+  // without the s flag: any char except '\n'
   ByteSet s = ByteSet::all();
   s.w['\n' >> 6] &= ~(1ULL << ('\n' & 63));
-  s.w['\r' >> 6] &= ~(1ULL << ('\r' & 63));
+  if (!go) s.w['\r' >> 6] &= ~(1ULL << ('\r' & 63));
   return s;
 }
 
@@ -58,7 +64,7 @@ int hexval(char c) {
 
 class Parser {
  public:
-  Parser(const std::string& re, std::vector<Ast>& nodes) : s_(re), n_(nodes) {}
+  Parser(const std::string& re, std::vector<Ast>& nodes, bool go = false) : s_(re), n_(nodes), go_(go) {}
 
   int parse() {
     int r = parse_alt();
@@ -69,6 +75,7 @@ class Parser {
  private:
   const std::string& s_;
   std::vector<Ast>& n_;
+  bool go_ = false;  // Go RE2 flavour (search mode)
   size_t p_ = 0;
   int depth_ = 0;
 
@@ -177,10 +184,10 @@ class Parser {
     switch (c) {
       case 'd': *out = set_digit(); return true;
       case 'w': *out = set_word(); return true;
-      case 's': *out = set_space(); return true;
+      case 's': *out = set_space(go_); return true;
       case 'D': *out = set_digit(); out->invert(); return true;
       case 'W': *out = set_word(); out->invert(); return true;
-      case 'S': *out = set_space(); out->invert(); return true;
+      case 'S': *out = set_space(go_); out->invert(); return true;
       default: return false;
     }
   }
@@ -312,7 +319,7 @@ class Parser {
       }
       case ')': err(CG_POLICY_REJECTED, "unmatched ')'");
       case '[': return parse_class();
-      case '.': return mkset(set_dot());
+      case '.': return mkset(set_dot(go_));
       case '^': {
         *assertion = true;
         Ast a;
@@ -637,7 +644,7 @@ bool regex_syntax_ok(const std::string& re, std::string* errmsg) {
 ByteDfa compile_regex(const std::string& re, const ByteSet& alphabet, MatchMode mode,
                       int max_states) {
   std::vector<Ast> nodes;
-  int root = Parser(re, nodes).parse();
+  int root = Parser(re, nodes, mode == MatchMode::Search).parse();
   NfaBuilder b(nodes);
   NfaBuilder::Frag f = b.build(root);
   int match = b.add(NState::MATCH);
@@ -691,6 +698,29 @@ ByteDfa dfa_star(const ByteSet& alphabet) {
     if (alphabet.test(b)) d.trans[256 + b] = 1;
   d.start = 1;
   return d;
+}
+
+ByteDfa dfa_escape_low(const ByteDfa& d) {
+  // state s keeps its transitions on bytes >= 4; bytes 0..3 move to an escape
+  // state e(s) reached on kEscByte, whose transitions on kEscBase + b are
+  // s's old transitions on b.  The escaped encoding is injective and prefix
+  // free, so the language maps one to one.
+  const int n = d.size();
+  ByteDfa o;
+  o.start = d.start;
+  o.accept = d.accept;
+  o.accept.resize((size_t)2 * n, 0);
+  o.trans.assign((size_t)2 * n * 256, 0);
+  for (int s = 1; s < n; ++s) {
+    for (int b = 4; b < 256; ++b) o.trans[(size_t)s * 256 + b] = d.next(s, b);
+    bool any = false;
+    for (int b = 0; b < 4; ++b) {
+      o.trans[(size_t)(n + s) * 256 + kEscBase + b] = d.next(s, b);
+      any |= d.next(s, b) != 0;
+    }
+    if (any) o.trans[(size_t)s * 256 + kEscByte] = n + s;
+  }
+  return dfa_minimize(o);
 }
 
 ByteDfa dfa_intersect(const ByteDfa& a, const ByteDfa& b) {

@@ -70,6 +70,11 @@ ByteDfa dfa_literal(const std::string& s, const ByteSet& alphabet);
 // alphabet* (present_match on a field, or "no constraint").
 ByteDfa dfa_star(const ByteSet& alphabet);
 ByteDfa dfa_intersect(const ByteDfa& a, const ByteDfa& b);
+// The same language over escaped strings: every byte b <= 3 of a string is
+// written as the pair {kEscByte, kEscBase + b} (proxylib field values, whose
+// bytes are arbitrary, while 0x00-0x02 structure the request string).
+constexpr int kEscByte = 0x03, kEscBase = 0x10;
+ByteDfa dfa_escape_low(const ByteDfa& d);
 // Moore partition refinement + canonical BFS renumbering (dead=0, start=1):
 // equal languages give identical tables.
 ByteDfa dfa_minimize(const ByteDfa& d);

@@ -281,6 +281,16 @@ def r2d2_request(line: bytes) -> tuple[bytes, bytes]:
     return fields[0], (fields[1] if len(fields) == 2 else b"")
 
 
+def escape_value(v: bytes) -> bytes:
+    """A proxylib field value in the engine's escaped form: bytes 0x00-0x03
+    become 0x03, 0x10 + b (regex.h kEscByte), so values may hold any byte
+    (a NUL inside an r2d2 cmd or file stays part of the string the rules
+    compare, r2d2parser.go:157-183)."""
+    if not any(b <= 3 for b in v):
+        return v
+    return b"".join(bytes([3, 0x10 + b]) if b <= 3 else bytes([b]) for b in v)
+
+
 class ProxylibPolicy:
     """A proxylib policy snapshot on a Classifier: ``update`` then batched
     ``matches`` for r2d2 requests (Instance.PolicyMatches, instance.go:157-165)."""
@@ -304,7 +314,7 @@ class ProxylibPolicy:
         """Requests given as their parser's (name, value) fields."""
         parts, off = [], [0]
         for fs in fields:
-            b = b"".join(k + b"\0" + v + b"\0" for k, v in fs)
+            b = b"".join(k + b"\0" + escape_value(v) + b"\0" for k, v in fs)
             parts.append(b)
             off.append(off[-1] + len(b))
         blob = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()

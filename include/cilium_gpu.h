@@ -150,6 +150,29 @@ int cg_l4_verdicts_dev(uint64_t h, uint32_t map_id, const cg_l4_tuple* d_tuples,
 int cg_l4_verdicts_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples,
                         size_t n, int32_t* verdicts);
 
+/* The verdict wrappers around __policy_can_access (bpf/lib/policy.h:126-163),
+ * selected by `mode`:
+ *   CG_L4_CAN_ACCESS  __policy_can_access itself: each tuple's CG_L4_F_INGRESS
+ *                     and CG_L4_F_FRAGMENT flags (what cg_l4_verdicts_* do);
+ *   CG_L4_INGRESS     policy_can_access_ingress (policy.h:126-146, called at
+ *                     bpf_lxc.c:814,948): dir = CT_INGRESS for every tuple,
+ *                     the tuple's is_fragment; any negative result becomes
+ *                     DROP_POLICY (so an unmatched fragment is -133, not -157);
+ *   CG_L4_EGRESS      policy_can_egress (policy.h:150-163, via
+ *                     policy_can_egress{4,6} at bpf_lxc.c:220,527): dir =
+ *                     CT_EGRESS, is_fragment = false; negative → DROP_POLICY.
+ * OR CG_L4_IGNORE_DROP to model a datapath built with IGNORE_DROP: the
+ * wrappers then return TC_ACT_OK instead of DROP_POLICY.  CG_L4_F_CB_POLICY
+ * (skb->cb[CB_POLICY]) is honoured in every mode, as in policy.h:98. */
+#define CG_L4_CAN_ACCESS 0u
+#define CG_L4_INGRESS 1u
+#define CG_L4_EGRESS 2u
+#define CG_L4_IGNORE_DROP 0x100u
+int cg_l4_policy_verdicts_dev(uint64_t h, uint32_t map_id, uint32_t mode, const cg_l4_tuple* d_tuples,
+                              size_t n, int32_t* d_verdicts, void* stream);
+int cg_l4_policy_verdicts_host(uint64_t h, uint32_t map_id, uint32_t mode, const cg_l4_tuple* tuples,
+                               size_t n, int32_t* verdicts);
+
 /* ======================================================================== */
 /* LPM: XDP CIDR prefilter — bpf/bpf_xdp.c:88-184,                           */
 /* pkg/datapath/prefilter/prefilter.go:57-298                                */
@@ -249,13 +272,22 @@ int cg_ipcache_resolve_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, siz
 /* The egress flow of bpf_lxc.c:509-527 over a batch: each tuple's remote
  * identity is lookup_ip4_remote_endpoint(remote_v4[i]) resolved as the
  * datapath does (WORLD_ID on a miss or sec_label 0), then
- * __policy_can_access as cg_l4_verdicts_*; the tuples' identity fields are
+ * policy_can_egress4 (policy.h:172-176 → policy_can_egress :150-163):
+ * dir = CT_EGRESS and is_fragment = false whatever the tuple's flags say,
+ * any negative result → DROP_POLICY.  The tuples' identity fields are
  * ignored.  remote_v4: network-order IPv4 addresses (iphdr.daddr).  Counters
  * advance as in cg_l4_verdicts_*. */
 int cg_l4_verdicts_ipcache_dev(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* d_remote_v4,
                                const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts, void* stream);
 int cg_l4_verdicts_ipcache_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint32_t* remote_v4,
                                 const cg_l4_tuple* tuples, size_t n, int32_t* verdicts);
+/* The IPv6 twin (bpf_lxc.c:205-220: lookup_ip6_remote_endpoint, then
+ * policy_can_egress6 → policy_can_egress): remote_v6 holds n 16-byte
+ * addresses in network order. */
+int cg_l4_verdicts_ipcache6_dev(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint8_t* d_remote_v6,
+                                const cg_l4_tuple* d_tuples, size_t n, int32_t* d_verdicts, void* stream);
+int cg_l4_verdicts_ipcache6_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, const uint8_t* remote_v6,
+                                 const cg_l4_tuple* tuples, size_t n, int32_t* verdicts);
 
 /* ======================================================================== */
 /* proxylib generic L7 (proxylib/proxylib/policymap.go:118-260)              */

@@ -31,6 +31,7 @@ def _load():
     p, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
     lib.or_last_error.restype = C.c_char_p
     lib.or_l4.argtypes = [p, p, sz, p, sz, p, p, p]
+    lib.or_l4_mode.argtypes = [p, p, sz, p, sz, p, p, p, u32]
     lib.or_prefilter.argtypes = [u32, p, sz, p, sz, p, sz, p, sz, p, p, sz, p, C.c_int]
     lib.or_ipcache.argtypes = [p, p, sz, p, sz, p, p, sz, p, C.c_int]
     lib.or_http_load.restype = p
@@ -60,16 +61,35 @@ def _ptr(a):
 
 
 # ------------------------------------------------------------------ L4 ----
-def l4(keys: np.ndarray, ports_be: np.ndarray, tuples: np.ndarray):
-    """__policy_can_access over tuples; returns (verdicts, packets, bytes per key)."""
+L4_CAN_ACCESS, L4_INGRESS, L4_EGRESS, L4_IGNORE_DROP = 0, 1, 2, 0x100
+
+
+def l4(keys: np.ndarray, ports_be: np.ndarray, tuples: np.ndarray, mode: int = L4_CAN_ACCESS):
+    """__policy_can_access over tuples (or a wrapper of it, see or_l4_mode);
+    returns (verdicts, packets, bytes per key)."""
     keys = np.ascontiguousarray(keys)
     ports_be = np.ascontiguousarray(ports_be, np.uint16)
     tuples = np.ascontiguousarray(tuples)
     out = np.zeros(max(len(tuples), 1), np.int32)
     pk = np.zeros(max(len(keys), 1), np.uint64)
     by = np.zeros(max(len(keys), 1), np.uint64)
-    lib().or_l4(_ptr(keys), _ptr(ports_be), len(keys), _ptr(tuples), len(tuples), _ptr(out), _ptr(pk), _ptr(by))
+    lib().or_l4_mode(_ptr(keys), _ptr(ports_be), len(keys), _ptr(tuples), len(tuples), _ptr(out), _ptr(pk),
+                     _ptr(by), mode)
     return out[:len(tuples)], pk[:len(keys)], by[:len(keys)]
+
+
+def l4_egress_via_ipcache(keys, ports_be, ik, iv, remote, tuples):
+    """The egress flow of bpf_lxc.c:509-527 (v4 remote: u32 network order)
+    / :205-220 (v6 remote: (n, 16) u8): the remote identity from the ipcache
+    oracle, then policy_can_egress.  Returns (verdicts, packets, bytes)."""
+    t = np.array(tuples, copy=True)
+    if remote.dtype == np.uint8:
+        _, o6 = ipcache(ik, iv, np.zeros(0, np.uint32), remote.reshape(-1, 16))
+        t["identity"] = o6[:, 0]
+    else:
+        o4, _ = ipcache(ik, iv, remote, np.zeros((0, 16), np.uint8))
+        t["identity"] = o4[:, 0]
+    return l4(keys, ports_be, t, L4_EGRESS)
 
 
 # ----------------------------------------------------------------- LPM ----

@@ -86,8 +86,15 @@ const char* or_last_error() { return g_err.c_str(); }
 // __policy_can_access for each tuple.  keys: n_keys × 8 bytes (struct
 // policy_key), ports_be: proxy_port as stored.  tuples: 12 bytes
 // {u32 identity, u16 dport(be), u8 proto, u8 flags(1 ingress, 2 frag, 4 cb_policy), u32 len}.
-int or_l4(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const uint8_t* tuples, size_t n,
-          int32_t* out, uint64_t* packets, uint64_t* bytes) {
+//
+// mode selects the caller (bpf/lib/policy.h:126-163): 0 = __policy_can_access
+// with the tuple's direction/fragment flags; 1 = policy_can_access_ingress
+// (dir CT_INGRESS, the tuple's is_fragment, `if (ret >= TC_ACT_OK) return
+// ret;` else DROP_POLICY); 2 = policy_can_egress (dir CT_EGRESS, is_fragment
+// false, `if (ret >= 0) return ret;` else DROP_POLICY).  mode | 0x100 =
+// IGNORE_DROP: the wrappers return TC_ACT_OK instead of DROP_POLICY.
+int or_l4_mode(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const uint8_t* tuples, size_t n,
+               int32_t* out, uint64_t* packets, uint64_t* bytes, uint32_t mode) {
   std::unordered_map<PolicyKey, size_t, PolicyKeyHash> map;
   std::vector<PolicyEntry> ent(n_keys);
   for (size_t i = 0; i < n_keys; ++i) {
@@ -114,6 +121,12 @@ int or_l4(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const ui
     int dir = (flags & 1) ? CT_INGRESS : CT_EGRESS;
     bool is_fragment = flags & 2;
     bool cb_policy = flags & 4;
+    const uint32_t wrapper = mode & 3;
+    if (wrapper == 1) dir = CT_INGRESS;  // policy_can_access_ingress passes CT_INGRESS
+    if (wrapper == 2) {                  // policy_can_egress passes CT_EGRESS, false
+      dir = CT_EGRESS;
+      is_fragment = false;
+    }
     // __policy_can_access, policy.h:46-110
     PolicyKey key{identity, dport, proto, (uint8_t)(!dir)};
     PolicyEntry* policy = nullptr;
@@ -150,6 +163,7 @@ int or_l4(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const ui
     else
       ret = DROP_POLICY;
   done:
+    if (wrapper != 0 && ret < TC_ACT_OK) ret = (mode & 0x100) ? TC_ACT_OK : DROP_POLICY;
     out[i] = ret;
   }
   if (packets)
@@ -157,6 +171,11 @@ int or_l4(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const ui
   if (bytes)
     for (size_t i = 0; i < n_keys; ++i) bytes[i] = ent[i].bytes;
   return 0;
+}
+
+int or_l4(const uint8_t* keys, const uint16_t* ports_be, size_t n_keys, const uint8_t* tuples, size_t n,
+          int32_t* out, uint64_t* packets, uint64_t* bytes) {
+  return or_l4_mode(keys, ports_be, n_keys, tuples, n, out, packets, bytes, 0);
 }
 
 }  // extern "C"

@@ -25,6 +25,23 @@ class ParseError(ValueError):
     pass
 
 
+def go_regexp(pattern: str):
+    """Go regexp (RE2 syntax) as a Python pattern over latin-1 decoded bytes:
+    ASCII-only \\d \\w, '.' without the s flag excludes only '\\n' (as in
+    Python), and RE2's \\s is [\\t\\n\\f\\r ] (no \\v, unlike Python)."""
+    out, i = [], 0
+    while i < len(pattern):
+        c = pattern[i]
+        if c == "\\" and i + 1 < len(pattern):
+            nx = pattern[i + 1]
+            out.append({"s": "[\\t\\n\\f\\r ]", "S": "[^\\t\\n\\f\\r ]"}.get(nx, c + nx))
+            i += 2
+            continue
+        out.append(c)
+        i += 1
+    return re.compile("".join(out), re.ASCII)
+
+
 class _R2d2Rule:
     def __init__(self, rule: dict):
         self.cmd, self.file_re = "", None
@@ -33,7 +50,7 @@ class _R2d2Rule:
                 self.cmd = v
             elif k == "file":
                 if v != "":
-                    self.file_re = re.compile(v)
+                    self.file_re = go_regexp(v)
             else:
                 raise ParseError("Unsupported key: " + k)
         if self.cmd not in ("", "READ", "WRITE", "HALT", "RESET"):
@@ -69,7 +86,7 @@ class _CassandraRule:
                 self.action = v
             elif k == "query_table":
                 if v != "":
-                    self.table_re = re.compile(v)
+                    self.table_re = go_regexp(v)
             else:
                 raise ParseError("Unsupported key: " + k)
         if self.action:

@@ -101,3 +101,18 @@ def test_regex_vectors():
             buf = np.frombuffer(sb, np.uint8) if sb else np.zeros(1, np.uint8)
             assert N.lib.cg_diag_regex_match(p, len(p), buf.ctypes.data, len(sb), 0, C.byref(res)) == 0
             assert res.value == exp, (c["pattern"], s)
+
+
+def test_oracle_l4_wrappers_branch_table():
+    """The oracle's policy_can_access_ingress / policy_can_egress restatement
+    (bpf/lib/policy.h:126-163) on the branch-table rows, against the values
+    derived by hand from the reference's branch structure."""
+    from test_gpu_parity import WRAPPER_EXPECT, wrapper_case
+    from cilium_amd.policy import htons
+    keys, ports, t = wrapper_case()
+    for mode, want in WRAPPER_EXPECT.items():
+        got, _, _ = oracle.l4(keys, ports, t, mode)
+        assert got.tolist() == [htons(v) if v > 0 else v for v in want], mode
+    # mode 0 is __policy_can_access itself: fragments and ingress misses keep their codes
+    raw, _, _ = oracle.l4(keys, ports, t, 0)
+    assert -157 in raw.tolist()

@@ -75,6 +75,67 @@ def test_l4_branch_table(gpu):
     del keys
 
 
+# Expected results of the wrappers for the branch-table rows above
+# (bpf/lib/policy.h:126-163): ingress forces CT_INGRESS and keeps the
+# fragment flag; egress forces CT_EGRESS and is_fragment = false; both
+# collapse negatives to DROP_POLICY (or TC_ACT_OK under IGNORE_DROP).
+WRAPPER_ROWS = [
+    (100, 80, 6, 1, 100), (100, 81, 6, 1, 100), (100, 80, 6, 1 | 2, 100), (101, 53, 17, 0, 60),
+    (101, 53, 17, 1, 60), (101, 53, 17, 2, 60), (101, 54, 17, 4, 60), (200, 443, 6, 0, 1500),
+    (200, 443, 6, 1, 1500), (100, 80, 6, 0, 100), (200, 443, 6, 2, 1500), (7, 9, 6, 2, 40),
+]
+WRAPPER_EXPECT = {
+    N.CG_L4_INGRESS: [10001, 0, 0, -133, -133, -133, 0, -133, -133, 10001, -133, -133],
+    N.CG_L4_EGRESS: [-133, -133, -133, 0, 0, 0, 0, 0, 0, -133, 0, -133],
+    N.CG_L4_INGRESS | N.CG_L4_IGNORE_DROP: [10001, 0, 0, 0, 0, 0, 0, 0, 0, 10001, 0, 0],
+    N.CG_L4_EGRESS | N.CG_L4_IGNORE_DROP: [0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0],
+}
+
+
+def wrapper_case():
+    keys = np.zeros(4, dtype=[("sec_label", "<u4"), ("dport", "<u2"), ("protocol", "u1"), ("egress", "u1")])
+    keys[:] = [(100, htons(80), 6, 0), (100, 0, 0, 0), (0, htons(53), 17, 1), (200, htons(443), 6, 1)]
+    ports = np.array([htons(10001), htons(7777), 0, 0], np.uint16)
+    t = np.zeros(len(WRAPPER_ROWS), L4_TUPLE_DTYPE)
+    for i, (ident, port, proto, flags, ln) in enumerate(WRAPPER_ROWS):
+        t[i] = (ident, htons(port), proto, flags, ln)
+    return keys, ports, t
+
+
+@pytest.mark.parametrize("mode", sorted(WRAPPER_EXPECT))
+def test_l4_wrappers_branch_table(gpu, mode):
+    keys, ports, t = wrapper_case()
+    pm = _l4_map(gpu, keys, ports)
+    got = pm.verdicts(t, mode)
+    exp = [htons(v) if v > 0 else v for v in WRAPPER_EXPECT[mode]]
+    assert got.tolist() == exp
+    o, pk, by = oracle.l4(keys, ports, t, mode)
+    assert o.tolist() == exp
+    dump = {(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection): e for k, e in pm.dump_to_slice()}
+    for i, k in enumerate(keys):
+        e = dump[(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"]))]
+        assert (e.Packets, e.Bytes) == (int(pk[i]), int(by[i]))
+    pm.destroy()
+
+
+@pytest.mark.parametrize("mode", [N.CG_L4_INGRESS, N.CG_L4_EGRESS, N.CG_L4_INGRESS | N.CG_L4_IGNORE_DROP])
+def test_l4_wrappers_config2(gpu, mode):
+    """policy_can_access_ingress / policy_can_egress over the config-2 map
+    and 2M tuples with mixed direction/fragment flags: verdicts and counters."""
+    keys, ports = synth.l4_table()
+    pm = _l4_map(gpu, keys, ports)
+    tuples = synth.l4_tuples(2_000_000, keys, seed=mode)
+    got = pm.verdicts(tuples, mode)
+    exp, pk, by = oracle.l4(keys, ports, tuples, mode)
+    assert np.array_equal(got, exp)
+    assert not (exp == -157).any()
+    dump = {(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection): e for k, e in pm.dump_to_slice()}
+    gpk = np.array([dump[(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"]))].Packets
+                    for k in keys], np.uint64)
+    assert np.array_equal(gpk, pk)
+    pm.destroy()
+
+
 def test_l4_empty_and_ragged(gpu):
     keys, ports = synth.l4_table(n_entries=1000, n_ids=500)
     pm = _l4_map(gpu, keys, ports)

@@ -213,34 +213,43 @@ def test_gpu_empty_ragged_and_update(gpu):
     assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
 
 
-# ------------------------------------------- ipcache → L4 (bpf_lxc.c:509-527)
-def _ipc_l4_case(n_entries: int, n: int, seed: int):
+# ----------------------- ipcache → L4 egress (bpf_lxc.c:509-527 v4, :205-220 v6)
+def _ipc_l4_case(n_entries: int, n: int, seed: int, family: int = 4):
+    """Tuples whose flags include ingress and fragment bits: the egress flow
+    must ignore both (policy_can_egress4/6 pass CT_EGRESS and is_fragment
+    false, bpf/lib/policy.h:150-177)."""
     keys, ports = synth.l4_table(n_entries=n_entries, n_ids=1024, seed=seed)
     ids = np.unique(keys["sec_label"])
     ik, iv = synth.ipcache_entries(20_000, n_nodes=64, seed=seed)
     rng = np.random.default_rng(seed)
     iv = iv.copy()
     iv[:, 0] = rng.choice(np.append(ids, [0, 2, 999_999]), len(iv))
-    a4, _ = synth.ipcache_addresses(n, ik, seed=seed)
-    tuples = synth.l4_tuples(len(a4), keys, n_ids=1024, seed=seed)
-    o4, _ = oracle.ipcache(ik, iv, a4, np.zeros((0, 16), np.uint8))
-    t2 = tuples.copy()
-    t2["identity"] = o4[:, 0]
-    exp, _, _ = oracle.l4(keys, ports, t2)
-    return keys, ports, ik, iv, a4, tuples, exp
+    a4, a6 = synth.ipcache_addresses(n, ik, seed=seed)
+    remote = a4 if family == 4 else np.ascontiguousarray(a6, np.uint8).reshape(-1, 16)
+    tuples = synth.l4_tuples(len(remote), keys, n_ids=1024, seed=seed)
+    tuples["flags"] |= rng.choice(np.array([0, 1, 2, 3], np.uint8), len(tuples), p=[0.4, 0.4, 0.1, 0.1])
+    exp, pk, by = oracle.l4_egress_via_ipcache(keys, ports, ik, iv, remote, tuples)
+    return keys, ports, ik, iv, remote, tuples, exp, pk, by
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("family", [4, 6])
 @pytest.mark.parametrize("n_entries", [2048, 65536])  # LDS-fingerprint kernel and the global one
-def test_gpu_l4_via_ipcache(gpu, n_entries):
-    keys, ports, ik, iv, a4, tuples, exp = _ipc_l4_case(n_entries, 300_000, 7)
+def test_gpu_l4_via_ipcache(gpu, n_entries, family):
+    keys, ports, ik, iv, remote, tuples, exp, pk, by = _ipc_l4_case(n_entries, 300_000, 7, family)
     pm = gpu.policy_map(max_entries=max(n_entries, 16384))
     pm.allow_keys(keys, ports)
     ic = gpu.ipcache()
     ic.update(ik, iv)
-    got = pm.verdicts_via_ipcache(ic, a4, tuples)
+    got = pm.verdicts_via_ipcache(ic, remote, tuples)
     assert np.array_equal(got, exp)
-    assert (exp == 0).any() and (exp < 0).any()
+    # egress wrapper: only DROP_POLICY, never DROP_FRAG_NOSUPPORT
+    assert (exp == 0).any() and (exp == -133).any() and not (exp == -157).any()
+    dump = {(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection): e for k, e in pm.dump_to_slice()}
+    for i in range(0, len(keys), 61):
+        k = keys[i]
+        e = dump[(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"]))]
+        assert (e.Packets, e.Bytes) == (int(pk[i]), int(by[i]))
 
 
 def test_destroy(host):

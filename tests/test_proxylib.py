@@ -356,3 +356,57 @@ def test_policy_text_forms():
     r = pp[0]["rules"][0]
     assert r["remote_policies"] == [5, 6]
     assert r["l7_rules"] == {"l7_rules": [{"rule": {"query_action": "select", "query_table": "^db\\."}}]}
+
+
+# ----------------------------------------- arbitrary bytes in r2d2 fields --
+# r2d2 compares the whole cmd and runs Go's regexp on the whole file
+# (r2d2parser.go:61-85, :157-183): a NUL or control byte inside either is
+# part of the string, not a separator, and there is no HTTP codec to reject
+# it.  The engine escapes such bytes (proxylib.escape_value) instead of
+# cutting or denying the request.
+CTRL_POLS = [
+    {"name": "c1", "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"cmd": "READ"}}]}}]}]},
+    {"name": "c2", "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"file": "^pub$"}}, {"rule": {"file": "a.b"}},
+                                                       {"rule": {"cmd": "WRITE", "file": "x\\sy"}}]}}]}]},
+]
+CTRL_LINES = [b"READ\0x foo", b"READ a\x01b", b"READ pub\0secret", b"READ pub", b"WRITE a\rb", b"WRITE a\nb",
+              b"WRITE x\x0by", b"WRITE x\ty", b"READ \x03\x10", b"READ a\x7fb", b"READ\x02 pub", b"HALT",
+              b"READ a\x00b", b"\0\0\0\0 \x01\x02\x03"]
+
+
+def _ctrl_cases():
+    return [(n, line) for n in ("c1", "c2") for line in CTRL_LINES]
+
+
+def _ctrl_check(cl, gpu: bool):
+    pl = P.ProxylibPolicy(cl)
+    pl.update(CTRL_POLS)
+    o = ProxylibOracle(CTRL_POLS)
+    cases = _ctrl_cases()
+    cmds, files = zip(*[P.r2d2_request(line) for _, line in cases])
+    pol = [pl.index(n) for n, _ in cases]
+    one = [1] * len(cases)
+    got = (pl.matches if gpu else pl.matches_host_diag)(pol, one, [80] * len(cases), one, cmds, files)
+    exp = [o.matches(n, True, 80, 1, c, f) for (n, _), c, f in zip(cases, cmds, files)]
+    assert got.tolist() == [int(x) for x in exp], [(c, g, e) for c, g, e in zip(cases, got, exp) if g != e]
+    # the cases the review named: cmd "READ\0x" is not READ; "pub\0secret" is not ^pub$;
+    # control bytes are compared, not rejected
+    d = dict(zip(cases, got.tolist()))
+    assert d[("c1", b"READ\0x foo")] == 0 and d[("c1", b"READ a\x01b")] == 1
+    assert d[("c2", b"READ pub\0secret")] == 0 and d[("c2", b"READ pub")] == 1
+
+
+def test_control_bytes_tables_vs_oracle(host):
+    _ctrl_check(host, gpu=False)
+
+
+@pytest.mark.gpu
+def test_gpu_control_bytes_vs_oracle(gpu):
+    _ctrl_check(gpu, gpu=True)
+
+
+def test_escape_value():
+    assert P.escape_value(b"abc") == b"abc"
+    assert P.escape_value(b"a\0b\x03") == b"a\x03\x10b\x03\x13"

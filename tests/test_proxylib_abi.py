@@ -228,3 +228,27 @@ def test_gpu_shim_random_vs_oracle():
         for c in conns.values():
             c.close()
     _lib.CloseModule(inst)
+
+
+@pytest.mark.gpu
+def test_gpu_r2d2_control_bytes_through_ondata():
+    """NUL and control bytes inside r2d2 frames, through OnData, against the
+    oracle (r2d2parser.go:148-199 frames on "\\r\\n" only)."""
+    from oracle.proxylib_ref import ProxylibOracle
+    from test_proxylib import CTRL_LINES, CTRL_POLS
+    from cilium_amd import proxylib as P
+    inst = open_module([(b"node-id", b"gpu-ctrl")], "0")
+    assert inst != 0
+    t = json.dumps(CTRL_POLS).encode()
+    assert N.lib.cg_proxylib_policy_update(inst, t, len(t)) == N.CG_OK
+    o = ProxylibOracle(CTRL_POLS)
+    for name in ("c1", "c2"):
+        c = Conn(inst, policy=name.encode())
+        frames = [line + b"\r\n" for line in CTRL_LINES]
+        rc, ops = c.on_data([b"".join(frames)], cap=len(frames) + 1)
+        exp = [o.matches(name, True, 80, 1, *P.r2d2_request(line)) for line in CTRL_LINES]
+        assert rc == F_OK
+        assert ops == [(PASS if e else DROP, len(f)) for e, f in zip(exp, frames)] + [(MORE, 1)], name
+        assert c.injected_reply() == b"ERROR\r\n" * sum(1 for e in exp if not e)
+        c.close()
+    _lib.CloseModule(inst)
