@@ -200,13 +200,15 @@ def batch_parts(batch: np.ndarray):
     return ntiles, toff, chunks, ttab
 
 
-def replicate_batch(b, reps: int, dev, torch):
+def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False):
     """Device batch of `reps` copies of packed batch b, laid out as the packer
     lays out a batch of reps x D requests: each program's tiles (its `reps`
     copies) are contiguous and cut into chunks of CHUNK_TILES
     (http_pack.cc).  Returns (device batch, nslots, tile_map, data_bytes)
     where tile_map[t] is the tile of the first copy of b's tile t and
-    data_bytes the bytes of the packed input (tables + tiles)."""
+    data_bytes the bytes of the packed input (tables + tiles).  With
+    return_groups, also [(first tile in b, tiles, first tile of copy 0)] per
+    program group: copy r of b's tile first + j is tile at + r * tiles + j."""
     ntiles, toff, chunks, ttab = batch_parts(b.batch)
     groups = []  # (prog, first tile, ntiles) of each program group of b
     for prog, first, nt, _ in chunks:
@@ -256,6 +258,8 @@ def replicate_batch(b, reps: int, dev, torch):
             d[g0 + done * gb:g0 + (done + k) * gb].copy_(d[g0:g0 + k * gb])
             done += k
         tile_map[first:first + nt] = np.arange(at, at + nt)
+    if return_groups:
+        return d, pos * 64, tile_map, total - 64, [(first, nt, at) for first, nt, at, _, _, _ in placed]
     return d, pos * 64, tile_map, total - 64
 
 

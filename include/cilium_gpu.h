@@ -384,10 +384,12 @@ int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* in
  * Request r is raw[raw_off[r] .. raw_off[r+1]): request-line, header fields,
  * empty line.  Writes the cg_http_pack header lists (:method, :path with the
  * query, :authority from Host, then the other headers as sent) into hdr_blob
- * / hdr_off (n+1 entries) and ok[r] = 0 for a head the codec rejects
- * (bad request-line, non-token name, control byte in a value, no final
- * CRLF): pack those with policy UINT32_MAX so they are denied, as Envoy
- * answers 400 before the filter.  hdr_blob NULL = size query (*blob_used). */
+ * / hdr_off (n+1 entries) and ok[r] = 0 (ok may be NULL) for a head the
+ * codec rejects (bad request-line, non-token name, control byte in a value,
+ * no final CRLF).  A rejected head's list is one entry whose value is the
+ * byte 0x7F, which cg_http_pack flags CG_HTTP_F_MALFORMED: it is denied
+ * under any policy, as Envoy answers 400 before the filter.  hdr_blob NULL
+ * = size query (*blob_used). */
 int cg_http_parse_heads(const uint8_t* raw, const uint64_t* raw_off, size_t n, uint8_t* hdr_blob,
                         size_t blob_cap, uint64_t* hdr_off, size_t* blob_used, uint8_t* ok);
 

@@ -114,3 +114,21 @@ def test_gpu_raw_path(gpu):
                           np.full(n, synth.SPACESHIP_ID, np.uint32), *_blob(raws))
     got = gpu.http_verdicts(b)
     assert all(got[i] == 0 for i, (_, e) in enumerate(CASES) if e is None)
+
+
+def test_rejected_heads_denied_without_ok(host):
+    """A head the codec rejects is denied even when the caller packs it under
+    a real policy whose port allows everything (no HTTP rules): its header
+    list carries a DEL value the packer flags malformed."""
+    pols = [{"name": "open", "policy": 1, "ingress_per_port_policies": [
+        {"port": 80, "rules": [{"remote_policies": [7]}]}]}]
+    host.update_http_policy(pols)
+    good = b"GET /x HTTP/1.1\r\nHost: a\r\n\r\n"
+    bad = [b"GET /x HTTP/1.1\r\nHost: a\x01b\r\n\r\n", b"GET /x HTTP/1.1\r\n", b"G@T /x HTTP/1.1\r\n\r\n"]
+    raws = [good] + bad
+    blob, off, ok = Classifier.parse_http_heads(*_blob(raws))
+    assert ok.tolist() == [1, 0, 0, 0]
+    n = len(raws)
+    b = host.pack_http(np.zeros(n, np.uint32), np.ones(n, np.uint8), np.full(n, 80, np.uint16),
+                       np.full(n, 7, np.uint32), blob, off)
+    assert host.http_eval_host_diag(b).tolist() == [1, 0, 0, 0]
