@@ -42,11 +42,40 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="rehearse the N-rank launch, rendezvous and counter all-reduce on the CPU (gloo, the "
+                         "library's host table walker on a small batch): no GPU, and not a measurement")
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` run without a launcher: start N rank processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, as
+    torch.distributed.run sets them) before this process touches a GPU, and
+    return the worst exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args.gpus))
+    if args.cpu_rehearsal:
+        return rehearse(args)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,8 +108,8 @@ def main():
     d_batch, nslots, tile_map, data_bytes = replicate_batch(b, reps, dev, torch)
     d_arena = torch.from_numpy(b.arena).to(dev)
     d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
-    nprog_ctr = int(cl.read_counters(0).size)
-    d_ctr = torch.zeros(max(nprog_ctr, 1), dtype=torch.int64, device=dev)
+    n_ctr = cl.allreduce_counter_count()
+    d_ctr = torch.zeros(max(n_ctr, 1), dtype=torch.int64, device=dev)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     kev = []  # (start, end) HIP events around each verdict-kernel launch, on its stream
@@ -94,8 +123,9 @@ def main():
             e1.record(stream)
             kev.append((e0, e1))
         if dist is not None:
-            from cilium_amd import _native as N
-            N.check(N.lib.cg_counters_copy_dev(cl.h, 0, 0, d_ctr.data_ptr(), nprog_ctr, stream.cuda_stream))
+            # the only collective: per-rule hits and per-program allowed/
+            # denied counters, summed over ranks (RCCL over xGMI)
+            cl.counters_copy_dev(d_ctr, n_ctr, stream=stream.cuda_stream)
             with torch.cuda.stream(stream):
                 dist.all_reduce(d_ctr)
 
@@ -148,8 +178,10 @@ def main():
     # same unit as `achieved`: HBM bytes per launch over the measured launch time
     traffic = traffic_bytes / (kernel_ms * 1e-3) / 1e9 if traffic_bytes else None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pols, info, args.cpu_seconds)
+    if dist is not None:
+        dist.barrier()
 
     if rank == 0:
         line = {
@@ -171,7 +203,7 @@ def main():
                        "requests_per_gpu": B, "rules": int(stats["rules"]), "programs": int(stats["programs"]),
                        "dfa_states": int(stats["states"]), "table_bytes": int(stats["table_bytes"]),
                        "compile_s": round(compile_s, 3), "packed_bytes_per_request": per_launch_bytes / B,
-                       "parallelism": f"dp{world}"},
+                       "allreduce_counters": n_ctr, "parallelism": f"dp{world}"},
             "request_gbps": value * per_launch_bytes / B / 1e9,
             "allow_fraction": allow_frac,
             "parity_check": check,
@@ -186,6 +218,89 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     cl.close()
+
+
+def rehearse(args):
+    """--cpu-rehearsal: the N>1 control flow of main() without a GPU — gloo
+    rendezvous on 127.0.0.1, one shard per rank (bench's per-rank seed), the
+    shard classified by the library's host table walker (diagnostics, never a
+    verdict path), the per-program allowed/denied counters all-reduced, the
+    max-over-ranks wall time, and rank 0's single JSON line.  Its value is
+    not a measurement (the line says so)."""
+    import torch
+    import torch.distributed as dist
+
+    from cilium_amd import synth
+    from cilium_amd.classifier import Classifier
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    cl = Classifier(device=-1)
+    pols, info = synth.http10k_rules(n_rules=2000, n_ports=16)
+    cl.update_http_policy(pols)
+    D = max(64, min(args.requests_per_gpu, args.distinct))
+    rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
+    b = cl.pack_http(**rq)
+    nprog = int(cl.http_policy_stats()["programs"])
+    ctr = torch.zeros(2 * nprog, dtype=torch.int64)
+
+    def step():
+        slot_v = cl.http_eval_host_diag_slots(b)
+        ctr.add_(torch.from_numpy(program_counts(b, slot_v, nprog)))
+        if world > 1:
+            t = ctr.clone()
+            dist.all_reduce(t)
+            return t
+        return ctr
+
+    for _ in range(args.warmup):
+        step()
+    ctr.zero_()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        total = step()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": D * world * args.steps / wall, "unit": "verdicts/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+                          "config": {"workload": "CPU rehearsal of the N-rank path (host table walker, gloo)",
+                                     "requests_per_gpu": D, "parallelism": f"dp{world}"},
+                          "rehearsal": True,
+                          "allreduced_requests": int(total.sum()), "expected_requests": D * world * args.steps}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    cl.close()
+
+
+def program_counts(b, slot_v: np.ndarray, nprog: int) -> np.ndarray:
+    """allowed/denied per program from slot verdicts (what the kernel's
+    per-program counters hold after one pass over batch b)."""
+    hdr = b.batch[:64]
+    nchunks = int(hdr[8:12].view(np.uint32)[0])
+    chunks = b.batch[64:64 + 16 * nchunks].view(np.uint32).reshape(nchunks, 4)
+    c = np.zeros(2 * nprog, np.int64)
+    for prog, first, nt, _ in chunks:
+        if prog >= nprog:
+            continue
+        sl = slice(int(first) * 64, int(first + nt) * 64)
+        real = b.order[sl] != 0xFFFFFFFF
+        v = slot_v[sl][real].astype(np.int64)
+        c[2 * prog] += int(v.sum())
+        c[2 * prog + 1] += int((1 - v).sum())
+    return c
 
 
 def batch_parts(batch: np.ndarray):

@@ -43,6 +43,9 @@ CG_PF_DYN4, CG_PF_DYN6, CG_PF_FIX4, CG_PF_FIX6 = 1, 2, 4, 8
 CG_XDP_DROP, CG_XDP_PASS = 1, 2
 CG_WORLD_ID = 2
 
+CG_CTR_HTTP_PROGRAMS, CG_CTR_KAFKA, CG_CTR_PREFILTER, CG_CTR_HTTP_RULES, CG_CTR_HTTP_ALLREDUCE = 0, 1, 2, 3, 4
+CG_HTTP_RULE_NO_HTTP, CG_HTTP_RULE_SCOPE_ALLOW = 0xFFFFFFFF, 0xFFFFFFFE
+
 CG_HTTP_TILE = 64
 CG_HTTP_UNITS = 9
 
@@ -119,6 +122,7 @@ SIGNATURES = {
     "cg_http_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_http_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_http_policy_stats": (C.c_int, [_u64, C.POINTER(_u64), _sz]),
+    "cg_http_rule_info_get": (C.c_int, [_u64, _p, _sz, C.POINTER(_sz)]),
     "cg_http_batch_bytes": (_sz, [_u64, _sz]),
     "cg_http_batch_slots": (_sz, [_u64, _sz]),
     "cg_http_pack": (C.c_int, [_u64, _sz, _p, _p, _p, _p, _p, _p, _p, _sz, _p, C.POINTER(_sz), _p, _sz,
@@ -137,6 +141,7 @@ SIGNATURES = {
     "cg_reset_counters": (C.c_int, [_u64]),
     "cg_diag_regex_match": (C.c_int, [C.c_char_p, _sz, _p, _sz, _u32, C.POINTER(C.c_uint8)]),
     "cg_diag_http_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
+    "cg_diag_http_rules_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_diag_kafka_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
     "cg_diag_l4_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p]),
     "cg_diag_ipcache_eval_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),

@@ -179,6 +179,48 @@ class Classifier:
         """Enqueue the verdict kernel on device buffers; d_out is in slot order."""
         N.check(N.lib.cg_http_verdicts_dev(self.h, _p(d_batch), nslots, _p(d_arena), _p(d_out), stream))
 
+    HTTP_RULE_INFO_DTYPE = np.dtype([("policy", "<u4"), ("ingress", "<u4"), ("port", "<u4"), ("scope", "<u4"),
+                                     ("rule", "<u4"), ("http_rule", "<u4")])
+
+    def http_rule_info(self) -> np.ndarray:
+        """What each per-rule hit counter counts (cg_http_rule_info_get):
+        (policy, ingress, program port, scope 0 exact / 1 port 0, rule,
+        http_rule)."""
+        n = C.c_size_t()
+        N.check(N.lib.cg_http_rule_info_get(self.h, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), self.HTTP_RULE_INFO_DTYPE)
+        N.check(N.lib.cg_http_rule_info_get(self.h, _p(out), n.value, C.byref(n)))
+        return out[:n.value]
+
+    def http_rule_hits(self) -> np.ndarray:
+        """Per-rule first-match hit counters (cg_read_counters CG_CTR_HTTP_RULES)."""
+        return self.read_counters(N.CG_CTR_HTTP_RULES)
+
+    def allreduce_counter_count(self) -> int:
+        """Length of the HTTP all-reduce vector (CG_CTR_HTTP_ALLREDUCE)."""
+        return self.counters_device_ptr(N.CG_CTR_HTTP_ALLREDUCE)[1]
+
+    def counters_copy_dev(self, d_dst, n: int, stream=None, what: int = N.CG_CTR_HTTP_ALLREDUCE) -> None:
+        """Async device copy of a counter set (default: the HTTP all-reduce
+        vector) into d_dst on `stream`."""
+        N.check(N.lib.cg_counters_copy_dev(self.h, what, 0, _p(d_dst), n, stream))
+
+    def http_rules_host_diag(self, b: "HttpBatch") -> np.ndarray:
+        """Compiler diagnostics only: per request the rule counter it hits."""
+        out = np.zeros(max(b.n, 1), np.uint32)
+        N.check(N.lib.cg_diag_http_rules_host(self.h, _p(b.batch), b.nslots, _p(b.order), b.n, _p(b.arena),
+                                              b.arena.nbytes, _p(out)))
+        return out[:b.n]
+
+    def http_eval_host_diag_slots(self, b: "HttpBatch") -> np.ndarray:
+        """Compiler diagnostics only: the host walk's verdict per batch slot."""
+        v = self.http_eval_host_diag(b)
+        out = np.zeros(b.nslots, np.uint8)
+        order = b.order[:b.nslots]
+        real = order < b.n
+        out[real] = v[order[real]]
+        return out
+
     def http_eval_host_diag(self, b: "HttpBatch") -> np.ndarray:
         """Compiler diagnostics only: walk the compiled tables on the CPU."""
         out = np.zeros(max(b.n, 1), np.uint8)

@@ -778,6 +778,15 @@ int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index) {
   });
 }
 
+int cg_http_rule_info_get(uint64_t h, cg_http_rule_info* out, size_t cap, size_t* n) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = http_snap(*e);
+    if (n) *n = s->rule_info.size();
+    if (out) memcpy(out, s->rule_info.data(), std::min(cap, s->rule_info.size()) * sizeof(cg_http_rule_info));
+  });
+}
+
 int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
   return guarded([&] {
     auto e = get(h);
@@ -971,10 +980,20 @@ int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n, c
 static void counters_loc(Engine& e, uint32_t what, uint32_t id, void** p, size_t* n) {
   *p = nullptr;
   *n = 0;
-  if (what == 0) {
+  if (what == CG_CTR_HTTP_PROGRAMS || what == CG_CTR_HTTP_RULES || what == CG_CTR_HTTP_ALLREDUCE) {
     auto s = http_snap(e);
-    *p = s->d_counters.get();
-    *n = s->progs.size() * 2;
+    uint64_t* base = s->d_counters.as<uint64_t>();
+    const size_t np = s->progs.size() * 2, nr = s->rule_info.size();
+    if (what == CG_CTR_HTTP_PROGRAMS) {
+      *p = base;
+      *n = np;
+    } else if (what == CG_CTR_HTTP_RULES) {
+      *p = base ? base + np + 1 : nullptr;
+      *n = nr;
+    } else {
+      *p = base;
+      *n = np + 1 + nr;
+    }
   } else if (what == 1) {
     auto s = kafka_snap(e);
     *p = s->d_counters.get();
@@ -1054,6 +1073,19 @@ int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t 
   return guarded([&] {
     ByteDfa d = compile_regex(std::string(re, re_len), ByteSet::all(), search ? MatchMode::Search : MatchMode::Full);
     *result = dfa_run(d, std::string((const char*)s, len)) ? 1 : 0;
+  });
+}
+
+int cg_diag_http_rules_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order, size_t n,
+                            const uint8_t* arena, size_t arena_len, uint32_t* rule) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = http_snap(*e);
+    std::vector<uint8_t> slots(nslots);
+    std::vector<uint32_t> r(nslots);
+    http_eval_host(*s, (const uint8_t*)batch, arena, arena_len, slots.data(), r.data());
+    for (size_t i = 0; i < nslots; ++i)
+      if (order[i] < n) rule[order[i]] = r[i];
   });
 }
 

@@ -5,6 +5,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "../../include/cilium_gpu.h"
+
 #if defined(__HIP__) || defined(__HIPCC__)
 #define CG_HD __host__ __device__
 #else
@@ -139,8 +141,12 @@ struct HttpProg {
   uint32_t cell_count;      // as one piece: parts' comb cells, label tables, masks,
   uint32_t rtab_off;        // remote-identity table: {u32 identity, u32 mask offset}
   uint32_t rtab_mask;       // slots, open addressing by hash32(identity)
-  uint32_t pad[2];
+  uint32_t rule_base;       // this program's first per-rule hit counter
+  uint32_t nrules;          // mask bits = rules (HttpSnapshot::rule_info)
 };
+// Per-rule hit counters a workgroup keeps in LDS for its current program
+// (programs with more rules count straight into global memory).
+constexpr uint32_t kLdsRuleHits = 1024;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; states >= self_lo default to themselves.
@@ -209,6 +215,7 @@ struct HttpDev {
   uint32_t lds_cells;            // max cells a workgroup stages in LDS
   uint32_t n_global_progs;       // walked programs too large for LDS
   unsigned long long* counters;  // [prog*2] allowed, [prog*2+1] denied, [2*nprogs] stale batches
+  unsigned long long* rule_hits; // counters + 2*nprogs + 1: first-match hits per rule
 };
 
 CG_HD inline uint32_t hash32(uint32_t x) {

@@ -50,7 +50,9 @@ constexpr uint8_t kAbsent = 0x01;
 constexpr uint8_t kRestAbsent = 0x02;  // every remaining field absent (ends the string)
 constexpr int kMaxUnionStates = 400000;  // before minimization, per part
 constexpr int kMaxPartStates = 65535;    // u16 transition entries
-constexpr uint32_t kMaxLdsCells = 40944;  // 160 KiB less 64 B of static LDS (counters): one program table per workgroup
+// 160 KiB less the static LDS (allowed/denied pair, per-rule hit counters):
+// one program table per workgroup
+constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits) / 4;
 
 enum class MKind { Exact, Regex, Present, Search };
 struct MatcherSpec {
@@ -497,36 +499,69 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
 
 
   // Build one program from the merged PNPR list; returns program id.
-  auto build_prog = [&](const std::vector<const ScopeSpec*>& scopes, uint32_t key) -> uint32_t {
+  //
+  // Mask bits are rules in Envoy's evaluation order: the exact port's
+  // PortNetworkPolicyRules, then port 0's; within a PNPR one bit per
+  // HttpNetworkPolicyRule (one bit for a PNPR without HTTP rules).  A
+  // request's first matching rule is then the lowest bit of (its accept
+  // label | the "always" bits) & its remote row, and its per-rule hit counter
+  // is rule_base + that bit.  A scope without HTTP rules allows everything
+  // (:129-138): first in the order it decides the program alone (allow-all,
+  // nothing attributed); after the exact port's rules it is one more
+  // always-matching bit whose counter records "allowed by the wildcard
+  // scope" (rule_info http = CG_HTTP_RULE_SCOPE_ALLOW).
+  auto build_prog = [&](const std::vector<const ScopeSpec*>& scopes, uint32_t key, uint32_t pol_idx,
+                        uint32_t ingress, uint32_t port) -> uint32_t {
     HttpProg pg{};
     uint32_t pid = (uint32_t)S.progs.size();
-    bool allow_all = false;
+    struct Bit {
+      const PnprSpec* pnpr;  // nullptr: an allow-all scope
+      uint32_t scope, pnpr_idx, http_idx;
+    };
+    std::vector<Bit> bits;
+    std::vector<uint32_t> pnpr_first;  // first bit of each entry of pnprs
     std::vector<const PnprSpec*> pnprs;
-    for (const ScopeSpec* sc : scopes) {
+    for (uint32_t si = 0; si < scopes.size(); ++si) {
+      const ScopeSpec* sc = scopes[si];
       bool have_http = false;
       for (const auto& r : sc->rules) have_http |= r.has_http;
-      if (!have_http || sc->rules.empty()) allow_all = true;  // :129-138
-      for (const auto& r : sc->rules) pnprs.push_back(&r);
+      if (!have_http || sc->rules.empty()) {  // :129-138
+        if (si == 0) {
+          pg.flags = kProgAllowAll;
+          S.progs.push_back(pg);
+          S.prog_key.push_back(key);
+          return pid;
+        }
+        bits.push_back({nullptr, si, 0, CG_HTTP_RULE_SCOPE_ALLOW});
+        break;  // rules after an allow-all scope are never reached
+      }
+      for (uint32_t ri = 0; ri < sc->rules.size(); ++ri) {
+        const PnprSpec& r = sc->rules[ri];
+        pnprs.push_back(&r);
+        pnpr_first.push_back((uint32_t)bits.size());
+        if (r.http.empty()) bits.push_back({&r, si, ri, CG_HTTP_RULE_NO_HTTP});
+        for (uint32_t hi = 0; hi < r.http.size(); ++hi) bits.push_back({&r, si, ri, hi});
+      }
     }
-    if (allow_all) {
-      pg.flags = kProgAllowAll;
-      S.progs.push_back(pg);
-      S.prog_key.push_back(key);
-      return pid;
-    }
-    const uint32_t R = (uint32_t)pnprs.size();
+    const uint32_t R = (uint32_t)bits.size();
     const uint32_t W = (R + 63) / 64;
     pg.mask_words = W;
-    // always: PNPRs with no HTTP rules match any payload (:98-107)
+    pg.rule_base = (uint32_t)S.rule_info.size();
+    pg.nrules = R;
+    for (const Bit& b : bits) S.rule_info.push_back({pol_idx, ingress, port, b.scope, b.pnpr_idx, b.http_idx});
+    // always: PNPRs with no HTTP rules (and an allow-all scope) match any
+    // payload (:98-107); open: bits of PNPRs without a remote set
     std::vector<uint64_t> always(W, 0), open(W, 0);
     std::map<uint32_t, std::vector<uint64_t>> by_remote;
     for (uint32_t j = 0; j < R; ++j) {
-      if (pnprs[j]->http.empty()) always[j >> 6] |= 1ULL << (j & 63);
-      if (!pnprs[j]->has_remotes) open[j >> 6] |= 1ULL << (j & 63);
+      const Bit& b = bits[j];
+      if (!b.pnpr || b.pnpr->http.empty()) always[j >> 6] |= 1ULL << (j & 63);
+      if (!b.pnpr || !b.pnpr->has_remotes) open[j >> 6] |= 1ULL << (j & 63);
     }
     for (uint32_t j = 0; j < R; ++j) {
-      if (!pnprs[j]->has_remotes) continue;
-      for (uint64_t rid : pnprs[j]->remotes) {
+      const Bit& b = bits[j];
+      if (!b.pnpr || !b.pnpr->has_remotes) continue;
+      for (uint64_t rid : b.pnpr->remotes) {
         if (rid > 0xFFFFFFFFULL) continue;  // can never equal a u32 identity
         auto it = by_remote.find((uint32_t)rid);
         if (it == by_remote.end()) it = by_remote.emplace((uint32_t)rid, open).first;
@@ -535,11 +570,13 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     }
     for (uint64_t w : always)
       if (w) pg.flags |= kProgHasAlways;
-    // union rules
+    // union rules: each HTTP rule tags its own bit
     std::vector<URule> urules;
     std::map<std::vector<int>, size_t> dedupe;
-    for (uint32_t j = 0; j < R; ++j) {
+    for (uint32_t j = 0; j < (uint32_t)pnprs.size(); ++j) {
+      uint32_t bit = pnpr_first[j];
       for (const auto& hr : pnprs[j]->http) {
+        const uint32_t tag = bit++;
         std::vector<std::vector<const MatcherSpec*>> per_field(F);
         for (const auto& m : hr) per_field[field_idx[m.name]].push_back(&m);
         std::vector<int> fd(F);
@@ -552,9 +589,9 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
         auto it = dedupe.find(fd);
         if (it == dedupe.end()) {
           dedupe[fd] = urules.size();
-          urules.push_back({fd, {j}});
+          urules.push_back({fd, {tag}});
         } else {
-          urules[it->second].tags.push_back(j);
+          urules[it->second].tags.push_back(tag);
         }
       }
     }
@@ -655,14 +692,14 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       auto w = ports.find(0);
       if (w != ports.end()) wild = &w->second;
       if (p.deny_unlisted) S.dflt[pi * 2 + d] = kProgDeny;
-      if (wild) S.dflt[pi * 2 + d] = build_prog({wild}, (pi << 17) | ((uint32_t)d << 16));
+      if (wild) S.dflt[pi * 2 + d] = build_prog({wild}, (pi << 17) | ((uint32_t)d << 16), pi, d, 0);
       for (const auto& [port, sc] : ports) {
         if (port == 0) continue;
         if (port > 0xFFFF) continue;  // can never equal a 16-bit destination port
         std::vector<const ScopeSpec*> scs{&sc};
         if (wild) scs.push_back(wild);
         uint32_t key = (pi << 17) | ((uint32_t)d << 16) | port;
-        phash.push_back({key, build_prog(scs, key)});
+        phash.push_back({key, build_prog(scs, key, pi, d, port)});
       }
     }
   }
@@ -704,7 +741,9 @@ void HttpSnapshot::upload(Engine& e) {
   d_parts.upload_vec(parts);
   d_cells.upload_vec(cells);
   d_dflt.upload_vec(dflt);
-  d_counters.alloc((std::max<size_t>(progs.size(), 1) * 2 + 1) * sizeof(uint64_t));
+  // [2 * prog] allowed, [2 * prog + 1] denied, [2 * nprogs] stale batches,
+  // then one hit counter per rule (rule_info order): the all-reduce vector
+  d_counters.alloc((std::max<size_t>(progs.size(), 1) * 2 + 1 + rule_info.size()) * sizeof(uint64_t));
   d_counters.zero();
   dev.progs = d_progs.as<HttpProg>();
   dev.parts = d_parts.as<HttpPart>();
@@ -726,6 +765,7 @@ void HttpSnapshot::upload(Engine& e) {
     if (!(pg.flags & kProgAllowAll) && !((pg.flags & kProgRebased) && pg.cell_count <= dev.lds_cells))
       dev.n_global_progs++;
   dev.counters = d_counters.as<unsigned long long>();
+  dev.rule_hits = dev.counters + 2 * (size_t)dev.nprogs + 1;
 }
 
 }  // namespace cg

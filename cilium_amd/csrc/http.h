@@ -27,6 +27,8 @@ struct HttpSnapshot {
   std::vector<uint32_t> dflt;
   // (policy, ingress, port) of each program, for counter attribution
   std::vector<uint32_t> prog_key;
+  // what each per-rule hit counter counts (HttpProg.rule_base + bit)
+  std::vector<cg_http_rule_info> rule_info;
 
   uint32_t epoch = 0;
   uint64_t total_states = 0;
@@ -57,7 +59,9 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
 // Walk the snapshot's tables on the host exactly as the kernel does, for
 // every slot of a batch (diagnostics / compiler tests only; the verdict API
 // never calls this).  out has one byte per slot.
+// rule (optional, one per slot): the global index of the first rule that
+// allows the slot (the per-rule hit counter it adds to), or UINT32_MAX.
 void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* arena, size_t arena_len,
-                    uint8_t* out);
+                    uint8_t* out, uint32_t* rule = nullptr);
 
 }  // namespace cg

@@ -276,7 +276,7 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
 }
 
 void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* arena, size_t arena_len,
-                    uint8_t* out) {
+                    uint8_t* out, uint32_t* rule) {
   HttpBatchHeader h;
   memcpy(&h, batch, sizeof(h));
   if (h.magic != kBatchMagic || h.epoch != s.epoch) fail(CG_INVALID_ARGUMENT, "batch packed for another snapshot");
@@ -298,6 +298,7 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
       const uint8_t flags = meta[7];
       uint8_t v = 0;
       out[sl] = 0;
+      if (rule) rule[sl] = 0xFFFFFFFFu;
       if (flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED)) continue;
       if (prog == kProgDeny) continue;
       if (prog == kProgAllow) {
@@ -332,9 +333,15 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
           break;
         }
       }
-      for (uint32_t w = 0; w < pg.mask_words; ++w)
-        if (bmask(pg.always_off, w) & bmask(roff, w)) v = 1;
-      for (uint32_t pi = 0; pi < pg.part_count && !v; ++pi) {
+      // first rule (lowest bit) the mask at block offset a shares with the row
+      uint32_t hit = 0xFFFFFFFFu;
+      auto first = [&](uint32_t a) {
+        for (uint32_t w = 0; w < pg.mask_words; ++w)
+          if (const uint64_t x = bmask(a, w) & bmask(roff, w)) return w * 64 + (uint32_t)__builtin_ctzll(x);
+        return 0xFFFFFFFFu;
+      };
+      hit = std::min(hit, first(pg.always_off));
+      for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
         const HttpPart& pt = s.parts[pg.part_begin + pi];
         const uint32_t* cells = s.cells.data() + pt.walk_off;
         uint32_t st = pt.start;
@@ -344,11 +351,11 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         }
         const uint32_t lab = comb_label(cells, st);
         if (lab == kCombNoLabel) continue;
-        const uint32_t a = pt.acc_off + lab * 2 * pg.mask_words;
-        for (uint32_t w = 0; w < pg.mask_words; ++w)
-          if (bmask(a, w) & bmask(roff, w)) v = 1;
+        hit = std::min(hit, first(pt.acc_off + lab * 2 * pg.mask_words));
       }
+      v = hit != 0xFFFFFFFFu;
       out[sl] = v;
+      if (rule && v) rule[sl] = pg.rule_base + hit;
     }
   }
 }

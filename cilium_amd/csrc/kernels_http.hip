@@ -115,11 +115,24 @@ __device__ __forceinline__ unsigned long long blk_word(const uint32_t* __restric
   return *reinterpret_cast<const unsigned long long*>(blk + a + 2 * w);
 }
 
-// Do the PNPR masks at block offsets a and row share a rule?
-__device__ __forceinline__ bool meets(const uint32_t* __restrict__ blk, uint32_t a, uint32_t row, uint32_t W) {
-  for (uint32_t w = 0; w < W; ++w)
-    if (blk_word(blk, a, w) & blk_word(blk, row, w)) return true;
-  return false;
+// The first rule (lowest bit) the rule masks at block offsets a and row
+// share, or kNoHit: the first rule that allows the request, in Envoy's
+// evaluation order (http.cc build_prog).
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t first_meet(const uint32_t* __restrict__ blk, uint32_t a, uint32_t row,
+                                               uint32_t W) {
+  for (uint32_t w = 0; w < W; ++w) {
+    const unsigned long long x = blk_word(blk, a, w) & blk_word(blk, row, w);
+    if (x) return w * 64 + (uint32_t)__builtin_ctzll(x);
+  }
+  return kNoHit;
+}
+
+// One first-match hit of rule `hit` of program pg: into the workgroup's LDS
+// counters when the program's rules fit them, else into global memory.
+__device__ __forceinline__ void count_hit(const HttpDev& T, const HttpProg& pg, uint32_t hit, uint32_t* s_hits) {
+  if (s_hits && pg.nrules <= kLdsRuleHits) atomicAdd(&s_hits[hit], 1u);
+  else atomicAdd(&T.rule_hits[pg.rule_base + hit], 1ULL);
 }
 
 // K tiles of a program (tile j takes part only if valid[j]): walk every
@@ -135,12 +148,13 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
                                            const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
                                            uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
-                                           uint32_t& n_deny) {
+                                           uint32_t& n_deny, uint32_t* s_hits) {
   TileRef tr[K];
   uint2 meta[K];
   uint32_t row[K];
   uint32_t units = 0, tu[K];  // string units: of the K tiles (the longest, wave-uniform), of each
-  bool counted[K], overflow[K], verdict[K];
+  bool counted[K], overflow[K];
+  uint32_t hit[K];
   bool any_overflow = false;
   const uint32_t W = pg.mask_words;
 #pragma unroll
@@ -155,7 +169,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     overflow[j] = counted[j] && (flags & CG_HTTP_F_OVERFLOW);
     any_overflow |= overflow[j];
     row[j] = remote_row(blk, pg, meta[j].x);
-    verdict[j] = false;
+    hit[j] = kNoHit;
   }
   any_overflow = __any(any_overflow);
   for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
@@ -202,16 +216,17 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t lab = counted[j] && st[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
-      if (lab != 0xFFFFu && !verdict[j]) verdict[j] = meets(blk, pt.acc_off + lab * 2 * W, row[j], W);
+      if (lab != 0xFFFFu) hit[j] = min(hit[j], first_meet(blk, pt.acc_off + lab * 2 * W, row[j], W));
     }
   }
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    if (counted[j] && !verdict[j] && (pg.flags & kProgHasAlways))
-      verdict[j] = meets(blk, pg.always_off, row[j], W);
-    if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict[j];
-    n_allow += counted[j] && verdict[j];
-    n_deny += counted[j] && !verdict[j];
+    if (counted[j] && (pg.flags & kProgHasAlways)) hit[j] = min(hit[j], first_meet(blk, pg.always_off, row[j], W));
+    const bool verdict = counted[j] && hit[j] != kNoHit;
+    if (verdict) count_hit(T, pg, hit[j], s_hits);
+    if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict;
+    n_allow += counted[j] && verdict;
+    n_deny += counted[j] && !verdict;
   }
 }
 
@@ -229,7 +244,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
                                             const TileRef tr, uint32_t t,
                                             const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                             uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
-                                            uint32_t& n_deny) {
+                                            uint32_t& n_deny, uint32_t* s_hits) {
   const uint2 meta = tr.meta[lane];
   uint4 unit[N > 0 ? N : 1];
 #pragma unroll
@@ -249,26 +264,29 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
     const uint32_t sa = walk_overflow(blk, self_lo, pt.start, arena, arena_bytes, meta, overflow);
     if (overflow) st = sa;
   }
-  bool verdict = false;
+  uint32_t hit = kNoHit;
   if (counted) {
     const uint32_t lab = st ? (blk[st - 1] >> 16) : 0xFFFFu;
     const bool always = pg.flags & kProgHasAlways;
     if (lab != 0xFFFFu || always) {
       const uint32_t row = remote_row(blk, pg, meta.x);
-      if (lab != 0xFFFFu) verdict = meets(blk, pt.acc_off + lab * 2 * pg.mask_words, row, pg.mask_words);
-      if (!verdict && always) verdict = meets(blk, pg.always_off, row, pg.mask_words);
+      if (lab != 0xFFFFu) hit = first_meet(blk, pt.acc_off + lab * 2 * pg.mask_words, row, pg.mask_words);
+      if (always) hit = min(hit, first_meet(blk, pg.always_off, row, pg.mask_words));
     }
   }
+  const bool verdict = hit != kNoHit;
+  if (verdict) count_hit(T, pg, hit, s_hits);
   out[(size_t)t * kWave + lane] = (uint8_t)verdict;
   n_allow += counted && verdict;
   n_deny += counted && !verdict;
 }
 
 // End of a workgroup's run of chunks of program `prog`: wave totals are
-// summed in LDS, then one thread adds them to the global counters.  Ends
-// with every wave past a barrier, so the caller may restage lcells.
+// summed in LDS, then one thread adds them to the global counters, and the
+// program's LDS rule-hit counters go to global memory (and are cleared).
+// Ends with every wave past a barrier, so the caller may restage lcells.
 __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, uint32_t& n_allow, uint32_t& n_deny,
-                                             uint32_t lane, uint32_t* s_cnt) {
+                                             uint32_t lane, uint32_t* s_cnt, uint32_t* s_hits) {
   const bool real = prog < T.nprogs;  // uniform
   if (real) {
     for (int o = 32; o > 0; o >>= 1) {
@@ -287,6 +305,17 @@ __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, ui
     if (real && s_cnt[1]) atomicAdd(&T.counters[2 * prog + 1], (unsigned long long)s_cnt[1]);
     s_cnt[0] = s_cnt[1] = 0;
   }
+  if (real && s_hits) {
+    const uint32_t base = T.progs[prog].rule_base, nr = T.progs[prog].nrules;
+    if (nr <= kLdsRuleHits)
+      for (uint32_t i = threadIdx.x; i < nr; i += blockDim.x) {
+        const uint32_t c = s_hits[i];
+        if (c) {
+          atomicAdd(&T.rule_hits[base + i], (unsigned long long)c);
+          s_hits[i] = 0;
+        }
+      }
+  }
 }
 
 // Workgroups take chunks round-robin.  kGlobal = false: chunks of trivial
@@ -297,7 +326,7 @@ __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, ui
 template <bool kGlobal>
 __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
                                             const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                            uint32_t* lcells, uint32_t* s_cnt) {
+                                            uint32_t* lcells, uint32_t* s_cnt, uint32_t* s_hits) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
   const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
   const uint64_t toff = H->tiles_off, arena_bytes = H->arena_bytes;
@@ -338,7 +367,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
     const bool lds = walkp && (pg.flags & kProgRebased) && pg.cell_count <= T.lds_cells;
     if (kGlobal != (walkp && !lds)) continue;  // the other kernel's chunk
     if (prog != cur) {  // uniform across the workgroup: same chunk sequence
-      flush_counts(T, cur, n_allow, n_deny, lane, s_cnt);
+      flush_counts(T, cur, n_allow, n_deny, lane, s_cnt, s_hits);
       if (lds)
         for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
       __syncthreads();
@@ -360,7 +389,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         const uint32_t tile[1] = {t};
         const bool valid[1] = {true};
         http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, ttab, tile, valid, arena, arena_bytes, out, lane,
-                      n_allow, n_deny);
+                      n_allow, n_deny, s_hits);
       }
     } else if (pg.part_count == 1) {
       const HttpPart pt = T.parts[pg.part_begin];
@@ -370,11 +399,11 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         switch (tt.units) {  // wave-uniform
 #define CG_TILE_N(n) \
   case n:            \
-    http_tile_n<n>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny); \
+    http_tile_n<n>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny, s_hits); \
     break;
           CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
           default:
-            http_tile_n<8>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny);
+            http_tile_n<8>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny, s_hits);
 #undef CG_TILE_N
         }
       }
@@ -390,11 +419,11 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
           tile[j] = valid[j] ? t : t0;
         }
         http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, ttab, tile, valid, arena, arena_bytes, out, lane,
-                                  n_allow, n_deny);
+                                  n_allow, n_deny, s_hits);
       }
     }
   }
-  flush_counts(T, cur, n_allow, n_deny, lane, s_cnt);
+  flush_counts(T, cur, n_allow, n_deny, lane, s_cnt, s_hits);
 }
 
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
@@ -402,14 +431,20 @@ __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8,
     uint8_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
   __shared__ uint32_t s_cnt[2];
-  http_chunks<false>(T, batch, nslots, arena, out, lcells, s_cnt);
+  __shared__ uint32_t s_hits[kLdsRuleHits];
+  for (uint32_t i = threadIdx.x; i < kLdsRuleHits; i += blockDim.x) s_hits[i] = 0;
+  if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
+  __syncthreads();
+  http_chunks<false>(T, batch, nslots, arena, out, lcells, s_cnt, s_hits);
 }
 
 __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
                                                                    size_t nslots, const uint8_t* __restrict__ arena,
                                                                    uint8_t* __restrict__ out) {
   __shared__ uint32_t s_cnt[2];
-  http_chunks<true>(T, batch, nslots, arena, out, nullptr, s_cnt);
+  if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
+  __syncthreads();
+  http_chunks<true>(T, batch, nslots, arena, out, nullptr, s_cnt, nullptr);
 }
 
 }  // namespace
@@ -430,7 +465,8 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
     static std::set<int> attr_set;
     std::lock_guard<std::mutex> lk(mu);
     if (attr_set.insert(dev).second)
-      (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64);
+      (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024 - 64 - 4 * kLdsRuleHits);
     auto it = occ_cache.find({dev, lds});
     if (it == occ_cache.end()) {
       // one resident wave of workgroups: as many per CU as LDS and registers

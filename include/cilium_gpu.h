@@ -332,6 +332,29 @@ int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index);
 /* Snapshot statistics: programs, DFA parts, total states, table bytes. */
 int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n);
 
+/* Per-rule hit counters (what = CG_CTR_HTTP_RULES in cg_read_counters): a
+ * request Envoy allows through a rule is counted once, on the FIRST rule
+ * that allows it in Envoy's evaluation order (PolicyInstance::Allowed →
+ * PortNetworkPolicy::Matches: the port's own PortNetworkPolicyRules, then
+ * port 0's, each rule's HttpNetworkPolicyRules in order,
+ * cilium_network_policy.h:90-192).  Counter i counts the rule described by
+ * entry i of cg_http_rule_info_get; a rule of port 0's scope has one counter
+ * per exact-port program it is merged into and one in the wildcard-port
+ * program.  Requests allowed because no HTTP policy applies (no policy for
+ * the port, a port without HTTP rules) are attributed to no rule; denied
+ * requests to none (their per-program denied counter counts them). */
+typedef struct {
+  uint32_t policy;     /* policy index (cg_http_policy_index) */
+  uint32_t ingress;    /* 1 ingress, 0 egress */
+  uint32_t port;       /* the program's destination port; 0 = the wildcard-port program */
+  uint32_t scope;      /* 0: the rule is in this port's PortNetworkPolicy, 1: in port 0's */
+  uint32_t rule;       /* PortNetworkPolicyRule index within its scope */
+  uint32_t http_rule;  /* HttpNetworkPolicyRule index within it, or one of: */
+} cg_http_rule_info;
+#define CG_HTTP_RULE_NO_HTTP 0xFFFFFFFFu     /* the PortNetworkPolicyRule has no HTTP rules */
+#define CG_HTTP_RULE_SCOPE_ALLOW 0xFFFFFFFEu /* port 0 has no HTTP rules: it allows the rest */
+int cg_http_rule_info_get(uint64_t h, cg_http_rule_info* out, size_t cap, size_t* n);
+
 /* Packed request batches.  A record is an 8-byte meta word plus its field
  * string in 16-byte units (at most CG_HTTP_SLOT_BYTES in the record; longer
  * strings go to the overflow arena).  Records are stored tile-transposed in
@@ -452,8 +475,17 @@ int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
 /* ======================================================================== */
 /* what: 0 = HTTP per-program {allowed, denied} u64 pairs,
  *       1 = Kafka per-redirect {allowed, denied} u64 pairs,
- *       2 = prefilter {drop, pass} u64 pair for pf_or_map.
+ *       2 = prefilter {drop, pass} u64 pair for pf_or_map,
+ *       3 = HTTP per-rule first-match hits (cg_http_rule_info_get order),
+ *       4 = the HTTP all-reduce vector: the per-program pairs, the stale-
+ *           batch count, then the per-rule hits (one contiguous device
+ *           buffer, summed across GPUs by RCCL).
  * Writes min(cap, available) u64 values, *n = available. */
+#define CG_CTR_HTTP_PROGRAMS 0u
+#define CG_CTR_KAFKA 1u
+#define CG_CTR_PREFILTER 2u
+#define CG_CTR_HTTP_RULES 3u
+#define CG_CTR_HTTP_ALLREDUCE 4u
 int cg_read_counters(uint64_t h, uint32_t what, uint32_t pf_or_map, uint64_t* out, size_t cap,
                      size_t* n);
 /* Same, into a device buffer (for an RCCL all-reduce across GPUs). */
@@ -478,6 +510,10 @@ int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t 
  * do, to test the compilers without a GPU. */
 int cg_diag_http_eval_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
                            size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out);
+/* The same walk, reporting per request the per-rule hit counter it adds to
+ * (cg_http_rule_info_get index), or UINT32_MAX when no rule allows it. */
+int cg_diag_http_rules_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
+                            size_t n, const uint8_t* arena, size_t arena_len, uint32_t* rule);
 int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
                             const uint32_t* arena, size_t arena_len, uint8_t* out);
 int cg_diag_l4_eval_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, size_t n,

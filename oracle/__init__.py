@@ -38,6 +38,7 @@ def _load():
     lib.or_http_load.argtypes = [C.c_char_p, sz]
     lib.or_http_free.argtypes = [p]
     lib.or_http_eval.argtypes = [p, sz, p, p, p, p, p, p, p, C.c_int]
+    lib.or_http_eval_attr.argtypes = [p, sz, p, p, p, p, p, p, p, p, C.c_int]
     lib.or_regex_match.argtypes = [C.c_char_p, sz, p, sz, C.c_int]
     lib.or_kafka_load.restype = p
     lib.or_kafka_load.argtypes = [C.c_char_p, sz]
@@ -184,6 +185,25 @@ class HttpOracle:
         lib().or_http_eval(self.h, n, _ptr(policy), _ptr(ingress), _ptr(port), _ptr(remote), _ptr(hdr_blob),
                            _ptr(hdr_off), _ptr(out), nthreads)
         return out[:n]
+
+    def eval_attr(self, policy, ingress, port, remote, hdr_blob, hdr_off, nthreads: int = 1):
+        """Verdicts plus, per request, the rule that allowed it in Envoy's
+        evaluation order: (n, 4) u32 {program port, scope, rule, http_rule},
+        program port 0xFFFFFFFF when no rule allowed it (oracle.cc Attr)."""
+        n = len(policy)
+        policy = np.ascontiguousarray(policy, np.uint32)
+        ingress = np.ascontiguousarray(ingress, np.uint8)
+        port = np.ascontiguousarray(port, np.uint16)
+        remote = np.ascontiguousarray(remote, np.uint32)
+        hdr_blob = np.ascontiguousarray(hdr_blob, np.uint8)
+        if len(hdr_blob) == 0:
+            hdr_blob = np.zeros(1, np.uint8)
+        hdr_off = np.ascontiguousarray(hdr_off, np.uint64)
+        out = np.zeros(max(n, 1), np.uint8)
+        attr = np.zeros((max(n, 1), 4), np.uint32)
+        lib().or_http_eval_attr(self.h, n, _ptr(policy), _ptr(ingress), _ptr(port), _ptr(remote), _ptr(hdr_blob),
+                                _ptr(hdr_off), _ptr(out), _ptr(attr), nthreads)
+        return out[:n], attr[:n]
 
 
 def regex_match(re: bytes, s: bytes, search: bool = False) -> int:

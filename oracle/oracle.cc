@@ -387,6 +387,45 @@ struct PortRules {
   }
 };
 
+// Which rule allowed a request, in Envoy's evaluation order: the
+// PortNetworkPolicyRules of the request's port (scope 0), then port 0's
+// (scope 1; scope 0 when the port has no rules of its own and port 0's are
+// the only ones); within them the first PortNetworkPolicyRule that matches
+// and its first matching HttpNetworkPolicyRule (0xFFFFFFFF: it has none;
+// 0xFFFFFFFE: port 0 has no HTTP rules and allows the request).
+// prog_port = 0xFFFFFFFF: allowed or denied without a rule.
+struct Attr {
+  uint32_t prog_port = 0xFFFFFFFFu, scope = 0, rule = 0, http = 0;
+};
+constexpr uint32_t kNoHttp = 0xFFFFFFFFu, kScopeAllow = 0xFFFFFFFEu;
+
+// PortNetworkPolicyRule::Matches, reporting the HTTP rule that matched.
+bool rule_first(const PortRule& r, uint64_t remote, const Headers& h, uint32_t* http) {
+  if (!r.allowed_remotes.empty() && !r.allowed_remotes.count(remote)) return false;
+  if (r.http_rules.empty()) {
+    *http = kNoHttp;
+    return true;
+  }
+  for (uint32_t i = 0; i < r.http_rules.size(); ++i)
+    if (match_headers(h, r.http_rules[i])) {
+      *http = i;
+      return true;
+    }
+  return false;
+}
+
+// PortNetworkPolicyRules::Matches: 0 no match, 1 matched by (rule, http),
+// 2 allowed without HTTP rules.
+int rules_first(const PortRules& rs, uint64_t remote, const Headers& h, uint32_t* rule, uint32_t* http) {
+  if (!rs.have_http_rules || rs.rules.empty()) return 2;
+  for (uint32_t i = 0; i < rs.rules.size(); ++i)
+    if (rule_first(rs.rules[i], remote, h, http)) {
+      *rule = i;
+      return 1;
+    }
+  return 0;
+}
+
 // PortNetworkPolicy (:152-195)
 struct PortPolicy {
   std::unordered_map<uint32_t, PortRules> rules;
@@ -403,6 +442,27 @@ struct PortPolicy {
       found = true;
     }
     return !found;
+  }
+  // matches() with the attribution of the allowing rule (Attr above)
+  bool first(uint32_t port, uint64_t remote, const Headers& h, Attr* a) const {
+    auto ex = rules.find(port);
+    auto wd = rules.find(0);
+    const bool has_ex = ex != rules.end() && port != 0;
+    if (has_ex) {
+      uint32_t r = 0, hh = 0;
+      const int m = rules_first(ex->second, remote, h, &r, &hh);
+      if (m == 1) *a = Attr{port, 0, r, hh};
+      if (m) return true;
+    }
+    if (wd != rules.end()) {
+      uint32_t r = 0, hh = 0;
+      const int m = rules_first(wd->second, remote, h, &r, &hh);
+      const uint32_t pp = has_ex ? port : 0, sc = has_ex ? 1 : 0;
+      if (m == 1) *a = Attr{pp, sc, r, hh};
+      if (m == 2 && has_ex) *a = Attr{pp, sc, 0, kScopeAllow};
+      if (m) return true;
+    }
+    return !has_ex && wd == rules.end();
   }
 };
 
@@ -490,8 +550,10 @@ void or_http_free(void* h) { delete (HttpOracle*)h; }
 
 // NetworkPolicyMap::Allowed (:223-237) per request.  Headers arrive as
 // "name\0value\0..." pairs; names are lower-cased like Envoy's codec does.
-int or_http_eval(void* h, size_t n, const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
-                 const uint32_t* remote, const uint8_t* blob, const uint64_t* off, uint8_t* out, int nthreads) {
+// attr (optional): 4 u32 per request {prog_port, scope, rule, http} (Attr).
+int or_http_eval_attr(void* h, size_t n, const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                      const uint32_t* remote, const uint8_t* blob, const uint64_t* off, uint8_t* out, uint32_t* attr,
+                      int nthreads) {
   const HttpOracle* o = (const HttpOracle*)h;
   std::atomic<int> err{0};
   run_threads(n, nthreads, [&](size_t a, size_t b) {
@@ -520,15 +582,30 @@ int or_http_eval(void* h, size_t n, const uint32_t* policy, const uint8_t* ingre
           const unsigned char c = (unsigned char)ch;
           if ((c < 0x20 && c != 0x09) || c == 0x7F) malformed = true;
         }
+      if (attr) {
+        const Attr none;
+        memcpy(attr + 4 * i, &none, 16);
+      }
       if (policy[i] >= o->policies.size() || malformed) {
         out[i] = 0;  // "No policy found for endpoint" → deny (:232-235)
         continue;
       }
       const PolicyInstance& pi = o->policies[policy[i]];
-      out[i] = pi.dir[ingress[i] ? 1 : 0].matches(port[i], remote[i], hs) ? 1 : 0;
+      if (attr) {
+        Attr a;
+        out[i] = pi.dir[ingress[i] ? 1 : 0].first(port[i], remote[i], hs, &a) ? 1 : 0;
+        memcpy(attr + 4 * i, &a, 16);
+      } else {
+        out[i] = pi.dir[ingress[i] ? 1 : 0].matches(port[i], remote[i], hs) ? 1 : 0;
+      }
     }
   });
   return err;
+}
+
+int or_http_eval(void* h, size_t n, const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                 const uint32_t* remote, const uint8_t* blob, const uint64_t* off, uint8_t* out, int nthreads) {
+  return or_http_eval_attr(h, n, policy, ingress, port, remote, blob, off, out, nullptr, nthreads);
 }
 
 // std::regex_match (ECMAScript) of s against re: 1/0, or -1 if re is invalid.

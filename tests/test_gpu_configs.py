@@ -122,8 +122,8 @@ def test_config3_prefilter_1m_prefixes_1b_addresses(gpu):
     pf.set_endpoints(ep4, ep6)
     o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6, nthreads=16)
     reps = 250
-    d4 = torch.from_numpy(np.ascontiguousarray(v4).view(np.uint8)).cuda().repeat(reps)
-    d6 = torch.from_numpy(np.ascontiguousarray(v6).view(np.uint8)).cuda().repeat(reps)
+    d4 = torch.from_numpy(np.ascontiguousarray(v4).reshape(-1).view(np.uint8)).cuda().repeat(reps)
+    d6 = torch.from_numpy(np.ascontiguousarray(v6).reshape(-1).view(np.uint8)).cuda().repeat(reps)
     n4, n6 = len(v4) * reps, len(v6) * reps
     assert n4 + n6 == 1_000_000_000
     d_o4 = torch.empty(n4, dtype=torch.uint8, device="cuda")
