@@ -1,7 +1,9 @@
 """The N>1 path on CPU: two ranks over gloo (127.0.0.1), each classifying
-its own shard of the 10K-rule workload (per-rank seed as in bench.py),
-then all-reducing the per-program allowed/denied counters — the only
-collective on this path."""
+its own shard of the 10K-rule workload (per-rank seed as in bench.py) with
+the engine's compiled tables (the library's host walker: no GPU here), then
+all-reducing the counter vector — per-program allowed/denied and per-rule
+first-match hits, the only collective on this path — and
+`bench.py --gpus 2` spawning its own ranks (--cpu-rehearsal)."""
 import os
 import socket
 
@@ -49,18 +51,22 @@ def _worker(rank, world, port, q):
         cl.update_http_policy(pols)
         rq = synth.http10k_requests(4096, info, seed=synth.SEED ^ (rank * 7919))  # bench.py's shard seed
         b = cl.pack_http(**rq)
+        # the engine's tables walked on the host (the GPU kernel's walk); the
+        # oracle only checks them
+        slot_v = cl.http_eval_host_diag_slots(b).astype(np.int64)
+        rules = cl.http_rules_host_diag(b)
         exp = oracle.HttpOracle(pols).eval(**rq)
-        slot_v = np.zeros(b.nslots, np.int64)
-        real = b.order != 0xFFFFFFFF
-        slot_v[real] = exp[b.order[real]]
+        assert np.array_equal(cl.http_eval_host_diag(b), exp)
         nprog = cl.http_policy_stats()["programs"]
-        mine = _per_program_counts(cl, b, slot_v, nprog)
+        hits = np.bincount(rules[rules != 0xFFFFFFFF], minlength=len(cl.http_rule_info())).astype(np.int64)
+        mine = np.concatenate([_per_program_counts(cl, b, slot_v, nprog), [0], hits])
         t = torch.from_numpy(mine.copy())
         dist.all_reduce(t)
         gathered = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gathered, torch.from_numpy(mine.copy()))
-        ok = bool(torch.equal(t, sum(gathered))) and int(t.sum()) == 4096 * world
-        q.put((rank, ok, int(t.sum())))
+        ok = bool(torch.equal(t, sum(gathered))) and int(t[:2 * nprog].sum()) == 4096 * world
+        ok = ok and int(t[2 * nprog + 1:].sum()) == int(t[0:2 * nprog:2].sum())  # every allow attributed
+        q.put((rank, ok, int(t[:2 * nprog].sum())))
     finally:
         dist.destroy_process_group()
 
@@ -78,3 +84,23 @@ def test_two_rank_counter_allreduce():
         p.join(60)
     assert all(ok for _, ok, _ in res), res
     assert all(total == 8192 for _, _, total in res)
+
+
+@pytest.mark.timeout(300)
+def test_bench_spawns_two_ranks_cpu_rehearsal():
+    """`bench.py --gpus 2` starts its own two ranks (no launcher), which meet
+    over gloo on 127.0.0.1, all-reduce the counters and print ONE line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu-rehearsal",
+                        "--steps", "2", "--warmup", "1", "--requests-per-gpu", "2048"],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["rehearsal"] is True
+    assert d["allreduced_requests"] == d["expected_requests"] == 2048 * 2 * 2
