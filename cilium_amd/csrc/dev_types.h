@@ -139,14 +139,14 @@ struct HttpProg {
   uint32_t default_remote;  // block offset of the PNPR mask of identities not in the table
   uint32_t cell_begin;      // the program's block in cells[], staged into LDS
   uint32_t cell_count;      // as one piece: parts' comb cells, label tables, masks,
-  uint32_t rtab_off;        // remote-identity table: {u32 identity, u32 mask offset}
-  uint32_t rtab_mask;       // slots, open addressing by hash32(identity)
+  uint32_t rtab_off;        // remote-identity table: 2-choice buckets (rtab_buckets())
+  uint32_t rtab_nb;         // buckets (any count)
   uint32_t rule_base;       // this program's first per-rule hit counter
   uint32_t nrules;          // mask bits = rules (HttpSnapshot::rule_info)
 };
 // Per-rule hit counters a workgroup keeps in LDS for its current program
 // (programs with more rules count straight into global memory).
-constexpr uint32_t kLdsRuleHits = 1024;
+constexpr uint32_t kLdsRuleHits = 512;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; states >= self_lo default to themselves.
@@ -226,6 +226,18 @@ CG_HD inline uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
+// Remote-identity table of a program (staged into LDS with it): buckets of
+// 8 u32 cells — 4 identities, then their 4 mask-row block offsets (kNoRow =
+// empty slot) — and every identity in one of its two buckets, so a lookup
+// reads at most two buckets (2-choice cuckoo, load up to ~90%: no
+// power-of-two padding and no probe chains).  Bucket choices: the two
+// hashes' high bits scaled to [0, nb).
+constexpr uint32_t kRtabBucketCells = 8;
+CG_HD inline uint32_t rtab_b1(uint32_t id, uint32_t nb) { return (uint32_t)(((uint64_t)hash32(id) * nb) >> 32); }
+CG_HD inline uint32_t rtab_b2(uint32_t id, uint32_t nb) {
+  return (uint32_t)(((uint64_t)hash32(id ^ 0x9E3779B9u) * nb) >> 32);
+}
+
 CG_HD inline uint32_t hash64to32(uint64_t k) {
   k = l4_hash1(k);
   return (uint32_t)k;

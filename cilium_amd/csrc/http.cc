@@ -33,6 +33,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <random>
 #include <set>
 #include <unordered_map>
 
@@ -284,8 +285,15 @@ struct VecHash64 {
 struct TooBig {};
 
 // Layered union construction over `rules` (indices into all_rules).
+//
+// A label keeps, per PortNetworkPolicyRule, only its lowest matched rule bit:
+// a remote identity is allowed all of a PNPR's bits or none, so the first
+// rule that allows a request is the lowest bit of (label & row) either way,
+// and states that differ only in a PNPR's later matches stay merged (the
+// union stays as small as with one bit per PNPR).  group[b] = the first bit
+// of b's PNPR.
 ClsDfa build_union(const FieldDfaCache& fc, const std::vector<URule>& all_rules,
-                   const std::vector<int>& rules, int F, uint32_t W,
+                   const std::vector<int>& rules, int F, uint32_t W, const std::vector<uint32_t>& group,
                    std::vector<std::vector<uint64_t>>& label_masks) {
   // global byte classes: SEP alone, refined by every field DFA's columns
   std::vector<int> cls(256, 1);
@@ -328,6 +336,12 @@ ClsDfa build_union(const FieldDfaCache& fc, const std::vector<URule>& all_rules,
     std::vector<uint64_t> m(W, 0);
     for (size_t i = 1; i < st.size(); ++i)
       for (uint32_t t : all_rules[(size_t)(st[i] >> 32)].tags) m[t >> 6] |= 1ULL << (t & 63);
+    uint32_t kept_group = 0xFFFFFFFFu;  // keep the lowest bit of each PNPR group
+    for (uint32_t b = 0; b < 64 * W; ++b) {
+      if (!((m[b >> 6] >> (b & 63)) & 1)) continue;
+      if (group[b] == kept_group) m[b >> 6] &= ~(1ULL << (b & 63));
+      else kept_group = group[b];
+    }
     auto it = mask_ids.emplace(m, (uint32_t)mask_ids.size() + 1);
     if (it.second) label_masks.push_back(m);
     return it.first->second;
@@ -430,12 +444,12 @@ struct PartOut {
 };
 
 void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, std::vector<int> rules,
-                 int F, uint32_t W, std::vector<PartOut>& out) {
+                 int F, uint32_t W, const std::vector<uint32_t>& group, std::vector<PartOut>& out) {
   if (rules.empty()) return;
   PartOut p;
   bool ok = true;
   try {
-    ClsDfa raw = build_union(fc, all_rules, rules, F, W, p.label_masks);
+    ClsDfa raw = build_union(fc, all_rules, rules, F, W, group, p.label_masks);
     p.dfa = minimize_cls(raw);
     std::vector<uint32_t> labels(p.dfa.size(), kCombNoLabel);
     for (int s = 0; s < p.dfa.size(); ++s)
@@ -453,8 +467,8 @@ void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, s
   if (rules.size() == 1) fail(CG_UNSUPPORTED, "a single HTTP rule exceeds the DFA state budget");
   std::vector<int> a(rules.begin(), rules.begin() + rules.size() / 2);
   std::vector<int> b(rules.begin() + rules.size() / 2, rules.end());
-  build_parts(fc, all_rules, a, F, W, out);
-  build_parts(fc, all_rules, b, F, W, out);
+  build_parts(fc, all_rules, a, F, W, group, out);
+  build_parts(fc, all_rules, b, F, W, group, out);
 }
 
 }  // namespace
@@ -599,10 +613,12 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     std::vector<int> idx(urules.size());
     for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
     std::vector<PartOut> parts;
-    build_parts(fc, urules, idx, F, W, parts);
+    std::vector<uint32_t> group(64 * (size_t)W, 0xFFFFFFFEu);
+    for (uint32_t j = 0; j < R; ++j) group[j] = (j && bits[j].pnpr == bits[j - 1].pnpr) ? group[j - 1] : j;
+    build_parts(fc, urules, idx, F, W, group, parts);
     pg.part_begin = (uint32_t)S.parts.size();
     pg.part_count = (uint32_t)parts.size();
-    if (S.cells.size() & 1) S.cells.push_back(kCombEmpty);  // blocks start 8-byte aligned
+    while (S.cells.size() & 3) S.cells.push_back(kCombEmpty);  // blocks start 16-byte aligned
     pg.cell_begin = (uint32_t)S.cells.size();
     size_t block = 0;
     for (const auto& po : parts) block += po.comb.cells.size();
@@ -647,9 +663,9 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     }
     pg.always_off = put_mask(always);
     // remote-identity table (PortNetworkPolicyRule remote sets, :90-97):
-    // open addressing over {u32 identity, u32 block offset of its PNPR
-    // mask} slots, masks deduplicated; unlisted identities get the mask of
-    // the PNPRs without a remote set
+    // identity → block offset of its rule mask row (rows deduplicated;
+    // dev_types.h rtab_b1/rtab_b2 buckets); unlisted identities get the row
+    // of the rules without a remote set
     {
       std::map<std::vector<uint64_t>, uint32_t> rows;
       auto row_of = [&](const std::vector<uint64_t>& m) {
@@ -660,19 +676,55 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       pg.default_remote = row_of(open);
       std::vector<std::pair<uint32_t, uint32_t>> ent;
       for (auto& [rid, m] : by_remote) ent.push_back({rid, row_of(m)});
-      const uint32_t cap = next_pow2(std::max<size_t>((4 * ent.size() + 2) / 3, 8));  // load ≤ 3/4
-      if (S.cells.size() & 1) S.cells.push_back(0);
-      pg.rtab_off = (uint32_t)S.cells.size() - pg.cell_begin;
-      pg.rtab_mask = cap - 1;
-      const size_t at = S.cells.size();
-      S.cells.resize(at + 2 * (size_t)cap, 0);
-      for (size_t i = 0; i < cap; ++i) S.cells[at + 2 * i + 1] = kNoRow;
-      for (auto [rid, off] : ent) {
-        uint32_t h = hash32(rid) & pg.rtab_mask;
-        while (S.cells[at + 2 * h + 1] != kNoRow) h = (h + 1) & pg.rtab_mask;
-        S.cells[at + 2 * h] = rid;
-        S.cells[at + 2 * h + 1] = off;
+      // 2-choice cuckoo placement into the fewest buckets that take it
+      uint32_t nb = (uint32_t)std::max<size_t>((ent.size() * 10 / 9 + 3) / 4, 1);
+      std::vector<std::pair<uint32_t, uint32_t>> slots;  // (identity, row) per slot, row kNoRow = empty
+      for (;; nb += nb / 8 + 1) {
+        slots.assign((size_t)nb * 4, {0u, kNoRow});
+        std::mt19937 rng(0xC111A);
+        auto put = [&](uint32_t bk, const std::pair<uint32_t, uint32_t>& e) {
+          for (int sl = 0; sl < 4; ++sl)
+            if (slots[(size_t)bk * 4 + sl].second == kNoRow) {
+              slots[(size_t)bk * 4 + sl] = e;
+              return true;
+            }
+          return false;
+        };
+        bool ok = true;
+        for (const auto& e : ent) {
+          auto cur = e;
+          uint32_t from = 0xFFFFFFFFu;
+          bool placed = false;
+          for (int kick = 0; kick < 500 && !placed; ++kick) {
+            const uint32_t c1 = rtab_b1(cur.first, nb), c2 = rtab_b2(cur.first, nb);
+            if (put(c1, cur) || put(c2, cur)) {
+              placed = true;
+              break;
+            }
+            // evict from the bucket the current entry did not come from
+            const uint32_t vb = c1 == from ? c2 : c2 == from ? c1 : (rng() & 1) ? c1 : c2;
+            std::swap(cur, slots[(size_t)vb * 4 + (rng() & 3)]);
+            from = vb;
+          }
+          if (!placed) {
+            ok = false;
+            break;
+          }
+        }
+        if (ok) break;
       }
+      while ((S.cells.size() - pg.cell_begin) & 3) S.cells.push_back(0);  // buckets 16-byte aligned
+
+      pg.rtab_off = (uint32_t)S.cells.size() - pg.cell_begin;
+      pg.rtab_nb = nb;
+      const size_t at = S.cells.size();
+      S.cells.resize(at + kRtabBucketCells * (size_t)nb, 0);
+      for (uint32_t k = 0; k < nb; ++k)
+        for (int sl = 0; sl < 4; ++sl) {
+          S.cells[at + kRtabBucketCells * k + sl] = slots[(size_t)k * 4 + sl].first;
+          S.cells[at + kRtabBucketCells * k + 4 + sl] = slots[(size_t)k * 4 + sl].second;
+        }
+      const uint32_t cap = 4 * nb;
       S.total_remote_slots += cap;
     }
     S.cells.push_back(0);  // spare words: the kernel reads two mask words whatever the width

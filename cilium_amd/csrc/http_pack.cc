@@ -325,14 +325,11 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
       const uint32_t* blk = s.cells.data() + pg.cell_begin;
       auto bmask = [&](uint32_t o, uint32_t w) { return (uint64_t)blk[o + 2 * w] | (uint64_t)blk[o + 2 * w + 1] << 32; };
       uint32_t roff = pg.default_remote;
-      for (uint32_t h = hash32(remote) & pg.rtab_mask;; h = (h + 1) & pg.rtab_mask) {
-        const uint32_t key = blk[pg.rtab_off + 2 * h], row = blk[pg.rtab_off + 2 * h + 1];
-        if (row == kNoRow) break;
-        if (key == remote) {
-          roff = row;
-          break;
+      for (uint32_t bk : {rtab_b1(remote, pg.rtab_nb), rtab_b2(remote, pg.rtab_nb)})
+        for (uint32_t sl = 0; sl < 4; ++sl) {
+          const uint32_t* b = blk + pg.rtab_off + kRtabBucketCells * bk;
+          if (b[sl] == remote && b[4 + sl] != kNoRow) roff = b[4 + sl];
         }
-      }
       // first rule (lowest bit) the mask at block offset a shares with the row
       uint32_t hit = 0xFFFFFFFFu;
       auto first = [&](uint32_t a) {

@@ -13,6 +13,8 @@
 // the current tile walks, and units within a tile load two ahead.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <set>
@@ -100,14 +102,23 @@ __device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ c
 // Block offset of the PNPR mask of remote identity `remote`: the program's
 // remote table (open addressing, {identity, mask offset} slots).
 __device__ __forceinline__ uint32_t remote_row(const uint32_t* __restrict__ blk, const HttpProg& pg, uint32_t remote) {
-  uint32_t h = hash32(remote) & pg.rtab_mask;
-  for (uint32_t probe = 0; probe <= pg.rtab_mask; ++probe) {
-    const uint2 slot = *reinterpret_cast<const uint2*>(blk + pg.rtab_off + 2 * h);
-    if (slot.y == kNoRow) break;
-    if (slot.x == remote) return slot.y;
-    h = (h + 1) & pg.rtab_mask;
-  }
-  return pg.default_remote;
+  // both candidate buckets read together (dev_types.h rtab_b1/rtab_b2)
+  const uint32_t* b1 = blk + pg.rtab_off + kRtabBucketCells * rtab_b1(remote, pg.rtab_nb);
+  const uint32_t* b2 = blk + pg.rtab_off + kRtabBucketCells * rtab_b2(remote, pg.rtab_nb);
+  const uint4 k1 = *reinterpret_cast<const uint4*>(b1), k2 = *reinterpret_cast<const uint4*>(b2);
+  const uint4 r1 = *reinterpret_cast<const uint4*>(b1 + 4), r2 = *reinterpret_cast<const uint4*>(b2 + 4);
+  uint32_t row = pg.default_remote;
+  // an empty slot (row kNoRow) never matches: its identity word is 0 and
+  // its row is skipped
+  row = (k1.x == remote && r1.x != kNoRow) ? r1.x : row;
+  row = (k1.y == remote && r1.y != kNoRow) ? r1.y : row;
+  row = (k1.z == remote && r1.z != kNoRow) ? r1.z : row;
+  row = (k1.w == remote && r1.w != kNoRow) ? r1.w : row;
+  row = (k2.x == remote && r2.x != kNoRow) ? r2.x : row;
+  row = (k2.y == remote && r2.y != kNoRow) ? r2.y : row;
+  row = (k2.z == remote && r2.z != kNoRow) ? r2.z : row;
+  row = (k2.w == remote && r2.w != kNoRow) ? r2.w : row;
+  return row;
 }
 
 // u64 word w of the block mask at block offset a (u32 units, 8-byte aligned).
@@ -128,11 +139,22 @@ __device__ __forceinline__ uint32_t first_meet(const uint32_t* __restrict__ blk,
   return kNoHit;
 }
 
-// One first-match hit of rule `hit` of program pg: into the workgroup's LDS
-// counters when the program's rules fit them, else into global memory.
-__device__ __forceinline__ void count_hit(const HttpDev& T, const HttpProg& pg, uint32_t hit, uint32_t* s_hits) {
-  if (s_hits && pg.nrules <= kLdsRuleHits) atomicAdd(&s_hits[hit], 1u);
-  else atomicAdd(&T.rule_hits[pg.rule_base + hit], 1ULL);
+// The first-match hits of a wave's 64 requests (hit = rule bit, or kNoHit),
+// called by the whole wave: lanes hold requests in the packer's string order,
+// so equal hits come in runs; each run's first lane adds the run length —
+// into the workgroup's LDS counters when the program's rules fit them, else
+// into global memory.  One atomic per run instead of 64 same-address ones.
+__device__ __forceinline__ void count_hits(const HttpDev& T, const HttpProg& pg, uint32_t hit, uint32_t* s_hits,
+                                           uint32_t lane) {
+  const uint32_t prev = __shfl_up(hit, 1, kWave);
+  const bool head = lane == 0 || prev != hit;
+  const unsigned long long heads = __ballot(head);
+  if (head && hit != kNoHit) {
+    const unsigned long long later = heads & ~((2ULL << lane) - 1);  // heads of the runs after this one
+    const uint32_t len = (later ? (uint32_t)__builtin_ctzll(later) : 64u) - lane;
+    if (s_hits && pg.nrules <= kLdsRuleHits) atomicAdd(&s_hits[hit], len);
+    else atomicAdd(&T.rule_hits[pg.rule_base + hit], (unsigned long long)len);
+  }
 }
 
 // K tiles of a program (tile j takes part only if valid[j]): walk every
@@ -223,7 +245,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   for (int j = 0; j < K; ++j) {
     if (counted[j] && (pg.flags & kProgHasAlways)) hit[j] = min(hit[j], first_meet(blk, pg.always_off, row[j], W));
     const bool verdict = counted[j] && hit[j] != kNoHit;
-    if (verdict) count_hit(T, pg, hit[j], s_hits);
+    count_hits(T, pg, verdict ? hit[j] : kNoHit, s_hits, lane);
     if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict;
     n_allow += counted[j] && verdict;
     n_deny += counted[j] && !verdict;
@@ -275,7 +297,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
     }
   }
   const bool verdict = hit != kNoHit;
-  if (verdict) count_hit(T, pg, hit, s_hits);
+  count_hits(T, pg, hit, s_hits, lane);
   out[(size_t)t * kWave + lane] = (uint8_t)verdict;
   n_allow += counted && verdict;
   n_deny += counted && !verdict;
@@ -478,6 +500,9 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
           nb < 1)
         nb = 1;
       it = occ_cache.emplace(std::make_pair(dev, lds), nb).first;
+      if (getenv("CILIUM_GPU_DEBUG"))
+        fprintf(stderr, "[cilium-gpu] http_kernel: device %d, %zu B dynamic LDS, %d workgroups per CU\n", dev, lds,
+                nb);
     }
     occ = it->second;
   }
