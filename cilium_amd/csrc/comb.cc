@@ -50,6 +50,12 @@ bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable*
     std::stable_sort(order.begin(), order.end(),
                      [&](int a, int b) { return rows[a].exc.size() > rows[b].exc.size(); });
     uint32_t lo_hint = group == 0 ? 1 : self_lo;
+    if (group == 1) {  // the dead state first: the lowest self-default base
+      while (lo_hint <= max_base && used[lo_hint - 1]) ++lo_hint;
+      if (lo_hint > max_base) return false;
+      base[0] = lo_hint;
+      used[lo_hint - 1] = 1;
+    }
     for (int s : order) {
       const Row& r = rows[s];
       while (lo_hint < cap && used[lo_hint - 1]) ++lo_hint;
@@ -73,9 +79,10 @@ bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable*
     }
   }
   uint32_t ncells = 257;
-  for (int s = 1; s < n; ++s) ncells = std::max(ncells, base[s] + 256);
+  for (int s = 0; s < n; ++s) ncells = std::max(ncells, base[s] + 256);
   out->cells.assign(ncells, kCombEmpty);
   out->state_enc = base;
+  out->cells[base[0] - 1] = 0xFFFFu | (kCombNoLabel << 16);  // D: no label, no exceptions
   for (int s = 1; s < n; ++s) {
     const uint32_t b0 = base[s];
     out->cells[b0 - 1] = 0xFFFFu | ((labels[s] & 0xFFFFu) << 16);
@@ -84,8 +91,8 @@ bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable*
       out->cells[b0 + x] = b0 | (base[t] << 16);
     }
   }
-  out->start = n > 1 ? base[1] : 0;
-  out->self_lo = self_lo;
+  out->start = n > 1 ? base[1] : base[0];
+  out->dead = base[0];
   out->exceptions = excs;
   return true;
 }
@@ -97,10 +104,9 @@ void rebase_comb(CombTable* t, uint32_t off) {
     const uint32_t next = c >> 16;
     c = ((c & 0xFFFF) + off) | ((next ? next + off : 0) << 16);
   }
-  for (uint32_t& s : t->state_enc)
-    if (s) s += off;
-  if (t->start) t->start += off;
-  t->self_lo += off;
+  for (uint32_t& s : t->state_enc) s += off;
+  t->start += off;
+  t->dead += off;
 }
 
 }  // namespace cg

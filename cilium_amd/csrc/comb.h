@@ -7,21 +7,23 @@
 // dead or itself — and only its exception bytes are stored, packed first-fit
 // into one array of 32-bit cells indexed by byte value (row displacement,
 // Tarjan–Yao), so the kernel needs no byte-class lookup.  A state IS its base
-// (a 16-bit cell index); rows whose default is the state itself get the
-// bases at or above a per-table threshold `self_lo`:
+// (a 16-bit cell index).  The dead state D is a row of its own with no
+// exceptions, at the lowest base of the rows whose default is the state
+// itself; every row defaulting to dead sits below it:
 //
 //   cell[S + b]  = S | next(S, b) << 16      when b is an exception of S
 //   cell[S - 1]  = 0xFFFF | label << 16      (header; 0xFFFF is never a base;
 //                                             label = accept-set index or 0xFFFF)
 //
-//   next(S, b) = cell[S+b].lo == S ? cell[S+b].hi : (S >= self_lo ? S : 0)
+//   next(S, b) = cell[S+b].lo == S ? cell[S+b].hi : max(S, D)
 //
-// The dead state is S = 0 (base 0 is never given to a state, so no check
-// half-word is ever 0).  Accepting states are made absorbing (self, no
-// exceptions): the request strings these tables read end with the last
-// field's separator, after which every accepting row is dead anyway, so the
-// kernel may keep stepping through the zero padding of a record without
-// checking the string length per byte.
+// so the default costs one v_max_u32 per step (a dead-default row has S < D,
+// a self row S > D, and D defaults to itself).  Base 0 is never given to a
+// state, so no check half-word is ever 0.  Accepting states are made
+// absorbing (self, no exceptions): the request strings these tables read end
+// with the last field's separator, after which every accepting row is dead
+// anyway, so the kernel may keep stepping through the zero padding of a
+// record without checking the string length per byte.
 //
 // Bases are table-local; `rebase_comb` shifts them by the table's offset
 // inside a program's cell block so that all parts of a program share one
@@ -41,9 +43,9 @@ constexpr uint32_t kCombNoLabel = 0xFFFF;
 
 struct CombTable {
   std::vector<uint32_t> cells;
-  std::vector<uint32_t> state_enc;  // base of each DFA state (0 for dead)
+  std::vector<uint32_t> state_enc;  // base of each DFA state (state 0 = dead: D)
   uint32_t start = 0;
-  uint32_t self_lo = 0;             // states >= self_lo default to themselves
+  uint32_t dead = 0;                // the dead state; states >= dead default to themselves
   uint64_t exceptions = 0;
 };
 
@@ -56,12 +58,12 @@ bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable*
 // Shift every base of `t` by `off` (its position inside a program block).
 void rebase_comb(CombTable* t, uint32_t off);
 
-inline uint32_t comb_next(const uint32_t* cells, uint32_t self_lo, uint32_t s, uint32_t b) {
+inline uint32_t comb_next(const uint32_t* cells, uint32_t dead, uint32_t s, uint32_t b) {
   const uint32_t e = cells[s + b];
   if ((e & 0xFFFF) == s) return e >> 16;
-  return s >= self_lo ? s : 0;
+  return s > dead ? s : dead;
 }
 
-inline uint32_t comb_label(const uint32_t* cells, uint32_t s) { return s ? cells[s - 1] >> 16 : kCombNoLabel; }
+inline uint32_t comb_label(const uint32_t* cells, uint32_t s) { return cells[s - 1] >> 16; }
 
 }  // namespace cg

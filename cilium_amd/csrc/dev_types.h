@@ -149,7 +149,8 @@ struct HttpProg {
 constexpr uint32_t kLdsRuleHits = 512;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
-// cell index relative to `walk_off`; states >= self_lo default to themselves.
+// cell index relative to `walk_off`; `dead` is the dead state, states above it
+// default to themselves and states below it to `dead` (comb.h).
 // An accepting state's header cell holds its accept label; the label's PNPR
 // mask (u64 words stored as u32 pairs, 8-byte aligned) is at block offset
 // acc_off + label * 2 * mask_words, block = cells + cell_begin.  When a program's DFA
@@ -163,7 +164,7 @@ struct HttpPart {
   uint32_t acc_off;   // block offset of accept label 0's PNPR mask (label l: + l * 2 * mask_words)
   uint32_t start;     // start state
   uint32_t nstates;
-  uint32_t self_lo;
+  uint32_t dead;
   uint32_t walk_off;  // cells[] offset the states are relative to
   uint32_t pad;
 };
@@ -230,13 +231,13 @@ CG_HD inline uint32_t hash32(uint32_t x) {
 // 8 u32 cells — 4 identities, then their 4 mask-row block offsets (kNoRow =
 // empty slot) — and every identity in one of its two buckets, so a lookup
 // reads at most two buckets (2-choice cuckoo, load up to ~90%: no
-// power-of-two padding and no probe chains).  Bucket choices: the two
-// hashes' high bits scaled to [0, nb).
+// power-of-two padding and no probe chains).  Bucket choices: one hash,
+// scaled to [0, nb) directly and after a second odd multiplier.
 constexpr uint32_t kRtabBucketCells = 8;
-CG_HD inline uint32_t rtab_b1(uint32_t id, uint32_t nb) { return (uint32_t)(((uint64_t)hash32(id) * nb) >> 32); }
-CG_HD inline uint32_t rtab_b2(uint32_t id, uint32_t nb) {
-  return (uint32_t)(((uint64_t)hash32(id ^ 0x9E3779B9u) * nb) >> 32);
-}
+CG_HD inline uint32_t rtab_b1h(uint32_t h, uint32_t nb) { return (uint32_t)(((uint64_t)h * nb) >> 32); }
+CG_HD inline uint32_t rtab_b2h(uint32_t h, uint32_t nb) { return (uint32_t)(((uint64_t)(h * 0x85EBCA77u) * nb) >> 32); }
+CG_HD inline uint32_t rtab_b1(uint32_t id, uint32_t nb) { return rtab_b1h(hash32(id), nb); }
+CG_HD inline uint32_t rtab_b2(uint32_t id, uint32_t nb) { return rtab_b2h(hash32(id), nb); }
 
 CG_HD inline uint32_t hash64to32(uint64_t k) {
   k = l4_hash1(k);

@@ -633,7 +633,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       hp.walk_off = rebase ? pg.cell_begin : hp.cell_off;
       hp.nstates = (uint32_t)d.size();
       hp.start = cb.start;
-      hp.self_lo = cb.self_lo;
+      hp.dead = cb.dead;
       hp.ncells = (uint32_t)cb.cells.size();
       S.cells.insert(S.cells.end(), cb.cells.begin(), cb.cells.end());
       S.total_states += d.size();

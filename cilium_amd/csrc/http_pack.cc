@@ -343,8 +343,8 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         const uint32_t* cells = s.cells.data() + pt.walk_off;
         uint32_t st = pt.start;
         for (unsigned char ch : str) {
-          st = comb_next(cells, pt.self_lo, st, ch);
-          if (!st) break;
+          st = comb_next(cells, pt.dead, st, ch);
+          if (st == pt.dead) break;
         }
         const uint32_t lab = comb_label(cells, st);
         if (lab == kCombNoLabel) continue;

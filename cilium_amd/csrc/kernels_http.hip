@@ -38,15 +38,16 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
 }
 
 // One comb transition (comb.h), branch-free: every lane reads the table and
-// selects.  A dead lane (S = 0) reads cells[b], whose check half is never 0.
+// selects; the miss target max(S, dead) is one VALU (the walk is VALU-issue
+// bound: each wave64 instruction holds the SIMD for 4 cycles).
 // The walk is VALU-issue bound (PMC: ~60% of SIMD cycles issue VALU), so the
 // select uses SDWA word selects: compare the check half and pick the next
 // half in two instructions.  It goes through VCC, which serializes several
 // chains per lane — one chain per lane (kTilesPerWave = 1) measured fastest.
-__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+__device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st,
                                              uint32_t b) {
   const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + ((st << 2) + (b << 2)));
-  const uint32_t dflt = st >= self_lo ? st : 0u;
+  const uint32_t dflt = max(st, dead);
   // nx = e.lo == st ? e.hi : dflt
   uint32_t nx;
   asm("v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
@@ -59,9 +60,9 @@ __device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells
 }
 
 // Records longer than a slot live in the overflow arena: byte loop.
-__device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+__device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st,
                                               const uint8_t* __restrict__ arena, uint32_t aoff, uint32_t len) {
-  for (uint32_t p = 0; p < len && st != 0; ++p) st = comb_step(cells, self_lo, st, arena[aoff + p]);
+  for (uint32_t p = 0; p < len && st != dead; ++p) st = comb_step(cells, dead, st, arena[aoff + p]);
   return st;
 }
 
@@ -88,23 +89,24 @@ __device__ __forceinline__ uint4 tile_unit(const TileRef& tr, uint32_t units, ui
 // The overflow string of a lane whose meta word is m (arena entry: u32 length,
 // bytes).  An entry reaching past the batch's arena (arena_bytes, from its
 // header) ends in the dead state: the request is denied.
-__device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ cells, uint32_t self_lo, uint32_t st,
+__device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st,
                                                  const uint8_t* __restrict__ arena, uint64_t arena_bytes, uint2 m,
                                                  bool ov) {
   if (!ov) return st;
   const uint64_t aoff = (uint64_t)(m.y & 0xFFFFFFu) * 16u;
-  if (aoff + 4 > arena_bytes) return 0;
+  if (aoff + 4 > arena_bytes) return dead;
   const uint32_t len = *reinterpret_cast<const uint32_t*>(arena + aoff);
-  if (aoff + 4 + len > arena_bytes) return 0;
-  return walk_arena(cells, self_lo, st, arena, (uint32_t)aoff + 4, len);
+  if (aoff + 4 + len > arena_bytes) return dead;
+  return walk_arena(cells, dead, st, arena, (uint32_t)aoff + 4, len);
 }
 
 // Block offset of the PNPR mask of remote identity `remote`: the program's
 // remote table (open addressing, {identity, mask offset} slots).
 __device__ __forceinline__ uint32_t remote_row(const uint32_t* __restrict__ blk, const HttpProg& pg, uint32_t remote) {
   // both candidate buckets read together (dev_types.h rtab_b1/rtab_b2)
-  const uint32_t* b1 = blk + pg.rtab_off + kRtabBucketCells * rtab_b1(remote, pg.rtab_nb);
-  const uint32_t* b2 = blk + pg.rtab_off + kRtabBucketCells * rtab_b2(remote, pg.rtab_nb);
+  const uint32_t h = hash32(remote);
+  const uint32_t* b1 = blk + pg.rtab_off + kRtabBucketCells * rtab_b1h(h, pg.rtab_nb);
+  const uint32_t* b2 = blk + pg.rtab_off + kRtabBucketCells * rtab_b2h(h, pg.rtab_nb);
   const uint4 k1 = *reinterpret_cast<const uint4*>(b1), k2 = *reinterpret_cast<const uint4*>(b2);
   const uint4 r1 = *reinterpret_cast<const uint4*>(b1 + 4), r2 = *reinterpret_cast<const uint4*>(b2 + 4);
   uint32_t row = pg.default_remote;
@@ -218,11 +220,11 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
 #pragma unroll
-          for (int j = 0; j < K; ++j) st[j] = comb_step(cells, pt.self_lo, st[j], get_byte(cur[j], k));
+          for (int j = 0; j < K; ++j) st[j] = comb_step(cells, pt.dead, st[j], get_byte(cur[j], k));
         }
         bool alive = false;
 #pragma unroll
-        for (int j = 0; j < K; ++j) alive |= st[j] != 0;
+        for (int j = 0; j < K; ++j) alive |= st[j] != pt.dead;
         if (!more || !__any(alive)) break;
 #pragma unroll
         for (int j = 0; j < K; ++j) cur[j] = nxt[j];
@@ -231,13 +233,13 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     if (any_overflow) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const uint32_t sa = walk_overflow(cells, pt.self_lo, pt.start, arena, arena_bytes, meta[j], overflow[j]);
+        const uint32_t sa = walk_overflow(cells, pt.dead, pt.start, arena, arena_bytes, meta[j], overflow[j]);
         if (overflow[j]) st[j] = sa;
       }
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t lab = counted[j] && st[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
+      const uint32_t lab = counted[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
       if (lab != 0xFFFFu) hit[j] = min(hit[j], first_meet(blk, pt.acc_off + lab * 2 * W, row[j], W));
     }
   }
@@ -252,43 +254,61 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   }
 }
 
+// The first string units of a wave's NEXT tile (and its meta block), loaded
+// while the current tile walks: the walk is VALU-bound and a tile's loads
+// would otherwise be waited for at its start, so each wave keeps the next
+// tile's head in flight under the current walk.  kPre units (4 VGPRs each)
+// bound the registers this costs at 8 waves per SIMD.
+constexpr int kPre = 1;
+struct TilePre {
+  uint2 meta;
+  uint4 u[kPre];
+};
+__device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units, uint32_t lane, TilePre& p) {
+  p.meta = tr.meta[lane];
+#pragma unroll
+  for (int k = 0; k < kPre; ++k) p.u[k] = tile_unit(tr, units, k + 1, lane);  // stays inside the tile
+}
+
 // One tile of a one-part program whose block `blk` is in LDS, its string
-// units count N known up front (tile table): straight-line code.  Every load
-// of the tile issues at its start — meta, then the N string units — so the
-// tile pays one memory latency, which the SIMD's other waves cover; the
-// remote-identity lookup reads the LDS block after the walk, only for lanes
-// that reached an accepting state.  No early exit: lanes
-// whose string ended (or died) keep stepping through zero padding or the
-// dead state, which cannot change their verdict.
+// units count N known up front (tile table): straight-line code.  The tile's
+// meta and first kPre units arrive prefetched (cur); the rest load at its
+// start, then the next tile's head is issued (has_next) — so a wave pays a
+// memory latency only for a tile's later units, which the walk of its first
+// ones covers.  The remote-identity lookup reads the LDS block after the
+// walk, only for lanes that reached an accepting state.  No early exit:
+// lanes whose string ended (or died) keep stepping through zero padding or
+// the dead state, which cannot change their verdict.
 template <int N>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
-                                            uint32_t prog, const uint32_t* __restrict__ blk,
-                                            const TileRef tr, uint32_t t,
-                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                            uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
-                                            uint32_t& n_deny, uint32_t* s_hits) {
-  const uint2 meta = tr.meta[lane];
+                                            uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
+                                            const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
+                                            TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
+                                            uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane,
+                                            uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits) {
+  const uint2 meta = cur.meta;
   uint4 unit[N > 0 ? N : 1];
 #pragma unroll
-  for (int k = 0; k < N; ++k) unit[k] = tr.units[k * kWave + lane];
+  for (int k = 0; k < N; ++k) unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : tr.units[k * kWave + lane];
+  if (has_next) tile_prefetch(trn, nunits, lane, nxt);
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t flags = meta.y >> 24;
   const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
   const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
-  const uint32_t self_lo = pt.self_lo;
+  const uint32_t dead = pt.dead;
   uint32_t st = pt.start;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) st = comb_step(blk, self_lo, st, get_byte(unit[k], i));
+    for (int i = 0; i < 16; ++i) st = comb_step(blk, dead, st, get_byte(unit[k], i));
   }
   if (__any(overflow)) {
-    const uint32_t sa = walk_overflow(blk, self_lo, pt.start, arena, arena_bytes, meta, overflow);
+    const uint32_t sa = walk_overflow(blk, dead, pt.start, arena, arena_bytes, meta, overflow);
     if (overflow) st = sa;
   }
   uint32_t hit = kNoHit;
   if (counted) {
-    const uint32_t lab = st ? (blk[st - 1] >> 16) : 0xFFFFu;
+    const uint32_t lab = blk[st - 1] >> 16;
     const bool always = pg.flags & kProgHasAlways;
     if (lab != 0xFFFFu || always) {
       const uint32_t row = remote_row(blk, pg, meta.x);
@@ -415,18 +435,32 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       }
     } else if (pg.part_count == 1) {
       const HttpPart pt = T.parts[pg.part_begin];
-      for (uint32_t t = ch.first_tile + wave; t < tend; t += nw) {
-        const HttpTile tt = ttab[t];
-        const TileRef tb = tile_ref(tiles, tt);
-        switch (tt.units) {  // wave-uniform
-#define CG_TILE_N(n) \
-  case n:            \
-    http_tile_n<n>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny, s_hits); \
+      uint32_t t = ch.first_tile + wave;
+      if (t < tend) {
+        HttpTile tt = ttab[t];
+        TileRef tb = tile_ref(tiles, tt);
+        TilePre pre;
+        tile_prefetch(tb, tt.units, lane, pre);
+        for (; t < tend; t += nw) {
+          const bool has_next = t + nw < tend;
+          const HttpTile ttn = ttab[has_next ? t + nw : t];
+          const TileRef tbn = tile_ref(tiles, ttn);
+          TilePre nxt = pre;
+          switch (tt.units) {  // wave-uniform
+#define CG_TILE_N(n)                                                                                                 \
+  case n:                                                                                                            \
+    http_tile_n<n>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes, out, lane, \
+                   n_allow, n_deny, s_hits);                                                                         \
     break;
-          CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
-          default:
-            http_tile_n<8>(T, pg, pt, prog, lcells, tb, t, arena, arena_bytes, out, lane, n_allow, n_deny, s_hits);
+            CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
+            default:
+              http_tile_n<8>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes,
+                             out, lane, n_allow, n_deny, s_hits);
 #undef CG_TILE_N
+          }
+          tt = ttn;
+          tb = tbn;
+          pre = nxt;
         }
       }
     } else {

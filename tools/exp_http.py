@@ -43,6 +43,8 @@ VARIANTS = {
                   "          urules[it->second].tags.push_back(pnpr_first[j]);")],
     "hotdata": [("        const TileRef tb = tile_ref(tiles, tt);",
                  "        const TileRef tb = tile_ref(tiles, ttab[ch.first_tile]);")],
+    "pre1": [("constexpr int kPre = 2;", "constexpr int kPre = 1;")],
+    "pre3": [("constexpr int kPre = 2;", "constexpr int kPre = 3;")],
     "deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
     "deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
 }
