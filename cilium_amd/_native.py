@@ -52,6 +52,9 @@ CG_HTTP_UNITS = 9
 CG_KAFKA_MAX_TOPICS = 12
 CG_KAFKA_K_NIL, CG_KAFKA_K_TYPED, CG_KAFKA_K_CONSUMER_METADATA = 0, 1, 2
 CG_KAFKA_UNKNOWN_STR = 0xFFFFFFFF
+CG_KAFKA_TOPICS_IN_ARENA = 255
+CG_KAFKA_DECODE_OK, CG_KAFKA_DECODE_ERROR = 0, 1
+CG_KAFKA_V_DENY, CG_KAFKA_V_ALLOW, CG_KAFKA_V_CLOSE = 0, 1, 2
 
 
 class CiliumGPUError(RuntimeError):
@@ -135,6 +138,10 @@ SIGNATURES = {
     "cg_kafka_intern": (C.c_int, [_u64, _u32, C.c_char_p, _sz, C.POINTER(_u32)]),
     "cg_kafka_verdicts_dev": (C.c_int, [_u64, _p, _sz, _p, _p, _p]),
     "cg_kafka_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
+    "cg_kafka_decode_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _sz, C.POINTER(_sz), _p]),
+    "cg_kafka_decode_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _sz, C.POINTER(_sz), _p, _p]),
+    "cg_kafka_verdicts_raw_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p]),
+    "cg_diag_kafka_decode_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _sz, C.POINTER(_sz), _p]),
     "cg_read_counters": (C.c_int, [_u64, _u32, _u32, _p, _sz, C.POINTER(_sz)]),
     "cg_counters_device_ptr": (C.c_int, [_u64, _u32, _u32, C.POINTER(_p), C.POINTER(_sz)]),
     "cg_counters_copy_dev": (C.c_int, [_u64, _u32, _u32, _p, _sz, _p]),

@@ -19,8 +19,8 @@ BUILD = HERE / "_build"
 LIB = HERE / "libciliumgpu.so"
 ARCH = "gfx950"
 
-SOURCES = ["runtime.cc", "regex.cc", "clsdfa.cc", "comb.cc", "http.cc", "l4.cc", "lpm.cc", "ipcache.cc", "kafka.cc", "http_pack.cc", "capi.cc", "proxylib_shim.cc", "http_parse.cc",
-           "kernels.hip", "kernels_http.hip", "kernels_ipcache.hip"]
+SOURCES = ["runtime.cc", "regex.cc", "clsdfa.cc", "comb.cc", "http.cc", "l4.cc", "lpm.cc", "ipcache.cc", "kafka.cc", "http_pack.cc", "capi.cc", "proxylib_shim.cc", "http_parse.cc", "kafka_wire.cc",
+           "kernels.hip", "kernels_http.hip", "kernels_ipcache.hip", "kernels_kafka.hip"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -58,7 +58,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(LIB),
-               "-lpthread"]
+               "-lpthread", "-lz"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

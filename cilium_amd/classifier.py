@@ -278,15 +278,62 @@ class Classifier:
                 if t not in cache_t:
                     cache_t[t] = self.kafka_intern("topic", t)
                 ids.append(cache_t[t])
-            if len(ids) > 255:
-                raise ValueError("more than 255 topics in one request")
-            reqs["n_topics"][i] = len(ids)
+            reqs["n_topics"][i] = min(len(ids), N.CG_KAFKA_TOPICS_IN_ARENA)
             if len(ids) <= N.CG_KAFKA_MAX_TOPICS:
                 reqs["topic_ids"][i, :len(ids)] = ids
             else:
                 reqs["topic_ids"][i, 0] = len(arena)
+                if len(ids) >= N.CG_KAFKA_TOPICS_IN_ARENA:
+                    reqs["topic_ids"][i, 1] = len(ids)
                 arena.extend(ids)
         return reqs, np.asarray(arena if arena else [0], np.uint32)
+
+    def kafka_decode(self, raw, raw_off, redirect, remote, diag_cpu: bool = False):
+        """ReadRequest on the wire bytes of n requests (request i is
+        raw[raw_off[i]:raw_off[i+1]]) on the GPU → (records, arena, status);
+        diag_cpu=True runs the host decoder instead (cross-checks only)."""
+        raw = np.ascontiguousarray(raw, np.uint8)
+        off = np.ascontiguousarray(raw_off, np.uint64)
+        n = len(off) - 1
+        red = np.ascontiguousarray(redirect, np.uint16)
+        rem = np.ascontiguousarray(remote, np.uint32)
+        if len(red) != n or len(rem) != n:
+            raise ValueError("redirect/remote must have one entry per request")
+        reqs = np.zeros(max(n, 1), KAFKA_REQ_DTYPE)
+        status = np.zeros(max(n, 1), np.uint8)
+        fn = N.lib.cg_diag_kafka_decode_host if diag_cpu else N.lib.cg_kafka_decode_host
+        cap = 64
+        while True:
+            arena = np.zeros(cap, np.uint32)
+            used = C.c_size_t()
+            rc = fn(self.h, _p(raw), _p(off), n, _p(red), _p(rem), _p(reqs), _p(arena), cap, C.byref(used),
+                    _p(status))
+            if rc == N.CG_MAP_FULL and used.value > cap:
+                cap = used.value
+                continue
+            N.check(rc)
+            return reqs[:n], arena[:max(used.value, 1)], status[:n]
+
+    def kafka_decode_dev(self, d_raw, d_off, n: int, d_redirect, d_remote, d_reqs, d_arena, arena_cap: int,
+                         d_status, stream=None) -> int:
+        """cg_kafka_decode_dev; returns the arena entries used (raises on CG_MAP_FULL)."""
+        used = C.c_size_t()
+        N.check(N.lib.cg_kafka_decode_dev(self.h, _p(d_raw), _p(d_off), n, _p(d_redirect), _p(d_remote),
+                                          _p(d_reqs), _p(d_arena), arena_cap, C.byref(used), _p(d_status), stream))
+        return used.value
+
+    def kafka_verdicts_raw(self, raw, raw_off, redirect, remote) -> np.ndarray:
+        """Wire bytes → CG_KAFKA_V_* per request (decode + verdict on the GPU)."""
+        raw = np.ascontiguousarray(raw, np.uint8)
+        off = np.ascontiguousarray(raw_off, np.uint64)
+        n = len(off) - 1
+        red = np.ascontiguousarray(redirect, np.uint16)
+        rem = np.ascontiguousarray(remote, np.uint32)
+        if len(red) != n or len(rem) != n:
+            raise ValueError("redirect/remote must have one entry per request")
+        out = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_kafka_verdicts_raw_host(self.h, _p(raw), _p(off), n, _p(red), _p(rem), _p(out)))
+        return out[:n]
 
     def kafka_verdicts(self, reqs: np.ndarray, arena: Optional[np.ndarray] = None) -> np.ndarray:
         n = len(reqs)

@@ -976,6 +976,151 @@ int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n, c
   });
 }
 
+// ------------------------------------------------------- Kafka decode ----
+// The GPU decode of n staged requests on `st`, then the host decode of the
+// requests the device deferred (gzip / snappy message payloads): their bytes
+// come back, kafka_decode_host_one rewrites their record and status, and
+// their long topic lists go after the device's arena entries.  Returns the
+// arena entries used (may exceed arena_cap: nothing written beyond it).
+static size_t kafka_decode_on(Engine& e, const KafkaSnapshot& s, StagingSlot& sl, const uint8_t* d_raw,
+                              const uint64_t* d_off, size_t n, const uint16_t* d_red, const uint32_t* d_rem,
+                              cg_kafka_request* d_reqs, uint32_t* d_arena, size_t arena_cap, uint8_t* d_status,
+                              hipStream_t st) {
+  auto* ctr = (unsigned long long*)sl.dev_buf(7, 16);
+  hip_check(hipMemsetAsync(ctr, 0, 16, st), "hipMemsetAsync");
+  check_launch(launch_kafka_decode(s.ddict[0], s.ddict[1], d_raw, d_off, n, d_red, d_rem, d_reqs, d_arena,
+                                   arena_cap, ctr, d_status, st, e.cus),
+               "kafka decode kernel launch");
+  auto* hc = (unsigned long long*)sl.host_buf(7, 16);
+  hip_check(hipMemcpyAsync(hc, ctr, 16, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  size_t used = (size_t)hc[0];
+  if (hc[1] == 0) return used;
+  std::vector<uint8_t> status(n);
+  std::vector<uint64_t> off(n + 1);
+  hip_check(hipMemcpy(status.data(), d_status, n, hipMemcpyDeviceToHost), "D2H");
+  hip_check(hipMemcpy(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost), "D2H");
+  std::vector<uint8_t> bytes;
+  std::vector<uint32_t> spill;
+  for (size_t i = 0; i < n; ++i) {
+    if (status[i] != 2) continue;  // kKwDefer
+    const uint64_t len = off[i + 1] > off[i] ? off[i + 1] - off[i] : 0;
+    bytes.resize(len);
+    if (len) hip_check(hipMemcpy(bytes.data(), d_raw + off[i], len, hipMemcpyDeviceToHost), "D2H");
+    cg_kafka_request q;
+    hip_check(hipMemcpy(&q, d_reqs + i, sizeof(q), hipMemcpyDeviceToHost), "D2H");
+    const size_t base = spill.size();
+    const uint8_t rc = kafka_decode_host_one(s, bytes.data(), len, q.policy, q.remote, &q, &spill);
+    if (rc == CG_KAFKA_DECODE_OK && q.n_topics > CG_KAFKA_MAX_TOPICS) q.topic_ids[0] = (uint32_t)(used + base);
+    hip_check(hipMemcpy(d_reqs + i, &q, sizeof(q), hipMemcpyHostToDevice), "H2D");
+    hip_check(hipMemcpy(d_status + i, &rc, 1, hipMemcpyHostToDevice), "H2D");
+  }
+  if (!spill.empty() && used + spill.size() <= arena_cap)
+    hip_check(hipMemcpy(d_arena + used, spill.data(), spill.size() * 4, hipMemcpyHostToDevice), "H2D");
+  return used + spill.size();
+}
+
+static void check_offsets(const uint64_t* off, size_t n) {
+  if (!off) fail(CG_INVALID_ARGUMENT, "NULL raw_off");
+  for (size_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) fail(CG_INVALID_ARGUMENT, "raw_off must be non-decreasing");
+}
+
+int cg_kafka_decode_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,
+                        const uint16_t* d_redirect, const uint32_t* d_remote, cg_kafka_request* d_reqs,
+                        uint32_t* d_arena, size_t arena_cap, size_t* arena_used, uint8_t* d_status, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = kafka_snap(*e);
+    if (!arena_used) fail(CG_INVALID_ARGUMENT, "NULL arena_used");
+    *arena_used = 0;
+    if (!n) return;
+    e->set_device();
+    auto lease = e->staging.acquire(e->device);
+    const size_t used = kafka_decode_on(*e, *s, *lease, d_raw, d_raw_off, n, d_redirect, d_remote, d_reqs, d_arena,
+                                        d_arena ? arena_cap : 0, d_status, (hipStream_t)stream_of(*e, stream));
+    *arena_used = used;
+    if (used > (d_arena ? arena_cap : 0)) fail(CG_MAP_FULL, "Kafka topic arena too small");
+  });
+}
+
+// Stage raw requests, offsets, redirects and remotes on a lease (buffers
+// 0..3) and decode them into lease buffers 4 (records), 5 (statuses), 6 (arena).
+struct KafkaStaged {
+  cg_kafka_request* reqs;
+  uint8_t* status;
+  uint32_t* arena;
+  size_t used;
+};
+static KafkaStaged kafka_stage_decode(Engine& e, const KafkaSnapshot& s, StagingSlot& sl, const uint8_t* raw,
+                                      const uint64_t* raw_off, size_t n, const uint16_t* redirect,
+                                      const uint32_t* remote, size_t arena_cap) {
+  check_offsets(raw_off, n);
+  if (!redirect || !remote || (raw_off[n] && !raw)) fail(CG_INVALID_ARGUMENT, "NULL raw/redirect/remote");
+  const auto st = (hipStream_t)sl.stream;
+  const uint8_t* d_raw = (const uint8_t*)stage_in(sl, 0, raw, raw_off[n]);
+  const uint64_t* d_off = (const uint64_t*)stage_in(sl, 1, raw_off, (n + 1) * 8);
+  const uint16_t* d_red = (const uint16_t*)stage_in(sl, 2, redirect, n * 2);
+  const uint32_t* d_rem = (const uint32_t*)stage_in(sl, 3, remote, n * 4);
+  KafkaStaged k;
+  k.reqs = (cg_kafka_request*)sl.dev_buf(4, n * sizeof(cg_kafka_request));
+  k.status = (uint8_t*)sl.dev_buf(5, n);
+  k.arena = (uint32_t*)sl.dev_buf(6, std::max<size_t>(arena_cap, 1) * 4);
+  k.used = kafka_decode_on(e, s, sl, d_raw, d_off, n, d_red, d_rem, k.reqs, k.arena, arena_cap, k.status, st);
+  return k;
+}
+
+int cg_kafka_decode_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n, const uint16_t* redirect,
+                         const uint32_t* remote, cg_kafka_request* reqs, uint32_t* arena, size_t arena_cap,
+                         size_t* arena_used, uint8_t* status) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = kafka_snap(*e);
+    if (!arena_used || (n && (!reqs || !status))) fail(CG_INVALID_ARGUMENT, "NULL reqs/status/arena_used");
+    *arena_used = 0;
+    if (!n) return;
+    if (!arena) arena_cap = 0;
+    e->set_device();
+    auto lease = e->staging.acquire(e->device);
+    const KafkaStaged k = kafka_stage_decode(*e, *s, *lease, raw, raw_off, n, redirect, remote, arena_cap);
+    *arena_used = k.used;
+    if (k.used > arena_cap) fail(CG_MAP_FULL, "Kafka topic arena too small");
+    const auto st = (hipStream_t)lease->stream;
+    hip_check(hipMemcpyAsync(reqs, k.reqs, n * sizeof(cg_kafka_request), hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipMemcpyAsync(status, k.status, n, hipMemcpyDeviceToHost, st), "D2H");
+    if (k.used) hip_check(hipMemcpyAsync(arena, k.arena, k.used * 4, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  });
+}
+
+int cg_kafka_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                               const uint16_t* redirect, const uint32_t* remote, uint8_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = kafka_snap(*e);
+    if (n && !out) fail(CG_INVALID_ARGUMENT, "NULL out");
+    if (!n) return;
+    check_offsets(raw_off, n);
+    e->set_device();
+    auto lease = e->staging.acquire(e->device);
+    // a request's topic list needs at least 2 bytes per topic
+    const size_t cap = (size_t)(raw_off[n] - raw_off[0]) / 2 + 16;
+    const KafkaStaged k = kafka_stage_decode(*e, *s, *lease, raw, raw_off, n, redirect, remote, cap);
+    if (k.used > cap) fail(CG_UNKNOWN_ERROR, "Kafka topic arena bound exceeded");
+    const auto st = (hipStream_t)lease->stream;
+    uint8_t* d_v = (uint8_t*)lease->dev_buf(0, n + 16);  // the raw bytes are no longer needed
+    check_launch(launch_kafka(s->dev, k.reqs, n, k.arena, d_v, st, e->cus), "kafka kernel launch");
+    uint8_t* hv = (uint8_t*)lease->host_buf(4, 2 * n);
+    hip_check(hipMemcpyAsync(hv, d_v, n, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipMemcpyAsync(hv + n, k.status, n, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    for (size_t i = 0; i < n; ++i) out[i] = hv[n + i] == CG_KAFKA_DECODE_OK ? hv[i] : CG_KAFKA_V_CLOSE;
+  });
+}
+
 // ------------------------------------------------------------ counters ----
 static void counters_loc(Engine& e, uint32_t what, uint32_t id, void** p, size_t* n) {
   *p = nullptr;
@@ -1224,6 +1369,26 @@ int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n, 
     auto e = get(h);
     auto s = kafka_snap(*e);
     for (size_t i = 0; i < n; ++i) out[i] = kafka_eval_host(*s, reqs[i], arena, arena_len);
+  });
+}
+
+int cg_diag_kafka_decode_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                              const uint16_t* redirect, const uint32_t* remote, cg_kafka_request* reqs,
+                              uint32_t* arena, size_t arena_cap, size_t* arena_used, uint8_t* status) {
+  return guarded([&] {
+    auto e = get(h);
+    auto s = kafka_snap(*e);
+    if (!arena_used || (n && (!reqs || !status || !redirect || !remote))) fail(CG_INVALID_ARGUMENT, "NULL argument");
+    *arena_used = 0;
+    if (!n) return;
+    check_offsets(raw_off, n);
+    std::vector<uint32_t> spill;
+    for (size_t i = 0; i < n; ++i)
+      status[i] = kafka_decode_host_one(*s, raw + raw_off[i], raw_off[i + 1] - raw_off[i], redirect[i], remote[i],
+                                        &reqs[i], &spill);
+    *arena_used = spill.size();
+    if (spill.size() > (arena ? arena_cap : 0)) fail(CG_MAP_FULL, "Kafka topic arena too small");
+    if (!spill.empty()) memcpy(arena, spill.data(), spill.size() * 4);
   });
 }
 

@@ -305,6 +305,20 @@ struct KafkaDev {
   unsigned long long* counters;   // [redirect*2] allowed, [+1] denied
 };
 
+// Rule strings (topics, clientIDs) for interning on the device: open
+// addressing over FNV-1a, slot = {hash, len, blob offset, id}, len ~0 empty.
+struct KafkaDictDev {
+  const uint32_t* slots;  // 4 u32 per slot
+  const uint8_t* blob;
+  uint32_t mask, pad;
+};
+constexpr uint32_t kKfDictEmpty = 0xFFFFFFFFu;
+CG_HD inline uint32_t kf_fnv1a(const uint8_t* p, uint32_t n) {
+  uint32_t h = 2166136261u;
+  for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 16777619u;
+  return h;
+}
+
 // ------------------------------------------------------------- ipcache ----
 // cilium_ipcache (bpf/lib/maps.h:135-159), looked up by
 // lookup_ip{4,6}_remote_endpoint (bpf/lib/eps.h:48-115) and resolved as the

@@ -83,7 +83,7 @@ class PinnedMem {
 // device buffers and pinned host buffers, so host calls make no hipMalloc /
 // hipFree and copy with async DMA instead of pageable hipMemcpy.
 struct StagingSlot {
-  static constexpr int kBufs = 4;
+  static constexpr int kBufs = 8;
   void* stream = nullptr;  // hipStream_t
   DevMem dev[kBufs];
   PinnedMem host[kBufs];

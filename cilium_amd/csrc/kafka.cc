@@ -231,6 +231,32 @@ void add_group(KafkaSnapshot& S, uint32_t gid, const std::vector<RuleSpec>& rs,
 
 }  // namespace
 
+namespace {
+
+void build_dict(const std::unordered_map<std::string, uint32_t>& m, std::vector<uint32_t>* slots,
+                std::vector<uint8_t>* blob, uint32_t* mask) {
+  uint32_t cap = 16;
+  while (cap < 2 * m.size()) cap <<= 1;
+  *mask = cap - 1;
+  slots->assign((size_t)cap * 4, 0);
+  for (uint32_t i = 0; i < cap; ++i) (*slots)[i * 4 + 1] = kKfDictEmpty;
+  blob->clear();
+  for (const auto& [str, id] : m) {
+    const uint8_t* p = (const uint8_t*)str.data();
+    const uint32_t h = kf_fnv1a(p, (uint32_t)str.size());
+    uint32_t s = h & *mask;
+    while ((*slots)[s * 4 + 1] != kKfDictEmpty) s = (s + 1) & *mask;
+    (*slots)[s * 4 + 0] = h;
+    (*slots)[s * 4 + 1] = (uint32_t)str.size();
+    (*slots)[s * 4 + 2] = (uint32_t)blob->size();
+    (*slots)[s * 4 + 3] = id;
+    blob->insert(blob->end(), p, p + str.size());
+  }
+  if (blob->empty()) blob->push_back(0);
+}
+
+}  // namespace
+
 std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
   Json root = JsonParser(json, len).parse();
   if (root.type != Json::ARR) fail(CG_POLICY_REJECTED, "expected a list of Kafka redirects");
@@ -338,6 +364,8 @@ std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len) {
     S.ngroups = 1;
   }
   if (S.dflt_group.empty()) S.dflt_group.push_back(0);
+  for (int w = 0; w < 2; ++w) build_dict(w == 0 ? S.topic_ids : S.client_ids, &S.dict_slots[w], &S.dict_blob[w],
+                                        &S.dict_mask[w]);
   return snap;
 }
 
@@ -381,11 +409,13 @@ uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& q, const
     if (rule_matches(s.rules[su.x_off + i], q)) return 1;
   if (nt == 0) return 0;
   const uint32_t* topics = q.topic_ids;
+  uint32_t ntot = nt;
   if (nt > CG_KAFKA_MAX_TOPICS) {
-    if ((size_t)q.topic_ids[0] + nt > arena_len) return 0;
+    if (nt == CG_KAFKA_TOPICS_IN_ARENA) ntot = q.topic_ids[1];
+    if ((size_t)q.topic_ids[0] + ntot > arena_len) return 0;
     topics = arena + q.topic_ids[0];
   }
-  for (uint32_t t = 0; t < nt; ++t) {
+  for (uint32_t t = 0; t < ntot; ++t) {
     const uint64_t key = ((uint64_t)g << 32) | topics[t];
     uint32_t h = kf_hash(key) & s.thash_mask;
     bool cov = false;
@@ -424,6 +454,11 @@ void KafkaSnapshot::upload(Engine& e) {
   dev.dflt_group = d_dflt.as<uint32_t>();
   dev.nredirects = (uint32_t)dflt_group.size();
   dev.counters = d_counters.as<unsigned long long>();
+  for (int w = 0; w < 2; ++w) {
+    d_dslots[w].upload_vec(dict_slots[w]);
+    d_dblob[w].upload_vec(dict_blob[w]);
+    ddict[w] = KafkaDictDev{d_dslots[w].as<uint32_t>(), d_dblob[w].as<uint8_t>(), dict_mask[w], 0};
+  }
 }
 
 }  // namespace cg

@@ -26,12 +26,23 @@ struct KafkaSnapshot {
   uint32_t ghash_mask = 0;
   std::vector<uint32_t> dflt_group;
 
-  DevMem d_rules, d_sums, d_thash, d_chash, d_ghash, d_dflt, d_counters;
+  // device dictionaries of the rule strings (0 topics, 1 clientIDs)
+  std::vector<uint32_t> dict_slots[2];  // 4 u32 per slot (KafkaDictDev)
+  std::vector<uint8_t> dict_blob[2];
+  uint32_t dict_mask[2] = {0, 0};
+
+  DevMem d_rules, d_sums, d_thash, d_chash, d_ghash, d_dflt, d_counters, d_dslots[2], d_dblob[2];
   KafkaDev dev{};
+  KafkaDictDev ddict[2] = {};
   void upload(Engine& e);
 };
 
 std::shared_ptr<KafkaSnapshot> kafka_compile(const char* json, size_t len);
+// Decode one request's bytes on the host (kafka_wire.cc): the record,
+// topics beyond CG_KAFKA_MAX_TOPICS appended to *spill (record offset
+// relative to spill's start); returns CG_KAFKA_DECODE_OK / _ERROR.
+uint8_t kafka_decode_host_one(const KafkaSnapshot& s, const uint8_t* raw, uint64_t len, uint16_t redirect,
+                              uint32_t remote, cg_kafka_request* q, std::vector<uint32_t>* spill);
 uint8_t kafka_eval_host(const KafkaSnapshot& s, const cg_kafka_request& r, const uint32_t* arena,
                         size_t arena_len);
 

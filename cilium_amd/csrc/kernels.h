@@ -24,5 +24,12 @@ int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* o
                    IpcVal* out6, void* stream, int cus);
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
                  void* stream, int cus);
+// Kafka wire decode (kernels_kafka.hip): records + statuses (kKwDefer for the
+// host to finish); ctr[0] arena entries reserved, ctr[1] deferred requests
+// (both zeroed by the caller).
+int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients, const uint8_t* raw,
+                        const uint64_t* off, size_t n, const uint16_t* redirect, const uint32_t* remote, void* recs,
+                        uint32_t* arena, size_t arena_cap, unsigned long long* ctr, uint8_t* status, void* stream,
+                        int cus);
 
 }  // namespace cg

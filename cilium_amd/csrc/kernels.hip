@@ -560,6 +560,7 @@ __device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, c
   // topic ids re-read from the record (cached)
   const uint32_t* tids = reinterpret_cast<const uint32_t*>(r + 1);
   const uint32_t* tsrc = nt > CG_KAFKA_MAX_TOPICS ? arena + tids[0] : tids;
+  if (nt == CG_KAFKA_TOPICS_IN_ARENA) nt = tids[1];
   for (uint32_t t = 0; t < nt; ++t) {
     const unsigned long long k = ((unsigned long long)g << 32) | tsrc[t];
     uint32_t hh = kf_hash(k) & T.thash_mask;

@@ -448,13 +448,15 @@ typedef struct {
   int16_t api_key;      /* RequestMessage.kind */
   int16_t api_version;  /* RequestMessage.version */
   uint8_t kind;         /* CG_KAFKA_K_*: which typed request ReadRequest produced */
-  uint8_t n_topics;     /* topics in topic_ids (> CG_KAFKA_MAX_TOPICS: overflow) */
+  uint8_t n_topics;     /* topics in topic_ids (> CG_KAFKA_MAX_TOPICS: in the arena at
+                           topic_ids[0]; CG_KAFKA_TOPICS_IN_ARENA: count in topic_ids[1]) */
   uint16_t policy;      /* redirect index (UINT16_MAX unknown → deny) */
   uint32_t remote;      /* source identity (0 = unknown: wildcard rules only) */
   uint32_t client_id;   /* interned ClientID (CG_KAFKA_UNKNOWN_STR if not a rule string) */
   uint32_t topic_ids[CG_KAFKA_MAX_TOPICS]; /* interned topics; overflow: [0] = arena offset */
 } cg_kafka_request;
 
+#define CG_KAFKA_TOPICS_IN_ARENA 255  /* n_topics value for 255+ topics */
 #define CG_KAFKA_K_NIL 0      /* request == nil (unparsed kinds) */
 #define CG_KAFKA_K_TYPED 1    /* Produce/Fetch/Offset/Metadata/OffsetCommit/OffsetFetch */
 #define CG_KAFKA_K_CONSUMER_METADATA 2
@@ -463,6 +465,52 @@ typedef struct {
 /* Intern a string against the installed Kafka snapshot's topic / clientID
  * dictionaries (what=0 topic, 1 clientID). */
 int cg_kafka_intern(uint64_t h, uint32_t what, const char* s, size_t len, uint32_t* id);
+
+/* Kafka requests from their wire bytes: ReadRequest (pkg/kafka/request.go:
+ * 186-229) with the vendored optiopay/kafka decoders it calls (proto
+ * ReadReq and Read{Produce,Fetch,Offset,Metadata,ConsumerMetadata,
+ * OffsetCommit,OffsetFetch}Req, messages.go:124-166,504,767,1033,1173,1389,
+ * 1591,1810; produce message sets parsed in full with CRC32 checks and
+ * gzip / snappy payloads inflated, as pkg/proxy/kafka.go:449-451 configures).
+ * Request i is raw[raw_off[i] .. raw_off[i+1]): the connection's bytes from
+ * the start of the request (ReadReq reads 4 + size of them).  Writes one
+ * cg_kafka_request per request (topics and clientID interned against the
+ * installed snapshot, redirect[i] / remote[i] copied) and status[i]:
+ * CG_KAFKA_DECODE_OK, or CG_KAFKA_DECODE_ERROR when ReadRequest returns an
+ * error — the proxy closes the connection (kafka.go:340-347); such a
+ * record is marked to be denied (policy UINT16_MAX).  Topic lists longer
+ * than CG_KAFKA_MAX_TOPICS go to `arena` (arena_cap u32 entries); *arena_used
+ * gets the entries the batch needs, and the call fails with CG_MAP_FULL
+ * when that exceeds arena_cap (arena_cap >= raw bytes / 2 always suffices).
+ * raw_off must be non-decreasing; raw holds raw_off[n] bytes.  The decode
+ * runs on the GPU (cg_kafka_decode_dev on staged copies). */
+#define CG_KAFKA_DECODE_OK 0
+#define CG_KAFKA_DECODE_ERROR 1
+int cg_kafka_decode_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                         const uint16_t* redirect, const uint32_t* remote, cg_kafka_request* reqs,
+                         uint32_t* arena, size_t arena_cap, size_t* arena_used, uint8_t* status);
+
+/* The same decode on the GPU (one lane per request, raw bytes in HBM),
+ * records and statuses in device memory.  d_raw_off holds n + 1 offsets.
+ * Requests carrying gzip / snappy messages are finished by the host
+ * decoder (the device reports them, the call decodes them on the CPU and
+ * patches their records before returning), so this call synchronizes.
+ * d_arena: arena_cap u32 entries of device memory for long topic lists;
+ * *arena_used and CG_MAP_FULL as for cg_kafka_decode_host.  A decreasing
+ * offset pair is read as an empty request. */
+int cg_kafka_decode_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,
+                        const uint16_t* d_redirect, const uint32_t* d_remote, cg_kafka_request* d_reqs,
+                        uint32_t* d_arena, size_t arena_cap, size_t* arena_used, uint8_t* d_status,
+                        void* stream);
+
+/* Raw requests → verdicts in one call (decode on the GPU, then the verdict
+ * kernel): out[i] = 1 forward, 0 deny (ErrTopicAuthorizationFailed),
+ * 2 = ReadRequest failed (connection closed). */
+#define CG_KAFKA_V_DENY 0
+#define CG_KAFKA_V_ALLOW 1
+#define CG_KAFKA_V_CLOSE 2
+int cg_kafka_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                               const uint16_t* redirect, const uint32_t* remote, uint8_t* out);
 
 /* kafkaRedirect.canAccess per request: out[i] = 1 allow, 0 deny. */
 int cg_kafka_verdicts_dev(uint64_t h, const cg_kafka_request* d_reqs, size_t n,
@@ -516,6 +564,11 @@ int cg_diag_http_rules_host(uint64_t h, const void* batch, size_t nslots, const 
                             size_t n, const uint8_t* arena, size_t arena_len, uint32_t* rule);
 int cg_diag_kafka_eval_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
                             const uint32_t* arena, size_t arena_len, uint8_t* out);
+/* cg_kafka_decode_host's decode on the CPU (the host decoder that also
+ * finishes compressed produce requests), for cross-checking the GPU. */
+int cg_diag_kafka_decode_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                              const uint16_t* redirect, const uint32_t* remote, cg_kafka_request* reqs,
+                              uint32_t* arena, size_t arena_cap, size_t* arena_used, uint8_t* status);
 int cg_diag_l4_eval_host(uint64_t h, uint32_t map_id, const cg_l4_tuple* tuples, size_t n,
                          int32_t* verdicts);
 /* The ipcache tables walked on the host exactly as ipcache_kernel does. */

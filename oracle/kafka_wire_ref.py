@@ -154,6 +154,9 @@ def _snappy_block(src: bytes) -> bytes:
     v, n = _uvarint(src)
     if n <= 0 or v > 0xFFFFFFFF:
         raise _Err(False)
+    if v > MAX_PARSE_BUF:
+        # decoded or not, readMessageSet rejects a set this long
+        raise _Err(False)
     dst = bytearray(v)
     d, s = 0, n
     while s < len(src):
@@ -236,7 +239,7 @@ def gunzip(b: bytes) -> bytes:
     FNAME/FCOMMENT strings of < 512 bytes, FHCRC checked), raw deflate, then
     CRC32 and ISIZE.  Input ending cleanly before a header ends the stream;
     anything else that is not a member is an error."""
-    out, pos = [], 0
+    out, pos, total = [], 0, 0
     first = True
     while True:
         if pos == len(b) and not first:
@@ -269,10 +272,12 @@ def gunzip(b: bytes) -> bytes:
             q += 2
         do = zlib.decompressobj(-15)
         try:
-            data = do.decompress(b[q:])
+            # past maxParseBufSize the set is rejected whatever follows
+            data = do.decompress(b[q:], MAX_PARSE_BUF + 1 - total)
         except zlib.error:
             raise _Err(False)
-        if not do.eof or len(do.unused_data) < 8:
+        total += len(data)
+        if total > MAX_PARSE_BUF or not do.eof or len(do.unused_data) < 8:
             raise _Err(False)
         crc, isize = struct.unpack("<II", do.unused_data[:8])
         if crc != zlib.crc32(data) & 0xFFFFFFFF or isize != len(data) & 0xFFFFFFFF:
@@ -358,6 +363,10 @@ def _topic_array(dec: _Dec, per_partition, nullable=False):
         m = dec.array_len(False)
         for _ in range(m):
             per_partition()
+            if dec.err is not None:
+                break
+        if dec.err is not None:
+            break  # every later read is a no-op: the outcome is the error
     return names
 
 
@@ -417,6 +426,8 @@ def _decode(raw: bytes):
         dec.i32()
         n = dec.array_len(False)
         for _ in range(n):
+            if dec.err is not None:
+                break
             topics.append(dec.string())
             m = dec.array_len(False)
             for _ in range(m):
@@ -456,7 +467,11 @@ def _decode(raw: bytes):
         topics = _topic_array(dec, part)
     elif kind == 3:  # metadata
         n = dec.array_len(True)
-        topics = None if n < 0 else [dec.string() for _ in range(n)]
+        topics = None if n < 0 else []
+        for _ in range(max(n, 0)):
+            if dec.err is not None:
+                break
+            topics.append(dec.string())
         if ver >= 4:
             dec.i8()
     elif kind == 8:  # offset commit

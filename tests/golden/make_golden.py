@@ -186,6 +186,38 @@ def kafka_kats() -> dict:
 
 
 # ---------------------------------------------------------------- LPM KATs --
+def kafka_wire_kats() -> dict:
+    """Wire bytes of the requests pkg/proxy/kafka_test.go:184-258 sends
+    through the proxy (optiopay client: broker.go:296 metadata with the
+    broker's clientID, broker.go:818 ProduceReq with NewProducerConf's
+    RequiredAcks -1 / 5 s timeout, messages "first" and "second"), encoded
+    per the vendored proto encoders (cilium_amd.kafka_requests), with the
+    verdicts that test asserts and the decode ReadRequest yields; plus the
+    ReadReq / ReadRequest error cases (messages.go:131, request.go:195-198)."""
+    from cilium_amd import kafka_requests as K
+    rules = [{"apiKey": "metadata", "apiVersion": "0"},
+             {"apiKey": "produce", "apiVersion": "0", "topic": "allowedTopic"}]
+    msgs = [(None, b"first"), (None, b"second")]
+
+    def prod(topic):
+        return K.produce(0, b"tester", [(topic, [(0, msgs)])], acks=-1, timeout_ms=5000)
+    cases = [
+        ("pkg/proxy/kafka_test.go:215 (Dial: metadata, all topics)", K.metadata(0, b"tester", None), 1,
+         [3, 0, "typed", "tester", []]),
+        ("pkg/proxy/kafka_test.go:246 (leader lookup: metadata for allowedTopic)",
+         K.metadata(0, b"tester", [b"allowedTopic"]), 1, [3, 0, "typed", "tester", ["allowedTopic"]]),
+        ("pkg/proxy/kafka_test.go:246-249", prod(b"allowedTopic"), 1, [0, 0, "typed", "tester", ["allowedTopic"]]),
+        ("pkg/proxy/kafka_test.go:251-253", prod(b"disallowedTopic"), 0,
+         [0, 0, "typed", "tester", ["disallowedTopic"]]),
+        ("pkg/kafka/request.go:195-198 (length < 12)", bytes([0, 0, 0, 6, 0, 3, 0, 0, 0, 1]), 2, None),
+        ("vendor/github.com/optiopay/kafka/proto/messages.go:131 (size <= 0)", bytes([0, 0, 0, 0, 0, 3]), 2, None),
+        ("vendor/github.com/optiopay/kafka/proto/messages.go:141-147 (size > maxParseBufSize)",
+         bytes([0, 0x64, 0, 0, 0, 3]) + bytes(8), 2, None),
+    ]
+    return {"rules": rules, "cases": [{"source": src, "hex": raw.hex(), "expect": v, "decoded": d}
+                                      for src, raw, v, d in cases]}
+
+
 def lpm_kats() -> dict:
     """test/bpf/unit-test.c:77-102 (prefix p/len covers a iff a & mask == p)."""
     c = [("255.255.255.255/32", "255.255.255.255", 1), ("255.255.255.255/32", "255.240.0.0", 0),
@@ -279,7 +311,7 @@ def proxylib_kats() -> dict:
 
 def main():
     files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
-             "kafka_kat.json": kafka_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors()}
+             "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors()}
     for name, data in files.items():
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(data, f, indent=1, sort_keys=False)
