@@ -306,9 +306,11 @@ struct KafkaDev {
 };
 
 // Rule strings (topics, clientIDs) for interning on the device: open
-// addressing over FNV-1a, slot = {hash, len, blob offset, id}, len ~0 empty.
+// addressing over FNV-1a, 32-byte slots {hash, len (~0 empty), id, blob
+// offset of the bytes past the first 16, the first 16 bytes zero-padded}.
+constexpr uint32_t kKfDictSlotWords = 8;
 struct KafkaDictDev {
-  const uint32_t* slots;  // 4 u32 per slot
+  const uint32_t* slots;  // kKfDictSlotWords u32 per slot
   const uint8_t* blob;
   uint32_t mask, pad;
 };

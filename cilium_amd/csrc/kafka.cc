@@ -238,19 +238,22 @@ void build_dict(const std::unordered_map<std::string, uint32_t>& m, std::vector<
   uint32_t cap = 16;
   while (cap < 2 * m.size()) cap <<= 1;
   *mask = cap - 1;
-  slots->assign((size_t)cap * 4, 0);
-  for (uint32_t i = 0; i < cap; ++i) (*slots)[i * 4 + 1] = kKfDictEmpty;
+  constexpr uint32_t W = kKfDictSlotWords;
+  slots->assign((size_t)cap * W, 0);
+  for (uint32_t i = 0; i < cap; ++i) (*slots)[i * W + 1] = kKfDictEmpty;
   blob->clear();
   for (const auto& [str, id] : m) {
     const uint8_t* p = (const uint8_t*)str.data();
     const uint32_t h = kf_fnv1a(p, (uint32_t)str.size());
     uint32_t s = h & *mask;
-    while ((*slots)[s * 4 + 1] != kKfDictEmpty) s = (s + 1) & *mask;
-    (*slots)[s * 4 + 0] = h;
-    (*slots)[s * 4 + 1] = (uint32_t)str.size();
-    (*slots)[s * 4 + 2] = (uint32_t)blob->size();
-    (*slots)[s * 4 + 3] = id;
-    blob->insert(blob->end(), p, p + str.size());
+    while ((*slots)[s * W + 1] != kKfDictEmpty) s = (s + 1) & *mask;
+    uint32_t* e = slots->data() + (size_t)s * W;
+    e[0] = h;
+    e[1] = (uint32_t)str.size();
+    e[2] = id;
+    e[3] = (uint32_t)blob->size();
+    for (size_t k = 0; k < str.size() && k < 16; ++k) e[4 + k / 4] |= (uint32_t)p[k] << (8 * (k % 4));
+    if (str.size() > 16) blob->insert(blob->end(), p + 16, p + str.size());
   }
   if (blob->empty()) blob->push_back(0);
 }

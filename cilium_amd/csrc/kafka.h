@@ -27,7 +27,7 @@ struct KafkaSnapshot {
   std::vector<uint32_t> dflt_group;
 
   // device dictionaries of the rule strings (0 topics, 1 clientIDs)
-  std::vector<uint32_t> dict_slots[2];  // 4 u32 per slot (KafkaDictDev)
+  std::vector<uint32_t> dict_slots[2];  // kKfDictSlotWords u32 per slot (KafkaDictDev)
   std::vector<uint8_t> dict_blob[2];
   uint32_t dict_mask[2] = {0, 0};
 

@@ -27,38 +27,93 @@ namespace cg {
 namespace {
 
 constexpr uint32_t kKwThreads = 256;
+constexpr uint32_t kKwWaves = kKwThreads / 64;
+// per-wave LDS stage of the wave's 64 requests (bytes; 0 = none): requests
+// reaching past it read HBM directly
+constexpr uint32_t kKwStage = 4096;
+// CRC-32 tables (slicing-by-kKwSlices, kKwSlices KiB of LDS per block)
+constexpr uint32_t kKwSlices = 8;
 
-// CRC-32 (IEEE, reflected), slicing-by-8 over tables t[k][256] in LDS.
+// CRC-32 (IEEE, reflected), slicing-by-kKwSlices over tables t[k][256] in
+// LDS: byte j of a kKwSlices-byte block goes through table kKwSlices-1-j.
+// The unaligned head and the tail (< kKwSlices bytes) go through the same
+// tables up to 4 bytes per step, so no per-byte dependency chain remains.
 struct LdsCrc {
   const uint32_t* t;
+  // r (0..4) bytes of p in one step
+  __device__ __forceinline__ uint32_t small(uint32_t c, const uint8_t* p, uint32_t r) const {
+    if (!r) return c;
+    uint32_t d = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t v = p[k < r ? k : r - 1];
+      d |= (k < r ? v : 0u) << (8 * k);
+    }
+    const uint32_t x = c ^ d;
+    uint32_t o = r == 4 ? 0u : c >> (8 * r);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+      if (j < r) o ^= t[(r - 1 - j) * 256 + ((x >> (8 * j)) & 0xFF)];
+    return o;
+  }
   __device__ uint32_t operator()(const uint8_t* p, uint32_t n) const {
     uint32_t c = 0xFFFFFFFFu;
-    while (n && ((uintptr_t)p & 3)) {
-      c = t[(c ^ *p++) & 0xFF] ^ (c >> 8);
-      --n;
+    uint32_t h = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
+    h = h < n ? h : n;
+    c = small(c, p, h);
+    p += h;
+    n -= h;
+    for (; n >= kKwSlices; n -= kKwSlices, p += kKwSlices) {
+      uint32_t w[kKwSlices / 4];
+#pragma unroll
+      for (uint32_t q = 0; q < kKwSlices / 4; ++q) w[q] = reinterpret_cast<const uint32_t*>(p)[q];
+      w[0] ^= c;
+      c = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kKwSlices; ++j) c ^= t[(kKwSlices - 1 - j) * 256 + ((w[j / 4] >> (8 * (j % 4))) & 0xFF)];
     }
-    for (; n >= 8; n -= 8, p += 8) {
-      const uint32_t a = *reinterpret_cast<const uint32_t*>(p) ^ c;
-      const uint32_t b = *reinterpret_cast<const uint32_t*>(p + 4);
-      c = t[7 * 256 + (a & 0xFF)] ^ t[6 * 256 + ((a >> 8) & 0xFF)] ^ t[5 * 256 + ((a >> 16) & 0xFF)] ^
-          t[4 * 256 + (a >> 24)] ^ t[3 * 256 + (b & 0xFF)] ^ t[2 * 256 + ((b >> 8) & 0xFF)] ^
-          t[256 + ((b >> 16) & 0xFF)] ^ t[b >> 24];
+    while (n) {
+      const uint32_t r = n < 4 ? n : 4;
+      c = small(c, p, r);
+      p += r;
+      n -= r;
     }
-    while (n--) c = t[(c ^ *p++) & 0xFF] ^ (c >> 8);
     return ~c;
   }
 };
 
-__device__ uint32_t kw_intern(const KafkaDictDev& d, const uint8_t* p, uint32_t n) {
-  const uint32_t h = kf_fnv1a(p, n);
+// Intern p[0, n): FNV-1a over the bytes, one 32-byte slot per probe.  The
+// first 16 bytes are loaded with clamped indices (independent loads, no
+// per-byte branch) and compared in registers against the slot's copy.
+__device__ __forceinline__ uint32_t kw_intern(const KafkaDictDev& d, const uint8_t* p, uint32_t n) {
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  uint32_t h = 2166136261u;
+  if (n) {
+    const uint32_t m = n < 16 ? n : 16;
+    uint32_t c[16];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) c[k] = p[k < m ? k : m - 1];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t v = k < m ? c[k] : 0u;
+      if (k < m) h = (h ^ v) * 16777619u;
+      const uint32_t sh = v << (8 * (k & 3));
+      if (k < 4) w0 |= sh;
+      else if (k < 8) w1 |= sh;
+      else if (k < 12) w2 |= sh;
+      else w3 |= sh;
+    }
+    for (uint32_t k = 16; k < n; ++k) h = (h ^ p[k]) * 16777619u;
+  }
   uint32_t s = h & d.mask;
-  for (uint32_t k = 0; k <= d.mask; ++k, s = (s + 1) & d.mask) {
-    const uint4 e = *reinterpret_cast<const uint4*>(d.slots + (size_t)s * 4);
-    if (e.y == kKfDictEmpty) break;
-    if (e.x == h && e.y == n) {
-      uint32_t j = 0;
-      while (j < n && d.blob[e.z + j] == p[j]) ++j;
-      if (j == n) return e.w;
+  for (uint32_t probe = 0; probe <= d.mask; ++probe, s = (s + 1) & d.mask) {
+    const uint4* e = reinterpret_cast<const uint4*>(d.slots + (size_t)s * kKfDictSlotWords);
+    const uint4 hd = e[0], pre = e[1];
+    if (hd.y == kKfDictEmpty) break;
+    if (hd.x == h && hd.y == n && pre.x == w0 && pre.y == w1 && pre.z == w2 && pre.w == w3) {
+      uint32_t j = 16;
+      while (j < n && d.blob[hd.w + j - 16] == p[j]) ++j;
+      if (j >= n) return hd.z;
     }
   }
   return CG_KAFKA_UNKNOWN_STR;
@@ -86,19 +141,66 @@ struct DevDefer {
   __device__ uint8_t operator()(uint32_t, const uint8_t*, uint32_t, int16_t) const { return kKwDefer; }
 };
 
+// One request: decode from p (its bytes, in LDS or HBM), write the record
+// and status.
+__device__ __forceinline__ void decode_one(const KafkaDictDev& dt, const KafkaDictDev& dc, const LdsCrc& crc,
+                                           const uint8_t* p, uint32_t len, size_t i, uint32_t red, uint32_t rem,
+                                           uint4* __restrict__ recs, uint32_t* __restrict__ arena,
+                                           unsigned long long arena_cap, unsigned long long* __restrict__ ctr,
+                                           uint8_t* __restrict__ status) {
+  uint4* rec = recs + i * 4;
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  rec[1] = zero;
+  rec[2] = zero;
+  rec[3] = zero;
+  KwRequest r;
+  DevSink sink{&dt, p, reinterpret_cast<uint32_t*>(rec + 1), CG_KAFKA_MAX_TOPICS, CG_KAFKA_MAX_TOPICS};
+  uint8_t st = kw_decode(p, len, crc, &r, sink, DevDefer{});
+  uint32_t nt = sink.nt, t0 = 0, t1 = 0;
+  if (st == kKwOk && nt > CG_KAFKA_MAX_TOPICS) {
+    const unsigned long long at = atomicAdd(ctr, (unsigned long long)nt);
+    const bool fits = at + nt <= arena_cap;
+    KwRequest r2;
+    DevSink s2{&dt, p, arena + (fits ? at : 0), fits ? nt : 0u, 0xFFFFFFFFu};
+    kw_decode(p, len, crc, &r2, s2, DevDefer{});
+    t0 = (uint32_t)at;
+    t1 = nt >= CG_KAFKA_TOPICS_IN_ARENA ? nt : 0;
+  }
+  if (st == kKwDefer) atomicAdd(ctr + 1, 1ull);
+  uint4 h;
+  if (st == kKwOk) {
+    const uint32_t ntb = nt < CG_KAFKA_TOPICS_IN_ARENA ? nt : CG_KAFKA_TOPICS_IN_ARENA;
+    h = make_uint4((uint32_t)(uint16_t)r.api_key | (uint32_t)(uint16_t)r.version << 16,
+                   (uint32_t)r.cls | ntb << 8 | red << 16, rem, kw_intern(dc, p + r.client_off, r.client_len));
+    if (nt > CG_KAFKA_MAX_TOPICS) rec[1] = make_uint4(t0, t1, 0, 0);
+  } else {
+    // ReadRequest failed: a record that is denied.  A deferred one keeps
+    // its redirect for the host decoder, which rewrites the record.
+    h = make_uint4(0, CG_KAFKA_K_NIL | (st == kKwDefer ? red : 0xFFFFu) << 16, rem, 0);
+    if (sink.k) {  // topics pass 1 stored before the error
+      rec[1] = zero;
+      rec[2] = zero;
+      rec[3] = zero;
+    }
+  }
+  rec[0] = h;
+  status[i] = st;
+}
+
 __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
     KafkaDictDev dt, KafkaDictDev dc, const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off, size_t n,
     const uint16_t* __restrict__ redirect, const uint32_t* __restrict__ remote, uint4* __restrict__ recs,
     uint32_t* __restrict__ arena, unsigned long long arena_cap, unsigned long long* __restrict__ ctr,
     uint8_t* __restrict__ status) {
-  __shared__ uint32_t s_crc[8 * 256];
+  __shared__ uint32_t s_crc[kKwSlices * 256];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[kKwWaves][kKwStage ? kKwStage : 16];
   for (uint32_t i = threadIdx.x; i < 256; i += kKwThreads) {
     uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
     s_crc[i] = c;
   }
   __syncthreads();
-  for (uint32_t k = 1; k < 8; ++k) {
+  for (uint32_t k = 1; k < kKwSlices; ++k) {
     for (uint32_t i = threadIdx.x; i < 256; i += kKwThreads) {
       const uint32_t prev = s_crc[(k - 1) * 256 + i];
       s_crc[k * 256 + i] = (prev >> 8) ^ s_crc[prev & 0xFF];
@@ -106,51 +208,39 @@ __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
     __syncthreads();
   }
   const LdsCrc crc{s_crc};
-  const size_t stride = (size_t)gridDim.x * kKwThreads;
-  for (size_t i = (size_t)blockIdx.x * kKwThreads + threadIdx.x; i < n; i += stride) {
-    const uint64_t a = off[i], b = off[i + 1];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t* stage = s_stage[wid];
+  const size_t groups = (n + 63) / 64;
+  for (size_t g = (size_t)blockIdx.x * kKwWaves + wid; g < groups; g += (size_t)gridDim.x * kKwWaves) {
+    const size_t i0 = g * 64, i = i0 + lane;
+    const bool live = i < n;
+    const size_t last = i0 + 63 < n ? i0 + 63 : n - 1;
+    const uint64_t a = off[live ? i : last], b = off[(live ? i : last) + 1];
+    // the wave's bytes [off[i0], off[last+1]) (every byte of it belongs to
+    // some request when the end is above the start), up to kKwStage of them
+    // from a 16-byte boundary, loaded coalesced into this wave's LDS stage
+    const uint64_t start = off[i0], end = off[last + 1];
+    const uint64_t lo = start & ~15ull;
+    uint64_t hi = end > start ? end : start;
+    hi = (hi + 15) & ~15ull;
+    if (hi > lo + kKwStage) hi = lo + kKwStage;
+    if (kKwStage) {
+      for (uint64_t x = lo + lane * 16; x < hi; x += 64 * 16)
+        *reinterpret_cast<uint4*>(stage + (x - lo)) = *reinterpret_cast<const uint4*>(raw + x);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     const uint64_t len64 = b > a ? b - a : 0;
     const uint32_t len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
-    const uint8_t* p = raw + a;
-    const uint32_t red = redirect[i], rem = remote[i];
-    uint4* rec = recs + i * 4;
-    const uint4 zero = make_uint4(0, 0, 0, 0);
-    rec[1] = zero;
-    rec[2] = zero;
-    rec[3] = zero;
-    KwRequest r;
-    DevSink sink{&dt, p, reinterpret_cast<uint32_t*>(rec + 1), CG_KAFKA_MAX_TOPICS, CG_KAFKA_MAX_TOPICS};
-    uint8_t st = kw_decode(p, len, crc, &r, sink, DevDefer{});
-    uint32_t nt = sink.nt, t0 = 0, t1 = 0;
-    if (st == kKwOk && nt > CG_KAFKA_MAX_TOPICS) {
-      const unsigned long long at = atomicAdd(ctr, (unsigned long long)nt);
-      const bool fits = at + nt <= arena_cap;
-      KwRequest r2;
-      DevSink s2{&dt, p, arena + (fits ? at : 0), fits ? nt : 0u, 0xFFFFFFFFu};
-      kw_decode(p, len, crc, &r2, s2, DevDefer{});
-      t0 = (uint32_t)at;
-      t1 = nt >= CG_KAFKA_TOPICS_IN_ARENA ? nt : 0;
-    }
-    if (st == kKwDefer) atomicAdd(ctr + 1, 1ull);
-    uint4 h;
-    if (st == kKwOk) {
-      const uint32_t ntb = nt < CG_KAFKA_TOPICS_IN_ARENA ? nt : CG_KAFKA_TOPICS_IN_ARENA;
-      h = make_uint4((uint32_t)(uint16_t)r.api_key | (uint32_t)(uint16_t)r.version << 16,
-                     (uint32_t)r.cls | ntb << 8 | red << 16, rem,
-                     kw_intern(dc, p + r.client_off, r.client_len));
-      if (nt > CG_KAFKA_MAX_TOPICS) rec[1] = make_uint4(t0, t1, 0, 0);
-    } else {
-      // ReadRequest failed: a record that is denied.  A deferred one keeps
-      // its redirect for the host decoder, which rewrites the record.
-      h = make_uint4(0, CG_KAFKA_K_NIL | (st == kKwDefer ? red : 0xFFFFu) << 16, rem, 0);
-      if (sink.k) {  // topics pass 1 stored before the error
-        rec[1] = zero;
-        rec[2] = zero;
-        rec[3] = zero;
-      }
-    }
-    rec[0] = h;
-    status[i] = st;
+    const bool staged = kKwStage && a >= lo && a + len <= hi;
+    // one copy of the decoder over flat addresses (a wave-uniform split into
+    // an LDS copy and an HBM copy measured slower: twice the code)
+    if (live)
+      decode_one(dt, dc, crc, staged ? stage + (a - lo) : raw + a, len, i, redirect[i], remote[i], recs, arena,
+                 arena_cap, ctr, status);
+    // every lane has read its bytes before the stage is refilled
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -161,8 +251,8 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
                         uint32_t* arena, size_t arena_cap, unsigned long long* ctr, uint8_t* status, void* stream,
                         int cus) {
   if (n == 0) return hipSuccess;
-  const size_t need = (n + kKwThreads - 1) / kKwThreads;
-  const int grid = (int)std::min<size_t>(need, (size_t)std::max(cus, 1) * 8);
+  const size_t need = (n + kKwThreads - 1) / kKwThreads;  // one 64-request group per wave
+  const int grid = (int)std::min<size_t>(need, (size_t)std::max(cus, 1) * (4096 / kKwThreads));
   hipLaunchKernelGGL(kafka_decode_kernel, dim3(grid), dim3(kKwThreads), 0, (hipStream_t)stream, topics, clients,
                      raw, off, n, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap, ctr, status);
   return hipGetLastError();

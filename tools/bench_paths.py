@@ -156,6 +156,74 @@ def bench_kafka(torch, dev, stream, cl, args, threads):
                 {"config": {"workload": "BASELINE config 4: 1K Kafka rules, 100M requests", "requests": n}})
 
 
+def kafka_wire_pool(D: int, info: dict, seed: int = 0x4B):
+    """D distinct uncompressed wire requests of config 4's mix (apiKey /
+    version / topics / clientID as synth.kafka_requests draws them)."""
+    from cilium_amd import kafka_requests as K
+    from cilium_amd import synth
+    rq = synth.kafka_requests(D, info, seed=seed)
+    rng = np.random.default_rng(seed)
+    reqs = [K.encode(int(rq["api_key"][i]), int(rq["api_version"][i]), rq["client_id"][i], rq["topics"][i], rng)
+            for i in range(D)]
+    return reqs, rq
+
+
+def bench_kafka_wire(torch, dev, stream, cl, args, threads):
+    """Config 4's request mix as wire bytes: kafka_decode_kernel (ReadRequest
+    + the optiopay decoders, CRC-32 of every produce message) then
+    kafka_kernel, per request."""
+    from oracle import kafka_wire_ref as R
+    from cilium_amd import kafka_requests as K
+    from cilium_amd import synth
+    pols, info = synth.kafka_policy()
+    cl.update_kafka_policy(pols)
+    D, reps = 65_536, 256
+    pool, rq = kafka_wire_pool(D, info)
+    raw, off = K.concat(pool)
+    red = np.zeros(D, np.uint16)
+    rem = np.asarray(rq["remote"], np.uint32)
+    v = cl.kafka_verdicts_raw(raw[: int(off[4096])], off[:4097], red[:4096], rem[:4096])
+    want = cl.kafka_verdicts(*cl.pack_kafka(**{k: x[:4096] for k, x in rq.items()}))
+    assert np.array_equal(v, want), "raw-bytes Kafka verdicts differ from the field-packed path"
+    tot = int(off[-1])
+    d_raw = tile_dev(torch, raw, reps, dev)
+    offs = torch.from_numpy(off[:-1].view(np.int64).copy()).to(dev)
+    d_off = (offs.unsqueeze(0) + torch.arange(reps, device=dev, dtype=torch.int64).unsqueeze(1) * tot).reshape(-1)
+    d_off = torch.cat([d_off, torch.tensor([tot * reps], dtype=torch.int64, device=dev)])
+    n = D * reps
+    d_red = torch.zeros(n, dtype=torch.int16, device=dev)
+    d_rem = torch.from_numpy(rem.view(np.int32)).to(dev).repeat(reps)
+    d_reqs = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
+    cap = tot * reps // 2 + 16
+    d_a = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_o = torch.empty(n, dtype=torch.uint8, device=dev)
+    ss = stream.cuda_stream
+
+    def decode():
+        cl.kafka_decode_dev(d_raw, d_off, n, d_red, d_rem, d_reqs, d_a, cap, d_st, stream=ss)
+
+    def both():
+        decode()
+        cl.kafka_verdicts_dev(d_reqs, n, d_a, d_o, stream=ss)
+    sec = timed(torch, stream, decode, args.steps, 2)
+    sec2 = timed(torch, stream, both, args.steps, 1)
+    # copies carry their original's verdict
+    orig = d_o[:D].clone()
+    assert bool((d_o.view(reps, D) == orig.unsqueeze(0)).all()), "copies' verdicts differ"
+    assert np.array_equal(orig.cpu().numpy(), cl.kafka_verdicts_raw(raw, off, red, rem))
+    bpi = tot / D + 8 + 2 + 4 + 64 + 1
+    sample = pool[:20_000]
+    cpu = cpu_rate(lambda: [R.decode(r) for r in sample], len(sample), args.cpu_seconds)
+    out = line("Kafka wire decode requests/s (ReadRequest on raw bytes), config 4 mix", n, sec, bpi,
+               "kafka_decode_kernel", cpu, "20K requests of the same mix through oracle/kafka_wire_ref.decode, "
+               "1 thread (pure Python)", 1,
+               {"config": {"workload": "BASELINE config 4 request mix as uncompressed wire bytes "
+                           f"({tot / D:.1f} B/request avg), 1K rules", "requests": n},
+                "decode_plus_verdict": {"value": n / sec2, "ms_per_launch": sec2 * 1e3}})
+    return out
+
+
 def bench_ipcache(torch, dev, stream, cl, args, threads):
     import oracle
     from cilium_amd import synth
@@ -328,7 +396,7 @@ def main():
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
-           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc}
+           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()

@@ -48,6 +48,21 @@ VARIANTS = {
     "deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
     "deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
 }
+# Kafka wire decode variants (kernels_kafka.hip): thread count / LDS stage.
+def _kw(threads, stage):
+    return [("kernels_kafka.hip", "constexpr uint32_t kKwThreads = 256;", f"constexpr uint32_t kKwThreads = {threads};"),
+            ("kernels_kafka.hip", "constexpr uint32_t kKwStage = 4096;", f"constexpr uint32_t kKwStage = {stage};")]
+
+
+VARIANTS.update({
+    "kw_base": [],
+    "kw_t256_s4k": _kw(256, 4096),
+    "kw_t256_s2k": _kw(256, 2048),
+    "kw_nostage": _kw(256, 0),
+    "kw_nostage_t128": _kw(128, 0),
+    "kw_nocrc": [("kernels_kafka.hip", "    uint32_t c = 0xFFFFFFFFu;\n    uint32_t h = (4u",
+                  "    if (n > 0) return p[0];\n    uint32_t c = 0xFFFFFFFFu;\n    uint32_t h = (4u")],
+})
 
 
 def build_variant(name, subs):
@@ -60,7 +75,9 @@ def build_variant(name, subs):
         src = files.get(fn) or (B.CSRC / fn).read_text()
         assert a in src, (name, fn, a)
         files[fn] = src.replace(a, b)
-    files.setdefault("kernels_http.hip", (B.CSRC / "kernels_http.hip").read_text())
+    if not any(fn.endswith(".hip") for fn in files):
+        files["kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip"] = \
+            (B.CSRC / ("kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip")).read_text()
     objs = []
     for fn, src in files.items():
         f = OUT / f"{name}_{fn}"
@@ -72,7 +89,7 @@ def build_variant(name, subs):
     others = [B.BUILD / (s + ".o") for s in B.SOURCES if s not in files]
     lib = OUT / f"lib_{name}.so"
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *map(str, others), *map(str, objs),
-                    "-o", str(lib), "-lpthread"], check=True)
+                    "-o", str(lib), "-lpthread", "-lz"], check=True)
     print("built", lib)
 
 
