@@ -8,11 +8,15 @@
 
 namespace cg {
 
-bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable* out, uint32_t max_base) {
+bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable* out, uint32_t max_base,
+                bool by_class) {
   const int n = d.size();
+  // row width: 256 bytes, or the byte classes
+  const int width = by_class ? d.ncls : 256;
+  auto tr = [&](int s, int x) { return d.trans[(size_t)s * d.ncls + (by_class ? x : d.clsmap[x])]; };
   struct Row {
     bool self = false;
-    std::vector<uint8_t> exc;  // exception bytes
+    std::vector<uint8_t> exc;  // exception bytes (classes)
   };
   std::vector<Row> rows(n);
   for (int s = 1; s < n; ++s) {
@@ -25,20 +29,20 @@ bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable*
       continue;
     }
     int self_n = 0, dead_n = 0;
-    for (int b = 0; b < 256; ++b) {
-      int t = d.trans[(size_t)s * d.ncls + d.clsmap[b]];
+    for (int b = 0; b < width; ++b) {
+      int t = tr(s, b);
       self_n += t == s;
       dead_n += t == 0;
     }
     r.self = self_n > dead_n;
     const int dflt = r.self ? s : 0;
-    for (int b = 0; b < 256; ++b)
-      if (d.trans[(size_t)s * d.ncls + d.clsmap[b]] != dflt) r.exc.push_back((uint8_t)b);
+    for (int b = 0; b < width; ++b)
+      if (tr(s, b) != dflt) r.exc.push_back((uint8_t)b);
   }
   // placement: rows defaulting to dead first, then self rows at bases above
   // all of them; within each group most exceptions first, first fit.  A
   // state also owns the header cell base-1, so bases are unique.
-  const uint32_t cap = max_base + 257;
+  const uint32_t cap = max_base + width + 1;
   std::vector<uint8_t> used(cap, 0);
   std::vector<uint32_t> base(n, 0);
   uint64_t excs = 0;
@@ -78,27 +82,56 @@ bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable*
       if (group == 0) self_lo = std::max(self_lo, b0 + 1);
     }
   }
-  uint32_t ncells = 257;
-  for (int s = 0; s < n; ++s) ncells = std::max(ncells, base[s] + 256);
+  uint32_t ncells = width + 1;
+  for (int s = 0; s < n; ++s) ncells = std::max(ncells, base[s] + width);
   out->cells.assign(ncells, kCombEmpty);
   out->state_enc = base;
   out->cells[base[0] - 1] = 0xFFFFu | (kCombNoLabel << 16);  // D: no label, no exceptions
   for (int s = 1; s < n; ++s) {
     const uint32_t b0 = base[s];
     out->cells[b0 - 1] = 0xFFFFu | ((labels[s] & 0xFFFFu) << 16);
-    for (uint8_t x : rows[s].exc) {
-      int t = d.trans[(size_t)s * d.ncls + d.clsmap[x]];
-      out->cells[b0 + x] = b0 | (base[t] << 16);
-    }
+    for (uint8_t x : rows[s].exc) out->cells[b0 + x] = b0 | (base[tr(s, x)] << 16);
   }
   out->start = n > 1 ? base[1] : base[0];
   out->dead = base[0];
   out->exceptions = excs;
+  out->by_class = by_class;
+  out->scaled = false;
   return true;
+}
+
+bool scale_comb(CombTable* t) {
+  uint32_t top = t->dead;
+  for (uint32_t s : t->state_enc) top = std::max(top, s);
+  if (4ull * top > 0xFFFC) return false;
+  for (uint32_t& c : t->cells) {
+    if (c == kCombEmpty) continue;
+    if ((c & 0xFFFF) == 0xFFFF) continue;  // header: 0xFFFF is never a multiple of 4
+    c = ((c & 0xFFFF) * 4) | (((c >> 16) * 4) << 16);
+  }
+  for (uint32_t& s : t->state_enc) s *= 4;
+  t->start *= 4;
+  t->dead *= 4;
+  t->scaled = true;
+  return true;
+}
+
+ClsDfa zero_class_first(const ClsDfa& d) {
+  const int z = d.clsmap[0];
+  if (z == 0) return d;
+  ClsDfa o = d;
+  for (int b = 0; b < 256; ++b) {
+    const int c = d.clsmap[b];
+    o.clsmap[b] = (uint8_t)(c == z ? 0 : c == 0 ? z : c);
+  }
+  for (int s = 0; s < d.size(); ++s)
+    std::swap(o.trans[(size_t)s * d.ncls + 0], o.trans[(size_t)s * d.ncls + z]);
+  return o;
 }
 
 void rebase_comb(CombTable* t, uint32_t off) {
   if (off == 0) return;
+  if (t->scaled) fail(CG_UNKNOWN_ERROR, "internal: rebase of a scaled comb table");
   for (uint32_t& c : t->cells) {
     if (c == kCombEmpty || (c & 0xFFFF) == 0xFFFF) continue;  // empty / header
     const uint32_t next = c >> 16;

@@ -28,6 +28,12 @@
 // Bases are table-local; `rebase_comb` shifts them by the table's offset
 // inside a program's cell block so that all parts of a program share one
 // pointer (the LDS block) — possible while the block stays below 0xFFFF cells.
+//
+// Class mode (by_class): rows are indexed by byte class (cell[S + c], c <
+// ncls) instead of byte, and `scale_comb` stores every state as its byte
+// offset 4*S (the header of S is at byte offset 4*S - 4).  The packer then
+// writes each string byte b as the code 4*clsmap[b] (one byte, so ncls <=
+// 64), and a step's cell address is state + code: one add, no shift.
 #pragma once
 
 #include <cstdint>
@@ -42,6 +48,8 @@ constexpr uint32_t kCombEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kCombNoLabel = 0xFFFF;
 
 struct CombTable {
+  bool by_class = false;            // rows indexed by byte class (see above)
+  bool scaled = false;              // states stored as byte offsets 4*S
   std::vector<uint32_t> cells;
   std::vector<uint32_t> state_enc;  // base of each DFA state (state 0 = dead: D)
   uint32_t start = 0;
@@ -53,17 +61,28 @@ struct CombTable {
 // accepting state must have no live transition (throws Error otherwise).
 // Returns false if the table needs a base beyond `max_base`.
 bool build_comb(const ClsDfa& d, const std::vector<uint32_t>& labels, CombTable* out,
-                uint32_t max_base = kCombMaxBase);
+                uint32_t max_base = kCombMaxBase, bool by_class = false);
 
 // Shift every base of `t` by `off` (its position inside a program block).
 void rebase_comb(CombTable* t, uint32_t off);
 
-inline uint32_t comb_next(const uint32_t* cells, uint32_t dead, uint32_t s, uint32_t b) {
-  const uint32_t e = cells[s + b];
+// States → byte offsets 4*S (class mode); false if a state exceeds 16 bits.
+bool scale_comb(CombTable* t);
+
+// The DFA with its byte classes renumbered so that byte 0x00 (the record
+// padding) is class 0: code 0 then walks as the padding byte.
+ClsDfa zero_class_first(const ClsDfa& d);
+
+// One step: s a state (raw: base, scaled: byte offset), x the byte (raw) or
+// its code 4*class (scaled).
+inline uint32_t comb_next(const uint32_t* cells, uint32_t dead, uint32_t s, uint32_t x, bool scaled = false) {
+  const uint32_t e = scaled ? cells[(s + x) >> 2] : cells[s + x];
   if ((e & 0xFFFF) == s) return e >> 16;
   return s > dead ? s : dead;
 }
 
-inline uint32_t comb_label(const uint32_t* cells, uint32_t s) { return cells[s - 1] >> 16; }
+inline uint32_t comb_label(const uint32_t* cells, uint32_t s, bool scaled = false) {
+  return (scaled ? cells[(s >> 2) - 1] : cells[s - 1]) >> 16;
+}
 
 }  // namespace cg

@@ -158,6 +158,9 @@ constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // cell_begin for every part), so the kernel walks all parts through one
 // pointer — the LDS copy.
 constexpr uint32_t kProgRebased = 4;
+// One part in class mode (kPartClass): the packer writes the program's
+// strings as class codes (HttpSnapshot::prog_code).
+constexpr uint32_t kProgClass = 8;
 struct HttpPart {
   uint32_t cell_off;  // first cell of this part in cells[]
   uint32_t ncells;
@@ -166,8 +169,9 @@ struct HttpPart {
   uint32_t nstates;
   uint32_t dead;
   uint32_t walk_off;  // cells[] offset the states are relative to
-  uint32_t pad;
+  uint32_t mode;      // 0: byte-indexed rows; kPartClass: class rows, states as byte offsets (comb.h)
 };
+constexpr uint32_t kPartClass = 1;
 // Special program ids in the program lookup.
 constexpr uint32_t kProgAllow = 0xFFFFFFFEu;  // no policy for the port → allow
 constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
@@ -228,16 +232,35 @@ CG_HD inline uint32_t hash32(uint32_t x) {
   return x;
 }
 // Remote-identity table of a program (staged into LDS with it): buckets of
-// 8 u32 cells — 4 identities, then their 4 mask-row block offsets (kNoRow =
-// empty slot) — and every identity in one of its two buckets, so a lookup
-// reads at most two buckets (2-choice cuckoo, load up to ~90%: no
-// power-of-two padding and no probe chains).  Bucket choices: one hash,
-// scaled to [0, nb) directly and after a second odd multiplier.
+// 8 u32 cells — 4 identities, then their 4 mask-row block offsets — and
+// every identity in one of its two buckets, so a lookup reads at most two
+// buckets (2-choice cuckoo, load up to ~90%: no power-of-two padding and no
+// probe chains).  An empty slot holds the program's `rtab_empty` identity
+// (one not in its table) with the default row, so matching it changes
+// nothing and the kernel needs no emptiness test.  The bucket hashes use
+// 24-bit multiplies only (full-rate v_mul_u32_u24 / v_mul_hi_u32_u24; the
+// 32-bit ones issue at a quarter rate) and scale to [0, nb), nb < 65536.
 constexpr uint32_t kRtabBucketCells = 8;
-CG_HD inline uint32_t rtab_b1h(uint32_t h, uint32_t nb) { return (uint32_t)(((uint64_t)h * nb) >> 32); }
-CG_HD inline uint32_t rtab_b2h(uint32_t h, uint32_t nb) { return (uint32_t)(((uint64_t)(h * 0x85EBCA77u) * nb) >> 32); }
-CG_HD inline uint32_t rtab_b1(uint32_t id, uint32_t nb) { return rtab_b1h(hash32(id), nb); }
-CG_HD inline uint32_t rtab_b2(uint32_t id, uint32_t nb) { return rtab_b2h(hash32(id), nb); }
+CG_HD inline uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, b);
+#else
+  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
+#endif
+}
+CG_HD inline uint32_t mulhi24(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (b & 0xFFFFFFu)) >> 32);
+}
+CG_HD inline uint32_t rtab_hash(uint32_t id) {
+  const uint32_t a = id ^ (id >> 15);
+  return mul24(a, 0x9E3779u) ^ (a >> 17);
+}
+CG_HD inline uint32_t rtab_b1h(uint32_t h, uint32_t nb) { return mulhi24(h, nb << 8); }
+CG_HD inline uint32_t rtab_b2h(uint32_t h, uint32_t nb) {
+  return mulhi24(mul24(h ^ (h >> 11), 0x85EBCBu) >> 8, nb << 8);  // product bits 8..31
+}
+CG_HD inline uint32_t rtab_b1(uint32_t id, uint32_t nb) { return rtab_b1h(rtab_hash(id), nb); }
+CG_HD inline uint32_t rtab_b2(uint32_t id, uint32_t nb) { return rtab_b2h(rtab_hash(id), nb); }
 
 CG_HD inline uint32_t hash64to32(uint64_t k) {
   k = l4_hash1(k);

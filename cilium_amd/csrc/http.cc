@@ -29,6 +29,9 @@
 #include "http.h"
 
 #include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <cstring>
 #include <functional>
@@ -461,6 +464,9 @@ void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, s
     ok = false;
   }
   if (ok) {
+    if (getenv("CILIUM_GPU_DEBUG"))
+      fprintf(stderr, "[cilium-gpu] http part: %zu rules, %d states, %d byte classes, %zu comb cells\n", rules.size(),
+              p.dfa.size(), p.dfa.ncls, p.comb.cells.size());
     out.push_back(std::move(p));
     return;
   }
@@ -616,6 +622,26 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     std::vector<uint32_t> group(64 * (size_t)W, 0xFFFFFFFEu);
     for (uint32_t j = 0; j < R; ++j) group[j] = (j && bits[j].pnpr == bits[j - 1].pnpr) ? group[j - 1] : j;
     build_parts(fc, urules, idx, F, W, group, parts);
+    // one part over at most 64 byte classes: class-indexed rows with states
+    // as byte offsets (comb.h), the strings packed as class codes
+    std::array<uint8_t, 256> code{};
+    if (parts.size() == 1 && parts[0].dfa.ncls <= 64) {
+      ClsDfa z = zero_class_first(parts[0].dfa);
+      std::vector<uint32_t> labels(z.size(), kCombNoLabel);
+      for (int st = 0; st < z.size(); ++st)
+        if (z.label[st]) labels[st] = z.label[st] - 1;
+      CombTable cc;
+      if (build_comb(z, labels, &cc, kCombMaxBase, true) && scale_comb(&cc)) {
+        parts[0].dfa = std::move(z);
+        parts[0].comb = std::move(cc);
+        pg.flags |= kProgClass;
+        for (int b = 0; b < 256; ++b) code[b] = (uint8_t)(4 * parts[0].dfa.clsmap[b]);
+      }
+    }
+    if (pg.flags & kProgClass) {
+      S.prog_code.resize(pid + 1);
+      S.prog_code[pid] = code;
+    }
     pg.part_begin = (uint32_t)S.parts.size();
     pg.part_count = (uint32_t)parts.size();
     while (S.cells.size() & 3) S.cells.push_back(kCombEmpty);  // blocks start 16-byte aligned
@@ -635,6 +661,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       hp.start = cb.start;
       hp.dead = cb.dead;
       hp.ncells = (uint32_t)cb.cells.size();
+      hp.mode = cb.scaled ? kPartClass : 0;
       S.cells.insert(S.cells.end(), cb.cells.begin(), cb.cells.end());
       S.total_states += d.size();
       S.total_exceptions += cb.exceptions;
@@ -680,6 +707,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
       uint32_t nb = (uint32_t)std::max<size_t>((ent.size() * 10 / 9 + 3) / 4, 1);
       std::vector<std::pair<uint32_t, uint32_t>> slots;  // (identity, row) per slot, row kNoRow = empty
       for (;; nb += nb / 8 + 1) {
+        if (nb >= 65536) fail(CG_POLICY_REJECTED, "too many remote identities in one HTTP policy scope");
         slots.assign((size_t)nb * 4, {0u, kNoRow});
         std::mt19937 rng(0xC111A);
         auto put = [&](uint32_t bk, const std::pair<uint32_t, uint32_t>& e) {
@@ -717,12 +745,17 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
 
       pg.rtab_off = (uint32_t)S.cells.size() - pg.cell_begin;
       pg.rtab_nb = nb;
+      // empty slots: an identity the table does not hold, with the default row
+      uint32_t empty_id = 0;
+      while (by_remote.count(empty_id)) ++empty_id;
       const size_t at = S.cells.size();
       S.cells.resize(at + kRtabBucketCells * (size_t)nb, 0);
       for (uint32_t k = 0; k < nb; ++k)
         for (int sl = 0; sl < 4; ++sl) {
-          S.cells[at + kRtabBucketCells * k + sl] = slots[(size_t)k * 4 + sl].first;
-          S.cells[at + kRtabBucketCells * k + 4 + sl] = slots[(size_t)k * 4 + sl].second;
+          const auto& e = slots[(size_t)k * 4 + sl];
+          const bool empty = e.second == kNoRow;
+          S.cells[at + kRtabBucketCells * k + sl] = empty ? empty_id : e.first;
+          S.cells[at + kRtabBucketCells * k + 4 + sl] = empty ? pg.default_remote : e.second;
         }
       const uint32_t cap = 4 * nb;
       S.total_remote_slots += cap;
@@ -771,6 +804,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
   }
   if (S.cells.empty()) S.cells.push_back(kCombEmpty);
   if (S.progs.empty()) S.progs.push_back(HttpProg{});
+  S.prog_code.resize(S.progs.size());
   if (S.parts.empty()) S.parts.push_back(HttpPart{});
   if (S.dflt.empty()) S.dflt.push_back(kProgDeny);
   return snap;

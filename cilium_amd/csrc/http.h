@@ -1,6 +1,7 @@
 // http.h — HTTP L7 policy snapshot: NPDS JSON → programs of union DFAs.
 #pragma once
 
+#include <array>
 #include <map>
 #include <memory>
 #include <string>
@@ -27,6 +28,8 @@ struct HttpSnapshot {
   std::vector<uint32_t> dflt;
   // (policy, ingress, port) of each program, for counter attribution
   std::vector<uint32_t> prog_key;
+  // class-mode programs (kProgClass): string byte b is packed as code[b]
+  std::vector<std::array<uint8_t, 256>> prog_code;
   // what each per-rule hit counter counts (HttpProg.rule_base + bit)
   std::vector<cg_http_rule_info> rule_info;
 

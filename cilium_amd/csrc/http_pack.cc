@@ -146,6 +146,10 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
       }
       if (last < F) strs.push_back(kRestAbsent);
       soff[i + 1] = strs.size();
+      if (prog[i] < s.progs.size() && (s.progs[prog[i]].flags & kProgClass)) {
+        const auto& code = s.prog_code[prog[i]];
+        for (size_t k = soff[i]; k < soff[i + 1]; ++k) strs[k] = code[strs[k]];
+      }
     }
   }
   auto str_len = [&](size_t i) -> size_t { return build ? soff[i + 1] - soff[i] : 0; };
@@ -328,7 +332,7 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
       for (uint32_t bk : {rtab_b1(remote, pg.rtab_nb), rtab_b2(remote, pg.rtab_nb)})
         for (uint32_t sl = 0; sl < 4; ++sl) {
           const uint32_t* b = blk + pg.rtab_off + kRtabBucketCells * bk;
-          if (b[sl] == remote && b[4 + sl] != kNoRow) roff = b[4 + sl];
+          if (b[sl] == remote) roff = b[4 + sl];
         }
       // first rule (lowest bit) the mask at block offset a shares with the row
       uint32_t hit = 0xFFFFFFFFu;
@@ -341,12 +345,13 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
       for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
         const HttpPart& pt = s.parts[pg.part_begin + pi];
         const uint32_t* cells = s.cells.data() + pt.walk_off;
+        const bool scaled = pt.mode == kPartClass;
         uint32_t st = pt.start;
         for (unsigned char ch : str) {
-          st = comb_next(cells, pt.dead, st, ch);
+          st = comb_next(cells, pt.dead, st, ch, scaled);
           if (st == pt.dead) break;
         }
-        const uint32_t lab = comb_label(cells, st);
+        const uint32_t lab = comb_label(cells, st, scaled);
         if (lab == kCombNoLabel) continue;
         hit = std::min(hit, first(pt.acc_off + lab * 2 * pg.mask_words));
       }

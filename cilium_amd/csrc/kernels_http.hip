@@ -59,10 +59,73 @@ __device__ __forceinline__ uint32_t comb_step(const uint32_t* __restrict__ cells
   return nx;
 }
 
+// The class-mode step (comb.h): states are byte offsets and the string
+// holds class codes 4*c, so the cell address is st + code — one SDWA add
+// with the byte select, no shift.  The block sits at LDS address 0 in the
+// fast path, so the add is the whole address.
+__device__ __forceinline__ uint32_t comb_step_cls(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st,
+                                                 uint32_t code) {
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + (st + code));
+  const uint32_t dflt = max(st, dead);
+  uint32_t nx;
+  asm("v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_sdwa %0, %3, %1, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+      : "=v"(nx)
+      : "v"(e), "v"(st), "v"(dflt)
+      : "vcc");
+  return nx;
+}
+
+template <bool kCls>
+__device__ __forceinline__ uint32_t step(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st, uint32_t x) {
+  return kCls ? comb_step_cls(cells, dead, st, x) : comb_step(cells, dead, st, x);
+}
+
+// Class-mode step on byte B of word w, block at LDS address 0 (the fast
+// path): four VALU.  Written out because the compiler adds the dynamic-LDS
+// base (0) as an operand and then splits the byte select from the add.
+template <int B>
+__device__ __forceinline__ uint32_t lds_cls_step(uint32_t dead, uint32_t st, uint32_t w) {
+  uint32_t e, d, nx;
+#define CG_CLS_STEP(b)                                                                                   \
+  asm volatile("v_add_u32_sdwa %0, %3, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" b \
+               "\n\tds_read_b32 %0, %0\n\t"                                                              \
+               "v_max_u32 %1, %5, %3\n\t"                                                                \
+               "s_waitcnt lgkmcnt(0)\n\t"                                                                \
+               "v_cmp_eq_u32_sdwa vcc, %0, %3 src0_sel:WORD_0 src1_sel:DWORD\n\t"                       \
+               "s_nop 1\n\t"                                                                             \
+               "v_cndmask_b32_sdwa %2, %1, %0, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "  \
+               "src1_sel:WORD_1"                                                                        \
+               : "=&v"(e), "=&v"(d), "=v"(nx)                                                           \
+               : "v"(st), "v"(w), "s"(dead)                                                             \
+               : "vcc")
+  if (B == 0) CG_CLS_STEP("BYTE_0");
+  else if (B == 1) CG_CLS_STEP("BYTE_1");
+  else if (B == 2) CG_CLS_STEP("BYTE_2");
+  else CG_CLS_STEP("BYTE_3");
+#undef CG_CLS_STEP
+  return nx;
+}
+
+template <int I>
+__device__ __forceinline__ uint32_t lds_cls_step16(uint32_t dead, uint32_t st, const uint4& u) {
+  const uint32_t w = I < 4 ? u.x : I < 8 ? u.y : I < 12 ? u.z : u.w;
+  return lds_cls_step<I & 3>(dead, st, w);
+}
+
+// Accept label of state st (its header cell).
+template <bool kCls>
+__device__ __forceinline__ uint32_t state_label(const uint32_t* __restrict__ cells, uint32_t st) {
+  return (kCls ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(cells) + st - 4) : cells[st - 1]) >>
+         16;
+}
+
 // Records longer than a slot live in the overflow arena: byte loop.
+template <bool kCls>
 __device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st,
                                               const uint8_t* __restrict__ arena, uint32_t aoff, uint32_t len) {
-  for (uint32_t p = 0; p < len && st != dead; ++p) st = comb_step(cells, dead, st, arena[aoff + p]);
+  for (uint32_t p = 0; p < len && st != dead; ++p) st = step<kCls>(cells, dead, st, arena[aoff + p]);
   return st;
 }
 
@@ -89,6 +152,7 @@ __device__ __forceinline__ uint4 tile_unit(const TileRef& tr, uint32_t units, ui
 // The overflow string of a lane whose meta word is m (arena entry: u32 length,
 // bytes).  An entry reaching past the batch's arena (arena_bytes, from its
 // header) ends in the dead state: the request is denied.
+template <bool kCls>
 __device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ cells, uint32_t dead, uint32_t st,
                                                  const uint8_t* __restrict__ arena, uint64_t arena_bytes, uint2 m,
                                                  bool ov) {
@@ -97,29 +161,28 @@ __device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ c
   if (aoff + 4 > arena_bytes) return dead;
   const uint32_t len = *reinterpret_cast<const uint32_t*>(arena + aoff);
   if (aoff + 4 + len > arena_bytes) return dead;
-  return walk_arena(cells, dead, st, arena, (uint32_t)aoff + 4, len);
+  return walk_arena<kCls>(cells, dead, st, arena, (uint32_t)aoff + 4, len);
 }
 
 // Block offset of the PNPR mask of remote identity `remote`: the program's
 // remote table (open addressing, {identity, mask offset} slots).
 __device__ __forceinline__ uint32_t remote_row(const uint32_t* __restrict__ blk, const HttpProg& pg, uint32_t remote) {
   // both candidate buckets read together (dev_types.h rtab_b1/rtab_b2)
-  const uint32_t h = hash32(remote);
+  const uint32_t h = rtab_hash(remote);
   const uint32_t* b1 = blk + pg.rtab_off + kRtabBucketCells * rtab_b1h(h, pg.rtab_nb);
   const uint32_t* b2 = blk + pg.rtab_off + kRtabBucketCells * rtab_b2h(h, pg.rtab_nb);
   const uint4 k1 = *reinterpret_cast<const uint4*>(b1), k2 = *reinterpret_cast<const uint4*>(b2);
   const uint4 r1 = *reinterpret_cast<const uint4*>(b1 + 4), r2 = *reinterpret_cast<const uint4*>(b2 + 4);
+  // an empty slot holds an identity outside the table with the default row
   uint32_t row = pg.default_remote;
-  // an empty slot (row kNoRow) never matches: its identity word is 0 and
-  // its row is skipped
-  row = (k1.x == remote && r1.x != kNoRow) ? r1.x : row;
-  row = (k1.y == remote && r1.y != kNoRow) ? r1.y : row;
-  row = (k1.z == remote && r1.z != kNoRow) ? r1.z : row;
-  row = (k1.w == remote && r1.w != kNoRow) ? r1.w : row;
-  row = (k2.x == remote && r2.x != kNoRow) ? r2.x : row;
-  row = (k2.y == remote && r2.y != kNoRow) ? r2.y : row;
-  row = (k2.z == remote && r2.z != kNoRow) ? r2.z : row;
-  row = (k2.w == remote && r2.w != kNoRow) ? r2.w : row;
+  row = k1.x == remote ? r1.x : row;
+  row = k1.y == remote ? r1.y : row;
+  row = k1.z == remote ? r1.z : row;
+  row = k1.w == remote ? r1.w : row;
+  row = k2.x == remote ? r2.x : row;
+  row = k2.y == remote ? r2.y : row;
+  row = k2.z == remote ? r2.z : row;
+  row = k2.w == remote ? r2.w : row;
   return row;
 }
 
@@ -198,6 +261,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   any_overflow = __any(any_overflow);
   for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
     const HttpPart pt = T.parts[pg.part_begin + pi];
+    const bool cls = pt.mode == kPartClass;  // uniform
     const uint32_t* __restrict__ cells = rebased ? blk : T.cells + pt.walk_off;
     uint32_t st[K];
 #pragma unroll
@@ -217,10 +281,18 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
 #pragma unroll
           for (int j = 0; j < K; ++j) nxt[j] = tile_unit(tr[j], tu[j], u + 2, lane);
         }
+        if (cls) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+          for (int k = 0; k < 16; ++k) {
 #pragma unroll
-          for (int j = 0; j < K; ++j) st[j] = comb_step(cells, pt.dead, st[j], get_byte(cur[j], k));
+            for (int j = 0; j < K; ++j) st[j] = comb_step_cls(cells, pt.dead, st[j], get_byte(cur[j], k));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) st[j] = comb_step(cells, pt.dead, st[j], get_byte(cur[j], k));
+          }
         }
         bool alive = false;
 #pragma unroll
@@ -233,13 +305,16 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     if (any_overflow) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const uint32_t sa = walk_overflow(cells, pt.dead, pt.start, arena, arena_bytes, meta[j], overflow[j]);
+        const uint32_t sa =
+            cls ? walk_overflow<true>(cells, pt.dead, pt.start, arena, arena_bytes, meta[j], overflow[j])
+                : walk_overflow<false>(cells, pt.dead, pt.start, arena, arena_bytes, meta[j], overflow[j]);
         if (overflow[j]) st[j] = sa;
       }
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t lab = counted[j] ? (cells[st[j] - 1] >> 16) : 0xFFFFu;
+      const uint32_t lab =
+          counted[j] ? (cls ? state_label<true>(cells, st[j]) : state_label<false>(cells, st[j])) : 0xFFFFu;
       if (lab != 0xFFFFu) hit[j] = min(hit[j], first_meet(blk, pt.acc_off + lab * 2 * W, row[j], W));
     }
   }
@@ -279,7 +354,7 @@ __device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units,
 // walk, only for lanes that reached an accepting state.  No early exit:
 // lanes whose string ended (or died) keep stepping through zero padding or
 // the dead state, which cannot change their verdict.
-template <int N>
+template <int N, bool kCls>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
                                             uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
                                             const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
@@ -287,9 +362,13 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
                                             uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane,
                                             uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits) {
   const uint2 meta = cur.meta;
-  uint4 unit[N > 0 ? N : 1];
+  // a rolling window of kWin units: unit k + kWin loads when unit k starts
+  // walking (16 dependent steps cover its latency), so long tiles hold
+  // kWin units in registers, not N
+  constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;
+  uint4 unit[kWin];
 #pragma unroll
-  for (int k = 0; k < N; ++k) unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : tr.units[k * kWave + lane];
+  for (int k = 0; k < kWin && k < N; ++k) unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : tr.units[k * kWave + lane];
   if (has_next) tile_prefetch(trn, nunits, lane, nxt);
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t flags = meta.y >> 24;
@@ -299,20 +378,41 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   uint32_t st = pt.start;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
+    const uint4 u = unit[k % kWin];
+    if (k + kWin < N) unit[k % kWin] = tr.units[(k + kWin) * kWave + lane];
+    if (kCls) {
+      st = lds_cls_step16<0>(dead, st, u);
+      st = lds_cls_step16<1>(dead, st, u);
+      st = lds_cls_step16<2>(dead, st, u);
+      st = lds_cls_step16<3>(dead, st, u);
+      st = lds_cls_step16<4>(dead, st, u);
+      st = lds_cls_step16<5>(dead, st, u);
+      st = lds_cls_step16<6>(dead, st, u);
+      st = lds_cls_step16<7>(dead, st, u);
+      st = lds_cls_step16<8>(dead, st, u);
+      st = lds_cls_step16<9>(dead, st, u);
+      st = lds_cls_step16<10>(dead, st, u);
+      st = lds_cls_step16<11>(dead, st, u);
+      st = lds_cls_step16<12>(dead, st, u);
+      st = lds_cls_step16<13>(dead, st, u);
+      st = lds_cls_step16<14>(dead, st, u);
+      st = lds_cls_step16<15>(dead, st, u);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) st = comb_step(blk, dead, st, get_byte(unit[k], i));
+      for (int i = 0; i < 16; ++i) st = step<kCls>(blk, dead, st, get_byte(u, i));
+    }
   }
   if (__any(overflow)) {
-    const uint32_t sa = walk_overflow(blk, dead, pt.start, arena, arena_bytes, meta, overflow);
+    const uint32_t sa = walk_overflow<kCls>(blk, dead, pt.start, arena, arena_bytes, meta, overflow);
     if (overflow) st = sa;
   }
   uint32_t hit = kNoHit;
   if (counted) {
-    const uint32_t lab = blk[st - 1] >> 16;
+    const uint32_t lab = state_label<kCls>(blk, st);
     const bool always = pg.flags & kProgHasAlways;
     if (lab != 0xFFFFu || always) {
       const uint32_t row = remote_row(blk, pg, meta.x);
-      if (lab != 0xFFFFu) hit = first_meet(blk, pt.acc_off + lab * 2 * pg.mask_words, row, pg.mask_words);
+      if (lab != 0xFFFFu) hit = first_meet(blk, pt.acc_off + mul24(lab, 2 * pg.mask_words), row, pg.mask_words);
       if (always) hit = min(hit, first_meet(blk, pg.always_off, row, pg.mask_words));
     }
   }
@@ -321,6 +421,43 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   out[(size_t)t * kWave + lane] = (uint8_t)verdict;
   n_allow += counted && verdict;
   n_deny += counted && !verdict;
+}
+
+// A wave's tiles t, t + nw, ... < tend of a one-part program whose block is
+// in LDS: each tile's walk specialized on its string units (wave-uniform).
+template <bool kCls>
+__device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg& pg, const HttpPart& pt, uint32_t prog,
+                                               const uint32_t* __restrict__ lcells, const uint8_t* __restrict__ tiles,
+                                               const HttpTile* __restrict__ ttab, uint32_t t, uint32_t tend,
+                                               uint32_t nw, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                               uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
+                                               uint32_t& n_deny, uint32_t* s_hits) {
+  if (t >= tend) return;
+  HttpTile tt = ttab[t];
+  TileRef tb = tile_ref(tiles, tt);
+  TilePre pre;
+  tile_prefetch(tb, tt.units, lane, pre);
+  for (; t < tend; t += nw) {
+    const bool has_next = t + nw < tend;
+    const HttpTile ttn = ttab[has_next ? t + nw : t];
+    const TileRef tbn = tile_ref(tiles, ttn);
+    TilePre nxt = pre;
+    switch (tt.units) {  // wave-uniform
+#define CG_TILE_N(n)                                                                                                \
+  case n:                                                                                                           \
+    http_tile_n<n, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes, out, \
+                         lane, n_allow, n_deny, s_hits);                                                            \
+    break;
+      CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
+      default:
+        http_tile_n<8, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes,
+                             out, lane, n_allow, n_deny, s_hits);
+#undef CG_TILE_N
+    }
+    tt = ttn;
+    tb = tbn;
+    pre = nxt;
+  }
 }
 
 // End of a workgroup's run of chunks of program `prog`: wave totals are
@@ -435,34 +572,12 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       }
     } else if (pg.part_count == 1) {
       const HttpPart pt = T.parts[pg.part_begin];
-      uint32_t t = ch.first_tile + wave;
-      if (t < tend) {
-        HttpTile tt = ttab[t];
-        TileRef tb = tile_ref(tiles, tt);
-        TilePre pre;
-        tile_prefetch(tb, tt.units, lane, pre);
-        for (; t < tend; t += nw) {
-          const bool has_next = t + nw < tend;
-          const HttpTile ttn = ttab[has_next ? t + nw : t];
-          const TileRef tbn = tile_ref(tiles, ttn);
-          TilePre nxt = pre;
-          switch (tt.units) {  // wave-uniform
-#define CG_TILE_N(n)                                                                                                 \
-  case n:                                                                                                            \
-    http_tile_n<n>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes, out, lane, \
-                   n_allow, n_deny, s_hits);                                                                         \
-    break;
-            CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
-            default:
-              http_tile_n<8>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes,
+      if (pt.mode == kPartClass)
+        one_part_tiles<true>(T, pg, pt, prog, lcells, tiles, ttab, ch.first_tile + wave, tend, nw, arena, arena_bytes,
                              out, lane, n_allow, n_deny, s_hits);
-#undef CG_TILE_N
-          }
-          tt = ttn;
-          tb = tbn;
-          pre = nxt;
-        }
-      }
+      else
+        one_part_tiles<false>(T, pg, pt, prog, lcells, tiles, ttab, ch.first_tile + wave, tend, nw, arena,
+                              arena_bytes, out, lane, n_allow, n_deny, s_hits);
     } else {
       // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)
       for (uint32_t t0 = ch.first_tile + wave; t0 < tend; t0 += kTilesPerWave * nw) {
@@ -485,9 +600,12 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
     uint8_t* __restrict__ out) {
+  // dynamic LDS only, so the program block starts at LDS address 0 (a
+  // class-mode step's address is then just state + code): [block:
+  // T.lds_cells][rule hits: kLdsRuleHits][allowed, denied]
   extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
-  __shared__ uint32_t s_cnt[2];
-  __shared__ uint32_t s_hits[kLdsRuleHits];
+  uint32_t* s_hits = lcells + T.lds_cells;
+  uint32_t* s_cnt = s_hits + kLdsRuleHits;
   for (uint32_t i = threadIdx.x; i < kLdsRuleHits; i += blockDim.x) s_hits[i] = 0;
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
@@ -513,7 +631,7 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   // from several threads)
   int dev = 0;
   (void)hipGetDevice(&dev);
-  const size_t lds = (size_t)t.lds_cells * 4;
+  const size_t lds = ((size_t)t.lds_cells + kLdsRuleHits + 2) * 4;
   int occ = 1;
   {
     static std::mutex mu;
@@ -521,8 +639,7 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
     static std::set<int> attr_set;
     std::lock_guard<std::mutex> lk(mu);
     if (attr_set.insert(dev).second)
-      (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024 - 64 - 4 * kLdsRuleHits);
+      (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     auto it = occ_cache.find({dev, lds});
     if (it == occ_cache.end()) {
       // one resident wave of workgroups: as many per CU as LDS and registers
