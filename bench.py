@@ -332,7 +332,8 @@ def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False):
         else:
             groups.append([int(prog), int(first), int(nt)])
     kib = ttab[:, 0].astype(np.int64)  # tile offsets in 512-byte granules (HttpTile.at)
-    units = ttab[:, 1].astype(np.int64)
+    units_field = ttab[:, 1].astype(np.int64)  # HttpTile.units: units | last-unit bytes << 16
+    units = units_field & 0xFFFF
     span = 1 + 2 * units               # granules per tile: meta block + 1 KiB units
     big, new_tt, placed, pos, kpos = [], [], [], 0, 0
     for prog, first, nt in groups:
@@ -342,7 +343,7 @@ def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False):
         g_kib = int(kib[first + nt - 1] + span[first + nt - 1] - kib[first])
         rel = kib[first:first + nt] - kib[first]
         for r in range(reps):
-            new_tt.append(np.stack([kpos + r * g_kib + rel, units[first:first + nt]], axis=1))
+            new_tt.append(np.stack([kpos + r * g_kib + rel, units_field[first:first + nt]], axis=1))
         placed.append((first, nt, pos, int(kib[first]), g_kib, kpos))
         pos += run
         kpos += reps * g_kib

@@ -143,7 +143,13 @@ struct HttpProg {
   uint32_t rtab_nb;         // buckets (any count)
   uint32_t rule_base;       // this program's first per-rule hit counter
   uint32_t nrules;          // mask bits = rules (HttpSnapshot::rule_info)
+  // kProgRemoteDirect: identities rdir_base .. rdir_base + rdir_len - 1 map
+  // to their mask row through a u16 array at block offset rdir_off (others:
+  // default_remote) — one LDS read instead of the bucket search
+  uint32_t rdir_base, rdir_len, rdir_off, pad;
 };
+constexpr uint32_t kProgRemoteDirect = 16;
+constexpr uint32_t kRdirMaxSpan = 8192;
 // Per-rule hit counters a workgroup keeps in LDS for its current program
 // (programs with more rules count straight into global memory).
 constexpr uint32_t kLdsRuleHits = 512;
@@ -200,8 +206,12 @@ struct HttpBatchHeader {
 };
 struct HttpTile {
   uint32_t at;     // tile data at tiles_off + at * 512: the 512-byte meta block
-  uint32_t units;  // (8 bytes per lane), then `units` 1 KiB string units (0..8)
+  uint32_t units;  // (8 bytes per lane), then `units` 1 KiB string units (0..8) in bits 0..15;
+                   // bits 16..31: string bytes its lanes hold in the last unit (1..16), the
+                   // rest of that unit being padding the walk may skip (0: walk all 16)
 };
+CG_HD inline uint32_t tile_units(const HttpTile& t) { return t.units & 0xFFFFu; }
+CG_HD inline uint32_t tile_tail(const HttpTile& t) { return t.units >> 16; }
 struct HttpChunk {
   uint32_t prog;
   uint32_t first_tile;

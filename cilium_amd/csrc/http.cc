@@ -759,6 +759,27 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
         }
       const uint32_t cap = 4 * nb;
       S.total_remote_slots += cap;
+      // identities over a short span (identities are allocated densely): a
+      // direct u16 row array as well, which the kernel prefers
+      if (!ent.empty()) {
+        uint32_t lo = ent[0].first, hi = ent[0].first;
+        bool rows16 = pg.default_remote < 0x10000;
+        for (const auto& e : ent) {
+          lo = std::min(lo, e.first);
+          hi = std::max(hi, e.first);
+          rows16 &= e.second < 0x10000;
+        }
+        if (rows16 && hi - lo < kRdirMaxSpan) {
+          const uint32_t len = hi - lo + 1;
+          std::vector<uint16_t> t(len + 1, (uint16_t)pg.default_remote);
+          for (const auto& e : ent) t[e.first - lo] = (uint16_t)e.second;
+          pg.rdir_base = lo;
+          pg.rdir_len = len;
+          pg.rdir_off = (uint32_t)S.cells.size() - pg.cell_begin;
+          for (uint32_t k = 0; k < len; k += 2) S.cells.push_back((uint32_t)t[k] | (uint32_t)t[k + 1] << 16);
+          pg.flags |= kProgRemoteDirect;
+        }
+      }
     }
     S.cells.push_back(0);  // spare words: the kernel reads two mask words whatever the width
     S.cells.push_back(0);

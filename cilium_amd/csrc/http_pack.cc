@@ -198,11 +198,26 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
     HttpTile& t = ttab[slot_of[i] / CG_HTTP_TILE];
     t.units = std::max(t.units, walked_units(i));
   }
+  // the bytes the lanes of a tile hold in its last unit (padding past the
+  // longest one need not be walked: comb.h, padding never changes a label)
+  {
+    std::vector<uint32_t> tail(ttab.size(), 0);
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t wu = walked_units(i);
+      HttpTile& t = ttab[slot_of[i] / CG_HTTP_TILE];
+      if (wu && wu == t.units) {
+        uint32_t& tl = tail[slot_of[i] / CG_HTTP_TILE];
+        tl = std::max<uint32_t>(tl, (uint32_t)(str_len(i) - 16 * (wu - 1)));
+      }
+    }
+    for (size_t k = 0; k < ttab.size(); ++k)
+      if (ttab[k].units) ttab[k].units |= (tail[k] ? tail[k] : 16u) << 16;
+  }
   uint64_t gran = 0;
   for (auto& t : ttab) {
     if (gran > 0xFFFFFFFFull) fail(CG_INVALID_ARGUMENT, "batch beyond 2 TiB");
     t.at = (uint32_t)gran;
-    gran += 1 + 2 * t.units;
+    gran += 1 + 2 * tile_units(t);
   }
   const size_t max_tiles = http_batch_slots(s, n) / CG_HTTP_TILE;
   const size_t hdr = header_bytes(max_tiles);
@@ -324,11 +339,16 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         if ((size_t)off + 4 + len > arena_len) continue;
         str.assign((const char*)arena + off + 4, len);
       } else {
-        for (uint32_t u = 0; u < ttab[sl / CG_HTTP_TILE].units; ++u) str.append((const char*)unit_ptr(sl, u + 1), 16);
+        for (uint32_t u = 0; u < tile_units(ttab[sl / CG_HTTP_TILE]); ++u)
+          str.append((const char*)unit_ptr(sl, u + 1), 16);
       }
       const uint32_t* blk = s.cells.data() + pg.cell_begin;
       auto bmask = [&](uint32_t o, uint32_t w) { return (uint64_t)blk[o + 2 * w] | (uint64_t)blk[o + 2 * w + 1] << 32; };
       uint32_t roff = pg.default_remote;
+      if (pg.flags & kProgRemoteDirect) {
+        if (remote - pg.rdir_base < pg.rdir_len)
+          roff = ((const uint16_t*)(s.cells.data() + pg.cell_begin + pg.rdir_off))[remote - pg.rdir_base];
+      } else
       for (uint32_t bk : {rtab_b1(remote, pg.rtab_nb), rtab_b2(remote, pg.rtab_nb)})
         for (uint32_t sl = 0; sl < 4; ++sl) {
           const uint32_t* b = blk + pg.rtab_off + kRtabBucketCells * bk;

@@ -167,6 +167,12 @@ __device__ __forceinline__ uint32_t walk_overflow(const uint32_t* __restrict__ c
 // Block offset of the PNPR mask of remote identity `remote`: the program's
 // remote table (open addressing, {identity, mask offset} slots).
 __device__ __forceinline__ uint32_t remote_row(const uint32_t* __restrict__ blk, const HttpProg& pg, uint32_t remote) {
+  if (pg.flags & kProgRemoteDirect) {  // uniform: the direct array (dev_types.h)
+    const uint32_t d = remote - pg.rdir_base;
+    const bool in = d < pg.rdir_len;
+    const uint32_t v = reinterpret_cast<const uint16_t*>(blk + pg.rdir_off)[in ? d : 0];
+    return in ? v : pg.default_remote;
+  }
   // both candidate buckets read together (dev_types.h rtab_b1/rtab_b2)
   const uint32_t h = rtab_hash(remote);
   const uint32_t* b1 = blk + pg.rtab_off + kRtabBucketCells * rtab_b1h(h, pg.rtab_nb);
@@ -211,12 +217,14 @@ __device__ __forceinline__ uint32_t first_meet(const uint32_t* __restrict__ blk,
 // into global memory.  One atomic per run instead of 64 same-address ones.
 __device__ __forceinline__ void count_hits(const HttpDev& T, const HttpProg& pg, uint32_t hit, uint32_t* s_hits,
                                            uint32_t lane) {
-  const uint32_t prev = __shfl_up(hit, 1, kWave);
-  const bool head = lane == 0 || prev != hit;
+  // the previous lane's hit: one DPP wave shift (lane 0 gets ~hit, a head)
+  const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)~hit, (int)hit, 0x138 /* wave_shr:1 */, 0xF, 0xF,
+                                                              false);
+  const bool head = prev != hit;
   const unsigned long long heads = __ballot(head);
   if (head && hit != kNoHit) {
-    const unsigned long long later = heads & ~((2ULL << lane) - 1);  // heads of the runs after this one
-    const uint32_t len = (later ? (uint32_t)__builtin_ctzll(later) : 64u) - lane;
+    const unsigned long long later = heads >> lane >> 1;  // heads of the runs after this one
+    const uint32_t len = later ? (uint32_t)__builtin_ctzll(later) + 1u : 64u - lane;
     if (s_hits && pg.nrules <= kLdsRuleHits) atomicAdd(&s_hits[hit], len);
     else atomicAdd(&T.rule_hits[pg.rule_base + hit], (unsigned long long)len);
   }
@@ -248,7 +256,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   for (int j = 0; j < K; ++j) {
     const HttpTile tt = ttab[tile[j]];
     tr[j] = tile_ref(tiles, tt);
-    tu[j] = valid[j] ? tt.units : 0u;
+    tu[j] = valid[j] ? tile_units(tt) : 0u;
     units = max(units, tu[j]);
     meta[j] = tr[j].meta[lane];
     const uint32_t flags = meta[j].y >> 24;
@@ -358,7 +366,7 @@ template <int N, bool kCls>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
                                             uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
                                             const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
-                                            TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
+                                            uint32_t tail, TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
                                             uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane,
                                             uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits) {
   const uint2 meta = cur.meta;
@@ -380,26 +388,39 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   for (int k = 0; k < N; ++k) {
     const uint4 u = unit[k % kWin];
     if (k + kWin < N) unit[k % kWin] = tr.units[(k + kWin) * kWave + lane];
+    // the last unit: only the 4-byte groups holding some lane's string
+    // (tail, wave-uniform), the rest is padding
+    const bool last = k == N - 1;
     if (kCls) {
       st = lds_cls_step16<0>(dead, st, u);
       st = lds_cls_step16<1>(dead, st, u);
       st = lds_cls_step16<2>(dead, st, u);
       st = lds_cls_step16<3>(dead, st, u);
-      st = lds_cls_step16<4>(dead, st, u);
-      st = lds_cls_step16<5>(dead, st, u);
-      st = lds_cls_step16<6>(dead, st, u);
-      st = lds_cls_step16<7>(dead, st, u);
-      st = lds_cls_step16<8>(dead, st, u);
-      st = lds_cls_step16<9>(dead, st, u);
-      st = lds_cls_step16<10>(dead, st, u);
-      st = lds_cls_step16<11>(dead, st, u);
-      st = lds_cls_step16<12>(dead, st, u);
-      st = lds_cls_step16<13>(dead, st, u);
-      st = lds_cls_step16<14>(dead, st, u);
-      st = lds_cls_step16<15>(dead, st, u);
+      if (!last || tail > 4) {
+        st = lds_cls_step16<4>(dead, st, u);
+        st = lds_cls_step16<5>(dead, st, u);
+        st = lds_cls_step16<6>(dead, st, u);
+        st = lds_cls_step16<7>(dead, st, u);
+      }
+      if (!last || tail > 8) {
+        st = lds_cls_step16<8>(dead, st, u);
+        st = lds_cls_step16<9>(dead, st, u);
+        st = lds_cls_step16<10>(dead, st, u);
+        st = lds_cls_step16<11>(dead, st, u);
+      }
+      if (!last || tail > 12) {
+        st = lds_cls_step16<12>(dead, st, u);
+        st = lds_cls_step16<13>(dead, st, u);
+        st = lds_cls_step16<14>(dead, st, u);
+        st = lds_cls_step16<15>(dead, st, u);
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) st = step<kCls>(blk, dead, st, get_byte(u, i));
+      for (int g = 0; g < 4; ++g) {
+        if (last && g > 0 && tail <= 4u * g) break;
+#pragma unroll
+        for (int i = 4 * g; i < 4 * g + 4; ++i) st = step<kCls>(blk, dead, st, get_byte(u, i));
+      }
     }
   }
   if (__any(overflow)) {
@@ -436,21 +457,21 @@ __device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg&
   HttpTile tt = ttab[t];
   TileRef tb = tile_ref(tiles, tt);
   TilePre pre;
-  tile_prefetch(tb, tt.units, lane, pre);
+  tile_prefetch(tb, tile_units(tt), lane, pre);
   for (; t < tend; t += nw) {
     const bool has_next = t + nw < tend;
     const HttpTile ttn = ttab[has_next ? t + nw : t];
     const TileRef tbn = tile_ref(tiles, ttn);
     TilePre nxt = pre;
-    switch (tt.units) {  // wave-uniform
+    switch (tile_units(tt)) {  // wave-uniform
 #define CG_TILE_N(n)                                                                                                \
   case n:                                                                                                           \
-    http_tile_n<n, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes, out, \
+    http_tile_n<n, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t, arena, arena_bytes, out, \
                          lane, n_allow, n_deny, s_hits);                                                            \
     break;
       CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
       default:
-        http_tile_n<8, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, ttn.units, nxt, t, arena, arena_bytes,
+        http_tile_n<8, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t, arena, arena_bytes,
                              out, lane, n_allow, n_deny, s_hits);
 #undef CG_TILE_N
     }

@@ -115,7 +115,12 @@ def _rand_matcher(rng):
     return {"name": name, "value": rng.choice(VALUES), "regex": rng.random() < 0.5}
 
 
-def _rand_policy(rng, n_pol=3):
+# remote identity universes: a dense span (the kernel's direct identity → row
+# array) and one spread past kRdirMaxSpan (the 2-choice bucket table)
+ID_SETS = {"dense": [1, 2, 3, 4], "spread": [1, 2, 70000, 16777300]}
+
+
+def _rand_policy(rng, n_pol=3, ids=(1, 2, 3, 4)):
     pols = []
     for pi in range(n_pol):
         p = {"name": f"p{pi}", "policy": pi}
@@ -127,7 +132,7 @@ def _rand_policy(rng, n_pol=3):
             for port in ports:
                 rules = []
                 for _ in range(rng.randint(0, 3)):
-                    r = {"remote_policies": sorted(rng.sample([1, 2, 3, 4], rng.randint(0, 2)))}
+                    r = {"remote_policies": sorted(rng.sample(list(ids), rng.randint(0, 2)))}
                     if rng.random() < 0.85:
                         r["http_rules"] = {"http_rules": [
                             {"headers": [_rand_matcher(rng) for _ in range(rng.randint(0, 3))]}
@@ -139,7 +144,7 @@ def _rand_policy(rng, n_pol=3):
     return pols
 
 
-def _rand_requests(rng, n, n_pol):
+def _rand_requests(rng, n, n_pol, ids=(1, 2, 3, 4)):
     reqs = []
     for _ in range(n):
         hs = []
@@ -164,16 +169,17 @@ def _rand_requests(rng, n, n_pol):
     return dict(policy=np.array([rng.randint(0, n_pol) for _ in range(n)], np.uint32),  # n_pol = unknown
                 ingress=np.array([rng.randint(0, 1) for _ in range(n)], np.uint8),
                 port=np.array([rng.choice([80, 81, 8080, 9]) for _ in range(n)], np.uint16),
-                remote=np.array([rng.randint(0, 5) for _ in range(n)], np.uint32),
+                remote=np.array([rng.choice([0, 5] + list(ids)) for _ in range(n)], np.uint32),
                 hdr_blob=np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy(),
                 hdr_off=np.array(off, np.uint64))
 
 
+@pytest.mark.parametrize("ids", sorted(ID_SETS))
 @pytest.mark.parametrize("seed", range(12))
-def test_http_random_policies(host, seed):
+def test_http_random_policies(host, seed, ids):
     rng = random.Random(seed)
-    pols = _rand_policy(rng)
-    rq = _rand_requests(rng, 600, len(pols))
+    pols = _rand_policy(rng, ids=ID_SETS[ids])
+    rq = _rand_requests(rng, 600, len(pols), ids=ID_SETS[ids])
     try:
         orc = oracle.HttpOracle(pols)
     except ValueError:

@@ -247,6 +247,52 @@ def test_http_10k_parity(gpu):
     assert 0.3 < got.mean() < 0.95
 
 
+@pytest.mark.parametrize("ids", ["dense", "spread"])
+@pytest.mark.parametrize("seed", range(6))
+def test_http_random_policies(gpu, seed, ids):
+    """Random policies (header matchers of every kind, ports, remotes) on the
+    GPU: both class-mode and byte-mode programs, and both remote lookups
+    (the direct identity array for a dense span, the bucket table for a
+    spread one)."""
+    import random
+    from test_cpu_differential import ID_SETS, _rand_policy, _rand_requests
+    rng = random.Random(100 + seed)
+    pols = _rand_policy(rng, ids=ID_SETS[ids])
+    rq = _rand_requests(rng, 3000, len(pols), ids=ID_SETS[ids])
+    try:
+        orc = oracle.HttpOracle(pols)
+    except ValueError:
+        return
+    gpu.update_http_policy(pols)
+    assert np.array_equal(gpu.http_verdicts(gpu.pack_http(**rq)), orc.eval(**rq))
+
+
+def test_http_many_byte_classes(gpu):
+    """A program over more than 64 byte classes keeps byte-indexed comb rows
+    (the class-code packing needs a class code in one byte): 90 exact paths
+    of distinct characters, requests hitting and missing them."""
+    chars = [chr(c) for c in range(0x21, 0x7B) if chr(c) not in "\\"][:90]
+    rules = [{"headers": [{"name": ":path", "exact_match": "/" + c + c}]} for c in chars]
+    pols = [{"name": "many", "policy": 0, "ingress_per_port_policies": [
+        {"port": 80, "protocol": "TCP", "rules": [{"remote_policies": [], "http_rules": {"http_rules": rules}}]}]}]
+    rng = np.random.default_rng(3)
+    reqs = []
+    for i in range(4000):
+        c, d = chars[int(rng.integers(0, len(chars)))], chars[int(rng.integers(0, len(chars)))]
+        reqs.append([(":path", "/" + c + (c if i % 2 else d)), (":method", "GET")])
+    parts, off = [], [0]
+    for hs in reqs:
+        b = b"".join(k.encode() + b"\0" + v.encode() + b"\0" for k, v in hs)
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    n = len(reqs)
+    rq = dict(policy=np.zeros(n, np.uint32), ingress=np.ones(n, np.uint8), port=np.full(n, 80, np.uint16),
+              remote=np.arange(n, dtype=np.uint32) % 7, hdr_blob=np.frombuffer(b"".join(parts), np.uint8).copy(),
+              hdr_off=np.array(off, np.uint64))
+    got = _http_check(gpu, pols, rq)
+    assert got.any() and not got.all()
+
+
 def test_http_overflow_records(gpu):
     pols = synth.starwars_policy()
     rq = synth.starwars_requests(3000, seed=11)

@@ -35,18 +35,9 @@ NOCTR = ("""  count_hits(T, pg, hit, s_hits, lane);
   out[(size_t)t * kWave + lane] = (uint8_t)verdict;""", """  out[(size_t)t * kWave + lane] = (uint8_t)verdict;""")
 VARIANTS = {
     "base": [],
-    "nowalk": [NOWALK],
-    "early": [EARLY],
-    "noctr": [NOCTR],
-    "pnprtags": [("http.cc", "          urules.push_back({fd, {tag}});", "          urules.push_back({fd, {pnpr_first[j]}});"),
-                 ("http.cc", "          urules[it->second].tags.push_back(tag);",
-                  "          urules[it->second].tags.push_back(pnpr_first[j]);")],
-    "hotdata": [("        const TileRef tb = tile_ref(tiles, tt);",
-                 "        const TileRef tb = tile_ref(tiles, ttab[ch.first_tile]);")],
-    "pre1": [("constexpr int kPre = 2;", "constexpr int kPre = 1;")],
-    "pre3": [("constexpr int kPre = 2;", "constexpr int kPre = 3;")],
-    "deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
-    "deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
+    "nodirect": [("http.cc", "        if (rows16 && hi - lo < kRdirMaxSpan) {", "        if (false) {")],
+    "nocount": [("kernels_http.hip", "  count_hits(T, pg, hit, s_hits, lane);\n  out[(size_t)t * kWave + lane] = (uint8_t)verdict;",
+                 "  out[(size_t)t * kWave + lane] = (uint8_t)verdict;")],
 }
 # Kafka wire decode variants (kernels_kafka.hip): thread count / LDS stage.
 def _kw(threads, stage):
