@@ -201,13 +201,38 @@ __device__ __forceinline__ unsigned long long blk_word(const uint32_t* __restric
 // share, or kNoHit: the first rule that allows the request, in Envoy's
 // evaluation order (http.cc build_prog).
 constexpr uint32_t kNoHit = 0xFFFFFFFFu;
+template <int W>
+__device__ __forceinline__ uint32_t first_meet_w(const uint32_t* __restrict__ blk, uint32_t a, uint32_t row) {
+  // every word read up front, no per-lane exits: the lowest word with a
+  // shared bit wins
+  unsigned long long x[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) x[w] = blk_word(blk, a, w) & blk_word(blk, row, w);
+  unsigned long long sel = 0;
+  uint32_t base = 0;
+#pragma unroll
+  for (int w = W - 1; w >= 0; --w) {
+    const bool nz = x[w] != 0;
+    sel = nz ? x[w] : sel;
+    base = nz ? 64u * w : base;
+  }
+  return sel ? base + (uint32_t)__builtin_ctzll(sel) : kNoHit;
+}
+
 __device__ __forceinline__ uint32_t first_meet(const uint32_t* __restrict__ blk, uint32_t a, uint32_t row,
                                                uint32_t W) {
-  for (uint32_t w = 0; w < W; ++w) {
-    const unsigned long long x = blk_word(blk, a, w) & blk_word(blk, row, w);
-    if (x) return w * 64 + (uint32_t)__builtin_ctzll(x);
+  switch (W) {  // uniform
+    case 1: return first_meet_w<1>(blk, a, row);
+    case 2: return first_meet_w<2>(blk, a, row);
+    case 3: return first_meet_w<3>(blk, a, row);
+    case 4: return first_meet_w<4>(blk, a, row);
+    default:
+      for (uint32_t w = 0; w < W; ++w) {
+        const unsigned long long x = blk_word(blk, a, w) & blk_word(blk, row, w);
+        if (x) return w * 64 + (uint32_t)__builtin_ctzll(x);
+      }
+      return kNoHit;
   }
-  return kNoHit;
 }
 
 // The first-match hits of a wave's 64 requests (hit = rule bit, or kNoHit),
