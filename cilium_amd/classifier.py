@@ -134,14 +134,20 @@ class Classifier:
             hdr_blob = np.zeros(1, np.uint8)
         used = C.c_size_t()
         nslots = C.c_size_t()
-        N.check(N.lib.cg_http_pack(self.h, n, _p(policy), _p(ingress), _p(port), _p(remote), _p(hdr_blob),
-                                   _p(hdr_off), None, 0, None, C.byref(nslots), None, 0, C.byref(used)))
-        batch = np.zeros(N.lib.cg_http_batch_bytes(self.h, n), np.uint8)
-        order = np.zeros(max(N.lib.cg_http_batch_slots(self.h, n), 1), np.uint32)
-        arena = np.zeros(max(used.value, 16), np.uint8)
+        # one packing pass: the overflow arena sized by a bound (a request's
+        # string is at most its header bytes + a marker and a separator per
+        # walked field; an entry adds a 4-byte length and 16-byte alignment),
+        # allocated without touching its pages, then trimmed
+        stats = (C.c_uint64 * 12)()
+        N.check(N.lib.cg_http_policy_stats(self.h, stats, 12))
+        cap = (int(hdr_off[n]) - int(hdr_off[0]) if n else 0) + n * (int(stats[4]) + 24) + 16
+        arena = np.empty(cap, np.uint8)
+        batch = np.empty(N.lib.cg_http_batch_bytes(self.h, n), np.uint8)
+        order = np.empty(max(N.lib.cg_http_batch_slots(self.h, n), 1), np.uint32)
         N.check(N.lib.cg_http_pack(self.h, n, _p(policy), _p(ingress), _p(port), _p(remote), _p(hdr_blob),
                                    _p(hdr_off), _p(batch), batch.nbytes, _p(order), C.byref(nslots), _p(arena),
                                    arena.nbytes, C.byref(used)))
+        arena = arena[:max(used.value, 16)].copy()
         return HttpBatch(batch, arena, order[:nslots.value], nslots.value, n)
 
     @staticmethod

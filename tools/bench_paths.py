@@ -224,6 +224,50 @@ def bench_kafka_wire(torch, dev, stream, cl, args, threads):
     return out
 
 
+def bench_http_host(torch, dev, stream, cl, args, threads):
+    """Config 5 through the host entry points: cg_http_pack (CPU, the
+    packer: field extraction, program lookup, class coding, tile layout) and
+    cg_http_verdicts_host (pinned staging → H2D → http_kernel → D2H →
+    request order).  The kernel-only rate is bench.py's line."""
+    import oracle
+    from cilium_amd import synth
+    pols, info = synth.http10k_rules()
+    cl.update_http_policy(pols)
+    n = 4_000_000
+    rq = synth.http10k_requests(n, info, distinct=200_000)
+    t_pack = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        b = cl.pack_http(**rq)
+        t_pack.append(time.perf_counter() - t0)
+    got = cl.http_verdicts(b)  # warm
+    t_e2e = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        got = cl.http_verdicts(b)
+        t_e2e.append(time.perf_counter() - t0)
+    sub = {k: v[:50_000] for k, v in rq.items() if k not in ("hdr_blob", "hdr_off")}
+    sub["hdr_off"] = rq["hdr_off"][:50_001]
+    sub["hdr_blob"] = rq["hdr_blob"]
+    assert np.array_equal(got[:50_000], oracle.HttpOracle(pols).eval(**sub, nthreads=threads)), \
+        "host-path verdicts differ from the oracle"
+    tp, te = min(t_pack), min(t_e2e)
+    batch_bytes = b.used_bytes() + int(b.arena.nbytes)
+    hdr_bytes = int(rq["hdr_off"][-1])
+    return {"metric": "HTTP host path, config 5: cg_http_pack + cg_http_verdicts_host", "value": n / (tp + te),
+            "unit": "verdicts/s", "n_gpus": 1, "higher_is_better": True, "data": "synthetic",
+            "pack": {"value": n / tp, "unit": "requests/s",
+                     "cores": int(os.environ.get("CILIUM_GPU_PACK_THREADS", "0")) or min(16, os.cpu_count() or 1),
+                     "header_MBps": hdr_bytes / tp / 1e6,
+                     "ms": tp * 1e3},
+            "verdicts_host": {"value": n / te, "unit": "verdicts/s", "ms": te * 1e3,
+                              "batch_bytes": batch_bytes, "staged_GBps": batch_bytes / te / 1e9,
+                              "pcie_peak_GBps": 63.0,
+                              "note": "pinned staging memcpy + H2D + kernel + D2H + request-order scatter"},
+            "config": {"workload": "BASELINE config 5 (10K-rule HTTP) requests through the host entry points",
+                       "requests": n, "header_bytes": hdr_bytes}}
+
+
 def bench_ipcache(torch, dev, stream, cl, args, threads):
     import oracle
     from cilium_amd import synth
@@ -396,7 +440,7 @@ def main():
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
-           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire}
+           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire, "httphost": bench_http_host}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()

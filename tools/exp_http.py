@@ -35,13 +35,9 @@ NOCTR = ("""  count_hits(T, pg, hit, s_hits, lane);
   out[(size_t)t * kWave + lane] = (uint8_t)verdict;""", """  out[(size_t)t * kWave + lane] = (uint8_t)verdict;""")
 VARIANTS = {
     "base": [],
-    "w3": [('kernels_http.hip', '  constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;', '  constexpr int kWin = N < 3 ? (N > 0 ? N : 1) : 3;')],
-    "w3early": [('kernels_http.hip', '  constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;', '  constexpr int kWin = N < 3 ? (N > 0 ? N : 1) : 3;'),
-                ("kernels_http.hip", "  uint32_t st = pt.start;\n#pragma unroll\n  for (int k = 0; k < N; ++k) {\n    const uint4 u = unit[k % kWin];",
-                 "  const bool direct = pg.flags & kProgRemoteDirect;\n  uint32_t row_early = 0;\n  if (direct) row_early = remote_row(blk, pg, meta.x);\n"
-                 "  uint32_t st = pt.start;\n#pragma unroll\n  for (int k = 0; k < N; ++k) {\n    const uint4 u = unit[k % kWin];"),
-                ("kernels_http.hip", "      const uint32_t row = remote_row(blk, pg, meta.x);\n      if (lab != 0xFFFFu) hit = first_meet(",
-                 "      const uint32_t row = direct ? row_early : remote_row(blk, pg, meta.x);\n      if (lab != 0xFFFFu) hit = first_meet(")],
+    "nosort": [("http_pack.cc", "  if (build) {\n    // each bucket sorted as", "  if (false) {\n    // each bucket sorted as")],
+    "lensort": [("http_pack.cc", "        if (a.pre[0] != b.pre[0]) return a.pre[0] < b.pre[0];",
+                 "        if (a.len != b.len) return a.len < b.len;\n        if (a.pre[0] != b.pre[0]) return a.pre[0] < b.pre[0];")],
 }
 # Kafka wire decode variants (kernels_kafka.hip): thread count / LDS stage.
 def _kw(threads, stage):
