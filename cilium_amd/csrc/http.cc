@@ -58,7 +58,11 @@ constexpr int kMaxPartStates = 65535;    // u16 transition entries
 // one program table per workgroup
 constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits) / 4;
 
-enum class MKind { Exact, Regex, Present, Search };
+// ListExact/ListPrefix/ListSearch (proxylib only): the field is a list of
+// escaped items, each followed by the pair {0x03, 0x14}, and every item must
+// equal / start with / contain a match of the value (memcached keys,
+// proxylib/memcached/parser.go:54-97; zero items match)
+enum class MKind { Exact, Regex, Present, Search, ListExact, ListPrefix, ListSearch };
 struct MatcherSpec {
   std::string name;  // lowercase
   MKind kind;
@@ -100,6 +104,9 @@ MatcherSpec parse_matcher(const Json& h) {
   // engine extension for proxylib parsers: an unanchored Go regexp.MatchString
   // (proxylib/r2d2/r2d2parser.go:80), compiled in MatchMode::Search
   const Json* rs = h.get("regex_search");
+  const Json* le = h.get("list_exact");
+  const Json* lp = h.get("list_prefix");
+  const Json* ls = h.get("list_search");
   const Json* val = h.get("value");
   const Json* inv = h.get("invert_match");
   if (inv && inv->type == Json::BOOL && inv->b) fail(CG_UNSUPPORTED, "invert_match");
@@ -114,6 +121,15 @@ MatcherSpec parse_matcher(const Json& h) {
   } else if (rs) {
     m.kind = MKind::Search;
     m.value = rs->as_str("regex_search");
+  } else if (le) {
+    m.kind = MKind::ListExact;
+    m.value = le->as_str("list_exact");
+  } else if (lp) {
+    m.kind = MKind::ListPrefix;
+    m.value = lp->as_str("list_prefix");
+  } else if (ls) {
+    m.kind = MKind::ListSearch;
+    m.value = ls->as_str("list_search");
   } else if (pr) {
     m.kind = MKind::Present;
   } else if (val) {
@@ -231,7 +247,7 @@ struct FieldDfaCache {
     return any_id;
   }
   int single(const MatcherSpec& m) {
-    std::string key = std::string(1, "ERPS"[(int)m.kind]) + ":" + m.value;
+    std::string key = std::string(1, "ERPSLKQ"[(int)m.kind]) + ":" + m.value;
     auto it = by_key.find(key);
     if (it != by_key.end()) return it->second;
     // Envoy values never hold 0x00-0x02 (the codec rejects them); proxylib
@@ -244,8 +260,14 @@ struct FieldDfaCache {
       case MKind::Regex: d = compile_regex(m.value, va, MatchMode::Full); break;
       case MKind::Present: d = dfa_star(va); break;
       case MKind::Search: d = compile_regex(m.value, va, MatchMode::Search); break;
+      case MKind::ListExact: d = dfa_literal(m.value, va); break;
+      case MKind::ListPrefix: d = dfa_prefix(m.value, va); break;
+      case MKind::ListSearch: d = compile_regex(m.value, va, MatchMode::Search); break;
     }
+    const bool list = m.kind == MKind::ListExact || m.kind == MKind::ListPrefix || m.kind == MKind::ListSearch;
+    if (list && !raw) fail(CG_POLICY_REJECTED, "list matchers are for proxylib policies");
     if (raw) d = dfa_escape_low(d);
+    if (list) d = dfa_list(d);
     return add(std::move(d), key);
   }
   int conj(const std::vector<const MatcherSpec*>& ms) {
@@ -784,6 +806,15 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
     S.cells.push_back(0);  // spare words: the kernel reads two mask words whatever the width
     S.cells.push_back(0);
     pg.cell_count = (uint32_t)S.cells.size() - pg.cell_begin;
+    if (getenv("CILIUM_GPU_DEBUG")) {
+      size_t comb = 0, labels = 0;
+      for (uint32_t i = 0; i < pg.part_count; ++i) {
+        comb += S.parts[pg.part_begin + i].ncells;
+        labels += parts[i].label_masks.size();
+      }
+      fprintf(stderr, "[cilium-gpu] http program %u: block %u cells (comb %zu, %zu labels x %u words, remote table %u "
+              "buckets, direct %u)\n", pid, pg.cell_count, comb, labels, 2 * pg.mask_words, pg.rtab_nb, pg.rdir_len);
+    }
     S.progs.push_back(pg);
     S.prog_key.push_back(key);
     return pid;

@@ -198,7 +198,8 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
           for (size_t k = 0; k < vlen; ++k) {
             if (v[k] <= 0x02) malformed[i] = 1;
             if (v[k] == 0x03) {
-              if (k + 1 >= vlen || v[k + 1] < 0x10 || v[k + 1] > 0x13) malformed[i] = 1;
+              // an escape pair, or the list-item separator pair {0x03, 0x14}
+              if (k + 1 >= vlen || v[k + 1] < 0x10 || v[k + 1] > 0x14) malformed[i] = 1;
               ++k;
             }
           }

@@ -6,8 +6,10 @@
 //   OnData                       connection.go:118-174 (op loop) +
 //                                r2d2/r2d2parser.go:148-199 (line framing)
 //   policy translation           proxylib/proxylib/policymap.go:118-206 with the
-//                                r2d2 (r2d2parser.go:91-123) and cassandra
-//                                (cassandraparser.go:97-131) rule parsers
+//                                r2d2 (r2d2parser.go:91-123), cassandra
+//                                (cassandraparser.go:97-131) and memcache
+//                                (memcached/parser.go:104-147) rule parsers
+//   memcache OnData              proxylib_memcache.cc (text and binary)
 //
 // The policy verdicts of every request frame found in one OnData call are
 // evaluated as one batch by http_kernel (no CPU evaluation path).
@@ -24,6 +26,7 @@
 #include "../../include/cilium_proxylib.h"
 #include "common.h"
 #include "json.h"
+#include "proxylib_memcache.h"
 
 using namespace cg;
 
@@ -38,6 +41,7 @@ struct Instance {
 struct Conn {
   std::shared_ptr<Instance> inst;
   std::string parser, policy;
+  McState mc;  // memcache parser state
   bool ingress = false;
   uint32_t src_id = 0, dst_id = 0, port = 0;
   GoSlice* orig_buf = nullptr;
@@ -161,7 +165,113 @@ std::vector<std::string> cassandra_rules(const Json* l7) {
   return out;
 }
 
-bool known_parser(const std::string& p) { return p == "r2d2" || p == "cassandra"; }
+// MemcacheOpCodeMap (memcached/parser.go:210-474): a rule command → the
+// text commands and binary opcodes it allows
+struct McCommands {
+  std::vector<std::string> text;
+  std::vector<uint8_t> binary;
+};
+const std::map<std::string, McCommands>& memcache_opcode_map() {
+  static const std::map<std::string, McCommands> m = [] {
+    std::map<std::string, McCommands> x;
+    x["add"] = {{"add"}, {2, 18}};
+    x["set"] = {{"set"}, {1, 17}};
+    x["replace"] = {{"replace"}, {3, 19}};
+    x["append"] = {{"append"}, {14, 25}};
+    x["prepend"] = {{"prepend"}, {15, 26}};
+    x["cas"] = {{"cas"}, {}};
+    x["incr"] = {{"incr"}, {5, 21}};
+    x["decr"] = {{"decr"}, {6, 22}};
+    x["storage"] = {{"add", "set", "replace", "append", "prepend", "cas", "incr", "decr"},
+                    {1, 2, 3, 5, 6, 17, 18, 19, 21, 22, 25, 26}};
+    x["get"] = {{"get", "gets"}, {0, 9, 12, 13}};
+    x["delete"] = {{"delete"}, {4, 20}};
+    x["touch"] = {{"touch"}, {28}};
+    x["gat"] = {{"gat", "gats"}, {29, 30}};
+    x["writeGroup"] = {{"add", "set", "replace", "append", "prepend", "cas", "incr", "decr", "delete", "touch"},
+                       {1, 2, 3, 4, 5, 6, 17, 18, 19, 20, 21, 22, 25, 26, 28}};
+    x["slabs"] = {{"slabs"}, {}};
+    x["lru"] = {{"lru"}, {}};
+    x["lru_crawler"] = {{"lru_crawler"}, {}};
+    x["watch"] = {{"watch"}, {}};
+    x["stats"] = {{"stats"}, {16}};
+    x["flush_all"] = {{"flush_all"}, {8, 24}};
+    x["cache_memlimit"] = {{"cache_memlimit"}, {}};
+    x["version"] = {{"version"}, {11}};
+    x["misbehave"] = {{"misbehave"}, {}};
+    x["quit"] = {{"quit"}, {7, 23}};
+    x["noop"] = {{}, {10}};
+    x["verbosity"] = {{}, {27}};
+    const char* bin_only[] = {"sasl-list-mechs", "sasl-auth", "sasl-step", "rget", "rset", "rsetq", "rappend",
+                              "rappendq", "rprepend", "rprependq", "rdelete", "rdeleteq", "rincr", "rincrq", "rdecr",
+                              "rdecrq", "set-vbucket", "get-vbucket", "del-vbucket", "tap-connect", "tap-mutation",
+                              "tap-delete", "tap-flush", "tap-opaque", "tap-vbucket-set", "tap-checkpoint-start",
+                              "tap-checkpoint-end"};
+    const uint8_t bin_code[] = {32, 33, 34, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63, 64, 65,
+                                66, 67, 68, 69, 70, 71};
+    for (size_t i = 0; i < sizeof(bin_code); ++i) x[bin_only[i]] = {{}, {bin_code[i]}};
+    return x;
+  }();
+  return m;
+}
+
+// The request fields a memcache frame is packed as: mccmd = "t" + command
+// or "b" + opcode byte, mckeys = each key then the separator pair {0x03,
+// 0x14} (values escaped, proxylib_shim OnData).
+std::string m_list(const char* kind, const std::string& v) {
+  return std::string("{\"name\":\"mckeys\",\"") + kind + "\":" + jstr(v) + "}";
+}
+
+// L7RuleParser (memcached/parser.go:104-147) → engine rules: one per allowed
+// command token (an exact mccmd) AND the key matcher.  A rule with no
+// command and no key matches every request; an unknown command with no key
+// too (commandFound false, br.empty), with a key it is a parse error.
+std::vector<std::string> memcache_rules(const Json* l7) {
+  std::vector<std::string> out;
+  for (const Json& e : l7->arr) {
+    std::string key_exact, key_prefix, key_regex;
+    bool found = false, has_regex = false;
+    const McCommands* cmds = nullptr;
+    if (const Json* r = e.get("rule"))
+      for (const auto& [k, v] : r->obj) {
+        if (k == "command") {
+          auto it = memcache_opcode_map().find(v.as_str("command"));
+          found = it != memcache_opcode_map().end();
+          cmds = found ? &it->second : nullptr;
+        } else if (k == "keyExact") {
+          key_exact = v.as_str("keyExact");
+        } else if (k == "keyPrefix") {
+          key_prefix = v.as_str("keyPrefix");
+        } else if (k == "keyRegex") {
+          key_regex = v.as_str("keyRegex");
+          has_regex = true;  // regexp.MustCompile(""): a regex that matches every key
+        } else {
+          fail(CG_POLICY_REJECTED, "Unsupported key: " + k);
+        }
+      }
+    if (!found) {
+      if (!key_exact.empty() || !key_prefix.empty() || has_regex)
+        fail(CG_POLICY_REJECTED, "command not specified but key was provided");
+      out.push_back("");  // empty rule: matches everything
+      continue;
+    }
+    // Matches: keyExact if non-empty, else keyPrefix, else the regex
+    std::string km;
+    if (!key_exact.empty()) km = m_list("list_exact", key_exact);
+    else if (!key_prefix.empty()) km = m_list("list_prefix", key_prefix);
+    else if (has_regex) km = m_list("list_search", key_regex);
+    for (const auto& t : cmds->text) out.push_back(join(km.empty() ? std::vector<std::string>{m_exact("mccmd", "t" + t)}
+                                                                   : std::vector<std::string>{m_exact("mccmd", "t" + t), km}));
+    for (uint8_t b : cmds->binary) {
+      const std::string tok = std::string("b") + (char)b;
+      out.push_back(join(km.empty() ? std::vector<std::string>{m_exact("mccmd", tok)}
+                                    : std::vector<std::string>{m_exact("mccmd", tok), km}));
+    }
+  }
+  return out;
+}
+
+bool known_parser(const std::string& p) { return p == "r2d2" || p == "cassandra" || p == "memcache"; }
 
 std::string translate(const char* json, size_t len) {
   Json root = JsonParser(json, len).parse();
@@ -205,7 +315,7 @@ std::string translate(const char* json, size_t len) {
               const Json* l7 = nullptr;
               if (const Json* lr = r.get("l7_rules")) l7 = lr->get("l7_rules");
               if (!l7p.empty() && l7 && l7->type == Json::ARR)
-                ms = l7p == "r2d2" ? r2d2_rules(l7) : cassandra_rules(l7);
+                ms = l7p == "r2d2" ? r2d2_rules(l7) : l7p == "memcache" ? memcache_rules(l7) : cassandra_rules(l7);
               std::string rr = "{";
               bool any = false;
               if (const Json* rp = r.get("remote_policies")) {
@@ -252,6 +362,99 @@ size_t inject(GoSlice* buf, const char* data, size_t n) {  // connection.go:190-
   memcpy((char*)buf->data + off, data, k);
   buf->len += (int64_t)k;
   return k;
+}
+
+// values escaped for the proxylib snapshot (bytes 0x00-0x03 → 0x03, 0x10 +
+// b): a NUL or control byte inside a field stays part of the string the
+// rules see, as in r2d2parser.go:157-183
+std::string esc(const std::string& v) {
+  std::string o;
+  o.reserve(v.size());
+  for (unsigned char ch : v) {
+    if (ch <= 0x03) {
+      o += (char)0x03;
+      o += (char)(0x10 + ch);
+    } else {
+      o += (char)ch;
+    }
+  }
+  return o;
+}
+
+std::string field(const char* name, const std::string& escaped) {
+  return std::string(name) + '\0' + escaped + '\0';
+}
+
+// PolicyMatches (connection.go:176-179) for the request records of one
+// OnData call — each record a run of field() entries — as one host-staged
+// GPU batch.  Caller holds inst.mu.  Returns false on an engine error.
+bool gpu_verdicts(Instance& inst, const Conn& c, const std::vector<std::string>& recs, std::vector<uint8_t>* allow) {
+  const size_t n = recs.size();
+  allow->assign(n, 0);
+  if (n == 0) return true;
+  uint32_t pidx = 0xFFFFFFFFu;
+  // no such policy (or none installed): PolicyMatches is false → DROP
+  if (cg_http_policy_index(inst.engine, c.policy.c_str(), &pidx) != CG_OK) return true;
+  std::vector<uint32_t> pol(n, pidx), remote(n, c.src_id);  // Matches passes SrcId
+  std::vector<uint8_t> ing(n, c.ingress ? 1 : 0);
+  std::vector<uint16_t> port(n, (uint16_t)(c.port > 0xFFFF ? 0 : c.port));
+  std::string blob;
+  std::vector<uint64_t> off{0};
+  for (const std::string& r : recs) {
+    blob += r;
+    off.push_back(blob.size());
+  }
+  if (blob.empty()) blob.push_back('\0');
+  size_t nslots = 0, used = 0;
+  int rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
+                        (const uint8_t*)blob.data(), off.data(), nullptr, 0, nullptr, &nslots, nullptr, 0, &used);
+  if (rc != CG_OK) return false;
+  std::vector<uint8_t> batch(cg_http_batch_bytes(inst.engine, n));
+  std::vector<uint32_t> order(cg_http_batch_slots(inst.engine, n) + 1);
+  std::vector<uint8_t> arena(used > 16 ? used : 16);
+  rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
+                    (const uint8_t*)blob.data(), off.data(), batch.data(), batch.size(), order.data(), &nslots,
+                    arena.data(), arena.size(), &used);
+  if (rc != CG_OK) return false;
+  rc = cg_http_verdicts_host(inst.engine, batch.data(), nslots, order.data(), n, arena.data(), arena.size(),
+                             allow->data());
+  return rc == CG_OK;
+}
+
+// A memcache request as the fields its rules are compiled over (see
+// memcache_rules): mccmd "t" + command or "b" + two hex digits of the
+// opcode, mckeys every key then the separator pair {0x03, 0x14}.
+std::string memcache_record(const McMeta& m) {
+  static const char hex[] = "0123456789abcdef";
+  std::string cmd = m.binary() ? std::string{'b', hex[m.opcode >> 4], hex[m.opcode & 15]} : "t" + m.command;
+  std::string keys;
+  for (const std::string& k : m.keys) keys += esc(k) + "\x03\x14";
+  return field("mccmd", esc(cmd)) + field("mckeys", keys);
+}
+
+// memcache OnData: a dry run on copies of the parser state collects the
+// request frames this call will decide (the frame sequence does not depend
+// on the verdicts: a denial is a DROP of the same length), one GPU batch
+// decides them, and the real run consumes the verdicts in order.
+FilterResult memcache_data(Conn& c, bool reply, bool end_stream, const GoSlice* data, GoSlice* ops) {
+  std::vector<uint8_t> allow;
+  if (!reply) {
+    McState dry = c.mc;
+    std::vector<FilterOp> scratch((size_t)(ops->cap > 0 ? ops->cap : 1));
+    GoSlice sops{scratch.data(), ops->len, ops->cap};
+    std::vector<std::string> recs;
+    memcache_on_data(dry, false, end_stream, data, &sops, nullptr, [&](const McMeta& m) {
+      recs.push_back(memcache_record(m));
+      return true;
+    });
+    Instance& inst = *c.inst;
+    std::lock_guard<std::mutex> lk(inst.mu);
+    if (!gpu_verdicts(inst, c, recs, &allow)) return FILTER_UNKNOWN_ERROR;
+  }
+  size_t next = 0;
+  return memcache_on_data(c.mc, reply, end_stream, data, ops, c.reply_buf, [&](const McMeta&) {
+    return next < allow.size() && allow[next++] != 0;
+  });
 }
 
 }  // namespace
@@ -320,7 +523,8 @@ FilterResult OnNewConnection(uint64_t instanceId, GoString proto, uint64_t conne
   if (!inst) return FILTER_INVALID_INSTANCE;
   auto c = std::make_shared<Conn>();
   c->parser = gostr(proto);
-  if (c->parser != "r2d2") return FILTER_UNKNOWN_PARSER;  // parser factories implemented here: r2d2
+  // parser factories implemented here: r2d2, memcache
+  if (c->parser != "r2d2" && c->parser != "memcache") return FILTER_UNKNOWN_PARSER;
   // net.SplitHostPort + ParseUint(port, 10, 32), port != 0 (connection.go:71-78)
   const std::string da = gostr(dstAddr);
   const size_t colon = da.rfind(':');
@@ -351,7 +555,6 @@ void Close(uint64_t connectionId) {
 }
 
 FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoSlice* data, GoSlice* filterOps) {
-  (void)endStream;
   std::shared_ptr<Conn> c;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -360,6 +563,7 @@ FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoS
     c = it->second;
   }
   if (!data || !filterOps) return FILTER_UNKNOWN_ERROR;
+  if (c->parser == "memcache") return memcache_data(*c, reply != 0, endStream != 0, data, filterOps);
   // r2d2 reads bytes.Join(dataArray) (r2d2parser.go:151)
   std::string in;
   const GoSlice* parts = static_cast<const GoSlice*>(data->data);
@@ -396,59 +600,18 @@ FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoS
   // one GPU batch for the request frames
   std::vector<uint8_t> allow(frames.size(), 1);
   std::vector<size_t> reqs;
+  std::vector<std::string> recs;
   for (size_t i = 0; i < frames.size(); ++i)
-    if (frames[i].request) reqs.push_back(i);
-  Instance& inst = *c->inst;
-  std::lock_guard<std::mutex> lk(inst.mu);
-  uint32_t pidx = 0xFFFFFFFFu;
-  if (!reqs.empty() && cg_http_policy_index(inst.engine, c->policy.c_str(), &pidx) != CG_OK) {
-    // no such policy (or none installed): PolicyMatches is false → DROP
-    for (size_t i : reqs) allow[i] = 0;
-    reqs.clear();
-  }
-  if (!reqs.empty()) {
-    const size_t n = reqs.size();
-    std::vector<uint32_t> pol(n, pidx), remote(n, c->src_id);  // Matches passes SrcId (connection.go:176-179)
-    std::vector<uint8_t> ing(n, c->ingress ? 1 : 0);
-    std::vector<uint16_t> port(n, (uint16_t)(c->port > 0xFFFF ? 0 : c->port));
-    std::string blob;
-    std::vector<uint64_t> off{0};
-    // values escaped for the proxylib snapshot (bytes 0x00-0x03 → 0x03,
-    // 0x10 + b): a NUL or control byte inside cmd/file stays part of the
-    // string the rules see, as in r2d2parser.go:157-183
-    auto esc = [](const std::string& v) {
-      std::string o;
-      for (unsigned char ch : v) {
-        if (ch <= 0x03) {
-          o += (char)0x03;
-          o += (char)(0x10 + ch);
-        } else {
-          o += (char)ch;
-        }
-      }
-      return o;
-    };
-    for (size_t i : reqs) {
-      blob += std::string("cmd") + '\0' + esc(frames[i].cmd) + '\0' + "file" + '\0' + esc(frames[i].file) + '\0';
-      off.push_back(blob.size());
+    if (frames[i].request) {
+      reqs.push_back(i);
+      recs.push_back(field("cmd", esc(frames[i].cmd)) + field("file", esc(frames[i].file)));
     }
-    if (blob.empty()) blob.push_back('\0');
-    size_t nslots = 0, used = 0;
-    int rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
-                          (const uint8_t*)blob.data(), off.data(), nullptr, 0, nullptr, &nslots, nullptr, 0, &used);
-    if (rc != CG_OK) return FILTER_UNKNOWN_ERROR;
-    std::vector<uint8_t> batch(cg_http_batch_bytes(inst.engine, n));
-    std::vector<uint32_t> order(cg_http_batch_slots(inst.engine, n) + 1);
-    std::vector<uint8_t> arena(used > 16 ? used : 16);
-    rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
-                      (const uint8_t*)blob.data(), off.data(), batch.data(), batch.size(), order.data(), &nslots,
-                      arena.data(), arena.size(), &used);
-    if (rc != CG_OK) return FILTER_UNKNOWN_ERROR;
-    std::vector<uint8_t> out(n);
-    rc = cg_http_verdicts_host(inst.engine, batch.data(), nslots, order.data(), n, arena.data(), arena.size(),
-                               out.data());
-    if (rc != CG_OK) return FILTER_UNKNOWN_ERROR;
-    for (size_t k = 0; k < n; ++k) allow[reqs[k]] = out[k];
+  if (!recs.empty()) {
+    Instance& inst = *c->inst;
+    std::lock_guard<std::mutex> lk(inst.mu);
+    std::vector<uint8_t> out;
+    if (!gpu_verdicts(inst, *c, recs, &out)) return FILTER_UNKNOWN_ERROR;
+    for (size_t k = 0; k < reqs.size(); ++k) allow[reqs[k]] = out[k];
   }
   FilterOp* ops = static_cast<FilterOp*>(filterOps->data);
   for (size_t i = 0; i < frames.size(); ++i) {

@@ -700,6 +700,55 @@ ByteDfa dfa_star(const ByteSet& alphabet) {
   return d;
 }
 
+ByteDfa dfa_prefix(const std::string& s, const ByteSet& alphabet) {
+  ByteDfa d;
+  const int n = (int)s.size();
+  d.accept.assign(n + 2, 0);
+  d.trans.assign((size_t)(n + 2) * 256, 0);
+  bool ok = true;
+  for (int i = 0; i < n; ++i) {
+    const uint8_t b = (uint8_t)s[i];
+    if (!alphabet.test(b)) ok = false;
+    d.trans[(size_t)(i + 1) * 256 + b] = i + 2;
+  }
+  if (ok) {
+    d.accept[n + 1] = 1;
+    for (int b = 0; b < 256; ++b)
+      if (alphabet.test(b)) d.trans[(size_t)(n + 1) * 256 + b] = n + 1;
+  }
+  d.start = 1;
+  return dfa_minimize(d);
+}
+
+ByteDfa dfa_list(const ByteDfa& item) {
+  // item states keep their rows; an accepting state's move on kEscByte goes
+  // to a fresh state Y(s) that continues the item on kEscBase..+3 (as the
+  // old escape state did) and ends it on kEscSep, back to a fresh start S'
+  // that copies the item's start row and is the only accepting state
+  const int n = item.size();
+  std::vector<int> acc;
+  for (int s = 1; s < n; ++s)
+    if (item.accept[s]) acc.push_back(s);
+  const int sp = n + (int)acc.size();
+  ByteDfa o;
+  o.accept.assign((size_t)sp + 1, 0);
+  o.trans.assign((size_t)(sp + 1) * 256, 0);
+  for (int s = 1; s < n; ++s)
+    for (int b = 0; b < 256; ++b) o.trans[(size_t)s * 256 + b] = item.next(s, b);
+  for (size_t k = 0; k < acc.size(); ++k) {
+    const int s = acc[k], y = n + (int)k;
+    const int e = item.next(s, kEscByte);
+    if (e)
+      for (int b = kEscBase; b < kEscBase + 4; ++b) o.trans[(size_t)y * 256 + b] = item.next(e, b);
+    o.trans[(size_t)y * 256 + kEscSep] = sp;
+    o.trans[(size_t)s * 256 + kEscByte] = y;
+  }
+  for (int b = 0; b < 256; ++b) o.trans[(size_t)sp * 256 + b] = o.trans[(size_t)item.start * 256 + b];
+  o.accept[sp] = 1;
+  o.start = sp;
+  return dfa_minimize(o);
+}
+
 ByteDfa dfa_escape_low(const ByteDfa& d) {
   // state s keeps its transitions on bytes >= 4; bytes 0..3 move to an escape
   // state e(s) reached on kEscByte, whose transitions on kEscBase + b are

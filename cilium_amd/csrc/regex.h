@@ -75,6 +75,13 @@ ByteDfa dfa_intersect(const ByteDfa& a, const ByteDfa& b);
 // bytes are arbitrary, while 0x00-0x02 structure the request string).
 constexpr int kEscByte = 0x03, kEscBase = 0x10;
 ByteDfa dfa_escape_low(const ByteDfa& d);
+// Strings starting with `s` (then any bytes of the alphabet).
+ByteDfa dfa_prefix(const std::string& s, const ByteSet& alphabet);
+// A list of escaped items, each followed by the separator pair {kEscByte,
+// kEscSep} (which no escaped string contains): (item SEP)*, every item in
+// the language of the escaped DFA `item` (memcached key lists).
+constexpr int kEscSep = 0x14;
+ByteDfa dfa_list(const ByteDfa& item);
 // Moore partition refinement + canonical BFS renumbering (dead=0, start=1):
 // equal languages give identical tables.
 ByteDfa dfa_minimize(const ByteDfa& d);

@@ -135,6 +135,82 @@ def cassandra_rule_parser(l7_rules: list) -> list[list[dict]]:
 
 register_l7_rule_parser("cassandra", cassandra_rule_parser)
 
+# MemcacheOpCodeMap (proxylib/memcached/parser.go:212-474): rule command →
+# (text commands, binary opcodes)
+_MC_STORE = ("add", "set", "replace", "append", "prepend", "cas", "incr", "decr")
+MEMCACHE_COMMANDS: dict[str, tuple[tuple[str, ...], tuple[int, ...]]] = {
+    "add": (("add",), (2, 18)), "set": (("set",), (1, 17)), "replace": (("replace",), (3, 19)),
+    "append": (("append",), (14, 25)), "prepend": (("prepend",), (15, 26)), "cas": (("cas",), ()),
+    "incr": (("incr",), (5, 21)), "decr": (("decr",), (6, 22)),
+    "storage": (_MC_STORE, (1, 2, 3, 5, 6, 17, 18, 19, 21, 22, 25, 26)),
+    "get": (("get", "gets"), (0, 9, 12, 13)), "delete": (("delete",), (4, 20)), "touch": (("touch",), (28,)),
+    "gat": (("gat", "gats"), (29, 30)),
+    "writeGroup": (_MC_STORE + ("delete", "touch"), (1, 2, 3, 4, 5, 6, 17, 18, 19, 20, 21, 22, 25, 26, 28)),
+    "slabs": (("slabs",), ()), "lru": (("lru",), ()), "lru_crawler": (("lru_crawler",), ()),
+    "watch": (("watch",), ()), "stats": (("stats",), (16,)), "flush_all": (("flush_all",), (8, 24)),
+    "cache_memlimit": (("cache_memlimit",), ()), "version": (("version",), (11,)),
+    "misbehave": (("misbehave",), ()), "quit": (("quit",), (7, 23)), "noop": ((), (10,)),
+    "verbosity": ((), (27,)), "sasl-list-mechs": ((), (32,)), "sasl-auth": ((), (33,)), "sasl-step": ((), (34,)),
+}
+MEMCACHE_COMMANDS.update({n: ((), (48 + i,)) for i, n in enumerate(
+    ("rget", "rset", "rsetq", "rappend", "rappendq", "rprepend", "rprependq", "rdelete", "rdeleteq", "rincr",
+     "rincrq", "rdecr", "rdecrq", "set-vbucket", "get-vbucket", "del-vbucket", "tap-connect", "tap-mutation",
+     "tap-delete", "tap-flush", "tap-opaque", "tap-vbucket-set", "tap-checkpoint-start", "tap-checkpoint-end"))})
+
+
+def memcache_rule_parser(l7_rules: list) -> list[list[dict]]:
+    """L7RuleParser (proxylib/memcached/parser.go:114-148).  Rule.Matches
+    (:46-100) is the command (a text command or binary opcode in the rule's
+    set) AND, for the first non-empty of keyExact / keyPrefix / keyRegex, a
+    test that EVERY key of the request passes.  A request is packed as the
+    fields ``mccmd`` ("t" + command, or "b" + two hex digits of the opcode)
+    and ``mckeys`` (each key, escaped, then the separator pair 0x03 0x14), so
+    the key test is a list matcher over the separated keys; one engine rule
+    per allowed command token.  No command: an empty rule (matches
+    everything) unless a key is given, which is a ParseError."""
+    out = []
+    for l7 in l7_rules:
+        rule = l7.get("rule") or {}
+        cmds, exact, prefix, regex = None, "", "", None
+        for k, v in rule.items():
+            if k == "command":
+                cmds = MEMCACHE_COMMANDS.get(v)
+            elif k == "keyExact":
+                exact = v
+            elif k == "keyPrefix":
+                prefix = v
+            elif k == "keyRegex":
+                regex = v
+            else:
+                raise ParseError(f"Unsupported key: {k}")
+        if cmds is None:
+            if exact or prefix or regex is not None:
+                raise ParseError("command not specified but key was provided")
+            out.append([])
+            continue
+        key = ([{"name": "mckeys", "list_exact": exact}] if exact else
+               [{"name": "mckeys", "list_prefix": prefix}] if prefix else
+               [{"name": "mckeys", "list_search": regex}] if regex is not None else [])
+        toks = ["t" + t for t in cmds[0]] + ["b%02x" % b for b in cmds[1]]
+        out.extend([{"name": "mccmd", "exact_match": t}] + key for t in toks)
+    return out
+
+
+register_l7_rule_parser("memcache", memcache_rule_parser)
+
+
+def memcache_request(command: bytes, opcode: int, keys: Sequence[bytes]) -> list[tuple[bytes, bytes]]:
+    """A memcache request's fields (MemcacheMeta, memcached/meta/meta.go):
+    a text command (``command`` non-empty) or a binary opcode, and its keys.
+    The separators are appended after escaping (pack_fields escapes values),
+    so they are passed pre-escaped via the raw form of ``mckeys``."""
+    cmd = b"t" + command if command else b"b%02x" % opcode
+    return [(b"mccmd", cmd), (b"mckeys", _RawField(b"".join(escape_value(k) + b"\x03\x14" for k in keys)))]
+
+
+class _RawField(bytes):
+    """A field value already in the engine's escaped form."""
+
 
 def _translate_port(pp: dict) -> Optional[dict]:
     """newPortNetworkPolicyRules (policymap.go:118-148) for one port; None =
@@ -314,7 +390,7 @@ class ProxylibPolicy:
         """Requests given as their parser's (name, value) fields."""
         parts, off = [], [0]
         for fs in fields:
-            b = b"".join(k + b"\0" + escape_value(v) + b"\0" for k, v in fs)
+            b = b"".join(k + b"\0" + (v if isinstance(v, _RawField) else escape_value(v)) + b"\0" for k, v in fs)
             parts.append(b)
             off.append(off[-1] + len(b))
         blob = np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy()

@@ -309,9 +309,138 @@ def proxylib_kats() -> dict:
             "r2d2": r2d2, "cassandra": cass}
 
 
+# proxylib_memcached_test.go request/reply buffers (:30-118)
+_MC = {
+    "setHelloText": b"set key 0 0 5\r\nhello\r\n",
+    "getKeysText": b"get key1 key2 key3\r\n",
+    "gatKeysText": b"gat 5 key1 key2 key3\r\n",
+    "getResponse": b"VALUE key3 0 4\r\nxDDD\r\nVALUE key4 0 3\r\nxDD\r\nEND\r\n",
+    "deleteText": b"delete key\r\n",
+    "incrText": b"incr key 5\r\n",
+    "touchText": b"touch key 55\r\n",
+    "slabsText": b"slabs automove 1\r\n",
+    "okText": b"OK\r\n",
+    "lruCrawlerText": b"lru_crawler metadump all\r\n",
+    "statsText": b"stats\r\n",
+    "flushAllText": b"flush_all 15\r\n",
+    "watchText": b"watch mutations\r\n",
+    "watchReply": b"OK\r\n" + b"".join(
+        b"ts=%s gid=%d type=item_store key=key%d status=stored cmd=set ttl=500 clsid=1\r\n" % (ts, g, k)
+        for ts, g, k in ((b"1538135970.404892", 5, 3), (b"1538135970.404898", 6, 4), (b"1538135974.340708", 7, 3),
+                         (b"1538135974.340714", 8, 4), (b"1538135976.436863", 9, 3))),
+    "lruCrawlerResponse": b"key=key3 exp=1538047402 la=1538046902 cas=1 fetch=no cls=1 size=67\r\n"
+                          b"key=key4 exp=1538047402 la=1538046902 cas=2 fetch=no cls=1 size=66\r\nEND\r\n",
+    "statsResponse": b"".join(b"STAT %s\r\n" % x for x in (
+        b"evictions 0", b"reclaimed 2", b"crawler_reclaimed", b"crawler_items_checked 18", b"lrutail_reflocked 0",
+        b"moves_to_cold 6", b"moves_to_warm 0", b"moves_within_lru 0", b"direct_reclaims 0",
+        b"lru_bumps_dropped 0")) + b"END\r\n",
+    "notFound": b"NOT_FOUND\r\n",
+    "stored": b"STORED\r\n",
+    "getHello": bytes([128, 0, 0, 5, 0, 0, 0, 0, 0, 0, 0, 5] + [0] * 12) + b"Hello",
+    "getHelloResp": bytes([129, 0, 0, 0, 4, 0, 0, 0, 0, 0, 0, 9] + [0] * 16) + b"World",
+    "setHello": bytes([128, 1, 0, 5, 8, 0, 0, 0, 0, 0, 0, 18] + [0] * 20) + b"HelloWorld",
+}
+_MC_TEXT_DENIED = b"CLIENT_ERROR access denied\r\n"  # text/parser.go DeniedMsg
+_MC_BIN_DENIED = bytes([0x81, 0, 0, 0, 0, 0, 0, 8, 0, 0, 0, 0x0d] + [0] * 12) + b"access denied"  # binary/parser.go:194-205
+
+
+def memcache_kats() -> dict:
+    """TestMemcache (proxylib/proxylib_memcached_test.go:120-732): per case the
+    L7 rule map entries and the OnData calls with their expected ops and reply
+    inject buffer.  The harness's conventions are data here too: inject
+    buffers of capacity 30 (CheckOnNewConnection(..., 30, ...)), an ops slice
+    of capacity 1 + 2·len(expected ops) (helpers_test.go:133) and the
+    expected buffer truncated to what the buffer holds (checkBuf, :101-110)."""
+    M, P, D, I = 0, 1, 2, 3
+    B = _MC
+    L = {k: len(v) for k, v in B.items()}
+
+    def call(reply, chunks, ops, inject=b""):
+        return {"reply": reply, "chunks": [c.hex() for c in chunks], "ops": ops, "inject": inject.hex()}
+
+    ke = lambda v: ["keyExact", v]
+    cmd = lambda v: ["command", v]
+    td, bd = _MC_TEXT_DENIED, _MC_BIN_DENIED
+    cases = [
+        ("text set pass", 170, [[ke(""), cmd("set")]],
+         [call(False, [B["setHelloText"]], [[P, L["setHelloText"]], [M, 2]]), call(True, [B["stored"]], [[P, L["stored"]]])]),
+        ("text set drop", 191, [[ke("trolo"), cmd("set")]],
+         [call(False, [B["setHelloText"]], [[D, L["setHelloText"]], [M, 2]], td)]),
+        ("text get pass", 209, [[ke(""), cmd("get")]],
+         [call(False, [B["getKeysText"]] * 2, [[P, L["getKeysText"]]] * 2 + [[M, 2]]),
+          call(True, [B["getResponse"]] * 2, [[P, L["getResponse"]]] * 2)]),
+        ("text get more", 229, [[ke(""), cmd("get")]], [call(False, [B["getResponse"][:5]], [[M, 2]])]),
+        ("text get drop", 246, [[ke(""), cmd("set")]],
+         [call(False, [B["getKeysText"]], [[D, L["getKeysText"]], [M, 2]], td)]),
+        ("text gat pass", 263, [[ke(""), cmd("gat")]],
+         [call(False, [B["gatKeysText"]] * 2, [[P, L["gatKeysText"]]] * 2 + [[M, 2]]),
+          call(True, [B["getResponse"]] * 2, [[P, L["getResponse"]]] * 2)]),
+        ("text gat more", 283, [[ke(""), cmd("gat")]], [call(False, [B["getResponse"][:5]], [[M, 2]])]),
+        ("text gat drop", 300, [[ke(""), cmd("set")]],
+         [call(False, [B["gatKeysText"]], [[D, L["gatKeysText"]], [M, 2]], td)]),
+        ("text delete pass", 317, [[ke(""), cmd("delete")]],
+         [call(False, [B["deleteText"]], [[P, L["deleteText"]], [M, 2]]), call(True, [B["notFound"]], [[P, L["notFound"]]])]),
+        ("text delete drop", 339, [[ke(""), cmd("set")]],
+         [call(False, [B["deleteText"]], [[D, L["deleteText"]], [M, 2]], td)]),
+        ("text incr pass", 356, [[ke(""), cmd("incr")]],
+         [call(False, [B["incrText"]], [[P, L["incrText"]], [M, 2]]), call(True, [B["notFound"]], [[P, L["notFound"]]])]),
+        ("text incr drop", 378, [[ke("otherKey"), cmd("incr")]],
+         [call(False, [B["incrText"]], [[D, L["incrText"]], [M, 2]], td)]),
+        ("text touch pass", 395, [[ke("key"), cmd("touch")]],
+         [call(False, [B["touchText"]], [[P, L["touchText"]], [M, 2]]), call(True, [B["notFound"]], [[P, L["notFound"]]])]),
+        ("text touch drop", 417, [[ke("otherKey"), cmd("touch")]],
+         [call(False, [B["touchText"]], [[D, L["touchText"]], [M, 2]], td)]),
+        ("text slabs pass", 434, [[cmd("slabs")]],
+         [call(False, [B["slabsText"]], [[P, L["slabsText"]], [M, 2]]), call(True, [B["okText"]], [[P, L["okText"]]])]),
+        ("text slabs drop", 452, [[ke("otherKey"), cmd("touch")]],
+         [call(False, [B["slabsText"]], [[D, L["slabsText"]], [M, 2]], td)]),
+        ("text lru_crawler response req more and pass", 469, [[cmd("lru_crawler")]],
+         [call(False, [B["lruCrawlerText"]], [[P, L["lruCrawlerText"]], [M, 2]]),
+          call(True, [B["lruCrawlerResponse"][:5]], [[M, 2]]),
+          call(True, [B["lruCrawlerResponse"]], [[P, L["lruCrawlerResponse"]]])]),
+        ("text stats response req more and pass", 489, [[cmd("stats")]],
+         [call(False, [B["statsText"]], [[P, L["statsText"]], [M, 2]]),
+          call(True, [B["statsResponse"][:5]], [[M, 2]]),
+          call(True, [B["statsResponse"]], [[P, L["statsResponse"]]])]),
+        ("text flush_all pass", 510, [[cmd("flush_all")]],
+         [call(False, [B["flushAllText"]], [[P, L["flushAllText"]], [M, 2]])]),
+        ("text flush_all denied", 525, [[cmd("get")]],
+         [call(False, [B["flushAllText"]], [[D, L["flushAllText"]], [M, 2]], td)]),
+        ("text watch passed", 540, [[cmd("watch")]],
+         [call(False, [B["watchText"]], [[P, L["watchText"]], [M, 2]]),
+          call(True, [B["watchReply"]], [[P, 4]] + [[P, 91]] * 5)]),
+        ("text partial linefeed", 558, [[ke(""), cmd("set")]],
+         [call(False, [B["getKeysText"][:-1]], [[M, 1]])]),
+        ("text set pass on empty rule", 576, [],
+         [call(False, [B["setHelloText"]], [[P, L["setHelloText"]], [M, 2]]), call(True, [B["stored"]], [[P, L["stored"]]])]),
+        ("bin get pass exact key", 592, [[ke("Hello"), cmd("get")]],
+         [call(False, [B["getHello"]], [[P, L["getHello"]], [M, 24]])]),
+        ("bin get pass prefix key", 609, [[["keyPrefix", "Hell"], cmd("get")]],
+         [call(False, [B["getHello"]], [[P, L["getHello"]], [M, 24]])]),
+        ("bin get pass regex key", 626, [[["keyRegex", "^.el.o$"], cmd("get")]],
+         [call(False, [B["getHello"]], [[P, L["getHello"]], [M, 24]])]),
+        ("bin get drop", 643, [[ke(""), cmd("set")]],
+         [call(False, [B["getHello"]], [[D, L["getHello"]], [M, 24]], bd)]),
+        ("bin get more", 660, [[ke(""), cmd("get")]], [call(False, [B["getHello"][:10]], [[M, 14]])]),
+        ("bin get split", 676, [[ke(""), cmd("get")]],
+         [call(False, [B["getHello"][:10], B["getHello"][10:]], [[P, L["getHello"]], [M, 24]])]),
+        ("bin get remaining key", 694, [[ke(""), cmd("get")]], [call(False, [B["getHello"][:26]], [[M, 3]])]),
+        ("bin set drop and allow", 712, [[ke(""), cmd("set")]],
+         [call(False, [B["setHello"], B["getHello"]], [[P, L["setHello"]], [D, L["getHello"]], [M, 24]], bd),
+          call(True, [B["getHelloResp"]], [[P, L["getHelloResp"]], [I, len(bd)]], bd)]),
+    ]
+    out = []
+    for name, line, rules, calls in cases:
+        out.append({"name": name, "src": f"proxylib/proxylib_memcached_test.go:{line}", "rules": rules,
+                    "calls": calls})
+    return {"generator": "tests/golden/make_golden.py memcache_kats()", "buf_cap": 30, "remote": 1, "port": 80,
+            "remote_policies": [1, 3, 4], "cases": out}
+
+
 def main():
     files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
-             "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors()}
+             "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
+             "memcache_kat.json": memcache_kats()}
     for name, data in files.items():
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(data, f, indent=1, sort_keys=False)

@@ -57,11 +57,12 @@ class Conn:
     """A connection with caller-owned inject buffers (cap 1024 each)."""
     _next = [1000]
 
-    def __init__(self, inst, proto=b"r2d2", ingress=True, src=1, dst=2, dst_addr=b"2.2.2.2:80", policy=b"cp1"):
-        self.orig_mem = C.create_string_buffer(1024)
-        self.reply_mem = C.create_string_buffer(1024)
-        self.orig = GoSlice(C.cast(self.orig_mem, C.c_void_p), 0, 1024)
-        self.reply = GoSlice(C.cast(self.reply_mem, C.c_void_p), 0, 1024)
+    def __init__(self, inst, proto=b"r2d2", ingress=True, src=1, dst=2, dst_addr=b"2.2.2.2:80", policy=b"cp1",
+                 buf_cap=1024):
+        self.orig_mem = C.create_string_buffer(buf_cap)
+        self.reply_mem = C.create_string_buffer(buf_cap)
+        self.orig = GoSlice(C.cast(self.orig_mem, C.c_void_p), 0, buf_cap)
+        self.reply = GoSlice(C.cast(self.reply_mem, C.c_void_p), 0, buf_cap)
         Conn._next[0] += 1
         self.id = Conn._next[0]
         self.rc = _lib.OnNewConnection(inst, gs(proto), self.id, ingress, src, dst, gs(b"1.1.1.1:34567"),
@@ -80,6 +81,12 @@ class Conn:
 
     def injected_reply(self) -> bytes:
         return self.reply_mem.raw[:self.reply.len]
+
+    def take_reply(self) -> bytes:
+        """The reply inject buffer's contents, then empty it (CheckOnData)."""
+        b = self.injected_reply()
+        self.reply.len = 0
+        return b
 
     def close(self):
         _lib.Close(self.id)
