@@ -216,7 +216,7 @@ const std::map<std::string, McCommands>& memcache_opcode_map() {
 }
 
 // The request fields a memcache frame is packed as: mccmd = "t" + command
-// or "b" + opcode byte, mckeys = each key then the separator pair {0x03,
+// or "b" + two hex digits of the opcode, mckeys = each key then the separator pair {0x03,
 // 0x14} (values escaped, proxylib_shim OnData).
 std::string m_list(const char* kind, const std::string& v) {
   return std::string("{\"name\":\"mckeys\",\"") + kind + "\":" + jstr(v) + "}";
@@ -263,7 +263,8 @@ std::vector<std::string> memcache_rules(const Json* l7) {
     for (const auto& t : cmds->text) out.push_back(join(km.empty() ? std::vector<std::string>{m_exact("mccmd", "t" + t)}
                                                                    : std::vector<std::string>{m_exact("mccmd", "t" + t), km}));
     for (uint8_t b : cmds->binary) {
-      const std::string tok = std::string("b") + (char)b;
+      static const char hex[] = "0123456789abcdef";
+      const std::string tok{'b', hex[b >> 4], hex[b & 15]};
       out.push_back(join(km.empty() ? std::vector<std::string>{m_exact("mccmd", tok)}
                                     : std::vector<std::string>{m_exact("mccmd", tok), km}));
     }

@@ -26,10 +26,11 @@ def _policy(name, rules, remotes=(1, 3, 4), port=80):
 
 
 def _oracle_matches(rules, remotes=(1, 3, 4), remote=1):
-    """PolicyMatches for one port rule: the remote set, then an OR over the
-    L7 rules; no L7 rules → any payload (policymap.go:91-171)."""
+    """PolicyMatches for a port with one rule: no L7 rules on the port →
+    allowed from anyone (PortNetworkPolicyRules.Matches, policymap.go:150-158);
+    else the remote set, then an OR over the L7 rules (:91-111)."""
     rs = [MR.Rule(dict(r)) for r in rules]
-    return lambda m: remote in remotes and (not rs or any(r.matches(m) for r in rs))
+    return lambda m: not rs or (remote in remotes and any(r.matches(m) for r in rs))
 
 
 def _check_buf(got: bytes, want: bytes):
