@@ -180,6 +180,7 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pols, info, args.cpu_seconds)
+        cpu["best_cpu_dfa"] = cpu_dfa_line(cl, info, min(args.cpu_seconds, 4.0), cpu["cores"])
     if dist is not None:
         dist.barrier()
 
@@ -397,23 +398,66 @@ def pmc_traffic(requests_per_launch: int):
     return per_item * requests_per_launch, os.path.relpath(files[-1], ROOT)
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(pols, info, seconds: float) -> dict:
     """Oracle = Envoy's algorithm (per-request PortNetworkPolicy scan with
     std::regex_match), on a bounded sample, threads = the host cores given to
-    this process."""
+    this process; plus the same on one core."""
     import oracle
     from cilium_amd import synth
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     orc = oracle.HttpOracle(pols)
     rq = synth.http10k_requests(100_000, info, seed=synth.SEED ^ 0xC0FFEE)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        orc.eval(**rq, nthreads=threads)
-        done += len(rq["policy"])
-    el = time.perf_counter() - t0
+
+    def rate(nthreads, secs, sub):
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            orc.eval(**sub, nthreads=nthreads)
+            done += len(sub["policy"])
+        return done, time.perf_counter() - t0
+    done, el = rate(threads, seconds, rq)
+    k = 5_000
+    one = {key: v[:k] for key, v in rq.items() if key not in ("hdr_blob", "hdr_off")}
+    one["hdr_off"], one["hdr_blob"] = rq["hdr_off"][:k + 1], rq["hdr_blob"]
+    d1, e1 = rate(1, min(seconds / 4, 3.0), one)
     return {"value": done / el, "unit": "verdicts/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "single_core": d1 / e1,
             "sample": f"{done} requests of the same 10K-rule workload ({el:.1f} s, {threads} threads, "
-                      f"std::regex_match per matcher as Envoy)"}
+                      f"std::regex_match per matcher as Envoy); single core: {d1} requests in {e1:.1f} s"}
+
+
+def cpu_dfa_line(cl, info, seconds: float, threads: int) -> dict:
+    """"Best CPU" line: the engine's own compiled union DFAs
+    walked on the host (cg_diag_http_eval_host — the table compilers' CPU
+    walker, never a verdict entry point), one packed batch per thread."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from cilium_amd import synth
+    per = 65_536
+    batches = [cl.pack_http(**synth.http10k_requests(per, info, seed=synth.SEED ^ (0xD0 + t)))
+               for t in range(threads)]
+    cl.http_eval_host_diag(batches[0])
+    t1 = time.perf_counter()
+    cl.http_eval_host_diag(batches[0])
+    single = per / (time.perf_counter() - t1)
+    with ThreadPoolExecutor(threads) as ex:
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(cl.http_eval_host_diag, batches))
+            done += per * threads
+        el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "verdicts/s", "cores": threads, "single_core": single,
+            "sample": f"{done} requests: comb-table DFA walk of the packed batches on the host ({el:.1f} s)"}
 
 
 if __name__ == "__main__":

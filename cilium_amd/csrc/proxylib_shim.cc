@@ -10,6 +10,7 @@
 //                                (cassandraparser.go:97-131) and memcache
 //                                (memcached/parser.go:104-147) rule parsers
 //   memcache OnData              proxylib_memcache.cc (text and binary)
+//   cassandra OnData             proxylib_cassandra.cc (frames, queries, prepared ids)
 //
 // The policy verdicts of every request frame found in one OnData call are
 // evaluated as one batch by http_kernel (no CPU evaluation path).
@@ -26,6 +27,7 @@
 #include "../../include/cilium_proxylib.h"
 #include "common.h"
 #include "json.h"
+#include "proxylib_cassandra.h"
 #include "proxylib_memcache.h"
 
 using namespace cg;
@@ -41,7 +43,8 @@ struct Instance {
 struct Conn {
   std::shared_ptr<Instance> inst;
   std::string parser, policy;
-  McState mc;  // memcache parser state
+  McState mc;     // memcache parser state
+  CassState cs;   // cassandra parser state
   bool ingress = false;
   uint32_t src_id = 0, dst_id = 0, port = 0;
   GoSlice* orig_buf = nullptr;
@@ -458,6 +461,39 @@ FilterResult memcache_data(Conn& c, bool reply, bool end_stream, const GoSlice* 
   });
 }
 
+// A cassandra path as the fields its rules are compiled over (see
+// cassandra_rules): cshape, then action and table for query-like paths.
+std::string cassandra_record(const std::string& path) {
+  const CassFields f = cassandra_path_fields(path);
+  std::string r = field("cshape", std::string(1, f.shape));
+  if (f.shape == 'L') r += field("action", esc(f.action)) + field("table", esc(f.table));
+  return r;
+}
+
+// cassandra OnData: as memcache_data — the paths a dry run on a copy of the
+// parser state collects do not depend on the verdicts (a denial is a DROP of
+// the same frame), one GPU batch decides them, the real run consumes them.
+FilterResult cassandra_data(Conn& c, bool reply, bool end_stream, const GoSlice* data, GoSlice* ops) {
+  std::vector<uint8_t> allow;
+  if (!reply) {
+    CassState dry = c.cs;
+    std::vector<FilterOp> scratch((size_t)(ops->cap > 0 ? ops->cap : 1));
+    GoSlice sops{scratch.data(), ops->len, ops->cap};
+    std::vector<std::string> recs;
+    cassandra_on_data(dry, false, end_stream, data, &sops, nullptr, [&](const std::string& path) {
+      recs.push_back(cassandra_record(path));
+      return true;
+    });
+    Instance& inst = *c.inst;
+    std::lock_guard<std::mutex> lk(inst.mu);
+    if (!gpu_verdicts(inst, c, recs, &allow)) return FILTER_UNKNOWN_ERROR;
+  }
+  size_t next = 0;
+  return cassandra_on_data(c.cs, reply, end_stream, data, ops, c.reply_buf, [&](const std::string&) {
+    return next < allow.size() && allow[next++] != 0;
+  });
+}
+
 }  // namespace
 
 extern "C" {
@@ -524,8 +560,8 @@ FilterResult OnNewConnection(uint64_t instanceId, GoString proto, uint64_t conne
   if (!inst) return FILTER_INVALID_INSTANCE;
   auto c = std::make_shared<Conn>();
   c->parser = gostr(proto);
-  // parser factories implemented here: r2d2, memcache
-  if (c->parser != "r2d2" && c->parser != "memcache") return FILTER_UNKNOWN_PARSER;
+  // parser factories implemented here: r2d2, memcache, cassandra
+  if (c->parser != "r2d2" && c->parser != "memcache" && c->parser != "cassandra") return FILTER_UNKNOWN_PARSER;
   // net.SplitHostPort + ParseUint(port, 10, 32), port != 0 (connection.go:71-78)
   const std::string da = gostr(dstAddr);
   const size_t colon = da.rfind(':');
@@ -565,6 +601,7 @@ FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoS
   }
   if (!data || !filterOps) return FILTER_UNKNOWN_ERROR;
   if (c->parser == "memcache") return memcache_data(*c, reply != 0, endStream != 0, data, filterOps);
+  if (c->parser == "cassandra") return cassandra_data(*c, reply != 0, endStream != 0, data, filterOps);
   // r2d2 reads bytes.Join(dataArray) (r2d2parser.go:151)
   std::string in;
   const GoSlice* parts = static_cast<const GoSlice*>(data->data);

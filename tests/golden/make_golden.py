@@ -437,10 +437,52 @@ def memcache_kats() -> dict:
             "remote_policies": [1, 3, 4], "cases": out}
 
 
+_CASS_OPTIONS = "040000000500000000"
+_CASS_QUERY = ("0400000407000000760000006f53454c45435420636c75737465725f6e616d652c20646174615f63656e7465722c207261"
+               "636b2c20746f6b656e732c20706172746974696f6e65722c20736368656d615f76657273696f6e2046524f4d2073797374"
+               "656d2e6c6f63616c205748455245206b65793d276c6f63616c27000100")
+_CASS_UNAUTH_S4 = bytes([0x84, 0, 0, 4, 0, 0, 0, 0, 0x1a, 0, 0, 0x21, 0, 0, 0x14]) + b"Request Unauthorized"
+
+
+def cassandra_kats() -> dict:
+    """cassandraparser_test.go:56-280: per case the policy (protobuf text, or
+    none: the connection names a policy that is not installed), the OnData
+    calls' input slices (hex), the expected ops and the reply inject buffer.
+    The harness's conventions are data too: an ops slice of capacity
+    len(expected ops) (test_util.go:100), inject buffers of capacity 1024
+    (:88-90), connection remote identity 1 on ingress port 80 (:79-92 with
+    the tests' CheckNewConnectionOK(..., true, 1, 2, ..., "2.2.2.2:80", ...))."""
+    M, P, D = 0, 1, 2
+    q = _CASS_QUERY
+    L = lambda h: len(h) // 2
+    cases = [
+        ("TestCassandraOnDataNoHeader", "56-61", None, "no-policy", [["0400"]], [[[M, 7]]], [""]),
+        ("TestCassandraOnDataOptionsReq", "63-92", _cassandra_policy("cp6", "query_action", "select"), "cp6",
+         [[_CASS_OPTIONS]], [[[P, 9], [M, 9]]], [""]),
+        ("TestCassandraOnDataPartialReq", "94-120", _cassandra_policy("cp5", "query_table", ".*"), "cp5",
+         [[q[:-2]]], [[[M, 1]]], [""]),
+        ("TestCassandraOnDataQueryReq", "122-149", _cassandra_policy("cp4", "query_table", ".*"), "cp4",
+         [[q]], [[[P, L(q)], [M, 9]]], [""]),
+        ("TestCassandraOnDataSplitQueryReq", "151-178", _cassandra_policy("cp3", "query_table", ".*"), "cp3",
+         [[q[:20], q[20:]]], [[[P, L(q)], [M, 9]]], [""]),
+        ("TestCassandraOnDataMultiReq", "180-211", _cassandra_policy("cp2", "query_table", ".*"), "cp2",
+         [[_CASS_OPTIONS, q]], [[[P, 9], [P, L(q)], [M, 9]]], [""]),
+        ("TestSimpleCassandraPolicy", "213-280", _cassandra_policy("cp1", "query_table", "no-match"), "cp1",
+         [[_CASS_OPTIONS, q]], [[[P, 9], [D, L(q)], [M, 9]]], [_CASS_UNAUTH_S4.hex()]),
+    ]
+    out = []
+    for name, lines, pol, pname, calls, ops, inj in cases:
+        out.append({"name": name, "src": f"proxylib/cassandra/cassandraparser_test.go:{lines}", "policy": pol,
+                    "policy_name": pname,
+                    "calls": [{"reply": False, "chunks": c, "ops": o, "inject": i} for c, o, i in zip(calls, ops, inj)]})
+    return {"generator": "tests/golden/make_golden.py cassandra_kats()", "buf_cap": 1024, "remote": 1, "port": 80,
+            "cases": out}
+
+
 def main():
     files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
              "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
-             "memcache_kat.json": memcache_kats()}
+             "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats()}
     for name, data in files.items():
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(data, f, indent=1, sort_keys=False)

@@ -70,6 +70,21 @@ def cpu_rate(fn, items, seconds):
     return n / (time.perf_counter() - t0)
 
 
+def cpu_rate_mt(fn, chunks, threads, seconds):
+    """cpu_rate over `threads` host threads: fn(chunk) on every chunk per
+    round (fn must release the GIL, as the ctypes oracle calls do)."""
+    if seconds <= 0:
+        return None
+    from concurrent.futures import ThreadPoolExecutor
+    items = sum(len(c) for c in chunks)
+    with ThreadPoolExecutor(threads) as ex:
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(fn, chunks))
+            n += items
+        return n / (time.perf_counter() - t0)
+
+
 def line(metric, n, sec, bytes_per_item, kernel, cpu, cpu_sample, threads, extra):
     achieved = n * bytes_per_item / sec / 1e9
     return {"metric": metric, "value": n / sec, "unit": "verdicts/s", "n_gpus": 1, "ms_per_launch": sec * 1e3,
@@ -95,10 +110,13 @@ def bench_l4(torch, dev, stream, cl, args, threads):
     n = D * reps
     d_o = torch.empty(n, dtype=torch.int32, device=dev)
     sec = timed(torch, stream, lambda: pm.verdicts_dev(d_t, n, d_o, stream=stream.cuda_stream), args.steps, 2)
-    sample = tup[:2_000_000]
-    cpu = cpu_rate(lambda: oracle.l4(keys, ports, sample), len(sample), args.cpu_seconds)
-    return line("L4 policymap verdicts/s (__policy_can_access), config 2", n, sec, 16, "l4_kernel", cpu,
-                f"2M tuples of the same workload, 1 thread (oracle.l4 is single-threaded)", 1,
+    chunks = [tup[i * 250_000:(i + 1) * 250_000] for i in range(threads)]
+    cpu = cpu_rate_mt(lambda c: oracle.l4(keys, ports, c), chunks, threads, args.cpu_seconds)
+    cpu1 = cpu_rate(lambda: oracle.l4(keys, ports, chunks[0]), len(chunks[0]), min(args.cpu_seconds, 2.0))
+    kern = "l4_fp_kernel"  # a 16,384-entry map's fingerprints + counters fit LDS
+    return line("L4 policymap verdicts/s (__policy_can_access), config 2", n, sec, 16, kern, cpu,
+                f"{threads} x 250K tuples of the same workload, {threads} threads (single-core: {cpu1:.4g}/s)"
+                if cpu else "", threads,
                 {"config": {"workload": "BASELINE config 2: 16,384-entry policy map, 100M tuples",
                             "entries": int(len(keys)), "tuples": n}})
 
@@ -363,11 +381,8 @@ def bench_l4ipc(torch, dev, stream, cl, args, threads):
     a4 = a4[:D]
     tup = synth.l4_tuples(D, keys)
     got = pm.verdicts_via_ipcache(ic, a4[:1_000_000], tup[:1_000_000])
-    o4, _ = oracle.ipcache(ik, iv, a4[:1_000_000], np.zeros((0, 16), np.uint8), nthreads=threads)
-    t2 = tup[:1_000_000].copy()
-    t2["identity"] = o4[:, 0]
-    exp, _, _ = oracle.l4(keys, ports, t2)
-    assert np.array_equal(got, exp), "ipcache+L4 verdicts differ from the oracle"
+    exp, _, _ = oracle.l4_egress_via_ipcache(keys, ports, ik, iv, a4[:1_000_000], tup[:1_000_000])
+    assert np.array_equal(got, exp), "ipcache+L4 verdicts differ from the oracle (policy_can_egress4)"
     d_t = tile_dev(torch, tup, reps, dev)
     d_a = tile_dev(torch, a4, reps, dev)
     n = D * reps
@@ -384,7 +399,7 @@ def bench_l4ipc(torch, dev, stream, cl, args, threads):
         r4, _ = oracle.ipcache(ik, iv, sa, np.zeros((0, 16), np.uint8), nthreads=threads)
         tt = st.copy()
         tt["identity"] = r4[:, 0]
-        oracle.l4(keys, ports, tt)
+        oracle.l4(keys, ports, tt, oracle.L4_EGRESS)
     cpu = cpu_rate(cpu_leg, len(st), args.cpu_seconds)
     return line("L4 verdicts/s with ipcache identities (bpf_lxc.c:509-527), config 2 map + 475K-entry ipcache", n,
                 sec, 20, "l4_fp_kernel<ipcache>", cpu,
