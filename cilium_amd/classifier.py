@@ -105,6 +105,11 @@ class Classifier:
             blob = blob.encode()
         N.check(N.lib.cg_http_policy_update(self.h, blob, len(blob)))
 
+    def update_http_policy_npds(self, discovery_response: bytes) -> None:
+        """Install NPDS NetworkPolicies from their wire form: a serialized
+        envoy.api.v2.DiscoveryResponse of cilium.NetworkPolicy resources."""
+        N.check(N.lib.cg_http_policy_update_npds(self.h, discovery_response, len(discovery_response)))
+
     def http_policy_index(self, name: str) -> int:
         v = C.c_uint32()
         rc = N.lib.cg_http_policy_index(self.h, name.encode(), C.byref(v))

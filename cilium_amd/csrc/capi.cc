@@ -762,6 +762,16 @@ int cg_http_policy_update(uint64_t h, const char* json, size_t len) {
   });
 }
 
+int cg_http_policy_update_npds(uint64_t h, const uint8_t* resp, size_t len) {
+  std::string json;
+  const int rc = guarded([&] {
+    if (!resp && len) fail(CG_INVALID_ARGUMENT, "NULL DiscoveryResponse");
+    json = npds_pb_to_json(resp, len);
+  });
+  if (rc != CG_OK) return rc;
+  return cg_http_policy_update(h, json.data(), json.size());
+}
+
 static std::shared_ptr<HttpSnapshot> http_snap(Engine& e) {
   std::lock_guard<std::mutex> lk(e.mu);
   if (!e.http) fail(CG_NOT_FOUND, "no HTTP policy installed");

@@ -48,6 +48,10 @@ struct HttpSnapshot {
 
 std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len);
 
+// NPDS wire form (serialized DiscoveryResponse of cilium.NetworkPolicy) →
+// the NPDS JSON http_compile and the proxylib translation read (npds_pb.cc).
+std::string npds_pb_to_json(const uint8_t* p, size_t n);
+
 // Upper bounds of a packed batch of n requests (slots, bytes).
 size_t http_batch_slots(const HttpSnapshot& s, size_t n);
 size_t http_batch_bytes(const HttpSnapshot& s, size_t n);

@@ -26,6 +26,7 @@
 #include "../../include/cilium_gpu.h"
 #include "../../include/cilium_proxylib.h"
 #include "common.h"
+#include "http.h"
 #include "json.h"
 #include "proxylib_cassandra.h"
 #include "proxylib_memcache.h"
@@ -513,6 +514,21 @@ int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len) {
   }
   std::lock_guard<std::mutex> lk(inst->mu);
   return cg_http_policy_update(inst->engine, eng.data(), eng.size());
+}
+
+int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* resp, size_t len) {
+  std::string json;
+  try {
+    if (!resp && len) fail(CG_INVALID_ARGUMENT, "NULL DiscoveryResponse");
+    json = npds_pb_to_json(resp, len);
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (...) {
+    set_error("NPDS protobuf decode failed");
+    return CG_UNKNOWN_ERROR;
+  }
+  return cg_proxylib_policy_update(instance, json.data(), json.size());
 }
 
 uint64_t OpenModule(GoSlice params, uint8_t debug) {

@@ -305,6 +305,12 @@ int cg_l4_verdicts_ipcache6_host(uint64_t h, uint32_t map_id, uint32_t ipc_id, c
  * previous snapshot stays.  Verdict contract: exact port, port 0, else deny. */
 int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len);
 
+/* The proxylib update from the NPDS wire form (a serialized DiscoveryResponse
+ * of cilium.NetworkPolicy resources, as Instance.PolicyUpdate receives it,
+ * proxylib/proxylib/instance.go:180-215, with the same Validate() rules as
+ * cg_http_policy_update_npds). */
+int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* discovery_response, size_t len);
+
 /* ======================================================================== */
 /* HTTP L7: Envoy cilium.l7policy — envoy/cilium_network_policy.h:40-237,    */
 /* envoy/cilium_l7policy.cc:127-182                                          */
@@ -326,6 +332,17 @@ int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len);
  * "PortNetworkPolicy: Duplicate port number", cilium_network_policy.h:160)
  * the previous snapshot stays and CG_POLICY_REJECTED is returned. */
 int cg_http_policy_update(uint64_t h, const char* npds_json, size_t len);
+
+/* The same update from the NPDS wire form: a serialized xDS
+ * envoy.api.v2.DiscoveryResponse whose resources are google.protobuf.Any
+ * of type "type.googleapis.com/cilium.NetworkPolicy" (envoy/cilium/npds.proto:
+ * 31-182, the StreamNetworkPolicies payload Envoy's NPDS subscription hands to
+ * NetworkPolicyMap::onConfigUpdate, envoy/cilium_network_policy.cc:46-60).
+ * The messages are validated as npds.pb.validate.go does (port <= 65535,
+ * unique remote_policies, non-empty rule lists, Kafka name patterns); a
+ * resource of another type, a malformed message or a failed validation
+ * rejects the whole update (CG_POLICY_REJECTED, previous snapshot stays). */
+int cg_http_policy_update_npds(uint64_t h, const uint8_t* discovery_response, size_t len);
 /* Index of a policy name in the installed snapshot (for the packer);
  * CG_NOT_FOUND → requests naming it are denied (cilium_network_policy.h:232-235). */
 int cg_http_policy_index(uint64_t h, const char* name, uint32_t* index);

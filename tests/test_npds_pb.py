@@ -1,0 +1,154 @@
+"""NPDS protobuf ingestion:
+cg_http_policy_update_npds / cg_proxylib_policy_update_npds take the wire form
+Envoy's and proxylib's NPDS clients receive — a serialized DiscoveryResponse of
+Any-wrapped cilium.NetworkPolicy (envoy/cilium/npds.proto:31-182).  Policies
+installed from protobuf must compile to the same tables as the same policies
+installed from JSON (checked by walking both on the host), reject what
+npds.pb.validate.go rejects, and give the reference fixtures' verdicts on the
+GPU."""
+import json
+
+import numpy as np
+import pytest
+
+import npds_pb as PB
+from cilium_amd import _native as N
+from cilium_amd import synth
+from cilium_amd.classifier import Classifier
+from kat_util import http_requests, load
+
+HTTP = load("http_kat.json")
+
+
+def _same_tables(pols, rq):
+    a, b = Classifier(device=-1), Classifier(device=-1)
+    try:
+        a.update_http_policy(pols)
+        b.update_http_policy_npds(PB.discovery_response(pols))
+        va = a.http_eval_host_diag(a.pack_http(**rq))
+        vb = b.http_eval_host_diag(b.pack_http(**rq))
+        assert np.array_equal(va, vb)
+        return va
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.parametrize("suite", HTTP["suites"], ids=lambda s: s["name"])
+def test_pb_http_kat_host(suite):
+    names = [p["name"] for p in suite["policy"]]
+    rq = http_requests(suite["requests"], lambda n: names.index(n) if n in names else 0xFFFFFFFF)
+    got = _same_tables(suite["policy"], rq)
+    exp = np.array([r["expect"] for r in suite["requests"]], np.uint8)
+    assert np.array_equal(got, exp)
+
+
+def test_pb_http10k_subset_host():
+    pols, info = synth.http10k_rules(n_rules=600)
+    rq = synth.http10k_requests(20_000, info)
+    v = _same_tables(pols, rq)
+    assert 0 < v.mean() < 1
+
+
+def test_pb_packed_and_unpacked_remotes():
+    pols = synth.starwars_policy()
+    rq = synth.starwars_requests(2000)
+    a, b = Classifier(device=-1), Classifier(device=-1)
+    a.update_http_policy_npds(PB.discovery_response(pols, packed=True))
+    b.update_http_policy_npds(PB.discovery_response(pols, packed=False))
+    assert np.array_equal(a.http_eval_host_diag(a.pack_http(**rq)), b.http_eval_host_diag(b.pack_http(**rq)))
+    a.close()
+    b.close()
+
+
+def _rc(cl, blob):
+    return N.lib.cg_http_policy_update_npds(cl.h, blob, len(blob))
+
+
+def test_pb_validation_rejects():
+    cl = Classifier(device=-1)
+    ok = [{"name": "p", "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [1, 2], "http_rules": {"http_rules": [{"headers": [
+            {"name": ":path", "regex_match": "/a.*"}]}]}}]}]}]
+    assert _rc(cl, PB.discovery_response(ok)) == N.CG_OK
+    bad_port = json.loads(json.dumps(ok))
+    bad_port[0]["ingress_per_port_policies"][0]["port"] = 65536
+    dup_remote = json.loads(json.dumps(ok))
+    dup_remote[0]["ingress_per_port_policies"][0]["rules"][0]["remote_policies"] = [3, 3]
+    empty_http = json.loads(json.dumps(ok))
+    empty_http[0]["ingress_per_port_policies"][0]["rules"][0]["http_rules"]["http_rules"] = []
+    for bad in (PB.discovery_response(bad_port), PB.discovery_response(dup_remote), PB.discovery_response(empty_http),
+                PB.discovery_response(ok, type_url="type.googleapis.com/cilium.Other"),
+                PB.discovery_response(ok)[:-9],  # truncated inside a field
+                b"\x12\xff\xff\xff\xff\x0f"):  # a length past the message
+        assert _rc(cl, bad) == N.CG_POLICY_REJECTED, bad
+    # the previous snapshot still serves
+    assert cl.http_policy_index("p") == 0
+    # an empty response installs no policies
+    assert _rc(cl, b"") == N.CG_OK
+    cl.close()
+
+
+def test_pb_unknown_fields_skipped():
+    pols = synth.starwars_policy()
+    blob = PB.discovery_response(pols)
+    # unknown fields of every wire type in the DiscoveryResponse
+    extra = PB.vi(9, 7) + PB.key(10, 1) + b"\x00" * 8 + PB.ld(11, b"xyz") + PB.key(12, 5) + b"\x00" * 4
+    cl = Classifier(device=-1)
+    assert _rc(cl, extra + blob + extra) == N.CG_OK
+    cl.close()
+
+
+def test_pb_proxylib_translation_codes():
+    from test_proxylib_abi import _lib, open_module
+    inst = open_module([(b"node-id", b"cpu-npds-pb")], "-1")
+
+    def upd(pols):
+        blob = PB.discovery_response(pols)
+        return N.lib.cg_proxylib_policy_update_npds(inst, blob, len(blob))
+
+    def l7(parser, *rs):
+        return {"l7_proto": parser, "l7_rules": {"l7_rules": [{"rule": r} for r in rs]}}
+
+    def pol(rules):
+        return [{"name": "p", "ingress_per_port_policies": [{"port": 80, "rules": rules}]}]
+
+    assert upd(pol([l7("r2d2", {"cmd": "READ", "file": "^/a"})])) == N.CG_OK
+    assert upd(pol([l7("cassandra", {"query_action": "select", "query_table": "t$"})])) == N.CG_OK
+    assert upd(pol([l7("cassandra", {"query_action": "explode"})])) == N.CG_POLICY_REJECTED
+    assert upd(pol([l7("r2d2", {"cmd": "JUMP"})])) == N.CG_POLICY_REJECTED
+    assert upd(pol([{"l7_proto": "r2d2", "l7_rules": {"l7_rules": []}}])) == N.CG_POLICY_REJECTED  # min_items
+    _lib.CloseModule(inst)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("suite", HTTP["suites"], ids=lambda s: s["name"])
+def test_gpu_pb_http_kat(suite):
+    cl = Classifier(device=0)
+    names = [p["name"] for p in suite["policy"]]
+    rq = http_requests(suite["requests"], lambda n: names.index(n) if n in names else 0xFFFFFFFF)
+    cl.update_http_policy_npds(PB.discovery_response(suite["policy"]))
+    got = cl.http_verdicts(cl.pack_http(**rq))
+    exp = np.array([r["expect"] for r in suite["requests"]], np.uint8)
+    assert np.array_equal(got, exp)
+    cl.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pb_proxylib_reference_policies():
+    """The reference's r2d2 test policies (tests/golden/proxylib_kat.json, as
+    protobuf text) installed from their binary form; frames through OnData."""
+    from cilium_amd import proxylib as P
+    from test_proxylib_abi import DROP, F_OK, MORE, PASS, Conn, _lib, open_module
+    kat = load("proxylib_kat.json")
+    inst = open_module([(b"node-id", b"gpu-npds-pb")], "0")
+    pols = [P.parse_policy_text(c["policy"]) for c in kat["r2d2"]]
+    blob = PB.discovery_response(pols)
+    assert N.lib.cg_proxylib_policy_update_npds(inst, blob, len(blob)) == N.CG_OK
+    for case, pol in zip(kat["r2d2"], pols):
+        c = Conn(inst, src=kat["remote"], dst_addr=b"2.2.2.2:%d" % kat["port"], policy=pol["name"].encode())
+        for line, allow in case["requests"]:
+            rc, ops = c.on_data([line.encode() + b"\r\n"])
+            assert rc == F_OK and ops == [(PASS if allow else DROP, len(line) + 2), (MORE, 1)], (case["src"], line)
+        c.close()
+    _lib.CloseModule(inst)

@@ -56,6 +56,25 @@ VARIANTS.update({
 })
 
 
+# L4 (kernels.hip): tuples per lane per iteration; counters skipped (a
+# measuring device: the per-entry counters stay zero).
+def _l4t(k):
+    return [("kernels.hip", "constexpr uint32_t kL4Tuples = 4;", f"constexpr uint32_t kL4Tuples = {k};")]
+
+
+_NOPIPE = ("kernels.hip", "constexpr bool kL4Pipe = true;", "constexpr bool kL4Pipe = false;")
+VARIANTS.update({
+    "l4_pipe4": _l4t(4),
+    "l4_pipe8": _l4t(8),
+    "l4_nopipe4": _l4t(4) + [_NOPIPE],
+    "l4_nopipe8": _l4t(8) + [_NOPIPE],
+    "l4_noctr": [("kernels.hip", "      if (which) l4_count(t, lcnt, val & 0xFFFF, w[u][2]);", "")],
+    # HTTP: dynamic (ticket) vs static chunk dealing
+    "h_dyn": [],
+    "h_static": [("constexpr bool kDynamicDeal = true;", "constexpr bool kDynamicDeal = false;")],
+})
+
+
 def build_variant(name, subs):
     """subs: (old, new) pairs on kernels_http.hip, or (file, old, new) on any
     csrc/ source; the changed sources are compiled into a private library."""
@@ -66,7 +85,7 @@ def build_variant(name, subs):
         src = files.get(fn) or (B.CSRC / fn).read_text()
         assert a in src, (name, fn, a)
         files[fn] = src.replace(a, b)
-    if not any(fn.endswith(".hip") for fn in files):
+    if not any(fn.endswith(".hip") for fn in files) and not name.startswith("l4_"):
         files["kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip"] = \
             (B.CSRC / ("kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip")).read_text()
     objs = []
