@@ -179,6 +179,29 @@ class Classifier:
         pol = np.where(ok.astype(bool), np.asarray(policy, np.uint32), np.uint32(0xFFFFFFFF)).astype(np.uint32)
         return self.pack_http(pol, ingress, port, remote, blob, off)
 
+    def http_verdicts_raw(self, policy, ingress, port, remote, raw_blob: np.ndarray, raw_off: np.ndarray) -> np.ndarray:
+        """cg_http_verdicts_raw_host: raw HTTP/1.x heads → verdicts, parsed,
+        packed and evaluated on the GPU (request order)."""
+        raw_blob = np.ascontiguousarray(raw_blob, np.uint8)
+        raw_off = np.ascontiguousarray(raw_off, np.uint64)
+        n = len(raw_off) - 1
+        if len(raw_blob) == 0:
+            raw_blob = np.zeros(1, np.uint8)
+        pol = np.ascontiguousarray(policy, np.uint32)
+        ing = np.ascontiguousarray(ingress, np.uint8)
+        prt = np.ascontiguousarray(port, np.uint16)
+        rem = np.ascontiguousarray(remote, np.uint32)
+        out = np.zeros(max(n, 1), np.uint8)
+        N.check(N.lib.cg_http_verdicts_raw_host(self.h, _p(raw_blob), _p(raw_off), n, _p(pol), _p(ing), _p(prt),
+                                                _p(rem), _p(out)))
+        return out[:n]
+
+    def http_verdicts_raw_dev(self, d_raw, d_off, n: int, d_policy, d_ingress, d_port, d_remote, d_out,
+                              stream=None) -> None:
+        """cg_http_verdicts_raw_dev on device tensors (synchronizes `stream`)."""
+        N.check(N.lib.cg_http_verdicts_raw_dev(self.h, _p(d_raw), _p(d_off), n, _p(d_policy), _p(d_ingress),
+                                               _p(d_port), _p(d_remote), _p(d_out), stream))
+
     def http_verdicts(self, b: "HttpBatch") -> np.ndarray:
         """Verdicts (1 allow / 0 deny) in request order, computed on the GPU."""
         out = np.zeros(max(b.n, 1), np.uint8)

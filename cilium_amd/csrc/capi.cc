@@ -872,6 +872,22 @@ int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const u
   });
 }
 
+int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,
+                             const uint32_t* d_policy, const uint8_t* d_ingress, const uint16_t* d_port,
+                             const uint32_t* d_remote, uint8_t* d_out, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = http_snap(*e);
+    if (n && (!d_raw_off || !d_policy || !d_ingress || !d_port || !d_remote || !d_out))
+      fail(CG_INVALID_ARGUMENT, "NULL device array");
+    e->set_device();
+    auto lease = e->staging.acquire(e->device);
+    http_verdicts_raw_on(*s, *lease, e->cus, d_raw, d_raw_off, n, d_policy, d_ingress, d_port, d_remote, d_out,
+                         stream_of(*e, stream));
+  });
+}
+
 // Copy a host array into the lease's pinned buffer i and DMA it to its
 // device buffer i (async on the lease's stream).
 static void* stage_in(StagingSlot& sl, int i, const void* src, size_t bytes) {
@@ -1128,6 +1144,38 @@ int cg_kafka_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* r
     hip_check(hipMemcpyAsync(hv + n, k.status, n, hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
     for (size_t i = 0; i < n; ++i) out[i] = hv[n + i] == CG_KAFKA_DECODE_OK ? hv[i] : CG_KAFKA_V_CLOSE;
+  });
+}
+
+int cg_http_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                              const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                              const uint32_t* remote, uint8_t* out) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = http_snap(*e);
+    if (!n) return;
+    check_offsets(raw_off, n);
+    if (!policy || !ingress || !port || !remote || !out || (raw_off[n] && !raw))
+      fail(CG_INVALID_ARGUMENT, "NULL raw/policy/ingress/port/remote/out");
+    e->set_device();
+    auto lease = e->staging.acquire(e->device);
+    const auto st = (hipStream_t)lease->stream;
+    // offsets rebased to the staged bytes
+    std::vector<uint64_t> off(raw_off, raw_off + n + 1);
+    for (auto& o : off) o -= raw_off[0];
+    const uint8_t* d_raw = (const uint8_t*)stage_in(*lease, 0, raw + raw_off[0], off[n]);
+    const uint64_t* d_off = (const uint64_t*)stage_in(*lease, 1, off.data(), (n + 1) * 8);
+    const uint32_t* d_pol = (const uint32_t*)stage_in(*lease, 2, policy, n * 4);
+    const uint8_t* d_ing = (const uint8_t*)stage_in(*lease, 3, ingress, n);
+    const uint16_t* d_port = (const uint16_t*)stage_in(*lease, 4, port, n * 2);
+    const uint32_t* d_rem = (const uint32_t*)stage_in(*lease, 5, remote, n * 4);
+    uint8_t* d_out = (uint8_t*)lease->dev_buf(6, n);
+    http_verdicts_raw_on(*s, *lease, e->cus, d_raw, d_off, n, d_pol, d_ing, d_port, d_rem, d_out, st);
+    uint8_t* ho = (uint8_t*)lease->host_buf(6, n);
+    hip_check(hipMemcpyAsync(ho, d_out, n, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    memcpy(out, ho, n);
   });
 }
 

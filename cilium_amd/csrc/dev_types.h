@@ -233,6 +233,43 @@ struct HttpDev {
   unsigned long long* rule_hits; // counters + 2*nprogs + 1: first-match hits per rule
 };
 
+// ---- HTTP/1 raw heads → batch on the device (kernels_http_raw.hip) ----
+// The packer's inputs derived on the GPU from raw request heads: the field
+// values (http_parse.cc semantics), the program (HttpSnapshot::lookup_prog),
+// the string and its class codes (http_pack.cc).  Fields beyond
+// kRawMaxFields are not supported on this path (CG_UNSUPPORTED); heads longer
+// than kRawMaxHead are rejected as Envoy's default 60 KiB header limit
+// (max_request_headers_kb) rejects them.
+constexpr uint32_t kRawMaxFields = 32;
+constexpr uint32_t kRawMaxHead = 61440;
+constexpr uint32_t kRawKeys = 10;  // bucket key: walked units 0..8, 9 = overflow arena
+constexpr uint32_t kRawTileGranules = 17;  // a tile's fixed stride: meta + 8 units (512-B granules)
+struct HttpRawDev {
+  const uint32_t* phash_keys;  // (policy << 17 | ingress << 16 | port) → program
+  const uint32_t* phash_vals;
+  uint32_t phash_mask;
+  uint32_t npolicies;
+  const uint32_t* dflt;        // [policy*2 + ingress]
+  const HttpProg* progs;
+  uint32_t nprogs;
+  uint32_t nfields;
+  int32_t f_method, f_path, f_authority;  // field index of each pseudo header, or -1
+  uint32_t fmask;              // field-name table: fmask + 1 slots
+  const uint32_t* fslots;      // per slot {FNV-1a of the lowercase name, name length (0 = empty), field, name offset}
+  const uint8_t* fnames;       // lowercase names
+  const uint8_t* codes;        // nprogs × 256: string byte → code (identity for byte-mode programs)
+};
+// FNV-1a, 32 bit, over lowercase bytes
+CG_HD inline uint32_t raw_fnv(uint32_t h, uint8_t c) { return (h ^ c) * 16777619u; }
+constexpr uint32_t kRawFnvInit = 2166136261u;
+// Per group (program; then allow, deny) of a raw batch: its first tile, its
+// request count and the first local slot of each bucket key (kRawKeys + 1).
+struct HttpRawGroup {
+  uint32_t tile0, count;
+  uint32_t bstart[kRawKeys + 1];
+  uint32_t prog;
+};
+
 CG_HD inline uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352dU;

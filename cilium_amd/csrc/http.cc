@@ -904,6 +904,7 @@ void HttpSnapshot::upload(Engine& e) {
       dev.n_global_progs++;
   dev.counters = d_counters.as<unsigned long long>();
   dev.rule_hits = dev.counters + 2 * (size_t)dev.nprogs + 1;
+  http_raw_upload(*this);
 }
 
 }  // namespace cg

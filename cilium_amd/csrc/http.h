@@ -41,6 +41,11 @@ struct HttpSnapshot {
 
   DevMem d_progs, d_parts, d_cells, d_dflt, d_counters;
   HttpDev dev{};
+  // raw HTTP/1 heads on the device (http_raw.cc): set by upload when the
+  // snapshot qualifies (not proxylib, at most kRawMaxFields fields)
+  DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes;
+  HttpRawDev raw{};
+  bool raw_ok = false;
 
   void upload(Engine& e);
   uint32_t lookup_prog(uint32_t policy, bool ingress, uint32_t port) const;
@@ -51,6 +56,14 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len);
 // NPDS wire form (serialized DiscoveryResponse of cilium.NetworkPolicy) →
 // the NPDS JSON http_compile and the proxylib translation read (npds_pb.cc).
 std::string npds_pb_to_json(const uint8_t* p, size_t n);
+
+// The raw-head path (http_raw.cc): device tables (called by upload), and
+// verdicts for n raw HTTP/1 request heads already in device memory, in
+// request order, on `stream` with the lease's workspace (synchronizes it).
+void http_raw_upload(HttpSnapshot& S);
+void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const uint8_t* d_raw,
+                          const uint64_t* d_off, size_t n, const uint32_t* d_policy, const uint8_t* d_ingress,
+                          const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, void* stream);
 
 // Upper bounds of a packed batch of n requests (slots, bytes).
 size_t http_batch_slots(const HttpSnapshot& s, size_t n);

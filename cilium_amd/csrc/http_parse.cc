@@ -32,6 +32,9 @@ bool header_char(uint8_t c) { return c == '\t' || (c >= 0x20 && c != 0x7F); }
 
 // Parses one head; appends "name\0value\0" pairs to out.  false = rejected.
 bool parse_head(const uint8_t* p, size_t n, std::string& out) {
+  // Envoy's default max_request_headers_kb (60 KiB) rejects longer heads;
+  // the device parser (kernels_http_raw.hip) applies the same bound
+  if (n > 61440) return false;
   size_t i = 0;
   auto line_end = [&](size_t from) -> size_t {
     for (size_t k = from; k + 1 < n; ++k)

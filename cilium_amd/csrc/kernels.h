@@ -32,4 +32,17 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
                         uint32_t* arena, size_t arena_cap, unsigned long long* ctr, uint8_t* status, void* stream,
                         int cus);
 
+// Raw HTTP/1 heads → batch (kernels_http_raw.hip; sequence in http_raw.cc).
+int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
+                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* hist,
+                         void* rinfo, unsigned long long* ovf_bytes, void* stream, int cus);
+int launch_http_raw_tiles(const HttpRawGroup* groups, uint32_t ngroups, uint32_t ntiles, HttpTile* ttab,
+                          uint8_t* tiles, uint32_t* order, void* stream);
+int launch_http_raw_emit(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
+                         const uint8_t* ingress, const uint32_t* remote, const void* rinfo, uint32_t* cursor,
+                         HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
+                         unsigned long long* arena_cursor, void* stream, int cus);
+int launch_http_raw_scatter(const uint32_t* order, const uint8_t* vslot, size_t nslots, uint8_t* out, void* stream,
+                            int cus);
+
 }  // namespace cg

@@ -62,43 +62,80 @@ __device__ __forceinline__ int32_t l4_wrap(int32_t v, uint32_t mode) {
 // read); bit p = slot*8 + j*2 + c for key j, bucket choice c.  A policy key
 // sits in one slot, so the lowest j whose slot key matches is the verdict;
 // candidates are walked in bit order and a j=0 match ends the walk.
+struct L4Cand {
+  uint64_t cand;   // candidate bits (slot*8 + j*2 + c)
+  uint32_t bk[6];  // bucket of (key j, choice c) at index j*2+c
+  uint32_t w0, pp, eg;
+};
+
 template <typename FpWord>
-__device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, uint32_t w0, uint32_t w1, bool frag,
-                                          uint32_t* val) {
+__device__ __forceinline__ L4Cand l4_candidates(const L4Dev& t, FpWord fpw, uint32_t w0, uint32_t w1, bool frag) {
+  L4Cand r;
   const uint32_t flags = w1 >> 24;
   // key.egress = !dir with dir = CT_INGRESS(1) / CT_EGRESS(0)
-  const uint32_t eg = (flags & CG_L4_F_INGRESS) ? 0u : (1u << 24);
-  const uint32_t pp = (w1 & 0xFFFFFF) | eg;  // dport | proto << 16 | egress << 24
-  const uint32_t P = w0 * kL4MulLo, Q = pp * kL4MulHi, E = eg * kL4MulHi;
-  const uint32_t hi[3] = {pp, eg, pp};
+  r.eg = (flags & CG_L4_F_INGRESS) ? 0u : (1u << 24);
+  r.pp = (w1 & 0xFFFFFF) | r.eg;  // dport | proto << 16 | egress << 24
+  r.w0 = w0;
+  const uint32_t P = w0 * kL4MulLo, Q = r.pp * kL4MulHi, E = r.eg * kL4MulHi;
   const uint32_t h[3] = {l4_fin(P + Q), l4_fin(P + E), l4_fin(Q)};
-  uint32_t bk[3][2];
-  uint64_t cand = 0;
+  r.cand = 0;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     uint32_t fp;
-    l4_place_h(h[j], t.bucket_mask, &bk[j][0], &bk[j][1], &fp);
+    l4_place_h(h[j], t.bucket_mask, &r.bk[2 * j], &r.bk[2 * j + 1], &fp);
     if (j != 1 && frag) continue;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const uint32_t x = fpw(bk[j][c]) ^ (fp * 0x01010101u);
+      const uint32_t x = fpw(r.bk[2 * j + c]) ^ (fp * 0x01010101u);
       const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;  // bit 8s+7: byte s zero
-      cand |= (uint64_t)(z >> 7) << (j * 2 + c);
+      r.cand |= (uint64_t)(z >> 7) << (j * 2 + c);
     }
   }
+  return r;
+}
+
+// The slot a candidate bit names (selects, not indexing: a dynamically
+// indexed array would live in scratch).
+__device__ __forceinline__ const uint4* l4_slot(const L4Dev& t, const L4Cand& r, int bit) {
+  const uint32_t jc = bit & 7;
+  // masks, not a select chain: the compiler turns that into a scratch array
+  const uint32_t b = (r.bk[0] & (0u - (jc == 0))) | (r.bk[1] & (0u - (jc == 1))) | (r.bk[2] & (0u - (jc == 2))) |
+                     (r.bk[3] & (0u - (jc == 3))) | (r.bk[4] & (0u - (jc == 4))) | (r.bk[5] & (0u - (jc >= 5)));
+  return reinterpret_cast<const uint4*>(t.slots + (size_t)b * 4 + (bit >> 3));
+}
+
+__device__ __forceinline__ bool l4_key_is(const L4Cand& r, int j, const uint4& v) {
+  const uint32_t klo = j == 2 ? 0u : r.w0;
+  const uint32_t khi = j == 1 ? r.eg : r.pp;
+  return v.x == klo && v.y == khi;
+}
+
+// Candidates walked in bit order; a key sits in one slot, so the lowest j
+// whose slot matches is the verdict, and a j=0 match ends the walk.  The
+// first candidate's slot arrives loaded (v0, issued together with the other
+// tuples' first loads); later ones load here (false fingerprint matches and
+// tuples that need more than one key are the minority).
+__device__ __forceinline__ int l4_walk(const L4Dev& t, const L4Cand& r, const uint4& v0, uint32_t* val) {
+  uint64_t cand = r.cand;
+  if (!cand) return 0;
   int best = 0;
+  {
+    const int bit = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    const int j = (bit & 7) >> 1;
+    if (l4_key_is(r, j, v0)) {
+      *val = v0.z;
+      best = j + 1;
+      if (j == 0) return best;
+    }
+  }
   while (cand) {
     const int bit = __builtin_ctzll(cand);
     cand &= cand - 1;
-    const int jc = bit & 7, j = jc >> 1;
+    const int j = (bit & 7) >> 1;
     if (best && j + 1 >= best) continue;
-    // selects, not indexing: a dynamically indexed array would live in scratch
-    const uint32_t b = jc == 0 ? bk[0][0] : jc == 1 ? bk[0][1] : jc == 2 ? bk[1][0]
-                     : jc == 3 ? bk[1][1] : jc == 4 ? bk[2][0] : bk[2][1];
-    const uint32_t klo = j == 2 ? 0u : w0;
-    const uint32_t khi = j == 0 ? hi[0] : j == 1 ? hi[1] : hi[2];
-    const uint4 v = *reinterpret_cast<const uint4*>(t.slots + (size_t)b * 4 + (bit >> 3));
-    if (v.x == klo && v.y == khi) {
+    const uint4 v = *l4_slot(t, r, bit);
+    if (l4_key_is(r, j, v)) {
       *val = v.z;
       best = j + 1;
       if (j == 0) break;
@@ -107,11 +144,29 @@ __device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, uint32_t w
   return best;
 }
 
+// The three policy_key lookups of __policy_can_access (bpf/lib/policy.h:61-109)
+// in priority order: j=0 {id, dport, proto, dir} (skipped for fragments),
+// j=1 {id, 0, 0, dir}, j=2 {0, dport, proto, dir} (skipped for fragments).
+// The keys share their hash products: h_j = fin(lo_j*M1 + hi_j*M2) with
+// lo in {id, id, 0} and hi in {pp, eg, pp}.
+//
+// Candidates come from the fingerprint words: a zero-byte test on word^fp
+// (it can flag a byte next to a true match as well, which only costs a slot
+// read); bit p = slot*8 + j*2 + c for key j, bucket choice c.
+template <typename FpWord>
+__device__ __forceinline__ int l4_resolve(const L4Dev& t, FpWord fpw, uint32_t w0, uint32_t w1, bool frag,
+                                          uint32_t* val) {
+  const L4Cand r = l4_candidates(t, fpw, w0, w1, frag);
+  const uint4 v0 = r.cand ? *l4_slot(t, r, __builtin_ctzll(r.cand)) : make_uint4(0, 0, 0, 0);
+  return l4_walk(t, r, v0, val);
+}
+
 // Counter entry in LDS: one u64 per entry id, packets in bits 40..63, bytes in
 // bits 0..39 (lengths below 64 KiB; longer ones go straight to the global
 // byte counter).  A block flushes before it has counted 2^24 tuples, so
 // neither field wraps (2^24 - 1 packets; (2^24 - 1) x 65535 bytes < 2^40).
 constexpr uint32_t kL4Tuples = 4;       // tuples per thread per iteration
+constexpr bool kL4Pipe = false;         // true: the next iteration's tuples load before this one resolves (measured equal)
 constexpr size_t kL4FlushTuples = (size_t)1 << 24;
 
 __device__ __forceinline__ void l4_count(const L4Dev& t, unsigned long long* lcnt, uint32_t id, uint32_t len) {
@@ -167,23 +222,41 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
   const size_t per_iter = (size_t)blockDim.x * kL4Tuples;
   const size_t stride = (size_t)gridDim.x * per_iter;
   size_t since_flush = 0;
-  for (size_t base = (size_t)blockIdx.x * per_iter; base < n; base += stride) {
-    uint32_t w[kL4Tuples][3];
-    uint4 a6[kL4Tuples];
+  // the next iteration's tuples load while this one resolves (software
+  // pipelining: one HBM latency per iteration is hidden under the hashing,
+  // fingerprint and slot phases of the previous one)
+  uint32_t w[kL4Tuples][3], wn[kL4Tuples][3];
+  uint4 a6[kL4Tuples], a6n[kL4Tuples];
+  auto load = [&](size_t b, uint32_t (&ww)[kL4Tuples][3], uint4 (&aa)[kL4Tuples]) {
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
-      size_t i = base + u * blockDim.x + threadIdx.x;
+      size_t i = b + u * blockDim.x + threadIdx.x;
       i = i < n ? i : n - 1;  // unconditional loads (see kafka_kernel)
       if (kFam == 6) {
         const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(addrs) + i);
-        a6[u] = make_uint4(x.x, x.y, x.z, x.w);
-        w[u][0] = 0;
+        aa[u] = make_uint4(x.x, x.y, x.z, x.w);
+        ww[u][0] = 0;
       } else {
-        w[u][0] = kFam == 4 ? __builtin_bswap32(__builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(addrs) + i))
-                            : __builtin_nontemporal_load(tuples + i * 3 + 0);
+        ww[u][0] = kFam == 4 ? __builtin_bswap32(__builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(addrs) + i))
+                             : __builtin_nontemporal_load(tuples + i * 3 + 0);
       }
-      w[u][1] = l4_mode_word(__builtin_nontemporal_load(tuples + i * 3 + 1), mode);
-      w[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
+      ww[u][1] = l4_mode_word(__builtin_nontemporal_load(tuples + i * 3 + 1), mode);
+      ww[u][2] = __builtin_nontemporal_load(tuples + i * 3 + 2);
+    }
+  };
+  if ((size_t)blockIdx.x * per_iter < n) load((size_t)blockIdx.x * per_iter, wn, a6n);
+  for (size_t base = (size_t)blockIdx.x * per_iter; base < n; base += stride) {
+#pragma unroll
+    for (uint32_t u = 0; u < kL4Tuples; ++u) {
+      w[u][0] = wn[u][0];
+      w[u][1] = wn[u][1];
+      w[u][2] = wn[u][2];
+      a6[u] = a6n[u];
+    }
+    if (kL4Pipe) {
+      if (base + stride < n) load(base + stride, wn, a6n);  // uniform
+    } else if (base + stride < n) {
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (kFam == 4) {  // the trie levels, each issued for all tuples of the lane
       uint64_t e[kL4Tuples];
@@ -219,13 +292,23 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], kr[u], vr[u].x);
     }
+    // candidates of every tuple, then every tuple's first slot load in
+    // flight together, then the walks
+    L4Cand rc[kL4Tuples];
+    uint4 v0[kL4Tuples];
+#pragma unroll
+    for (uint32_t u = 0; u < kL4Tuples; ++u)
+      rc[u] = l4_candidates(t, [&](uint32_t b) { return lfp[b]; }, w[u][0], w[u][1],
+                            (w[u][1] >> 24) & CG_L4_F_FRAGMENT);
+#pragma unroll
+    for (uint32_t u = 0; u < kL4Tuples; ++u)  // a lane with no candidate re-reads bucket 0's first slot
+      v0[u] = *l4_slot(t, rc[u], rc[u].cand ? __builtin_ctzll(rc[u].cand) : 0);
 #pragma unroll
     for (uint32_t u = 0; u < kL4Tuples; ++u) {
       const size_t i = base + u * blockDim.x + threadIdx.x;
       if (i >= n) continue;
-      const bool frag = (w[u][1] >> 24) & CG_L4_F_FRAGMENT;
       uint32_t val = 0;
-      const int which = l4_resolve(t, [&](uint32_t b) { return lfp[b]; }, w[u][0], w[u][1], frag, &val);
+      const int which = l4_walk(t, rc[u], v0[u], &val);
       __builtin_nontemporal_store(l4_wrap(l4_verdict(which, val, w[u][1] >> 24), mode), out + i);
       if (which) l4_count(t, lcnt, val & 0xFFFF, w[u][2]);
     }
@@ -235,6 +318,7 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
       l4_flush(t, lcnt);
       since_flush = 0;
     }
+    if (!kL4Pipe && base + stride < n) load(base + stride, wn, a6n);
   }
   l4_flush(t, lcnt);
 }

@@ -31,6 +31,11 @@ constexpr int kWave = 64;
 constexpr int kHttpThreads = 1024;
 constexpr int kTilesPerWave = 1;  // strings walked per lane at a time
 constexpr uint32_t kDealRun = 4;  // consecutive chunks per workgroup turn
+// Runs of chunks are taken from a per-launch ticket counter (dynamic
+// dealing): chunk costs vary with their tiles' string lengths, and a static
+// deal lets the unluckiest workgroup set the kernel's tail.
+constexpr bool kDynamicDeal = true;
+constexpr uint32_t kDealSlots = 256;  // launch ticket slots per device (ring)
 
 __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
   const uint32_t word = (k < 4) ? w.x : (k < 8) ? w.y : (k < 12) ? w.z : w.w;
@@ -551,7 +556,8 @@ __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, ui
 template <bool kGlobal>
 __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
                                             const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                            uint32_t* lcells, uint32_t* s_cnt, uint32_t* s_hits) {
+                                            uint32_t* lcells, uint32_t* s_cnt, uint32_t* s_hits,
+                                            uint32_t* __restrict__ deal) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
   const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
   const uint64_t toff = H->tiles_off, arena_bytes = H->arena_bytes;
@@ -579,8 +585,17 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
   uint32_t cur = kProgDeny;  // program of the current run (its block is in LDS if walked there)
   uint32_t n_allow = 0, n_deny = 0;
   // dealt in runs of kDealRun consecutive chunks (same program, mostly), so
-  // the block is restaged once per run
-  for (uint32_t cr = blockIdx.x * kDealRun; cr < nchunks; cr += gridDim.x * kDealRun)
+  // the block is restaged once per run; dynamic: a run per ticket
+  // the ticket lives in the dynamic LDS (s_cnt[2]): a static __shared__
+  // variable would move the program block off LDS address 0
+  uint32_t& s_ticket = s_cnt[2];
+  uint32_t cr = blockIdx.x * kDealRun;
+  if (kDynamicDeal && deal) {
+    if (threadIdx.x == 0) s_ticket = atomicAdd(&deal[0], 1u);
+    __syncthreads();
+    cr = s_ticket * kDealRun;
+  }
+  for (; cr < nchunks;) {
   for (uint32_t c = cr; c < min(nchunks, cr + kDealRun); ++c) {
     const HttpChunk ch = chunks[c];
     if (ch.first_tile + ch.ntiles > ntiles || ch.ntiles > kChunkTiles) continue;  // malformed chunk
@@ -640,31 +655,49 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       }
     }
   }
+    if (kDynamicDeal && deal) {
+      __syncthreads();  // every wave has read s_ticket
+      if (threadIdx.x == 0) s_ticket = atomicAdd(&deal[0], 1u);
+      __syncthreads();
+      cr = s_ticket * kDealRun;
+    } else {
+      cr += gridDim.x * kDealRun;
+    }
+  }
   flush_counts(T, cur, n_allow, n_deny, lane, s_cnt, s_hits);
+  if (kDynamicDeal && deal && threadIdx.x == 0) {
+    // the last workgroup out resets the slot for the next launch: every
+    // workgroup has drawn its final ticket before it counts itself done
+    __threadfence();
+    if (atomicAdd(&deal[1], 1u) == gridDim.x - 1) {
+      atomicExch(&deal[0], 0u);
+      atomicExch(&deal[1], 0u);
+    }
+  }
 }
 
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
-    uint8_t* __restrict__ out) {
+    uint8_t* __restrict__ out, uint32_t* __restrict__ deal) {
   // dynamic LDS only, so the program block starts at LDS address 0 (a
   // class-mode step's address is then just state + code): [block:
-  // T.lds_cells][rule hits: kLdsRuleHits][allowed, denied]
+  // T.lds_cells][rule hits: kLdsRuleHits][allowed, denied, deal ticket]
   extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
   uint32_t* s_hits = lcells + T.lds_cells;
   uint32_t* s_cnt = s_hits + kLdsRuleHits;
   for (uint32_t i = threadIdx.x; i < kLdsRuleHits; i += blockDim.x) s_hits[i] = 0;
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<false>(T, batch, nslots, arena, out, lcells, s_cnt, s_hits);
+  http_chunks<false>(T, batch, nslots, arena, out, lcells, s_cnt, s_hits, deal);
 }
 
 __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
                                                                    size_t nslots, const uint8_t* __restrict__ arena,
                                                                    uint8_t* __restrict__ out) {
-  __shared__ uint32_t s_cnt[2];
+  __shared__ uint32_t s_cnt[3];
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<true>(T, batch, nslots, arena, out, nullptr, s_cnt, nullptr);
+  http_chunks<true>(T, batch, nslots, arena, out, nullptr, s_cnt, nullptr, nullptr);
 }
 
 }  // namespace
@@ -677,13 +710,29 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   // from several threads)
   int dev = 0;
   (void)hipGetDevice(&dev);
-  const size_t lds = ((size_t)t.lds_cells + kLdsRuleHits + 2) * 4;
+  const size_t lds = ((size_t)t.lds_cells + kLdsRuleHits + 3) * 4;
   int occ = 1;
+  uint32_t* deal = nullptr;
   {
     static std::mutex mu;
     static std::map<std::pair<int, size_t>, int> occ_cache;
     static std::set<int> attr_set;
+    // per device a ring of {ticket, done} pairs, one per launch: each launch's
+    // last workgroup returns its pair to zero, and launches in flight on
+    // other streams hold other pairs (a pair comes back after kDealSlots
+    // launches)
+    static std::map<int, std::pair<uint32_t*, uint32_t>> deal_ring;
     std::lock_guard<std::mutex> lk(mu);
+    if (kDynamicDeal) {
+      auto& r = deal_ring[dev];
+      if (!r.first) {
+        void* p = nullptr;
+        if (hipMalloc(&p, kDealSlots * 2 * sizeof(uint32_t)) == hipSuccess &&
+            hipMemset(p, 0, kDealSlots * 2 * sizeof(uint32_t)) == hipSuccess)
+          r.first = static_cast<uint32_t*>(p);
+      }
+      if (r.first) deal = r.first + 2 * (r.second++ % kDealSlots);
+    }
     if (attr_set.insert(dev).second)
       (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     auto it = occ_cache.find({dev, lds});
@@ -706,7 +755,7 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   const size_t tiles = nslots / kWave;
   size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);
   hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
-                     (const uint8_t*)batch, nslots, arena, out);
+                     (const uint8_t*)batch, nslots, arena, out, deal);
   if (t.n_global_progs) {
     grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
     hipLaunchKernelGGL(http_kernel_global, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream, t,

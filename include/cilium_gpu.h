@@ -433,6 +433,26 @@ int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* in
 int cg_http_parse_heads(const uint8_t* raw, const uint64_t* raw_off, size_t n, uint8_t* hdr_blob,
                         size_t blob_cap, uint64_t* hdr_off, size_t* blob_used, uint8_t* ok);
 
+/* Raw HTTP/1 request heads to verdicts on the device: the codec step of
+ * cg_http_parse_heads, the packing of cg_http_pack and the verdicts of
+ * cg_http_verdicts_dev in one call, with the request bytes never leaving
+ * device memory (the consumer is AccessFilter::
+ * decodeHeaders, envoy/cilium_l7policy.cc:127-170).  Request r is
+ * d_raw[d_raw_off[r] .. d_raw_off[r+1]) with d_policy/d_ingress/d_port/
+ * d_remote as in cg_http_pack; d_out[r] = 1 allow, 0 deny, request order.
+ * Heads over 60 KiB are rejected (Envoy's default max_request_headers_kb).
+ * Runs on `stream` (NULL: the handle's) and synchronizes it (its workspace is
+ * the handle's).  CG_UNSUPPORTED when the snapshot walks more than 32 header
+ * fields or is a proxylib snapshot. */
+int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,
+                             const uint32_t* d_policy, const uint8_t* d_ingress, const uint16_t* d_port,
+                             const uint32_t* d_remote, uint8_t* d_out, void* stream);
+
+/* cg_http_verdicts_raw_dev from host memory (staged in, verdicts copied out). */
+int cg_http_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                              const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                              const uint32_t* remote, uint8_t* out);
+
 /* NetworkPolicyMap::Allowed per slot (cilium_network_policy.h:223-237):
  * d_out[slot] = 1 allow, 0 deny (→ 403), in batch slot order.  d_arena may
  * be NULL when no record overflowed.  Per-(policy,direction,port) allowed/

@@ -14,8 +14,13 @@ _FIELD = re.compile(rb"(" + _TOKEN + rb"):[ \t]*(.*?)[ \t]*\Z", re.S)
 _BAD_VALUE = re.compile(rb"[\x00-\x08\x0a-\x1f\x7f]")
 
 
+MAX_HEAD = 60 * 1024  # Envoy's default max_request_headers_kb
+
+
 def parse_head(raw: bytes):
     """→ list of (name, value) as the filter sees them, or None if rejected."""
+    if len(raw) > MAX_HEAD:
+        return None
     end = raw.find(b"\r\n\r\n")
     if end < 0:
         # no empty line: an incomplete head
