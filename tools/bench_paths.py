@@ -286,6 +286,47 @@ def bench_http_host(torch, dev, stream, cl, args, threads):
                        "requests": n, "header_bytes": hdr_bytes}}
 
 
+def bench_http_raw(torch, dev, stream, cl, args, threads):
+    """Config 5 requests as raw HTTP/1 heads resident in HBM →
+    cg_http_verdicts_raw_dev: the codec step, program lookup, packing and the
+    verdicts all on the GPU (kernels_http_raw.hip + http_kernel), one call
+    per step (it synchronizes its stream: a host layout step sits between
+    the scan and the emit kernels)."""
+    import oracle  # noqa: F401  (the check below uses the host path)
+    from cilium_amd import synth
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_http_parse import _blob, _raw_requests
+    pols, info = synth.http10k_rules()
+    cl.update_http_policy(pols)
+    D, reps = 65_536, 1_900
+    rq = synth.http10k_requests(D, info, seed=synth.SEED ^ 0x4A1)
+    raws = _raw_requests(rq)
+    blob, off = _blob(raws)
+    args_ = (rq["policy"], rq["ingress"], rq["port"], rq["remote"])
+    want = cl.http_verdicts(cl.pack_http_raw(*args_, blob, off))
+    tot = int(off[-1])
+    d_raw = tile_dev(torch, blob[:tot], reps, dev)
+    base = torch.arange(reps, dtype=torch.int64, device=dev).unsqueeze(1) * tot
+    d_off = torch.cat([(torch.from_numpy(off[:-1].astype(np.int64)).to(dev).unsqueeze(0) + base).reshape(-1),
+                       torch.tensor([tot * reps], dtype=torch.int64, device=dev)])
+    rep = lambda a, dt: tile_dev(torch, np.asarray(a).astype(dt), reps, dev)
+    d_pol, d_ing, d_port, d_rem = rep(args_[0], np.uint32), rep(args_[1], np.uint8), rep(args_[2], np.uint16), \
+        rep(args_[3], np.uint32)
+    n = D * reps
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    run = lambda: cl.http_verdicts_raw_dev(d_raw, d_off, n, d_pol, d_ing, d_port, d_rem, d_out,
+                                           stream=stream.cuda_stream)
+    sec = timed(torch, stream, run, args.steps, 1)
+    got = d_out.view(reps, D)
+    assert bool((got == torch.from_numpy(want).to(dev).unsqueeze(0)).all()), "raw-path verdicts differ from host path"
+    bpi = tot / D + 4 + 1 + 2 + 4 + 8 + 1  # head bytes, policy/ingress/port/remote, offset, verdict
+    return line("HTTP/1 raw heads → verdicts/s on the GPU (codec step + packing + http_kernel), config 5", n, sec,
+                bpi, "raw_scan+raw_emit+http_kernel", None, "", threads,
+                {"config": {"workload": f"BASELINE config 5 requests as raw HTTP/1 heads ({tot / D:.1f} B/head avg), "
+                            "10K rules", "requests": n},
+                 "request_gbps": n * (tot / D) / sec / 1e9})
+
+
 def bench_ipcache(torch, dev, stream, cl, args, threads):
     import oracle
     from cilium_amd import synth
@@ -455,7 +496,7 @@ def main():
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
-           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire, "httphost": bench_http_host}
+           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire, "httphost": bench_http_host, "httpraw": bench_http_raw}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()
