@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--layout", default="tile", choices=["tile", "copy"],
+                    help="order of the replicated tiles within a program group (replicate_batch)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="rehearse the N-rank launch, rendezvous and counter all-reduce on the CPU (gloo, the "
                          "library's host table walker on a small batch): no GPU, and not a measurement")
@@ -105,7 +107,7 @@ def main():
     b = cl.pack_http(**rq)
     reps = max(1, args.requests_per_gpu // D)
     B = reps * D                                  # requests per GPU per step
-    d_batch, nslots, tile_map, data_bytes = replicate_batch(b, reps, dev, torch)
+    d_batch, nslots, tile_map, data_bytes = replicate_batch(b, reps, dev, torch, layout=args.layout)
     d_arena = torch.from_numpy(b.arena).to(dev)
     d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
     n_ctr = cl.allreduce_counter_count()
@@ -316,15 +318,22 @@ def batch_parts(batch: np.ndarray):
     return ntiles, toff, chunks, ttab
 
 
-def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False):
+def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False, layout: str = "tile"):
     """Device batch of `reps` copies of packed batch b, laid out as the packer
-    lays out a batch of reps x D requests: each program's tiles (its `reps`
-    copies) are contiguous and cut into chunks of CHUNK_TILES
-    (http_pack.cc).  Returns (device batch, nslots, tile_map, data_bytes)
-    where tile_map[t] is the tile of the first copy of b's tile t and
-    data_bytes the bytes of the packed input (tables + tiles).  With
-    return_groups, also [(first tile in b, tiles, first tile of copy 0)] per
-    program group: copy r of b's tile first + j is tile at + r * tiles + j."""
+    lays out a batch of reps x D requests: each program's tiles are
+    contiguous and cut into chunks of CHUNK_TILES (http_pack.cc).
+
+    layout "tile" (default): within a program group the packer orders the
+    whole batch by string units (then content), so a large batch's tiles
+    ascend in units across the group; each of b's tiles is placed `reps`
+    times in a row, in b's (ascending) tile order.  layout "copy" (round 1)
+    repeats b's whole group `reps` times — an ascending run every D requests,
+    which no packer produces for one batch.
+
+    Returns (device batch, nslots, tile_map, data_bytes) where tile_map[t] is
+    the tile of the first copy of b's tile t and data_bytes the bytes of the
+    packed input (tables + tiles).  With return_groups, also [(first tile in
+    b, tiles, first tile of the group)] per program group."""
     ntiles, toff, chunks, ttab = batch_parts(b.batch)
     groups = []  # (prog, first tile, ntiles) of each program group of b
     for prog, first, nt, _ in chunks:
@@ -337,14 +346,23 @@ def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False):
     units = units_field & 0xFFFF
     span = 1 + 2 * units               # granules per tile: meta block + 1 KiB units
     big, new_tt, placed, pos, kpos = [], [], [], 0, 0
+    tile_map = np.zeros(ntiles, np.int64)
     for prog, first, nt in groups:
         run = nt * reps
         for k in range(0, run, CHUNK_TILES):
             big.append((prog, pos + k, min(CHUNK_TILES, run - k), 0))
         g_kib = int(kib[first + nt - 1] + span[first + nt - 1] - kib[first])
         rel = kib[first:first + nt] - kib[first]
-        for r in range(reps):
-            new_tt.append(np.stack([kpos + r * g_kib + rel, units_field[first:first + nt]], axis=1))
+        if layout == "copy":
+            for r in range(reps):
+                new_tt.append(np.stack([kpos + r * g_kib + rel, units_field[first:first + nt]], axis=1))
+            tile_map[first:first + nt] = np.arange(pos, pos + nt)
+        else:
+            sp = span[first:first + nt]
+            at0 = kpos + np.concatenate([[0], np.cumsum(sp * reps)[:-1]])  # first copy of each tile
+            at = (at0[:, None] + np.arange(reps)[None, :] * sp[:, None]).reshape(-1)
+            new_tt.append(np.stack([at, np.repeat(units_field[first:first + nt], reps)], axis=1))
+            tile_map[first:first + nt] = pos + np.arange(nt) * reps
         placed.append((first, nt, pos, int(kib[first]), g_kib, kpos))
         pos += run
         kpos += reps * g_kib
@@ -365,37 +383,25 @@ def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False):
     d[:hbytes].copy_(torch.from_numpy(head))
     data_end = int(kib[-1] + span[-1]) * 512 if ntiles else 0
     src = torch.from_numpy(b.batch[toff:toff + data_end]).to(dev)
-    tile_map = np.zeros(ntiles, np.int64)
     for first, nt, at, k0, g_kib, kp in placed:
         g0, gb = hbytes + kp * 512, g_kib * 512
-        d[g0:g0 + gb].copy_(src[k0 * 512:k0 * 512 + gb])
-        done = 1
-        while done < reps:  # doubling copies on the device
-            k = min(done, reps - done)
-            d[g0 + done * gb:g0 + (done + k) * gb].copy_(d[g0:g0 + k * gb])
-            done += k
-        tile_map[first:first + nt] = np.arange(at, at + nt)
+        if layout == "copy":
+            d[g0:g0 + gb].copy_(src[k0 * 512:k0 * 512 + gb])
+            done = 1
+            while done < reps:  # doubling copies on the device
+                k = min(done, reps - done)
+                d[g0 + done * gb:g0 + (done + k) * gb].copy_(d[g0:g0 + k * gb])
+                done += k
+        else:
+            # granule gather: each tile's granules `reps` times in a row
+            gran = src[k0 * 512:k0 * 512 + gb].view(-1, 512)
+            rel = kib[first:first + nt] - kib[first]
+            sp = span[first:first + nt]
+            idx = np.concatenate([np.tile(np.arange(r0, r0 + s), reps) for r0, s in zip(rel, sp)])
+            d[g0:g0 + gb * reps].view(-1, 512).copy_(gran[torch.from_numpy(idx).to(dev)])
     if return_groups:
         return d, pos * 64, tile_map, total - 64, [(first, nt, at) for first, nt, at, _, _, _ in placed]
     return d, pos * 64, tile_map, total - 64
-
-
-def pmc_traffic(requests_per_launch: int):
-    """HBM bytes per launch of the verdict kernel from the newest committed
-    PMC summary (profiles/r*_http_pmc.json, written by tools/pmc_summary.py
-    from separate rocprofv3 --pmc passes of the same workload: FETCH_SIZE ×2
-    gfx950 correction + WRITE_SIZE), scaled to this launch's request count.
-    rocprofv3 cannot run inside the timed process, hence a committed file."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_http_pmc.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        s = json.load(f)
-    per_item = s.get("hbm_bytes_per_item")
-    if not per_item:
-        return None, None
-    return per_item * requests_per_launch, os.path.relpath(files[-1], ROOT)
 
 
 def cpu_model() -> str:

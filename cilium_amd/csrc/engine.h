@@ -83,7 +83,7 @@ class PinnedMem {
 // device buffers and pinned host buffers, so host calls make no hipMalloc /
 // hipFree and copy with async DMA instead of pageable hipMemcpy.
 struct StagingSlot {
-  static constexpr int kBufs = 16;  // 0..7 host staging, 8..15 the raw HTTP path's workspace
+  static constexpr int kBufs = 19;  // 0..7 host staging, 8..18 the raw HTTP path's workspace
   void* stream = nullptr;  // hipStream_t
   DevMem dev[kBufs];
   PinnedMem host[kBufs];

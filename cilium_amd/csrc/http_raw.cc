@@ -92,8 +92,18 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   auto* ovf = (unsigned long long*)(small + hist_bytes);
   hip_check(hipMemsetAsync(small, 0, hist_bytes + 16, st), "hipMemsetAsync");
   void* rinfo = sl.dev_buf(9, n * 8);
-  hip_check(launch_http_raw_scan(s.raw, d_raw, d_off, n, d_policy, d_ingress, d_port, hist, rinfo, ovf, st, cus),
+  // per-block bucket counts → per-block slot offsets (when the bucket
+  // counters fit the kernels' LDS), else one global histogram
+  const bool lds_keys = http_raw_lds_keys(s.raw);
+  const uint32_t nblk = (uint32_t)http_raw_grid(n, cus);
+  uint32_t* bcount = lds_keys ? (uint32_t*)sl.dev_buf(16, (size_t)G * K * nblk * 4) : hist;
+  uint32_t* bbase = lds_keys ? (uint32_t*)sl.dev_buf(17, (size_t)G * K * nblk * 4) : nullptr;
+  auto* spans = (uint32_t*)sl.dev_buf(18, (size_t)std::max(s.raw.nfields, 1u) * n * 4);
+  hip_check(launch_http_raw_scan(s.raw, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, spans, ovf, st,
+                                 cus),
             "raw scan kernel launch");
+  if (lds_keys)
+    hip_check(launch_http_raw_prefix(bcount, G * K, nblk, bbase, hist, st), "raw prefix kernel launch");
   uint8_t* hh = (uint8_t*)sl.host_buf(8, hist_bytes + 16);
   hip_check(hipMemcpyAsync(hh, small, hist_bytes + 8, hipMemcpyDeviceToHost, st), "D2H");
   hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
@@ -157,8 +167,8 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   uint8_t* tdata = batch + hdr.tiles_off;
   hip_check(launch_http_raw_tiles(d_groups, (uint32_t)groups.size(), tiles, ttab, tdata, order, st),
             "raw tiles kernel launch");
-  hip_check(launch_http_raw_emit(s.raw, d_raw, d_off, n, d_ingress, d_remote, rinfo, d_cursor, ttab, tdata, order,
-                                 arena, ovf + 1, st, cus),
+  hip_check(launch_http_raw_emit(s.raw, d_raw, d_off, n, d_ingress, d_remote, rinfo, d_cursor, bbase, ttab, tdata,
+                                 order, arena, ovf + 1, spans, st, cus),
             "raw emit kernel launch");
   hip_check(launch_http(s.dev, batch, nslots, arena, vslot, st, cus), "http kernel launch");
   hip_check(launch_http_raw_scatter(order, vslot, nslots, d_out, st, cus), "raw scatter kernel launch");

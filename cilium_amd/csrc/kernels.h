@@ -33,15 +33,25 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
                         int cus);
 
 // Raw HTTP/1 heads → batch (kernels_http_raw.hip; sequence in http_raw.cc).
+// The scan and emit kernels run http_raw_grid(n, cus) blocks.  With
+// http_raw_lds_keys(R) the scan writes per-block bucket counts
+// (counts[key * grid + block]) and raw_prefix turns them into per-block slot
+// offsets (bbase) and totals (hist); otherwise the scan adds into a global
+// histogram (counts = hist) and the emit takes slots from global cursors.
+// spans: nfields × n u32 (field-major), the scan's value spans for the emit.
+size_t http_raw_grid(size_t n, int cus);
+bool http_raw_lds_keys(const HttpRawDev& R);
 int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
-                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* hist,
-                         void* rinfo, unsigned long long* ovf_bytes, void* stream, int cus);
+                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
+                         void* rinfo, uint32_t* spans, unsigned long long* ovf_bytes, void* stream, int cus);
+int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk, uint32_t* bbase, uint32_t* hist,
+                           void* stream);
 int launch_http_raw_tiles(const HttpRawGroup* groups, uint32_t ngroups, uint32_t ntiles, HttpTile* ttab,
                           uint8_t* tiles, uint32_t* order, void* stream);
 int launch_http_raw_emit(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint8_t* ingress, const uint32_t* remote, const void* rinfo, uint32_t* cursor,
-                         HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
-                         unsigned long long* arena_cursor, void* stream, int cus);
+                         const uint32_t* bbase, HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
+                         unsigned long long* arena_cursor, const uint32_t* spans, void* stream, int cus);
 int launch_http_raw_scatter(const uint32_t* order, const uint8_t* vslot, size_t nslots, uint8_t* out, void* stream,
                             int cus);
 

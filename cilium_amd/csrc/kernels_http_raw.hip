@@ -52,16 +52,20 @@ __device__ __forceinline__ bool tchar(uint32_t c) {
 }
 __device__ __forceinline__ uint32_t lower(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
-// A lane's head read through 16-byte aligned loads, one block kept in
-// registers; blocks reaching outside the head are assembled from byte loads
-// of the head's own bytes.
+// A lane's head: from its wave's LDS stage when the head lies inside it
+// (the common case), else through 16-byte aligned global loads with one
+// block kept in registers (blocks reaching outside the head are assembled
+// from byte loads of the head's own bytes).
 struct HeadReader {
   const uint8_t* p;
   uint32_t n;
+  const uint8_t* lp;  // the head in LDS, or nullptr
   uint64_t cur;
   uint4 w;
-  __device__ __forceinline__ HeadReader(const uint8_t* p_, uint32_t n_) : p(p_), n(n_), cur(~0ull), w{0, 0, 0, 0} {}
+  __device__ __forceinline__ HeadReader(const uint8_t* p_, uint32_t n_, const uint8_t* lp_)
+      : p(p_), n(n_), lp(lp_), cur(~0ull), w{0, 0, 0, 0} {}
   __device__ __forceinline__ uint32_t at(uint32_t k) {
+    if (lp) return lp[k];
     const uint64_t a = (uint64_t)(uintptr_t)(p + k);
     const uint64_t blk = a & ~15ull;
     if (blk != cur) {
@@ -92,6 +96,49 @@ struct HeadReader {
     return (x >> ((o & 3) * 8)) & 0xFFu;
   }
 };
+
+// The wave's 64 consecutive heads [off[i0], off[i1]) copied into its LDS
+// stage (kStage bytes) with coalesced 16-byte loads: returns the global
+// address the stage starts at (16-byte aligned) and, in *len, the bytes it
+// holds.  Bytes outside the heads' range are loaded byte-wise, only those
+// inside it.
+constexpr uint32_t kStage = 8192;
+__device__ __forceinline__ uint64_t stage_heads(const uint8_t* __restrict__ raw, uint64_t lo, uint64_t hi,
+                                                uint8_t* stage, uint32_t lane, uint32_t* len) {
+  const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
+  const uint64_t a0 = glo & ~15ull;
+  const uint32_t nb = (uint32_t)min<uint64_t>((ghi - a0 + 15) & ~15ull, kStage);
+  for (uint32_t j = lane * 16; j < nb; j += 64 * 16) {
+    const uint64_t a = a0 + j;
+    uint4 v;
+    if (a >= glo && a + 16 <= ghi) {
+      v = *reinterpret_cast<const uint4*>((uintptr_t)a);
+    } else {
+      uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) {
+        const uint64_t x = a + b;
+        const uint32_t byte = (x >= glo && x < ghi) ? *reinterpret_cast<const uint8_t*>((uintptr_t)x) : 0u;
+        const uint32_t sh = (b & 3) * 8;
+        if (b < 4) v0 |= byte << sh;
+        else if (b < 8) v1 |= byte << sh;
+        else if (b < 12) v2 |= byte << sh;
+        else v3 |= byte << sh;
+      }
+      v = make_uint4(v0, v1, v2, v3);
+    }
+    *reinterpret_cast<uint4*>(stage + j) = v;
+  }
+  *len = nb;
+  return a0;
+}
+
+// A wave's LDS writes visible to its own later reads (and its reads done
+// before it overwrites the stage)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // The field a header name (lowercase FNV-1a h, length nl, at head offset k)
 // is, or -1.
@@ -225,48 +272,112 @@ __device__ __forceinline__ uint32_t group_of(const HttpRawDev& R, uint32_t prog)
   return prog < R.nprogs ? prog : R.nprogs + (prog == kProgAllow ? 0u : 1u);
 }
 
-// ---- pass 1: program, string length, bucket key, histogram
+// Dynamic LDS of the scan and emit kernels: [spans: nfields × 256 u32]
+// [4 wave stages × kStage bytes][bucket counters/cursors: nkeys u32, when
+// they fit (lds_keys)].
+__device__ __forceinline__ uint8_t* wave_stage(uint32_t* lds, uint32_t F, uint32_t wave) {
+  return reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + wave * kStage;
+}
+__device__ __forceinline__ uint32_t* key_counters(uint32_t* lds, uint32_t F) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + 4 * kStage);
+}
+// The head of request i as a reader: in the stage if it lies inside it.
+__device__ __forceinline__ HeadReader head_of(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
+                                              size_t i, const uint8_t* stage, uint64_t sbase, uint32_t slen) {
+  const uint64_t a = off[i], b = off[i + 1];
+  const uint32_t n = b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
+  const uint64_t ga = (uint64_t)(uintptr_t)(raw + a);
+  const bool in = ga >= sbase && ga + n <= sbase + slen;
+  return HeadReader(raw + a, n, in ? stage + (ga - sbase) : nullptr);
+}
+
+// ---- pass 1: program, string length, bucket key; per-block bucket counts
+// (bcount[key * gridDim.x + block], lds_keys) or a global histogram
 __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, const uint8_t* __restrict__ raw,
                                                                const uint64_t* __restrict__ off, size_t n,
                                                                const uint32_t* __restrict__ policy,
                                                                const uint8_t* __restrict__ ingress,
                                                                const uint16_t* __restrict__ port,
-                                                               uint32_t* __restrict__ hist, uint2* __restrict__ rinfo,
+                                                               uint32_t* __restrict__ counts, uint2* __restrict__ rinfo,
+                                                               uint32_t* __restrict__ gspans,
                                                                unsigned long long* __restrict__ ovf_bytes,
-                                                               uint32_t lds_hist) {
+                                                               uint32_t lds_keys) {
   extern __shared__ uint32_t lds[];
+  const uint32_t F = max(R.nfields, 1u), wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* sp = lds + threadIdx.x;  // this lane's spans: sp[f * kRawThreads]
-  uint32_t* lh = lds + kRawMaxFields * kRawThreads;
-  const uint32_t nb = (R.nprogs + 2) * kRawKeys;
-  if (lds_hist)
-    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) lh[k] = 0;
+  uint8_t* stage = wave_stage(lds, F, wave);
+  uint32_t* lk = key_counters(lds, F);
+  const uint32_t nk = (R.nprogs + 2) * kRawKeys;
+  if (lds_keys)
+    for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = 0;
   __syncthreads();
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t prog = lookup_prog(R, policy[i], ingress[i] != 0, port[i]);
-    uint32_t key = 0, len = 0, bad = 0;
+  for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
+    const size_t i0 = base + (size_t)wave * 64;
+    if (i0 >= n) continue;  // wave-uniform
+    const size_t i = i0 + lane;
+    const bool live = i < n;
+    const uint32_t prog = live ? lookup_prog(R, policy[i], ingress[i] != 0, port[i]) : kProgDeny;
     // every request but an unknown policy's is parsed: a head the codec
     // rejects is denied in any program (flagged malformed)
-    if (prog != kProgDeny) {
-      const uint64_t a = off[i], b = off[i + 1];
-      HeadReader hr(raw + a, b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u);
-      if (!parse_head(R, hr, sp, kRawThreads)) {
-        bad = 1;
-      } else if (walked(R, prog)) {
-        uint32_t last;
-        len = string_len(R, sp, kRawThreads, &last);
-        key = len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
-        if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
+    const bool parse = live && prog != kProgDeny;
+    uint32_t slen = 0;
+    uint64_t sbase = 0;
+    if (__any(parse)) sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
+    wave_sync();
+    if (live) {
+      uint32_t key = 0, len = 0, bad = 0;
+      if (parse) {
+        HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
+        if (!parse_head(R, hr, sp, kRawThreads)) {
+          bad = 1;
+        } else if (walked(R, prog)) {
+          uint32_t last;
+          len = string_len(R, sp, kRawThreads, &last);
+          key = len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
+          // the value spans for the emit pass (field-major: coalesced)
+          for (uint32_t f = 0; f < R.nfields; ++f) gspans[(size_t)f * n + i] = sp[f * kRawThreads];
+          if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
+        }
       }
+      rinfo[i] = make_uint2(prog, len | bad << 31);
+      const uint32_t k = group_of(R, prog) * kRawKeys + key;
+      if (lds_keys) atomicAdd(&lk[k], 1u);
+      else atomicAdd(&counts[k], 1u);
     }
-    rinfo[i] = make_uint2(prog, len | bad << 31);
-    const uint32_t slot = group_of(R, prog) * kRawKeys + key;
-    if (lds_hist) atomicAdd(&lh[slot], 1u);
-    else atomicAdd(&hist[slot], 1u);
+    wave_sync();  // the stage is read before the next iteration overwrites it
   }
-  if (lds_hist) {
+  if (lds_keys) {
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x)
-      if (lh[k]) atomicAdd(&hist[k], lh[k]);
+    for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) counts[(size_t)k * gridDim.x + blockIdx.x] = lk[k];
+  }
+}
+
+// Per bucket key: exclusive prefix of the per-block counts (each block's
+// first slot offset within the key's bucket) and the key's total.
+__global__ __launch_bounds__(256) void raw_prefix_kernel(const uint32_t* __restrict__ bcount, uint32_t nblk,
+                                                         uint32_t* __restrict__ bbase, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t part[256];
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  const uint32_t* row = bcount + (size_t)k * nblk;
+  const uint32_t per = (nblk + 255) / 256, lo = min(t * per, nblk), hi = min(lo + per, nblk);
+  uint32_t sum = 0;
+  for (uint32_t j = lo; j < hi; ++j) sum += row[j];
+  part[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (uint32_t j = 0; j < 256; ++j) {
+      const uint32_t v = part[j];
+      part[j] = run;
+      run += v;
+    }
+    hist[k] = run;
+  }
+  __syncthreads();
+  uint32_t run = part[t];
+  for (uint32_t j = lo; j < hi; ++j) {
+    bbase[(size_t)k * nblk + j] = run;
+    run += row[j];
   }
 }
 
@@ -348,59 +459,85 @@ __device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr,
   if (last < R.nfields) o.put(code[2]);
 }
 
-// ---- pass 2: slots, meta, strings
+// ---- pass 2: slots, meta, strings.  Slots: the block's LDS cursor per key
+// (the key's first slot + this block's prefix, lds_keys), else a global
+// cursor per key.
 __global__ __launch_bounds__(kRawThreads) void raw_emit_kernel(
     HttpRawDev R, const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off, size_t n,
     const uint8_t* __restrict__ ingress, const uint32_t* __restrict__ remote, const uint2* __restrict__ rinfo,
-    uint32_t* __restrict__ cursor, HttpTile* __restrict__ ttab, uint8_t* __restrict__ tiles,
-    uint32_t* __restrict__ order, uint8_t* __restrict__ arena, unsigned long long* __restrict__ arena_cursor) {
+    uint32_t* __restrict__ cursor, const uint32_t* __restrict__ bbase, uint32_t lds_keys, HttpTile* __restrict__ ttab,
+    uint8_t* __restrict__ tiles, uint32_t* __restrict__ order, uint8_t* __restrict__ arena,
+    unsigned long long* __restrict__ arena_cursor, const uint32_t* __restrict__ gspans, uint32_t lds_codes) {
   extern __shared__ uint32_t lds[];
+  const uint32_t F = max(R.nfields, 1u), wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* sp = lds + threadIdx.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const uint2 ri = rinfo[i];
+  uint8_t* stage = wave_stage(lds, F, wave);
+  uint32_t* lk = key_counters(lds, F);
+  const uint32_t nk = (R.nprogs + 2) * kRawKeys;
+  if (lds_keys)
+    for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x)
+      lk[k] = cursor[k] + bbase[(size_t)k * gridDim.x + blockIdx.x];
+  // the programs' code maps in LDS (after the key cursors) when they fit
+  uint8_t* lcode = reinterpret_cast<uint8_t*>(lk + (lds_keys ? nk : 0));
+  if (lds_codes)
+    for (uint32_t k = threadIdx.x; k < R.nprogs * 64; k += blockDim.x)
+      reinterpret_cast<uint32_t*>(lcode)[k] = reinterpret_cast<const uint32_t*>(R.codes)[k];
+  __syncthreads();
+  for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
+    const size_t i0 = base + (size_t)wave * 64;
+    if (i0 >= n) continue;  // wave-uniform
+    const size_t i = i0 + lane;
+    const bool live = i < n;
+    const uint2 ri = live ? rinfo[i] : make_uint2(kProgDeny, 0);
     const uint32_t prog = ri.x, len = ri.y & 0x7FFFFFFFu;
-    const bool bad = ri.y >> 31, walk = walked(R, prog) && !bad;
-    const uint32_t key = !walk ? 0u : len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
-    const uint32_t slot = atomicAdd(&cursor[group_of(R, prog) * kRawKeys + key], 1u);
-    order[slot] = (uint32_t)i;
-    const uint32_t t = slot >> 6, lane = slot & 63;
-    const HttpTile tt = ttab[t];
-    uint8_t* tb = tiles + (size_t)tt.at * 512;
-    uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u);
-    uint32_t aoff16 = 0;
-    if (walked(R, prog) && !walk) {  // a rejected head in a walked tile: zero units
-      Out16 o(reinterpret_cast<uint4*>(tb + 512 + (size_t)lane * 16), 1024 / 16);
-      while (o.stored < tile_units(tt)) o.flush();
-    }
-    if (walk) {
-      const uint64_t a = off[i], b = off[i + 1];
-      HeadReader hr(raw + a, (uint32_t)(b - a));
-      parse_head(R, hr, sp, kRawThreads);  // accepted in pass 1
-      uint32_t last;
-      string_len(R, sp, kRawThreads, &last);
-      const uint8_t* code = R.codes + (size_t)prog * 256;
-      if (key == kRawKeys - 1) {  // overflow arena entry: u32 length, the string, 16-byte aligned
-        flags |= CG_HTTP_F_OVERFLOW;
-        const unsigned long long ao = atomicAdd(arena_cursor, (unsigned long long)((4 + len + 15) & ~15u));
-        aoff16 = (uint32_t)(ao / 16);
-        Out16 o(reinterpret_cast<uint4*>(arena + ao), 1);
-        o.w0 = len;
-        o.pos = 4;
-        emit_string(R, hr, sp, kRawThreads, last, code, o);
-        if (o.pos) o.flush();
-        Out16 z(reinterpret_cast<uint4*>(tb + 512 + (size_t)lane * 16), 1024 / 16);
-        while (z.stored < tile_units(tt)) z.flush();  // the tile's units are not this lane's string
-      } else {
-        const uint32_t units = tile_units(tt);
-        Out16 o(reinterpret_cast<uint4*>(tb + 512 + (size_t)lane * 16), 1024 / 16);
-        emit_string(R, hr, sp, kRawThreads, last, code, o);
-        if (o.pos) o.flush();
-        while (o.stored < units) o.flush();  // zero padding up to the tile's units
-        if (key == units && units)
-          atomicMax(&ttab[t].units, units | (len - 16 * (units - 1)) << 16);
+    const bool bad = ri.y >> 31, walk = live && walked(R, prog) && !bad;
+    uint32_t slen = 0;
+    uint64_t sbase = 0;
+    if (__any(walk)) sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
+    wave_sync();
+    if (live) {
+      const uint32_t key = !walk ? 0u : len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
+      const uint32_t k = group_of(R, prog) * kRawKeys + key;
+      const uint32_t slot = lds_keys ? atomicAdd(&lk[k], 1u) : atomicAdd(&cursor[k], 1u);
+      order[slot] = (uint32_t)i;
+      const uint32_t t = slot >> 6, sl = slot & 63;
+      const HttpTile tt = ttab[t];
+      uint8_t* tb = tiles + (size_t)tt.at * 512;
+      uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u);
+      uint32_t aoff16 = 0;
+      if (walked(R, prog) && !walk) {  // a rejected head in a walked tile: zero units
+        Out16 o(reinterpret_cast<uint4*>(tb + 512 + (size_t)sl * 16), 1024 / 16);
+        while (o.stored < tile_units(tt)) o.flush();
       }
+      if (walk) {
+        HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
+        for (uint32_t f = 0; f < R.nfields; ++f) sp[f * kRawThreads] = gspans[(size_t)f * n + i];  // pass 1's
+        uint32_t last;
+        string_len(R, sp, kRawThreads, &last);
+        const uint8_t* code = (lds_codes ? lcode : R.codes) + (size_t)prog * 256;
+        if (key == kRawKeys - 1) {  // overflow arena entry: u32 length, the string, 16-byte aligned
+          flags |= CG_HTTP_F_OVERFLOW;
+          const unsigned long long ao = atomicAdd(arena_cursor, (unsigned long long)((4 + len + 15) & ~15u));
+          aoff16 = (uint32_t)(ao / 16);
+          Out16 o(reinterpret_cast<uint4*>(arena + ao), 1);
+          o.w0 = len;
+          o.pos = 4;
+          emit_string(R, hr, sp, kRawThreads, last, code, o);
+          if (o.pos) o.flush();
+          Out16 z(reinterpret_cast<uint4*>(tb + 512 + (size_t)sl * 16), 1024 / 16);
+          while (z.stored < tile_units(tt)) z.flush();  // the tile's units are not this lane's string
+        } else {
+          const uint32_t units = tile_units(tt);
+          Out16 o(reinterpret_cast<uint4*>(tb + 512 + (size_t)sl * 16), 1024 / 16);
+          emit_string(R, hr, sp, kRawThreads, last, code, o);
+          if (o.pos) o.flush();
+          while (o.stored < units) o.flush();  // zero padding up to the tile's units
+          if (key == units && units) atomicMax(&ttab[t].units, units | (len - 16 * (units - 1)) << 16);
+        }
+      }
+      reinterpret_cast<uint2*>(tb)[sl] = make_uint2(remote[i], (aoff16 & 0xFFFFFFu) | flags << 24);
     }
-    reinterpret_cast<uint2*>(tb)[lane] = make_uint2(remote[i], (aoff16 & 0xFFFFFFu) | flags << 24);
+    wave_sync();
   }
 }
 
@@ -417,18 +554,37 @@ unsigned grid_for(size_t n, int cus, unsigned per_cu) {
   return (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)cus * per_cu));
 }
 
+// LDS of the scan / emit kernels (see wave_stage, key_counters)
+size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
+  const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
+  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + (lds_keys ? nk * 4 : 0) +
+         (lds_codes ? (size_t)R.nprogs * 256 : 0);
+}
+bool lds_codes_fit(const HttpRawDev& R) { return (size_t)R.nprogs * 256 <= 32 * 1024; }
+
 }  // namespace
 
+size_t http_raw_grid(size_t n, int cus) { return grid_for(n, cus, 4); }
+
+bool http_raw_lds_keys(const HttpRawDev& R) { return ((size_t)R.nprogs + 2) * kRawKeys * 4 <= 32 * 1024; }
+
 int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
-                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* hist,
-                         void* rinfo, unsigned long long* ovf_bytes, void* stream, int cus) {
+                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
+                         void* rinfo, uint32_t* spans, unsigned long long* ovf_bytes, void* stream, int cus) {
   if (!n) return 0;
-  const size_t nb = ((size_t)R.nprogs + 2) * kRawKeys;
-  const size_t spans = (size_t)kRawMaxFields * kRawThreads * 4;
-  const bool lds_hist = spans + nb * 4 <= 64 * 1024;
-  const size_t lds = spans + (lds_hist ? nb * 4 : 0);
-  hipLaunchKernelGGL(raw_scan_kernel, dim3(grid_for(n, cus, 8)), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw,
-                     off, n, policy, ingress, port, hist, (uint2*)rinfo, ovf_bytes, (uint32_t)lds_hist);
+  const bool lk = http_raw_lds_keys(R);
+  const size_t lds = raw_lds(R, lk, false);
+  (void)hipFuncSetAttribute((const void*)raw_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(raw_scan_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
+                     (hipStream_t)stream, R, raw, off, n, policy, ingress, port, counts, (uint2*)rinfo, spans,
+                     ovf_bytes, (uint32_t)lk);
+  return (int)hipGetLastError();
+}
+
+int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk, uint32_t* bbase, uint32_t* hist,
+                           void* stream) {
+  if (!nkeys) return 0;
+  hipLaunchKernelGGL(raw_prefix_kernel, dim3(nkeys), dim3(256), 0, (hipStream_t)stream, bcount, nblk, bbase, hist);
   return (int)hipGetLastError();
 }
 
@@ -442,12 +598,15 @@ int launch_http_raw_tiles(const HttpRawGroup* groups, uint32_t ngroups, uint32_t
 
 int launch_http_raw_emit(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint8_t* ingress, const uint32_t* remote, const void* rinfo, uint32_t* cursor,
-                         HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
-                         unsigned long long* arena_cursor, void* stream, int cus) {
+                         const uint32_t* bbase, HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
+                         unsigned long long* arena_cursor, const uint32_t* spans, void* stream, int cus) {
   if (!n) return 0;
-  const size_t lds = (size_t)kRawMaxFields * kRawThreads * 4;
-  hipLaunchKernelGGL(raw_emit_kernel, dim3(grid_for(n, cus, 8)), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw,
-                     off, n, ingress, remote, (const uint2*)rinfo, cursor, ttab, tiles, order, arena, arena_cursor);
+  const bool lk = http_raw_lds_keys(R), lc = lds_codes_fit(R);
+  const size_t lds = raw_lds(R, lk, lc);
+  (void)hipFuncSetAttribute((const void*)raw_emit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(raw_emit_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
+                     (hipStream_t)stream, R, raw, off, n, ingress, remote, (const uint2*)rinfo, cursor, bbase,
+                     (uint32_t)lk, ttab, tiles, order, arena, arena_cursor, spans, (uint32_t)lc);
   return (int)hipGetLastError();
 }
 
