@@ -404,6 +404,24 @@ def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False, layou
     return d, pos * 64, tile_map, total - 64
 
 
+def pmc_traffic(requests_per_launch: int):
+    """HBM bytes per launch of the verdict kernel from the newest committed
+    PMC summary (profiles/r*_http_pmc.json, written by tools/pmc_summary.py
+    from separate rocprofv3 --pmc passes of the same workload: FETCH_SIZE ×2
+    gfx950 correction + WRITE_SIZE), scaled to this launch's request count.
+    rocprofv3 cannot run inside the timed process, hence a committed file."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_http_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        s = json.load(f)
+    per_item = s.get("hbm_bytes_per_item")
+    if not per_item:
+        return None, None
+    return per_item * requests_per_launch, os.path.relpath(files[-1], ROOT)
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
