@@ -195,8 +195,10 @@ def test_config5_http10k_125m_batch(gpu):
     tiles_out = d_out.view(-1, 64)
     slot_exp_t = torch.from_numpy(slot_exp.reshape(-1, 64)).to(dev)
     for first, nt, at in groups:
-        got = tiles_out[at:at + nt * reps].view(reps, nt, 64)
-        assert bool((got == slot_exp_t[first:first + nt]).all()), (first, nt)
+        # tile-major replication (bench.replicate_batch): b's tile first + j
+        # is tiles at + j * reps ... at + j * reps + reps - 1
+        got = tiles_out[at:at + nt * reps].view(nt, reps, 64)
+        assert bool((got == slot_exp_t[first:first + nt].unsqueeze(1)).all()), (first, nt)
     c = gpu.read_counters(0)
     assert int(c[0::2].sum() + c[1::2].sum()) == reps * D
     assert int(c[0::2].sum()) == reps * int(exp.sum())
