@@ -69,6 +69,10 @@ VARIANTS.update({
     "l4_nopipe4": _l4t(4) + [_NOPIPE],
     "l4_nopipe8": _l4t(8) + [_NOPIPE],
     "l4_noctr": [("kernels.hip", "      if (which) l4_count(t, lcnt, val & 0xFFFF, w[u][2]);", "")],
+    # prefilter: addresses per lane (v4, v6)
+    "lpm_4_2": [("kernels.hip", "constexpr uint32_t kLpmV4 = 4, kLpmV6 = 2;", "constexpr uint32_t kLpmV4 = 4, kLpmV6 = 2;")],
+    "lpm_8_4": [("kernels.hip", "constexpr uint32_t kLpmV4 = 4, kLpmV6 = 2;", "constexpr uint32_t kLpmV4 = 8, kLpmV6 = 4;")],
+    "lpm_4_4": [("kernels.hip", "constexpr uint32_t kLpmV4 = 4, kLpmV6 = 2;", "constexpr uint32_t kLpmV4 = 4, kLpmV6 = 4;")],
     # HTTP: dynamic (ticket) vs static chunk dealing
     "h_dyn": [],
     "h_static": [("constexpr bool kDynamicDeal = true;", "constexpr bool kDynamicDeal = false;")],
@@ -85,7 +89,7 @@ def build_variant(name, subs):
         src = files.get(fn) or (B.CSRC / fn).read_text()
         assert a in src, (name, fn, a)
         files[fn] = src.replace(a, b)
-    if not any(fn.endswith(".hip") for fn in files) and not name.startswith("l4_"):
+    if not any(fn.endswith(".hip") for fn in files) and not name.startswith(("l4_", "lpm_")):
         files["kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip"] = \
             (B.CSRC / ("kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip")).read_text()
     objs = []
