@@ -52,6 +52,16 @@ __device__ __forceinline__ bool tchar(uint32_t c) {
 }
 __device__ __forceinline__ uint32_t lower(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
+// Four bytes that are all "plain": > 0x20 and not 0x7F (no control byte, no
+// SP / HTAB / CR): target and field-value bytes that need no decision.
+// hasless(q, 0x21) and haszero(q ^ 0x7F..) are exact presence tests.
+__device__ __forceinline__ bool all_plain(uint32_t q) {
+  const uint32_t lt = (q - 0x21212121u) & ~q & 0x80808080u;
+  const uint32_t y = q ^ 0x7F7F7F7Fu;
+  const uint32_t del = (y - 0x01010101u) & ~y & 0x80808080u;
+  return (lt | del) == 0;
+}
+
 // A lane's head: from its wave's LDS stage when the head lies inside it
 // (the common case), else through 16-byte aligned global loads with one
 // block kept in registers (blocks reaching outside the head are assembled
@@ -64,6 +74,21 @@ struct HeadReader {
   uint4 w;
   __device__ __forceinline__ HeadReader(const uint8_t* p_, uint32_t n_, const uint8_t* lp_)
       : p(p_), n(n_), lp(lp_), cur(~0ull), w{0, 0, 0, 0} {}
+  // bytes k..k+3 (little-endian; bytes past the head are unspecified): from
+  // LDS two aligned dword reads and a byte align, so a walk pays one LDS
+  // round trip per 4 bytes instead of one per byte
+  __device__ __forceinline__ uint32_t quad(uint32_t k) {
+    if (lp) {
+      const uintptr_t a = (uintptr_t)(lp + k);
+      const uint32_t* w4 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+      return __builtin_amdgcn_alignbyte(w4[1], w4[0], (uint32_t)(a & 3));
+    }
+    uint32_t q = 0;  // global: never past the head (it may end the buffer)
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+      if (k + j < n) q |= at(k + j) << (8 * j);
+    return q;
+  }
   __device__ __forceinline__ uint32_t at(uint32_t k) {
     if (lp) return lp[k];
     const uint64_t a = (uint64_t)(uintptr_t)(p + k);
@@ -169,6 +194,10 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, HeadReader& hr, 
   if (k == 0 || k >= n || hr.at(k) != ' ') return false;
   const uint32_t mlen = k++, t0 = k;
   while (k < n) {  // request-target
+    if (k + 4 <= n && all_plain(hr.quad(k))) {
+      k += 4;
+      continue;
+    }
     const uint32_t c = hr.at(k);
     if (c <= 0x20 || c == 0x7F) break;
     ++k;
@@ -191,16 +220,28 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, HeadReader& hr, 
     if (k + 1 >= n) return false;  // no CRLF left: incomplete head
     if (hr.at(k) == '\r' && hr.at(k + 1) == '\n') break;  // empty line: end of head
     uint32_t c = k, h = kRawFnvInit;
-    while (c < n) {
-      const uint32_t x = hr.at(c);
-      if (!tchar(x)) break;
-      h = raw_fnv(h, (uint8_t)lower(x));
-      ++c;
+    for (bool more = true; more && c < n;) {  // a quad at a time
+      const uint32_t q = hr.quad(c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t x = (q >> (8 * j)) & 0xFFu;
+        if (more && (c >= n || !tchar(x))) more = false;
+        if (more) {
+          h = raw_fnv(h, (uint8_t)lower(x));
+          ++c;
+        }
+      }
     }
     if (c == k || c >= n || hr.at(c) != ':') return false;
     const uint32_t nl = c - k;
     uint32_t v = c + 1, first = kAbsentSpan, lend = v;
     while (true) {  // field-value up to CRLF: IS_HEADER_CHAR, OWS trimmed
+      if (v + 4 <= n && all_plain(hr.quad(v))) {
+        if (first == kAbsentSpan) first = v;
+        v += 4;
+        lend = v;
+        continue;
+      }
       if (v >= n) return false;
       const uint32_t x = hr.at(v);
       if (x == '\r') {
@@ -452,7 +493,12 @@ __device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr,
       o.put(code[1]);
     } else {
       const uint32_t a = s >> 16, L = s & 0xFFFFu;
-      for (uint32_t k = 0; k < L; ++k) o.put(code[hr.at(a + k)]);
+      for (uint32_t k = 0; k < L; k += 4) {  // a quad at a time
+        const uint32_t q = hr.quad(a + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (k + j < L) o.put(code[(q >> (8 * j)) & 0xFFu]);
+      }
     }
     o.put(code[0]);
   }
@@ -558,7 +604,7 @@ unsigned grid_for(size_t n, int cus, unsigned per_cu) {
 size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
   return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + (lds_keys ? nk * 4 : 0) +
-         (lds_codes ? (size_t)R.nprogs * 256 : 0);
+         (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
 }
 bool lds_codes_fit(const HttpRawDev& R) { return (size_t)R.nprogs * 256 <= 32 * 1024; }
 
