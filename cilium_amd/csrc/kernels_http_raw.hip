@@ -127,7 +127,10 @@ struct HeadReader {
 // address the stage starts at (16-byte aligned) and, in *len, the bytes it
 // holds.  Bytes outside the heads' range are loaded byte-wise, only those
 // inside it.
-constexpr uint32_t kStage = 8192;
+// 6 KiB: 64 heads of ~70 B fit with room to spare (heads past the stage are
+// read from HBM), and four waves' stages leave room for 3+ workgroups per CU
+// (8 KiB: 1.69, 6 KiB: 2.01, 4 KiB: 1.12 G requests/s on config 5)
+constexpr uint32_t kStage = 6144;
 __device__ __forceinline__ uint64_t stage_heads(const uint8_t* __restrict__ raw, uint64_t lo, uint64_t hi,
                                                 uint8_t* stage, uint32_t lane, uint32_t* len) {
   const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
@@ -467,14 +470,25 @@ struct Out16 {
   uint4* dst;
   uint32_t stride;
   __device__ __forceinline__ Out16(uint4* d, uint32_t s) : w0(0), w1(0), w2(0), w3(0), pos(0), stored(0), dst(d), stride(s) {}
-  __device__ __forceinline__ void put(uint32_t b) {
-    const uint32_t sh = (pos & 3) * 8, q = pos >> 2;
-    w0 |= q == 0 ? b << sh : 0u;
-    w1 |= q == 1 ? b << sh : 0u;
-    w2 |= q == 2 ? b << sh : 0u;
-    w3 |= q == 3 ? b << sh : 0u;
-    if (++pos == 16) flush();
+  // nb (1..4) bytes, little-endian in v (its bytes past nb zero), at byte
+  // pos: one 64-bit shift spreads them over dword pos / 4 and the next; the
+  // part past the 16 bytes starts the next chunk
+  __device__ __forceinline__ void put4(uint32_t v, uint32_t nb) {
+    const uint64_t t = (uint64_t)v << ((pos & 3) * 8);
+    const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32), q = pos >> 2;
+    w0 |= lo & (0u - (q == 0));
+    w1 |= (lo & (0u - (q == 1))) | (hi & (0u - (q == 0)));
+    w2 |= (lo & (0u - (q == 2))) | (hi & (0u - (q == 1)));
+    w3 |= (lo & (0u - (q == 3))) | (hi & (0u - (q == 2)));
+    pos += nb;
+    if (pos >= 16) {
+      const uint32_t rest = pos - 16;
+      flush();
+      w0 = hi & (0u - (q == 3));
+      pos = rest;
+    }
   }
+  __device__ __forceinline__ void put(uint32_t b) { put4(b, 1); }
   __device__ __forceinline__ void flush() {
     *dst = make_uint4(w0, w1, w2, w3);
     dst += stride;
@@ -493,11 +507,11 @@ __device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr,
       o.put(code[1]);
     } else {
       const uint32_t a = s >> 16, L = s & 0xFFFFu;
-      for (uint32_t k = 0; k < L; k += 4) {  // a quad at a time
-        const uint32_t q = hr.quad(a + k);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (k + j < L) o.put(code[(q >> (8 * j)) & 0xFFu]);
+      for (uint32_t k = 0; k < L; k += 4) {  // a quad at a time: four code bytes, one insert
+        const uint32_t q = hr.quad(a + k), nb = min(L - k, 4u);
+        const uint32_t c = (uint32_t)code[q & 0xFFu] | (uint32_t)code[(q >> 8) & 0xFFu] << 8 |
+                           (uint32_t)code[(q >> 16) & 0xFFu] << 16 | (uint32_t)code[q >> 24] << 24;
+        o.put4(nb == 4 ? c : c & ((1u << (8 * nb)) - 1), nb);
       }
     }
     o.put(code[0]);
@@ -606,7 +620,9 @@ size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + (lds_keys ? nk * 4 : 0) +
          (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
 }
-bool lds_codes_fit(const HttpRawDev& R) { return (size_t)R.nprogs * 256 <= 32 * 1024; }
+// code maps in LDS only while small: a larger table costs workgroups per CU
+// (occupancy) more than its global (L1-cached) lookups cost
+bool lds_codes_fit(const HttpRawDev& R) { return (size_t)R.nprogs * 256 <= 4 * 1024; }
 
 }  // namespace
 

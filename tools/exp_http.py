@@ -79,6 +79,33 @@ VARIANTS.update({
 })
 
 
+# Raw HTTP path (kernels_http_raw.hip): LDS stage per wave, code maps in LDS
+# (occupancy: the stage and the code maps set how many workgroups fit a CU).
+def _rs(stage):
+    return [("kernels_http_raw.hip", "constexpr uint32_t kStage = 6144;", f"constexpr uint32_t kStage = {stage};")]
+
+
+_NOCODES = ("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }", "return false; }")
+VARIANTS.update({
+    "raw_base": [],
+    "raw_s6k": _rs(6144),
+    "raw_s4k": _rs(4096),
+    "raw_nocodes": [_NOCODES],
+    "raw_s6k_nocodes": _rs(6144) + [_NOCODES],
+    "raw_s5k": _rs(5120),
+    "raw_s5632": _rs(5632),
+    "raw_s7k": _rs(7168),
+    "raw_s5k_nocodes": _rs(5120) + [_NOCODES],
+    "raw_s5632_nocodes": _rs(5632) + [_NOCODES],
+    # measuring device (verdicts meaningless, memory-safe: separators and
+    # zero padding only, all valid codes): emit without the strings
+    "raw_nostr": [("kernels_http_raw.hip", "      for (uint32_t k = 0; k < L; k += 4) {  // a quad",
+                   "      for (uint32_t k = 0; k < 0; k += 4) {  // a quad")],
+    "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
+                      "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
+})
+
+
 def build_variant(name, subs):
     """subs: (old, new) pairs on kernels_http.hip, or (file, old, new) on any
     csrc/ source; the changed sources are compiled into a private library."""
