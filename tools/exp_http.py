@@ -76,6 +76,9 @@ VARIANTS.update({
     # HTTP: dynamic (ticket) vs static chunk dealing
     "h_dyn": [],
     "h_static": [("constexpr bool kDynamicDeal = true;", "constexpr bool kDynamicDeal = false;")],
+    # occupancy vs spills: 8 waves/SIMD caps VGPRs at 64 (40 B/lane of scratch)
+    "h_w7": [("amdgpu_waves_per_eu(8, 8)", "amdgpu_waves_per_eu(7, 8)")],
+    "h_w6": [("amdgpu_waves_per_eu(8, 8)", "amdgpu_waves_per_eu(6, 8)")],
 })
 
 
