@@ -1,17 +1,19 @@
 #!/bin/bash
-# PMC passes over one of the L4 / prefilter / Kafka kernels (each counter
-# group in its own rocprofv3 run; no tracing domains combined with --pmc).
-#   bash tools/gpu_pmc_paths.sh <tag> <path: l4|lpm|kafka>
+# PMC passes over bench_paths kernels (each counter group in its own
+# rocprofv3 run; no tracing domains combined with --pmc).
+#   bash tools/gpu_pmc_paths.sh <tag> <path> [<path> ...]
 cd "$GRAFT_REPO_ROOT" || exit 1
-tag=${1:-pmcp}; path=${2:-kafka}
-mkdir -p gpurun_out/$tag
+tag=${1:-pmcp}; shift
 export TMPDIR=/tmp
-cmd="python3 tools/bench_paths.py --paths $path --steps 2 --cpu-seconds 0"
-i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
-           "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum"; do
-  i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/$tag/p$i -o run -- $cmd > gpurun_out/$tag/p$i.log 2>&1 || exit $?
+for path in "$@"; do
+  out=gpurun_out/$tag/$path
+  mkdir -p $out
+  cmd="python3 tools/bench_paths.py --paths $path --steps 2 --cpu-seconds 0"
+  i=0
+  for grp in "FETCH_SIZE" "WRITE_SIZE" \
+             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" \
+             "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum"; do
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $out/p$i -o run -- $cmd > $out/p$i.log 2>&1 || exit $?
+  done
 done

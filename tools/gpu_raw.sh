@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU box: bench lines for the raw HTTP/1 path, L4 and L4+ipcache, then a
-# kernel trace of the raw path.
+# GPU box: raw-path + LPM tests, raw and lpm bench lines, raw kernel trace.
 cd "$GRAFT_REPO_ROOT" || exit 1
-out=gpurun_out/${1:-raw}
+out=gpurun_out/${1:-raw3}
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 600 python3 tools/bench_paths.py --paths httpraw,l4,l4ipc > $out/paths.jsonl 2> $out/paths.err || exit $?
+timeout -k 10 400 python3 -u -m pytest tests/test_http_raw_gpu.py tests/test_proxylib_cassandra.py tests/test_npds_pb.py -m gpu -x -v --timeout 200 --timeout-method thread > $out/pytest.log 2>&1 || exit $?
+timeout -k 10 600 python3 tools/bench_paths.py --paths httpraw > $out/paths.jsonl 2> $out/paths.err || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 tools/bench_paths.py --paths httpraw --steps 3 --cpu-seconds 0 > $out/prof.log 2>&1 || exit $?
