@@ -178,3 +178,40 @@ def test_head_size_limit_host_parser():
     _, _, good = Classifier.parse_http_heads(*_blob([ok, big]))
     assert good.tolist() == [1, 0]
     assert parse_head(ok) is not None and parse_head(big) is None
+
+
+@pytest.mark.gpu
+def test_gpu_raw_config5_full_size():
+    """BASELINE config 5's per-GPU batch as raw heads: 65,536 distinct
+    requests of the 10K-rule set (with client-style variations) laid out
+    1,900 times back to back — 124.5M heads, 8.7 GB resident — through the
+    device entry point in one call; every copy's verdicts equal the host
+    path's verdicts for the distinct requests (size-independent property:
+    verdicts are per request, whatever the batch around it)."""
+    import torch
+    cl = Classifier(device=0)
+    pols, info = synth.http10k_rules()
+    cl.update_http_policy(pols)
+    D, reps = 65_536, 1_900
+    rq = synth.http10k_requests(D, info, seed=synth.SEED ^ 0x4A1)
+    raws = _vary(_raw_requests(rq), np.random.default_rng(4), frac=0.02)  # long strings stay within the 256 MiB arena
+    blob, off = _blob(raws)
+    args = (rq["policy"], rq["ingress"], rq["port"], rq["remote"])
+    want = _host_path(cl, *args, raws)
+    dev = torch.device("cuda:0")
+    tot = int(off[-1])
+    d_raw = torch.from_numpy(blob[:tot]).to(dev).repeat(reps)
+    base = torch.arange(reps, dtype=torch.int64, device=dev).unsqueeze(1) * tot
+    d_off = torch.cat([(torch.from_numpy(off[:-1].astype(np.int64)).to(dev).unsqueeze(0) + base).reshape(-1),
+                       torch.tensor([tot * reps], dtype=torch.int64, device=dev)])
+    rep = lambda a, dt: torch.from_numpy(np.asarray(a).astype(dt)).to(dev).repeat(reps)
+    d_pol, d_ing = rep(args[0], np.int32), rep(args[1], np.uint8)
+    d_port, d_rem = rep(args[2], np.int16), rep(args[3], np.int32)
+    n = D * reps
+    d_out = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    cl.http_verdicts_raw_dev(d_raw, d_off, n, d_pol, d_ing, d_port, d_rem, d_out)
+    got = d_out.view(reps, D)
+    assert bool((got == torch.from_numpy(want).to(dev).unsqueeze(0)).all())
+    assert 0.1 < float(want.mean()) < 0.9
+    del d_raw, d_off, d_out
+    cl.close()
