@@ -110,7 +110,17 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   const uint32_t* hc = (const uint32_t*)hh;
   unsigned long long ovf_bytes;
   memcpy(&ovf_bytes, hh + hist_bytes, 8);
-  if (ovf_bytes / 16 >= (1ull << 24)) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
+  if (ovf_bytes / 16 >= (1ull << 24)) {
+    // the meta word holds arena offsets / 16 in 24 bits: a batch whose long
+    // strings need more than 256 MiB of arena runs as two halves (one head
+    // is at most kRawMaxHead bytes, so halving always ends)
+    if (n < 2) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
+    const size_t h = n / 2;
+    http_verdicts_raw_on(s, sl, cus, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
+    http_verdicts_raw_on(s, sl, cus, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
+                         d_out + h, stream);
+    return;
+  }
   // ---- layout: groups in program order (then allow, deny), 64-slot tiles,
   // chunks of <= kChunkTiles tiles, a cursor per (group, bucket)
   std::vector<HttpRawGroup> groups;

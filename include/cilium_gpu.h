@@ -441,7 +441,8 @@ int cg_http_parse_heads(const uint8_t* raw, const uint64_t* raw_off, size_t n, u
  * d_raw[d_raw_off[r] .. d_raw_off[r+1]) with d_policy/d_ingress/d_port/
  * d_remote as in cg_http_pack; d_out[r] = 1 allow, 0 deny, request order.
  * Heads over 60 KiB are rejected (Envoy's default max_request_headers_kb).
- * Runs on `stream` (NULL: the handle's) and synchronizes it (its workspace is
+ * A batch whose strings past the 128-byte slot need more than the 256 MiB
+ * overflow arena is evaluated in halves.  Runs on `stream` (NULL: the handle's) and synchronizes it (its workspace is
  * the handle's).  CG_UNSUPPORTED when the snapshot walks more than 32 header
  * fields or is a proxylib snapshot. */
 int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,

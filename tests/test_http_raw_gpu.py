@@ -215,3 +215,34 @@ def test_gpu_raw_config5_full_size():
     assert 0.1 < float(want.mean()) < 0.9
     del d_raw, d_off, d_out
     cl.close()
+
+
+@pytest.mark.gpu
+def test_gpu_raw_arena_split():
+    """A batch whose long strings need more than the 256 MiB overflow arena
+    (1M heads with 300-400-byte paths, ~350 MB of arena) is evaluated in
+    halves: verdicts equal the host path's for every copy."""
+    import torch
+    cl = Classifier(device=0)
+    pols, info = synth.http10k_rules()
+    cl.update_http_policy(pols)
+    D, reps = 16_384, 64
+    rq = synth.http10k_requests(D, info, seed=24)
+    rng = np.random.default_rng(5)
+    raws = [r.replace(b" HTTP/", b"/" + b"q" * int(rng.integers(300, 400)) + b" HTTP/", 1) for r in _raw_requests(rq)]
+    blob, off = _blob(raws)
+    args = (rq["policy"], rq["ingress"], rq["port"], rq["remote"])
+    want = _host_path(cl, *args, raws)
+    dev = torch.device("cuda:0")
+    tot = int(off[-1])
+    d_raw = torch.from_numpy(blob[:tot]).to(dev).repeat(reps)
+    base = torch.arange(reps, dtype=torch.int64, device=dev).unsqueeze(1) * tot
+    d_off = torch.cat([(torch.from_numpy(off[:-1].astype(np.int64)).to(dev).unsqueeze(0) + base).reshape(-1),
+                       torch.tensor([tot * reps], dtype=torch.int64, device=dev)])
+    rep = lambda a, dt: torch.from_numpy(np.asarray(a).astype(dt)).to(dev).repeat(reps)
+    n = D * reps
+    d_out = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    cl.http_verdicts_raw_dev(d_raw, d_off, n, rep(args[0], np.int32), rep(args[1], np.uint8), rep(args[2], np.int16),
+                             rep(args[3], np.int32), d_out)
+    assert bool((d_out.view(reps, D) == torch.from_numpy(want).to(dev).unsqueeze(0)).all())
+    cl.close()
