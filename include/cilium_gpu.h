@@ -412,7 +412,9 @@ size_t cg_http_batch_slots(uint64_t h, size_t n);
  * names compare case-insensitively and only the first value of a name is
  * seen (Envoy HeaderMap::get).  Records whose slot string exceeds 128 bytes
  * spill into the overflow arena: pass arena/arena_cap (may be NULL/0 to
- * query), *arena_used gets the bytes needed.  *nslots gets the batch's slot
+ * query), *arena_used gets the bytes needed; one batch's arena is at most
+ * 256 MiB (CG_INVALID_ARGUMENT beyond: pack such a request set as several
+ * batches; cg_http_verdicts_raw_* splits by itself).  *nslots gets the batch's slot
  * count; order must hold cg_http_batch_slots(h, n) entries. */
 int cg_http_pack(uint64_t h, size_t n, const uint32_t* policy, const uint8_t* ingress,
                  const uint16_t* port, const uint32_t* remote, const uint8_t* hdr_blob,
