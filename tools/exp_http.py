@@ -79,6 +79,11 @@ VARIANTS.update({
     # occupancy vs spills: 8 waves/SIMD caps VGPRs at 64 (40 B/lane of scratch)
     "h_w7": [("amdgpu_waves_per_eu(8, 8)", "amdgpu_waves_per_eu(7, 8)")],
     "h_w6": [("amdgpu_waves_per_eu(8, 8)", "amdgpu_waves_per_eu(6, 8)")],
+    # next-tile prefetch depth and the rolling unit window
+    "h_pre2": [("constexpr int kPre = 1;", "constexpr int kPre = 2;")],
+    "h_win2": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 2 ? (N > 0 ? N : 1) : 2;")],
+    "h_win3": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 3 ? (N > 0 ? N : 1) : 3;")],
+    "h_win6": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 6 ? (N > 0 ? N : 1) : 6;")],
 })
 
 
