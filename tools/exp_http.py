@@ -83,6 +83,14 @@ VARIANTS.update({
     "h_pre2": [("constexpr int kPre = 1;", "constexpr int kPre = 2;")],
     "h_win2": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 2 ? (N > 0 ? N : 1) : 2;")],
     "h_win3": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 3 ? (N > 0 ? N : 1) : 3;")],
+    # nontemporal meta / prefetched-unit loads off (the in-walk unit loads stay nontemporal)
+    "h_nt_units_only": [("#define NT_META(p) ld_nt(p)\n#define NT_PRE(p) ld_nt(p)", "#define NT_META(p) (*(p))\n#define NT_PRE(p) (*(p))")],
+    "h_old": [("#define NT_META(p) ld_nt(p)\n#define NT_PRE(p) ld_nt(p)", "#define NT_META(p) (*(p))\n#define NT_PRE(p) (*(p))"),
+              ("unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : ld_nt(tr.units + k * kWave + lane);",
+               "unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : tr.units[k * kWave + lane];"),
+              ("unit[k % kWin] = ld_nt(tr.units + (k + kWin) * kWave + lane);",
+               "unit[k % kWin] = tr.units[(k + kWin) * kWave + lane];")],
+    "h_nt_nometa": [("#define NT_META(p) ld_nt(p)", "#define NT_META(p) (*(p))")],
     "h_win6": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 6 ? (N > 0 ? N : 1) : 6;")],
 })
 
