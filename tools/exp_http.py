@@ -85,6 +85,8 @@ VARIANTS.update({
     "h_win3": [("constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;", "constexpr int kWin = N < 3 ? (N > 0 ? N : 1) : 3;")],
     # nontemporal meta / prefetched-unit loads off (the in-walk unit loads stay nontemporal)
     "h_nt_units_only": [("#define NT_META(p) ld_nt(p)\n#define NT_PRE(p) ld_nt(p)", "#define NT_META(p) (*(p))\n#define NT_PRE(p) (*(p))")],
+    "h_ntout": [("  out[(size_t)t * kWave + lane] = (uint8_t)verdict;\n  n_allow += counted && verdict;",
+                 "  __builtin_nontemporal_store((uint8_t)verdict, out + (size_t)t * kWave + lane);\n  n_allow += counted && verdict;")],
     "h_old": [("#define NT_META(p) ld_nt(p)\n#define NT_PRE(p) ld_nt(p)", "#define NT_META(p) (*(p))\n#define NT_PRE(p) (*(p))"),
               ("unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : ld_nt(tr.units + k * kWave + lane);",
                "unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : tr.units[k * kWave + lane];"),
@@ -115,6 +117,9 @@ VARIANTS.update({
     "raw_s5632_nocodes": _rs(5632) + [_NOCODES],
     # measuring device (verdicts meaningless, memory-safe: separators and
     # zero padding only, all valid codes): emit without the strings
+    "raw_ntstage": [("kernels_http_raw.hip", "      v = *reinterpret_cast<const uint4*>((uintptr_t)a);",
+                     "      { typedef unsigned int v4u __attribute__((ext_vector_type(4))); const v4u x = "
+                     "__builtin_nontemporal_load(reinterpret_cast<const v4u*>((uintptr_t)a)); v = make_uint4(x.x, x.y, x.z, x.w); }")],
     "raw_nostr": [("kernels_http_raw.hip", "      for (uint32_t k = 0; k < L; k += 4) {  // a quad",
                    "      for (uint32_t k = 0; k < 0; k += 4) {  // a quad")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
