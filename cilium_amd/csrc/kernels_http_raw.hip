@@ -6,12 +6,12 @@
 // :authority, rejected heads) and http_pack.cc (program lookup, the walked
 // string v_1 SEP .. v_F SEP / REST, class codes, grouping by program and
 // string units) run one lane per request:
-//   raw_scan_kernel   parse; program, string length, bucket key (program
+//   raw_scan_kernel   parse (value spans kept); program, string length, bucket key (program
 //                     group × string units) and the bucket histogram
 //   (host)            bucket counts → groups, chunks, bucket cursors
 //   raw_tiles_kernel  tile table (fixed 17-granule stride per tile, units =
 //                     the largest walked string the tile holds), padding slots
-//   raw_emit_kernel   parse again; a slot from the bucket cursor; meta, the
+//   raw_emit_kernel   the scan's value spans; a slot from the bucket cursor; meta, the
 //                     class-coded string units (zero padded) or an overflow
 //                     arena entry; the tile's tail bytes
 //   http_kernel       the verdicts (kernels_http.hip)
