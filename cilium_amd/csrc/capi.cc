@@ -76,6 +76,12 @@ void* stream_of(Engine& e, void* s) { return s ? s : e.stream; }
 
 void check_launch(int err, const char* what) { hip_check(err, what); }
 
+// A queued launch on `stream` reads this table set: record it on the set's
+// retirement fence (engine.h LaunchFence).
+void fence(const std::shared_ptr<DevTables>& t, void* stream) {
+  if (t) t->fence.record(stream);
+}
+
 CidrKey make_cidr(const cg_cidr& c) {
   CidrKey k;
   if (c.family != 4 && c.family != 6) fail(CG_INVALID_ADDRESS, "cidr family must be 4 or 6");
@@ -258,7 +264,10 @@ int cg_policymap_lookup(uint64_t h, uint32_t map_id, const cg_policy_key* key, c
       memset(entry, 0, sizeof(*entry));
       entry->proxy_port = it->second.proxy_port_be;
       // counters include every verdict call queued on this device so far
-      if (e->has_gpu()) hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      if (e->has_gpu()) {
+        e->set_device();
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      }
       m.read_counters(*e, it->second.id, &entry->packets, &entry->bytes);
     }
   });
@@ -273,6 +282,7 @@ int cg_policymap_dump(uint64_t h, uint32_t map_id, cg_policy_key* keys, cg_polic
     if (n) *n = m.order.size();
     std::vector<uint64_t> ctr;
     if (e->has_gpu() && m.d_counters) {
+      e->set_device();
       hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
       ctr.resize((size_t)m.max_entries * 2);
       hip_check(hipMemcpy(ctr.data(), m.d_counters->get(), ctr.size() * 8, hipMemcpyDeviceToHost), "D2H counters");
@@ -341,6 +351,7 @@ static void l4_dev(Engine& e, uint32_t map_id, uint32_t mode, const cg_l4_tuple*
   const L4View v = l4_view(e, map_id);
   e.set_device();
   check_launch(launch_l4(v.dev, d_t, n, d_out, mode, stream_of(e, s), e.cus), "l4 kernel launch");
+  fence(v.keep, stream_of(e, s));
 }
 
 static void l4_host(Engine& e, uint32_t map_id, uint32_t mode, const cg_l4_tuple* t, size_t n, int32_t* out) {
@@ -382,6 +393,8 @@ static void l4_ipc_dev(Engine& e, uint32_t map_id, uint32_t ipc_id, int family, 
   e.set_device();
   check_launch(launch_l4_ipcache(v.dev, iv.dev, family, d_addr, d_t, n, d_out, CG_L4_EGRESS, stream_of(e, s), e.cus),
                "l4 (ipcache) kernel launch");
+  fence(v.keep, stream_of(e, s));
+  fence(iv.keep, stream_of(e, s));
 }
 
 static void l4_ipc_host(Engine& e, uint32_t map_id, uint32_t ipc_id, int family, const void* addr,
@@ -570,6 +583,7 @@ int cg_prefilter_verdicts_dev(uint64_t h, uint32_t pf_id, const uint32_t* d_v4, 
     e->set_device();
     check_launch(launch_lpm(v.dev, v.v4f, v.v6f, d_v4, n4, d_out4, d_v6, n6, d_out6, stream_of(*e, stream), e->cus),
                  "lpm kernel launch");
+    fence(v.keep, stream_of(*e, stream));
   });
 }
 
@@ -697,6 +711,7 @@ int cg_ipcache_resolve_dev(uint64_t h, uint32_t ipc_id, const uint32_t* d_v4, si
     check_launch(launch_ipcache(v.dev, d_v4, n4, (IpcVal*)d_out4, d_v6, n6, (IpcVal*)d_out6, stream_of(*e, stream),
                                 e->cus),
                  "ipcache kernel launch");
+    fence(v.keep, stream_of(*e, stream));
   });
 }
 
@@ -766,7 +781,7 @@ int cg_http_policy_update_npds(uint64_t h, const uint8_t* resp, size_t len) {
   std::string json;
   const int rc = guarded([&] {
     if (!resp && len) fail(CG_INVALID_ARGUMENT, "NULL DiscoveryResponse");
-    json = npds_pb_to_json(resp, len);
+    json = npds_pb_to_json(resp, len, true);  // Envoy: proto3 strings must be UTF-8
   });
   if (rc != CG_OK) return rc;
   return cg_http_policy_update(h, json.data(), json.size());
@@ -869,6 +884,7 @@ int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const u
     e->set_device();
     check_launch(launch_http(s->dev, d_batch, nslots, d_arena, d_out, stream_of(*e, stream), e->cus),
                  "http kernel launch");
+    s->fence.record(stream_of(*e, stream));
   });
 }
 
@@ -979,6 +995,7 @@ int cg_kafka_verdicts_dev(uint64_t h, const cg_kafka_request* d_reqs, size_t n, 
     e->set_device();
     check_launch(launch_kafka(s->dev, d_reqs, n, d_arena, d_out, stream_of(*e, stream), e->cus),
                  "kafka kernel launch");
+    s->fence.record(stream_of(*e, stream));
   });
 }
 

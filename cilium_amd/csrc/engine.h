@@ -46,15 +46,36 @@ class DevMem {
   size_t n_ = 0;
 };
 
+// Retirement fence of a published table set.  Every launch that reads the
+// set records an event on its stream after the enqueue (one event per
+// stream, re-recorded, so the list stays as short as the set of streams);
+// the fence's destructor waits for those events.  Declared as the LAST
+// member of a table set, it is destroyed first, so the set's buffers are
+// freed only after every queued kernel that reads them has finished — no
+// reliance on hipFree synchronizing the device.
+class LaunchFence {
+ public:
+  LaunchFence() = default;
+  LaunchFence(const LaunchFence&) = delete;
+  LaunchFence& operator=(const LaunchFence&) = delete;
+  ~LaunchFence();
+  void record(void* stream);  // after a launch on `stream` that reads the set
+
+ private:
+  std::mutex mu_;
+  std::vector<std::pair<void*, void*>> ev_;  // (stream, hipEvent_t)
+};
+
 // One published build of a map's device tables.  A rebuild uploads into a
 // fresh set and swaps the shared_ptr under the handle lock; a launch copies
-// the shared_ptr (and the table view) under that lock and holds it past the
-// enqueue.  So neither a rebuild nor a destroy overwrites or frees tables a
-// queued kernel reads: an old set is freed when its last holder lets go, and
-// hipFree waits for the device's queued work before it returns.
+// the shared_ptr (and the table view) under that lock, enqueues, and records
+// the set's fence on its stream.  So neither a rebuild nor a destroy
+// overwrites or frees tables a queued kernel reads: an old set is freed when
+// its last holder lets go, after the kernels recorded on its fence finish.
 struct DevTables {
   std::vector<DevMem> bufs;
   std::shared_ptr<DevMem> counters;  // survives rebuilds (per-entry counters)
+  LaunchFence fence;                 // last member: destroyed (waited) first
   template <class T>
   T* add(const std::vector<T>& v) {
     bufs.emplace_back();

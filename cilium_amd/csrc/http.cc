@@ -62,11 +62,15 @@ constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits) / 4;
 // escaped items, each followed by the pair {0x03, 0x14}, and every item must
 // equal / start with / contain a match of the value (memcached keys,
 // proxylib/memcached/parser.go:54-97; zero items match)
-enum class MKind { Exact, Regex, Present, Search, ListExact, ListPrefix, ListSearch };
+// Prefix / Suffix / Range: Envoy HeaderMatchType::Prefix / Suffix / Range
+// (prefix_match, suffix_match, range_match); `invert` = invert_match.
+enum class MKind { Exact, Regex, Present, Search, ListExact, ListPrefix, ListSearch, Prefix, Suffix, Range };
 struct MatcherSpec {
   std::string name;  // lowercase
   MKind kind;
   std::string value;
+  bool invert = false;
+  int64_t range_start = 0, range_end = 0;  // Range: [start, end)
 };
 struct PnprSpec {
   bool has_remotes = false;
@@ -109,12 +113,29 @@ MatcherSpec parse_matcher(const Json& h) {
   const Json* ls = h.get("list_search");
   const Json* val = h.get("value");
   const Json* inv = h.get("invert_match");
-  if (inv && inv->type == Json::BOOL && inv->b) fail(CG_UNSUPPORTED, "invert_match");
-  for (const char* k : {"range_match", "prefix_match", "suffix_match"})
-    if (h.get(k)) fail(CG_UNSUPPORTED, std::string("header matcher ") + k);
+  const Json* px = h.get("prefix_match");
+  const Json* sx = h.get("suffix_match");
+  const Json* rg = h.get("range_match");
+  m.invert = inv && inv->type == Json::BOOL && inv->b;
   if (ex) {
     m.kind = MKind::Exact;
     m.value = ex->as_str("exact_match");
+  } else if (px) {
+    m.kind = MKind::Prefix;
+    m.value = px->as_str("prefix_match");
+  } else if (sx) {
+    m.kind = MKind::Suffix;
+    m.value = sx->as_str("suffix_match");
+  } else if (rg) {
+    if (rg->type != Json::OBJ) fail(CG_POLICY_REJECTED, "range_match must be an object");
+    m.kind = MKind::Range;
+    auto num = [&](const char* k) -> int64_t {
+      const Json* j = rg->get(k);
+      return j ? j->as_i64(k) : 0;
+    };
+    m.range_start = num("start");
+    m.range_end = num("end");
+    m.value = std::to_string(m.range_start) + "," + std::to_string(m.range_end);
   } else if (rx) {
     m.kind = MKind::Regex;
     m.value = rx->as_str("regex_match");
@@ -247,7 +268,7 @@ struct FieldDfaCache {
     return any_id;
   }
   int single(const MatcherSpec& m) {
-    std::string key = std::string(1, "ERPSLKQ"[(int)m.kind]) + ":" + m.value;
+    std::string key = std::string(1, "ERPSLKQXYZ"[(int)m.kind]) + (m.invert ? "!" : "") + ":" + m.value;
     auto it = by_key.find(key);
     if (it != by_key.end()) return it->second;
     // Envoy values never hold 0x00-0x02 (the codec rejects them); proxylib
@@ -256,14 +277,24 @@ struct FieldDfaCache {
     ByteSet va = raw ? ByteSet::all() : value_alphabet();
     ByteDfa d;
     switch (m.kind) {
-      case MKind::Exact: d = dfa_literal(m.value, va); break;
+      // Envoy HeaderMatchType::Value: an empty value matches any present
+      // header (HeaderUtility::matchHeaders "value_.empty() ||"); proxylib
+      // translations use exact "" for an empty field (proxylib.py cassandra)
+      case MKind::Exact: d = (!raw && m.value.empty()) ? dfa_star(va) : dfa_literal(m.value, va); break;
       case MKind::Regex: d = compile_regex(m.value, va, MatchMode::Full); break;
       case MKind::Present: d = dfa_star(va); break;
       case MKind::Search: d = compile_regex(m.value, va, MatchMode::Search); break;
       case MKind::ListExact: d = dfa_literal(m.value, va); break;
       case MKind::ListPrefix: d = dfa_prefix(m.value, va); break;
       case MKind::ListSearch: d = compile_regex(m.value, va, MatchMode::Search); break;
+      case MKind::Prefix: d = dfa_prefix(m.value, va); break;
+      case MKind::Suffix: d = dfa_suffix(m.value, va); break;
+      case MKind::Range: d = dfa_int_range(m.range_start, m.range_end, va); break;
     }
+    // invert_match: the header must be present (an absent one never
+    // matches: the absent marker is outside the value alphabet) and its
+    // value outside the matcher's language
+    if (m.invert) d = dfa_complement(d, va);
     const bool list = m.kind == MKind::ListExact || m.kind == MKind::ListPrefix || m.kind == MKind::ListSearch;
     if (list && !raw) fail(CG_POLICY_REJECTED, "list matchers are for proxylib policies");
     if (raw) d = dfa_escape_low(d);

@@ -46,6 +46,7 @@ struct HttpSnapshot {
   DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes;
   HttpRawDev raw{};
   bool raw_ok = false;
+  LaunchFence fence;  // last member: queued kernels finish before the buffers go (engine.h)
 
   void upload(Engine& e);
   uint32_t lookup_prog(uint32_t policy, bool ingress, uint32_t port) const;
@@ -55,7 +56,7 @@ std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len);
 
 // NPDS wire form (serialized DiscoveryResponse of cilium.NetworkPolicy) →
 // the NPDS JSON http_compile and the proxylib translation read (npds_pb.cc).
-std::string npds_pb_to_json(const uint8_t* p, size_t n);
+std::string npds_pb_to_json(const uint8_t* p, size_t n, bool strict_utf8);
 
 // The raw-head path (http_raw.cc): device tables (called by upload), and
 // verdicts for n raw HTTP/1 request heads already in device memory, in

@@ -43,6 +43,22 @@ struct Json {
     if (type != NUM || !is_int || neg) fail(CG_POLICY_REJECTED, std::string("expected unsigned integer for ") + what);
     return u;
   }
+  int64_t as_i64(const char* what) const {
+    if (type == STR) {  // protobuf-JSON encodes 64-bit ints as strings
+      const bool minus = !s.empty() && s[0] == '-';
+      uint64_t v = 0;
+      if (s.size() == (size_t)minus) fail(CG_POLICY_REJECTED, std::string("bad integer for ") + what);
+      for (size_t i = minus; i < s.size(); ++i) {
+        if (s[i] < '0' || s[i] > '9' || v > (uint64_t)1 << 63) fail(CG_POLICY_REJECTED, std::string("bad integer for ") + what);
+        v = v * 10 + (s[i] - '0');
+      }
+      if (v > (minus ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1)) fail(CG_POLICY_REJECTED, std::string("int64 out of range for ") + what);
+      return minus ? (int64_t)(0 - v) : (int64_t)v;
+    }
+    if (type != NUM || !is_int || u > (neg ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1))
+      fail(CG_POLICY_REJECTED, std::string("expected int64 for ") + what);
+    return neg ? (int64_t)(0 - u) : (int64_t)u;
+  }
   const std::string& as_str(const char* what) const {
     if (type != STR) fail(CG_POLICY_REJECTED, std::string("expected string for ") + what);
     return s;

@@ -34,6 +34,7 @@ struct KafkaSnapshot {
   DevMem d_rules, d_sums, d_thash, d_chash, d_ghash, d_dflt, d_counters, d_dslots[2], d_dblob[2];
   KafkaDev dev{};
   KafkaDictDev ddict[2] = {};
+  LaunchFence fence;  // last member: queued kernels finish before the buffers go (engine.h)
   void upload(Engine& e);
 };
 

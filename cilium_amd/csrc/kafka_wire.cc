@@ -178,15 +178,31 @@ bool snappy_go(const uint8_t* b, size_t n, std::vector<uint8_t>* out) {
 }
 
 // The host's Inflate for kw_message_set: decompress, then parse the inner set.
+// Intended deviations from readMessageSet (messages.go:363-500), which
+// recurses without a depth limit: at most kMaxDepth nested compressed sets,
+// and at most kBudget decoded bytes alive across the nesting levels of one
+// request (each level keeps its buffer while the inner set parses; Go bounds
+// only each level, at maxParseBufSize).  Past either bound the request is a
+// decode error (the connection closes) where Go would keep parsing.  KAT:
+// tests/test_kafka_wire.py test_nested_compression_bounds.
 struct HostInflate {
+  static constexpr int kMaxDepth = 64;
+  static constexpr size_t kBudget = (size_t)64 << 20;
   int depth = 0;
+  size_t* left = nullptr;  // decoded-byte budget shared by the levels
   uint8_t operator()(uint32_t codec, const uint8_t* p, uint32_t n, int16_t version) {
-    if (depth > 64) return kKwError;  // stack guard (each level needs its own compressed bytes)
+    if (depth >= kMaxDepth) return kKwError;  // stack guard
+    size_t own = kBudget;
+    size_t* budget = left ? left : &own;
     std::vector<uint8_t> dec;
     if (!(codec == 1 ? gunzip_go(p, n, &dec) : snappy_go(p, n, &dec))) return kKwError;
+    if (dec.size() > *budget) return kKwError;
+    *budget -= dec.size();
     KwStream inner{dec.data(), (uint32_t)dec.size(), 0};
-    HostInflate next{depth + 1};
-    return kw_message_set(&inner, (int32_t)dec.size(), version, HostCrc{}, next);
+    HostInflate next{depth + 1, budget};
+    const uint8_t rc = kw_message_set(&inner, (int32_t)dec.size(), version, HostCrc{}, next);
+    *budget += dec.size();  // this level's buffer goes with the return
+    return rc;
   }
 };
 

@@ -35,7 +35,6 @@ constexpr uint32_t kDealRun = 4;  // consecutive chunks per workgroup turn
 // dealing): chunk costs vary with their tiles' string lengths, and a static
 // deal lets the unluckiest workgroup set the kernel's tail.
 constexpr bool kDynamicDeal = true;
-constexpr uint32_t kDealSlots = 256;  // launch ticket slots per device (ring)
 
 __device__ __forceinline__ uint32_t get_byte(const uint4& w, int k) {
   const uint32_t word = (k < 4) ? w.x : (k < 8) ? w.y : (k < 12) ? w.z : w.w;
@@ -684,15 +683,6 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
     }
   }
   flush_counts(T, cur, n_allow, n_deny, lane, s_cnt, s_hits);
-  if (kDynamicDeal && deal && threadIdx.x == 0) {
-    // the last workgroup out resets the slot for the next launch: every
-    // workgroup has drawn its final ticket before it counts itself done
-    __threadfence();
-    if (atomicAdd(&deal[1], 1u) == gridDim.x - 1) {
-      atomicExch(&deal[0], 0u);
-      atomicExch(&deal[1], 0u);
-    }
-  }
 }
 
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
@@ -736,21 +726,22 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
     static std::mutex mu;
     static std::map<std::pair<int, size_t>, int> occ_cache;
     static std::set<int> attr_set;
-    // per device a ring of {ticket, done} pairs, one per launch: each launch's
-    // last workgroup returns its pair to zero, and launches in flight on
-    // other streams hold other pairs (a pair comes back after kDealSlots
-    // launches)
-    static std::map<int, std::pair<uint32_t*, uint32_t>> deal_ring;
+    // one ticket word per (device, stream), zeroed on the launch stream
+    // right before the kernel: launches on one stream run in order, so each
+    // starts from ticket 0 and no two launches in flight share a counter
+    // (launches on different streams hold different words)
+    static std::map<std::pair<int, void*>, uint32_t*> deal_words;
     std::lock_guard<std::mutex> lk(mu);
     if (kDynamicDeal) {
-      auto& r = deal_ring[dev];
-      if (!r.first) {
+      auto& w = deal_words[{dev, stream}];
+      if (!w) {
         void* p = nullptr;
-        if (hipMalloc(&p, kDealSlots * 2 * sizeof(uint32_t)) == hipSuccess &&
-            hipMemset(p, 0, kDealSlots * 2 * sizeof(uint32_t)) == hipSuccess)
-          r.first = static_cast<uint32_t*>(p);
+        if (hipMalloc(&p, 64) != hipSuccess) return (int)hipErrorOutOfMemory;
+        w = static_cast<uint32_t*>(p);
       }
-      if (r.first) deal = r.first + 2 * (r.second++ % kDealSlots);
+      deal = w;
+      const hipError_t rc = hipMemsetAsync(deal, 0, sizeof(uint32_t), (hipStream_t)stream);
+      if (rc != hipSuccess) return (int)rc;
     }
     if (attr_set.insert(dev).second)
       (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

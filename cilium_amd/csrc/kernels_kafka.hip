@@ -218,26 +218,35 @@ __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
     const uint64_t a = off[live ? i : last], b = off[(live ? i : last) + 1];
     // the wave's bytes [off[i0], off[last+1]) (every byte of it belongs to
     // some request when the end is above the start), up to kKwStage of them
-    // from a 16-byte boundary, loaded coalesced into this wave's LDS stage
-    const uint64_t start = off[i0], end = off[last + 1];
-    const uint64_t lo = start & ~15ull;
-    uint64_t hi = end > start ? end : start;
-    hi = (hi + 15) & ~15ull;
+    // from a 16-byte boundary of the POINTER, loaded coalesced into this
+    // wave's LDS stage.  Only bytes inside [start, end) are read: blocks that
+    // straddle either end go byte by byte, so a d_raw buffer that ends
+    // exactly at raw_off[n] (or starts unaligned) is never overrun.
+    const int64_t start = (int64_t)off[i0], end = (int64_t)off[last + 1];
+    const int64_t lo = start - (int64_t)(((uintptr_t)raw + (uint64_t)start) & 15);
+    int64_t hi = end > start ? end : start;
+    hi = lo + ((hi - lo + 15) & ~(int64_t)15);
     if (hi > lo + kKwStage) hi = lo + kKwStage;
     if (kKwStage) {
-      for (uint64_t x = lo + lane * 16; x < hi; x += 64 * 16)
-        *reinterpret_cast<uint4*>(stage + (x - lo)) = *reinterpret_cast<const uint4*>(raw + x);
+      for (int64_t x = lo + lane * 16; x < hi; x += 64 * 16) {
+        if (x >= start && x + 16 <= end) {
+          *reinterpret_cast<uint4*>(stage + (x - lo)) = *reinterpret_cast<const uint4*>(raw + x);
+        } else {
+          for (int k = 0; k < 16; ++k)
+            if (x + k >= start && x + k < end) stage[x - lo + k] = raw[x + k];
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     const uint64_t len64 = b > a ? b - a : 0;
     const uint32_t len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
-    const bool staged = kKwStage && a >= lo && a + len <= hi;
+    const bool staged = kKwStage && (int64_t)a >= lo && (int64_t)(a + len) <= hi;
     // one copy of the decoder over flat addresses (a wave-uniform split into
     // an LDS copy and an HBM copy measured slower: twice the code)
     if (live)
-      decode_one(dt, dc, crc, staged ? stage + (a - lo) : raw + a, len, i, redirect[i], remote[i], recs, arena,
+      decode_one(dt, dc, crc, staged ? stage + ((int64_t)a - lo) : raw + a, len, i, redirect[i], remote[i], recs, arena,
                  arena_cap, ctr, status);
     // every lane has read its bytes before the stage is refilled
     __builtin_amdgcn_wave_barrier();

@@ -16,9 +16,19 @@
 //                                             NetworkPolicy, else the update fails
 //
 // Proto3 wire rules kept: unknown fields are skipped, repeated scalars may be
-// packed or not, a repeated singular field's last occurrence wins (a
-// singular embedded message's occurrences merge), map entries with the same
-// key keep the last value.
+// packed or not, a repeated singular scalar's last occurrence wins, the
+// occurrences of a singular embedded message merge (their bytes are
+// concatenated and parsed once: HeaderMatcher.regex, range_match and the
+// http_rules / kafka_rules / l7_rules oneof members, whose rule lists
+// append), a oneof keeps its last member, map entries with the same key keep
+// the last value.
+//
+// String fields and UTF-8: Envoy's C++ protobuf runtime rejects a proto3
+// string field that is not valid UTF-8 at parse time, so the HTTP update
+// (cg_http_policy_update_npds) refuses the whole response; golang/protobuf
+// of the reference's era (proxylib, cg_proxylib_policy_update_npds) does not
+// check, and those bytes pass through unchanged (the engine's JSON reader
+// copies non-ASCII bytes verbatim).
 #include <cstring>
 #include <map>
 #include <set>
@@ -32,6 +42,33 @@
 namespace cg {
 
 namespace {
+
+thread_local bool t_strict_utf8 = false;
+
+bool utf8_ok(const std::string& s) {
+  size_t i = 0, n = s.size();
+  const auto* b = (const unsigned char*)s.data();
+  while (i < n) {
+    const unsigned c = b[i];
+    size_t k;
+    uint32_t cp;
+    if (c < 0x80) { ++i; continue; }
+    if ((c & 0xE0) == 0xC0) { k = 1; cp = c & 0x1F; }
+    else if ((c & 0xF0) == 0xE0) { k = 2; cp = c & 0x0F; }
+    else if ((c & 0xF8) == 0xF0) { k = 3; cp = c & 0x07; }
+    else return false;
+    if (n - i <= k) return false;  // truncated sequence
+    for (size_t j = 1; j <= k; ++j) {
+      if ((b[i + j] & 0xC0) != 0x80) return false;
+      cp = cp << 6 | (b[i + j] & 0x3F);
+    }
+    if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && (cp < 0x10000 || cp > 0x10FFFF)) ||
+        (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    i += k + 1;
+  }
+  return true;
+}
 
 struct Reader {
   const uint8_t* p;
@@ -97,8 +134,17 @@ uint64_t scalar(Reader& r, uint32_t wt) {
   return r.varint();
 }
 
+// a proto3 `string` field (UTF-8 checked on the Envoy path)
 std::string str(Reader& r, uint32_t wt) {
   if (wt != 2) fail(CG_POLICY_REJECTED, "NPDS protobuf: bad wire type for a string field");
+  std::string s = r.bytes();
+  if (t_strict_utf8 && !utf8_ok(s)) fail(CG_POLICY_REJECTED, "NPDS protobuf: string field is not valid UTF-8");
+  return s;
+}
+
+// an embedded message or `bytes` field (no UTF-8 rule)
+std::string msg_bytes(Reader& r, uint32_t wt) {
+  if (wt != 2) fail(CG_POLICY_REJECTED, "NPDS protobuf: bad wire type for an embedded message");
   return r.bytes();
 }
 
@@ -119,35 +165,53 @@ std::string jstr(const std::string& s) {
   return o + "\"";
 }
 
-// HeaderMatcher → the engine's matcher JSON.  The oneof keeps its last member.
+// HeaderMatcher → the engine's matcher JSON.  The oneof keeps its last member
+// (an embedded member's occurrences merge); range_match is envoy.type.Int64Range
+// {int64 start = 1; int64 end = 2}.
 std::string header_matcher(const std::string& msg) {
   Reader r = sub(msg);
-  std::string name, spec, value;
-  bool has_value = false, regex = false, invert = false;
+  std::string name, spec, value, bool_msg, range_msg;
+  bool has_value = false, invert = false;
+  uint32_t spec_field = 0;
   uint32_t f, wt;
   while (r.next(&f, &wt)) {
     switch (f) {
       case 1: name = str(r, wt); break;
       case 2: value = str(r, wt); has_value = true; break;
-      case 3: {  // google.protobuf.BoolValue {bool value = 1}
-        const std::string q_msg = str(r, wt);  // outlives its reader
-        Reader q = sub(q_msg);
-        uint32_t g, w;
-        while (q.next(&g, &w)) {
-          if (g == 1) regex = scalar(q, w) != 0;
-          else q.skip(w);
-        }
+      case 3: bool_msg += msg_bytes(r, wt); break;  // google.protobuf.BoolValue {bool value = 1}
+      case 4: spec = "\"exact_match\":" + jstr(str(r, wt)); spec_field = 4; break;
+      case 5: spec = "\"regex_match\":" + jstr(str(r, wt)); spec_field = 5; break;
+      case 6:
+        if (spec_field != 6) range_msg.clear();
+        range_msg += msg_bytes(r, wt);
+        spec_field = 6;
         break;
-      }
-      case 4: spec = "\"exact_match\":" + jstr(str(r, wt)); break;
-      case 5: spec = "\"regex_match\":" + jstr(str(r, wt)); break;
-      case 6: str(r, wt); spec = "\"range_match\":{}"; break;
-      case 7: spec = std::string("\"present_match\":") + (scalar(r, wt) ? "true" : "false"); break;
+      case 7: spec = std::string("\"present_match\":") + (scalar(r, wt) ? "true" : "false"); spec_field = 7; break;
       case 8: invert = scalar(r, wt) != 0; break;
-      case 9: spec = "\"prefix_match\":" + jstr(str(r, wt)); break;
-      case 10: spec = "\"suffix_match\":" + jstr(str(r, wt)); break;
+      case 9: spec = "\"prefix_match\":" + jstr(str(r, wt)); spec_field = 9; break;
+      case 10: spec = "\"suffix_match\":" + jstr(str(r, wt)); spec_field = 10; break;
       default: r.skip(wt);
     }
+  }
+  bool regex = false;
+  {
+    Reader q = sub(bool_msg);
+    uint32_t g, w;
+    while (q.next(&g, &w)) {
+      if (g == 1) regex = scalar(q, w) != 0;
+      else q.skip(w);
+    }
+  }
+  if (spec_field == 6) {
+    int64_t start = 0, end = 0;
+    Reader q = sub(range_msg);
+    uint32_t g, w;
+    while (q.next(&g, &w)) {
+      if (g == 1) start = (int64_t)scalar(q, w);
+      else if (g == 2) end = (int64_t)scalar(q, w);
+      else q.skip(w);
+    }
+    spec = "\"range_match\":{\"start\":" + std::to_string(start) + ",\"end\":" + std::to_string(end) + "}";
   }
   std::string o = "{\"name\":" + jstr(name);
   if (!spec.empty()) o += "," + spec;
@@ -188,93 +252,108 @@ std::string join(const std::vector<std::string>& xs) {
   return o;
 }
 
+// HttpNetworkPolicyRules {repeated HttpNetworkPolicyRule http_rules = 1}
+std::string http_rules_json(const std::string& msg) {
+  Reader q = sub(msg);
+  std::vector<std::string> rules;
+  uint32_t g, w;
+  while (q.next(&g, &w)) {
+    if (g != 1) {
+      q.skip(w);
+      continue;
+    }
+    const std::string h_msg = msg_bytes(q, w);  // outlives its reader
+    Reader h = sub(h_msg);
+    std::vector<std::string> hs;
+    uint32_t k, x;
+    while (h.next(&k, &x)) {
+      if (k == 1) hs.push_back(header_matcher(msg_bytes(h, x)));
+      else h.skip(x);
+    }
+    rules.push_back("{\"headers\":[" + join(hs) + "]}");
+  }
+  if (rules.empty()) fail(CG_POLICY_REJECTED, "HttpNetworkPolicyRules: value must contain at least 1 item");
+  return "\"http_rules\":{\"http_rules\":[" + join(rules) + "]}";
+}
+
+// KafkaNetworkPolicyRules {repeated KafkaNetworkPolicyRule kafka_rules = 1}
+std::string kafka_rules_json(const std::string& msg) {
+  Reader q = sub(msg);
+  std::vector<std::string> rules;
+  uint32_t g, w;
+  while (q.next(&g, &w)) {
+    if (g == 1) rules.push_back(kafka_rule(msg_bytes(q, w)));
+    else q.skip(w);
+  }
+  if (rules.empty()) fail(CG_POLICY_REJECTED, "KafkaNetworkPolicyRules: value must contain at least 1 item");
+  return "\"kafka_rules\":{\"kafka_rules\":[" + join(rules) + "]}";
+}
+
+// L7NetworkPolicyRules {repeated L7NetworkPolicyRule l7_rules = 1}, each a
+// map<string, string> rule = 1
+std::string l7_rules_json(const std::string& msg) {
+  Reader q = sub(msg);
+  std::vector<std::string> rules;
+  uint32_t g, w;
+  while (q.next(&g, &w)) {
+    if (g != 1) {
+      q.skip(w);
+      continue;
+    }
+    const std::string m_msg = msg_bytes(q, w);  // outlives its reader
+    Reader m = sub(m_msg);
+    std::map<std::string, std::string> kv;
+    uint32_t k, x;
+    while (m.next(&k, &x)) {
+      if (k != 1) {
+        m.skip(x);
+        continue;
+      }
+      const std::string en_msg = msg_bytes(m, x);  // outlives its reader
+      Reader en = sub(en_msg);
+      std::string key, val;
+      uint32_t a, b;
+      while (en.next(&a, &b)) {
+        if (a == 1) key = str(en, b);
+        else if (a == 2) val = str(en, b);
+        else en.skip(b);
+      }
+      kv[key] = val;
+    }
+    std::vector<std::string> es;
+    for (const auto& [k2, v2] : kv) es.push_back(jstr(k2) + ":" + jstr(v2));
+    rules.push_back("{\"rule\":{" + join(es) + "}}");
+  }
+  if (rules.empty()) fail(CG_POLICY_REJECTED, "L7NetworkPolicyRules: value must contain at least 1 item");
+  return "\"l7_rules\":{\"l7_rules\":[" + join(rules) + "]}";
+}
+
 std::string port_rule(const std::string& msg) {
   Reader r = sub(msg);
   std::vector<uint64_t> remotes;
-  std::string l7_proto, l7;  // l7: the oneof member's JSON ("" = none)
+  std::string l7_proto;
+  // the l7 oneof: its last member; occurrences of the same member merge
+  uint32_t l7_field = 0;
+  std::string l7_msg;
   uint32_t f, wt;
   while (r.next(&f, &wt)) {
     switch (f) {
       case 1: repeated_varints(r, wt, &remotes); break;
       case 2: l7_proto = str(r, wt); break;
-      case 100: {
-        const std::string q_msg = str(r, wt);  // outlives its reader
-        Reader q = sub(q_msg);
-        std::vector<std::string> rules;
-        uint32_t g, w;
-        while (q.next(&g, &w)) {
-          if (g != 1) {
-            q.skip(w);
-            continue;
-          }
-          const std::string h_msg = str(q, w);  // outlives its reader
-        Reader h = sub(h_msg);
-          std::vector<std::string> hs;
-          uint32_t k, x;
-          while (h.next(&k, &x)) {
-            if (k == 1) hs.push_back(header_matcher(str(h, x)));
-            else h.skip(x);
-          }
-          rules.push_back("{\"headers\":[" + join(hs) + "]}");
-        }
-        if (rules.empty()) fail(CG_POLICY_REJECTED, "HttpNetworkPolicyRules: value must contain at least 1 item");
-        l7 = "\"http_rules\":{\"http_rules\":[" + join(rules) + "]}";
+      case 100:
+      case 101:
+      case 102:
+        if (l7_field != f) l7_msg.clear();
+        l7_msg += msg_bytes(r, wt);
+        l7_field = f;
         break;
-      }
-      case 101: {
-        const std::string q_msg = str(r, wt);  // outlives its reader
-        Reader q = sub(q_msg);
-        std::vector<std::string> rules;
-        uint32_t g, w;
-        while (q.next(&g, &w)) {
-          if (g == 1) rules.push_back(kafka_rule(str(q, w)));
-          else q.skip(w);
-        }
-        if (rules.empty()) fail(CG_POLICY_REJECTED, "KafkaNetworkPolicyRules: value must contain at least 1 item");
-        l7 = "\"kafka_rules\":{\"kafka_rules\":[" + join(rules) + "]}";
-        break;
-      }
-      case 102: {
-        const std::string q_msg = str(r, wt);  // outlives its reader
-        Reader q = sub(q_msg);
-        std::vector<std::string> rules;
-        uint32_t g, w;
-        while (q.next(&g, &w)) {
-          if (g != 1) {
-            q.skip(w);
-            continue;
-          }
-          const std::string m_msg = str(q, w);  // outlives its reader
-        Reader m = sub(m_msg);
-          std::map<std::string, std::string> kv;  // map<string, string> rule = 1
-          uint32_t k, x;
-          while (m.next(&k, &x)) {
-            if (k != 1) {
-              m.skip(x);
-              continue;
-            }
-            const std::string en_msg = str(m, x);  // outlives its reader
-        Reader en = sub(en_msg);
-            std::string key, val;
-            uint32_t a, b;
-            while (en.next(&a, &b)) {
-              if (a == 1) key = str(en, b);
-              else if (a == 2) val = str(en, b);
-              else en.skip(b);
-            }
-            kv[key] = val;
-          }
-          std::vector<std::string> es;
-          for (const auto& [k2, v2] : kv) es.push_back(jstr(k2) + ":" + jstr(v2));
-          rules.push_back("{\"rule\":{" + join(es) + "}}");
-        }
-        if (rules.empty()) fail(CG_POLICY_REJECTED, "L7NetworkPolicyRules: value must contain at least 1 item");
-        l7 = "\"l7_rules\":{\"l7_rules\":[" + join(rules) + "]}";
-        break;
-      }
       default: r.skip(wt);
     }
   }
+  std::string l7;
+  if (l7_field == 100) l7 = http_rules_json(l7_msg);
+  else if (l7_field == 101) l7 = kafka_rules_json(l7_msg);
+  else if (l7_field == 102) l7 = l7_rules_json(l7_msg);
   std::set<uint64_t> uniq(remotes.begin(), remotes.end());
   if (uniq.size() != remotes.size())
     fail(CG_POLICY_REJECTED, "PortNetworkPolicyRule.RemotePolicies: repeated value must contain unique items");
@@ -295,7 +374,7 @@ std::string port_policy(const std::string& msg) {
     switch (f) {
       case 1: port = (uint32_t)scalar(r, wt); break;
       case 2: proto = (uint32_t)scalar(r, wt); break;
-      case 3: rules.push_back(port_rule(str(r, wt))); break;
+      case 3: rules.push_back(port_rule(msg_bytes(r, wt))); break;
       default: r.skip(wt);
     }
   }
@@ -314,8 +393,8 @@ std::string network_policy(const std::string& msg) {
     switch (f) {
       case 1: name = str(r, wt); break;
       case 2: policy = scalar(r, wt); break;
-      case 3: in.push_back(port_policy(str(r, wt))); break;
-      case 4: eg.push_back(port_policy(str(r, wt))); break;
+      case 3: in.push_back(port_policy(msg_bytes(r, wt))); break;
+      case 4: eg.push_back(port_policy(msg_bytes(r, wt))); break;
       default: r.skip(wt);
     }
   }
@@ -325,7 +404,12 @@ std::string network_policy(const std::string& msg) {
 
 }  // namespace
 
-std::string npds_pb_to_json(const uint8_t* p, size_t n) {
+std::string npds_pb_to_json(const uint8_t* p, size_t n, bool strict_utf8) {
+  struct Mode {
+    bool prev;
+    explicit Mode(bool m) : prev(t_strict_utf8) { t_strict_utf8 = m; }
+    ~Mode() { t_strict_utf8 = prev; }
+  } mode(strict_utf8);
   Reader r{p, p + n};
   std::vector<std::string> pols;
   uint32_t f, wt;
@@ -335,13 +419,13 @@ std::string npds_pb_to_json(const uint8_t* p, size_t n) {
       r.skip(wt);
       continue;
     }
-    const std::string a_msg = str(r, wt);  // outlives its reader
-        Reader a = sub(a_msg);
+    const std::string a_msg = msg_bytes(r, wt);  // outlives its reader
+    Reader a = sub(a_msg);
     std::string type, value;
     uint32_t g, w;
     while (a.next(&g, &w)) {
       if (g == 1) type = str(a, w);
-      else if (g == 2) value = str(a, w);
+      else if (g == 2) value = msg_bytes(a, w);
       else a.skip(w);
     }
     if (type != kType) fail(CG_POLICY_REJECTED, "NPDS resource is not a cilium.NetworkPolicy: " + type);

@@ -520,7 +520,7 @@ int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* resp, size_
   std::string json;
   try {
     if (!resp && len) fail(CG_INVALID_ARGUMENT, "NULL DiscoveryResponse");
-    json = npds_pb_to_json(resp, len);
+    json = npds_pb_to_json(resp, len, false);  // golang/protobuf: no UTF-8 check
   } catch (const Error& e) {
     set_error(e.msg);
     return e.code;

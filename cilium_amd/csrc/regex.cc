@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <deque>
 #include <map>
+#include <tuple>
 #include <unordered_map>
 
 namespace cg {
@@ -717,6 +718,167 @@ ByteDfa dfa_prefix(const std::string& s, const ByteSet& alphabet) {
       if (alphabet.test(b)) d.trans[(size_t)(n + 1) * 256 + b] = n + 1;
   }
   d.start = 1;
+  return dfa_minimize(d);
+}
+
+ByteDfa dfa_suffix(const std::string& s, const ByteSet& alphabet) {
+  const int n = (int)s.size();
+  for (unsigned char c : s)
+    if (!alphabet.test(c)) {  // no string over the alphabet ends with s
+      ByteDfa d;
+      d.accept.assign(2, 0);
+      d.trans.assign(2 * 256, 0);
+      return d;
+    }
+  // KMP failure function; automaton state q (0..n) = longest prefix of s
+  // that is a suffix of the input, as ByteDfa state q + 1 (0 stays dead)
+  std::vector<int> fail_(n + 1, 0);
+  for (int i = 1, k = 0; i < n; ++i) {
+    while (k && s[i] != s[k]) k = fail_[k];
+    if (s[i] == s[k]) ++k;
+    fail_[i + 1] = k;
+  }
+  ByteDfa d;
+  d.accept.assign(n + 2, 0);
+  d.trans.assign((size_t)(n + 2) * 256, 0);
+  d.accept[n + 1] = 1;
+  for (int q = 0; q <= n; ++q)
+    for (int b = 0; b < 256; ++b) {
+      if (!alphabet.test(b)) continue;
+      int k = q;
+      if (k == n) k = fail_[n];
+      while (k && (uint8_t)s[k] != b) k = fail_[k];
+      if (k < n && (uint8_t)s[k] == b) ++k;
+      d.trans[(size_t)(q + 1) * 256 + b] = k + 1;
+    }
+  d.start = 1;
+  return dfa_minimize(d);
+}
+
+ByteDfa dfa_complement(const ByteDfa& d, const ByteSet& alphabet) {
+  // live states keep their rows with acceptance flipped; moves into the dead
+  // state go to an accepting sink T instead (bytes outside the alphabet
+  // still die: those strings are not field values)
+  const int n = d.size(), T = n;
+  ByteDfa o;
+  o.accept.assign(n + 1, 0);
+  o.trans.assign((size_t)(n + 1) * 256, 0);
+  for (int s = 1; s < n; ++s) {
+    o.accept[s] = !d.accept[s];
+    for (int b = 0; b < 256; ++b) {
+      if (!alphabet.test(b)) continue;
+      const int t = d.next(s, b);
+      o.trans[(size_t)s * 256 + b] = t ? t : T;
+    }
+  }
+  o.accept[T] = 1;
+  for (int b = 0; b < 256; ++b)
+    if (alphabet.test(b)) o.trans[(size_t)T * 256 + b] = T;
+  o.start = d.start;
+  return dfa_minimize(o);
+}
+
+namespace {
+
+// A DFA under construction: rows of 256 targets (0 = dead).
+struct DfaBuild {
+  ByteDfa d;
+  DfaBuild() {
+    d.accept.assign(1, 0);
+    d.trans.assign(256, 0);
+  }
+  int add(bool acc) {
+    d.accept.push_back(acc);
+    d.trans.resize(d.trans.size() + 256, 0);
+    return d.size() - 1;
+  }
+  void set(int s, int b, int t) { d.trans[(size_t)s * 256 + b] = t; }
+};
+
+// Magnitude automaton: any number of leading '0's, then the significant
+// digits of m, accepting m in [lo, hi] (the all-zeros string is m = 0, needs
+// at least one digit).  States after k significant digits of prefix p are
+// (k, p vs lo's first k digits, p vs hi's first k digits) — the comparison
+// decides for numbers of lo's / hi's length, any other length in between is
+// in range.  Returns the entry state.
+int build_magnitude(DfaBuild& B, uint64_t lo, uint64_t hi) {
+  const bool zero_ok = lo == 0;
+  const uint64_t plo = lo == 0 ? 1 : lo;
+  const std::string L = std::to_string(plo), H = std::to_string(hi);
+  const bool any_pos = hi >= plo;
+  const int entry = B.add(false);
+  const int zeros = B.add(zero_ok);
+  for (int b = '0'; b <= '0'; ++b) {
+    B.set(entry, b, zeros);
+    B.set(zeros, b, zeros);
+  }
+  if (!any_pos) return entry;
+  std::map<std::tuple<int, int, int>, int> ids;
+  std::vector<std::tuple<int, int, int>> work;
+  auto state = [&](int k, int cl, int ch) -> int {
+    // numbers longer than hi never come back into range
+    if (k > (int)H.size()) return 0;
+    auto key = std::make_tuple(k, cl, ch);
+    auto it = ids.find(key);
+    if (it != ids.end()) return it->second;
+    const bool ge = k > (int)L.size() || (k == (int)L.size() && cl >= 0);
+    const bool le = k < (int)H.size() || (k == (int)H.size() && ch <= 0);
+    const int id = B.add(ge && le);
+    ids.emplace(key, id);
+    work.push_back(key);
+    return id;
+  };
+  auto cmp = [](int a, int b) { return a < b ? -1 : a > b ? 1 : 0; };
+  for (int dgt = 1; dgt <= 9; ++dgt) {
+    const int t = state(1, cmp('0' + dgt, L[0]), cmp('0' + dgt, H[0]));
+    B.set(entry, '0' + dgt, t);
+    B.set(zeros, '0' + dgt, t);
+  }
+  while (!work.empty()) {
+    auto [k, cl, ch] = work.back();
+    work.pop_back();
+    const int s = ids[std::make_tuple(k, cl, ch)];
+    for (int dgt = 0; dgt <= 9; ++dgt) {
+      const int c = '0' + dgt;
+      const int ncl = cl != 0 || k >= (int)L.size() ? cl : cmp(c, L[k]);
+      const int nch = ch != 0 || k >= (int)H.size() ? ch : cmp(c, H[k]);
+      B.set(s, c, state(k + 1, ncl, nch));
+    }
+  }
+  return entry;
+}
+
+}  // namespace
+
+ByteDfa dfa_int_range(int64_t start, int64_t end, const ByteSet& alphabet) {
+  DfaBuild B;
+  const int st = B.add(false);  // start: leading isspace bytes loop here
+  if (start < end) {
+    const int64_t last = end - 1;  // inclusive
+    const bool has_pos = last >= 0, has_neg = start < 0;
+    int pos = 0, neg = 0;
+    if (has_pos) pos = build_magnitude(B, start < 0 ? 0 : (uint64_t)start, (uint64_t)last);
+    if (has_neg) {
+      // |x| for the negative part; "-0..." reads as 0, in range iff 0 is
+      // (when the range also holds non-negatives, last >= 0 and |x| >= 1)
+      const uint64_t mlo = last < 0 ? (uint64_t)(-(last + 1)) + 1 : 1;
+      const uint64_t mhi = (uint64_t)(-(start + 1)) + 1;
+      neg = build_magnitude(B, has_pos ? 0 : mlo, mhi);
+    } else if (start == 0) {
+      neg = build_magnitude(B, 0, 0);  // only "-0..." (= 0) reads in range
+    }
+    for (int b : {' ', '\t', '\n', '\v', '\f', '\r'}) B.set(st, b, st);
+    if (has_pos) {
+      B.set(st, '+', pos);
+      for (int b = '0'; b <= '9'; ++b) B.set(st, b, B.d.next(pos, b));
+    }
+    if (neg) B.set(st, '-', neg);
+  }
+  B.d.start = st;
+  ByteDfa d = B.d;
+  for (int s = 0; s < d.size(); ++s)
+    for (int b = 0; b < 256; ++b)
+      if (!alphabet.test(b)) d.trans[(size_t)s * 256 + b] = 0;
   return dfa_minimize(d);
 }
 

@@ -77,6 +77,14 @@ constexpr int kEscByte = 0x03, kEscBase = 0x10;
 ByteDfa dfa_escape_low(const ByteDfa& d);
 // Strings starting with `s` (then any bytes of the alphabet).
 ByteDfa dfa_prefix(const std::string& s, const ByteSet& alphabet);
+// Strings ending with `s` (KMP automaton over the alphabet).
+ByteDfa dfa_suffix(const std::string& s, const ByteSet& alphabet);
+// alphabet* minus L(d): Envoy's invert_match over the strings a field can hold.
+ByteDfa dfa_complement(const ByteDfa& d, const ByteSet& alphabet);
+// Strings that Envoy's StringUtil::atol (strtol base 10 over the whole value,
+// ERANGE rejected) reads as an integer x with start <= x < end
+// (HeaderMatcher.range_match, envoy.type.Int64Range).
+ByteDfa dfa_int_range(int64_t start, int64_t end, const ByteSet& alphabet);
 // A list of escaped items, each followed by the separator pair {kEscByte,
 // kEscSep} (which no escaped string contains): (item SEP)*, every item in
 // the language of the escaped DFA `item` (memcached key lists).

@@ -59,6 +59,27 @@ void DevMem::zero() {
   if (p_ && n_) hip_check(hipMemset(p_, 0, n_), "hipMemset");
 }
 
+LaunchFence::~LaunchFence() {
+  for (auto& [st, ev] : ev_) {
+    (void)hipEventSynchronize((hipEvent_t)ev);
+    (void)hipEventDestroy((hipEvent_t)ev);
+  }
+}
+
+void LaunchFence::record(void* stream) {
+  std::lock_guard<std::mutex> lk(mu_);
+  void* ev = nullptr;
+  for (auto& [st, e] : ev_)
+    if (st == stream) ev = e;
+  if (!ev) {
+    hipEvent_t e;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    ev_.emplace_back(stream, (void*)e);
+    ev = e;
+  }
+  hip_check(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+}
+
 void Engine::set_device() const {
   if (device >= 0) hip_check(hipSetDevice(device), "hipSetDevice");
 }

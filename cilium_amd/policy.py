@@ -212,13 +212,32 @@ def npds_json(policies: list[dict]) -> bytes:
 
 
 def matcher_kind(m: dict) -> tuple[str, str]:
-    """Envoy HeaderData match type of an NPDS HeaderMatcher: ('E'|'R'|'P', value)."""
+    """Envoy HeaderData match type of an NPDS HeaderMatcher:
+    ('E'|'R'|'P'|'X' prefix|'S' suffix|'N' range, value), the type followed by
+    '!' for invert_match; a range's value is "start end"."""
+    inv = "!" if m.get("invert_match") else ""
     if "exact_match" in m:
-        return "E", m["exact_match"]
+        return "E" + inv, m["exact_match"]
     if "regex_match" in m:
-        return "R", m["regex_match"]
+        return "R" + inv, m["regex_match"]
+    if "prefix_match" in m:
+        return "X" + inv, m["prefix_match"]
+    if "suffix_match" in m:
+        return "S" + inv, m["suffix_match"]
+    if "range_match" in m:
+        r = m["range_match"] or {}
+        return "N" + inv, "%d %d" % (int(r.get("start", 0)), int(r.get("end", 0)))
     if "present_match" in m:
-        return "P", ""
+        return "P" + inv, ""
+    if "value" in m:
+        v = m["value"]
+        if not v:
+            return "P" + inv, ""
+        rx = m.get("regex", False)
+        if isinstance(rx, dict):
+            rx = rx.get("value", False)
+        return ("R" if rx else "E") + inv, v
+    return "P" + inv, ""
     if "value" in m:
         v = m["value"]
         if not v:

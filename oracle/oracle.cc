@@ -17,7 +17,11 @@
 //         pkg/policy/l4.go:118-141
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
+#include <climits>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <stdexcept>
@@ -325,12 +329,16 @@ std::string lower(std::string s) {
   return s;
 }
 
-// Envoy HeaderUtility::HeaderData (Value / Regex / Present match types).
+// Envoy HeaderUtility::HeaderData (Envoy @f936fc60, not vendored: restated
+// from the HeaderMatcher fields of pkg/envoy/envoy/api/v2/route/route.pb.go
+// :3185-3198 and the matchHeaders of that era).
 struct HeaderData {
   std::string name;  // LowerCaseString
-  char type;         // 'E' exact, 'R' regex, 'P' present
+  char type;         // 'E' exact (Value), 'R' regex, 'P' present, 'X' prefix, 'S' suffix, 'N' range
   std::string value;
   std::regex re;
+  bool invert = false;
+  int64_t start = 0, end = 0;  // 'N': Int64Range [start, end)
 };
 
 using Headers = std::vector<std::pair<std::string, std::string>>;
@@ -341,21 +349,43 @@ const std::string* header_get(const Headers& h, const std::string& name) {
   return nullptr;
 }
 
-// HeaderUtility::matchHeaders: every configured header must match.
-bool match_headers(const Headers& req, const std::vector<HeaderData>& cfg) {
-  for (const HeaderData& d : cfg) {
-    const std::string* v = header_get(req, d.name);
-    if (!v) return false;
-    switch (d.type) {
-      case 'E':
-        if (*v != d.value) return false;
-        break;
-      case 'R':
-        if (!std::regex_match(*v, d.re)) return false;
-        break;
-      default: break;  // present
+// StringUtil::atol (base 10): strtol over the whole string, ERANGE rejected.
+bool envoy_atol(const std::string& s, int64_t* out) {
+  if (s.empty()) return false;
+  char* end = nullptr;
+  errno = 0;
+  const long v = strtol(s.c_str(), &end, 10);
+  if (*end != '\0' || ((v == LONG_MAX || v == LONG_MIN) && errno == ERANGE)) return false;
+  *out = v;
+  return true;
+}
+
+// HeaderUtility::matchHeaders for one HeaderData: an absent header never
+// matches (whatever invert_match says); else the type's test, inverted by
+// invert_match.
+bool match_header(const Headers& req, const HeaderData& d) {
+  const std::string* v = header_get(req, d.name);
+  if (!v) return false;
+  bool m = true;
+  switch (d.type) {
+    case 'E': m = d.value.empty() || *v == d.value; break;  // HeaderMatchType::Value
+    case 'R': m = std::regex_match(*v, d.re); break;
+    case 'X': m = v->compare(0, d.value.size(), d.value) == 0 && v->size() >= d.value.size(); break;
+    case 'S': m = v->size() >= d.value.size() && v->compare(v->size() - d.value.size(), d.value.size(), d.value) == 0; break;
+    case 'N': {
+      int64_t x = 0;
+      m = envoy_atol(*v, &x) && x >= d.start && x < d.end;
+      break;
     }
+    default: break;  // present
   }
+  return m != d.invert;
+}
+
+// every configured header must match
+bool match_headers(const Headers& req, const std::vector<HeaderData>& cfg) {
+  for (const HeaderData& d : cfg)
+    if (!match_header(req, d)) return false;
   return true;
 }
 
@@ -485,7 +515,8 @@ extern "C" {
 //   port <port> <tcp 0|1>
 //   rule <has_http 0|1> <n> <remote>...
 //   http <nheaders>
-//   hdr <E|R|P> <len> <name> <len> <value>
+//   hdr <E|R|P|X|S|N>[!] <len> <name> <len> <value>   (! = invert_match;
+//                                   N: value "start end")
 void* or_http_load(const char* text, size_t len) {
   try {
     auto o = std::make_unique<HttpOracle>();
@@ -530,10 +561,14 @@ void* or_http_load(const char* text, size_t len) {
         hr = &pr->http_rules.back();
       } else if (w == "hdr") {
         HeaderData d;
-        d.type = r.word()[0];
+        const std::string t = r.word();
+        d.type = t[0];
+        d.invert = t.size() > 1 && t[1] == '!';
         d.name = lower(r.blob());
         d.value = r.blob();
         if (d.type == 'R') d.re = std::regex(d.value, std::regex::optimize);  // may throw: update rejected
+        if (d.type == 'N' && sscanf(d.value.c_str(), "%lld %lld", (long long*)&d.start, (long long*)&d.end) != 2)
+          throw std::runtime_error("bad range matcher");
         hr->push_back(std::move(d));
       } else {
         throw std::runtime_error("bad oracle policy token " + w);

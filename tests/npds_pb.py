@@ -35,6 +35,11 @@ def s(field: int, text) -> bytes:
     return ld(field, text.encode("latin-1") if isinstance(text, str) else bytes(text))
 
 
+def zigzag_free_int64(v: int) -> int:
+    """int64 as a protobuf varint (two's complement, 10 bytes when negative)."""
+    return v & ((1 << 64) - 1)
+
+
 def header_matcher(h: dict) -> bytes:
     out = s(1, h["name"])
     if "exact_match" in h:
@@ -43,10 +48,19 @@ def header_matcher(h: dict) -> bytes:
         out += s(5, h["regex_match"])
     elif "present_match" in h:
         out += vi(7, 1 if h["present_match"] else 0)
+    elif "prefix_match" in h:
+        out += s(9, h["prefix_match"])
+    elif "suffix_match" in h:
+        out += s(10, h["suffix_match"])
+    elif "range_match" in h:
+        r = h["range_match"]
+        out += ld(6, vi(1, zigzag_free_int64(int(r.get("start", 0)))) + vi(2, zigzag_free_int64(int(r.get("end", 0)))))
     elif "value" in h:
         out += s(2, h["value"])
         if h.get("regex"):
             out += ld(3, vi(1, 1))
+    if h.get("invert_match"):
+        out += vi(8, 1)
     return out
 
 

@@ -191,6 +191,89 @@ def test_http_random_policies(host, seed, ids):
     assert np.array_equal(host.http_eval_host_diag(b), orc.eval(**rq))
 
 
+NUM_VALUES = ["0", "5", "-5", "+12", "007", "-0", "12a", "", " 5", "\t7", "+", "-", "99",
+              "9223372036854775807", "9223372036854775808", "-9223372036854775808", "-9223372036854775809",
+              "000000000000000000000000000042", "1e3"]
+RANGES = [(0, 10), (-10, 0), (5, 6), (-9223372036854775808, 9223372036854775807), (100, 50), (-3, 13), (10, 100),
+          (-9223372036854775808, -1), (9223372036854775806, 9223372036854775807), (0, 0)]
+
+
+def _rand_matcher_ext(rng):
+    """Every HeaderMatcher form of route.pb.go:3185-3198 Envoy evaluates:
+    exact (empty = presence), regex, present, prefix, suffix, range, each
+    optionally inverted."""
+    name = rng.choice(HDR_NAMES)
+    k = rng.random()
+    vals = VALUES + NUM_VALUES
+    if k < 0.15:
+        m = {"name": name, "exact_match": rng.choice(vals)}
+    elif k < 0.3:
+        m = {"name": name, "regex_match": rng.choice(["/a.*", ".*b", "[0-9]+", "-?[0-9]", ".*", ""])}
+    elif k < 0.4:
+        m = {"name": name, "present_match": True}
+    elif k < 0.55:
+        m = {"name": name, "prefix_match": rng.choice(["", "/", "/a", "G", "9", "-", "h2"])}
+    elif k < 0.7:
+        m = {"name": name, "suffix_match": rng.choice(["", "b", "com", "ue", "7", "5", "/"])}
+    else:
+        a, b = rng.choice(RANGES)
+        m = {"name": name, "range_match": {"start": a, "end": b}}
+    if rng.random() < 0.3:
+        m["invert_match"] = True
+    return m
+
+
+def all_matcher_case(seed: int, n: int = 1500):
+    """Random policies over every matcher form and requests with numeric
+    and textual values: (policies, request arrays, request header lists)."""
+    rng = random.Random(900 + seed)
+    pols = []
+    for pi in range(3):
+        p = {"name": f"p{pi}", "policy": pi, "ingress_per_port_policies": [], "egress_per_port_policies": []}
+        for key in ("ingress_per_port_policies", "egress_per_port_policies"):
+            for port in rng.sample([0, 80, 81], rng.randint(1, 3)):
+                rules = []
+                for _ in range(rng.randint(1, 3)):
+                    r = {"remote_policies": sorted(rng.sample([1, 2, 3, 4], rng.randint(0, 2))),
+                         "http_rules": {"http_rules": [{"headers": [_rand_matcher_ext(rng)
+                                                                    for _ in range(rng.randint(1, 3))]}
+                                                       for _ in range(rng.randint(1, 3))]}}
+                    rules.append(r)
+                p[key].append({"port": port, "protocol": "TCP", "rules": rules})
+        pols.append(p)
+    reqs = []
+    for _ in range(n):
+        reqs.append([(nm, rng.choice(VALUES + NUM_VALUES)) for nm in HDR_NAMES if rng.random() < 0.75])
+    parts, off = [], [0]
+    for hs in reqs:
+        b = b"".join(k.encode() + b"\0" + v.encode() + b"\0" for k, v in hs)
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    rq = dict(policy=np.array([rng.randint(0, 3) for _ in range(n)], np.uint32),
+              ingress=np.array([rng.randint(0, 1) for _ in range(n)], np.uint8),
+              port=np.array([rng.choice([80, 81, 9]) for _ in range(n)], np.uint16),
+              remote=np.array([rng.choice([0, 1, 2, 3, 4]) for _ in range(n)], np.uint32),
+              hdr_blob=np.frombuffer(b"".join(parts) or b"\0", np.uint8).copy(),
+              hdr_off=np.array(off, np.uint64))
+    return pols, rq, reqs
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_http_random_policies_all_matchers(host, seed):
+    """prefix / suffix / range / invert / empty-exact matchers compiled into
+    the union DFAs (http.cc, regex.cc dfa_suffix / dfa_int_range /
+    dfa_complement) against the oracle's restatement of Envoy's matchHeaders
+    (oracle.cc match_header; strtol for ranges)."""
+    pols, rq, reqs = all_matcher_case(seed)
+    host.update_http_policy(pols)
+    b = host.pack_http(**rq)
+    want = oracle.HttpOracle(pols).eval(**rq)
+    got = host.http_eval_host_diag(b)
+    bad = np.nonzero(got != want)[0]
+    assert not len(bad), [(i, reqs[i], int(got[i]), int(want[i])) for i in bad[:5]]
+    assert 0.05 < want.mean() < 0.95
+
+
 def test_http_10k_compile_and_overflow(host):
     pols, info = synth.http10k_rules()
     rq = synth.http10k_requests(20_000, info)

@@ -267,6 +267,16 @@ def test_http_random_policies(gpu, seed, ids):
     assert np.array_equal(gpu.http_verdicts(gpu.pack_http(**rq)), orc.eval(**rq))
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_http_all_matcher_forms(gpu, seed):
+    """prefix / suffix / range / invert_match / empty exact on the GPU
+    against the oracle's matchHeaders restatement."""
+    from test_cpu_differential import all_matcher_case
+    pols, rq, _ = all_matcher_case(seed, 4000)
+    gpu.update_http_policy(pols)
+    assert np.array_equal(gpu.http_verdicts(gpu.pack_http(**rq)), oracle.HttpOracle(pols).eval(**rq))
+
+
 def test_http_many_byte_classes(gpu):
     """A program over more than 64 byte classes keeps byte-indexed comb rows
     (the class-code packing needs a class code in one byte): 90 exact paths

@@ -123,3 +123,29 @@ def test_host_decoder_edges(host):
     ]
     got = _check(host, edges)
     assert got[0][0] == 1 and got[7][0] == 0
+
+
+def _nested_produce(depth: int) -> bytes:
+    """A produce v0 request whose message set is `depth` gzip sets nested
+    one inside the other around one plain message."""
+    ms = K.message_set([(None, b"v")])
+    for _ in range(depth):
+        ms = K.message(None, gzip.compress(ms, mtime=0), K.CODEC_GZIP, 0)
+    body = K.i16(1) + K.i32(1000)
+    body += K.array([(b"t", [(0, ms)])],
+                    lambda t: K.string(t[0]) + K.array(t[1], lambda p: K.i32(p[0]) + K.i32(len(p[1])) + p[1]))
+    return K._request(K.PRODUCE, 0, b"c", body)
+
+
+def test_nested_compression_bounds(host):
+    """HostInflate's intended deviation (kafka_wire.cc): up to 64 nested
+    compressed sets decode as readMessageSet would; a 65th level is a decode
+    error (Go's recursion has no depth limit, so the oracle still parses)."""
+    _policy(host)
+    ok = [_nested_produce(d) for d in (1, 8, 64)]
+    _check(host, ok)
+    deep = _nested_produce(65)
+    assert R.decode(deep) is not None  # the reference semantics parse it
+    raw, off = K.concat([deep])
+    _, _, status = host.kafka_decode(raw, off, np.zeros(1, np.uint16), np.zeros(1, np.uint32), diag_cpu=True)
+    assert int(status[0]) != 0

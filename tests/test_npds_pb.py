@@ -121,6 +121,113 @@ def test_pb_proxylib_translation_codes():
     _lib.CloseModule(inst)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_pb_all_matcher_forms(seed):
+    """prefix / suffix / range (negative int64 varints) / invert_match from
+    the wire compile to the same tables as their JSON form."""
+    import random
+
+    from test_cpu_differential import HDR_NAMES, NUM_VALUES, VALUES, _rand_matcher_ext
+    rng = random.Random(seed)
+    pols = [{"name": f"p{i}", "policy": i, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [], "http_rules": {"http_rules": [
+            {"headers": [_rand_matcher_ext(rng) for _ in range(rng.randint(1, 3))]} for _ in range(3)]}}]}]}
+            for i in range(2)]
+    n = 800
+    parts, off = [], [0]
+    for _ in range(n):
+        b = b"".join(nm.encode() + b"\0" + rng.choice(VALUES + NUM_VALUES).encode() + b"\0"
+                     for nm in HDR_NAMES if rng.random() < 0.8)
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    rq = dict(policy=np.array([rng.randint(0, 1) for _ in range(n)], np.uint32), ingress=np.ones(n, np.uint8),
+              port=np.full(n, 80, np.uint16), remote=np.zeros(n, np.uint32),
+              hdr_blob=np.frombuffer(b"".join(parts), np.uint8).copy(), hdr_off=np.array(off, np.uint64))
+    v = _same_tables(pols, rq)
+    assert 0 < v.sum() < n
+
+
+def test_pb_singular_messages_merge():
+    """Occurrences of a singular embedded message merge (proto3): the
+    http_rules oneof member split in two appends its rule lists, a BoolValue
+    split in two keeps the set flag, and a later oneof member replaces the
+    earlier one."""
+    r1 = {"headers": [{"name": ":path", "regex_match": "/a.*"}]}
+    r2 = {"headers": [{"name": ":method", "exact_match": "GET"}]}
+
+    def rules_payload(*rs):
+        return b"".join(PB.ld(1, b"".join(PB.ld(1, PB.header_matcher(h)) for h in r["headers"])) for r in rs)
+
+    def pol_blob(port_rule_bytes):
+        pp = PB.vi(1, 80) + PB.ld(3, port_rule_bytes)
+        np_ = PB.s(1, "p") + PB.vi(2, 0) + PB.ld(3, pp)
+        return PB.s(1, "1") + PB.ld(2, PB.s(1, PB.TYPE_URL) + PB.ld(2, np_))
+
+    split = pol_blob(PB.ld(100, rules_payload(r1)) + PB.ld(100, rules_payload(r2)))
+    whole = [{"name": "p", "policy": 0, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [], "http_rules": {"http_rules": [r1, r2]}}]}]}]
+    # a kafka member first, then http: the last member (http) wins
+    replaced = pol_blob(PB.ld(101, PB.ld(1, PB.vi(1, 0))) + PB.ld(100, rules_payload(r1, r2)))
+    # deprecated {value, regex} with the BoolValue split: {value: true} then {}
+    hm = PB.s(1, ":path") + PB.s(2, "/a.*") + PB.ld(3, PB.vi(1, 1)) + PB.ld(3, b"")
+    boolsplit = pol_blob(PB.ld(100, PB.ld(1, PB.ld(1, hm))))
+    boolwhole = [{"name": "p", "policy": 0, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [], "http_rules": {"http_rules": [{"headers": [
+            {"name": ":path", "regex_match": "/a.*"}]}]}}]}]}]
+    reqs = [[(":path", "/abc"), (":method", "PUT")], [(":path", "/x"), (":method", "GET")],
+            [(":path", "/x"), (":method", "PUT")], [(":path", "/a"), (":method", "GET")]]
+    parts, off = [], [0]
+    for hs in reqs:
+        b = b"".join(k.encode() + b"\0" + v.encode() + b"\0" for k, v in hs)
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    n = len(reqs)
+    rq = dict(policy=np.zeros(n, np.uint32), ingress=np.ones(n, np.uint8), port=np.full(n, 80, np.uint16),
+              remote=np.zeros(n, np.uint32), hdr_blob=np.frombuffer(b"".join(parts), np.uint8).copy(),
+              hdr_off=np.array(off, np.uint64))
+
+    def walk_pb(blob):
+        cl = Classifier(device=-1)
+        cl.update_http_policy_npds(blob)
+        v = cl.http_eval_host_diag(cl.pack_http(**rq))
+        cl.close()
+        return v.tolist()
+
+    def walk_json(pols):
+        cl = Classifier(device=-1)
+        cl.update_http_policy(pols)
+        v = cl.http_eval_host_diag(cl.pack_http(**rq))
+        cl.close()
+        return v.tolist()
+
+    assert walk_pb(split) == walk_json(whole) == [1, 1, 0, 1]
+    assert walk_pb(replaced) == [1, 1, 0, 1]
+    assert walk_pb(boolsplit) == walk_json(boolwhole) == [1, 0, 0, 1]
+
+
+def test_pb_utf8_rule():
+    """A proto3 string field that is not UTF-8: Envoy's protobuf runtime
+    rejects the response (HTTP update), golang/protobuf of the reference era
+    accepts it (proxylib update)."""
+    bad = {"name": "p", "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [], "http_rules": {"http_rules": [{"headers": [
+            {"name": "x-a", "exact_match": b"\xff\xfe".decode("latin-1")}]}]}}]}]}
+    good = json.loads(json.dumps(bad))
+    good["ingress_per_port_policies"][0]["rules"][0]["http_rules"]["http_rules"][0]["headers"][0]["exact_match"] = \
+        "\u00e9t\u00e9".encode("utf-8").decode("latin-1")
+    cl = Classifier(device=-1)
+    assert _rc(cl, PB.discovery_response([bad])) == N.CG_POLICY_REJECTED
+    assert _rc(cl, PB.discovery_response([good])) == N.CG_OK
+    cl.close()
+    from test_proxylib_abi import _lib, open_module
+    inst = open_module([(b"node-id", b"cpu-npds-utf8")], "-1")
+    pl = [{"name": "p", "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"cmd": "READ", "file": "\xff"}}]}}]}]}]
+    blob = PB.discovery_response(pl)
+    assert N.lib.cg_proxylib_policy_update_npds(inst, blob, len(blob)) == N.CG_OK
+    _lib.CloseModule(inst)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("suite", HTTP["suites"], ids=lambda s: s["name"])
 def test_gpu_pb_http_kat(suite):
