@@ -142,9 +142,34 @@ class PortRuleKafka:
 
 @dataclass
 class L7Rules:
-    """api.L7Rules (pkg/policy/api/l4.go:65-85)."""
-    HTTP: list[PortRuleHTTP] = field(default_factory=list)
-    Kafka: list[PortRuleKafka] = field(default_factory=list)
+    """api.L7Rules (pkg/policy/api/l4.go:65-85).  None stands for Go's nil
+    slice: IsEmpty (l4.go:96-99) tells a nil list from an empty one."""
+    HTTP: Optional[list[PortRuleHTTP]] = None
+    Kafka: Optional[list[PortRuleKafka]] = None
+    L7Proto: str = ""
+    L7: Optional[list[dict]] = None  # []PortRuleL7 (key/value maps)
+
+    def len(self) -> int:
+        """Len (l4.go:87-93)."""
+        return len(self.HTTP or []) + len(self.Kafka or []) + len(self.L7 or [])
+
+    def is_empty(self) -> bool:
+        """IsEmpty (l4.go:95-99): every rule list nil."""
+        return self.HTTP is None and self.Kafka is None and self.L7 is None
+
+    @staticmethod
+    def from_json(d: Optional[dict]) -> Optional["L7Rules"]:
+        """The `rules` member of an api.PortRule (JSON tags http, kafka,
+        l7proto, l7)."""
+        if d is None:
+            return None
+        http = [PortRuleHTTP(Path=h.get("path", ""), Method=h.get("method", ""), Host=h.get("host", ""),
+                             Headers=list(h.get("headers") or [])) for h in d["http"]] if "http" in d else None
+        kafka = [PortRuleKafka(Role=k.get("role", ""), APIKey=k.get("apiKey", ""), APIVersion=k.get("apiVersion", ""),
+                               ClientID=k.get("clientID", ""), Topic=k.get("topic", ""))
+                 for k in d["kafka"]] if "kafka" in d else None
+        l7 = [dict(x) for x in d["l7"]] if "l7" in d else None
+        return L7Rules(HTTP=http, Kafka=kafka, L7Proto=d.get("l7proto", ""), L7=l7)
 
 
 # -------------------------------------------------------------- policymap --

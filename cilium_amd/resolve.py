@@ -16,6 +16,18 @@ cache and the Kafka redirect:
   ``get_network_policy``        — pkg/envoy/server.go:476-622 (+ sort.go)
 * ``kafka_redirect``            — pkg/proxy/redirect.go:68-82 (the L7DataMap a
   Kafka redirect holds), resolved to identity lists for cg_kafka_policy_update
+* ``Rule`` / ``IngressRule`` / ``EgressRule`` / ``PortRule`` — pkg/policy/api
+  (rule.go, ingress.go, egress.go, l4.go; JSON tags of the policy files)
+* ``Repository``                — pkg/policy/repository.go: AddList,
+  GetRulesMatching (:624-643), CanReachIngress/EgressRLocked (:80-99),
+  AllowsIngress/EgressLabelAccess, ResolveL4Ingress/EgressPolicy (:245-330),
+  wildcardL3L4Rule / wildcardL3L4Rules (:128-243); rule.go canReachIngress /
+  canReachEgress (:352-440), resolveL4Ingress/EgressPolicy (:227-294,
+  :521-566), mergeL4Ingress/Egress(Port) (:111-225, :442-519), mergeL4Port
+  (:36-109)
+* ``Endpoint`` policy compile   — pkg/endpoint/policy.go:195-371,616-639:
+  ComputePolicyEnforcement, resolveL4Policy, computeDesiredPolicyMapState
+  (L4 entries, localhost, world, L3 entries)
 
 Identity caches are ``{numeric_identity: labels}`` with labels given as
 ``{"source:key": value}`` (or plain ``{"key": value}``, source "any").
@@ -125,12 +137,12 @@ class L7DataMap(dict):
         if labels is not None:
             for sel, r in self.items():
                 if sel.matches(labels):
-                    out_http += r.HTTP
-                    out_kafka += r.Kafka
+                    out_http += r.HTTP or []
+                    out_kafka += r.Kafka or []
         r = self.get(WILDCARD)
         if r is not None:
-            out_http += r.HTTP
-            out_kafka += r.Kafka
+            out_http += r.HTTP or []
+            out_kafka += r.Kafka or []
         out.HTTP, out.Kafka = out_http, out_kafka
         return out
 
@@ -145,6 +157,7 @@ class L4Filter:
     L7Parser: str = PARSER_NONE
     L7RulesPerEp: L7DataMap = field(default_factory=L7DataMap)
     Ingress: bool = True
+    DerivedFromRules: list = field(default_factory=list)  # labels.LabelArrayList
 
     def is_redirect(self) -> bool:
         """l4.go:236-238"""
@@ -155,41 +168,46 @@ class L4Filter:
 
 
 def _rules_empty(r: Optional[L7Rules]) -> bool:
-    return r is None or (not r.HTTP and not r.Kafka)
+    """L7Rules.IsEmpty (api/l4.go:95-99), a nil *L7Rules included."""
+    return r is None or r.is_empty()
 
 
 def create_l4_filter(peer_endpoints: list, rules: Optional[L7Rules], port: int, protocol: str,
-                     ingress: bool) -> L4Filter:
+                     ingress: bool, rule_labels=None) -> L4Filter:
     """CreateL4Filter (l4.go:162-200): a wildcard peer list becomes
-    [WildcardEndpointSelector]; L7 rules only on TCP, parser HTTP > Kafka."""
+    [WildcardEndpointSelector]; L7 rules only on TCP, parser HTTP > Kafka >
+    the generic l7proto."""
     eps = [WILDCARD] if selects_all(peer_endpoints) else list(peer_endpoints)
     f = L4Filter(Port=int(port), Protocol=protocol, U8Proto=U8PROTO.get(protocol, 0), Endpoints=eps,
-                 Ingress=ingress)
+                 Ingress=ingress, DerivedFromRules=[rule_labels])
     if protocol == "TCP" and rules is not None:
         if rules.HTTP:
             f.L7Parser = PARSER_HTTP
         elif rules.Kafka:
             f.L7Parser = PARSER_KAFKA
-        if not _rules_empty(rules):
-            # addRulesForEndpoints (l4.go:143-156)
+        elif rules.L7Proto:
+            f.L7Parser = rules.L7Proto
+        if not _rules_empty(rules) and rules.len():
+            # addRulesForEndpoints (l4.go:143-156): eps is never empty here
             for sel in eps:
                 f.L7RulesPerEp[sel] = rules
     return f
 
 
 def create_l4_ingress_filter(from_endpoints: list, endpoints_with_l3_override: list, rules: Optional[L7Rules],
-                             port: int, protocol: str) -> L4Filter:
+                             port: int, protocol: str, rule_labels=None) -> L4Filter:
     """CreateL4IngressFilter (l4.go:209-223): selectors with an L3 override
     (host / world in the relevant modes) get wildcard L7 rules."""
-    f = create_l4_filter(from_endpoints, rules, port, protocol, True)
+    f = create_l4_filter(from_endpoints, rules, port, protocol, True, rule_labels)
     if not _rules_empty(rules):
         for sel in endpoints_with_l3_override:
             f.L7RulesPerEp[sel] = L7Rules()
     return f
 
 
-def create_l4_egress_filter(to_endpoints: list, rules: Optional[L7Rules], port: int, protocol: str) -> L4Filter:
-    return create_l4_filter(to_endpoints, rules, port, protocol, False)
+def create_l4_egress_filter(to_endpoints: list, rules: Optional[L7Rules], port: int, protocol: str,
+                            rule_labels=None) -> L4Filter:
+    return create_l4_filter(to_endpoints, rules, port, protocol, False, rule_labels)
 
 
 @dataclass
@@ -426,6 +444,481 @@ def kafka_redirect(name: str, f: L4Filter, identity_cache: Mapping[int, Mapping[
         else:
             sels.append({"identities": get_security_identities(identity_cache, sel), "rules": rules})
     return {"name": name, "selectors": sels}
+
+
+# ------------------------------------------------------------- api.Rule ----
+class PolicyMergeError(ValueError):
+    """mergeL4Port's conflicting-parser / conflicting-L7-type errors
+    (rule.go:52-96); the whole resolution fails, as the reference's does."""
+
+
+# EntitySelectorMapping (api/entity.go:71-84, :129-134)
+_ENTITY_SELECTORS = {
+    "all": [EndpointSelector()],
+    "world": [EndpointSelector.of({"reserved:world": ""})],
+    "host": [EndpointSelector.of({"reserved:host": ""})],
+    "init": [EndpointSelector.of({"reserved:init": ""})],
+    "cluster": [EndpointSelector.of({"reserved:host": ""}), EndpointSelector.of({"reserved:init": ""}),
+                EndpointSelector.of({"reserved:unmanaged": ""})],
+}
+
+
+def selector_from_json(d: Optional[dict]) -> EndpointSelector:
+    """api.EndpointSelector from its JSON (a k8s LabelSelector)."""
+    d = d or {}
+    me = [(e["key"], e["operator"], tuple(e.get("values") or ())) for e in d.get("matchExpressions") or []]
+    return EndpointSelector.of(d.get("matchLabels") or {}, me)
+
+
+def requirements_of(sel: EndpointSelector) -> tuple:
+    """ConvertToLabelSelectorRequirementSlice (api/selector.go): matchLabels
+    as In-requirements with one value, then the matchExpressions."""
+    return tuple((k, "In", (v,)) for k, v in sel.match_labels) + tuple(sel.match_expressions)
+
+
+def with_requirements(sel: EndpointSelector, reqs: tuple) -> EndpointSelector:
+    """A copy of `sel` whose MatchExpressions carry `reqs` as well
+    (rule.go:243-253, :530-541)."""
+    return EndpointSelector(sel.match_labels, tuple(sel.match_expressions) + tuple(reqs))
+
+
+@dataclass
+class PortProtocol:
+    """api.PortProtocol (api/l4.go:27-40)."""
+    Port: str
+    Protocol: str = "ANY"
+
+
+def parse_l4_proto(p: str) -> str:
+    """ParseL4Proto: "" → ANY, else upper-cased and validated."""
+    if not p:
+        return "ANY"
+    u = p.upper()
+    if u not in ("TCP", "UDP", "ANY"):
+        raise ValueError(f'invalid protocol "{u}", must be {{ tcp | udp | any }}')
+    return u
+
+
+def parse_port(port: str) -> int:
+    """strconv.ParseUint(port, 0, 16): decimal, 0x hex, 0 octal, 0b binary."""
+    s = port
+    try:
+        if s.startswith(("0x", "0X")):
+            v = int(s[2:], 16)
+        elif s.startswith(("0b", "0B")):
+            v = int(s[2:], 2)
+        elif s.startswith(("0o", "0O")):
+            v = int(s[2:], 8)
+        elif len(s) > 1 and s.startswith("0"):
+            v = int(s[1:], 8)
+        else:
+            v = int(s, 10)
+    except ValueError as e:
+        raise ValueError(f"Unable to parse port: {port!r}") from e
+    if not s or not s[-1].isalnum() or v > 0xFFFF or v < 0:
+        raise ValueError(f"Unable to parse port: {port!r}")
+    return v
+
+
+@dataclass
+class PortRule:
+    """api.PortRule (api/l4.go:44-60)."""
+    Ports: list = field(default_factory=list)   # [PortProtocol]
+    Rules: Optional[L7Rules] = None
+
+
+@dataclass
+class IngressRule:
+    """api.IngressRule (api/ingress.go); CIDR members are kept only to be
+    refused by the label-based resolution (not on this path)."""
+    FromEndpoints: list = field(default_factory=list)
+    FromRequires: list = field(default_factory=list)
+    FromEntities: list = field(default_factory=list)
+    ToPorts: list = field(default_factory=list)
+    FromCIDR: list = field(default_factory=list)
+
+    def source_selectors(self) -> list:
+        """GetSourceEndpointSelectors (ingress.go:111-115)."""
+        out = list(self.FromEndpoints)
+        for e in self.FromEntities:
+            out += _ENTITY_SELECTORS.get(e, [])
+        return out
+
+    def is_label_based(self) -> bool:
+        """IsLabelBased (ingress.go:120-122)."""
+        return not self.FromRequires and not self.FromCIDR
+
+
+@dataclass
+class EgressRule:
+    """api.EgressRule (api/egress.go)."""
+    ToEndpoints: list = field(default_factory=list)
+    ToRequires: list = field(default_factory=list)
+    ToEntities: list = field(default_factory=list)
+    ToPorts: list = field(default_factory=list)
+    ToCIDR: list = field(default_factory=list)
+
+    def destination_selectors(self) -> list:
+        """GetDestinationEndpointSelectors (egress.go:139-143)."""
+        out = list(self.ToEndpoints)
+        for e in self.ToEntities:
+            out += _ENTITY_SELECTORS.get(e, [])
+        return out
+
+    def is_label_based(self) -> bool:
+        """IsLabelBased (egress.go:148-150)."""
+        return not self.ToRequires and not self.ToCIDR
+
+
+@dataclass
+class Rule:
+    """api.Rule (api/rule.go:32-64)."""
+    EndpointSelector: EndpointSelector = field(default_factory=EndpointSelector)
+    Ingress: list = field(default_factory=list)
+    Egress: list = field(default_factory=list)
+    Labels: tuple = ()
+
+    @staticmethod
+    def from_json(d: dict) -> "Rule":
+        """A rule of a policy file (`cilium policy import` JSON)."""
+        def ports(lst):
+            out = []
+            for pr in lst or []:
+                pps = [PortProtocol(str(p.get("port", "")), p.get("protocol", "")) for p in pr.get("ports") or []]
+                out.append(PortRule(pps, L7Rules.from_json(pr.get("rules"))))
+            return out
+        ing = [IngressRule([selector_from_json(x) for x in r.get("fromEndpoints") or []],
+                           [selector_from_json(x) for x in r.get("fromRequires") or []],
+                           list(r.get("fromEntities") or []), ports(r.get("toPorts")),
+                           list(r.get("fromCIDR") or []) + list(r.get("fromCIDRSet") or []))
+               for r in d.get("ingress") or []]
+        eg = [EgressRule([selector_from_json(x) for x in r.get("toEndpoints") or []],
+                         [selector_from_json(x) for x in r.get("toRequires") or []],
+                         list(r.get("toEntities") or []), ports(r.get("toPorts")),
+                         list(r.get("toCIDR") or []) + list(r.get("toCIDRSet") or []) +
+                         list(r.get("toServices") or []))
+              for r in d.get("egress") or []]
+        labels = tuple(sorted(str(x) for x in d.get("labels") or []))
+        return Rule(selector_from_json(d.get("endpointSelector")), ing, eg, labels)
+
+    def sanitize(self) -> None:
+        """Rule.Sanitize (rule_validation.go:37-69, :316-358): every port
+        parses as a non-zero uint16, protocols are normalised (ParseL4Proto),
+        L7 rules only on TCP, at most 40 ports per PortRule, L7 rule
+        validation (PortRuleHTTP / PortRuleKafka Sanitize)."""
+        for rs in (self.Ingress, self.Egress):
+            for r in rs:
+                for pr in r.ToPorts:
+                    if len(pr.Ports) > 40:
+                        raise ValueError("too many ports, the max is 40")
+                    for pp in pr.Ports:
+                        if pp.Port == "":
+                            raise ValueError("Port must be specified")
+                        if parse_port(pp.Port) == 0:
+                            raise ValueError("Port cannot be 0")
+                        pp.Protocol = parse_l4_proto(pp.Protocol)
+                        if not _rules_empty(pr.Rules) and pp.Protocol != "TCP":
+                            raise ValueError(f"L7 rules can only apply exclusively to TCP, not {pp.Protocol}")
+                    if not _rules_empty(pr.Rules):
+                        kinds = sum(bool(x) for x in (pr.Rules.HTTP, pr.Rules.Kafka, pr.Rules.L7))
+                        if kinds > 1:
+                            raise ValueError("multiple L7 protocol rule types specified in single rule")
+                        for h in pr.Rules.HTTP or []:
+                            h.sanitize()
+                        for k in pr.Rules.Kafka or []:
+                            k.sanitize()
+
+
+def _copy_l7(r: L7Rules) -> L7Rules:
+    return L7Rules(HTTP=None if r.HTTP is None else list(r.HTTP), Kafka=None if r.Kafka is None else list(r.Kafka),
+                   L7Proto=r.L7Proto, L7=None if r.L7 is None else list(r.L7))
+
+
+def merge_l4_port(endpoints: list, existing: L4Filter, to_merge: L4Filter) -> None:
+    """mergeL4Port (rule.go:36-109): L3 union (a wildcard absorbs all), the
+    parsers must agree, L7 rules per selector appended without duplicates."""
+    if existing.allows_all_at_l3() or to_merge.allows_all_at_l3():
+        existing.Endpoints = [WILDCARD]
+    else:
+        existing.Endpoints = list(existing.Endpoints) + list(endpoints)
+    if to_merge.L7Parser != PARSER_NONE:
+        if existing.L7Parser == PARSER_NONE:
+            existing.L7Parser = to_merge.L7Parser
+        elif to_merge.L7Parser != existing.L7Parser:
+            raise PolicyMergeError(f"Cannot merge conflicting L7 parsers ({to_merge.L7Parser}/{existing.L7Parser})")
+    for sel, new in to_merge.L7RulesPerEp.items():
+        if sel not in existing.L7RulesPerEp:
+            existing.L7RulesPerEp[sel] = new
+            continue
+        ep = _copy_l7(existing.L7RulesPerEp[sel])
+        if new.HTTP:
+            if ep.Kafka or ep.L7Proto:
+                raise PolicyMergeError("Cannot merge conflicting L7 rule types")
+            for r in new.HTTP:
+                if r not in (ep.HTTP or []):
+                    ep.HTTP = (ep.HTTP or []) + [r]
+        elif new.Kafka:
+            if ep.HTTP or ep.L7Proto:
+                raise PolicyMergeError("Cannot merge conflicting L7 rule types")
+            for r in new.Kafka:
+                if r not in (ep.Kafka or []):
+                    ep.Kafka = (ep.Kafka or []) + [r]
+        elif new.L7Proto:
+            if ep.Kafka or ep.HTTP or (ep.L7Proto and ep.L7Proto != new.L7Proto):
+                raise PolicyMergeError("Cannot merge conflicting L7 rule types")
+            if not ep.L7Proto:
+                ep.L7Proto = new.L7Proto
+            for r in new.L7 or []:
+                if r not in (ep.L7 or []):
+                    ep.L7 = (ep.L7 or []) + [r]
+        existing.L7RulesPerEp[sel] = ep
+
+
+def _filter_key(pp: PortProtocol, proto: str) -> str:
+    return f"{pp.Port}/{proto}"
+
+
+def _merge_port(endpoints, override, r: PortRule, pp: PortProtocol, proto: str, labels, res: dict,
+                ingress: bool) -> int:
+    """mergeL4IngressPort (rule.go:121-141) / mergeL4EgressPort (:480-500)."""
+    def create():
+        port = parse_port(pp.Port)
+        if ingress:
+            return create_l4_ingress_filter(endpoints, override, r.Rules, port, proto, labels)
+        return create_l4_egress_filter(endpoints, r.Rules, port, proto, labels)
+    key = _filter_key(pp, proto)
+    if key not in res:
+        res[key] = create()
+        return 1
+    existing = res[key]
+    merged = L4Filter(existing.Port, existing.Protocol, existing.U8Proto, list(existing.Endpoints),
+                      existing.L7Parser, L7DataMap(existing.L7RulesPerEp), existing.Ingress,
+                      list(existing.DerivedFromRules))
+    merge_l4_port(endpoints, merged, create())
+    merged.DerivedFromRules.append(labels)
+    res[key] = merged
+    return 1
+
+
+def _merge_l4(peers: list, override: list, to_ports: list, labels, res: dict, ingress: bool) -> int:
+    """mergeL4Ingress (rule.go:143-225) / mergeL4Egress (:442-478): every
+    port of every PortRule; ANY becomes TCP then UDP."""
+    if not to_ports:
+        return 0
+    found = 0
+    for r in to_ports:
+        for pp in r.Ports:
+            protos = [pp.Protocol] if pp.Protocol != "ANY" else ["TCP", "UDP"]
+            for proto in protos:
+                found += _merge_port(peers, override, r, pp, proto, labels, res, ingress)
+    return found
+
+
+@dataclass
+class PolicyConfig:
+    """The daemon options that change resolution (pkg/option):
+    AlwaysAllowLocalhost() and HostAllowsWorld (rule.go:166-172)."""
+    always_allow_localhost: bool = True
+    host_allows_world: bool = False
+
+
+def resolve_rule_l4_ingress(r: Rule, to_labels, requirements: tuple, result: L4Policy,
+                            cfg: PolicyConfig = PolicyConfig()) -> Optional[L4Policy]:
+    """rule.resolveL4IngressPolicy (rule.go:227-294): None when the rule does
+    not select `to_labels` or contributes no filter; raises PolicyMergeError."""
+    if not r.EndpointSelector.matches(to_labels):
+        return None
+    override = []
+    if cfg.always_allow_localhost:
+        override.append(_ENTITY_SELECTORS["host"][0])
+        if cfg.host_allows_world:
+            override.append(_ENTITY_SELECTORS["world"][0])
+    found = 0
+    for ing in r.Ingress:
+        if requirements:
+            ing = IngressRule([with_requirements(sel, requirements) for sel in ing.FromEndpoints], ing.FromRequires,
+                              ing.FromEntities, ing.ToPorts, ing.FromCIDR)
+        peers = ing.source_selectors()
+        found += _merge_l4(peers, override, ing.ToPorts, r.Labels, result.Ingress, True)
+    return result if found else None
+
+
+def resolve_rule_l4_egress(r: Rule, from_labels, requirements: tuple, result: L4Policy) -> Optional[L4Policy]:
+    """rule.resolveL4EgressPolicy (rule.go:521-566)."""
+    if not r.EndpointSelector.matches(from_labels):
+        return None
+    found = 0
+    for eg in r.Egress:
+        if requirements:
+            eg = EgressRule([with_requirements(sel, requirements) for sel in eg.ToEndpoints], eg.ToRequires,
+                            eg.ToEntities, eg.ToPorts, eg.ToCIDR)
+        peers = eg.destination_selectors()
+        found += _merge_l4(peers, [], eg.ToPorts, r.Labels, result.Egress, False)
+    return result if found else None
+
+
+def wildcard_l3l4_rule(proto: str, port: int, endpoints: list, labels, l4map: dict) -> None:
+    """wildcardL3L4Rule (repository.go:128-166): a redirecting filter on the
+    port (any port when 0) gets an allow-all L7 rule for selectors allowed at
+    L3 (or L3/L4) only: HTTP [{}], a sanitized empty Kafka rule, or an
+    empty list of the generic parser's rules."""
+    for k, f in list(l4map.items()):
+        if proto != f.Protocol or (port != 0 and port != f.Port):
+            continue
+        if f.L7Parser == PARSER_NONE:
+            continue
+        per_ep = L7DataMap(f.L7RulesPerEp)
+        for sel in endpoints:
+            if f.L7Parser == PARSER_HTTP:
+                per_ep[sel] = L7Rules(HTTP=[PortRuleHTTP()])
+            elif f.L7Parser == PARSER_KAFKA:
+                kr = PortRuleKafka()
+                kr.sanitize()
+                per_ep[sel] = L7Rules(Kafka=[kr])
+            else:
+                per_ep[sel] = L7Rules(L7Proto=f.L7Parser, L7=[])
+        l4map[k] = L4Filter(f.Port, f.Protocol, f.U8Proto, list(f.Endpoints) + list(endpoints), f.L7Parser, per_ep,
+                            f.Ingress, list(f.DerivedFromRules) + [labels])
+
+
+class Repository:
+    """policy.Repository (pkg/policy/repository.go): an ordered rule list."""
+
+    def __init__(self, rules: Iterable[Rule] = (), cfg: Optional[PolicyConfig] = None):
+        self.rules: list[Rule] = []
+        self.cfg = cfg or PolicyConfig()
+        self.add_list(rules)
+
+    def add_list(self, rules: Iterable[Rule]) -> None:
+        """AddListLocked after PolicyAdd's Sanitize (daemon/policy.go:171)."""
+        rules = list(rules)
+        for r in rules:
+            r.sanitize()
+        self.rules += rules
+
+    def get_rules_matching(self, labels) -> tuple[bool, bool]:
+        """GetRulesMatching (:624-643): (ingress, egress) enforcement."""
+        ing = eg = False
+        for r in self.rules:
+            if r.EndpointSelector.matches(labels):
+                ing = ing or bool(r.Ingress)
+                eg = eg or bool(r.Egress)
+        return ing, eg
+
+    def can_reach_ingress(self, from_labels, to_labels) -> str:
+        """CanReachIngressRLocked (:80-99) over rule.canReachIngress
+        (rule.go:352-395): "allowed" / "denied" / "undecided"."""
+        decision = "undecided"
+        for r in self.rules:
+            d = self._rule_reach(r.EndpointSelector, r.Ingress, to_labels, from_labels, True)
+            if d == "denied":
+                return "denied"
+            if d == "allowed":
+                decision = "allowed"
+        return decision
+
+    def can_reach_egress(self, from_labels, to_labels) -> str:
+        """CanReachEgressRLocked over rule.canReachEgress (rule.go:399-440)."""
+        decision = "undecided"
+        for r in self.rules:
+            d = self._rule_reach(r.EndpointSelector, r.Egress, from_labels, to_labels, False)
+            if d == "denied":
+                return "denied"
+            if d == "allowed":
+                decision = "allowed"
+        return decision
+
+    @staticmethod
+    def _rule_reach(subject: EndpointSelector, dir_rules: list, subject_labels, peer_labels, ingress: bool) -> str:
+        if not subject.matches(subject_labels):
+            return "undecided"
+        for dr in dir_rules:
+            for sel in (dr.FromRequires if ingress else dr.ToRequires):
+                if not sel.matches(peer_labels):
+                    return "denied"
+        for dr in dir_rules:
+            for sel in (dr.source_selectors() if ingress else dr.destination_selectors()):
+                if sel.matches(peer_labels) and not dr.ToPorts:
+                    return "allowed"
+        return "undecided"
+
+    def allows_ingress_label_access(self, from_labels, to_labels) -> bool:
+        """AllowsIngressLabelAccess (:111-127)."""
+        return bool(self.rules) and self.can_reach_ingress(from_labels, to_labels) == "allowed"
+
+    def allows_egress_label_access(self, from_labels, to_labels) -> bool:
+        """AllowsEgressLabelAccess."""
+        return bool(self.rules) and self.can_reach_egress(from_labels, to_labels) == "allowed"
+
+    def resolve_l4_ingress_policy(self, to_labels) -> dict:
+        """ResolveL4IngressPolicy (:245-281): FromRequires of every rule
+        selecting to_labels constrain every FromEndpoints selector; rules are
+        merged in order; then wildcardL3L4Rules."""
+        reqs: tuple = ()
+        for r in self.rules:
+            if r.EndpointSelector.matches(to_labels):
+                for ing in r.Ingress:
+                    for sel in ing.FromRequires:
+                        reqs += requirements_of(sel)
+        result = L4Policy()
+        for r in self.rules:
+            resolve_rule_l4_ingress(r, to_labels, reqs, result, self.cfg)
+        self._wildcard_l3l4_rules(to_labels, True, result.Ingress)
+        return result.Ingress
+
+    def resolve_l4_egress_policy(self, from_labels) -> dict:
+        """ResolveL4EgressPolicy (:289-330)."""
+        reqs: tuple = ()
+        for r in self.rules:
+            if r.EndpointSelector.matches(from_labels):
+                for eg in r.Egress:
+                    for sel in eg.ToRequires:
+                        reqs += requirements_of(sel)
+        result = L4Policy()
+        for r in self.rules:
+            resolve_rule_l4_egress(r, from_labels, reqs, result)
+        self._wildcard_l3l4_rules(from_labels, False, result.Egress)
+        return result.Egress
+
+    def _wildcard_l3l4_rules(self, labels, ingress: bool, l4map: dict) -> None:
+        """wildcardL3L4Rules (:170-243)."""
+        for r in self.rules:
+            if not r.EndpointSelector.matches(labels):
+                continue
+            for dr in (r.Ingress if ingress else r.Egress):
+                if not dr.is_label_based():
+                    continue
+                peers = dr.source_selectors() if ingress else dr.destination_selectors()
+                if not dr.ToPorts:
+                    wildcard_l3l4_rule("TCP", 0, peers, r.Labels, l4map)
+                    wildcard_l3l4_rule("UDP", 0, peers, r.Labels, l4map)
+                else:
+                    for tp in dr.ToPorts:
+                        if _rules_empty(tp.Rules):
+                            for pp in tp.Ports:
+                                wildcard_l3l4_rule(pp.Protocol, parse_port(pp.Port), peers, r.Labels, l4map)
+
+
+def endpoint_policy_map_state(repo: Repository, labels, identity_cache: Mapping[int, Mapping[str, str]],
+                              redirect_ports: Optional[Mapping[tuple, int]] = None) -> dict[PolicyKey, int]:
+    """One endpoint's desired policy map state, as regeneratePolicy computes
+    it (pkg/endpoint/policy.go:482-560): ComputePolicyEnforcement
+    (GetRulesMatching, default enforcement mode), resolveL4Policy for the
+    enforced directions, then computeDesiredPolicyMapState — L4 entries,
+    localhost, world, and L3 entries for every identity (an unenforced
+    direction allows every identity)."""
+    ing_on, eg_on = repo.get_rules_matching(labels)
+    l4 = L4Policy(Ingress=repo.resolve_l4_ingress_policy(labels) if ing_on else {},
+                  Egress=repo.resolve_l4_egress_policy(labels) if eg_on else {})
+    desired = compute_desired_l4_policymap_entries(l4, identity_cache, redirect_ports or {})
+    determine_allow_localhost(desired, l4, repo.cfg.always_allow_localhost)
+    determine_allow_from_world(desired, repo.cfg.host_allows_world)
+    for ident, peer in identity_cache.items():
+        if not ing_on or repo.allows_ingress_label_access(peer, labels):
+            desired[PolicyKey(int(ident), 0, 0, int(TrafficDirection.Ingress))] = 0
+        if not eg_on or repo.allows_egress_label_access(labels, peer):
+            desired[PolicyKey(int(ident), 0, 0, int(TrafficDirection.Egress))] = 0
+    return desired
 
 
 __all__ = [n for n in dir() if not n.startswith("_")] + ["PortRuleHTTP"]

@@ -479,11 +479,186 @@ def cassandra_kats() -> dict:
             "cases": out}
 
 
+# ------------------------------------------------------ L4 merge (a9) ----
+_SRC_MERGE = "pkg/policy/l4Filter_test.go"
+_WC = {}                                   # api.WildcardEndpointSelector
+_A = {"matchLabels": {"id": "a"}}          # endpointSelectorA (:26-29)
+_C = {"matchLabels": {"id": "c"}}          # endpointSelectorC
+_HOST = {"matchLabels": {"reserved:host": ""}}  # ReservedEndpointSelectors[host]
+_GET = {"method": "GET", "path": "/"}
+
+
+def _ing(frm, port="80", rules=None):
+    pr = {"ports": [{"port": port, "protocol": "TCP"}]}
+    if rules is not None:
+        pr["rules"] = rules
+    r = {"toPorts": [pr]}
+    if frm is not None:
+        r["fromEndpoints"] = frm
+    return r
+
+
+def _flt(port, endpoints, parser, l7, derived, ingress=True):
+    return {"port": port, "protocol": "TCP", "u8proto": 6, "endpoints": endpoints, "parser": parser,
+            "l7": l7, "ingress": ingress, "derived": derived}
+
+
+def l4_merge_kats() -> dict:
+    """The 12-case merge table of l4Filter_test.go:40-66 (and its sub-cases)
+    as data: rules in the api.Rule JSON form, the context, the level the
+    test resolves at ("rule": rule.resolveL4IngressPolicy, no wildcard
+    step; "repo": Repository.ResolveL4IngressPolicy), and the asserted
+    outcome — the full expected L4Filter where the test DeepEquals one,
+    the asserted fields where it checks fields, an error, or nil."""
+    http = lambda *rs: {"http": list(rs)}  # noqa: E731
+    kafka = {"kafka": [{"topic": "foo"}]}
+    sel_a = {"matchLabels": {"id": "a"}}
+    cases = [
+        {"case": "1A", "src": f"{_SRC_MERGE}:75-115", "level": "repo", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC]), _ing([_WC])]}],
+         "check": {"80/TCP": {"port": 80, "ingress": True, "selects_all": True, "parser": "", "l7_len": 0}}},
+        {"case": "1B", "src": f"{_SRC_MERGE}:117-158", "level": "repo", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([]), _ing([])]}],
+         "check": {"80/TCP": {"port": 80, "ingress": True, "selects_all": True, "parser": "", "l7_len": 0}}},
+        {"case": "2A", "src": f"{_SRC_MERGE}:164-227", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC]), _ing([_WC], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _WC, "http": [_GET]}], 2)}},
+        {"case": "2B", "src": f"{_SRC_MERGE}:229-276", "level": "repo", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=http(_GET)), _ing([_WC])]}],
+         "check": {"80/TCP": {"port": 80, "ingress": True, "selects_all": True, "parser": "http", "l7_len": 1}}},
+        {"case": "3", "src": f"{_SRC_MERGE}:278-349", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=http(_GET)),
+                                                          _ing([_WC], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _WC, "http": [_GET]}], 2)}, "foo_nil": True},
+        {"case": "4", "src": f"{_SRC_MERGE}:351-423", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], "9092", kafka), _ing([_WC], "9092", kafka)]}],
+         "expect": {"9092/TCP": _flt(9092, [_WC], "kafka", [{"sel": _WC, "kafka": [{"topic": "foo"}]}], 2)},
+         "foo_nil": True},
+        {"case": "5A", "src": f"{_SRC_MERGE}:429-471", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=kafka), _ing([_WC], rules=http(_GET))]}],
+         "error": True},
+        {"case": "5B", "src": f"{_SRC_MERGE}:473-515", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=http(_GET)), _ing([_WC], rules=kafka)]}],
+         "error": True},
+        {"case": "5B+", "src": f"{_SRC_MERGE}:517-563", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [
+             _ing([_WC], rules=http(_GET)),
+             _ing([_WC], rules={"l7proto": "testing", "l7": [{"method": "PUT", "path": "/Foo"}]})]}],
+         "error": True},
+        {"case": "5B++", "src": f"{_SRC_MERGE}:565-610", "level": "rule", "dir": "egress", "from": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "egress": [
+             {"toEndpoints": [_C], "toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}],
+                                                "rules": {"l7proto": "testing"}}]},
+             {"toEndpoints": [_C], "toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}], "rules": http(_GET)}]}]}],
+         "error": True},
+        {"case": "6A", "src": f"{_SRC_MERGE}:616-670", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_A]), _ing([_WC])]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "", [], 2)}, "foo_nil": True},
+        {"case": "6B", "src": f"{_SRC_MERGE}:672-727", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC]), _ing([_A])]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "", [], 2)}, "foo_nil": True},
+        {"case": "7A", "src": f"{_SRC_MERGE}:733-799", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_A], rules=http(_GET)), _ing([_WC])]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _A, "http": [_GET]}], 2)}, "foo_nil": True},
+        {"case": "7B", "src": f"{_SRC_MERGE}:801-867", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC]), _ing([_A], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _A, "http": [_GET]}], 2)}, "foo_nil": True},
+        {"case": "8A", "src": f"{_SRC_MERGE}:875-949", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_A], rules=http(_GET)), _ing([_WC], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _WC, "http": [_GET]}, {"sel": _A, "http": [_GET]}], 2)},
+         "foo_nil": True},
+        {"case": "8B", "src": f"{_SRC_MERGE}:951-1026", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=http(_GET)), _ing([_A], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _WC, "http": [_GET]}, {"sel": _A, "http": [_GET]}], 2)},
+         "foo_nil": True},
+        {"case": "9A", "src": f"{_SRC_MERGE}:1033-1082", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_A], rules=kafka), _ing([_WC], rules=http(_GET))]}],
+         "error": True, "foo_nil": True},
+        {"case": "9B", "src": f"{_SRC_MERGE}:1084-1134", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=http(_GET)), _ing([_A], rules=kafka)]}],
+         "error": True, "foo_nil": True},
+        {"case": "10", "src": f"{_SRC_MERGE}:1136-1216", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_A], rules=http(_GET)), _ing([_C], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_A, _C], "http", [{"sel": _C, "http": [_GET]}, {"sel": _A, "http": [_GET]}], 2)},
+         "foo_nil": True},
+        {"case": "11", "src": f"{_SRC_MERGE}:1218-1280", "level": "rule", "to": {"id": "a"},
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_A]), _ing([_C])]}],
+         "expect": {"80/TCP": _flt(80, [_A, _C], "", [], 2)}, "foo_nil": True},
+        {"case": "12", "src": f"{_SRC_MERGE}:1282-1357", "level": "rule", "to": {"id": "a"}, "allow_localhost": True,
+         "rules": [{"endpointSelector": sel_a, "ingress": [_ing([_WC], rules=http(_GET))]}],
+         "expect": {"80/TCP": _flt(80, [_WC], "http", [{"sel": _WC, "http": [_GET]}, {"sel": _HOST, "empty": True}], 1)},
+         "foo_nil": True},
+    ]
+    # L7 outcomes the table's Notes column states (:46-66), resolved at the
+    # repository level (wildcardL3L4Rules included) and sent through NPDS:
+    # per source identity {id=a, id=c, id=b, host}, GET / and POST /
+    notes = {
+        "2B": {"note": "Rule 1 shadows rule 2", "allow": {"a": [1, 1], "c": [1, 1], "b": [1, 1]}},
+        "3": {"note": "Exactly duplicate rules (HTTP)", "allow": {"a": [1, 0], "c": [1, 0], "b": [1, 0]}},
+        "7A": {"note": "All traffic is allowed; traffic to A goes via proxy", "allow": {"a": [1, 1], "c": [1, 1], "b": [1, 1]}},
+        "7B": {"note": "Same as 7A, but import in reverse order", "allow": {"a": [1, 1], "c": [1, 1], "b": [1, 1]}},
+        "8A": {"note": "Rule 2 is the same as rule 1, except matching all L3", "allow": {"a": [1, 0], "c": [1, 0], "b": [1, 0]}},
+        "8B": {"note": "Same as 8A, but import in reverse order", "allow": {"a": [1, 0], "c": [1, 0], "b": [1, 0]}},
+        "10": {"note": "Allow at L7 for two distinct labels (disjoint set)", "allow": {"a": [1, 0], "c": [1, 0], "b": [0, 0]}},
+        "12": {"note": "Configure to allow localhost traffic always", "allow": {"a": [1, 0], "c": [1, 0], "b": [1, 0], "host": [1, 1]}},
+    }
+    for c in cases:
+        if c["case"] in notes:
+            c["l7_outcome"] = notes[c["case"]]
+    return {"generator": "tests/golden/make_golden.py l4_merge_kats()", "source": f"{_SRC_MERGE}:40-66", "cases": cases}
+
+
+def _manifest(name: str) -> list:
+    with open(os.path.join(REF, "test/runtime/manifests", name)) as f:
+        return json.load(f)
+
+
+REF = "/root/reference"
+
+
+def policies_e2e_kats() -> dict:
+    """test/runtime/Policies.go:380-443 ("L3/L4 Checks", "L4Policy Checks"):
+    the two policy files the tests import (test/runtime/manifests/
+    Policies-l3-policy.json, Policies-l4-policy.json, copied as data) and
+    every connectivity assertion.  Containers carry the label id.<name>
+    (test/helpers/cons.go); `ping` is ICMP, `http` a TCP connection to port
+    80 (Policies.go:317-345).  allRequests / httpRequestsPublic /
+    pingRequests are expanded to their IPv4 members (the policy map is
+    family-agnostic)."""
+    l3 = [
+        ("app1", "httpd1", "all", True), ("app2", "httpd1", "http", False),
+        ("app1", "httpd2", "http", True), ("app2", "httpd2", "http", False),
+        ("app3", "httpd2", "http", True), ("app3", "httpd2", "ping", False),
+        ("app3", "httpd3", "all", False), ("app2", "httpd3", "all", True),
+        ("app2", "httpd2", "all", False),
+    ]
+    l4 = []
+    for app in ("app1", "app2"):
+        l4 += [(app, "httpd1", "ping", False), (app, "httpd1", "http", True), (app, "httpd2", "ping", False),
+               (app, "httpd2", "http", True)]
+    l4 += [("app3", "httpd1", "all", False), ("app1", "httpd3", "ping", False)]
+    none = [("app1", "httpd1", "all", True), ("app2", "httpd1", "all", True), ("app2", "httpd2", "all", True)]
+    return {"generator": "tests/golden/make_golden.py policies_e2e_kats()",
+            "containers": ["app1", "app2", "app3", "httpd1", "httpd2", "httpd3"],
+            "suites": [
+                {"name": "L3/L4 Checks", "src": "test/runtime/Policies.go:380-413",
+                 "policy": _manifest("Policies-l3-policy.json"), "asserts": l3},
+                {"name": "L4Policy Checks", "src": "test/runtime/Policies.go:416-434",
+                 "policy": _manifest("Policies-l4-policy.json"), "asserts": l4},
+                {"name": "policies deleted", "src": "test/runtime/Policies.go:407-413,436-443",
+                 "policy": [], "asserts": none},
+            ]}
+
+
 def main():
     files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
              "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
-             "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats()}
+             "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
+             "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats()}
+    only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
+        if only and name not in only:
+            continue
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(data, f, indent=1, sort_keys=False)
             f.write("\n")

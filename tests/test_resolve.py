@@ -114,7 +114,7 @@ def test_create_l4_filter_and_relevant_rules():
     rules = L7Rules(HTTP=[HTTP2])
     f = R.create_l4_ingress_filter([SEL1], [SEL2], rules, 80, "TCP")
     assert f.L7Parser == R.PARSER_HTTP and f.is_redirect() and f.Ingress
-    assert f.L7RulesPerEp[SEL1] is rules and f.L7RulesPerEp[SEL2].HTTP == []
+    assert f.L7RulesPerEp[SEL1] is rules and f.L7RulesPerEp[SEL2].is_empty()
     assert R.L7DataMap(f.L7RulesPerEp).get_relevant_rules(CACHE[1002]).HTTP == [HTTP2]
     assert R.L7DataMap(f.L7RulesPerEp).get_relevant_rules(None).HTTP == []
     # UDP: no L7 (l4.go:185); wildcard peers → [WildcardEndpointSelector]
