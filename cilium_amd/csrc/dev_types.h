@@ -243,7 +243,6 @@ struct HttpDev {
 constexpr uint32_t kRawMaxFields = 32;
 constexpr uint32_t kRawMaxHead = 61440;
 constexpr uint32_t kRawKeys = 10;  // bucket key: walked units 0..8, 9 = overflow arena
-constexpr uint32_t kRawTileGranules = 17;  // a tile's fixed stride: meta + 8 units (512-B granules)
 struct HttpRawDev {
   const uint32_t* phash_keys;  // (policy << 17 | ingress << 16 | port) → program
   const uint32_t* phash_vals;
@@ -262,12 +261,10 @@ struct HttpRawDev {
 // FNV-1a, 32 bit, over lowercase bytes
 CG_HD inline uint32_t raw_fnv(uint32_t h, uint8_t c) { return (h ^ c) * 16777619u; }
 constexpr uint32_t kRawFnvInit = 2166136261u;
-// Per group (program; then allow, deny) of a raw batch: its first tile, its
-// request count and the first local slot of each bucket key (kRawKeys + 1).
-struct HttpRawGroup {
-  uint32_t tile0, count;
-  uint32_t bstart[kRawKeys + 1];
-  uint32_t prog;
+// A run of tiles of a raw batch with the same string units: tiles
+// [t0, next run's t0), tile t at granule base + (t - t0) * (1 + 2 * units).
+struct HttpRawRun {
+  uint32_t t0, units, base, pad;
 };
 
 CG_HD inline uint32_t hash32(uint32_t x) {

@@ -1,10 +1,9 @@
 // http_raw.cc — host side of the raw HTTP/1 path (kernels_http_raw.hip):
 // the snapshot's device tables for it, and the launch sequence
-//   scan → (bucket counts to the host) → layout → tiles → emit → http_kernel
-//   → scatter
+//   scan → (bucket counts to the host) → layout → rank → build → http_kernel
 // on one stream.  The host step is the layout of a few thousand bucket
-// counts (groups, chunk table, bucket cursors); request bytes never leave the
-// device.
+// counts (chunks, runs of equal-units tiles, bucket cursors); request bytes
+// never leave the device.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -85,12 +84,37 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   if (!n) return;
   const hipStream_t st = (hipStream_t)stream;
   const uint32_t np = (uint32_t)s.progs.size(), G = np + 2, K = kRawKeys;
-  // workspace: [histogram G*K u32][overflow bytes u64][arena cursor u64]
+  // workspace: [histogram G*K u32][overflow bytes u64][arena cursor u64][head bytes u64]
   const size_t hist_bytes = ((size_t)G * K * 4 + 7) & ~(size_t)7;
-  uint8_t* small = (uint8_t*)sl.dev_buf(8, hist_bytes + 16);
+  uint8_t* small = (uint8_t*)sl.dev_buf(8, hist_bytes + 24);
   uint32_t* hist = (uint32_t*)small;
   auto* ovf = (unsigned long long*)(small + hist_bytes);
   hip_check(hipMemsetAsync(small, 0, hist_bytes + 16, st), "hipMemsetAsync");
+  // the head bytes [off[0], off[n]) size the string buffer
+  hip_check(hipMemcpyAsync(small + hist_bytes + 16, d_off + n, 8, hipMemcpyDeviceToDevice, st), "D2D");
+  hip_check(hipMemcpyAsync(small + hist_bytes + 8, d_off, 8, hipMemcpyDeviceToDevice, st), "D2D");
+  uint8_t* hh = (uint8_t*)sl.host_buf(8, hist_bytes + 24);
+  hip_check(hipMemcpyAsync(hh, small, hist_bytes + 24, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  uint64_t o0, o1;
+  memcpy(&o0, hh + hist_bytes + 8, 8);
+  memcpy(&o1, hh + hist_bytes + 16, 8);
+  if (o1 < o0) fail(CG_INVALID_ARGUMENT, "raw_off must be non-decreasing");
+  hip_check(hipMemsetAsync(small + hist_bytes + 8, 0, 8, st), "hipMemsetAsync");  // the arena cursor
+  // string buffer: request i's record (16-byte header + uncoded string) at
+  // align16(off[i] - off[0]) + cst * i (kernels_http_raw.hip rec_off); the
+  // build pass addresses records in 16-byte units through u32 order words
+  const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 32 + 15) & ~(size_t)15);
+  const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * n + 16;
+  if (sbytes / 16 >= (1ull << 32)) {
+    if (n < 2) fail(CG_INVALID_ARGUMENT, "raw head too large");
+    const size_t h = n / 2;
+    http_verdicts_raw_on(s, sl, cus, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
+    http_verdicts_raw_on(s, sl, cus, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
+                         d_out + h, stream);
+    return;
+  }
+  uint8_t* sbuf = (uint8_t*)sl.dev_buf(15, sbytes);
   void* rinfo = sl.dev_buf(9, n * 8);
   // per-block bucket counts → per-block slot offsets (when the bucket
   // counters fit the kernels' LDS), else one global histogram
@@ -98,13 +122,11 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   const uint32_t nblk = (uint32_t)http_raw_grid(n, cus);
   uint32_t* bcount = lds_keys ? (uint32_t*)sl.dev_buf(16, (size_t)G * K * nblk * 4) : hist;
   uint32_t* bbase = lds_keys ? (uint32_t*)sl.dev_buf(17, (size_t)G * K * nblk * 4) : nullptr;
-  auto* spans = (uint32_t*)sl.dev_buf(18, (size_t)std::max(s.raw.nfields, 1u) * n * 4);
-  hip_check(launch_http_raw_scan(s.raw, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, spans, ovf, st,
-                                 cus),
+  hip_check(launch_http_raw_scan(s.raw, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, d_remote, sbuf,
+                                 cst, ovf, st, cus),
             "raw scan kernel launch");
   if (lds_keys)
     hip_check(launch_http_raw_prefix(bcount, G * K, nblk, bbase, hist, st), "raw prefix kernel launch");
-  uint8_t* hh = (uint8_t*)sl.host_buf(8, hist_bytes + 16);
   hip_check(hipMemcpyAsync(hh, small, hist_bytes + 8, hipMemcpyDeviceToHost, st), "D2H");
   hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   const uint32_t* hc = (const uint32_t*)hh;
@@ -122,28 +144,45 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
     return;
   }
   // ---- layout: groups in program order (then allow, deny), 64-slot tiles,
-  // chunks of <= kChunkTiles tiles, a cursor per (group, bucket)
-  std::vector<HttpRawGroup> groups;
+  // chunks of <= kChunkTiles tiles, runs of tiles with equal string units
+  // (a tile's units: the bucket key of its last walked slot; keys ascend
+  // within a group, overflow-arena slots last), a cursor per (group, key)
   std::vector<HttpChunk> chunks;
+  std::vector<HttpRawRun> runs;
   std::vector<uint32_t> cursors((size_t)G * K, 0);
-  uint32_t tiles = 0;
+  uint32_t tiles = 0, gran = 0;
+  auto add_run = [&](uint32_t t0, uint32_t t1, uint32_t units) {
+    if (t1 <= t0) return;
+    runs.push_back({t0, units, gran, 0});
+    gran += (t1 - t0) * (1 + 2 * units);
+  };
   for (uint32_t g = 0; g < G; ++g) {
-    HttpRawGroup gr{};
-    uint32_t cnt = 0;
+    uint32_t bstart[kRawKeys + 1], cnt = 0;
     for (uint32_t k = 0; k < K; ++k) {
-      gr.bstart[k] = cnt;
+      bstart[k] = cnt;
       cnt += hc[(size_t)g * K + k];
     }
-    gr.bstart[K] = cnt;
+    bstart[K] = cnt;
     if (!cnt) continue;
-    gr.tile0 = tiles;
-    gr.count = cnt;
-    gr.prog = g < np ? g : g == np ? kProgAllow : kProgDeny;
-    for (uint32_t k = 0; k < K; ++k) cursors[(size_t)g * K + k] = tiles * CG_HTTP_TILE + gr.bstart[k];
-    const uint32_t t = (cnt + CG_HTTP_TILE - 1) / CG_HTTP_TILE;
-    for (uint32_t k = 0; k < t; k += kChunkTiles) chunks.push_back({gr.prog, tiles + k, std::min(kChunkTiles, t - k), 0});
-    tiles += t;
-    groups.push_back(gr);
+    const uint32_t prog = g < np ? g : g == np ? kProgAllow : kProgDeny;
+    for (uint32_t k = 0; k < K; ++k) cursors[(size_t)g * K + k] = tiles * CG_HTTP_TILE + bstart[k];
+    const uint32_t T = (cnt + CG_HTTP_TILE - 1) / CG_HTTP_TILE;
+    for (uint32_t k = 0; k < T; k += kChunkTiles) chunks.push_back({prog, tiles + k, std::min(kChunkTiles, T - k), 0});
+    // tiles j with a walked slot: units = key of slot min(64j + 63, e - 1)
+    const uint32_t e = bstart[K - 1];
+    uint32_t j = 0;
+    while ((uint64_t)64 * j < e) {
+      const uint32_t last = std::min(64 * j + 63, e - 1);
+      uint32_t u = 0;
+      for (uint32_t k = 0; k + 1 < K; ++k)
+        if (bstart[k] <= last && last < bstart[k + 1]) u = k;
+      const uint32_t next = bstart[u + 1];  // first slot of a larger key (or e)
+      const uint32_t jend = next >= e ? (e + 63) / 64 : next / 64;
+      add_run(tiles + j, tiles + jend, u);
+      j = jend;
+    }
+    add_run(tiles + j, tiles + T, 0);  // only overflow-arena slots
+    tiles += T;
   }
   const size_t nslots = (size_t)tiles * CG_HTTP_TILE;
   HttpBatchHeader hdr{};
@@ -154,34 +193,33 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   hdr.nslots = nslots;
   hdr.ttab_off = sizeof(HttpBatchHeader) + sizeof(HttpChunk) * chunks.size();
   hdr.tiles_off = (hdr.ttab_off + sizeof(HttpTile) * tiles + 1023) & ~(uint64_t)1023;
-  hdr.total_bytes = hdr.tiles_off + (uint64_t)tiles * kRawTileGranules * 512;
+  hdr.total_bytes = hdr.tiles_off + (uint64_t)gran * 512;
   hdr.arena_bytes = ovf_bytes;
   uint8_t* batch = (uint8_t*)sl.dev_buf(10, hdr.total_bytes);
   const size_t head = hdr.ttab_off;
-  uint8_t* hb = (uint8_t*)sl.host_buf(9, head + groups.size() * sizeof(HttpRawGroup) + cursors.size() * 4);
+  uint8_t* hb = (uint8_t*)sl.host_buf(9, head + runs.size() * sizeof(HttpRawRun) + cursors.size() * 4);
   memcpy(hb, &hdr, sizeof(hdr));
   memcpy(hb + sizeof(hdr), chunks.data(), chunks.size() * sizeof(HttpChunk));
-  uint8_t* hg = hb + head;
-  memcpy(hg, groups.data(), groups.size() * sizeof(HttpRawGroup));
-  uint8_t* hcur = hg + groups.size() * sizeof(HttpRawGroup);
+  uint8_t* hr = hb + head;
+  memcpy(hr, runs.data(), runs.size() * sizeof(HttpRawRun));
+  uint8_t* hcur = hr + runs.size() * sizeof(HttpRawRun);
   memcpy(hcur, cursors.data(), cursors.size() * 4);
-  auto* d_groups = (HttpRawGroup*)sl.dev_buf(11, std::max<size_t>(groups.size(), 1) * sizeof(HttpRawGroup));
+  auto* d_runs = (HttpRawRun*)sl.dev_buf(11, std::max<size_t>(runs.size(), 1) * sizeof(HttpRawRun));
   auto* d_cursor = (uint32_t*)sl.dev_buf(12, cursors.size() * 4);
   hip_check(hipMemcpyAsync(batch, hb, head, hipMemcpyHostToDevice, st), "H2D");
-  hip_check(hipMemcpyAsync(d_groups, hg, groups.size() * sizeof(HttpRawGroup), hipMemcpyHostToDevice, st), "H2D");
+  hip_check(hipMemcpyAsync(d_runs, hr, runs.size() * sizeof(HttpRawRun), hipMemcpyHostToDevice, st), "H2D");
   hip_check(hipMemcpyAsync(d_cursor, hcur, cursors.size() * 4, hipMemcpyHostToDevice, st), "H2D");
   uint8_t* arena = (uint8_t*)sl.dev_buf(13, std::max<unsigned long long>(ovf_bytes, 16));
   auto* order = (uint32_t*)sl.dev_buf(14, nslots * 4);
-  uint8_t* vslot = (uint8_t*)sl.dev_buf(15, nslots);
+  hip_check(hipMemsetAsync(order, 0xFF, nslots * 4, st), "hipMemsetAsync");  // padding slots
   auto* ttab = (HttpTile*)(batch + hdr.ttab_off);
   uint8_t* tdata = batch + hdr.tiles_off;
-  hip_check(launch_http_raw_tiles(d_groups, (uint32_t)groups.size(), tiles, ttab, tdata, order, st),
-            "raw tiles kernel launch");
-  hip_check(launch_http_raw_emit(s.raw, d_raw, d_off, n, d_ingress, d_remote, rinfo, d_cursor, bbase, ttab, tdata,
-                                 order, arena, ovf + 1, spans, st, cus),
-            "raw emit kernel launch");
-  hip_check(launch_http(s.dev, batch, nslots, arena, vslot, st, cus), "http kernel launch");
-  hip_check(launch_http_raw_scatter(order, vslot, nslots, d_out, st, cus), "raw scatter kernel launch");
+  hip_check(launch_http_raw_rank(s.raw, n, d_off, cst, rinfo, d_cursor, bbase, order, st, cus),
+            "raw rank kernel launch");
+  hip_check(launch_http_raw_build(s.raw, d_runs, (uint32_t)runs.size(), tiles, ttab, tdata, order, sbuf, arena,
+                                  ovf + 1, st, cus),
+            "raw build kernel launch");
+  hip_check(launch_http(s.dev, batch, nslots, arena, d_out, st, cus, order), "http kernel launch");
   // the workspace belongs to the lease: done before it is handed back
   hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
 }

@@ -18,8 +18,10 @@ int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, int family, const v
                       size_t n, int32_t* out, uint32_t mode, void* stream, int cus);
 int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* v4, size_t n4,
                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus);
+// order (optional): out[order[slot]] instead of out[slot] (request order;
+// order 0xFFFFFFFF = padding, no write) — the raw-request batches.
 int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
-                void* stream, int cus);
+                void* stream, int cus, const uint32_t* order = nullptr);
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus);
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
@@ -33,26 +35,25 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
                         int cus);
 
 // Raw HTTP/1 heads → batch (kernels_http_raw.hip; sequence in http_raw.cc).
-// The scan and emit kernels run http_raw_grid(n, cus) blocks.  With
-// http_raw_lds_keys(R) the scan writes per-block bucket counts
-// (counts[key * grid + block]) and raw_prefix turns them into per-block slot
-// offsets (bbase) and totals (hist); otherwise the scan adds into a global
-// histogram (counts = hist) and the emit takes slots from global cursors.
-// spans: nfields × n u32 (field-major), the scan's value spans for the emit.
+// The scan and rank kernels run http_raw_grid(n, cus) blocks over the
+// requests in the same order.  With http_raw_lds_keys(R) the scan writes
+// per-block bucket counts (counts[key * grid + block]) and raw_prefix turns
+// them into per-block slot offsets (bbase) and totals (hist); otherwise the
+// scan adds into a global histogram (counts = hist) and the rank takes slots
+// from global cursors.  sbuf: the request-ordered string buffer
+// (records per request, http_raw.cc), cst its per-request stride.
 size_t http_raw_grid(size_t n, int cus);
 bool http_raw_lds_keys(const HttpRawDev& R);
 int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
-                         void* rinfo, uint32_t* spans, unsigned long long* ovf_bytes, void* stream, int cus);
+                         void* rinfo, const uint32_t* remote, uint8_t* sbuf, uint32_t cst,
+                         unsigned long long* ovf_bytes, void* stream, int cus);
 int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk, uint32_t* bbase, uint32_t* hist,
                            void* stream);
-int launch_http_raw_tiles(const HttpRawGroup* groups, uint32_t ngroups, uint32_t ntiles, HttpTile* ttab,
-                          uint8_t* tiles, uint32_t* order, void* stream);
-int launch_http_raw_emit(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
-                         const uint8_t* ingress, const uint32_t* remote, const void* rinfo, uint32_t* cursor,
-                         const uint32_t* bbase, HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
-                         unsigned long long* arena_cursor, const uint32_t* spans, void* stream, int cus);
-int launch_http_raw_scatter(const uint32_t* order, const uint8_t* vslot, size_t nslots, uint8_t* out, void* stream,
-                            int cus);
+int launch_http_raw_rank(const HttpRawDev& R, size_t n, const uint64_t* off, uint32_t cst, const void* rinfo,
+                         uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream, int cus);
+int launch_http_raw_build(const HttpRawDev& R, const HttpRawRun* runs, uint32_t nruns, uint32_t ntiles,
+                          HttpTile* ttab, uint8_t* tiles, uint32_t* order, const uint8_t* sbuf, uint8_t* arena,
+                          unsigned long long* arena_cursor, void* stream, int cus);
 
 }  // namespace cg

@@ -118,6 +118,22 @@ __device__ __forceinline__ uint32_t lds_cls_step16(uint32_t dead, uint32_t st, c
   return lds_cls_step<I & 3>(dead, st, w);
 }
 
+// Where verdicts go: out[slot] (slot order), or — for a batch built on the
+// device from raw requests (kernels_http_raw.hip) — out[order[slot]]
+// (request order; padding slots, order 0xFFFFFFFF, write nothing).
+struct VOut {
+  uint8_t* __restrict__ out;
+  const uint32_t* __restrict__ order;
+  __device__ __forceinline__ void put(size_t slot, uint32_t v) const {
+    if (order) {
+      const uint32_t r = order[slot];
+      if (r != 0xFFFFFFFFu) out[r] = (uint8_t)v;
+    } else {
+      out[slot] = (uint8_t)v;
+    }
+  }
+};
+
 // Accept label of state st (its header cell).
 template <bool kCls>
 __device__ __forceinline__ uint32_t state_label(const uint32_t* __restrict__ cells, uint32_t st) {
@@ -286,7 +302,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
                                            const uint8_t* __restrict__ tiles, const HttpTile* __restrict__ ttab,
                                            const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
-                                           uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
+                                           uint64_t arena_bytes, VOut out, uint32_t lane, uint32_t& n_allow,
                                            uint32_t& n_deny, uint32_t* s_hits) {
   TileRef tr[K];
   uint2 meta[K];
@@ -375,7 +391,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     if (counted[j] && (pg.flags & kProgHasAlways)) hit[j] = min(hit[j], first_meet(blk, pg.always_off, row[j], W));
     const bool verdict = counted[j] && hit[j] != kNoHit;
     count_hits(T, pg, verdict ? hit[j] : kNoHit, s_hits, lane);
-    if (valid[j]) out[(size_t)tile[j] * kWave + lane] = (uint8_t)verdict;
+    if (valid[j]) out.put((size_t)tile[j] * kWave + lane, verdict);
     n_allow += counted[j] && verdict;
     n_deny += counted[j] && !verdict;
   }
@@ -415,7 +431,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
                                             uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
                                             const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
                                             uint32_t tail, TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
-                                            uint64_t arena_bytes, uint8_t* __restrict__ out, uint32_t lane,
+                                            uint64_t arena_bytes, VOut out, uint32_t lane,
                                             uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits) {
   const uint2 meta = cur.meta;
   // a rolling window of kWin units: unit k + kWin loads when unit k starts
@@ -487,7 +503,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   }
   const bool verdict = hit != kNoHit;
   count_hits(T, pg, hit, s_hits, lane);
-  out[(size_t)t * kWave + lane] = (uint8_t)verdict;
+  out.put((size_t)t * kWave + lane, verdict);
   n_allow += counted && verdict;
   n_deny += counted && !verdict;
 }
@@ -499,7 +515,7 @@ __device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg&
                                                const uint32_t* __restrict__ lcells, const uint8_t* __restrict__ tiles,
                                                const HttpTile* __restrict__ ttab, uint32_t t, uint32_t tend,
                                                uint32_t nw, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                               uint8_t* __restrict__ out, uint32_t lane, uint32_t& n_allow,
+                                               VOut out, uint32_t lane, uint32_t& n_allow,
                                                uint32_t& n_deny, uint32_t* s_hits) {
   if (t >= tend) return;
   HttpTile tt = ttab[t];
@@ -573,7 +589,7 @@ __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, ui
 // so the rare path does not set the common one's register budget.
 template <bool kGlobal>
 __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
-                                            const uint8_t* __restrict__ arena, uint8_t* __restrict__ out,
+                                            const uint8_t* __restrict__ arena, VOut out,
                                             uint32_t* lcells, uint32_t* s_cnt, uint32_t* s_hits,
                                             uint32_t* __restrict__ deal) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
@@ -583,7 +599,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
     // packed against another snapshot (or not a batch): deny every slot
     if (kGlobal) return;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (size_t)gridDim.x * blockDim.x)
-      out[i] = 0;
+      out.put(i, 0);
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&T.counters[2 * T.nprogs], 1ULL);
     return;
   }
@@ -638,7 +654,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         // without HTTP rules → allow (cilium_network_policy.h:129-138,187-191)
         const uint32_t flags = tile_ref(tiles, ttab[t]).meta[lane].y >> 24;
         const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
-        out[(size_t)t * kWave + lane] = (uint8_t)(counted && (prog == kProgAllow || real) ? 1u : 0u);
+        out.put((size_t)t * kWave + lane, counted && (prog == kProgAllow || real) ? 1u : 0u);
         n_allow += real && counted;
       }
     } else if (kGlobal) {
@@ -687,7 +703,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
 
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
-    uint8_t* __restrict__ out, uint32_t* __restrict__ deal) {
+    uint8_t* __restrict__ out, const uint32_t* __restrict__ order, uint32_t* __restrict__ deal) {
   // dynamic LDS only, so the program block starts at LDS address 0 (a
   // class-mode step's address is then just state + code): [block:
   // T.lds_cells][rule hits: kLdsRuleHits][allowed, denied, deal ticket]
@@ -697,22 +713,23 @@ __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8,
   for (uint32_t i = threadIdx.x; i < kLdsRuleHits; i += blockDim.x) s_hits[i] = 0;
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<false>(T, batch, nslots, arena, out, lcells, s_cnt, s_hits, deal);
+  http_chunks<false>(T, batch, nslots, arena, VOut{out, order}, lcells, s_cnt, s_hits, deal);
 }
 
 __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
                                                                    size_t nslots, const uint8_t* __restrict__ arena,
-                                                                   uint8_t* __restrict__ out) {
+                                                                   uint8_t* __restrict__ out,
+                                                                   const uint32_t* __restrict__ order) {
   __shared__ uint32_t s_cnt[3];
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<true>(T, batch, nslots, arena, out, nullptr, s_cnt, nullptr, nullptr);
+  http_chunks<true>(T, batch, nslots, arena, VOut{out, order}, nullptr, s_cnt, nullptr, nullptr);
 }
 
 }  // namespace
 
 int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_t* arena, uint8_t* out, void* stream,
-                int cus) {
+                int cus, const uint32_t* order) {
   if (nslots == 0) return 0;
   // hipFuncSetAttribute and the occupancy answer are per device: cached per
   // device ordinal, set once under a lock (handles on several GPUs may launch
@@ -765,11 +782,11 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   const size_t tiles = nslots / kWave;
   size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);
   hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
-                     (const uint8_t*)batch, nslots, arena, out, deal);
+                     (const uint8_t*)batch, nslots, arena, out, order, deal);
   if (t.n_global_progs) {
     grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
     hipLaunchKernelGGL(http_kernel_global, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream, t,
-                       (const uint8_t*)batch, nslots, arena, out);
+                       (const uint8_t*)batch, nslots, arena, out, order);
   }
   return (int)hipGetLastError();
 }

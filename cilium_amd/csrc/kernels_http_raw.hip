@@ -5,17 +5,22 @@
 // The steps of http_parse.cc (the codec: request line, header fields, Host →
 // :authority, rejected heads) and http_pack.cc (program lookup, the walked
 // string v_1 SEP .. v_F SEP / REST, class codes, grouping by program and
-// string units) run one lane per request:
-//   raw_scan_kernel   parse (value spans kept); program, string length, bucket key (program
-//                     group × string units) and the bucket histogram
-//   (host)            bucket counts → groups, chunks, bucket cursors
-//   raw_tiles_kernel  tile table (fixed 17-granule stride per tile, units =
-//                     the largest walked string the tile holds), padding slots
-//   raw_emit_kernel   the scan's value spans; a slot from the bucket cursor; meta, the
-//                     class-coded string units (zero padded) or an overflow
-//                     arena entry; the tile's tail bytes
-//   http_kernel       the verdicts (kernels_http.hip)
-//   raw_scatter       slot verdicts back to request order
+// string units):
+//   raw_scan_kernel   one lane per head (the wave's heads staged in LDS):
+//                     parse, program, the walked string class-coded into a
+//                     request-ordered string buffer (16-byte aligned per
+//                     request), bucket key (program group × string units)
+//                     and the per-block bucket counts
+//   (host)            bucket counts → chunks, runs of equal-units tiles,
+//                     bucket cursors
+//   raw_rank_kernel   a slot per request from its bucket cursor: order[slot]
+//   raw_build_kernel  one wave per tile: each lane's string gathered from the
+//                     string buffer and stored unit-major (whole 1 KiB lines
+//                     per unit), meta words, the tile table entry (units and
+//                     tail from the wave's longest string), overflow strings
+//                     into the arena
+//   http_kernel       the verdicts, written straight to request order
+//                     through order[] (kernels_http.hip VOut)
 // Slots within a bucket come in atomic order: the verdicts are per request,
 // so they do not depend on it.
 #include <hip/hip_runtime.h>
@@ -335,15 +340,84 @@ __device__ __forceinline__ HeadReader head_of(const uint8_t* __restrict__ raw, c
   return HeadReader(raw + a, n, in ? stage + (ga - sbase) : nullptr);
 }
 
-// ---- pass 1: program, string length, bucket key; per-block bucket counts
-// (bcount[key * gridDim.x + block], lds_keys) or a global histogram
+// 16-byte chunks of a lane's output string: stored to dst, then dst +=
+// stride (uint4 units: a tile's next string unit, or the next arena line).
+struct Out16 {
+  uint32_t w0, w1, w2, w3;
+  uint32_t pos, stored;
+  uint4* dst;
+  uint32_t stride;
+  __device__ __forceinline__ Out16(uint4* d, uint32_t s) : w0(0), w1(0), w2(0), w3(0), pos(0), stored(0), dst(d), stride(s) {}
+  // nb (1..4) bytes, little-endian in v (its bytes past nb zero), at byte
+  // pos: one 64-bit shift spreads them over dword pos / 4 and the next; the
+  // part past the 16 bytes starts the next chunk
+  __device__ __forceinline__ void put4(uint32_t v, uint32_t nb) {
+    const uint64_t t = (uint64_t)v << ((pos & 3) * 8);
+    const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32), q = pos >> 2;
+    w0 |= lo & (0u - (q == 0));
+    w1 |= (lo & (0u - (q == 1))) | (hi & (0u - (q == 0)));
+    w2 |= (lo & (0u - (q == 2))) | (hi & (0u - (q == 1)));
+    w3 |= (lo & (0u - (q == 3))) | (hi & (0u - (q == 2)));
+    pos += nb;
+    if (pos >= 16) {
+      const uint32_t rest = pos - 16;
+      flush();
+      w0 = hi & (0u - (q == 3));
+      pos = rest;
+    }
+  }
+  __device__ __forceinline__ void put(uint32_t b) { put4(b, 1); }
+  __device__ __forceinline__ void flush() {
+    *dst = make_uint4(w0, w1, w2, w3);
+    dst += stride;
+    w0 = w1 = w2 = w3 = 0;
+    pos = 0;
+    ++stored;
+  }
+};
+
+// The walked string, uncoded (value bytes, SEP 0x00, absent 0x01, REST 0x02
+// — the bytes the program's code map takes), into o.
+__device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr, const uint32_t* sp, uint32_t stride,
+                                            uint32_t last, Out16& o) {
+  for (uint32_t f = 0; f < last; ++f) {
+    const uint32_t s = sp[f * stride];
+    if (s == kAbsentSpan) {
+      o.put4(1u, 2);  // absent, SEP
+      continue;
+    }
+    const uint32_t a = s >> 16, L = s & 0xFFFFu;
+    for (uint32_t k = 0; k < L; k += 4) {  // a quad at a time
+      const uint32_t q = hr.quad(a + k), nb = min(L - k, 4u);
+      o.put4(nb == 4 ? q : q & ((1u << (8 * nb)) - 1), nb);
+    }
+    o.put(0u);  // SEP
+  }
+  if (last < R.nfields) o.put(2u);  // REST
+}
+
+// A request's record in the string buffer (16-byte aligned, request order):
+// a 16-byte header {request index, remote identity, string length | flags
+// << 24, program} and the uncoded walked string.  A head of h bytes yields at
+// most h + 2F bytes of string (each absent field costs 2 bytes the head does
+// not hold; the request line and the blank line hold 13 bytes no string
+// does), so with a stride of cst >= 2F + 32 bytes per request the records
+// never overlap.
+__device__ __forceinline__ uint64_t rec_off(uint64_t head_rel, size_t i, uint32_t cst) {
+  return ((head_rel + 15) & ~15ull) + (uint64_t)cst * i;
+}
+
+// ---- pass 1: parse, program, string length, bucket key, the request's
+// record in the string buffer; per-block bucket counts (bcount[key * gridDim.x + block],
+// lds_keys) or a global histogram
 __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, const uint8_t* __restrict__ raw,
                                                                const uint64_t* __restrict__ off, size_t n,
                                                                const uint32_t* __restrict__ policy,
                                                                const uint8_t* __restrict__ ingress,
                                                                const uint16_t* __restrict__ port,
                                                                uint32_t* __restrict__ counts, uint2* __restrict__ rinfo,
-                                                               uint32_t* __restrict__ gspans,
+                                                               const uint32_t* __restrict__ remote,
+                                                               uint8_t* __restrict__ sbuf, uint32_t cst,
                                                                unsigned long long* __restrict__ ovf_bytes,
                                                                uint32_t lds_keys) {
   extern __shared__ uint32_t lds[];
@@ -354,6 +428,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   const uint32_t nk = (R.nprogs + 2) * kRawKeys;
   if (lds_keys)
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = 0;
+  const uint64_t off0 = off[0];
   __syncthreads();
   for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
     const size_t i0 = base + (size_t)wave * 64;
@@ -370,6 +445,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     wave_sync();
     if (live) {
       uint32_t key = 0, len = 0, bad = 0;
+      uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(off[i] - off0, i, cst));
       if (parse) {
         HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
         if (!parse_head(R, hr, sp, kRawThreads)) {
@@ -378,11 +454,15 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
           uint32_t last;
           len = string_len(R, sp, kRawThreads, &last);
           key = len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
-          // the value spans for the emit pass (field-major: coalesced)
-          for (uint32_t f = 0; f < R.nfields; ++f) gspans[(size_t)f * n + i] = sp[f * kRawThreads];
+          Out16 o(rec + 1, 1);
+          emit_string(R, hr, sp, kRawThreads, last, o);
+          if (o.pos) o.flush();
           if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
         }
       }
+      const uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
+                             (len > CG_HTTP_SLOT_BYTES ? CG_HTTP_F_OVERFLOW : 0u);
+      *rec = make_uint4((uint32_t)i, remote[i], len | flags << 24, prog);
       rinfo[i] = make_uint2(prog, len | bad << 31);
       const uint32_t k = group_of(R, prog) * kRawKeys + key;
       if (lds_keys) atomicAdd(&lk[k], 1u);
@@ -425,187 +505,130 @@ __global__ __launch_bounds__(256) void raw_prefix_kernel(const uint32_t* __restr
   }
 }
 
-// ---- tile table and padding slots
-__global__ __launch_bounds__(kRawThreads) void raw_tiles_kernel(const HttpRawGroup* __restrict__ groups,
-                                                                uint32_t ngroups, uint32_t ntiles,
-                                                                HttpTile* __restrict__ ttab,
-                                                                uint8_t* __restrict__ tiles,
-                                                                uint32_t* __restrict__ order) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  // the group holding tile t (groups ascending by tile0, all non-empty)
-  uint32_t lo = 0, hi = ngroups;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) / 2;
-    if (groups[mid].tile0 <= t) lo = mid;
-    else hi = mid;
-  }
-  const HttpRawGroup& g = groups[lo];
-  const uint32_t j = t - g.tile0;
-  // units: the largest walked string among the tile's slots (keys are
-  // ascending within the group; key kRawKeys-1 is the arena, walked 0)
-  const uint32_t e = g.bstart[kRawKeys - 1];
-  uint32_t units = 0;
-  if (64 * j < e) {
-    const uint32_t s_last = min(64 * j + 63, e - 1);
-    for (uint32_t k = 0; k + 1 < kRawKeys; ++k)
-      if (g.bstart[k] <= s_last && s_last < g.bstart[k + 1]) units = k;
-  }
-  ttab[t].at = t * kRawTileGranules;
-  ttab[t].units = units;
-  // padding slots after the group's requests
-  uint2* meta = reinterpret_cast<uint2*>(tiles + (size_t)t * kRawTileGranules * 512);
-  for (uint32_t l = 0; l < 64; ++l)
-    if (64 * j + l >= g.count) {
-      meta[l] = make_uint2(0, CG_HTTP_F_PAD << 24);
-      order[(size_t)t * 64 + l] = 0xFFFFFFFFu;
-    }
-}
-
-// 16-byte chunks of a lane's output string: stored to dst, then dst +=
-// stride (uint4 units: a tile's next string unit, or the next arena line).
-struct Out16 {
-  uint32_t w0, w1, w2, w3;
-  uint32_t pos, stored;
-  uint4* dst;
-  uint32_t stride;
-  __device__ __forceinline__ Out16(uint4* d, uint32_t s) : w0(0), w1(0), w2(0), w3(0), pos(0), stored(0), dst(d), stride(s) {}
-  // nb (1..4) bytes, little-endian in v (its bytes past nb zero), at byte
-  // pos: one 64-bit shift spreads them over dword pos / 4 and the next; the
-  // part past the 16 bytes starts the next chunk
-  __device__ __forceinline__ void put4(uint32_t v, uint32_t nb) {
-    const uint64_t t = (uint64_t)v << ((pos & 3) * 8);
-    const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32), q = pos >> 2;
-    w0 |= lo & (0u - (q == 0));
-    w1 |= (lo & (0u - (q == 1))) | (hi & (0u - (q == 0)));
-    w2 |= (lo & (0u - (q == 2))) | (hi & (0u - (q == 1)));
-    w3 |= (lo & (0u - (q == 3))) | (hi & (0u - (q == 2)));
-    pos += nb;
-    if (pos >= 16) {
-      const uint32_t rest = pos - 16;
-      flush();
-      w0 = hi & (0u - (q == 3));
-      pos = rest;
-    }
-  }
-  __device__ __forceinline__ void put(uint32_t b) { put4(b, 1); }
-  __device__ __forceinline__ void flush() {
-    *dst = make_uint4(w0, w1, w2, w3);
-    dst += stride;
-    w0 = w1 = w2 = w3 = 0;
-    pos = 0;
-    ++stored;
-  }
-};
-
-// The walked string through the program's code map into o.
-__device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr, const uint32_t* sp, uint32_t stride,
-                                            uint32_t last, const uint8_t* __restrict__ code, Out16& o) {
-  for (uint32_t f = 0; f < last; ++f) {
-    const uint32_t s = sp[f * stride];
-    if (s == kAbsentSpan) {
-      o.put(code[1]);
-    } else {
-      const uint32_t a = s >> 16, L = s & 0xFFFFu;
-      for (uint32_t k = 0; k < L; k += 4) {  // a quad at a time: four code bytes, one insert
-        const uint32_t q = hr.quad(a + k), nb = min(L - k, 4u);
-        const uint32_t c = (uint32_t)code[q & 0xFFu] | (uint32_t)code[(q >> 8) & 0xFFu] << 8 |
-                           (uint32_t)code[(q >> 16) & 0xFFu] << 16 | (uint32_t)code[q >> 24] << 24;
-        o.put4(nb == 4 ? c : c & ((1u << (8 * nb)) - 1), nb);
-      }
-    }
-    o.put(code[0]);
-  }
-  if (last < R.nfields) o.put(code[2]);
-}
-
-// ---- pass 2: slots, meta, strings.  Slots: the block's LDS cursor per key
-// (the key's first slot + this block's prefix, lds_keys), else a global
-// cursor per key.
-__global__ __launch_bounds__(kRawThreads) void raw_emit_kernel(
-    HttpRawDev R, const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off, size_t n,
-    const uint8_t* __restrict__ ingress, const uint32_t* __restrict__ remote, const uint2* __restrict__ rinfo,
-    uint32_t* __restrict__ cursor, const uint32_t* __restrict__ bbase, uint32_t lds_keys, HttpTile* __restrict__ ttab,
-    uint8_t* __restrict__ tiles, uint32_t* __restrict__ order, uint8_t* __restrict__ arena,
-    unsigned long long* __restrict__ arena_cursor, const uint32_t* __restrict__ gspans, uint32_t lds_codes) {
-  extern __shared__ uint32_t lds[];
-  const uint32_t F = max(R.nfields, 1u), wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* sp = lds + threadIdx.x;
-  uint8_t* stage = wave_stage(lds, F, wave);
-  uint32_t* lk = key_counters(lds, F);
+// ---- pass 2: a slot per request from its bucket's cursor — the block's
+// LDS cursor per key (the key's first slot + this block's prefix, lds_keys:
+// the same grid and request order as the scan), else a global cursor per key
+__global__ __launch_bounds__(kRawThreads) void raw_rank_kernel(HttpRawDev R, size_t n,
+                                                               const uint64_t* __restrict__ off, uint32_t cst,
+                                                               const uint2* __restrict__ rinfo,
+                                                               uint32_t* __restrict__ cursor,
+                                                               const uint32_t* __restrict__ bbase, uint32_t lds_keys,
+                                                               uint32_t* __restrict__ order) {
+  extern __shared__ uint32_t lk[];  // the bucket cursors (lds_keys)
   const uint32_t nk = (R.nprogs + 2) * kRawKeys;
   if (lds_keys)
-    for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x)
-      lk[k] = cursor[k] + bbase[(size_t)k * gridDim.x + blockIdx.x];
-  // the programs' code maps in LDS (after the key cursors) when they fit
-  uint8_t* lcode = reinterpret_cast<uint8_t*>(lk + (lds_keys ? nk : 0));
-  if (lds_codes)
-    for (uint32_t k = threadIdx.x; k < R.nprogs * 64; k += blockDim.x)
-      reinterpret_cast<uint32_t*>(lcode)[k] = reinterpret_cast<const uint32_t*>(R.codes)[k];
+    for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = cursor[k] + bbase[(size_t)k * gridDim.x + blockIdx.x];
+  const uint64_t off0 = off[0];
   __syncthreads();
   for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
-    const size_t i0 = base + (size_t)wave * 64;
-    if (i0 >= n) continue;  // wave-uniform
-    const size_t i = i0 + lane;
-    const bool live = i < n;
-    const uint2 ri = live ? rinfo[i] : make_uint2(kProgDeny, 0);
+    const size_t i = base + threadIdx.x;
+    if (i >= n) continue;
+    const uint2 ri = rinfo[i];
     const uint32_t prog = ri.x, len = ri.y & 0x7FFFFFFFu;
-    const bool bad = ri.y >> 31, walk = live && walked(R, prog) && !bad;
-    uint32_t slen = 0;
-    uint64_t sbase = 0;
-    if (__any(walk)) sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
-    wave_sync();
-    if (live) {
-      const uint32_t key = !walk ? 0u : len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
-      const uint32_t k = group_of(R, prog) * kRawKeys + key;
-      const uint32_t slot = lds_keys ? atomicAdd(&lk[k], 1u) : atomicAdd(&cursor[k], 1u);
-      order[slot] = (uint32_t)i;
-      const uint32_t t = slot >> 6, sl = slot & 63;
-      const HttpTile tt = ttab[t];
-      uint8_t* tb = tiles + (size_t)tt.at * 512;
-      uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u);
-      uint32_t aoff16 = 0;
-      if (walked(R, prog) && !walk) {  // a rejected head in a walked tile: zero units
-        Out16 o(reinterpret_cast<uint4*>(tb + 512 + (size_t)sl * 16), 1024 / 16);
-        while (o.stored < tile_units(tt)) o.flush();
-      }
-      if (walk) {
-        HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
-        for (uint32_t f = 0; f < R.nfields; ++f) sp[f * kRawThreads] = gspans[(size_t)f * n + i];  // pass 1's
-        uint32_t last;
-        string_len(R, sp, kRawThreads, &last);
-        const uint8_t* code = (lds_codes ? lcode : R.codes) + (size_t)prog * 256;
-        if (key == kRawKeys - 1) {  // overflow arena entry: u32 length, the string, 16-byte aligned
-          flags |= CG_HTTP_F_OVERFLOW;
-          const unsigned long long ao = atomicAdd(arena_cursor, (unsigned long long)((4 + len + 15) & ~15u));
-          aoff16 = (uint32_t)(ao / 16);
-          Out16 o(reinterpret_cast<uint4*>(arena + ao), 1);
-          o.w0 = len;
-          o.pos = 4;
-          emit_string(R, hr, sp, kRawThreads, last, code, o);
-          if (o.pos) o.flush();
-          Out16 z(reinterpret_cast<uint4*>(tb + 512 + (size_t)sl * 16), 1024 / 16);
-          while (z.stored < tile_units(tt)) z.flush();  // the tile's units are not this lane's string
-        } else {
-          const uint32_t units = tile_units(tt);
-          Out16 o(reinterpret_cast<uint4*>(tb + 512 + (size_t)sl * 16), 1024 / 16);
-          emit_string(R, hr, sp, kRawThreads, last, code, o);
-          if (o.pos) o.flush();
-          while (o.stored < units) o.flush();  // zero padding up to the tile's units
-          if (key == units && units) atomicMax(&ttab[t].units, units | (len - 16 * (units - 1)) << 16);
-        }
-      }
-      reinterpret_cast<uint2*>(tb)[sl] = make_uint2(remote[i], (aoff16 & 0xFFFFFFu) | flags << 24);
-    }
-    wave_sync();
+    const bool walk = walked(R, prog) && !(ri.y >> 31);
+    const uint32_t key = !walk ? 0u : len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
+    const uint32_t k = group_of(R, prog) * kRawKeys + key;
+    const uint32_t slot = lds_keys ? atomicAdd(&lk[k], 1u) : atomicAdd(&cursor[k], 1u);
+    order[slot] = (uint32_t)(rec_off(off[i] - off0, i, cst) / 16);  // the request's record
   }
 }
 
-__global__ void raw_scatter_kernel(const uint32_t* __restrict__ order, const uint8_t* __restrict__ vslot,
-                                   size_t nslots, uint8_t* __restrict__ out) {
-  for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t r = order[s];
-    if (r != 0xFFFFFFFFu) out[r] = vslot[s];
+// Four string bytes through a code map in LDS.
+__device__ __forceinline__ uint32_t code4(const uint8_t* lut, uint32_t q) {
+  return (uint32_t)lut[q & 0xFFu] | (uint32_t)lut[(q >> 8) & 0xFFu] << 8 | (uint32_t)lut[(q >> 16) & 0xFFu] << 16 |
+         (uint32_t)lut[q >> 24] << 24;
+}
+
+// ---- pass 3: one wave per tile.  The tile's granule offset and string units
+// come from its run (tiles of one group whose last walked slot has the same
+// bucket key).  Each lane gathers its request's record (header + string: one
+// contiguous read) and the wave stores unit u of all 64 lanes as one
+// contiguous 1 KiB, class-coded through the tile's program's code map (staged
+// in LDS per wave); strings past a slot go to the overflow arena (u32 length,
+// coded bytes, 16-byte aligned).  order[slot] becomes the request index (the
+// verdict kernel writes out[order[slot]]).
+__global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
+    HttpRawDev R, const HttpRawRun* __restrict__ runs, uint32_t nruns, uint32_t ntiles, HttpTile* __restrict__ ttab,
+    uint8_t* __restrict__ tiles, uint32_t* __restrict__ order, const uint8_t* __restrict__ sbuf,
+    uint8_t* __restrict__ arena, unsigned long long* __restrict__ arena_cursor) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_lut[kRawThreads / 64][256];
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* lut = s_lut[wave];
+  uint32_t lut_prog = 0xFFFFFFFFu;
+  const uint4* rec16 = reinterpret_cast<const uint4*>(sbuf);
+  for (uint32_t t = blockIdx.x * (kRawThreads / 64) + wave; t < ntiles; t += gridDim.x * (kRawThreads / 64)) {
+    const size_t slot = (size_t)t * 64 + lane;
+    const uint32_t r = order[slot];
+    // the run holding tile t (runs ascending by t0, covering every tile)
+    uint32_t lo = 0, hi = nruns;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (runs[mid].t0 <= t) lo = mid;
+      else hi = mid;
+    }
+    const HttpRawRun run = runs[lo];
+    const uint32_t units = run.units;
+    const uint32_t at = run.base + (t - run.t0) * (1 + 2 * units);
+    uint8_t* tb = tiles + (size_t)at * 512;
+    const bool pad = r == 0xFFFFFFFFu;
+    uint4 h = make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
+    if (!pad) h = rec16[r];
+    const uint32_t len = h.z & 0xFFFFFFu, flags = h.z >> 24;
+    const bool ovf = flags & CG_HTTP_F_OVERFLOW;
+    const uint32_t slen = (pad || ovf) ? 0u : len;
+    if (!pad) order[slot] = h.x;
+    // the tile's program (every request of a tile has it): its code map
+    const unsigned long long live = __ballot(len != 0);
+    if (live) {
+      const uint32_t prog = (uint32_t)__shfl((int)h.w, (int)__builtin_ctzll(live), 64);
+      if (prog != lut_prog) {
+        wave_sync();  // earlier lookups done
+        reinterpret_cast<uint32_t*>(lut)[lane] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)prog * 256)[lane];
+        wave_sync();
+        lut_prog = prog;
+      }
+    }
+    uint32_t aoff16 = 0;
+    if (ovf) {
+      const unsigned long long ao = atomicAdd(arena_cursor, (unsigned long long)((4 + len + 15) & ~15u));
+      aoff16 = (uint32_t)(ao / 16);
+      Out16 o(reinterpret_cast<uint4*>(arena + ao), 1);
+      o.w0 = len;
+      o.pos = 4;
+      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(rec16 + r + 1);
+      for (uint32_t k = 0; k < len; k += 4) {
+        const uint32_t nb = min(len - k, 4u);
+        const uint32_t c = code4(lut, s32[k / 4]);
+        o.put4(nb == 4 ? c : c & ((1u << (8 * nb)) - 1u), nb);
+      }
+      if (o.pos) o.flush();
+    }
+    // unit u of every lane: a whole 1 KiB per unit (zero past a string's end)
+    uint4* dst = reinterpret_cast<uint4*>(tb + 512) + lane;
+    for (uint32_t u = 0; u < units; ++u) {
+      uint4 c = make_uint4(0, 0, 0, 0);
+      if (16 * u < slen) {
+        const uint4 x = rec16[r + 1 + u];
+        c = make_uint4(code4(lut, x.x), code4(lut, x.y), code4(lut, x.z), code4(lut, x.w));
+        const uint32_t left = slen - 16 * u;  // the string's bytes in this unit
+        if (left < 16) {
+          const uint32_t m0 = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
+          const uint32_t m1 = left >= 8 ? 0xFFFFFFFFu : left <= 4 ? 0u : (1u << (8 * (left - 4))) - 1u;
+          const uint32_t m2 = left >= 12 ? 0xFFFFFFFFu : left <= 8 ? 0u : (1u << (8 * (left - 8))) - 1u;
+          const uint32_t m3 = left <= 12 ? 0u : (1u << (8 * (left - 12))) - 1u;
+          c = make_uint4(c.x & m0, c.y & m1, c.z & m2, c.w & m3);
+        }
+      }
+      dst[(size_t)u * 64] = c;
+    }
+    reinterpret_cast<uint2*>(tb)[lane] = make_uint2(h.y, (aoff16 & 0xFFFFFFu) | flags << 24);
+    // the tile's tail: the longest string's bytes in its last unit
+    uint32_t m = slen;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    if (lane == 0) {
+      const uint32_t tail = units ? m - 16 * (units - 1) : 0u;
+      ttab[t] = HttpTile{at, units | tail << 16};
+    }
   }
 }
 
@@ -632,14 +655,15 @@ bool http_raw_lds_keys(const HttpRawDev& R) { return ((size_t)R.nprogs + 2) * kR
 
 int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
-                         void* rinfo, uint32_t* spans, unsigned long long* ovf_bytes, void* stream, int cus) {
+                         void* rinfo, const uint32_t* remote, uint8_t* sbuf, uint32_t cst,
+                         unsigned long long* ovf_bytes, void* stream, int cus) {
   if (!n) return 0;
   const bool lk = http_raw_lds_keys(R);
   const size_t lds = raw_lds(R, lk, false);
   (void)hipFuncSetAttribute((const void*)raw_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(raw_scan_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
-                     (hipStream_t)stream, R, raw, off, n, policy, ingress, port, counts, (uint2*)rinfo, spans,
-                     ovf_bytes, (uint32_t)lk);
+                     (hipStream_t)stream, R, raw, off, n, policy, ingress, port, counts, (uint2*)rinfo, remote, sbuf,
+                     cst, ovf_bytes, (uint32_t)lk);
   return (int)hipGetLastError();
 }
 
@@ -650,33 +674,25 @@ int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk
   return (int)hipGetLastError();
 }
 
-int launch_http_raw_tiles(const HttpRawGroup* groups, uint32_t ngroups, uint32_t ntiles, HttpTile* ttab,
-                          uint8_t* tiles, uint32_t* order, void* stream) {
-  if (!ntiles) return 0;
-  hipLaunchKernelGGL(raw_tiles_kernel, dim3((ntiles + kRawThreads - 1) / kRawThreads), dim3(kRawThreads), 0,
-                     (hipStream_t)stream, groups, ngroups, ntiles, ttab, tiles, order);
-  return (int)hipGetLastError();
-}
-
-int launch_http_raw_emit(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
-                         const uint8_t* ingress, const uint32_t* remote, const void* rinfo, uint32_t* cursor,
-                         const uint32_t* bbase, HttpTile* ttab, uint8_t* tiles, uint32_t* order, uint8_t* arena,
-                         unsigned long long* arena_cursor, const uint32_t* spans, void* stream, int cus) {
+int launch_http_raw_rank(const HttpRawDev& R, size_t n, const uint64_t* off, uint32_t cst, const void* rinfo,
+                         uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream, int cus) {
   if (!n) return 0;
-  const bool lk = http_raw_lds_keys(R), lc = lds_codes_fit(R);
-  const size_t lds = raw_lds(R, lk, lc);
-  (void)hipFuncSetAttribute((const void*)raw_emit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(raw_emit_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
-                     (hipStream_t)stream, R, raw, off, n, ingress, remote, (const uint2*)rinfo, cursor, bbase,
-                     (uint32_t)lk, ttab, tiles, order, arena, arena_cursor, spans, (uint32_t)lc);
+  const bool lk = http_raw_lds_keys(R);
+  const size_t lds = lk ? ((size_t)R.nprogs + 2) * kRawKeys * 4 : 0;
+  hipLaunchKernelGGL(raw_rank_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
+                     (hipStream_t)stream, R, n, off, cst, (const uint2*)rinfo, cursor, bbase, (uint32_t)lk, order);
   return (int)hipGetLastError();
 }
 
-int launch_http_raw_scatter(const uint32_t* order, const uint8_t* vslot, size_t nslots, uint8_t* out, void* stream,
-                            int cus) {
-  if (!nslots) return 0;
-  hipLaunchKernelGGL(raw_scatter_kernel, dim3(grid_for(nslots, cus, 8)), dim3(kRawThreads), 0, (hipStream_t)stream,
-                     order, vslot, nslots, out);
+int launch_http_raw_build(const HttpRawDev& R, const HttpRawRun* runs, uint32_t nruns, uint32_t ntiles,
+                          HttpTile* ttab, uint8_t* tiles, uint32_t* order, const uint8_t* sbuf, uint8_t* arena,
+                          unsigned long long* arena_cursor, void* stream, int cus) {
+  if (!ntiles) return 0;
+  const unsigned waves = kRawThreads / 64;
+  const unsigned grid =
+      (unsigned)std::max<size_t>(1, std::min<size_t>((ntiles + waves - 1) / waves, (size_t)cus * 8));
+  hipLaunchKernelGGL(raw_build_kernel, dim3(grid), dim3(kRawThreads), 0, (hipStream_t)stream, R, runs, nruns, ntiles,
+                     ttab, tiles, order, sbuf, arena, arena_cursor);
   return (int)hipGetLastError();
 }
 

@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU box: raw-path + LPM tests, raw and lpm bench lines, raw kernel trace.
+# GPU box: raw-path tests, the raw bench line, raw kernel trace.
 cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/${1:-raw3}
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -u -m pytest tests/test_http_raw_gpu.py tests/test_proxylib_cassandra.py tests/test_npds_pb.py -m gpu -x -v --timeout 200 --timeout-method thread > $out/pytest.log 2>&1 || exit $?
+timeout -k 10 400 python3 -u -m pytest tests/test_http_raw_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread > $out/pytest.log 2>&1 || exit $?
 timeout -k 10 600 python3 tools/bench_paths.py --paths httpraw > $out/paths.jsonl 2> $out/paths.err || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 tools/bench_paths.py --paths httpraw --steps 3 --cpu-seconds 0 > $out/prof.log 2>&1 || exit $?
