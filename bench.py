@@ -5,13 +5,19 @@ config 5), one process per GPU.
 
 A step is one pass of the verdict kernel over the GPU's resident batch of B
 packed requests (default 125M = 1B / 8, so at N = 8 the node processes the
-config's 1B requests per step; scaling is weak: per-GPU work is fixed).
-After each step the per-program allowed/denied counters are all-reduced
-across ranks (RCCL) — the only collective on this path.
+config's 1B requests per step; scaling is weak: per-GPU work is fixed).  The
+batch holds --distinct (default 8M) distinct requests, each program group's
+tiles repeated to B.  After each step the per-rule and per-program counters
+are all-reduced across ranks (RCCL) — the only collective on this path.  The
+10K rules are compiled once (rank 0) and every rank imports the same table
+image (cg_http_policy_export / _import).
 
 Rank 0 prints one JSON line with throughput, the roofline of the verdict
-kernel (HIP events on the kernel's stream) and the CPU oracle (the
-Envoy-faithful std::regex rule scan) timed on a bounded sample on the host.
+kernel (HIP events on the kernel's stream), the same kernel on a 262K-distinct
+batch, the end-to-end raw path (config 5 as raw HTTP/1 heads resident in HBM
+→ cg_http_verdicts_raw_dev: parse, pack and verdicts on the GPU) and the CPU
+oracle (the Envoy-faithful std::regex rule scan) timed on a bounded sample on
+the host cores given to this GPU.
 """
 from __future__ import annotations
 
@@ -38,7 +44,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--requests-per-gpu", type=int, default=125_000_000)
-    ap.add_argument("--distinct", type=int, default=262_144)
+    ap.add_argument("--distinct", type=int, default=8_388_608)
+    ap.add_argument("--small-distinct", type=int, default=262_144,
+                    help="second measurement of the kernel on a batch with this many distinct requests (0: skip)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end raw-heads measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
@@ -98,17 +107,17 @@ def main():
     cl = Classifier(device=dev.index)
     pols, info = synth.http10k_rules()
     t0 = time.time()
-    cl.update_http_policy(pols)
+    share_policy(cl, pols, dist, rank, dev, torch)
     compile_s = time.time() - t0
     stats = cl.http_policy_stats()
 
     D = min(args.distinct - args.distinct % 64, args.requests_per_gpu)
-    rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
+    rq = synth.http10k_requests_fast(D, info, seed=synth.SEED ^ (rank * 7919))
     b = cl.pack_http(**rq)
     reps = max(1, args.requests_per_gpu // D)
     B = reps * D                                  # requests per GPU per step
     d_batch, nslots, tile_map, data_bytes = replicate_batch(b, reps, dev, torch, layout=args.layout)
-    d_arena = torch.from_numpy(b.arena).to(dev)
+    d_arena = torch.from_numpy(np.concatenate([b.arena.view(np.uint8), np.zeros(16, np.uint8)])).to(dev)
     d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
     n_ctr = cl.allreduce_counter_count()
     d_ctr = torch.zeros(max(n_ctr, 1), dtype=torch.int64, device=dev)
@@ -142,10 +151,11 @@ def main():
         got = np.zeros(D, np.uint8)
         real = b.order < D
         got[b.order[real]] = slots[real]
-        exp = oracle.HttpOracle(pols).eval(**rq, nthreads=min(16, os.cpu_count() or 1))
+        exp = oracle.HttpOracle(pols).eval(**rq, nthreads=host_threads())
         check = bool(np.array_equal(got, exp))
         if not check:
             raise SystemExit(f"verdicts differ from the oracle on {int((got != exp).sum())} of {D} requests")
+        del rq
 
     for _ in range(args.warmup):
         step()
@@ -179,6 +189,15 @@ def main():
     traffic_bytes, traffic_src = pmc_traffic(B)
     # same unit as `achieved`: HBM bytes per launch over the measured launch time
     traffic = traffic_bytes / (kernel_ms * 1e-3) / 1e9 if traffic_bytes else None
+    del d_batch, d_arena
+    small = None
+    if args.small_distinct and args.small_distinct < D:
+        small = kernel_on_batch(cl, info, args.small_distinct, args.requests_per_gpu, rank, dev, torch, stream,
+                                args.steps, args.warmup, args.layout)
+    e2e = None
+    if not args.no_e2e:
+        e2e = end_to_end(cl, pols, info, min(D, 4_194_304), args.requests_per_gpu, rank, dev, torch, stream,
+                         args.steps, min(args.warmup, 2), not args.no_check)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pols, info, args.cpu_seconds)
@@ -200,12 +219,15 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": f"synthetic: 10K generated PortRuleHTTP rules over 64 ports / 256 selectors of 1K identities; "
-                    f"{D} distinct packed requests (50% rule hits, 50% near misses) tiled to {B} per GPU",
+                    f"{D} distinct packed requests (50% rule hits, 50% near misses), each program group's tiles "
+                    f"repeated to {B} per GPU",
             "config": {"workload": "BASELINE config 5: 10K-rule L7 HTTP set (method/path/host/header regex union "
                                    "DFA), requests sharded across GPUs",
                        "requests_per_gpu": B, "rules": int(stats["rules"]), "programs": int(stats["programs"]),
                        "dfa_states": int(stats["states"]), "table_bytes": int(stats["table_bytes"]),
-                       "compile_s": round(compile_s, 3), "packed_bytes_per_request": per_launch_bytes / B,
+                       "compile_s": round(compile_s, 3), "distinct_requests": D,
+                       "policy_tables": "compiled once on rank 0, the same image imported by every rank",
+                       "packed_bytes_per_request": per_launch_bytes / B,
                        "allreduce_counters": n_ctr, "parallelism": f"dp{world}"},
             "request_gbps": value * per_launch_bytes / B / 1e9,
             "allow_fraction": allow_frac,
@@ -215,12 +237,144 @@ def main():
                          "kernel": "http_kernel", "kernel_ms": kernel_ms,
                          "bytes_per_launch": per_launch_bytes, "traffic_bytes_per_launch": traffic_bytes,
                          "traffic_source": traffic_src},
+            "distinct_262k": small,
+            "end_to_end": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     cl.close()
+
+
+def host_threads() -> int:
+    """Host threads given to this GPU's process: OMP_NUM_THREADS (16 on the
+    GPU box: its per-GPU CPU share), else the cores here up to 16."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
+def share_policy(cl, pols, dist, rank, dev, torch) -> None:
+    """Compile the rules once (rank 0) and give every rank the same compiled
+    table image: broadcast over the process group, imported
+    without recompiling.  One rank: compile."""
+    if dist is None or dist.get_world_size() == 1:
+        cl.update_http_policy(pols)
+        return
+    if rank == 0:
+        cl.update_http_policy(pols)
+        img = np.frombuffer(cl.export_http_policy(), np.uint8)
+        size = torch.tensor([img.size], dtype=torch.int64, device=dev)
+    else:
+        size = torch.zeros(1, dtype=torch.int64, device=dev)
+    dist.broadcast(size, 0)
+    buf = torch.empty(int(size.item()), dtype=torch.uint8, device=dev)
+    if rank == 0:
+        buf.copy_(torch.from_numpy(img.copy()))
+    dist.broadcast(buf, 0)
+    if rank != 0:
+        cl.import_http_policy(buf.cpu().numpy().tobytes())
+
+
+def kernel_on_batch(cl, info, distinct, per_gpu, rank, dev, torch, stream, steps, warmup, layout) -> dict:
+    """The verdict kernel on a batch of `distinct` requests repeated to
+    per_gpu (the round-2 bench layout), HIP events on its stream."""
+    from cilium_amd import synth
+    D = distinct - distinct % 64
+    rq = synth.http10k_requests_fast(D, info, seed=synth.SEED ^ (rank * 7919) ^ 0x262)
+    b = cl.pack_http(**rq)
+    reps = max(1, per_gpu // D)
+    d_batch, nslots, _, data_bytes = replicate_batch(b, reps, dev, torch, layout=layout)
+    d_arena = torch.from_numpy(np.concatenate([b.arena.view(np.uint8), np.zeros(16, np.uint8)])).to(dev)
+    d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
+    ev = []
+    for k in range(warmup + steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        cl.http_verdicts_dev(d_batch, nslots, d_arena, d_out, stream=stream.cuda_stream)
+        e1.record(stream)
+        if k >= warmup:
+            ev.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(z) for a, z in ev) / steps
+    B = reps * D
+    return {"distinct_requests": D, "requests": B, "kernel_ms": ms, "value": B / (ms * 1e-3),
+            "frac": (data_bytes + B) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
+def end_to_end(cl, pols, info, distinct, per_gpu, rank, dev, torch, stream, steps, warmup, check) -> dict:
+    """Config 5 as raw HTTP/1.1 request heads resident in HBM (request line,
+    Host, the rule's header), per request its policy / ingress / port /
+    remote identity and a u64 offset: cg_http_verdicts_raw_dev parses,
+    groups, packs and evaluates them on the GPU and writes verdicts in request
+    order.  One call per step (it waits on the host for the bucket counts
+    between its scan and its layout, so the clock is the host's).  Checked
+    bit-exact against the oracle (codec step oracle/http1_ref.py, then the
+    Envoy-faithful rule scan) on a subsample, and every copy against its
+    original."""
+    from cilium_amd import synth
+    D = distinct - distinct % 64
+    rq = synth.http10k_requests_fast(D, info, seed=synth.SEED ^ (rank * 7919) ^ 0xE2E, raw=True)
+    reps = max(1, per_gpu // D)
+    n = D * reps
+    blob, off = rq["raw_blob"], rq["raw_off"]
+    tot = int(off[-1])
+    d_raw = torch.empty(tot * reps, dtype=torch.uint8, device=dev)
+    d_raw[:tot].copy_(torch.from_numpy(blob[:tot]))
+    done = 1
+    while done < reps:
+        k = min(done, reps - done)
+        d_raw[done * tot:(done + k) * tot].copy_(d_raw[:k * tot])
+        done += k
+    base = torch.arange(reps, dtype=torch.int64, device=dev).unsqueeze(1) * tot
+    d_off = torch.cat([(torch.from_numpy(off[:-1].astype(np.int64)).to(dev).unsqueeze(0) + base).reshape(-1),
+                       torch.tensor([tot * reps], dtype=torch.int64, device=dev)])
+    rep = lambda a, dt: torch.from_numpy(np.asarray(a).astype(dt)).to(dev).repeat(reps)  # noqa: E731
+    d_pol, d_ing = rep(rq["policy"], np.int32), rep(rq["ingress"], np.uint8)
+    d_port, d_rem = rep(rq["port"].astype(np.int16), np.int16), rep(rq["remote"].astype(np.int32), np.int32)
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+
+    def run():
+        cl.http_verdicts_raw_dev(d_raw, d_off, n, d_pol, d_ing, d_port, d_rem, d_out, stream=stream.cuda_stream)
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    sec = (time.perf_counter() - t0) / steps
+    parity = None
+    if check:
+        import oracle
+        from oracle.http1_ref import parse_head
+        k = min(D, 20_000)
+        lists = [parse_head(bytes(blob[int(off[i]):int(off[i + 1])])) for i in range(k)]
+        hb, ho = [], [0]
+        for lst in lists:
+            one = b"".join(a + b"\0" + v + b"\0" for a, v in (lst or []))
+            hb.append(one)
+            ho.append(ho[-1] + len(one))
+        v = oracle.HttpOracle(pols).eval(rq["policy"][:k], rq["ingress"][:k], rq["port"][:k], rq["remote"][:k],
+                                         np.frombuffer(b"".join(hb) or b"\0", np.uint8).copy(),
+                                         np.asarray(ho, np.uint64), nthreads=host_threads())
+        exp = np.where([x is not None for x in lists], v, 0).astype(np.uint8)
+        first = d_out[:D]
+        same = bool((d_out.view(reps, D) == first.unsqueeze(0)).all())
+        parity = bool(np.array_equal(first[:k].cpu().numpy(), exp)) and same
+        if not parity:
+            raise SystemExit("end-to-end raw-path verdicts differ from the oracle")
+    in_bytes = tot * reps + n * (4 + 1 + 2 + 4 + 8)  # heads, policy, ingress, port, remote, offsets
+    per_req = (in_bytes + n) / n
+    achieved = (in_bytes + n) / sec / 1e9
+    return {"metric": "verdicts/s end to end: raw HTTP/1 heads in HBM -> verdicts in request order "
+                      "(cg_http_verdicts_raw_dev: codec step, program lookup, packing, http_kernel)",
+            "value": n / sec, "unit": "verdicts/s", "ms_per_step": sec * 1e3, "requests": n,
+            "distinct_requests": D, "head_bytes_per_request": tot / D, "request_gbps": tot * reps / sec / 1e9,
+            "parity_check": parity,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "bytes_per_request": per_req,
+                         "note": "algorithmic bytes = the call's inputs + the verdict; the path is bound by its "
+                                 "parse and layout kernels, not by HBM (profiles/r03*_raw_kernel_stats.csv)"}}
 
 
 def rehearse(args):
@@ -242,7 +396,7 @@ def rehearse(args):
         dist.init_process_group("gloo")
     cl = Classifier(device=-1)
     pols, info = synth.http10k_rules(n_rules=2000, n_ports=16)
-    cl.update_http_policy(pols)
+    share_policy(cl, pols, dist if world > 1 else None, rank, torch.device("cpu"), torch)
     D = max(64, min(args.requests_per_gpu, args.distinct))
     rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
     b = cl.pack_http(**rq)
@@ -435,13 +589,15 @@ def cpu_model() -> str:
 
 def cpu_baseline(pols, info, seconds: float) -> dict:
     """Oracle = Envoy's algorithm (per-request PortNetworkPolicy scan with
-    std::regex_match), on a bounded sample, threads = the host cores given to
-    this process; plus the same on one core."""
+    std::regex_match) over a 1M-request sample of the same workload, cycled
+    for a bounded time on the host cores given to this GPU (its share of the
+    node: OMP_NUM_THREADS on the GPU box); plus the same on one core (SURVEY
+    8(d))."""
     import oracle
     from cilium_amd import synth
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = host_threads()
     orc = oracle.HttpOracle(pols)
-    rq = synth.http10k_requests(100_000, info, seed=synth.SEED ^ 0xC0FFEE)
+    rq = synth.http10k_requests_fast(1_000_000, info, seed=synth.SEED ^ 0xC0FFEE)
 
     def rate(nthreads, secs, sub):
         done, t0 = 0, time.perf_counter()
@@ -456,8 +612,11 @@ def cpu_baseline(pols, info, seconds: float) -> dict:
     d1, e1 = rate(1, min(seconds / 4, 3.0), one)
     return {"value": done / el, "unit": "verdicts/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(), "single_core": d1 / e1,
-            "sample": f"{done} requests of the same 10K-rule workload ({el:.1f} s, {threads} threads, "
-                      f"std::regex_match per matcher as Envoy); single core: {d1} requests in {e1:.1f} s"}
+            "cores_note": f"the host threads given to this GPU's process ({threads}: its share of the node's "
+                          f"{os.cpu_count()} hardware threads); a node's 8 GPUs' shares run 8 such baselines",
+            "sample": f"{done} requests ({done / 1e6:.1f}M: a 1M-request sample of the same 10K-rule workload "
+                      f"cycled, {el:.1f} s, {threads} threads, std::regex_match per matcher as Envoy); "
+                      f"single core: {d1} requests in {e1:.1f} s"}
 
 
 def cpu_dfa_line(cl, info, seconds: float, threads: int) -> dict:
@@ -468,7 +627,7 @@ def cpu_dfa_line(cl, info, seconds: float, threads: int) -> dict:
 
     from cilium_amd import synth
     per = 65_536
-    batches = [cl.pack_http(**synth.http10k_requests(per, info, seed=synth.SEED ^ (0xD0 + t)))
+    batches = [cl.pack_http(**synth.http10k_requests_fast(per, info, seed=synth.SEED ^ (0xD0 + t)))
                for t in range(threads)]
     cl.http_eval_host_diag(batches[0])
     t1 = time.perf_counter()

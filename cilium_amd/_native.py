@@ -125,6 +125,9 @@ SIGNATURES = {
     "cg_l4_verdicts_ipcache6_host": (C.c_int, [_u64, _u32, _u32, _p, _p, _sz, _p]),
     "cg_http_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_http_policy_update_npds": (C.c_int, [_u64, C.c_char_p, _sz]),
+    "cg_http_pack_threads": (_u32, []),
+    "cg_http_policy_export": (C.c_int, [_u64, C.c_void_p, _sz, C.POINTER(_sz)]),
+    "cg_http_policy_import": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_http_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_http_policy_stats": (C.c_int, [_u64, C.POINTER(_u64), _sz]),
     "cg_http_rule_info_get": (C.c_int, [_u64, _p, _sz, C.POINTER(_sz)]),

@@ -110,6 +110,19 @@ class Classifier:
         envoy.api.v2.DiscoveryResponse of cilium.NetworkPolicy resources."""
         N.check(N.lib.cg_http_policy_update_npds(self.h, discovery_response, len(discovery_response)))
 
+    def export_http_policy(self) -> bytes:
+        """The installed HTTP snapshot's compiled tables as a flat image
+        (cg_http_policy_export): compile once, import everywhere."""
+        n = C.c_size_t()
+        N.check(N.lib.cg_http_policy_export(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        N.check(N.lib.cg_http_policy_export(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def import_http_policy(self, image: bytes) -> None:
+        """Publish a compiled image (cg_http_policy_import) without recompiling."""
+        N.check(N.lib.cg_http_policy_import(self.h, image, len(image)))
+
     def http_policy_index(self, name: str) -> int:
         v = C.c_uint32()
         rc = N.lib.cg_http_policy_index(self.h, name.encode(), C.byref(v))

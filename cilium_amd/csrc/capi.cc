@@ -787,6 +787,31 @@ int cg_http_policy_update_npds(uint64_t h, const uint8_t* resp, size_t len) {
   return cg_http_policy_update(h, json.data(), json.size());
 }
 
+static std::shared_ptr<HttpSnapshot> http_snap(Engine& e);
+
+int cg_http_policy_export(uint64_t h, void* buf, size_t cap, size_t* len) {
+  return guarded([&] {
+    auto e = get(h);
+    const std::vector<uint8_t> img = http_image_export(*http_snap(*e));
+    if (len) *len = img.size();
+    if (buf && cap >= img.size()) memcpy(buf, img.data(), img.size());
+    else if (buf) fail(CG_INVALID_ARGUMENT, "policy image buffer too small");
+  });
+}
+
+int cg_http_policy_import(uint64_t h, const void* buf, size_t len) {
+  return guarded([&] {
+    auto e = get(h);
+    std::shared_ptr<HttpSnapshot> snap = http_image_import(static_cast<const uint8_t*>(buf), len);
+    if (e->has_gpu()) {
+      e->set_device();
+      snap->upload(*e);
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->http = snap;  // publish
+  });
+}
+
 static std::shared_ptr<HttpSnapshot> http_snap(Engine& e) {
   std::lock_guard<std::mutex> lk(e.mu);
   if (!e.http) fail(CG_NOT_FOUND, "no HTTP policy installed");

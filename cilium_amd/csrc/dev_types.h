@@ -257,7 +257,22 @@ struct HttpRawDev {
   const uint32_t* fslots;      // per slot {FNV-1a of the lowercase name, name length (0 = empty), field, name offset}
   const uint8_t* fnames;       // lowercase names
   const uint8_t* codes;        // nprogs × 256: string byte → code (identity for byte-mode programs)
+  // field names by their lowercase key (raw_name_key): per slot 8 u32 {length
+  // (0 = empty), first 8 bytes (2 u32), last 8 bytes (2 u32; 0 when length
+  // <= 8), field, name offset, 0}; nkmask + 1 slots
+  const uint32_t* nkeys;
+  uint32_t nkmask;
 };
+// The key of a lowercase header name b[0, nl): its length, its first 8 bytes
+// and (nl > 8) its last 8 bytes, little-endian, zero past the name.
+CG_HD inline uint32_t raw_name_hash(uint32_t nl, uint32_t lo0, uint32_t lo1, uint32_t hi0, uint32_t hi1) {
+  uint32_t h = nl * 0x9E3779B1u;
+  h = (h ^ lo0) * 0x85EBCA77u;
+  h = (h ^ lo1) * 0xC2B2AE3Du;
+  h = (h ^ hi0) * 0x27D4EB2Fu;
+  h = (h ^ hi1) * 0x165667B1u;
+  return h ^ (h >> 15);
+}
 // FNV-1a, 32 bit, over lowercase bytes
 CG_HD inline uint32_t raw_fnv(uint32_t h, uint8_t c) { return (h ^ c) * 16777619u; }
 constexpr uint32_t kRawFnvInit = 2166136261u;

@@ -532,12 +532,16 @@ void build_parts(const FieldDfaCache& fc, const std::vector<URule>& all_rules, s
 
 }  // namespace
 
+uint32_t http_next_epoch() {
+  static std::atomic<uint32_t> g_epoch{0};
+  return ++g_epoch;
+}
+
 std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len) {
   std::vector<PolicySpec> pols = parse_npds(json, len);
   auto snap = std::make_shared<HttpSnapshot>();
   HttpSnapshot& S = *snap;
-  static std::atomic<uint32_t> g_epoch{0};
-  S.epoch = ++g_epoch;
+  S.epoch = http_next_epoch();
   if (pols.size() >= 0x7FFF) fail(CG_POLICY_REJECTED, "too many policies");
 
   // ---- field order

@@ -43,7 +43,7 @@ struct HttpSnapshot {
   HttpDev dev{};
   // raw HTTP/1 heads on the device (http_raw.cc): set by upload when the
   // snapshot qualifies (not proxylib, at most kRawMaxFields fields)
-  DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes;
+  DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes, d_nkeys;
   HttpRawDev raw{};
   bool raw_ok = false;
   LaunchFence fence;  // last member: queued kernels finish before the buffers go (engine.h)
@@ -53,6 +53,12 @@ struct HttpSnapshot {
 };
 
 std::shared_ptr<HttpSnapshot> http_compile(const char* json, size_t len);
+// A fresh batch epoch (packed batches carry the epoch of their snapshot).
+uint32_t http_next_epoch();
+// The compiled snapshot as a flat image and back (http_image.cc): compile
+// once, publish the same tables on every GPU / process.
+std::vector<uint8_t> http_image_export(const HttpSnapshot& s);
+std::shared_ptr<HttpSnapshot> http_image_import(const uint8_t* p, size_t n);
 
 // NPDS wire form (serialized DiscoveryResponse of cilium.NetworkPolicy) →
 // the NPDS JSON http_compile and the proxylib translation read (npds_pb.cc).

@@ -545,3 +545,6 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
 }
 
 }  // namespace cg
+
+// The packer's worker count for a large batch (what cg_http_pack uses).
+extern "C" uint32_t cg_http_pack_threads(void) { return cg::pack_threads((size_t)1 << 20); }

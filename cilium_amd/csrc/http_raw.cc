@@ -51,6 +51,33 @@ void http_raw_upload(HttpSnapshot& S) {
     for (unsigned char c : nm) names.push_back((uint8_t)((c >= 'A' && c <= 'Z') ? c + 32 : c));
   }
   if (names.empty()) names.push_back(0);
+  // the same names by (length, first 8, last 8) key (kernels_http_raw.hip
+  // field_of_key); name offsets index `names`
+  std::vector<uint32_t> nk(8 * (size_t)cap, 0);
+  for (uint32_t f = 0; f < F; ++f) {
+    const std::string& nm = S.fields[f];
+    if (nm.empty() || nm[0] == ':') continue;
+    const uint32_t nl = (uint32_t)nm.size();
+    auto byte = [&](uint32_t j) -> uint32_t {
+      const unsigned char c = (unsigned char)nm[j];
+      return (c >= 'A' && c <= 'Z') ? c + 32u : c;
+    };
+    auto word = [&](uint32_t at, uint32_t lim) {  // bytes at..at+3 below lim
+      uint32_t w = 0;
+      for (uint32_t j = 0; j < 4; ++j)
+        if (at + j < lim) w |= byte(at + j) << (8 * j);
+      return w;
+    };
+    const uint32_t lo0 = word(0, nl), lo1 = word(4, nl);
+    const uint32_t hi0 = nl > 8 ? word(nl - 8, nl) : 0u, hi1 = nl > 8 ? word(nl - 4, nl) : 0u;
+    uint32_t sl = raw_name_hash(nl, lo0, lo1, hi0, hi1) & (cap - 1);
+    while (nk[8 * (size_t)sl]) sl = (sl + 1) & (cap - 1);
+    uint32_t off = 0;  // the name's offset in `names` (from the FNV table)
+    for (uint32_t k = 0; k < cap; ++k)
+      if (slots[4 * (size_t)k + 1] && slots[4 * (size_t)k + 2] == f) off = slots[4 * (size_t)k + 3];
+    const uint32_t e[8] = {nl, lo0, lo1, hi0, hi1, f, off, 0};
+    memcpy(&nk[8 * (size_t)sl], e, sizeof e);
+  }
   std::vector<uint8_t> codes(std::max<size_t>(S.progs.size(), 1) * 256);
   for (size_t p = 0; p < S.progs.size(); ++p)
     for (int b = 0; b < 256; ++b)
@@ -60,6 +87,7 @@ void http_raw_upload(HttpSnapshot& S) {
   S.d_fslots.upload_vec(slots);
   S.d_fnames.upload_vec(names);
   S.d_codes.upload_vec(codes);
+  S.d_nkeys.upload_vec(nk);
   R.phash_keys = S.d_phk.as<uint32_t>();
   R.phash_vals = S.d_phv.as<uint32_t>();
   R.phash_mask = S.phash_mask;
@@ -72,6 +100,8 @@ void http_raw_upload(HttpSnapshot& S) {
   R.fslots = S.d_fslots.as<uint32_t>();
   R.fnames = S.d_fnames.as<uint8_t>();
   R.codes = S.d_codes.as<uint8_t>();
+  R.nkeys = S.d_nkeys.as<uint32_t>();
+  R.nkmask = cap - 1;
   S.raw_ok = true;
 }
 

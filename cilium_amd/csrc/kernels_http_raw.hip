@@ -136,6 +136,7 @@ struct HeadReader {
 // read from HBM), and four waves' stages leave room for 3+ workgroups per CU
 // (8 KiB: 1.69, 6 KiB: 2.01, 4 KiB: 1.12 G requests/s on config 5)
 constexpr uint32_t kStage = 6144;
+constexpr uint32_t kMaskWords = kStage / 32;  // u32 words per structural mask of a stage
 __device__ __forceinline__ uint64_t stage_heads(const uint8_t* __restrict__ raw, uint64_t lo, uint64_t hi,
                                                 uint8_t* stage, uint32_t lane, uint32_t* len) {
   const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
@@ -281,6 +282,151 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, HeadReader& hr, 
   return true;
 }
 
+// ---- structural masks of a wave's stage (data-parallel) ----------------
+// Two bitmaps over the stage's bytes, built by all 64 lanes (32 bytes per
+// lane per round): `special` = byte < 0x21 or DEL (SP, HTAB, CR, LF and every
+// control byte: what ends a plain run of target or field-value bytes) and
+// `nontchar` (not an RFC 7230 tchar: what ends a method or a header name).
+// A lane then parses its head line by line with find-next-set over the
+// bitmaps instead of byte loops.
+__device__ __forceinline__ uint32_t pack4(uint32_t hi_bits) {  // bits 7/15/23/31 → bits 0..3
+  return ((hi_bits >> 7) * 0x00204081u) >> 21 & 0xFu;
+}
+__device__ __forceinline__ uint32_t special4(uint32_t x) {
+  const uint32_t lt = ~(((x & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | x) & 0x80808080u;  // byte < 0x21
+  const uint32_t t = x ^ 0x7F7F7F7Fu;
+  const uint32_t del = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;  // byte == 0x7F
+  return pack4(lt | del);
+}
+__device__ __forceinline__ void build_masks(const uint8_t* stage, uint32_t slen, const uint8_t* tct, uint32_t* masks,
+                                            uint32_t lane) {
+  for (uint32_t w = lane; w * 32 < slen; w += 64) {
+    const uint4 a = *reinterpret_cast<const uint4*>(stage + 32 * w);
+    const uint4 b = *reinterpret_cast<const uint4*>(stage + 32 * w + 16);
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t sp = 0, nt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sp |= special4(d[k]) << (4 * k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nt |= (uint32_t)tct[(d[k] >> (8 * j)) & 0xFFu] << (4 * k + j);
+    }
+    masks[w] = sp;
+    masks[kMaskWords + w] = nt;
+  }
+}
+// First set bit at or after p (stage offsets), or lim when none before lim.
+__device__ __forceinline__ uint32_t next_set(const uint32_t* m, uint32_t p, uint32_t lim) {
+  uint32_t w = p >> 5;
+  uint32_t x = m[w] & (0xFFFFFFFFu << (p & 31));
+  while (!x) {
+    if (32 * (w + 1) >= lim) return lim;
+    x = m[++w];
+  }
+  return min(32 * w + (uint32_t)__builtin_ctz(x), lim);
+}
+__device__ __forceinline__ uint32_t sbyte(const uint8_t* st, uint32_t p) { return st[p]; }
+__device__ __forceinline__ uint32_t squad(const uint8_t* st, uint32_t p) {
+  const uint32_t* w4 = reinterpret_cast<const uint32_t*>(st + (p & ~3u));
+  return __builtin_amdgcn_alignbyte(w4[1], w4[0], p & 3u);
+}
+__device__ __forceinline__ uint32_t lower4(uint32_t x) {  // ASCII A-Z → a-z, per byte (bytes < 0x80)
+  const uint32_t y = x & 0x7F7F7F7Fu;
+  const uint32_t ge_a = y + 0x3F3F3F3Fu, gt_z = y + 0x25252525u;  // bit 7: byte >= 'A' / byte > 'Z'
+  return x | ((ge_a & ~gt_z & ~x & 0x80808080u) >> 2);
+}
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t x, uint32_t nb) {
+  return nb >= 4 ? x : x & ((1u << (8 * nb)) - 1u);
+}
+
+// The field a header name (stage bytes [k, k + nl)) is, or -1: the lowercase
+// (length, first 8, last 8) key in R.nkeys (raw_name_key), the bytes between
+// verified for longer names.
+__device__ __forceinline__ int field_of_key(const HttpRawDev& R, const uint8_t* st, uint32_t k, uint32_t nl) {
+  uint32_t lo0 = lower4(keep_bytes(squad(st, k), nl)), lo1 = 0, hi0 = 0, hi1 = 0;
+  if (nl > 4) lo1 = lower4(keep_bytes(squad(st, k + 4), nl - 4));
+  if (nl > 8) {
+    hi0 = lower4(squad(st, k + nl - 8));
+    hi1 = lower4(squad(st, k + nl - 4));
+  }
+  uint32_t sl = raw_name_hash(nl, lo0, lo1, hi0, hi1) & R.nkmask;
+  for (uint32_t probe = 0; probe <= R.nkmask; ++probe) {
+    const uint4 e = reinterpret_cast<const uint4*>(R.nkeys)[2 * sl];
+    if (e.x == 0) return -1;
+    const uint4 f = reinterpret_cast<const uint4*>(R.nkeys)[2 * sl + 1];
+    if (e.x == nl && e.y == lo0 && e.z == lo1 && e.w == hi0 && f.x == hi1) {
+      bool eq = true;
+      for (uint32_t j = 8; j + 8 < nl && eq; ++j) eq = lower(sbyte(st, k + j)) == R.fnames[f.z + j];
+      if (eq) return (int)f.y;
+    }
+    sl = (sl + 1) & R.nkmask;
+  }
+  return -1;
+}
+
+// parse_head over the stage with the structural masks: the head is stage
+// bytes [hs, he).  Same results as parse_head (http_parse.cc semantics).
+__device__ __forceinline__ bool parse_head_masks(const HttpRawDev& R, const uint8_t* st, const uint32_t* msp,
+                                                 const uint32_t* mnt, uint32_t hs, uint32_t he, uint32_t* sp,
+                                                 uint32_t stride) {
+  for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
+  if (he - hs > kRawMaxHead) return false;
+  const uint32_t m = next_set(mnt, hs, he);  // method: a tchar run, then SP
+  if (m == hs || m >= he || sbyte(st, m) != ' ') return false;
+  const uint32_t t0 = m + 1;
+  const uint32_t te = next_set(msp, t0, he);  // request-target: plain bytes, then SP
+  if (te == t0 || te >= he || sbyte(st, te) != ' ') return false;
+  uint32_t k = te + 1;
+  if (k + 10 > he) return false;  // "HTTP/" DIGIT "." DIGIT CRLF
+  {
+    const uint32_t q0 = squad(st, k), q1 = squad(st, k + 4), q2 = squad(st, k + 8);
+    const uint32_t d1 = q1 >> 8 & 0xFFu, d2 = q1 >> 24;
+    if (q0 != 0x50545448u || (q1 & 0xFFu) != '/' || d1 < '0' || d1 > '9' || (q1 >> 16 & 0xFFu) != '.' || d2 < '0' ||
+        d2 > '9' || (q2 & 0xFFFFu) != 0x0A0Du)
+      return false;
+  }
+  k += 10;
+  bool have_host = false;
+  uint32_t auth = kAbsentSpan;
+  while (true) {
+    if (k + 1 >= he) return false;  // no CRLF left: incomplete head
+    if ((squad(st, k) & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
+    const uint32_t c = next_set(mnt, k, he);  // name: a tchar run, then ':'
+    if (c == k || c >= he || sbyte(st, c) != ':') return false;
+    const uint32_t nl = c - k;
+    uint32_t v = c + 1, first = kAbsentSpan, lend = v, s;
+    while (true) {  // field-value to CRLF: IS_HEADER_CHAR, OWS trimmed
+      s = next_set(msp, v, he);
+      if (s > v) {
+        if (first == kAbsentSpan) first = v;
+        lend = s;
+      }
+      if (s >= he) return false;
+      const uint32_t x = sbyte(st, s);
+      if (x == ' ' || x == '\t') {
+        v = s + 1;
+        continue;
+      }
+      if (x == '\r' && s + 1 < he && sbyte(st, s + 1) == '\n') break;
+      return false;
+    }
+    const uint32_t span = first == kAbsentSpan ? ((s - hs) << 16) : ((first - hs) << 16 | (lend - first));
+    const bool is_host = nl == 4 && lower4(squad(st, k)) == 0x74736F68u;  // "host"
+    if (is_host) {
+      if (!have_host) auth = span;  // the first value is the one the filter sees
+      have_host = true;
+    } else {
+      const int f = field_of_key(R, st, k, nl);
+      if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = span;  // first value wins
+    }
+    k = s + 2;
+  }
+  if (R.f_method >= 0) sp[R.f_method * stride] = m - hs;
+  if (R.f_path >= 0) sp[R.f_path * stride] = (t0 - hs) << 16 | (te - t0);
+  if (R.f_authority >= 0 && have_host) sp[R.f_authority * stride] = auth;
+  return true;
+}
+
 // Length of the walked string (http_pack.cc): values of the fields up to the
 // last present one, each SEP-terminated (absent: 0x01), then REST (0x02) if
 // any field after it is absent.
@@ -321,14 +467,21 @@ __device__ __forceinline__ uint32_t group_of(const HttpRawDev& R, uint32_t prog)
   return prog < R.nprogs ? prog : R.nprogs + (prog == kProgAllow ? 0u : 1u);
 }
 
-// Dynamic LDS of the scan and emit kernels: [spans: nfields × 256 u32]
-// [4 wave stages × kStage bytes][bucket counters/cursors: nkeys u32, when
-// they fit (lds_keys)].
+// Dynamic LDS of the scan kernel: [spans: nfields × 256 u32][4 wave stages ×
+// kStage bytes][4 wave mask pairs × 2 × kStage bits][tchar table: 256 B]
+// [bucket counters: nkeys u32, when they fit (lds_keys)].
 __device__ __forceinline__ uint8_t* wave_stage(uint32_t* lds, uint32_t F, uint32_t wave) {
   return reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + wave * kStage;
 }
+__device__ __forceinline__ uint32_t* wave_masks(uint32_t* lds, uint32_t F, uint32_t wave) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + 4 * kStage) +
+         wave * 2 * kMaskWords;
+}
+__device__ __forceinline__ uint8_t* tchar_table(uint32_t* lds, uint32_t F) {
+  return reinterpret_cast<uint8_t*>(wave_masks(lds, F, 4));
+}
 __device__ __forceinline__ uint32_t* key_counters(uint32_t* lds, uint32_t F) {
-  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + 4 * kStage);
+  return reinterpret_cast<uint32_t*>(tchar_table(lds, F) + 256);
 }
 // The head of request i as a reader: in the stage if it lies inside it.
 __device__ __forceinline__ HeadReader head_of(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
@@ -424,10 +577,13 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   const uint32_t F = max(R.nfields, 1u), wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* sp = lds + threadIdx.x;  // this lane's spans: sp[f * kRawThreads]
   uint8_t* stage = wave_stage(lds, F, wave);
+  uint32_t* masks = wave_masks(lds, F, wave);
+  uint8_t* tct = tchar_table(lds, F);
   uint32_t* lk = key_counters(lds, F);
   const uint32_t nk = (R.nprogs + 2) * kRawKeys;
   if (lds_keys)
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = 0;
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = !tchar(b);
   const uint64_t off0 = off[0];
   __syncthreads();
   for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
@@ -441,14 +597,22 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     const bool parse = live && prog != kProgDeny;
     uint32_t slen = 0;
     uint64_t sbase = 0;
-    if (__any(parse)) sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
+    if (__any(parse)) {
+      sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
+      wave_sync();
+      build_masks(stage, slen, tct, masks, lane);
+    }
     wave_sync();
     if (live) {
       uint32_t key = 0, len = 0, bad = 0;
       uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(off[i] - off0, i, cst));
       if (parse) {
         HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
-        if (!parse_head(R, hr, sp, kRawThreads)) {
+        // heads inside the stage parse over its masks, the rest byte by byte
+        const bool ok = hr.lp ? parse_head_masks(R, stage, masks, masks + kMaskWords, (uint32_t)(hr.lp - stage),
+                                                 (uint32_t)(hr.lp - stage) + hr.n, sp, kRawThreads)
+                              : parse_head(R, hr, sp, kRawThreads);
+        if (!ok) {
           bad = 1;
         } else if (walked(R, prog)) {
           uint32_t last;
@@ -640,7 +804,8 @@ unsigned grid_for(size_t n, int cus, unsigned per_cu) {
 // LDS of the scan / emit kernels (see wave_stage, key_counters)
 size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
-  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + (lds_keys ? nk * 4 : 0) +
+  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + 4 * 2 * (kStage / 8) + 256 +
+         (lds_keys ? nk * 4 : 0) +
          (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
 }
 // code maps in LDS only while small: a larger table costs workgroups per CU

@@ -7,6 +7,8 @@ HTTP packer, numpy records for L4/LPM, field lists for Kafka).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from .policy import (PortRuleHTTP, PortRuleKafka, get_http_rule, htons, network_policy, port_network_policy,
@@ -462,3 +464,163 @@ def kafka_requests(n: int, info: dict, seed: int = SEED):
         tps.append(ts)
     return dict(redirect=np.zeros(n, np.uint32), remote=remote, api_key=key, api_version=ver, kind=kind,
                 client_id=client, topics=tps)
+
+
+# ------------------------------------------- config 5, vectorized generator
+def _assemble(parts: list, n: int) -> tuple[np.ndarray, np.ndarray, list]:
+    """Concatenate per-row byte segments: parts = [(data [n, W] uint8, lens
+    [n])]; returns (blob, offsets, start offset of each part per row)."""
+    total = np.zeros(n, np.int64)
+    for _, ln in parts:
+        total += ln
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(total, out=off[1:])
+    out = np.empty(int(off[-1]), np.uint8)
+    pos = off[:-1].copy()
+    starts = []
+    for data, ln in parts:
+        starts.append(pos.copy())
+        w = data.shape[1]
+        if w:
+            mask = np.arange(w)[None, :] < ln[:, None]
+            out[(pos[:, None] + np.arange(w)[None, :])[mask]] = data[mask]
+        pos += ln
+    return out, off.astype(np.uint64), starts
+
+
+def _table(strs: list) -> tuple[np.ndarray, np.ndarray]:
+    enc = [s.encode() if isinstance(s, str) else s for s in strs]
+    w = max((len(s) for s in enc), default=0)
+    t = np.zeros((len(enc), max(w, 1)), np.uint8)
+    for i, s in enumerate(enc):
+        t[i, :len(s)] = np.frombuffer(s, np.uint8)
+    return t, np.array([len(s) for s in enc], np.int64)
+
+
+def _const(s: bytes, n: int):
+    return np.broadcast_to(np.frombuffer(s, np.uint8), (n, len(s))), np.full(n, len(s), np.int64)
+
+
+def _pick(table, idx):
+    t, ln = table
+    return t[idx], ln[idx]
+
+
+def http10k_requests_fast(n: int, info: dict, seed: int = SEED, raw: bool = False, chunk: int = 1 << 20):
+    """n distinct config-5 requests drawn as http10k_requests draws them (50%
+    crafted to hit a random rule, 50% near misses with one field mutated),
+    built with vectorized numpy instead of a per-request loop.  Returns the
+    header-list form (hdr_blob / hdr_off, as cg_http_pack takes it) or, with
+    raw=True, raw HTTP/1.1 heads (raw_blob / raw_off: request line, Host,
+    the rule's header, blank line)."""
+    meta, sel_ids = info["meta"], info["sel_ids"]
+    K = len(meta)
+    kind = np.array([m["kind"] for m in meta], np.int64)
+    port_of = np.array([m["port"] for m in meta], np.uint16)
+    sel_of = np.array([m["sel"] for m in meta], np.int64)
+    has_host = np.array([bool(m["rule"].Host) for m in meta])
+    mopts = {"GET": ["GET"], "POST": ["POST"], "PUT": ["PUT"], "DELETE": ["DELETE"], "GET|HEAD": ["GET", "HEAD"],
+             "P(UT|OST)": ["PUT", "POST"]}
+    mnames = ["GET", "POST", "PUT", "DELETE", "HEAD", "PATCH"]
+    m_a = np.array([mnames.index(mopts[m["rule"].Method][0]) for m in meta], np.int64)
+    m_b = np.array([mnames.index(mopts[m["rule"].Method][-1]) for m in meta], np.int64)
+    methods = _table(mnames)
+    ks = _table([str(m["k"]) for m in meta])
+    words = _table([m["word"] for m in meta])
+    hdr_names = _table([m["rule"].Headers[0].split(" ", 1)[0].rstrip(":") if m["rule"].Headers else "" for m in meta])
+    hdr_vals = _table([m["rule"].Headers[0].split(" ", 1)[1] if m["rule"].Headers else "" for m in meta])
+    has_hdr = np.array([bool(m["rule"].Headers) for m in meta])
+    hosts_rule = _table([f"svc{m['k']}.example.com" for m in meta])
+    hosts_rand = _table([f"h{i}.example.com" for i in range(100)])
+    evil = b"evil.example.com"
+    sel_tab = np.zeros((len(sel_ids), max(len(s) for s in sel_ids)), np.uint32)
+    sel_len = np.array([len(s) for s in sel_ids], np.int64)
+    for i, s in enumerate(sel_ids):
+        sel_tab[i, :len(s)] = s
+    def one_chunk(c0: int):
+        rng = np.random.default_rng([seed ^ 0xFA57, c0])
+        c = min(chunk, n - c0)
+        rix = rng.integers(0, K, c)
+        hit = rng.random(c) < 0.5
+        which = np.where(hit, -1, rng.integers(0, 4, c))
+        kd = kind[rix]
+        midx = np.where(rng.random(c) < 0.5, m_a[rix], m_b[rix])
+        midx = np.where(which == 0, mnames.index("PATCH"), midx)
+        letters = rng.integers(97, 123, (c, 40)).astype(np.uint8)
+        tail_len = np.where(kd == 0, rng.integers(0, 40, c), np.where(kd == 1, rng.integers(1, 24, c), 0))
+        digit = (rng.integers(1, 10, c) + 48).astype(np.uint8).reshape(c, 1)
+        js = rng.random(c) < 0.5
+        z = np.zeros(c, np.int64)
+        one = np.ones(c, np.int64)
+        # path = pre1 [digit] pre2 k "/" [tail | word] [ext] [mutation "/x"]
+        pre1 = np.where(kd == 0, 6, np.where(kd == 1, 8, 4))  # "/api/v" | "/static/" | "/svc"
+        pre1_tab = _table(["/api/v", "/static/", "/svc"])
+        kd_i = np.where(kd == 0, 0, np.where(kd == 1, 1, 2))
+        p1, _ = _pick(pre1_tab, kd_i)
+        p2 = _const(b"/svc", c)
+        ext_tab = _table(["", ".js", ".css"])
+        ext_i = np.where(kd == 1, np.where(js, 1, 2), 0)
+        kt, kl = _pick(ks, rix)
+        wt, wl = _pick(words, rix)
+        path_parts = [(p1, pre1), (digit, np.where(kd == 0, 1, 0)), (p2[0], np.where(kd == 0, 4, 0)),
+                      (kt, kl), (_const(b"/", c)[0], one),
+                      (letters, tail_len), (wt, np.where(kd == 2, wl, 0)), _pick(ext_tab, ext_i),
+                      (_const(b"/x", c)[0], np.where(which == 2, 2, 0))]
+        hr_t, hr_l = _pick(hosts_rule, rix)
+        hx_t, hx_l = _pick(hosts_rand, rng.integers(0, 100, c))
+        w = max(hr_t.shape[1], hx_t.shape[1], len(evil))
+        ht = np.zeros((c, w), np.uint8)
+        hl = np.where(has_host[rix], hr_l, hx_l)
+        ht[:, :hr_t.shape[1]] = np.where(has_host[rix][:, None], hr_t, 0)
+        ht[:, :hx_t.shape[1]] |= np.where(has_host[rix][:, None], 0, hx_t).astype(np.uint8)
+        ev = which == 3
+        ht[ev] = 0
+        ht[ev, :len(evil)] = np.frombuffer(evil, np.uint8)
+        hl = np.where(ev, len(evil), hl)
+        mt, ml = _pick(methods, midx)
+        hn_t, hn_l = _pick(hdr_names, rix)
+        hv_t, hv_l = _pick(hdr_vals, rix)
+        hh = has_hdr[rix]
+        if raw:
+            parts = [(mt, ml), _const(b" ", c)] + path_parts + [_const(b" HTTP/1.1\r\nHost: ", c), (ht, hl),
+                                                                 _const(b"\r\n", c),
+                                                                 (hn_t, np.where(hh, hn_l, 0)),
+                                                                 (_const(b": ", c)[0], np.where(hh, 2, 0)),
+                                                                 (hv_t, np.where(hh, hv_l, 0)),
+                                                                 (_const(b"\r\n", c)[0], np.where(hh, 2, 0)),
+                                                                 _const(b"\r\n", c)]
+            path_first = 2
+        else:
+            parts = [_const(b":method\0", c), (mt, ml), _const(b"\0:path\0", c)] + path_parts + \
+                    [_const(b"\0:authority\0", c), (ht, hl), _const(b"\0", c),
+                     (hn_t, np.where(hh, hn_l, 0)), (_const(b"\0", c)[0], np.where(hh, 1, 0)),
+                     (hv_t, np.where(hh, hv_l, 0)), (_const(b"\0", c)[0], np.where(hh, 1, 0))]
+            path_first = 3
+        blob, off, starts = _assemble(parts, c)
+        # near miss 1: one path byte (after the first) becomes '~'
+        plen = sum(ln for _, ln in path_parts)
+        m1 = which == 1
+        if m1.any():
+            at = starts[path_first][m1] + 1 + (rng.random(int(m1.sum())) * (plen[m1] - 1)).astype(np.int64)
+            blob[at] = ord("~")
+        s = sel_of[rix]
+        rem = sel_tab[s, (rng.random(c) * sel_len[s]).astype(np.int64)]
+        return blob, off, port_of[rix], rem
+
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max(1, min(8, os.cpu_count() or 1))) as ex:
+        res = list(ex.map(one_chunk, range(0, n, chunk)))
+    blobs, offs, base, ports, remotes = [], [], 0, [], []
+    for blob, off, pt, rem in res:
+        blobs.append(blob)
+        offs.append(off[:-1] + np.uint64(base))
+        base += int(off[-1])
+        ports.append(pt)
+        remotes.append(rem)
+    off = np.concatenate(offs + [np.array([base], np.uint64)]).astype(np.uint64)
+    blob = np.concatenate(blobs) if blobs else np.zeros(1, np.uint8)
+    key = ("raw_blob", "raw_off") if raw else ("hdr_blob", "hdr_off")
+    return {"policy": np.zeros(n, np.uint32), "ingress": np.ones(n, np.uint8),
+            "port": np.concatenate(ports) if ports else np.zeros(0, np.uint16),
+            "remote": np.concatenate(remotes).astype(np.uint32) if remotes else np.zeros(0, np.uint32),
+            key[0]: blob, key[1]: off}

@@ -332,6 +332,17 @@ int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* discovery_r
  * "PortNetworkPolicy: Duplicate port number", cilium_network_policy.h:160)
  * the previous snapshot stays and CG_POLICY_REJECTED is returned. */
 int cg_http_policy_update(uint64_t h, const char* npds_json, size_t len);
+/* The installed HTTP snapshot's compiled tables as a flat image (unions,
+ * DFAs, remote tables, program index; a checksum) and its import on another
+ * handle — another GPU or process — without recompiling: SURVEY §8(e)
+ * "the host compiles once and uploads identical images to each GPU"; also the
+ * serialized table cache (§5 checkpoint / resume).  Export with buf = NULL
+ * returns the size in *len.  Import is all-or-nothing like an update; an
+ * image from another library build is CG_POLICY_REJECTED.  Replaces the
+ * per-worker re-translation of NetworkPolicyMap::onConfigUpdate
+ * (envoy/cilium_network_policy.cc) with one compile per node. */
+int cg_http_policy_export(uint64_t h, void* buf, size_t cap, size_t* len);
+int cg_http_policy_import(uint64_t h, const void* buf, size_t len);
 
 /* The same update from the NPDS wire form: a serialized xDS
  * envoy.api.v2.DiscoveryResponse whose resources are google.protobuf.Any
@@ -404,6 +415,9 @@ size_t cg_http_batch_slots(uint64_t h, size_t n);
 #define CG_HTTP_F_MALFORMED 0x04u /* field holds a byte Envoy's codec rejects */
 #define CG_HTTP_F_PAD 0x08u
 
+/* Worker threads cg_http_pack uses for a large batch (CILIUM_GPU_PACK_THREADS,
+ * else the hardware threads, at most 16). */
+uint32_t cg_http_pack_threads(void);
 /* Pack n requests.  Request i: policy index policy[i] (UINT32_MAX unknown),
  * direction ingress[i], destination port port[i], remote identity
  * remote[i] (source identity on ingress, destination on egress,

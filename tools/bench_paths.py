@@ -248,6 +248,7 @@ def bench_http_host(torch, dev, stream, cl, args, threads):
     cg_http_verdicts_host (pinned staging → H2D → http_kernel → D2H →
     request order).  The kernel-only rate is bench.py's line."""
     import oracle
+    from cilium_amd import _native as N
     from cilium_amd import synth
     pols, info = synth.http10k_rules()
     cl.update_http_policy(pols)
@@ -275,7 +276,7 @@ def bench_http_host(torch, dev, stream, cl, args, threads):
     return {"metric": "HTTP host path, config 5: cg_http_pack + cg_http_verdicts_host", "value": n / (tp + te),
             "unit": "verdicts/s", "n_gpus": 1, "higher_is_better": True, "data": "synthetic",
             "pack": {"value": n / tp, "unit": "requests/s",
-                     "cores": int(os.environ.get("CILIUM_GPU_PACK_THREADS", "0")) or min(16, os.cpu_count() or 1),
+                     "cores": int(N.lib.cg_http_pack_threads()),
                      "header_MBps": hdr_bytes / tp / 1e6,
                      "ms": tp * 1e3},
             "verdicts_host": {"value": n / te, "unit": "verdicts/s", "ms": te * 1e3,
