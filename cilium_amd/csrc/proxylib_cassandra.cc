@@ -5,13 +5,14 @@
 // joined input (its capacity) is legal in Go, so a query length reaching into
 // the next frame reads that frame's bytes; past the joined input, or an index
 // past the frame, is a runtime panic — CassPanic here, PARSER_ERROR in the op
-// loop (connection.go:119-135).  Queries are lowered and split with ASCII
-// rules; the reference's Unicode case mapping and Unicode spaces (strings.
-// ToLower / strings.Fields) for query bytes >= 0x80 are not reproduced.
+// loop (connection.go:119-135).  Queries are lowered and split as Go does it
+// (strings.ToLower / strings.Fields over decoded runes, go_text.h).
 #include "proxylib_cassandra.h"
 
 #include <algorithm>
 #include <cstring>
+
+#include "go_text.h"
 
 namespace cg {
 
@@ -102,26 +103,6 @@ const char* opcode_name(uint8_t op) {  // opcodeMap (:285-302)
   }
 }
 
-bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
-
-std::string lower(std::string s) {
-  for (char& c : s)
-    if (c >= 'A' && c <= 'Z') c = (char)(c - 'A' + 'a');
-  return s;
-}
-
-std::vector<std::string> fields_of(const std::string& s) {  // strings.Fields
-  std::vector<std::string> out;
-  size_t i = 0;
-  while (i < s.size()) {
-    while (i < s.size() && is_space(s[i])) ++i;
-    const size_t b = i;
-    while (i < s.size() && !is_space(s[i])) ++i;
-    if (i > b) out.push_back(s.substr(b, i - b));
-  }
-  return out;
-}
-
 std::string trim_chars(const std::string& s, const char* cut) {  // strings.Trim
   size_t b = 0, e = s.size();
   while (b < e && strchr(cut, s[b])) ++b;
@@ -132,7 +113,7 @@ std::string trim_chars(const std::string& s, const char* cut) {  // strings.Trim
 // parseQuery (:344-455): {action, table}, action "" = unparseable.
 std::pair<std::string, std::string> parse_query(CassState& st, std::string query) {
   while (!query.empty() && query.back() == ';') query.pop_back();  // TrimRight(query, ";")
-  const std::vector<std::string> f = fields_of(lower(query));
+  const std::vector<std::string> f = go::fields(go::to_lower(query));  // :373
   for (const std::string& x : f)
     if (x.size() >= 2 && (x.compare(0, 2, "--") == 0 || x.compare(0, 2, "/*") == 0 || x.compare(0, 2, "//") == 0))
       return {"", ""};
@@ -142,14 +123,14 @@ std::pair<std::string, std::string> parse_query(CassState& st, std::string query
     for (size_t i = 1; i < f.size(); ++i)
       if (f[i] == "from") {
         if (i + 1 >= f.size()) throw CassPanic{};  // fields[i+1]
-        table = f[i + 1];
+        table = go::to_lower(f[i + 1]);  // :402
       }
     if (table.empty()) return {"", ""};
   } else if (action == "insert") {
     if (f.size() < 3) return {"", ""};
-    table = f[2];
+    table = go::to_lower(f[2]);  // :414
   } else if (action == "update") {
-    table = f[1];
+    table = go::to_lower(f[1]);  // :417
   } else if (action == "use") {
     st.keyspace = trim_chars(f[1], "\"\\'");
     table = st.keyspace;

@@ -7,6 +7,8 @@
 #include <cstring>
 #include <string_view>
 
+#include "go_text.h"
+
 namespace cg {
 
 const char kMcTextDenied[] = "CLIENT_ERROR access denied\r\n";
@@ -42,62 +44,7 @@ std::string join(const Input& in) {
   return s;
 }
 
-// ---- bytes.Fields: runs of unicode.IsSpace, UTF-8 decoded as Go does
-// (invalid or overlong sequences, surrogates: one RuneError byte)
-uint32_t decode_rune(const uint8_t* p, size_t n, size_t* w) {
-  const uint8_t c = p[0];
-  *w = 1;
-  if (c < 0x80) return c;
-  auto cont = [&](size_t i) { return i < n && (p[i] & 0xC0) == 0x80; };
-  if (c >= 0xC2 && c <= 0xDF && cont(1)) {
-    *w = 2;
-    return (uint32_t)(c & 0x1F) << 6 | (p[1] & 0x3F);
-  }
-  if (c >= 0xE0 && c <= 0xEF && cont(1) && cont(2)) {
-    if (c == 0xE0 && p[1] < 0xA0) return 0xFFFD;  // overlong
-    if (c == 0xED && p[1] > 0x9F) return 0xFFFD;  // surrogate
-    *w = 3;
-    return (uint32_t)(c & 0x0F) << 12 | (uint32_t)(p[1] & 0x3F) << 6 | (p[2] & 0x3F);
-  }
-  if (c >= 0xF0 && c <= 0xF4 && cont(1) && cont(2) && cont(3)) {
-    if (c == 0xF0 && p[1] < 0x90) return 0xFFFD;
-    if (c == 0xF4 && p[1] > 0x8F) return 0xFFFD;
-    *w = 4;
-    return (uint32_t)(c & 0x07) << 18 | (uint32_t)(p[1] & 0x3F) << 12 | (uint32_t)(p[2] & 0x3F) << 6 | (p[3] & 0x3F);
-  }
-  return 0xFFFD;
-}
-
-bool is_space(uint32_t r) {
-  switch (r) {
-    case '\t': case '\n': case '\v': case '\f': case '\r': case ' ': case 0x85: case 0xA0:
-    case 0x1680: case 0x2028: case 0x2029: case 0x202F: case 0x205F: case 0x3000:
-      return true;
-    default:
-      return r >= 0x2000 && r <= 0x200A;
-  }
-}
-
-std::vector<std::string> fields(std::string_view s) {
-  std::vector<std::string> out;
-  const uint8_t* p = (const uint8_t*)s.data();
-  size_t i = 0, start = 0;
-  bool in = false;
-  while (i < s.size()) {
-    size_t w;
-    const uint32_t r = decode_rune(p + i, s.size() - i, &w);
-    if (is_space(r)) {
-      if (in) out.emplace_back(s.substr(start, i - start));
-      in = false;
-    } else if (!in) {
-      in = true;
-      start = i;
-    }
-    i += w;
-  }
-  if (in) out.emplace_back(s.substr(start));
-  return out;
-}
+using go::fields;  // bytes.Fields over decoded runes (go_text.h)
 
 bool has_prefix(const std::string& s, const char* p) { return s.compare(0, strlen(p), p) == 0; }
 

@@ -13,12 +13,14 @@ Go runtime semantics it keeps: a frame is a slice of the joined input whose
 capacity runs to the end of that input (bytes.Join of one slice: an append to
 nil, capacity rounded to a Go 1.10 malloc size class and zero-filled), so
 slice expressions may read past the frame; index expressions past the frame,
-and slices past the capacity, panic → PARSER_ERROR.  Queries are handled with
-ASCII case folding and ASCII whitespace (the reference's Unicode rules for
-bytes >= 0x80 are not restated: parity unpinned for such queries).  Pinned by
+and slices past the capacity, panic → PARSER_ERROR.  Queries are lowered and
+split with Go's strings.ToLower / strings.Fields over decoded runes
+(memcache_ref.go_to_lower / go_fields; Go 1.10 = Unicode 10.0).  Pinned by
 the reference's cassandraparser_test.go cases (tests/golden/cassandra_kat.json).
 """
 from __future__ import annotations
+
+from .memcache_ref import go_fields, go_to_lower
 
 MORE, PASS, DROP, INJECT, ERROR = 0, 1, 2, 3, 4
 NOP = 256
@@ -75,25 +77,8 @@ class _Buf:
         return int.from_bytes(self.sl(lo, lo + 2), "big")
 
 
-_WS = b" \t\n\v\f\r"
-
-
-def _fields(b: bytes) -> list[bytes]:
-    out, cur = [], bytearray()
-    for ch in b:
-        if ch in _WS:
-            if cur:
-                out.append(bytes(cur))
-                cur = bytearray()
-        else:
-            cur.append(ch)
-    if cur:
-        out.append(bytes(cur))
-    return out
-
-
-def _lower(b: bytes) -> bytes:
-    return bytes(c + 32 if 65 <= c <= 90 else c for c in b)
+_fields = go_fields
+_lower = go_to_lower
 
 
 class Connection:
@@ -126,15 +111,15 @@ class Connection:
                 if f[i] == b"from":
                     if i + 1 >= len(f):
                         raise _Panic()
-                    table = f[i + 1]
+                    table = _lower(f[i + 1])
             if not table:
                 return b"", b""
         elif action == b"insert":
             if len(f) < 3:
                 return b"", b""
-            table = f[2]
+            table = _lower(f[2])
         elif action == b"update":
-            table = f[1]
+            table = _lower(f[1])
         elif action == b"use":
             self.keyspace = f[1].strip(b"\"\\'")
             table = self.keyspace

@@ -154,6 +154,49 @@ def go_fields(b: bytes) -> list[bytes]:
     return out
 
 
+# unicode.ToLower as Go 1.10 applies it (Unicode 10.0 simple mapping): the
+# first code point of Python's one-character lower() (U+0130's full mapping
+# starts with Go's U+0069), minus the case pairs Unicode 11-13 added.
+_POST_UNICODE_10 = ((0x1C90, 0x1CBF), (0x16E40, 0x16E5F), (0xA7B8, 0xA7CA), (0xA7F5, 0xA7F6))
+
+
+def go_lower_rune(r: int) -> int:
+    if r < 0x80:
+        return r + 32 if 65 <= r <= 90 else r
+    if 0xD800 <= r <= 0xDFFF or r > 0x10FFFF or any(lo <= r <= hi for lo, hi in _POST_UNICODE_10):
+        return r
+    return ord(chr(r).lower()[0])
+
+
+def _enc(r: int) -> bytes:
+    if 0xD800 <= r <= 0xDFFF or r > 0x10FFFF:
+        r = 0xFFFD
+    return chr(r).encode("utf-8")
+
+
+def go_to_lower(b: bytes) -> bytes:
+    """strings.ToLower (Go 1.10): ASCII lowered in place; otherwise
+    strings.Map(unicode.ToLower): bytes up to the first rune the mapping
+    changes are kept verbatim, every rune from there on is re-encoded (an
+    invalid byte becomes U+FFFD)."""
+    if all(c < 0x80 for c in b):
+        return bytes(c + 32 if 65 <= c <= 90 else c for c in b)
+    i = 0
+    while i < len(b):
+        r, w = _rune(b, i)
+        if go_lower_rune(r) != r:
+            break
+        i += w
+    if i == len(b):
+        return b
+    out = bytearray(b[:i])
+    while i < len(b):
+        r, w = _rune(b, i)
+        out += _enc(go_lower_rune(r))
+        i += w
+    return bytes(out)
+
+
 def go_atoi(s: bytes):
     """strconv.Atoi on a 64-bit platform: None on error."""
     t = s.decode("latin-1")

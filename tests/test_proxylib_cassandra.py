@@ -61,17 +61,26 @@ def test_oracle_query_parsing():
     assert _q(c, b"select") == (b"", b"")
     with pytest.raises(CR._Panic):
         _q(c, b"select a from")
+    # Go's Unicode rules (cassandraparser.go:373): NBSP / ideographic space
+    # separate fields, U+0130 lowers to "i", the rest re-encoded after a change
+    assert _q(c, "SELECT\u00a0a FROM\u3000ÜSERS".encode()) == (b"select", "ks.üsers".encode())
+    assert _q(c, "UPDATE İ.T SET".encode()) == (b"update", b"i.t")
+    assert _q(c, b"SELECT a FROM \xffX.\xc3\x9c") == (b"select", "\ufffdx.ü".encode())  # changed at 'S'
+    assert _q(c, b"select a from \xffX.t") == (b"select", b"\xffx.t")  # \xff before the first change
+    assert _q(c, b"select a from \xffx.t") == (b"select", b"\xffx.t")
 
 
 # ---- random frame streams ------------------------------------------------
-WORDS = [b"t", b"users", b"ks.t", b"system.local", b"Sys.Peers", b"a.b.c", b"'quoted'", b"x/y"]
+WORDS = [b"t", b"users", b"ks.t", b"system.local", b"Sys.Peers", b"a.b.c", b"'quoted'", b"x/y",
+         "ÜSERS".encode(), "Ks.İtem".encode(), "ks.Σ\u00a0x".encode(), b"\xffKS.T", "ks.t\u3000".encode()]
 QUERIES = [
     b"SELECT a FROM {t} WHERE k=1", b"select * from {t};", b"DELETE FROM {t} WHERE a=1", b"INSERT INTO {t} (a) VALUES (1)",
     b"UPDATE {t} SET a=1", b"USE {k}", b"use \"{k}\"", b"CREATE TABLE IF NOT EXISTS {t} (a int)", b"CREATE TABLE {t} (a int)",
     b"DROP TABLE IF EXISTS {t}", b"DROP TABLE {t}", b"CREATE KEYSPACE {k} WITH r", b"DROP KEYSPACE IF EXISTS {k}",
     b"ALTER TABLE {t} ADD x int", b"TRUNCATE {t}", b"truncate table {t}", b"CREATE INDEX ON {t}(a)",
     b"CREATE MATERIALIZED VIEW v AS SELECT", b"CREATE CUSTOM INDEX i ON {t}(a)", b"LIST ROLES", b"create role r",
-    b"Select A From {t}\tWhere", b"CREATE TABLE IF {t}",
+    b"Select A From {t}\tWhere", b"CREATE TABLE IF {t}", "SELECT\u2003a FROM {t}".encode(),
+    "UPDATE\u0085{t} SET".encode(),
 ]
 BAD_QUERIES = [b"GRANT ALL ON {t}", b"select * from", b"select a from {t} -- c", b"select", b"insert {t}",
                b"drop table if exists"]
@@ -208,7 +217,7 @@ def _rand_rules(rng):
             r["query_action"] = str(rng.choice(["select", "insert", "update", "delete", "use", "create-table",
                                                 "drop-table", "drop-keyspace", "alter-table", "truncate-table"]))
         if rng.random() < 0.7:
-            r["query_table"] = str(rng.choice(["^ks\\.", "t$", ".*", "system\\..*", "^\\.", "users", "a\\.b"]))
+            r["query_table"] = str(rng.choice(["^ks\\.", "t$", ".*", "system\\..*", "^\\.", "users", "a\\.b", "üsers", "ks\\.i"]))
         rules.append(r)
     return rules
 
