@@ -140,6 +140,8 @@ SIGNATURES = {
     "cg_http_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_http_verdicts_raw_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p, _p]),
     "cg_http_verdicts_raw_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p]),
+    "cg_http_verdicts_fields_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p, _p]),
+    "cg_http_verdicts_fields_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p]),
     "cg_kafka_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_kafka_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_kafka_intern": (C.c_int, [_u64, _u32, C.c_char_p, _sz, C.POINTER(_u32)]),

@@ -195,6 +195,17 @@ class Classifier:
     def http_verdicts_raw(self, policy, ingress, port, remote, raw_blob: np.ndarray, raw_off: np.ndarray) -> np.ndarray:
         """cg_http_verdicts_raw_host: raw HTTP/1.x heads → verdicts, parsed,
         packed and evaluated on the GPU (request order)."""
+        return self._verdicts_from_host(N.lib.cg_http_verdicts_raw_host, policy, ingress, port, remote, raw_blob,
+                                        raw_off)
+
+    def http_verdicts_fields(self, policy, ingress, port, remote, hdr_blob: np.ndarray,
+                             hdr_off: np.ndarray) -> np.ndarray:
+        """cg_http_verdicts_fields_host: cg_http_pack header lists → verdicts,
+        grouped, packed and evaluated on the GPU (request order)."""
+        return self._verdicts_from_host(N.lib.cg_http_verdicts_fields_host, policy, ingress, port, remote, hdr_blob,
+                                        hdr_off)
+
+    def _verdicts_from_host(self, fn, policy, ingress, port, remote, raw_blob, raw_off) -> np.ndarray:
         raw_blob = np.ascontiguousarray(raw_blob, np.uint8)
         raw_off = np.ascontiguousarray(raw_off, np.uint64)
         n = len(raw_off) - 1
@@ -205,8 +216,7 @@ class Classifier:
         prt = np.ascontiguousarray(port, np.uint16)
         rem = np.ascontiguousarray(remote, np.uint32)
         out = np.zeros(max(n, 1), np.uint8)
-        N.check(N.lib.cg_http_verdicts_raw_host(self.h, _p(raw_blob), _p(raw_off), n, _p(pol), _p(ing), _p(prt),
-                                                _p(rem), _p(out)))
+        N.check(fn(self.h, _p(raw_blob), _p(raw_off), n, _p(pol), _p(ing), _p(prt), _p(rem), _p(out)))
         return out[:n]
 
     def http_verdicts_raw_dev(self, d_raw, d_off, n: int, d_policy, d_ingress, d_port, d_remote, d_out,
@@ -214,6 +224,12 @@ class Classifier:
         """cg_http_verdicts_raw_dev on device tensors (synchronizes `stream`)."""
         N.check(N.lib.cg_http_verdicts_raw_dev(self.h, _p(d_raw), _p(d_off), n, _p(d_policy), _p(d_ingress),
                                                _p(d_port), _p(d_remote), _p(d_out), stream))
+
+    def http_verdicts_fields_dev(self, d_blob, d_off, n: int, d_policy, d_ingress, d_port, d_remote, d_out,
+                                 stream=None) -> None:
+        """cg_http_verdicts_fields_dev on device tensors (synchronizes `stream`)."""
+        N.check(N.lib.cg_http_verdicts_fields_dev(self.h, _p(d_blob), _p(d_off), n, _p(d_policy), _p(d_ingress),
+                                                  _p(d_port), _p(d_remote), _p(d_out), stream))
 
     def http_verdicts(self, b: "HttpBatch") -> np.ndarray:
         """Verdicts (1 allow / 0 deny) in request order, computed on the GPU."""

@@ -7,6 +7,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -924,8 +925,24 @@ int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d
       fail(CG_INVALID_ARGUMENT, "NULL device array");
     e->set_device();
     auto lease = e->staging.acquire(e->device);
-    http_verdicts_raw_on(*s, *lease, e->cus, d_raw, d_raw_off, n, d_policy, d_ingress, d_port, d_remote, d_out,
-                         stream_of(*e, stream));
+    http_verdicts_raw_on(*s, *lease, e->cus, RawInput::Heads, d_raw, d_raw_off, n, d_policy, d_ingress, d_port,
+                         d_remote, d_out, stream_of(*e, stream));
+  });
+}
+
+int cg_http_verdicts_fields_dev(uint64_t h, const uint8_t* d_hdr_blob, const uint64_t* d_hdr_off, size_t n,
+                                const uint32_t* d_policy, const uint8_t* d_ingress, const uint16_t* d_port,
+                                const uint32_t* d_remote, uint8_t* d_out, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = http_snap(*e);
+    if (n && (!d_hdr_off || !d_policy || !d_ingress || !d_port || !d_remote || !d_out))
+      fail(CG_INVALID_ARGUMENT, "NULL device array");
+    e->set_device();
+    auto lease = e->staging.acquire(e->device);
+    http_verdicts_raw_on(*s, *lease, e->cus, RawInput::Lists, d_hdr_blob, d_hdr_off, n, d_policy, d_ingress, d_port,
+                         d_remote, d_out, stream_of(*e, stream));
   });
 }
 
@@ -1189,36 +1206,117 @@ int cg_kafka_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* r
   });
 }
 
+// Requests from host memory through the device path.  A large call runs in
+// chunks of ~kHostChunkBytes on two workers, each with its own lease
+// (pinned buffers + stream): while one worker copies its chunk into pinned
+// memory (several threads) the other's chunk is on the bus or the GPU.
+constexpr size_t kHostChunkBytes = (size_t)160 << 20;
+
+static void run_host_chunk(const HttpSnapshot& s, Engine& e, StagingSlot& sl, RawInput in, const uint8_t* raw,
+                           const uint64_t* raw_off, size_t a, size_t b, const uint32_t* policy,
+                           const uint8_t* ingress, const uint16_t* port, const uint32_t* remote, uint8_t* out,
+                           unsigned copy_threads) {
+  const size_t m = b - a;
+  const uint64_t base = raw_off[a], bytes = raw_off[b] - base;
+  const auto st = (hipStream_t)sl.stream;
+  uint8_t* h_raw = (uint8_t*)sl.host_buf(0, bytes);
+  uint64_t* h_off = (uint64_t*)sl.host_buf(1, (m + 1) * 8);
+  uint32_t* h_pol = (uint32_t*)sl.host_buf(2, m * 4);
+  uint8_t* h_ing = (uint8_t*)sl.host_buf(3, m);
+  uint16_t* h_port = (uint16_t*)sl.host_buf(4, m * 2);
+  uint32_t* h_rem = (uint32_t*)sl.host_buf(5, m * 4);
+  // the copies, split over threads by request ranges
+  auto copy = [&](size_t i0, size_t i1) {
+    const uint64_t b0 = raw_off[a + i0] - base, b1 = raw_off[a + i1] - base;
+    if (b1 > b0) memcpy(h_raw + b0, raw + base + b0, b1 - b0);
+    for (size_t i = i0; i < i1; ++i) h_off[i] = raw_off[a + i] - base;  // rebased to the staged bytes
+    memcpy(h_pol + i0, policy + a + i0, (i1 - i0) * 4);
+    memcpy(h_ing + i0, ingress + a + i0, i1 - i0);
+    memcpy(h_port + i0, port + a + i0, (i1 - i0) * 2);
+    memcpy(h_rem + i0, remote + a + i0, (i1 - i0) * 4);
+  };
+  const unsigned nt = m < 65536 ? 1u : copy_threads;
+  if (nt <= 1) {
+    copy(0, m);
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back(copy, m * t / nt, m * (t + 1) / nt);
+    for (auto& x : th) x.join();
+  }
+  h_off[m] = bytes;
+  auto h2d = [&](int i, const void* hsrc, size_t nb) {
+    void* d = sl.dev_buf(i, nb);
+    if (nb) hip_check(hipMemcpyAsync(d, hsrc, nb, hipMemcpyHostToDevice, st), "H2D");
+    return d;
+  };
+  const uint8_t* d_raw = (const uint8_t*)h2d(0, h_raw, bytes);
+  const uint64_t* d_off = (const uint64_t*)h2d(1, h_off, (m + 1) * 8);
+  const uint32_t* d_pol = (const uint32_t*)h2d(2, h_pol, m * 4);
+  const uint8_t* d_ing = (const uint8_t*)h2d(3, h_ing, m);
+  const uint16_t* d_port = (const uint16_t*)h2d(4, h_port, m * 2);
+  const uint32_t* d_rem = (const uint32_t*)h2d(5, h_rem, m * 4);
+  uint8_t* d_out = (uint8_t*)sl.dev_buf(6, m);
+  http_verdicts_raw_on(s, sl, e.cus, in, d_raw, d_off, m, d_pol, d_ing, d_port, d_rem, d_out, st);
+  uint8_t* ho = (uint8_t*)sl.host_buf(6, m);
+  hip_check(hipMemcpyAsync(ho, d_out, m, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  memcpy(out + a, ho, m);
+}
+
+static void verdicts_raw_from_host(uint64_t h, RawInput in, const uint8_t* raw, const uint64_t* raw_off, size_t n,
+                                   const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                                   const uint32_t* remote, uint8_t* out) {
+  auto e = get(h);
+  e->require_gpu();
+  auto s = http_snap(*e);
+  if (!n) return;
+  check_offsets(raw_off, n);
+  if (!policy || !ingress || !port || !remote || !out || (raw_off[n] != raw_off[0] && !raw))
+    fail(CG_INVALID_ARGUMENT, "NULL raw/policy/ingress/port/remote/out");
+  const uint64_t total = raw_off[n] - raw_off[0] + 19 * (uint64_t)n;
+  const size_t nchunks = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(n / 4096 + 1, total / kHostChunkBytes + 1));
+  const unsigned nw = nchunks > 1 ? 2u : 1u;
+  const unsigned copy_threads = std::max(1u, cg_http_pack_threads() / nw);
+  std::exception_ptr err;
+  std::mutex mu;
+  auto worker = [&](unsigned w) {
+    try {
+      e->set_device();
+      auto lease = e->staging.acquire(e->device);
+      for (size_t k = w; k < nchunks; k += nw) {
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          if (err) return;
+        }
+        run_host_chunk(*s, *e, *lease, in, raw, raw_off, n * k / nchunks, n * (k + 1) / nchunks, policy, ingress,
+                       port, remote, out, copy_threads);
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+    }
+  };
+  if (nw == 1) {
+    worker(0);
+  } else {
+    std::thread t1(worker, 1u);
+    worker(0);
+    t1.join();
+  }
+  if (err) std::rethrow_exception(err);
+}
+
 int cg_http_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off, size_t n,
                               const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                               const uint32_t* remote, uint8_t* out) {
-  return guarded([&] {
-    auto e = get(h);
-    e->require_gpu();
-    auto s = http_snap(*e);
-    if (!n) return;
-    check_offsets(raw_off, n);
-    if (!policy || !ingress || !port || !remote || !out || (raw_off[n] && !raw))
-      fail(CG_INVALID_ARGUMENT, "NULL raw/policy/ingress/port/remote/out");
-    e->set_device();
-    auto lease = e->staging.acquire(e->device);
-    const auto st = (hipStream_t)lease->stream;
-    // offsets rebased to the staged bytes
-    std::vector<uint64_t> off(raw_off, raw_off + n + 1);
-    for (auto& o : off) o -= raw_off[0];
-    const uint8_t* d_raw = (const uint8_t*)stage_in(*lease, 0, raw + raw_off[0], off[n]);
-    const uint64_t* d_off = (const uint64_t*)stage_in(*lease, 1, off.data(), (n + 1) * 8);
-    const uint32_t* d_pol = (const uint32_t*)stage_in(*lease, 2, policy, n * 4);
-    const uint8_t* d_ing = (const uint8_t*)stage_in(*lease, 3, ingress, n);
-    const uint16_t* d_port = (const uint16_t*)stage_in(*lease, 4, port, n * 2);
-    const uint32_t* d_rem = (const uint32_t*)stage_in(*lease, 5, remote, n * 4);
-    uint8_t* d_out = (uint8_t*)lease->dev_buf(6, n);
-    http_verdicts_raw_on(*s, *lease, e->cus, d_raw, d_off, n, d_pol, d_ing, d_port, d_rem, d_out, st);
-    uint8_t* ho = (uint8_t*)lease->host_buf(6, n);
-    hip_check(hipMemcpyAsync(ho, d_out, n, hipMemcpyDeviceToHost, st), "D2H");
-    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-    memcpy(out, ho, n);
-  });
+  return guarded([&] { verdicts_raw_from_host(h, RawInput::Heads, raw, raw_off, n, policy, ingress, port, remote, out); });
+}
+
+int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
+                                 const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                                 const uint32_t* remote, uint8_t* out) {
+  return guarded(
+      [&] { verdicts_raw_from_host(h, RawInput::Lists, hdr_blob, hdr_off, n, policy, ingress, port, remote, out); });
 }
 
 // ------------------------------------------------------------ counters ----

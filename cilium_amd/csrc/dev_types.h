@@ -243,6 +243,11 @@ struct HttpDev {
 constexpr uint32_t kRawMaxFields = 32;
 constexpr uint32_t kRawMaxHead = 61440;
 constexpr uint32_t kRawKeys = 10;  // bucket key: walked units 0..8, 9 = overflow arena
+// The same machinery takes cg_http_pack's "name\0value\0" header lists
+// (cg_http_verdicts_fields_*): value spans are 16-bit offsets into a
+// request's list, so one list holds at most kFieldsMaxList bytes (Envoy's
+// headers past its 60 KiB default limit never reach the filter).
+constexpr uint32_t kFieldsMaxList = 65535;
 struct HttpRawDev {
   const uint32_t* phash_keys;  // (policy << 17 | ingress << 16 | port) → program
   const uint32_t* phash_vals;
@@ -262,6 +267,8 @@ struct HttpRawDev {
   // <= 8), field, name offset, 0}; nkmask + 1 slots
   const uint32_t* nkeys;
   uint32_t nkmask;
+  uint32_t raw_values;  // proxylib snapshot: header lists carry escaped values (http_pack.cc)
+  int32_t f_empty;      // field index of the empty name, or -1 (header lists only)
 };
 // The key of a lowercase header name b[0, nl): its length, its first 8 bytes
 // and (nl > 8) its last 8 bytes, little-endian, zero past the name.

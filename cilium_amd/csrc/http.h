@@ -41,11 +41,12 @@ struct HttpSnapshot {
 
   DevMem d_progs, d_parts, d_cells, d_dflt, d_counters;
   HttpDev dev{};
-  // raw HTTP/1 heads on the device (http_raw.cc): set by upload when the
-  // snapshot qualifies (not proxylib, at most kRawMaxFields fields)
+  // raw HTTP/1 heads and header lists on the device (http_raw.cc): tables
+  // set by upload when the snapshot has at most kRawMaxFields fields; raw
+  // heads also need a non-proxylib snapshot
   DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes, d_nkeys;
   HttpRawDev raw{};
-  bool raw_ok = false;
+  bool raw_ok = false, lists_ok = false;
   LaunchFence fence;  // last member: queued kernels finish before the buffers go (engine.h)
 
   void upload(Engine& e);
@@ -65,10 +66,13 @@ std::shared_ptr<HttpSnapshot> http_image_import(const uint8_t* p, size_t n);
 std::string npds_pb_to_json(const uint8_t* p, size_t n, bool strict_utf8);
 
 // The raw-head path (http_raw.cc): device tables (called by upload), and
-// verdicts for n raw HTTP/1 request heads already in device memory, in
-// request order, on `stream` with the lease's workspace (synchronizes it).
+// verdicts for n requests already in device memory, in request order, on
+// `stream` with the lease's workspace (synchronizes it).  Request i is
+// d_raw[d_off[i], d_off[i+1]): an HTTP/1 head (RawInput::Heads) or a
+// cg_http_pack header list "name\0value\0..." (RawInput::Lists).
+enum class RawInput { Heads, Lists };
 void http_raw_upload(HttpSnapshot& S);
-void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const uint8_t* d_raw,
+void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawInput in, const uint8_t* d_raw,
                           const uint64_t* d_off, size_t n, const uint32_t* d_policy, const uint8_t* d_ingress,
                           const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, void* stream);
 

@@ -25,12 +25,13 @@ uint32_t next_pow2(uint32_t x) {
 }  // namespace
 
 void http_raw_upload(HttpSnapshot& S) {
-  S.raw_ok = false;
+  S.raw_ok = S.lists_ok = false;
   S.raw = HttpRawDev{};
   const uint32_t F = (uint32_t)S.fields.size();
-  if (S.raw_values || F > kRawMaxFields) return;  // proxylib snapshots take escaped values, not heads
+  if (F > kRawMaxFields) return;
   HttpRawDev& R = S.raw;
-  R.f_method = R.f_path = R.f_authority = -1;
+  R.f_method = R.f_path = R.f_authority = R.f_empty = -1;
+  R.raw_values = S.raw_values ? 1u : 0u;
   const uint32_t cap = next_pow2(std::max<uint32_t>(2 * F, 4));
   std::vector<uint32_t> slots(4 * (size_t)cap, 0);
   std::vector<uint8_t> names;
@@ -39,7 +40,10 @@ void http_raw_upload(HttpSnapshot& S) {
     if (nm == ":method") R.f_method = (int32_t)f;
     else if (nm == ":path") R.f_path = (int32_t)f;
     else if (nm == ":authority") R.f_authority = (int32_t)f;
-    if (nm.empty() || nm[0] == ':') continue;  // pseudo headers never come from a header line
+    else if (nm.empty()) R.f_empty = (int32_t)f;
+    // pseudo headers are in the tables for header lists; a head's header line
+    // never names one (':' is not a token byte)
+    if (nm.empty()) continue;
     uint32_t h = kRawFnvInit;
     for (unsigned char c : nm) h = raw_fnv(h, (uint8_t)((c >= 'A' && c <= 'Z') ? c + 32 : c));
     uint32_t sl = h & (cap - 1);
@@ -56,7 +60,7 @@ void http_raw_upload(HttpSnapshot& S) {
   std::vector<uint32_t> nk(8 * (size_t)cap, 0);
   for (uint32_t f = 0; f < F; ++f) {
     const std::string& nm = S.fields[f];
-    if (nm.empty() || nm[0] == ':') continue;
+    if (nm.empty()) continue;
     const uint32_t nl = (uint32_t)nm.size();
     auto byte = [&](uint32_t j) -> uint32_t {
       const unsigned char c = (unsigned char)nm[j];
@@ -102,15 +106,19 @@ void http_raw_upload(HttpSnapshot& S) {
   R.codes = S.d_codes.as<uint8_t>();
   R.nkeys = S.d_nkeys.as<uint32_t>();
   R.nkmask = cap - 1;
-  S.raw_ok = true;
+  S.lists_ok = true;
+  S.raw_ok = !S.raw_values;  // proxylib snapshots take escaped values, not heads
 }
 
-void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const uint8_t* d_raw,
+void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawInput in, const uint8_t* d_raw,
                           const uint64_t* d_off, size_t n, const uint32_t* d_policy, const uint8_t* d_ingress,
                           const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, void* stream) {
-  if (!s.raw_ok)
-    fail(CG_UNSUPPORTED, "raw HTTP/1 heads: the snapshot has more than " + std::to_string(kRawMaxFields) +
-                             " header fields, or is a proxylib snapshot");
+  const bool lists = in == RawInput::Lists;
+  if (lists ? !s.lists_ok : !s.raw_ok)
+    fail(CG_UNSUPPORTED, lists ? "header lists on the device: the snapshot has more than " +
+                                     std::to_string(kRawMaxFields) + " header fields"
+                               : "raw HTTP/1 heads: the snapshot has more than " + std::to_string(kRawMaxFields) +
+                                     " header fields, or is a proxylib snapshot");
   if (!n) return;
   const hipStream_t st = (hipStream_t)stream;
   const uint32_t np = (uint32_t)s.progs.size(), G = np + 2, K = kRawKeys;
@@ -139,8 +147,8 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   if (sbytes / 16 >= (1ull << 32)) {
     if (n < 2) fail(CG_INVALID_ARGUMENT, "raw head too large");
     const size_t h = n / 2;
-    http_verdicts_raw_on(s, sl, cus, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
-    http_verdicts_raw_on(s, sl, cus, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
+    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
+    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
                          d_out + h, stream);
     return;
   }
@@ -152,8 +160,8 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   const uint32_t nblk = (uint32_t)http_raw_grid(n, cus);
   uint32_t* bcount = lds_keys ? (uint32_t*)sl.dev_buf(16, (size_t)G * K * nblk * 4) : hist;
   uint32_t* bbase = lds_keys ? (uint32_t*)sl.dev_buf(17, (size_t)G * K * nblk * 4) : nullptr;
-  hip_check(launch_http_raw_scan(s.raw, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, d_remote, sbuf,
-                                 cst, ovf, st, cus),
+  hip_check(launch_http_raw_scan(s.raw, lists, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, d_remote,
+                                 sbuf, cst, ovf, st, cus),
             "raw scan kernel launch");
   if (lds_keys)
     hip_check(launch_http_raw_prefix(bcount, G * K, nblk, bbase, hist, st), "raw prefix kernel launch");
@@ -162,14 +170,17 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, const
   const uint32_t* hc = (const uint32_t*)hh;
   unsigned long long ovf_bytes;
   memcpy(&ovf_bytes, hh + hist_bytes, 8);
+  if (ovf_bytes & kRawListTooLong)
+    fail(CG_INVALID_ARGUMENT, "a header list beyond " + std::to_string(kFieldsMaxList) +
+                                  " bytes (evaluate it with cg_http_pack)");
   if (ovf_bytes / 16 >= (1ull << 24)) {
     // the meta word holds arena offsets / 16 in 24 bits: a batch whose long
     // strings need more than 256 MiB of arena runs as two halves (one head
     // is at most kRawMaxHead bytes, so halving always ends)
     if (n < 2) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
     const size_t h = n / 2;
-    http_verdicts_raw_on(s, sl, cus, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
-    http_verdicts_raw_on(s, sl, cus, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
+    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
+    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
                          d_out + h, stream);
     return;
   }

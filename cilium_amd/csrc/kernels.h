@@ -41,10 +41,13 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
 // them into per-block slot offsets (bbase) and totals (hist); otherwise the
 // scan adds into a global histogram (counts = hist) and the rank takes slots
 // from global cursors.  sbuf: the request-ordered string buffer
-// (records per request, http_raw.cc), cst its per-request stride.
+// (records per request, http_raw.cc), cst its per-request stride.  lists:
+// the requests are cg_http_pack header lists instead of HTTP/1 heads (a list
+// longer than kFieldsMaxList sets kRawListTooLong in *ovf_bytes).
+constexpr unsigned long long kRawListTooLong = 1ull << 63;
 size_t http_raw_grid(size_t n, int cus);
 bool http_raw_lds_keys(const HttpRawDev& R);
-int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
+int launch_http_raw_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
                          void* rinfo, const uint32_t* remote, uint8_t* sbuf, uint32_t cst,
                          unsigned long long* ovf_bytes, void* stream, int cus);

@@ -427,6 +427,113 @@ __device__ __forceinline__ bool parse_head_masks(const HttpRawDev& R, const uint
   return true;
 }
 
+// ---- header lists (cg_http_pack input): "name\0value\0" pairs ----------
+// http_pack.cc semantics: names compare case-insensitively (ASCII), the first
+// value of a name wins, a value byte the codec rejects (or, proxylib
+// snapshots, a raw byte <= 0x02 / a bad 0x03 escape pair) flags the request
+// malformed; a pair cut short by the list's end has what it has.
+__device__ __forceinline__ bool list_stop(uint32_t c, bool raw_values) {  // ends a plain run of value bytes
+  return raw_values ? c <= 3 : ((c < 0x20 && c != 0x09) || c == 0x7F);  // both include the NUL terminator
+}
+__device__ __forceinline__ uint32_t zero4(uint32_t x) {  // bit per zero byte
+  return pack4(~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u);
+}
+// masks: `stop` (list_stop, from the table tct) and `zero` (NUL)
+__device__ __forceinline__ void build_masks_lists(const uint8_t* stage, uint32_t slen, const uint8_t* tct,
+                                                  uint32_t* masks, uint32_t lane) {
+  for (uint32_t w = lane; w * 32 < slen; w += 64) {
+    const uint4 a = *reinterpret_cast<const uint4*>(stage + 32 * w);
+    const uint4 b = *reinterpret_cast<const uint4*>(stage + 32 * w + 16);
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t st = 0, zr = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      zr |= zero4(d[k]) << (4 * k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st |= (uint32_t)tct[(d[k] >> (8 * j)) & 0xFFu] << (4 * k + j);
+    }
+    masks[w] = st;
+    masks[kMaskWords + w] = zr;
+  }
+}
+
+// The value bytes [v, e) of a proxylib snapshot's list: false when one is a
+// raw byte <= 0x02 or a 0x03 not followed by 0x10..0x14 (http_pack.cc).
+template <class Byte, class NextStop>
+__device__ __forceinline__ bool escapes_ok(uint32_t v, uint32_t e, Byte byte, NextStop next_stop) {
+  bool ok = true;
+  for (uint32_t s = next_stop(v, e); s < e;) {
+    if (byte(s) <= 2) {
+      ok = false;
+      s = next_stop(s + 1, e);
+      continue;
+    }
+    const uint32_t y = s + 1 < e ? byte(s + 1) : 0u;  // 0x03: an escape pair
+    if (y < 0x10 || y > 0x14) ok = false;
+    const uint32_t nx = s + (s + 1 < e ? 2u : 1u);
+    s = nx < e ? next_stop(nx, e) : e;
+  }
+  return ok;
+}
+
+// A list inside the stage, bytes [hs, he), over its masks.
+__device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const uint8_t* st, const uint32_t* mstop,
+                                                 const uint32_t* mzero, uint32_t hs, uint32_t he, uint32_t* sp,
+                                                 uint32_t stride) {
+  for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
+  bool ok = true;
+  for (uint32_t k = hs; k < he;) {
+    const uint32_t ne = next_set(mzero, k, he), nl = ne - k;
+    const uint32_t v = ne < he ? ne + 1 : he;
+    uint32_t e;
+    if (!R.raw_values) {
+      const uint32_t s = v < he ? next_set(mstop, v, he) : he;
+      e = s;
+      if (s < he && sbyte(st, s) != 0) {  // a byte the codec rejects
+        ok = false;
+        e = next_set(mzero, s, he);
+      }
+    } else {
+      e = v < he ? next_set(mzero, v, he) : he;
+      ok &= escapes_ok(
+          v, e, [&](uint32_t x) { return sbyte(st, x); }, [&](uint32_t x, uint32_t lim) { return next_set(mstop, x, lim); });
+    }
+    const int f = nl ? field_of_key(R, st, k, nl) : R.f_empty;
+    if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = (v - hs) << 16 | (e - v);  // first value wins
+    k = e < he ? e + 1 : he;
+  }
+  return ok;
+}
+
+// A list outside the stage, byte by byte.
+__device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, HeadReader& hr, uint32_t* sp, uint32_t stride) {
+  for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
+  const uint32_t n = hr.n;
+  bool ok = true;
+  for (uint32_t k = 0; k < n;) {
+    uint32_t c = k, h = kRawFnvInit;
+    for (uint32_t x; c < n && (x = hr.at(c)) != 0; ++c) h = raw_fnv(h, (uint8_t)lower(x));
+    const uint32_t nl = c - k, v = c < n ? c + 1 : n;
+    uint32_t e = v;
+    while (e < n && hr.at(e) != 0) ++e;
+    if (!R.raw_values) {
+      for (uint32_t j = v; j < e; ++j)
+        if (list_stop(hr.at(j), false)) ok = false;
+    } else {
+      ok &= escapes_ok(
+          v, e, [&](uint32_t x) { return hr.at(x); },
+          [&](uint32_t x, uint32_t lim) {
+            while (x < lim && hr.at(x) > 3) ++x;
+            return x;
+          });
+    }
+    const int f = nl ? field_of(R, hr, h, nl, k) : R.f_empty;
+    if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = v << 16 | (e - v);
+    k = e < n ? e + 1 : n;
+  }
+  return ok;
+}
+
 // Length of the walked string (http_pack.cc): values of the fields up to the
 // last present one, each SEP-terminated (absent: 0x01), then REST (0x02) if
 // any field after it is absent.
@@ -562,7 +669,8 @@ __device__ __forceinline__ uint64_t rec_off(uint64_t head_rel, size_t i, uint32_
 
 // ---- pass 1: parse, program, string length, bucket key, the request's
 // record in the string buffer; per-block bucket counts (bcount[key * gridDim.x + block],
-// lds_keys) or a global histogram
+// lds_keys) or a global histogram.  kLists: header lists, not heads.
+template <bool kLists>
 __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, const uint8_t* __restrict__ raw,
                                                                const uint64_t* __restrict__ off, size_t n,
                                                                const uint32_t* __restrict__ policy,
@@ -583,7 +691,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   const uint32_t nk = (R.nprogs + 2) * kRawKeys;
   if (lds_keys)
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = 0;
-  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = !tchar(b);
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = kLists ? list_stop(b, R.raw_values) : !tchar(b);
   const uint64_t off0 = off[0];
   __syncthreads();
   for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
@@ -600,7 +708,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     if (__any(parse)) {
       sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
       wave_sync();
-      build_masks(stage, slen, tct, masks, lane);
+      if (kLists) build_masks_lists(stage, slen, tct, masks, lane);
+      else build_masks(stage, slen, tct, masks, lane);
     }
     wave_sync();
     if (live) {
@@ -608,10 +717,21 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
       uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(off[i] - off0, i, cst));
       if (parse) {
         HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
-        // heads inside the stage parse over its masks, the rest byte by byte
-        const bool ok = hr.lp ? parse_head_masks(R, stage, masks, masks + kMaskWords, (uint32_t)(hr.lp - stage),
-                                                 (uint32_t)(hr.lp - stage) + hr.n, sp, kRawThreads)
-                              : parse_head(R, hr, sp, kRawThreads);
+        // heads / lists inside the stage parse over its masks, the rest byte by byte
+        const uint32_t hs = (uint32_t)(hr.lp - stage);
+        bool ok;
+        if (kLists) {
+          if (hr.n > kFieldsMaxList) {  // spans would not fit: the call fails
+            atomicOr(ovf_bytes, kRawListTooLong);
+            ok = false;
+          } else {
+            ok = hr.lp ? parse_list_masks(R, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
+                       : parse_list_bytes(R, hr, sp, kRawThreads);
+          }
+        } else {
+          ok = hr.lp ? parse_head_masks(R, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
+                     : parse_head(R, hr, sp, kRawThreads);
+        }
         if (!ok) {
           bad = 1;
         } else if (walked(R, prog)) {
@@ -818,17 +938,17 @@ size_t http_raw_grid(size_t n, int cus) { return grid_for(n, cus, 4); }
 
 bool http_raw_lds_keys(const HttpRawDev& R) { return ((size_t)R.nprogs + 2) * kRawKeys * 4 <= 32 * 1024; }
 
-int launch_http_raw_scan(const HttpRawDev& R, const uint8_t* raw, const uint64_t* off, size_t n,
+int launch_http_raw_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
                          void* rinfo, const uint32_t* remote, uint8_t* sbuf, uint32_t cst,
                          unsigned long long* ovf_bytes, void* stream, int cus) {
   if (!n) return 0;
   const bool lk = http_raw_lds_keys(R);
   const size_t lds = raw_lds(R, lk, false);
-  (void)hipFuncSetAttribute((const void*)raw_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(raw_scan_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
-                     (hipStream_t)stream, R, raw, off, n, policy, ingress, port, counts, (uint2*)rinfo, remote, sbuf,
-                     cst, ovf_bytes, (uint32_t)lk);
+  auto kern = lists ? raw_scan_kernel<true> : raw_scan_kernel<false>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(kern, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw,
+                     off, n, policy, ingress, port, counts, (uint2*)rinfo, remote, sbuf, cst, ovf_bytes, (uint32_t)lk);
   return (int)hipGetLastError();
 }
 

@@ -470,6 +470,27 @@ int cg_http_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* ra
                               const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                               const uint32_t* remote, uint8_t* out);
 
+/* Parsed header lists to verdicts on the device: the input of cg_http_pack
+ * (request i's "name\0value\0" pairs in d_hdr_blob[d_hdr_off[i] ..
+ * d_hdr_off[i+1]), names case-insensitive, first value wins, the codec's
+ * value check — the header map AccessFilter::decodeHeaders sees,
+ * envoy/cilium_l7policy.cc:127-182) grouped, sorted and packed by the raw
+ * path's kernels instead of on the host, then cg_http_verdicts_dev; d_out[i]
+ * = 1 allow, 0 deny, request order.  Proxylib snapshots take escaped values
+ * as cg_http_pack does.  One request's list holds at most 65535 bytes
+ * (CG_INVALID_ARGUMENT beyond; Envoy's default header limit is 60 KiB).
+ * Stream and synchronization as cg_http_verdicts_raw_dev; CG_UNSUPPORTED when
+ * the snapshot walks more than 32 header fields. */
+int cg_http_verdicts_fields_dev(uint64_t h, const uint8_t* d_hdr_blob, const uint64_t* d_hdr_off, size_t n,
+                                const uint32_t* d_policy, const uint8_t* d_ingress, const uint16_t* d_port,
+                                const uint32_t* d_remote, uint8_t* d_out, void* stream);
+
+/* cg_http_verdicts_fields_dev from host memory (staged in, verdicts copied
+ * out): the drop-in for cg_http_pack + cg_http_verdicts_host. */
+int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
+                                 const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                                 const uint32_t* remote, uint8_t* out);
+
 /* NetworkPolicyMap::Allowed per slot (cilium_network_policy.h:223-237):
  * d_out[slot] = 1 allow, 0 deny (→ 403), in batch slot order.  d_arena may
  * be NULL when no record overflowed.  Per-(policy,direction,port) allowed/

@@ -250,15 +250,16 @@ def test_gpu_raw_arena_split():
 
 @pytest.mark.gpu
 def test_gpu_raw_header_name_keys(gpu):
-    """Header names of every length 1..40 referenced by rules, sent in mixed
+    """Header names of lengths 1..64 referenced by rules, sent in mixed
     case, among names that share length, first 8 and last 8 bytes with a rule
     name (the structural parser's name key: the middle is verified) — on the
     device against the host path and the oracle."""
     import random
     rng = random.Random(7)
-    names = ["".join(rng.choice("abcdefghijklmnopqrstuvwxyz-0123456789") for _ in range(L)) for L in range(1, 41)]
-    names += ["x-aaaaaaaa-1-bbbbbbbb", "x-aaaaaaaa-2-bbbbbbbb", "X-Long-Header-Name-For-Key-Tests"]
-    rules = [{"headers": [{"name": nm.lower(), "exact_match": "v%d" % i}]} for i, nm in enumerate(names)]
+    lengths = list(range(1, 21)) + [23, 26, 29, 32, 35, 38, 40, 47, 64]  # 29 + 3 below: the 32-field limit
+    names = ["".join(rng.choice("abcdefghijklmnopqrstuvwxyz-0123456789") for _ in range(L)) for L in lengths]
+    names += ["x-aaaaaaaa-1-bbbbbbbb", "x-aaaaaaaa-2-bbbbbbbb", "x-long-header-name-for-key-tests"]
+    rules = [{"headers": [{"name": nm, "exact_match": "v%d" % i}]} for i, nm in enumerate(names)]
     pols = [{"name": "p", "policy": 0, "ingress_per_port_policies": [
         {"port": 80, "rules": [{"remote_policies": [], "http_rules": {"http_rules": rules}}]}]}]
     gpu.update_http_policy(pols)
@@ -269,7 +270,7 @@ def test_gpu_raw_header_name_keys(gpu):
         for _ in range(rng.randint(0, 4)):
             nm = rng.choice(names + decoys)
             nm = "".join(c.upper() if rng.random() < 0.5 else c for c in nm)
-            i = names.index(nm.lower()) if nm.lower() in [x.lower() for x in names] else 0
+            i = names.index(nm.lower()) if nm.lower() in names else 0
             val = "v%d" % (i if rng.random() < 0.7 else rng.randint(0, len(names)))
             hs.append(b"%s:%s%s" % (nm.encode(), rng.choice([b"", b" ", b"\t "]), val.encode()))
         raws.append(b"GET /x HTTP/1.1\r\n" + b"".join(h + b"\r\n" for h in hs) + b"\r\n")

@@ -329,6 +329,74 @@ def bench_http_raw(torch, dev, stream, cl, args, threads):
                  "request_gbps": n * (tot / D) / sec / 1e9})
 
 
+def bench_http_fields(torch, dev, stream, cl, args, threads):
+    """Config 5 requests as parsed header lists (cg_http_pack's input, the
+    header map Envoy's filter sees) → verdicts with the grouping, sorting and
+    packing on the GPU (kernels_http_raw.hip list mode + http_kernel):
+    * device entry: 124.5M lists resident in HBM, cg_http_verdicts_fields_dev,
+      HIP-event timed;
+    * host entry: 8M lists in host memory, cg_http_verdicts_fields_host
+      (pinned staging on 2 workers, H2D, kernels, D2H), wall clock, against
+      the host packer path (cg_http_pack + cg_http_verdicts_host) on the same
+      lists."""
+    import oracle
+    from cilium_amd import synth
+    pols, info = synth.http10k_rules()
+    cl.update_http_policy(pols)
+    D, reps = 1 << 20, 119
+    rq = synth.http10k_requests_fast(D, info, seed=synth.SEED ^ 0xF1E1D)
+    blob, off = rq["hdr_blob"], rq["hdr_off"]
+    args_ = (rq["policy"], rq["ingress"], rq["port"], rq["remote"])
+    want = cl.http_verdicts(cl.pack_http(*args_, blob, off))
+    k = 20_000
+    exp = oracle.HttpOracle(pols).eval(*(np.asarray(a)[:k] for a in args_), blob, off[:k + 1], nthreads=threads)
+    assert np.array_equal(want[:k], exp), "host-path verdicts differ from the oracle"
+    tot = int(off[-1])
+    d_blob = tile_dev(torch, np.asarray(blob[:tot]), reps, dev)
+    base = torch.arange(reps, dtype=torch.int64, device=dev).unsqueeze(1) * tot
+    d_off = torch.cat([(torch.from_numpy(off[:-1].astype(np.int64)).to(dev).unsqueeze(0) + base).reshape(-1),
+                       torch.tensor([tot * reps], dtype=torch.int64, device=dev)])
+    rep = lambda a, dt: tile_dev(torch, np.asarray(a).astype(dt), reps, dev)
+    d_pol, d_ing, d_port, d_rem = rep(args_[0], np.uint32), rep(args_[1], np.uint8), rep(args_[2], np.uint16), \
+        rep(args_[3], np.uint32)
+    n = D * reps
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    run = lambda: cl.http_verdicts_fields_dev(d_blob, d_off, n, d_pol, d_ing, d_port, d_rem, d_out,
+                                              stream=stream.cuda_stream)
+    sec = timed(torch, stream, run, args.steps, 1)
+    assert bool((d_out.view(reps, D) == torch.from_numpy(want).to(dev).unsqueeze(0)).all()), \
+        "device list-path verdicts differ from the host path"
+    del d_blob, d_off, d_pol, d_ing, d_port, d_rem, d_out
+    torch.cuda.empty_cache()
+    # host entry on 8M lists (8 distinct 1M pools)
+    H = 8 * D
+    hq = synth.http10k_requests_fast(H, info, seed=synth.SEED ^ 0x8E1D)
+    hargs = (hq["policy"], hq["ingress"], hq["port"], hq["remote"], hq["hdr_blob"], hq["hdr_off"])
+    got = cl.http_verdicts_fields(*hargs)  # warm (pinned buffers, workers)
+    t_host = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        got = cl.http_verdicts_fields(*hargs)
+        t_host.append(time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    ref = cl.http_verdicts(cl.pack_http(*hargs))
+    t_pack_path = time.perf_counter() - t0
+    assert np.array_equal(got, ref), "host-entry list-path verdicts differ from the host packer path"
+    th = min(t_host)
+    hbytes = int(hq["hdr_off"][-1])
+    bpi = tot / D + 4 + 1 + 2 + 4 + 8 + 1  # list bytes, policy/ingress/port/remote, offset, verdict
+    return line("HTTP header lists → verdicts/s, packing on the GPU (cg_http_verdicts_fields_dev), config 5", n, sec,
+                bpi, "raw_scan(lists)+raw_rank+raw_build+http_kernel", None, "", threads,
+                {"config": {"workload": f"BASELINE config 5 requests as header lists ({tot / D:.1f} B/list avg), "
+                            "10K rules, 1M distinct tiled", "requests": n},
+                 "host_entry": {"value": H / th, "unit": "verdicts/s", "ms": th * 1e3, "requests": H,
+                                "list_bytes": hbytes, "staged_GBps": (hbytes + 19 * H) / th / 1e9,
+                                "note": "cg_http_verdicts_fields_host: lists in host memory, pinned staging on 2 "
+                                        "workers, H2D, kernels, D2H (PCIe-inclusive)"},
+                 "host_packer_path": {"value": H / t_pack_path, "unit": "verdicts/s", "ms": t_pack_path * 1e3,
+                                      "note": "cg_http_pack (CPU) + cg_http_verdicts_host on the same lists"}})
+
+
 def bench_ipcache(torch, dev, stream, cl, args, threads):
     import oracle
     from cilium_amd import synth
@@ -498,7 +566,8 @@ def main():
     cl = Classifier(device=0)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
-           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire, "httphost": bench_http_host, "httpraw": bench_http_raw}
+           "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire, "httphost": bench_http_host, "httpraw": bench_http_raw,
+           "httpfields": bench_http_fields}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()
