@@ -267,6 +267,8 @@ struct HttpRawDev {
   // <= 8), field, name offset, 0}; nkmask + 1 slots
   const uint32_t* nkeys;
   uint32_t nkmask;
+  uint32_t fnames_bytes;  // size of fnames
+  const uint32_t* walk_bits;  // bit p: program p is walked (not allow-all)
   uint32_t raw_values;  // proxylib snapshot: header lists carry escaped values (http_pack.cc)
   int32_t f_empty;      // field index of the empty name, or -1 (header lists only)
 };

@@ -44,7 +44,7 @@ struct HttpSnapshot {
   // raw HTTP/1 heads and header lists on the device (http_raw.cc): tables
   // set by upload when the snapshot has at most kRawMaxFields fields; raw
   // heads also need a non-proxylib snapshot
-  DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes, d_nkeys;
+  DevMem d_phk, d_phv, d_fslots, d_fnames, d_codes, d_nkeys, d_walk;
   HttpRawDev raw{};
   bool raw_ok = false, lists_ok = false;
   LaunchFence fence;  // last member: queued kernels finish before the buffers go (engine.h)

@@ -91,6 +91,10 @@ void http_raw_upload(HttpSnapshot& S) {
   S.d_fslots.upload_vec(slots);
   S.d_fnames.upload_vec(names);
   S.d_codes.upload_vec(codes);
+  std::vector<uint32_t> walk((S.progs.size() + 31) / 32 + 1, 0);
+  for (size_t p = 0; p < S.progs.size(); ++p)
+    if (!(S.progs[p].flags & kProgAllowAll)) walk[p / 32] |= 1u << (p % 32);
+  S.d_walk.upload_vec(walk);
   S.d_nkeys.upload_vec(nk);
   R.phash_keys = S.d_phk.as<uint32_t>();
   R.phash_vals = S.d_phv.as<uint32_t>();
@@ -103,8 +107,10 @@ void http_raw_upload(HttpSnapshot& S) {
   R.fmask = cap - 1;
   R.fslots = S.d_fslots.as<uint32_t>();
   R.fnames = S.d_fnames.as<uint8_t>();
+  R.fnames_bytes = (uint32_t)names.size();
   R.codes = S.d_codes.as<uint8_t>();
   R.nkeys = S.d_nkeys.as<uint32_t>();
+  R.walk_bits = S.d_walk.as<uint32_t>();
   R.nkmask = cap - 1;
   S.lists_ok = true;
   S.raw_ok = !S.raw_values;  // proxylib snapshots take escaped values, not heads

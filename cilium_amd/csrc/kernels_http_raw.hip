@@ -26,6 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
+#include <type_traits>
 
 #include "../../include/cilium_gpu.h"
 #include "dev_types.h"
@@ -37,6 +40,30 @@ namespace {
 
 constexpr int kRawThreads = 256;
 constexpr uint32_t kAbsentSpan = 0xFFFFFFFFu;
+
+// Explicit address spaces for the scan's LDS stage, bitmaps, spans and tables
+// and for the heads in HBM: through generic pointers every stage access
+// compiled to a flat load (waiting on vmcnt like an HBM load).
+#define CG_LDS __attribute__((address_space(3)))
+#define CG_GLB __attribute__((address_space(1)))
+typedef CG_LDS uint8_t lds_u8;
+typedef CG_LDS uint32_t lds_u32;
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));  // (HIP's uint4 class takes no address space)
+typedef CG_LDS v4u32 lds_v4;
+typedef const CG_GLB v4u32 glb_v4;
+__device__ __forceinline__ uint4 to_uint4(v4u32 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ v4u32 to_v4(uint4 v) { return v4u32{v.x, v.y, v.z, v.w}; }
+typedef const CG_GLB uint8_t glb_u8;
+typedef const CG_GLB uint32_t glb_u32;
+// The lookup tables of the scan (name keys, field slots, names, program
+// hash): staged in LDS when they fit, else read from HBM.
+template <class P32, class P8>
+struct RawTabs {
+  P32 nkeys, fslots, phk, phv, walk;
+  P8 fnames;
+};
+using LdsTabs = RawTabs<const lds_u32*, const lds_u8*>;
+using GlbTabs = RawTabs<glb_u32*, glb_u8*>;
 
 // RFC 7230 tchar as two 64-bit masks (bytes 0..63, 64..127)
 constexpr uint64_t tchar_lo() {
@@ -72,21 +99,22 @@ __device__ __forceinline__ bool all_plain(uint32_t q) {
 // block kept in registers (blocks reaching outside the head are assembled
 // from byte loads of the head's own bytes).
 struct HeadReader {
-  const uint8_t* p;
+  glb_u8* p;
   uint32_t n;
-  const uint8_t* lp;  // the head in LDS, or nullptr
+  const lds_u8* lp;  // the head in LDS (in)
+  bool in;
   uint64_t cur;
   uint4 w;
-  __device__ __forceinline__ HeadReader(const uint8_t* p_, uint32_t n_, const uint8_t* lp_)
-      : p(p_), n(n_), lp(lp_), cur(~0ull), w{0, 0, 0, 0} {}
+  __device__ __forceinline__ HeadReader(glb_u8* p_, uint32_t n_, const lds_u8* lp_, bool in_)
+      : p(p_), n(n_), lp(lp_), in(in_), cur(~0ull), w{0, 0, 0, 0} {}
   // bytes k..k+3 (little-endian; bytes past the head are unspecified): from
   // LDS two aligned dword reads and a byte align, so a walk pays one LDS
   // round trip per 4 bytes instead of one per byte
   __device__ __forceinline__ uint32_t quad(uint32_t k) {
-    if (lp) {
-      const uintptr_t a = (uintptr_t)(lp + k);
-      const uint32_t* w4 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-      return __builtin_amdgcn_alignbyte(w4[1], w4[0], (uint32_t)(a & 3));
+    if (in) {
+      const uint32_t a = (uint32_t)(uintptr_t)(lp + k);
+      const lds_u32* w4 = (const lds_u32*)(uintptr_t)(a & ~3u);
+      return __builtin_amdgcn_alignbyte(w4[1], w4[0], a & 3u);
     }
     uint32_t q = 0;  // global: never past the head (it may end the buffer)
 #pragma unroll
@@ -95,20 +123,20 @@ struct HeadReader {
     return q;
   }
   __device__ __forceinline__ uint32_t at(uint32_t k) {
-    if (lp) return lp[k];
+    if (in) return lp[k];
     const uint64_t a = (uint64_t)(uintptr_t)(p + k);
     const uint64_t blk = a & ~15ull;
     if (blk != cur) {
       cur = blk;
       const uint64_t lo = (uint64_t)(uintptr_t)p, hi = lo + n;
       if (blk >= lo && blk + 16 <= hi) {
-        w = *reinterpret_cast<const uint4*>((uintptr_t)blk);
+        w = to_uint4(*(glb_v4*)(uintptr_t)blk);
       } else {
         uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
 #pragma unroll
         for (int b = 0; b < 16; ++b) {
           const uint64_t x = blk + b;
-          const uint32_t byte = (x >= lo && x < hi) ? *reinterpret_cast<const uint8_t*>((uintptr_t)x) : 0u;
+          const uint32_t byte = (x >= lo && x < hi) ? *(glb_u8*)(uintptr_t)x : 0u;
           const uint32_t sh = (b & 3) * 8;
           if (b < 4) v0 |= byte << sh;
           else if (b < 8) v1 |= byte << sh;
@@ -137,8 +165,8 @@ struct HeadReader {
 // (8 KiB: 1.69, 6 KiB: 2.01, 4 KiB: 1.12 G requests/s on config 5)
 constexpr uint32_t kStage = 6144;
 constexpr uint32_t kMaskWords = kStage / 32;  // u32 words per structural mask of a stage
-__device__ __forceinline__ uint64_t stage_heads(const uint8_t* __restrict__ raw, uint64_t lo, uint64_t hi,
-                                                uint8_t* stage, uint32_t lane, uint32_t* len) {
+__device__ __forceinline__ uint64_t stage_heads(glb_u8* raw, uint64_t lo, uint64_t hi, lds_u8* stage, uint32_t lane,
+                                                uint32_t* len) {
   const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
   const uint64_t a0 = glo & ~15ull;
   const uint32_t nb = (uint32_t)min<uint64_t>((ghi - a0 + 15) & ~15ull, kStage);
@@ -146,13 +174,13 @@ __device__ __forceinline__ uint64_t stage_heads(const uint8_t* __restrict__ raw,
     const uint64_t a = a0 + j;
     uint4 v;
     if (a >= glo && a + 16 <= ghi) {
-      v = *reinterpret_cast<const uint4*>((uintptr_t)a);
+      v = to_uint4(*(glb_v4*)(uintptr_t)a);
     } else {
       uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
 #pragma unroll
       for (int b = 0; b < 16; ++b) {
         const uint64_t x = a + b;
-        const uint32_t byte = (x >= glo && x < ghi) ? *reinterpret_cast<const uint8_t*>((uintptr_t)x) : 0u;
+        const uint32_t byte = (x >= glo && x < ghi) ? *(glb_u8*)(uintptr_t)x : 0u;
         const uint32_t sh = (b & 3) * 8;
         if (b < 4) v0 |= byte << sh;
         else if (b < 8) v1 |= byte << sh;
@@ -161,7 +189,7 @@ __device__ __forceinline__ uint64_t stage_heads(const uint8_t* __restrict__ raw,
       }
       v = make_uint4(v0, v1, v2, v3);
     }
-    *reinterpret_cast<uint4*>(stage + j) = v;
+    *(lds_v4*)(stage + j) = to_v4(v);
   }
   *len = nb;
   return a0;
@@ -176,14 +204,16 @@ __device__ __forceinline__ void wave_sync() {
 
 // The field a header name (lowercase FNV-1a h, length nl, at head offset k)
 // is, or -1.
-__device__ __forceinline__ int field_of(const HttpRawDev& R, HeadReader& hr, uint32_t h, uint32_t nl, uint32_t k) {
+template <class Tabs>
+__device__ __forceinline__ int field_of(const HttpRawDev& R, const Tabs& T, HeadReader& hr, uint32_t h, uint32_t nl,
+                                        uint32_t k) {
   uint32_t sl = h & R.fmask;
   for (uint32_t probe = 0; probe <= R.fmask; ++probe) {
-    const uint4 e = reinterpret_cast<const uint4*>(R.fslots)[sl];
+    const uint4 e = make_uint4(T.fslots[4 * sl], T.fslots[4 * sl + 1], T.fslots[4 * sl + 2], T.fslots[4 * sl + 3]);
     if (e.y == 0) return -1;
     if (e.x == h && e.y == nl) {
       bool eq = true;
-      for (uint32_t j = 0; j < nl && eq; ++j) eq = lower(hr.at(k + j)) == R.fnames[e.w + j];
+      for (uint32_t j = 0; j < nl && eq; ++j) eq = lower(hr.at(k + j)) == T.fnames[e.w + j];
       if (eq) return (int)e.z;
     }
     sl = (sl + 1) & R.fmask;
@@ -194,7 +224,9 @@ __device__ __forceinline__ int field_of(const HttpRawDev& R, HeadReader& hr, uin
 // parse_head (http_parse.cc) for one head: the value span {start << 16 |
 // length} of every field it sets in sp[f * stride] (kAbsentSpan otherwise);
 // false = the codec rejects the head.
-__device__ __forceinline__ bool parse_head(const HttpRawDev& R, HeadReader& hr, uint32_t* sp, uint32_t stride) {
+template <class Tabs>
+__device__ __forceinline__ bool parse_head(const HttpRawDev& R, const Tabs& T, HeadReader& hr, lds_u32* sp,
+                                           uint32_t stride) {
   for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
   const uint32_t n = hr.n;
   if (n > kRawMaxHead) return false;
@@ -271,7 +303,7 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, HeadReader& hr, 
       if (!have_host) auth = span;  // the first value is the one the filter sees
       have_host = true;
     } else {
-      const int f = field_of(R, hr, h, nl, k);
+      const int f = field_of(R, T, hr, h, nl, k);
       if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = span;  // first value wins
     }
     k = v + 2;
@@ -298,11 +330,11 @@ __device__ __forceinline__ uint32_t special4(uint32_t x) {
   const uint32_t del = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;  // byte == 0x7F
   return pack4(lt | del);
 }
-__device__ __forceinline__ void build_masks(const uint8_t* stage, uint32_t slen, const uint8_t* tct, uint32_t* masks,
+__device__ __forceinline__ void build_masks(const lds_u8* stage, uint32_t slen, const lds_u8* tct, lds_u32* masks,
                                             uint32_t lane) {
   for (uint32_t w = lane; w * 32 < slen; w += 64) {
-    const uint4 a = *reinterpret_cast<const uint4*>(stage + 32 * w);
-    const uint4 b = *reinterpret_cast<const uint4*>(stage + 32 * w + 16);
+    const uint4 a = to_uint4(*(const lds_v4*)(stage + 32 * w));
+    const uint4 b = to_uint4(*(const lds_v4*)(stage + 32 * w + 16));
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     uint32_t sp = 0, nt = 0;
 #pragma unroll
@@ -316,7 +348,7 @@ __device__ __forceinline__ void build_masks(const uint8_t* stage, uint32_t slen,
   }
 }
 // First set bit at or after p (stage offsets), or lim when none before lim.
-__device__ __forceinline__ uint32_t next_set(const uint32_t* m, uint32_t p, uint32_t lim) {
+__device__ __forceinline__ uint32_t next_set(const lds_u32* m, uint32_t p, uint32_t lim) {
   uint32_t w = p >> 5;
   uint32_t x = m[w] & (0xFFFFFFFFu << (p & 31));
   while (!x) {
@@ -325,9 +357,9 @@ __device__ __forceinline__ uint32_t next_set(const uint32_t* m, uint32_t p, uint
   }
   return min(32 * w + (uint32_t)__builtin_ctz(x), lim);
 }
-__device__ __forceinline__ uint32_t sbyte(const uint8_t* st, uint32_t p) { return st[p]; }
-__device__ __forceinline__ uint32_t squad(const uint8_t* st, uint32_t p) {
-  const uint32_t* w4 = reinterpret_cast<const uint32_t*>(st + (p & ~3u));
+__device__ __forceinline__ uint32_t sbyte(const lds_u8* st, uint32_t p) { return st[p]; }
+__device__ __forceinline__ uint32_t squad(const lds_u8* st, uint32_t p) {
+  const lds_u32* w4 = (const lds_u32*)(st + (p & ~3u));
   return __builtin_amdgcn_alignbyte(w4[1], w4[0], p & 3u);
 }
 __device__ __forceinline__ uint32_t lower4(uint32_t x) {  // ASCII A-Z → a-z, per byte (bytes < 0x80)
@@ -342,7 +374,9 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t x, uint32_t nb) {
 // The field a header name (stage bytes [k, k + nl)) is, or -1: the lowercase
 // (length, first 8, last 8) key in R.nkeys (raw_name_key), the bytes between
 // verified for longer names.
-__device__ __forceinline__ int field_of_key(const HttpRawDev& R, const uint8_t* st, uint32_t k, uint32_t nl) {
+template <class Tabs>
+__device__ __forceinline__ int field_of_key(const HttpRawDev& R, const Tabs& T, const lds_u8* st, uint32_t k,
+                                            uint32_t nl) {
   uint32_t lo0 = lower4(keep_bytes(squad(st, k), nl)), lo1 = 0, hi0 = 0, hi1 = 0;
   if (nl > 4) lo1 = lower4(keep_bytes(squad(st, k + 4), nl - 4));
   if (nl > 8) {
@@ -351,13 +385,14 @@ __device__ __forceinline__ int field_of_key(const HttpRawDev& R, const uint8_t* 
   }
   uint32_t sl = raw_name_hash(nl, lo0, lo1, hi0, hi1) & R.nkmask;
   for (uint32_t probe = 0; probe <= R.nkmask; ++probe) {
-    const uint4 e = reinterpret_cast<const uint4*>(R.nkeys)[2 * sl];
-    if (e.x == 0) return -1;
-    const uint4 f = reinterpret_cast<const uint4*>(R.nkeys)[2 * sl + 1];
-    if (e.x == nl && e.y == lo0 && e.z == lo1 && e.w == hi0 && f.x == hi1) {
+    const uint32_t e0 = T.nkeys[8 * sl];
+    if (e0 == 0) return -1;
+    if (e0 == nl && T.nkeys[8 * sl + 1] == lo0 && T.nkeys[8 * sl + 2] == lo1 && T.nkeys[8 * sl + 3] == hi0 &&
+        T.nkeys[8 * sl + 4] == hi1) {
+      const uint32_t name_off = T.nkeys[8 * sl + 6];
       bool eq = true;
-      for (uint32_t j = 8; j + 8 < nl && eq; ++j) eq = lower(sbyte(st, k + j)) == R.fnames[f.z + j];
-      if (eq) return (int)f.y;
+      for (uint32_t j = 8; j + 8 < nl && eq; ++j) eq = lower(sbyte(st, k + j)) == T.fnames[name_off + j];
+      if (eq) return (int)T.nkeys[8 * sl + 5];
     }
     sl = (sl + 1) & R.nkmask;
   }
@@ -366,9 +401,10 @@ __device__ __forceinline__ int field_of_key(const HttpRawDev& R, const uint8_t* 
 
 // parse_head over the stage with the structural masks: the head is stage
 // bytes [hs, he).  Same results as parse_head (http_parse.cc semantics).
-__device__ __forceinline__ bool parse_head_masks(const HttpRawDev& R, const uint8_t* st, const uint32_t* msp,
-                                                 const uint32_t* mnt, uint32_t hs, uint32_t he, uint32_t* sp,
-                                                 uint32_t stride) {
+template <class Tabs>
+__device__ __forceinline__ bool parse_head_masks(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
+                                                 const lds_u32* msp, const lds_u32* mnt, uint32_t hs, uint32_t he,
+                                                 lds_u32* sp, uint32_t stride) {
   for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
   if (he - hs > kRawMaxHead) return false;
   const uint32_t m = next_set(mnt, hs, he);  // method: a tchar run, then SP
@@ -416,7 +452,7 @@ __device__ __forceinline__ bool parse_head_masks(const HttpRawDev& R, const uint
       if (!have_host) auth = span;  // the first value is the one the filter sees
       have_host = true;
     } else {
-      const int f = field_of_key(R, st, k, nl);
+      const int f = field_of_key(R, T, st, k, nl);
       if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = span;  // first value wins
     }
     k = s + 2;
@@ -439,11 +475,11 @@ __device__ __forceinline__ uint32_t zero4(uint32_t x) {  // bit per zero byte
   return pack4(~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u);
 }
 // masks: `stop` (list_stop, from the table tct) and `zero` (NUL)
-__device__ __forceinline__ void build_masks_lists(const uint8_t* stage, uint32_t slen, const uint8_t* tct,
-                                                  uint32_t* masks, uint32_t lane) {
+__device__ __forceinline__ void build_masks_lists(const lds_u8* stage, uint32_t slen, const lds_u8* tct,
+                                                  lds_u32* masks, uint32_t lane) {
   for (uint32_t w = lane; w * 32 < slen; w += 64) {
-    const uint4 a = *reinterpret_cast<const uint4*>(stage + 32 * w);
-    const uint4 b = *reinterpret_cast<const uint4*>(stage + 32 * w + 16);
+    const uint4 a = to_uint4(*(const lds_v4*)(stage + 32 * w));
+    const uint4 b = to_uint4(*(const lds_v4*)(stage + 32 * w + 16));
     const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     uint32_t st = 0, zr = 0;
 #pragma unroll
@@ -477,9 +513,10 @@ __device__ __forceinline__ bool escapes_ok(uint32_t v, uint32_t e, Byte byte, Ne
 }
 
 // A list inside the stage, bytes [hs, he), over its masks.
-__device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const uint8_t* st, const uint32_t* mstop,
-                                                 const uint32_t* mzero, uint32_t hs, uint32_t he, uint32_t* sp,
-                                                 uint32_t stride) {
+template <class Tabs>
+__device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
+                                                 const lds_u32* mstop, const lds_u32* mzero, uint32_t hs, uint32_t he,
+                                                 lds_u32* sp, uint32_t stride) {
   for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
   bool ok = true;
   for (uint32_t k = hs; k < he;) {
@@ -498,7 +535,7 @@ __device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const uint
       ok &= escapes_ok(
           v, e, [&](uint32_t x) { return sbyte(st, x); }, [&](uint32_t x, uint32_t lim) { return next_set(mstop, x, lim); });
     }
-    const int f = nl ? field_of_key(R, st, k, nl) : R.f_empty;
+    const int f = nl ? field_of_key(R, T, st, k, nl) : R.f_empty;
     if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = (v - hs) << 16 | (e - v);  // first value wins
     k = e < he ? e + 1 : he;
   }
@@ -506,7 +543,9 @@ __device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const uint
 }
 
 // A list outside the stage, byte by byte.
-__device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, HeadReader& hr, uint32_t* sp, uint32_t stride) {
+template <class Tabs>
+__device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, const Tabs& T, HeadReader& hr, lds_u32* sp,
+                                                 uint32_t stride) {
   for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
   const uint32_t n = hr.n;
   bool ok = true;
@@ -527,7 +566,7 @@ __device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, HeadReader
             return x;
           });
     }
-    const int f = nl ? field_of(R, hr, h, nl, k) : R.f_empty;
+    const int f = nl ? field_of(R, T, hr, h, nl, k) : R.f_empty;
     if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = v << 16 | (e - v);
     k = e < n ? e + 1 : n;
   }
@@ -537,7 +576,7 @@ __device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, HeadReader
 // Length of the walked string (http_pack.cc): values of the fields up to the
 // last present one, each SEP-terminated (absent: 0x01), then REST (0x02) if
 // any field after it is absent.
-__device__ __forceinline__ uint32_t string_len(const HttpRawDev& R, const uint32_t* sp, uint32_t stride,
+__device__ __forceinline__ uint32_t string_len(const HttpRawDev& R, const lds_u32* sp, uint32_t stride,
                                                uint32_t* last_out) {
   uint32_t last = 0, len = 0;
   for (uint32_t f = 0; f < R.nfields; ++f) {
@@ -553,19 +592,25 @@ __device__ __forceinline__ uint32_t string_len(const HttpRawDev& R, const uint32
   return len;
 }
 
-__device__ __forceinline__ uint32_t lookup_prog(const HttpRawDev& R, uint32_t policy, bool ingress, uint32_t port) {
+template <class Tabs>
+__device__ __forceinline__ uint32_t lookup_prog(const HttpRawDev& R, const Tabs& T, uint32_t policy, bool ingress,
+                                                uint32_t port) {
   if (policy >= R.npolicies) return kProgDeny;
   const uint32_t key = (policy << 17) | ((uint32_t)ingress << 16) | (port & 0xFFFF);
   uint32_t h = hash32(key) & R.phash_mask;
   for (uint32_t probe = 0; probe <= R.phash_mask; ++probe) {
-    const uint32_t kk = R.phash_keys[h];
-    if (kk == key) return R.phash_vals[h];
+    const uint32_t kk = T.phk[h];
+    if (kk == key) return T.phv[h];
     if (kk == 0xFFFFFFFFu) break;
     h = (h + 1) & R.phash_mask;
   }
   return R.dflt[policy * 2 + (ingress ? 1 : 0)];
 }
 
+template <class Tabs>
+__device__ __forceinline__ bool walked_t(const HttpRawDev& R, const Tabs& T, uint32_t prog) {
+  return prog < R.nprogs && ((T.walk[prog >> 5] >> (prog & 31)) & 1u);
+}
 __device__ __forceinline__ bool walked(const HttpRawDev& R, uint32_t prog) {
   return prog < R.nprogs && !(R.progs[prog].flags & kProgAllowAll);
 }
@@ -577,27 +622,36 @@ __device__ __forceinline__ uint32_t group_of(const HttpRawDev& R, uint32_t prog)
 // Dynamic LDS of the scan kernel: [spans: nfields × 256 u32][4 wave stages ×
 // kStage bytes][4 wave mask pairs × 2 × kStage bits][tchar table: 256 B]
 // [bucket counters: nkeys u32, when they fit (lds_keys)].
-__device__ __forceinline__ uint8_t* wave_stage(uint32_t* lds, uint32_t F, uint32_t wave) {
-  return reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + wave * kStage;
+__device__ __forceinline__ lds_u8* wave_stage(lds_u32* lds, uint32_t F, uint32_t wave) {
+  return (lds_u8*)(lds + F * kRawThreads) + wave * kStage;
 }
-__device__ __forceinline__ uint32_t* wave_masks(uint32_t* lds, uint32_t F, uint32_t wave) {
-  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(lds + F * kRawThreads) + 4 * kStage) +
-         wave * 2 * kMaskWords;
+__device__ __forceinline__ lds_u32* wave_masks(lds_u32* lds, uint32_t F, uint32_t wave) {
+  return (lds_u32*)((lds_u8*)(lds + F * kRawThreads) + 4 * kStage) + wave * 2 * kMaskWords;
 }
-__device__ __forceinline__ uint8_t* tchar_table(uint32_t* lds, uint32_t F) {
-  return reinterpret_cast<uint8_t*>(wave_masks(lds, F, 4));
+__device__ __forceinline__ lds_u8* tchar_table(lds_u32* lds, uint32_t F) { return (lds_u8*)wave_masks(lds, F, 4); }
+__device__ __forceinline__ lds_u32* key_counters(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + 256); }
+// [name keys: 8 u32 per slot][field slots: 4 u32 per slot][names, u32
+// words][program hash keys][values] after the key counters, when they fit
+// (lds_tables): the lookups every header line and request makes, at LDS
+// latency instead of L1/L2
+struct RawTableWords {
+  uint32_t nk, fs, fn, ph, wb;
+};
+__host__ __device__ __forceinline__ RawTableWords raw_table_words(const HttpRawDev& R) {
+  return {8 * (R.nkmask + 1), 4 * (R.fmask + 1), (R.fnames_bytes + 3) / 4, R.phash_mask + 1, (R.nprogs + 31) / 32 + 1};
 }
-__device__ __forceinline__ uint32_t* key_counters(uint32_t* lds, uint32_t F) {
-  return reinterpret_cast<uint32_t*>(tchar_table(lds, F) + 256);
+__host__ __device__ __forceinline__ uint32_t raw_tables_lds_words(const HttpRawDev& R) {
+  const RawTableWords w = raw_table_words(R);
+  return w.nk + w.fs + w.fn + 2 * w.ph + w.wb;
 }
 // The head of request i as a reader: in the stage if it lies inside it.
-__device__ __forceinline__ HeadReader head_of(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
-                                              size_t i, const uint8_t* stage, uint64_t sbase, uint32_t slen) {
+__device__ __forceinline__ HeadReader head_of(glb_u8* raw, const uint64_t* __restrict__ off, size_t i,
+                                              const lds_u8* stage, uint64_t sbase, uint32_t slen) {
   const uint64_t a = off[i], b = off[i + 1];
   const uint32_t n = b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
   const uint64_t ga = (uint64_t)(uintptr_t)(raw + a);
   const bool in = ga >= sbase && ga + n <= sbase + slen;
-  return HeadReader(raw + a, n, in ? stage + (ga - sbase) : nullptr);
+  return HeadReader(raw + a, n, stage + (in ? (uint32_t)(ga - sbase) : 0u), in);
 }
 
 // 16-byte chunks of a lane's output string: stored to dst, then dst +=
@@ -638,7 +692,7 @@ struct Out16 {
 
 // The walked string, uncoded (value bytes, SEP 0x00, absent 0x01, REST 0x02
 // — the bytes the program's code map takes), into o.
-__device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr, const uint32_t* sp, uint32_t stride,
+__device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr, const lds_u32* sp, uint32_t stride,
                                             uint32_t last, Out16& o) {
   for (uint32_t f = 0; f < last; ++f) {
     const uint32_t s = sp[f * stride];
@@ -669,9 +723,59 @@ __device__ __forceinline__ uint64_t rec_off(uint64_t head_rel, size_t i, uint32_
 
 // ---- pass 1: parse, program, string length, bucket key, the request's
 // record in the string buffer; per-block bucket counts (bcount[key * gridDim.x + block],
-// lds_keys) or a global histogram.  kLists: header lists, not heads.
-template <bool kLists>
-__global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, const uint8_t* __restrict__ raw,
+// lds_keys) or a global histogram.  kLists: header lists, not heads;
+// kMasks: requests inside the stage parse over its structural bitmaps (else
+// through HeadReader's dword steps).
+// A lane's request inputs, loaded two iterations ahead of their use.
+struct RawIn {
+  uint32_t pol, ing, port;
+  uint64_t a, b;  // off[i], off[i + 1]
+};
+__device__ __forceinline__ RawIn raw_in(const uint64_t* __restrict__ off, const uint32_t* __restrict__ policy,
+                                        const uint8_t* __restrict__ ingress, const uint16_t* __restrict__ port,
+                                        size_t i, size_t n) {
+  const size_t j = i < n ? i : (n ? n - 1 : 0);  // unconditional loads (no branch around them)
+  RawIn r;
+  r.pol = i < n ? policy[j] : 0xFFFFFFFFu;
+  r.ing = ingress[j];
+  r.port = port[j];
+  r.a = off[j];
+  r.b = off[j + 1];
+  if (i >= n) r.a = r.b;  // empty
+  return r;
+}
+constexpr uint32_t kStageVecs = kStage / (64 * 16);  // 16-B loads per lane for a whole stage
+// The stage of the wave whose lanes hold `in` (64 consecutive requests, lanes
+// past n empty): its 16-B aligned blocks into registers.  Every block loaded
+// holds at least one byte of the wave's heads, so no load leaves their pages.
+struct StageRegs {
+  uint4 v[kStageVecs];
+  uint64_t base;
+  uint32_t len;
+};
+__device__ __forceinline__ void stage_load(glb_u8* raw, const RawIn& in, uint32_t lane, StageRegs& S) {
+  const uint64_t lo = __shfl(in.a, 0, 64);
+  // the last lane's end (empty lanes past n repeat off[n])
+  const uint64_t hi = __shfl(in.b, 63, 64);
+  const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
+  const uint64_t a0 = glo & ~15ull;
+  const uint32_t nb = hi > lo ? (uint32_t)min<uint64_t>((ghi - a0 + 15) & ~15ull, kStage) : 0u;
+  S.base = a0;
+  S.len = nb;
+#pragma unroll
+  for (uint32_t j = 0; j < kStageVecs; ++j) {
+    const uint32_t o = (j * 64 + lane) * 16;
+    const uint64_t a = o < nb ? a0 + o : a0;  // past the stage: a harmless repeat of the first block
+    S.v[j] = nb ? to_uint4(*(glb_v4*)(uintptr_t)a) : make_uint4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void stage_store(const StageRegs& S, lds_u8* stage, uint32_t lane) {
+#pragma unroll
+  for (uint32_t j = 0; j < kStageVecs; ++j) *(lds_v4*)(stage + (j * 64 + lane) * 16) = to_v4(S.v[j]);
+}
+
+template <bool kLists, bool kMasks, bool kLdsTabs>
+__global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, const uint8_t* __restrict__ raw_g,
                                                                const uint64_t* __restrict__ off, size_t n,
                                                                const uint32_t* __restrict__ policy,
                                                                const uint8_t* __restrict__ ingress,
@@ -681,42 +785,91 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
                                                                uint8_t* __restrict__ sbuf, uint32_t cst,
                                                                unsigned long long* __restrict__ ovf_bytes,
                                                                uint32_t lds_keys) {
-  extern __shared__ uint32_t lds[];
+  extern __shared__ uint32_t lds_[];
+  lds_u32* lds = (lds_u32*)lds_;
+  glb_u8* raw = (glb_u8*)raw_g;
   const uint32_t F = max(R.nfields, 1u), wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* sp = lds + threadIdx.x;  // this lane's spans: sp[f * kRawThreads]
-  uint8_t* stage = wave_stage(lds, F, wave);
-  uint32_t* masks = wave_masks(lds, F, wave);
-  uint8_t* tct = tchar_table(lds, F);
-  uint32_t* lk = key_counters(lds, F);
+  lds_u32* sp = lds + threadIdx.x;  // this lane's spans: sp[f * kRawThreads]
+  lds_u8* stage = wave_stage(lds, F, wave);
+  lds_u32* masks = wave_masks(lds, F, wave);
+  lds_u8* tct = tchar_table(lds, F);
+  lds_u32* lk = key_counters(lds, F);
   const uint32_t nk = (R.nprogs + 2) * kRawKeys;
   if (lds_keys)
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = 0;
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = kLists ? list_stop(b, R.raw_values) : !tchar(b);
+  // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
+  using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
+  Tabs T;
+  if constexpr (kLdsTabs) {
+    const RawTableWords w = raw_table_words(R);
+    lds_u32* t = lk + (lds_keys ? nk : 0u);
+    lds_u32* tfs = t + w.nk;
+    lds_u32* tfn = tfs + w.fs;
+    lds_u32* tpk = tfn + w.fn;
+    lds_u32* tpv = tpk + w.ph;
+    lds_u32* twb = tpv + w.ph;
+    for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
+    for (uint32_t k = threadIdx.x; k < w.fs; k += blockDim.x) tfs[k] = R.fslots[k];
+    for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
+      uint32_t v = 0;
+      for (uint32_t j = 0; j < 4; ++j)
+        if (4 * k + j < R.fnames_bytes) v |= (uint32_t)R.fnames[4 * k + j] << (8 * j);
+      tfn[k] = v;
+    }
+    for (uint32_t k = threadIdx.x; k < w.ph; k += blockDim.x) {
+      tpk[k] = R.phash_keys[k];
+      tpv[k] = R.phash_vals[k];
+    }
+    for (uint32_t k = threadIdx.x; k < w.wb; k += blockDim.x) twb[k] = R.walk_bits[k];
+    T = LdsTabs{t, tfs, tpk, tpv, twb, (const lds_u8*)tfn};
+  } else {
+    T = GlbTabs{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+                (glb_u32*)R.walk_bits, (glb_u8*)R.fnames};
+  }
   const uint64_t off0 = off[0];
   __syncthreads();
-  for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
+  // software pipeline per wave: iteration k parses stage k from LDS while the
+  // stage of k + 1 is in flight into registers and the inputs of k + 2 load
+  const size_t gstride = (size_t)gridDim.x * kRawThreads;
+  size_t base = (size_t)blockIdx.x * kRawThreads;
+  // (a wave with no requests skips the loop and meets the others at the flush)
+  RawIn cur = raw_in(off, policy, ingress, port, base + wave * 64 + lane, n);
+  RawIn nxt = raw_in(off, policy, ingress, port, base + gstride + wave * 64 + lane, n);
+  StageRegs S;
+  if (base + (size_t)wave * 64 < n) stage_load(raw, cur, lane, S);
+  for (; base < n; base += gstride) {
     const size_t i0 = base + (size_t)wave * 64;
-    if (i0 >= n) continue;  // wave-uniform
+    if (i0 >= n) break;  // wave-uniform
     const size_t i = i0 + lane;
     const bool live = i < n;
-    const uint32_t prog = live ? lookup_prog(R, policy[i], ingress[i] != 0, port[i]) : kProgDeny;
-    // every request but an unknown policy's is parsed: a head the codec
-    // rejects is denied in any program (flagged malformed)
-    const bool parse = live && prog != kProgDeny;
-    uint32_t slen = 0;
-    uint64_t sbase = 0;
-    if (__any(parse)) {
-      sbase = stage_heads(raw, off[i0], off[min(i0 + 64, n)], stage, lane, &slen);
-      wave_sync();
+    const RawIn nn = raw_in(off, policy, ingress, port, base + 2 * gstride + wave * 64 + lane, n);
+    const uint32_t rem = remote[live ? i : 0];
+    // stage k: registers → LDS (the previous iteration's reads are done)
+    wave_sync();
+    stage_store(S, stage, lane);
+    const uint64_t sbase = S.base;
+    const uint32_t slen = S.len;
+    // stage k + 1 into registers, under this iteration's parse
+    if (base + gstride < n) stage_load(raw, nxt, lane, S);
+    wave_sync();
+    if (kMasks) {
       if (kLists) build_masks_lists(stage, slen, tct, masks, lane);
       else build_masks(stage, slen, tct, masks, lane);
+      wave_sync();
     }
-    wave_sync();
+    const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing != 0, cur.port) : kProgDeny;
     if (live) {
+      // every request but an unknown policy's is parsed: a head the codec
+      // rejects is denied in any program (flagged malformed)
+      const bool parse = prog != kProgDeny;
       uint32_t key = 0, len = 0, bad = 0;
-      uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(off[i] - off0, i, cst));
+      uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(cur.a - off0, i, cst));
       if (parse) {
-        HeadReader hr = head_of(raw, off, i, stage, sbase, slen);
+        const uint32_t hn = cur.b > cur.a ? (uint32_t)min<uint64_t>(cur.b - cur.a, 0xFFFFFFFFull) : 0u;
+        const uint64_t ga = (uint64_t)(uintptr_t)(raw + cur.a);
+        const bool in = ga >= sbase && ga + hn <= sbase + slen;
+        HeadReader hr(raw + cur.a, hn, stage + (in ? (uint32_t)(ga - sbase) : 0u), in);
         // heads / lists inside the stage parse over its masks, the rest byte by byte
         const uint32_t hs = (uint32_t)(hr.lp - stage);
         bool ok;
@@ -725,16 +878,18 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
             atomicOr(ovf_bytes, kRawListTooLong);
             ok = false;
           } else {
-            ok = hr.lp ? parse_list_masks(R, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
-                       : parse_list_bytes(R, hr, sp, kRawThreads);
+            ok = kMasks && hr.in
+                     ? parse_list_masks(R, T, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
+                     : parse_list_bytes(R, T, hr, sp, kRawThreads);
           }
         } else {
-          ok = hr.lp ? parse_head_masks(R, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
-                     : parse_head(R, hr, sp, kRawThreads);
+          ok = kMasks && hr.in
+                   ? parse_head_masks(R, T, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
+                   : parse_head(R, T, hr, sp, kRawThreads);
         }
         if (!ok) {
           bad = 1;
-        } else if (walked(R, prog)) {
+        } else if (walked_t(R, T, prog)) {
           uint32_t last;
           len = string_len(R, sp, kRawThreads, &last);
           key = len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
@@ -744,15 +899,16 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
           if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
         }
       }
-      const uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
+      const uint32_t flags = (cur.ing ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
                              (len > CG_HTTP_SLOT_BYTES ? CG_HTTP_F_OVERFLOW : 0u);
-      *rec = make_uint4((uint32_t)i, remote[i], len | flags << 24, prog);
+      *rec = make_uint4((uint32_t)i, rem, len | flags << 24, prog);
       rinfo[i] = make_uint2(prog, len | bad << 31);
       const uint32_t k = group_of(R, prog) * kRawKeys + key;
-      if (lds_keys) atomicAdd(&lk[k], 1u);
+      if (lds_keys) __hip_atomic_fetch_add(&lk[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else atomicAdd(&counts[k], 1u);
     }
-    wave_sync();  // the stage is read before the next iteration overwrites it
+    cur = nxt;
+    nxt = nn;
   }
   if (lds_keys) {
     __syncthreads();
@@ -922,10 +1078,11 @@ unsigned grid_for(size_t n, int cus, unsigned per_cu) {
 }
 
 // LDS of the scan / emit kernels (see wave_stage, key_counters)
+bool lds_tables_fit(const HttpRawDev& R) { return raw_tables_lds_words(R) * 4 <= 8 * 1024; }
 size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
   return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + 4 * 2 * (kStage / 8) + 256 +
-         (lds_keys ? nk * 4 : 0) +
+         (lds_keys ? nk * 4 : 0) + (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 : 0) +
          (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
 }
 // code maps in LDS only while small: a larger table costs workgroups per CU
@@ -945,7 +1102,19 @@ int launch_http_raw_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, co
   if (!n) return 0;
   const bool lk = http_raw_lds_keys(R);
   const size_t lds = raw_lds(R, lk, false);
-  auto kern = lists ? raw_scan_kernel<true> : raw_scan_kernel<false>;
+  // CG_RAW_PARSE=bytes: HeadReader parsing for staged requests too (A/B)
+  static const bool masks = [] {
+    const char* e = getenv("CG_RAW_PARSE");
+    return !(e && std::string(e) == "bytes");
+  }();
+  const bool tabs = lds_tables_fit(R);
+  decltype(&raw_scan_kernel<false, false, false>) kern;
+  if (lists)
+    kern = masks ? (tabs ? raw_scan_kernel<true, true, true> : raw_scan_kernel<true, true, false>)
+                 : (tabs ? raw_scan_kernel<true, false, true> : raw_scan_kernel<true, false, false>);
+  else
+    kern = masks ? (tabs ? raw_scan_kernel<false, true, true> : raw_scan_kernel<false, true, false>)
+                 : (tabs ? raw_scan_kernel<false, false, true> : raw_scan_kernel<false, false, false>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(kern, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw,
                      off, n, policy, ingress, port, counts, (uint2*)rinfo, remote, sbuf, cst, ovf_bytes, (uint32_t)lk);
