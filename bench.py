@@ -15,8 +15,9 @@ image (cg_http_policy_export / _import).
 Rank 0 prints one JSON line with throughput, the roofline of the verdict
 kernel (HIP events on the kernel's stream), the same kernel on a 262K-distinct
 batch, the end-to-end raw path (config 5 as raw HTTP/1 heads resident in HBM
-→ cg_http_verdicts_raw_dev: parse, pack and verdicts on the GPU) and the CPU
-oracle (the Envoy-faithful std::regex rule scan) timed on a bounded sample on
+→ cg_http_verdicts_raw_dev: parse, pack and verdicts on the GPU), the host
+entry (the distinct requests as header lists in host memory →
+cg_http_verdicts_fields_host, PCIe-inclusive) and the CPU oracle (the Envoy-faithful std::regex rule scan) timed on a bounded sample on
 the host cores given to this GPU.
 """
 from __future__ import annotations
@@ -155,7 +156,6 @@ def main():
         check = bool(np.array_equal(got, exp))
         if not check:
             raise SystemExit(f"verdicts differ from the oracle on {int((got != exp).sum())} of {D} requests")
-        del rq
 
     for _ in range(args.warmup):
         step()
@@ -186,6 +186,10 @@ def main():
     achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
     allow_frac = float(d_out.float().sum().item()) / B
 
+    host = None
+    if not args.no_e2e:
+        host = host_entry_fields(cl, rq, got if check else None)
+    del rq
     traffic_bytes, traffic_src = pmc_traffic(B)
     # same unit as `achieved`: HBM bytes per launch over the measured launch time
     traffic = traffic_bytes / (kernel_ms * 1e-3) / 1e9 if traffic_bytes else None
@@ -239,6 +243,7 @@ def main():
                          "traffic_source": traffic_src},
             "distinct_262k": small,
             "end_to_end": e2e,
+            "host_entry": host,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -273,6 +278,29 @@ def share_policy(cl, pols, dist, rank, dev, torch) -> None:
     dist.broadcast(buf, 0)
     if rank != 0:
         cl.import_http_policy(buf.cpu().numpy().tobytes())
+
+
+def host_entry_fields(cl, rq, ref) -> dict:
+    """The Envoy-side entry (envoy/cilium_l7policy.cc:127-182): the same
+    distinct requests as header lists in HOST memory through
+    cg_http_verdicts_fields_host (staged over PCIe in chunks, grouped, sorted
+    and packed on the GPU, verdicts copied back), wall clock; bit-exact
+    against the device batch's (oracle-checked) verdicts."""
+    args_ = (rq["policy"], rq["ingress"], rq["port"], rq["remote"], rq["hdr_blob"], rq["hdr_off"])
+    n = len(rq["policy"])
+    got = cl.http_verdicts_fields(*args_)  # warm: pinned buffers, workers
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        got = cl.http_verdicts_fields(*args_)
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    list_bytes = int(rq["hdr_off"][-1])
+    return {"metric": "verdicts/s through the host entry: header lists in host memory -> verdicts "
+                      "(cg_http_verdicts_fields_host, PCIe-inclusive)",
+            "value": n / t, "unit": "verdicts/s", "ms": t * 1e3, "requests": n,
+            "staged_GBps": (list_bytes + 19 * n) / t / 1e9,
+            "parity_check": None if ref is None else bool(np.array_equal(got, ref))}
 
 
 def kernel_on_batch(cl, info, distinct, per_gpu, rank, dev, torch, stream, steps, warmup, layout) -> dict:

@@ -285,10 +285,10 @@ CG_HD inline uint32_t raw_name_hash(uint32_t nl, uint32_t lo0, uint32_t lo1, uin
 // FNV-1a, 32 bit, over lowercase bytes
 CG_HD inline uint32_t raw_fnv(uint32_t h, uint8_t c) { return (h ^ c) * 16777619u; }
 constexpr uint32_t kRawFnvInit = 2166136261u;
-// A run of tiles of a raw batch with the same string units: tiles
-// [t0, next run's t0), tile t at granule base + (t - t0) * (1 + 2 * units).
+// A run of tiles of a raw batch with the same string units and program:
+// tiles [t0, next run's t0), tile t at granule base + (t - t0) * (1 + 2 * units).
 struct HttpRawRun {
-  uint32_t t0, units, base, pad;
+  uint32_t t0, units, base, prog;
 };
 
 CG_HD inline uint32_t hash32(uint32_t x) {

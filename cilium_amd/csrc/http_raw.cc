@@ -149,7 +149,8 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   // align16(off[i] - off[0]) + cst * i (kernels_http_raw.hip rec_off); the
   // build pass addresses records in 16-byte units through u32 order words
   const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 32 + 15) & ~(size_t)15);
-  const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * n + 16;
+  // (+256: the build kernel reads whole 16-B chunks up to 8 units past a record's start)
+  const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * n + 256;
   if (sbytes / 16 >= (1ull << 32)) {
     if (n < 2) fail(CG_INVALID_ARGUMENT, "raw head too large");
     const size_t h = n / 2;
@@ -198,9 +199,9 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   std::vector<HttpRawRun> runs;
   std::vector<uint32_t> cursors((size_t)G * K, 0);
   uint32_t tiles = 0, gran = 0;
-  auto add_run = [&](uint32_t t0, uint32_t t1, uint32_t units) {
+  auto add_run = [&](uint32_t t0, uint32_t t1, uint32_t units, uint32_t prog) {
     if (t1 <= t0) return;
-    runs.push_back({t0, units, gran, 0});
+    runs.push_back({t0, units, gran, prog});
     gran += (t1 - t0) * (1 + 2 * units);
   };
   for (uint32_t g = 0; g < G; ++g) {
@@ -225,10 +226,10 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
         if (bstart[k] <= last && last < bstart[k + 1]) u = k;
       const uint32_t next = bstart[u + 1];  // first slot of a larger key (or e)
       const uint32_t jend = next >= e ? (e + 63) / 64 : next / 64;
-      add_run(tiles + j, tiles + jend, u);
+      add_run(tiles + j, tiles + jend, u, prog);
       j = jend;
     }
-    add_run(tiles + j, tiles + T, 0);  // only overflow-arena slots
+    add_run(tiles + j, tiles + T, 0, prog);  // only overflow-arena slots
     tiles += T;
   }
   const size_t nslots = (size_t)tiles * CG_HTTP_TILE;

@@ -979,14 +979,16 @@ __device__ __forceinline__ uint32_t code4(const uint8_t* lut, uint32_t q) {
          (uint32_t)lut[q >> 24] << 24;
 }
 
-// ---- pass 3: one wave per tile.  The tile's granule offset and string units
-// come from its run (tiles of one group whose last walked slot has the same
-// bucket key).  Each lane gathers its request's record (header + string: one
-// contiguous read) and the wave stores unit u of all 64 lanes as one
-// contiguous 1 KiB, class-coded through the tile's program's code map (staged
-// in LDS per wave); strings past a slot go to the overflow arena (u32 length,
-// coded bytes, 16-byte aligned).  order[slot] becomes the request index (the
-// verdict kernel writes out[order[slot]]).
+// ---- pass 3: tiles, a contiguous range per wave (so the run holding a
+// tile advances instead of being searched).  The tile's records are gathered
+// cooperatively: L = pow2 >= 1 + units lanes per record, lane `sub` of a
+// record's group reading its 16-B chunk `sub` (0 = the header, c = string
+// unit c - 1), so one load instruction touches 64 / L records' lines instead
+// of 64; each lane class-codes its chunk through the program's code map
+// (LDS, per wave) and stores it straight to its place in the tile (unit
+// sub - 1 of slot s: whole 1 KiB units once the tile's passes are done).
+// Header lanes write the meta word and order[slot] = request index, and copy
+// strings past the slot into the overflow arena.
 __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
     HttpRawDev R, const HttpRawRun* __restrict__ runs, uint32_t nruns, uint32_t ntiles, HttpTile* __restrict__ ttab,
     uint8_t* __restrict__ tiles, uint32_t* __restrict__ order, const uint8_t* __restrict__ sbuf,
@@ -996,74 +998,89 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
   uint8_t* lut = s_lut[wave];
   uint32_t lut_prog = 0xFFFFFFFFu;
   const uint4* rec16 = reinterpret_cast<const uint4*>(sbuf);
-  for (uint32_t t = blockIdx.x * (kRawThreads / 64) + wave; t < ntiles; t += gridDim.x * (kRawThreads / 64)) {
-    const size_t slot = (size_t)t * 64 + lane;
-    const uint32_t r = order[slot];
-    // the run holding tile t (runs ascending by t0, covering every tile)
-    uint32_t lo = 0, hi = nruns;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) / 2;
-      if (runs[mid].t0 <= t) lo = mid;
-      else hi = mid;
+  const uint32_t nwaves = gridDim.x * (kRawThreads / 64), gw = blockIdx.x * (kRawThreads / 64) + wave;
+  const uint32_t tpw = (ntiles + nwaves - 1) / nwaves;
+  uint32_t t = gw * tpw;
+  const uint32_t tend = min(ntiles, t + tpw);
+  if (t >= tend) return;
+  // the run holding t (runs ascending by t0, covering every tile)
+  uint32_t lo = 0, hi = nruns;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (runs[mid].t0 <= t) lo = mid;
+    else hi = mid;
+  }
+  uint32_t ri = lo;
+  HttpRawRun run = runs[ri];
+  uint32_t next_t0 = ri + 1 < nruns ? runs[ri + 1].t0 : 0xFFFFFFFFu;
+  for (; t < tend; ++t) {
+    while (t >= next_t0) {
+      ++ri;
+      run = runs[ri];
+      next_t0 = ri + 1 < nruns ? runs[ri + 1].t0 : 0xFFFFFFFFu;
     }
-    const HttpRawRun run = runs[lo];
     const uint32_t units = run.units;
     const uint32_t at = run.base + (t - run.t0) * (1 + 2 * units);
     uint8_t* tb = tiles + (size_t)at * 512;
-    const bool pad = r == 0xFFFFFFFFu;
-    uint4 h = make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
-    if (!pad) h = rec16[r];
-    const uint32_t len = h.z & 0xFFFFFFu, flags = h.z >> 24;
-    const bool ovf = flags & CG_HTTP_F_OVERFLOW;
-    const uint32_t slen = (pad || ovf) ? 0u : len;
-    if (!pad) order[slot] = h.x;
-    // the tile's program (every request of a tile has it): its code map
-    const unsigned long long live = __ballot(len != 0);
-    if (live) {
-      const uint32_t prog = (uint32_t)__shfl((int)h.w, (int)__builtin_ctzll(live), 64);
-      if (prog != lut_prog) {
-        wave_sync();  // earlier lookups done
-        reinterpret_cast<uint32_t*>(lut)[lane] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)prog * 256)[lane];
-        wave_sync();
-        lut_prog = prog;
-      }
+    if (run.prog < R.nprogs && run.prog != lut_prog) {  // the program's code map (wave-uniform)
+      wave_sync();  // earlier lookups done
+      reinterpret_cast<uint32_t*>(lut)[lane] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)run.prog * 256)[lane];
+      wave_sync();
+      lut_prog = run.prog;
     }
-    uint32_t aoff16 = 0;
-    if (ovf) {
-      const unsigned long long ao = atomicAdd(arena_cursor, (unsigned long long)((4 + len + 15) & ~15u));
-      aoff16 = (uint32_t)(ao / 16);
-      Out16 o(reinterpret_cast<uint4*>(arena + ao), 1);
-      o.w0 = len;
-      o.pos = 4;
-      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(rec16 + r + 1);
-      for (uint32_t k = 0; k < len; k += 4) {
-        const uint32_t nb = min(len - k, 4u);
-        const uint32_t c = code4(lut, s32[k / 4]);
-        o.put4(nb == 4 ? c : c & ((1u << (8 * nb)) - 1u), nb);
-      }
-      if (o.pos) o.flush();
-    }
-    // unit u of every lane: a whole 1 KiB per unit (zero past a string's end)
-    uint4* dst = reinterpret_cast<uint4*>(tb + 512) + lane;
-    for (uint32_t u = 0; u < units; ++u) {
-      uint4 c = make_uint4(0, 0, 0, 0);
-      if (16 * u < slen) {
-        const uint4 x = rec16[r + 1 + u];
-        c = make_uint4(code4(lut, x.x), code4(lut, x.y), code4(lut, x.z), code4(lut, x.w));
-        const uint32_t left = slen - 16 * u;  // the string's bytes in this unit
-        if (left < 16) {
-          const uint32_t m0 = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
-          const uint32_t m1 = left >= 8 ? 0xFFFFFFFFu : left <= 4 ? 0u : (1u << (8 * (left - 4))) - 1u;
-          const uint32_t m2 = left >= 12 ? 0xFFFFFFFFu : left <= 8 ? 0u : (1u << (8 * (left - 8))) - 1u;
-          const uint32_t m3 = left <= 12 ? 0u : (1u << (8 * (left - 12))) - 1u;
-          c = make_uint4(c.x & m0, c.y & m1, c.z & m2, c.w & m3);
+    const uint32_t r = order[(size_t)t * 64 + lane];  // the slot's record (16-B units), or padding
+    const uint32_t L = units == 0 ? 1u : (units < 2 ? 2u : units < 4 ? 4u : units < 8 ? 8u : 16u);
+    const uint32_t per = 64 / L, sub = lane & (L - 1), grp = lane & ~(L - 1);
+    uint32_t m = 0;  // the longest slot string among this lane's header slots
+    for (uint32_t pass = 0; pass < L; ++pass) {
+      const uint32_t s = pass * per + lane / L;  // this lane's slot in this pass
+      const uint32_t rs = (uint32_t)__shfl((int)r, (int)s, 64);
+      const bool pad = rs == 0xFFFFFFFFu;
+      uint4 x = make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
+      if (!pad && sub <= units) x = rec16[(size_t)rs + sub];
+      // the record's header word (len | flags << 24), from its group's lane 0
+      const uint32_t hz = (uint32_t)__shfl((int)x.z, (int)grp, 64);
+      const uint32_t len = hz & 0xFFFFFFu, flags = hz >> 24;
+      const bool ovf = flags & CG_HTTP_F_OVERFLOW;
+      const uint32_t slen = (pad || ovf) ? 0u : len;
+      if (sub == 0) {
+        uint32_t aoff16 = 0;
+        if (ovf) {
+          const unsigned long long ao = atomicAdd(arena_cursor, (unsigned long long)((4 + len + 15) & ~15u));
+          aoff16 = (uint32_t)(ao / 16);
+          Out16 o(reinterpret_cast<uint4*>(arena + ao), 1);
+          o.w0 = len;
+          o.pos = 4;
+          const uint32_t* s32 = reinterpret_cast<const uint32_t*>(rec16 + rs + 1);
+          for (uint32_t k = 0; k < len; k += 4) {
+            const uint32_t nb = min(len - k, 4u);
+            const uint32_t c = code4(lut, s32[k / 4]);
+            o.put4(nb == 4 ? c : c & ((1u << (8 * nb)) - 1u), nb);
+          }
+          if (o.pos) o.flush();
         }
+        if (!pad) order[(size_t)t * 64 + s] = x.x;
+        reinterpret_cast<uint2*>(tb)[s] = make_uint2(x.y, (aoff16 & 0xFFFFFFu) | flags << 24);
+        m = max(m, slen);
+      } else if (sub <= units) {
+        // unit sub - 1 of slot s, zero past the string's end
+        uint4 c = make_uint4(0, 0, 0, 0);
+        const uint32_t u = sub - 1;
+        if (16 * u < slen) {
+          c = make_uint4(code4(lut, x.x), code4(lut, x.y), code4(lut, x.z), code4(lut, x.w));
+          const uint32_t left = slen - 16 * u;  // the string's bytes in this unit
+          if (left < 16) {
+            const uint32_t m0 = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
+            const uint32_t m1 = left >= 8 ? 0xFFFFFFFFu : left <= 4 ? 0u : (1u << (8 * (left - 4))) - 1u;
+            const uint32_t m2 = left >= 12 ? 0xFFFFFFFFu : left <= 8 ? 0u : (1u << (8 * (left - 8))) - 1u;
+            const uint32_t m3 = left <= 12 ? 0u : (1u << (8 * (left - 12))) - 1u;
+            c = make_uint4(c.x & m0, c.y & m1, c.z & m2, c.w & m3);
+          }
+        }
+        reinterpret_cast<uint4*>(tb + 512)[(size_t)u * 64 + s] = c;
       }
-      dst[(size_t)u * 64] = c;
     }
-    reinterpret_cast<uint2*>(tb)[lane] = make_uint2(h.y, (aoff16 & 0xFFFFFFu) | flags << 24);
     // the tile's tail: the longest string's bytes in its last unit
-    uint32_t m = slen;
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
     if (lane == 0) {
       const uint32_t tail = units ? m - 16 * (units - 1) : 0u;
