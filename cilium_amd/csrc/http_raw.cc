@@ -128,9 +128,10 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   if (!n) return;
   const hipStream_t st = (hipStream_t)stream;
   const uint32_t np = (uint32_t)s.progs.size(), G = np + 2, K = kRawKeys;
-  // workspace: [histogram G*K u32][overflow bytes u64][arena cursor u64][head bytes u64]
+  // workspace: [histogram G*K u32][overflow bytes u64][arena cursor u64][head
+  // bytes u64][deferred-request count u32, pad]
   const size_t hist_bytes = ((size_t)G * K * 4 + 7) & ~(size_t)7;
-  uint8_t* small = (uint8_t*)sl.dev_buf(8, hist_bytes + 24);
+  uint8_t* small = (uint8_t*)sl.dev_buf(8, hist_bytes + 32);
   uint32_t* hist = (uint32_t*)small;
   auto* ovf = (unsigned long long*)(small + hist_bytes);
   hip_check(hipMemsetAsync(small, 0, hist_bytes + 16, st), "hipMemsetAsync");
@@ -144,11 +145,13 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   memcpy(&o0, hh + hist_bytes + 8, 8);
   memcpy(&o1, hh + hist_bytes + 16, 8);
   if (o1 < o0) fail(CG_INVALID_ARGUMENT, "raw_off must be non-decreasing");
-  hip_check(hipMemsetAsync(small + hist_bytes + 8, 0, 8, st), "hipMemsetAsync");  // the arena cursor
+  // the arena cursor, the head-bytes slot, the deferred-request count
+  hip_check(hipMemsetAsync(small + hist_bytes + 8, 0, 24, st), "hipMemsetAsync");
+  auto* dcount = (uint32_t*)(small + hist_bytes + 24);
   // string buffer: request i's record (16-byte header + uncoded string) at
   // align16(off[i] - off[0]) + cst * i (kernels_http_raw.hip rec_off); the
   // build pass addresses records in 16-byte units through u32 order words
-  const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 32 + 15) & ~(size_t)15);
+  const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 48 + 15) & ~(size_t)15);
   // (+256: the build kernel reads whole 16-B chunks up to 8 units past a record's start)
   const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * n + 256;
   if (sbytes / 16 >= (1ull << 32)) {
@@ -164,11 +167,12 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   // per-block bucket counts → per-block slot offsets (when the bucket
   // counters fit the kernels' LDS), else one global histogram
   const bool lds_keys = http_raw_lds_keys(s.raw);
-  const uint32_t nblk = (uint32_t)http_raw_grid(n, cus);
+  const uint32_t nblk = (uint32_t)http_raw_grid(s.raw, lists, n, cus);
   uint32_t* bcount = lds_keys ? (uint32_t*)sl.dev_buf(16, (size_t)G * K * nblk * 4) : hist;
   uint32_t* bbase = lds_keys ? (uint32_t*)sl.dev_buf(17, (size_t)G * K * nblk * 4) : nullptr;
+  auto* dlist = (uint32_t*)sl.dev_buf(18, n * 4);
   hip_check(launch_http_raw_scan(s.raw, lists, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, d_remote,
-                                 sbuf, cst, ovf, st, cus),
+                                 sbuf, cst, ovf, dlist, dcount, st, cus),
             "raw scan kernel launch");
   if (lds_keys)
     hip_check(launch_http_raw_prefix(bcount, G * K, nblk, bbase, hist, st), "raw prefix kernel launch");
@@ -262,7 +266,7 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   hip_check(hipMemsetAsync(order, 0xFF, nslots * 4, st), "hipMemsetAsync");  // padding slots
   auto* ttab = (HttpTile*)(batch + hdr.ttab_off);
   uint8_t* tdata = batch + hdr.tiles_off;
-  hip_check(launch_http_raw_rank(s.raw, n, d_off, cst, rinfo, d_cursor, bbase, order, st, cus),
+  hip_check(launch_http_raw_rank(s.raw, lists, n, d_off, cst, rinfo, d_cursor, bbase, order, st, cus),
             "raw rank kernel launch");
   hip_check(launch_http_raw_build(s.raw, d_runs, (uint32_t)runs.size(), tiles, ttab, tdata, order, sbuf, arena,
                                   ovf + 1, st, cus),

@@ -35,7 +35,7 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
                         int cus);
 
 // Raw HTTP/1 heads → batch (kernels_http_raw.hip; sequence in http_raw.cc).
-// The scan and rank kernels run http_raw_grid(n, cus) blocks over the
+// The scan and rank kernels run http_raw_grid(R, lists, n, cus) blocks over the
 // requests in the same order.  With http_raw_lds_keys(R) the scan writes
 // per-block bucket counts (counts[key * grid + block]) and raw_prefix turns
 // them into per-block slot offsets (bbase) and totals (hist); otherwise the
@@ -43,18 +43,21 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
 // from global cursors.  sbuf: the request-ordered string buffer
 // (records per request, http_raw.cc), cst its per-request stride.  lists:
 // the requests are cg_http_pack header lists instead of HTTP/1 heads (a list
-// longer than kFieldsMaxList sets kRawListTooLong in *ovf_bytes).
+// longer than kFieldsMaxList sets kRawListTooLong in *ovf_bytes).  Requests
+// outside their wave's LDS stage are appended to dlist (*dcount, zeroed by
+// the caller; room for n) and finished by a second kernel of the launch.
 constexpr unsigned long long kRawListTooLong = 1ull << 63;
-size_t http_raw_grid(size_t n, int cus);
+size_t http_raw_grid(const HttpRawDev& R, bool lists, size_t n, int cus);
 bool http_raw_lds_keys(const HttpRawDev& R);
 int launch_http_raw_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
                          void* rinfo, const uint32_t* remote, uint8_t* sbuf, uint32_t cst,
-                         unsigned long long* ovf_bytes, void* stream, int cus);
+                         unsigned long long* ovf_bytes, uint32_t* dlist, uint32_t* dcount, void* stream, int cus);
 int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk, uint32_t* bbase, uint32_t* hist,
                            void* stream);
-int launch_http_raw_rank(const HttpRawDev& R, size_t n, const uint64_t* off, uint32_t cst, const void* rinfo,
-                         uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream, int cus);
+int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const uint64_t* off, uint32_t cst,
+                         const void* rinfo, uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream,
+                         int cus);
 int launch_http_raw_build(const HttpRawDev& R, const HttpRawRun* runs, uint32_t nruns, uint32_t ntiles,
                           HttpTile* ttab, uint8_t* tiles, uint32_t* order, const uint8_t* sbuf, uint8_t* arena,
                           unsigned long long* arena_cursor, void* stream, int cus);

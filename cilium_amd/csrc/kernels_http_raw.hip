@@ -26,6 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
@@ -39,6 +42,28 @@ namespace cg {
 namespace {
 
 constexpr int kRawThreads = 256;
+
+// CG_RAW_CLOCKS (experiment builds only, tools/exp_http.py raw_clocks): the
+// scan's phases timed per wave with the shader clock; one wave prints its
+// totals at the end
+#ifdef CG_RAW_CLOCKS
+#define RAW_CLK(v) v = clock64()
+#define RAW_ACC(slot, a, b) clk[slot] += (b) - (a)
+// inside parse_head_fast: time since the last mark into g_pclk[slot]
+__device__ unsigned long long g_pclk[8];
+#define RAW_PMARK(slot)                                                           \
+  do {                                                                           \
+    const uint64_t now_ = clock64();                                             \
+    if (blockIdx.x == 7 && threadIdx.x == 64) g_pclk[slot] += now_ - pm_;        \
+    pm_ = now_;                                                                  \
+  } while (0)
+#define RAW_PSTART uint64_t pm_ = clock64()
+#else
+#define RAW_CLK(v)
+#define RAW_ACC(slot, a, b)
+#define RAW_PMARK(slot)
+#define RAW_PSTART
+#endif
 constexpr uint32_t kAbsentSpan = 0xFFFFFFFFu;
 
 // Explicit address spaces for the scan's LDS stage, bitmaps, spans and tables
@@ -59,7 +84,7 @@ typedef const CG_GLB uint32_t glb_u32;
 // hash): staged in LDS when they fit, else read from HBM.
 template <class P32, class P8>
 struct RawTabs {
-  P32 nkeys, fslots, phk, phv, walk;
+  P32 nkeys, fslots, phk, phv, walk, dflt;
   P8 fnames;
 };
 using LdsTabs = RawTabs<const lds_u32*, const lds_u8*>;
@@ -155,46 +180,11 @@ struct HeadReader {
   }
 };
 
-// The wave's 64 consecutive heads [off[i0], off[i1]) copied into its LDS
-// stage (kStage bytes) with coalesced 16-byte loads: returns the global
-// address the stage starts at (16-byte aligned) and, in *len, the bytes it
-// holds.  Bytes outside the heads' range are loaded byte-wise, only those
-// inside it.
 // 6 KiB: 64 heads of ~70 B fit with room to spare (heads past the stage are
 // read from HBM), and four waves' stages leave room for 3+ workgroups per CU
 // (8 KiB: 1.69, 6 KiB: 2.01, 4 KiB: 1.12 G requests/s on config 5)
 constexpr uint32_t kStage = 6144;
 constexpr uint32_t kMaskWords = kStage / 32;  // u32 words per structural mask of a stage
-__device__ __forceinline__ uint64_t stage_heads(glb_u8* raw, uint64_t lo, uint64_t hi, lds_u8* stage, uint32_t lane,
-                                                uint32_t* len) {
-  const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
-  const uint64_t a0 = glo & ~15ull;
-  const uint32_t nb = (uint32_t)min<uint64_t>((ghi - a0 + 15) & ~15ull, kStage);
-  for (uint32_t j = lane * 16; j < nb; j += 64 * 16) {
-    const uint64_t a = a0 + j;
-    uint4 v;
-    if (a >= glo && a + 16 <= ghi) {
-      v = to_uint4(*(glb_v4*)(uintptr_t)a);
-    } else {
-      uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-#pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        const uint64_t x = a + b;
-        const uint32_t byte = (x >= glo && x < ghi) ? *(glb_u8*)(uintptr_t)x : 0u;
-        const uint32_t sh = (b & 3) * 8;
-        if (b < 4) v0 |= byte << sh;
-        else if (b < 8) v1 |= byte << sh;
-        else if (b < 12) v2 |= byte << sh;
-        else v3 |= byte << sh;
-      }
-      v = make_uint4(v0, v1, v2, v3);
-    }
-    *(lds_v4*)(stage + j) = to_v4(v);
-  }
-  *len = nb;
-  return a0;
-}
-
 // A wave's LDS writes visible to its own later reads (and its reads done
 // before it overwrites the stage)
 __device__ __forceinline__ void wave_sync() {
@@ -371,18 +361,46 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t x, uint32_t nb) {
   return nb >= 4 ? x : x & ((1u << (8 * nb)) - 1u);
 }
 
-// The field a header name (stage bytes [k, k + nl)) is, or -1: the lowercase
-// (length, first 8, last 8) key in R.nkeys (raw_name_key), the bytes between
-// verified for longer names.
+// The special / nontchar bits of 128 stage bytes from `base` (a multiple of
+// 32) in registers: a lane's find-next-set over its head is register work,
+// the LDS masks are read past the window only (heads beyond ~100 bytes).
+struct MaskWin {
+  uint64_t s0, s1, n0, n1;
+  uint32_t base;
+};
+__device__ __forceinline__ MaskWin load_win(const lds_u32* msp, const lds_u32* mnt, uint32_t hs) {
+  const uint32_t w = hs >> 5;
+  MaskWin W;
+  W.base = w << 5;
+  W.s0 = (uint64_t)msp[w] | (uint64_t)msp[w + 1] << 32;
+  W.s1 = (uint64_t)msp[w + 2] | (uint64_t)msp[w + 3] << 32;
+  W.n0 = (uint64_t)mnt[w] | (uint64_t)mnt[w + 1] << 32;
+  W.n1 = (uint64_t)mnt[w + 2] | (uint64_t)mnt[w + 3] << 32;
+  return W;
+}
+// first set bit of (lo, hi) at or after bit r, or 128
+__device__ __forceinline__ uint32_t win_next(uint64_t lo, uint64_t hi, uint32_t r) {
+  const uint64_t a = r < 64 ? lo & (~0ull << r) : 0ull;
+  const uint64_t b = r < 64 ? hi : (r < 128 ? hi & (~0ull << (r - 64)) : 0ull);
+  return a ? (uint32_t)__builtin_ctzll(a) : (b ? 64u + (uint32_t)__builtin_ctzll(b) : 128u);
+}
+// next_set over a window (p >= base), the LDS mask past it
+__device__ __forceinline__ uint32_t wnext(uint64_t lo, uint64_t hi, uint32_t base, const lds_u32* m, uint32_t p,
+                                          uint32_t lim) {
+  if (p >= lim) return lim;
+  const uint32_t x = win_next(lo, hi, p - base);
+  if (x < 128) return min(base + x, lim);
+  if (base + 128 >= lim) return lim;
+  return next_set(m, max(p, base + 128), lim);
+}
+
+// The field of a header name from its key words (lowercased by the caller;
+// lo1 / hi0 / hi1 zero where the name is shorter), or -1: R.nkeys
+// (raw_name_key), the bytes between the first and last 8 verified for longer
+// names.
 template <class Tabs>
-__device__ __forceinline__ int field_of_key(const HttpRawDev& R, const Tabs& T, const lds_u8* st, uint32_t k,
-                                            uint32_t nl) {
-  uint32_t lo0 = lower4(keep_bytes(squad(st, k), nl)), lo1 = 0, hi0 = 0, hi1 = 0;
-  if (nl > 4) lo1 = lower4(keep_bytes(squad(st, k + 4), nl - 4));
-  if (nl > 8) {
-    hi0 = lower4(squad(st, k + nl - 8));
-    hi1 = lower4(squad(st, k + nl - 4));
-  }
+__device__ __forceinline__ int field_of_words(const HttpRawDev& R, const Tabs& T, const lds_u8* st, uint32_t k,
+                                              uint32_t nl, uint32_t lo0, uint32_t lo1, uint32_t hi0, uint32_t hi1) {
   uint32_t sl = raw_name_hash(nl, lo0, lo1, hi0, hi1) & R.nkmask;
   for (uint32_t probe = 0; probe <= R.nkmask; ++probe) {
     const uint32_t e0 = T.nkeys[8 * sl];
@@ -399,67 +417,107 @@ __device__ __forceinline__ int field_of_key(const HttpRawDev& R, const Tabs& T, 
   return -1;
 }
 
-// parse_head over the stage with the structural masks: the head is stage
-// bytes [hs, he).  Same results as parse_head (http_parse.cc semantics).
+// A parsed request: the value span {start - hs << 16 | length} of each field
+// it sets, in sp[f * stride] for the bits of `present`, and the sum of their
+// lengths (the walked string's length follows: walked_len).
+struct Parsed {
+  uint32_t present, vsum;
+  __device__ __forceinline__ void set(lds_u32* sp, uint32_t stride, uint32_t f, uint32_t span) {
+    sp[f * stride] = span;
+    present |= 1u << f;
+    vsum += span & 0xFFFFu;
+  }
+};
+__device__ __forceinline__ uint32_t walked_len(const HttpRawDev& R, const Parsed& P, uint32_t* last_out) {
+  const uint32_t last = P.present ? 32u - (uint32_t)__builtin_clz(P.present) : 0u;
+  const uint32_t np = (uint32_t)__popc(P.present);
+  *last_out = last;
+  return P.vsum + np + 2u * (last - np) + (last < R.nfields ? 1u : 0u);
+}
+
+// parse_head (http_parse.cc semantics) for a head inside the stage, bytes
+// [hs, he), over the structural masks.  Reads are issued in batches: the
+// request line's delimiter bytes and version in one round trip, then per
+// header line its first bytes, the name's end byte and key words and the
+// value's first two specials in one.
 template <class Tabs>
-__device__ __forceinline__ bool parse_head_masks(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
-                                                 const lds_u32* msp, const lds_u32* mnt, uint32_t hs, uint32_t he,
-                                                 lds_u32* sp, uint32_t stride) {
-  for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
+__device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
+                                                const lds_u32* msp, const lds_u32* mnt, uint32_t hs, uint32_t he,
+                                                lds_u32* sp, uint32_t stride, Parsed& P) {
+  RAW_PSTART;
+  P.present = P.vsum = 0;
   if (he - hs > kRawMaxHead) return false;
-  const uint32_t m = next_set(mnt, hs, he);  // method: a tchar run, then SP
-  if (m == hs || m >= he || sbyte(st, m) != ' ') return false;
+  const MaskWin W = load_win(msp, mnt, hs);
+  auto nS = [&](uint32_t p) { return wnext(W.s0, W.s1, W.base, msp, p, he); };
+  auto nN = [&](uint32_t p) { return wnext(W.n0, W.n1, W.base, mnt, p, he); };
+  const uint32_t m = nN(hs);  // method: a tchar run, then SP
   const uint32_t t0 = m + 1;
-  const uint32_t te = next_set(msp, t0, he);  // request-target: plain bytes, then SP
-  if (te == t0 || te >= he || sbyte(st, te) != ' ') return false;
-  uint32_t k = te + 1;
-  if (k + 10 > he) return false;  // "HTTP/" DIGIT "." DIGIT CRLF
+  const uint32_t te = nS(t0);  // request-target: plain bytes, then SP
   {
-    const uint32_t q0 = squad(st, k), q1 = squad(st, k + 4), q2 = squad(st, k + 8);
-    const uint32_t d1 = q1 >> 8 & 0xFFu, d2 = q1 >> 24;
-    if (q0 != 0x50545448u || (q1 & 0xFFu) != '/' || d1 < '0' || d1 > '9' || (q1 >> 16 & 0xFFu) != '.' || d2 < '0' ||
-        d2 > '9' || (q2 & 0xFFFFu) != 0x0A0Du)
+    // SP at m; " HTTP/" DIGIT "." DIGIT CRLF at te
+    const uint32_t bm = sbyte(st, m), q0 = squad(st, te), q1 = squad(st, te + 4), q2 = squad(st, te + 8);
+    if (m == hs || m >= he || te == t0 || te + 11 > he) return false;
+    if (bm != ' ' || q0 != 0x54544820u || (q1 & 0xFFFFu) != 0x2F50u || (q1 >> 24) != '.' ||
+        (q1 >> 16 & 0xFFu) - '0' > 9u || (q2 & 0xFFu) - '0' > 9u || (q2 >> 8 & 0xFFFFu) != 0x0A0Du)
       return false;
   }
-  k += 10;
+  RAW_PMARK(0);  // window, request line
+  uint32_t k = te + 11;
   bool have_host = false;
   uint32_t auth = kAbsentSpan;
   while (true) {
     if (k + 1 >= he) return false;  // no CRLF left: incomplete head
-    if ((squad(st, k) & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
-    const uint32_t c = next_set(mnt, k, he);  // name: a tchar run, then ':'
-    if (c == k || c >= he || sbyte(st, c) != ':') return false;
+    const uint32_t c = nN(k);       // name: a tchar run, then ':'
+    const uint32_t s1 = nS(c + 1);  // the value's first special, and the one after it
+    const uint32_t s2 = nS(s1 + 1);
+    const uint32_t qk = squad(st, k), bc = sbyte(st, c), r1 = squad(st, k + 4), r2 = squad(st, c - 8),
+                   r3 = squad(st, c - 4), q1 = squad(st, s1), q2 = squad(st, s2);
+    RAW_PMARK(1);  // a line's searches and reads
+    if ((qk & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
+    if (c == k || c >= he || bc != ':') return false;
     const uint32_t nl = c - k;
-    uint32_t v = c + 1, first = kAbsentSpan, lend = v, s;
-    while (true) {  // field-value to CRLF: IS_HEADER_CHAR, OWS trimmed
-      s = next_set(msp, v, he);
+    // field-value to CRLF: IS_HEADER_CHAR, OWS trimmed
+    uint32_t v = c + 1, first = kAbsentSpan, lend = v, s = s1, q = q1;
+    for (uint32_t it = 0;; ++it) {
       if (s > v) {
         if (first == kAbsentSpan) first = v;
         lend = s;
       }
       if (s >= he) return false;
-      const uint32_t x = sbyte(st, s);
+      const uint32_t x = q & 0xFFu;
       if (x == ' ' || x == '\t') {
         v = s + 1;
+        if (it == 0) {
+          s = s2;
+          q = q2;
+        } else {
+          s = nS(v);
+          q = squad(st, s);
+        }
         continue;
       }
-      if (x == '\r' && s + 1 < he && sbyte(st, s + 1) == '\n') break;
+      if (x == '\r' && s + 1 < he && (q >> 8 & 0xFFu) == '\n') break;
       return false;
     }
+    RAW_PMARK(2);  // value loop
     const uint32_t span = first == kAbsentSpan ? ((s - hs) << 16) : ((first - hs) << 16 | (lend - first));
-    const bool is_host = nl == 4 && lower4(squad(st, k)) == 0x74736F68u;  // "host"
-    if (is_host) {
+    const uint32_t lo0 = lower4(keep_bytes(qk, nl));
+    if (nl == 4 && lo0 == 0x74736F68u) {  // "host"
       if (!have_host) auth = span;  // the first value is the one the filter sees
       have_host = true;
     } else {
-      const int f = field_of_key(R, T, st, k, nl);
-      if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = span;  // first value wins
+      const uint32_t lo1 = nl > 4 ? lower4(keep_bytes(r1, nl - 4)) : 0u;
+      const uint32_t hi0 = nl > 8 ? lower4(r2) : 0u, hi1 = nl > 8 ? lower4(r3) : 0u;
+      const int f = field_of_words(R, T, st, k, nl, lo0, lo1, hi0, hi1);
+      if (f >= 0 && !(P.present >> f & 1u)) P.set(sp, stride, (uint32_t)f, span);  // first value wins
     }
     k = s + 2;
+    RAW_PMARK(3);  // name key, span
   }
-  if (R.f_method >= 0) sp[R.f_method * stride] = m - hs;
-  if (R.f_path >= 0) sp[R.f_path * stride] = (t0 - hs) << 16 | (te - t0);
-  if (R.f_authority >= 0 && have_host) sp[R.f_authority * stride] = auth;
+  RAW_PMARK(4);
+  if (R.f_method >= 0) P.set(sp, stride, (uint32_t)R.f_method, m - hs);
+  if (R.f_path >= 0) P.set(sp, stride, (uint32_t)R.f_path, (t0 - hs) << 16 | (te - t0));
+  if (R.f_authority >= 0 && have_host) P.set(sp, stride, (uint32_t)R.f_authority, auth);
   return true;
 }
 
@@ -514,10 +572,10 @@ __device__ __forceinline__ bool escapes_ok(uint32_t v, uint32_t e, Byte byte, Ne
 
 // A list inside the stage, bytes [hs, he), over its masks.
 template <class Tabs>
-__device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
-                                                 const lds_u32* mstop, const lds_u32* mzero, uint32_t hs, uint32_t he,
-                                                 lds_u32* sp, uint32_t stride) {
-  for (uint32_t f = 0; f < R.nfields; ++f) sp[f * stride] = kAbsentSpan;
+__device__ __forceinline__ bool parse_list_fast(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
+                                                const lds_u32* mstop, const lds_u32* mzero, uint32_t hs, uint32_t he,
+                                                lds_u32* sp, uint32_t stride, Parsed& P) {
+  P.present = P.vsum = 0;
   bool ok = true;
   for (uint32_t k = hs; k < he;) {
     const uint32_t ne = next_set(mzero, k, he), nl = ne - k;
@@ -535,8 +593,14 @@ __device__ __forceinline__ bool parse_list_masks(const HttpRawDev& R, const Tabs
       ok &= escapes_ok(
           v, e, [&](uint32_t x) { return sbyte(st, x); }, [&](uint32_t x, uint32_t lim) { return next_set(mstop, x, lim); });
     }
-    const int f = nl ? field_of_key(R, T, st, k, nl) : R.f_empty;
-    if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = (v - hs) << 16 | (e - v);  // first value wins
+    int f = R.f_empty;
+    if (nl) {
+      const uint32_t lo0 = lower4(keep_bytes(squad(st, k), nl));
+      const uint32_t lo1 = nl > 4 ? lower4(keep_bytes(squad(st, k + 4), nl - 4)) : 0u;
+      const uint32_t hi0 = nl > 8 ? lower4(squad(st, k + nl - 8)) : 0u, hi1 = nl > 8 ? lower4(squad(st, k + nl - 4)) : 0u;
+      f = field_of_words(R, T, st, k, nl, lo0, lo1, hi0, hi1);
+    }
+    if (f >= 0 && !(P.present >> f & 1u)) P.set(sp, stride, (uint32_t)f, (v - hs) << 16 | (e - v));  // first value wins
     k = e < he ? e + 1 : he;
   }
   return ok;
@@ -604,7 +668,7 @@ __device__ __forceinline__ uint32_t lookup_prog(const HttpRawDev& R, const Tabs&
     if (kk == 0xFFFFFFFFu) break;
     h = (h + 1) & R.phash_mask;
   }
-  return R.dflt[policy * 2 + (ingress ? 1 : 0)];
+  return T.dflt[policy * 2 + (ingress ? 1 : 0)];
 }
 
 template <class Tabs>
@@ -634,26 +698,20 @@ __device__ __forceinline__ lds_u32* key_counters(lds_u32* lds, uint32_t F) { ret
 // words][program hash keys][values] after the key counters, when they fit
 // (lds_tables): the lookups every header line and request makes, at LDS
 // latency instead of L1/L2
+// [default programs: 2 u32 per policy] — every table a lane reads inside the
+// loop: one global load there would make the wave wait for the next stage's
+// loads too (vmcnt counts in issue order)
 struct RawTableWords {
-  uint32_t nk, fs, fn, ph, wb;
+  uint32_t nk, fs, fn, ph, wb, df;
 };
 __host__ __device__ __forceinline__ RawTableWords raw_table_words(const HttpRawDev& R) {
-  return {8 * (R.nkmask + 1), 4 * (R.fmask + 1), (R.fnames_bytes + 3) / 4, R.phash_mask + 1, (R.nprogs + 31) / 32 + 1};
+  return {8 * (R.nkmask + 1), 4 * (R.fmask + 1), (R.fnames_bytes + 3) / 4, R.phash_mask + 1, (R.nprogs + 31) / 32 + 1,
+          2 * R.npolicies};
 }
 __host__ __device__ __forceinline__ uint32_t raw_tables_lds_words(const HttpRawDev& R) {
   const RawTableWords w = raw_table_words(R);
-  return w.nk + w.fs + w.fn + 2 * w.ph + w.wb;
+  return w.nk + w.fs + w.fn + 2 * w.ph + w.wb + w.df;
 }
-// The head of request i as a reader: in the stage if it lies inside it.
-__device__ __forceinline__ HeadReader head_of(glb_u8* raw, const uint64_t* __restrict__ off, size_t i,
-                                              const lds_u8* stage, uint64_t sbase, uint32_t slen) {
-  const uint64_t a = off[i], b = off[i + 1];
-  const uint32_t n = b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
-  const uint64_t ga = (uint64_t)(uintptr_t)(raw + a);
-  const bool in = ga >= sbase && ga + n <= sbase + slen;
-  return HeadReader(raw + a, n, stage + (in ? (uint32_t)(ga - sbase) : 0u), in);
-}
-
 // 16-byte chunks of a lane's output string: stored to dst, then dst +=
 // stride (uint4 units: a tile's next string unit, or the next arena line).
 struct Out16 {
@@ -710,38 +768,91 @@ __device__ __forceinline__ void emit_string(const HttpRawDev& R, HeadReader& hr,
   if (last < R.nfields) o.put(2u);  // REST
 }
 
+// 16 bytes of the stage from byte p (any alignment): five dword reads (one
+// round trip) and four byte aligns.
+__device__ __forceinline__ uint4 sread16(const lds_u8* st, uint32_t p) {
+  const lds_u32* w = (const lds_u32*)(st + (p & ~3u));
+  const uint32_t r = p & 3u, a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(b, a, r), __builtin_amdgcn_alignbyte(c, b, r),
+                    __builtin_amdgcn_alignbyte(d, c, r), __builtin_amdgcn_alignbyte(e, d, r));
+}
+// Unaligned stores (the byte address of a string position): the hardware
+// runs in unaligned mode (amdhsa), and one lane's stores to overlapping bytes
+// land in program order, so each store may leave bytes past its end that a
+// later store of the same string overwrites.
+typedef unsigned int u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
+typedef unsigned int u32_u __attribute__((aligned(1)));
+__device__ __forceinline__ void st16u(uint8_t* p, uint4 v) { *(u32x4_u*)p = u32x4_u{v.x, v.y, v.z, v.w}; }
+__device__ __forceinline__ void st4u(uint8_t* p, uint32_t v) { *(u32_u*)p = v; }
+// x with its bytes from nb (0..16) on zeroed
+__device__ __forceinline__ uint4 keep16(uint4 x, uint32_t nb) {
+  auto m = [&](uint32_t j) { return nb >= 4 * j + 4 ? 0xFFFFFFFFu : nb <= 4 * j ? 0u : (1u << (8 * (nb - 4 * j))) - 1u; };
+  return make_uint4(x.x & m(0), x.y & m(1), x.z & m(2), x.w & m(3));
+}
+// The walked string of a request parsed from the stage (emit_string's
+// output) stored at out: its present fields in order, each value copied 16
+// bytes at a time with its SEP (the zero byte after it in the last chunk),
+// each run of absent fields below the last present one as 0x01 SEP pairs.
+// Stores reach up to 15 bytes past the string (the record stride leaves
+// room: http_raw.cc cst).
+__device__ __forceinline__ void emit_direct(const HttpRawDev& R, const lds_u8* st, uint32_t hs, const lds_u32* sp,
+                                            uint32_t stride, const Parsed& P, uint32_t last, uint8_t* out) {
+  uint32_t f = 0, pos = 0;
+  for (uint32_t rem = P.present; rem; rem &= rem - 1) {
+    const uint32_t g = (uint32_t)__builtin_ctz(rem);
+    for (; f + 2 <= g; f += 2, pos += 4) st4u(out + pos, 0x00010001u);  // two absent fields
+    if (f < g) {
+      st4u(out + pos, 1u);
+      pos += 2;
+    }
+    const uint32_t sv = sp[g * stride], a = hs + (sv >> 16), L = sv & 0xFFFFu;
+    for (uint32_t k = 0; k <= L; k += 16) st16u(out + pos + k, keep16(sread16(st, a + k), min(L - k, 16u)));
+    pos += L + 1;
+    f = g + 1;
+  }
+  if (last < R.nfields) st4u(out + pos, 2u);  // REST
+}
+
 // A request's record in the string buffer (16-byte aligned, request order):
 // a 16-byte header {request index, remote identity, string length | flags
 // << 24, program} and the uncoded walked string.  A head of h bytes yields at
 // most h + 2F bytes of string (each absent field costs 2 bytes the head does
 // not hold; the request line and the blank line hold 13 bytes no string
-// does), so with a stride of cst >= 2F + 32 bytes per request the records
-// never overlap.
+// does; a list at most its own bytes + 2F + 1), so with a stride of cst >=
+// 2F + 48 bytes per request the records never overlap, the 15 bytes the
+// scan's last unaligned store may write past a string included.
 __device__ __forceinline__ uint64_t rec_off(uint64_t head_rel, size_t i, uint32_t cst) {
   return ((head_rel + 15) & ~15ull) + (uint64_t)cst * i;
 }
 
 // ---- pass 1: parse, program, string length, bucket key, the request's
 // record in the string buffer; per-block bucket counts (bcount[key * gridDim.x + block],
-// lds_keys) or a global histogram.  kLists: header lists, not heads;
-// kMasks: requests inside the stage parse over its structural bitmaps (else
-// through HeadReader's dword steps).
+// lds_keys) or a global histogram.  kLists: header lists, not heads.
+// Requests inside the wave's stage parse over its structural bitmaps;
+// the others are deferred to raw_defer_kernel.
 // A lane's request inputs, loaded two iterations ahead of their use.
 struct RawIn {
-  uint32_t pol, ing, port;
-  uint64_t a, b;  // off[i], off[i + 1]
+  uint32_t pol, rem, ip;  // policy, remote identity, ingress | port << 8
+  uint32_t len;           // head bytes (off[i + 1] - off[i], clamped)
+  uint64_t a;             // off[i]
+  __device__ __forceinline__ uint32_t ing() const { return ip & 0xFFu; }
+  __device__ __forceinline__ uint32_t port() const { return ip >> 8; }
 };
 __device__ __forceinline__ RawIn raw_in(const uint64_t* __restrict__ off, const uint32_t* __restrict__ policy,
                                         const uint8_t* __restrict__ ingress, const uint16_t* __restrict__ port,
-                                        size_t i, size_t n) {
-  const size_t j = i < n ? i : (n ? n - 1 : 0);  // unconditional loads (no branch around them)
+                                        const uint32_t* __restrict__ remote, size_t i, size_t n) {
+  // unconditional loads, selects after them: a load skipped on some path
+  // makes the compiler's wait for any older load a wait for every load
+  // (vmcnt(0)), the next stage's included
+  const size_t j = i < n ? i : (n ? n - 1 : 0);
   RawIn r;
-  r.pol = i < n ? policy[j] : 0xFFFFFFFFu;
-  r.ing = ingress[j];
-  r.port = port[j];
-  r.a = off[j];
-  r.b = off[j + 1];
-  if (i >= n) r.a = r.b;  // empty
+  const uint32_t pol = policy[j];
+  r.pol = i < n ? pol : 0xFFFFFFFFu;
+  r.ip = (uint32_t)ingress[j] | (uint32_t)port[j] << 8;
+  r.rem = remote[j];
+  const uint64_t a = off[j], b = off[j + 1];
+  r.a = i < n ? a : b;  // past n: empty at off[n]
+  r.len = i < n && b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
   return r;
 }
 constexpr uint32_t kStageVecs = kStage / (64 * 16);  // 16-B loads per lane for a whole stage
@@ -753,20 +864,26 @@ struct StageRegs {
   uint64_t base;
   uint32_t len;
 };
-__device__ __forceinline__ void stage_load(glb_u8* raw, const RawIn& in, uint32_t lane, StageRegs& S) {
+__device__ __forceinline__ void stage_load(glb_u8* raw, const RawIn& in, uint32_t lane, StageRegs& S,
+                                           const uint64_t* safe) {
   const uint64_t lo = __shfl(in.a, 0, 64);
-  // the last lane's end (empty lanes past n repeat off[n])
-  const uint64_t hi = __shfl(in.b, 63, 64);
+  // the last lane's end (empty lanes past n sit at off[n])
+  const uint64_t hi = __shfl(in.a + in.len, 63, 64);
   const uint64_t glo = (uint64_t)(uintptr_t)(raw + lo), ghi = (uint64_t)(uintptr_t)(raw + hi);
   const uint64_t a0 = glo & ~15ull;
   const uint32_t nb = hi > lo ? (uint32_t)min<uint64_t>((ghi - a0 + 15) & ~15ull, kStage) : 0u;
   S.base = a0;
   S.len = nb;
+  // every load issued (no branch around one, no select after one: either
+  // makes the compiler wait for it here): past the stage a harmless repeat of
+  // the first block; a wave without head bytes reads a block of off[] instead
+  // (readable; nothing of an empty stage is parsed)
+  const uint64_t src0 = nb ? a0 : ((uint64_t)(uintptr_t)safe & ~15ull);
 #pragma unroll
   for (uint32_t j = 0; j < kStageVecs; ++j) {
     const uint32_t o = (j * 64 + lane) * 16;
-    const uint64_t a = o < nb ? a0 + o : a0;  // past the stage: a harmless repeat of the first block
-    S.v[j] = nb ? to_uint4(*(glb_v4*)(uintptr_t)a) : make_uint4(0, 0, 0, 0);
+    const uint64_t a = o < nb ? a0 + o : src0;
+    S.v[j] = to_uint4(*(glb_v4*)(uintptr_t)a);
   }
 }
 __device__ __forceinline__ void stage_store(const StageRegs& S, lds_u8* stage, uint32_t lane) {
@@ -774,7 +891,12 @@ __device__ __forceinline__ void stage_store(const StageRegs& S, lds_u8* stage, u
   for (uint32_t j = 0; j < kStageVecs; ++j) *(lds_v4*)(stage + (j * 64 + lane) * 16) = to_v4(S.v[j]);
 }
 
-template <bool kLists, bool kMasks, bool kLdsTabs>
+// Bucket key of a request: walked string units (0..8) or the overflow key.
+__device__ __forceinline__ uint32_t bucket_key(uint32_t len) {
+  return len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
+}
+
+template <bool kLists, bool kLdsTabs>
 __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, const uint8_t* __restrict__ raw_g,
                                                                const uint64_t* __restrict__ off, size_t n,
                                                                const uint32_t* __restrict__ policy,
@@ -784,7 +906,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
                                                                const uint32_t* __restrict__ remote,
                                                                uint8_t* __restrict__ sbuf, uint32_t cst,
                                                                unsigned long long* __restrict__ ovf_bytes,
-                                                               uint32_t lds_keys) {
+                                                               uint32_t lds_keys, uint32_t* __restrict__ dlist,
+                                                               uint32_t* __restrict__ dcount) {
   extern __shared__ uint32_t lds_[];
   lds_u32* lds = (lds_u32*)lds_;
   glb_u8* raw = (glb_u8*)raw_g;
@@ -809,6 +932,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     lds_u32* tpk = tfn + w.fn;
     lds_u32* tpv = tpk + w.ph;
     lds_u32* twb = tpv + w.ph;
+    lds_u32* tdf = twb + w.wb;
     for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
     for (uint32_t k = threadIdx.x; k < w.fs; k += blockDim.x) tfs[k] = R.fslots[k];
     for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
@@ -822,10 +946,11 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
       tpv[k] = R.phash_vals[k];
     }
     for (uint32_t k = threadIdx.x; k < w.wb; k += blockDim.x) twb[k] = R.walk_bits[k];
-    T = LdsTabs{t, tfs, tpk, tpv, twb, (const lds_u8*)tfn};
+    for (uint32_t k = threadIdx.x; k < w.df; k += blockDim.x) tdf[k] = R.dflt[k];
+    T = LdsTabs{t, tfs, tpk, tpv, twb, tdf, (const lds_u8*)tfn};
   } else {
     T = GlbTabs{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
-                (glb_u32*)R.walk_bits, (glb_u8*)R.fnames};
+                (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
   }
   const uint64_t off0 = off[0];
   __syncthreads();
@@ -834,74 +959,74 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   const size_t gstride = (size_t)gridDim.x * kRawThreads;
   size_t base = (size_t)blockIdx.x * kRawThreads;
   // (a wave with no requests skips the loop and meets the others at the flush)
-  RawIn cur = raw_in(off, policy, ingress, port, base + wave * 64 + lane, n);
-  RawIn nxt = raw_in(off, policy, ingress, port, base + gstride + wave * 64 + lane, n);
+  RawIn cur = raw_in(off, policy, ingress, port, remote, base + wave * 64 + lane, n);
+  RawIn nxt = raw_in(off, policy, ingress, port, remote, base + gstride + wave * 64 + lane, n);
   StageRegs S;
-  if (base + (size_t)wave * 64 < n) stage_load(raw, cur, lane, S);
+  stage_load(raw, cur, lane, S, off);
+#ifdef CG_RAW_CLOCKS
+  uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0;
+#endif
   for (; base < n; base += gstride) {
     const size_t i0 = base + (size_t)wave * 64;
     if (i0 >= n) break;  // wave-uniform
+    RAW_CLK(c0);
     const size_t i = i0 + lane;
     const bool live = i < n;
-    const RawIn nn = raw_in(off, policy, ingress, port, base + 2 * gstride + wave * 64 + lane, n);
-    const uint32_t rem = remote[live ? i : 0];
+    const RawIn nn = raw_in(off, policy, ingress, port, remote, base + 2 * gstride + wave * 64 + lane, n);
     // stage k: registers → LDS (the previous iteration's reads are done)
     wave_sync();
     stage_store(S, stage, lane);
     const uint64_t sbase = S.base;
     const uint32_t slen = S.len;
     // stage k + 1 into registers, under this iteration's parse
-    if (base + gstride < n) stage_load(raw, nxt, lane, S);
+    stage_load(raw, nxt, lane, S, off);  // (past n: no bytes, nothing staged)
     wave_sync();
-    if (kMasks) {
-      if (kLists) build_masks_lists(stage, slen, tct, masks, lane);
-      else build_masks(stage, slen, tct, masks, lane);
-      wave_sync();
+    RAW_CLK(c1);
+    if (kLists) build_masks_lists(stage, slen, tct, masks, lane);
+    else build_masks(stage, slen, tct, masks, lane);
+    wave_sync();
+    RAW_CLK(c2);
+#ifdef CG_RAW_CLOCKS
+    c3 = c4 = c2;
+#endif
+    const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing() != 0, cur.port()) : kProgDeny;
+    // every request but an unknown policy's is parsed: a head the codec
+    // rejects is denied in any program (flagged malformed)
+    const uint32_t hn = cur.len;
+    const uint64_t ga = (uint64_t)(uintptr_t)(raw + cur.a);
+    const bool in = ga >= sbase && ga + hn <= sbase + slen;
+    // a request outside the stage goes to raw_defer_kernel (one append per wave)
+    const bool defer = live && prog != kProgDeny && !in;
+    const unsigned long long dm = __ballot(defer);
+    if (dm) {
+      uint32_t dbase = 0;
+      if (lane == (uint32_t)__builtin_ctzll(dm)) dbase = atomicAdd(dcount, (uint32_t)__popcll(dm));
+      dbase = (uint32_t)__shfl((int)dbase, (int)__builtin_ctzll(dm), 64);
+      if (defer) dlist[dbase + (uint32_t)__popcll(dm & ((1ull << lane) - 1))] = (uint32_t)i;
     }
-    const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing != 0, cur.port) : kProgDeny;
-    if (live) {
-      // every request but an unknown policy's is parsed: a head the codec
-      // rejects is denied in any program (flagged malformed)
-      const bool parse = prog != kProgDeny;
+    if (live && !defer) {
       uint32_t key = 0, len = 0, bad = 0;
       uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(cur.a - off0, i, cst));
-      if (parse) {
-        const uint32_t hn = cur.b > cur.a ? (uint32_t)min<uint64_t>(cur.b - cur.a, 0xFFFFFFFFull) : 0u;
-        const uint64_t ga = (uint64_t)(uintptr_t)(raw + cur.a);
-        const bool in = ga >= sbase && ga + hn <= sbase + slen;
-        HeadReader hr(raw + cur.a, hn, stage + (in ? (uint32_t)(ga - sbase) : 0u), in);
-        // heads / lists inside the stage parse over its masks, the rest byte by byte
-        const uint32_t hs = (uint32_t)(hr.lp - stage);
-        bool ok;
-        if (kLists) {
-          if (hr.n > kFieldsMaxList) {  // spans would not fit: the call fails
-            atomicOr(ovf_bytes, kRawListTooLong);
-            ok = false;
-          } else {
-            ok = kMasks && hr.in
-                     ? parse_list_masks(R, T, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
-                     : parse_list_bytes(R, T, hr, sp, kRawThreads);
-          }
-        } else {
-          ok = kMasks && hr.in
-                   ? parse_head_masks(R, T, stage, masks, masks + kMaskWords, hs, hs + hr.n, sp, kRawThreads)
-                   : parse_head(R, T, hr, sp, kRawThreads);
-        }
+      if (prog != kProgDeny) {
+        const uint32_t hs = (uint32_t)(ga - sbase);
+        Parsed P;
+        const bool ok = kLists ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
+                               : parse_head_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P);
+        RAW_CLK(c3);
         if (!ok) {
           bad = 1;
         } else if (walked_t(R, T, prog)) {
           uint32_t last;
-          len = string_len(R, sp, kRawThreads, &last);
-          key = len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
-          Out16 o(rec + 1, 1);
-          emit_string(R, hr, sp, kRawThreads, last, o);
-          if (o.pos) o.flush();
+          len = walked_len(R, P, &last);
+          key = bucket_key(len);
+          emit_direct(R, stage, hs, sp, kRawThreads, P, last, reinterpret_cast<uint8_t*>(rec + 1));
           if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
+          RAW_CLK(c4);
         }
       }
-      const uint32_t flags = (cur.ing ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
+      const uint32_t flags = (cur.ing() ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
                              (len > CG_HTTP_SLOT_BYTES ? CG_HTTP_F_OVERFLOW : 0u);
-      *rec = make_uint4((uint32_t)i, rem, len | flags << 24, prog);
+      *rec = make_uint4((uint32_t)i, cur.rem, len | flags << 24, prog);
       rinfo[i] = make_uint2(prog, len | bad << 31);
       const uint32_t k = group_of(R, prog) * kRawKeys + key;
       if (lds_keys) __hip_atomic_fetch_add(&lk[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -909,10 +1034,93 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     }
     cur = nxt;
     nxt = nn;
+    RAW_CLK(c5);
+    RAW_ACC(0, c0, c1);  // stage store (waits for the stage's loads)
+    RAW_ACC(1, c1, c2);  // structural masks
+    RAW_ACC(2, c2, c3);  // program lookup + parse
+    RAW_ACC(3, c3, c4);  // string length + emission
+    RAW_ACC(4, c4, c5);  // record header, rinfo, counters
+    RAW_ACC(5, c0, c5);
+#ifdef CG_RAW_CLOCKS
+    clk[6] += 1;
+#endif
   }
+#ifdef CG_RAW_CLOCKS
+  if (blockIdx.x == 7 && threadIdx.x == 64) {
+    printf("raw_scan clocks (wave 1 of block 7, %llu iterations): stage %llu masks %llu parse %llu emit %llu tail %llu total %llu\n",
+           (unsigned long long)clk[6], (unsigned long long)clk[0], (unsigned long long)clk[1], (unsigned long long)clk[2],
+           (unsigned long long)clk[3], (unsigned long long)clk[4], (unsigned long long)clk[5]);
+    printf("parse clocks: request line %llu, line reads %llu, values %llu, names %llu, end %llu\n", g_pclk[0], g_pclk[1],
+           g_pclk[2], g_pclk[3], g_pclk[4]);
+  }
+#endif
   if (lds_keys) {
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) counts[(size_t)k * gridDim.x + blockIdx.x] = lk[k];
+  }
+}
+
+// ---- pass 1b: the requests the scan deferred (heads / lists not inside
+// their wave's stage: long ones), one lane each, read byte by byte from HBM
+// through HeadReader with the tables in global memory.  Their bucket counts
+// go to the scan block that met them (nblk: the scan's grid), after it.
+template <bool kLists>
+__global__ __launch_bounds__(kRawThreads) void raw_defer_kernel(HttpRawDev R, const uint8_t* __restrict__ raw,
+                                                                const uint64_t* __restrict__ off,
+                                                                const uint32_t* __restrict__ policy,
+                                                                const uint8_t* __restrict__ ingress,
+                                                                const uint16_t* __restrict__ port,
+                                                                uint32_t* __restrict__ counts, uint32_t nblk,
+                                                                uint32_t lds_keys, uint2* __restrict__ rinfo,
+                                                                const uint32_t* __restrict__ remote,
+                                                                uint8_t* __restrict__ sbuf, uint32_t cst,
+                                                                unsigned long long* __restrict__ ovf_bytes,
+                                                                const uint32_t* __restrict__ dlist,
+                                                                const uint32_t* __restrict__ dcount) {
+  extern __shared__ uint32_t lds_[];
+  lds_u32* sp = (lds_u32*)lds_ + threadIdx.x;
+  const GlbTabs T{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+                  (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+  const uint32_t nd = *dcount;
+  const uint64_t off0 = off[0];
+  for (uint32_t j = blockIdx.x * kRawThreads + threadIdx.x; j < nd; j += gridDim.x * kRawThreads) {
+    const size_t i = dlist[j];
+    const uint64_t a = off[i], b = off[i + 1];
+    const uint32_t hn = b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
+    const uint32_t prog = lookup_prog(R, T, policy[i], ingress[i] != 0, port[i]);
+    HeadReader hr((glb_u8*)raw + a, hn, (const lds_u8*)0, false);
+    uint32_t key = 0, len = 0, bad = 0;
+    uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(a - off0, i, cst));
+    bool ok;
+    if (kLists) {
+      if (hn > kFieldsMaxList) {  // spans would not fit: the call fails
+        atomicOr(ovf_bytes, kRawListTooLong);
+        ok = false;
+      } else {
+        ok = parse_list_bytes(R, T, hr, sp, kRawThreads);
+      }
+    } else {
+      ok = parse_head(R, T, hr, sp, kRawThreads);
+    }
+    if (!ok) {
+      bad = 1;
+    } else if (walked(R, prog)) {
+      uint32_t last;
+      len = string_len(R, sp, kRawThreads, &last);
+      key = bucket_key(len);
+      Out16 o(rec + 1, 1);
+      emit_string(R, hr, sp, kRawThreads, last, o);
+      if (o.pos) o.flush();
+      if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
+    }
+    const uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
+                           (len > CG_HTTP_SLOT_BYTES ? CG_HTTP_F_OVERFLOW : 0u);
+    *rec = make_uint4((uint32_t)i, remote[i], len | flags << 24, prog);
+    rinfo[i] = make_uint2(prog, len | bad << 31);
+    const uint32_t k = group_of(R, prog) * kRawKeys + key;
+    // the scan's block of request i (grid-stride order, kRawThreads per block)
+    if (lds_keys) atomicAdd(&counts[(size_t)k * nblk + (i / kRawThreads) % nblk], 1u);
+    else atomicAdd(&counts[k], 1u);
   }
 }
 
@@ -1106,35 +1314,63 @@ size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
 // (occupancy) more than its global (L1-cached) lookups cost
 bool lds_codes_fit(const HttpRawDev& R) { return (size_t)R.nprogs * 256 <= 4 * 1024; }
 
+using ScanKernel = decltype(&raw_scan_kernel<false, false>);
+ScanKernel scan_kernel_for(const HttpRawDev& R, bool lists) {
+  const bool tabs = lds_tables_fit(R);
+  if (lists) return tabs ? raw_scan_kernel<true, true> : raw_scan_kernel<true, false>;
+  return tabs ? raw_scan_kernel<false, true> : raw_scan_kernel<false, false>;
+}
+
 }  // namespace
 
-size_t http_raw_grid(size_t n, int cus) { return grid_for(n, cus, 4); }
+// One resident round of scan workgroups: as many per CU as the scan's LDS
+// and registers allow (a grid past that runs a second, mostly idle round:
+// 4 requested per CU with 3 resident took 2 rounds of 475 stages per wave).
+size_t http_raw_grid(const HttpRawDev& R, bool lists, size_t n, int cus) {
+  const ScanKernel kern = scan_kernel_for(R, lists);
+  const size_t lds = raw_lds(R, http_raw_lds_keys(R), false);
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, size_t>, int> occ;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int per_cu = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = occ.find({dev, (const void*)kern, lds});
+    if (it == occ.end()) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kRawThreads, lds) != hipSuccess || nb < 1)
+        nb = 1;
+      it = occ.emplace(std::make_tuple(dev, (const void*)kern, lds), nb).first;
+    }
+    per_cu = it->second;
+  }
+  return grid_for(n, cus, (unsigned)per_cu);
+}
 
 bool http_raw_lds_keys(const HttpRawDev& R) { return ((size_t)R.nprogs + 2) * kRawKeys * 4 <= 32 * 1024; }
 
 int launch_http_raw_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off, size_t n,
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, uint32_t* counts,
                          void* rinfo, const uint32_t* remote, uint8_t* sbuf, uint32_t cst,
-                         unsigned long long* ovf_bytes, void* stream, int cus) {
+                         unsigned long long* ovf_bytes, uint32_t* dlist, uint32_t* dcount, void* stream, int cus) {
   if (!n) return 0;
   const bool lk = http_raw_lds_keys(R);
   const size_t lds = raw_lds(R, lk, false);
-  // CG_RAW_PARSE=bytes: HeadReader parsing for staged requests too (A/B)
-  static const bool masks = [] {
-    const char* e = getenv("CG_RAW_PARSE");
-    return !(e && std::string(e) == "bytes");
-  }();
-  const bool tabs = lds_tables_fit(R);
-  decltype(&raw_scan_kernel<false, false, false>) kern;
-  if (lists)
-    kern = masks ? (tabs ? raw_scan_kernel<true, true, true> : raw_scan_kernel<true, true, false>)
-                 : (tabs ? raw_scan_kernel<true, false, true> : raw_scan_kernel<true, false, false>);
-  else
-    kern = masks ? (tabs ? raw_scan_kernel<false, true, true> : raw_scan_kernel<false, true, false>)
-                 : (tabs ? raw_scan_kernel<false, false, true> : raw_scan_kernel<false, false, false>);
+  const ScanKernel kern = scan_kernel_for(R, lists);
+  const unsigned grid = (unsigned)http_raw_grid(R, lists, n, cus);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(kern, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw,
-                     off, n, policy, ingress, port, counts, (uint2*)rinfo, remote, sbuf, cst, ovf_bytes, (uint32_t)lk);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw, off, n, policy, ingress,
+                     port, counts, (uint2*)rinfo, remote, sbuf, cst, ovf_bytes, (uint32_t)lk, dlist, dcount);
+  // the deferred requests (their count stays on the device: a small grid
+  // that exits at once when there are none)
+  const size_t dlds = (size_t)std::max(R.nfields, 1u) * kRawThreads * 4;
+  const auto dk = lists ? raw_defer_kernel<true> : raw_defer_kernel<false>;
+  (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(dk, dim3((unsigned)std::max(1, cus) * 2), dim3(kRawThreads), dlds, (hipStream_t)stream, R, raw, off,
+                     policy, ingress, port, counts, grid, (uint32_t)lk, (uint2*)rinfo, remote, sbuf, cst, ovf_bytes,
+                     (const uint32_t*)dlist, (const uint32_t*)dcount);
   return (int)hipGetLastError();
 }
 
@@ -1145,12 +1381,13 @@ int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk
   return (int)hipGetLastError();
 }
 
-int launch_http_raw_rank(const HttpRawDev& R, size_t n, const uint64_t* off, uint32_t cst, const void* rinfo,
-                         uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream, int cus) {
+int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const uint64_t* off, uint32_t cst,
+                         const void* rinfo, uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream,
+                         int cus) {
   if (!n) return 0;
   const bool lk = http_raw_lds_keys(R);
   const size_t lds = lk ? ((size_t)R.nprogs + 2) * kRawKeys * 4 : 0;
-  hipLaunchKernelGGL(raw_rank_kernel, dim3((unsigned)http_raw_grid(n, cus)), dim3(kRawThreads), lds,
+  hipLaunchKernelGGL(raw_rank_kernel, dim3((unsigned)http_raw_grid(R, lists, n, cus)), dim3(kRawThreads), lds,
                      (hipStream_t)stream, R, n, off, cst, (const uint2*)rinfo, cursor, bbase, (uint32_t)lk, order);
   return (int)hipGetLastError();
 }

@@ -122,6 +122,8 @@ VARIANTS.update({
                      "__builtin_nontemporal_load(reinterpret_cast<const v4u*>((uintptr_t)a)); v = make_uint4(x.x, x.y, x.z, x.w); }")],
     "raw_nostr": [("kernels_http_raw.hip", "      for (uint32_t k = 0; k < L; k += 4) {  // a quad",
                    "      for (uint32_t k = 0; k < 0; k += 4) {  // a quad")],
+    # the scan's phases timed with the shader clock (printed by one wave)
+    "raw_clocks": [("kernels_http_raw.hip", "#include <hip/hip_runtime.h>\n", "#include <hip/hip_runtime.h>\n#define CG_RAW_CLOCKS 1\n")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
                       "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
 })
