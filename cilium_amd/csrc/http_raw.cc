@@ -266,7 +266,7 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   hip_check(hipMemsetAsync(order, 0xFF, nslots * 4, st), "hipMemsetAsync");  // padding slots
   auto* ttab = (HttpTile*)(batch + hdr.ttab_off);
   uint8_t* tdata = batch + hdr.tiles_off;
-  hip_check(launch_http_raw_rank(s.raw, lists, n, d_off, cst, rinfo, d_cursor, bbase, order, st, cus),
+  hip_check(launch_http_raw_rank(s.raw, lists, n, rinfo, d_cursor, bbase, order, st, cus),
             "raw rank kernel launch");
   hip_check(launch_http_raw_build(s.raw, d_runs, (uint32_t)runs.size(), tiles, ttab, tdata, order, sbuf, arena,
                                   ovf + 1, st, cus),

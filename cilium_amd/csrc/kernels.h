@@ -55,9 +55,8 @@ int launch_http_raw_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, co
                          unsigned long long* ovf_bytes, uint32_t* dlist, uint32_t* dcount, void* stream, int cus);
 int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk, uint32_t* bbase, uint32_t* hist,
                            void* stream);
-int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const uint64_t* off, uint32_t cst,
-                         const void* rinfo, uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream,
-                         int cus);
+int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const void* rinfo, uint32_t* cursor,
+                         const uint32_t* bbase, uint32_t* order, void* stream, int cus);
 int launch_http_raw_build(const HttpRawDev& R, const HttpRawRun* runs, uint32_t nruns, uint32_t ntiles,
                           HttpTile* ttab, uint8_t* tiles, uint32_t* order, const uint8_t* sbuf, uint8_t* arena,
                           unsigned long long* arena_cursor, void* stream, int cus);

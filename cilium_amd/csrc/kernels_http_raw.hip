@@ -467,13 +467,18 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
   uint32_t auth = kAbsentSpan;
   while (true) {
     if (k + 1 >= he) return false;  // no CRLF left: incomplete head
+    // a line starting with a special byte is the empty line (CRLF) or a
+    // rejected head: one bit test, no searches
+    if (wnext(W.s0, W.s1, W.base, msp, k, he) == k) {
+      if ((squad(st, k) & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
+      return false;
+    }
     const uint32_t c = nN(k);       // name: a tchar run, then ':'
     const uint32_t s1 = nS(c + 1);  // the value's first special, and the one after it
     const uint32_t s2 = nS(s1 + 1);
     const uint32_t qk = squad(st, k), bc = sbyte(st, c), r1 = squad(st, k + 4), r2 = squad(st, c - 8),
                    r3 = squad(st, c - 4), q1 = squad(st, s1), q2 = squad(st, s2);
     RAW_PMARK(1);  // a line's searches and reads
-    if ((qk & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
     if (c == k || c >= he || bc != ':') return false;
     const uint32_t nl = c - k;
     // field-value to CRLF: IS_HEADER_CHAR, OWS trimmed
@@ -501,11 +506,13 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
     }
     RAW_PMARK(2);  // value loop
     const uint32_t span = first == kAbsentSpan ? ((s - hs) << 16) : ((first - hs) << 16 | (lend - first));
-    const uint32_t lo0 = lower4(keep_bytes(qk, nl));
-    if (nl == 4 && lo0 == 0x74736F68u) {  // "host"
+    // "host" in any case: OR-ing 0x20 lowers letters and maps no other
+    // token byte onto one
+    if (nl == 4 && (qk | 0x20202020u) == 0x74736F68u) {
       if (!have_host) auth = span;  // the first value is the one the filter sees
       have_host = true;
     } else {
+      const uint32_t lo0 = lower4(keep_bytes(qk, nl));
       const uint32_t lo1 = nl > 4 ? lower4(keep_bytes(r1, nl - 4)) : 0u;
       const uint32_t hi0 = nl > 8 ? lower4(r2) : 0u, hi1 = nl > 8 ? lower4(r3) : 0u;
       const int f = field_of_words(R, T, st, k, nl, lo0, lo1, hi0, hi1);
@@ -1027,8 +1034,9 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
       const uint32_t flags = (cur.ing() ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
                              (len > CG_HTTP_SLOT_BYTES ? CG_HTTP_F_OVERFLOW : 0u);
       *rec = make_uint4((uint32_t)i, cur.rem, len | flags << 24, prog);
-      rinfo[i] = make_uint2(prog, len | bad << 31);
       const uint32_t k = group_of(R, prog) * kRawKeys + key;
+      // for the rank: the bucket and the record (16-B units)
+      rinfo[i] = make_uint2(k, (uint32_t)(rec_off(cur.a - off0, i, cst) / 16));
       if (lds_keys) __hip_atomic_fetch_add(&lk[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else atomicAdd(&counts[k], 1u);
     }
@@ -1116,8 +1124,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_defer_kernel(HttpRawDev R, co
     const uint32_t flags = (ingress[i] ? CG_HTTP_F_INGRESS : 0u) | (bad ? CG_HTTP_F_MALFORMED : 0u) |
                            (len > CG_HTTP_SLOT_BYTES ? CG_HTTP_F_OVERFLOW : 0u);
     *rec = make_uint4((uint32_t)i, remote[i], len | flags << 24, prog);
-    rinfo[i] = make_uint2(prog, len | bad << 31);
     const uint32_t k = group_of(R, prog) * kRawKeys + key;
+    rinfo[i] = make_uint2(k, (uint32_t)(rec_off(a - off0, i, cst) / 16));
     // the scan's block of request i (grid-stride order, kRawThreads per block)
     if (lds_keys) atomicAdd(&counts[(size_t)k * nblk + (i / kRawThreads) % nblk], 1u);
     else atomicAdd(&counts[k], 1u);
@@ -1155,9 +1163,11 @@ __global__ __launch_bounds__(256) void raw_prefix_kernel(const uint32_t* __restr
 
 // ---- pass 2: a slot per request from its bucket's cursor — the block's
 // LDS cursor per key (the key's first slot + this block's prefix, lds_keys:
-// the same grid and request order as the scan), else a global cursor per key
+// the same grid and request order as the scan), else a global cursor per
+// key: order[slot] = the request's record.  rinfo[i] = {bucket, record in
+// 16-B units} from the scan; kRankU requests per thread in flight.
+constexpr uint32_t kRankU = 4;
 __global__ __launch_bounds__(kRawThreads) void raw_rank_kernel(HttpRawDev R, size_t n,
-                                                               const uint64_t* __restrict__ off, uint32_t cst,
                                                                const uint2* __restrict__ rinfo,
                                                                uint32_t* __restrict__ cursor,
                                                                const uint32_t* __restrict__ bbase, uint32_t lds_keys,
@@ -1166,18 +1176,21 @@ __global__ __launch_bounds__(kRawThreads) void raw_rank_kernel(HttpRawDev R, siz
   const uint32_t nk = (R.nprogs + 2) * kRawKeys;
   if (lds_keys)
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = cursor[k] + bbase[(size_t)k * gridDim.x + blockIdx.x];
-  const uint64_t off0 = off[0];
   __syncthreads();
-  for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += (size_t)gridDim.x * kRawThreads) {
-    const size_t i = base + threadIdx.x;
-    if (i >= n) continue;
-    const uint2 ri = rinfo[i];
-    const uint32_t prog = ri.x, len = ri.y & 0x7FFFFFFFu;
-    const bool walk = walked(R, prog) && !(ri.y >> 31);
-    const uint32_t key = !walk ? 0u : len > CG_HTTP_SLOT_BYTES ? kRawKeys - 1 : (len + 15) / 16;
-    const uint32_t k = group_of(R, prog) * kRawKeys + key;
-    const uint32_t slot = lds_keys ? atomicAdd(&lk[k], 1u) : atomicAdd(&cursor[k], 1u);
-    order[slot] = (uint32_t)(rec_off(off[i] - off0, i, cst) / 16);  // the request's record
+  const size_t gs = (size_t)gridDim.x * kRawThreads;
+  for (size_t base = (size_t)blockIdx.x * kRawThreads; base < n; base += kRankU * gs) {
+    uint2 ri[kRankU];
+#pragma unroll
+    for (uint32_t u = 0; u < kRankU; ++u) {
+      const size_t i = base + u * gs + threadIdx.x;
+      ri[u] = rinfo[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kRankU; ++u) {
+      if (base + u * gs + threadIdx.x >= n) continue;
+      const uint32_t slot = lds_keys ? atomicAdd(&lk[ri[u].x], 1u) : atomicAdd(&cursor[ri[u].x], 1u);
+      order[slot] = ri[u].y;
+    }
   }
 }
 
@@ -1381,14 +1394,13 @@ int launch_http_raw_prefix(const uint32_t* bcount, uint32_t nkeys, uint32_t nblk
   return (int)hipGetLastError();
 }
 
-int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const uint64_t* off, uint32_t cst,
-                         const void* rinfo, uint32_t* cursor, const uint32_t* bbase, uint32_t* order, void* stream,
-                         int cus) {
+int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const void* rinfo, uint32_t* cursor,
+                         const uint32_t* bbase, uint32_t* order, void* stream, int cus) {
   if (!n) return 0;
   const bool lk = http_raw_lds_keys(R);
   const size_t lds = lk ? ((size_t)R.nprogs + 2) * kRawKeys * 4 : 0;
   hipLaunchKernelGGL(raw_rank_kernel, dim3((unsigned)http_raw_grid(R, lists, n, cus)), dim3(kRawThreads), lds,
-                     (hipStream_t)stream, R, n, off, cst, (const uint2*)rinfo, cursor, bbase, (uint32_t)lk, order);
+                     (hipStream_t)stream, R, n, (const uint2*)rinfo, cursor, bbase, (uint32_t)lk, order);
   return (int)hipGetLastError();
 }
 
