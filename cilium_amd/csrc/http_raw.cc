@@ -151,7 +151,8 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   // string buffer: request i's record (16-byte header + uncoded string) at
   // align16(off[i] - off[0]) + cst * i (kernels_http_raw.hip rec_off); the
   // build pass addresses records in 16-byte units through u32 order words
-  const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 48 + 15) & ~(size_t)15);
+  // (+128: room to move a record to a line start, kernels_http_raw.hip rec_off)
+  const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 48 + 15) & ~(size_t)15) + 128;
   // (+256: the build kernel reads whole 16-B chunks up to 8 units past a record's start)
   const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * n + 256;
   if (sbytes / 16 >= (1ull << 32)) {

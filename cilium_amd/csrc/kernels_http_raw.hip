@@ -827,7 +827,8 @@ __device__ __forceinline__ void emit_direct(const HttpRawDev& R, const lds_u8* s
 // not hold; the request line and the blank line hold 13 bytes no string
 // does; a list at most its own bytes + 2F + 1), so with a stride of cst >=
 // 2F + 48 bytes per request the records never overlap, the 15 bytes the
-// scan's last unaligned store may write past a string included.
+// scan's last unaligned store may write past a string included; 128 more let
+// the scan move a record to the next 128-B line start (see the scan).
 __device__ __forceinline__ uint64_t rec_off(uint64_t head_rel, size_t i, uint32_t cst) {
   return ((head_rel + 15) & ~15ull) + (uint64_t)cst * i;
 }
@@ -1013,7 +1014,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     }
     if (live && !defer) {
       uint32_t key = 0, len = 0, bad = 0;
-      uint4* rec = reinterpret_cast<uint4*>(sbuf + rec_off(cur.a - off0, i, cst));
+      uint64_t rpos = rec_off(cur.a - off0, i, cst);  // the record's byte offset (16-B aligned)
+      uint4* rec = reinterpret_cast<uint4*>(sbuf + rpos);
       if (prog != kProgDeny) {
         const uint32_t hs = (uint32_t)(ga - sbase);
         Parsed P;
@@ -1026,6 +1028,14 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
           uint32_t last;
           len = walked_len(R, P, &last);
           key = bucket_key(len);
+          // a record the build reads (header + len rounded to 16) that would
+          // straddle a 128-B line moves to the next line start when it fits
+          // one: the build gathers one line per record instead of two
+          const uint32_t ext = 16 + ((len + 15) & ~15u);
+          if ((rpos & 127) + ext > 128 && ext <= 128) {
+            rpos = (rpos + 127) & ~127ull;
+            rec = reinterpret_cast<uint4*>(sbuf + rpos);
+          }
           emit_direct(R, stage, hs, sp, kRawThreads, P, last, reinterpret_cast<uint8_t*>(rec + 1));
           if (len > CG_HTTP_SLOT_BYTES) atomicAdd(ovf_bytes, (unsigned long long)((4 + len + 15) & ~15u));
           RAW_CLK(c4);
@@ -1036,7 +1046,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
       *rec = make_uint4((uint32_t)i, cur.rem, len | flags << 24, prog);
       const uint32_t k = group_of(R, prog) * kRawKeys + key;
       // for the rank: the bucket and the record (16-B units)
-      rinfo[i] = make_uint2(k, (uint32_t)(rec_off(cur.a - off0, i, cst) / 16));
+      rinfo[i] = make_uint2(k, (uint32_t)(rpos / 16));
       if (lds_keys) __hip_atomic_fetch_add(&lk[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       else atomicAdd(&counts[k], 1u);
     }
@@ -1192,6 +1202,14 @@ __global__ __launch_bounds__(kRawThreads) void raw_rank_kernel(HttpRawDev R, siz
       order[slot] = ri[u].y;
     }
   }
+}
+
+// Nontemporal 16-byte load / store (streaming data read or written once)
+__device__ __forceinline__ uint4 ld_nt16(const uint4* p) {
+  return to_uint4(__builtin_nontemporal_load(reinterpret_cast<const v4u32*>(p)));
+}
+__device__ __forceinline__ void st_nt16(uint4* p, uint4 v) {
+  __builtin_nontemporal_store(to_v4(v), reinterpret_cast<v4u32*>(p));
 }
 
 // Four string bytes through a code map in LDS.

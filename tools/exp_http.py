@@ -124,6 +124,14 @@ VARIANTS.update({
                    "      for (uint32_t k = 0; k < 0; k += 4) {  // a quad")],
     # the scan's phases timed with the shader clock (printed by one wave)
     "raw_clocks": [("kernels_http_raw.hip", "#include <hip/hip_runtime.h>\n", "#include <hip/hip_runtime.h>\n#define CG_RAW_CLOCKS 1\n")],
+    # raw_build_kernel measuring devices / variants: no class coding (verdicts
+    # meaningless), nontemporal record loads, nontemporal tile stores
+    "rb_nocode": [("kernels_http_raw.hip", "      c = make_uint4(code4(lut, x.x), code4(lut, x.y), code4(lut, x.z), code4(lut, x.w));",
+                   "      c = x;")],
+    "rb_ntload": [("kernels_http_raw.hip", "      if (!pad && sub <= units) x = rec16[(size_t)rs + sub];",
+                   "      if (!pad && sub <= units) x = ld_nt16(rec16 + (size_t)rs + sub);")],
+    "rb_ntstore": [("kernels_http_raw.hip", "        reinterpret_cast<uint4*>(tb + 512)[(size_t)u * 64 + s] = c;",
+                    "        st_nt16(reinterpret_cast<uint4*>(tb + 512) + (size_t)u * 64 + s, c);")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
                       "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
 })
