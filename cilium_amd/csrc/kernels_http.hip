@@ -409,7 +409,18 @@ struct TilePre {
   uint2 meta;
   uint4 u[kPre];
 };
-__device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units, uint32_t lane, TilePre& p) {
+// The lane index recomputed where a tile address needs it (volatile: not
+// CSE'd with the kernel's copy, which the register allocator otherwise
+// spills at 64 VGPRs and reloads per tile — a scratch load that made the
+// next tile's prefetch wait for this tile's unit loads).
+__device__ __forceinline__ uint32_t lane_now() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+__device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units, uint32_t, TilePre& p) {
+  const uint32_t lane = lane_now();
   p.meta = NT_META(tr.meta + lane);
 #pragma unroll
   for (int k = 0; k < kPre; ++k)  // stays inside the tile (see tile_unit)
@@ -440,7 +451,8 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   constexpr int kWin = N < 4 ? (N > 0 ? N : 1) : 4;
   uint4 unit[kWin];
 #pragma unroll
-  for (int k = 0; k < kWin && k < N; ++k) unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : ld_nt(tr.units + k * kWave + lane);
+  for (int k = 0; k < kWin && k < N; ++k)
+    unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : ld_nt(tr.units + k * kWave + lane_now());
   if (has_next) tile_prefetch(trn, nunits, lane, nxt);
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t flags = meta.y >> 24;
@@ -451,7 +463,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     const uint4 u = unit[k % kWin];
-    if (k + kWin < N) unit[k % kWin] = ld_nt(tr.units + (k + kWin) * kWave + lane);
+    if (k + kWin < N) unit[k % kWin] = ld_nt(tr.units + (k + kWin) * kWave + lane_now());
     // the last unit: only the 4-byte groups holding some lane's string
     // (tail, wave-uniform), the rest is padding
     const bool last = k == N - 1;

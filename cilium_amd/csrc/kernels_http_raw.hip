@@ -365,33 +365,39 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t x, uint32_t nb) {
 // 32) in registers: a lane's find-next-set over its head is register work,
 // the LDS masks are read past the window only (heads beyond ~100 bytes).
 struct MaskWin {
-  uint64_t s0, s1, n0, n1;
+  uint32_t s[4], n[4];  // mask words base / 32 .. + 3
   uint32_t base;
 };
 __device__ __forceinline__ MaskWin load_win(const lds_u32* msp, const lds_u32* mnt, uint32_t hs) {
   const uint32_t w = hs >> 5;
   MaskWin W;
   W.base = w << 5;
-  W.s0 = (uint64_t)msp[w] | (uint64_t)msp[w + 1] << 32;
-  W.s1 = (uint64_t)msp[w + 2] | (uint64_t)msp[w + 3] << 32;
-  W.n0 = (uint64_t)mnt[w] | (uint64_t)mnt[w + 1] << 32;
-  W.n1 = (uint64_t)mnt[w + 2] | (uint64_t)mnt[w + 3] << 32;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    W.s[j] = msp[w + j];
+    W.n[j] = mnt[w + j];
+  }
   return W;
 }
-// first set bit of (lo, hi) at or after bit r, or 128
-__device__ __forceinline__ uint32_t win_next(uint64_t lo, uint64_t hi, uint32_t r) {
-  const uint64_t a = r < 64 ? lo & (~0ull << r) : 0ull;
-  const uint64_t b = r < 64 ? hi : (r < 128 ? hi & (~0ull << (r - 64)) : 0ull);
-  return a ? (uint32_t)__builtin_ctzll(a) : (b ? 64u + (uint32_t)__builtin_ctzll(b) : 128u);
+// window word j (0..3; 0 past the window), selected without a branch
+__device__ __forceinline__ uint32_t win_word(const uint32_t (&w)[4], uint32_t j) {
+  return j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : j == 3 ? w[3] : 0u;
 }
-// next_set over a window (p >= base), the LDS mask past it
-__device__ __forceinline__ uint32_t wnext(uint64_t lo, uint64_t hi, uint32_t base, const lds_u32* m, uint32_t p,
+// next_set over a window (p >= base): the 64 bits from the word holding p
+// (at least 33 from p) in registers, then the LDS mask
+__device__ __forceinline__ uint32_t wnext(const uint32_t (&w)[4], uint32_t base, const lds_u32* m, uint32_t p,
                                           uint32_t lim) {
-  if (p >= lim) return lim;
-  const uint32_t x = win_next(lo, hi, p - base);
-  if (x < 128) return min(base + x, lim);
-  if (base + 128 >= lim) return lim;
-  return next_set(m, max(p, base + 128), lim);
+  const uint32_t r = p - base, j = r >> 5;
+  const uint64_t x = (((uint64_t)win_word(w, j + 1) << 32) | win_word(w, j)) >> (r & 31);
+  if (x) return min(p + (uint32_t)__builtin_ctzll(x), lim);
+  // the first bit the pair did not cover (the window ends after word 3)
+  const uint32_t q = j < 4 ? base + 32 * min(j + 2, 4u) : p;
+  return q >= lim ? lim : next_set(m, q, lim);
+}
+// the bit at p (p >= base)
+__device__ __forceinline__ bool wbit(const uint32_t (&w)[4], uint32_t base, const lds_u32* m, uint32_t p) {
+  const uint32_t r = p - base;
+  return r < 128 ? (win_word(w, r >> 5) >> (r & 31)) & 1u : (m[p >> 5] >> (p & 31)) & 1u;
 }
 
 // The field of a header name from its key words (lowercased by the caller;
@@ -448,8 +454,8 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
   P.present = P.vsum = 0;
   if (he - hs > kRawMaxHead) return false;
   const MaskWin W = load_win(msp, mnt, hs);
-  auto nS = [&](uint32_t p) { return wnext(W.s0, W.s1, W.base, msp, p, he); };
-  auto nN = [&](uint32_t p) { return wnext(W.n0, W.n1, W.base, mnt, p, he); };
+  auto nS = [&](uint32_t p) { return p >= he ? he : wnext(W.s, W.base, msp, p, he); };
+  auto nN = [&](uint32_t p) { return p >= he ? he : wnext(W.n, W.base, mnt, p, he); };
   const uint32_t m = nN(hs);  // method: a tchar run, then SP
   const uint32_t t0 = m + 1;
   const uint32_t te = nS(t0);  // request-target: plain bytes, then SP
@@ -469,7 +475,7 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
     if (k + 1 >= he) return false;  // no CRLF left: incomplete head
     // a line starting with a special byte is the empty line (CRLF) or a
     // rejected head: one bit test, no searches
-    if (wnext(W.s0, W.s1, W.base, msp, k, he) == k) {
+    if (wbit(W.s, W.base, msp, k)) {
       if ((squad(st, k) & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
       return false;
     }
@@ -981,6 +987,9 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     const size_t i = i0 + lane;
     const bool live = i < n;
     const RawIn nn = raw_in(off, policy, ingress, port, remote, base + 2 * gstride + wave * 64 + lane, n);
+    // the program (LDS tables): done while the stage's loads and the previous
+    // iteration's record stores drain (the stage store below waits for both)
+    const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing() != 0, cur.port()) : kProgDeny;
     // stage k: registers → LDS (the previous iteration's reads are done)
     wave_sync();
     stage_store(S, stage, lane);
@@ -997,7 +1006,6 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
 #ifdef CG_RAW_CLOCKS
     c3 = c4 = c2;
 #endif
-    const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing() != 0, cur.port()) : kProgDeny;
     // every request but an unknown policy's is parsed: a head the codec
     // rejects is denied in any program (flagged malformed)
     const uint32_t hn = cur.len;

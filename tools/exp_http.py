@@ -132,6 +132,9 @@ VARIANTS.update({
                    "      if (!pad && sub <= units) x = ld_nt16(rec16 + (size_t)rs + sub);")],
     "rb_ntstore": [("kernels_http_raw.hip", "        reinterpret_cast<uint4*>(tb + 512)[(size_t)u * 64 + s] = c;",
                     "        st_nt16(reinterpret_cast<uint4*>(tb + 512) + (size_t)u * 64 + s, c);")],
+    # the tile walkers' lane offset as the kernel's (spilled) copy instead of recomputed
+    "h_nolanenow": [('  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\\n\\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));',
+                     "  l = threadIdx.x & 63;")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
                       "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
 })
