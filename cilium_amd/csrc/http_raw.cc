@@ -116,85 +116,125 @@ void http_raw_upload(HttpSnapshot& S) {
   S.raw_ok = !S.raw_values;  // proxylib snapshots take escaped values, not heads
 }
 
-void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawInput in, const uint8_t* d_raw,
-                          const uint64_t* d_off, size_t n, const uint32_t* d_policy, const uint8_t* d_ingress,
-                          const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, void* stream) {
-  const bool lists = in == RawInput::Lists;
-  if (lists ? !s.lists_ok : !s.raw_ok)
-    fail(CG_UNSUPPORTED, lists ? "header lists on the device: the snapshot has more than " +
-                                     std::to_string(kRawMaxFields) + " header fields"
-                               : "raw HTTP/1 heads: the snapshot has more than " + std::to_string(kRawMaxFields) +
-                                     " header fields, or is a proxylib snapshot");
-  if (!n) return;
-  const hipStream_t st = (hipStream_t)stream;
+namespace {
+
+// One raw call between its phases (raw_scan_phase → raw_rest_phase).  Tried:
+// two halves on two streams, the second half's scan under the first half's
+// rank and build — the streams shared one hardware queue, so nothing
+// overlapped (21.7 against 21.3 ms), not kept.
+struct RawCall {
+  const HttpSnapshot* s;
+  StagingSlot* sl;
+  int cus;
+  RawInput in;
+  const uint8_t* d_raw;
+  const uint64_t* d_off;
+  size_t n;
+  const uint32_t *d_policy, *d_remote;
+  const uint8_t* d_ingress;
+  const uint16_t* d_port;
+  uint8_t* d_out;
+  hipStream_t st;
+  // set by raw_scan_phase
+  size_t hist_bytes = 0;
+  uint8_t *small = nullptr, *hh = nullptr;
+  uint32_t* hist = nullptr;
+  unsigned long long* ovf = nullptr;
+  uint8_t* sbuf = nullptr;
+  void* rinfo = nullptr;
+  uint32_t *bbase = nullptr, nblk = 0;
+  RawCall half(size_t a, size_t m) const {
+    RawCall c = *this;
+    c.d_off = d_off + a;
+    c.n = m;
+    c.d_policy = d_policy + a;
+    c.d_ingress = d_ingress + a;
+    c.d_port = d_port + a;
+    c.d_remote = d_remote + a;
+    c.d_out = d_out + a;
+    return c;
+  }
+};
+
+// Workspace, the offsets' range, scan (+ deferred requests) and prefix
+// launched, their counts copied back (async).  false: the string buffer
+// would pass 2^32 16-B units — the caller splits the call.
+bool raw_scan_phase(RawCall& c) {
+  const HttpSnapshot& s = *c.s;
   const uint32_t np = (uint32_t)s.progs.size(), G = np + 2, K = kRawKeys;
   // workspace: [histogram G*K u32][overflow bytes u64][arena cursor u64][head
   // bytes u64][deferred-request count u32, pad]
-  const size_t hist_bytes = ((size_t)G * K * 4 + 7) & ~(size_t)7;
-  uint8_t* small = (uint8_t*)sl.dev_buf(8, hist_bytes + 32);
-  uint32_t* hist = (uint32_t*)small;
-  auto* ovf = (unsigned long long*)(small + hist_bytes);
-  hip_check(hipMemsetAsync(small, 0, hist_bytes + 16, st), "hipMemsetAsync");
+  c.hist_bytes = ((size_t)G * K * 4 + 7) & ~(size_t)7;
+  const size_t hist_bytes = c.hist_bytes;
+  c.small = (uint8_t*)c.sl->dev_buf(8, hist_bytes + 32);
+  uint8_t* small = c.small;
+  c.hist = (uint32_t*)small;
+  c.ovf = (unsigned long long*)(small + hist_bytes);
+  hip_check(hipMemsetAsync(small, 0, hist_bytes + 16, c.st), "hipMemsetAsync");
   // the head bytes [off[0], off[n]) size the string buffer
-  hip_check(hipMemcpyAsync(small + hist_bytes + 16, d_off + n, 8, hipMemcpyDeviceToDevice, st), "D2D");
-  hip_check(hipMemcpyAsync(small + hist_bytes + 8, d_off, 8, hipMemcpyDeviceToDevice, st), "D2D");
-  uint8_t* hh = (uint8_t*)sl.host_buf(8, hist_bytes + 24);
-  hip_check(hipMemcpyAsync(hh, small, hist_bytes + 24, hipMemcpyDeviceToHost, st), "D2H");
-  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  hip_check(hipMemcpyAsync(small + hist_bytes + 16, c.d_off + c.n, 8, hipMemcpyDeviceToDevice, c.st), "D2D");
+  hip_check(hipMemcpyAsync(small + hist_bytes + 8, c.d_off, 8, hipMemcpyDeviceToDevice, c.st), "D2D");
+  c.hh = (uint8_t*)c.sl->host_buf(8, hist_bytes + 24);
+  hip_check(hipMemcpyAsync(c.hh, small, hist_bytes + 24, hipMemcpyDeviceToHost, c.st), "D2H");
+  hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
   uint64_t o0, o1;
-  memcpy(&o0, hh + hist_bytes + 8, 8);
-  memcpy(&o1, hh + hist_bytes + 16, 8);
+  memcpy(&o0, c.hh + hist_bytes + 8, 8);
+  memcpy(&o1, c.hh + hist_bytes + 16, 8);
   if (o1 < o0) fail(CG_INVALID_ARGUMENT, "raw_off must be non-decreasing");
   // the arena cursor, the head-bytes slot, the deferred-request count
-  hip_check(hipMemsetAsync(small + hist_bytes + 8, 0, 24, st), "hipMemsetAsync");
+  hip_check(hipMemsetAsync(small + hist_bytes + 8, 0, 24, c.st), "hipMemsetAsync");
   auto* dcount = (uint32_t*)(small + hist_bytes + 24);
-  // string buffer: request i's record (16-byte header + uncoded string) at
-  // align16(off[i] - off[0]) + cst * i (kernels_http_raw.hip rec_off); the
-  // build pass addresses records in 16-byte units through u32 order words
+  // string buffer: request i's record (16-byte header + uncoded string) in
+  // its region at align16(off[i] - off[0]) + cst * i (kernels_http_raw.hip
+  // rec_off); the build pass addresses records in 16-byte units through u32
+  // order words
   // (+128: room to move a record to a line start, kernels_http_raw.hip rec_off)
   const uint32_t cst = (uint32_t)((2 * std::max<size_t>(s.raw.nfields, 1) + 48 + 15) & ~(size_t)15) + 128;
   // (+256: the build kernel reads whole 16-B chunks up to 8 units past a record's start)
-  const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * n + 256;
+  const size_t sbytes = ((o1 - o0 + 15) & ~(uint64_t)15) + (size_t)cst * c.n + 256;
   if (sbytes / 16 >= (1ull << 32)) {
-    if (n < 2) fail(CG_INVALID_ARGUMENT, "raw head too large");
-    const size_t h = n / 2;
-    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
-    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
-                         d_out + h, stream);
-    return;
+    if (c.n < 2) fail(CG_INVALID_ARGUMENT, "raw head too large");
+    return false;
   }
-  uint8_t* sbuf = (uint8_t*)sl.dev_buf(15, sbytes);
-  void* rinfo = sl.dev_buf(9, n * 8);
+  c.sbuf = (uint8_t*)c.sl->dev_buf(15, sbytes);
+  c.rinfo = c.sl->dev_buf(9, c.n * 8);
   // per-block bucket counts → per-block slot offsets (when the bucket
   // counters fit the kernels' LDS), else one global histogram
   const bool lds_keys = http_raw_lds_keys(s.raw);
-  const uint32_t nblk = (uint32_t)http_raw_grid(s.raw, lists, n, cus);
-  uint32_t* bcount = lds_keys ? (uint32_t*)sl.dev_buf(16, (size_t)G * K * nblk * 4) : hist;
-  uint32_t* bbase = lds_keys ? (uint32_t*)sl.dev_buf(17, (size_t)G * K * nblk * 4) : nullptr;
-  auto* dlist = (uint32_t*)sl.dev_buf(18, n * 4);
-  hip_check(launch_http_raw_scan(s.raw, lists, d_raw, d_off, n, d_policy, d_ingress, d_port, bcount, rinfo, d_remote,
-                                 sbuf, cst, ovf, dlist, dcount, st, cus),
+  const bool lists = c.in == RawInput::Lists;
+  c.nblk = (uint32_t)http_raw_grid(s.raw, lists, c.n, c.cus);
+  uint32_t* bcount = lds_keys ? (uint32_t*)c.sl->dev_buf(16, (size_t)G * K * c.nblk * 4) : c.hist;
+  c.bbase = lds_keys ? (uint32_t*)c.sl->dev_buf(17, (size_t)G * K * c.nblk * 4) : nullptr;
+  auto* dlist = (uint32_t*)c.sl->dev_buf(18, c.n * 4);
+  hip_check(launch_http_raw_scan(s.raw, lists, c.d_raw, c.d_off, c.n, c.d_policy, c.d_ingress, c.d_port, bcount,
+                                 c.rinfo, c.d_remote, c.sbuf, cst, c.ovf, dlist, dcount, c.st, c.cus),
             "raw scan kernel launch");
   if (lds_keys)
-    hip_check(launch_http_raw_prefix(bcount, G * K, nblk, bbase, hist, st), "raw prefix kernel launch");
-  hip_check(hipMemcpyAsync(hh, small, hist_bytes + 8, hipMemcpyDeviceToHost, st), "D2H");
-  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-  const uint32_t* hc = (const uint32_t*)hh;
+    hip_check(launch_http_raw_prefix(bcount, G * K, c.nblk, c.bbase, c.hist, c.st), "raw prefix kernel launch");
+  hip_check(hipMemcpyAsync(c.hh, small, hist_bytes + 8, hipMemcpyDeviceToHost, c.st), "D2H");
+  return true;
+}
+
+// Waits for the scan's counts, lays the batch out, launches rank, build and
+// http_kernel (no final sync).  false: the long strings need more than the
+// 256 MiB overflow arena — the caller splits the call.
+bool raw_rest_phase(RawCall& c) {
+  const HttpSnapshot& s = *c.s;
+  const uint32_t np = (uint32_t)s.progs.size(), G = np + 2, K = kRawKeys;
+  const size_t hist_bytes = c.hist_bytes;
+  hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
+  const uint32_t* hc = (const uint32_t*)c.hh;
   unsigned long long ovf_bytes;
-  memcpy(&ovf_bytes, hh + hist_bytes, 8);
+  memcpy(&ovf_bytes, c.hh + hist_bytes, 8);
   if (ovf_bytes & kRawListTooLong)
     fail(CG_INVALID_ARGUMENT, "a header list beyond " + std::to_string(kFieldsMaxList) +
                                   " bytes (evaluate it with cg_http_pack)");
+  // the meta word holds arena offsets / 16 in 24 bits: a batch whose long
+  // strings need more than 256 MiB of arena runs as two halves (one head is
+  // at most kRawMaxHead bytes, so halving always ends)
   if (ovf_bytes / 16 >= (1ull << 24)) {
-    // the meta word holds arena offsets / 16 in 24 bits: a batch whose long
-    // strings need more than 256 MiB of arena runs as two halves (one head
-    // is at most kRawMaxHead bytes, so halving always ends)
-    if (n < 2) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
-    const size_t h = n / 2;
-    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off, h, d_policy, d_ingress, d_port, d_remote, d_out, stream);
-    http_verdicts_raw_on(s, sl, cus, in, d_raw, d_off + h, n - h, d_policy + h, d_ingress + h, d_port + h, d_remote + h,
-                         d_out + h, stream);
-    return;
+    if (c.n < 2) fail(CG_INVALID_ARGUMENT, "overflow arena beyond 256 MiB");
+    return false;
   }
   // ---- layout: groups in program order (then allow, deny), 64-slot tiles,
   // chunks of <= kChunkTiles tiles, runs of tiles with equal string units
@@ -248,33 +288,62 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
   hdr.tiles_off = (hdr.ttab_off + sizeof(HttpTile) * tiles + 1023) & ~(uint64_t)1023;
   hdr.total_bytes = hdr.tiles_off + (uint64_t)gran * 512;
   hdr.arena_bytes = ovf_bytes;
-  uint8_t* batch = (uint8_t*)sl.dev_buf(10, hdr.total_bytes);
+  uint8_t* batch = (uint8_t*)c.sl->dev_buf(10, hdr.total_bytes);
   const size_t head = hdr.ttab_off;
-  uint8_t* hb = (uint8_t*)sl.host_buf(9, head + runs.size() * sizeof(HttpRawRun) + cursors.size() * 4);
+  uint8_t* hb = (uint8_t*)c.sl->host_buf(9, head + runs.size() * sizeof(HttpRawRun) + cursors.size() * 4);
   memcpy(hb, &hdr, sizeof(hdr));
   memcpy(hb + sizeof(hdr), chunks.data(), chunks.size() * sizeof(HttpChunk));
   uint8_t* hr = hb + head;
   memcpy(hr, runs.data(), runs.size() * sizeof(HttpRawRun));
   uint8_t* hcur = hr + runs.size() * sizeof(HttpRawRun);
   memcpy(hcur, cursors.data(), cursors.size() * 4);
-  auto* d_runs = (HttpRawRun*)sl.dev_buf(11, std::max<size_t>(runs.size(), 1) * sizeof(HttpRawRun));
-  auto* d_cursor = (uint32_t*)sl.dev_buf(12, cursors.size() * 4);
-  hip_check(hipMemcpyAsync(batch, hb, head, hipMemcpyHostToDevice, st), "H2D");
-  hip_check(hipMemcpyAsync(d_runs, hr, runs.size() * sizeof(HttpRawRun), hipMemcpyHostToDevice, st), "H2D");
-  hip_check(hipMemcpyAsync(d_cursor, hcur, cursors.size() * 4, hipMemcpyHostToDevice, st), "H2D");
-  uint8_t* arena = (uint8_t*)sl.dev_buf(13, std::max<unsigned long long>(ovf_bytes, 16));
-  auto* order = (uint32_t*)sl.dev_buf(14, nslots * 4);
-  hip_check(hipMemsetAsync(order, 0xFF, nslots * 4, st), "hipMemsetAsync");  // padding slots
+  auto* d_runs = (HttpRawRun*)c.sl->dev_buf(11, std::max<size_t>(runs.size(), 1) * sizeof(HttpRawRun));
+  auto* d_cursor = (uint32_t*)c.sl->dev_buf(12, cursors.size() * 4);
+  hip_check(hipMemcpyAsync(batch, hb, head, hipMemcpyHostToDevice, c.st), "H2D");
+  hip_check(hipMemcpyAsync(d_runs, hr, runs.size() * sizeof(HttpRawRun), hipMemcpyHostToDevice, c.st), "H2D");
+  hip_check(hipMemcpyAsync(d_cursor, hcur, cursors.size() * 4, hipMemcpyHostToDevice, c.st), "H2D");
+  uint8_t* arena = (uint8_t*)c.sl->dev_buf(13, std::max<unsigned long long>(ovf_bytes, 16));
+  auto* order = (uint32_t*)c.sl->dev_buf(14, nslots * 4);
+  hip_check(hipMemsetAsync(order, 0xFF, nslots * 4, c.st), "hipMemsetAsync");  // padding slots
   auto* ttab = (HttpTile*)(batch + hdr.ttab_off);
   uint8_t* tdata = batch + hdr.tiles_off;
-  hip_check(launch_http_raw_rank(s.raw, lists, n, rinfo, d_cursor, bbase, order, st, cus),
+  const bool lists = c.in == RawInput::Lists;
+  hip_check(launch_http_raw_rank(s.raw, lists, c.n, c.rinfo, d_cursor, c.bbase, order, c.st, c.cus),
             "raw rank kernel launch");
-  hip_check(launch_http_raw_build(s.raw, d_runs, (uint32_t)runs.size(), tiles, ttab, tdata, order, sbuf, arena,
-                                  ovf + 1, st, cus),
+  hip_check(launch_http_raw_build(s.raw, d_runs, (uint32_t)runs.size(), tiles, ttab, tdata, order, c.sbuf, arena,
+                                  c.ovf + 1, c.st, c.cus),
             "raw build kernel launch");
-  hip_check(launch_http(s.dev, batch, nslots, arena, d_out, st, cus, order), "http kernel launch");
+  hip_check(launch_http(s.dev, batch, nslots, arena, c.d_out, c.st, c.cus, order), "http kernel launch");
+  return true;
+}
+
+// A call (or half) run start to end on its stream; halves when it is too
+// large for one pass.
+void raw_sequential(RawCall c) {
+  if (!c.n) return;
+  if (!raw_scan_phase(c) || !raw_rest_phase(c)) {
+    const size_t h = c.n / 2;
+    raw_sequential(c.half(0, h));
+    raw_sequential(c.half(h, c.n - h));
+    return;
+  }
   // the workspace belongs to the lease: done before it is handed back
-  hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+  hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
+}
+
+}  // namespace
+
+void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawInput in, const uint8_t* d_raw,
+                          const uint64_t* d_off, size_t n, const uint32_t* d_policy, const uint8_t* d_ingress,
+                          const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, void* stream) {
+  const bool lists = in == RawInput::Lists;
+  if (lists ? !s.lists_ok : !s.raw_ok)
+    fail(CG_UNSUPPORTED, lists ? "header lists on the device: the snapshot has more than " +
+                                     std::to_string(kRawMaxFields) + " header fields"
+                               : "raw HTTP/1 heads: the snapshot has more than " + std::to_string(kRawMaxFields) +
+                                     " header fields, or is a proxylib snapshot");
+  raw_sequential(RawCall{&s, &sl, cus, in, d_raw, d_off, n, d_policy, d_remote, d_ingress, d_port, d_out,
+                         (hipStream_t)stream});
 }
 
 }  // namespace cg

@@ -320,22 +320,40 @@ __device__ __forceinline__ uint32_t special4(uint32_t x) {
   const uint32_t del = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;  // byte == 0x7F
   return pack4(lt | del);
 }
+// 16 stage bytes per lane per round (rounds wave-uniform, so a lane's pair
+// partner is always active): the half-words of a mask word come from lanes
+// 2m and 2m + 1, joined by a DPP pair swap.  (32 bytes per lane left the
+// last of three rounds a fifth full at config 5's ~4.5 KB stages.)
+__device__ __forceinline__ uint32_t pair_swap(uint32_t x) {  // quad_perm [1, 0, 3, 2]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+template <class Classify>
+__device__ __forceinline__ void build_masks16(const lds_u8* stage, uint32_t slen, lds_u32* masks, uint32_t lane,
+                                              Classify classify) {
+  for (uint32_t r = 0; r * 1024 < slen; ++r) {
+    const uint32_t u = r * 64 + lane;  // this lane's 16-byte unit
+    const uint4 a = to_uint4(*(const lds_v4*)(stage + 16 * u));
+    uint32_t m0, m1;  // 16-bit masks of the unit
+    classify(a, m0, m1);
+    const uint32_t o0 = pair_swap(m0), o1 = pair_swap(m1);
+    if (!(lane & 1u)) {
+      masks[u >> 1] = m0 | o0 << 16;
+      masks[kMaskWords + (u >> 1)] = m1 | o1 << 16;
+    }
+  }
+}
 __device__ __forceinline__ void build_masks(const lds_u8* stage, uint32_t slen, const lds_u8* tct, lds_u32* masks,
                                             uint32_t lane) {
-  for (uint32_t w = lane; w * 32 < slen; w += 64) {
-    const uint4 a = to_uint4(*(const lds_v4*)(stage + 32 * w));
-    const uint4 b = to_uint4(*(const lds_v4*)(stage + 32 * w + 16));
-    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t sp = 0, nt = 0;
+  build_masks16(stage, slen, masks, lane, [&](const uint4& a, uint32_t& sp, uint32_t& nt) {
+    const uint32_t d[4] = {a.x, a.y, a.z, a.w};
+    sp = nt = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 4; ++k) {
       sp |= special4(d[k]) << (4 * k);
 #pragma unroll
       for (int j = 0; j < 4; ++j) nt |= (uint32_t)tct[(d[k] >> (8 * j)) & 0xFFu] << (4 * k + j);
     }
-    masks[w] = sp;
-    masks[kMaskWords + w] = nt;
-  }
+  });
 }
 // First set bit at or after p (stage offsets), or lim when none before lim.
 __device__ __forceinline__ uint32_t next_set(const lds_u32* m, uint32_t p, uint32_t lim) {
@@ -548,20 +566,16 @@ __device__ __forceinline__ uint32_t zero4(uint32_t x) {  // bit per zero byte
 // masks: `stop` (list_stop, from the table tct) and `zero` (NUL)
 __device__ __forceinline__ void build_masks_lists(const lds_u8* stage, uint32_t slen, const lds_u8* tct,
                                                   lds_u32* masks, uint32_t lane) {
-  for (uint32_t w = lane; w * 32 < slen; w += 64) {
-    const uint4 a = to_uint4(*(const lds_v4*)(stage + 32 * w));
-    const uint4 b = to_uint4(*(const lds_v4*)(stage + 32 * w + 16));
-    const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t st = 0, zr = 0;
+  build_masks16(stage, slen, masks, lane, [&](const uint4& a, uint32_t& st, uint32_t& zr) {
+    const uint32_t d[4] = {a.x, a.y, a.z, a.w};
+    st = zr = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 4; ++k) {
       zr |= zero4(d[k]) << (4 * k);
 #pragma unroll
       for (int j = 0; j < 4; ++j) st |= (uint32_t)tct[(d[k] >> (8 * j)) & 0xFFu] << (4 * k + j);
     }
-    masks[w] = st;
-    masks[kMaskWords + w] = zr;
-  }
+  });
 }
 
 // The value bytes [v, e) of a proxylib snapshot's list: false when one is a
@@ -718,7 +732,9 @@ struct RawTableWords {
   uint32_t nk, fs, fn, ph, wb, df;
 };
 __host__ __device__ __forceinline__ RawTableWords raw_table_words(const HttpRawDev& R) {
-  return {8 * (R.nkmask + 1), 4 * (R.fmask + 1), (R.fnames_bytes + 3) / 4, R.phash_mask + 1, (R.nprogs + 31) / 32 + 1,
+  // (the FNV field slots are not staged: only the deferred requests' byte
+  // path looks names up through them, from global memory)
+  return {8 * (R.nkmask + 1), 0, (R.fnames_bytes + 3) / 4, R.phash_mask + 1, (R.nprogs + 31) / 32 + 1,
           2 * R.npolicies};
 }
 __host__ __device__ __forceinline__ uint32_t raw_tables_lds_words(const HttpRawDev& R) {
@@ -948,7 +964,6 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
     lds_u32* twb = tpv + w.ph;
     lds_u32* tdf = twb + w.wb;
     for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
-    for (uint32_t k = threadIdx.x; k < w.fs; k += blockDim.x) tfs[k] = R.fslots[k];
     for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
       uint32_t v = 0;
       for (uint32_t j = 0; j < 4; ++j)
@@ -1037,11 +1052,12 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
           len = walked_len(R, P, &last);
           key = bucket_key(len);
           // a record the build reads (header + len rounded to 16) that would
-          // straddle a 128-B line moves to the next line start when it fits
-          // one: the build gathers one line per record instead of two
-          const uint32_t ext = 16 + ((len + 15) & ~15u);
-          if ((rpos & 127) + ext > 128 && ext <= 128) {
-            rpos = (rpos + 127) & ~127ull;
+          // straddle a 64-B sector (records up to 64 B) or a 128-B line
+          // (up to 128 B) moves to the next one's start: the build gathers
+          // one sector / line per record instead of two
+          const uint32_t ext = 16 + ((len + 15) & ~15u), g = ext <= 64 ? 64u : 128u;
+          if ((rpos & (g - 1)) + ext > g && ext <= 128) {
+            rpos = (rpos + g - 1) & ~(uint64_t)(g - 1);
             rec = reinterpret_cast<uint4*>(sbuf + rpos);
           }
           emit_direct(R, stage, hs, sp, kRawThreads, P, last, reinterpret_cast<uint8_t*>(rec + 1));

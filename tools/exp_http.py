@@ -135,6 +135,15 @@ VARIANTS.update({
     # the tile walkers' lane offset as the kernel's (spilled) copy instead of recomputed
     "h_nolanenow": [('  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\\n\\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));',
                      "  l = threadIdx.x & 63;")],
+    # measuring device (verdicts land in order[] in slot order, out[] is not
+    # written): raw-mode http_kernel without the verdict scatter
+    "h_noscatter": [("      const uint32_t r = order[slot];\n      if (r != 0xFFFFFFFFu) out[r] = (uint8_t)v;",
+                     "      const uint32_t r = order[slot];\n      if (r != 0xFFFFFFFFu) const_cast<uint32_t*>(order)[slot] = v;")],
+    # 5 KiB stages with the scan capped at 128 VGPRs (4 waves per SIMD when
+    # LDS allows: 40.9 KB per block at config 5)
+    "raw_s5k_w4": _rs(5120) + [("kernels_http_raw.hip",
+                                "__global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(",
+                                "__global__ __launch_bounds__(kRawThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void raw_scan_kernel(")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
                       "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
 })
