@@ -813,17 +813,12 @@ typedef unsigned int u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
 typedef unsigned int u32_u __attribute__((aligned(1)));
 __device__ __forceinline__ void st16u(uint8_t* p, uint4 v) { *(u32x4_u*)p = u32x4_u{v.x, v.y, v.z, v.w}; }
 __device__ __forceinline__ void st4u(uint8_t* p, uint32_t v) { *(u32_u*)p = v; }
-// x with its bytes from nb (0..16) on zeroed
-__device__ __forceinline__ uint4 keep16(uint4 x, uint32_t nb) {
-  auto m = [&](uint32_t j) { return nb >= 4 * j + 4 ? 0xFFFFFFFFu : nb <= 4 * j ? 0u : (1u << (8 * (nb - 4 * j))) - 1u; };
-  return make_uint4(x.x & m(0), x.y & m(1), x.z & m(2), x.w & m(3));
-}
 // The walked string of a request parsed from the stage (emit_string's
 // output) stored at out: its present fields in order, each value copied 16
-// bytes at a time with its SEP (the zero byte after it in the last chunk),
-// each run of absent fields below the last present one as 0x01 SEP pairs.
-// Stores reach up to 15 bytes past the string (the record stride leaves
-// room: http_raw.cc cst).
+// bytes at a time and followed by its SEP, each run of absent fields below
+// the last present one as 0x01 SEP pairs.  Stores reach up to 15 bytes past
+// the string (the record stride leaves room: http_raw.cc cst); the build
+// reads the string's length only.
 __device__ __forceinline__ void emit_direct(const HttpRawDev& R, const lds_u8* st, uint32_t hs, const lds_u32* sp,
                                             uint32_t stride, const Parsed& P, uint32_t last, uint8_t* out) {
   uint32_t f = 0, pos = 0;
@@ -835,7 +830,10 @@ __device__ __forceinline__ void emit_direct(const HttpRawDev& R, const lds_u8* s
       pos += 2;
     }
     const uint32_t sv = sp[g * stride], a = hs + (sv >> 16), L = sv & 0xFFFFu;
-    for (uint32_t k = 0; k <= L; k += 16) st16u(out + pos + k, keep16(sread16(st, a + k), min(L - k, 16u)));
+    // whole 16-byte chunks of stage bytes (the bytes past L are overwritten:
+    // first by the SEP below, then by what follows it), then the SEP
+    for (uint32_t k = 0; k < L; k += 16) st16u(out + pos + k, sread16(st, a + k));
+    out[pos + L] = 0;  // SEP
     pos += L + 1;
     f = g + 1;
   }
@@ -1200,7 +1198,7 @@ __global__ __launch_bounds__(256) void raw_prefix_kernel(const uint32_t* __restr
 // the same grid and request order as the scan), else a global cursor per
 // key: order[slot] = the request's record.  rinfo[i] = {bucket, record in
 // 16-B units} from the scan; kRankU requests per thread in flight.
-constexpr uint32_t kRankU = 4;
+constexpr uint32_t kRankU = 8;
 __global__ __launch_bounds__(kRawThreads) void raw_rank_kernel(HttpRawDev R, size_t n,
                                                                const uint2* __restrict__ rinfo,
                                                                uint32_t* __restrict__ cursor,

@@ -144,6 +144,7 @@ VARIANTS.update({
     "raw_s5k_w4": _rs(5120) + [("kernels_http_raw.hip",
                                 "__global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(",
                                 "__global__ __launch_bounds__(kRawThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void raw_scan_kernel(")],
+    "rank_u4": [("kernels_http_raw.hip", "constexpr uint32_t kRankU = 8;", "constexpr uint32_t kRankU = 4;")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
                       "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
 })
