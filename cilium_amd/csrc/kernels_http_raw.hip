@@ -408,8 +408,12 @@ __device__ __forceinline__ uint32_t wnext(const uint32_t (&w)[4], uint32_t base,
   const uint32_t r = p - base, j = r >> 5;
   const uint64_t x = (((uint64_t)win_word(w, j + 1) << 32) | win_word(w, j)) >> (r & 31);
   if (x) return min(p + (uint32_t)__builtin_ctzll(x), lim);
-  // the first bit the pair did not cover (the window ends after word 3)
-  const uint32_t q = j < 4 ? base + 32 * min(j + 2, 4u) : p;
+  if (j < 2) {  // the window's other two words (long targets and values)
+    const uint64_t y = ((uint64_t)win_word(w, j + 3) << 32) | win_word(w, j + 2);
+    if (y) return min(base + 32 * (j + 2) + (uint32_t)__builtin_ctzll(y), lim);
+  }
+  // the first bit the window did not cover
+  const uint32_t q = j < 4 ? base + 128 : p;
   return q >= lim ? lim : next_set(m, q, lim);
 }
 // the bit at p (p >= base)
