@@ -1543,17 +1543,22 @@ int cg_diag_prefilter_eval_host(uint64_t h, uint32_t pf_id, const uint32_t* v4, 
       uint64_t hi = be64(v6 + 32 * i), lo = be64(v6 + 32 * i + 8);
       bool drop = false;
       if (p.v6_filter) {
-        const uint64_t t = hi >> (64 - p.v6_bits);
-        const int64_t cnt = p.v6_idx[(size_t)1 << p.v6_bits];
-        int64_t L = p.v6_idx[t], R = std::min<int64_t>(p.v6_idx[t + 1], cnt - 1);
-        int64_t ans = -1;
-        while (L <= R) {
-          int64_t mid = (L + R) >> 1;
-          std::pair<uint64_t, uint64_t> lo_m{p.v6_iv[4 * mid], p.v6_iv[4 * mid + 1]};
-          if (!(std::make_pair(hi, lo) < lo_m)) ans = mid, L = mid + 1;
-          else R = mid - 1;
+        const uint32_t t = (uint32_t)(hi >> (64 - p.v6_bits));
+        uint32_t m;
+        const uint32_t code = v6_code_of(p.v6_code[t >> 4], t, &m);
+        drop = code == 1;
+        if (code == kLpmPartial) {
+          const uint32_t e = p.v6_mix[m], span = e & 15;
+          int64_t R = e >> 4, L = span == 15 ? 0 : R - span;
+          int64_t ans = -1;
+          while (L <= R) {
+            int64_t mid = (L + R) >> 1;
+            std::pair<uint64_t, uint64_t> lo_m{p.v6_iv[4 * mid], p.v6_iv[4 * mid + 1]};
+            if (!(std::make_pair(hi, lo) < lo_m)) ans = mid, L = mid + 1;
+            else R = mid - 1;
+          }
+          drop = ans >= 0 && !(std::make_pair(p.v6_iv[4 * ans + 2], p.v6_iv[4 * ans + 3]) < std::make_pair(hi, lo));
         }
-        drop = ans >= 0 && !(std::make_pair(p.v6_iv[4 * ans + 2], p.v6_iv[4 * ans + 3]) < std::make_pair(hi, lo));
       }
       if (!drop) drop = !ep6(be64(v6 + 32 * i + 16), be64(v6 + 32 * i + 24));
       out6[i] = drop ? CG_XDP_DROP : CG_XDP_PASS;

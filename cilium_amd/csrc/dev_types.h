@@ -92,9 +92,16 @@ CG_HD inline void l4_place(uint64_t key, uint32_t mask, uint32_t* b1, uint32_t* 
 // partial /24's 256-bit leaf (4 x u64 over the last octet) is leaf_base of its
 // /16 plus the partial /24s before it in the chunk.
 // IPv6: disjoint covered intervals sorted by lo, 32-B records {lo hi-word,
-// lo lo-word, hi hi-word, hi lo-word}, indexed by the top v6_bits address bits
-// (sized so buckets hold ~1 interval): v6_idx[t] = first interval whose
-// hi >= t << (128 - v6_bits), v6_idx[1 << v6_bits] = count.
+// lo lo-word, hi hi-word, hi lo-word}, bucketed by the top v6_bits address
+// bits (~2 buckets per interval).  Level 1 is the v4 scheme again: one 2-bit
+// code per bucket (0 no interval touches it, 1 one interval covers it, 2
+// mixed), 16 per u64 word whose high half counts the mixed buckets before the
+// word — 512 KiB at 2^20 buckets, L2 resident, and it settles every address
+// outside the mixed buckets.  A mixed bucket's u32 in v6_mix is R << 4 |
+// min(R - L, 15): its candidate intervals are [L, R] (L = first interval with
+// hi >= the bucket start, R = the last one with lo <= the bucket end; 15
+// means "search from 0", correct because earlier intervals end before the
+// bucket), so a mixed lookup reads one 4-B entry and the interval records.
 // Local endpoints (cilium_lxc): open addressing, linear probing, 0 = empty
 // slot (the all-zero address is a flag of its own).
 constexpr uint32_t kLpmPartial = 2;
@@ -104,8 +111,9 @@ struct LpmDev {
   const uint32_t* mid;       // 16 words per mixed /16: its /24 codes
   const uint32_t* leaf_base; // per mixed /16: partial /24s before it
   const uint64_t* leaves;    // 4 u64 per partial /24, in address order
-  const uint32_t* v6_idx;    // (1 << v6_bits) + 1 entries (nullptr: no v6 filter)
-  const uint64_t* v6_iv;     // 4 u64 per interval
+  const uint64_t* v6_code;   // (1 << v6_bits) / 16 words (nullptr: no v6 filter)
+  const uint32_t* v6_mix;    // per mixed bucket (at least one entry)
+  const uint64_t* v6_iv;     // 4 u64 per interval (at least one record)
   uint32_t v6_bits;
   const uint32_t* ep4_keys;  // v4 endpoint table (network-order addresses)
   uint32_t ep4_mask;
@@ -123,6 +131,12 @@ CG_HD inline uint32_t ep_hash128(uint64_t hi, uint64_t lo) {
 }
 // Partial-block count among the 16 2-bit codes of a word (code 2 = binary 10).
 CG_HD inline uint32_t lpm_partials(uint32_t w) { return w & ~(w << 1) & 0xAAAAAAAAu; }
+// IPv6 bucket tb: its code (0/1/2) and, for a mixed one, its v6_mix index.
+CG_HD inline uint32_t v6_code_of(uint64_t cw, uint32_t tb, uint32_t* m) {
+  const uint32_t w = (uint32_t)cw, sh = 2 * (tb & 15);
+  *m = (uint32_t)(cw >> 32) + (uint32_t)__builtin_popcount(lpm_partials(w) & ((1u << sh) - 1));
+  return (w >> sh) & 3;
+}
 
 // ---------------------------------------------------------------- HTTP ----
 // Program = one (policy, direction, port) evaluation: Envoy's exact-port

@@ -414,7 +414,7 @@ __device__ __forceinline__ bool le128(uint64_t ah, uint64_t al, uint64_t bh, uin
 }
 
 // Binary search over intervals [L, R] for the last lo <= addr (more than two
-// candidates in the bucket: rare with ~2 buckets per interval).
+// candidates in a mixed bucket: rare with ~2 buckets per interval).
 __device__ __forceinline__ int64_t v6_search(const LpmDev& t, uint64_t hi, uint64_t lo, int64_t L, int64_t R) {
   int64_t ans = -1;
   while (L <= R) {
@@ -482,7 +482,6 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
     }
   }
   // ---- IPv6: {saddr[16], daddr[16]} per packet
-  const int64_t icnt = v6f ? (int64_t)t.v6_idx[(size_t)1 << t.v6_bits] : 0;
   for (size_t base = (size_t)blockIdx.x * blockDim.x * kLpmV6; base < n6; base += nthreads * kLpmV6) {
     uint64_t sh[kLpmV6], sl[kLpmV6], dh[kLpmV6], dl[kLpmV6];
 #pragma unroll
@@ -496,31 +495,34 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
       dh[u] = bswap64(u64_of(b.x, b.y));
       dl[u] = bswap64(u64_of(b.z, b.w));
     }
-    int64_t L[kLpmV6], R[kLpmV6];
+    uint64_t cw[kLpmV6];
     uint4 e[kLpmV6];
     uint32_t eh[kLpmV6];
 #pragma unroll
     for (uint32_t u = 0; u < kLpmV6; ++u) {
-      if (v6f) {
-        const uint64_t tb = sh[u] >> (64 - t.v6_bits);
-        L[u] = t.v6_idx[tb];
-        R[u] = t.v6_idx[tb + 1];
-      } else {
-        L[u] = 0;
-        R[u] = -1;
-      }
+      cw[u] = v6f ? t.v6_code[sh[u] >> (68 - t.v6_bits)] : 0;
       eh[u] = ep_hash128(dh[u], dl[u]) & t.ep6_mask;
       e[u] = *reinterpret_cast<const uint4*>(t.ep6_keys + 2 * (size_t)eh[u]);
     }
-    // the top two candidates of each bucket, loaded together
+    // level 2 (mixed buckets only; the others read entry 0, a hot line,
+    // instead of branching around the load)
+    uint32_t code[kLpmV6], mx[kLpmV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kLpmV6; ++u) {
+      uint32_t m;
+      code[u] = v6_code_of(cw[u], (uint32_t)(sh[u] >> (64 - t.v6_bits)), &m);
+      mx[u] = t.v6_mix[code[u] == kLpmPartial ? m : 0];
+    }
+    // the top two candidates of a mixed bucket, loaded together
+    int64_t L[kLpmV6], R[kLpmV6];
     uint4 c1lo[kLpmV6], c1hi[kLpmV6], c0lo[kLpmV6], c0hi[kLpmV6];
 #pragma unroll
     for (uint32_t u = 0; u < kLpmV6; ++u) {
-      R[u] = R[u] < icnt - 1 ? R[u] : icnt - 1;
-      // empty bucket (most random addresses): read record 0, a cache-resident
-      // line, instead of branching around the loads
-      const bool any = R[u] >= L[u];
-      const int64_t r1 = any ? R[u] : 0, r0 = any && R[u] - 1 >= L[u] ? R[u] - 1 : 0;
+      const bool mixed = code[u] == kLpmPartial;
+      const uint32_t span = mx[u] & 15;
+      R[u] = mixed ? (int64_t)(mx[u] >> 4) : -1;
+      L[u] = span == 15 ? 0 : R[u] - span;
+      const int64_t r1 = mixed ? R[u] : 0, r0 = mixed && R[u] - 1 >= L[u] ? R[u] - 1 : r1;
       const uint4* p1 = reinterpret_cast<const uint4*>(t.v6_iv + 4 * r1);
       const uint4* p0 = reinterpret_cast<const uint4*>(t.v6_iv + 4 * r0);
       c1lo[u] = p1[0];
@@ -532,8 +534,8 @@ __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, 
     for (uint32_t u = 0; u < kLpmV6; ++u) {
       const size_t j = base + u * blockDim.x + threadIdx.x;
       if (j >= n6) continue;
-      bool drop = false;
-      if (R[u] >= L[u]) {
+      bool drop = code[u] == 1;
+      if (code[u] == kLpmPartial) {
         uint64_t eh_ = 0, el_ = 0;
         bool found = false;
         if (le128(u64_of(c1lo[u].x, c1lo[u].y), u64_of(c1lo[u].z, c1lo[u].w), sh[u], sl[u])) {

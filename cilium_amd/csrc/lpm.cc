@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <array>
 #include <map>
+#include <stdexcept>
 
 namespace cg {
 
@@ -124,7 +125,8 @@ void PrefilterState::rebuild(Engine& e) {
   }
 
   // ---------------- IPv6 intervals + top-bits index
-  v6_idx.clear();
+  v6_code.clear();
+  v6_mix.clear();
   v6_iv.clear();
   if (v6_filter) {
     std::vector<std::pair<U128, U128>> iv;
@@ -162,20 +164,34 @@ void PrefilterState::rebuild(Engine& e) {
       v6_iv.push_back(x.second.first);
       v6_iv.push_back(x.second.second);
     }
-    // index bits: about two buckets per interval, 16..22 bits
+    // bucket bits: about two buckets per interval, 16..22 bits
     uint32_t bits = 16;
     while (bits < 22 && (1ull << bits) < 2 * mg.size()) ++bits;
     v6_bits = bits;
-    v6_idx.assign((1u << bits) + 1, 0);
-    size_t i = 0;
-    for (uint32_t t = 0; t < (1u << bits); ++t) {
-      uint64_t block_start = (uint64_t)t << (64 - bits);
-      while (i < mg.size() && mg[i].second.first < block_start) ++i;
-      v6_idx[t] = (uint32_t)i;
+    if (mg.size() >= (1u << 28)) throw std::runtime_error("prefilter: too many IPv6 intervals");
+    const uint32_t nb = 1u << bits;
+    v6_code.assign(nb / 16, 0);
+    size_t i = 0;  // first interval with hi >= the bucket start
+    uint32_t nmixed = 0;
+    for (uint32_t t = 0; t < nb; ++t) {
+      if ((t & 15) == 0) v6_code[t >> 4] = (uint64_t)nmixed << 32;
+      const U128 bs{(uint64_t)t << (64 - bits), 0};
+      const U128 be{t + 1 == nb ? ~0ULL : ((uint64_t)(t + 1) << (64 - bits)) - 1, ~0ULL};
+      while (i < mg.size() && mg[i].second < bs) ++i;
+      size_t r = i;  // one past the last interval with lo <= the bucket end
+      while (r < mg.size() && mg[r].first <= be) ++r;
+      uint64_t code = 0;
+      if (r > i) code = (r == i + 1 && mg[i].first <= bs && mg[i].second >= be) ? 1 : kLpmPartial;
+      v6_code[t >> 4] |= code << (2 * (t & 15));
+      if (code != kLpmPartial) continue;
+      ++nmixed;
+      const uint32_t R = (uint32_t)(r - 1), span = (uint32_t)std::min<size_t>(r - 1 - i, 15);
+      v6_mix.push_back(R << 4 | span);
     }
-    v6_idx[1u << bits] = (uint32_t)mg.size();
-    if (v6_iv.empty()) v6_iv.assign(4, 0);
   }
+  // the kernel reads entry 0 / record 0 unconditionally
+  if (v6_mix.empty()) v6_mix.assign(1, 0);
+  if (v6_iv.empty()) v6_iv.assign(4, 0);
 
   // ---------------- endpoint tables (0 = empty slot)
   {
@@ -228,10 +244,11 @@ void PrefilterState::rebuild(Engine& e) {
       d.leaves = t->add(leaves);
     }
     if (v6_filter) {
-      d.v6_idx = t->add(v6_idx);
-      d.v6_iv = t->add(v6_iv);
+      d.v6_code = t->add(v6_code);
       d.v6_bits = v6_bits;
     }
+    d.v6_mix = t->add(v6_mix);
+    d.v6_iv = t->add(v6_iv);
     d.ep4_keys = t->add(ep4_keys);
     d.ep4_mask = (uint32_t)ep4_keys.size() - 1;
     d.ep4_zero = ep4_zero;

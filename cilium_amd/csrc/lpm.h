@@ -39,7 +39,8 @@ struct PrefilterState {
   // device structures
   std::vector<uint32_t> top, top_rank, mid, leaf_base;
   std::vector<uint64_t> leaves;
-  std::vector<uint32_t> v6_idx;
+  std::vector<uint64_t> v6_code;  // 16 bucket codes | mixed buckets before the word << 32
+  std::vector<uint32_t> v6_mix;   // per mixed bucket: R << 4 | min(R - L, 15)
   std::vector<uint64_t> v6_iv;
   uint32_t v6_bits = 16;
   std::vector<uint32_t> ep4_keys;

@@ -452,3 +452,55 @@ def test_prefilter_dense_partials(host, seed):
     o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6)
     assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
     assert 0.05 < (o4 == 1).mean() < 0.95 and 0.05 < (o6 == 1).mean() < 0.95
+
+
+def v6_bucket_case(seed: int):
+    """IPv6 bucket classes: short prefixes covering whole top-bits buckets
+    (code 1), prefixes ending on bucket edges, the last bucket (ffff::/16),
+    ::/0-adjacent ranges and adjacent prefixes that merge, with addresses
+    at and beside every interval edge."""
+    from cilium_amd.classifier import CIDR_DTYPE
+    rng = np.random.default_rng(100 + seed)
+    m = 2000
+    pfx = np.zeros(m, CIDR_DTYPE)
+    plen = np.where(rng.random(m) < 0.05, rng.integers(6, 24, m), rng.integers(24, 129, m))
+    a6 = rng.integers(0, 256, (m, 16), dtype=np.uint8)
+    a6[:50, :2] = 0xFF  # the last buckets
+    a6[50:100, :2] = 0x00  # the first ones
+    for i in range(16):
+        keep = np.clip(plen - 8 * i, 0, 8)
+        a6[:, i] &= ((0xFF << (8 - keep)) & 0xFF).astype(np.uint8)
+    pfx["family"] = 6
+    pfx["prefixlen"] = plen
+    pfx["addr"] = a6
+    # addresses: each prefix's first and last address, one past/before them
+    lo = a6.copy()
+    hi = a6.copy()
+    for i in range(16):
+        host_bits = np.clip(8 * (i + 1) - plen, 0, 8)
+        hi[:, i] |= ((1 << host_bits) - 1).astype(np.uint8)
+
+    def step(x, d):
+        v = int.from_bytes(bytes(x), "big") + d
+        return list((v % (1 << 128)).to_bytes(16, "big"))
+    edges = [lo, hi, np.array([step(x, -1) for x in lo], np.uint8), np.array([step(x, 1) for x in hi], np.uint8)]
+    src = np.concatenate(edges + [rng.integers(0, 256, (4 * m, 16), dtype=np.uint8)])
+    v6 = np.zeros((len(src), 32), np.uint8)
+    v6[:, :16] = src
+    v4 = np.zeros((1, 2), np.uint32)
+    ep4 = np.zeros(0, np.uint32)
+    ep6 = rng.integers(0, 256, (16, 16), dtype=np.uint8)
+    v6[:, 16:] = ep6[rng.integers(0, 16, len(src))]  # local destinations: drops come from the CIDRs
+    return pfx, v4, v6, ep4, ep6
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_prefilter_v6_bucket_codes(host, seed):
+    pfx, v4, v6, ep4, ep6 = v6_bucket_case(seed)
+    pf = host.prefilter(dyn4=True, dyn6=True, max_lpm=1 << 20)
+    pf.insert(0, pfx)
+    pf.set_endpoints(ep4, ep6)
+    g4, g6 = pf.eval_host_diag(v4, v6)
+    o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6)
+    assert np.array_equal(g6, o6)
+    assert 0.05 < (o6 == 1).mean() < 0.95

@@ -208,6 +208,20 @@ def test_prefilter_dense_partials(gpu, seed):
     assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_prefilter_v6_bucket_codes(gpu, seed):
+    """Whole-bucket, edge-aligned and first/last-bucket IPv6 prefixes with
+    addresses on and beside every interval edge (bucket codes 0/1/2)."""
+    from test_cpu_differential import v6_bucket_case
+    pfx, v4, v6, ep4, ep6 = v6_bucket_case(seed)
+    pf = gpu.prefilter(dyn4=True, dyn6=True, max_lpm=1 << 20)
+    pf.insert(0, pfx)
+    pf.set_endpoints(ep4, ep6)
+    g4, g6 = pf.verdicts(v4, v6)
+    o4, o6 = oracle.prefilter(pf.config, pfx, ep4, ep6, v4, v6)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
+
+
 def test_prefilter_edges(gpu):
     pf = gpu.prefilter(dyn4=True, dyn6=True)
     pf.insert(0, ["0.0.0.0/1", "10.0.0.0/8", "192.168.1.128/25", "::/1", "2001:db8::/32", "fe80::1/128"])
