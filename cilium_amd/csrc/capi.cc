@@ -755,9 +755,14 @@ int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, s
       uint64_t hi = 0, lo = 0;
       for (int k = 0; k < 8; ++k) hi = hi << 8 | v6[16 * i + k];
       for (int k = 8; k < 16; ++k) lo = lo << 8 | v6[16 * i + k];
-      const uint64_t tb = hi >> (64 - t.v6_bits);
-      const uint32_t run = ipc_v6_run(t, hi, lo, t.idx6[tb], t.idx6[tb + 1]);
-      const uint64_t v = t.runs6[4 * (size_t)run + 2];
+      const uint32_t tb = (uint32_t)(hi >> (64 - t.v6_bits));
+      uint32_t k, L, R;
+      uint64_t v = kIpcMiss;
+      if (ipc_v6_bucket(t.code6[tb >> 5], tb, &k)) {
+        L = t.ent6[2 * (size_t)k];
+        R = t.ent6[2 * (size_t)k + 1];
+        v = t.runs6[4 * (size_t)ipc_v6_run(t, hi, lo, L, R) + 2];
+      }
       out6[i] = cg_remote_endpoint_info{(uint32_t)v, (uint32_t)(v >> 32)};
     }
   });

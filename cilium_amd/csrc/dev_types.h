@@ -435,11 +435,23 @@ CG_HD inline uint32_t kf_fnv1a(const uint8_t* p, uint32_t n) {
 // word, tunnel in the high word), so a lookup ends at its last table level.
 // A resolved identity is never 0, so identity 0 marks a pointer: the high
 // word is then the index of the next level's 256-entry chunk.
-//  IPv4: 16-8-8 stride trie.  l16[a >> 16], then 2-KiB chunks.
+//  IPv4: 16-8-8 stride trie of 2-KiB chunks under a 16-B summary per /16
+//        (1 MiB, mostly L2 resident): {background value (identity, tunnel),
+//        chunk, lo | hi << 8 | direct << 16}.  /24 indices outside [lo, hi]
+//        resolve to the background without touching a chunk (most /16 chunks
+//        hold one short range: a node's /24, a /17../28 prefix); inside it
+//        the chunk's entry is read, and a pointer there leads to the /32
+//        chunk.  direct: the range is one /24 whose entry is a pointer, and
+//        chunk names its /32 chunk, skipping a level.
 //  IPv6: the prefixes partition the address space into runs with one
 //        longest-prefix value each; runs are 32-B records {start hi, start lo,
-//        value, 0} sorted by start, and idx6[t] = the last run starting at or
-//        before the t-th (1 << v6_bits)-aligned block.
+//        value, 0} sorted by start.  The top v6_bits address bits pick a
+//        bucket; a bit per bucket (32 per u64 word, the high half counting
+//        the set bits before the word: 256 KiB at 2^20 buckets, L2
+//        resident) is clear when one WORLD run spans the whole bucket, which
+//        settles the lookup.  A set bucket's u32 pair in ent6 is {L, R}: the
+//        runs meeting the bucket (a node's /64 of pods crowds ~50 runs into
+//        one bucket, so the search range is kept exact).
 constexpr uint32_t kWorldId = 2;  // bpf/node_config.h:35
 constexpr uint64_t kIpcMiss = kWorldId;  // {WORLD_ID, 0}
 struct alignas(8) IpcVal {
@@ -447,23 +459,41 @@ struct alignas(8) IpcVal {
   uint32_t tunnel;  // tunnel_endpoint as stored (network-order bytes)
 };
 struct IpcacheDev {
-  const uint64_t* l16;     // 65536 entries
+  const uint32_t* l16x;    // 4 words per /16 (16-B aligned)
   const uint64_t* chunks;  // 256 entries per chunk
-  const uint32_t* idx6;    // (1 << v6_bits) + 1
+  const uint64_t* code6;   // (1 << v6_bits) / 32 words
+  const uint32_t* ent6;    // {L, R} per set bucket (at least one pair)
   const uint64_t* runs6;   // 4 u64 per run
   uint32_t v6_bits;
   uint32_t nruns6;
 };
 
+// The /16 summary word's range test; returns the chunk entry index to read
+// (UINT64_MAX: the background is the answer).
+CG_HD inline uint64_t ipc_v4_level2(uint32_t chunk, uint32_t r, uint32_t a) {
+  const uint32_t k = (a >> 8) & 255;
+  if (k < (r & 255) || k > ((r >> 8) & 255)) return ~0ULL;
+  return (uint64_t)chunk * 256 + ((r >> 16) ? (a & 255) : k);
+}
 CG_HD inline uint64_t ipc_v4_value(const IpcacheDev& t, uint32_t a) {  // a in host order
-  uint64_t e = t.l16[a >> 16];
-  if ((uint32_t)e == 0) e = t.chunks[(size_t)(e >> 32) * 256 + ((a >> 8) & 255)];
+  const uint32_t* x = t.l16x + 4 * (size_t)(a >> 16);
+  const uint64_t j = ipc_v4_level2(x[2], x[3], a);
+  if (j == ~0ULL) return (uint64_t)x[1] << 32 | x[0];
+  uint64_t e = t.chunks[j];
   if ((uint32_t)e == 0) e = t.chunks[(size_t)(e >> 32) * 256 + (a & 255)];
   return e;
 }
 
 CG_HD inline bool ipc_le128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
   return ah < bh || (ah == bh && al <= bl);
+}
+
+// IPv6 bucket tb of code word cw: false when one WORLD run spans it; else
+// *idx = its ent6 index.
+CG_HD inline bool ipc_v6_bucket(uint64_t cw, uint32_t tb, uint32_t* idx) {
+  const uint32_t w = (uint32_t)cw, b = tb & 31;
+  *idx = (uint32_t)(cw >> 32) + (uint32_t)__builtin_popcount(w & ((1u << b) - 1));
+  return (w >> b) & 1;
 }
 
 // Last run whose start is <= (hi, lo), searched in [L, R] (run L qualifies).

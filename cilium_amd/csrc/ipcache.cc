@@ -10,6 +10,7 @@
 #include "ipcache.h"
 
 #include <algorithm>
+#include <stdexcept>
 #include <tuple>
 
 namespace cg {
@@ -85,6 +86,49 @@ void IpcacheState::build_tables() {
   }
   if (chunks.empty()) chunks.assign(256, kIpcMiss);
 
+  // /16 summaries: background = the most frequent value among the chunk's
+  // entries, [lo, hi] = the /24s holding anything else
+  l16x.assign(65536 * 4, 0);
+  {
+    std::vector<uint64_t> vals(256);
+    for (uint32_t q = 0; q < 65536; ++q) {
+      uint32_t* x = &l16x[4 * (size_t)q];
+      const uint64_t e = l16[q];
+      uint64_t bg = e;
+      uint32_t chunk = 0, lo = 1, hi = 0, direct = 0;
+      if ((uint32_t)e == 0) {
+        const uint32_t c = (uint32_t)(e >> 32);
+        const uint64_t* ent = &chunks[(size_t)c * 256];
+        vals.assign(ent, ent + 256);
+        std::sort(vals.begin(), vals.end());
+        bg = kIpcMiss;
+        size_t best = 0;
+        for (size_t i = 0; i < 256;) {
+          size_t j = i;
+          while (j < 256 && vals[j] == vals[i]) ++j;
+          if ((uint32_t)vals[i] != 0 && j - i > best) best = j - i, bg = vals[i];
+          i = j;
+        }
+        lo = 256;
+        for (uint32_t k = 0; k < 256; ++k)
+          if (ent[k] != bg) {
+            lo = std::min(lo, k);
+            hi = k;
+          }
+        if (lo == 256) lo = 1, hi = 0;
+        chunk = c;
+        if (lo == hi && (uint32_t)ent[lo] == 0) {
+          direct = 1;
+          chunk = (uint32_t)(ent[lo] >> 32);
+        }
+      }
+      x[0] = (uint32_t)bg;
+      x[1] = (uint32_t)(bg >> 32);
+      x[2] = chunk;
+      x[3] = lo | hi << 8 | direct << 16;
+    }
+  }
+
   // ---- IPv6: sweep the nested prefix intervals into runs of one value.
   std::sort(v6.begin(), v6.end(), [](const auto& a, const auto& b) {
     return std::get<0>(a) != std::get<0>(b) ? std::get<0>(a) < std::get<0>(b) : std::get<1>(a) < std::get<1>(b);
@@ -125,21 +169,33 @@ void IpcacheState::build_tables() {
   uint32_t bits = 16;
   while (bits < 22 && (1ull << bits) < 2 * runs.size()) ++bits;
   v6_bits = bits;
-  idx6.assign((1u << bits) + 1, 0);
-  size_t r = 0;
-  for (uint32_t t = 0; t < (1u << bits); ++t) {
+  const uint32_t nb = 1u << bits;
+  code6.assign(nb / 32, 0);
+  ent6.clear();
+  size_t L = 0;  // last run starting at or before the bucket start
+  uint64_t nset = 0;
+  for (uint32_t t = 0; t < nb; ++t) {
+    if ((t & 31) == 0) code6[t >> 5] = nset << 32;
     const U128 start{(uint64_t)t << (64 - bits), 0};
-    while (r + 1 < runs.size() && runs[r + 1].first <= start) ++r;
-    idx6[t] = (uint32_t)r;
+    const U128 end{t + 1 == nb ? ~0ULL : ((uint64_t)(t + 1) << (64 - bits)) - 1, ~0ULL};
+    while (L + 1 < runs.size() && runs[L + 1].first <= start) ++L;
+    size_t R = L;  // last run starting at or before the bucket end
+    while (R + 1 < runs.size() && runs[R + 1].first <= end) ++R;
+    if (R == L && runs[L].second == kIpcMiss) continue;
+    code6[t >> 5] |= 1ULL << (t & 31);
+    ++nset;
+    ent6.push_back((uint32_t)L);
+    ent6.push_back((uint32_t)R);
   }
-  idx6[1u << bits] = (uint32_t)runs.size() - 1;
+  if (ent6.empty()) ent6.assign(2, 0);
 }
 
 IpcacheDev IpcacheState::host_view() const {
   IpcacheDev v{};
-  v.l16 = l16.data();
+  v.l16x = l16x.data();
   v.chunks = chunks.data();
-  v.idx6 = idx6.data();
+  v.code6 = code6.data();
+  v.ent6 = ent6.data();
   v.runs6 = runs6.data();
   v.v6_bits = v6_bits;
   v.nruns6 = (uint32_t)(runs6.size() / 4);
@@ -152,9 +208,10 @@ void IpcacheState::rebuild(Engine& e) {
     e.set_device();
     auto t = std::make_shared<DevTables>();
     IpcacheDev d{};
-    d.l16 = t->add(l16);
+    d.l16x = t->add(l16x);
     d.chunks = t->add(chunks);
-    d.idx6 = t->add(idx6);
+    d.code6 = t->add(code6);
+    d.ent6 = t->add(ent6);
     d.runs6 = t->add(runs6);
     d.v6_bits = v6_bits;
     d.nruns6 = (uint32_t)(runs6.size() / 4);

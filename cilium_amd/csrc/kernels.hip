@@ -260,37 +260,51 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
     }
     if (kFam == 4) {  // the trie levels, each issued for all tuples of the lane
       uint64_t e[kL4Tuples];
-#pragma unroll
-      for (uint32_t u = 0; u < kL4Tuples; ++u) e[u] = ipc.l16[w[u][0] >> 16];
+      uint4 x[kL4Tuples];
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u)
-        if ((uint32_t)e[u] == 0) e[u] = ipc.chunks[(size_t)(e[u] >> 32) * 256 + ((w[u][0] >> 8) & 255)];
+        x[u] = *reinterpret_cast<const uint4*>(ipc.l16x + 4 * (size_t)(w[u][0] >> 16));
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) {
+        const uint64_t j = ipc_v4_level2(x[u].z, x[u].w, w[u][0]);
+        e[u] = ((uint64_t)x[u].y << 32) | x[u].x;
+        if (j != ~0ULL) e[u] = ipc.chunks[j];
+      }
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u)
         if ((uint32_t)e[u] == 0) e[u] = ipc.chunks[(size_t)(e[u] >> 32) * 256 + (w[u][0] & 255)];
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = (uint32_t)e[u];
     }
-    if (kFam == 6) {  // index words, then each bucket's last run, for all tuples of the lane
-      uint64_t hi[kL4Tuples], lo[kL4Tuples];
+    if (kFam == 6) {  // bucket bits, entries, then each bucket's last run, for all tuples of the lane
+      uint64_t hi[kL4Tuples], lo[kL4Tuples], cw[kL4Tuples];
       uint32_t L[kL4Tuples], R[kL4Tuples];
+      uint2 ent[kL4Tuples];
+      bool set[kL4Tuples];
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) {
         hi[u] = __builtin_bswap64(((uint64_t)a6[u].y << 32) | a6[u].x);
         lo[u] = __builtin_bswap64(((uint64_t)a6[u].w << 32) | a6[u].z);
-        const uint64_t tb = hi[u] >> (64 - ipc.v6_bits);
-        L[u] = ipc.idx6[tb];
-        R[u] = ipc.idx6[tb + 1];
+        cw[u] = ipc.code6[hi[u] >> (69 - ipc.v6_bits)];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kL4Tuples; ++u) {
+        uint32_t k;
+        set[u] = ipc_v6_bucket(cw[u], (uint32_t)(hi[u] >> (64 - ipc.v6_bits)), &k);
+        ent[u] = reinterpret_cast<const uint2*>(ipc.ent6)[set[u] ? k : 0];
       }
       uint4 kr[kL4Tuples], vr[kL4Tuples];
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) {
-        const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R[u]);
+        L[u] = ent[u].x;
+        R[u] = ent[u].y;
+        const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)(set[u] ? R[u] : 0));
         kr[u] = rec[0];
         vr[u] = rec[1];
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], kr[u], vr[u].x);
+      for (uint32_t u = 0; u < kL4Tuples; ++u)
+        w[u][0] = set[u] ? ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], kr[u], vr[u].x) : (uint32_t)kIpcMiss;
     }
     // candidates of every tuple, then every tuple's first slot load in
     // flight together, then the walks
@@ -338,10 +352,15 @@ __global__ __launch_bounds__(256) void l4_kernel(L4Dev t, IpcacheDev ipc, const 
       const uint4 x = reinterpret_cast<const uint4*>(addrs)[i];
       const uint64_t hi = __builtin_bswap64(((uint64_t)x.y << 32) | x.x);
       const uint64_t lo = __builtin_bswap64(((uint64_t)x.w << 32) | x.z);
-      const uint64_t tb = hi >> (64 - ipc.v6_bits);
-      const uint32_t L = ipc.idx6[tb], R = ipc.idx6[tb + 1];
-      const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R);
-      w0 = ipc_v6_identity(ipc, hi, lo, L, R, rec[0], rec[1].x);
+      const uint32_t tb = (uint32_t)(hi >> (64 - ipc.v6_bits));
+      uint32_t k, L, R;
+      w0 = (uint32_t)kIpcMiss;
+      if (ipc_v6_bucket(ipc.code6[tb >> 5], tb, &k)) {
+        L = ipc.ent6[2 * (size_t)k];
+        R = ipc.ent6[2 * (size_t)k + 1];
+        const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R);
+        w0 = ipc_v6_identity(ipc, hi, lo, L, R, rec[0], rec[1].x);
+      }
     } else {
       w0 = tuples[i * 3 + 0];
     }

@@ -3,9 +3,9 @@
 // address → {security identity, tunnel endpoint}.
 //
 // Integer work bound by the input/output stream plus dependent table loads
-// (IPv4: the /16 entry, then up to two 2-KiB chunks; IPv6: two index words,
-// the bucket's last 32-B run record, a short binary search when that run
-// starts after the address).  Entries carry the resolved value inline, so
+// (IPv4: the /16 summary, then up to two 2-KiB chunks; IPv6: the bucket bit,
+// then for a bucket not spanned by one WORLD run its entry, its last 32-B run
+// record, and a short binary search when that run starts after the address).  Entries carry the resolved value inline, so
 // the last table load is the answer.  Each lane resolves
 // several addresses with every level's loads issued for all of them before
 // the next level, so a wave keeps 4 (v4) / 2 (v6) independent chains in
@@ -22,7 +22,7 @@ namespace cg {
 
 namespace {
 
-constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;  // addresses per lane per iteration
+constexpr uint32_t kIpcV4 = 8, kIpcV6 = 2;  // addresses per lane per iteration
 constexpr int kIpcThreads = 256;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -47,11 +47,15 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       i = i < n4 ? i : n4 - 1;  // unconditional loads: no vmcnt(0) under a branch
       a[u] = __builtin_bswap32(__builtin_nontemporal_load(v4 + i));
     }
+    uint4 x[kIpcV4];
 #pragma unroll
-    for (uint32_t u = 0; u < kIpcV4; ++u) e[u] = t.l16[a[u] >> 16];
+    for (uint32_t u = 0; u < kIpcV4; ++u) x[u] = *reinterpret_cast<const uint4*>(t.l16x + 4 * (size_t)(a[u] >> 16));
 #pragma unroll
-    for (uint32_t u = 0; u < kIpcV4; ++u)
-      if ((uint32_t)e[u] == 0) e[u] = t.chunks[(size_t)(e[u] >> 32) * 256 + ((a[u] >> 8) & 255)];
+    for (uint32_t u = 0; u < kIpcV4; ++u) {
+      const uint64_t j = ipc_v4_level2(x[u].z, x[u].w, a[u]);
+      e[u] = u64_of(x[u].x, x[u].y);
+      if (j != ~0ULL) e[u] = t.chunks[j];
+    }
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV4; ++u)
       if ((uint32_t)e[u] == 0) e[u] = t.chunks[(size_t)(e[u] >> 32) * 256 + (a[u] & 255)];
@@ -73,18 +77,26 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       hi[u] = __builtin_bswap64(u64_of(x.x, x.y));
       lo[u] = __builtin_bswap64(u64_of(x.z, x.w));
     }
+    // bucket bit (L2 resident), then a set bucket's entry and its last run;
+    // WORLD-spanned buckets read entry / run 0, hot lines, instead of
+    // branching around the loads
+    uint64_t cw[kIpcV6];
+#pragma unroll
+    for (uint32_t u = 0; u < kIpcV6; ++u) cw[u] = t.code6[hi[u] >> (69 - t.v6_bits)];
+    bool set[kIpcV6];
+    uint2 ent[kIpcV6];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
-      const uint64_t tb = hi[u] >> (64 - t.v6_bits);
-      L[u] = t.idx6[tb];
-      R[u] = t.idx6[tb + 1];
+      uint32_t k;
+      set[u] = ipc_v6_bucket(cw[u], (uint32_t)(hi[u] >> (64 - t.v6_bits)), &k);
+      ent[u] = reinterpret_cast<const uint2*>(t.ent6)[set[u] ? k : 0];
     }
-    // the bucket's last run, loaded for every lane at once: with ~2 buckets
-    // per run it settles most addresses without a search
     uint4 kr[kIpcV6], vr[kIpcV6];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
-      const uint4* rec = reinterpret_cast<const uint4*>(t.runs6 + 4 * (size_t)R[u]);
+      L[u] = ent[u].x;
+      R[u] = ent[u].y;
+      const uint4* rec = reinterpret_cast<const uint4*>(t.runs6 + 4 * (size_t)(set[u] ? R[u] : 0));
       kr[u] = rec[0];
       vr[u] = rec[1];
     }
@@ -93,7 +105,8 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       const size_t j = base + u * blockDim.x + threadIdx.x;
       if (j >= n6) continue;
       uint64_t v = u64_of(vr[u].x, vr[u].y);
-      if (!ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u]))
+      if (!set[u]) v = kIpcMiss;
+      else if (!ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u]))
         v = t.runs6[4 * (size_t)ipc_v6_run(t, hi[u], lo[u], L[u], R[u] - 1) + 2];
       store_val(v, out6 + j);
     }

@@ -162,6 +162,48 @@ def test_tables_nested_dense(host):
     assert CIDR_DTYPE.itemsize == 20
 
 
+def v6_bucket_case(seed: int):
+    """IPv6 top-bits buckets of every kind: spanned by one WORLD run (bit
+    clear), spanned by one non-WORLD run (short prefixes), a few runs, and
+    crowded ones (a binary search over ~800 runs), with the first
+    and last buckets taken, and addresses on and beside every run edge."""
+    import random
+    rnd = random.Random(200 + seed)
+    nets = []
+    for _ in range(40):  # whole buckets, some with identity 0
+        nets.append((rnd.getrandbits(128), rnd.randrange(6, 20)))
+    crowd = rnd.getrandbits(16) << 112  # 400 prefixes under one /16
+    for _ in range(400):
+        nets.append((crowd | rnd.getrandbits(112), rnd.randrange(40, 129)))
+    for _ in range(400):
+        nets.append((rnd.getrandbits(128), rnd.randrange(24, 129)))
+    nets += [(0, 24), ((1 << 128) - 1, 128), (((1 << 16) - 1) << 112, 16)]
+    keys, vals, edges = [], [], []
+    for a, plen in nets:
+        net = ipaddress.IPv6Network((a, plen), strict=False)
+        keys.append(str(net))
+        vals.append([0 if len(vals) % 9 == 4 else 3000 + len(vals), len(vals)])
+        lo, hi = int(net.network_address), int(net.broadcast_address)
+        edges += [lo, hi, (lo - 1) % (1 << 128), (hi + 1) % (1 << 128)]
+    addrs = edges + [rnd.getrandbits(128) for _ in range(2000)] + \
+        [crowd | rnd.getrandbits(112) for _ in range(2000)]
+    a6 = np.array([list(x.to_bytes(16, "big")) for x in addrs], np.uint8)
+    return keys, np.array(vals, np.uint32), a6
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_tables_v6_buckets(host, seed):
+    from cilium_amd.classifier import IPCache
+    keys, vals, a6 = v6_bucket_case(seed)
+    ic = host.ipcache()
+    ic.update(keys, vals)
+    a4 = np.zeros(1, np.uint32)
+    g4, g6 = ic.eval_host_diag(a4, a6)
+    o4, o6 = oracle.ipcache(IPCache._keys(keys), vals, a4, a6)
+    assert np.array_equal(g6, o6)
+    assert 0.05 < (o6[:, 0] == WORLD).mean() < 0.95
+
+
 def test_host_handle_refuses_resolve(host):
     ic = host.ipcache()
     with pytest.raises(N.CiliumGPUError) as ei:
@@ -189,6 +231,19 @@ def test_gpu_parity_full_map(gpu):
     o4, o6 = oracle.ipcache(k, v, a4, a6, nthreads=16)
     assert np.array_equal(g4, o4)
     assert np.array_equal(g6, o6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(2))
+def test_gpu_v6_buckets(gpu, seed):
+    from cilium_amd.classifier import IPCache
+    keys, vals, a6 = v6_bucket_case(seed)
+    ic = gpu.ipcache()
+    ic.update(keys, vals)
+    a4 = np.zeros(1, np.uint32)
+    g4, g6 = ic.resolve(a4, a6)
+    o4, o6 = oracle.ipcache(IPCache._keys(keys), vals, a4, a6)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
 
 
 @pytest.mark.gpu

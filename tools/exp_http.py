@@ -147,6 +147,11 @@ VARIANTS.update({
     "rank_u4": [("kernels_http_raw.hip", "constexpr uint32_t kRankU = 8;", "constexpr uint32_t kRankU = 4;")],
     "raw_ldscodes": [("kernels_http_raw.hip", "return (size_t)R.nprogs * 256 <= 4 * 1024; }",
                       "return (size_t)R.nprogs * 256 <= 32 * 1024; }")],
+    # ipcache: addresses per lane (v4, v6)
+    "ipc_v6u4": [("kernels_ipcache.hip", "constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;",
+                  "constexpr uint32_t kIpcV4 = 4, kIpcV6 = 4;")],
+    "ipc_v4u8": [("kernels_ipcache.hip", "constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;",
+                  "constexpr uint32_t kIpcV4 = 8, kIpcV6 = 2;")],
 })
 
 

@@ -1,18 +1,20 @@
 """Summarise a tools/gpu_lpm_split.sh run: per-family FETCH bytes and L2
 hits/misses per address (FETCH_SIZE KB x 1024 x 2, the gfx950 correction).
 
-    python tools/lpm_split_summary.py gpurun_out/ls2
+    python tools/lpm_split_summary.py gpurun_out/ls2 [kernel]
 """
 import collections
 import csv
 import os
 import sys
 
+KERNEL = "lpm"
+
 
 def per_dispatch(path):
     d = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
-        if "lpm" in r["Kernel_Name"]:
+        if KERNEL in r["Kernel_Name"]:
             d[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
     out = collections.defaultdict(list)
     for (dsp, c), v in sorted(d.items()):
@@ -34,4 +36,6 @@ def main(root):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2:  # kernel name fragment, e.g. ipcache (tools/ipc_split.py: same 70M / 30M split)
+        KERNEL = sys.argv[2]
     main(sys.argv[1])
