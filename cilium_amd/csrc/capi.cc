@@ -759,9 +759,12 @@ int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, s
       uint32_t k, L, R;
       uint64_t v = kIpcMiss;
       if (ipc_v6_bucket(t.code6[tb >> 5], tb, &k)) {
-        L = t.ent6[2 * (size_t)k];
-        R = t.ent6[2 * (size_t)k + 1];
-        v = t.runs6[4 * (size_t)ipc_v6_run(t, hi, lo, L, R) + 2];
+        L = t.ent6[4 * (size_t)k];
+        R = t.ent6[4 * (size_t)k + 1];
+        const uint32_t crowd = t.ent6[4 * (size_t)k + 2];
+        v = t.runs6[4 * (size_t)R + 2];
+        if (!ipc_le128(t.runs6[4 * (size_t)R], t.runs6[4 * (size_t)R + 1], hi, lo))
+          v = ipc_v6_search_value(t, hi, lo, L, R, crowd);
       }
       out6[i] = cg_remote_endpoint_info{(uint32_t)v, (uint32_t)(v >> 32)};
     }

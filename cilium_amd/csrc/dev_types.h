@@ -449,9 +449,12 @@ CG_HD inline uint32_t kf_fnv1a(const uint8_t* p, uint32_t n) {
 //        bucket; a bit per bucket (32 per u64 word, the high half counting
 //        the set bits before the word: 256 KiB at 2^20 buckets, L2
 //        resident) is clear when one WORLD run spans the whole bucket, which
-//        settles the lookup.  A set bucket's u32 pair in ent6 is {L, R}: the
-//        runs meeting the bucket (a node's /64 of pods crowds ~50 runs into
-//        one bucket, so the search range is kept exact).
+//        settles the lookup.  A set bucket's 16-B ent6 entry is {L, R, crowd,
+//        0}: runs L..R meet the bucket.  A node's /64 of pods crowds ~50
+//        runs into one bucket; such a bucket (8..255 runs) names a 128-B
+//        crowd6 line {prefix P of the starts of runs L+1..R (top s bits),
+//        s, 65 u8 offsets from L}: the 6 address bits after P pick one of 64
+//        sub-ranges, cutting a ~6-step binary search to about one record.
 constexpr uint32_t kWorldId = 2;  // bpf/node_config.h:35
 constexpr uint64_t kIpcMiss = kWorldId;  // {WORLD_ID, 0}
 struct alignas(8) IpcVal {
@@ -462,7 +465,8 @@ struct IpcacheDev {
   const uint32_t* l16x;    // 4 words per /16 (16-B aligned)
   const uint64_t* chunks;  // 256 entries per chunk
   const uint64_t* code6;   // (1 << v6_bits) / 32 words
-  const uint32_t* ent6;    // {L, R} per set bucket (at least one pair)
+  const uint32_t* ent6;    // {L, R, crowd, 0} per set bucket (at least one entry)
+  const uint8_t* crowd6;   // 128 B per crowded bucket (kIpcNoCrowd: none)
   const uint64_t* runs6;   // 4 u64 per run
   uint32_t v6_bits;
   uint32_t nruns6;
@@ -496,6 +500,29 @@ CG_HD inline bool ipc_v6_bucket(uint64_t cw, uint32_t tb, uint32_t* idx) {
   return (w >> b) & 1;
 }
 
+constexpr uint32_t kIpcNoCrowd = 0xFFFFFFFFu;
+// Narrow a crowded bucket's run range [*L, *R] for address (hi, lo) with its
+// crowd6 line d (runs L+1..R start inside the window of prefix P).
+CG_HD inline void ipc_v6_narrow(const uint8_t* d, uint64_t hi, uint64_t lo, uint32_t* L, uint32_t* R) {
+  const uint64_t ph = reinterpret_cast<const uint64_t*>(d)[0], pl = reinterpret_cast<const uint64_t*>(d)[1];
+  const uint32_t s = reinterpret_cast<const uint32_t*>(d)[4];  // 1..122
+  const uint64_t mh = s >= 64 ? ~0ULL : ~0ULL << (64 - s), ml = s > 64 ? ~0ULL << (128 - s) : 0;
+  const uint64_t ah = hi & mh, al = lo & ml;
+  if (ah < ph || (ah == ph && al < pl)) {  // before the window: run L
+    *R = *L;
+    return;
+  }
+  if (ah > ph || (ah == ph && al > pl)) {  // after it: run R
+    *L = *R;
+    return;
+  }
+  const uint32_t sh = 122 - s;  // the 6 bits below the prefix
+  const uint32_t i = (uint32_t)((sh >= 64 ? hi >> (sh - 64) : sh == 0 ? lo : (lo >> sh) | (hi << (64 - sh))) & 63);
+  const uint32_t base = *L;
+  *L = base + d[24 + i];
+  *R = base + d[25 + i];
+}
+
 // Last run whose start is <= (hi, lo), searched in [L, R] (run L qualifies).
 CG_HD inline uint32_t ipc_v6_run(const IpcacheDev& t, uint64_t hi, uint64_t lo, uint32_t L, uint32_t R) {
   while (L < R) {
@@ -504,6 +531,20 @@ CG_HD inline uint32_t ipc_v6_run(const IpcacheDev& t, uint64_t hi, uint64_t lo, 
     else R = m - 1;
   }
   return L;
+}
+
+// A set bucket's value when its last run R starts after the address: the
+// search over [L, R - 1], narrowed first in a crowded bucket.
+CG_HD inline uint64_t ipc_v6_search_value(const IpcacheDev& t, uint64_t hi, uint64_t lo, uint32_t L, uint32_t R,
+                                          uint32_t crowd) {
+  uint32_t l = L, r = R - 1;
+  if (crowd != kIpcNoCrowd) {
+    uint32_t rr = R;
+    ipc_v6_narrow(t.crowd6 + 128 * (size_t)crowd, hi, lo, &l, &rr);
+    r = rr < R - 1 ? rr : R - 1;
+    l = l < r ? l : r;
+  }
+  return t.runs6[4 * (size_t)ipc_v6_run(t, hi, lo, l, r) + 2];
 }
 
 }  // namespace cg

@@ -10,6 +10,7 @@
 #include "ipcache.h"
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 #include <tuple>
 
@@ -172,6 +173,7 @@ void IpcacheState::build_tables() {
   const uint32_t nb = 1u << bits;
   code6.assign(nb / 32, 0);
   ent6.clear();
+  crowd6.clear();
   size_t L = 0;  // last run starting at or before the bucket start
   uint64_t nset = 0;
   for (uint32_t t = 0; t < nb; ++t) {
@@ -184,10 +186,37 @@ void IpcacheState::build_tables() {
     if (R == L && runs[L].second == kIpcMiss) continue;
     code6[t >> 5] |= 1ULL << (t & 31);
     ++nset;
-    ent6.push_back((uint32_t)L);
-    ent6.push_back((uint32_t)R);
+    uint32_t crowd = kIpcNoCrowd;
+    if (R - L >= 8 && R - L < 255) {
+      // prefix of the starts of runs L+1..R (sorted: the first and last agree on it)
+      const U128 a = runs[L + 1].first, b = runs[R].first;
+      const uint64_t xh = a.first ^ b.first, xl = a.second ^ b.second;
+      uint32_t sp = xh ? (uint32_t)__builtin_clzll(xh) : xl ? 64 + (uint32_t)__builtin_clzll(xl) : 128;
+      sp = std::min<uint32_t>(sp, 122);
+      const uint64_t mh = sp >= 64 ? ~0ULL : ~0ULL << (64 - sp), ml = sp > 64 ? ~0ULL << (128 - sp) : 0;
+      const U128 P{a.first & mh, a.second & ml};
+      crowd = (uint32_t)(crowd6.size() / 128);
+      crowd6.resize(crowd6.size() + 128, 0);
+      uint8_t* d = &crowd6[(size_t)crowd * 128];
+      std::memcpy(d, &P.first, 8);
+      std::memcpy(d + 8, &P.second, 8);
+      std::memcpy(d + 16, &sp, 4);
+      // sub[i] = last run (offset from L) starting at or before P + i * 2^(122 - sp)
+      const uint32_t sh = 122 - sp;
+      typedef unsigned __int128 u128;
+      const u128 pv = (u128)P.first << 64 | P.second, step = (u128)1 << sh;
+      size_t r = L;
+      for (uint32_t i = 0; i <= 64; ++i) {
+        const u128 qv = pv + step * i;  // wraps only for i = 64 at the top window
+        const U128 q = (i && qv < pv) ? U128{~0ULL, ~0ULL} : U128{(uint64_t)(qv >> 64), (uint64_t)qv};
+        while (r + 1 <= R && runs[r + 1].first <= q) ++r;
+        d[24 + i] = (uint8_t)(r - L);
+      }
+    }
+    ent6.insert(ent6.end(), {(uint32_t)L, (uint32_t)R, crowd, 0});
   }
-  if (ent6.empty()) ent6.assign(2, 0);
+  if (ent6.empty()) ent6.assign(4, 0);
+  if (crowd6.empty()) crowd6.assign(128, 0);
 }
 
 IpcacheDev IpcacheState::host_view() const {
@@ -196,6 +225,7 @@ IpcacheDev IpcacheState::host_view() const {
   v.chunks = chunks.data();
   v.code6 = code6.data();
   v.ent6 = ent6.data();
+  v.crowd6 = crowd6.data();
   v.runs6 = runs6.data();
   v.v6_bits = v6_bits;
   v.nruns6 = (uint32_t)(runs6.size() / 4);
@@ -212,6 +242,7 @@ void IpcacheState::rebuild(Engine& e) {
     d.chunks = t->add(chunks);
     d.code6 = t->add(code6);
     d.ent6 = t->add(ent6);
+    d.crowd6 = t->add(crowd6);
     d.runs6 = t->add(runs6);
     d.v6_bits = v6_bits;
     d.nruns6 = (uint32_t)(runs6.size() / 4);

@@ -22,6 +22,7 @@ struct IpcacheState {
   // host copies of the device tables (also walked by cg_diag_ipcache_eval_host)
   std::vector<uint64_t> l16, chunks, runs6, code6;  // l16: the /16 level while building
   std::vector<uint32_t> l16x, ent6;
+  std::vector<uint8_t> crowd6;
   uint32_t v6_bits = 16;
   std::shared_ptr<DevTables> tab;  // the published device tables (engine.h)
   IpcacheDev dev{};                // view of tab; copy it together with tab

@@ -195,9 +195,9 @@ __device__ void l4_flush(const L4Dev& t, unsigned long long* lcnt) {
 // lookup_ip{4,6}_remote_endpoint resolved to sec_label, or WORLD_ID on a miss
 // or a zero sec_label (the tables store that resolution, dev_types.h).
 __device__ __forceinline__ uint32_t ipc_v6_identity(const IpcacheDev& ipc, uint64_t hi, uint64_t lo, uint32_t L,
-                                                    uint32_t R, uint4 kr, uint32_t v) {
+                                                    uint32_t R, uint32_t crowd, uint4 kr, uint32_t v) {
   if (!ipc_le128(((uint64_t)kr.y << 32) | kr.x, ((uint64_t)kr.w << 32) | kr.z, hi, lo))
-    v = (uint32_t)ipc.runs6[4 * (size_t)ipc_v6_run(ipc, hi, lo, L, R - 1) + 2];
+    v = (uint32_t)ipc_v6_search_value(ipc, hi, lo, L, R, crowd);
   return v;
 }
 
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
     if (kFam == 6) {  // bucket bits, entries, then each bucket's last run, for all tuples of the lane
       uint64_t hi[kL4Tuples], lo[kL4Tuples], cw[kL4Tuples];
       uint32_t L[kL4Tuples], R[kL4Tuples];
-      uint2 ent[kL4Tuples];
+      uint4 ent[kL4Tuples];
       bool set[kL4Tuples];
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) {
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
       for (uint32_t u = 0; u < kL4Tuples; ++u) {
         uint32_t k;
         set[u] = ipc_v6_bucket(cw[u], (uint32_t)(hi[u] >> (64 - ipc.v6_bits)), &k);
-        ent[u] = reinterpret_cast<const uint2*>(ipc.ent6)[set[u] ? k : 0];
+        ent[u] = reinterpret_cast<const uint4*>(ipc.ent6)[set[u] ? k : 0];
       }
       uint4 kr[kL4Tuples], vr[kL4Tuples];
 #pragma unroll
@@ -304,7 +304,8 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
       }
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u)
-        w[u][0] = set[u] ? ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], kr[u], vr[u].x) : (uint32_t)kIpcMiss;
+        w[u][0] = set[u] ? ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], ent[u].z, kr[u], vr[u].x)
+                         : (uint32_t)kIpcMiss;
     }
     // candidates of every tuple, then every tuple's first slot load in
     // flight together, then the walks
@@ -356,10 +357,11 @@ __global__ __launch_bounds__(256) void l4_kernel(L4Dev t, IpcacheDev ipc, const 
       uint32_t k, L, R;
       w0 = (uint32_t)kIpcMiss;
       if (ipc_v6_bucket(ipc.code6[tb >> 5], tb, &k)) {
-        L = ipc.ent6[2 * (size_t)k];
-        R = ipc.ent6[2 * (size_t)k + 1];
+        const uint4 en = reinterpret_cast<const uint4*>(ipc.ent6)[k];
+        L = en.x;
+        R = en.y;
         const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R);
-        w0 = ipc_v6_identity(ipc, hi, lo, L, R, rec[0], rec[1].x);
+        w0 = ipc_v6_identity(ipc, hi, lo, L, R, en.z, rec[0], rec[1].x);
       }
     } else {
       w0 = tuples[i * 3 + 0];

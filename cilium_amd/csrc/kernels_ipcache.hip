@@ -84,12 +84,12 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) cw[u] = t.code6[hi[u] >> (69 - t.v6_bits)];
     bool set[kIpcV6];
-    uint2 ent[kIpcV6];
+    uint4 ent[kIpcV6];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
       uint32_t k;
       set[u] = ipc_v6_bucket(cw[u], (uint32_t)(hi[u] >> (64 - t.v6_bits)), &k);
-      ent[u] = reinterpret_cast<const uint2*>(t.ent6)[set[u] ? k : 0];
+      ent[u] = reinterpret_cast<const uint4*>(t.ent6)[set[u] ? k : 0];
     }
     uint4 kr[kIpcV6], vr[kIpcV6];
 #pragma unroll
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       uint64_t v = u64_of(vr[u].x, vr[u].y);
       if (!set[u]) v = kIpcMiss;
       else if (!ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u]))
-        v = t.runs6[4 * (size_t)ipc_v6_run(t, hi[u], lo[u], L[u], R[u] - 1) + 2];
+        v = ipc_v6_search_value(t, hi[u], lo[u], L[u], R[u], ent[u].z);
       store_val(v, out6 + j);
     }
   }

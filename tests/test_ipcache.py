@@ -165,7 +165,8 @@ def test_tables_nested_dense(host):
 def v6_bucket_case(seed: int):
     """IPv6 top-bits buckets of every kind: spanned by one WORLD run (bit
     clear), spanned by one non-WORLD run (short prefixes), a few runs, and
-    crowded ones (a binary search over ~800 runs), with the first
+    crowded ones (a node /64 of pods: the 64-way crowd line; and ~800
+    runs: a plain binary search), with the first
     and last buckets taken, and addresses on and beside every run edge."""
     import random
     rnd = random.Random(200 + seed)
@@ -177,6 +178,10 @@ def v6_bucket_case(seed: int):
         nets.append((crowd | rnd.getrandbits(112), rnd.randrange(40, 129)))
     for _ in range(400):
         nets.append((rnd.getrandbits(128), rnd.randrange(24, 129)))
+    pods = rnd.getrandbits(64) << 64  # a node /64 of 40 pods: a crowded bucket (8..255 runs)
+    nets += [(pods | rnd.getrandbits(64), 128) for _ in range(40)]
+    near = pods | (rnd.getrandbits(8) << 56)  # and 30 pods sharing 72 bits (a narrow window)
+    nets += [(near | rnd.getrandbits(56), 128) for _ in range(30)]
     nets += [(0, 24), ((1 << 128) - 1, 128), (((1 << 16) - 1) << 112, 16)]
     keys, vals, edges = [], [], []
     for a, plen in nets:
@@ -186,7 +191,8 @@ def v6_bucket_case(seed: int):
         lo, hi = int(net.network_address), int(net.broadcast_address)
         edges += [lo, hi, (lo - 1) % (1 << 128), (hi + 1) % (1 << 128)]
     addrs = edges + [rnd.getrandbits(128) for _ in range(2000)] + \
-        [crowd | rnd.getrandbits(112) for _ in range(2000)]
+        [crowd | rnd.getrandbits(112) for _ in range(2000)] + \
+        [pods | rnd.getrandbits(64) for _ in range(1000)] + [near | rnd.getrandbits(56) for _ in range(1000)]
     a6 = np.array([list(x.to_bytes(16, "big")) for x in addrs], np.uint8)
     return keys, np.array(vals, np.uint32), a6
 
