@@ -501,26 +501,33 @@ CG_HD inline bool ipc_v6_bucket(uint64_t cw, uint32_t tb, uint32_t* idx) {
 }
 
 constexpr uint32_t kIpcNoCrowd = 0xFFFFFFFFu;
+// Where (hi, lo) falls against a crowd line's window (prefix P, top s bits):
+// 0 before it (the answer is run L), 1 after it (run R), 2 inside it, with
+// *i the sub-range of the 6 bits below P.
+CG_HD inline uint32_t ipc_v6_window(uint64_t ph, uint64_t pl, uint32_t s, uint64_t hi, uint64_t lo, uint32_t* i) {
+  const uint64_t mh = s >= 64 ? ~0ULL : ~0ULL << (64 - s), ml = s > 64 ? ~0ULL << (128 - s) : 0;
+  const uint64_t ah = hi & mh, al = lo & ml;
+  if (ah < ph || (ah == ph && al < pl)) return 0;
+  if (ah > ph || (ah == ph && al > pl)) return 1;
+  const uint32_t sh = 122 - s;  // s in 1..122
+  *i = (uint32_t)((sh >= 64 ? hi >> (sh - 64) : sh == 0 ? lo : (lo >> sh) | (hi << (64 - sh))) & 63);
+  return 2;
+}
 // Narrow a crowded bucket's run range [*L, *R] for address (hi, lo) with its
 // crowd6 line d (runs L+1..R start inside the window of prefix P).
 CG_HD inline void ipc_v6_narrow(const uint8_t* d, uint64_t hi, uint64_t lo, uint32_t* L, uint32_t* R) {
-  const uint64_t ph = reinterpret_cast<const uint64_t*>(d)[0], pl = reinterpret_cast<const uint64_t*>(d)[1];
-  const uint32_t s = reinterpret_cast<const uint32_t*>(d)[4];  // 1..122
-  const uint64_t mh = s >= 64 ? ~0ULL : ~0ULL << (64 - s), ml = s > 64 ? ~0ULL << (128 - s) : 0;
-  const uint64_t ah = hi & mh, al = lo & ml;
-  if (ah < ph || (ah == ph && al < pl)) {  // before the window: run L
+  uint32_t i = 0;
+  const uint32_t w = ipc_v6_window(reinterpret_cast<const uint64_t*>(d)[0], reinterpret_cast<const uint64_t*>(d)[1],
+                                   reinterpret_cast<const uint32_t*>(d)[4], hi, lo, &i);
+  if (w == 0) {
     *R = *L;
-    return;
-  }
-  if (ah > ph || (ah == ph && al > pl)) {  // after it: run R
+  } else if (w == 1) {
     *L = *R;
-    return;
+  } else {
+    const uint32_t base = *L;
+    *L = base + d[24 + i];
+    *R = base + d[25 + i];
   }
-  const uint32_t sh = 122 - s;  // the 6 bits below the prefix
-  const uint32_t i = (uint32_t)((sh >= 64 ? hi >> (sh - 64) : sh == 0 ? lo : (lo >> sh) | (hi << (64 - sh))) & 63);
-  const uint32_t base = *L;
-  *L = base + d[24 + i];
-  *R = base + d[25 + i];
 }
 
 // Last run whose start is <= (hi, lo), searched in [L, R] (run L qualifies).

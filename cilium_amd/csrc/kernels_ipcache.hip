@@ -91,23 +91,46 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       set[u] = ipc_v6_bucket(cw[u], (uint32_t)(hi[u] >> (64 - t.v6_bits)), &k);
       ent[u] = reinterpret_cast<const uint4*>(t.ent6)[set[u] ? k : 0];
     }
-    uint4 kr[kIpcV6], vr[kIpcV6];
+    // a plain set bucket: its last run (most buckets hold one run); a crowded
+    // one: its crowd line's prefix and shift instead (the last run rarely
+    // holds a pod address, so it is not read)
+    uint4 kr[kIpcV6], vr[kIpcV6], cp[kIpcV6], cs[kIpcV6];
+    bool crowd[kIpcV6];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
       L[u] = ent[u].x;
       R[u] = ent[u].y;
-      const uint4* rec = reinterpret_cast<const uint4*>(t.runs6 + 4 * (size_t)(set[u] ? R[u] : 0));
+      crowd[u] = set[u] && ent[u].z != kIpcNoCrowd;
+      const uint4* rec = reinterpret_cast<const uint4*>(t.runs6 + 4 * (size_t)(set[u] && !crowd[u] ? R[u] : 0));
       kr[u] = rec[0];
       vr[u] = rec[1];
+      const uint4* cl = reinterpret_cast<const uint4*>(t.crowd6 + 128 * (size_t)(crowd[u] ? ent[u].z : 0));
+      cp[u] = cl[0];
+      cs[u] = cl[1];
     }
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
       const size_t j = base + u * blockDim.x + threadIdx.x;
       if (j >= n6) continue;
       uint64_t v = u64_of(vr[u].x, vr[u].y);
-      if (!set[u]) v = kIpcMiss;
-      else if (!ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u]))
-        v = ipc_v6_search_value(t, hi[u], lo[u], L[u], R[u], ent[u].z);
+      if (!set[u]) {
+        v = kIpcMiss;
+      } else if (crowd[u]) {
+        uint32_t i = 0, l = L[u], r = R[u];
+        const uint32_t w = ipc_v6_window(u64_of(cp[u].x, cp[u].y), u64_of(cp[u].z, cp[u].w), cs[u].x, hi[u], lo[u], &i);
+        if (w == 0) {
+          r = l;
+        } else if (w == 1) {
+          l = r;
+        } else {
+          const uint8_t* sub = t.crowd6 + 128 * (size_t)ent[u].z + 24;
+          l = L[u] + sub[i];
+          r = L[u] + sub[i + 1];
+        }
+        v = t.runs6[4 * (size_t)ipc_v6_run(t, hi[u], lo[u], l, r) + 2];
+      } else if (!ipc_le128(u64_of(kr[u].x, kr[u].y), u64_of(kr[u].z, kr[u].w), hi[u], lo[u])) {
+        v = ipc_v6_search_value(t, hi[u], lo[u], L[u], R[u], kIpcNoCrowd);
+      }
       store_val(v, out6 + j);
     }
   }
