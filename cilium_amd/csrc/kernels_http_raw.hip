@@ -1278,6 +1278,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
   uint32_t ri = lo;
   HttpRawRun run = runs[ri];
   uint32_t next_t0 = ri + 1 < nruns ? runs[ri + 1].t0 : 0xFFFFFFFFu;
+  uint32_t rn = order[(size_t)t * 64 + lane];  // the next tile's slot records, one tile ahead
   for (; t < tend; ++t) {
     while (t >= next_t0) {
       ++ri;
@@ -1293,16 +1294,27 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
       wave_sync();
       lut_prog = run.prog;
     }
-    const uint32_t r = order[(size_t)t * 64 + lane];  // the slot's record (16-B units), or padding
+    const uint32_t r = rn;  // the slot's record (16-B units), or padding
+    rn = order[(size_t)min(t + 1, tend - 1) * 64 + lane];
     const uint32_t L = units == 0 ? 1u : (units < 2 ? 2u : units < 4 ? 4u : units < 8 ? 8u : 16u);
     const uint32_t per = 64 / L, sub = lane & (L - 1), grp = lane & ~(L - 1);
     uint32_t m = 0;  // the longest slot string among this lane's header slots
+    // pass p + 1's chunk is loaded before pass p is coded and stored, so a
+    // wave keeps two gathers in flight (unconditional: padding slots and
+    // lanes past the record read chunk 0, then take the padding header)
+    uint32_t rsn = (uint32_t)__shfl((int)r, (int)(lane / L), 64);
+    bool okn = rsn != 0xFFFFFFFFu && sub <= units;
+    uint4 xn = rec16[okn ? (size_t)rsn + sub : 0];
     for (uint32_t pass = 0; pass < L; ++pass) {
       const uint32_t s = pass * per + lane / L;  // this lane's slot in this pass
-      const uint32_t rs = (uint32_t)__shfl((int)r, (int)s, 64);
+      const uint32_t rs = rsn;
       const bool pad = rs == 0xFFFFFFFFu;
-      uint4 x = make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
-      if (!pad && sub <= units) x = rec16[(size_t)rs + sub];
+      const uint4 x = okn ? xn : make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
+      if (pass + 1 < L) {
+        rsn = (uint32_t)__shfl((int)r, (int)(s + per), 64);
+        okn = rsn != 0xFFFFFFFFu && sub <= units;
+        xn = rec16[okn ? (size_t)rsn + sub : 0];
+      }
       // the record's header word (len | flags << 24), from its group's lane 0
       const uint32_t hz = (uint32_t)__shfl((int)x.z, (int)grp, 64);
       const uint32_t len = hz & 0xFFFFFFu, flags = hz >> 24;
