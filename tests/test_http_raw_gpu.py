@@ -182,22 +182,26 @@ def test_head_size_limit_host_parser():
 
 @pytest.mark.gpu
 def test_gpu_raw_config5_full_size():
-    """BASELINE config 5's per-GPU batch as raw heads: 65,536 distinct
+    """BASELINE config 5's per-GPU batch as raw heads: 1,048,576 distinct
     requests of the 10K-rule set (with client-style variations) laid out
-    1,900 times back to back — 124.5M heads, 8.7 GB resident — through the
+    119 times back to back — 124.8M heads, 8.7 GB resident — through the
     device entry point in one call; every copy's verdicts equal the host
     path's verdicts for the distinct requests (size-independent property:
-    verdicts are per request, whatever the batch around it)."""
+    verdicts are per request, whatever the batch around it), and those equal
+    the oracle's for all 1,048,576 distinct heads."""
     import torch
     cl = Classifier(device=0)
     pols, info = synth.http10k_rules()
     cl.update_http_policy(pols)
-    D, reps = 65_536, 1_900
+    D, reps = 1 << 20, 119
     rq = synth.http10k_requests(D, info, seed=synth.SEED ^ 0x4A1)
     raws = _vary(_raw_requests(rq), np.random.default_rng(4), frac=0.02)  # long strings stay within the 256 MiB arena
     blob, off = _blob(raws)
     args = (rq["policy"], rq["ingress"], rq["port"], rq["remote"])
     want = _host_path(cl, *args, raws)
+    # every distinct head against the oracle (codec step + Envoy rule scan),
+    # so each of the 124.8M device verdicts below is oracle-checked
+    assert np.array_equal(want, _oracle(pols, *args, raws))
     dev = torch.device("cuda:0")
     tot = int(off[-1])
     d_raw = torch.from_numpy(blob[:tot]).to(dev).repeat(reps)
@@ -233,6 +237,9 @@ def test_gpu_raw_arena_split():
     blob, off = _blob(raws)
     args = (rq["policy"], rq["ingress"], rq["port"], rq["remote"])
     want = _host_path(cl, *args, raws)
+    # every distinct head against the oracle (codec step + Envoy rule scan),
+    # so each of the 124.8M device verdicts below is oracle-checked
+    assert np.array_equal(want, _oracle(pols, *args, raws))
     dev = torch.device("cuda:0")
     tot = int(off[-1])
     d_raw = torch.from_numpy(blob[:tot]).to(dev).repeat(reps)
