@@ -302,6 +302,7 @@ constexpr uint32_t kRawFnvInit = 2166136261u;
 // tiles [t0, next run's t0), tile t at granule base + (t - t0) * (1 + 2 * units).
 struct HttpRawRun {
   uint32_t t0, units, base, prog;
+  uint32_t send;  // one past the last real slot of the run's group (later slots are padding)
 };
 
 CG_HD inline uint32_t hash32(uint32_t x) {

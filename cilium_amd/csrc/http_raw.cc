@@ -244,9 +244,9 @@ bool raw_rest_phase(RawCall& c) {
   std::vector<HttpRawRun> runs;
   std::vector<uint32_t> cursors((size_t)G * K, 0);
   uint32_t tiles = 0, gran = 0;
-  auto add_run = [&](uint32_t t0, uint32_t t1, uint32_t units, uint32_t prog) {
+  auto add_run = [&](uint32_t t0, uint32_t t1, uint32_t units, uint32_t prog, uint32_t send) {
     if (t1 <= t0) return;
-    runs.push_back({t0, units, gran, prog});
+    runs.push_back({t0, units, gran, prog, send});
     gran += (t1 - t0) * (1 + 2 * units);
   };
   for (uint32_t g = 0; g < G; ++g) {
@@ -271,10 +271,10 @@ bool raw_rest_phase(RawCall& c) {
         if (bstart[k] <= last && last < bstart[k + 1]) u = k;
       const uint32_t next = bstart[u + 1];  // first slot of a larger key (or e)
       const uint32_t jend = next >= e ? (e + 63) / 64 : next / 64;
-      add_run(tiles + j, tiles + jend, u, prog);
+      add_run(tiles + j, tiles + jend, u, prog, tiles * CG_HTTP_TILE + cnt);
       j = jend;
     }
-    add_run(tiles + j, tiles + T, 0, prog);  // only overflow-arena slots
+    add_run(tiles + j, tiles + T, 0, prog, tiles * CG_HTTP_TILE + cnt);  // only overflow-arena slots
     tiles += T;
   }
   const size_t nslots = (size_t)tiles * CG_HTTP_TILE;
@@ -303,8 +303,7 @@ bool raw_rest_phase(RawCall& c) {
   hip_check(hipMemcpyAsync(d_runs, hr, runs.size() * sizeof(HttpRawRun), hipMemcpyHostToDevice, c.st), "H2D");
   hip_check(hipMemcpyAsync(d_cursor, hcur, cursors.size() * 4, hipMemcpyHostToDevice, c.st), "H2D");
   uint8_t* arena = (uint8_t*)c.sl->dev_buf(13, std::max<unsigned long long>(ovf_bytes, 16));
-  auto* order = (uint32_t*)c.sl->dev_buf(14, nslots * 4);
-  hip_check(hipMemsetAsync(order, 0xFF, nslots * 4, c.st), "hipMemsetAsync");  // padding slots
+  auto* order = (uint32_t*)c.sl->dev_buf(14, nslots * 4);  // padding entries: written by the build kernel
   auto* ttab = (HttpTile*)(batch + hdr.ttab_off);
   uint8_t* tdata = batch + hdr.tiles_off;
   const bool lists = c.in == RawInput::Lists;

@@ -1302,17 +1302,20 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
     // pass p + 1's chunk is loaded before pass p is coded and stored, so a
     // wave keeps two gathers in flight (unconditional: padding slots and
     // lanes past the record read chunk 0, then take the padding header)
+    // slots at or past the group's end are padding (their order entries are
+    // not initialised: written below)
+    const uint32_t nreal = run.send > t * 64 ? min(run.send - t * 64, 64u) : 0u;
     uint32_t rsn = (uint32_t)__shfl((int)r, (int)(lane / L), 64);
-    bool okn = rsn != 0xFFFFFFFFu && sub <= units;
+    bool okn = lane / L < nreal && sub <= units;
     uint4 xn = rec16[okn ? (size_t)rsn + sub : 0];
     for (uint32_t pass = 0; pass < L; ++pass) {
       const uint32_t s = pass * per + lane / L;  // this lane's slot in this pass
       const uint32_t rs = rsn;
-      const bool pad = rs == 0xFFFFFFFFu;
+      const bool pad = s >= nreal;
       const uint4 x = okn ? xn : make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
       if (pass + 1 < L) {
         rsn = (uint32_t)__shfl((int)r, (int)(s + per), 64);
-        okn = rsn != 0xFFFFFFFFu && sub <= units;
+        okn = s + per < nreal && sub <= units;
         xn = rec16[okn ? (size_t)rsn + sub : 0];
       }
       // the record's header word (len | flags << 24), from its group's lane 0
@@ -1336,7 +1339,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
           }
           if (o.pos) o.flush();
         }
-        if (!pad) order[(size_t)t * 64 + s] = x.x;
+        order[(size_t)t * 64 + s] = pad ? 0xFFFFFFFFu : x.x;
         reinterpret_cast<uint2*>(tb)[s] = make_uint2(x.y, (aoff16 & 0xFFFFFFu) | flags << 24);
         m = max(m, slen);
       } else if (sub <= units) {

@@ -323,7 +323,7 @@ def bench_http_raw(torch, dev, stream, cl, args, threads):
         assert bool((got == torch.from_numpy(want).to(dev).unsqueeze(0)).all()), "raw-path verdicts differ from host path"
     bpi = tot / D + 4 + 1 + 2 + 4 + 8 + 1  # head bytes, policy/ingress/port/remote, offset, verdict
     return line("HTTP/1 raw heads → verdicts/s on the GPU (codec step + packing + http_kernel), config 5", n, sec,
-                bpi, "raw_scan+raw_emit+http_kernel", None, "", threads,
+                bpi, "raw_scan+raw_rank+raw_build+http_kernel", None, "", threads,
                 {"config": {"workload": f"BASELINE config 5 requests as raw HTTP/1 heads ({tot / D:.1f} B/head avg), "
                             "10K rules", "requests": n},
                  "request_gbps": n * (tot / D) / sec / 1e9})
