@@ -1299,25 +1299,15 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
     const uint32_t L = units == 0 ? 1u : (units < 2 ? 2u : units < 4 ? 4u : units < 8 ? 8u : 16u);
     const uint32_t per = 64 / L, sub = lane & (L - 1), grp = lane & ~(L - 1);
     uint32_t m = 0;  // the longest slot string among this lane's header slots
-    // pass p + 1's chunk is loaded before pass p is coded and stored, so a
-    // wave keeps two gathers in flight (unconditional: padding slots and
-    // lanes past the record read chunk 0, then take the padding header)
     // slots at or past the group's end are padding (their order entries are
     // not initialised: written below)
     const uint32_t nreal = run.send > t * 64 ? min(run.send - t * 64, 64u) : 0u;
-    uint32_t rsn = (uint32_t)__shfl((int)r, (int)(lane / L), 64);
-    bool okn = lane / L < nreal && sub <= units;
-    uint4 xn = rec16[okn ? (size_t)rsn + sub : 0];
-    for (uint32_t pass = 0; pass < L; ++pass) {
-      const uint32_t s = pass * per + lane / L;  // this lane's slot in this pass
-      const uint32_t rs = rsn;
+    // one pass: slot s = pass * per + lane / L; x = its chunk (raw load, ok =
+    // a real slot and a chunk of the record)
+    auto body = [&](uint32_t pass, uint32_t rs, bool ok, uint4 xr) {
+      const uint32_t s = pass * per + lane / L;
       const bool pad = s >= nreal;
-      const uint4 x = okn ? xn : make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
-      if (pass + 1 < L) {
-        rsn = (uint32_t)__shfl((int)r, (int)(s + per), 64);
-        okn = s + per < nreal && sub <= units;
-        xn = rec16[okn ? (size_t)rsn + sub : 0];
-      }
+      const uint4 x = ok ? xr : make_uint4(0, 0, CG_HTTP_F_PAD << 24, 0);
       // the record's header word (len | flags << 24), from its group's lane 0
       const uint32_t hz = (uint32_t)__shfl((int)x.z, (int)grp, 64);
       const uint32_t len = hz & 0xFFFFFFu, flags = hz >> 24;
@@ -1358,6 +1348,27 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
           }
         }
         reinterpret_cast<uint4*>(tb + 512)[(size_t)u * 64 + s] = c;
+      }
+    };
+    auto fetch = [&](uint32_t pass, uint32_t& rs, bool& ok, uint4& x) {
+      const uint32_t s = pass * per + lane / L;
+      rs = (uint32_t)__shfl((int)r, (int)s, 64);
+      ok = s < nreal && sub <= units;
+      x = rec16[ok ? (size_t)rs + sub : 0];  // unconditional: others read chunk 0
+    };
+    // two passes' chunks in flight: A holds pass p, B pass p + 1; each is
+    // refilled (p + 2, p + 3) right after it is consumed
+    uint32_t rsA = 0, rsB = 0;
+    bool okA = false, okB = false;
+    uint4 xA = make_uint4(0, 0, 0, 0), xB = xA;
+    fetch(0, rsA, okA, xA);
+    if (L > 1) fetch(1, rsB, okB, xB);
+    for (uint32_t pass = 0; pass < L; pass += 2) {
+      body(pass, rsA, okA, xA);
+      if (pass + 2 < L) fetch(pass + 2, rsA, okA, xA);
+      if (pass + 1 < L) {
+        body(pass + 1, rsB, okB, xB);
+        if (pass + 3 < L) fetch(pass + 3, rsB, okB, xB);
       }
     }
     // the tile's tail: the longest string's bytes in its last unit
