@@ -451,7 +451,7 @@ __device__ __forceinline__ int64_t v6_search(const LpmDev& t, uint64_t hi, uint6
   return ans;
 }
 
-constexpr uint32_t kLpmV4 = 4, kLpmV6 = 2;  // addresses per lane per iteration
+constexpr uint32_t kLpmV4 = 8, kLpmV6 = 2;  // addresses per lane per iteration
 
 __global__ __launch_bounds__(256) void lpm_kernel(LpmDev t, bool v4f, bool v6f, const uint2* __restrict__ v4,
                                                   size_t n4, uint8_t* __restrict__ out4,
