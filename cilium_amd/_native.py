@@ -32,6 +32,8 @@ CG_NOT_FOUND = 22
 CG_NO_MAP = 23
 CG_UNSUPPORTED = 24
 
+CG_REGEX_ECMA, CG_REGEX_GO = 0, 1
+
 CG_L4_F_INGRESS = 0x01
 CG_L4_F_FRAGMENT = 0x02
 CG_L4_F_CB_POLICY = 0x04
@@ -156,6 +158,7 @@ SIGNATURES = {
     "cg_counters_copy_dev": (C.c_int, [_u64, _u32, _u32, _p, _sz, _p]),
     "cg_reset_counters": (C.c_int, [_u64]),
     "cg_diag_regex_match": (C.c_int, [C.c_char_p, _sz, _p, _sz, _u32, C.POINTER(C.c_uint8)]),
+    "cg_regex_validate": (C.c_int, [C.c_char_p, _sz, _u32]),
     "cg_diag_http_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_diag_http_rules_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
     "cg_diag_kafka_eval_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
@@ -183,6 +186,13 @@ lib = _load()
 def check(rc: int) -> None:
     if rc != CG_OK:
         raise CiliumGPUError(rc, lib.cg_last_error().decode(errors="replace"))
+
+
+def regex_validate(pattern, flavour: int = CG_REGEX_GO) -> None:
+    """cg_regex_validate: raises CiliumGPUError(CG_POLICY_REJECTED) with
+    the parser's message when `pattern` is not valid in `flavour`."""
+    b = pattern.encode("utf-8", "surrogateescape") if isinstance(pattern, str) else bytes(pattern)
+    check(lib.cg_regex_validate(b, len(b), flavour))
 
 
 def ptr(a) -> int | None:

@@ -1416,14 +1416,40 @@ int cg_reset_counters(uint64_t h) {
   });
 }
 
+// ------------------------------------------------------ regex syntax ----
+int cg_regex_validate(const char* re, size_t re_len, uint32_t flavour) {
+  return guarded([&] {
+    std::string err;
+    const RegexFlavour f = flavour == CG_REGEX_GO ? RegexFlavour::Go : RegexFlavour::Ecma;
+    if (flavour > CG_REGEX_GO) fail(CG_INVALID_ARGUMENT, "unknown regex flavour");
+    if (!regex_syntax_ok(std::string(re, re_len), &err, f)) fail(CG_POLICY_REJECTED, err);
+  });
+}
+
 // ------------------------------------------------------- diagnostics ----
 // Host-side walkers of the compiled tables and the regex compiler, for the
 // CPU test-suite only.  No verdict entry point calls them.
 int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t len, uint32_t search,
                         uint8_t* result) {
   return guarded([&] {
-    ByteDfa d = compile_regex(std::string(re, re_len), ByteSet::all(), search ? MatchMode::Search : MatchMode::Full);
-    *result = dfa_run(d, std::string((const char*)s, len)) ? 1 : 0;
+    // the last compiled patterns are kept: tests run one pattern on many strings
+    static std::mutex mu;
+    static std::map<std::pair<std::string, bool>, std::shared_ptr<const ByteDfa>> cache;
+    const auto key = std::make_pair(std::string(re, re_len), search != 0);
+    std::shared_ptr<const ByteDfa> d;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      auto it = cache.find(key);
+      if (it != cache.end()) d = it->second;
+    }
+    if (!d) {
+      d = std::make_shared<const ByteDfa>(
+          compile_regex(key.first, ByteSet::all(), search ? MatchMode::Search : MatchMode::Full));
+      std::lock_guard<std::mutex> g(mu);
+      if (cache.size() >= 64) cache.clear();
+      cache.emplace(key, d);
+    }
+    *result = dfa_run(*d, std::string((const char*)s, len)) ? 1 : 0;
   });
 }
 

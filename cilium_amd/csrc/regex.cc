@@ -1,5 +1,6 @@
-// regex.cc — ECMAScript-subset parser, Thompson NFA, subset construction,
-// minimization.  See regex.h for the semantics contract.
+// regex.cc — the ECMAScript front end (Envoy's std::regex), the shared
+// assertion-aware subset construction (regex_impl.h) and the DFA utilities.
+// See regex.h for the semantics contract; regex_go.cc is the Go front end.
 #include "regex.h"
 
 #include <algorithm>
@@ -8,52 +9,100 @@
 #include <tuple>
 #include <unordered_map>
 
+#include "regex_impl.h"
+
 namespace cg {
 
 namespace {
 
-// ---------------------------------------------------------------- AST ----
-struct Ast {
-  enum Kind { EMPTY, SET, CAT, ALT, REP, BOL, EOL };
-  Kind kind = EMPTY;
-  ByteSet set;
-  std::vector<int> kids;
-  int min = 0, max = 0;  // REP; max < 0 = unbounded
+struct VecHash {
+  size_t operator()(const std::vector<int>& v) const {
+    uint64_t h = 0x9e3779b97f4a7c15ULL ^ v.size();
+    for (int x : v) h = mix64(h ^ (uint64_t)(uint32_t)x);
+    return (size_t)h;
+  }
 };
 
 constexpr int kMaxRepeat = 1000;
 
-ByteSet set_digit() {
+// ------------------------------------------------ ECMAScript byte classes --
+// libstdc++ regex_traits<char> in the "C" locale: ctype<char>::is on the
+// byte as unsigned char (bytes >= 0x80 belong to no class).
+enum CType : uint16_t {
+  kUpper = 1, kLower = 2, kAlpha = 4, kDigit = 8, kXdigit = 16, kSpace = 32, kPrint = 64, kGraph = 128,
+  kCntrl = 256, kPunct = 512, kAlnum = 1024, kBlank = 2048, kUnder = 4096,
+};
+bool c_is(int b, uint16_t mask) {
+  if (b >= 0x80) return false;
+  const bool upper = b >= 'A' && b <= 'Z', lower = b >= 'a' && b <= 'z', digit = b >= '0' && b <= '9';
+  const bool alpha = upper || lower, space = b == ' ' || (b >= '\t' && b <= '\r');
+  const bool print = b >= 0x20 && b < 0x7f, graph = b > 0x20 && b < 0x7f;
+  uint16_t m = 0;
+  if (upper) m |= kUpper;
+  if (lower) m |= kLower;
+  if (alpha) m |= kAlpha;
+  if (digit) m |= kDigit;
+  if (digit || (b >= 'a' && b <= 'f') || (b >= 'A' && b <= 'F')) m |= kXdigit;
+  if (space) m |= kSpace;
+  if (print) m |= kPrint;
+  if (graph) m |= kGraph;
+  if (b < 0x20 || b == 0x7f) m |= kCntrl;
+  if (graph && !alpha && !digit) m |= kPunct;
+  if (alpha || digit) m |= kAlnum;
+  if (b == ' ' || b == '\t') m |= kBlank;
+  return (m & mask) || ((mask & kUnder) && b == '_');
+}
+ByteSet ctype_set(uint16_t mask) {
   ByteSet s;
-  s.set_range('0', '9');
+  for (int b = 0; b < 256; ++b)
+    if (c_is(b, mask)) s.set(b);
   return s;
 }
-ByteSet set_word() {
-  ByteSet s;
-  s.set_range('0', '9');
-  s.set_range('a', 'z');
-  s.set_range('A', 'Z');
-  s.set('_');
-  return s;
-}
-// Two flavours share the parser: Envoy's std::regex (ECMAScript, full
-// match) and Go's regexp (RE2 syntax, proxylib's MatchString search).  They
-// differ, on bytes, in '.' and '\s'.
-ByteSet set_space(bool go) {
-  // libstdc++ ctype<char> "space" in the C locale; Go RE2 \s is [\t\n\f\r ]
-  // (no \v: regexp/syntax perl_groups.go)
-  ByteSet s;
-  for (int c : {' ', '\t', '\n', '\f', '\r'}) s.set(c);
-  if (!go) s.set('\v');
-  return s;
-}
-ByteSet set_dot(bool go) {
-  // libstdc++ _AnyMatcher<ecma>: any char except '\n' and '\r'; Go RE2
-  // without the s flag: any char except '\n'
+ByteSet set_digit() { return ctype_set(kDigit); }
+ByteSet set_word() { return ctype_set(kAlnum | kUnder); }
+ByteSet set_space() { return ctype_set(kSpace); }  // [\t\n\v\f\r ]
+ByteSet set_dot() {
+  // libstdc++ _AnyMatcher<ecma>: any char except '\n' and '\r'
   ByteSet s = ByteSet::all();
   s.w['\n' >> 6] &= ~(1ULL << ('\n' & 63));
-  if (!go) s.w['\r' >> 6] &= ~(1ULL << ('\r' & 63));
+  s.w['\r' >> 6] &= ~(1ULL << ('\r' & 63));
   return s;
+}
+
+// regex_traits::lookup_classname (case-insensitive name)
+bool class_by_name(std::string n, uint16_t* mask) {
+  for (auto& c : n)
+    if (c >= 'A' && c <= 'Z') c = c - 'A' + 'a';
+  static const std::pair<const char*, uint16_t> kNames[] = {
+      {"d", kDigit},      {"w", kAlnum | kUnder}, {"s", kSpace},   {"alnum", kAlnum}, {"alpha", kAlpha},
+      {"blank", kBlank},  {"cntrl", kCntrl},      {"digit", kDigit}, {"graph", kGraph}, {"lower", kLower},
+      {"print", kPrint},  {"punct", kPunct},      {"space", kSpace}, {"upper", kUpper}, {"xdigit", kXdigit}};
+  for (auto& e : kNames)
+    if (n == e.first) {
+      *mask = e.second;
+      return true;
+    }
+  return false;
+}
+
+// regex_traits::lookup_collatename: the POSIX names of the 128 ASCII
+// characters (exact spelling; the index is the character)
+int collate_by_name(const std::string& n) {
+  static const char* const kNames[128] = {
+      "NUL", "SOH", "STX", "ETX", "EOT", "ENQ", "ACK", "alert", "backspace", "tab", "newline", "vertical-tab",
+      "form-feed", "carriage-return", "SO", "SI", "DLE", "DC1", "DC2", "DC3", "DC4", "NAK", "SYN", "ETB", "CAN",
+      "EM", "SUB", "ESC", "IS4", "IS3", "IS2", "IS1", "space", "exclamation-mark", "quotation-mark", "number-sign",
+      "dollar-sign", "percent-sign", "ampersand", "apostrophe", "left-parenthesis", "right-parenthesis",
+      "asterisk", "plus-sign", "comma", "hyphen", "period", "slash", "zero", "one", "two", "three", "four", "five",
+      "six", "seven", "eight", "nine", "colon", "semicolon", "less-than-sign", "equals-sign", "greater-than-sign",
+      "question-mark", "commercial-at", "A", "B", "C", "D", "E", "F", "G", "H", "I", "J", "K", "L", "M", "N", "O",
+      "P", "Q", "R", "S", "T", "U", "V", "W", "X", "Y", "Z", "left-square-bracket", "backslash",
+      "right-square-bracket", "circumflex", "underscore", "grave-accent", "a", "b", "c", "d", "e", "f", "g", "h",
+      "i", "j", "k", "l", "m", "n", "o", "p", "q", "r", "s", "t", "u", "v", "w", "x", "y", "z",
+      "left-curly-bracket", "vertical-line", "right-curly-bracket", "tilde", "DEL"};
+  for (int i = 0; i < 128; ++i)
+    if (n == kNames[i]) return i;
+  return -1;
 }
 
 int hexval(char c) {
@@ -63,22 +112,37 @@ int hexval(char c) {
   return -1;
 }
 
-class Parser {
+rx::SymSet to_sym(const ByteSet& b) {
+  rx::SymSet s(256);
+  for (int i = 0; i < 4; ++i) s.w[i] = b.w[i];
+  return s;
+}
+
+// ECMAScript grammar as libstdc++ (GCC 11, this image's std::regex — the
+// oracle's engine) scans and compiles it (bits/regex_scanner.tcc,
+// regex_compiler.tcc), lowered to a Prog over bytes.
+class EcmaParser {
  public:
-  Parser(const std::string& re, std::vector<Ast>& nodes, bool go = false) : s_(re), n_(nodes), go_(go) {}
+  EcmaParser(const std::string& re, rx::Prog& prog) : s_(re), g_(prog) {}
 
   int parse() {
     int r = parse_alt();
     if (p_ != s_.size()) err(CG_POLICY_REJECTED, "unmatched ')'");
+    // std::regex accepts the pattern; a construct in it is beyond a DFA
+    if (!unsupported_.empty()) fail(CG_UNSUPPORTED, "regex \"" + s_ + "\": " + unsupported_);
     return r;
   }
 
  private:
   const std::string& s_;
-  std::vector<Ast>& n_;
-  bool go_ = false;  // Go RE2 flavour (search mode)
+  rx::Prog& g_;
   size_t p_ = 0;
   int depth_ = 0;
+  // capture groups: started so far (libstdc++ _M_subexpr_count - 1) and
+  // still open (_M_paren_stack), for the validity of a backreference
+  int ncap_ = 0;
+  std::vector<int> open_caps_;
+  std::string unsupported_;  // first construct a DFA cannot express
 
   [[noreturn]] void err(int code, const std::string& m) {
     fail(code, "regex \"" + s_ + "\": " + m + " at offset " + std::to_string(p_));
@@ -86,15 +150,12 @@ class Parser {
   bool eof() const { return p_ >= s_.size(); }
   char peek() const { return s_[p_]; }
 
-  int mk(Ast a) {
-    n_.push_back(std::move(a));
-    return (int)n_.size() - 1;
-  }
-  int mkset(const ByteSet& s) {
-    Ast a;
-    a.kind = Ast::SET;
-    a.set = s;
-    return mk(a);
+  int mkset(const ByteSet& s) { return g_.add_set(to_sym(s)); }
+  int mkassert(uint8_t as) {
+    rx::Node n;
+    n.kind = rx::Node::ASSERT;
+    n.as = as;
+    return g_.add(n);
   }
 
   int parse_alt() {
@@ -106,21 +167,21 @@ class Parser {
     }
     --depth_;
     if (alts.size() == 1) return alts[0];
-    Ast a;
-    a.kind = Ast::ALT;
+    rx::Node a;
+    a.kind = rx::Node::ALT;
     a.kids = alts;
-    return mk(a);
+    return g_.add(a);
   }
 
   int parse_cat() {
     std::vector<int> items;
     while (!eof() && peek() != '|' && peek() != ')') items.push_back(parse_quant());
-    if (items.empty()) return mk(Ast{});
+    if (items.empty()) return g_.add(rx::Node{});
     if (items.size() == 1) return items[0];
-    Ast a;
-    a.kind = Ast::CAT;
+    rx::Node a;
+    a.kind = rx::Node::CAT;
     a.kids = items;
-    return mk(a);
+    return g_.add(a);
   }
 
   bool parse_int(int* v) {
@@ -138,7 +199,6 @@ class Parser {
   int parse_quant() {
     bool assertion = false;
     int atom = parse_atom(&assertion);
-    bool quantified = false;
     while (!eof()) {
       char c = peek();
       int mn, mx;
@@ -168,134 +228,190 @@ class Parser {
       // "a?+") as nested repeats; a trailing '?' only marks one lazy.
       if (assertion) err(CG_POLICY_REJECTED, "nothing to repeat");
       if (!eof() && peek() == '?') ++p_;
-      Ast a;
-      a.kind = Ast::REP;
+      rx::Node a;
+      a.kind = rx::Node::REP;
       a.kids = {atom};
       a.min = mn;
       a.max = mx;
-      atom = mk(a);
-      quantified = true;
+      atom = g_.add(a);
     }
     return atom;
   }
 
-  // Class escape inside or outside brackets; returns true and fills `out`
-  // for \d\D\w\W\s\S, else false (p_ unchanged).
+  // Class escape \d\D\w\W\s\S (the scanner's quoted_class token).
   bool class_escape(char c, ByteSet* out) {
     switch (c) {
       case 'd': *out = set_digit(); return true;
       case 'w': *out = set_word(); return true;
-      case 's': *out = set_space(go_); return true;
+      case 's': *out = set_space(); return true;
       case 'D': *out = set_digit(); out->invert(); return true;
       case 'W': *out = set_word(); out->invert(); return true;
-      case 'S': *out = set_space(go_); out->invert(); return true;
+      case 'S': *out = set_space(); out->invert(); return true;
       default: return false;
     }
   }
 
-  // Character escape after '\' (p_ at the char after '\').  Returns the byte.
+  // _M_eat_escape_ecma for an escape that yields one character (p_ at the
+  // char after '\'); class escapes and \b \B are handled by the callers.
   int char_escape(bool in_class) {
     if (eof()) err(CG_POLICY_REJECTED, "trailing backslash");
     char c = s_[p_++];
     switch (c) {
+      case '0': return 0;  // NUL; following digits are ordinary
+      case 'b': return '\b';  // in a bracket only (callers)
       case 'f': return '\f';
       case 'n': return '\n';
       case 'r': return '\r';
       case 't': return '\t';
       case 'v': return '\v';
-      case 'b':
-        if (in_class) return '\b';
-        err(CG_UNSUPPORTED, "word boundary \\b");
-      case 'B': err(CG_UNSUPPORTED, "word boundary \\B");
-      case '0':
-        if (!eof() && peek() >= '0' && peek() <= '9') err(CG_UNSUPPORTED, "octal escape");
-        return 0;
-      case 'x': {
-        if (p_ + 2 > s_.size()) err(CG_POLICY_REJECTED, "bad \\x escape");
-        int h = hexval(s_[p_]), l = hexval(s_[p_ + 1]);
-        if (h < 0 || l < 0) err(CG_POLICY_REJECTED, "bad \\x escape");
-        p_ += 2;
-        return h * 16 + l;
-      }
+      case 'x':
       case 'u': {
-        if (p_ + 4 > s_.size()) err(CG_POLICY_REJECTED, "bad \\u escape");
+        const int nd = c == 'x' ? 2 : 4;
         int v = 0;
-        for (int i = 0; i < 4; ++i) {
-          int d = hexval(s_[p_ + i]);
-          if (d < 0) err(CG_POLICY_REJECTED, "bad \\u escape");
-          v = v * 16 + d;
+        for (int i = 0; i < nd; ++i) {
+          if (eof() || hexval(peek()) < 0) err(CG_POLICY_REJECTED, "bad \\x / \\u escape");
+          v = v * 16 + hexval(s_[p_++]);
         }
-        p_ += 4;
-        if (v > 0xFF) err(CG_UNSUPPORTED, "\\u escape beyond one byte");
-        return v;
+        return v & 0xFF;  // assigned to a char: Ł reads as 0x41
       }
-      case 'c': {
-        if (eof() || !((peek() >= 'a' && peek() <= 'z') || (peek() >= 'A' && peek() <= 'Z')))
-          err(CG_POLICY_REJECTED, "bad \\c escape");
-        // libstdc++ (the engine Envoy ran) matches "\cX" as the letter X
-        // itself, not the control character; measured against std::regex.
+      case 'c':
+        // libstdc++ reads "\cX" as the character X itself, for any X
+        if (eof()) err(CG_POLICY_REJECTED, "bad \\c escape");
         return (unsigned char)s_[p_++];
-      }
       default:
-        if (c >= '1' && c <= '9') err(CG_UNSUPPORTED, "backreference");
+        if (c >= '1' && c <= '9') {
+          // a backreference token (all following digits): "Unexpected
+          // character" inside a bracket; outside one valid iff the group
+          // exists and is closed (_M_insert_backref) — then std::regex
+          // supports it and a DFA does not
+          if (in_class) err(CG_POLICY_REJECTED, "backreference in bracket");
+          long idx = c - '0';
+          while (!eof() && peek() >= '0' && peek() <= '9') {
+            idx = idx * 10 + (s_[p_++] - '0');
+            if (idx > 0x7fffffff) err(CG_POLICY_REJECTED, "invalid back reference");
+          }
+          if (idx > ncap_) err(CG_POLICY_REJECTED, "back-reference index exceeds group count");
+          for (int o : open_caps_)
+            if (o == idx) err(CG_POLICY_REJECTED, "back-reference to an open group");
+          if (unsupported_.empty()) unsupported_ = "backreference";
+          return -1;
+        }
         return (unsigned char)c;  // identity escape
     }
   }
 
+  // _M_eat_class: the name up to the first `ch`, then "ch]"
+  std::string eat_class_name(char ch) {
+    size_t e = s_.find(ch, p_);
+    if (e == std::string::npos || e + 1 >= s_.size() || s_[e + 1] != ']')
+      err(CG_POLICY_REJECTED, "unterminated [: [. or [= in bracket");
+    std::string n = s_.substr(p_, e - p_);
+    p_ = e + 2;
+    return n;
+  }
+
+  // A bracket expression as _M_expression_term walks it: a cached last
+  // character (the possible start of a range), or a class just added.
   int parse_class() {
-    // p_ just after '['
     bool neg = false;
     if (!eof() && peek() == '^') {
       neg = true;
       ++p_;
     }
     ByteSet set;
-    for (;;) {
+    enum { NONE, CHAR, CLASS } last = NONE;
+    int last_c = 0;
+    auto push_char = [&](int ch) {
+      if (last == CHAR) set.set(last_c);
+      last = CHAR;
+      last_c = ch;
+    };
+    auto push_class = [&]() {
+      if (last == CHAR) set.set(last_c);
+      last = CLASS;
+    };
+    // One scanner token; kinds: 'c' char (ord/hex), 'q' quoted class,
+    // '.' collating symbol, ':' class name, '=' equivalence class, '-'
+    // dash, ']' end.
+    struct Tok {
+      char kind;
+      int ch;
+      ByteSet set;
+    };
+    auto next_tok = [&]() -> Tok {
       if (eof()) err(CG_POLICY_REJECTED, "unterminated [");
-      char c = peek();
-      // ECMAScript (libstdc++ _M_scan_in_bracket): ']' always closes the
-      // bracket, so "[]" matches nothing and "[^]" matches any byte.
-      if (c == ']') {
-        ++p_;
-        break;
-      }
-      // one class atom
-      int lo = -1;
-      ByteSet esc;
-      ++p_;
-      if (c == '\\') {
-        if (!eof() && class_escape(peek(), &esc)) {
+      const char c = s_[p_++];
+      Tok t{'c', (unsigned char)c, ByteSet{}};
+      if (c == '-') {
+        t.kind = '-';
+      } else if (c == ']') {
+        t.kind = ']';
+      } else if (c == '[') {
+        if (eof()) err(CG_POLICY_REJECTED, "unexpected '[' at end of bracket");
+        const char k = peek();
+        if (k == '.' || k == ':' || k == '=') {
           ++p_;
-          set.merge(esc);
-          if (!eof() && peek() == '-' && p_ + 1 < s_.size() && s_[p_ + 1] != ']')
-            err(CG_POLICY_REJECTED, "class escape in range");
-          continue;
+          const std::string n = eat_class_name(k);
+          t.kind = k;
+          if (k == ':') {
+            uint16_t mask;
+            if (!class_by_name(n, &mask)) err(CG_POLICY_REJECTED, "invalid character class [:" + n + ":]");
+            t.set = ctype_set(mask);
+          } else {
+            const int e = collate_by_name(n);
+            if (e < 0) err(CG_POLICY_REJECTED, "invalid collating element");
+            if (k == '.') {
+              t.ch = e;
+            } else {
+              // transform_primary: equal after tolower
+              auto low = [](int b) { return b >= 'A' && b <= 'Z' ? b + 32 : b; };
+              for (int b = 0; b < 256; ++b)
+                if (low(b) == low(e)) t.set.set(b);
+            }
+          }
         }
-        lo = char_escape(true);
-      } else if (c == '[' && !eof() && (peek() == ':' || peek() == '.' || peek() == '=')) {
-        err(CG_UNSUPPORTED, "POSIX bracket expression");
-      } else {
-        lo = (unsigned char)c;
-      }
-      // range?
-      if (!eof() && peek() == '-' && p_ + 1 < s_.size() && s_[p_ + 1] != ']') {
-        ++p_;
-        char d = s_[p_++];
-        int hi;
-        if (d == '\\') {
-          if (!eof() && class_escape(peek(), &esc)) err(CG_POLICY_REJECTED, "class escape in range");
-          hi = char_escape(true);
+      } else if (c == '\\') {
+        if (!eof() && class_escape(peek(), &t.set)) {
+          ++p_;
+          t.kind = 'q';
         } else {
-          hi = (unsigned char)d;
+          t.ch = char_escape(true);
         }
-        // libstdc++ compares the range ends as (signed) char.
-        int slo = (int8_t)lo, shi = (int8_t)hi;
-        if (slo > shi) err(CG_POLICY_REJECTED, "invalid range");
-        for (int v = slo; v <= shi; ++v) set.set((uint8_t)(int8_t)v);
-      } else {
-        set.set(lo);
+      }
+      return t;
+    };
+    for (;;) {
+      Tok t = next_tok();
+      if (t.kind == ']') break;
+      if (t.kind == '.' || t.kind == 'c') {
+        push_char(t.ch);
+      } else if (t.kind == ':' || t.kind == '=' || t.kind == 'q') {
+        push_class();
+        set.merge(t.set);
+      } else {  // '-'
+        if (!eof() && peek() == ']') {
+          ++p_;
+          push_char('-');
+          break;
+        }
+        if (last == CLASS) err(CG_POLICY_REJECTED, "invalid start of range");
+        if (last == CHAR) {
+          Tok e = next_tok();
+          int hi;
+          if (e.kind == 'c') hi = e.ch;
+          else if (e.kind == '-') hi = '-';
+          else err(CG_POLICY_REJECTED, "invalid end of range");
+          // libstdc++ compares the range ends as (signed) char
+          const int slo = (int8_t)last_c, shi = (int8_t)hi;
+          if (slo > shi) err(CG_POLICY_REJECTED, "invalid range");
+          for (int v = slo; v <= shi; ++v) set.set((uint8_t)(int8_t)v);
+          last = NONE;
+        } else {
+          push_char('-');  // ECMAScript: a dash outside a range is a char
+        }
       }
     }
+    if (last == CHAR) set.set(last_c);
     if (neg) set.invert();
     return mkset(set);
   }
@@ -304,47 +420,50 @@ class Parser {
     char c = s_[p_++];
     switch (c) {
       case '(': {
+        int cap = 0;
         if (!eof() && peek() == '?') {
           if (p_ + 1 < s_.size() && s_[p_ + 1] == ':') {
             p_ += 2;
           } else if (p_ + 1 < s_.size() && (s_[p_ + 1] == '=' || s_[p_ + 1] == '!')) {
-            err(CG_UNSUPPORTED, "lookahead");
+            p_ += 2;
+            *assertion = true;  // libstdc++ _M_assertion: no quantifier may follow
+            if (unsupported_.empty()) unsupported_ = "lookahead";
           } else {
             err(CG_POLICY_REJECTED, "bad group");
           }
+        } else {
+          cap = ++ncap_;
+          open_caps_.push_back(cap);
         }
         int r = parse_alt();
         if (eof() || peek() != ')') err(CG_POLICY_REJECTED, "missing ')'");
         ++p_;
+        if (cap) open_caps_.pop_back();
         return r;
       }
       case ')': err(CG_POLICY_REJECTED, "unmatched ')'");
       case '[': return parse_class();
-      case '.': return mkset(set_dot(go_));
-      case '^': {
-        *assertion = true;
-        Ast a;
-        a.kind = Ast::BOL;
-        return mk(a);
-      }
-      case '$': {
-        *assertion = true;
-        Ast a;
-        a.kind = Ast::EOL;
-        return mk(a);
-      }
+      case '.': return mkset(set_dot());
+      case '^': *assertion = true; return mkassert(rx::kBeginText);
+      case '$': *assertion = true; return mkassert(rx::kEndText);
       case '*':
       case '+':
       case '?':
       case '{': --p_; err(CG_POLICY_REJECTED, "nothing to repeat");
       case '\\': {
+        if (!eof() && (peek() == 'b' || peek() == 'B')) {
+          *assertion = true;
+          return mkassert(s_[p_++] == 'b' ? rx::kWordB : rx::kNotWordB);
+        }
         ByteSet esc;
         if (!eof() && class_escape(peek(), &esc)) {
           ++p_;
           return mkset(esc);
         }
+        const int ch = char_escape(false);
+        if (ch < 0) return g_.add(rx::Node{});  // backreference (unsupported_ is set)
         ByteSet s;
-        s.set(char_escape(false));
+        s.set(ch);
         return mkset(s);
       }
       default: {
@@ -356,19 +475,30 @@ class Parser {
   }
 };
 
+void ecma_compile(const std::string& re, rx::Prog* g) {
+  g->nsym = 256;
+  g->root = EcmaParser(re, *g).parse();
+  g->word.assign(256, 0);
+  g->newline.assign(256, 0);
+  const ByteSet w = set_word();
+  for (int b = 0; b < 256; ++b) g->word[b] = w.test(b);
+  g->newline['\n'] = 1;
+}
+
 // ---------------------------------------------------------------- NFA ----
 struct NState {
-  enum Type : uint8_t { SET, EPS, SPLIT, BOL, EOL, MATCH };
+  enum Type : uint8_t { SET, EPS, SPLIT, ASSERT, MATCH };
   Type type = EPS;
+  uint8_t as = 0;
   int out = -1, out1 = -1;
-  ByteSet set;
+  int set = -1;
 };
 
 constexpr int kMaxNfa = 200000;
 
 class NfaBuilder {
  public:
-  NfaBuilder(const std::vector<Ast>& ast) : a_(ast) {}
+  explicit NfaBuilder(const rx::Prog& g) : g_(g) {}
   std::vector<NState> st;
 
   int add(NState::Type t) {
@@ -390,58 +520,51 @@ class NfaBuilder {
     return {a.in, b.out};
   }
   Frag build(int id) {
-    const Ast& n = a_[id];
+    const rx::Node& n = g_.nodes[id];
     switch (n.kind) {
-      case Ast::EMPTY: return eps();
-      case Ast::SET: {
+      case rx::Node::EMPTY: return eps();
+      case rx::Node::SET: {
         int s = add(NState::SET);
         st[s].set = n.set;
         int e = add(NState::EPS);
         st[s].out = e;
         return {s, e};
       }
-      case Ast::BOL:
-      case Ast::EOL: {
-        int s = add(n.kind == Ast::BOL ? NState::BOL : NState::EOL);
+      case rx::Node::ASSERT: {
+        int s = add(NState::ASSERT);
+        st[s].as = n.as;
         int e = add(NState::EPS);
         st[s].out = e;
         return {s, e};
       }
-      case Ast::CAT: {
+      case rx::Node::CAT: {
         Frag f = build(n.kids[0]);
         for (size_t i = 1; i < n.kids.size(); ++i) f = cat(f, build(n.kids[i]));
         return f;
       }
-      case Ast::ALT: {
+      case rx::Node::ALT: {
         int e = add(NState::EPS);
-        int entry = -1;
-        // chain of SPLITs
-        int prev_split = -1;
+        int entry = -1, prev_split = -1;
         for (size_t i = 0; i < n.kids.size(); ++i) {
           Frag f = build(n.kids[i]);
           st[f.out].out = e;
           if (i + 1 < n.kids.size()) {
             int sp = add(NState::SPLIT);
             st[sp].out = f.in;
-            if (prev_split < 0)
-              entry = sp;
-            else
-              st[prev_split].out1 = sp;
+            if (prev_split < 0) entry = sp;
+            else st[prev_split].out1 = sp;
             prev_split = sp;
           } else {
-            if (prev_split < 0)
-              entry = f.in;
-            else
-              st[prev_split].out1 = f.in;
+            if (prev_split < 0) entry = f.in;
+            else st[prev_split].out1 = f.in;
           }
         }
         return {entry, e};
       }
-      case Ast::REP: {
+      case rx::Node::REP: {
         Frag f = eps();
         for (int i = 0; i < n.min; ++i) f = cat(f, build(n.kids[0]));
         if (n.max < 0) {
-          // star
           Frag body = build(n.kids[0]);
           int sp = add(NState::SPLIT);
           int e = add(NState::EPS);
@@ -467,201 +590,258 @@ class NfaBuilder {
   }
 
  private:
-  const std::vector<Ast>& a_;
+  const rx::Prog& g_;
 };
 
-struct VecHash {
-  size_t operator()(const std::vector<int>& v) const {
-    uint64_t h = 0x9e3779b97f4a7c15ULL ^ v.size();
-    for (int x : v) h = mix64(h ^ (uint64_t)(uint32_t)x);
-    return (size_t)h;
-  }
-};
+// ------------------------------------------------- subset construction ---
+// DFA state = (kept NFA states, kind of the previous symbol, decoder state).
+// Kept: SET and MATCH states, and lookahead assertions (End*, word
+// boundaries) waiting for the next symbol.  Begin* assertions are settled
+// when reached, from the previous symbol's kind.
+enum PrevKind : int { kStart = 0, kNl = 1, kWord = 2, kOther = 3 };
 
 class Subset {
  public:
-  Subset(const std::vector<NState>& st, int start, const ByteSet& alpha)
-      : st_(st), start_(start), alpha_(alpha), mark_(st.size(), 0) {}
+  Subset(const std::vector<NState>& st, const rx::Prog& g, const rx::Decoder& dec, const ByteSet& alpha)
+      : st_(st), g_(g), dec_(dec), alpha_(alpha), mark_(st.size(), 0) {
+    for (const auto& s : st_) {
+      if (s.type != NState::ASSERT) continue;
+      if (s.as == rx::kBeginText || s.as == rx::kBeginLine) need_begin_ = true;
+      if (s.as == rx::kBeginLine) need_nl_ = true;
+      if (s.as == rx::kWordB || s.as == rx::kNotWordB) need_word_ = true;
+    }
+  }
 
-  ByteDfa run(int max_states) {
-    // byte classes: partition 0..255 by every SET state's set and the alphabet
-    std::vector<ByteSet> sets;
-    for (const auto& s : st_)
-      if (s.type == NState::SET) sets.push_back(s.set);
-    sets.push_back(alpha_);
-    std::vector<int> cls(256, 0);
+  ByteDfa run(int start, int max_states) {
+    // symbols that every SET and the assertions treat alike share a class
+    std::vector<int> symcls(g_.nsym);
     {
-      std::map<std::vector<bool>, int> sig2id;
-      for (int b = 0; b < 256; ++b) {
-        std::vector<bool> sig(sets.size());
-        for (size_t i = 0; i < sets.size(); ++i) sig[i] = sets[i].test(b);
-        auto it = sig2id.emplace(sig, (int)sig2id.size()).first;
-        cls[b] = it->second;
+      std::map<std::vector<uint8_t>, int> sig2id;
+      std::vector<int> sets_used;
+      for (const auto& s : st_)
+        if (s.type == NState::SET) sets_used.push_back(s.set);
+      std::sort(sets_used.begin(), sets_used.end());
+      sets_used.erase(std::unique(sets_used.begin(), sets_used.end()), sets_used.end());
+      for (int y = 0; y < g_.nsym; ++y) {
+        std::vector<uint8_t> sig;
+        sig.reserve(sets_used.size() + 2);
+        for (int k : sets_used) sig.push_back(g_.sets[k].test(y));
+        sig.push_back(g_.word[y]);
+        sig.push_back(g_.newline[y]);
+        symcls[y] = sig2id.emplace(sig, (int)sig2id.size()).first->second;
       }
     }
-    int ncls = 0;
-    for (int b = 0; b < 256; ++b) ncls = std::max(ncls, cls[b] + 1);
-    std::vector<int> rep(ncls, -1);
-    for (int b = 0; b < 256; ++b)
-      if (rep[cls[b]] < 0) rep[cls[b]] = b;
+    // byte classes: equal alphabet membership and, from every decoder
+    // state, equal next state and equal emitted symbol classes
+    std::vector<int> bcls(256);
+    std::vector<int> rep;
+    {
+      std::map<std::vector<int>, int> sig2id;
+      for (int b = 0; b < 256; ++b) {
+        std::vector<int> sig{alpha_.test(b)};
+        for (int q = 0; q < dec_.nstates; ++q) {
+          const size_t k = (size_t)q * 256 + b;
+          sig.push_back(dec_.next[k]);
+          sig.push_back(dec_.nemit[k]);
+          for (int e = 0; e < dec_.nemit[k]; ++e) sig.push_back(symcls[dec_.emit[k * 4 + e]]);
+        }
+        auto it = sig2id.emplace(sig, (int)sig2id.size());
+        bcls[b] = it.first->second;
+        if (it.second) rep.push_back(b);
+      }
+    }
 
-    // DFA states: key = (is_start flag folded in as -1 marker) + kept NFA states.
     std::unordered_map<std::vector<int>, int, VecHash> ids;
-    std::vector<std::vector<int>> sets_of;
-    std::vector<uint8_t> is_start;
+    std::vector<std::vector<int>> keys;
     ByteDfa d;
-    d.trans.assign(256, 0);  // dead
+    d.trans.assign(256, 0);
     d.accept.push_back(0);
-    sets_of.push_back({});
-    is_start.push_back(0);
+    keys.push_back({});
 
-    std::vector<int> s0 = closure({start_}, true);
-    std::vector<int> key0 = s0;
-    key0.insert(key0.begin(), -1);
-    ids[key0] = 1;
-    sets_of.push_back(s0);
-    is_start.push_back(1);
-    d.trans.resize(2 * 256, 0);
-    d.accept.push_back(accepts(s0, true));
+    auto intern = [&](std::vector<int> kept, int pk, int q) -> int {
+      if (kept.empty()) return 0;
+      kept.push_back(-1 - canon(pk));
+      kept.push_back(-16 - q);
+      auto it = ids.find(kept);
+      if (it != ids.end()) return it->second;
+      if ((int)keys.size() >= max_states) fail(CG_UNSUPPORTED, "regex DFA exceeds state budget");
+      const int id = (int)keys.size();
+      ids.emplace(kept, id);
+      keys.push_back(std::move(kept));
+      d.trans.resize((size_t)(id + 1) * 256, 0);
+      d.accept.push_back(0);
+      return id;
+    };
 
-    std::deque<int> work{1};
-    std::vector<int> moved;
+    std::vector<int> s0 = closure({start}, kStart, false, -1);
+    const int first = intern(s0, kStart, 0);
+    if (first == 0) {  // no string can match
+      d.accept.push_back(0);
+      d.trans.resize(2 * 256, 0);
+      d.start = 1;
+      return d;
+    }
+    std::deque<int> work{first};
+    std::vector<bool> done(2, false);
     while (!work.empty()) {
-      int ds = work.front();
+      const int ds = work.front();
       work.pop_front();
-      std::vector<int> cur = sets_of[ds];
-      for (int c = 0; c < ncls; ++c) {
-        int b = rep[c];
+      if ((int)done.size() <= ds) done.resize(ds + 1, false);
+      if (done[ds]) continue;
+      done[ds] = true;
+      std::vector<int> key = keys[ds];
+      const int q = -16 - key.back();
+      key.pop_back();
+      const int pk = -1 - key.back();
+      key.pop_back();
+      // acceptance: the decoder's pending bytes flush as symbols, then the
+      // end of input settles the pending assertions
+      {
+        std::vector<int> k = key;
+        int p = pk;
+        for (int i = 0; i < dec_.pending[q] && !k.empty(); ++i) {
+          k = step(k, p, dec_.flush);
+          p = kind(dec_.flush);
+        }
+        if (!k.empty()) {
+          std::vector<int> r = closure(k, p, true, -1);
+          for (int x : r)
+            if (st_[x].type == NState::MATCH) d.accept[ds] = 1;
+        }
+      }
+      for (size_t c = 0; c < rep.size(); ++c) {
+        const int b = rep[c];
         int target = 0;
         if (alpha_.test(b)) {
-          moved.clear();
-          for (int ns : cur)
-            if (st_[ns].type == NState::SET && st_[ns].set.test(b)) moved.push_back(st_[ns].out);
-          if (!moved.empty()) {
-            std::vector<int> nx = closure(moved, false);
-            if (!nx.empty()) {
-              auto it = ids.find(nx);
-              if (it == ids.end()) {
-                if ((int)sets_of.size() >= max_states)
-                  fail(CG_UNSUPPORTED, "regex DFA exceeds state budget");
-                target = (int)sets_of.size();
-                ids.emplace(nx, target);
-                sets_of.push_back(nx);
-                is_start.push_back(0);
-                d.trans.resize((size_t)(target + 1) * 256, 0);
-                d.accept.push_back(accepts(nx, false));
-                work.push_back(target);
-              } else {
-                target = it->second;
-              }
-            }
+          const size_t kk = (size_t)q * 256 + b;
+          std::vector<int> k = key;
+          int p = pk;
+          for (int e = 0; e < dec_.nemit[kk] && !k.empty(); ++e) {
+            const int y = dec_.emit[kk * 4 + e];
+            k = step(k, p, y);
+            p = kind(y);
           }
+          target = intern(k, p, dec_.next[kk]);
+          if (target && ((int)done.size() <= target || !done[target])) work.push_back(target);
         }
         for (int bb = 0; bb < 256; ++bb)
-          if (cls[bb] == c) d.trans[(size_t)ds * 256 + bb] = target;
+          if (bcls[bb] == (int)c) d.trans[(size_t)ds * 256 + bb] = target;
       }
     }
-    d.start = 1;
+    d.start = first;
     return d;
   }
 
  private:
   const std::vector<NState>& st_;
-  int start_;
+  const rx::Prog& g_;
+  const rx::Decoder& dec_;
   ByteSet alpha_;
   std::vector<uint32_t> mark_;
   uint32_t gen_ = 0;
+  bool need_begin_ = false, need_nl_ = false, need_word_ = false;
 
-  // epsilon closure; keeps SET, EOL and MATCH states (sorted, unique).
-  std::vector<int> closure(const std::vector<int>& seeds, bool at_start) {
+  int kind(int y) const { return g_.newline[y] ? kNl : g_.word[y] ? kWord : kOther; }
+  int canon(int pk) const {
+    if (pk == kStart && !need_begin_) return kOther;
+    if (pk == kNl && !need_nl_) return kOther;
+    if (pk == kWord && !need_word_) return kOther;
+    return pk;
+  }
+  // next: a symbol, or -1 = end of input (when `known`)
+  bool holds(uint8_t as, int pk, int next) const {
+    const bool pw = pk == kWord, nw = next >= 0 && g_.word[next];
+    switch (as) {
+      case rx::kBeginText: return pk == kStart;
+      case rx::kBeginLine: return pk == kStart || pk == kNl;
+      case rx::kEndText: return next < 0;
+      case rx::kEndLine: return next < 0 || g_.newline[next];
+      case rx::kWordB: return pw != nw;
+      case rx::kNotWordB: return pw == nw;
+    }
+    return false;
+  }
+
+  // epsilon closure at a position whose previous symbol has kind pk; with
+  // `known`, the next symbol (or the end) settles every assertion
+  std::vector<int> closure(const std::vector<int>& seeds, int pk, bool known, int next) {
     ++gen_;
-    std::vector<int> stack(seeds.begin(), seeds.end());
+    std::vector<int> stack(seeds.rbegin(), seeds.rend());
     std::vector<int> kept;
     while (!stack.empty()) {
-      int s = stack.back();
+      const int s = stack.back();
       stack.pop_back();
       if (s < 0 || mark_[s] == gen_) continue;
       mark_[s] = gen_;
       const NState& n = st_[s];
       switch (n.type) {
         case NState::SET:
-        case NState::MATCH:
-        case NState::EOL: kept.push_back(s); break;
+        case NState::MATCH: kept.push_back(s); break;
         case NState::EPS: stack.push_back(n.out); break;
         case NState::SPLIT:
-          stack.push_back(n.out);
           stack.push_back(n.out1);
+          stack.push_back(n.out);
           break;
-        case NState::BOL:
-          if (at_start) stack.push_back(n.out);
+        case NState::ASSERT: {
+          const bool look = n.as != rx::kBeginText && n.as != rx::kBeginLine;
+          if (look && !known) kept.push_back(s);
+          else if (holds(n.as, pk, next)) stack.push_back(n.out);
           break;
+        }
       }
     }
     std::sort(kept.begin(), kept.end());
     return kept;
   }
 
-  // Is MATCH reachable at end of input from this set?
-  uint8_t accepts(const std::vector<int>& set, bool at_start) {
-    ++gen_;
-    std::vector<int> stack(set.begin(), set.end());
-    while (!stack.empty()) {
-      int s = stack.back();
-      stack.pop_back();
-      if (s < 0 || mark_[s] == gen_) continue;
-      mark_[s] = gen_;
-      const NState& n = st_[s];
-      switch (n.type) {
-        case NState::MATCH: return 1;
-        case NState::SET: break;
-        case NState::EOL:
-        case NState::EPS: stack.push_back(n.out); break;
-        case NState::SPLIT:
-          stack.push_back(n.out);
-          stack.push_back(n.out1);
-          break;
-        case NState::BOL:
-          if (at_start) stack.push_back(n.out);
-          break;
-      }
-    }
-    return 0;
+  // consume symbol y from the kept set k (previous kind pk)
+  std::vector<int> step(const std::vector<int>& k, int pk, int y) {
+    std::vector<int> r = closure(k, pk, true, y);
+    std::vector<int> moved;
+    for (int x : r)
+      if (st_[x].type == NState::SET && g_.sets[st_[x].set].test(y)) moved.push_back(st_[x].out);
+    if (moved.empty()) return {};
+    return closure(moved, kind(y), false, -1);
   }
 };
 
 }  // namespace
 
-bool regex_syntax_ok(const std::string& re, std::string* errmsg) {
-  try {
-    std::vector<Ast> nodes;
-    Parser(re, nodes).parse();
-    return true;
-  } catch (const Error& e) {
-    if (errmsg) *errmsg = e.msg;
-    return false;
-  }
+namespace rx {
+
+Decoder identity_decoder() {
+  Decoder d;
+  d.nstates = 1;
+  d.next.assign(256, 0);
+  d.nemit.assign(256, 1);
+  d.emit.assign(256 * 4, 0);
+  for (int b = 0; b < 256; ++b) d.emit[(size_t)b * 4] = (uint16_t)b;
+  d.pending.assign(1, 0);
+  return d;
 }
 
-ByteDfa compile_regex(const std::string& re, const ByteSet& alphabet, MatchMode mode,
-                      int max_states) {
-  std::vector<Ast> nodes;
-  int root = Parser(re, nodes, mode == MatchMode::Search).parse();
-  NfaBuilder b(nodes);
-  NfaBuilder::Frag f = b.build(root);
-  int match = b.add(NState::MATCH);
+ByteDfa build_dfa(Prog g, const Decoder& dec, const ByteSet& alphabet, bool search, int max_states) {
+  // one extra symbol set: every symbol (search's surrounding loops)
+  SymSet all(g.nsym);
+  for (int y = 0; y < g.nsym; ++y) all.set(y);
+  g.sets.push_back(all);
+  const int all_id = (int)g.sets.size() - 1;
+  NfaBuilder b(g);
+  NfaBuilder::Frag f = b.build(g.root);
+  const int match = b.add(NState::MATCH);
   int start = f.in;
-  if (mode == MatchMode::Search) {
-    // (any byte)* re (any byte)*  — a '^' inside re still only matches at
-    // offset 0 (closure follows BOL edges only in the start set).
+  if (search) {
+    // (any symbol)* re (any symbol)* — a begin assertion inside re still
+    // holds only at offset 0 (the previous kind is kStart only there)
     int pre = b.add(NState::SPLIT);
     int pre_set = b.add(NState::SET);
-    b.st[pre_set].set = ByteSet::all();
+    b.st[pre_set].set = all_id;
     b.st[pre_set].out = pre;
     b.st[pre].out = pre_set;
     b.st[pre].out1 = f.in;
     int post = b.add(NState::SPLIT);
     int post_set = b.add(NState::SET);
-    b.st[post_set].set = ByteSet::all();
+    b.st[post_set].set = all_id;
     b.st[post_set].out = post;
     b.st[post].out = post_set;
     b.st[post].out1 = match;
@@ -670,9 +850,37 @@ ByteDfa compile_regex(const std::string& re, const ByteSet& alphabet, MatchMode 
   } else {
     b.st[f.out].out = match;
   }
-  Subset sub(b.st, start, alphabet);
-  ByteDfa d = sub.run(max_states);
-  return dfa_minimize(d);
+  Subset sub(b.st, g, dec, alphabet);
+  return dfa_minimize(sub.run(start, max_states));
+}
+
+}  // namespace rx
+
+bool regex_syntax_ok(const std::string& re, std::string* errmsg, RegexFlavour flavour) {
+  try {
+    if (flavour == RegexFlavour::Go) {
+      rx::go_syntax_check(re);
+    } else {
+      rx::Prog g;
+      EcmaParser(re, g).parse();
+    }
+    return true;
+  } catch (const Error& e) {
+    if (errmsg) *errmsg = e.msg;
+    return false;
+  }
+}
+
+ByteDfa compile_regex(const std::string& re, const ByteSet& alphabet, MatchMode mode, int max_states) {
+  rx::Prog g;
+  rx::Decoder dec;
+  if (mode == MatchMode::Search) {
+    rx::go_compile(re, &g, &dec);
+  } else {
+    ecma_compile(re, &g);
+    dec = rx::identity_decoder();
+  }
+  return rx::build_dfa(g, dec, alphabet, mode == MatchMode::Search, max_states);
 }
 
 ByteDfa dfa_literal(const std::string& s, const ByteSet& alphabet) {

@@ -1,19 +1,26 @@
 // regex.h — regex → minimized byte DFA compiler (host side).
 //
-// Semantics follow what the reference enforces for HTTP header matchers:
-// Envoy's HeaderUtility::matchHeaders with `regex_match`, i.e. a std::regex
-// (ECMAScript grammar, libstdc++, char = signed byte) applied with
-// std::regex_match — a FULL-string match (envoy/cilium_network_policy.h:68-71,
-// Envoy pinned at f936fc60 in envoy/WORKSPACE:10-16).  Go's regexp is only
-// used by the agent to validate Path/Method (pkg/policy/api/http.go:66-84).
-// An unanchored "search" mode serves proxylib parsers, which call Go
-// regexp.MatchString (proxylib/r2d2/r2d2parser.go:80).
+// Two flavours, each with the semantics of the engine the reference runs:
 //
-// Supported subset: literals, escapes (\d\D\w\W\s\S \f\n\r\t\v \0 \xHH
-// \uHHHH≤0xFF \cX, identity escapes), '.', bracket classes with ranges and
-// negation, groups (...) and (?:...), alternation, quantifiers * + ? {n}
-// {n,} {n,m} (greedy or lazy — the same language), anchors ^ $.
-// Rejected with CG_UNSUPPORTED: backreferences, lookaround, \b \B.
+// * Full match (MatchMode::Full): Envoy's HeaderUtility::matchHeaders with
+//   `regex_match`, i.e. a std::regex (ECMAScript grammar, libstdc++, char =
+//   signed byte, "C" locale) applied with std::regex_match — a FULL-string
+//   match (envoy/cilium_network_policy.h:68-71, Envoy pinned at f936fc60 in
+//   envoy/WORKSPACE:10-16).  Supported: literals, escapes (\d\D\w\W\s\S
+//   \f\n\r\t\v \0 \xHH \uHHHH (low byte, as assigned to a char) \cX,
+//   identity escapes), '.', bracket expressions with ranges, negation,
+//   [:class:], [.collating-element.] and [=equivalence-class=], groups
+//   (...) (?:...), alternation, quantifiers * + ? {n} {n,} {n,m} (greedy or
+//   lazy: the same language), anchors ^ $ and word boundaries \b \B.
+//   Rejected with CG_UNSUPPORTED (std::regex accepts them, a DFA cannot
+//   express them): backreferences and lookahead.
+//
+// * Search (MatchMode::Search): Go 1.10 regexp.MatchString, as proxylib's
+//   parsers call it (proxylib/r2d2/r2d2parser.go:80,103,
+//   cassandra/cassandraparser.go:89,113, memcached/parser.go:91,132) —
+//   RE2 syntax with the Perl flags (regexp/syntax), matched over UTF-8
+//   runes where each invalid byte is one U+FFFD rune (regex_go.cc).
+//   Every Go-valid pattern compiles, within the NFA/DFA size budgets.
 #pragma once
 
 #include <cstdint>
@@ -96,7 +103,9 @@ ByteDfa dfa_minimize(const ByteDfa& d);
 // Simulate (tests/diagnostics only).
 bool dfa_run(const ByteDfa& d, const std::string& s);
 
-// Parse-only check (used by PortRuleHTTP sanitize mirror).
-bool regex_syntax_ok(const std::string& re, std::string* err);
+// Parse-only check: Ecma = std::regex's grammar (what Envoy compiles), Go =
+// regexp.Compile's (PortRuleHTTP.Sanitize, pkg/policy/api/http.go:66-84).
+enum class RegexFlavour { Ecma, Go };
+bool regex_syntax_ok(const std::string& re, std::string* err, RegexFlavour flavour = RegexFlavour::Ecma);
 
 }  // namespace cg

@@ -35,13 +35,15 @@ class PortRuleHTTP:
 
     def sanitize(self) -> None:
         """PortRuleHTTP.Sanitize (http.go:66-84): Path and Method must compile
-        as Go regexps; Host and Headers are not validated.  Go RE2 syntax is
-        approximated with Python's ``re`` (both reject e.g. a leading '*')."""
+        as Go regexps (regexp.Compile: Go 1.10 regexp/syntax, checked by the
+        engine's Go front end, cg_regex_validate); Host and Headers are not
+        validated."""
+        from . import _native as N
         for what, v in (("path", self.Path), ("method", self.Method)):
             if v:
                 try:
-                    re.compile(v)
-                except re.error as e:
+                    N.regex_validate(v, N.CG_REGEX_GO)
+                except N.CiliumGPUError as e:
                     raise PolicyValidationError(f"invalid {what} regexp {v!r}: {e}") from e
 
     def to_json(self) -> dict:
@@ -106,7 +108,9 @@ KAFKA_API_KEY_MAP = {
     "deleteacls": 31, "describeconfigs": 32, "alterconfigs": 33,
 }
 KAFKA_MAX_TOPIC_LEN = 255
-_KAFKA_TOPIC_VALID = re.compile(r"^[a-zA-Z0-9\\._\\-]+$")  # api/kafka.go:244 (Go raw string)
+# api/kafka.go:244, the Go raw string `^[a-zA-Z0-9\\._\\-]+$`; Go's '$' is the
+# end of text (Python's would also take a final "\n"), hence \Z
+_KAFKA_TOPIC_VALID = re.compile(r"^[a-zA-Z0-9\\._\\-]+\Z")
 
 
 @dataclass
@@ -263,12 +267,3 @@ def matcher_kind(m: dict) -> tuple[str, str]:
             rx = rx.get("value", False)
         return ("R" if rx else "E") + inv, v
     return "P" + inv, ""
-    if "value" in m:
-        v = m["value"]
-        if not v:
-            return "P", ""
-        rx = m.get("regex", False)
-        if isinstance(rx, dict):
-            rx = rx.get("value", False)
-        return ("R" if rx else "E"), v
-    return "P", ""

@@ -500,23 +500,28 @@ def parse_l4_proto(p: str) -> str:
 
 
 def parse_port(port: str) -> int:
-    """strconv.ParseUint(port, 0, 16): decimal, 0x hex, 0 octal, 0b binary."""
-    s = port
-    try:
-        if s.startswith(("0x", "0X")):
-            v = int(s[2:], 16)
-        elif s.startswith(("0b", "0B")):
-            v = int(s[2:], 2)
-        elif s.startswith(("0o", "0O")):
-            v = int(s[2:], 8)
-        elif len(s) > 1 and s.startswith("0"):
-            v = int(s[1:], 8)
-        else:
-            v = int(s, 10)
-    except ValueError as e:
-        raise ValueError(f"Unable to parse port: {port!r}") from e
-    if not s or not s[-1].isalnum() or v > 0xFFFF or v < 0:
+    """strconv.ParseUint(port, 0, 16) as Go 1.10 has it: base 0 reads a
+    "0x"/"0X" prefix as hex and a leading "0" as octal, else decimal; every
+    remaining byte must be a digit of that base (no sign, space or '_'; the
+    0b / 0o prefixes came in Go 1.13); the value must fit 16 bits."""
+    s, base = port, 10
+    if s[:1] == "0" and len(s) > 1 and s[1] in "xX":
+        if len(s) < 3:
+            raise ValueError(f"Unable to parse port: {port!r}")
+        s, base = s[2:], 16
+    elif s[:1] == "0":
+        s, base = s[1:], 8
+    if not port:
         raise ValueError(f"Unable to parse port: {port!r}")
+    v = 0
+    for c in s:
+        o = ord(c)
+        d = o - 48 if 48 <= o <= 57 else o - 87 if 97 <= o <= 122 else o - 55 if 65 <= o <= 90 else 99
+        if d >= base:
+            raise ValueError(f"Unable to parse port: {port!r}")
+        v = v * base + d
+        if v > 0xFFFF:
+            raise ValueError(f"Unable to parse port: {port!r}")
     return v
 
 

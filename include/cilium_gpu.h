@@ -622,11 +622,20 @@ int cg_reset_counters(uint64_t h);
 /* Synchronize the handle's stream. */
 int cg_sync(uint64_t h);
 
+/* Regex syntax check, no compilation: flavour CG_REGEX_GO = Go 1.10
+ * regexp.Compile's grammar (PortRuleHTTP.Sanitize,
+ * pkg/policy/api/http.go:66-84; proxylib's regexp.MustCompile,
+ * proxylib/r2d2/r2d2parser.go:103), CG_REGEX_ECMA = std::regex's (what
+ * Envoy compiles for regex_match, envoy/cilium_network_policy.h:68-71).
+ * Returns CG_OK or CG_POLICY_REJECTED (message in cg_last_error). */
+enum { CG_REGEX_ECMA = 0, CG_REGEX_GO = 1 };
+int cg_regex_validate(const char* re, size_t re_len, uint32_t flavour);
+
 /* ======================================================================== */
 /* Diagnostics (CPU test-suite only; no verdict entry point calls these)    */
 /* ======================================================================== */
 /* Compile `re` with the engine's regex compiler and run the DFA on s
- * (search = 0: full match as std::regex_match; 1: unanchored). */
+ * (search = 0: std::regex_match, ECMAScript; 1: Go regexp.MatchString). */
 int cg_diag_regex_match(const char* re, size_t re_len, const uint8_t* s, size_t len,
                         uint32_t search, uint8_t* result);
 /* Walk the compiled HTTP / Kafka tables on the host, exactly as the kernels

@@ -84,9 +84,9 @@ class Rule:
                 found = v in OPCODES
                 self.commands = OPCODES.get(v, (frozenset(), frozenset()))
             elif k == "keyExact":
-                self.key_exact = v.encode("latin-1")
+                self.key_exact = v.encode("utf-8", "surrogateescape")
             elif k == "keyPrefix":
-                self.key_prefix = v.encode("latin-1")
+                self.key_prefix = v.encode("utf-8", "surrogateescape")
             elif k == "keyRegex":
                 self.regex = go_regexp(v)
             else:

@@ -12,34 +12,43 @@ the way the Go code does:
   r2d2Rule.Matches / ruleParser  proxylib/r2d2/r2d2parser.go:61-123
   CassandraRule.Matches / parser proxylib/cassandra/cassandraparser.go:40-131
 
-Go ``regexp.MatchString`` is restated with Python ``re.search`` on
-printable-ASCII inputs with the RE2/ECMAScript/Python common syntax subset
-(SURVEY §8(c)); pure-Python loops, so it is sized for small cases.
+Go ``regexp.MustCompile`` + ``MatchString`` is oracle/go_regexp_ref.py
+(Go 1.10 regexp/syntax restated; inputs stepped as utf8.DecodeRune steps,
+an invalid byte being one U+FFFD).  Rule strings arrive as JSON text (Go
+strings: UTF-8); request fields as bytes, passed here latin-1 decoded.
+Pure-Python loops, so it is sized for small cases.
 """
 from __future__ import annotations
 
-import re
+from .go_regexp_ref import GoRegexp, GoSyntaxError
 
 
 class ParseError(ValueError):
     pass
 
 
-def go_regexp(pattern: str):
-    """Go regexp (RE2 syntax) as a Python pattern over latin-1 decoded bytes:
-    ASCII-only \\d \\w, '.' without the s flag excludes only '\\n' (as in
-    Python), and RE2's \\s is [\\t\\n\\f\\r ] (no \\v, unlike Python)."""
-    out, i = [], 0
-    while i < len(pattern):
-        c = pattern[i]
-        if c == "\\" and i + 1 < len(pattern):
-            nx = pattern[i + 1]
-            out.append({"s": "[\\t\\n\\f\\r ]", "S": "[^\\t\\n\\f\\r ]"}.get(nx, c + nx))
-            i += 2
-            continue
-        out.append(c)
-        i += 1
-    return re.compile("".join(out), re.ASCII)
+class _GoSearch:
+    """regexp.MustCompile(pattern) (a syntax error panics: ParseError);
+    search(s) = MatchString on the bytes s holds (latin-1 decoded)."""
+
+    def __init__(self, pattern: str):
+        try:
+            self.re = GoRegexp(pattern.encode("utf-8", "surrogateescape"))
+        except GoSyntaxError as e:
+            raise ParseError("regexp: " + str(e)) from e
+
+    def search(self, s: str) -> bool:
+        return self.re.match_string(s.encode("latin-1"))
+
+
+def go_regexp(pattern: str) -> _GoSearch:
+    return _GoSearch(pattern)
+
+
+def _b(s: str) -> str:
+    """A rule string (UTF-8 in Go) as the latin-1 text of its bytes, so it
+    compares byte for byte with request fields."""
+    return s.encode("utf-8", "surrogateescape").decode("latin-1")
 
 
 class _R2d2Rule:
@@ -47,7 +56,7 @@ class _R2d2Rule:
         self.cmd, self.file_re = "", None
         for k, v in rule.items():
             if k == "cmd":
-                self.cmd = v
+                self.cmd = _b(v)
             elif k == "file":
                 if v != "":
                     self.file_re = go_regexp(v)
@@ -83,7 +92,7 @@ class _CassandraRule:
         self.action, self.table_re = "", None
         for k, v in rule.items():
             if k == "query_action":
-                self.action = v
+                self.action = _b(v)
             elif k == "query_table":
                 if v != "":
                     self.table_re = go_regexp(v)

@@ -650,11 +650,64 @@ def policies_e2e_kats() -> dict:
             ]}
 
 
+
+# ---------------------------------------------------------- Go regexp KATs --
+def go_regex_kats() -> dict:
+    """Go 1.10 regexp (RE2 syntax, Perl flags) known answers for the proxylib
+    rule regexes (r2d2parser.go:80,103, cassandraparser.go:89,113,
+    memcached/parser.go:91,132) and Sanitize (pkg/policy/api/http.go:66-84).
+    Go's regexp is not vendored in the reference; the syntax lists restate
+    regexp/syntax/parse_test.go's published invalidRegexps / onlyPerl /
+    onlyPOSIX lists (the Go 1.10 entries), the match cases Go's documented
+    behaviour (package regexp/syntax doc: ASCII \\b \\d \\s \\w, \\z, flags;
+    utf8.DecodeRune: an invalid byte is one U+FFFD rune; unicode.SimpleFold
+    orbits for (?i)).  Inputs are hex."""
+    invalid = [  # parse_test.go invalidRegexps (Go 1.10) + onlyPOSIX in Perl mode + Perl-only refusals
+        "(", ")", "(a", "a)", "(a))", "(a|b|", "a|b|)", "(a|b|))", "(a|b", "a|b)", "(a|b))", "[a-z", "([a-z)",
+        "[a-z)", "([a-z]))", "x{1001}", "x{9876543210}", "x{2,1}", "x{1,9876543210}", "\udcff",  # = the byte 0xff (invalid UTF-8) under surrogateescape
+        "(?P<name>a", "(?P<name>", "(?P<name", "(?P<x y>a)", "(?P<>a)", "[a-Z]", "(?i)[a-Z]", "a{100000}",
+        "a{100000,}", "a++", "a**", "a?*", "a+*", "a{1}*", ".{1}{2}.{3}",
+        "(?=a)", "(?!a)", "(?<=a)", "(?<!a)", "\\1", "a\\1", "\\8", "\\C", "(?P=n)", "(?<n>a)", "\\Z", "[\\b]",
+        "\\pX", "\\p{Foo}", "\\p{", "[[:foo:]]", "\\x{110000}", "\\x{}", "\\xg0", "\\", "a\\", "*", "+a",
+        "a|*", "(*)", "(?i-)", "(?-)", "(?i", "(?z)", "\\e", "\\cA", "\\u0041", "[\\z]", "(?i)(?P<n>x"]
+    valid = [  # onlyPerl + Perl-mode constructs
+        "[a-b-c]", "\\Qabc\\E", "\\Q*+?{[\\E", "\\Q\\\\E", "\\Q\\\\\\E", "\\Q\\\\\\\\E", "\\Q\\\\\\\\\\E",
+        "(?:a)", "(?P<name>a)", "(?i)abc", "(?i:a)b", "(?s).", "(?m)^a$", "(?U)a+", "(?is-m:x)", "(?)", "a{,2}",
+        "x{1000}", "x{0,1000}", "x{2}{", "\\_", "[]a]", "[^]a]", "^*", "\\b+", "$?", "\\pL", "\\p{Greek}", "\\PN",
+        "\\p{^Lu}", "\\P{^Lu}", "\\p{Any}", "\\x{10FFFF}", "\\x41", "\\101", "\\0", "\\z", "\\A",
+        "[[:alpha:]]", "[[:^space:]x]", "[[:alpha]", "[\\d-z]", "\\a\\f\\t\\n\\r\\v", "é+", "[é-ú]", "(?i)ǅ",
+        "a||b", "()", "(|a)", "\\.\\*\\-\\ "]
+    H = lambda s: (s.encode() if isinstance(s, str) else s).hex()  # noqa: E731
+    matches = [
+        ("(?i)k", "\u212a", True), ("(?i)s", "\u017f", True), ("k", "K", False), ("(?i)K", "k", True),
+        ("(?i)[^k]", "\u212a", False), ("(?i)\\W", "\u212a", False), ("(?i)ǅ", "ǆ", True), ("(?i)µ", "Μ", True),
+        ("(?i)\\p{Lu}", "a", True), ("\\p{Lu}", "a", False), ("(?i)[[:lower:]]", "\u212a", True),
+        (".", b"\xff", True), ("^.$", "€", True), ("^...$", "€", False), ("^.$", b"\xe2\x82", False),
+        ("^..$", b"\xe2\x82", True), ("^..$", b"\xe2\x82a", False), ("^...$", b"\xe2\x82a", True),
+        ("^.$", b"\xed\xa0\x80", False), ("^...$", b"\xed\xa0\x80", True), ("^[^a]$", b"\xc0", True),
+        ("[^a]", "\n", True), (".", "\n", False), ("(?s).", "\n", True), ("\\s", "\v", False),
+        ("[[:space:]]", "\v", True), ("\\bfoo\\b", "a foo.", True), ("\\bfoo\\b", "afoo", False),
+        ("\\Bfoo", "afoo", True), ("\\b", "é", False), ("\\B", "", True), ("^b$", "a\nb", False),
+        ("(?m)^b$", "a\nb", True), ("a$", "a\n", False), ("a\\z", "a", True), ("(?m)a$", "a\nb", True),
+        ("\\pL", "é", True), ("\\pL", "1", False), ("\\p{Greek}", "α", True), ("\\p{Han}", "中", True),
+        ("\\PL", "中", False), ("\\pN", "٣", True), ("\\d", "٣", False), ("\\Qa.b\\E", "axb", False),
+        ("\\Qa.b\\E", "a.b", True), ("a{,2}", "a{,2}", True), ("a{,2}", "aa", False), ("\\x{e9}", "é", True),
+        ("[é-ú]", "ó", True), ("^é+$", "éé", True), ("^é+$", b"\xc3\xa9\xc3", False), ("\\101", "A", True),
+        ("(?i)(?-i:a)A", "aa", True), ("(?i)(?-i:a)A", "Aa", False), ("a(?i)b|c", "C", True), ("(a(?i)b)c", "aBC", False),
+        ("[[:word:]]", "_", True), ("(?U)a+?", "a", True), ("^(?:ab|a)c$", "abc", True), ("\\p{Greek}", "µ", False),
+        ("(?i)\\p{Greek}", "µ", True), ("\\x{FFFD}x", b"\xefx", None)]
+    return {"source": "Go 1.10 regexp/syntax (parse_test.go lists, package documentation); see the docstring of "
+                      "tests/golden/make_golden.py:go_regex_kats",
+            "invalid": invalid, "valid": valid,
+            "matches": [{"pattern": p, "input": H(s), "match": m} for p, s, m in matches]}
+
+
 def main():
     files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
              "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
              "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
-             "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats()}
+             "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
+             "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
         if only and name not in only:

@@ -221,10 +221,19 @@ def test_pb_utf8_rule():
     cl.close()
     from test_proxylib_abi import _lib, open_module
     inst = open_module([(b"node-id", b"cpu-npds-utf8")], "-1")
+    # a memcache keyExact is []byte(v): the non-UTF-8 string installs
+    # (memcached/parser.go:125-130) ...
     pl = [{"name": "p", "ingress_per_port_policies": [{"port": 80, "rules": [
-        {"l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"cmd": "READ", "file": "\xff"}}]}}]}]}]
+        {"l7_proto": "memcache", "l7_rules": {"l7_rules": [{"rule": {"command": "get", "keyExact": "\xff"}}]}}]}]}]
     blob = PB.discovery_response(pl)
     assert N.lib.cg_proxylib_policy_update_npds(inst, blob, len(blob)) == N.CG_OK
+    # ... while an r2d2 file regex goes through regexp.MustCompile, which
+    # refuses invalid UTF-8: the rule parser panics and the update fails
+    # (r2d2parser.go:103, instance.go:169-176)
+    pl[0]["ingress_per_port_policies"][0]["rules"][0] = {
+        "l7_proto": "r2d2", "l7_rules": {"l7_rules": [{"rule": {"cmd": "READ", "file": "\xff"}}]}}
+    blob = PB.discovery_response(pl)
+    assert N.lib.cg_proxylib_policy_update_npds(inst, blob, len(blob)) == N.CG_POLICY_REJECTED
     _lib.CloseModule(inst)
 
 
