@@ -751,8 +751,13 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   const size_t lds = ((size_t)t.lds_cells + kLdsRuleHits + 3) * 4;
   int occ = 1;
   uint32_t* deal = nullptr;
+  // The ticket reset and both launches are enqueued under one lock: two
+  // host threads sharing a stream must not interleave as memset A, memset
+  // B, kernel A, kernel B (B would start from A's spent ticket count and
+  // write no verdicts).
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
   {
-    static std::mutex mu;
     static std::map<std::pair<int, size_t>, int> occ_cache;
     static std::set<int> attr_set;
     // one ticket word per (device, stream), zeroed on the launch stream
@@ -760,7 +765,6 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
     // starts from ticket 0 and no two launches in flight share a counter
     // (launches on different streams hold different words)
     static std::map<std::pair<int, void*>, uint32_t*> deal_words;
-    std::lock_guard<std::mutex> lk(mu);
     if (kDynamicDeal) {
       auto& w = deal_words[{dev, stream}];
       if (!w) {

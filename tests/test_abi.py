@@ -11,6 +11,8 @@ import pytest
 from cilium_amd import _native as N
 from cilium_amd import synth
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "cilium_gpu.h")
 
 
@@ -96,3 +98,46 @@ def test_stale_batch_rejected(host):
     host.update_http_policy(synth.starwars_policy())  # new snapshot
     with pytest.raises(N.CiliumGPUError):
         host.http_eval_host_diag(b)
+
+
+def test_c_abi_harness(tmp_path):
+    """tests/native/abi_harness.c: gcc (C11, -Werror) against
+    include/cilium_gpu.h, linked to libciliumgpu.so — static_asserts on the
+    BPF-map and record layouts, then the control-plane calls and the host
+    table walks on a device = -1 handle (verdict calls: CG_NO_DEVICE)."""
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no gcc")
+    lib = os.path.join(ROOT, "cilium_amd")
+    exe = str(tmp_path / "abi_harness")
+    subprocess.run([gcc, "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "abi_harness.c"), "-o", exe, "-L", lib, "-lciliumgpu",
+                    "-Wl,-rpath," + lib], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout
+
+
+def test_go_binding_names_exist_in_header():
+    """go/gpuclassifier (the cgo package; no Go toolchain in this image):
+    every C identifier it references is declared by include/cilium_gpu.h (or
+    is a cgo builtin), and each struct field it names is a field of that
+    struct in the header."""
+    import glob
+    hdr = open(os.path.join(ROOT, "include", "cilium_gpu.h")).read()
+    builtin = {"CString", "GoString", "free", "CBytes", "size_t", "int", "char", "uint8_t", "uint16_t",
+               "uint32_t", "uint64_t", "int16_t", "int32_t", "int64_t"}
+    names = set()
+    for f in glob.glob(os.path.join(ROOT, "go", "gpuclassifier", "*.go")):
+        src = open(f).read()
+        names |= set(re.findall(r"\bC\.([A-Za-z_][A-Za-z0-9_]*)", src))
+        for struct, body in re.findall(r"C\.(cg_[a-z_0-9]+)\{([^}]*)\}", src):
+            m = re.search(r"typedef struct \{([^}]*)\}\s*" + struct + ";", hdr)
+            assert m, struct
+            for field in re.findall(r"(\w+):", body):
+                assert re.search(r"\b" + field + r"\b", m.group(1)), (struct, field)
+    missing = [n for n in sorted(names) if n not in builtin and not re.search(r"\b" + n + r"\b", hdr)]
+    assert not missing, missing
+    assert len(names) > 40

@@ -169,3 +169,61 @@ def test_http_policy_image_roundtrip():
     assert np.array_equal(b.http_eval_host_diag(b.pack_http(**rq)), va)
     a.close()
     b.close()
+
+
+def _fnv64(b: bytes) -> int:
+    h = 1469598103934665603
+    for x in b:
+        h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def _reseal(body: bytes) -> bytes:
+    """An image body with a valid trailing FNV-64 (http_image.cc): FNV is no
+    MAC, so the structural checks are what stands between a crafted image and
+    the kernels."""
+    return body + _fnv64(body).to_bytes(8, "little")
+
+
+def test_http_policy_image_structural_corruption():
+    """Images whose checksum is recomputed after damaging a word: every one is
+    either rejected (CG_POLICY_REJECTED, the previous snapshot serving) or
+    imported and then walked by the host verdict path without reading outside
+    its tables (the walker runs under the ASan build in tools/sanitize)."""
+    import numpy as np
+
+    from cilium_amd import _native as N
+    from cilium_amd import synth
+    from cilium_amd.classifier import Classifier
+    a, b = Classifier(device=-1), Classifier(device=-1)
+    a.update_http_policy(synth.starwars_policy())
+    img = a.export_http_policy()
+    rq = synth.starwars_requests(300, seed=4)
+    good = a.http_eval_host_diag(a.pack_http(**rq))
+    body = bytearray(img[:-8])
+    rng = np.random.default_rng(7)
+    rejected = accepted = 0
+    for k in range(600):
+        bad = bytearray(body)
+        for _ in range(int(rng.integers(1, 3))):
+            i = int(rng.integers(8, len(bad) - 4)) & ~3  # a word past magic and version
+            v = int.from_bytes(bad[i:i + 4], "little")
+            v = [v ^ (1 << int(rng.integers(0, 32))), 0xFFFFFFFF, 0, v + 1, v + 0x10000, int(rng.integers(0, 2**32))][
+                int(rng.integers(0, 6))] & 0xFFFFFFFF
+            bad[i:i + 4] = v.to_bytes(4, "little")
+        blob = _reseal(bytes(bad))
+        rc = N.lib.cg_http_policy_import(b.h, blob, len(blob))
+        if rc == N.CG_OK:
+            accepted += 1
+            try:
+                b.http_eval_host_diag(b.pack_http(**rq))
+            except N.CiliumGPUError:
+                pass
+        else:
+            assert rc == N.CG_POLICY_REJECTED
+            rejected += 1
+    assert rejected > 100 and accepted > 50, (rejected, accepted)
+    b.import_http_policy(img)
+    assert np.array_equal(b.http_eval_host_diag(b.pack_http(**rq)), good)
+    a.close()
+    b.close()

@@ -55,6 +55,47 @@ def test_http_deal_many_launches_two_streams(gpu):
     assert not bad, f"launches with wrong verdicts: {bad[:10]}"
 
 
+def test_http_deal_two_threads_one_stream(gpu):
+    """Two host threads issue cg_http_verdicts_dev on one shared stream: the
+    ticket reset and its launch are enqueued under one lock, so no launch
+    starts from another's spent ticket (every output checked)."""
+    torch = _torch()
+    pols = synth.starwars_policy()
+    gpu.update_http_policy(pols)
+    rq = synth.starwars_requests(20_000, seed=78)
+    b = gpu.pack_http(**rq)
+    exp = oracle.HttpOracle(pols).eval(**rq)
+    slot_exp = np.zeros(b.nslots, np.uint8)
+    real = b.order < b.n
+    slot_exp[real] = exp[b.order[real]]
+    dev = torch.device("cuda", 0)
+    d_batch = torch.from_numpy(b.batch.view(np.uint8)).to(dev)
+    d_arena = torch.from_numpy(np.concatenate([b.arena.view(np.uint8), np.zeros(16, np.uint8)])).to(dev)
+    per_thread = 200
+    outs = torch.full((2, per_thread, b.nslots), 7, dtype=torch.uint8, device=dev)
+    shared = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    errors = []
+
+    def issue(k):
+        try:
+            for j in range(per_thread):
+                gpu.http_verdicts_dev(d_batch, b.nslots, d_arena, outs[k, j], stream=shared.cuda_stream)
+        except Exception as e:  # noqa: BLE001 — surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=issue, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    want = torch.from_numpy(slot_exp).to(dev)
+    bad = (outs.view(2 * per_thread, -1) != want.unsqueeze(0)).any(dim=1).nonzero().flatten().tolist()
+    assert not bad, f"launches with wrong verdicts: {bad[:10]}"
+
+
 def test_l4_tables_retired_after_queued_launches(gpu):
     """Queue several big L4 launches on a caller stream, then replace and
     rebuild the map's tables before they run: the queued launches still see

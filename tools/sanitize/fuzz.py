@@ -78,13 +78,29 @@ def fuzz_json(rng, iters):
     cl.close()
 
 
+def _fnv64(b: bytes) -> int:
+    h = 1469598103934665603
+    for x in b:
+        h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
 def fuzz_image(rng, iters):
+    """Mutated images with the trailing FNV-64 recomputed (a checksum is no
+    MAC), so the structural checks are exercised; every accepted image is
+    walked by the host verdict path."""
     cl = Classifier(device=-1)
     cl.update_http_policy(synth.starwars_policy())
     img = cl.export_http_policy()
+    rq = synth.starwars_requests(64, seed=9)
     for _ in range(iters):
-        blob = mutate(img, rng)
-        N.lib.cg_http_policy_import(cl.h, blob, len(blob))
+        body = mutate(img[:-8], rng)
+        blob = body + _fnv64(body).to_bytes(8, "little")
+        if N.lib.cg_http_policy_import(cl.h, blob, len(blob)) == N.CG_OK:
+            try:
+                cl.http_eval_host_diag(cl.pack_http(**rq))
+            except N.CiliumGPUError:
+                pass
     cl.close()
 
 
