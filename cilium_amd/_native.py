@@ -140,6 +140,8 @@ SIGNATURES = {
     "cg_http_parse_heads": (C.c_int, [_p, _p, _sz, _p, _sz, _p, C.POINTER(_sz), _p]),
     "cg_http_verdicts_dev": (C.c_int, [_u64, _p, _sz, _p, _p, _p]),
     "cg_http_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p]),
+    "cg_http_verdicts_rules_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p, _sz, _p, _p]),
+    "cg_http_verdicts_rules_dev": (C.c_int, [_u64, _p, _sz, _p, _p, _p, _p]),
     "cg_http_verdicts_raw_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p, _p]),
     "cg_http_verdicts_raw_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p]),
     "cg_http_verdicts_fields_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p, _p]),

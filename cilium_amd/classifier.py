@@ -242,6 +242,20 @@ class Classifier:
         """Enqueue the verdict kernel on device buffers; d_out is in slot order."""
         N.check(N.lib.cg_http_verdicts_dev(self.h, _p(d_batch), nslots, _p(d_arena), _p(d_out), stream))
 
+    def http_verdicts_rules(self, b: "HttpBatch") -> tuple[np.ndarray, np.ndarray]:
+        """Verdicts and, per request, the first matching rule's counter
+        index (http_rule_info order; 0xFFFFFFFF: no rule allows), on the GPU."""
+        out = np.zeros(max(b.n, 1), np.uint8)
+        rule = np.zeros(max(b.n, 1), np.uint32)
+        N.check(N.lib.cg_http_verdicts_rules_host(self.h, _p(b.batch), b.nslots, _p(b.order), b.n, _p(b.arena),
+                                                  b.arena.nbytes, _p(out), _p(rule)))
+        return out[:b.n], rule[:b.n]
+
+    def http_verdicts_rules_dev(self, d_batch, nslots: int, d_arena, d_out, d_rule, stream=None) -> None:
+        """http_verdicts_dev with the per-slot first-matching-rule output."""
+        N.check(N.lib.cg_http_verdicts_rules_dev(self.h, _p(d_batch), nslots, _p(d_arena), _p(d_out), _p(d_rule),
+                                                 stream))
+
     HTTP_RULE_INFO_DTYPE = np.dtype([("policy", "<u4"), ("ingress", "<u4"), ("port", "<u4"), ("scope", "<u4"),
                                      ("rule", "<u4"), ("http_rule", "<u4")])
 

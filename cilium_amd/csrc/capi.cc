@@ -922,6 +922,20 @@ int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const u
   });
 }
 
+int cg_http_verdicts_rules_dev(uint64_t h, const void* d_batch, size_t nslots, const uint8_t* d_arena, uint8_t* d_out,
+                               uint32_t* d_rule, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = http_snap(*e);
+    if (nslots && !d_rule) fail(CG_INVALID_ARGUMENT, "NULL rule array");
+    e->set_device();
+    check_launch(launch_http(s->dev, d_batch, nslots, d_arena, d_out, stream_of(*e, stream), e->cus, nullptr, d_rule),
+                 "http kernel launch");
+    s->fence.record(stream_of(*e, stream));
+  });
+}
+
 int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,
                              const uint32_t* d_policy, const uint8_t* d_ingress, const uint16_t* d_port,
                              const uint32_t* d_remote, uint8_t* d_out, void* stream) {
@@ -965,9 +979,25 @@ static void* stage_in(StagingSlot& sl, int i, const void* src, size_t bytes) {
   return d;
 }
 
+static void http_verdicts_host_impl(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
+                                    size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out, uint32_t* rule);
+
 int cg_http_verdicts_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order, size_t n,
                           const uint8_t* arena, size_t arena_len, uint8_t* out) {
+  return guarded([&] { http_verdicts_host_impl(h, batch, nslots, order, n, arena, arena_len, out, nullptr); });
+}
+
+int cg_http_verdicts_rules_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order, size_t n,
+                                const uint8_t* arena, size_t arena_len, uint8_t* out, uint32_t* rule) {
   return guarded([&] {
+    if (n && !rule) fail(CG_INVALID_ARGUMENT, "NULL rule array");
+    http_verdicts_host_impl(h, batch, nslots, order, n, arena, arena_len, out, rule);
+  });
+}
+
+static void http_verdicts_host_impl(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
+                                    size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out, uint32_t* rule) {
+  {
     auto e = get(h);
     e->require_gpu();
     auto s = http_snap(*e);
@@ -984,15 +1014,23 @@ int cg_http_verdicts_host(uint64_t h, const void* batch, size_t nslots, const ui
     void* dr = stage_in(*lease, 0, batch, batch_used_bytes(batch));
     void* da = stage_in(*lease, 1, arena, hdr.arena_bytes);
     void* dout = lease->dev_buf(2, nslots + 1);
-    check_launch(launch_http(s->dev, dr, nslots, (const uint8_t*)da, (uint8_t*)dout, lease->stream, e->cus),
+    uint32_t* drule = rule ? (uint32_t*)lease->dev_buf(3, (nslots + 1) * 4) : nullptr;
+    check_launch(launch_http(s->dev, dr, nslots, (const uint8_t*)da, (uint8_t*)dout, lease->stream, e->cus, nullptr,
+                             drule),
                  "http kernel launch");
     uint8_t* slots = (uint8_t*)lease->host_buf(2, nslots + 1);
+    uint32_t* rslots = rule ? (uint32_t*)lease->host_buf(3, (nslots + 1) * 4) : nullptr;
     if (nslots)
       hip_check(hipMemcpyAsync(slots, dout, nslots, hipMemcpyDeviceToHost, (hipStream_t)lease->stream), "D2H");
+    if (nslots && rule)
+      hip_check(hipMemcpyAsync(rslots, drule, nslots * 4, hipMemcpyDeviceToHost, (hipStream_t)lease->stream), "D2H");
     hip_check(hipStreamSynchronize((hipStream_t)lease->stream), "hipStreamSynchronize");
     for (size_t i = 0; i < nslots; ++i)
-      if (order[i] < n) out[order[i]] = slots[i];
-  });
+      if (order[i] < n) {
+        out[order[i]] = slots[i];
+        if (rule) rule[order[i]] = rslots[i];
+      }
+  }
 }
 
 // --------------------------------------------------------------- Kafka ----

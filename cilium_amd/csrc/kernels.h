@@ -20,8 +20,10 @@ int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* 
                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus);
 // order (optional): out[order[slot]] instead of out[slot] (request order;
 // order 0xFFFFFFFF = padding, no write) — the raw-request batches.
+// rule (optional): per slot (or order[slot]) the first matching rule's
+// counter index, 0xFFFFFFFF when no rule allows.
 int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
-                void* stream, int cus, const uint32_t* order = nullptr);
+                void* stream, int cus, const uint32_t* order = nullptr, uint32_t* rule = nullptr);
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus);
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,

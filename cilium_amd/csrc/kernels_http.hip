@@ -121,15 +121,25 @@ __device__ __forceinline__ uint32_t lds_cls_step16(uint32_t dead, uint32_t st, c
 // Where verdicts go: out[slot] (slot order), or — for a batch built on the
 // device from raw requests (kernels_http_raw.hip) — out[order[slot]]
 // (request order; padding slots, order 0xFFFFFFFF, write nothing).
+// With `rule` set (cg_http_verdicts_rules_*), the request's first matching
+// rule goes beside it: the per-rule counter index it adds to
+// (HttpProg.rule_base + hit, cg_http_rule_info order) or 0xFFFFFFFF when no
+// rule allows it — the access-log attribution of pkg/proxy/accesslog/
+// record.go:36-47 and the policy trace of pkg/policy/policy.go:29-70.
 struct VOut {
   uint8_t* __restrict__ out;
   const uint32_t* __restrict__ order;
-  __device__ __forceinline__ void put(size_t slot, uint32_t v) const {
+  uint32_t* __restrict__ rule;
+  __device__ __forceinline__ void put(size_t slot, uint32_t v, uint32_t r_idx = 0xFFFFFFFFu) const {
     if (order) {
       const uint32_t r = order[slot];
-      if (r != 0xFFFFFFFFu) out[r] = (uint8_t)v;
+      if (r != 0xFFFFFFFFu) {
+        out[r] = (uint8_t)v;
+        if (rule) rule[r] = r_idx;
+      }
     } else {
       out[slot] = (uint8_t)v;
+      if (rule) rule[slot] = r_idx;
     }
   }
 };
@@ -391,7 +401,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
     if (counted[j] && (pg.flags & kProgHasAlways)) hit[j] = min(hit[j], first_meet(blk, pg.always_off, row[j], W));
     const bool verdict = counted[j] && hit[j] != kNoHit;
     count_hits(T, pg, verdict ? hit[j] : kNoHit, s_hits, lane);
-    if (valid[j]) out.put((size_t)tile[j] * kWave + lane, verdict);
+    if (valid[j]) out.put((size_t)tile[j] * kWave + lane, verdict, verdict ? pg.rule_base + hit[j] : kNoHit);
     n_allow += counted[j] && verdict;
     n_deny += counted[j] && !verdict;
   }
@@ -515,7 +525,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   }
   const bool verdict = hit != kNoHit;
   count_hits(T, pg, hit, s_hits, lane);
-  out.put((size_t)t * kWave + lane, verdict);
+  out.put((size_t)t * kWave + lane, verdict, verdict ? pg.rule_base + hit : kNoHit);
   n_allow += counted && verdict;
   n_deny += counted && !verdict;
 }
@@ -715,7 +725,8 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
 
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
-    uint8_t* __restrict__ out, const uint32_t* __restrict__ order, uint32_t* __restrict__ deal) {
+    uint8_t* __restrict__ out, const uint32_t* __restrict__ order, uint32_t* __restrict__ deal,
+    uint32_t* __restrict__ rule) {
   // dynamic LDS only, so the program block starts at LDS address 0 (a
   // class-mode step's address is then just state + code): [block:
   // T.lds_cells][rule hits: kLdsRuleHits][allowed, denied, deal ticket]
@@ -725,23 +736,24 @@ __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8,
   for (uint32_t i = threadIdx.x; i < kLdsRuleHits; i += blockDim.x) s_hits[i] = 0;
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<false>(T, batch, nslots, arena, VOut{out, order}, lcells, s_cnt, s_hits, deal);
+  http_chunks<false>(T, batch, nslots, arena, VOut{out, order, rule}, lcells, s_cnt, s_hits, deal);
 }
 
 __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
                                                                    size_t nslots, const uint8_t* __restrict__ arena,
                                                                    uint8_t* __restrict__ out,
-                                                                   const uint32_t* __restrict__ order) {
+                                                                   const uint32_t* __restrict__ order,
+                                                                   uint32_t* __restrict__ rule) {
   __shared__ uint32_t s_cnt[3];
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<true>(T, batch, nslots, arena, VOut{out, order}, nullptr, s_cnt, nullptr, nullptr);
+  http_chunks<true>(T, batch, nslots, arena, VOut{out, order, rule}, nullptr, s_cnt, nullptr, nullptr);
 }
 
 }  // namespace
 
 int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_t* arena, uint8_t* out, void* stream,
-                int cus, const uint32_t* order) {
+                int cus, const uint32_t* order, uint32_t* rule) {
   if (nslots == 0) return 0;
   // hipFuncSetAttribute and the occupancy answer are per device: cached per
   // device ordinal, set once under a lock (handles on several GPUs may launch
@@ -798,11 +810,11 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   const size_t tiles = nslots / kWave;
   size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);
   hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
-                     (const uint8_t*)batch, nslots, arena, out, order, deal);
+                     (const uint8_t*)batch, nslots, arena, out, order, deal, rule);
   if (t.n_global_progs) {
     grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
     hipLaunchKernelGGL(http_kernel_global, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream, t,
-                       (const uint8_t*)batch, nslots, arena, out, order);
+                       (const uint8_t*)batch, nslots, arena, out, order, rule);
   }
   return (int)hipGetLastError();
 }

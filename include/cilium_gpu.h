@@ -502,6 +502,18 @@ int cg_http_verdicts_dev(uint64_t h, const void* d_batch, size_t nslots, const u
  * for request i (un-permuting through order). */
 int cg_http_verdicts_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
                           size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out);
+/* The same verdicts with each request's first matching rule beside it:
+ * d_rule[slot] = the per-rule counter index it adds to (cg_http_rule_info_get
+ * order: the PortNetworkPolicyRule / HTTP rule that allowed it, Envoy's
+ * evaluation order), or UINT32_MAX when no rule allows it (denied, or
+ * allowed because no HTTP policy applies).  Replaces the access log's rule
+ * attribution (pkg/proxy/accesslog/record.go:36-47) and the policy trace
+ * (pkg/policy/policy.go:29-70) for every request of a batch. */
+int cg_http_verdicts_rules_dev(uint64_t h, const void* d_batch, size_t nslots, const uint8_t* d_arena,
+                               uint8_t* d_out, uint32_t* d_rule, void* stream);
+int cg_http_verdicts_rules_host(uint64_t h, const void* batch, size_t nslots, const uint32_t* order,
+                                size_t n, const uint8_t* arena, size_t arena_len, uint8_t* out,
+                                uint32_t* rule);
 
 /* ======================================================================== */
 /* Kafka L7: pkg/kafka/policy.go:144-225 via pkg/proxy/kafka.go:117-153      */

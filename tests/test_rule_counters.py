@@ -128,3 +128,39 @@ def test_gpu_rule_counters_random(gpu, seed):
     v, _, counts = _oracle_counts(pols, rq, info)
     assert np.array_equal(got, v)
     assert np.array_equal(gpu.http_rule_hits(), counts)
+
+
+@pytest.mark.gpu
+def test_gpu_per_request_rule_attribution_10k(gpu):
+    """cg_http_verdicts_rules_*: every request's first matching rule from the
+    kernel equals the oracle's first-match attribution (or_http_eval_attr,
+    Envoy's evaluation order) and the host walker's (cg_diag_http_rules_host);
+    verdicts unchanged."""
+    pols, info10 = synth.http10k_rules()
+    rq = synth.http10k_requests(200_000, info10, seed=91, distinct=100_000)
+    gpu.update_http_policy(pols)
+    b = gpu.pack_http(**rq)
+    v, rule = gpu.http_verdicts_rules(b)
+    info = gpu.http_rule_info()
+    ov, per_req, _ = _oracle_counts(pols, rq, info, nthreads=16)
+    assert np.array_equal(v, ov)
+    assert np.array_equal(rule, per_req)
+    assert np.array_equal(rule, gpu.http_rules_host_diag(b))
+    assert 0.2 < (rule != 0xFFFFFFFF).mean() < 0.8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_per_request_rule_attribution_random(gpu, seed):
+    rng = random.Random(950 + seed)
+    pols = _rand_policy(rng)
+    rq = _rand_requests(rng, 3000, len(pols))
+    try:
+        oracle.HttpOracle(pols)
+    except ValueError:
+        return
+    gpu.update_http_policy(pols)
+    b = gpu.pack_http(**rq)
+    v, rule = gpu.http_verdicts_rules(b)
+    ov, per_req, _ = _oracle_counts(pols, rq, gpu.http_rule_info())
+    assert np.array_equal(v, ov) and np.array_equal(rule, per_req)

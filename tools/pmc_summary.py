@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--algo-bytes", type=float, default=0.0, help="algorithmic bytes per item")
     ap.add_argument("--out", default="")
     ap.add_argument("--last", type=int, default=0, help="only the last N dispatches of the kernel")
+    ap.add_argument("--workload", default="", help="what the profiled command ran (recorded in the summary)")
     a = ap.parse_args()
     per = collections.defaultdict(list)
     resources = {}
@@ -40,7 +41,7 @@ def main():
             per[c].append(v)
     avg = {c: sum(v) / len(v) for c, v in per.items()}
     out = {"kernel": a.kernel, "counters_per_dispatch": avg, "dispatches": {c: len(v) for c, v in per.items()},
-           "resources": resources}
+           "resources": resources, "workload": a.workload, "items_per_dispatch": a.items}
     if "FETCH_SIZE" in avg:
         fetch = avg["FETCH_SIZE"] * 1024 * 2  # KB → B, ×2 gfx950 streaming-read correction
         write = avg.get("WRITE_SIZE", 0.0) * 1024
