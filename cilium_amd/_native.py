@@ -119,6 +119,7 @@ SIGNATURES = {
     "cg_ipcache_dump": (C.c_int, [_u64, _u32, _p, _p, _sz, C.POINTER(_sz)]),
     "cg_ipcache_resolve_dev": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p, _p]),
     "cg_ipcache_resolve_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
+    "cg_proxylib_stats": (C.c_int, [_u64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "cg_proxylib_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_proxylib_policy_update_npds": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_l4_verdicts_ipcache_dev": (C.c_int, [_u64, _u32, _u32, _p, _p, _sz, _p, _p]),
@@ -150,6 +151,7 @@ SIGNATURES = {
     "cg_kafka_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_kafka_intern": (C.c_int, [_u64, _u32, C.c_char_p, _sz, C.POINTER(_u32)]),
     "cg_kafka_verdicts_dev": (C.c_int, [_u64, _p, _sz, _p, _p, _p]),
+    "cg_kafka_verdicts_split_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p]),
     "cg_kafka_verdicts_host": (C.c_int, [_u64, _p, _sz, _p, _sz, _p]),
     "cg_kafka_decode_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _sz, C.POINTER(_sz), _p]),
     "cg_kafka_decode_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _sz, C.POINTER(_sz), _p, _p]),

@@ -422,6 +422,12 @@ class Classifier:
     def kafka_verdicts_dev(self, d_reqs, n: int, d_arena, d_out, stream=None) -> None:
         N.check(N.lib.cg_kafka_verdicts_dev(self.h, _p(d_reqs), n, _p(d_arena), _p(d_out), stream))
 
+    def kafka_verdicts_split_dev(self, d_heads, d_topics, n: int, d_arena, d_out, stream=None) -> None:
+        """cg_kafka_verdicts_split_dev: 16-byte heads and 48-byte topic tails
+        in separate device arrays."""
+        N.check(N.lib.cg_kafka_verdicts_split_dev(self.h, _p(d_heads), _p(d_topics), n, _p(d_arena), _p(d_out),
+                                                  stream))
+
     def kafka_eval_host_diag(self, reqs: np.ndarray, arena: Optional[np.ndarray] = None) -> np.ndarray:
         n = len(reqs)
         out = np.zeros(max(n, 1), np.uint8)

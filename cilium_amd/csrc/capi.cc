@@ -1087,6 +1087,20 @@ int cg_kafka_verdicts_dev(uint64_t h, const cg_kafka_request* d_reqs, size_t n, 
   });
 }
 
+int cg_kafka_verdicts_split_dev(uint64_t h, const cg_kafka_request_head* d_heads, const uint32_t* d_topics,
+                                size_t n, const uint32_t* d_arena, uint8_t* d_out, void* stream) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    auto s = kafka_snap(*e);
+    if (n && (!d_heads || !d_topics || !d_out)) fail(CG_INVALID_ARGUMENT, "NULL heads/topics/out");
+    e->set_device();
+    check_launch(launch_kafka(s->dev, d_heads, n, d_arena, d_out, stream_of(*e, stream), e->cus, d_topics),
+                 "kafka kernel launch");
+    s->fence.record(stream_of(*e, stream));
+  });
+}
+
 int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n, const uint32_t* arena,
                            size_t arena_len, uint8_t* out) {
   return guarded([&] {

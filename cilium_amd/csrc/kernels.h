@@ -26,8 +26,10 @@ int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* 
                 void* stream, int cus, const uint32_t* order = nullptr, uint32_t* rule = nullptr);
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus);
+// tails (optional): the split layout — reqs holds 16-byte heads, tails the
+// 48-byte topic ids of each request (cg_kafka_verdicts_split_*).
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
-                 void* stream, int cus);
+                 void* stream, int cus, const void* tails = nullptr);
 // Kafka wire decode (kernels_kafka.hip): records + statuses (kKwDefer for the
 // host to finish); ctr[0] arena entries reserved, ctr[1] deferred requests
 // (both zeroed by the caller).

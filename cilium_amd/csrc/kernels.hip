@@ -641,7 +641,7 @@ __device__ __forceinline__ void kf_flush(unsigned long long* counters, uint32_t 
 
 // Slow part of one request: clientID table (typed requests against clientID
 // rules), exception rules, then per topic the (group, topic) rule list.
-__device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, const uint32_t* __restrict__ arena,
+__device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint32_t* tids, const uint32_t* __restrict__ arena,
                                          uint32_t g, uint32_t si, uint4 tail, int key, int ver, uint32_t kind,
                                          uint32_t c, uint32_t nt, uint32_t client) {
   const bool vin = ver >= 0 && ver < 64;
@@ -664,8 +664,7 @@ __device__ __forceinline__ uint32_t kf_slow(const KafkaDev& T, const uint4* r, c
   for (uint32_t j = 0; j < tail.z; ++j)
     if (kf_rule_matches(T.rules[tail.y + j], key, ver, kind, client)) return 1;
   if (nt == 0) return 0;
-  // topic ids re-read from the record (cached)
-  const uint32_t* tids = reinterpret_cast<const uint32_t*>(r + 1);
+  // topic ids re-read from the record, or its topic tail (cached)
   const uint32_t* tsrc = nt > CG_KAFKA_MAX_TOPICS ? arena + tids[0] : tids;
   if (nt == CG_KAFKA_TOPICS_IN_ARENA) nt = tids[1];
   for (uint32_t t = 0; t < nt; ++t) {
@@ -712,23 +711,36 @@ struct KfCount {
   }
 };
 
-__device__ __forceinline__ void kf_slow_one(const KafkaDev& T, const uint4* __restrict__ reqs,
+// Where a request's 16-byte head and 48-byte topic ids are: the 64-byte
+// record (cg_kafka_request: head stride 4 uint4, topics right after it) or
+// the split layout (cg_kafka_verdicts_split_*: heads and topic tails in two
+// arrays, so the common path reads 16 bytes per request, not a 64-byte line).
+struct KfLayout {
+  const uint4* __restrict__ heads;
+  const uint4* __restrict__ tails;
+  uint32_t hstride, tstride;  // in uint4
+  __device__ __forceinline__ const uint4* head(size_t i) const { return heads + i * hstride; }
+  __device__ __forceinline__ const uint32_t* tids(size_t i) const {
+    return reinterpret_cast<const uint32_t*>(tails + i * tstride);
+  }
+};
+
+__device__ __forceinline__ void kf_slow_one(const KafkaDev& T, const KfLayout& L,
                                             const uint32_t* __restrict__ arena, uint8_t* __restrict__ out,
                                             uint32_t i, uint32_t g, KfCount& cnt) {
-  const uint4* r = reqs + (size_t)i * 4;
-  const uint4 h = r[0];
+  const uint4 h = *L.head(i);
   const int key = (int16_t)(h.x & 0xFFFF), ver = (int16_t)(h.x >> 16);
   const uint32_t kind = h.y & 0xFF, nt = (h.y >> 8) & 0xFF, red = h.y >> 16;
   const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
   const uint32_t c = kind == CG_KAFKA_K_TYPED ? 0 : kind == CG_KAFKA_K_CONSUMER_METADATA ? 1 : 2;
   const uint32_t si = g * kKfSumsPerGroup + (nt == 0 ? kKfBuckets : 0) + b;
   const uint4 tail = *reinterpret_cast<const uint4*>(&T.sums[si].any);
-  const uint32_t v = kf_slow(T, r, arena, g, si, tail, key, ver, kind, c, nt, h.w);
+  const uint32_t v = kf_slow(T, L.tids(i), arena, g, si, tail, key, ver, kind, c, nt, h.w);
   out[i] = (uint8_t)v;
   cnt.add(T, red, v);
 }
 
-__global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, const uint4* __restrict__ reqs, size_t n,
+__global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, KfLayout L, size_t n,
                                                               const uint32_t* __restrict__ arena,
                                                               uint8_t* __restrict__ out) {
   __shared__ uint32_t q_i[kKafkaQueue], q_g[kKafkaQueue];
@@ -747,7 +759,7 @@ __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, const 
       // unconditional (clamped) loads: a load under a branch gets its own
       // vmcnt(0) at the join, which would serialize the four
       const size_t ic = i < n ? i : n - 1;
-      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(reqs + ic * 4));
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(L.head(ic)));
       h[u] = make_uint4(v.x, v.y, v.z, v.w);
     }
     // group slot probes (first probe for every request; further ones rare)
@@ -829,7 +841,7 @@ __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, const 
     uint32_t nq = q_n;
     while (nq >= kKafkaThreads) {
       const uint32_t p = nq - kKafkaThreads + threadIdx.x;
-      kf_slow_one(T, reqs, arena, out, q_i[p], q_g[p], cnt);
+      kf_slow_one(T, L, arena, out, q_i[p], q_g[p], cnt);
       nq -= kKafkaThreads;
       __syncthreads();
       if (threadIdx.x == 0) q_n = nq;
@@ -837,7 +849,7 @@ __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, const 
     }
   }
   __syncthreads();
-  if (threadIdx.x < q_n) kf_slow_one(T, reqs, arena, out, q_i[threadIdx.x], q_g[threadIdx.x], cnt);
+  if (threadIdx.x < q_n) kf_slow_one(T, L, arena, out, q_i[threadIdx.x], q_g[threadIdx.x], cnt);
   // the common case: every lane of the wave counted for the same redirect
   const uint32_t first = __builtin_amdgcn_readfirstlane(cnt.red);
   if (__all(cnt.red == first)) {
@@ -933,12 +945,14 @@ int launch_lpm(const LpmDev& t, bool v4f, bool v6f, const uint32_t* v4, size_t n
 }
 
 int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* arena, uint8_t* out,
-                 void* stream, int cus) {
+                 void* stream, int cus, const void* tails) {
   if (n == 0) return 0;
   const int occ = resident_cached((const void*)kafka_kernel, kKafkaThreads);
+  // tails == nullptr: 64-byte records; else 16-byte heads + 48-byte tails
+  const KfLayout L = tails ? KfLayout{(const uint4*)reqs, (const uint4*)tails, 1, 3}
+                           : KfLayout{(const uint4*)reqs, (const uint4*)reqs + 1, 4, 4};
   hipLaunchKernelGGL(kafka_kernel, dim3(grid_for(n, kKafkaThreads * kKafkaReqs, cus, occ)), dim3(kKafkaThreads), 0,
-                     (hipStream_t)stream, t,
-                     (const uint4*)reqs, n, arena, out);
+                     (hipStream_t)stream, t, L, n, arena, out);
   return (int)hipGetLastError();
 }
 

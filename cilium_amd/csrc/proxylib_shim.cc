@@ -18,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <set>
 #include <string>
@@ -35,10 +36,33 @@ using namespace cg;
 
 namespace {
 
+// One OnData call's request records waiting for their verdicts.
+struct VerdictReq {
+  const std::vector<std::string>* recs;
+  uint32_t policy;  // cg_http_policy_index of the connection's policy
+  bool ingress;
+  uint16_t port;
+  uint32_t remote;  // Matches passes SrcId (connection.go:176-179)
+  std::vector<uint8_t>* out;
+  bool done = false, ok = false;
+};
+
 struct Instance {
   uint64_t engine = 0;
   std::string key;
-  std::mutex mu;  // serializes verdict batches on the engine stream
+  std::mutex mu;  // serializes verdict batches and policy updates on the engine
+  // Cross-connection batching (flat combining): concurrent OnData calls of
+  // different connections queue their records; whichever finds no batch in
+  // flight takes everything queued and decides it as one GPU batch, while
+  // the calls arriving meanwhile queue for the next one.  A lone call is
+  // decided at once (no timer); under concurrency one launch and one sync
+  // serve many connections.  Each connection's own OnData stays
+  // single-threaded (libcilium.h:79-80).
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::vector<VerdictReq*> queue;
+  bool flushing = false;
+  uint64_t batches = 0, calls = 0;  // decided batches / calls (cg_proxylib_stats)
 };
 
 struct Conn {
@@ -390,25 +414,31 @@ std::string field(const char* name, const std::string& escaped) {
   return std::string(name) + '\0' + escaped + '\0';
 }
 
-// PolicyMatches (connection.go:176-179) for the request records of one
-// OnData call — each record a run of field() entries — as one host-staged
-// GPU batch.  Caller holds inst.mu.  Returns false on an engine error.
-bool gpu_verdicts(Instance& inst, const Conn& c, const std::vector<std::string>& recs, std::vector<uint8_t>* allow) {
-  const size_t n = recs.size();
-  allow->assign(n, 0);
+// PolicyMatches (connection.go:176-179) for the request records of the
+// queued OnData calls, as one host-staged GPU batch.  Caller holds inst.mu.
+// Returns false on an engine error.
+bool gpu_verdicts(Instance& inst, const std::vector<VerdictReq*>& reqs) {
+  size_t n = 0;
+  for (const VerdictReq* r : reqs) {
+    r->out->assign(r->recs->size(), 0);
+    n += r->recs->size();
+  }
   if (n == 0) return true;
-  uint32_t pidx = 0xFFFFFFFFu;
-  // no such policy (or none installed): PolicyMatches is false → DROP
-  if (cg_http_policy_index(inst.engine, c.policy.c_str(), &pidx) != CG_OK) return true;
-  std::vector<uint32_t> pol(n, pidx), remote(n, c.src_id);  // Matches passes SrcId
-  std::vector<uint8_t> ing(n, c.ingress ? 1 : 0);
-  std::vector<uint16_t> port(n, (uint16_t)(c.port > 0xFFFF ? 0 : c.port));
+  std::vector<uint32_t> pol, remote;
+  std::vector<uint8_t> ing;
+  std::vector<uint16_t> port;
+  pol.reserve(n), remote.reserve(n), ing.reserve(n), port.reserve(n);
   std::string blob;
   std::vector<uint64_t> off{0};
-  for (const std::string& r : recs) {
-    blob += r;
-    off.push_back(blob.size());
-  }
+  for (const VerdictReq* r : reqs)
+    for (const std::string& rec : *r->recs) {
+      pol.push_back(r->policy);
+      ing.push_back(r->ingress ? 1 : 0);
+      port.push_back(r->port);
+      remote.push_back(r->remote);
+      blob += rec;
+      off.push_back(blob.size());
+    }
   if (blob.empty()) blob.push_back('\0');
   size_t nslots = 0, used = 0;
   int rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
@@ -416,14 +446,57 @@ bool gpu_verdicts(Instance& inst, const Conn& c, const std::vector<std::string>&
   if (rc != CG_OK) return false;
   std::vector<uint8_t> batch(cg_http_batch_bytes(inst.engine, n));
   std::vector<uint32_t> order(cg_http_batch_slots(inst.engine, n) + 1);
-  std::vector<uint8_t> arena(used > 16 ? used : 16);
+  std::vector<uint8_t> arena(used > 16 ? used : 16), allow(n);
   rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
                     (const uint8_t*)blob.data(), off.data(), batch.data(), batch.size(), order.data(), &nslots,
                     arena.data(), arena.size(), &used);
   if (rc != CG_OK) return false;
   rc = cg_http_verdicts_host(inst.engine, batch.data(), nslots, order.data(), n, arena.data(), arena.size(),
-                             allow->data());
-  return rc == CG_OK;
+                             allow.data());
+  if (rc != CG_OK) return false;
+  size_t k = 0;
+  for (VerdictReq* r : reqs)
+    for (size_t i = 0; i < r->recs->size(); ++i) (*r->out)[i] = allow[k++];
+  return true;
+}
+
+// Verdicts for one OnData call's records (see Instance: the calls queued
+// meanwhile share the GPU batch).
+bool decide(Conn& c, const std::vector<std::string>& recs, std::vector<uint8_t>* out) {
+  out->assign(recs.size(), 0);
+  if (recs.empty()) return true;
+  Instance& inst = *c.inst;
+  uint32_t pidx = 0xFFFFFFFFu;
+  // no such policy (or none installed): PolicyMatches is false → DROP
+  if (cg_http_policy_index(inst.engine, c.policy.c_str(), &pidx) != CG_OK) return true;
+  VerdictReq me{&recs, pidx, c.ingress, (uint16_t)(c.port > 0xFFFF ? 0 : c.port), c.src_id, out};
+  std::unique_lock<std::mutex> lk(inst.qmu);
+  inst.queue.push_back(&me);
+  while (!me.done) {
+    if (inst.flushing) {
+      inst.qcv.wait(lk);
+      continue;
+    }
+    inst.flushing = true;
+    std::vector<VerdictReq*> batch;
+    batch.swap(inst.queue);
+    lk.unlock();
+    bool ok;
+    {
+      std::lock_guard<std::mutex> g(inst.mu);
+      ok = gpu_verdicts(inst, batch);
+    }
+    lk.lock();
+    for (VerdictReq* r : batch) {
+      r->ok = ok;
+      r->done = true;
+    }
+    inst.batches += 1;
+    inst.calls += batch.size();
+    inst.flushing = false;
+    inst.qcv.notify_all();
+  }
+  return me.ok;
 }
 
 // A memcache request as the fields its rules are compiled over (see
@@ -452,9 +525,7 @@ FilterResult memcache_data(Conn& c, bool reply, bool end_stream, const GoSlice* 
       recs.push_back(memcache_record(m));
       return true;
     });
-    Instance& inst = *c.inst;
-    std::lock_guard<std::mutex> lk(inst.mu);
-    if (!gpu_verdicts(inst, c, recs, &allow)) return FILTER_UNKNOWN_ERROR;
+    if (!decide(c, recs, &allow)) return FILTER_UNKNOWN_ERROR;
   }
   size_t next = 0;
   return memcache_on_data(c.mc, reply, end_stream, data, ops, c.reply_buf, [&](const McMeta&) {
@@ -485,9 +556,7 @@ FilterResult cassandra_data(Conn& c, bool reply, bool end_stream, const GoSlice*
       recs.push_back(cassandra_record(path));
       return true;
     });
-    Instance& inst = *c.inst;
-    std::lock_guard<std::mutex> lk(inst.mu);
-    if (!gpu_verdicts(inst, c, recs, &allow)) return FILTER_UNKNOWN_ERROR;
+    if (!decide(c, recs, &allow)) return FILTER_UNKNOWN_ERROR;
   }
   size_t next = 0;
   return cassandra_on_data(c.cs, reply, end_stream, data, ops, c.reply_buf, [&](const std::string&) {
@@ -514,6 +583,15 @@ int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len) {
   }
   std::lock_guard<std::mutex> lk(inst->mu);
   return cg_http_policy_update(inst->engine, eng.data(), eng.size());
+}
+
+int cg_proxylib_stats(uint64_t instance, uint64_t* batches, uint64_t* calls) {
+  auto inst = find_instance(instance);
+  if (!inst) return CG_INVALID_INSTANCE;
+  std::lock_guard<std::mutex> lk(inst->qmu);
+  if (batches) *batches = inst->batches;
+  if (calls) *calls = inst->calls;
+  return CG_OK;
 }
 
 int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* resp, size_t len) {
@@ -661,10 +739,8 @@ FilterResult OnData(uint64_t connectionId, uint8_t reply, uint8_t endStream, GoS
       recs.push_back(field("cmd", esc(frames[i].cmd)) + field("file", esc(frames[i].file)));
     }
   if (!recs.empty()) {
-    Instance& inst = *c->inst;
-    std::lock_guard<std::mutex> lk(inst.mu);
     std::vector<uint8_t> out;
-    if (!gpu_verdicts(inst, *c, recs, &out)) return FILTER_UNKNOWN_ERROR;
+    if (!decide(*c, recs, &out)) return FILTER_UNKNOWN_ERROR;
     for (size_t k = 0; k < reqs.size(); ++k) allow[reqs[k]] = out[k];
   }
   FilterOp* ops = static_cast<FilterOp*>(filterOps->data);

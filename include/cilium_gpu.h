@@ -311,6 +311,11 @@ int cg_proxylib_policy_update(uint64_t instance, const char* json, size_t len);
  * cg_http_policy_update_npds). */
 int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* discovery_response, size_t len);
 
+/* OnData calls with request frames whose verdicts the instance has decided,
+ * and the GPU batches that decided them: concurrent calls of different
+ * connections share a batch (flat combining; calls > batches under load). */
+int cg_proxylib_stats(uint64_t instance, uint64_t* batches, uint64_t* calls);
+
 /* ======================================================================== */
 /* HTTP L7: Envoy cilium.l7policy — envoy/cilium_network_policy.h:40-237,    */
 /* envoy/cilium_l7policy.cc:127-182                                          */
@@ -604,6 +609,22 @@ int cg_kafka_verdicts_dev(uint64_t h, const cg_kafka_request* d_reqs, size_t n,
                           const uint32_t* d_arena, uint8_t* d_out, void* stream);
 int cg_kafka_verdicts_host(uint64_t h, const cg_kafka_request* reqs, size_t n,
                            const uint32_t* arena, size_t arena_len, uint8_t* out);
+/* The same verdicts over the record split in two arrays: d_heads[i] = the
+ * first 16 bytes of cg_kafka_request i, d_topics[12 i .. 12 i + 11] = its
+ * topic_ids.  Most requests are settled from the head alone (the decision
+ * summaries), so HBM moves 16 bytes per request instead of a 64-byte record
+ * line; topic tails are read only for the requests that need their topics. */
+typedef struct {
+  int16_t api_key;
+  int16_t api_version;
+  uint8_t kind;
+  uint8_t n_topics;
+  uint16_t policy;
+  uint32_t remote;
+  uint32_t client_id;
+} cg_kafka_request_head;
+int cg_kafka_verdicts_split_dev(uint64_t h, const cg_kafka_request_head* d_heads, const uint32_t* d_topics,
+                                size_t n, const uint32_t* d_arena, uint8_t* d_out, void* stream);
 
 /* ======================================================================== */
 /* Counters                                                                  */

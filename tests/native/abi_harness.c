@@ -50,6 +50,8 @@ _Static_assert(offsetof(cg_kafka_request, remote) == 8, "kafka_request.remote");
 _Static_assert(offsetof(cg_kafka_request, client_id) == 12, "kafka_request.client_id");
 _Static_assert(offsetof(cg_kafka_request, topic_ids) == 16, "kafka_request.topic_ids");
 _Static_assert(sizeof(cg_http_rule_info) == 24, "http_rule_info");
+_Static_assert(sizeof(cg_kafka_request_head) == 16, "kafka_request_head");
+_Static_assert(offsetof(cg_kafka_request_head, client_id) == offsetof(cg_kafka_request, client_id), "head prefix");
 _Static_assert(sizeof(cg_kv) == 2 * sizeof(void*), "kv");
 
 static int failures = 0;

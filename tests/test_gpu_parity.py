@@ -383,3 +383,35 @@ def test_kafka_edge_parity(gpu):
         reqs, arena = gpu.pack_kafka(**rq)
         got = gpu.kafka_verdicts(reqs, arena)
         assert np.array_equal(got, oracle.KafkaOracle(pols).eval(**rq)), f"seed {seed}"
+
+
+@pytest.mark.gpu
+def test_gpu_kafka_split_layout(gpu):
+    """cg_kafka_verdicts_split_dev: the same verdicts and per-redirect
+    counters as the 64-byte records (and the oracle), with heads and topic
+    tails in separate arrays — overflow-arena topic lists included."""
+    import torch
+    pols, info = synth.kafka_policy(n_rules=400, n_topics=60, n_clients=12, seed=5)
+    gpu.update_kafka_policy(pols)
+    rq = synth.kafka_requests(300_000, info, seed=6)
+    reqs, arena = gpu.pack_kafka(**rq)
+    exp = oracle.KafkaOracle(pols).eval(**rq, nthreads=16)
+    n = len(reqs)
+    raw = reqs.view(np.uint8).reshape(n, 64)
+    dev = torch.device("cuda", 0)
+    d_heads = torch.from_numpy(np.ascontiguousarray(raw[:, :16])).to(dev)
+    d_topics = torch.from_numpy(np.ascontiguousarray(raw[:, 16:])).to(dev)
+    d_arena = torch.from_numpy(arena if len(arena) else np.zeros(1, np.uint32)).to(dev)
+    d_out = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+    gpu.reset_counters()
+    s = torch.cuda.current_stream().cuda_stream
+    gpu.kafka_verdicts_split_dev(d_heads, d_topics, n, d_arena, d_out, stream=s)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), exp)
+    c_split = gpu.read_counters(1).copy()
+    gpu.reset_counters()
+    d_reqs = torch.from_numpy(raw.copy()).to(dev)
+    gpu.kafka_verdicts_dev(d_reqs, n, d_arena, d_out, stream=s)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), exp)
+    assert np.array_equal(gpu.read_counters(1), c_split)

@@ -259,3 +259,60 @@ def test_gpu_r2d2_control_bytes_through_ondata():
         assert c.injected_reply() == b"ERROR\r\n" * sum(1 for e in exp if not e)
         c.close()
     _lib.CloseModule(inst)
+
+
+@pytest.mark.gpu
+def test_gpu_ondata_concurrent_connections_share_batches():
+    """16 threads, one connection each (different remote identities and
+    policies), OnData concurrently: every call's ops match the oracle, and
+    the instance's flat-combining batcher decided the calls in fewer GPU
+    batches than calls (cg_proxylib_stats)."""
+    import threading
+
+    import numpy as np
+
+    from oracle.proxylib_ref import ProxylibOracle
+    from test_proxylib import _rand_policies
+    from cilium_amd import proxylib as P
+    inst = open_module([(b"node-id", b"gpu-concurrent")], "0")
+    assert inst != 0
+    rng = np.random.default_rng(404)
+    pols = _rand_policies(rng)
+    t = json.dumps(pols).encode()
+    assert N.lib.cg_proxylib_policy_update(inst, t, len(t)) == N.CG_OK
+    o = ProxylibOracle(pols)
+    files = [b"/public/a", b"a.txt", b"secret", b"aaa", b"foo7", b"ssss", b"", b"x/y", b"sx"]
+    errors = []
+
+    def worker(k):
+        try:
+            r = np.random.default_rng(k)
+            name = f"p{k % 3}"
+            port = [80, 8080, 443][k % 3]
+            remote = int(k % 8)
+            c = Conn(inst, ingress=True, src=remote, dst=9, dst_addr=b"10.0.0.1:%d" % port, policy=name.encode())
+            assert c.rc == F_OK
+            for _ in range(60):
+                lines = [bytes(r.choice([b"READ", b"WRITE", b"HALT"])) + b" " + bytes(r.choice(files))
+                         for _ in range(int(r.integers(1, 17)))]
+                rc, ops = c.on_data([b"".join(x + b"\r\n" for x in lines)])
+                exp = [(PASS if o.matches(name, True, port, remote, *P.r2d2_request(x)) else DROP, len(x) + 2)
+                       for x in lines]
+                assert rc == F_OK and ops == exp + [(MORE, 1)], (k, lines, ops)
+                c.take_reply()
+        except Exception as e:  # noqa: BLE001 — surfaced below
+            errors.append(repr(e))
+
+    b0, c0 = C.c_uint64(), C.c_uint64()
+    N.lib.cg_proxylib_stats(inst, C.byref(b0), C.byref(c0))
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join()
+    b1, c1 = C.c_uint64(), C.c_uint64()
+    N.lib.cg_proxylib_stats(inst, C.byref(b1), C.byref(c1))
+    _lib.CloseModule(inst)
+    assert not errors, errors[:3]
+    calls, batches = c1.value - c0.value, b1.value - b0.value
+    assert calls >= 16 * 60 * 0.9 and batches < calls, (calls, batches)
