@@ -305,6 +305,40 @@ struct HttpRawRun {
   uint32_t send;  // one past the last real slot of the run's group (later slots are padding)
 };
 
+// bucket key of a request on the device-layout path: its group (program,
+// then allow and deny) x its walked string's 16-byte units (0..8); longer
+// strings are walked by raw_walk_kernel, not slotted
+constexpr uint32_t kRawUnits = 9;
+// The raw path's device-built batch (kernels_http_raw.hip, http_raw.cc): the
+// scan takes slot s of bucket key k from a per-key counter; slots come in
+// chunks of 64 * ext (ext tiles, a power of two <= kChunkTiles), the first
+// slot of a chunk takes a chunk id from ctl[kRawCtlChunks] and publishes it
+// in dir[k * dpk + c] as seq << 32 | id (seq: the sub-batch's tag, so the
+// directory is never cleared).  Tile t = id * ext + (s / 64) % ext keeps its
+// data at granule t * kRawTileGran (room for 8 units), slot s % 64.
+constexpr uint32_t kRawTileGran = 1 + 2 * 8;
+constexpr uint32_t kRawCntStride = 64;  // u32 between two keys' counters (own 256-B line)
+enum : uint32_t {
+  kRawCtlChunks = 0,  // chunk ids taken
+  kRawCtlWalk = 1,    // requests on the walk list (raw_walk_kernel)
+  kRawCtlDefer = 2,   // requests on the deferred list (heads outside their wave's stage)
+  kRawCtlError = 3,   // bit 0: a chunk past the layout's bounds (its requests walked instead)
+  kRawCtlWords = 16
+};
+struct RawLayoutDev {
+  uint32_t* kcnt;            // [key * kRawCntStride] slots taken
+  unsigned long long* dir;   // [key * dpk + c]
+  HttpChunk* chunks;         // in id order: {prog, first tile, ntiles, key} (raw_seal_kernel sorts them)
+  HttpTile* ttab;            // units | tail << 16 by atomicMax (zeroed per sub-batch), at by the slot-0 lane
+  uint8_t* tiles;            // tile data
+  uint32_t* order;           // slot → request index
+  uint32_t* ctl;             // kRawCtl*
+  uint32_t* walk;            // request indices for raw_walk_kernel
+  uint32_t* dlist;           // request indices for raw_defer_kernel
+  uint32_t dpk, ext, cshift; // directory entries per key, tiles per chunk, log2(64 * ext)
+  uint32_t seq, maxchunks, nkeys;
+};
+
 CG_HD inline uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352dU;

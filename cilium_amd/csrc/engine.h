@@ -104,12 +104,19 @@ class PinnedMem {
 // device buffers and pinned host buffers, so host calls make no hipMalloc /
 // hipFree and copy with async DMA instead of pageable hipMemcpy.
 struct StagingSlot {
-  static constexpr int kBufs = 19;  // 0..7 host staging, 8..18 the raw HTTP path's workspace
+  static constexpr int kBufs = 26;  // 0..7 host staging, 8..18 the raw HTTP path's workspace, 19..25 its device-layout sequence's
   void* stream = nullptr;  // hipStream_t
   DevMem dev[kBufs];
   PinnedMem host[kBufs];
   void* dev_buf(int i, size_t bytes);  // grow-only device buffer i
   void* host_buf(int i, size_t bytes); // grow-only pinned buffer i
+  // The raw HTTP path leaves its work queued on the caller's stream: the
+  // event after its last launch (hipEvent_t) and that stream, so the next
+  // raw call on this slot from another stream waits for it on the device;
+  // raw_seq tags its chunk directory (http_raw.cc).
+  void* raw_ev = nullptr;
+  void* raw_stream = nullptr;
+  uint32_t raw_seq = 0;
   ~StagingSlot();
 };
 

@@ -3,11 +3,17 @@
 //   scan → (bucket counts to the host) → layout → rank → build → http_kernel
 // on one stream.  The host step is the layout of a few thousand bucket
 // counts (chunks, runs of equal-units tiles, bucket cursors); request bytes
-// never leave the device.
+// never leave the device.  CILIUM_GPU_RAW_LAYOUT=device selects the
+// device-layout sequence instead (raw_device_layout):
+//   clear → scan (+ deferred) → seal → http_kernel → walk
+// per sub-batch, all on the caller's stream, with no copy back and no host
+// synchronization (the layout is raw_seal_kernel's).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "http.h"
 #include "kernels.h"
@@ -330,6 +336,111 @@ void raw_sequential(RawCall c) {
   hip_check(hipStreamSynchronize(c.st), "hipStreamSynchronize");
 }
 
+// Requests per sub-batch: the layout's bounds (slots, tiles, directory) are
+// reserved for the worst case of a sub-batch — every request in one bucket,
+// every string 8 units long — so the reservation is sized by requests, never
+// by what the scan finds (no host round trip); 2^25 requests reserve ~4.8 GB
+// of tile data on the 10K-rule set.
+constexpr size_t kRawSubBatch = (size_t)1 << 25;
+
+uint32_t floor_pow2(uint32_t x) {
+  uint32_t p = 1;
+  while (p * 2 <= x) p *= 2;
+  return p;
+}
+
+// One sub-batch of the device-layout path, enqueued on `st`: clear the
+// counters and tile table, scan, seal, http_kernel, walk.  The workspace is
+// the slot's buffers 19..25 (the default sequence's are 8..18).
+void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists, const uint8_t* d_raw,
+                  const uint64_t* d_off, size_t m, const uint32_t* d_policy, const uint8_t* d_ingress,
+                  const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, hipStream_t st) {
+  const uint32_t np = (uint32_t)s.progs.size(), K = (np + 2) * kRawUnits;
+  // tiles per chunk: the chunk table's 64 when the sub-batch fills several
+  // chunks per bucket, fewer for small ones (each bucket's last chunk is
+  // partly empty)
+  const uint32_t ext = floor_pow2((uint32_t)std::min<size_t>(kChunkTiles, std::max<size_t>(1, m / (64 * (size_t)K))));
+  uint32_t cshift = 6;
+  while ((1u << cshift) < 64 * ext) ++cshift;
+  const size_t per_chunk = (size_t)64 * ext;
+  const uint32_t dpk = (uint32_t)((m + per_chunk - 1) / per_chunk);
+  // every chunk holds a slot: at most m of them, and at most one partly
+  // filled per bucket
+  const uint32_t maxchunks = (uint32_t)std::min<size_t>(m, (size_t)dpk + K);
+  const size_t maxtiles = (size_t)maxchunks * ext;
+  if (maxtiles * kRawTileGran >= (1ull << 32)) fail(CG_INVALID_ARGUMENT, "raw batch layout too large");
+  // batch: header, chunk table, tile table, tile data (1 KiB aligned)
+  const uint64_t ttab_off = sizeof(HttpBatchHeader) + (uint64_t)sizeof(HttpChunk) * maxchunks;
+  const uint64_t tiles_off = (ttab_off + sizeof(HttpTile) * maxtiles + 1023) & ~(uint64_t)1023;
+  const uint64_t total = tiles_off + (uint64_t)maxtiles * kRawTileGran * 512;
+  const size_t ctl_bytes = (size_t)K * kRawCntStride * 4 + kRawCtlWords * 4;
+  const size_t dir_bytes = (size_t)K * dpk * 8;
+  // the directory: fresh memory is cleared once (entries carry the
+  // sub-batch tag, so a live one is never confused with an old one)
+  const bool fresh_dir = !sl.dev[20].get() || sl.dev[20].size() < dir_bytes;
+  RawLayoutDev L{};
+  uint8_t* ctl = (uint8_t*)sl.dev_buf(19, ctl_bytes);
+  L.kcnt = (uint32_t*)ctl;
+  L.ctl = (uint32_t*)(ctl + (size_t)K * kRawCntStride * 4);
+  L.dir = (unsigned long long*)sl.dev_buf(20, dir_bytes);
+  if (fresh_dir) hip_check(hipMemsetAsync(L.dir, 0, sl.dev[20].size(), st), "hipMemsetAsync");
+  uint8_t* batch = (uint8_t*)sl.dev_buf(21, total);
+  L.ttab = (HttpTile*)(batch + ttab_off);
+  L.tiles = batch + tiles_off;
+  L.chunks = (HttpChunk*)sl.dev_buf(22, (size_t)maxchunks * sizeof(HttpChunk));
+  L.order = (uint32_t*)sl.dev_buf(23, maxtiles * 64 * 4);
+  L.walk = (uint32_t*)sl.dev_buf(24, m * 4);
+  L.dlist = (uint32_t*)sl.dev_buf(25, m * 4);
+  L.dpk = dpk;
+  L.ext = ext;
+  L.cshift = cshift;
+  L.seq = ++sl.raw_seq;
+  if (!L.seq) L.seq = ++sl.raw_seq;  // 0 is the cleared directory's tag
+  L.maxchunks = maxchunks;
+  L.nkeys = K;
+  hip_check(hipMemsetAsync(ctl, 0, ctl_bytes, st), "hipMemsetAsync");
+  hip_check(hipMemsetAsync(L.ttab, 0, sizeof(HttpTile) * maxtiles, st), "hipMemsetAsync");
+  hip_check(launch_http_raw_dl_scan(s.raw, lists, d_raw, d_off, m, d_policy, d_ingress, d_port, d_remote, L, st, cus),
+            "raw scan kernel launch");
+  hip_check(launch_http_raw_seal(s.raw, L, batch, s.epoch, ttab_off, tiles_off, total, st), "raw seal kernel launch");
+  hip_check(launch_http(s.dev, batch, maxtiles * 64, nullptr, d_out, st, cus, L.order, nullptr, (uint32_t)m), "http kernel launch");
+  hip_check(launch_http_raw_walk(s.dev, s.raw, lists, d_raw, d_off, d_policy, d_ingress, d_port, d_remote, L, d_out,
+                                 st, cus),
+            "raw walk kernel launch");
+}
+
+// The device-layout path: sub-batches enqueued on `stream`, nothing waited
+// for on the host.
+void raw_device_layout(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists, const uint8_t* d_raw,
+                       const uint64_t* d_off, size_t n, const uint32_t* d_policy, const uint8_t* d_ingress,
+                       const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, void* stream) {
+  const hipStream_t st = (hipStream_t)stream;
+  // the slot's last raw call may still be queued on another stream: this
+  // stream waits for it on the device (no host wait)
+  if (sl.raw_ev && sl.raw_stream != stream) hip_check(hipStreamWaitEvent(st, (hipEvent_t)sl.raw_ev, 0), "hipStreamWaitEvent");
+  // (CILIUM_GPU_RAW_SUBBATCH: a smaller sub-batch, for tests)
+  size_t sub = kRawSubBatch;
+  if (const char* v = getenv("CILIUM_GPU_RAW_SUBBATCH")) sub = std::min(kRawSubBatch, std::max<size_t>(64, strtoull(v, nullptr, 10)));
+  for (size_t a = 0; a < n; a += sub) {
+    const size_t m = std::min(sub, n - a);
+    raw_dl_subbatch(s, sl, cus, lists, d_raw, d_off + a, m, d_policy + a, d_ingress + a, d_port + a, d_remote + a,
+                 d_out + a, st);
+  }
+  if (!sl.raw_ev) {
+    hipEvent_t e;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    sl.raw_ev = e;
+  }
+  hip_check(hipEventRecord((hipEvent_t)sl.raw_ev, st), "hipEventRecord");
+  sl.raw_stream = stream;
+}
+
+// CILIUM_GPU_RAW_LAYOUT=device selects the device-layout path (read per call).
+bool device_layout_selected() {
+  const char* v = getenv("CILIUM_GPU_RAW_LAYOUT");
+  return v && std::string(v) == "device";
+}
+
 }  // namespace
 
 void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawInput in, const uint8_t* d_raw,
@@ -341,6 +452,11 @@ void http_verdicts_raw_on(const HttpSnapshot& s, StagingSlot& sl, int cus, RawIn
                                      std::to_string(kRawMaxFields) + " header fields"
                                : "raw HTTP/1 heads: the snapshot has more than " + std::to_string(kRawMaxFields) +
                                      " header fields, or is a proxylib snapshot");
+  if (!n) return;
+  if (device_layout_selected()) {
+    raw_device_layout(s, sl, cus, lists, d_raw, d_off, n, d_policy, d_ingress, d_port, d_remote, d_out, stream);
+    return;
+  }
   raw_sequential(RawCall{&s, &sl, cus, in, d_raw, d_off, n, d_policy, d_remote, d_ingress, d_port, d_out,
                          (hipStream_t)stream});
 }

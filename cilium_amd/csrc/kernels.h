@@ -19,11 +19,13 @@ int launch_l4_ipcache(const L4Dev& t, const IpcacheDev& ipc, int family, const v
 int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* v4, size_t n4,
                uint8_t* out4, const uint8_t* v6, size_t n6, uint8_t* out6, void* stream, int cus);
 // order (optional): out[order[slot]] instead of out[slot] (request order;
-// order 0xFFFFFFFF = padding, no write) — the raw-request batches.
+// an entry >= nout, e.g. 0xFFFFFFFF = padding, writes nothing) — the
+// raw-request batches.
 // rule (optional): per slot (or order[slot]) the first matching rule's
 // counter index, 0xFFFFFFFF when no rule allows.
 int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
-                void* stream, int cus, const uint32_t* order = nullptr, uint32_t* rule = nullptr);
+                void* stream, int cus, const uint32_t* order = nullptr, uint32_t* rule = nullptr,
+                uint32_t nout = 0xFFFFFFFFu);
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus);
 // tails (optional): the split layout — reqs holds 16-byte heads, tails the
@@ -64,5 +66,24 @@ int launch_http_raw_rank(const HttpRawDev& R, bool lists, size_t n, const void* 
 int launch_http_raw_build(const HttpRawDev& R, const HttpRawRun* runs, uint32_t nruns, uint32_t ntiles,
                           HttpTile* ttab, uint8_t* tiles, uint32_t* order, const uint8_t* sbuf, uint8_t* arena,
                           unsigned long long* arena_cursor, void* stream, int cus);
+
+// The device-layout path (CILIUM_GPU_RAW_LAYOUT=device; sequence, all on
+// one stream with no host round trip, in http_raw.cc):
+// launch_http_raw_dl_scan (scan + deferred requests) puts each request into its
+// slot of the batch laid out by L (dev_types.h RawLayoutDev) or on L's walk
+// list; launch_http_raw_seal pads the last tiles and writes the chunk table
+// and header; then launch_http over the batch (order = L.order) and
+// launch_http_raw_walk for the walk list.  lists: the requests are
+// cg_http_pack header lists instead of HTTP/1 heads.
+size_t http_raw_dl_grid(const HttpRawDev& R, bool lists, size_t n, int cus);
+bool http_raw_seal_sorts(const HttpRawDev& R);
+int launch_http_raw_dl_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off, size_t n,
+                            const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                            const uint32_t* remote, const RawLayoutDev& L, void* stream, int cus);
+int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch, uint32_t epoch, uint64_t ttab_off,
+                         uint64_t tiles_off, uint64_t total_bytes, void* stream);
+int launch_http_raw_walk(const HttpDev& T, const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off,
+                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, const uint32_t* remote,
+                         const RawLayoutDev& L, uint8_t* out, void* stream, int cus);
 
 }  // namespace cg

@@ -35,6 +35,7 @@
 
 #include "../../include/cilium_gpu.h"
 #include "dev_types.h"
+#include "http_walk.h"
 #include "kernels.h"
 
 namespace cg {
@@ -1380,6 +1381,515 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
   }
 }
 
+// ---- the device-layout path (CILIUM_GPU_RAW_LAYOUT=device, http_raw.cc) --
+// The steps of the path above without its host round trips:
+//   raw_scan_dl_kernel   parse as raw_scan_kernel, then the request takes a
+//                        slot of its bucket (program group x string units)
+//                        from a per-bucket counter and writes its class-coded
+//                        string units, meta word and order entry straight
+//                        into the tile-transposed batch http_kernel reads
+//   raw_defer_dl_kernel  the same for requests outside their wave's stage
+//   raw_seal_kernel      last tiles padded, chunk table grouped by program,
+//                        batch header — the layout the host computes above
+//   http_kernel          the verdicts, in request order through order[]
+//   raw_walk_kernel      requests whose string passes the 128-byte slot:
+//                        walked one lane each over the tables in HBM
+// Dynamic LDS of raw_scan_dl_kernel: raw_scan_kernel's without the bucket
+// counters (the lookup tables follow the tchar table).
+__device__ __forceinline__ lds_u32* raw_tables(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + 256); }
+
+// ---- the walked string, class-coded, straight into its tile slot ---------
+// http_pack.cc's string: the values of the fields up to the last present
+// one, each SEP-terminated (an absent one: 0x01 SEP), then REST (0x02) when a
+// later field is absent; every byte through the program's code map (identity
+// for byte-mode programs).  Bytes gather in 16; each full unit is coded and
+// stored to the slot's next string unit (1 KiB apart in the tile); in the
+// last unit the bytes past the string stay zero (the walk's padding).
+struct TileOut {
+  uint32_t w0, w1, w2, w3, pos;
+  uint4* dst;               // the slot's next string unit
+  const uint8_t* lut;       // the program's code map
+  __device__ __forceinline__ TileOut(uint4* d, const uint8_t* l) : w0(0), w1(0), w2(0), w3(0), pos(0), dst(d), lut(l) {}
+  // nb (1..4) bytes, little-endian in v (its bytes past nb zero), at byte
+  // pos: one 64-bit shift spreads them over dword pos / 4 and the next; the
+  // part past the 16 bytes starts the next unit
+  __device__ __forceinline__ void put4(uint32_t v, uint32_t nb) {
+    const uint64_t t = (uint64_t)v << ((pos & 3) * 8);
+    const uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32), q = pos >> 2;
+    w0 |= lo & (0u - (q == 0));
+    w1 |= (lo & (0u - (q == 1))) | (hi & (0u - (q == 0)));
+    w2 |= (lo & (0u - (q == 2))) | (hi & (0u - (q == 1)));
+    w3 |= (lo & (0u - (q == 3))) | (hi & (0u - (q == 2)));
+    pos += nb;
+    if (pos >= 16) {
+      const uint32_t rest = pos - 16;
+      flush();
+      w0 = hi & (0u - (q == 3));
+      pos = rest;
+    }
+  }
+  __device__ __forceinline__ void put(uint32_t b) { put4(b, 1); }
+  __device__ __forceinline__ void flush() {
+    *dst = make_uint4(code4(lut, w0), code4(lut, w1), code4(lut, w2), code4(lut, w3));
+    dst += 64;
+    w0 = w1 = w2 = w3 = 0;
+    pos = 0;
+  }
+  // the last, partial unit: its coded bytes, zero past the string
+  __device__ __forceinline__ void finish() {
+    if (!pos) return;
+    const uint32_t p = pos;
+    auto keep = [&](uint32_t c, uint32_t at) {  // bytes of dword `at` below p
+      return p >= at + 4 ? c : p <= at ? 0u : c & ((1u << (8 * (p - at))) - 1u);
+    };
+    *dst = make_uint4(keep(code4(lut, w0), 0), keep(code4(lut, w1), 4), keep(code4(lut, w2), 8),
+                      keep(code4(lut, w3), 12));
+  }
+};
+
+// The string of a request parsed from the stage (parse_head_fast /
+// parse_list_fast spans, relative to hs) into o.
+__device__ __forceinline__ void emit_stage(const HttpRawDev& R, const lds_u8* st, uint32_t hs, const lds_u32* sp,
+                                           uint32_t stride, const Parsed& P, uint32_t last, TileOut& o) {
+  uint32_t f = 0;
+  for (uint32_t rem = P.present; rem; rem &= rem - 1) {
+    const uint32_t g = (uint32_t)__builtin_ctz(rem);
+    for (; f + 2 <= g; f += 2) o.put4(0x00010001u, 4);  // two absent fields
+    if (f < g) o.put4(1u, 2);
+    const uint32_t sv = sp[g * stride], a = hs + (sv >> 16), L = sv & 0xFFFFu;
+    for (uint32_t k = 0; k < L; k += 4) {  // a quad at a time
+      const uint32_t nb = min(L - k, 4u);
+      o.put4(keep_bytes(squad(st, a + k), nb), nb);
+    }
+    o.put(0u);  // SEP
+    f = g + 1;
+  }
+  if (last < R.nfields) o.put(2u);  // REST
+  o.finish();
+}
+
+// The string of a request parsed through a HeadReader (parse_head /
+// parse_list_bytes spans, absolute, kAbsentSpan for absent fields) into o.
+__device__ __forceinline__ void emit_reader(const HttpRawDev& R, HeadReader& hr, const lds_u32* sp, uint32_t stride,
+                                            uint32_t last, TileOut& o) {
+  for (uint32_t f = 0; f < last; ++f) {
+    const uint32_t s = sp[f * stride];
+    if (s == kAbsentSpan) {
+      o.put4(1u, 2);  // absent, SEP
+      continue;
+    }
+    const uint32_t a = s >> 16, L = s & 0xFFFFu;
+    for (uint32_t k = 0; k < L; k += 4) {
+      const uint32_t nb = min(L - k, 4u);
+      o.put4(keep_bytes(hr.quad(a + k), nb), nb);
+    }
+    o.put(0u);
+  }
+  if (last < R.nfields) o.put(2u);
+  o.finish();
+}
+
+// ---- slots: the batch laid out on the device (dev_types.h RawLayoutDev) ---
+// Every lane with `want` takes the next slot of its bucket key; the first
+// slot of a chunk takes a chunk id and publishes it (never waiting first), the
+// others wait for their chunk's id.  ok = false: the layout's bounds were
+// passed or the chunk's id never came (neither happens for the sizes
+// http_raw.cc reserves; ctl[kRawCtlError] records it) — the lane's request
+// is walked by raw_walk_kernel instead.
+constexpr uint32_t kSpinMax = 1u << 14;  // ~15 ms of polling: a legitimate wait is microseconds
+struct RawSlot {
+  uint8_t* tb;  // the tile's data
+  uint32_t t, l;
+  bool ok;
+};
+__device__ __forceinline__ RawSlot raw_slot(const RawLayoutDev& L, bool want, uint32_t key, uint32_t prog) {
+  RawSlot r{nullptr, 0, 0, false};
+  uint32_t s = 0;
+  if (want) s = atomicAdd(&L.kcnt[(size_t)key * kRawCntStride], 1u);
+  const uint32_t c = s >> L.cshift;
+  if (want && (s & ((1u << L.cshift) - 1u)) == 0 && c < L.dpk) {  // publish the chunk
+    const uint32_t id = atomicAdd(&L.ctl[kRawCtlChunks], 1u);
+    const bool fits = id < L.maxchunks;
+    if (fits) L.chunks[id] = HttpChunk{prog, id * L.ext, L.ext, key};
+    else atomicOr(&L.ctl[kRawCtlError], 1u);
+    __hip_atomic_store(&L.dir[(size_t)key * L.dpk + c], (unsigned long long)L.seq << 32 | (fits ? id : 0xFFFFFFFFu),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!want) return r;
+  if (c >= L.dpk) {
+    atomicOr(&L.ctl[kRawCtlError], 1u);
+    return r;
+  }
+  const unsigned long long* e = &L.dir[(size_t)key * L.dpk + c];
+  unsigned long long v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t it = 0; (uint32_t)(v >> 32) != L.seq && it < kSpinMax; ++it) {
+    __builtin_amdgcn_s_sleep(2);
+    v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint32_t id = (uint32_t)v;
+  if ((uint32_t)(v >> 32) != L.seq || id == 0xFFFFFFFFu) {
+    atomicOr(&L.ctl[kRawCtlError], 2u);
+    return r;
+  }
+  r.t = id * L.ext + ((s >> 6) & (L.ext - 1u));
+  r.l = s & 63u;
+  r.tb = L.tiles + (size_t)r.t * (kRawTileGran * 512);
+  r.ok = true;
+  return r;
+}
+
+// One lane's request into its slot: meta word, order entry, the tile's data
+// offset (slot 0) and, for walked strings, the units (emit) and the tile's
+// tail (atomicMax on units | tail << 16, zeroed per sub-batch).
+template <class Emit>
+__device__ __forceinline__ void raw_fill(const RawLayoutDev& L, const RawSlot& sl, uint32_t i, uint32_t rem,
+                                         uint32_t flags, uint32_t units, uint32_t len, Emit emit) {
+  reinterpret_cast<uint2*>(sl.tb)[sl.l] = make_uint2(rem, flags << 24);
+  L.order[(size_t)sl.t * 64 + sl.l] = i;
+  if (sl.l == 0) L.ttab[sl.t].at = sl.t * kRawTileGran;
+  if (units) {
+    emit(reinterpret_cast<uint4*>(sl.tb + 512) + sl.l);
+    atomicMax(&L.ttab[sl.t].units, units | (len - 16u * (units - 1u)) << 16);
+  }
+}
+
+// Append the lanes with `take` to a request list (count at *cnt): one atomic
+// per wave.
+__device__ __forceinline__ void list_append(uint32_t* list, uint32_t* cnt, bool take, uint32_t i, uint32_t lane) {
+  const unsigned long long m = __ballot(take);
+  if (!m) return;
+  const int first = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if ((int)lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, first, 64);
+  if (take) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = i;
+}
+// ---- the scan: parse, program, string, slot and tile ---------------------
+// One lane per request, a wave's 64 heads (lists) staged in LDS: parse over
+// the structural bitmaps, look the program up, and put the request straight
+// into its slot of the device-built batch — class-coded string units, meta
+// word, order entry.  A request whose walked string passes the slot
+// (CG_HTTP_SLOT_BYTES) goes on the walk list; one outside its wave's stage on
+// the deferred list (raw_defer_kernel).  kLists: header lists, not heads.
+template <bool kLists, bool kLdsTabs>
+__global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, const uint8_t* __restrict__ raw_g,
+                                                               const uint64_t* __restrict__ off, size_t n,
+                                                               const uint32_t* __restrict__ policy,
+                                                               const uint8_t* __restrict__ ingress,
+                                                               const uint16_t* __restrict__ port,
+                                                               const uint32_t* __restrict__ remote, RawLayoutDev L) {
+  extern __shared__ uint32_t lds_[];
+  lds_u32* lds = (lds_u32*)lds_;
+  glb_u8* raw = (glb_u8*)raw_g;
+  const uint32_t F = max(R.nfields, 1u), wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  lds_u32* sp = lds + threadIdx.x;  // this lane's spans: sp[f * kRawThreads]
+  lds_u8* stage = wave_stage(lds, F, wave);
+  lds_u32* masks = wave_masks(lds, F, wave);
+  lds_u8* tct = tchar_table(lds, F);
+  for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = kLists ? list_stop(b, R.raw_values) : !tchar(b);
+  // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
+  using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
+  Tabs T;
+  if constexpr (kLdsTabs) {
+    const RawTableWords w = raw_table_words(R);
+    lds_u32* t = raw_tables(lds, F);
+    lds_u32* tfs = t + w.nk;
+    lds_u32* tfn = tfs + w.fs;
+    lds_u32* tpk = tfn + w.fn;
+    lds_u32* tpv = tpk + w.ph;
+    lds_u32* twb = tpv + w.ph;
+    lds_u32* tdf = twb + w.wb;
+    for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
+    for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
+      uint32_t v = 0;
+      for (uint32_t j = 0; j < 4; ++j)
+        if (4 * k + j < R.fnames_bytes) v |= (uint32_t)R.fnames[4 * k + j] << (8 * j);
+      tfn[k] = v;
+    }
+    for (uint32_t k = threadIdx.x; k < w.ph; k += blockDim.x) {
+      tpk[k] = R.phash_keys[k];
+      tpv[k] = R.phash_vals[k];
+    }
+    for (uint32_t k = threadIdx.x; k < w.wb; k += blockDim.x) twb[k] = R.walk_bits[k];
+    for (uint32_t k = threadIdx.x; k < w.df; k += blockDim.x) tdf[k] = R.dflt[k];
+    T = LdsTabs{t, tfs, tpk, tpv, twb, tdf, (const lds_u8*)tfn};
+  } else {
+    T = GlbTabs{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+                (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+  }
+  __syncthreads();
+  // software pipeline per wave: iteration k parses stage k from LDS while the
+  // stage of k + 1 is in flight into registers and the inputs of k + 2 load
+  const size_t gstride = (size_t)gridDim.x * kRawThreads;
+  size_t base = (size_t)blockIdx.x * kRawThreads;
+  RawIn cur = raw_in(off, policy, ingress, port, remote, base + wave * 64 + lane, n);
+  RawIn nxt = raw_in(off, policy, ingress, port, remote, base + gstride + wave * 64 + lane, n);
+  StageRegs S;
+  stage_load(raw, cur, lane, S, off);
+  for (; base < n; base += gstride) {
+    const size_t i0 = base + (size_t)wave * 64;
+    if (i0 >= n) break;  // wave-uniform
+    const size_t i = i0 + lane;
+    const bool live = i < n;
+    const RawIn nn = raw_in(off, policy, ingress, port, remote, base + 2 * gstride + wave * 64 + lane, n);
+    const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing() != 0, cur.port()) : kProgDeny;
+    // stage k: registers → LDS (the previous iteration's reads are done)
+    wave_sync();
+    stage_store(S, stage, lane);
+    const uint64_t sbase = S.base;
+    const uint32_t slen = S.len;
+    // stage k + 1 into registers, under this iteration's parse
+    stage_load(raw, nxt, lane, S, off);  // (past n: no bytes, nothing staged)
+    wave_sync();
+    if (kLists) build_masks_lists(stage, slen, tct, masks, lane);
+    else build_masks(stage, slen, tct, masks, lane);
+    wave_sync();
+    // every request but an unknown policy's is parsed: a head the codec
+    // rejects is denied in any program (flagged malformed)
+    const uint32_t hn = cur.len;
+    const uint64_t ga = (uint64_t)(uintptr_t)(raw + cur.a);
+    const bool in = ga >= sbase && ga + hn <= sbase + slen;
+    const bool defer = live && prog != kProgDeny && !in;
+    list_append(L.dlist, &L.ctl[kRawCtlDefer], defer, (uint32_t)i, lane);
+    const uint32_t hs = (uint32_t)(ga - sbase);
+    uint32_t flags = cur.ing() ? CG_HTTP_F_INGRESS : 0u, units = 0, len = 0, last = 0;
+    bool walk = false;
+    Parsed P;
+    P.present = P.vsum = 0;
+    if (live && !defer && prog != kProgDeny) {
+      const bool ok = kLists ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
+                             : parse_head_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P);
+      if (!ok) {
+        flags |= CG_HTTP_F_MALFORMED;
+      } else if (walked_t(R, T, prog)) {
+        len = walked_len(R, P, &last);
+        if (len > CG_HTTP_SLOT_BYTES) walk = true;
+        else units = (len + 15) / 16;
+      }
+    }
+    const bool want = live && !defer && !walk;
+    const RawSlot sl = raw_slot(L, want, group_of(R, prog) * kRawUnits + units, prog);
+    walk |= want && !sl.ok;
+    list_append(L.walk, &L.ctl[kRawCtlWalk], walk, (uint32_t)i, lane);
+    if (want && sl.ok) {
+      raw_fill(L, sl, (uint32_t)i, cur.rem, flags, units, len, [&](uint4* dst) {
+        TileOut o(dst, R.codes + (size_t)prog * 256);
+        emit_stage(R, stage, hs, sp, kRawThreads, P, last, o);
+      });
+    }
+    cur = nxt;
+    nxt = nn;
+  }
+}
+
+// ---- the deferred requests (heads / lists not inside their wave's stage:
+// long ones), one lane each, read from HBM through HeadReader with the tables
+// in global memory, into their slots as the scan does.
+template <bool kLists>
+__global__ __launch_bounds__(kRawThreads) void raw_defer_dl_kernel(HttpRawDev R, const uint8_t* __restrict__ raw,
+                                                                const uint64_t* __restrict__ off,
+                                                                const uint32_t* __restrict__ policy,
+                                                                const uint8_t* __restrict__ ingress,
+                                                                const uint16_t* __restrict__ port,
+                                                                const uint32_t* __restrict__ remote, RawLayoutDev L) {
+  extern __shared__ uint32_t lds_[];
+  lds_u32* sp = (lds_u32*)lds_ + threadIdx.x;
+  const GlbTabs T{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+                  (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+  const uint32_t nd = L.ctl[kRawCtlDefer], lane = threadIdx.x & 63;
+  const uint32_t gs = gridDim.x * kRawThreads;
+  for (uint32_t base = blockIdx.x * kRawThreads; base < nd; base += gs) {  // uniform per workgroup
+    const uint32_t j = base + threadIdx.x;
+    const bool live = j < nd;
+    const uint32_t i = live ? L.dlist[j] : 0u;
+    const uint64_t a = off[i], b = off[i + 1];
+    const uint32_t hn = b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
+    const uint32_t prog = live ? lookup_prog(R, T, policy[i], ingress[i] != 0, port[i]) : kProgDeny;
+    HeadReader hr((glb_u8*)raw + a, hn, (const lds_u8*)0, false);
+    uint32_t flags = ingress[i] ? CG_HTTP_F_INGRESS : 0u, units = 0, len = 0, last = 0;
+    bool walk = false;
+    if (live) {
+      // a list's spans are 16-bit offsets: longer lists (past Envoy's 60 KiB
+      // header limit) are rejected
+      const bool ok = kLists ? hn <= kFieldsMaxList && parse_list_bytes(R, T, hr, sp, kRawThreads)
+                             : parse_head(R, T, hr, sp, kRawThreads);
+      if (!ok) {
+        flags |= CG_HTTP_F_MALFORMED;
+      } else if (walked(R, prog)) {
+        len = string_len(R, sp, kRawThreads, &last);
+        if (len > CG_HTTP_SLOT_BYTES) walk = true;
+        else units = (len + 15) / 16;
+      }
+    }
+    const bool want = live && !walk;
+    const RawSlot sl = raw_slot(L, want, group_of(R, prog) * kRawUnits + units, prog);
+    walk |= want && !sl.ok;
+    list_append(L.walk, &L.ctl[kRawCtlWalk], walk, i, lane);
+    if (want && sl.ok) {
+      raw_fill(L, sl, i, remote[i], flags, units, len, [&](uint4* dst) {
+        TileOut o(dst, R.codes + (size_t)prog * 256);
+        emit_reader(R, hr, sp, kRawThreads, last, o);
+      });
+    }
+  }
+}
+
+// ---- the batch's tables, one workgroup: each key's last chunk gets its tile
+// count and its last tile's free slots become padding (meta PAD, order
+// 0xFFFFFFFF, zero units); the chunk table, grouped by program (so a
+// workgroup's run of chunks shares the staged program block), and the header
+// go to the front of the batch.
+constexpr uint32_t kSealThreads = 1024;
+__global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, RawLayoutDev L, uint8_t* __restrict__ batch,
+                                                                uint32_t epoch, uint64_t ttab_off, uint64_t tiles_off,
+                                                                uint64_t total_bytes, uint32_t sort) {
+  extern __shared__ uint32_t sh[];  // [group counts][group cursors] (sort)
+  const uint32_t G = R.nprogs + 2, tid = threadIdx.x;
+  const uint32_t nch = min(L.ctl[kRawCtlChunks], L.maxchunks);
+  for (uint32_t k = tid; k < L.nkeys; k += kSealThreads) {
+    const uint32_t cnt = L.kcnt[(size_t)k * kRawCntStride];
+    if (!cnt) continue;
+    const uint32_t c = (cnt - 1) >> L.cshift;
+    if (c >= L.dpk) continue;
+    const unsigned long long v = L.dir[(size_t)k * L.dpk + c];
+    const uint32_t id = (uint32_t)v;
+    if ((uint32_t)(v >> 32) != L.seq || id >= L.maxchunks) continue;
+    const uint32_t used = cnt - (c << L.cshift), nt = (used + 63) >> 6;
+    L.chunks[id].ntiles = nt;
+    const uint32_t t = id * L.ext + nt - 1, units = k % kRawUnits;
+    uint8_t* tb = L.tiles + (size_t)t * (kRawTileGran * 512);
+    for (uint32_t l = used - (nt - 1) * 64; l < 64; ++l) {
+      reinterpret_cast<uint2*>(tb)[l] = make_uint2(0, CG_HTTP_F_PAD << 24);
+      L.order[(size_t)t * 64 + l] = 0xFFFFFFFFu;
+      for (uint32_t u = 0; u < units; ++u) reinterpret_cast<uint4*>(tb + 512)[u * 64 + l] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  HttpChunk* dst = reinterpret_cast<HttpChunk*>(batch + sizeof(HttpBatchHeader));
+  auto group = [&](uint32_t prog) { return prog < R.nprogs ? prog : R.nprogs + (prog == kProgAllow ? 0u : 1u); };
+  if (sort) {
+    uint32_t* cntg = sh;
+    uint32_t* cur = sh + G;
+    for (uint32_t g = tid; g < G; g += kSealThreads) cntg[g] = 0;
+    __syncthreads();
+    for (uint32_t id = tid; id < nch; id += kSealThreads) atomicAdd(&cntg[group(L.chunks[id].prog)], 1u);
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t run = 0;
+      for (uint32_t g = 0; g < G; ++g) {
+        cur[g] = run;
+        run += cntg[g];
+      }
+    }
+    __syncthreads();
+    for (uint32_t id = tid; id < nch; id += kSealThreads) {
+      const HttpChunk ch = L.chunks[id];
+      dst[atomicAdd(&cur[group(ch.prog)], 1u)] = HttpChunk{ch.prog, ch.first_tile, ch.ntiles, 0};
+    }
+  } else {
+    for (uint32_t id = tid; id < nch; id += kSealThreads) {
+      const HttpChunk ch = L.chunks[id];
+      dst[id] = HttpChunk{ch.prog, ch.first_tile, ch.ntiles, 0};
+    }
+  }
+  if (tid == 0) {
+    HttpBatchHeader h{};
+    h.magic = kBatchMagic;
+    h.epoch = epoch;
+    h.nchunks = nch;
+    h.ntiles = L.maxchunks * L.ext;
+    h.tiles_off = tiles_off;
+    h.nslots = (uint64_t)h.ntiles * 64;
+    h.ttab_off = ttab_off;
+    h.total_bytes = total_bytes;
+    h.arena_bytes = 0;
+    *reinterpret_cast<HttpBatchHeader*>(batch) = h;
+  }
+}
+
+// ---- the walk list: requests whose walked string passes the slot (and any
+// the layout could not take), one lane each — re-parsed from HBM, the string
+// built on the fly through the program's code map and walked over the
+// program's tables in global memory; the verdict, its counters and rule hit
+// as http_kernel gives them (kernels_http.hip http_tiles).
+__device__ __forceinline__ uint32_t walk_request(const HttpDev& T, const HttpRawDev& R, const HttpProg& pg,
+                                                 uint32_t prog, HeadReader& hr, const lds_u32* sp, uint32_t stride,
+                                                 uint32_t remote) {
+  using namespace walk;
+  const uint32_t* blk = T.cells + pg.cell_begin;
+  const bool rebased = pg.flags & kProgRebased;
+  const uint8_t* lut = R.codes + (size_t)prog * 256;
+  uint32_t last;
+  (void)string_len(R, sp, stride, &last);
+  const uint32_t row = remote_row(blk, pg, remote), W = pg.mask_words;
+  uint32_t hit = kNoHit;
+  for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
+    const HttpPart pt = T.parts[pg.part_begin + pi];
+    const bool cls = pt.mode == kPartClass;
+    const uint32_t* cells = rebased ? blk : T.cells + pt.walk_off;
+    uint32_t st = pt.start;
+    auto stp = [&](uint32_t b) {
+      const uint32_t x = lut[b];
+      st = cls ? step<true>(cells, pt.dead, st, x) : step<false>(cells, pt.dead, st, x);
+    };
+    for (uint32_t f = 0; f < last && st != pt.dead; ++f) {
+      const uint32_t s = sp[f * stride];
+      if (s == kAbsentSpan) {
+        stp(1u);
+      } else {
+        const uint32_t a = s >> 16, len = s & 0xFFFFu;
+        for (uint32_t k = 0; k < len && st != pt.dead; ++k) stp(hr.at(a + k));
+      }
+      stp(0u);
+    }
+    if (last < R.nfields) stp(2u);
+    const uint32_t lab = cls ? state_label<true>(cells, st) : state_label<false>(cells, st);
+    if (lab != 0xFFFFu) hit = min(hit, first_meet(blk, pt.acc_off + lab * 2 * W, row, W));
+  }
+  if (pg.flags & kProgHasAlways) hit = min(hit, first_meet(blk, pg.always_off, row, W));
+  return hit;
+}
+
+template <bool kLists>
+__global__ __launch_bounds__(kRawThreads) void raw_walk_kernel(HttpDev HT, HttpRawDev R, const uint8_t* __restrict__ raw,
+                                                               const uint64_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ policy,
+                                                               const uint8_t* __restrict__ ingress,
+                                                               const uint16_t* __restrict__ port,
+                                                               const uint32_t* __restrict__ remote, RawLayoutDev L,
+                                                               uint8_t* __restrict__ out) {
+  extern __shared__ uint32_t lds_[];
+  lds_u32* sp = (lds_u32*)lds_ + threadIdx.x;
+  const GlbTabs T{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+                  (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+  const uint32_t nw = L.ctl[kRawCtlWalk];
+  for (uint32_t j = blockIdx.x * kRawThreads + threadIdx.x; j < nw; j += gridDim.x * kRawThreads) {
+    const uint32_t i = L.walk[j];
+    const uint64_t a = off[i], b = off[i + 1];
+    const uint32_t hn = b > a ? (uint32_t)min<uint64_t>(b - a, 0xFFFFFFFFull) : 0u;
+    const uint32_t prog = lookup_prog(R, T, policy[i], ingress[i] != 0, port[i]);
+    HeadReader hr((glb_u8*)raw + a, hn, (const lds_u8*)0, false);
+    const bool ok = prog == kProgDeny ? false
+                    : kLists          ? hn <= kFieldsMaxList && parse_list_bytes(R, T, hr, sp, kRawThreads)
+                                      : parse_head(R, T, hr, sp, kRawThreads);
+    uint32_t v = 0;
+    if (prog == kProgAllow) {
+      v = ok;  // no policy for the port
+    } else if (prog < R.nprogs) {
+      const HttpProg pg = HT.progs[prog];
+      if (pg.flags & kProgAllowAll) {
+        v = ok;
+        if (ok) atomicAdd(&HT.counters[2 * prog], 1ull);
+      } else if (ok) {
+        const uint32_t hit = walk_request(HT, R, pg, prog, hr, sp, kRawThreads, remote[i]);
+        v = hit != walk::kNoHit;
+        atomicAdd(&HT.counters[2 * prog + (v ? 0 : 1)], 1ull);
+        if (v) atomicAdd(&HT.rule_hits[pg.rule_base + hit], 1ull);
+      }
+    }
+    out[i] = (uint8_t)v;
+  }
+}
 unsigned grid_for(size_t n, int cus, unsigned per_cu) {
   const size_t want = (n + kRawThreads - 1) / kRawThreads;
   return (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)cus * per_cu));
@@ -1402,6 +1912,13 @@ ScanKernel scan_kernel_for(const HttpRawDev& R, bool lists) {
   const bool tabs = lds_tables_fit(R);
   if (lists) return tabs ? raw_scan_kernel<true, true> : raw_scan_kernel<true, false>;
   return tabs ? raw_scan_kernel<false, true> : raw_scan_kernel<false, false>;
+}
+
+using DlScanKernel = decltype(&raw_scan_dl_kernel<false, false>);
+DlScanKernel dl_scan_kernel_for(const HttpRawDev& R, bool lists) {
+  const bool tabs = lds_tables_fit(R);
+  if (lists) return tabs ? raw_scan_dl_kernel<true, true> : raw_scan_dl_kernel<true, false>;
+  return tabs ? raw_scan_dl_kernel<false, true> : raw_scan_dl_kernel<false, false>;
 }
 
 }  // namespace
@@ -1483,6 +2000,73 @@ int launch_http_raw_build(const HttpRawDev& R, const HttpRawRun* runs, uint32_t 
       (unsigned)std::max<size_t>(1, std::min<size_t>((ntiles + waves - 1) / waves, (size_t)cus * 8));
   hipLaunchKernelGGL(raw_build_kernel, dim3(grid), dim3(kRawThreads), 0, (hipStream_t)stream, R, runs, nruns, ntiles,
                      ttab, tiles, order, sbuf, arena, arena_cursor);
+  return (int)hipGetLastError();
+}
+
+// As http_raw_grid, for raw_scan_dl_kernel.
+size_t http_raw_dl_grid(const HttpRawDev& R, bool lists, size_t n, int cus) {
+  const DlScanKernel kern = dl_scan_kernel_for(R, lists);
+  const size_t lds = raw_lds(R, false, false);
+  static std::mutex mu;
+  static std::map<std::tuple<int, const void*, size_t>, int> occ;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int per_cu = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = occ.find({dev, (const void*)kern, lds});
+    if (it == occ.end()) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kRawThreads, lds) != hipSuccess || nb < 1)
+        nb = 1;
+      it = occ.emplace(std::make_tuple(dev, (const void*)kern, lds), nb).first;
+    }
+    per_cu = it->second;
+  }
+  return grid_for(n, cus, (unsigned)per_cu);
+}
+
+int launch_http_raw_dl_scan(const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off, size_t n,
+                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, const uint32_t* remote,
+                         const RawLayoutDev& L, void* stream, int cus) {
+  if (!n) return 0;
+  const size_t lds = raw_lds(R, false, false);
+  const DlScanKernel kern = dl_scan_kernel_for(R, lists);
+  const unsigned grid = (unsigned)http_raw_dl_grid(R, lists, n, cus);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kRawThreads), lds, (hipStream_t)stream, R, raw, off, n, policy, ingress,
+                     port, remote, L);
+  // the deferred requests (their count stays on the device: a small grid
+  // that exits at once when there are none)
+  const size_t dlds = (size_t)std::max(R.nfields, 1u) * kRawThreads * 4;
+  const auto dk = lists ? raw_defer_dl_kernel<true> : raw_defer_dl_kernel<false>;
+  (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(dk, dim3((unsigned)std::max(1, cus) * 2), dim3(kRawThreads), dlds, (hipStream_t)stream, R, raw, off,
+                     policy, ingress, port, remote, L);
+  return (int)hipGetLastError();
+}
+
+bool http_raw_seal_sorts(const HttpRawDev& R) { return ((size_t)R.nprogs + 2) * 8 <= 64 * 1024; }
+
+int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch, uint32_t epoch, uint64_t ttab_off,
+                         uint64_t tiles_off, uint64_t total_bytes, void* stream) {
+  const bool sort = http_raw_seal_sorts(R);
+  const size_t lds = sort ? ((size_t)R.nprogs + 2) * 8 : 0;
+  (void)hipFuncSetAttribute((const void*)raw_seal_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(raw_seal_kernel, dim3(1), dim3(kSealThreads), lds, (hipStream_t)stream, R, L, (uint8_t*)batch,
+                     epoch, ttab_off, tiles_off, total_bytes, (uint32_t)sort);
+  return (int)hipGetLastError();
+}
+
+int launch_http_raw_walk(const HttpDev& T, const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off,
+                         const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, const uint32_t* remote,
+                         const RawLayoutDev& L, uint8_t* out, void* stream, int cus) {
+  const size_t lds = (size_t)std::max(R.nfields, 1u) * kRawThreads * 4;
+  const auto wk = lists ? raw_walk_kernel<true> : raw_walk_kernel<false>;
+  (void)hipFuncSetAttribute((const void*)wk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(wk, dim3((unsigned)std::max(1, cus) * 2), dim3(kRawThreads), lds, (hipStream_t)stream, T, R, raw,
+                     off, policy, ingress, port, remote, L, out);
   return (int)hipGetLastError();
 }
 

@@ -122,6 +122,10 @@ void* StagingSlot::host_buf(int i, size_t bytes) {
 }
 
 StagingSlot::~StagingSlot() {
+  if (raw_ev) {
+    (void)hipEventSynchronize((hipEvent_t)raw_ev);
+    (void)hipEventDestroy((hipEvent_t)raw_ev);
+  }
   if (stream) {
     (void)hipStreamSynchronize((hipStream_t)stream);
     (void)hipStreamDestroy((hipStream_t)stream);
