@@ -415,7 +415,8 @@ std::string field(const char* name, const std::string& escaped) {
 }
 
 // PolicyMatches (connection.go:176-179) for the request records of the
-// queued OnData calls, as one host-staged GPU batch.  Caller holds inst.mu.
+// queued OnData calls, as one host-staged GPU batch.  Caller holds inst.mu
+// (decide's flusher).
 // Returns false on an engine error.
 bool gpu_verdicts(Instance& inst, const std::vector<VerdictReq*>& reqs) {
   size_t n = 0;
@@ -481,10 +482,12 @@ bool decide(Conn& c, const std::vector<std::string>& recs, std::vector<uint8_t>*
     std::vector<VerdictReq*> batch;
     batch.swap(inst.queue);
     lk.unlock();
-    bool ok;
-    {
+    bool ok = false;
+    try {  // the waiters must be released whatever happens here
       std::lock_guard<std::mutex> g(inst.mu);
       ok = gpu_verdicts(inst, batch);
+    } catch (...) {
+      ok = false;
     }
     lk.lock();
     for (VerdictReq* r : batch) {
