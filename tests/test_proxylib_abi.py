@@ -15,6 +15,7 @@ from cilium_amd import _native as N
 HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "cilium_proxylib.h")
 MORE, PASS, DROP = 0, 1, 2
 F_OK, F_UNKNOWN_PARSER, F_UNKNOWN_CONNECTION, F_INVALID_ADDRESS, F_INVALID_INSTANCE = 0, 3, 4, 5, 6
+F_UNKNOWN_ERROR = 7
 
 
 class GoString(C.Structure):
@@ -318,3 +319,43 @@ def test_gpu_ondata_concurrent_connections_share_batches():
     assert not errors, errors[:3]
     calls, batches = c1.value - c0.value, b1.value - b0.value
     assert calls >= 16 * 60 * 0.9 and batches < calls, (calls, batches)
+
+
+def test_ondata_combiner_concurrency_without_device():
+    """The flat-combining batcher under 16 concurrent connections on a
+    handle without a GPU: every call with request frames reaches the shared
+    queue, each flush fails (no device) and releases all the calls it took —
+    every OnData returns the engine error, none waits forever, and the
+    instance's counts add up (cg_proxylib_stats: calls = calls made, batches
+    <= calls)."""
+    import threading
+
+    inst = open_module([(b"node-id", b"cpu-combiner")], "-1")
+    assert inst != 0
+    t = json.dumps(R2D2_POLICIES).encode()
+    assert N.lib.cg_proxylib_policy_update(inst, t, len(t)) == N.CG_OK
+    rcs, per = [], 40
+
+    def worker(k):
+        c = Conn(inst, policy=b"cp2", src=k)
+        assert c.rc == F_OK
+        for j in range(per):
+            rc, ops = c.on_data([b"READ f%d\r\nWRITE g%d\r\n" % (j, j)], cap=3)
+            rcs.append((rc, ops))
+        c.close()
+
+    b0, c0 = C.c_uint64(), C.c_uint64()
+    N.lib.cg_proxylib_stats(inst, C.byref(b0), C.byref(c0))
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join(timeout=120)
+        assert not x.is_alive(), "an OnData call never returned"
+    b1, c1 = C.c_uint64(), C.c_uint64()
+    N.lib.cg_proxylib_stats(inst, C.byref(b1), C.byref(c1))
+    _lib.CloseModule(inst)
+    assert len(rcs) == 16 * per
+    assert all(rc == F_UNKNOWN_ERROR and ops == [] for rc, ops in rcs), rcs[:3]
+    calls, batches = c1.value - c0.value, b1.value - b0.value
+    assert calls == 16 * per and 1 <= batches <= calls, (calls, batches)
