@@ -746,6 +746,35 @@ __host__ __device__ __forceinline__ uint32_t raw_tables_lds_words(const HttpRawD
   const RawTableWords w = raw_table_words(R);
   return w.nk + w.fs + w.fn + 2 * w.ph + w.wb + w.df;
 }
+// The scan's lookup tables (RawTableWords order) copied into LDS at t, or
+// their global copies (GlbTabs); the caller's barrier follows.
+__device__ __forceinline__ void stage_tables(const HttpRawDev& R, lds_u32* t, LdsTabs& T) {
+  const RawTableWords w = raw_table_words(R);
+  lds_u32* tfs = t + w.nk;
+  lds_u32* tfn = tfs + w.fs;
+  lds_u32* tpk = tfn + w.fn;
+  lds_u32* tpv = tpk + w.ph;
+  lds_u32* twb = tpv + w.ph;
+  lds_u32* tdf = twb + w.wb;
+  for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
+  for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; ++j)
+      if (4 * k + j < R.fnames_bytes) v |= (uint32_t)R.fnames[4 * k + j] << (8 * j);
+    tfn[k] = v;
+  }
+  for (uint32_t k = threadIdx.x; k < w.ph; k += blockDim.x) {
+    tpk[k] = R.phash_keys[k];
+    tpv[k] = R.phash_vals[k];
+  }
+  for (uint32_t k = threadIdx.x; k < w.wb; k += blockDim.x) twb[k] = R.walk_bits[k];
+  for (uint32_t k = threadIdx.x; k < w.df; k += blockDim.x) tdf[k] = R.dflt[k];
+  T = LdsTabs{t, tfs, tpk, tpv, twb, tdf, (const lds_u8*)tfn};
+}
+__device__ __forceinline__ void stage_tables(const HttpRawDev& R, lds_u32*, GlbTabs& T) {
+  T = GlbTabs{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+              (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+}
 // 16-byte chunks of a lane's output string: stored to dst, then dst +=
 // stride (uint4 units: a tile's next string unit, or the next arena line).
 struct Out16 {
@@ -957,33 +986,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
-  if constexpr (kLdsTabs) {
-    const RawTableWords w = raw_table_words(R);
-    lds_u32* t = lk + (lds_keys ? nk : 0u);
-    lds_u32* tfs = t + w.nk;
-    lds_u32* tfn = tfs + w.fs;
-    lds_u32* tpk = tfn + w.fn;
-    lds_u32* tpv = tpk + w.ph;
-    lds_u32* twb = tpv + w.ph;
-    lds_u32* tdf = twb + w.wb;
-    for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
-    for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
-      uint32_t v = 0;
-      for (uint32_t j = 0; j < 4; ++j)
-        if (4 * k + j < R.fnames_bytes) v |= (uint32_t)R.fnames[4 * k + j] << (8 * j);
-      tfn[k] = v;
-    }
-    for (uint32_t k = threadIdx.x; k < w.ph; k += blockDim.x) {
-      tpk[k] = R.phash_keys[k];
-      tpv[k] = R.phash_vals[k];
-    }
-    for (uint32_t k = threadIdx.x; k < w.wb; k += blockDim.x) twb[k] = R.walk_bits[k];
-    for (uint32_t k = threadIdx.x; k < w.df; k += blockDim.x) tdf[k] = R.dflt[k];
-    T = LdsTabs{t, tfs, tpk, tpv, twb, tdf, (const lds_u8*)tfn};
-  } else {
-    T = GlbTabs{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
-                (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
-  }
+  stage_tables(R, lk + (lds_keys ? nk : 0u), T);
   const uint64_t off0 = off[0];
   __syncthreads();
   // software pipeline per wave: iteration k parses stage k from LDS while the
@@ -1590,33 +1593,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
   // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
-  if constexpr (kLdsTabs) {
-    const RawTableWords w = raw_table_words(R);
-    lds_u32* t = raw_tables(lds, F);
-    lds_u32* tfs = t + w.nk;
-    lds_u32* tfn = tfs + w.fs;
-    lds_u32* tpk = tfn + w.fn;
-    lds_u32* tpv = tpk + w.ph;
-    lds_u32* twb = tpv + w.ph;
-    lds_u32* tdf = twb + w.wb;
-    for (uint32_t k = threadIdx.x; k < w.nk; k += blockDim.x) t[k] = R.nkeys[k];
-    for (uint32_t k = threadIdx.x; k < w.fn; k += blockDim.x) {
-      uint32_t v = 0;
-      for (uint32_t j = 0; j < 4; ++j)
-        if (4 * k + j < R.fnames_bytes) v |= (uint32_t)R.fnames[4 * k + j] << (8 * j);
-      tfn[k] = v;
-    }
-    for (uint32_t k = threadIdx.x; k < w.ph; k += blockDim.x) {
-      tpk[k] = R.phash_keys[k];
-      tpv[k] = R.phash_vals[k];
-    }
-    for (uint32_t k = threadIdx.x; k < w.wb; k += blockDim.x) twb[k] = R.walk_bits[k];
-    for (uint32_t k = threadIdx.x; k < w.df; k += blockDim.x) tdf[k] = R.dflt[k];
-    T = LdsTabs{t, tfs, tpk, tpv, twb, tdf, (const lds_u8*)tfn};
-  } else {
-    T = GlbTabs{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
-                (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
-  }
+  stage_tables(R, raw_tables(lds, F), T);
   __syncthreads();
   // software pipeline per wave: iteration k parses stage k from LDS while the
   // stage of k + 1 is in flight into registers and the inputs of k + 2 load
