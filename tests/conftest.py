@@ -10,6 +10,15 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "run_last: a code path with no GPU run behind it yet; runs after the rest")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Tests marked run_last go to the end of the run (stable order
+    otherwise): a fault in a path that has not run on a GPU before cannot
+    cut the verified tests' run short."""
+    items[:] = [i for i in items if i.get_closest_marker("run_last") is None] + \
+               [i for i in items if i.get_closest_marker("run_last") is not None]
 
 
 @pytest.fixture(scope="session")

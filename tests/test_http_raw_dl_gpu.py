@@ -26,7 +26,7 @@ from test_http_fields_gpu import _vary as _fields_vary
 from test_http_parse import _blob, _raw_requests
 from test_http_raw_gpu import _host_path, _oracle, _vary
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.run_last]
 
 
 @pytest.fixture
