@@ -323,6 +323,8 @@ enum : uint32_t {
   kRawCtlWalk = 1,    // requests on the walk list (raw_walk_kernel)
   kRawCtlDefer = 2,   // requests on the deferred list (heads outside their wave's stage)
   kRawCtlError = 3,   // bit 0: a chunk past the layout's bounds (its requests walked instead)
+                      // bit 1: a slot whose chunk id was not seen in time (late list)
+  kRawCtlLate = 4,    // slots on the late list
   kRawCtlWords = 16
 };
 struct RawLayoutDev {
@@ -335,8 +337,13 @@ struct RawLayoutDev {
   uint32_t* ctl;             // kRawCtl*
   uint32_t* walk;            // request indices for raw_walk_kernel
   uint32_t* dlist;           // request indices for raw_defer_kernel
+  // slots taken whose lane gave up waiting for the chunk id (key << 32 | s):
+  // the request is walked, and raw_seal_kernel pads the slot once every id
+  // is published, so http_kernel never reads an unfilled slot
+  unsigned long long* late;
   uint32_t dpk, ext, cshift; // directory entries per key, tiles per chunk, log2(64 * ext)
   uint32_t seq, maxchunks, nkeys;
+  uint32_t spin;             // polls of a chunk id before giving up (CILIUM_GPU_RAW_SPIN, tests)
 };
 
 CG_HD inline uint32_t hash32(uint32_t x) {

@@ -104,7 +104,7 @@ class PinnedMem {
 // device buffers and pinned host buffers, so host calls make no hipMalloc /
 // hipFree and copy with async DMA instead of pageable hipMemcpy.
 struct StagingSlot {
-  static constexpr int kBufs = 26;  // 0..7 host staging, 8..18 the raw HTTP path's workspace, 19..25 its device-layout sequence's
+  static constexpr int kBufs = 27;  // 0..7 host staging, 8..18 the raw HTTP path's workspace, 19..26 its device-layout sequence's
   void* stream = nullptr;  // hipStream_t
   DevMem dev[kBufs];
   PinnedMem host[kBufs];

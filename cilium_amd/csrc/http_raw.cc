@@ -351,7 +351,7 @@ uint32_t floor_pow2(uint32_t x) {
 
 // One sub-batch of the device-layout path, enqueued on `st`: clear the
 // counters and tile table, scan, seal, http_kernel, walk.  The workspace is
-// the slot's buffers 19..25 (the default sequence's are 8..18).
+// the slot's buffers 19..26 (the default sequence's are 8..18).
 void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists, const uint8_t* d_raw,
                   const uint64_t* d_off, size_t m, const uint32_t* d_policy, const uint8_t* d_ingress,
                   const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, hipStream_t st) {
@@ -391,6 +391,11 @@ void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists
   L.order = (uint32_t*)sl.dev_buf(23, maxtiles * 64 * 4);
   L.walk = (uint32_t*)sl.dev_buf(24, m * 4);
   L.dlist = (uint32_t*)sl.dev_buf(25, m * 4);
+  L.late = (unsigned long long*)sl.dev_buf(26, m * 8);
+  // polls of a chunk id before a lane gives up (~15 ms: a legitimate wait is
+  // microseconds); CILIUM_GPU_RAW_SPIN lowers it so tests reach the late path
+  L.spin = 1u << 14;
+  if (const char* v = getenv("CILIUM_GPU_RAW_SPIN")) L.spin = (uint32_t)std::min<unsigned long long>(L.spin, strtoull(v, nullptr, 10));
   L.dpk = dpk;
   L.ext = ext;
   L.cshift = cshift;

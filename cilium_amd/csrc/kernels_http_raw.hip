@@ -1450,10 +1450,10 @@ __device__ __forceinline__ void emit_reader(const HttpRawDev& R, HeadReader& hr,
 // Every lane with `want` takes the next slot of its bucket key; the first
 // slot of a chunk takes a chunk id and publishes it (never waiting first), the
 // others wait for their chunk's id.  ok = false: the layout's bounds were
-// passed or the chunk's id never came (neither happens for the sizes
-// http_raw.cc reserves; ctl[kRawCtlError] records it) — the lane's request
-// is walked by raw_walk_kernel instead.
-constexpr uint32_t kSpinMax = 1u << 14;  // ~15 ms of polling: a legitimate wait is microseconds
+// passed or the chunk's id was not seen within L.spin polls (neither happens
+// for the sizes http_raw.cc reserves; ctl[kRawCtlError] records it) — the
+// lane's request is walked by raw_walk_kernel instead, and a slot it had
+// taken in a chunk goes on the late list for raw_seal_kernel to pad.
 struct RawSlot {
   uint8_t* tb;  // the tile's data
   uint32_t t, l;
@@ -1479,15 +1479,18 @@ __device__ __forceinline__ RawSlot raw_slot(const RawLayoutDev& L, bool want, ui
   }
   const unsigned long long* e = &L.dir[(size_t)key * L.dpk + c];
   unsigned long long v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t it = 0; (uint32_t)(v >> 32) != L.seq && it < kSpinMax; ++it) {
+  for (uint32_t it = 0; (uint32_t)(v >> 32) != L.seq && it < L.spin; ++it) {
     __builtin_amdgcn_s_sleep(2);
     v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint32_t id = (uint32_t)v;
-  if ((uint32_t)(v >> 32) != L.seq || id == 0xFFFFFFFFu) {
+  if ((uint32_t)(v >> 32) != L.seq) {  // not seen in time: the seal pads the slot
     atomicOr(&L.ctl[kRawCtlError], 2u);
+    const uint32_t j = atomicAdd(&L.ctl[kRawCtlLate], 1u);
+    L.late[j] = (unsigned long long)key << 32 | s;  // (one per slot taken: j < slots <= capacity)
     return r;
   }
+  if (id == 0xFFFFFFFFu) return r;  // a chunk past maxchunks (bit 0 set): not in the chunk table
   r.t = id * L.ext + ((s >> 6) & (L.ext - 1u));
   r.l = s & 63u;
   r.tb = L.tiles + (size_t)r.t * (kRawTileGran * 512);
@@ -1694,6 +1697,23 @@ __global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, Ra
       L.order[(size_t)t * 64 + l] = 0xFFFFFFFFu;
       for (uint32_t u = 0; u < units; ++u) reinterpret_cast<uint4*>(tb + 512)[u * 64 + l] = make_uint4(0, 0, 0, 0);
     }
+  }
+  // the late slots (taken, never filled: their requests are walked): every
+  // chunk id is published by now, so each becomes padding in place — meta
+  // PAD (no counters), order 0xFFFFFFFF (no verdict), and the tile's data
+  // offset when it is the tile's slot 0 (whose lane writes it otherwise)
+  const uint32_t nlate = L.ctl[kRawCtlLate];
+  for (uint32_t j = tid; j < nlate; j += kSealThreads) {
+    const unsigned long long x = L.late[j];
+    const uint32_t k = (uint32_t)(x >> 32), sl = (uint32_t)x, c = sl >> L.cshift;
+    const unsigned long long v = L.dir[(size_t)k * L.dpk + c];
+    const uint32_t id = (uint32_t)v;
+    if ((uint32_t)(v >> 32) != L.seq || id >= L.maxchunks) continue;  // not in the chunk table
+    const uint32_t t = id * L.ext + ((sl >> 6) & (L.ext - 1u)), l = sl & 63u;
+    uint8_t* tb = L.tiles + (size_t)t * (kRawTileGran * 512);
+    reinterpret_cast<uint2*>(tb)[l] = make_uint2(0, CG_HTTP_F_PAD << 24);
+    L.order[(size_t)t * 64 + l] = 0xFFFFFFFFu;
+    if (l == 0) L.ttab[t].at = t * kRawTileGran;
   }
   __syncthreads();
   HttpChunk* dst = reinterpret_cast<HttpChunk*>(batch + sizeof(HttpBatchHeader));

@@ -14,6 +14,7 @@
 //
 // The policy verdicts of every request frame found in one OnData call are
 // evaluated as one batch by http_kernel (no CPU evaluation path).
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -39,7 +40,10 @@ namespace {
 // One OnData call's request records waiting for their verdicts.
 struct VerdictReq {
   const std::vector<std::string>* recs;
-  uint32_t policy;  // cg_http_policy_index of the connection's policy
+  // the connection's policy by name: the flusher resolves it under inst.mu,
+  // against the snapshot the batch is packed and decided with (the Go
+  // proxylib looks the policy up at match time, policymap.go:208-236)
+  const std::string* policy;
   bool ingress;
   uint16_t port;
   uint32_t remote;  // Matches passes SrcId (connection.go:176-179)
@@ -63,6 +67,9 @@ struct Instance {
   std::vector<VerdictReq*> queue;
   bool flushing = false;
   uint64_t batches = 0, calls = 0;  // decided batches / calls (cg_proxylib_stats)
+  // batching window (cg_proxylib_set_batching): a flusher waits until
+  // min_calls calls are queued or max_wait_us has passed since it took over
+  uint32_t min_calls = 1, max_wait_us = 0;
 };
 
 struct Conn {
@@ -420,9 +427,21 @@ std::string field(const char* name, const std::string& escaped) {
 // Returns false on an engine error.
 bool gpu_verdicts(Instance& inst, const std::vector<VerdictReq*>& reqs) {
   size_t n = 0;
-  for (const VerdictReq* r : reqs) {
+  // policy names → indices in the current snapshot; an unknown name (or no
+  // policy installed) leaves its calls all-DROP (PolicyMatches false)
+  std::map<std::string, uint32_t> idx;
+  std::vector<uint32_t> rpol(reqs.size());
+  for (size_t j = 0; j < reqs.size(); ++j) {
+    const VerdictReq* r = reqs[j];
     r->out->assign(r->recs->size(), 0);
-    n += r->recs->size();
+    auto it = idx.find(*r->policy);
+    if (it == idx.end()) {
+      uint32_t p = 0xFFFFFFFFu;
+      if (cg_http_policy_index(inst.engine, r->policy->c_str(), &p) != CG_OK) p = 0xFFFFFFFFu;
+      it = idx.emplace(*r->policy, p).first;
+    }
+    rpol[j] = it->second;
+    if (rpol[j] != 0xFFFFFFFFu) n += r->recs->size();
   }
   if (n == 0) return true;
   std::vector<uint32_t> pol, remote;
@@ -431,15 +450,18 @@ bool gpu_verdicts(Instance& inst, const std::vector<VerdictReq*>& reqs) {
   pol.reserve(n), remote.reserve(n), ing.reserve(n), port.reserve(n);
   std::string blob;
   std::vector<uint64_t> off{0};
-  for (const VerdictReq* r : reqs)
+  for (size_t j = 0; j < reqs.size(); ++j) {
+    const VerdictReq* r = reqs[j];
+    if (rpol[j] == 0xFFFFFFFFu) continue;
     for (const std::string& rec : *r->recs) {
-      pol.push_back(r->policy);
+      pol.push_back(rpol[j]);
       ing.push_back(r->ingress ? 1 : 0);
       port.push_back(r->port);
       remote.push_back(r->remote);
       blob += rec;
       off.push_back(blob.size());
     }
+  }
   if (blob.empty()) blob.push_back('\0');
   size_t nslots = 0, used = 0;
   int rc = cg_http_pack(inst.engine, n, pol.data(), ing.data(), port.data(), remote.data(),
@@ -456,8 +478,11 @@ bool gpu_verdicts(Instance& inst, const std::vector<VerdictReq*>& reqs) {
                              allow.data());
   if (rc != CG_OK) return false;
   size_t k = 0;
-  for (VerdictReq* r : reqs)
+  for (size_t j = 0; j < reqs.size(); ++j) {
+    if (rpol[j] == 0xFFFFFFFFu) continue;
+    VerdictReq* r = reqs[j];
     for (size_t i = 0; i < r->recs->size(); ++i) (*r->out)[i] = allow[k++];
+  }
   return true;
 }
 
@@ -467,18 +492,20 @@ bool decide(Conn& c, const std::vector<std::string>& recs, std::vector<uint8_t>*
   out->assign(recs.size(), 0);
   if (recs.empty()) return true;
   Instance& inst = *c.inst;
-  uint32_t pidx = 0xFFFFFFFFu;
-  // no such policy (or none installed): PolicyMatches is false → DROP
-  if (cg_http_policy_index(inst.engine, c.policy.c_str(), &pidx) != CG_OK) return true;
-  VerdictReq me{&recs, pidx, c.ingress, (uint16_t)(c.port > 0xFFFF ? 0 : c.port), c.src_id, out};
+  VerdictReq me{&recs, &c.policy, c.ingress, (uint16_t)(c.port > 0xFFFF ? 0 : c.port), c.src_id, out};
   std::unique_lock<std::mutex> lk(inst.qmu);
   inst.queue.push_back(&me);
+  if (inst.flushing || inst.min_calls > 1) inst.qcv.notify_all();  // a flusher may be waiting for company
   while (!me.done) {
     if (inst.flushing) {
       inst.qcv.wait(lk);
       continue;
     }
     inst.flushing = true;
+    if (inst.min_calls > 1 && inst.max_wait_us > 0) {  // batching window
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(inst.max_wait_us);
+      inst.qcv.wait_until(lk, until, [&] { return inst.queue.size() >= inst.min_calls; });
+    }
     std::vector<VerdictReq*> batch;
     batch.swap(inst.queue);
     lk.unlock();
@@ -594,6 +621,15 @@ int cg_proxylib_stats(uint64_t instance, uint64_t* batches, uint64_t* calls) {
   std::lock_guard<std::mutex> lk(inst->qmu);
   if (batches) *batches = inst->batches;
   if (calls) *calls = inst->calls;
+  return CG_OK;
+}
+
+int cg_proxylib_set_batching(uint64_t instance, uint32_t min_calls, uint32_t max_wait_us) {
+  auto inst = find_instance(instance);
+  if (!inst) return CG_INVALID_INSTANCE;
+  std::lock_guard<std::mutex> lk(inst->qmu);
+  inst->min_calls = min_calls ? min_calls : 1;
+  inst->max_wait_us = max_wait_us;
   return CG_OK;
 }
 

@@ -21,15 +21,15 @@ const (
 // CountersPrefilter.
 func (e *Engine) ReadCounters(what, pfOrMap uint32) ([]uint64, error) {
 	var n C.size_t
-	if err := check(C.cg_read_counters(e.h, C.uint32_t(what), C.uint32_t(pfOrMap), nil, 0, &n)); err != nil {
+	if err := call(func() C.int { return C.cg_read_counters(e.h, C.uint32_t(what), C.uint32_t(pfOrMap), nil, 0, &n) }); err != nil {
 		return nil, err
 	}
 	out := make([]uint64, int(n))
 	if n == 0 {
 		return out, nil
 	}
-	err := check(C.cg_read_counters(e.h, C.uint32_t(what), C.uint32_t(pfOrMap), (*C.uint64_t)(unsafe.Pointer(&out[0])),
-		n, &n))
+	err := call(func() C.int { return C.cg_read_counters(e.h, C.uint32_t(what), C.uint32_t(pfOrMap), (*C.uint64_t)(unsafe.Pointer(&out[0])),
+		n, &n) })
 	return out, err
 }
 
@@ -38,9 +38,9 @@ func (e *Engine) ReadCounters(what, pfOrMap uint32) ([]uint64, error) {
 func (e *Engine) CountersDevice(what, pfOrMap uint32) (unsafe.Pointer, int, error) {
 	var p unsafe.Pointer
 	var n C.size_t
-	err := check(C.cg_counters_device_ptr(e.h, C.uint32_t(what), C.uint32_t(pfOrMap), &p, &n))
+	err := call(func() C.int { return C.cg_counters_device_ptr(e.h, C.uint32_t(what), C.uint32_t(pfOrMap), &p, &n) })
 	return p, int(n), err
 }
 
 // ResetCounters zeroes every counter of the handle.
-func (e *Engine) ResetCounters() error { return check(C.cg_reset_counters(e.h)) }
+func (e *Engine) ResetCounters() error { return call(func() C.int { return C.cg_reset_counters(e.h) }) }

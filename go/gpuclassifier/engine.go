@@ -24,6 +24,7 @@ import "C"
 
 import (
 	"fmt"
+	"runtime"
 	"strconv"
 	"unsafe"
 )
@@ -58,7 +59,13 @@ type Error struct {
 
 func (e *Error) Error() string { return fmt.Sprintf("libciliumgpu [%d]: %s", e.Code, e.Msg) }
 
-func check(rc C.int) error {
+// call runs one engine call and, on failure, reads cg_last_error on the same
+// OS thread: the message is thread-local in the library (runtime.cc), and a
+// goroutine may move between threads from one cgo call to the next.
+func call(f func() C.int) error {
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	rc := f()
 	if rc == C.CG_OK {
 		return nil
 	}
@@ -76,9 +83,15 @@ func Open(device int) (*Engine, error) {
 	defer C.free(unsafe.Pointer(k))
 	defer C.free(unsafe.Pointer(v))
 	kv := C.cg_kv{key: k, value: v}
-	h := C.cg_open(&kv, 1, 0)
-	if h == 0 { // OpenModule convention: 0 = error
-		return nil, &Error{Code: NoDevice, Msg: C.GoString(C.cg_last_error())}
+	var h C.uint64_t
+	err := call(func() C.int {
+		if h = C.cg_open(&kv, 1, 0); h == 0 { // OpenModule convention: 0 = error
+			return C.CG_NO_DEVICE
+		}
+		return C.CG_OK
+	})
+	if err != nil {
+		return nil, err
 	}
 	return &Engine{h: h}, nil
 }
@@ -95,7 +108,7 @@ func (e *Engine) Close() {
 func Version() string { return C.GoString(C.cg_version()) }
 
 // Sync waits for the handle's stream.
-func (e *Engine) Sync() error { return check(C.cg_sync(e.h)) }
+func (e *Engine) Sync() error { return call(func() C.int { return C.cg_sync(e.h) }) }
 
 // RegexValidate checks a pattern without compiling it: go = Go 1.10
 // regexp.Compile's syntax (PortRuleHTTP.Sanitize,
@@ -108,7 +121,7 @@ func RegexValidate(re string, goSyntax bool) error {
 	}
 	cs := C.CString(re)
 	defer C.free(unsafe.Pointer(cs))
-	return check(C.cg_regex_validate(cs, C.size_t(len(re)), flavour))
+	return call(func() C.int { return C.cg_regex_validate(cs, C.size_t(len(re)), flavour) })
 }
 
 // bytesPtr is the address of a byte slice's first element, nil when empty.

@@ -12,7 +12,7 @@ import "unsafe"
 // Envoy's NetworkPolicyMap::onConfigUpdate compiles.  All-or-nothing: on
 // PolicyRejected the previous snapshot keeps serving.
 func (e *Engine) UpdateNPDS(discoveryResponse []byte) error {
-	return check(C.cg_http_policy_update_npds(e.h, bytesPtr(discoveryResponse), C.size_t(len(discoveryResponse))))
+	return call(func() C.int { return C.cg_http_policy_update_npds(e.h, bytesPtr(discoveryResponse), C.size_t(len(discoveryResponse))) })
 }
 
 // UpdateNetworkPoliciesJSON installs the protobuf-JSON form of the same
@@ -20,7 +20,7 @@ func (e *Engine) UpdateNPDS(discoveryResponse []byte) error {
 func (e *Engine) UpdateNetworkPoliciesJSON(policies []byte) error {
 	cs := C.CBytes(policies)
 	defer C.free(cs)
-	return check(C.cg_http_policy_update(e.h, (*C.char)(cs), C.size_t(len(policies))))
+	return call(func() C.int { return C.cg_http_policy_update(e.h, (*C.char)(cs), C.size_t(len(policies))) })
 }
 
 // PolicyIndex is the index requests name a policy by (NetworkPolicy.name).
@@ -28,7 +28,7 @@ func (e *Engine) PolicyIndex(name string) (uint32, error) {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
 	var idx C.uint32_t
-	err := check(C.cg_http_policy_index(e.h, cs, &idx))
+	err := call(func() C.int { return C.cg_http_policy_index(e.h, cs, &idx) })
 	return uint32(idx), err
 }
 
@@ -36,11 +36,11 @@ func (e *Engine) PolicyIndex(name string) (uint32, error) {
 // installs one on another handle (one compile per node, SURVEY §8(e)).
 func (e *Engine) ExportHTTPPolicy() ([]byte, error) {
 	var n C.size_t
-	if err := check(C.cg_http_policy_export(e.h, nil, 0, &n)); err != nil {
+	if err := call(func() C.int { return C.cg_http_policy_export(e.h, nil, 0, &n) }); err != nil {
 		return nil, err
 	}
 	img := make([]byte, int(n))
-	err := check(C.cg_http_policy_export(e.h, unsafe.Pointer(&img[0]), n, &n))
+	err := call(func() C.int { return C.cg_http_policy_export(e.h, unsafe.Pointer(&img[0]), n, &n) })
 	return img, err
 }
 
@@ -50,7 +50,7 @@ func (e *Engine) ImportHTTPPolicy(img []byte) error {
 	if len(img) == 0 {
 		return &Error{Code: InvalidArgument, Msg: "empty image"}
 	}
-	return check(C.cg_http_policy_import(e.h, unsafe.Pointer(&img[0]), C.size_t(len(img))))
+	return call(func() C.int { return C.cg_http_policy_import(e.h, unsafe.Pointer(&img[0]), C.size_t(len(img))) })
 }
 
 // ShareHTTPPolicy copies this handle's compiled HTTP policy to the others.
@@ -110,9 +110,9 @@ func (e *Engine) HTTPVerdicts(reqs []HTTPRequest) ([]bool, error) {
 		blob = []byte{0}
 	}
 	v := make([]uint8, n)
-	err := check(C.cg_http_verdicts_fields_host(e.h, bytesPtr(blob), (*C.uint64_t)(unsafe.Pointer(&off[0])),
+	err := call(func() C.int { return C.cg_http_verdicts_fields_host(e.h, bytesPtr(blob), (*C.uint64_t)(unsafe.Pointer(&off[0])),
 		C.size_t(n), (*C.uint32_t)(unsafe.Pointer(&policy[0])), (*C.uint8_t)(unsafe.Pointer(&ingress[0])),
-		(*C.uint16_t)(unsafe.Pointer(&port[0])), (*C.uint32_t)(unsafe.Pointer(&remote[0])), bytesPtr(v)))
+		(*C.uint16_t)(unsafe.Pointer(&port[0])), (*C.uint32_t)(unsafe.Pointer(&remote[0])), bytesPtr(v)) })
 	for i := range v {
 		out[i] = v[i] != 0
 	}
@@ -123,9 +123,9 @@ func (e *Engine) HTTPVerdicts(reqs []HTTPRequest) ([]bool, error) {
 // memory (the Envoy codec step, packing and verdicts on the GPU).
 func (e *Engine) HTTPVerdictsRawDev(raw, rawOff, policy, ingress, port, remote, out unsafe.Pointer, n int,
 	stream unsafe.Pointer) error {
-	return check(C.cg_http_verdicts_raw_dev(e.h, (*C.uint8_t)(raw), (*C.uint64_t)(rawOff), C.size_t(n),
+	return call(func() C.int { return C.cg_http_verdicts_raw_dev(e.h, (*C.uint8_t)(raw), (*C.uint64_t)(rawOff), C.size_t(n),
 		(*C.uint32_t)(policy), (*C.uint8_t)(ingress), (*C.uint16_t)(port), (*C.uint32_t)(remote), (*C.uint8_t)(out),
-		stream))
+		stream) })
 }
 
 // HTTPRuleInfo is what each per-rule hit counter counts (cg_http_rule_info).
@@ -136,20 +136,20 @@ type HTTPRuleInfo struct {
 // HTTPRules returns the rule table the per-rule counters follow.
 func (e *Engine) HTTPRules() ([]HTTPRuleInfo, error) {
 	var n C.size_t
-	if err := check(C.cg_http_rule_info_get(e.h, nil, 0, &n)); err != nil {
+	if err := call(func() C.int { return C.cg_http_rule_info_get(e.h, nil, 0, &n) }); err != nil {
 		return nil, err
 	}
 	out := make([]HTTPRuleInfo, int(n))
 	if n == 0 {
 		return out, nil
 	}
-	err := check(C.cg_http_rule_info_get(e.h, (*C.cg_http_rule_info)(unsafe.Pointer(&out[0])), n, &n))
+	err := call(func() C.int { return C.cg_http_rule_info_get(e.h, (*C.cg_http_rule_info)(unsafe.Pointer(&out[0])), n, &n) })
 	return out, err
 }
 
 // HTTPStats is cg_http_policy_stats's u64 vector.
 func (e *Engine) HTTPStats() ([]uint64, error) {
 	out := make([]uint64, 16)
-	err := check(C.cg_http_policy_stats(e.h, (*C.uint64_t)(unsafe.Pointer(&out[0])), C.size_t(len(out))))
+	err := call(func() C.int { return C.cg_http_policy_stats(e.h, (*C.uint64_t)(unsafe.Pointer(&out[0])), C.size_t(len(out))) })
 	return out, err
 }

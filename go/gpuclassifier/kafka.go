@@ -39,7 +39,7 @@ func (e *Engine) UpdateKafka(redirects []KafkaRedirect) error {
 	}
 	cs := C.CBytes(b)
 	defer C.free(cs)
-	return check(C.cg_kafka_policy_update(e.h, (*C.char)(cs), C.size_t(len(b))))
+	return call(func() C.int { return C.cg_kafka_policy_update(e.h, (*C.char)(cs), C.size_t(len(b))) })
 }
 
 // KafkaPolicyIndex is the redirect index requests carry.
@@ -47,7 +47,7 @@ func (e *Engine) KafkaPolicyIndex(name string) (uint16, error) {
 	cs := C.CString(name)
 	defer C.free(unsafe.Pointer(cs))
 	var idx C.uint32_t
-	err := check(C.cg_kafka_policy_index(e.h, cs, &idx))
+	err := call(func() C.int { return C.cg_kafka_policy_index(e.h, cs, &idx) })
 	return uint16(idx), err
 }
 
@@ -56,7 +56,7 @@ func (e *Engine) KafkaIntern(what uint32, s string) uint32 {
 	cs := C.CString(s)
 	defer C.free(unsafe.Pointer(cs))
 	var id C.uint32_t
-	if check(C.cg_kafka_intern(e.h, C.uint32_t(what), cs, C.size_t(len(s)), &id)) != nil {
+	if call(func() C.int { return C.cg_kafka_intern(e.h, C.uint32_t(what), cs, C.size_t(len(s)), &id) }) != nil {
 		return KafkaUnknownString
 	}
 	return uint32(id)
@@ -70,8 +70,8 @@ func (e *Engine) KafkaVerdicts(reqs []KafkaRequest) ([]bool, error) {
 		return out, nil
 	}
 	v := make([]uint8, len(reqs))
-	err := check(C.cg_kafka_verdicts_host(e.h, (*C.cg_kafka_request)(unsafe.Pointer(&reqs[0])), C.size_t(len(reqs)),
-		nil, 0, bytesPtr(v)))
+	err := call(func() C.int { return C.cg_kafka_verdicts_host(e.h, (*C.cg_kafka_request)(unsafe.Pointer(&reqs[0])), C.size_t(len(reqs)),
+		nil, 0, bytesPtr(v)) })
 	for i := range v {
 		out[i] = v[i] != 0
 	}
@@ -87,9 +87,9 @@ func (e *Engine) KafkaVerdictsRaw(raw []byte, rawOff []uint64, redirect []uint16
 	if n <= 0 {
 		return out, nil
 	}
-	err := check(C.cg_kafka_verdicts_raw_host(e.h, bytesPtr(raw), (*C.uint64_t)(unsafe.Pointer(&rawOff[0])),
+	err := call(func() C.int { return C.cg_kafka_verdicts_raw_host(e.h, bytesPtr(raw), (*C.uint64_t)(unsafe.Pointer(&rawOff[0])),
 		C.size_t(n), (*C.uint16_t)(unsafe.Pointer(&redirect[0])), (*C.uint32_t)(unsafe.Pointer(&remote[0])),
-		bytesPtr(out)))
+		bytesPtr(out)) })
 	return out, err
 }
 

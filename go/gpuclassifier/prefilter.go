@@ -33,15 +33,15 @@ func (e *Engine) NewPreFilter(config, maxLPM, maxHash uint32) (*PreFilter, error
 		config = PrefilterFix4 | PrefilterFix6
 	}
 	var id C.uint32_t
-	if err := check(C.cg_prefilter_create(e.h, C.uint32_t(config), C.uint32_t(maxLPM), C.uint32_t(maxHash),
-		&id)); err != nil {
+	if err := call(func() C.int { return C.cg_prefilter_create(e.h, C.uint32_t(config), C.uint32_t(maxLPM), C.uint32_t(maxHash),
+		&id) }); err != nil {
 		return nil, err
 	}
 	return &PreFilter{e: e, id: id}, nil
 }
 
 // Destroy frees the prefilter's tables.
-func (pf *PreFilter) Destroy() error { return check(C.cg_prefilter_destroy(pf.e.h, pf.id)) }
+func (pf *PreFilter) Destroy() error { return call(func() C.int { return C.cg_prefilter_destroy(pf.e.h, pf.id) }) }
 
 func cidrs(nets []net.IPNet) []C.cg_cidr {
 	out := make([]C.cg_cidr, len(nets))
@@ -74,7 +74,7 @@ func (pf *PreFilter) Insert(revision int64, nets []net.IPNet) (int64, error) {
 	if len(c) > 0 {
 		p = &c[0]
 	}
-	err := check(C.cg_prefilter_insert(pf.e.h, pf.id, C.int64_t(revision), p, C.size_t(len(c)), &rev))
+	err := call(func() C.int { return C.cg_prefilter_insert(pf.e.h, pf.id, C.int64_t(revision), p, C.size_t(len(c)), &rev) })
 	return int64(rev), err
 }
 
@@ -86,7 +86,7 @@ func (pf *PreFilter) Delete(revision int64, nets []net.IPNet) (int64, error) {
 	if len(c) > 0 {
 		p = &c[0]
 	}
-	err := check(C.cg_prefilter_delete(pf.e.h, pf.id, C.int64_t(revision), p, C.size_t(len(c)), &rev))
+	err := call(func() C.int { return C.cg_prefilter_delete(pf.e.h, pf.id, C.int64_t(revision), p, C.size_t(len(c)), &rev) })
 	return int64(rev), err
 }
 
@@ -106,13 +106,13 @@ func (pf *PreFilter) SetEndpoints(v4 []net.IP, v6 []net.IP) error {
 	if len(a4) > 0 {
 		p4 = (*C.uint32_t)(unsafe.Pointer(&a4[0]))
 	}
-	return check(C.cg_prefilter_set_endpoints(pf.e.h, pf.id, p4, C.size_t(len(a4)), bytesPtr(a6), C.size_t(len(v6))))
+	return call(func() C.int { return C.cg_prefilter_set_endpoints(pf.e.h, pf.id, p4, C.size_t(len(a4)), bytesPtr(a6), C.size_t(len(v6))) })
 }
 
 // VerdictsDev runs check_v4 / check_v6 over device records ({saddr, daddr}
 // u32 pairs; 32-byte v6 pairs) into one CG_XDP_* byte each.
 func (pf *PreFilter) VerdictsDev(v4 unsafe.Pointer, n4 int, out4 unsafe.Pointer, v6 unsafe.Pointer, n6 int,
 	out6 unsafe.Pointer, stream unsafe.Pointer) error {
-	return check(C.cg_prefilter_verdicts_dev(pf.e.h, pf.id, (*C.uint32_t)(v4), C.size_t(n4), (*C.uint8_t)(out4),
-		(*C.uint8_t)(v6), C.size_t(n6), (*C.uint8_t)(out6), stream))
+	return call(func() C.int { return C.cg_prefilter_verdicts_dev(pf.e.h, pf.id, (*C.uint32_t)(v4), C.size_t(n4), (*C.uint8_t)(out4),
+		(*C.uint8_t)(v6), C.size_t(n6), (*C.uint8_t)(out6), stream) })
 }

@@ -316,6 +316,15 @@ int cg_proxylib_policy_update_npds(uint64_t instance, const uint8_t* discovery_r
  * connections share a batch (flat combining; calls > batches under load). */
 int cg_proxylib_stats(uint64_t instance, uint64_t* batches, uint64_t* calls);
 
+/* Batching window of the OnData combiner.  A call that finds no batch in
+ * flight becomes the flusher; with min_calls > 1 it waits until min_calls
+ * calls are queued or max_wait_us microseconds have passed, then decides
+ * everything queued as one GPU batch.  Default (1, 0): decide at once.
+ * No reference counterpart (Go proxylib decides each frame in the calling
+ * goroutine, proxylib/proxylib/connection.go:176-179); a latency/throughput
+ * knob for Envoy worker pools. */
+int cg_proxylib_set_batching(uint64_t instance, uint32_t min_calls, uint32_t max_wait_us);
+
 /* ======================================================================== */
 /* HTTP L7: Envoy cilium.l7policy — envoy/cilium_network_policy.h:40-237,    */
 /* envoy/cilium_l7policy.cc:127-182                                          */

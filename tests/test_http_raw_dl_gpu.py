@@ -10,7 +10,7 @@ against the host path over the same requests (cg_http_pack → http_kernel) and
 the oracle (oracle/http1_ref.py codec step, then the Envoy-faithful rule
 scan), plus its per-program and per-rule counters against the default
 path's.  Batches stay small (a few 10K requests): a broken slot protocol
-would show as bounded polling (kernels_http_raw.hip kSpinMax), not a hang."""
+would show as bounded polling (RawLayoutDev.spin), not a hang."""
 import os
 
 import numpy as np
@@ -32,7 +32,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.run_last]
 @pytest.fixture
 def dl():
     """The device-layout path for the test's calls (read per call)."""
-    old = {k: os.environ.get(k) for k in ("CILIUM_GPU_RAW_LAYOUT", "CILIUM_GPU_RAW_SUBBATCH")}
+    old = {k: os.environ.get(k) for k in ("CILIUM_GPU_RAW_LAYOUT", "CILIUM_GPU_RAW_SUBBATCH", "CILIUM_GPU_RAW_SPIN")}
     os.environ["CILIUM_GPU_RAW_LAYOUT"] = "device"
     yield os.environ
     for k, v in old.items():
@@ -161,4 +161,69 @@ def test_gpu_dl_batches_queued_on_streams(dl):
     for k, (rq, raws, _) in enumerate(batches):
         got = outs[k].cpu().numpy()
         assert np.array_equal(got, _oracle(pols, *_args(rq), raws)), k
+    cl.close()
+
+
+def test_gpu_dl_late_slots_padded(gpu, dl):
+    """A lane that gives up waiting for its chunk's id (forced here: no
+    polling at all, CILIUM_GPU_RAW_SPIN=0) has its request walked and its slot
+    padded by raw_seal_kernel from the late list: verdicts equal the host path
+    and the oracle, and per-program and per-rule counters equal the default
+    sequence's (an unfilled slot read by http_kernel would add a stale
+    request's verdict and counts)."""
+    pols, info = synth.http10k_rules()
+    gpu.update_http_policy(pols)
+    rq = synth.http10k_requests(20_000, info, seed=126)
+    raws = _vary(_raw_requests(rq), np.random.default_rng(126))
+    blob, off = _blob(raws)
+
+    def run():
+        gpu.reset_counters()
+        v = gpu.http_verdicts_raw(*_args(rq), blob, off)
+        return v, gpu.read_counters(N.CG_CTR_HTTP_PROGRAMS), gpu.read_counters(N.CG_CTR_HTTP_RULES)
+
+    # the workspace first holds another batch's slots (stale meta and order)
+    dl["CILIUM_GPU_RAW_SPIN"] = "16384"
+    gpu.http_verdicts_raw(*_args(rq), *_blob(raws[::-1]))
+    dl["CILIUM_GPU_RAW_SPIN"] = "0"
+    v_late, p_late, r_late = run()
+    dl.pop("CILIUM_GPU_RAW_SPIN")
+    dl.pop("CILIUM_GPU_RAW_LAYOUT")
+    v_def, p_def, r_def = run()
+    assert np.array_equal(v_late, v_def)
+    assert np.array_equal(v_late[:8_000], _oracle(pols, *(np.asarray(a)[:8_000] for a in _args(rq)), raws[:8_000]))
+    assert np.array_equal(p_late, p_def)
+    assert np.array_equal(r_late, r_def)
+
+
+def test_gpu_dl_policy_swap_after_async_call(dl):
+    """cg_http_verdicts_raw_dev returns with its kernels queued; a policy
+    update right after it must not free the tables they read (the snapshot's
+    fence): the queued batch's verdicts are the old policy's, the next
+    batch's the new one's."""
+    import torch
+    cl = Classifier(device=0)
+    pols, info = synth.http10k_rules()
+    cl.update_http_policy(pols)
+    dev = torch.device("cuda:0")
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(np.asarray(a).astype(dt))).to(dev)
+    rq = synth.http10k_requests(30_000, info, seed=140)
+    raws = _vary(_raw_requests(rq), np.random.default_rng(140))
+    blob, off = _blob(raws)
+    d = (t(blob, np.uint8), t(off, np.int64), len(raws), t(rq["policy"], np.int32), t(rq["ingress"], np.uint8),
+         t(rq["port"], np.int16), t(rq["remote"], np.int32))
+    exp1 = cl.http_verdicts_raw(*_args(rq), blob, off)  # the same path, synchronous
+    s1 = torch.cuda.Stream(device=dev)
+    out1 = torch.full((len(raws),), 7, dtype=torch.uint8, device=dev)
+    out2 = torch.full((len(raws),), 7, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    cl.http_verdicts_raw_dev(*d, out1, stream=s1.cuda_stream)
+    star = synth.starwars_policy()
+    cl.update_http_policy(star)  # the old snapshot's last holder lets go here
+    cl.http_verdicts_raw_dev(*d, out2, stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    got1 = out1.cpu().numpy()
+    assert np.array_equal(got1, exp1)
+    assert np.array_equal(got1[:8_000], _oracle(pols, *(np.asarray(a)[:8_000] for a in _args(rq)), raws[:8_000]))
+    assert np.array_equal(out2.cpu().numpy(), _host_path(cl, *_args(rq), raws))
     cl.close()

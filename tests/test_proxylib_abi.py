@@ -266,8 +266,11 @@ def test_gpu_r2d2_control_bytes_through_ondata():
 def test_gpu_ondata_concurrent_connections_share_batches():
     """16 threads, one connection each (different remote identities and
     policies), OnData concurrently: every call's ops match the oracle, and
-    the instance's flat-combining batcher decided the calls in fewer GPU
-    batches than calls (cg_proxylib_stats)."""
+    the instance's accounting adds up (cg_proxylib_stats: every call counted,
+    1 <= batches <= calls). Whether calls combine depends on Python threads
+    overlapping inside OnData under the GIL, so it is reported, not asserted;
+    tests/test_ondata_combine_gpu.py holds the flusher to make combining
+    deterministic, and tools/ondata_bench.cc measures it from C threads."""
     import threading
 
     import numpy as np
@@ -318,7 +321,8 @@ def test_gpu_ondata_concurrent_connections_share_batches():
     _lib.CloseModule(inst)
     assert not errors, errors[:3]
     calls, batches = c1.value - c0.value, b1.value - b0.value
-    assert calls >= 16 * 60 * 0.9 and batches < calls, (calls, batches)
+    print(f"ondata concurrent: calls={calls} batches={batches}")
+    assert calls == 16 * 60 and 1 <= batches <= calls, (calls, batches)
 
 
 def test_ondata_combiner_concurrency_without_device():
@@ -359,3 +363,42 @@ def test_ondata_combiner_concurrency_without_device():
     assert all(rc == F_UNKNOWN_ERROR and ops == [] for rc, ops in rcs), rcs[:3]
     calls, batches = c1.value - c0.value, b1.value - b0.value
     assert calls == 16 * per and 1 <= batches <= calls, (calls, batches)
+
+
+def test_ondata_batching_window_without_device():
+    """cg_proxylib_set_batching on a handle without a GPU: 16 connections
+    released from one barrier per round, window of 16 calls — each round's
+    calls are taken as ONE batch (whose flush fails: no device), every call
+    returns the engine error, none waits past the window."""
+    import threading
+
+    inst = open_module([(b"node-id", b"cpu-window")], "-1")
+    assert inst != 0
+    assert N.lib.cg_proxylib_set_batching(inst + 999, 16, 1000) == N.CG_INVALID_INSTANCE
+    t = json.dumps(R2D2_POLICIES).encode()
+    assert N.lib.cg_proxylib_policy_update(inst, t, len(t)) == N.CG_OK
+    assert N.lib.cg_proxylib_set_batching(inst, 16, 5_000_000) == N.CG_OK
+    rounds, bar, rcs = 3, threading.Barrier(16), []
+
+    def worker(k):
+        c = Conn(inst, policy=b"cp2", src=k)
+        assert c.rc == F_OK
+        for j in range(rounds):
+            bar.wait()
+            rcs.append(c.on_data([b"READ f%d\r\n" % j], cap=2))
+            bar.wait()
+        c.close()
+
+    b0, c0 = C.c_uint64(), C.c_uint64()
+    N.lib.cg_proxylib_stats(inst, C.byref(b0), C.byref(c0))
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join(timeout=120)
+        assert not x.is_alive(), "an OnData call never returned"
+    b1, c1 = C.c_uint64(), C.c_uint64()
+    N.lib.cg_proxylib_stats(inst, C.byref(b1), C.byref(c1))
+    _lib.CloseModule(inst)
+    assert all(rc == F_UNKNOWN_ERROR and ops == [] for rc, ops in rcs), rcs[:3]
+    assert (c1.value - c0.value, b1.value - b0.value) == (16 * rounds, rounds)
