@@ -175,10 +175,7 @@ def main():
     t_end = time.perf_counter()
     wall = t_end - t_start
     kernel_ms = sum(a.elapsed_time(z) for a, z in kev) / args.steps
-    if dist is not None:
-        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
+    wall = max_over_ranks(wall, dist, dev, torch)
 
     total_req = B * world * args.steps
     value = total_req / wall
@@ -263,6 +260,15 @@ def host_threads() -> int:
     """Host threads given to this GPU's process: OMP_NUM_THREADS (16 on the
     GPU box: its per-GPU CPU share), else the cores here up to 16."""
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
+def max_over_ranks(sec: float, dist, dev, torch) -> float:
+    """The job's time: the slowest rank's timed region (all-reduce MAX)."""
+    if dist is None or dist.get_world_size() == 1:
+        return sec
+    tt = torch.tensor([sec], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
 
 
 def share_policy(cl, pols, dist, rank, dev, torch) -> None:
@@ -459,11 +465,7 @@ def rehearse(args):
         total = step()
     if world > 1:
         dist.barrier()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
+    wall = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None, torch.device("cpu"), torch)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": D * world * args.steps / wall, "unit": "verdicts/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

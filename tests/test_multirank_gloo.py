@@ -104,3 +104,58 @@ def test_bench_spawns_two_ranks_cpu_rehearsal():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["rehearsal"] is True
     assert d["allreduced_requests"] == d["expected_requests"] == 2048 * 2 * 2
+
+
+def _bench_collectives_worker(rank, world, port, q):
+    """bench.py's own collectives on gloo: share_policy (rank 0 compiles, the
+    image's size and bytes broadcast, the other ranks import it) and
+    max_over_ranks (the job time = the slowest rank's)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import hashlib
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        from cilium_amd import synth
+        from cilium_amd.classifier import Classifier
+        cl = Classifier(device=-1)
+        pols, info = synth.http10k_rules(n_rules=1500, n_ports=16)
+        bench.share_policy(cl, pols, dist, rank, torch.device("cpu"), torch)
+        img = cl.export_http_policy()
+        h = torch.tensor(list(hashlib.sha256(img).digest()), dtype=torch.uint8)
+        hs = [torch.zeros_like(h) for _ in range(world)]
+        dist.all_gather(hs, h)
+        same_image = all(torch.equal(x, hs[0]) for x in hs)
+        # every rank decides the same sample with its (imported) tables
+        rq = synth.http10k_requests(2048, info, seed=99)
+        v = torch.from_numpy(cl.http_eval_host_diag(cl.pack_http(**rq)).astype(np.int64))
+        vs = [torch.zeros_like(v) for _ in range(world)]
+        dist.all_gather(vs, v)
+        same_verdicts = all(torch.equal(x, vs[0]) for x in vs)
+        wall = bench.max_over_ranks(0.5 + rank, dist, torch.device("cpu"), torch)
+        one = bench.max_over_ranks(0.25, None, torch.device("cpu"), torch)
+        q.put((rank, same_image, same_verdicts, wall, one))
+        cl.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bench_collectives_image_broadcast_and_max_time():
+    """Every collective bench.py issues besides the counter all-reduce
+    (covered above): the compiled image broadcast and the max-over-ranks
+    time, on 3 gloo ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_bench_collectives_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert [r for r, *_ in res] == [0, 1, 2]
+    assert all(img and ver for _, img, ver, _, _ in res), res
+    assert all(w == 2.5 and one == 0.25 for *_, w, one in res), res

@@ -152,6 +152,17 @@ VARIANTS.update({
                   "constexpr uint32_t kIpcV4 = 4, kIpcV6 = 4;")],
     "ipc_v4u8": [("kernels_ipcache.hip", "constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;",
                   "constexpr uint32_t kIpcV4 = 8, kIpcV6 = 2;")],
+    # round 5 measuring devices on the class-mode walker (verdicts meaningless;
+    # every LDS address stays inside the block or reads LDS out of range as 0):
+    # the DFA step without its LDS read (same VALU count), and no walk at all
+    # (the unit loads stay: the step's asm still consumes every unit word)
+    "h_nolds": [('"\\n\\tds_read_b32 %0, %0\\n\\t"', '"\\n\\tv_mov_b32 %0, %3\\n\\t"')],
+    "h_nowalk": [('  if (B == 0) CG_CLS_STEP("BYTE_0");',
+                  '  if (true) {\n    asm volatile("v_mov_b32 %0, %1" : "=v"(nx) : "v"(st), "v"(w));\n    return nx;\n  }\n'
+                  '  if (B == 0) CG_CLS_STEP("BYTE_0");')],
+    # chunks per dealt run (program block restaged once per run)
+    "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
+    "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
 })
 
 
