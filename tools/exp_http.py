@@ -160,6 +160,11 @@ VARIANTS.update({
     "h_nowalk": [('  if (B == 0) CG_CLS_STEP("BYTE_0");',
                   '  if (true) {\n    asm volatile("v_mov_b32 %0, %1" : "=v"(nx) : "v"(st), "v"(w));\n    return nx;\n  }\n'
                   '  if (B == 0) CG_CLS_STEP("BYTE_0");')],
+    # two tiles per wave, one request of each per lane, two LDS chains
+    # (lds_cls_step2); h_pair_w1: a one-unit rolling window per chain
+    "h_pair": [("constexpr bool kPairTiles = false;", "constexpr bool kPairTiles = true;")],
+    "h_pair_w1": [("constexpr bool kPairTiles = false;", "constexpr bool kPairTiles = true;"),
+                  ("  constexpr int kW = N < 2 ? (N > 0 ? N : 1) : 2;", "  constexpr int kW = 1;")],
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
