@@ -344,7 +344,13 @@ struct RawLayoutDev {
   uint32_t dpk, ext, cshift; // directory entries per key, tiles per chunk, log2(64 * ext)
   uint32_t seq, maxchunks, nkeys;
   uint32_t spin;             // polls of a chunk id before giving up (CILIUM_GPU_RAW_SPIN, tests)
+  // slot counters per bucket key and stripe: a workgroup takes its slots from
+  // stripe blockIdx % stripes of its key (vkey = key * stripes + stripe), so
+  // each hot key's returning atomics spread over `stripes` addresses
+  uint32_t stripes;
 };
+// the stripe-expanded bucket key of a request of key k in workgroup b
+CG_HD inline uint32_t raw_vkey(const RawLayoutDev& L, uint32_t k, uint32_t b) { return k * L.stripes + (b & (L.stripes - 1u)); }
 
 CG_HD inline uint32_t hash32(uint32_t x) {
   x ^= x >> 16;

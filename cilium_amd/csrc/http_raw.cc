@@ -355,7 +355,12 @@ uint32_t floor_pow2(uint32_t x) {
 void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists, const uint8_t* d_raw,
                   const uint64_t* d_off, size_t m, const uint32_t* d_policy, const uint8_t* d_ingress,
                   const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, hipStream_t st) {
-  const uint32_t np = (uint32_t)s.progs.size(), K = (np + 2) * kRawUnits;
+  // slot counters striped per workgroup (RawLayoutDev.stripes): a bucket
+  // key's requests take slots from `stripes` counters, so the returning
+  // atomics of a hot key do not serialize on one address
+  uint32_t S = 16;
+  if (const char* v = getenv("CILIUM_GPU_RAW_STRIPES")) S = floor_pow2((uint32_t)std::max(1, std::min(64, atoi(v))));
+  const uint32_t np = (uint32_t)s.progs.size(), K = (np + 2) * kRawUnits * S;
   // tiles per chunk: the chunk table's 64 when the sub-batch fills several
   // chunks per bucket, fewer for small ones (each bucket's last chunk is
   // partly empty)
@@ -363,10 +368,20 @@ void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists
   uint32_t cshift = 6;
   while ((1u << cshift) < 64 * ext) ++cshift;
   const size_t per_chunk = (size_t)64 * ext;
-  const uint32_t dpk = (uint32_t)((m + per_chunk - 1) / per_chunk);
+  // directory entries per (key, stripe): the requests one stripe's
+  // workgroups can take slots for — the scan's grid-stride share plus the
+  // deferred kernel's (every request at most once in either)
+  const size_t it256 = (m + 255) / 256;
+  auto share = [&](size_t grid) {
+    grid = std::max<size_t>(grid, 1);
+    return ((grid + S - 1) / S) * ((it256 + grid - 1) / grid) * 256;
+  };
+  const size_t per_stripe = std::min(m, share(http_raw_dl_grid(s.raw, lists, m, cus))) +
+                            std::min(m, share((size_t)std::max(1, cus) * 2));
+  const uint32_t dpk = (uint32_t)((std::min(m, per_stripe) + per_chunk - 1) / per_chunk);
   // every chunk holds a slot: at most m of them, and at most one partly
-  // filled per bucket
-  const uint32_t maxchunks = (uint32_t)std::min<size_t>(m, (size_t)dpk + K);
+  // filled per (key, stripe)
+  const uint32_t maxchunks = (uint32_t)std::min<size_t>(m, (m + per_chunk - 1) / per_chunk + K);
   const size_t maxtiles = (size_t)maxchunks * ext;
   if (maxtiles * kRawTileGran >= (1ull << 32)) fail(CG_INVALID_ARGUMENT, "raw batch layout too large");
   // batch: header, chunk table, tile table, tile data (1 KiB aligned)
@@ -403,6 +418,7 @@ void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists
   if (!L.seq) L.seq = ++sl.raw_seq;  // 0 is the cleared directory's tag
   L.maxchunks = maxchunks;
   L.nkeys = K;
+  L.stripes = S;
   hip_check(hipMemsetAsync(ctl, 0, ctl_bytes, st), "hipMemsetAsync");
   hip_check(hipMemsetAsync(L.ttab, 0, sizeof(HttpTile) * maxtiles, st), "hipMemsetAsync");
   hip_check(launch_http_raw_dl_scan(s.raw, lists, d_raw, d_off, m, d_policy, d_ingress, d_port, d_remote, L, st, cus),

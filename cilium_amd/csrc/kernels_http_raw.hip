@@ -1602,7 +1602,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
       }
     }
     const bool want = live && !defer && !walk;
-    const RawSlot sl = raw_slot(L, want, group_of(R, prog) * kRawUnits + units, prog);
+    const RawSlot sl = raw_slot(L, want, raw_vkey(L, group_of(R, prog) * kRawUnits + units, blockIdx.x), prog);
     walk |= want && !sl.ok;
     list_append(L.walk, &L.ctl[kRawCtlWalk], walk, (uint32_t)i, lane);
     if (want && sl.ok) {
@@ -1656,7 +1656,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_defer_dl_kernel(HttpRawDev R,
       }
     }
     const bool want = live && !walk;
-    const RawSlot sl = raw_slot(L, want, group_of(R, prog) * kRawUnits + units, prog);
+    const RawSlot sl = raw_slot(L, want, raw_vkey(L, group_of(R, prog) * kRawUnits + units, blockIdx.x), prog);
     walk |= want && !sl.ok;
     list_append(L.walk, &L.ctl[kRawCtlWalk], walk, i, lane);
     if (want && sl.ok) {
@@ -1690,7 +1690,7 @@ __global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, Ra
     if ((uint32_t)(v >> 32) != L.seq || id >= L.maxchunks) continue;
     const uint32_t used = cnt - (c << L.cshift), nt = (used + 63) >> 6;
     L.chunks[id].ntiles = nt;
-    const uint32_t t = id * L.ext + nt - 1, units = k % kRawUnits;
+    const uint32_t t = id * L.ext + nt - 1, units = (k / L.stripes) % kRawUnits;
     uint8_t* tb = L.tiles + (size_t)t * (kRawTileGran * 512);
     for (uint32_t l = used - (nt - 1) * 64; l < 64; ++l) {
       reinterpret_cast<uint2*>(tb)[l] = make_uint2(0, CG_HTTP_F_PAD << 24);
