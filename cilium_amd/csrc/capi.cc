@@ -14,6 +14,7 @@
 #include "engine.h"
 #include "http.h"
 #include "kafka.h"
+#include "kafka_wire.h"
 #include "kernels.h"
 #include "l4.h"
 #include "ipcache.h"
@@ -1135,16 +1136,25 @@ static size_t kafka_decode_on(Engine& e, const KafkaSnapshot& s, StagingSlot& sl
                               const uint64_t* d_off, size_t n, const uint16_t* d_red, const uint32_t* d_rem,
                               cg_kafka_request* d_reqs, uint32_t* d_arena, size_t arena_cap, uint8_t* d_status,
                               hipStream_t st) {
-  auto* ctr = (unsigned long long*)sl.dev_buf(7, 16);
-  hip_check(hipMemsetAsync(ctr, 0, 16, st), "hipMemsetAsync");
+  // counters: topic arena entries, requests the decode kernel deferred,
+  // inflate bytes reserved, payloads inflated on the device, requests the
+  // inflate kernel deferred (to the host)
+  auto* ctr = (unsigned long long*)sl.dev_buf(7, 40);
+  hip_check(hipMemsetAsync(ctr, 0, 40, st), "hipMemsetAsync");
+  // the decode kernel's deferred requests (compressed sets) and the
+  // payloads' decoded bytes (grow-only; a payload past it goes to the host)
+  auto* dlist = (uint32_t*)sl.dev_buf(28, n * 4);
+  uint8_t* zarena = (uint8_t*)sl.dev_buf(27, kKafkaInflateArena);
   check_launch(launch_kafka_decode(s.ddict[0], s.ddict[1], d_raw, d_off, n, d_red, d_rem, d_reqs, d_arena,
-                                   arena_cap, ctr, d_status, st, e.cus),
+                                   arena_cap, ctr, d_status, st, e.cus, dlist, zarena, kKafkaInflateArena),
                "kafka decode kernel launch");
-  auto* hc = (unsigned long long*)sl.host_buf(7, 16);
-  hip_check(hipMemcpyAsync(hc, ctr, 16, hipMemcpyDeviceToHost, st), "D2H");
+  auto* hc = (unsigned long long*)sl.host_buf(7, 40);
+  hip_check(hipMemcpyAsync(hc, ctr, 40, hipMemcpyDeviceToHost, st), "D2H");
   hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   size_t used = (size_t)hc[0];
-  if (hc[1] == 0) return used;
+  e.kafka_inflated.fetch_add(hc[3]);
+  e.kafka_deferred.fetch_add(hc[4]);
+  if (hc[4] == 0) return used;
   std::vector<uint8_t> status(n);
   std::vector<uint64_t> off(n + 1);
   hip_check(hipMemcpy(status.data(), d_status, n, hipMemcpyDeviceToHost), "D2H");
@@ -1173,6 +1183,14 @@ static void check_offsets(const uint64_t* off, size_t n) {
   if (!off) fail(CG_INVALID_ARGUMENT, "NULL raw_off");
   for (size_t i = 0; i < n; ++i)
     if (off[i + 1] < off[i]) fail(CG_INVALID_ARGUMENT, "raw_off must be non-decreasing");
+}
+
+int cg_kafka_decode_stats(uint64_t h, uint64_t* device_inflated, uint64_t* host_deferred) {
+  return guarded([&] {
+    auto e = get(h);
+    if (device_inflated) *device_inflated = e->kafka_inflated.load();
+    if (host_deferred) *host_deferred = e->kafka_deferred.load();
+  });
 }
 
 int cg_kafka_decode_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,

@@ -104,7 +104,8 @@ class PinnedMem {
 // device buffers and pinned host buffers, so host calls make no hipMalloc /
 // hipFree and copy with async DMA instead of pageable hipMemcpy.
 struct StagingSlot {
-  static constexpr int kBufs = 27;  // 0..7 host staging, 8..18 the raw HTTP path's workspace, 19..26 its device-layout sequence's
+  static constexpr int kBufs = 29;  // 0..7 host staging, 8..18 the raw HTTP path's workspace, 19..26 its device-layout
+                                    // sequence's, 27-28 the Kafka decoder's inflate arena and deferred list
   void* stream = nullptr;  // hipStream_t
   DevMem dev[kBufs];
   PinnedMem host[kBufs];
@@ -166,6 +167,9 @@ struct Engine {
   std::shared_ptr<HttpSnapshot> http;
   std::shared_ptr<KafkaSnapshot> kafka;
   StagingPool staging;  // the "_host" entry points' buffers and streams
+  // Kafka decode: compressed payloads decoded on the device / requests the
+  // host decoder finished (cg_kafka_decode_stats)
+  std::atomic<uint64_t> kafka_inflated{0}, kafka_deferred{0};
 
   bool has_gpu() const { return device >= 0; }
   void require_gpu() const {

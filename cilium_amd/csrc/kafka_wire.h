@@ -24,8 +24,10 @@
 // reads the same bytes.Buffer, and readMessageSet's early returns (short
 // set, bad CRC, empty message) leave the rest of a message set unread for
 // the next partition's decoder.  Compressed messages (gzip, snappy) are
-// decompressed and their inner set parsed by the host only (`Inflate`); the
-// device reports them as kKwDefer and the host decodes those requests.
+// decompressed and their inner set parsed through `Inflate`: zlib and a
+// snappy restatement on the host (kafka_wire.cc), kw_inflate.h on the device
+// (kernels_kafka.hip), which hands what it cannot finish to the host as
+// kKwDefer.
 #pragma once
 
 #include <cstddef>
@@ -36,11 +38,14 @@
 namespace cg {
 
 constexpr uint32_t kKafkaMaxParseBuf = 100u * 65535u;  // utils.go:9
+// Device bytes per decode call for compressed payloads decoded on the GPU
+// (kernels_kafka.hip DevInflate); a payload past it is decoded by the host.
+constexpr size_t kKafkaInflateArena = (size_t)64 << 20;
 
 // Decoder outcomes (also the cg_kafka_decode status values).
 constexpr uint8_t kKwOk = CG_KAFKA_DECODE_OK;
 constexpr uint8_t kKwError = CG_KAFKA_DECODE_ERROR;
-constexpr uint8_t kKwDefer = 2;  // a compressed message: only the host decoder can finish it
+constexpr uint8_t kKwDefer = 2;  // a compressed message the device decoder hands to the host
 
 // io.ReadFull over a shared bytes.Buffer, optionally through io.LimitReader.
 // err: 0 none, 1 EOF / ErrUnexpectedEOF, 2 another error (sticky).

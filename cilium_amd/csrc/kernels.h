@@ -38,7 +38,7 @@ int launch_kafka(const KafkaDev& t, const void* reqs, size_t n, const uint32_t* 
 int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients, const uint8_t* raw,
                         const uint64_t* off, size_t n, const uint16_t* redirect, const uint32_t* remote, void* recs,
                         uint32_t* arena, size_t arena_cap, unsigned long long* ctr, uint8_t* status, void* stream,
-                        int cus);
+                        int cus, uint32_t* defer_list, uint8_t* zarena, size_t zcap);
 
 // Raw HTTP/1 heads → batch (kernels_http_raw.hip; sequence in http_raw.cc).
 // The scan and rank kernels run http_raw_grid(R, lists, n, cus) blocks over the

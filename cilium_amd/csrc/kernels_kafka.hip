@@ -7,9 +7,10 @@
 // snapshot's rule-string dictionaries (FNV-1a open addressing, the bytes
 // compared against the dictionary blob).  Produce message sets are parsed in
 // full: each message's CRC-32 is computed slicing-by-8 from tables in LDS
-// (8 KiB per block), the request's bytes read as aligned dwords.  A request
-// whose message set holds a gzip / snappy message ends as kKwDefer; the host
-// decodes those (cg_kafka_decode_dev, capi.cc).
+// (8 KiB per block), the request's bytes read as aligned dwords.  A gzip /
+// snappy message's payload is decoded on the device too (DevInflate,
+// kw_inflate.h); the few the device cannot finish end as kKwDefer and the
+// host decodes those requests (cg_kafka_decode_dev, capi.cc).
 //
 // Topic lists longer than CG_KAFKA_MAX_TOPICS go to the arena: the first pass
 // learns the count, then a second pass of that request (only) writes the ids
@@ -22,6 +23,7 @@
 
 #include "kafka_wire.h"
 #include "kernels.h"
+#include "kw_inflate.h"
 
 namespace cg {
 namespace {
@@ -141,13 +143,51 @@ struct DevDefer {
   __device__ uint8_t operator()(uint32_t, const uint8_t*, uint32_t, int16_t) const { return kKwDefer; }
 };
 
+// A compressed message's payload decoded on the device (kw_inflate.h) into a
+// reservation of the call's inflate arena, then its inner set parsed
+// (messages.go:460-480).  The reservation is sized before decoding: gzip from
+// the member's trailing ISIZE, snappy from its length varint(s).  What the
+// device does not finish goes to the host decoder (kKwDefer): a payload it
+// cannot size, a full arena, a second gzip member, output past the sized
+// buffer, and compressed sets nested inside compressed sets.
+struct DevInflate {
+  uint8_t* arena;
+  unsigned long long cap;
+  unsigned long long* used;  // bytes reserved (ctr[2])
+  unsigned long long* done;  // payloads decoded on the device (ctr[3])
+  const LdsCrc* crc;
+  __device__ uint8_t operator()(uint32_t codec, const uint8_t* p, uint32_t n, int16_t version) const {
+    if (!arena) return kKwDefer;
+    uint64_t need = 0;
+    if (codec == 1) {
+      if (n >= 4) need = (uint64_t)p[n - 4] | (uint64_t)p[n - 3] << 8 | (uint64_t)p[n - 2] << 16 | (uint64_t)p[n - 1] << 24;
+    } else if (!kwz::snappy_size(p, n, &need)) {
+      return kKwDefer;
+    }
+    if (need > kKafkaMaxParseBuf) return kKwDefer;
+    const unsigned long long at = atomicAdd(used, (unsigned long long)need);
+    if (at + need > cap) return kKwDefer;
+    uint8_t* dst = arena + at;
+    uint32_t got = 0;
+    const int r = codec == 1 ? kwz::gunzip_one(p, n, dst, (uint32_t)need, &got, *crc)
+                             : kwz::snappy_go(p, n, dst, (uint32_t)need, &got);
+    if (r == kwz::kKwzMore) return kKwDefer;
+    if (r != kwz::kKwzOk) return kKwError;
+    atomicAdd(done, 1ull);
+    KwStream inner{dst, got, 0};
+    return kw_message_set(&inner, (int32_t)got, version, *crc, DevDefer{});
+  }
+};
+
 // One request: decode from p (its bytes, in LDS or HBM), write the record
 // and status.
+template <class Inflate>
 __device__ __forceinline__ void decode_one(const KafkaDictDev& dt, const KafkaDictDev& dc, const LdsCrc& crc,
                                            const uint8_t* p, uint32_t len, size_t i, uint32_t red, uint32_t rem,
                                            uint4* __restrict__ recs, uint32_t* __restrict__ arena,
                                            unsigned long long arena_cap, unsigned long long* __restrict__ ctr,
-                                           uint8_t* __restrict__ status) {
+                                           uint8_t* __restrict__ status, const Inflate& inflate,
+                                           unsigned long long* defer_ctr, uint32_t* defer_list) {
   uint4* rec = recs + i * 4;
   const uint4 zero = make_uint4(0, 0, 0, 0);
   rec[1] = zero;
@@ -155,18 +195,21 @@ __device__ __forceinline__ void decode_one(const KafkaDictDev& dt, const KafkaDi
   rec[3] = zero;
   KwRequest r;
   DevSink sink{&dt, p, reinterpret_cast<uint32_t*>(rec + 1), CG_KAFKA_MAX_TOPICS, CG_KAFKA_MAX_TOPICS};
-  uint8_t st = kw_decode(p, len, crc, &r, sink, DevDefer{});
+  uint8_t st = kw_decode(p, len, crc, &r, sink, inflate);
   uint32_t nt = sink.nt, t0 = 0, t1 = 0;
   if (st == kKwOk && nt > CG_KAFKA_MAX_TOPICS) {
     const unsigned long long at = atomicAdd(ctr, (unsigned long long)nt);
     const bool fits = at + nt <= arena_cap;
     KwRequest r2;
     DevSink s2{&dt, p, arena + (fits ? at : 0), fits ? nt : 0u, 0xFFFFFFFFu};
-    kw_decode(p, len, crc, &r2, s2, DevDefer{});
+    kw_decode(p, len, crc, &r2, s2, inflate);
     t0 = (uint32_t)at;
     t1 = nt >= CG_KAFKA_TOPICS_IN_ARENA ? nt : 0;
   }
-  if (st == kKwDefer) atomicAdd(ctr + 1, 1ull);
+  if (st == kKwDefer) {
+    const unsigned long long j = atomicAdd(defer_ctr, 1ull);
+    if (defer_list) defer_list[j] = (uint32_t)i;
+  }
   uint4 h;
   if (st == kKwOk) {
     const uint32_t ntb = nt < CG_KAFKA_TOPICS_IN_ARENA ? nt : CG_KAFKA_TOPICS_IN_ARENA;
@@ -191,7 +234,7 @@ __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
     KafkaDictDev dt, KafkaDictDev dc, const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off, size_t n,
     const uint16_t* __restrict__ redirect, const uint32_t* __restrict__ remote, uint4* __restrict__ recs,
     uint32_t* __restrict__ arena, unsigned long long arena_cap, unsigned long long* __restrict__ ctr,
-    uint8_t* __restrict__ status) {
+    uint8_t* __restrict__ status, uint32_t* __restrict__ defer_list) {
   __shared__ uint32_t s_crc[kKwSlices * 256];
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[kKwWaves][kKwStage ? kKwStage : 16];
   for (uint32_t i = threadIdx.x; i < 256; i += kKwThreads) {
@@ -247,9 +290,49 @@ __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
     // an LDS copy and an HBM copy measured slower: twice the code)
     if (live)
       decode_one(dt, dc, crc, staged ? stage + ((int64_t)a - lo) : raw + a, len, i, redirect[i], remote[i], recs, arena,
-                 arena_cap, ctr, status);
+                 arena_cap, ctr, status, DevDefer{}, ctr + 1, defer_list);
     // every lane has read its bytes before the stage is refilled
     __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// The requests the decode kernel deferred (defer_list[0, ctr[1])): decoded
+// again, one lane each from HBM, with their compressed payloads decoded on
+// the device (DevInflate).  A separate kernel, so the inflate code's
+// registers and scratch do not set the common decoder's occupancy.  What it
+// still defers (ctr[4]) the host decodes.
+__global__ __launch_bounds__(kKwThreads) void kafka_inflate_kernel(
+    KafkaDictDev dt, KafkaDictDev dc, const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off,
+    const uint16_t* __restrict__ redirect, const uint32_t* __restrict__ remote, uint4* __restrict__ recs,
+    uint32_t* __restrict__ arena, unsigned long long arena_cap, unsigned long long* __restrict__ ctr,
+    uint8_t* __restrict__ status, const uint32_t* __restrict__ defer_list, uint8_t* __restrict__ zarena,
+    unsigned long long zcap) {
+  __shared__ uint32_t s_crc[kKwSlices * 256];
+  const unsigned long long nd = ctr[1];
+  if (nd == 0) return;  // uniform: the common case
+  for (uint32_t i = threadIdx.x; i < 256; i += kKwThreads) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    s_crc[i] = c;
+  }
+  __syncthreads();
+  for (uint32_t k = 1; k < kKwSlices; ++k) {
+    for (uint32_t i = threadIdx.x; i < 256; i += kKwThreads) {
+      const uint32_t prev = s_crc[(k - 1) * 256 + i];
+      s_crc[k * 256 + i] = (prev >> 8) ^ s_crc[prev & 0xFF];
+    }
+    __syncthreads();
+  }
+  const LdsCrc crc{s_crc};
+  const DevInflate inflate{zarena, zcap, ctr + 2, ctr + 3, &crc};
+  for (unsigned long long j = (unsigned long long)blockIdx.x * kKwThreads + threadIdx.x; j < nd;
+       j += (unsigned long long)gridDim.x * kKwThreads) {
+    const uint32_t i = defer_list[j];
+    const uint64_t a = off[i], b = off[i + 1];
+    const uint64_t len64 = b > a ? b - a : 0;
+    const uint32_t len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
+    decode_one(dt, dc, crc, raw + a, len, i, redirect[i], remote[i], recs, arena, arena_cap, ctr, status, inflate,
+               ctr + 4, (uint32_t*)nullptr);
   }
 }
 
@@ -258,12 +341,18 @@ __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
 int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients, const uint8_t* raw,
                         const uint64_t* off, size_t n, const uint16_t* redirect, const uint32_t* remote, void* recs,
                         uint32_t* arena, size_t arena_cap, unsigned long long* ctr, uint8_t* status, void* stream,
-                        int cus) {
+                        int cus, uint32_t* defer_list, uint8_t* zarena, size_t zcap) {
   if (n == 0) return hipSuccess;
   const size_t need = (n + kKwThreads - 1) / kKwThreads;  // one 64-request group per wave
   const int grid = (int)std::min<size_t>(need, (size_t)std::max(cus, 1) * (4096 / kKwThreads));
   hipLaunchKernelGGL(kafka_decode_kernel, dim3(grid), dim3(kKwThreads), 0, (hipStream_t)stream, topics, clients,
-                     raw, off, n, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap, ctr, status);
+                     raw, off, n, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap, ctr, status,
+                     defer_list);
+  // the deferred requests (their count stays on the device: a small grid
+  // that exits at once when there are none)
+  hipLaunchKernelGGL(kafka_inflate_kernel, dim3((unsigned)std::max(cus, 1)), dim3(kKwThreads), 0, (hipStream_t)stream,
+                     topics, clients, raw, off, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap,
+                     ctr, status, defer_list, zarena, (unsigned long long)zcap);
   return hipGetLastError();
 }
 

@@ -591,6 +591,13 @@ int cg_kafka_decode_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off
                          const uint16_t* redirect, const uint32_t* remote, cg_kafka_request* reqs,
                          uint32_t* arena, size_t arena_cap, size_t* arena_used, uint8_t* status);
 
+/* Kafka decode accounting of the handle, cumulative: compressed message
+ * payloads (gzip / snappy, optiopay proto/messages.go:460-480) decoded on
+ * the GPU, and requests the device handed to the host decoder (a nested
+ * compressed set, a second gzip member, a payload past the per-call inflate
+ * arena).  Either pointer may be NULL. */
+int cg_kafka_decode_stats(uint64_t h, uint64_t* device_inflated, uint64_t* host_deferred);
+
 /* The same decode on the GPU (one lane per request, raw bytes in HBM),
  * records and statuses in device memory.  d_raw_off holds n + 1 offsets.
  * Requests carrying gzip / snappy messages are finished by the host

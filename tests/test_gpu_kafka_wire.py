@@ -156,3 +156,30 @@ def test_gpu_decode_full_size_copies(gpu):
     got = records_view(first.cpu().numpy().reshape(-1).view(KAFKA_REQ_DTYPE), arena.cpu().numpy().view(np.uint32),
                        d_st[:n0].cpu().numpy())
     assert got == base
+
+
+def test_gpu_compressed_sets_decoded_on_device(gpu, host):
+    """Produce requests whose message sets hold gzip / snappy / xerial
+    messages (kafka_corpus codecs, including two-member gzip and nested
+    codecs) decode on the GPU (kafka_inflate_kernel, kw_inflate.h) to the
+    host decoder's records and the oracle's; only what the device cannot
+    finish (a second gzip member, a nested compressed set) reaches the host
+    (cg_kafka_decode_stats)."""
+    import ctypes as C
+    _, topics, clients, ids = _policy(gpu, host)
+    reqs = corpus(31, 3000, topics, clients, mutate_frac=0.1)
+    n = len(reqs)
+    raw, off = K.concat(reqs)
+    red = np.zeros(n, np.uint16)
+    rem = np.asarray(ids, np.uint32)[np.arange(n) % len(ids)]
+    i0, d0 = C.c_uint64(), C.c_uint64()
+    assert N.lib.cg_kafka_decode_stats(gpu.h, C.byref(i0), C.byref(d0)) == N.CG_OK
+    g = gpu.kafka_decode(raw, off, red, rem)
+    i1, d1 = C.c_uint64(), C.c_uint64()
+    assert N.lib.cg_kafka_decode_stats(gpu.h, C.byref(i1), C.byref(d1)) == N.CG_OK
+    h = host.kafka_decode(raw, off, red, rem, diag_cpu=True)
+    assert records_view(*g) == records_view(*h)
+    assert records_view(*g) == oracle_view([R.decode(r) for r in reqs], red, rem, host.kafka_intern)
+    inflated, deferred = i1.value - i0.value, d1.value - d0.value
+    print(f"compressed payloads decoded on the device: {inflated}, requests finished by the host: {deferred}")
+    assert inflated > 100 and deferred < inflated / 4, (inflated, deferred)
