@@ -165,6 +165,20 @@ VARIANTS.update({
     "h_pair": [("constexpr bool kPairTiles = false;", "constexpr bool kPairTiles = true;")],
     "h_pair_w1": [("constexpr bool kPairTiles = false;", "constexpr bool kPairTiles = true;"),
                   ("  constexpr int kW = N < 2 ? (N > 0 ? N : 1) : 2;", "  constexpr int kW = 1;")],
+    # measuring device: the device-layout scan's string units written
+    # uncoded (no per-byte code-map loads; verdicts meaningless)
+    "rawdl_nocode": [("raw_emit.h", "CG_HD inline uint32_t code4(const uint8_t* lut, uint32_t q) {\n  return",
+                      "CG_HD inline uint32_t code4(const uint8_t* lut, uint32_t q) {\n  return q; return"),
+                     ("kernels_http_raw.hip", "#include <hip/hip_runtime.h>", "#include <hip/hip_runtime.h>")],
+    # measuring devices: the device-layout scan without its string units
+    # (no code-map loads, no unit stores), and without the slot protocol (a
+    # slot computed from the request index: no atomics, no directory polls)
+    "rawdl_noemit": [("kernels_http_raw.hip", "        emit_stage(R, stage, hs, sp, kRawThreads, P, last, o);",
+                      "        (void)o;")],
+    "rawdl_noslot": [("kernels_http_raw.hip",
+                      "    const RawSlot sl = raw_slot(L, want, raw_vkey(L, group_of(R, prog) * kRawUnits + units, blockIdx.x), prog);",
+                      "    const uint32_t tfake = (uint32_t)((i >> 6) % L.maxchunks);\n"
+                      "    const RawSlot sl{L.tiles + (size_t)tfake * (kRawTileGran * 512), tfake, (uint32_t)(i & 63), want};")],
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
@@ -185,11 +199,18 @@ def build_variant(name, subs):
         files["kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip"] = \
             (B.CSRC / ("kernels_kafka.hip" if name.startswith("kw_") else "kernels_http.hip")).read_text()
     objs = []
+    # a variant's sources go to their own directory: a changed header there
+    # is found first by the changed sources' quote includes
+    vdir = OUT / name
+    vdir.mkdir(exist_ok=True)
     for fn, src in files.items():
-        f = OUT / f"{name}_{fn}"
-        f.write_text(src.replace('"../../include/', f'"{ROOT}/include/'))
-        obj = OUT / f"{name}_{fn}.o"
-        cmd = [B.HIPCC, *B._flags(fn), "-I", str(B.CSRC), "-I", str(ROOT / "include"), "-c", str(f), "-o", str(obj)]
+        (vdir / fn).write_text(src.replace('"../../include/', f'"{ROOT}/include/'))
+    for fn in files:
+        if fn.endswith(".h"):
+            continue
+        obj = vdir / f"{fn}.o"
+        cmd = [B.HIPCC, *B._flags(fn), "-I", str(B.CSRC), "-I", str(ROOT / "include"), "-c", str(vdir / fn), "-o",
+               str(obj)]
         subprocess.run(cmd, check=True)
         objs.append(obj)
     others = [B.BUILD / (s + ".o") for s in B.SOURCES if s not in files]
