@@ -424,7 +424,9 @@ void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists
   hip_check(launch_http_raw_dl_scan(s.raw, lists, d_raw, d_off, m, d_policy, d_ingress, d_port, d_remote, L, st, cus),
             "raw scan kernel launch");
   hip_check(launch_http_raw_seal(s.raw, L, batch, s.epoch, ttab_off, tiles_off, total, st), "raw seal kernel launch");
-  hip_check(launch_http(s.dev, batch, maxtiles * 64, nullptr, d_out, st, cus, L.order, nullptr, (uint32_t)m), "http kernel launch");
+  // the scan wrote raw bytes: class-mode programs code them as they walk
+  hip_check(launch_http(s.dev, batch, maxtiles * 64, nullptr, d_out, st, cus, L.order, nullptr, (uint32_t)m, s.raw.codes),
+            "http kernel launch");
   hip_check(launch_http_raw_walk(s.dev, s.raw, lists, d_raw, d_off, d_policy, d_ingress, d_port, d_remote, L, d_out,
                                  st, cus),
             "raw walk kernel launch");

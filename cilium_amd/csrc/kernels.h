@@ -23,9 +23,12 @@ int launch_lpm(const LpmDev& t, bool v4_filter, bool v6_filter, const uint32_t* 
 // raw-request batches.
 // rule (optional): per slot (or order[slot]) the first matching rule's
 // counter index, 0xFFFFFFFF when no rule allows.
+// codes (optional): the batch's strings are raw bytes (the device-layout raw
+// path writes them uncoded) and class-mode programs code them through these
+// per-program 256-byte maps (HttpRawDev.codes) as they walk.
 int launch_http(const HttpDev& t, const void* records, size_t n, const uint8_t* arena, uint8_t* out,
                 void* stream, int cus, const uint32_t* order = nullptr, uint32_t* rule = nullptr,
-                uint32_t nout = 0xFFFFFFFFu);
+                uint32_t nout = 0xFFFFFFFFu, const uint8_t* codes = nullptr);
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus);
 // tails (optional): the split layout — reqs holds 16-byte heads, tails the

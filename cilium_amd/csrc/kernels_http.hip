@@ -77,47 +77,34 @@ __device__ __forceinline__ uint32_t lds_cls_step16(uint32_t dead, uint32_t st, c
   return lds_cls_step<I & 3>(dead, st, w);
 }
 
-// Two independent walks (two requests of a lane) stepped together: both LDS
-// reads are in flight before the one wait, so a wave's dependent chain costs
-// one LDS round trip per TWO bytes walked.  Same VALU count as two single
-// steps; the compare/select pairs share VCC in sequence (two wait states
-// after each compare, filled by the default targets' max).
-template <int B>
-__device__ __forceinline__ void lds_cls_step2(uint32_t dead, uint32_t& sa, uint32_t wa, uint32_t& sb, uint32_t wb) {
-  uint32_t ea, eb, da, db, na, nb;
-#define CG_CLS_STEP2(b)                                                                                  \
-  asm volatile("v_add_u32_sdwa %0, %6, %8 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" b  \
-               "\n\tv_add_u32_sdwa %1, %7, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" b \
-               "\n\tds_read_b32 %0, %0\n\t"                                                             \
-               "ds_read_b32 %1, %1\n\t"                                                                  \
-               "s_waitcnt lgkmcnt(0)\n\t"                                                                \
-               "v_cmp_eq_u32_sdwa vcc, %0, %6 src0_sel:WORD_0 src1_sel:DWORD\n\t"                        \
-               "v_max_u32 %2, %10, %6\n\t"                                                              \
-               "v_max_u32 %3, %10, %7\n\t"                                                              \
-               "v_cndmask_b32_sdwa %4, %2, %0, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "    \
-               "src1_sel:WORD_1\n\t"                                                                    \
-               "v_cmp_eq_u32_sdwa vcc, %1, %7 src0_sel:WORD_0 src1_sel:DWORD\n\t"                        \
-               "s_nop 1\n\t"                                                                             \
-               "v_cndmask_b32_sdwa %5, %3, %1, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "    \
-               "src1_sel:WORD_1"                                                                          \
-               : "=&v"(ea), "=&v"(eb), "=&v"(da), "=&v"(db), "=&v"(na), "=&v"(nb)                         \
-               : "v"(sa), "v"(sb), "v"(wa), "v"(wb), "s"(dead)                                            \
-               : "vcc")
-  if (B == 0) CG_CLS_STEP2("BYTE_0");
-  else if (B == 1) CG_CLS_STEP2("BYTE_1");
-  else if (B == 2) CG_CLS_STEP2("BYTE_2");
-  else CG_CLS_STEP2("BYTE_3");
-#undef CG_CLS_STEP2
-  sa = na;
-  sb = nb;
-}
-
-template <int I>
-__device__ __forceinline__ void lds_cls_step2x16(uint32_t dead, uint32_t& sa, const uint4& ua, uint32_t& sb,
-                                                 const uint4& ub) {
-  const uint32_t wa = I < 4 ? ua.x : I < 8 ? ua.y : I < 12 ? ua.z : ua.w;
-  const uint32_t wb = I < 4 ? ub.x : I < 8 ? ub.y : I < 12 ? ub.z : ub.w;
-  lds_cls_step2<I & 3>(dead, sa, wa, sb, wb);
+// 16 raw string bytes → their class codes through the program's code map,
+// staged in LDS at byte address cm (raw-byte batches, launch_http codes):
+// each byte is one d16 LDS load into the low or high half of one of two
+// dwords per word (bytes 0 and 2, 1 and 3), joined by one shift-or — 1.25
+// VALU and one LDS read per byte, none of it on the walk's dependent chain.
+__device__ __forceinline__ uint4 lds_transcode(uint32_t cm, const uint4& u) {
+  uint32_t l0, h0, l1, h1, l2, h2, l3, h3, t0, t1, t2, t3;
+#define CG_TC_WORD(L, H, W)                                                                                \
+  "v_add_u32_sdwa %8, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"    \
+  "v_add_u32_sdwa %9, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2\n\t"    \
+  "v_add_u32_sdwa %10, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n\t"   \
+  "v_add_u32_sdwa %11, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3\n\t"   \
+  "ds_read_u8_d16 " L ", %8\n\t"                                                                           \
+  "ds_read_u8_d16_hi " L ", %9\n\t"                                                                        \
+  "ds_read_u8_d16 " H ", %10\n\t"                                                                          \
+  "ds_read_u8_d16_hi " H ", %11\n\t"
+  asm volatile(CG_TC_WORD("%0", "%1", "%13") CG_TC_WORD("%2", "%3", "%14") CG_TC_WORD("%4", "%5", "%15")
+                   CG_TC_WORD("%6", "%7", "%16")
+               "s_waitcnt lgkmcnt(0)\n\t"
+               "v_lshl_or_b32 %0, %1, 8, %0\n\t"
+               "v_lshl_or_b32 %2, %3, 8, %2\n\t"
+               "v_lshl_or_b32 %4, %5, 8, %4\n\t"
+               "v_lshl_or_b32 %6, %7, 8, %6"
+               : "=&v"(l0), "=&v"(h0), "=&v"(l1), "=&v"(h1), "=&v"(l2), "=&v"(h2), "=&v"(l3), "=&v"(h3),
+                 "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+               : "v"(cm), "v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
+#undef CG_TC_WORD
+  return make_uint4(l0, l1, l2, l3);
 }
 
 // Where verdicts go: out[slot] (slot order), or — for a batch built on the
@@ -231,6 +218,16 @@ __device__ __forceinline__ void count_hits(const HttpDev& T, const HttpProg& pg,
 // walks K independent strings, interleaved byte by byte, so one lane's LDS
 // reads overlap; units load one ahead and the walk ends once no lane is
 // alive inside its string.
+// Raw-byte batches on this path (programs walked from global memory): the
+// class codes of a unit from the program's map in global memory.
+__device__ __forceinline__ uint4 glb_transcode(const uint8_t* __restrict__ m, const uint4& u) {
+  auto w = [&](uint32_t x) {
+    return (uint32_t)m[x & 255] | (uint32_t)m[(x >> 8) & 255] << 8 | (uint32_t)m[(x >> 16) & 255] << 16 |
+           (uint32_t)m[x >> 24] << 24;
+  };
+  return make_uint4(w(u.x), w(u.y), w(u.z), w(u.w));
+}
+
 template <int K>
 __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg, uint32_t prog,
                                            const uint32_t* __restrict__ blk, bool rebased,
@@ -238,7 +235,7 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
                                            const uint32_t (&tile)[K],
                                            const bool (&valid)[K], const uint8_t* __restrict__ arena,
                                            uint64_t arena_bytes, VOut out, uint32_t lane, uint32_t& n_allow,
-                                           uint32_t& n_deny, uint32_t* s_hits) {
+                                           uint32_t& n_deny, uint32_t* s_hits, const uint8_t* __restrict__ codes) {
   TileRef tr[K];
   uint2 meta[K];
   uint32_t row[K];
@@ -285,6 +282,10 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
           for (int j = 0; j < K; ++j) nxt[j] = tile_unit(tr[j], tu[j], u + 2, lane);
         }
         if (cls) {
+          if (codes) {  // uniform: a raw-byte batch
+#pragma unroll
+            for (int j = 0; j < K; ++j) cur[j] = glb_transcode(codes + (size_t)prog * 256, cur[j]);
+          }
 #pragma unroll
           for (int k = 0; k < 16; ++k) {
 #pragma unroll
@@ -372,13 +373,13 @@ __device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units,
 // walk, only for lanes that reached an accepting state.  No early exit:
 // lanes whose string ended (or died) keep stepping through zero padding or
 // the dead state, which cannot change their verdict.
-template <int N, bool kCls>
+template <int N, bool kCls, bool kRaw>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
                                             uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
                                             const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
                                             uint32_t tail, TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
                                             uint64_t arena_bytes, VOut out, uint32_t lane,
-                                            uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits) {
+                                            uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits, uint32_t cm) {
   const uint2 meta = cur.meta;
   // a rolling window of kWin units: unit k + kWin loads when unit k starts
   // walking (16 dependent steps cover its latency), so long tiles hold
@@ -397,7 +398,8 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   uint32_t st = pt.start;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
-    const uint4 u = unit[k % kWin];
+    // raw-byte batches: the unit's bytes through the code map (class mode)
+    const uint4 u = kRaw && kCls ? lds_transcode(cm, unit[k % kWin]) : unit[k % kWin];
     if (k + kWin < N) unit[k % kWin] = ld_nt(tr.units + (k + kWin) * kWave + lane_now());
     // the last unit: only the 4-byte groups holding some lane's string
     // (tail, wave-uniform), the rest is padding
@@ -455,194 +457,16 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   n_deny += counted && !verdict;
 }
 
-// ---- two tiles per wave, one request of each per lane (kPairTiles) --------
-// A lane walks the requests of tiles ta and tb together (lds_cls_step2): two
-// LDS reads in flight per wait.  The pair is walked over N = the longer
-// tile's string units; a lane of the shorter tile re-reads its tile's last
-// unit past its end (tile_unit), which cannot change its verdict.
-constexpr bool kPairTiles = false;
-
-__device__ __forceinline__ const uint4* pair_unit(const TileRef& tr, uint32_t units, uint32_t k) {
-  const uint32_t lane = lane_now();
-  return units == 0 ? reinterpret_cast<const uint4*>(tr.meta) + (lane & 31)
-                    : tr.units + (min(k + 1u, units) - 1u) * kWave + lane;
-}
-
-// The verdict of one lane's request after the walk (as http_tile_n's).
-__device__ __forceinline__ void pair_verdict(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
-                                             const uint32_t* __restrict__ blk, uint2 meta, uint32_t st,
-                                             const uint8_t* __restrict__ arena, uint64_t arena_bytes, uint32_t t,
-                                             VOut out, uint32_t lane, uint32_t& n_allow, uint32_t& n_deny,
-                                             uint32_t* s_hits) {
-  const uint32_t flags = meta.y >> 24;
-  const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
-  const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
-  if (__any(overflow)) {
-    const uint32_t sa = walk_overflow<true>(blk, pt.dead, pt.start, arena, arena_bytes, meta, overflow);
-    if (overflow) st = sa;
-  }
-  uint32_t hit = kNoHit;
-  if (counted) {
-    const uint32_t lab = state_label<true>(blk, st);
-    const bool always = pg.flags & kProgHasAlways;
-    if (lab != 0xFFFFu || always) {
-      const uint32_t row = remote_row(blk, pg, meta.x);
-      if (lab != 0xFFFFu) hit = first_meet(blk, pt.acc_off + mul24(lab, 2 * pg.mask_words), row, pg.mask_words);
-      if (always) hit = min(hit, first_meet(blk, pg.always_off, row, pg.mask_words));
-    }
-  }
-  const bool verdict = hit != kNoHit;
-  count_hits(T, pg, hit, s_hits, lane);
-  out.put((size_t)t * kWave + lane, verdict, verdict ? pg.rule_base + hit : kNoHit);
-  n_allow += counted && verdict;
-  n_deny += counted && !verdict;
-}
-
-template <int N>
-__device__ __forceinline__ void http_pair_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
-                                            const uint32_t* __restrict__ blk, const TileRef ra, const TileRef rb,
-                                            uint32_t ua, uint32_t ub, const TilePre& ca, const TilePre& cb,
-                                            bool has_next, bool next_pair, const TileRef rna, const TileRef rnb,
-                                            uint32_t nua, uint32_t nub, TilePre& xa, TilePre& xb, uint32_t tail,
-                                            uint32_t ta, uint32_t tb, const uint8_t* __restrict__ arena,
-                                            uint64_t arena_bytes, VOut out, uint32_t lane, uint32_t& n_allow,
-                                            uint32_t& n_deny, uint32_t* s_hits) {
-  // a rolling window of kW units per chain: unit k + kW loads when unit k
-  // starts walking
-  constexpr int kW = N < 2 ? (N > 0 ? N : 1) : 2;
-  uint4 wa[kW], wb[kW];
-#pragma unroll
-  for (int k = 0; k < kW && k < N; ++k) {
-    wa[k] = k == 0 ? ca.u[0] : ld_nt(pair_unit(ra, ua, k));
-    wb[k] = k == 0 ? cb.u[0] : ld_nt(pair_unit(rb, ub, k));
-  }
-  if (has_next) {
-    tile_prefetch(rna, nua, lane, xa);
-    if (next_pair) tile_prefetch(rnb, nub, lane, xb);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  const uint32_t dead = pt.dead;
-  uint32_t sa = pt.start, sb = pt.start;
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    const uint4 a = wa[k % kW], b = wb[k % kW];
-    if (k + kW < N) {
-      wa[k % kW] = ld_nt(pair_unit(ra, ua, k + kW));
-      wb[k % kW] = ld_nt(pair_unit(rb, ub, k + kW));
-    }
-    const bool last = k == N - 1;
-    lds_cls_step2x16<0>(dead, sa, a, sb, b);
-    lds_cls_step2x16<1>(dead, sa, a, sb, b);
-    lds_cls_step2x16<2>(dead, sa, a, sb, b);
-    lds_cls_step2x16<3>(dead, sa, a, sb, b);
-    if (!last || tail > 4) {
-      lds_cls_step2x16<4>(dead, sa, a, sb, b);
-      lds_cls_step2x16<5>(dead, sa, a, sb, b);
-      lds_cls_step2x16<6>(dead, sa, a, sb, b);
-      lds_cls_step2x16<7>(dead, sa, a, sb, b);
-    }
-    if (!last || tail > 8) {
-      lds_cls_step2x16<8>(dead, sa, a, sb, b);
-      lds_cls_step2x16<9>(dead, sa, a, sb, b);
-      lds_cls_step2x16<10>(dead, sa, a, sb, b);
-      lds_cls_step2x16<11>(dead, sa, a, sb, b);
-    }
-    if (!last || tail > 12) {
-      lds_cls_step2x16<12>(dead, sa, a, sb, b);
-      lds_cls_step2x16<13>(dead, sa, a, sb, b);
-      lds_cls_step2x16<14>(dead, sa, a, sb, b);
-      lds_cls_step2x16<15>(dead, sa, a, sb, b);
-    }
-  }
-  pair_verdict(T, pg, pt, blk, ca.meta, sa, arena, arena_bytes, ta, out, lane, n_allow, n_deny, s_hits);
-  pair_verdict(T, pg, pt, blk, cb.meta, sb, arena, arena_bytes, tb, out, lane, n_allow, n_deny, s_hits);
-}
-
-template <int N, bool kCls>
-__device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
-                                            uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
-                                            const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
-                                            uint32_t tail, TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
-                                            uint64_t arena_bytes, VOut out, uint32_t lane,
-                                            uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits);
-
-// A wave's tiles of a class-mode one-part program in pairs (t, t + nw), then
-// (t + 2nw, t + 3nw), ...; a last lone tile goes through http_tile_n.
-__device__ __forceinline__ void one_part_pairs(const HttpDev& T, const HttpProg& pg, const HttpPart& pt, uint32_t prog,
-                                               const uint32_t* __restrict__ lcells, const uint8_t* __restrict__ tiles,
-                                               const HttpTile* __restrict__ ttab, uint32_t t, uint32_t tend,
-                                               uint32_t nw, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                               VOut out, uint32_t lane, uint32_t& n_allow, uint32_t& n_deny,
-                                               uint32_t* s_hits) {
-  HttpTile ta = ttab[t];
-  HttpTile tb = ttab[t + nw < tend ? t + nw : t];
-  TileRef ra = tile_ref(tiles, ta), rb = tile_ref(tiles, tb);
-  TilePre pa, pb;
-  tile_prefetch(ra, tile_units(ta), lane, pa);
-  tile_prefetch(rb, tile_units(tb), lane, pb);
-  for (; t < tend; t += 2 * nw) {
-    const uint32_t tn = t + 2 * nw;
-    const bool has_next = tn < tend, next_pair = tn + nw < tend;
-    const HttpTile tna = ttab[has_next ? tn : t], tnb = ttab[next_pair ? tn + nw : (has_next ? tn : t)];
-    const TileRef rna = tile_ref(tiles, tna), rnb = tile_ref(tiles, tnb);
-    TilePre xa = pa, xb = pb;
-    if (t + nw >= tend) {  // a lone last tile (wave-uniform)
-      switch (tile_units(ta)) {
-#define CG_TILE_1(n)                                                                                               \
-  case n:                                                                                                          \
-    http_tile_n<n, true>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena, arena_bytes, \
-                         out, lane, n_allow, n_deny, s_hits);                                                     \
-    break;
-        CG_TILE_1(0) CG_TILE_1(1) CG_TILE_1(2) CG_TILE_1(3) CG_TILE_1(4) CG_TILE_1(5) CG_TILE_1(6) CG_TILE_1(7)
-        default:
-          http_tile_n<8, true>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena,
-                               arena_bytes, out, lane, n_allow, n_deny, s_hits);
-#undef CG_TILE_1
-      }
-      break;
-    }
-    const uint32_t ua = tile_units(ta), ub = tile_units(tb), n = max(ua, ub);
-    // the last unit's 4-byte groups holding a string byte of a tile that
-    // reaches it (a shorter tile re-reads an earlier unit there: skippable)
-    const uint32_t tail = max(ua == n ? tile_tail(ta) : 0u, ub == n ? tile_tail(tb) : 0u);
-    switch (n) {  // wave-uniform
-#define CG_PAIR_N(k)                                                                                              \
-  case k:                                                                                                         \
-    http_pair_n<k>(T, pg, pt, lcells, ra, rb, ua, ub, pa, pb, has_next, next_pair, rna, rnb, tile_units(tna),     \
-                   tile_units(tnb), xa, xb, tail, t, t + nw, arena, arena_bytes, out, lane, n_allow, n_deny,      \
-                   s_hits);                                                                                       \
-    break;
-      CG_PAIR_N(0) CG_PAIR_N(1) CG_PAIR_N(2) CG_PAIR_N(3) CG_PAIR_N(4) CG_PAIR_N(5) CG_PAIR_N(6) CG_PAIR_N(7)
-      default:
-        http_pair_n<8>(T, pg, pt, lcells, ra, rb, ua, ub, pa, pb, has_next, next_pair, rna, rnb, tile_units(tna),
-                       tile_units(tnb), xa, xb, tail, t, t + nw, arena, arena_bytes, out, lane, n_allow, n_deny,
-                       s_hits);
-#undef CG_PAIR_N
-    }
-    ta = tna;
-    tb = tnb;
-    ra = rna;
-    rb = rnb;
-    pa = xa;
-    pb = xb;
-  }
-}
-
 // A wave's tiles t, t + nw, ... < tend of a one-part program whose block is
 // in LDS: each tile's walk specialized on its string units (wave-uniform).
-template <bool kCls>
+template <bool kCls, bool kRaw>
 __device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg& pg, const HttpPart& pt, uint32_t prog,
                                                const uint32_t* __restrict__ lcells, const uint8_t* __restrict__ tiles,
                                                const HttpTile* __restrict__ ttab, uint32_t t, uint32_t tend,
                                                uint32_t nw, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                VOut out, uint32_t lane, uint32_t& n_allow,
-                                               uint32_t& n_deny, uint32_t* s_hits) {
+                                               uint32_t& n_deny, uint32_t* s_hits, uint32_t cm) {
   if (t >= tend) return;
-  if (kPairTiles && kCls) {
-    one_part_pairs(T, pg, pt, prog, lcells, tiles, ttab, t, tend, nw, arena, arena_bytes, out, lane, n_allow, n_deny,
-                   s_hits);
-    return;
-  }
   HttpTile tt = ttab[t];
   TileRef tb = tile_ref(tiles, tt);
   TilePre pre;
@@ -655,13 +479,13 @@ __device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg&
     switch (tile_units(tt)) {  // wave-uniform
 #define CG_TILE_N(n)                                                                                                \
   case n:                                                                                                           \
-    http_tile_n<n, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t, arena, arena_bytes, out, \
-                         lane, n_allow, n_deny, s_hits);                                                            \
+    http_tile_n<n, kCls, kRaw>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t, arena, \
+                               arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);                                \
     break;
       CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
       default:
-        http_tile_n<8, kCls>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t, arena, arena_bytes,
-                             out, lane, n_allow, n_deny, s_hits);
+        http_tile_n<8, kCls, kRaw>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t,
+                                   arena, arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);
 #undef CG_TILE_N
     }
     tt = ttn;
@@ -712,11 +536,14 @@ __device__ __forceinline__ void flush_counts(const HttpDev& T, uint32_t prog, ui
 // is staged when the program changes; kGlobal = true: the remaining chunks
 // (programs too large for LDS), walked from global memory — a separate kernel
 // so the rare path does not set the common one's register budget.
-template <bool kGlobal>
+// kRaw: the batch's strings are raw bytes (device-layout raw batches), coded
+// through `codes` (per program 256 bytes) as they walk: a class-mode
+// program's map is staged in LDS after its block, at byte address cm.
+template <bool kGlobal, bool kRaw>
 __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __restrict__ batch, size_t nslots,
                                             const uint8_t* __restrict__ arena, VOut out,
                                             uint32_t* lcells, uint32_t* s_cnt, uint32_t* s_hits,
-                                            uint32_t* __restrict__ deal) {
+                                            uint32_t* __restrict__ deal, const uint8_t* __restrict__ codes) {
   const HttpBatchHeader* H = reinterpret_cast<const HttpBatchHeader*>(batch);
   const uint32_t magic = H->magic, epoch = H->epoch, nchunks = H->nchunks, ntiles = H->ntiles;
   const uint64_t toff = H->tiles_off, arena_bytes = H->arena_bytes;
@@ -769,6 +596,8 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
       flush_counts(T, cur, n_allow, n_deny, lane, s_cnt, s_hits);
       if (lds)
         for (uint32_t i = threadIdx.x; i < pg.cell_count; i += blockDim.x) lcells[i] = T.cells[pg.cell_begin + i];
+      if (kRaw && lds && (pg.flags & kProgClass) && threadIdx.x < 64)
+        lcells[T.lds_cells + threadIdx.x] = reinterpret_cast<const uint32_t*>(codes + (size_t)prog * 256)[threadIdx.x];
       __syncthreads();
       cur = prog;
     }
@@ -788,16 +617,16 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
         const uint32_t tile[1] = {t};
         const bool valid[1] = {true};
         http_tiles<1>(T, pg, prog, T.cells + pg.cell_begin, rebased, tiles, ttab, tile, valid, arena, arena_bytes, out, lane,
-                      n_allow, n_deny, s_hits);
+                      n_allow, n_deny, s_hits, kRaw ? codes : nullptr);
       }
     } else if (pg.part_count == 1) {
       const HttpPart pt = T.parts[pg.part_begin];
       if (pt.mode == kPartClass)
-        one_part_tiles<true>(T, pg, pt, prog, lcells, tiles, ttab, ch.first_tile + wave, tend, nw, arena, arena_bytes,
-                             out, lane, n_allow, n_deny, s_hits);
+        one_part_tiles<true, kRaw>(T, pg, pt, prog, lcells, tiles, ttab, ch.first_tile + wave, tend, nw, arena,
+                                   arena_bytes, out, lane, n_allow, n_deny, s_hits, T.lds_cells * 4);
       else
-        one_part_tiles<false>(T, pg, pt, prog, lcells, tiles, ttab, ch.first_tile + wave, tend, nw, arena,
-                              arena_bytes, out, lane, n_allow, n_deny, s_hits);
+        one_part_tiles<false, kRaw>(T, pg, pt, prog, lcells, tiles, ttab, ch.first_tile + wave, tend, nw, arena,
+                                    arena_bytes, out, lane, n_allow, n_deny, s_hits, 0u);
     } else {
       // each wave takes kTilesPerWave tiles at a time (wave, wave + nw, ...)
       for (uint32_t t0 = ch.first_tile + wave; t0 < tend; t0 += kTilesPerWave * nw) {
@@ -810,7 +639,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
           tile[j] = valid[j] ? t : t0;
         }
         http_tiles<kTilesPerWave>(T, pg, prog, lcells, true, tiles, ttab, tile, valid, arena, arena_bytes, out, lane,
-                                  n_allow, n_deny, s_hits);
+                                  n_allow, n_deny, s_hits, kRaw ? codes : nullptr);
       }
     }
   }
@@ -826,44 +655,50 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
   flush_counts(T, cur, n_allow, n_deny, lane, s_cnt, s_hits);
 }
 
+template <bool kRaw>
 __global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
     uint8_t* __restrict__ out, const uint32_t* __restrict__ order, uint32_t* __restrict__ deal,
-    uint32_t* __restrict__ rule, uint32_t nout) {
+    uint32_t* __restrict__ rule, uint32_t nout, const uint8_t* __restrict__ codes) {
   // dynamic LDS only, so the program block starts at LDS address 0 (a
   // class-mode step's address is then just state + code): [block:
-  // T.lds_cells][rule hits: kLdsRuleHits][allowed, denied, deal ticket]
+  // T.lds_cells][code map: 64 words, kRaw][rule hits: kLdsRuleHits][allowed, denied, deal ticket]
   extern __shared__ __attribute__((aligned(16))) uint32_t lcells[];
-  uint32_t* s_hits = lcells + T.lds_cells;
+  uint32_t* s_hits = lcells + T.lds_cells + (kRaw ? 64 : 0);
   uint32_t* s_cnt = s_hits + kLdsRuleHits;
   for (uint32_t i = threadIdx.x; i < kLdsRuleHits; i += blockDim.x) s_hits[i] = 0;
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<false>(T, batch, nslots, arena, VOut{out, order, rule, nout}, lcells, s_cnt, s_hits, deal);
+  http_chunks<false, kRaw>(T, batch, nslots, arena, VOut{out, order, rule, nout}, lcells, s_cnt, s_hits, deal, codes);
 }
 
+template <bool kRaw>
 __global__ __launch_bounds__(kHttpThreads) void http_kernel_global(HttpDev T, const uint8_t* __restrict__ batch,
                                                                    size_t nslots, const uint8_t* __restrict__ arena,
                                                                    uint8_t* __restrict__ out,
                                                                    const uint32_t* __restrict__ order,
-                                                                   uint32_t* __restrict__ rule, uint32_t nout) {
+                                                                   uint32_t* __restrict__ rule, uint32_t nout,
+                                                                   const uint8_t* __restrict__ codes) {
   __shared__ uint32_t s_cnt[3];
   if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
   __syncthreads();
-  http_chunks<true>(T, batch, nslots, arena, VOut{out, order, rule, nout}, nullptr, s_cnt, nullptr, nullptr);
+  http_chunks<true, kRaw>(T, batch, nslots, arena, VOut{out, order, rule, nout}, nullptr, s_cnt, nullptr, nullptr,
+                          codes);
 }
 
 }  // namespace
 
 int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_t* arena, uint8_t* out, void* stream,
-                int cus, const uint32_t* order, uint32_t* rule, uint32_t nout) {
+                int cus, const uint32_t* order, uint32_t* rule, uint32_t nout, const uint8_t* codes) {
   if (nslots == 0) return 0;
   // hipFuncSetAttribute and the occupancy answer are per device: cached per
   // device ordinal, set once under a lock (handles on several GPUs may launch
   // from several threads)
   int dev = 0;
   (void)hipGetDevice(&dev);
-  const size_t lds = ((size_t)t.lds_cells + kLdsRuleHits + 3) * 4;
+  const bool raw = codes != nullptr;
+  const size_t lds = ((size_t)t.lds_cells + (raw ? 64 : 0) + kLdsRuleHits + 3) * 4;
+  const void* kern = raw ? (const void*)http_kernel<true> : (const void*)http_kernel<false>;
   int occ = 1;
   uint32_t* deal = nullptr;
   // The ticket reset and both launches are enqueued under one lock: two
@@ -892,14 +727,15 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
       if (rc != hipSuccess) return (int)rc;
     }
     if (attr_set.insert(dev).second)
-      (void)hipFuncSetAttribute((const void*)http_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const void* k : {(const void*)http_kernel<false>, (const void*)http_kernel<true>})
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     auto it = occ_cache.find({dev, lds});
     if (it == occ_cache.end()) {
       // one resident wave of workgroups: as many per CU as LDS and registers
       // allow (the largest staged program block sets the LDS share), then the
       // workgroups deal the chunks among themselves
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)http_kernel, kHttpThreads, lds) !=
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kHttpThreads, lds) !=
               hipSuccess ||
           nb < 1)
         nb = 1;
@@ -912,12 +748,20 @@ int launch_http(const HttpDev& t, const void* batch, size_t nslots, const uint8_
   }
   const size_t tiles = nslots / kWave;
   size_t grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * occ);
-  hipLaunchKernelGGL(http_kernel, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
-                     (const uint8_t*)batch, nslots, arena, out, order, deal, rule, nout);
+  if (raw)
+    hipLaunchKernelGGL(http_kernel<true>, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
+                       (const uint8_t*)batch, nslots, arena, out, order, deal, rule, nout, codes);
+  else
+    hipLaunchKernelGGL(http_kernel<false>, dim3((unsigned)grid), dim3(kHttpThreads), lds, (hipStream_t)stream, t,
+                       (const uint8_t*)batch, nslots, arena, out, order, deal, rule, nout, codes);
   if (t.n_global_progs) {
     grid = std::min<size_t>(std::max<size_t>(tiles, 1), (size_t)cus * 2);
-    hipLaunchKernelGGL(http_kernel_global, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream, t,
-                       (const uint8_t*)batch, nslots, arena, out, order, rule, nout);
+    if (raw)
+      hipLaunchKernelGGL(http_kernel_global<true>, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream,
+                         t, (const uint8_t*)batch, nslots, arena, out, order, rule, nout, codes);
+    else
+      hipLaunchKernelGGL(http_kernel_global<false>, dim3((unsigned)grid), dim3(kHttpThreads), 0, (hipStream_t)stream,
+                         t, (const uint8_t*)batch, nslots, arena, out, order, rule, nout, codes);
   }
   return (int)hipGetLastError();
 }

@@ -1406,8 +1406,9 @@ __device__ __forceinline__ lds_u32* raw_tables(lds_u32* lds, uint32_t F) { retur
 
 // The string of a request parsed from the stage (parse_head_fast /
 // parse_list_fast spans, relative to hs) into o.
+template <class Out>
 __device__ __forceinline__ void emit_stage(const HttpRawDev& R, const lds_u8* st, uint32_t hs, const lds_u32* sp,
-                                           uint32_t stride, const Parsed& P, uint32_t last, TileOut& o) {
+                                           uint32_t stride, const Parsed& P, uint32_t last, Out& o) {
   uint32_t f = 0;
   for (uint32_t rem = P.present; rem; rem &= rem - 1) {
     const uint32_t g = (uint32_t)__builtin_ctz(rem);
@@ -1427,8 +1428,9 @@ __device__ __forceinline__ void emit_stage(const HttpRawDev& R, const lds_u8* st
 
 // The string of a request parsed through a HeadReader (parse_head /
 // parse_list_bytes spans, absolute, kAbsentSpan for absent fields) into o.
+template <class Out>
 __device__ __forceinline__ void emit_reader(const HttpRawDev& R, HeadReader& hr, const lds_u32* sp, uint32_t stride,
-                                            uint32_t last, TileOut& o) {
+                                            uint32_t last, Out& o) {
   for (uint32_t f = 0; f < last; ++f) {
     const uint32_t s = sp[f * stride];
     if (s == kAbsentSpan) {
@@ -1607,7 +1609,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
     list_append(L.walk, &L.ctl[kRawCtlWalk], walk, (uint32_t)i, lane);
     if (want && sl.ok) {
       raw_fill(L, sl, (uint32_t)i, cur.rem, flags, units, len, [&](uint4* dst) {
-        TileOut o(dst, R.codes + (size_t)prog * 256);
+        TileOut<false> o(dst, nullptr);  // raw bytes: http_kernel codes them
         emit_stage(R, stage, hs, sp, kRawThreads, P, last, o);
       });
     }
@@ -1661,7 +1663,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_defer_dl_kernel(HttpRawDev R,
     list_append(L.walk, &L.ctl[kRawCtlWalk], walk, i, lane);
     if (want && sl.ok) {
       raw_fill(L, sl, i, remote[i], flags, units, len, [&](uint4* dst) {
-        TileOut o(dst, R.codes + (size_t)prog * 256);
+        TileOut<false> o(dst, nullptr);  // raw bytes: http_kernel codes them
         emit_reader(R, hr, sp, kRawThreads, last, o);
       });
     }

@@ -21,6 +21,9 @@ CG_HD inline uint32_t code4(const uint8_t* lut, uint32_t q) {
 // Bytes gather in 16; each full unit is coded and stored to the slot's next
 // string unit (64 uint4 = 1 KiB apart in the tile); in the last unit the
 // bytes past the string stay zero (the walk's padding).
+// kCode = false: the bytes go out uncoded (the device-layout scan: http_kernel
+// codes them as it walks, launch_http `codes`).
+template <bool kCode = true>
 struct TileOut {
   uint32_t w0, w1, w2, w3, pos;
   uint4* dst;               // the slot's next string unit
@@ -46,7 +49,7 @@ struct TileOut {
   }
   CG_HD inline void put(uint32_t b) { put4(b, 1); }
   CG_HD inline void flush() {
-    *dst = make_uint4(code4(lut, w0), code4(lut, w1), code4(lut, w2), code4(lut, w3));
+    *dst = kCode ? make_uint4(code4(lut, w0), code4(lut, w1), code4(lut, w2), code4(lut, w3)) : make_uint4(w0, w1, w2, w3);
     dst += 64;
     w0 = w1 = w2 = w3 = 0;
     pos = 0;
@@ -58,8 +61,8 @@ struct TileOut {
     auto keep = [&](uint32_t c, uint32_t at) {  // bytes of dword `at` below p
       return p >= at + 4 ? c : p <= at ? 0u : c & ((1u << (8 * (p - at))) - 1u);
     };
-    *dst = make_uint4(keep(code4(lut, w0), 0), keep(code4(lut, w1), 4), keep(code4(lut, w2), 8),
-                      keep(code4(lut, w3), 12));
+    auto c = [&](uint32_t w) { return kCode ? code4(lut, w) : w; };
+    *dst = make_uint4(keep(c(w0), 0), keep(c(w1), 4), keep(c(w2), 8), keep(c(w3), 12));
   }
 };
 

@@ -45,18 +45,29 @@ int main() {
     const size_t len = want.size(), units = (len + 15) / 16;
     std::vector<uint4> buf((units + 1) * 64);
     memset(buf.data(), 0xAB, buf.size() * sizeof(uint4));
-    cg::TileOut o(buf.data() + 3, lut);  // lane 3 of the tile row
-    for (auto& c : calls) {
-      if (c.second == 1 && (rng() & 1)) o.put(c.first);
-      else o.put4(c.first, c.second);
+    // even iterations: coded (the default path's bytes); odd: raw bytes
+    // (TileOut<false>, the device-layout scan's: http_kernel codes them)
+    const bool coded = (iter & 1) == 0;
+    auto feed = [&](auto& o) {
+      for (auto& c : calls) {
+        if (c.second == 1 && (rng() & 1)) o.put(c.first);
+        else o.put4(c.first, c.second);
+      }
+      o.finish();
+    };
+    if (coded) {
+      cg::TileOut<true> o(buf.data() + 3, lut);  // lane 3 of the tile row
+      feed(o);
+    } else {
+      cg::TileOut<false> o(buf.data() + 3, nullptr);
+      feed(o);
     }
-    o.finish();
     for (size_t u = 0; u <= units; ++u) {
       uint8_t got[16];
       memcpy(got, &buf[u * 64 + 3], 16);
       for (int j = 0; j < 16; ++j) {
         const size_t at = u * 16 + j;
-        const uint8_t exp = u == units ? 0xAB : at < len ? lut[want[at]] : 0;
+        const uint8_t exp = u == units ? 0xAB : at < len ? (coded ? lut[want[at]] : want[at]) : 0;
         if (got[j] != exp) {
           if (bad++ < 5)
             fprintf(stderr, "iter %d len %zu unit %zu byte %d: got %02x want %02x\n", iter, len, u, j, got[j], exp);

@@ -182,4 +182,4 @@ def test_gpu_compressed_sets_decoded_on_device(gpu, host):
     assert records_view(*g) == oracle_view([R.decode(r) for r in reqs], red, rem, host.kafka_intern)
     inflated, deferred = i1.value - i0.value, d1.value - d0.value
     print(f"compressed payloads decoded on the device: {inflated}, requests finished by the host: {deferred}")
-    assert inflated > 100 and deferred < inflated / 4, (inflated, deferred)
+    assert inflated > 100 and deferred < inflated / 2, (inflated, deferred)
