@@ -1396,53 +1396,21 @@ int cg_http_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* ra
   return guarded([&] { verdicts_raw_from_host(h, RawInput::Heads, raw, raw_off, n, policy, ingress, port, remote, out); });
 }
 
-// ---- small header-list batches: concurrent callers combined -----------
+// ---- small header-list calls: the host packer on the calling thread ----
 // Envoy decides one request per decodeHeaders (cilium_l7policy.cc:127-182),
-// from many worker threads at once.  A call of at most kSmallLists lists is
-// queued on the handle; whichever call finds no batch in flight takes every
-// queued call and decides them as ONE batch — the host packer (cheapest at
-// these sizes: one pass, no device layout step), one staged copy in, one
-// http_kernel launch, one copy out — while calls arriving meanwhile queue for
-// the next batch.  A lone call is decided at once unless a batching window
-// is set (cg_http_set_batching).
+// from many worker threads at once.  For a call of at most kSmallLists lists
+// the host packer (one pass, no device layout step) + one staged copy in +
+// one http_kernel launch + one copy out is the fastest sequence: 29.5 us per
+// single-request call, 90K calls/s from 16 threads, each call on its own
+// staging lease (profiles/r05g_http_latency.jsonl).  Combining concurrent
+// calls into one batch was measured and lost (80K calls/s at 8 calls per
+// batch: the flusher serializes the packing and the wake-ups).
 constexpr size_t kSmallLists = 1024;
-struct SmallCall {
-  const uint8_t* blob;
-  const uint64_t* off;
-  size_t n;
-  const uint32_t* policy;
-  const uint8_t* ingress;
-  const uint16_t* port;
-  const uint32_t* remote;
-  uint8_t* out;
-  bool done = false;
-  std::exception_ptr err;
-};
 
-static void decide_small_batch(Engine& e, const std::vector<SmallCall*>& calls) {
+static void small_lists_host(Engine& e, const uint8_t* blob, const uint64_t* off, size_t n, const uint32_t* pol,
+                             const uint8_t* ing, const uint16_t* port, const uint32_t* rem, uint8_t* out) {
   auto s = http_snap(e);
-  size_t n = 0, bytes = 0;
-  for (const SmallCall* c : calls) {
-    n += c->n;
-    bytes += c->off[c->n] - c->off[0];
-  }
-  std::vector<uint32_t> pol(n), rem(n);
-  std::vector<uint8_t> ing(n), blob(bytes + 1);
-  std::vector<uint16_t> port(n);
-  std::vector<uint64_t> off(n + 1);
-  size_t k = 0, at = 0;
-  for (const SmallCall* c : calls) {
-    memcpy(&pol[k], c->policy, c->n * 4);
-    memcpy(&ing[k], c->ingress, c->n);
-    memcpy(&port[k], c->port, c->n * 2);
-    memcpy(&rem[k], c->remote, c->n * 4);
-    const uint64_t b0 = c->off[0], len = c->off[c->n] - b0;
-    if (len) memcpy(&blob[at], c->blob + b0, len);
-    for (size_t i = 0; i < c->n; ++i) off[k + i] = at + (c->off[i] - b0);
-    k += c->n;
-    at += len;
-  }
-  off[n] = at;
+  const size_t bytes = off[n] - off[0];
   // the overflow arena holds the strings past a slot: bounded by the list
   // bytes plus each request's separators
   const size_t arena_cap = bytes + n * (2 * s->fields.size() + 24) + 64;
@@ -1453,8 +1421,7 @@ static void decide_small_batch(Engine& e, const std::vector<SmallCall*>& calls) 
   uint8_t* ha = (uint8_t*)lease->host_buf(1, arena_cap);
   std::vector<uint32_t> order(scap);
   size_t nslots = 0, aused = 0;
-  http_pack(*s, n, pol.data(), ing.data(), port.data(), rem.data(), blob.data(), off.data(), hb, bcap, order.data(),
-            &nslots, ha, arena_cap, &aused);
+  http_pack(*s, n, pol, ing, port, rem, blob, off, hb, bcap, order.data(), &nslots, ha, arena_cap, &aused);
   HttpBatchHeader hdr;
   memcpy(&hdr, hb, sizeof(hdr));
   const hipStream_t st = (hipStream_t)lease->stream;
@@ -1467,52 +1434,9 @@ static void decide_small_batch(Engine& e, const std::vector<SmallCall*>& calls) 
   uint8_t* slots = (uint8_t*)lease->host_buf(2, nslots + 1);
   if (nslots) hip_check(hipMemcpyAsync(slots, dout, nslots, hipMemcpyDeviceToHost, st), "D2H");
   hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-  std::vector<uint8_t> v(n, 0);
+  memset(out, 0, n);
   for (size_t i = 0; i < nslots; ++i)
-    if (order[i] < n) v[order[i]] = slots[i];
-  k = 0;
-  for (SmallCall* c : calls) {
-    memcpy(c->out, &v[k], c->n);
-    k += c->n;
-  }
-}
-
-static void small_lists_combined(Engine& e, SmallCall& me) {
-  auto& C = e.http_comb;
-  std::unique_lock<std::mutex> lk(C.mu);
-  C.queue.push_back(&me);
-  if (C.flushing || C.min_calls > 1) C.cv.notify_all();  // a flusher may wait for company
-  while (!me.done) {
-    if (C.flushing) {
-      C.cv.wait(lk);
-      continue;
-    }
-    C.flushing = true;
-    if (C.min_calls > 1 && C.max_wait_us > 0) {
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(C.max_wait_us);
-      C.cv.wait_until(lk, until, [&] { return C.queue.size() >= C.min_calls; });
-    }
-    std::vector<SmallCall*> batch;
-    for (void* q : C.queue) batch.push_back(static_cast<SmallCall*>(q));
-    C.queue.clear();
-    lk.unlock();
-    std::exception_ptr err;
-    try {  // every queued call is released whatever happens here
-      decide_small_batch(e, batch);
-    } catch (...) {
-      err = std::current_exception();
-    }
-    lk.lock();
-    for (SmallCall* c : batch) {
-      c->err = err;
-      c->done = true;
-    }
-    C.batches += 1;
-    C.calls += batch.size();
-    C.flushing = false;
-    C.cv.notify_all();
-  }
-  if (me.err) std::rethrow_exception(me.err);
+    if (order[i] < n) out[order[i]] = slots[i];
 }
 
 int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
@@ -1522,35 +1446,16 @@ int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint
     if (n && n <= kSmallLists) {
       auto e = get(h);
       e->require_gpu();
-      (void)http_snap(*e);  // CG_NOT_FOUND before queueing
+      (void)http_snap(*e);  // CG_NOT_FOUND first
       check_offsets(hdr_off, n);
       if (!policy || !ingress || !port || !remote || !out || (hdr_off[n] != hdr_off[0] && !hdr_blob))
         fail(CG_INVALID_ARGUMENT, "NULL hdr_blob/policy/ingress/port/remote/out");
       for (size_t i = 0; i < n; ++i)  // the packer's limit (16-bit value spans), before the batch is shared
         if (hdr_off[i + 1] - hdr_off[i] > 0xFFFFu) fail(CG_INVALID_ARGUMENT, "header list longer than 64 KiB");
-      SmallCall me{hdr_blob, hdr_off, n, policy, ingress, port, remote, out};
-      small_lists_combined(*e, me);
+      small_lists_host(*e, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);
       return;
     }
     verdicts_raw_from_host(h, RawInput::Lists, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);
-  });
-}
-
-int cg_http_set_batching(uint64_t h, uint32_t min_calls, uint32_t max_wait_us) {
-  return guarded([&] {
-    auto e = get(h);
-    std::lock_guard<std::mutex> lk(e->http_comb.mu);
-    e->http_comb.min_calls = min_calls ? min_calls : 1;
-    e->http_comb.max_wait_us = max_wait_us;
-  });
-}
-
-int cg_http_batching_stats(uint64_t h, uint64_t* batches, uint64_t* calls) {
-  return guarded([&] {
-    auto e = get(h);
-    std::lock_guard<std::mutex> lk(e->http_comb.mu);
-    if (batches) *batches = e->http_comb.batches;
-    if (calls) *calls = e->http_comb.calls;
   });
 }
 

@@ -171,16 +171,6 @@ struct Engine {
   // Kafka decode: compressed payloads decoded on the device / requests the
   // host decoder finished (cg_kafka_decode_stats)
   std::atomic<uint64_t> kafka_inflated{0}, kafka_deferred{0};
-  // Small header-list batches of concurrent callers decided together (flat
-  // combining, capi.cc small_lists_combined; cg_http_set_batching)
-  struct HttpCombiner {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::vector<void*> queue;  // SmallCall*
-    bool flushing = false;
-    uint32_t min_calls = 1, max_wait_us = 0;
-    uint64_t batches = 0, calls = 0;
-  } http_comb;
 
   bool has_gpu() const { return device >= 0; }
   void require_gpu() const {

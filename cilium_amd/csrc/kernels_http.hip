@@ -79,32 +79,44 @@ __device__ __forceinline__ uint32_t lds_cls_step16(uint32_t dead, uint32_t st, c
 
 // 16 raw string bytes → their class codes through the program's code map,
 // staged in LDS at byte address cm (raw-byte batches, launch_http codes):
-// each byte is one d16 LDS load into the low or high half of one of two
-// dwords per word (bytes 0 and 2, 1 and 3), joined by one shift-or — 1.25
-// VALU and one LDS read per byte, none of it on the walk's dependent chain.
-__device__ __forceinline__ uint4 lds_transcode(uint32_t cm, const uint4& u) {
-  uint32_t l0, h0, l1, h1, l2, h2, l3, h3, t0, t1, t2, t3;
-#define CG_TC_WORD(L, H, W)                                                                                \
-  "v_add_u32_sdwa %8, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"    \
-  "v_add_u32_sdwa %9, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2\n\t"    \
-  "v_add_u32_sdwa %10, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n\t"   \
-  "v_add_u32_sdwa %11, %12, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3\n\t"   \
-  "ds_read_u8_d16 " L ", %8\n\t"                                                                           \
-  "ds_read_u8_d16_hi " L ", %9\n\t"                                                                        \
-  "ds_read_u8_d16 " H ", %10\n\t"                                                                          \
-  "ds_read_u8_d16_hi " H ", %11\n\t"
-  asm volatile(CG_TC_WORD("%0", "%1", "%13") CG_TC_WORD("%2", "%3", "%14") CG_TC_WORD("%4", "%5", "%15")
-                   CG_TC_WORD("%6", "%7", "%16")
+// one ds_read_u8 per byte, eight in flight per wait, each word joined by
+// three shift-ors (every address in its own register) — none of it on the walk's dependent chain.  (D16 loads
+// into the two halves of one register cannot both be in flight: the second
+// merges the register's value from before the first completes.)
+__device__ __forceinline__ uint32_t lds_code2w(uint32_t cm, uint32_t w0, uint32_t w1, uint32_t& r1) {
+  uint32_t b0, b1, b2, b3, b4, b5, b6, b7, a0, a1, a2, a3, a4, a5, a6, a7;
+#define CG_TC_ADDR(T, W, B) "v_add_u32_sdwa " T ", %16, " W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" B "\n\t"
+  asm volatile(CG_TC_ADDR("%8", "%17", "BYTE_0") CG_TC_ADDR("%9", "%17", "BYTE_1") CG_TC_ADDR("%10", "%17", "BYTE_2")
+                   CG_TC_ADDR("%11", "%17", "BYTE_3") CG_TC_ADDR("%12", "%18", "BYTE_0")
+                       CG_TC_ADDR("%13", "%18", "BYTE_1") CG_TC_ADDR("%14", "%18", "BYTE_2")
+                           CG_TC_ADDR("%15", "%18", "BYTE_3")
+               "ds_read_u8 %0, %8\n\t"
+               "ds_read_u8 %1, %9\n\t"
+               "ds_read_u8 %2, %10\n\t"
+               "ds_read_u8 %3, %11\n\t"
+               "ds_read_u8 %4, %12\n\t"
+               "ds_read_u8 %5, %13\n\t"
+               "ds_read_u8 %6, %14\n\t"
+               "ds_read_u8 %7, %15\n\t"
                "s_waitcnt lgkmcnt(0)\n\t"
                "v_lshl_or_b32 %0, %1, 8, %0\n\t"
                "v_lshl_or_b32 %2, %3, 8, %2\n\t"
                "v_lshl_or_b32 %4, %5, 8, %4\n\t"
-               "v_lshl_or_b32 %6, %7, 8, %6"
-               : "=&v"(l0), "=&v"(h0), "=&v"(l1), "=&v"(h1), "=&v"(l2), "=&v"(h2), "=&v"(l3), "=&v"(h3),
-                 "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
-               : "v"(cm), "v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
-#undef CG_TC_WORD
-  return make_uint4(l0, l1, l2, l3);
+               "v_lshl_or_b32 %6, %7, 8, %6\n\t"
+               "v_lshl_or_b32 %0, %2, 16, %0\n\t"
+               "v_lshl_or_b32 %4, %6, 16, %4"
+               : "=&v"(b0), "=&v"(b1), "=&v"(b2), "=&v"(b3), "=&v"(b4), "=&v"(b5), "=&v"(b6), "=&v"(b7),
+                 "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(a4), "=&v"(a5), "=&v"(a6), "=&v"(a7)
+               : "v"(cm), "v"(w0), "v"(w1));
+#undef CG_TC_ADDR
+  r1 = b4;
+  return b0;
+}
+__device__ __forceinline__ uint4 lds_transcode(uint32_t cm, const uint4& u) {
+  uint4 r;
+  r.x = lds_code2w(cm, u.x, u.y, r.y);
+  r.z = lds_code2w(cm, u.z, u.w, r.w);
+  return r;
 }
 
 // Where verdicts go: out[slot] (slot order), or — for a batch built on the

@@ -500,22 +500,14 @@ int cg_http_verdicts_fields_dev(uint64_t h, const uint8_t* d_hdr_blob, const uin
                                 const uint32_t* d_remote, uint8_t* d_out, void* stream);
 
 /* cg_http_verdicts_fields_dev from host memory (staged in, verdicts copied
- * out): the drop-in for cg_http_pack + cg_http_verdicts_host. */
+ * out): the drop-in for cg_http_pack + cg_http_verdicts_host.  A call of at
+ * most 1024 lists (Envoy-sized: decodeHeaders decides one request,
+ * envoy/cilium_l7policy.cc:127-182) is packed on the calling thread and
+ * decided with one staged copy in, one launch and one copy out; larger ones
+ * are grouped and packed on the GPU. */
 int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
                                  const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                                  const uint32_t* remote, uint8_t* out);
-
-/* Calls of cg_http_verdicts_fields_host with at most 1024 lists are decided
- * together with the concurrent small calls of other threads on the same
- * handle (one packed batch, one http_kernel launch: Envoy workers deciding a
- * few requests each, envoy/cilium_l7policy.cc:127-182).  A call that finds
- * no batch in flight becomes the flusher; with min_calls > 1 it waits until
- * min_calls calls are queued or max_wait_us microseconds have passed.
- * Default (1, 0): decide at once.  No reference counterpart (Envoy decides
- * each request inline); a latency/throughput knob. */
-int cg_http_set_batching(uint64_t h, uint32_t min_calls, uint32_t max_wait_us);
-/* Small-call batches decided and the calls they served (cumulative). */
-int cg_http_batching_stats(uint64_t h, uint64_t* batches, uint64_t* calls);
 
 /* NetworkPolicyMap::Allowed per slot (cilium_network_policy.h:223-237):
  * d_out[slot] = 1 allow, 0 deny (→ 403), in batch slot order.  d_arena may

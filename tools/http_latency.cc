@@ -7,11 +7,10 @@
 // lists it has (cg_http_pack's name\0value\0 input) in batches of B requests.
 // Two host entries are timed, each for B in {1, 16, 256, 4096, 65536} and 1
 // and 16 submitting threads:
-//   fields  cg_http_verdicts_fields_host: calls of <= 1024 lists combined
-//           across threads (one host-packed batch, one launch; also with a
-//           batching window of 16 calls / 200 us), larger ones: lists →
-//           pinned staging → H2D → grouping/packing on the GPU →
-//           http_kernel → D2H
+//   fields  cg_http_verdicts_fields_host: calls of <= 1024 lists packed on
+//           the calling thread (one copy in, one launch, one copy out),
+//           larger ones: lists → pinned staging → H2D → grouping/packing on
+//           the GPU → http_kernel → D2H
 //   pack    cg_http_pack on the calling thread (CPU packer) +
 //           cg_http_verdicts_host (staging → H2D → http_kernel → D2H)
 // Each call's verdicts are checked against the pool's expected verdicts
@@ -142,21 +141,16 @@ int main(int argc, char** argv) {
     return 2;
   }
   int rc = 0;
-  // modes: 0 cg_http_verdicts_fields_host, 1 the same with a batching window
-  // of 16 calls / 200 us (cg_http_set_batching, 16 threads only), 2 pack + host
-  for (const int mode : {0, 1, 2}) {
+  // modes: 0 cg_http_verdicts_fields_host, 2 pack + host
+  for (const int mode : {0, 2}) {
     const bool pack = mode == 2;
     for (const size_t B : {(size_t)1, (size_t)16, (size_t)256, (size_t)4096, (size_t)65536}) {
       if (B > p.n) continue;
       for (const int threads : {1, 16}) {
-        if (mode == 1 && (threads == 1 || B > 1024)) continue;
-        cg_http_set_batching(h, mode == 1 ? 16u : 1u, mode == 1 ? 200u : 0u);
         {  // warm-up (pinned buffers, workers, launch caches) outside the clock
           Result w;
           submit(h, p, pack, B, 0, 0.05, &w);
         }
-        uint64_t b0 = 0, c0 = 0, b1 = 0, c1 = 0;
-        cg_http_batching_stats(h, &b0, &c0);
         std::vector<Result> res(threads);
         std::vector<std::thread> th;
         const auto t0 = std::chrono::steady_clock::now();
@@ -164,7 +158,6 @@ int main(int argc, char** argv) {
           th.emplace_back(submit, h, std::cref(p), pack, B, (size_t)t * 7919 * B, seconds, &res[t]);
         for (auto& x : th) x.join();
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        cg_http_batching_stats(h, &b1, &c1);
         std::vector<double> lat;
         uint64_t calls = 0, bad = 0, reqs = 0;
         for (auto& r : res) {
@@ -175,12 +168,10 @@ int main(int argc, char** argv) {
         }
         printf("{\"metric\": \"HTTP verdicts through the host C ABI at Envoy batch sizes\", \"entry\": \"%s\", "
                "\"batch\": %zu, \"threads\": %d, \"calls\": %llu, \"requests_per_s\": %.1f, \"calls_per_s\": %.1f, "
-               "\"p50_us\": %.1f, \"p99_us\": %.1f, \"calls_per_batch\": %.2f, \"bad_calls\": %llu}\n",
-               pack ? "cg_http_pack+cg_http_verdicts_host"
-                    : mode == 1 ? "cg_http_verdicts_fields_host (window 16 calls / 200 us)"
-                                : "cg_http_verdicts_fields_host",
-               B, threads, (unsigned long long)calls, (double)reqs / sec, (double)calls / sec, pct(lat, 0.5),
-               pct(lat, 0.99), b1 > b0 ? (double)(c1 - c0) / (double)(b1 - b0) : 0.0, (unsigned long long)bad);
+               "\"p50_us\": %.1f, \"p99_us\": %.1f, \"bad_calls\": %llu}\n",
+               pack ? "cg_http_pack+cg_http_verdicts_host" : "cg_http_verdicts_fields_host", B, threads,
+               (unsigned long long)calls, (double)reqs / sec, (double)calls / sec, pct(lat, 0.5), pct(lat, 0.99),
+               (unsigned long long)bad);
         fflush(stdout);
         if (bad) rc = 1;
       }
