@@ -49,10 +49,10 @@ def parse():
     ap.add_argument("--small-distinct", type=int, default=262_144,
                     help="second measurement of the kernel on a batch with this many distinct requests (0: skip)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end raw-heads measurement")
-    ap.add_argument("--e2e-layout", default="host", choices=["host", "device"],
-                    help="raw path sequence for end_to_end: host (bucket counts laid out on the host) or device "
-                         "(CILIUM_GPU_RAW_LAYOUT=device: slots, chunk table and header on the device, no host "
-                         "round trip)")
+    ap.add_argument("--e2e-layout", default="device", choices=["host", "device"],
+                    help="raw path sequence for end_to_end: device (the default: slots, chunk table and header "
+                         "on the device, no host round trip) or host (CILIUM_GPU_RAW_LAYOUT=host: the round-3 "
+                         "sequence, bucket counts laid out on the host)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
@@ -201,8 +201,7 @@ def main():
                                 args.steps, args.warmup, args.layout)
     e2e = None
     if not args.no_e2e:
-        if args.e2e_layout == "device":
-            os.environ["CILIUM_GPU_RAW_LAYOUT"] = "device"
+        os.environ["CILIUM_GPU_RAW_LAYOUT"] = args.e2e_layout
         e2e = end_to_end(cl, pols, info, min(D, 4_194_304), args.requests_per_gpu, rank, dev, torch, stream,
                          args.steps, min(args.warmup, 2), not args.no_check)
         e2e["layout"] = args.e2e_layout
@@ -348,9 +347,9 @@ def end_to_end(cl, pols, info, distinct, per_gpu, rank, dev, torch, stream, step
     remote identity and a u64 offset: cg_http_verdicts_raw_dev parses,
     groups, packs and evaluates them on the GPU and writes verdicts in request
     order.  One call per step; the clock is the host's around all steps
-    (the default sequence waits on the host for the bucket counts between its
-    scan and its layout; with --e2e-layout device the calls only enqueue and
-    the steps queue back to back on the stream).  Checked
+    (the device-layout sequence, the default, only enqueues: the steps queue
+    back to back on the stream; --e2e-layout host runs the round-3 sequence,
+    which waits on the host for the bucket counts between scan and layout).  Checked
     bit-exact against the oracle (codec step oracle/http1_ref.py, then the
     Envoy-faithful rule scan) on a subsample, and every copy against its
     original."""

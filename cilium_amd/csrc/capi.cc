@@ -1357,6 +1357,9 @@ static void verdicts_raw_from_host(uint64_t h, RawInput in, const uint8_t* raw, 
   check_offsets(raw_off, n);
   if (!policy || !ingress || !port || !remote || !out || (raw_off[n] != raw_off[0] && !raw))
     fail(CG_INVALID_ARGUMENT, "NULL raw/policy/ingress/port/remote/out");
+  if (in == RawInput::Lists)  // the 16-bit value spans (the device path would deny it)
+    for (size_t i = 0; i < n; ++i)
+      if (raw_off[i + 1] - raw_off[i] > 0xFFFFu) fail(CG_INVALID_ARGUMENT, "header list longer than 64 KiB");
   const uint64_t total = raw_off[n] - raw_off[0] + 19 * (uint64_t)n;
   const size_t nchunks = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(n / 4096 + 1, total / kHostChunkBytes + 1));
   const unsigned nw = nchunks > 1 ? 2u : 1u;

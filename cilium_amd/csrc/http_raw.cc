@@ -458,10 +458,12 @@ void raw_device_layout(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lis
   sl.raw_stream = stream;
 }
 
-// CILIUM_GPU_RAW_LAYOUT=device selects the device-layout path (read per call).
+// The device-layout path is the default (round 5: faster end to end and no
+// host synchronization); CILIUM_GPU_RAW_LAYOUT=host selects the round-3
+// sequence (read per call).
 bool device_layout_selected() {
   const char* v = getenv("CILIUM_GPU_RAW_LAYOUT");
-  return v && std::string(v) == "device";
+  return !(v && std::string(v) == "host");
 }
 
 }  // namespace

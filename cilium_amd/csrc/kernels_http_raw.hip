@@ -1670,45 +1670,41 @@ __global__ __launch_bounds__(kRawThreads) void raw_defer_dl_kernel(HttpRawDev R,
   }
 }
 
-// ---- the batch's tables, one workgroup: each key's last chunk gets its tile
-// count and its last tile's free slots become padding (meta PAD, order
-// 0xFFFFFFFF, zero units); the chunk table, grouped by program (so a
-// workgroup's run of chunks shares the staged program block), and the header
-// go to the front of the batch.
-constexpr uint32_t kSealThreads = 1024;
-__global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, RawLayoutDev L, uint8_t* __restrict__ batch,
-                                                                uint32_t epoch, uint64_t ttab_off, uint64_t tiles_off,
-                                                                uint64_t total_bytes, uint32_t sort) {
-  extern __shared__ uint32_t sh[];  // [group counts][group cursors] (sort)
-  const uint32_t G = R.nprogs + 2, tid = threadIdx.x;
-  const uint32_t nch = min(L.ctl[kRawCtlChunks], L.maxchunks);
-  for (uint32_t k = tid; k < L.nkeys; k += kSealThreads) {
+// ---- each key's last chunk gets its tile count and its last tile's free
+// slots become padding (meta PAD, order 0xFFFFFFFF, zero units): one wave per
+// (key, stripe), one lane per slot (coalesced stores).  Then the late slots
+// (taken, never filled: their requests are walked): every chunk id is
+// published by now, so each becomes padding in place — meta PAD (no
+// counters), order 0xFFFFFFFF (no verdict), and the tile's data offset when
+// it is the tile's slot 0 (whose lane writes it otherwise).
+constexpr uint32_t kPadThreads = 256;
+__global__ __launch_bounds__(kPadThreads) void raw_pad_kernel(RawLayoutDev L) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t k = blockIdx.x * (kPadThreads / 64) + (threadIdx.x >> 6);  // wave-uniform
+  if (k < L.nkeys) {
     const uint32_t cnt = L.kcnt[(size_t)k * kRawCntStride];
-    if (!cnt) continue;
-    const uint32_t c = (cnt - 1) >> L.cshift;
-    if (c >= L.dpk) continue;
-    const unsigned long long v = L.dir[(size_t)k * L.dpk + c];
-    const uint32_t id = (uint32_t)v;
-    if ((uint32_t)(v >> 32) != L.seq || id >= L.maxchunks) continue;
-    const uint32_t used = cnt - (c << L.cshift), nt = (used + 63) >> 6;
-    L.chunks[id].ntiles = nt;
-    const uint32_t t = id * L.ext + nt - 1, units = (k / L.stripes) % kRawUnits;
-    uint8_t* tb = L.tiles + (size_t)t * (kRawTileGran * 512);
-    for (uint32_t l = used - (nt - 1) * 64; l < 64; ++l) {
-      reinterpret_cast<uint2*>(tb)[l] = make_uint2(0, CG_HTTP_F_PAD << 24);
-      L.order[(size_t)t * 64 + l] = 0xFFFFFFFFu;
-      for (uint32_t u = 0; u < units; ++u) reinterpret_cast<uint4*>(tb + 512)[u * 64 + l] = make_uint4(0, 0, 0, 0);
+    const uint32_t c = cnt ? (cnt - 1) >> L.cshift : 0u;
+    if (cnt && c < L.dpk) {
+      const unsigned long long v = L.dir[(size_t)k * L.dpk + c];
+      const uint32_t id = (uint32_t)v;
+      if ((uint32_t)(v >> 32) == L.seq && id < L.maxchunks) {
+        const uint32_t used = cnt - (c << L.cshift), nt = (used + 63) >> 6;
+        if (lane == 0) L.chunks[id].ntiles = nt;
+        const uint32_t t = id * L.ext + nt - 1, units = (k / L.stripes) % kRawUnits;
+        uint8_t* tb = L.tiles + (size_t)t * (kRawTileGran * 512);
+        if (lane >= used - (nt - 1) * 64) {
+          reinterpret_cast<uint2*>(tb)[lane] = make_uint2(0, CG_HTTP_F_PAD << 24);
+          L.order[(size_t)t * 64 + lane] = 0xFFFFFFFFu;
+          for (uint32_t u = 0; u < units; ++u) reinterpret_cast<uint4*>(tb + 512)[u * 64 + lane] = make_uint4(0, 0, 0, 0);
+        }
+      }
     }
   }
-  // the late slots (taken, never filled: their requests are walked): every
-  // chunk id is published by now, so each becomes padding in place — meta
-  // PAD (no counters), order 0xFFFFFFFF (no verdict), and the tile's data
-  // offset when it is the tile's slot 0 (whose lane writes it otherwise)
   const uint32_t nlate = L.ctl[kRawCtlLate];
-  for (uint32_t j = tid; j < nlate; j += kSealThreads) {
+  for (uint32_t j = blockIdx.x * kPadThreads + threadIdx.x; j < nlate; j += gridDim.x * kPadThreads) {
     const unsigned long long x = L.late[j];
-    const uint32_t k = (uint32_t)(x >> 32), sl = (uint32_t)x, c = sl >> L.cshift;
-    const unsigned long long v = L.dir[(size_t)k * L.dpk + c];
+    const uint32_t kk = (uint32_t)(x >> 32), sl = (uint32_t)x, c = sl >> L.cshift;
+    const unsigned long long v = L.dir[(size_t)kk * L.dpk + c];
     const uint32_t id = (uint32_t)v;
     if ((uint32_t)(v >> 32) != L.seq || id >= L.maxchunks) continue;  // not in the chunk table
     const uint32_t t = id * L.ext + ((sl >> 6) & (L.ext - 1u)), l = sl & 63u;
@@ -1717,7 +1713,18 @@ __global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, Ra
     L.order[(size_t)t * 64 + l] = 0xFFFFFFFFu;
     if (l == 0) L.ttab[t].at = t * kRawTileGran;
   }
-  __syncthreads();
+}
+
+// ---- the batch's tables, one workgroup (after raw_pad_kernel): the chunk
+// table, grouped by program (so a workgroup's run of chunks shares the
+// staged program block), and the header go to the front of the batch.
+constexpr uint32_t kSealThreads = 1024;
+__global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, RawLayoutDev L, uint8_t* __restrict__ batch,
+                                                                uint32_t epoch, uint64_t ttab_off, uint64_t tiles_off,
+                                                                uint64_t total_bytes, uint32_t sort) {
+  extern __shared__ uint32_t sh[];  // [group counts][group cursors] (sort)
+  const uint32_t G = R.nprogs + 2, tid = threadIdx.x;
+  const uint32_t nch = min(L.ctl[kRawCtlChunks], L.maxchunks);
   HttpChunk* dst = reinterpret_cast<HttpChunk*>(batch + sizeof(HttpBatchHeader));
   auto group = [&](uint32_t prog) { return prog < R.nprogs ? prog : R.nprogs + (prog == kProgAllow ? 0u : 1u); };
   if (sort) {
@@ -2007,6 +2014,8 @@ int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch
   const bool sort = http_raw_seal_sorts(R);
   const size_t lds = sort ? ((size_t)R.nprogs + 2) * 8 : 0;
   (void)hipFuncSetAttribute((const void*)raw_seal_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  const unsigned pad_grid = std::max(1u, (L.nkeys + kPadThreads / 64 - 1) / (kPadThreads / 64));
+  hipLaunchKernelGGL(raw_pad_kernel, dim3(pad_grid), dim3(kPadThreads), 0, (hipStream_t)stream, L);
   hipLaunchKernelGGL(raw_seal_kernel, dim3(1), dim3(kSealThreads), lds, (hipStream_t)stream, R, L, (uint8_t*)batch,
                      epoch, ttab_off, tiles_off, total_bytes, (uint32_t)sort);
   return (int)hipGetLastError();

@@ -471,10 +471,15 @@ int cg_http_parse_heads(const uint8_t* raw, const uint64_t* raw_off, size_t n, u
  * d_raw[d_raw_off[r] .. d_raw_off[r+1]) with d_policy/d_ingress/d_port/
  * d_remote as in cg_http_pack; d_out[r] = 1 allow, 0 deny, request order.
  * Heads over 60 KiB are rejected (Envoy's default max_request_headers_kb).
- * A batch whose strings past the 128-byte slot need more than the 256 MiB
- * overflow arena is evaluated in halves.  Runs on `stream` (NULL: the handle's) and synchronizes it (its workspace is
- * the handle's).  CG_UNSUPPORTED when the snapshot walks more than 32 header
- * fields or is a proxylib snapshot. */
+ * Enqueued on `stream` (NULL: the handle's) and returns without waiting:
+ * slots, tiles, chunk table and header are laid out on the device, strings
+ * past the 128-byte slot walked one lane each; a later call on another
+ * stream waits for this one on the device.  An offset range that runs
+ * backwards is an empty (rejected) request — the call has returned before
+ * the device reads the offsets.  CILIUM_GPU_RAW_LAYOUT=host selects the
+ * round-3 sequence instead (host layout step, synchronizes the stream,
+ * CG_INVALID_ARGUMENT for backward offsets).  CG_UNSUPPORTED when the
+ * snapshot walks more than 32 header fields or is a proxylib snapshot. */
 int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d_raw_off, size_t n,
                              const uint32_t* d_policy, const uint8_t* d_ingress, const uint16_t* d_port,
                              const uint32_t* d_remote, uint8_t* d_out, void* stream);
@@ -492,7 +497,8 @@ int cg_http_verdicts_raw_host(uint64_t h, const uint8_t* raw, const uint64_t* ra
  * path's kernels instead of on the host, then cg_http_verdicts_dev; d_out[i]
  * = 1 allow, 0 deny, request order.  Proxylib snapshots take escaped values
  * as cg_http_pack does.  One request's list holds at most 65535 bytes
- * (CG_INVALID_ARGUMENT beyond; Envoy's default header limit is 60 KiB).
+ * (Envoy's default header limit is 60 KiB): a longer one is denied here (the
+ * host entry and the round-3 sequence refuse the call, CG_INVALID_ARGUMENT).
  * Stream and synchronization as cg_http_verdicts_raw_dev; CG_UNSUPPORTED when
  * the snapshot walks more than 32 header fields. */
 int cg_http_verdicts_fields_dev(uint64_t h, const uint8_t* d_hdr_blob, const uint64_t* d_hdr_off, size_t n,

@@ -1,5 +1,6 @@
-"""The raw path's device-layout sequence (CILIUM_GPU_RAW_LAYOUT=device,
-http_raw.cc raw_device_layout): the scan takes each request's slot from a
+"""The raw path's device-layout sequence (the default since round 5;
+CILIUM_GPU_RAW_LAYOUT=host selects the round-3 sequence; http_raw.cc
+raw_device_layout): the scan takes each request's slot from a
 per-bucket counter and writes its class-coded string straight into the
 tile-transposed batch, raw_seal_kernel pads the last tiles and writes the
 chunk table, http_kernel decides, raw_walk_kernel decides the strings past
@@ -125,7 +126,7 @@ def test_gpu_dl_counters_match_default_path(gpu, dl):
         return v, gpu.read_counters(N.CG_CTR_HTTP_PROGRAMS), gpu.read_counters(N.CG_CTR_HTTP_RULES)
 
     v_dl, p_dl, r_dl = run()
-    dl.pop("CILIUM_GPU_RAW_LAYOUT")
+    dl["CILIUM_GPU_RAW_LAYOUT"] = "host"  # the round-3 sequence
     v_def, p_def, r_def = run()
     assert np.array_equal(v_dl, v_def)
     assert np.array_equal(p_dl, p_def)
@@ -188,7 +189,7 @@ def test_gpu_dl_late_slots_padded(gpu, dl):
     dl["CILIUM_GPU_RAW_SPIN"] = "0"
     v_late, p_late, r_late = run()
     dl.pop("CILIUM_GPU_RAW_SPIN")
-    dl.pop("CILIUM_GPU_RAW_LAYOUT")
+    dl["CILIUM_GPU_RAW_LAYOUT"] = "host"  # the round-3 sequence
     v_def, p_def, r_def = run()
     assert np.array_equal(v_late, v_def)
     assert np.array_equal(v_late[:8_000], _oracle(pols, *(np.asarray(a)[:8_000] for a in _args(rq)), raws[:8_000]))

@@ -303,10 +303,9 @@ def bench_http_raw(torch, dev, stream, cl, args, threads):
     """Config 5 requests as raw HTTP/1 heads resident in HBM →
     cg_http_verdicts_raw_dev: the codec step, program lookup, packing and the
     verdicts all on the GPU (kernels_http_raw.hip + http_kernel), one call
-    per step (the default sequence synchronizes its stream: a host layout
-    step sits between the scan and the emit kernels; with
-    CILIUM_GPU_RAW_LAYOUT=device in the environment the device-layout
-    sequence runs instead and the calls only enqueue)."""
+    per step (the device-layout sequence, the default, only enqueues; with
+    CILIUM_GPU_RAW_LAYOUT=host in the environment the round-3 sequence runs
+    instead, which synchronizes its stream for a host layout step)."""
     import oracle  # noqa: F401  (the check below uses the host path)
     from cilium_amd import synth
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -337,8 +336,8 @@ def bench_http_raw(torch, dev, stream, cl, args, threads):
         assert bool((got == torch.from_numpy(want).to(dev).unsqueeze(0)).all()), "raw-path verdicts differ from host path"
     bpi = tot / D + 4 + 1 + 2 + 4 + 8 + 1  # head bytes, policy/ingress/port/remote, offset, verdict
     return line("HTTP/1 raw heads → verdicts/s on the GPU (codec step + packing + http_kernel), config 5", n, sec,
-                bpi, ("raw_scan_dl+raw_seal+http_kernel+raw_walk" if os.environ.get("CILIUM_GPU_RAW_LAYOUT") == "device"
-                      else "raw_scan+raw_rank+raw_build+http_kernel"), None, "", threads,
+                bpi, ("raw_scan+raw_rank+raw_build+http_kernel" if os.environ.get("CILIUM_GPU_RAW_LAYOUT") == "host"
+                      else "raw_scan_dl+raw_pad+raw_seal+http_kernel<raw>+raw_walk"), None, "", threads,
                 {"config": {"workload": f"BASELINE config 5 requests as raw HTTP/1 heads ({tot / D:.1f} B/head avg), "
                             "10K rules", "requests": n},
                  "request_gbps": n * (tot / D) / sec / 1e9})
@@ -401,7 +400,8 @@ def bench_http_fields(torch, dev, stream, cl, args, threads):
     hbytes = int(hq["hdr_off"][-1])
     bpi = tot / D + 4 + 1 + 2 + 4 + 8 + 1  # list bytes, policy/ingress/port/remote, offset, verdict
     return line("HTTP header lists → verdicts/s, packing on the GPU (cg_http_verdicts_fields_dev), config 5", n, sec,
-                bpi, "raw_scan(lists)+raw_rank+raw_build+http_kernel", None, "", threads,
+                bpi, ("raw_scan(lists)+raw_rank+raw_build+http_kernel" if os.environ.get("CILIUM_GPU_RAW_LAYOUT") == "host"
+                      else "raw_scan_dl(lists)+raw_pad+raw_seal+http_kernel<raw>+raw_walk"), None, "", threads,
                 {"config": {"workload": f"BASELINE config 5 requests as header lists ({tot / D:.1f} B/list avg), "
                             "10K rules, 1M distinct tiled", "requests": n},
                  "host_entry": {"value": H / th, "unit": "verdicts/s", "ms": th * 1e3, "requests": H,
