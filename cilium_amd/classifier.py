@@ -221,8 +221,9 @@ class Classifier:
 
     def http_verdicts_raw_dev(self, d_raw, d_off, n: int, d_policy, d_ingress, d_port, d_remote, d_out,
                               stream=None) -> None:
-        """cg_http_verdicts_raw_dev on device tensors: enqueued on `stream`
-        (None: the null stream), returns without waiting for the device."""
+        """cg_http_verdicts_raw_dev on device tensors: enqueued on `stream`,
+        returns without waiting for the device (None: the handle's stream,
+        waited for)."""
         N.check(N.lib.cg_http_verdicts_raw_dev(self.h, _p(d_raw), _p(d_off), n, _p(d_policy), _p(d_ingress),
                                                _p(d_port), _p(d_remote), _p(d_out), stream))
 

@@ -955,6 +955,9 @@ int cg_http_verdicts_raw_dev(uint64_t h, const uint8_t* d_raw, const uint64_t* d
     // the device-layout sequence returns with its kernels still queued on
     // the stream, reading the snapshot's tables: keep the snapshot alive
     s->fence.record(stream_of(*e, stream));
+    // no stream given: the handle's, waited for (a caller that wants the
+    // call asynchronous names its stream)
+    if (!stream) hip_check(hipStreamSynchronize((hipStream_t)stream_of(*e, stream)), "hipStreamSynchronize");
   });
 }
 
@@ -972,6 +975,7 @@ int cg_http_verdicts_fields_dev(uint64_t h, const uint8_t* d_hdr_blob, const uin
     http_verdicts_raw_on(*s, *lease, e->cus, RawInput::Lists, d_hdr_blob, d_hdr_off, n, d_policy, d_ingress, d_port,
                          d_remote, d_out, stream_of(*e, stream));
     s->fence.record(stream_of(*e, stream));  // as cg_http_verdicts_raw_dev
+    if (!stream) hip_check(hipStreamSynchronize((hipStream_t)stream_of(*e, stream)), "hipStreamSynchronize");
   });
 }
 

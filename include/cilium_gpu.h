@@ -471,7 +471,8 @@ int cg_http_parse_heads(const uint8_t* raw, const uint64_t* raw_off, size_t n, u
  * d_raw[d_raw_off[r] .. d_raw_off[r+1]) with d_policy/d_ingress/d_port/
  * d_remote as in cg_http_pack; d_out[r] = 1 allow, 0 deny, request order.
  * Heads over 60 KiB are rejected (Envoy's default max_request_headers_kb).
- * Enqueued on `stream` (NULL: the handle's) and returns without waiting:
+ * Enqueued on `stream` and returns without waiting (NULL: the handle's
+ * stream, waited for before the call returns):
  * slots, tiles, chunk table and header are laid out on the device, strings
  * past the 128-byte slot walked one lane each; a later call on another
  * stream waits for this one on the device.  An offset range that runs
