@@ -217,7 +217,10 @@ def test_gpu_fields_dev_tensors():
             rep(rq["remote"], np.int32))
     d_out = torch.full((D * reps,), 7, dtype=torch.uint8, device=dev)
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())  # the inputs were made on the current stream
+    # enqueued on s, returns without waiting (the device-layout sequence)
     cl.http_verdicts_fields_dev(d_blob, d_off, D * reps, *args, d_out, stream=C_stream(s))
+    s.synchronize()
     assert bool((d_out.view(reps, D) == torch.from_numpy(want).to(dev).unsqueeze(0)).all())
     cl.close()
 

@@ -179,6 +179,11 @@ VARIANTS.update({
                       "    const RawSlot sl = raw_slot(L, want, raw_vkey(L, group_of(R, prog) * kRawUnits + units, blockIdx.x), prog);",
                       "    const uint32_t tfake = (uint32_t)((i >> 6) % L.maxchunks);\n"
                       "    const RawSlot sl{L.tiles + (size_t)tfake * (kRawTileGran * 512), tfake, (uint32_t)(i & 63), want};")],
+    # a wave issuing its tile's loads (window + next tile's head) at raised
+    # priority, so the loads leave before other waves' walk steps
+    "h_prio": [("  const uint2 meta = cur.meta;\n", "  __builtin_amdgcn_s_setprio(3);\n  const uint2 meta = cur.meta;\n"),
+               ("  if (has_next) tile_prefetch(trn, nunits, lane, nxt);\n  __builtin_amdgcn_sched_barrier(0);",
+                "  if (has_next) tile_prefetch(trn, nunits, lane, nxt);\n  __builtin_amdgcn_s_setprio(0);\n  __builtin_amdgcn_sched_barrier(0);")],
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
