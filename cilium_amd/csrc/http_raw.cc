@@ -357,8 +357,9 @@ void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists
                   const uint16_t* d_port, const uint32_t* d_remote, uint8_t* d_out, hipStream_t st) {
   // slot counters striped per workgroup (RawLayoutDev.stripes): a bucket
   // key's requests take slots from `stripes` counters, so the returning
-  // atomics of a hot key do not serialize on one address
-  uint32_t S = 16;
+  // atomics of a hot key do not serialize on one address (8: measured best
+  // of 4/8/16 on config 5, profiles/r05m_stripes.txt)
+  uint32_t S = 8;
   if (const char* v = getenv("CILIUM_GPU_RAW_STRIPES")) S = floor_pow2((uint32_t)std::max(1, std::min(64, atoi(v))));
   const uint32_t np = (uint32_t)s.progs.size(), K = (np + 2) * kRawUnits * S;
   // tiles per chunk: the chunk table's 64 when the sub-batch fills several

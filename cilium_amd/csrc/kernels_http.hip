@@ -33,6 +33,7 @@ using namespace walk;
 constexpr int kWave = 64;
 constexpr int kHttpThreads = 1024;
 constexpr int kTilesPerWave = 1;  // strings walked per lane at a time
+constexpr int kHttpWaves = 8;     // waves per SIMD http_kernel is built for (64 VGPRs)
 constexpr uint32_t kDealRun = 4;  // consecutive chunks per workgroup turn
 // Runs of chunks are taken from a per-launch ticket counter (dynamic
 // dealing): chunk costs vary with their tiles' string lengths, and a static
@@ -117,6 +118,49 @@ __device__ __forceinline__ uint4 lds_transcode(uint32_t cm, const uint4& u) {
   r.x = lds_code2w(cm, u.x, u.y, r.y);
   r.z = lds_code2w(cm, u.z, u.w, r.w);
   return r;
+}
+
+// Two independent walks (two requests of a lane) stepped together: both LDS
+// reads are in flight before the one wait, so a wave's dependent chain costs
+// one LDS round trip per TWO bytes walked.  Same VALU count as two single
+// steps; the compare/select pairs share VCC in sequence (two wait states
+// after each compare, filled by the default targets' max).
+template <int B>
+__device__ __forceinline__ void lds_cls_step2(uint32_t dead, uint32_t& sa, uint32_t wa, uint32_t& sb, uint32_t wb) {
+  uint32_t ea, eb, da, db, na, nb;
+#define CG_CLS_STEP2(b)                                                                                  \
+  asm volatile("v_add_u32_sdwa %0, %6, %8 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" b  \
+               "\n\tv_add_u32_sdwa %1, %7, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" b \
+               "\n\tds_read_b32 %0, %0\n\t"                                                             \
+               "ds_read_b32 %1, %1\n\t"                                                                  \
+               "s_waitcnt lgkmcnt(0)\n\t"                                                                \
+               "v_cmp_eq_u32_sdwa vcc, %0, %6 src0_sel:WORD_0 src1_sel:DWORD\n\t"                        \
+               "v_max_u32 %2, %10, %6\n\t"                                                              \
+               "v_max_u32 %3, %10, %7\n\t"                                                              \
+               "v_cndmask_b32_sdwa %4, %2, %0, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "    \
+               "src1_sel:WORD_1\n\t"                                                                    \
+               "v_cmp_eq_u32_sdwa vcc, %1, %7 src0_sel:WORD_0 src1_sel:DWORD\n\t"                        \
+               "s_nop 1\n\t"                                                                             \
+               "v_cndmask_b32_sdwa %5, %3, %1, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD "    \
+               "src1_sel:WORD_1"                                                                          \
+               : "=&v"(ea), "=&v"(eb), "=&v"(da), "=&v"(db), "=&v"(na), "=&v"(nb)                         \
+               : "v"(sa), "v"(sb), "v"(wa), "v"(wb), "s"(dead)                                            \
+               : "vcc")
+  if (B == 0) CG_CLS_STEP2("BYTE_0");
+  else if (B == 1) CG_CLS_STEP2("BYTE_1");
+  else if (B == 2) CG_CLS_STEP2("BYTE_2");
+  else CG_CLS_STEP2("BYTE_3");
+#undef CG_CLS_STEP2
+  sa = na;
+  sb = nb;
+}
+
+template <int I>
+__device__ __forceinline__ void lds_cls_step2x16(uint32_t dead, uint32_t& sa, const uint4& ua, uint32_t& sb,
+                                                 const uint4& ub) {
+  const uint32_t wa = I < 4 ? ua.x : I < 8 ? ua.y : I < 12 ? ua.z : ua.w;
+  const uint32_t wb = I < 4 ? ub.x : I < 8 ? ub.y : I < 12 ? ub.z : ub.w;
+  lds_cls_step2<I & 3>(dead, sa, wa, sb, wb);
 }
 
 // Where verdicts go: out[slot] (slot order), or — for a batch built on the
@@ -469,6 +513,184 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   n_deny += counted && !verdict;
 }
 
+// ---- two tiles per wave, one request of each per lane (kPairTiles) --------
+// A lane walks the requests of tiles ta and tb together (lds_cls_step2): two
+// LDS reads in flight per wait.  The pair is walked over N = the longer
+// tile's string units; a lane of the shorter tile re-reads its tile's last
+// unit past its end (tile_unit), which cannot change its verdict.
+// Off: measured at 8 waves per SIMD (64 VGPRs) it spills and loses (§3.1);
+// kept for a 4-waves-per-SIMD build (kHttpWaves = 4), where the second
+// chain stands in for the halved occupancy.
+constexpr bool kPairTiles = false;
+
+__device__ __forceinline__ const uint4* pair_unit(const TileRef& tr, uint32_t units, uint32_t k) {
+  const uint32_t lane = lane_now();
+  return units == 0 ? reinterpret_cast<const uint4*>(tr.meta) + (lane & 31)
+                    : tr.units + (min(k + 1u, units) - 1u) * kWave + lane;
+}
+
+// The verdict of one lane's request after the walk (as http_tile_n's).
+__device__ __forceinline__ void pair_verdict(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
+                                             const uint32_t* __restrict__ blk, uint2 meta, uint32_t st,
+                                             const uint8_t* __restrict__ arena, uint64_t arena_bytes, uint32_t t,
+                                             VOut out, uint32_t lane, uint32_t& n_allow, uint32_t& n_deny,
+                                             uint32_t* s_hits) {
+  const uint32_t flags = meta.y >> 24;
+  const bool counted = !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+  const bool overflow = counted && (flags & CG_HTTP_F_OVERFLOW);
+  if (__any(overflow)) {
+    const uint32_t sa = walk_overflow<true>(blk, pt.dead, pt.start, arena, arena_bytes, meta, overflow);
+    if (overflow) st = sa;
+  }
+  uint32_t hit = kNoHit;
+  if (counted) {
+    const uint32_t lab = state_label<true>(blk, st);
+    const bool always = pg.flags & kProgHasAlways;
+    if (lab != 0xFFFFu || always) {
+      const uint32_t row = remote_row(blk, pg, meta.x);
+      if (lab != 0xFFFFu) hit = first_meet(blk, pt.acc_off + mul24(lab, 2 * pg.mask_words), row, pg.mask_words);
+      if (always) hit = min(hit, first_meet(blk, pg.always_off, row, pg.mask_words));
+    }
+  }
+  const bool verdict = hit != kNoHit;
+  count_hits(T, pg, hit, s_hits, lane);
+  out.put((size_t)t * kWave + lane, verdict, verdict ? pg.rule_base + hit : kNoHit);
+  n_allow += counted && verdict;
+  n_deny += counted && !verdict;
+}
+
+template <int N, bool kRaw>
+__device__ __forceinline__ void http_pair_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
+                                            const uint32_t* __restrict__ blk, const TileRef ra, const TileRef rb,
+                                            uint32_t ua, uint32_t ub, const TilePre& ca, const TilePre& cb,
+                                            bool has_next, bool next_pair, const TileRef rna, const TileRef rnb,
+                                            uint32_t nua, uint32_t nub, TilePre& xa, TilePre& xb, uint32_t tail,
+                                            uint32_t ta, uint32_t tb, const uint8_t* __restrict__ arena,
+                                            uint64_t arena_bytes, VOut out, uint32_t lane, uint32_t& n_allow,
+                                            uint32_t& n_deny, uint32_t* s_hits, uint32_t cm) {
+  // a rolling window of kW units per chain: unit k + kW loads when unit k
+  // starts walking
+  constexpr int kW = N < 2 ? (N > 0 ? N : 1) : 2;
+  uint4 wa[kW], wb[kW];
+#pragma unroll
+  for (int k = 0; k < kW && k < N; ++k) {
+    wa[k] = k == 0 ? ca.u[0] : ld_nt(pair_unit(ra, ua, k));
+    wb[k] = k == 0 ? cb.u[0] : ld_nt(pair_unit(rb, ub, k));
+  }
+  if (has_next) {
+    tile_prefetch(rna, nua, lane, xa);
+    if (next_pair) tile_prefetch(rnb, nub, lane, xb);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const uint32_t dead = pt.dead;
+  uint32_t sa = pt.start, sb = pt.start;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const uint4 a = kRaw ? lds_transcode(cm, wa[k % kW]) : wa[k % kW];
+    const uint4 b = kRaw ? lds_transcode(cm, wb[k % kW]) : wb[k % kW];
+    if (k + kW < N) {
+      wa[k % kW] = ld_nt(pair_unit(ra, ua, k + kW));
+      wb[k % kW] = ld_nt(pair_unit(rb, ub, k + kW));
+    }
+    const bool last = k == N - 1;
+    lds_cls_step2x16<0>(dead, sa, a, sb, b);
+    lds_cls_step2x16<1>(dead, sa, a, sb, b);
+    lds_cls_step2x16<2>(dead, sa, a, sb, b);
+    lds_cls_step2x16<3>(dead, sa, a, sb, b);
+    if (!last || tail > 4) {
+      lds_cls_step2x16<4>(dead, sa, a, sb, b);
+      lds_cls_step2x16<5>(dead, sa, a, sb, b);
+      lds_cls_step2x16<6>(dead, sa, a, sb, b);
+      lds_cls_step2x16<7>(dead, sa, a, sb, b);
+    }
+    if (!last || tail > 8) {
+      lds_cls_step2x16<8>(dead, sa, a, sb, b);
+      lds_cls_step2x16<9>(dead, sa, a, sb, b);
+      lds_cls_step2x16<10>(dead, sa, a, sb, b);
+      lds_cls_step2x16<11>(dead, sa, a, sb, b);
+    }
+    if (!last || tail > 12) {
+      lds_cls_step2x16<12>(dead, sa, a, sb, b);
+      lds_cls_step2x16<13>(dead, sa, a, sb, b);
+      lds_cls_step2x16<14>(dead, sa, a, sb, b);
+      lds_cls_step2x16<15>(dead, sa, a, sb, b);
+    }
+  }
+  pair_verdict(T, pg, pt, blk, ca.meta, sa, arena, arena_bytes, ta, out, lane, n_allow, n_deny, s_hits);
+  pair_verdict(T, pg, pt, blk, cb.meta, sb, arena, arena_bytes, tb, out, lane, n_allow, n_deny, s_hits);
+}
+
+template <int N, bool kCls, bool kRaw>
+__device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
+                                            uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
+                                            const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
+                                            uint32_t tail, TilePre& nxt, uint32_t t, const uint8_t* __restrict__ arena,
+                                            uint64_t arena_bytes, VOut out, uint32_t lane,
+                                            uint32_t& n_allow, uint32_t& n_deny, uint32_t* s_hits, uint32_t cm);
+
+// A wave's tiles of a class-mode one-part program in pairs (t, t + nw), then
+// (t + 2nw, t + 3nw), ...; a last lone tile goes through http_tile_n.
+template <bool kRaw>
+__device__ __forceinline__ void one_part_pairs(const HttpDev& T, const HttpProg& pg, const HttpPart& pt, uint32_t prog,
+                                               const uint32_t* __restrict__ lcells, const uint8_t* __restrict__ tiles,
+                                               const HttpTile* __restrict__ ttab, uint32_t t, uint32_t tend,
+                                               uint32_t nw, const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                               VOut out, uint32_t lane, uint32_t& n_allow, uint32_t& n_deny,
+                                               uint32_t* s_hits, uint32_t cm) {
+  HttpTile ta = ttab[t];
+  HttpTile tb = ttab[t + nw < tend ? t + nw : t];
+  TileRef ra = tile_ref(tiles, ta), rb = tile_ref(tiles, tb);
+  TilePre pa, pb;
+  tile_prefetch(ra, tile_units(ta), lane, pa);
+  tile_prefetch(rb, tile_units(tb), lane, pb);
+  for (; t < tend; t += 2 * nw) {
+    const uint32_t tn = t + 2 * nw;
+    const bool has_next = tn < tend, next_pair = tn + nw < tend;
+    const HttpTile tna = ttab[has_next ? tn : t], tnb = ttab[next_pair ? tn + nw : (has_next ? tn : t)];
+    const TileRef rna = tile_ref(tiles, tna), rnb = tile_ref(tiles, tnb);
+    TilePre xa = pa, xb = pb;
+    if (t + nw >= tend) {  // a lone last tile (wave-uniform)
+      switch (tile_units(ta)) {
+#define CG_TILE_1(n)                                                                                               \
+  case n:                                                                                                          \
+    http_tile_n<n, true, kRaw>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena,          \
+                               arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);                              \
+    break;
+        CG_TILE_1(0) CG_TILE_1(1) CG_TILE_1(2) CG_TILE_1(3) CG_TILE_1(4) CG_TILE_1(5) CG_TILE_1(6) CG_TILE_1(7)
+        default:
+          http_tile_n<8, true, kRaw>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena,
+                                     arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);
+#undef CG_TILE_1
+      }
+      break;
+    }
+    const uint32_t ua = tile_units(ta), ub = tile_units(tb), n = max(ua, ub);
+    // the last unit's 4-byte groups holding a string byte of a tile that
+    // reaches it (a shorter tile re-reads an earlier unit there: skippable)
+    const uint32_t tail = max(ua == n ? tile_tail(ta) : 0u, ub == n ? tile_tail(tb) : 0u);
+    switch (n) {  // wave-uniform
+#define CG_PAIR_N(k)                                                                                              \
+  case k:                                                                                                         \
+    http_pair_n<k, kRaw>(T, pg, pt, lcells, ra, rb, ua, ub, pa, pb, has_next, next_pair, rna, rnb,              \
+                         tile_units(tna), tile_units(tnb), xa, xb, tail, t, t + nw, arena, arena_bytes, out, lane, \
+                         n_allow, n_deny, s_hits, cm);                                                            \
+    break;
+      CG_PAIR_N(0) CG_PAIR_N(1) CG_PAIR_N(2) CG_PAIR_N(3) CG_PAIR_N(4) CG_PAIR_N(5) CG_PAIR_N(6) CG_PAIR_N(7)
+      default:
+        http_pair_n<8, kRaw>(T, pg, pt, lcells, ra, rb, ua, ub, pa, pb, has_next, next_pair, rna, rnb,
+                             tile_units(tna), tile_units(tnb), xa, xb, tail, t, t + nw, arena, arena_bytes, out, lane,
+                             n_allow, n_deny, s_hits, cm);
+#undef CG_PAIR_N
+    }
+    ta = tna;
+    tb = tnb;
+    ra = rna;
+    rb = rnb;
+    pa = xa;
+    pb = xb;
+  }
+}
+
 // A wave's tiles t, t + nw, ... < tend of a one-part program whose block is
 // in LDS: each tile's walk specialized on its string units (wave-uniform).
 template <bool kCls, bool kRaw>
@@ -479,6 +701,11 @@ __device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg&
                                                VOut out, uint32_t lane, uint32_t& n_allow,
                                                uint32_t& n_deny, uint32_t* s_hits, uint32_t cm) {
   if (t >= tend) return;
+  if (kPairTiles && kCls) {
+    one_part_pairs<kRaw>(T, pg, pt, prog, lcells, tiles, ttab, t, tend, nw, arena, arena_bytes, out, lane, n_allow,
+                         n_deny, s_hits, cm);
+    return;
+  }
   HttpTile tt = ttab[t];
   TileRef tb = tile_ref(tiles, tt);
   TilePre pre;
@@ -668,7 +895,7 @@ __device__ __forceinline__ void http_chunks(const HttpDev& T, const uint8_t* __r
 }
 
 template <bool kRaw>
-__global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void http_kernel(
+__global__ __launch_bounds__(kHttpThreads) __attribute__((amdgpu_waves_per_eu(kHttpWaves, kHttpWaves))) void http_kernel(
     HttpDev T, const uint8_t* __restrict__ batch, size_t nslots, const uint8_t* __restrict__ arena,
     uint8_t* __restrict__ out, const uint32_t* __restrict__ order, uint32_t* __restrict__ deal,
     uint32_t* __restrict__ rule, uint32_t nout, const uint8_t* __restrict__ codes) {

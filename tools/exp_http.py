@@ -184,6 +184,15 @@ VARIANTS.update({
     "h_prio": [("  const uint2 meta = cur.meta;\n", "  __builtin_amdgcn_s_setprio(3);\n  const uint2 meta = cur.meta;\n"),
                ("  if (has_next) tile_prefetch(trn, nunits, lane, nxt);\n  __builtin_amdgcn_sched_barrier(0);",
                 "  if (has_next) tile_prefetch(trn, nunits, lane, nxt);\n  __builtin_amdgcn_s_setprio(0);\n  __builtin_amdgcn_sched_barrier(0);")],
+    # 4 waves per SIMD (128 VGPRs, one 1024-thread workgroup per CU): the
+    # registers spent on a second chain (pairs) and / or deeper prefetch
+    "h_pair_w4": [("constexpr bool kPairTiles = false;", "constexpr bool kPairTiles = true;"),
+                  ("constexpr int kHttpWaves = 8;", "constexpr int kHttpWaves = 4;")],
+    "h_pair_w4_pre2": [("constexpr bool kPairTiles = false;", "constexpr bool kPairTiles = true;"),
+                       ("constexpr int kHttpWaves = 8;", "constexpr int kHttpWaves = 4;"),
+                       ("constexpr int kPre = 1;", "constexpr int kPre = 2;")],
+    "h_w4_pre4": [("constexpr int kHttpWaves = 8;", "constexpr int kHttpWaves = 4;"),
+                  ("constexpr int kPre = 1;", "constexpr int kPre = 4;")],
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
