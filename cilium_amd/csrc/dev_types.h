@@ -317,6 +317,9 @@ constexpr uint32_t kRawUnits = 9;
 // directory is never cleared).  Tile t = id * ext + (s / 64) % ext keeps its
 // data at granule t * kRawTileGran (room for 8 units), slot s % 64.
 constexpr uint32_t kRawTileGran = 1 + 2 * 8;
+// threads per workgroup of the raw scan kernels (the device layout's
+// directory bound counts grid-stride iterations of this many requests)
+constexpr uint32_t kRawScanThreads = 256;
 constexpr uint32_t kRawCntStride = 64;  // u32 between two keys' counters (own 256-B line)
 enum : uint32_t {
   kRawCtlChunks = 0,  // chunk ids taken

@@ -372,10 +372,10 @@ void raw_dl_subbatch(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lists
   // directory entries per (key, stripe): the requests one stripe's
   // workgroups can take slots for — the scan's grid-stride share plus the
   // deferred kernel's (every request at most once in either)
-  const size_t it256 = (m + 255) / 256;
+  const size_t T = kRawScanThreads, itT = (m + T - 1) / T;
   auto share = [&](size_t grid) {
     grid = std::max<size_t>(grid, 1);
-    return ((grid + S - 1) / S) * ((it256 + grid - 1) / grid) * 256;
+    return ((grid + S - 1) / S) * ((itT + grid - 1) / grid) * T;
   };
   const size_t per_stripe = std::min(m, share(http_raw_dl_grid(s.raw, lists, m, cus))) +
                             std::min(m, share((size_t)std::max(1, cus) * 2));

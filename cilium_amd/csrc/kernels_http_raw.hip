@@ -29,6 +29,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
@@ -43,7 +44,8 @@ namespace cg {
 
 namespace {
 
-constexpr int kRawThreads = 256;
+constexpr int kRawThreads = (int)kRawScanThreads;
+constexpr uint32_t kRawWaves = kRawThreads / 64;
 
 // CG_RAW_CLOCKS (experiment builds only, tools/exp_http.py raw_clocks): the
 // scan's phases timed per wave with the shader clock; one wave prints its
@@ -723,9 +725,9 @@ __device__ __forceinline__ lds_u8* wave_stage(lds_u32* lds, uint32_t F, uint32_t
   return (lds_u8*)(lds + F * kRawThreads) + wave * kStage;
 }
 __device__ __forceinline__ lds_u32* wave_masks(lds_u32* lds, uint32_t F, uint32_t wave) {
-  return (lds_u32*)((lds_u8*)(lds + F * kRawThreads) + 4 * kStage) + wave * 2 * kMaskWords;
+  return (lds_u32*)((lds_u8*)(lds + F * kRawThreads) + kRawWaves * kStage) + wave * 2 * kMaskWords;
 }
-__device__ __forceinline__ lds_u8* tchar_table(lds_u32* lds, uint32_t F) { return (lds_u8*)wave_masks(lds, F, 4); }
+__device__ __forceinline__ lds_u8* tchar_table(lds_u32* lds, uint32_t F) { return (lds_u8*)wave_masks(lds, F, kRawWaves); }
 __device__ __forceinline__ lds_u32* key_counters(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + 256); }
 // [name keys: 8 u32 per slot][field slots: 4 u32 per slot][names, u32
 // words][program hash keys][values] after the key counters, when they fit
@@ -1562,11 +1564,13 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
   RawIn nxt = raw_in(off, policy, ingress, port, remote, base + gstride + wave * 64 + lane, n);
   StageRegs S;
   stage_load(raw, cur, lane, S, off);
+  uint64_t clk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0;
   for (; base < n; base += gstride) {
     const size_t i0 = base + (size_t)wave * 64;
     if (i0 >= n) break;  // wave-uniform
     const size_t i = i0 + lane;
     const bool live = i < n;
+    RAW_CLK(c0);
     const RawIn nn = raw_in(off, policy, ingress, port, remote, base + 2 * gstride + wave * 64 + lane, n);
     const uint32_t prog = live ? lookup_prog(R, T, cur.pol, cur.ing() != 0, cur.port()) : kProgDeny;
     // stage k: registers → LDS (the previous iteration's reads are done)
@@ -1577,9 +1581,11 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
     // stage k + 1 into registers, under this iteration's parse
     stage_load(raw, nxt, lane, S, off);  // (past n: no bytes, nothing staged)
     wave_sync();
+    RAW_CLK(c1);
     if (kLists) build_masks_lists(stage, slen, tct, masks, lane);
     else build_masks(stage, slen, tct, masks, lane);
     wave_sync();
+    RAW_CLK(c2);
     // every request but an unknown policy's is parsed: a head the codec
     // rejects is denied in any program (flagged malformed)
     const uint32_t hn = cur.len;
@@ -1603,8 +1609,10 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
         else units = (len + 15) / 16;
       }
     }
+    RAW_CLK(c3);
     const bool want = live && !defer && !walk;
     const RawSlot sl = raw_slot(L, want, raw_vkey(L, group_of(R, prog) * kRawUnits + units, blockIdx.x), prog);
+    RAW_CLK(c4);
     walk |= want && !sl.ok;
     list_append(L.walk, &L.ctl[kRawCtlWalk], walk, (uint32_t)i, lane);
     if (want && sl.ok) {
@@ -1613,9 +1621,31 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
         emit_stage(R, stage, hs, sp, kRawThreads, P, last, o);
       });
     }
+    RAW_CLK(c5);
+    RAW_ACC(0, c0, c1);  // program lookup, stage store (waits for the stage's loads)
+    RAW_ACC(1, c1, c2);  // structural masks
+    RAW_ACC(2, c2, c3);  // parse, walked length
+    RAW_ACC(3, c3, c4);  // slot (atomic, directory)
+    RAW_ACC(4, c4, c5);  // lists, emission
+    RAW_ACC(5, c0, c5);
+#ifdef CG_RAW_CLOCKS
+    clk[6] += 1;
+#endif
+    (void)c6;
     cur = nxt;
     nxt = nn;
   }
+#ifdef CG_RAW_CLOCKS
+  if (blockIdx.x == 7 && threadIdx.x == 64) {
+    printf("raw_scan_dl clocks (wave 1 of block 7, %llu iterations): stage %llu masks %llu parse %llu slot %llu emit %llu total %llu\n",
+           (unsigned long long)clk[6], (unsigned long long)clk[0], (unsigned long long)clk[1], (unsigned long long)clk[2],
+           (unsigned long long)clk[3], (unsigned long long)clk[4], (unsigned long long)clk[5]);
+    printf("parse clocks: request line %llu, line reads %llu, values %llu, names %llu, end %llu\n", g_pclk[0], g_pclk[1],
+           g_pclk[2], g_pclk[3], g_pclk[4]);
+  }
+#else
+  (void)clk;
+#endif
 }
 
 // ---- the deferred requests (heads / lists not inside their wave's stage:
@@ -1859,7 +1889,7 @@ unsigned grid_for(size_t n, int cus, unsigned per_cu) {
 bool lds_tables_fit(const HttpRawDev& R) { return raw_tables_lds_words(R) * 4 <= 8 * 1024; }
 size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
-  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + 4 * (size_t)kStage + 4 * 2 * (kStage / 8) + 256 +
+  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + kRawWaves * (size_t)kStage + kRawWaves * 2 * (kStage / 8) + 256 +
          (lds_keys ? nk * 4 : 0) + (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 : 0) +
          (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
 }
@@ -1981,6 +2011,9 @@ size_t http_raw_dl_grid(const HttpRawDev& R, bool lists, size_t n, int cus) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, kRawThreads, lds) != hipSuccess || nb < 1)
         nb = 1;
       it = occ.emplace(std::make_tuple(dev, (const void*)kern, lds), nb).first;
+      if (getenv("CILIUM_GPU_DEBUG"))
+        fprintf(stderr, "[cilium-gpu] raw_scan_dl_kernel<%d>: %zu B of LDS per workgroup, %d workgroups per CU\n",
+                (int)lists, lds, nb);
     }
     per_cu = it->second;
   }

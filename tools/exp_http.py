@@ -193,6 +193,14 @@ VARIANTS.update({
                        ("constexpr int kPre = 1;", "constexpr int kPre = 2;")],
     "h_w4_pre4": [("constexpr int kHttpWaves = 8;", "constexpr int kHttpWaves = 4;"),
                   ("constexpr int kPre = 1;", "constexpr int kPre = 4;")],
+    # the scans at 512 threads per workgroup (spans / tables amortized over 8
+    # waves) with 5 KiB stages: 2 workgroups = 4 waves per SIMD at config 5;
+    # and 5 KiB stages alone (256 threads)
+    "rawdl_t512_s5k": [("dev_types.h", "constexpr uint32_t kRawScanThreads = 256;",
+                        "constexpr uint32_t kRawScanThreads = 512;"),
+                       ("kernels_http_raw.hip", "constexpr uint32_t kStage = 6144;", "constexpr uint32_t kStage = 5120;"),
+                       ("http_raw.cc", "#include", "#include")],
+    "rawdl_s5k": _rs(5120),
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
@@ -217,6 +225,11 @@ def build_variant(name, subs):
     # is found first by the changed sources' quote includes
     vdir = OUT / name
     vdir.mkdir(exist_ok=True)
+    # every header goes there too (a changed one included from an unchanged
+    # header would otherwise be found twice under #pragma once)
+    for h in B.CSRC.glob("*.h"):
+        if h.name not in files:
+            (vdir / h.name).write_text(h.read_text().replace('"../../include/', f'"{ROOT}/include/'))
     for fn, src in files.items():
         (vdir / fn).write_text(src.replace('"../../include/', f'"{ROOT}/include/'))
     for fn in files:
