@@ -725,10 +725,12 @@ struct KfLayout {
   }
 };
 
+// One queued request: its head words x (apiKey | version << 16), y (kind,
+// topic count, redirect) and w (clientID) come from the queue, not from HBM
+// again (the head was read nontemporal: a re-read is a second fetch).
 __device__ __forceinline__ void kf_slow_one(const KafkaDev& T, const KfLayout& L,
                                             const uint32_t* __restrict__ arena, uint8_t* __restrict__ out,
-                                            uint32_t i, uint32_t g, KfCount& cnt) {
-  const uint4 h = *L.head(i);
+                                            uint32_t i, uint32_t g, uint4 h, KfCount& cnt) {
   const int key = (int16_t)(h.x & 0xFFFF), ver = (int16_t)(h.x >> 16);
   const uint32_t kind = h.y & 0xFF, nt = (h.y >> 8) & 0xFF, red = h.y >> 16;
   const uint32_t b = (key >= 0 && key < 64) ? (uint32_t)key : 64u;
@@ -743,7 +745,7 @@ __device__ __forceinline__ void kf_slow_one(const KafkaDev& T, const KfLayout& L
 __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, KfLayout L, size_t n,
                                                               const uint32_t* __restrict__ arena,
                                                               uint8_t* __restrict__ out) {
-  __shared__ uint32_t q_i[kKafkaQueue], q_g[kKafkaQueue];
+  __shared__ uint32_t q_i[kKafkaQueue], q_g[kKafkaQueue], q_x[kKafkaQueue], q_y[kKafkaQueue], q_w[kKafkaQueue];
   __shared__ uint32_t q_n;
   if (threadIdx.x == 0) q_n = 0;
   __syncthreads();
@@ -830,6 +832,9 @@ __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, KfLayo
           const uint32_t p = qb + (uint32_t)__popcll(m & ((1ULL << lane) - 1));
           q_i[p] = (uint32_t)i;
           q_g[p] = g[u];
+          q_x[p] = h[u].x;
+          q_y[p] = h[u].y;
+          q_w[p] = h[u].w;
         }
       }
       if (live && !slow) {
@@ -841,7 +846,7 @@ __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, KfLayo
     uint32_t nq = q_n;
     while (nq >= kKafkaThreads) {
       const uint32_t p = nq - kKafkaThreads + threadIdx.x;
-      kf_slow_one(T, L, arena, out, q_i[p], q_g[p], cnt);
+      kf_slow_one(T, L, arena, out, q_i[p], q_g[p], make_uint4(q_x[p], q_y[p], 0u, q_w[p]), cnt);
       nq -= kKafkaThreads;
       __syncthreads();
       if (threadIdx.x == 0) q_n = nq;
@@ -849,7 +854,10 @@ __global__ __launch_bounds__(kKafkaThreads) void kafka_kernel(KafkaDev T, KfLayo
     }
   }
   __syncthreads();
-  if (threadIdx.x < q_n) kf_slow_one(T, L, arena, out, q_i[threadIdx.x], q_g[threadIdx.x], cnt);
+  if (threadIdx.x < q_n) {
+    const uint32_t p = threadIdx.x;
+    kf_slow_one(T, L, arena, out, q_i[p], q_g[p], make_uint4(q_x[p], q_y[p], 0u, q_w[p]), cnt);
+  }
   // the common case: every lane of the wave counted for the same redirect
   const uint32_t first = __builtin_amdgcn_readfirstlane(cnt.red);
   if (__all(cnt.red == first)) {
