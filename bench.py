@@ -534,9 +534,10 @@ def replicate_batch(b, reps: int, dev, torch, return_groups: bool = False, layou
         else:
             groups.append([int(prog), int(first), int(nt)])
     kib = ttab[:, 0].astype(np.int64)  # tile offsets in 512-byte granules (HttpTile.at)
-    units_field = ttab[:, 1].astype(np.int64)  # HttpTile.units: units | last-unit bytes << 16
-    units = units_field & 0xFFFF
-    span = 1 + 2 * units               # granules per tile: meta block + 1 KiB units
+    units_field = ttab[:, 1].astype(np.int64)  # HttpTile.units: units | half-last << 15 | last-unit bytes << 16
+    units = units_field & 0x7FFF
+    half = (units_field >> 15) & 1
+    span = 1 + 2 * units - half        # granules per tile: meta block + 1 KiB units (the last one 512 B when half)
     big, new_tt, placed, pos, kpos = [], [], [], 0, 0
     tile_map = np.zeros(ntiles, np.int64)
     for prog, first, nt in groups:

@@ -167,6 +167,9 @@ constexpr uint32_t kRdirMaxSpan = 8192;
 // Per-rule hit counters a workgroup keeps in LDS for its current program
 // (programs with more rules count straight into global memory).
 constexpr uint32_t kLdsRuleHits = 512;
+// 160 KiB less the static LDS (allowed/denied pair, per-rule hit counters):
+// the largest program table a workgroup stages (http.cc, http_pack.cc)
+constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits) / 4;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; `dead` is the dead state, states above it
@@ -200,11 +203,14 @@ constexpr uint32_t kProgDeny = 0xFFFFFFFFu;   // unknown policy → deny
 // tile table, then the tiles (1 KiB aligned).  A tile is 64 request records
 // stored unit-major: the meta block (8 bytes per lane), then `units` 16-byte
 // string units, each one contiguous 1 KiB (string unit u ≥ 1 of lane l at
-// tile + 512 + (u-1)*1024 + l*16).  The
+// tile + 512 + (u-1)*1024 + l*16).  A tile whose lanes hold at most 8 bytes
+// in its last unit may store that unit as a half unit (kTileHalfLast: 8 bytes
+// per lane, 512 B, lane l at its start + l*8): cg_http_pack does, the
+// device-built batches do not.  The
 // packer groups requests by program so every chunk (≤ kChunkTiles tiles)
 // belongs to one program and a workgroup can stage that program's table in
 // LDS.  Slot order is returned to the caller (order[]).
-constexpr uint32_t kBatchMagic = 0x33484743u;  // "CGH3"
+constexpr uint32_t kBatchMagic = 0x34484743u;  // "CGH4"
 constexpr uint32_t kChunkTiles = 64;
 struct HttpBatchHeader {
   uint32_t magic;
@@ -220,12 +226,18 @@ struct HttpBatchHeader {
 };
 struct HttpTile {
   uint32_t at;     // tile data at tiles_off + at * 512: the 512-byte meta block
-  uint32_t units;  // (8 bytes per lane), then `units` 1 KiB string units (0..8) in bits 0..15;
+  uint32_t units;  // (8 bytes per lane), then `units` 1 KiB string units (0..8) in bits 0..14;
+                   // bit 15 (kTileHalfLast): the last of them is a 512-B half unit;
                    // bits 16..31: string bytes its lanes hold in the last unit (1..16), the
                    // rest of that unit being padding the walk may skip (0: walk all 16)
 };
-CG_HD inline uint32_t tile_units(const HttpTile& t) { return t.units & 0xFFFFu; }
+constexpr uint32_t kTileHalfLast = 0x8000u;
+CG_HD inline uint32_t tile_units(const HttpTile& t) { return t.units & 0x7FFFu; }
 CG_HD inline uint32_t tile_tail(const HttpTile& t) { return t.units >> 16; }
+CG_HD inline bool tile_half(const HttpTile& t) { return (t.units & kTileHalfLast) != 0; }
+// 512-byte granules of a tile's data: the meta block, two per full unit, one
+// for a half unit
+CG_HD inline uint32_t tile_granules(const HttpTile& t) { return 1 + 2 * tile_units(t) - (tile_half(t) ? 1u : 0u); }
 struct HttpChunk {
   uint32_t prog;
   uint32_t first_tile;

@@ -54,9 +54,6 @@ constexpr uint8_t kAbsent = 0x01;
 constexpr uint8_t kRestAbsent = 0x02;  // every remaining field absent (ends the string)
 constexpr int kMaxUnionStates = 400000;  // before minimization, per part
 constexpr int kMaxPartStates = 65535;    // u16 transition entries
-// 160 KiB less the static LDS (allowed/denied pair, per-rule hit counters):
-// one program table per workgroup
-constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits) / 4;
 
 // ListExact/ListPrefix/ListSearch (proxylib only): the field is a list of
 // escaped items, each followed by the pair {0x03, 0x14}, and every item must

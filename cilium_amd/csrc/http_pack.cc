@@ -43,9 +43,12 @@ constexpr size_t kMetaBytes = (size_t)CG_HTTP_TILE * CG_HTTP_META_BYTES;  // the
 constexpr size_t kGranule = 512;  // tile offsets count 512-byte granules
 constexpr size_t kMaxTileBytes = kMetaBytes + (size_t)(CG_HTTP_UNITS - 1) * kUnitBytes;
 
-// byte offset of unit u (0 = meta block) of a tile at granule g, lane l
-inline size_t tile_unit_at(uint32_t g, uint32_t u, size_t lane) {
-  return (size_t)g * kGranule + (u ? kMetaBytes + (size_t)(u - 1) * kUnitBytes + lane * 16 : lane * CG_HTTP_META_BYTES);
+// byte offset of unit u (0 = meta block) of tile t, lane l (its last unit
+// a half unit of 8 bytes per lane when tile_half)
+inline size_t tile_unit_at(const HttpTile& t, uint32_t u, size_t lane) {
+  const bool half = u && u == tile_units(t) && tile_half(t);
+  return (size_t)t.at * kGranule +
+         (u ? kMetaBytes + (size_t)(u - 1) * kUnitBytes + lane * (half ? 8 : 16) : lane * CG_HTTP_META_BYTES);
 }
 
 bool name_eq_ci(const uint8_t* a, size_t an, const std::string& lower_b) {
@@ -350,6 +353,14 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   // and the bytes its lanes hold in that last unit (padding past the longest
   // one need not be walked: comb.h, padding never changes a label)
   std::vector<HttpTile> ttab(tiles);
+  // half last units only in tiles of programs http_kernel walks one part at
+  // a time from LDS (one_part_tiles; its other walkers read whole units)
+  std::vector<uint8_t> half_ok(tiles, 0);
+  for (const HttpChunk& c : chunks) {
+    const bool ok = c.prog < np && !(s.progs[c.prog].flags & kProgAllowAll) && s.progs[c.prog].part_count == 1 &&
+                    (s.progs[c.prog].flags & kProgRebased) && s.progs[c.prog].cell_count <= kMaxLdsCells;
+    std::fill(half_ok.begin() + c.first_tile, half_ok.begin() + c.first_tile + c.ntiles, (uint8_t)ok);
+  }
   parallel_ranges(tiles, nt, [&](size_t a, size_t b, unsigned) {
     for (size_t k = a; k < b; ++k) {
       uint32_t units = 0, tail = 0;
@@ -362,7 +373,10 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
         if (i != 0xFFFFFFFFu && walked_units(i) == units)
           tail = std::max<uint32_t>(tail, (uint32_t)(str_len(i) - 16 * (units - 1)));
       }
-      ttab[k].units = units | (units ? (tail ? tail : 16u) << 16 : 0u);
+      if (units && !tail) tail = 16;
+      // a last unit holding at most 8 bytes of any lane is stored as a half
+      // unit: 512 B less per tile (config 5: 6.7% of the batch)
+      ttab[k].units = units | (units && tail <= 8 && half_ok[k] ? kTileHalfLast : 0u) | tail << 16;
     }
   });
   lap("ttab");
@@ -370,7 +384,7 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   for (auto& t : ttab) {
     if (gran > 0xFFFFFFFFull) fail(CG_INVALID_ARGUMENT, "batch beyond 2 TiB");
     t.at = (uint32_t)gran;
-    gran += 1 + 2 * tile_units(t);
+    gran += tile_granules(t);
   }
   const size_t max_tiles = http_batch_slots(s, n) / CG_HTTP_TILE;
   const size_t hdr = header_bytes(max_tiles);
@@ -378,7 +392,7 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   if (batch && need > batch_cap) fail(CG_INVALID_ARGUMENT, "batch buffer too small");
   uint8_t* data = batch ? (uint8_t*)batch + hdr : nullptr;
   auto unit_ptr = [&](size_t slot, uint32_t u) {
-    return data + tile_unit_at(ttab[slot / CG_HTTP_TILE].at, u, slot % CG_HTTP_TILE);
+    return data + tile_unit_at(ttab[slot / CG_HTTP_TILE], u, slot % CG_HTTP_TILE);
   };
   // overflow arena entries in request order: u32 length then the string,
   // 16-byte aligned
@@ -412,7 +426,7 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
   if (batch || (arena && build)) {
     parallel_ranges(tiles, nt, [&](size_t a, size_t b, unsigned) {
       for (size_t k = a; k < b; ++k) {
-        if (batch) memset(data + (size_t)ttab[k].at * kGranule, 0, (1 + 2 * (size_t)tile_units(ttab[k])) * kGranule);
+        if (batch) memset(data + (size_t)ttab[k].at * kGranule, 0, (size_t)tile_granules(ttab[k]) * kGranule);
         for (size_t l = 0; l < CG_HTTP_TILE; ++l) {
           const size_t sl = k * CG_HTTP_TILE + l;
           const uint32_t i = req_of_slot[sl];
@@ -444,8 +458,12 @@ void http_pack(const HttpSnapshot& s, size_t n, const uint32_t* policy, const ui
           if (batch) {
             memcpy(unit_ptr(sl, 0), meta, CG_HTTP_META_BYTES);
             const uint32_t wu = walked_units(i);
-            for (uint32_t u = 0; u < wu; ++u)
-              memcpy(unit_ptr(sl, u + 1), str + u * 16, std::min<size_t>(16, len - u * 16));
+            const HttpTile& tt = ttab[k];
+            for (uint32_t u = 0; u < wu; ++u) {
+              // (a half unit holds the tile's last ≤ 8 bytes of every lane)
+              const size_t cap = u + 1 == tile_units(tt) && tile_half(tt) ? 8 : 16;
+              memcpy(unit_ptr(sl, u + 1), str + u * 16, std::min<size_t>(cap, len - u * 16));
+            }
           }
         }
       }
@@ -465,7 +483,7 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
   const HttpTile* ttab = (const HttpTile*)(batch + h.ttab_off);
   const uint8_t* data = batch + h.tiles_off;
   auto unit_ptr = [&](size_t slot, uint32_t u) {
-    return data + tile_unit_at(ttab[slot / CG_HTTP_TILE].at, u, slot % CG_HTTP_TILE);
+    return data + tile_unit_at(ttab[slot / CG_HTTP_TILE], u, slot % CG_HTTP_TILE);
   };
   for (uint32_t c = 0; c < h.nchunks; ++c) {
     const uint32_t prog = chunks[c].prog;
@@ -501,8 +519,12 @@ void http_eval_host(const HttpSnapshot& s, const uint8_t* batch, const uint8_t* 
         if ((size_t)off + 4 + len > arena_len) continue;
         str.assign((const char*)arena + off + 4, len);
       } else {
-        for (uint32_t u = 0; u < tile_units(ttab[sl / CG_HTTP_TILE]); ++u)
-          str.append((const char*)unit_ptr(sl, u + 1), 16);
+        const HttpTile& tt = ttab[sl / CG_HTTP_TILE];
+        for (uint32_t u = 0; u < tile_units(tt); ++u) {
+          const bool half = u + 1 == tile_units(tt) && tile_half(tt);
+          str.append((const char*)unit_ptr(sl, u + 1), half ? 8 : 16);
+          if (half) str.append(8, '\0');
+        }
       }
       const uint32_t* blk = s.cells.data() + pg.cell_begin;
       auto bmask = [&](uint32_t o, uint32_t w) { return (uint64_t)blk[o + 2 * w] | (uint64_t)blk[o + 2 * w + 1] << 32; };

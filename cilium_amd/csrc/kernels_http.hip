@@ -201,18 +201,25 @@ __device__ __forceinline__ uint32_t walk_arena(const uint32_t* __restrict__ cell
 // A tile's meta block (8 bytes per lane: remote identity, overflow arena
 // offset / 16 | flags << 24) and its string units (unit u ≥ 1 of lane l at
 // units[(u - 1) * 64 + l]).
+// `half`: the tile's last unit is a half unit (kTileHalfLast: 8 bytes per
+// lane; its other 8 bytes read as zero padding).
 struct TileRef {
   const uint2* meta;
   const uint4* units;
+  bool half;
 };
 __device__ __forceinline__ TileRef tile_ref(const uint8_t* __restrict__ tiles, const HttpTile& tt) {
   const uint8_t* base = tiles + (size_t)tt.at * 512;
-  return {reinterpret_cast<const uint2*>(base), reinterpret_cast<const uint4*>(base + kWave * CG_HTTP_META_BYTES)};
+  return {reinterpret_cast<const uint2*>(base), reinterpret_cast<const uint4*>(base + kWave * CG_HTTP_META_BYTES),
+          tile_half(tt)};
 }
 
-// String unit u (1-based) of a tile holding `units` of them; past them a lane
-// re-reads the tile's last unit, or its meta block when it has none (bytes
-// it never walks within its string) — never beyond the tile.
+// String unit u (1-based) of a tile holding `units` whole units (the
+// generic walker's tiles: cg_http_pack gives half last units only to
+// one-part LDS programs, and http_chunks denies a half tile that reaches
+// another walker); past them a lane re-reads the tile's last unit, or its
+// meta block when it has none (bytes it never walks within its string) —
+// never beyond the tile.
 __device__ __forceinline__ uint4 tile_unit(const TileRef& tr, uint32_t units, uint32_t u, uint32_t lane) {
   if (units == 0) return reinterpret_cast<const uint4*>(tr.meta)[lane & 31];
   return tr.units[(min(u, units) - 1) * kWave + lane];
@@ -231,6 +238,14 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
 __device__ __forceinline__ uint2 ld_nt(const uint2* p) {
   const u32x2_nt x = __builtin_nontemporal_load(reinterpret_cast<const u32x2_nt*>(p));
   return make_uint2(x.x, x.y);
+}
+// unit k of lane l, nontemporal: 16 bytes, or 8 and zeros from a half unit
+__device__ __forceinline__ uint4 ld_nt_unit(const TileRef& tr, uint32_t k, uint32_t l, bool half) {
+  if (half) {
+    const uint2 v = ld_nt(reinterpret_cast<const uint2*>(tr.units + k * kWave) + l);
+    return make_uint4(v.x, v.y, 0u, 0u);
+  }
+  return ld_nt(tr.units + k * kWave + l);
 }
 
 // The overflow string of a lane whose meta word is m (arena entry: u32 length,
@@ -304,11 +319,14 @@ __device__ __forceinline__ void http_tiles(const HttpDev& T, const HttpProg& pg,
   for (int j = 0; j < K; ++j) {
     const HttpTile tt = ttab[tile[j]];
     tr[j] = tile_ref(tiles, tt);
-    tu[j] = valid[j] ? tile_units(tt) : 0u;
+    // (a half last unit never reaches this walker from cg_http_pack: such a
+    // tile is denied unwalked, its units never read as whole ones)
+    const bool half = tile_half(tt);
+    tu[j] = valid[j] && !half ? tile_units(tt) : 0u;
     units = max(units, tu[j]);
     meta[j] = tr[j].meta[lane];
     const uint32_t flags = meta[j].y >> 24;
-    counted[j] = valid[j] && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
+    counted[j] = valid[j] && !half && !(flags & (CG_HTTP_F_PAD | CG_HTTP_F_MALFORMED));
     overflow[j] = counted[j] && (flags & CG_HTTP_F_OVERFLOW);
     any_overflow |= overflow[j];
     row[j] = remote_row(blk, pg, meta[j].x);
@@ -415,9 +433,11 @@ __device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units,
   const uint32_t lane = lane_now();
   p.meta = NT_META(tr.meta + lane);
 #pragma unroll
-  for (int k = 0; k < kPre; ++k)  // stays inside the tile (see tile_unit)
-    p.u[k] = NT_PRE(units == 0 ? reinterpret_cast<const uint4*>(tr.meta) + (lane & 31)
-                               : tr.units + (min(k + 1u, units) - 1) * kWave + lane);
+  for (int k = 0; k < kPre; ++k) {  // stays inside the tile (see tile_unit)
+    const uint32_t kk = min(k + 1u, units) - 1;
+    if (units == 0) p.u[k] = NT_PRE(reinterpret_cast<const uint4*>(tr.meta) + (lane & 31));
+    else p.u[k] = ld_nt_unit(tr, kk, lane, tr.half && kk + 1 == units);
+  }
 }
 
 // One tile of a one-part program whose block `blk` is in LDS, its string
@@ -429,7 +449,7 @@ __device__ __forceinline__ void tile_prefetch(const TileRef& tr, uint32_t units,
 // walk, only for lanes that reached an accepting state.  No early exit:
 // lanes whose string ended (or died) keep stepping through zero padding or
 // the dead state, which cannot change their verdict.
-template <int N, bool kCls, bool kRaw>
+template <int N, bool kCls, bool kRaw, bool kHalf>
 __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg, const HttpPart& pt,
                                             uint32_t prog, const uint32_t* __restrict__ blk, const TileRef tr,
                                             const TilePre& cur, bool has_next, const TileRef trn, uint32_t nunits,
@@ -444,7 +464,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   uint4 unit[kWin];
 #pragma unroll
   for (int k = 0; k < kWin && k < N; ++k)
-    unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : ld_nt(tr.units + k * kWave + lane_now());
+    unit[k] = k < kPre ? cur.u[k < kPre ? k : 0] : ld_nt_unit(tr, k, lane_now(), kHalf && k == N - 1);
   if (has_next) tile_prefetch(trn, nunits, lane, nxt);
   __builtin_amdgcn_sched_barrier(0);
   const uint32_t flags = meta.y >> 24;
@@ -456,7 +476,7 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
   for (int k = 0; k < N; ++k) {
     // raw-byte batches: the unit's bytes through the code map (class mode)
     const uint4 u = kRaw && kCls ? lds_transcode(cm, unit[k % kWin]) : unit[k % kWin];
-    if (k + kWin < N) unit[k % kWin] = ld_nt(tr.units + (k + kWin) * kWave + lane_now());
+    if (k + kWin < N) unit[k % kWin] = ld_nt_unit(tr, k + kWin, lane_now(), kHalf && k + kWin == N - 1);
     // the last unit: only the 4-byte groups holding some lane's string
     // (tail, wave-uniform), the rest is padding
     const bool last = k == N - 1;
@@ -523,10 +543,11 @@ __device__ __forceinline__ void http_tile_n(const HttpDev& T, const HttpProg& pg
 // chain stands in for the halved occupancy.
 constexpr bool kPairTiles = false;
 
-__device__ __forceinline__ const uint4* pair_unit(const TileRef& tr, uint32_t units, uint32_t k) {
+__device__ __forceinline__ uint4 pair_unit(const TileRef& tr, uint32_t units, uint32_t k) {
   const uint32_t lane = lane_now();
-  return units == 0 ? reinterpret_cast<const uint4*>(tr.meta) + (lane & 31)
-                    : tr.units + (min(k + 1u, units) - 1u) * kWave + lane;
+  if (units == 0) return ld_nt(reinterpret_cast<const uint4*>(tr.meta) + (lane & 31));
+  const uint32_t kk = min(k + 1u, units) - 1u;
+  return ld_nt_unit(tr, kk, lane, tr.half && kk + 1 == units);
 }
 
 // The verdict of one lane's request after the walk (as http_tile_n's).
@@ -574,8 +595,8 @@ __device__ __forceinline__ void http_pair_n(const HttpDev& T, const HttpProg& pg
   uint4 wa[kW], wb[kW];
 #pragma unroll
   for (int k = 0; k < kW && k < N; ++k) {
-    wa[k] = k == 0 ? ca.u[0] : ld_nt(pair_unit(ra, ua, k));
-    wb[k] = k == 0 ? cb.u[0] : ld_nt(pair_unit(rb, ub, k));
+    wa[k] = k == 0 ? ca.u[0] : (pair_unit(ra, ua, k));
+    wb[k] = k == 0 ? cb.u[0] : (pair_unit(rb, ub, k));
   }
   if (has_next) {
     tile_prefetch(rna, nua, lane, xa);
@@ -589,8 +610,8 @@ __device__ __forceinline__ void http_pair_n(const HttpDev& T, const HttpProg& pg
     const uint4 a = kRaw ? lds_transcode(cm, wa[k % kW]) : wa[k % kW];
     const uint4 b = kRaw ? lds_transcode(cm, wb[k % kW]) : wb[k % kW];
     if (k + kW < N) {
-      wa[k % kW] = ld_nt(pair_unit(ra, ua, k + kW));
-      wb[k % kW] = ld_nt(pair_unit(rb, ub, k + kW));
+      wa[k % kW] = (pair_unit(ra, ua, k + kW));
+      wb[k % kW] = (pair_unit(rb, ub, k + kW));
     }
     const bool last = k == N - 1;
     lds_cls_step2x16<0>(dead, sa, a, sb, b);
@@ -653,13 +674,15 @@ __device__ __forceinline__ void one_part_pairs(const HttpDev& T, const HttpProg&
       switch (tile_units(ta)) {
 #define CG_TILE_1(n)                                                                                               \
   case n:                                                                                                          \
-    http_tile_n<n, true, kRaw>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena,          \
-                               arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);                              \
+    if (!kRaw && tile_half(ta))                                                                                    \
+      http_tile_n<n, true, kRaw, true>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena,  \
+                                       arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);                      \
+    else                                                                                                           \
+      http_tile_n<n, true, kRaw, false>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena, \
+                                        arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);                     \
     break;
         CG_TILE_1(0) CG_TILE_1(1) CG_TILE_1(2) CG_TILE_1(3) CG_TILE_1(4) CG_TILE_1(5) CG_TILE_1(6) CG_TILE_1(7)
-        default:
-          http_tile_n<8, true, kRaw>(T, pg, pt, prog, lcells, ra, pa, false, ra, 0, tile_tail(ta), xa, t, arena,
-                                     arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);
+        default: CG_TILE_1(8)
 #undef CG_TILE_1
       }
       break;
@@ -718,13 +741,15 @@ __device__ __forceinline__ void one_part_tiles(const HttpDev& T, const HttpProg&
     switch (tile_units(tt)) {  // wave-uniform
 #define CG_TILE_N(n)                                                                                                \
   case n:                                                                                                           \
-    http_tile_n<n, kCls, kRaw>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t, arena, \
-                               arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);                                \
+    if (!kRaw && n > 0 && tile_half(tt))                                                                            \
+      http_tile_n<n, kCls, kRaw, true>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), \
+                                       nxt, t, arena, arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);          \
+    else                                                                                                            \
+      http_tile_n<n, kCls, kRaw, false>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), \
+                                        nxt, t, arena, arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);         \
     break;
       CG_TILE_N(0) CG_TILE_N(1) CG_TILE_N(2) CG_TILE_N(3) CG_TILE_N(4) CG_TILE_N(5) CG_TILE_N(6) CG_TILE_N(7)
-      default:
-        http_tile_n<8, kCls, kRaw>(T, pg, pt, prog, lcells, tb, pre, has_next, tbn, tile_units(ttn), tile_tail(tt), nxt, t,
-                                   arena, arena_bytes, out, lane, n_allow, n_deny, s_hits, cm);
+      default: CG_TILE_N(8)
 #undef CG_TILE_N
     }
     tt = ttn;

@@ -403,12 +403,15 @@ int cg_http_rule_info_get(uint64_t h, cg_http_rule_info* out, size_t cap, size_t
  * tiles of 64: a tile is its 512-byte meta block then as many string units as
  * its longest string needs (string unit u ≥ 1 of lane l at tile + 512 +
  * (u-1)*1024 + l*16), so a wavefront's 16-byte load of a unit is one
- * contiguous 1 KiB read.  The
+ * contiguous 1 KiB read; when no lane holds more than 8 bytes in the last
+ * unit, that unit is stored as a 512-byte half unit (8 bytes per lane; tile
+ * table bit 15), in tiles of programs walked from LDS one part at a time.  The
  * packer resolves each request's (policy, direction, port) evaluation
  * program on the host and groups requests by program (padding each group to
  * whole tiles), so a workgroup stages one program's DFA in LDS.  A batch is
  * a 64-byte header (its total_bytes field = the batch's size), a chunk
- * table, a tile table ({offset in KiB, units} per tile), then the tiles;
+ * table, a tile table ({offset in 512-B granules, units | half << 15 |
+ * last-unit bytes << 16} per tile), then the tiles;
  * slots are in grouped order and order[slot] gives the request index
  * (UINT32_MAX for padding).  Size the buffers with cg_http_batch_bytes /
  * cg_http_batch_slots (upper bounds for n requests under the installed

@@ -29,7 +29,9 @@ def main():
         agg = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if f"::{a.kernel}(" not in name:
+            # "kernel" matches the kernel and its template instances unless
+            # it names one ("http_kernel" ⊇ "http_kernel<false>")
+            if f"::{a.kernel}(" not in name and ("<" in a.kernel or f"::{a.kernel}<" not in name):
                 continue
             agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
             resources = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
