@@ -342,6 +342,7 @@ void raw_sequential(RawCall c) {
 // by what the scan finds (no host round trip); 2^25 requests reserve ~4.8 GB
 // of tile data on the 10K-rule set.
 constexpr size_t kRawSubBatch = (size_t)1 << 25;
+constexpr size_t kRawSubBatchMax = (size_t)1 << 27;  // CILIUM_GPU_RAW_SUBBATCH's ceiling
 
 uint32_t floor_pow2(uint32_t x) {
   uint32_t p = 1;
@@ -442,9 +443,10 @@ void raw_device_layout(const HttpSnapshot& s, StagingSlot& sl, int cus, bool lis
   // the slot's last raw call may still be queued on another stream: this
   // stream waits for it on the device (no host wait)
   if (sl.raw_ev && sl.raw_stream != stream) hip_check(hipStreamWaitEvent(st, (hipEvent_t)sl.raw_ev, 0), "hipStreamWaitEvent");
-  // (CILIUM_GPU_RAW_SUBBATCH: a smaller sub-batch, for tests)
+  // (CILIUM_GPU_RAW_SUBBATCH: another sub-batch size — smaller for tests, up
+  // to 2^27 for the measurements of larger ones)
   size_t sub = kRawSubBatch;
-  if (const char* v = getenv("CILIUM_GPU_RAW_SUBBATCH")) sub = std::min(kRawSubBatch, std::max<size_t>(64, strtoull(v, nullptr, 10)));
+  if (const char* v = getenv("CILIUM_GPU_RAW_SUBBATCH")) sub = std::min(kRawSubBatchMax, std::max<size_t>(64, strtoull(v, nullptr, 10)));
   for (size_t a = 0; a < n; a += sub) {
     const size_t m = std::min(sub, n - a);
     raw_dl_subbatch(s, sl, cus, lists, d_raw, d_off + a, m, d_policy + a, d_ingress + a, d_port + a, d_remote + a,
