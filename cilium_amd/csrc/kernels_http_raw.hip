@@ -405,19 +405,19 @@ __device__ __forceinline__ MaskWin load_win(const lds_u32* msp, const lds_u32* m
 __device__ __forceinline__ uint32_t win_word(const uint32_t (&w)[4], uint32_t j) {
   return j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : j == 3 ? w[3] : 0u;
 }
-// next_set over a window (p >= base): the 64 bits from the word holding p
-// (at least 33 from p) in registers, then the LDS mask
+// next_set over a window (p >= base): the 128 bits as two 64-bit halves in
+// registers — the rest of p's half, then the high half — then the LDS mask
 __device__ __forceinline__ uint32_t wnext(const uint32_t (&w)[4], uint32_t base, const lds_u32* m, uint32_t p,
                                           uint32_t lim) {
-  const uint32_t r = p - base, j = r >> 5;
-  const uint64_t x = (((uint64_t)win_word(w, j + 1) << 32) | win_word(w, j)) >> (r & 31);
-  if (x) return min(p + (uint32_t)__builtin_ctzll(x), lim);
-  if (j < 2) {  // the window's other two words (long targets and values)
-    const uint64_t y = ((uint64_t)win_word(w, j + 3) << 32) | win_word(w, j + 2);
-    if (y) return min(base + 32 * (j + 2) + (uint32_t)__builtin_ctzll(y), lim);
-  }
+  const uint32_t r = p - base;
+  const uint64_t lo = (uint64_t)w[1] << 32 | w[0], hi = (uint64_t)w[3] << 32 | w[2];
+  const bool inlo = r < 64;
+  const uint64_t a = r < 128 ? (inlo ? lo : hi) >> (r & 63) : 0ull;
+  const uint64_t b = inlo ? hi : 0ull;
+  if (a) return min(p + (uint32_t)__builtin_ctzll(a), lim);
+  if (b) return min(base + 64 + (uint32_t)__builtin_ctzll(b), lim);
   // the first bit the window did not cover
-  const uint32_t q = j < 4 ? base + 128 : p;
+  const uint32_t q = r < 128 ? base + 128 : p;
   return q >= lim ? lim : next_set(m, q, lim);
 }
 // the bit at p (p >= base)
