@@ -2017,6 +2017,8 @@ size_t http_raw_dl_grid(const HttpRawDev& R, bool lists, size_t n, int cus) {
     }
     per_cu = it->second;
   }
+  // (CILIUM_GPU_RAW_SCAN_WG: fewer workgroups per CU, for measurements)
+  if (const char* v = getenv("CILIUM_GPU_RAW_SCAN_WG")) per_cu = std::max(1, std::min(per_cu, atoi(v)));
   return grid_for(n, cus, (unsigned)per_cu);
 }
 
