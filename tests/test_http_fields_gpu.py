@@ -122,6 +122,24 @@ def test_gpu_fields_10k_rules(gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_fields_host_entry_many_chunks(gpu, monkeypatch):
+    """The host entry's chunked staging (capi.cc verdicts_raw_from_host: two
+    workers, each its own pinned buffers and stream) at 1 MiB chunks: ~25
+    chunks of one call, every chunk boundary inside the batch, verdicts in
+    request order equal to the host packer path's."""
+    pols, info = synth.http10k_rules()
+    gpu.update_http_policy(pols)
+    rq = synth.http10k_requests(250_000, info, seed=34)
+    lists = _vary(_split(rq["hdr_blob"], rq["hdr_off"]), np.random.default_rng(15), frac=0.1)
+    blob, off = _join(lists)
+    want = _host_path(gpu, *_args(rq), blob, off)
+    monkeypatch.setenv("CILIUM_GPU_HOST_CHUNK_MB", "1")
+    assert np.array_equal(gpu.http_verdicts_fields(*_args(rq), blob, off), want)
+    monkeypatch.delenv("CILIUM_GPU_HOST_CHUNK_MB")
+    assert np.array_equal(gpu.http_verdicts_fields(*_args(rq), blob, off), want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_gpu_fields_all_matcher_forms(gpu, seed):
     from test_cpu_differential import all_matcher_case
