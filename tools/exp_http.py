@@ -201,6 +201,10 @@ VARIANTS.update({
                        ("kernels_http_raw.hip", "constexpr uint32_t kStage = 6144;", "constexpr uint32_t kStage = 5120;"),
                        ("http_raw.cc", "#include", "#include")],
     "rawdl_s5k": _rs(5120),
+    # measuring devices (verdict counters / rows wrong, verdicts still
+    # written): no per-rule hit counting, no remote-identity row lookup
+    "h_nohits": [("  count_hits(T, pg, hit, s_hits, lane);\n", "")],
+    "h_norow": [("const uint32_t row = remote_row(blk, pg, meta.x);", "const uint32_t row = pg.default_remote;")],
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
