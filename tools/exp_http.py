@@ -137,8 +137,8 @@ VARIANTS.update({
                      "  l = threadIdx.x & 63;")],
     # measuring device (verdicts land in order[] in slot order, out[] is not
     # written): raw-mode http_kernel without the verdict scatter
-    "h_noscatter": [("      const uint32_t r = order[slot];\n      if (r != 0xFFFFFFFFu) out[r] = (uint8_t)v;",
-                     "      const uint32_t r = order[slot];\n      if (r != 0xFFFFFFFFu) const_cast<uint32_t*>(order)[slot] = v;")],
+    "h_noscatter": [("      const uint32_t r = order[slot];\n      if (r < nout) {\n        out[r] = (uint8_t)v;",
+                     "      const uint32_t r = order[slot];\n      if (r < nout) {\n        const_cast<uint32_t*>(order)[slot] = v;")],
     # 5 KiB stages with the scan capped at 128 VGPRs (4 waves per SIMD when
     # LDS allows: 40.9 KB per block at config 5)
     "raw_s5k_w4": _rs(5120) + [("kernels_http_raw.hip",
