@@ -205,6 +205,9 @@ VARIANTS.update({
     # written): no per-rule hit counting, no remote-identity row lookup
     "h_nohits": [("  count_hits(T, pg, hit, s_hits, lane);\n", "")],
     "h_norow": [("const uint32_t row = remote_row(blk, pg, meta.x);", "const uint32_t row = pg.default_remote;")],
+    # Kafka verdict kernel: requests per lane per iteration (queue sized with it)
+    "kv_r2": [("kernels.hip", "constexpr uint32_t kKafkaReqs = 4;", "constexpr uint32_t kKafkaReqs = 2;")],
+    "kv_r8": [("kernels.hip", "constexpr uint32_t kKafkaReqs = 4;", "constexpr uint32_t kKafkaReqs = 8;")],
     # chunks per dealt run (program block restaged once per run)
     "h_deal8": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 8;")],
     "h_deal2": [("constexpr uint32_t kDealRun = 4;", "constexpr uint32_t kDealRun = 2;")],
