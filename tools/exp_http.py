@@ -205,6 +205,8 @@ VARIANTS.update({
     # written): no per-rule hit counting, no remote-identity row lookup
     "h_nohits": [("  count_hits(T, pg, hit, s_hits, lane);\n", "")],
     "h_norow": [("const uint32_t row = remote_row(blk, pg, meta.x);", "const uint32_t row = pg.default_remote;")],
+    # verdict bytes stored nontemporal (slot-order batches)
+    "h_ntout": [("      out[slot] = (uint8_t)v;\n", "      __builtin_nontemporal_store((uint8_t)v, out + slot);\n")],
     # Kafka verdict kernel: requests per lane per iteration (queue sized with it)
     "kv_r2": [("kernels.hip", "constexpr uint32_t kKafkaReqs = 4;", "constexpr uint32_t kKafkaReqs = 2;")],
     "kv_r8": [("kernels.hip", "constexpr uint32_t kKafkaReqs = 4;", "constexpr uint32_t kKafkaReqs = 8;")],
