@@ -13,7 +13,7 @@ import oracle
 from cilium_amd import synth
 from test_http_parse import _blob, _raw_requests
 
-pytestmark = [pytest.mark.gpu, pytest.mark.run_last]
+pytestmark = [pytest.mark.gpu]
 
 
 def test_gpu_mixed_entries_from_threads(gpu):
