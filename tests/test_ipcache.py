@@ -5,10 +5,13 @@ Reference: cilium_ipcache (bpf/lib/maps.h:135-159), lookup_ip{4,6}_remote_endpoi
 with sec_label != 0 gives {sec_label, tunnel_endpoint}, else WORLD_ID), map ops
 of pkg/maps/ipcache/ipcache.go:36-130.
 
-The reference has no unit test of this lookup (pkg/maps/ipcache has no
-_test.go); the KAT below is written from the branch structure of those lines
-— parity for it is pinned by that restatement only ("parity unpinned" at
-reference-test level).  The oracle is oracle.cc `or_ipcache` (the
+The reference has no unit test of the LPM lookup itself (pkg/maps/ipcache has
+no _test.go); the KAT below is written from the branch structure of those
+lines.  The agent-side tests of pkg/ipcache (ipcache_test.go TestIPCache,
+TestKeyToIPNet) are replayed at the end of this file as the map ops and
+lookups they imply — they pin host keys, update/delete and prefix parsing
+against the reference's own cases, but no longest-prefix choice between
+overlapping CIDRs (partially pinned).  The oracle is oracle.cc `or_ipcache` (the
 LPM_LOOKUP_FN probe order, eps.h:86-108); the product's tables are checked
 against it on the CPU (host walker of the same tables) and on the GPU.
 """
@@ -311,6 +314,126 @@ def test_gpu_l4_via_ipcache(gpu, n_entries, family):
         k = keys[i]
         e = dump[(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"]))]
         assert (e.Packets, e.Bytes) == (int(pk[i]), int(by[i]))
+
+
+# ------------- replay of the reference's own ipcache tests (pkg/ipcache) ----
+# TestIPCache (pkg/ipcache/ipcache_test.go:37-176) drives the agent-side cache,
+# whose listener turns each effective change into one BPF map op
+# (pkg/datapath/ipcache/listener.go:97-119: Upsert → Map.Update of the host
+# /32 or /128 key, Delete → Map.Delete).  The steps below are that test's
+# sequence reduced to the map ops it produces — calls the agent drops make no
+# op: Delete of an absent IP (ipcache.go:347-350), a Kubernetes-source upsert
+# over a kvstore entry (ipcache.go:233-236, test line 63) and an upsert of the
+# same identity (ipcache.go:240-242, test line 69) — and each LookupByIP /
+# LookupByPrefix assertion becomes an expected datapath resolve / exact-key
+# lookup (test file line in the comment).
+REF_IPCACHE_STEPS = [
+    ("upsert", "10.0.0.15", 68), ("expect", "10.0.0.15", 68),              # :48-59
+    ("delete", "10.0.0.15"), ("expect", "10.0.0.15", None),                # :78-86
+    ("upsert", "10.0.0.15", 68), ("upsert", "10.0.0.15", 69),              # :88-97
+    ("expect", "10.0.0.15", 69),
+    ("delete", "10.0.0.15"),                                               # :110
+    ("upsert", "192.168.0.1", 5), ("expect", "192.168.0.1", 5),            # :117-127
+    ("upsert", "20.3.75.3", 67), ("expect", "20.3.75.3", 67),
+    ("upsert", "27.2.2.2", 29), ("expect", "27.2.2.2", 29),
+    ("upsert", "127.0.0.1", 29), ("expect", "127.0.0.1", 29),
+    ("expect", "127.0.0.1", 29),                                           # 5th upsert: same identity, no op
+    ("delete", "27.2.2.2"), ("expect", "27.2.2.2", None),                  # :137
+    ("expect", "127.0.0.1", 29), ("prefix", "127.0.0.1/32", 29),           # :147-153
+    ("delete", "127.0.0.1"), ("prefix", "127.0.0.1/32", None),             # :155-161
+    ("delete", "192.168.0.1"), ("expect", "192.168.0.1", None),            # :164-171
+    ("delete", "20.3.75.3"), ("expect", "20.3.75.3", None),
+]
+# TestKeyToIPNet (ipcache_test.go:178-243): the kvstore keys' IP part and the
+# net.ParseCIDR result it must equal; host keys are full-length prefixes.
+REF_KEY_NETS = [("f00d::a00:0:0:c164", "f00d::a00:0:0:c164/128", True),
+                ("f00d::a00:0:0:0/64", "f00d::a00:0:0:0/64", False),
+                ("10.0.114.197", "10.0.114.197/32", True),
+                ("10.0.114.0/24", "10.0.114.0/24", False)]
+REF_KEY_BAD = ["10.abfd.114.197", "192.0.2.3/54"]  # ipcache_test.go:231, :238
+
+
+def _host_key(ip: str) -> str:
+    a = ipaddress.ip_address(ip)
+    return f"{ip}/{a.max_prefixlen}"
+
+
+def _addr_arrays(ips):
+    v4 = [ip for ip in ips if ipaddress.ip_address(ip).version == 4]
+    v6 = [ip for ip in ips if ipaddress.ip_address(ip).version == 6]
+    a4 = np.array([int.from_bytes(ipaddress.ip_address(a).packed, "little") for a in v4], np.uint32)
+    a6 = np.array([list(ipaddress.ip_address(a).packed) for a in v6], np.uint8).reshape(-1, 16)
+    return v4, v6, a4, a6
+
+
+def _replay_ref_steps(cl, resolve):
+    ic = cl.ipcache()
+    checked = 0
+    for step in REF_IPCACHE_STEPS:
+        op, ip = step[0], step[1]
+        if op == "upsert":
+            ic.upsert(_host_key(ip), step[2])
+        elif op == "delete":
+            ic.delete([_host_key(ip)])
+        elif op == "prefix":
+            got = ic.lookup(ip)
+            assert (got[0] if got else None) == step[2], step
+            checked += 1
+        else:
+            _, _, a4, a6 = _addr_arrays([ip])
+            g4, g6 = resolve(ic, a4, a6)
+            g = (g4 if len(a4) else g6)[0]
+            assert tuple(g.tolist()) == ((step[2], 0) if step[2] is not None else (WORLD, 0)), step
+            checked += 1
+    assert ic.dump() == []  # the test ends with both caches empty (:173-174)
+    return checked
+
+
+def _key_net_case(cl, resolve):
+    for bad in REF_KEY_BAD:
+        with pytest.raises(ValueError):
+            IPCacheKeys([bad])
+    ic = cl.ipcache()
+    keys = [k for k, _, _ in REF_KEY_NETS]
+    ic.update(keys, [[1000 + i, 0] for i in range(len(keys))])
+    assert sorted(c for c, _, _ in ic.dump()) == sorted(str(ipaddress.ip_network(n, strict=False)) for _, n, _ in REF_KEY_NETS)
+    for i, (k, net, host) in enumerate(REF_KEY_NETS):
+        assert ic.lookup(net) == (1000 + i, 0)
+        nw = ipaddress.ip_network(net, strict=False)  # net.ParseCIDR masks: f00d::a00:0:0:0/64 is f00d::/64
+        assert (nw.prefixlen == nw.max_prefixlen) == host
+    # the host key shadows its /64 or /24; the rest of the prefix resolves to it
+    ips = ["f00d::a00:0:0:c164", "f00d::a00:0:0:c165", "f00d::a00:ffff:ffff:ffff", "f00d::ffff:0:0:0", "f00d:0:0:1::",
+           "10.0.114.197", "10.0.114.196", "10.0.114.255", "10.0.115.197"]
+    want = {"f00d::a00:0:0:c164": 1000, "f00d::a00:0:0:c165": 1001, "f00d::a00:ffff:ffff:ffff": 1001,
+            "f00d::ffff:0:0:0": 1001, "f00d:0:0:1::": WORLD, "10.0.114.197": 1002, "10.0.114.196": 1003, "10.0.114.255": 1003,
+            "10.0.115.197": WORLD}
+    v4, v6, a4, a6 = _addr_arrays(ips)
+    g4, g6 = resolve(ic, a4, a6)
+    got = dict(zip(v4 + v6, [int(x) for x in g4[:, 0]] + [int(x) for x in g6[:, 0]]))
+    assert got == want
+
+
+def IPCacheKeys(keys):
+    from cilium_amd.classifier import IPCache
+    return IPCache._keys(keys)
+
+
+def test_ref_ipcache_replay_host(host):
+    assert _replay_ref_steps(host, lambda ic, a4, a6: ic.eval_host_diag(a4, a6)) == 14
+
+
+def test_ref_key_to_ipnet_host(host):
+    _key_net_case(host, lambda ic, a4, a6: ic.eval_host_diag(a4, a6))
+
+
+@pytest.mark.gpu
+def test_gpu_ref_ipcache_replay(gpu):
+    assert _replay_ref_steps(gpu, lambda ic, a4, a6: ic.resolve(a4, a6)) == 14
+
+
+@pytest.mark.gpu
+def test_gpu_ref_key_to_ipnet(gpu):
+    _key_net_case(gpu, lambda ic, a4, a6: ic.resolve(a4, a6))
 
 
 def test_destroy(host):
