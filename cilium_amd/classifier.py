@@ -456,6 +456,21 @@ class Classifier:
         N.check(N.lib.cg_reset_counters(self.h))
 
 
+class PolicyEntriesDump(list):
+    """policymap.PolicyEntriesDump (policymap.go:92-106): the (PolicyKey,
+    PolicyEntry) pairs DumpToSlice returns, sortable as the reference sorts
+    them — by TrafficDirection, then Identity."""
+
+    def less(self, i: int, j: int) -> bool:
+        a, b = self[i][0], self[j][0]
+        if a.TrafficDirection < b.TrafficDirection:
+            return True
+        return a.TrafficDirection <= b.TrafficDirection and a.Identity < b.Identity
+
+    def sorted(self) -> "PolicyEntriesDump":
+        return PolicyEntriesDump(sorted(self, key=lambda ke: (ke[0].TrafficDirection, ke[0].Identity)))
+
+
 class PolicyMap:
     """pkg/maps/policymap.PolicyMap on the device."""
 
@@ -511,14 +526,15 @@ class PolicyMap:
         key = self._keys([PolicyKey(identity, htons(dport), proto, int(direction))])
         N.check(N.lib.cg_policymap_delete(self.cl.h, self.id, _p(key), 1))
 
-    def dump_to_slice(self) -> list[tuple[PolicyKey, PolicyEntry]]:
+    def dump_to_slice(self) -> PolicyEntriesDump:
         n = C.c_size_t()
         N.check(N.lib.cg_policymap_dump(self.cl.h, self.id, None, None, 0, C.byref(n)))
         keys = np.zeros(max(n.value, 1), POLICY_KEY_DTYPE)
         ents = (N.PolicyEntryC * max(n.value, 1))()
         N.check(N.lib.cg_policymap_dump(self.cl.h, self.id, _p(keys), C.addressof(ents), n.value, C.byref(n)))
-        return [(PolicyKey(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"])),
-                 PolicyEntry(e.proxy_port, e.packets, e.bytes)) for k, e in zip(keys[:n.value], ents[:n.value])]
+        return PolicyEntriesDump(
+            (PolicyKey(int(k["sec_label"]), int(k["dport"]), int(k["protocol"]), int(k["egress"])),
+             PolicyEntry(e.proxy_port, e.packets, e.bytes)) for k, e in zip(keys[:n.value], ents[:n.value]))
 
     def destroy(self) -> None:
         """Free the map's device tables (cg_policymap_destroy)."""

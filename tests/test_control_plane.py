@@ -138,6 +138,31 @@ def test_policymap_control_plane(host):
                       np.zeros(1, np.uint16))
 
 
+def test_policy_entries_dump_less():
+    """policymap_test.go:31-143 TestPolicyEntriesDump_Less, case for case
+    (Ingress = 0, Egress = 1: policymap.go TrafficDirection)."""
+    from cilium_amd.classifier import PolicyEntriesDump, PolicyEntry
+    e = PolicyEntry(0, 0, 0)
+
+    def dump(*keys):
+        return PolicyEntriesDump((PolicyKey(*k), e) for k in keys)
+    cases = [("same element", dump((0, 0, 0, 0)), 0, 0, False),
+             ("identity smaller", dump((0, 0, 0, 0), (1, 0, 0, 0)), 0, 1, True),
+             ("direction smaller", dump((0, 0, 0, 0), (1, 0, 0, 1)), 0, 1, True),
+             ("identity bigger", dump((1, 0, 0, 1), (0, 0, 0, 1)), 0, 1, False)]
+    for name, p, i, j, want in cases:
+        assert p.less(i, j) == want, name
+
+
+def test_policymap_dump_sorted(host):
+    pm = host.policy_map(max_entries=16)
+    for ident, d in [(7, 1), (3, 0), (9, 0), (1, 1), (5, 0)]:
+        pm.allow(ident, 80, 6, d, 0)
+    s = pm.dump_to_slice().sorted()
+    assert [(k.TrafficDirection, k.Identity) for k, _ in s] == [(0, 3), (0, 5), (0, 9), (1, 1), (1, 7)]
+    assert all(not s.less(j, i) for i in range(len(s)) for j in range(i + 1, len(s)))
+
+
 def test_http_policy_image_roundtrip():
     """cg_http_policy_export / _import: the compiled 10K-rule tables moved to
     another handle give identical verdicts (host walk), keep the policy index
