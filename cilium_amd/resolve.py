@@ -728,9 +728,12 @@ class PolicyConfig:
 
 
 def resolve_rule_l4_ingress(r: Rule, to_labels, requirements: tuple, result: L4Policy,
-                            cfg: PolicyConfig = PolicyConfig()) -> Optional[L4Policy]:
+                            cfg: PolicyConfig = PolicyConfig(), from_labels=None) -> Optional[L4Policy]:
     """rule.resolveL4IngressPolicy (rule.go:227-294): None when the rule does
-    not select `to_labels` or contributes no filter; raises PolicyMergeError."""
+    not select `to_labels` or contributes no filter; raises PolicyMergeError.
+    `from_labels` is SearchContext.From: when given, an ingress rule whose
+    source selectors all miss it contributes nothing (mergeL4Ingress,
+    rule.go:152-157)."""
     if not r.EndpointSelector.matches(to_labels):
         return None
     override = []
@@ -744,6 +747,8 @@ def resolve_rule_l4_ingress(r: Rule, to_labels, requirements: tuple, result: L4P
             ing = IngressRule([with_requirements(sel, requirements) for sel in ing.FromEndpoints], ing.FromRequires,
                               ing.FromEntities, ing.ToPorts, ing.FromCIDR)
         peers = ing.source_selectors()
+        if from_labels is not None and ing.ToPorts and peers and not any(p.matches(from_labels) for p in peers):
+            continue
         found += _merge_l4(peers, override, ing.ToPorts, r.Labels, result.Ingress, True)
     return result if found else None
 
@@ -855,10 +860,11 @@ class Repository:
         """AllowsEgressLabelAccess."""
         return bool(self.rules) and self.can_reach_egress(from_labels, to_labels) == "allowed"
 
-    def resolve_l4_ingress_policy(self, to_labels) -> dict:
+    def resolve_l4_ingress_policy(self, to_labels, from_labels=None) -> dict:
         """ResolveL4IngressPolicy (:245-281): FromRequires of every rule
         selecting to_labels constrain every FromEndpoints selector; rules are
-        merged in order; then wildcardL3L4Rules."""
+        merged in order; then wildcardL3L4Rules.  `from_labels`: the search
+        context's From (None for endpoint regeneration, which sets only To)."""
         reqs: tuple = ()
         for r in self.rules:
             if r.EndpointSelector.matches(to_labels):
@@ -867,7 +873,7 @@ class Repository:
                         reqs += requirements_of(sel)
         result = L4Policy()
         for r in self.rules:
-            resolve_rule_l4_ingress(r, to_labels, reqs, result, self.cfg)
+            resolve_rule_l4_ingress(r, to_labels, reqs, result, self.cfg, from_labels)
         self._wildcard_l3l4_rules(to_labels, True, result.Ingress)
         return result.Ingress
 

@@ -608,6 +608,148 @@ def l4_merge_kats() -> dict:
     return {"generator": "tests/golden/make_golden.py l4_merge_kats()", "source": f"{_SRC_MERGE}:40-66", "cases": cases}
 
 
+_SRC_REPO = "pkg/policy/repository_test.go"
+
+
+def repository_kats() -> dict:
+    """Repository-level assertions of pkg/policy/repository_test.go, as data
+    in the l4_merge_kats() schema: TestCanReachIngress / TestCanReachEgress
+    (every AllowsIngressRLocked / AllowsEgressRLocked decision; no DPorts, so
+    the label verdict), TestWildcardL3Rules{Ingress,Egress},
+    TestWildcardL4Rules{Ingress,Egress}, TestWildcardL3RulesIngressFromEntities
+    / EgressToEntities, TestL3DependentL4{Ingress,Egress}FromRequires and
+    TestMinikubeGettingStarted (the full expected L4PolicyMaps, including
+    DerivedFromRules label lists).  Selectors "id=x" parse to source any,
+    key id; rule labels ParseLabel("L3") to "L3"."""
+    sel = lambda v: {"matchLabels": {"id": v}}  # noqa: E731
+    one = lambda k: {"matchLabels": {k: ""}}  # noqa: E731
+    world = {"matchLabels": {"reserved:world": ""}}  # EntitySelectorMapping[world]
+    get = {"method": "GET", "path": "/"}
+    tp = lambda port, rules=None: [{"ports": [{"port": port, "protocol": "TCP"}], **({"rules": rules} if rules else {})}]  # noqa: E731
+    produce = {"kafka": [{"apiKey": "produce"}]}
+
+    def flt(port, eps, parser, l7, derived, ingress=True):
+        d = _flt(port, eps, parser, l7, len(derived), ingress)
+        d["derived_labels"] = derived
+        return d
+    cases = []
+    # TestCanReachIngress (:193-285) / TestCanReachEgress (:287-383)
+    reach_in = [{"endpointSelector": one("bar"), "ingress": [{"fromEndpoints": [one("foo")]}], "labels": ["tag1"]},
+                {"endpointSelector": one("groupA"), "ingress": [{"fromRequires": [one("groupA")]}], "labels": ["tag1"]},
+                {"endpointSelector": one("bar2"), "ingress": [{"fromEndpoints": [one("foo")]}], "labels": ["tag1"]}]
+    reach_eg = [{"endpointSelector": one("foo"), "egress": [{"toEndpoints": [one("bar")]}], "labels": ["tag1"]},
+                {"endpointSelector": one("groupA"), "egress": [{"toRequires": [one("groupA")]}], "labels": ["tag1"]},
+                {"endpointSelector": one("foo"), "egress": [{"toEndpoints": [one("bar2")]}], "labels": ["tag1"]}]
+    L = lambda *ks: {k: "" for k in ks}  # noqa: E731
+    cases.append({"case": "CanReachIngress", "src": f"{_SRC_REPO}:193-285", "kind": "reach", "dir": "ingress",
+                  "empty_repo": [[L("foo"), L("bar"), "undecided", False]], "rules": reach_in,
+                  "asserts": [[L("foo"), L("bar"), True], [L("foo"), L("bar2"), True],
+                              [L("foo", "groupA"), L("bar", "groupA"), True],
+                              [L("foo", "groupB"), L("bar", "groupA"), False],
+                              [L("foo", "groupB"), L("bar", "groupB"), True], [L("foo"), L("bar3"), False]]})
+    cases.append({"case": "CanReachEgress", "src": f"{_SRC_REPO}:287-383", "kind": "reach", "dir": "egress",
+                  "empty_repo": [[L("foo"), L("bar"), "undecided", False]], "rules": reach_eg,
+                  "asserts": [[L("foo"), L("bar"), True], [L("foo"), L("bar2"), True],
+                              [L("foo", "groupA"), L("bar", "groupA"), True],
+                              [L("bar", "groupA"), L("foo", "groupB"), False],
+                              [L("foo", "groupB"), L("bar", "groupB"), True], [L("foo"), L("bar3"), False]]})
+    # TestWildcardL3RulesIngress (:385-542)
+    cases.append({"case": "WildcardL3RulesIngress", "src": f"{_SRC_REPO}:385-542", "level": "repo", "to": {"id": "foo"},
+                  "rules": [{"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar1")]}], "labels": ["L3"]},
+                            {"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar2")], "toPorts": tp("9092", produce)}], "labels": ["kafka"]},
+                            {"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar2")], "toPorts": tp("80", {"http": [get]})}], "labels": ["http"]},
+                            {"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar2")], "toPorts": tp("9090", {"l7proto": "tester", "l7": [get]})}], "labels": ["l7"]}],
+                  "expect": {"9092/TCP": flt(9092, [sel("bar2"), sel("bar1")], "kafka",
+                                             [{"sel": sel("bar2"), "kafka": [{"apiKey": "produce"}]}, {"sel": sel("bar1"), "kafka": [{}]}],
+                                             [["kafka"], ["L3"]]),
+                             "80/TCP": flt(80, [sel("bar2"), sel("bar1")], "http",
+                                           [{"sel": sel("bar2"), "http": [get]}, {"sel": sel("bar1"), "http": [{}]}], [["http"], ["L3"]]),
+                             "9090/TCP": flt(9090, [sel("bar2"), sel("bar1")], "tester",
+                                             [{"sel": sel("bar2"), "l7proto": "tester", "l7": [get]},
+                                              {"sel": sel("bar1"), "l7proto": "tester", "l7": []}], [["l7"], ["L3"]])}})
+    # TestWildcardL4RulesIngress (:544-683)
+    cases.append({"case": "WildcardL4RulesIngress", "src": f"{_SRC_REPO}:544-683", "level": "repo", "to": {"id": "foo"},
+                  "rules": [{"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar1")], "toPorts": tp("9092")}], "labels": ["L4"]},
+                            {"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar2")], "toPorts": tp("9092", produce)}], "labels": ["kafka"]},
+                            {"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar1")], "toPorts": tp("80")}], "labels": ["L4"]},
+                            {"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar2")], "toPorts": tp("80", {"http": [get]})}], "labels": ["http"]}],
+                  "expect": {"80/TCP": flt(80, [sel("bar1"), sel("bar2"), sel("bar1")], "http",
+                                           [{"sel": sel("bar1"), "http": [{}]}, {"sel": sel("bar2"), "http": [get]}],
+                                           [["L4"], ["http"], ["L4"]]),
+                             "9092/TCP": flt(9092, [sel("bar1"), sel("bar2"), sel("bar1")], "kafka",
+                                             [{"sel": sel("bar1"), "kafka": [{}]}, {"sel": sel("bar2"), "kafka": [{"apiKey": "produce"}]}],
+                                             [["L4"], ["kafka"], ["L4"]])}})
+    # TestL3DependentL4IngressFromRequires (:685-746) / Egress (:748-808)
+    req_sel = {"matchLabels": {"id": "bar1"}, "matchExpressions": [{"key": "id", "operator": "In", "values": ["bar2"]}]}
+    cases.append({"case": "L3DependentL4IngressFromRequires", "src": f"{_SRC_REPO}:685-746", "level": "repo", "to": {"id": "foo"},
+                  "rules": [{"endpointSelector": sel("foo"), "ingress": [{"fromEndpoints": [sel("bar1")], "toPorts": tp("80")},
+                                                                           {"fromRequires": [sel("bar2")]}]}],
+                  "expect": {"80/TCP": flt(80, [req_sel], "", [], [[]])}})
+    cases.append({"case": "L3DependentL4EgressFromRequires", "src": f"{_SRC_REPO}:748-808", "level": "repo", "dir": "egress",
+                  "from": {"id": "foo"},
+                  "rules": [{"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar1")], "toPorts": tp("80")},
+                                                                          {"toRequires": [sel("bar2")]}]}],
+                  "expect": {"80/TCP": flt(80, [req_sel], "", [], [[]], ingress=False)}})
+    # TestWildcardL3RulesEgress (:810-926) / TestWildcardL4RulesEgress (:928-1067)
+    cases.append({"case": "WildcardL3RulesEgress", "src": f"{_SRC_REPO}:810-926", "level": "repo", "dir": "egress",
+                  "from": {"id": "foo"},
+                  "rules": [{"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar1")]}], "labels": ["L4"]},
+                            {"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar2")], "toPorts": tp("9092", produce)}], "labels": ["kafka"]},
+                            {"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar2")], "toPorts": tp("80", {"http": [get]})}], "labels": ["http"]}],
+                  "expect": {"9092/TCP": flt(9092, [sel("bar2"), sel("bar1")], "kafka",
+                                             [{"sel": sel("bar1"), "kafka": [{}]}, {"sel": sel("bar2"), "kafka": [{"apiKey": "produce"}]}],
+                                             [["kafka"], ["L4"]], ingress=False),
+                             "80/TCP": flt(80, [sel("bar2"), sel("bar1")], "http",
+                                           [{"sel": sel("bar1"), "http": [{}]}, {"sel": sel("bar2"), "http": [get]}],
+                                           [["http"], ["L4"]], ingress=False)}})
+    cases.append({"case": "WildcardL4RulesEgress", "src": f"{_SRC_REPO}:928-1067", "level": "repo", "dir": "egress",
+                  "from": {"id": "foo"},
+                  "rules": [{"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar1")], "toPorts": tp("9092")}], "labels": ["L3"]},
+                            {"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar2")], "toPorts": tp("9092", produce)}], "labels": ["kafka"]},
+                            {"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar1")], "toPorts": tp("80")}], "labels": ["L3"]},
+                            {"endpointSelector": sel("foo"), "egress": [{"toEndpoints": [sel("bar2")], "toPorts": tp("80", {"http": [get]})}], "labels": ["http"]}],
+                  "expect": {"80/TCP": flt(80, [sel("bar1"), sel("bar2"), sel("bar1")], "http",
+                                           [{"sel": sel("bar1"), "http": [{}]}, {"sel": sel("bar2"), "http": [get]}],
+                                           [["L3"], ["http"], ["L3"]], ingress=False),
+                             "9092/TCP": flt(9092, [sel("bar1"), sel("bar2"), sel("bar1")], "kafka",
+                                             [{"sel": sel("bar1"), "kafka": [{}]}, {"sel": sel("bar2"), "kafka": [{"apiKey": "produce"}]}],
+                                             [["L3"], ["kafka"], ["L3"]], ingress=False)}})
+    # TestWildcardL3RulesIngressFromEntities (:1069-1189) / EgressToEntities (:1191-1311)
+    for name, src, d, peer, ent in (("WildcardL3RulesIngressFromEntities", "1069-1189", "ingress", "fromEndpoints", "fromEntities"),
+                                    ("WildcardL3RulesEgressToEntities", "1191-1311", "egress", "toEndpoints", "toEntities")):
+        c = {"case": name, "src": f"{_SRC_REPO}:{src}", "level": "repo",
+             "rules": [{"endpointSelector": sel("foo"), d: [{ent: ["world"]}], "labels": ["L3"]},
+                       {"endpointSelector": sel("foo"), d: [{peer: [sel("bar2")], "toPorts": tp("9092", produce)}], "labels": ["kafka"]},
+                       {"endpointSelector": sel("foo"), d: [{peer: [sel("bar2")], "toPorts": tp("80", {"http": [get]})}], "labels": ["http"]}],
+             "expect": {"9092/TCP": flt(9092, [sel("bar2"), world], "kafka",
+                                        [{"sel": world, "kafka": [{}]}, {"sel": sel("bar2"), "kafka": [{"apiKey": "produce"}]}],
+                                        [["kafka"], ["L3"]], ingress=d == "ingress"),
+                        "80/TCP": flt(80, [sel("bar2"), world], "http",
+                                      [{"sel": world, "http": [{}]}, {"sel": sel("bar2"), "http": [get]}],
+                                      [["http"], ["L3"]], ingress=d == "ingress")}}
+        if d == "ingress":
+            c["to"] = {"id": "foo"}
+        else:
+            c["dir"], c["from"] = "egress", {"id": "foo"}
+        cases.append(c)
+    # TestMinikubeGettingStarted (:1313-1453): from app2 the merged filter,
+    # from app3 nothing (mergeL4Ingress's ctx.From check, rule.go:152-157)
+    mk_rules = [{"endpointSelector": sel("app1"), "ingress": [{"fromEndpoints": [sel("app2")], "toPorts": tp("80")}]},
+                {"endpointSelector": sel("app1"), "ingress": [{"fromEndpoints": [sel("app2")], "toPorts": tp("80", {"http": [get]})}]},
+                {"endpointSelector": sel("app1"), "ingress": [{"fromEndpoints": [sel("app2")], "toPorts": tp("80", {"http": [get]})}]}]
+    cases.append({"case": "MinikubeGettingStarted", "src": f"{_SRC_REPO}:1313-1453", "level": "repo",
+                  "to": {"id": "app1"}, "ctx_from": {"id": "app2"}, "rules": mk_rules,
+                  "empty_repo": [[{"id": "app2"}, {"id": "app1"}, "undecided", False],
+                                 [{"id": "app3"}, {"id": "app1"}, "undecided", False]],
+                  "expect": {"80/TCP": flt(80, [sel("app2")] * 4, "http", [{"sel": sel("app2"), "http": [{}]}],
+                                           [[], [], [], []])},
+                  "l7_outcome": {"note": "app2 passes every request (L7 wildcard from the L4-only rule); app3 has no "
+                                         "filter", "allow": {"app2": [1, 1], "app3": [0, 0]}}})
+    cases.append({"case": "MinikubeGettingStarted/app3", "src": f"{_SRC_REPO}:1446-1452", "level": "repo",
+                  "to": {"id": "app1"}, "ctx_from": {"id": "app3"}, "rules": mk_rules, "expect": {}})
+    return {"generator": "tests/golden/make_golden.py repository_kats()", "source": _SRC_REPO, "cases": cases}
+
+
 def _manifest(name: str) -> list:
     with open(os.path.join(REF, "test/runtime/manifests", name)) as f:
         return json.load(f)
@@ -707,6 +849,7 @@ def main():
              "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
              "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
+             "repository_kat.json": repository_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():

@@ -1,0 +1,147 @@
+"""Repository resolution pinned to
+pkg/policy/repository_test.go (tests/golden/repository_kat.json, written by
+make_golden.py repository_kats()):
+
+- TestCanReachIngress / TestCanReachEgress: every label decision;
+- TestWildcardL3Rules*, TestWildcardL4Rules*, the FromEntities / ToEntities
+  variants, TestL3DependentL4*FromRequires and TestMinikubeGettingStarted:
+  the whole expected L4PolicyMap (ports, selectors in order, parser, L7 rules
+  per selector, DerivedFromRules label lists);
+- TestMinikubeGettingStarted carried on through NPDS → http_kernel and the
+  endpoint's policy map → l4_fp_kernel (host walk on the CPU, the kernels on
+  the GPU).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from cilium_amd import _native as N
+from cilium_amd import resolve as R
+from cilium_amd.classifier import L4_TUPLE_DTYPE, POLICY_KEY_DTYPE
+from cilium_amd.policy import L7Rules, PortRuleHTTP, PortRuleKafka, htons
+from kat_util import load
+
+KAT = load("repository_kat.json")
+PROXY_PORT = 15001
+
+
+def _rules(case):
+    return [R.Rule.from_json(r) for r in case["rules"]]
+
+
+def _l7(entry) -> L7Rules:
+    http = [PortRuleHTTP(Path=h.get("path", ""), Method=h.get("method", "")) for h in entry["http"]] \
+        if "http" in entry else None
+    kafka = [PortRuleKafka(APIKey=k.get("apiKey", ""), Topic=k.get("topic", "")) for k in entry["kafka"]] \
+        if "kafka" in entry else None
+    if "l7proto" in entry:
+        return L7Rules(L7Proto=entry["l7proto"], L7=list(entry["l7"]))
+    return L7Rules(HTTP=http, Kafka=kafka)
+
+
+# the unit tests run with option.Config's zero value: AllowLocalhost is not
+# "always", so no host override selector is added (rule.go:166-172)
+CFG = R.PolicyConfig(always_allow_localhost=False)
+
+
+def _resolve(case):
+    repo = R.Repository(_rules(case), CFG)
+    if case.get("dir") == "egress":
+        return repo.resolve_l4_egress_policy(case["from"])
+    return repo.resolve_l4_ingress_policy(case["to"], case.get("ctx_from"))
+
+
+RESOLVE = [c for c in KAT["cases"] if c.get("level") == "repo"]
+REACH = [c for c in KAT["cases"] if c.get("kind") == "reach"]
+
+
+@pytest.mark.parametrize("case", RESOLVE, ids=lambda c: c["case"])
+def test_repository_resolution(case):
+    got = _resolve(case)
+    assert set(got) == set(case["expect"])
+    for key, want in case["expect"].items():
+        f = got[key]
+        assert (f.Port, f.Protocol, f.U8Proto, f.Ingress) == (want["port"], want["protocol"], want["u8proto"],
+                                                             want["ingress"])
+        assert f.Endpoints == [R.selector_from_json(s) for s in want["endpoints"]]
+        assert f.L7Parser == want["parser"]
+        assert dict(f.L7RulesPerEp) == {R.selector_from_json(e["sel"]): _l7(e) for e in want["l7"]}
+        assert [tuple(x) for x in f.DerivedFromRules] == [tuple(sorted(d)) for d in want["derived_labels"]]
+
+
+@pytest.mark.parametrize("case", REACH + [c for c in RESOLVE if "empty_repo" in c], ids=lambda c: c["case"])
+def test_repository_reach(case):
+    empty = R.Repository()
+    for frm, to, decision, allowed in case.get("empty_repo", []):
+        assert empty.can_reach_ingress(frm, to) == decision
+        assert empty.allows_ingress_label_access(frm, to) == allowed
+    if case.get("kind") != "reach":
+        return
+    repo = R.Repository(_rules(case))
+    for frm, to, allowed in case["asserts"]:
+        if case["dir"] == "ingress":
+            assert repo.allows_ingress_label_access(frm, to) == allowed, (frm, to)
+        else:
+            assert repo.allows_egress_label_access(frm, to) == allowed, (frm, to)
+
+
+# ----------------------------------- TestMinikubeGettingStarted → kernels ----
+MK = next(c for c in KAT["cases"] if c["case"] == "MinikubeGettingStarted")
+MK_IDS = {"app1": 300, "app2": 301, "app3": 302}
+MK_CACHE = {i: {"id": n} for n, i in MK_IDS.items()}
+
+
+def _mk_chain():
+    """Endpoint app1's NPDS and policy map (port 80 redirected to the proxy);
+    GET / and POST / from app2 and app3."""
+    repo = R.Repository(_rules(MK), CFG)
+    l4map = repo.resolve_l4_ingress_policy(MK["to"])
+    npds = R.get_network_policy("ep-app1", MK_IDS["app1"], R.L4Policy(Ingress=l4map), True, False, MK_CACHE)
+    state = R.endpoint_policy_map_state(repo, MK["to"], MK_CACHE, {(True, "TCP", 80): PROXY_PORT})
+    srcs = list(MK["l7_outcome"]["allow"])
+    blob, off, remote = b"", [0], []
+    for s in srcs:
+        for m in ("GET", "POST"):
+            blob += b":method\0" + m.encode() + b"\0:path\0/\0"
+            off.append(len(blob))
+            remote.append(MK_IDS[s])
+    n = len(remote)
+    rq = dict(policy=np.zeros(n, np.uint32), ingress=np.ones(n, np.uint8), port=np.full(n, 80, np.uint16),
+              remote=np.array(remote, np.uint32), hdr_blob=np.frombuffer(blob, np.uint8).copy(),
+              hdr_off=np.array(off, np.uint64))
+    want = np.array([a for s in srcs for a in MK["l7_outcome"]["allow"][s]], np.uint8)
+    keys = np.zeros(len(state), POLICY_KEY_DTYPE)
+    ports = np.zeros(len(state), np.uint16)
+    for i, (k, p) in enumerate(state.items()):
+        keys[i] = (k.Identity, htons(k.DestPort), k.Nexthdr, k.TrafficDirection)
+        ports[i] = htons(p)
+    t = np.zeros(len(srcs), L4_TUPLE_DTYPE)
+    t["identity"] = [MK_IDS[s] for s in srcs]
+    t["dport"] = htons(80)
+    t["proto"] = 6
+    t["flags"] = N.CG_L4_F_INGRESS
+    t["len"] = 100
+    exp_l4 = np.array([htons(PROXY_PORT) if any(MK["l7_outcome"]["allow"][s]) else -133 for s in srcs], np.int32)
+    assert np.array_equal(oracle.HttpOracle([npds]).eval(**rq), want)
+    assert np.array_equal(oracle.l4(keys, ports, t)[0], exp_l4)
+    return npds, rq, want, keys, ports, t, exp_l4
+
+
+def test_minikube_chain_host(host):
+    npds, rq, want, keys, ports, t, exp_l4 = _mk_chain()
+    host.update_http_policy([npds])
+    assert np.array_equal(host.http_eval_host_diag(host.pack_http(**rq)), want)
+    pm = host.policy_map()
+    pm.allow_keys(keys, ports)
+    assert np.array_equal(pm.eval_host_diag(t), exp_l4)
+
+
+@pytest.mark.gpu
+def test_gpu_minikube_chain(gpu):
+    npds, rq, want, keys, ports, t, exp_l4 = _mk_chain()
+    gpu.update_http_policy([npds])
+    assert np.array_equal(gpu.http_verdicts(gpu.pack_http(**rq)), want)
+    pm = gpu.policy_map()
+    pm.allow_keys(keys, ports)
+    assert np.array_equal(pm.verdicts(t), exp_l4)
+    pm.destroy()
