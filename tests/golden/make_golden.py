@@ -747,6 +747,69 @@ def repository_kats() -> dict:
                                          "filter", "allow": {"app2": [1, 1], "app3": [0, 0]}}})
     cases.append({"case": "MinikubeGettingStarted/app3", "src": f"{_SRC_REPO}:1446-1452", "level": "repo",
                   "to": {"id": "app1"}, "ctx_from": {"id": "app3"}, "rules": mk_rules, "expect": {}})
+    # rule-level resolution, pkg/policy/rule_test.go (rule.resolveL4IngressPolicy
+    # / resolveL4EgressPolicy on a fresh L4Policy; "rules" of more than one are
+    # resolved in turn into the same result; "expect": null is a nil result)
+    src = "pkg/policy/rule_test.go"
+    wc = {}
+    tp2 = lambda ports, rules=None: [{"ports": [{"port": p_, "protocol": pr} for p_, pr in ports],  # noqa: E731
+                                      **({"rules": rules} if rules else {})}]
+    http_get = {"http": [get]}
+    kfoo, kbar = {"kafka": [{"topic": "foo"}]}, {"kafka": [{"topic": "bar"}]}
+    l4p_in = [{"toPorts": tp2([("80", "TCP"), ("8080", "TCP")], http_get)}]
+    l4p_eg = [{"toPorts": tp2([("3000", "ANY")])}]
+    eg3000 = {"3000/TCP": flt(3000, [wc], "", [], [[]], ingress=False),
+              "3000/UDP": dict(flt(3000, [wc], "", [], [[]], ingress=False), protocol="UDP", u8proto=17)}
+    rl = lambda d, rules: {"endpointSelector": one("bar"), d: rules}  # noqa: E731
+    rcase = lambda name, lines, d, rules, expect, at="bar", **kw: dict(  # noqa: E731
+        {"case": name, "src": f"{src}:{lines}", "level": "rule", "dir": d,
+         ("to" if d == "ingress" else "from"): L(at), "rules": rules, "expect": expect}, **kw)
+    cases += [
+        rcase("L4Policy/rule1/ingress", "117-202", "ingress", [rl("ingress", l4p_in)],
+              {"80/TCP": flt(80, [wc], "http", [{"sel": wc, "http": [get]}], [[]]),
+               "8080/TCP": flt(8080, [wc], "http", [{"sel": wc, "http": [get]}], [[]])}),
+        rcase("L4Policy/rule1/egress", "117-202", "egress", [rl("egress", l4p_eg)], eg3000),
+        rcase("L4Policy/rule1/not-selected-in", "204-218", "ingress", [rl("ingress", l4p_in)], None, at="foo"),
+        rcase("L4Policy/rule1/not-selected-eg", "204-218", "egress", [rl("egress", l4p_eg)], None, at="foo"),
+        rcase("L4Policy/rule2/ingress", "220-304", "ingress",
+              [rl("ingress", [{"toPorts": tp2([("80", "TCP")])}, {"toPorts": tp2([("80", "TCP")], http_get)}])],
+              {"80/TCP": flt(80, [wc], "http", [{"sel": wc, "http": [get]}], [[], []])}),
+        rcase("L4Policy/rule2/egress", "220-304", "egress", [rl("egress", l4p_eg)], eg3000),
+        rcase("MergeL4PolicyIngress", "324-369", "ingress",
+              [rl("ingress", [{"fromEndpoints": [one("foo")], "toPorts": tp2([("80", "TCP")])},
+                              {"fromEndpoints": [one("baz")], "toPorts": tp2([("80", "TCP")])}])],
+              {"80/TCP": flt(80, [one("foo"), one("baz")], "", [], [[], []])}),
+        rcase("MergeL4PolicyEgress", "371-423", "egress",
+              [rl("egress", [{"toEndpoints": [one("foo")], "toPorts": tp2([("80", "TCP")])},
+                             {"toEndpoints": [one("baz")], "toPorts": tp2([("80", "TCP")])}])],
+              {"80/TCP": flt(80, [one("foo"), one("baz")], "", [], [[], []], ingress=False)}),
+    ]
+    for d, peer, lines in (("ingress", "fromEndpoints", ("425-506", "508-569", "571-579", "581-645")),
+                           ("egress", "toEndpoints", ("647-724", "726-795", "797-800", "802-863"))):
+        ing = d == "ingress"
+        r1 = rl(d, [{"toPorts": tp2([("80", "TCP")])}, {"toPorts": tp2([("80", "TCP")], http_get)},
+                    {peer: [one("foo")], "toPorts": tp2([("80", "TCP")], http_get)}])
+        r2 = rl(d, ([] if ing else [{"toPorts": tp2([("80", "TCP")])}]) +
+                [{"toPorts": tp2([("80", "TCP")], kfoo)}, {peer: [one("foo")], "toPorts": tp2([("80", "TCP")], kfoo)}])
+        r3 = rl(d, [{peer: [one("foo")], "toPorts": tp2([("80", "TCP")], kfoo)},
+                    dict({"toPorts": tp2([("80", "TCP")], kbar)}, **({peer: [wc]} if ing else {}))])
+        name = "MergeL7Policy" + ("Ingress" if ing else "Egress")
+        cases += [
+            rcase(f"{name}/rule1", lines[0], d, [r1],
+                  {"80/TCP": flt(80, [wc], "http", [{"sel": wc, "http": [get]}, {"sel": one("foo"), "http": [get]}],
+                                 [[], [], []], ingress=ing)}),
+            rcase(f"{name}/rule1/not-selected", lines[0], d, [r1], None, at="foo"),
+            rcase(f"{name}/rule2", lines[1], d, [r2],
+                  {"80/TCP": flt(80, [wc], "kafka", [{"sel": wc, "kafka": [{"topic": "foo"}]},
+                                                     {"sel": one("foo"), "kafka": [{"topic": "foo"}]}],
+                                 [[], []] if ing else [[], [], []], ingress=ing)}),
+            rcase(f"{name}/rule2/not-selected", lines[1], d, [r2], None, at="foo"),
+            rcase(f"{name}/rule3", lines[3], d, [r3],
+                  {"80/TCP": flt(80, [wc], "kafka", [{"sel": one("foo"), "kafka": [{"topic": "foo"}]},
+                                                     {"sel": wc, "kafka": [{"topic": "bar"}]}], [[], []], ingress=ing)}),
+        ]
+        if ing:  # rule1's result, then rule2 into it: conflicting parsers (:571-579)
+            cases.append(rcase(f"{name}/rule1+rule2", lines[2], d, [r1, r2], None, error=True))
     return {"generator": "tests/golden/make_golden.py repository_kats()", "source": _SRC_REPO, "cases": cases}
 
 

@@ -3,6 +3,9 @@ pkg/policy/repository_test.go (tests/golden/repository_kat.json, written by
 make_golden.py repository_kats()):
 
 - TestCanReachIngress / TestCanReachEgress: every label decision;
+- pkg/policy/rule_test.go TestL4Policy, TestMergeL4Policy{Ingress,Egress},
+  TestMergeL7Policy{Ingress,Egress}: rule-level results (nil, error or the
+  whole expected map);
 - TestWildcardL3Rules*, TestWildcardL4Rules*, the FromEntities / ToEntities
   variants, TestL3DependentL4*FromRequires and TestMinikubeGettingStarted:
   the whole expected L4PolicyMap (ports, selectors in order, parser, L7 rules
@@ -45,19 +48,36 @@ CFG = R.PolicyConfig(always_allow_localhost=False)
 
 
 def _resolve(case):
+    egress = case.get("dir") == "egress"
+    if case["level"] == "rule":  # rule.resolveL4{In,E}gressPolicy into one result, in turn
+        res, found = R.L4Policy(), None
+        for r in _rules(case):
+            r.sanitize()
+            found = (R.resolve_rule_l4_egress(r, case["from"], (), res) if egress else
+                     R.resolve_rule_l4_ingress(r, case["to"], (), res, CFG))
+        if found is None:
+            return None
+        return found.Egress if egress else found.Ingress
     repo = R.Repository(_rules(case), CFG)
-    if case.get("dir") == "egress":
+    if egress:
         return repo.resolve_l4_egress_policy(case["from"])
     return repo.resolve_l4_ingress_policy(case["to"], case.get("ctx_from"))
 
 
-RESOLVE = [c for c in KAT["cases"] if c.get("level") == "repo"]
+RESOLVE = [c for c in KAT["cases"] if c.get("level") in ("repo", "rule")]
 REACH = [c for c in KAT["cases"] if c.get("kind") == "reach"]
 
 
 @pytest.mark.parametrize("case", RESOLVE, ids=lambda c: c["case"])
 def test_repository_resolution(case):
+    if case.get("error"):
+        with pytest.raises(R.PolicyMergeError):
+            _resolve(case)
+        return
     got = _resolve(case)
+    if case["expect"] is None:
+        assert got is None
+        return
     assert set(got) == set(case["expect"])
     for key, want in case["expect"].items():
         f = got[key]
