@@ -144,6 +144,17 @@ class PortRuleKafka:
                 "clientID": self.ClientID, "topic": self.Topic}
 
 
+def go_fields(d: Optional[dict]) -> dict:
+    """A JSON object's members as encoding/json matches them to struct
+    fields: a key names the field whose tag it equals under case folding
+    (json.Unmarshal; the reference's policy files write "HTTP" for the `http`
+    tag, test/runtime/manifests/Policies-l7-simple.json:14), and of several
+    keys naming one field the last decoded wins.  Keys are returned
+    lower-cased; callers look up lower-case tags.  Label maps (matchLabels)
+    are data, not fields, and are not passed through this."""
+    return {k.lower(): v for k, v in (d or {}).items()}
+
+
 @dataclass
 class L7Rules:
     """api.L7Rules (pkg/policy/api/l4.go:65-85).  None stands for Go's nil
@@ -164,15 +175,17 @@ class L7Rules:
     @staticmethod
     def from_json(d: Optional[dict]) -> Optional["L7Rules"]:
         """The `rules` member of an api.PortRule (JSON tags http, kafka,
-        l7proto, l7)."""
+        l7proto, l7; field names matched as encoding/json does: go_fields)."""
         if d is None:
             return None
+        d = go_fields(d)
         http = [PortRuleHTTP(Path=h.get("path", ""), Method=h.get("method", ""), Host=h.get("host", ""),
-                             Headers=list(h.get("headers") or [])) for h in d["http"]] if "http" in d else None
-        kafka = [PortRuleKafka(Role=k.get("role", ""), APIKey=k.get("apiKey", ""), APIVersion=k.get("apiVersion", ""),
-                               ClientID=k.get("clientID", ""), Topic=k.get("topic", ""))
-                 for k in d["kafka"]] if "kafka" in d else None
-        l7 = [dict(x) for x in d["l7"]] if "l7" in d else None
+                             Headers=list(h.get("headers") or [])) for h in map(go_fields, d["http"])] \
+            if d.get("http") is not None else None
+        kafka = [PortRuleKafka(Role=k.get("role", ""), APIKey=k.get("apikey", ""), APIVersion=k.get("apiversion", ""),
+                               ClientID=k.get("clientid", ""), Topic=k.get("topic", ""))
+                 for k in map(go_fields, d["kafka"])] if d.get("kafka") is not None else None
+        l7 = [dict(x) for x in d["l7"]] if d.get("l7") is not None else None
         return L7Rules(HTTP=http, Kafka=kafka, L7Proto=d.get("l7proto", ""), L7=l7)
 
 

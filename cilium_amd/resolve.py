@@ -38,8 +38,8 @@ import functools
 from dataclasses import dataclass, field
 from typing import Iterable, Mapping, Optional
 
-from .policy import (L7Rules, PolicyKey, PortRuleHTTP, PortRuleKafka, TrafficDirection, get_http_rule, htons,
-                     port_network_policy_rule)
+from .policy import (L7Rules, PolicyKey, PortRuleHTTP, PortRuleKafka, TrafficDirection, get_http_rule, go_fields,
+                     htons, port_network_policy_rule)
 
 # pkg/identity/numericidentity.go:27-75
 RESERVED_UNKNOWN, RESERVED_HOST, RESERVED_WORLD, RESERVED_UNMANAGED, RESERVED_HEALTH, RESERVED_INIT = 0, 1, 2, 3, 4, 5
@@ -465,9 +465,10 @@ _ENTITY_SELECTORS = {
 
 def selector_from_json(d: Optional[dict]) -> EndpointSelector:
     """api.EndpointSelector from its JSON (a k8s LabelSelector)."""
-    d = d or {}
-    me = [(e["key"], e["operator"], tuple(e.get("values") or ())) for e in d.get("matchExpressions") or []]
-    return EndpointSelector.of(d.get("matchLabels") or {}, me)
+    d = go_fields(d)
+    me = [(e["key"], e["operator"], tuple(e.get("values") or ()))
+          for e in map(go_fields, d.get("matchexpressions") or [])]
+    return EndpointSelector.of(d.get("matchlabels") or {}, me)
 
 
 def requirements_of(sel: EndpointSelector) -> tuple:
@@ -588,23 +589,25 @@ class Rule:
         """A rule of a policy file (`cilium policy import` JSON)."""
         def ports(lst):
             out = []
-            for pr in lst or []:
-                pps = [PortProtocol(str(p.get("port", "")), p.get("protocol", "")) for p in pr.get("ports") or []]
+            for pr in map(go_fields, lst or []):
+                pps = [PortProtocol(str(p.get("port", "")), p.get("protocol", ""))
+                       for p in map(go_fields, pr.get("ports") or [])]
                 out.append(PortRule(pps, L7Rules.from_json(pr.get("rules"))))
             return out
-        ing = [IngressRule([selector_from_json(x) for x in r.get("fromEndpoints") or []],
-                           [selector_from_json(x) for x in r.get("fromRequires") or []],
-                           list(r.get("fromEntities") or []), ports(r.get("toPorts")),
-                           list(r.get("fromCIDR") or []) + list(r.get("fromCIDRSet") or []))
-               for r in d.get("ingress") or []]
-        eg = [EgressRule([selector_from_json(x) for x in r.get("toEndpoints") or []],
-                         [selector_from_json(x) for x in r.get("toRequires") or []],
-                         list(r.get("toEntities") or []), ports(r.get("toPorts")),
-                         list(r.get("toCIDR") or []) + list(r.get("toCIDRSet") or []) +
-                         list(r.get("toServices") or []))
-              for r in d.get("egress") or []]
+        d = go_fields(d)  # json.Unmarshal's field matching (policy.go_fields)
+        ing = [IngressRule([selector_from_json(x) for x in r.get("fromendpoints") or []],
+                           [selector_from_json(x) for x in r.get("fromrequires") or []],
+                           list(r.get("fromentities") or []), ports(r.get("toports")),
+                           list(r.get("fromcidr") or []) + list(r.get("fromcidrset") or []))
+               for r in map(go_fields, d.get("ingress") or [])]
+        eg = [EgressRule([selector_from_json(x) for x in r.get("toendpoints") or []],
+                         [selector_from_json(x) for x in r.get("torequires") or []],
+                         list(r.get("toentities") or []), ports(r.get("toports")),
+                         list(r.get("tocidr") or []) + list(r.get("tocidrset") or []) +
+                         list(r.get("toservices") or []))
+              for r in map(go_fields, d.get("egress") or [])]
         labels = tuple(sorted(str(x) for x in d.get("labels") or []))
-        return Rule(selector_from_json(d.get("endpointSelector")), ing, eg, labels)
+        return Rule(selector_from_json(d.get("endpointselector")), ing, eg, labels)
 
     def sanitize(self) -> None:
         """Rule.Sanitize (rule_validation.go:37-69, :316-358): every port

@@ -856,6 +856,36 @@ def policies_e2e_kats() -> dict:
 
 
 
+def policies_l7_kats() -> dict:
+    """test/runtime/Policies.go:495-560 ("L7 Checks"): the two L7 policy files
+    it imports (Policies-l7-simple.json, Policies-l7-multiple.json, copied as
+    data) and every connectivity assertion.  `public` / `private` are curl
+    GETs of http://server:80/public and /private (Policies.go:326-347; the
+    IPv6 twins assert the same and are folded in), `all` adds ping
+    (allRequests, :295-299).  The runtime daemon runs with allow-localhost
+    "auto", which is "policy" outside Kubernetes (daemon.go:1144-1147,
+    config.go:298-309): the host is subject to the rules."""
+    simple = [("app1", "httpd1", "public", True), ("app1", "httpd1", "private", False),
+              ("host", "httpd1", "public", True), ("host", "httpd1", "private", False),
+              ("app2", "httpd1", "public", False),
+              ("app2", "httpd2", "public", True), ("app2", "httpd2", "private", False)]
+    multiple = [("app1", "httpd1", "public", True), ("app1", "httpd1", "private", False),
+                ("app2", "httpd1", "public", False),
+                ("app2", "httpd2", "public", True), ("app2", "httpd2", "private", False)]
+    none = [("app1", "httpd1", "all", True), ("app2", "httpd1", "all", True)]
+    return {"generator": "tests/golden/make_golden.py policies_l7_kats()",
+            "containers": ["app1", "app2", "app3", "httpd1", "httpd2", "httpd3"],
+            "allow_localhost": False,
+            "suites": [
+                {"name": "L7 simple", "src": "test/runtime/Policies.go:495-521",
+                 "policy": _manifest("Policies-l7-simple.json"), "asserts": simple},
+                {"name": "L7 deleted", "src": "test/runtime/Policies.go:523-531", "policy": [], "asserts": none},
+                {"name": "L7 multiple", "src": "test/runtime/Policies.go:533-550",
+                 "policy": _manifest("Policies-l7-multiple.json"), "asserts": multiple},
+                {"name": "L7 multiple deleted", "src": "test/runtime/Policies.go:552-559", "policy": [],
+                 "asserts": none},
+            ]}
+
 # ---------------------------------------------------------- Go regexp KATs --
 def go_regex_kats() -> dict:
     """Go 1.10 regexp (RE2 syntax, Perl flags) known answers for the proxylib
@@ -912,7 +942,7 @@ def main():
              "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
              "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
-             "repository_kat.json": repository_kats(),
+             "repository_kat.json": repository_kats(), "policies_l7_kat.json": policies_l7_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():

@@ -217,7 +217,9 @@ def _e2e_cases(suite):
 
 def _e2e_maps(suite):
     ids, cache = _e2e_world()
-    repo = R.Repository([R.Rule.from_json(r) for r in suite["policy"]], R.PolicyConfig(always_allow_localhost=True))
+    # the runtime daemon's allow-localhost "auto" is "policy" outside
+    # Kubernetes (daemon.go:1144-1147, option/config.go:298-309)
+    repo = R.Repository([R.Rule.from_json(r) for r in suite["policy"]], R.PolicyConfig(always_allow_localhost=False))
     states = {n: R.endpoint_policy_map_state(repo, cache[ids[n]], cache) for n in ids}
     return ids, states
 
