@@ -886,6 +886,45 @@ def policies_l7_kats() -> dict:
                  "asserts": none},
             ]}
 
+def kafka_runtime_kats() -> dict:
+    """test/runtime/kafka.go:149-200 ("Kafka Policy Ingress", "Kafka Policy
+    Role Ingress"): the policy files (Policies-kafka.json,
+    Policies-kafka-Role.json, copied as data) and what the test observes,
+    as the requests that decide it: the console producer's produce and the
+    consumer's metadata / fetch on allowedTopic succeed; the consumer on
+    disallowTopic fails — under the role policy its metadata request is the
+    one refused (the test waits for "{disallowTopic=TOPIC_AUTHORIZATION_FAILED}",
+    :196), under the apiKey policy metadata passes ({"apiKey": "metadata"}
+    has no topic) and the fetch is refused.  "enforced" is the endpoint
+    summary (:155-158): policy enabled on the kafka container only.
+    Containers carry id.<name> (kafka.go:45-56); kind 1 = a typed request
+    (CG_KAFKA_K_TYPED)."""
+    def rq(src, key, topic, allow, note):
+        return {"from": src, "api_key": key, "api_version": 0, "kind": 1, "client_id": "console",
+                "topics": [topic], "allow": allow, "note": note}
+    common = [rq("client", 0, "allowedTopic", True, "produce allowedTopic (:160-163)"),
+              rq("client", 3, "allowedTopic", True, "metadata allowedTopic (consumer, :165-170)"),
+              rq("client", 1, "allowedTopic", True, "fetch allowedTopic (:165-170)"),
+              rq("client", 1, "disallowTopic", False, "fetch disallowTopic (:172-174, :192-197)")]
+    l4 = [["client", "kafka", 9092, "redirect"], ["host", "kafka", 9092, "redirect"],
+          ["zook", "kafka", 9092, "drop"], ["client", "zook", 2181, "allow"],
+          # kafka's own L3-only rule also lands on the 9092 redirect (wildcardL3L4Rule,
+          # repository.go:128-166): its map key is the port's, with the proxy port
+          ["kafka", "kafka", 9092, "redirect"]]
+    return {"generator": "tests/golden/make_golden.py kafka_runtime_kats()",
+            "containers": ["zook", "client", "kafka"], "port": 9092,
+            "suites": [
+                {"name": "Kafka Policy Ingress", "src": "test/runtime/kafka.go:149-175",
+                 "policy": _manifest("Policies-kafka.json"), "enforced": {"zook": False, "client": False, "kafka": True},
+                 "l4": l4, "requests": common + [rq("client", 3, "disallowTopic", True,
+                                                    "metadata disallowTopic: {apiKey: metadata} has no topic")]},
+                {"name": "Kafka Policy Role Ingress", "src": "test/runtime/kafka.go:177-200",
+                 "policy": _manifest("Policies-kafka-Role.json"),
+                 "enforced": {"zook": False, "client": False, "kafka": True},
+                 "l4": l4, "requests": common + [rq("client", 3, "disallowTopic", False,
+                                                    "metadata disallowTopic: TOPIC_AUTHORIZATION_FAILED (:192-197)")]},
+            ]}
+
 # ---------------------------------------------------------- Go regexp KATs --
 def go_regex_kats() -> dict:
     """Go 1.10 regexp (RE2 syntax, Perl flags) known answers for the proxylib
@@ -943,6 +982,7 @@ def main():
              "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
              "repository_kat.json": repository_kats(), "policies_l7_kat.json": policies_l7_kats(),
+             "kafka_runtime_kat.json": kafka_runtime_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
