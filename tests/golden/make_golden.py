@@ -884,6 +884,17 @@ def policies_l7_kats() -> dict:
                  "policy": _manifest("Policies-l7-multiple.json"), "asserts": multiple},
                 {"name": "L7 multiple deleted", "src": "test/runtime/Policies.go:552-559", "policy": [],
                  "asserts": none},
+                # L3-dependent L7 egress (:637-697): app3's port-80 egress is one
+                # redirect for both servers; the proxy statistics after the four
+                # app3 probes, each sent as http and http6: 8 requests received,
+                # 2 denied, 6 forwarded (checkProxyStatistics at :696)
+                {"name": "L3-dependent L7 egress", "src": "test/runtime/Policies.go:637-697",
+                 "policy": _manifest("Policies-l3-dependent-l7-egress.json"),
+                 "asserts": [("host", "httpd2", "public", True), ("app3", "httpd1", "public", True),
+                             ("app3", "httpd1", "private", False), ("app3", "httpd2", "public", True),
+                             ("app3", "httpd2", "private", True)],
+                 "proxy_stats": {"endpoint": "app3", "direction": "egress", "twins": 2, "received": 8,
+                                 "denied": 2, "forwarded": 6}},
             ]}
 
 def kafka_runtime_kats() -> dict:

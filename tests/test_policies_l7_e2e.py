@@ -1,4 +1,5 @@
-"""test/runtime/Policies.go:495-560 ("L7 Checks") end to end
+"""test/runtime/Policies.go:495-560 ("L7 Checks") and :637-697 ("L3-Dependent
+L7 Egress", with its proxy statistics) end to end
 (tests/golden/policies_l7_kat.json): the policy files → Repository → per
 endpoint policy map state (L4 redirects to proxy ports) and NPDS → every
 curl / ping assertion as the datapath and the proxy decide it:
@@ -85,18 +86,32 @@ def _connectivity(suite, l4_fn, http_fn):
     http_fn(request dict) → u8 verdicts under the suite's NPDS list."""
     ids, _, _ = _endpoints(suite)
     idx = {n: i for i, n in enumerate(KAT["containers"])}
+    stats = suite.get("proxy_stats")
+    seen = {"received": 0, "denied": 0}
+
+    def proxy(ep, ingress, remote, kind):  # one request through `ep`'s proxy
+        allowed = bool(http_fn(_request(idx[ep], ingress, remote, kind))[0])
+        if stats and ep == stats["endpoint"] and ingress == (stats["direction"] == "ingress"):
+            seen["received"] += stats["twins"]  # http and http6 send one request each
+            seen["denied"] += 0 if allowed else stats["twins"]
+        return allowed
     got = []
     for cli, srv, kind, _ in _probes(suite):
         ok = True
         if cli != "host":  # the client's egress (bpf_lxc.c:527 policy_can_egress)
             v = int(l4_fn(cli, _tuple(ids[srv], kind, False), oracle.L4_EGRESS)[0])
-            ok = v >= 0 and (v == 0 or kind == "ping" or bool(http_fn(_request(idx[cli], 0, ids[srv], kind))[0]))
+            ok = v >= 0 and (v == 0 or kind == "ping" or proxy(cli, 0, ids[srv], kind))
         if ok:  # the server's ingress (bpf_lxc.c:948 policy_can_access_ingress)
             v = int(l4_fn(srv, _tuple(ids[cli], kind, True), oracle.L4_INGRESS)[0])
-            ok = v >= 0 and (v == 0 or kind == "ping" or bool(http_fn(_request(idx[srv], 1, ids[cli], kind))[0]))
+            ok = v >= 0 and (v == 0 or kind == "ping" or proxy(srv, 1, ids[cli], kind))
         got.append(ok)
     want = [p[3] for p in _probes(suite)]
-    return [(p[0], p[1], p[2]) for p, g, w in zip(_probes(suite), got, want) if g != w]
+    bad = [(p[0], p[1], p[2]) for p, g, w in zip(_probes(suite), got, want) if g != w]
+    if stats:  # checkProxyStatistics (Policies.go:659-696)
+        fwd = seen["received"] - seen["denied"]
+        if (seen["received"], seen["denied"], fwd) != (stats["received"], stats["denied"], stats["forwarded"]):
+            bad.append(("proxy statistics", seen, fwd))
+    return bad
 
 
 @pytest.mark.parametrize("suite", KAT["suites"], ids=lambda s: s["name"])
