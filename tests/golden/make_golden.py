@@ -926,15 +926,44 @@ def kafka_runtime_kats() -> dict:
             "containers": ["zook", "client", "kafka"], "port": 9092,
             "suites": [
                 {"name": "Kafka Policy Ingress", "src": "test/runtime/kafka.go:149-175",
-                 "policy": _manifest("Policies-kafka.json"), "enforced": {"zook": False, "client": False, "kafka": True},
+                 "policy": _manifest("Policies-kafka.json"),
+                 "enforced": {"zook": [False, False], "client": [False, False], "kafka": [True, False]},
                  "l4": l4, "requests": common + [rq("client", 3, "disallowTopic", True,
                                                     "metadata disallowTopic: {apiKey: metadata} has no topic")]},
                 {"name": "Kafka Policy Role Ingress", "src": "test/runtime/kafka.go:177-200",
                  "policy": _manifest("Policies-kafka-Role.json"),
-                 "enforced": {"zook": False, "client": False, "kafka": True},
+                 "enforced": {"zook": [False, False], "client": [False, False], "kafka": [True, False]},
                  "l4": l4, "requests": common + [rq("client", 3, "disallowTopic", False,
                                                     "metadata disallowTopic: TOPIC_AUTHORIZATION_FAILED (:192-197)")]},
+                # test/k8sT/KafkaPolicies.go:150-247 with kafka-sw-security-policy.yaml
+                # (CNP specs, copied as data); pods labelled app=<name>
+                # (kafka-sw-app.yaml); policy enabled "Both" on kafka only
+                {"name": "k8s KafkaPolicies", "src": "test/k8sT/KafkaPolicies.go:150-247",
+                 "containers": ["kafka", "empire-hq", "empire-outpost", "empire-backup", "kube-dns"],
+                 "labels": {"kafka": {"k8s:app": "kafka"}, "empire-hq": {"k8s:app": "empire-hq"},
+                            "empire-outpost": {"k8s:app": "empire-outpost", "k8s:outpostid": "8888"},
+                            "empire-backup": {"k8s:app": "empire-backup"}, "kube-dns": {"k8s:k8s-app": "kube-dns"}},
+                 "policy": _k8s_manifest("kafka-sw-security-policy.yaml"),
+                 "enforced": {"kafka": [True, True], "empire-hq": [False, False], "empire-outpost": [False, False],
+                              "empire-backup": [False, False], "kube-dns": [False, False]},
+                 "l4": [["empire-hq", "kafka", 9092, "redirect"], ["empire-outpost", "kafka", 9092, "redirect"],
+                        ["empire-backup", "kafka", 9092, "redirect"], ["host", "kafka", 9092, "redirect"],
+                        ["kube-dns", "kafka", 9092, "drop"]],
+                 "requests": [rq("empire-hq", 0, "empire-announce", True, "prodHqAnnounce (:218-220)"),
+                              rq("empire-outpost", 1, "empire-announce", True, "conOutpostAnnoune (:222-224)"),
+                              rq("empire-hq", 0, "deathstar-plans", True, "prodHqDeathStar (:230-232)"),
+                              rq("empire-backup", 0, "empire-announce", False, "prodBackAnnounce (:238-240)"),
+                              rq("empire-outpost", 1, "deathstar-plans", False, "conOutDeathStar (:242-244)"),
+                              rq("empire-outpost", 0, "empire-announce", False, "prodOutAnnounce (:246-248)")]},
             ]}
+
+
+def _k8s_manifest(name: str) -> list:
+    """A CiliumNetworkPolicy's rules (`specs`) from test/k8sT/manifests."""
+    import yaml
+    with open(os.path.join(REF, "test/k8sT/manifests", name)) as f:
+        doc = yaml.safe_load(f)
+    return doc.get("specs") or [doc["spec"]]
 
 # ---------------------------------------------------------- Go regexp KATs --
 def go_regex_kats() -> dict:

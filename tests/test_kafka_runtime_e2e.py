@@ -1,4 +1,5 @@
-"""test/runtime/kafka.go:149-200 end to end (tests/golden/kafka_runtime_kat.json):
+"""test/runtime/kafka.go:149-200 and test/k8sT/KafkaPolicies.go:150-247 end to
+end (tests/golden/kafka_runtime_kat.json):
 the policy files → Repository → the kafka endpoint's ingress map (9092
 redirected to the Kafka proxy) and its redirect's rules (redirect.go:68-82)
 → the requests that decide what the runtime test observes, and which
@@ -20,21 +21,24 @@ KAT = load("kafka_runtime_kat.json")
 PROXY = {(True, "TCP", KAT["port"]): 15010}
 
 
-def _world():
-    ids = {n: 256 + i for i, n in enumerate(KAT["containers"])}
+def _world(suite):
+    names = suite.get("containers", KAT["containers"])
+    ids = {n: 256 + i for i, n in enumerate(names)}
     ids["host"] = R.RESERVED_HOST
     cache = {R.RESERVED_HOST: {"reserved:host": ""}, R.RESERVED_WORLD: {"reserved:world": ""}}
-    for n in KAT["containers"]:
-        cache[ids[n]] = {f"container:id.{n}": ""}
-    return ids, cache
+    for n in names:
+        cache[ids[n]] = suite["labels"][n] if "labels" in suite else {f"container:id.{n}": ""}
+    return names, ids, cache
 
 
 def _resolve(suite):
-    ids, cache = _world()
-    # the runtime daemon: allow-localhost "auto" = "policy" outside Kubernetes
-    repo = R.Repository([R.Rule.from_json(r) for r in suite["policy"]], R.PolicyConfig(always_allow_localhost=False))
-    enforced = {n: repo.get_rules_matching(cache[ids[n]])[0] for n in KAT["containers"]}
-    maps = {n: _keys_ports(R.endpoint_policy_map_state(repo, cache[ids[n]], cache, PROXY)) for n in KAT["containers"]}
+    names, ids, cache = _world(suite)
+    # allow-localhost "auto": "policy" outside Kubernetes (the runtime suites),
+    # "always" under it (daemon.go:1144-1147)
+    always = "labels" in suite
+    repo = R.Repository([R.Rule.from_json(r) for r in suite["policy"]], R.PolicyConfig(always_allow_localhost=always))
+    enforced = {n: list(repo.get_rules_matching(cache[ids[n]])) for n in names}
+    maps = {n: _keys_ports(R.endpoint_policy_map_state(repo, cache[ids[n]], cache, PROXY)) for n in names}
     f = repo.resolve_l4_ingress_policy(cache[ids["kafka"]])[f"{KAT['port']}/TCP"]
     assert f.L7Parser == R.PARSER_KAFKA
     redirect = R.kafka_redirect("kafka-9092-ingress", f, cache)
