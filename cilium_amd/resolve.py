@@ -360,7 +360,8 @@ def get_port_network_policy_rule(sel: EndpointSelector, parser: str, rules: L7Ru
                                  denied: Iterable[int] = ()) -> Optional[dict]:
     """getPortNetworkPolicyRule (server.go:476-537).  None = no remote
     identity matches (rule discarded).  Kafka rules are not translated for
-    Envoy (:516-517)."""
+    Envoy (:516-517); any other parser's rules are key-value pairs
+    (getL7Rule, :326-334) under `l7_proto`, unsorted (:519-533)."""
     denied = set(denied)
     remotes: list[int] = []
     if not sel.is_wildcard() or denied:
@@ -372,7 +373,11 @@ def get_port_network_policy_rule(sel: EndpointSelector, parser: str, rules: L7Ru
         hs = [get_http_rule(h)[0] or [] for h in rules.HTTP]
         hs.sort(key=functools.cmp_to_key(_http_rule_cmp))   # SortHTTPNetworkPolicyRules
         http = hs
-    return port_network_policy_rule(remotes, http)
+    r = port_network_policy_rule(remotes, http)
+    if parser not in (PARSER_NONE, PARSER_HTTP, PARSER_KAFKA) and rules.L7:
+        r["l7_proto"] = parser
+        r["l7_rules"] = {"l7_rules": [{"rule": dict(kv)} for kv in rules.L7]}
+    return r
 
 
 ALLOW_ALL_PORT_NETWORK_POLICY = [  # server.go:50-57: port 0, no rules
@@ -399,7 +404,7 @@ def get_direction_network_policy(l4map: Mapping[str, L4Filter], enforced: bool,
             r = get_port_network_policy_rule(sel, f.L7Parser, l7, identity_cache, denied)
             if r is None:
                 continue
-            if not r["remote_policies"] and "http_rules" not in r:
+            if not r["remote_policies"] and "http_rules" not in r and "l7_rules" not in r:  # rule.L7 == nil
                 allow_all = True
                 pnp["rules"] = []
                 break

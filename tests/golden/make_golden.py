@@ -958,6 +958,42 @@ def kafka_runtime_kats() -> dict:
             ]}
 
 
+def memcache_runtime_kats() -> dict:
+    """test/runtime/memcache.go:96-320: the memcache policy files (copied as
+    data) and each client operation the test asserts, as the request frame
+    the proxylib memcache parser sees — binary (python-binary-memcached:
+    set = opcode 0x01, get = 0x00, get_multi = one GETKQ 0x0d frame per key)
+    or text ("set k 0 500 n", "get k").  Clients are labelled
+    memcache-client, the server id.memcache (memcache.go:45-60)."""
+    def op(proto, cmd, keys, allow, note):
+        opcode = {"set": 1, "get": 0, "getkq": 13}[cmd]
+        return {"proto": proto, "command": "" if proto == "binary" else cmd, "opcode": opcode, "keys": keys,
+                "allow": allow, "note": note}
+    return {"generator": "tests/golden/make_golden.py memcache_runtime_kats()", "port": 11211,
+            "suites": [
+                {"name": "allow all actions", "src": "test/runtime/memcache.go:140-154,242-258",
+                 "policy": _manifest("Policies-memcache-allow.json"),
+                 "ops": [op("binary", "set", ["test2"], True, "setKeyBinary"), op("binary", "get", ["test2"], True, "getKeyBinary"),
+                         op("text", "set", ["test2"], True, "setKeyText STORED"), op("text", "get", ["test2"], True, "getKeyText VALUE")]},
+                {"name": "disallow set", "src": "test/runtime/memcache.go:156-180,260-285",
+                 "policy": _manifest("Policies-memcache-disallow-set.json"),
+                 "ops": [op("binary", "set", ["keyAfterPolicy"], False, "Set key should be prohibited by policy"),
+                         op("binary", "get", ["before"], True, "get key set before the policy"),
+                         op("text", "set", ["keyAfterPolicy"], False, "access denied"),
+                         op("text", "get", ["before"], True, "get key set before the policy")]},
+                {"name": "allow only key", "src": "test/runtime/memcache.go:182-199,287-307",
+                 "policy": _manifest("Policies-memcache-allow-key.json"),
+                 "ops": [op("binary", "set", ["allowed"], True, "set allowed"), op("binary", "get", ["allowed"], True, "get allowed"),
+                         op("binary", "set", ["disallowed"], False, "Able to set disallowed key"),
+                         op("text", "set", ["allowed"], True, "set allowed"), op("text", "get", ["allowed"], True, "get allowed"),
+                         op("text", "set", ["disallowed"], False, "access denied")]},
+                {"name": "multi-get", "src": "test/runtime/memcache.go:201-216",
+                 "policy": _manifest("Policies-memcache-allow-key-get.json"),
+                 "ops": [op("binary", "getkq", ["allowed"], True, "get_multi: the allowed key's frame"),
+                         op("binary", "getkq", ["disallowed"], False, "get_multi: Able to get multiple keys with disallowed")]},
+            ]}
+
+
 def _k8s_manifest(name: str) -> list:
     """A CiliumNetworkPolicy's rules (`specs`) from test/k8sT/manifests."""
     import yaml
@@ -1022,7 +1058,7 @@ def main():
              "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
              "repository_kat.json": repository_kats(), "policies_l7_kat.json": policies_l7_kats(),
-             "kafka_runtime_kat.json": kafka_runtime_kats(),
+             "kafka_runtime_kat.json": kafka_runtime_kats(), "memcache_runtime_kat.json": memcache_runtime_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
