@@ -994,6 +994,30 @@ def memcache_runtime_kats() -> dict:
             ]}
 
 
+def cassandra_runtime_kats() -> dict:
+    """test/runtime/cassandra.go:127-170: the two cassandra policy files
+    (copied as data) and cqlsh's requests as the proxylib cassandra parser's
+    paths (cassandraparser.go:486-578, "/opcode[/action/table]"): the
+    session's startup and system-table reads the policy's "^system.*" rule
+    exists for, the test's INSERT and SELECT on posts_db.posts.  Policy
+    enforcement is on for cass-server only (:131-135, :153-157)."""
+    session = [("/startup", True, "cqlsh startup"), ("/query/select/system.local", True, "cqlsh: system.local"),
+               ("/query/select/system_schema.tables", True, "cqlsh: schema read")]
+    return {"generator": "tests/golden/make_golden.py cassandra_runtime_kats()", "port": 9042,
+            "suites": [
+                {"name": "allow all actions", "src": "test/runtime/cassandra.go:127-145",
+                 "policy": _manifest("Policies-cassandra-allow-all.json"),
+                 "ops": [{"path": p_, "allow": a, "note": n} for p_, a, n in session + [
+                     ("/query/insert/posts_db.posts", True, "INSERT alice (:138-139)"),
+                     ("/query/select/posts_db.posts", True, "SELECT * FROM posts_db.posts (:142-144)")]]},
+                {"name": "disallow insert", "src": "test/runtime/cassandra.go:147-169",
+                 "policy": _manifest("Policies-cassandra-no-insert-posts.json"),
+                 "ops": [{"path": p_, "allow": a, "note": n} for p_, a, n in session + [
+                     ("/query/insert/posts_db.posts", False, "INSERT bob denied (:160-161)"),
+                     ("/query/select/posts_db.posts", True, "SELECT allowed (:164-168)")]]},
+            ]}
+
+
 def _k8s_manifest(name: str) -> list:
     """A CiliumNetworkPolicy's rules (`specs`) from test/k8sT/manifests."""
     import yaml
@@ -1059,6 +1083,7 @@ def main():
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
              "repository_kat.json": repository_kats(), "policies_l7_kat.json": policies_l7_kats(),
              "kafka_runtime_kat.json": kafka_runtime_kats(), "memcache_runtime_kat.json": memcache_runtime_kats(),
+             "cassandra_runtime_kat.json": cassandra_runtime_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
