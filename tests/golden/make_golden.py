@@ -857,6 +857,8 @@ def policies_e2e_kats() -> dict:
 
 
 def policies_l7_kats() -> dict:
+    k8s = {"containers": ["app1", "app2", "app3"], "allow_localhost": True,
+           "labels": {f"app{i}": {"k8s:id": f"app{i}", "k8s:zgroup": "testapp"} for i in (1, 2, 3)}}
     """test/runtime/Policies.go:495-560 ("L7 Checks"): the two L7 policy files
     it imports (Policies-l7-simple.json, Policies-l7-multiple.json, copied as
     data) and every connectivity assertion.  `public` / `private` are curl
@@ -895,7 +897,19 @@ def policies_l7_kats() -> dict:
                              ("app3", "httpd2", "private", True)],
                  "proxy_stats": {"endpoint": "app3", "direction": "egress", "twins": 2, "received": 8,
                                  "denied": 2, "forwarded": 6}},
-            ]}
+            ] + [dict(k8s, **sv) for sv in (
+                # test/k8sT/Policies.go:249-343 on demo.yaml's pods (labels id=appN,
+                # zgroup=testapp); allow-localhost resolves to "always" under
+                # Kubernetes (daemon.go:1144-1147)
+                {"name": "k8s L3/L4 policy", "src": "test/k8sT/Policies.go:253-282",
+                 "policy": _k8s_manifest("l3-l4-policy.yaml"),
+                 "asserts": [("app2", "app1", "public", True), ("app3", "app1", "public", False)]},
+                {"name": "k8s L7 policy", "src": "test/k8sT/Policies.go:289-318",
+                 "policy": _k8s_manifest("l7-policy.yaml"),
+                 "asserts": [("app2", "app1", "public", True), ("app2", "app1", "private", False),
+                             ("app3", "app1", "public", False), ("app3", "app1", "private", False)]},
+                {"name": "k8s L7 policy deleted", "src": "test/k8sT/Policies.go:330-342", "policy": [],
+                 "asserts": [("app3", "app1", "public", True), ("app2", "app1", "public", True)]})]}
 
 def kafka_runtime_kats() -> dict:
     """test/runtime/kafka.go:149-200 ("Kafka Policy Ingress", "Kafka Policy

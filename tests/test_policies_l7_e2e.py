@@ -1,5 +1,6 @@
-"""test/runtime/Policies.go:495-560 ("L7 Checks") and :637-697 ("L3-Dependent
-L7 Egress", with its proxy statistics) end to end
+"""test/runtime/Policies.go:495-560 ("L7 Checks"), :637-697 ("L3-Dependent
+L7 Egress", with its proxy statistics) and test/k8sT/Policies.go:249-343 (the
+CNP L3/L4 and L7 policies on demo.yaml's pods) end to end
 (tests/golden/policies_l7_kat.json): the policy files → Repository → per
 endpoint policy map state (L4 redirects to proxy ports) and NPDS → every
 curl / ping assertion as the datapath and the proxy decide it:
@@ -32,24 +33,28 @@ PROXY = {(True, "TCP", 80): 15001, (False, "TCP", 80): 15002, (True, "TCP", 8080
 PATHS = {"public": b"/public", "private": b"/private"}
 
 
-def _world():
-    names = KAT["containers"]
+def _names(suite):
+    return suite.get("containers", KAT["containers"])
+
+
+def _world(suite):
+    names = _names(suite)
     ids = {n: 256 + i for i, n in enumerate(names)}
     ids["host"] = R.RESERVED_HOST
     cache = {R.RESERVED_HOST: {"reserved:host": ""}, R.RESERVED_WORLD: {"reserved:world": ""}}
     for n in names:
-        cache[ids[n]] = {f"container:id.{n}": ""}
+        cache[ids[n]] = suite["labels"][n] if "labels" in suite else {f"container:id.{n}": ""}
     return ids, cache
 
 
 def _endpoints(suite):
-    """Per container: (policy map keys, proxy ports) and its NPDS, in the order
-    of KAT["containers"] (the NPDS list index is the policy index)."""
-    ids, cache = _world()
+    """Per container: (policy map keys, proxy ports) and its NPDS, in the
+    suite's container order (the NPDS list index is the policy index)."""
+    ids, cache = _world(suite)
     repo = R.Repository([R.Rule.from_json(r) for r in suite["policy"]],
-                        R.PolicyConfig(always_allow_localhost=KAT["allow_localhost"]))
+                        R.PolicyConfig(always_allow_localhost=suite.get("allow_localhost", KAT["allow_localhost"])))
     maps, npds = {}, []
-    for n in KAT["containers"]:
+    for n in _names(suite):
         lbl = cache[ids[n]]
         ing_on, eg_on = repo.get_rules_matching(lbl)
         l4 = R.L4Policy(Ingress=repo.resolve_l4_ingress_policy(lbl) if ing_on else {},
@@ -85,7 +90,7 @@ def _connectivity(suite, l4_fn, http_fn):
     """l4_fn(name, tuples, mode) → i32 verdicts at endpoint `name`'s map;
     http_fn(request dict) → u8 verdicts under the suite's NPDS list."""
     ids, _, _ = _endpoints(suite)
-    idx = {n: i for i, n in enumerate(KAT["containers"])}
+    idx = {n: i for i, n in enumerate(_names(suite))}
     stats = suite.get("proxy_stats")
     seen = {"received": 0, "denied": 0}
 
