@@ -858,7 +858,8 @@ def policies_e2e_kats() -> dict:
 
 def policies_l7_kats() -> dict:
     k8s = {"containers": ["app1", "app2", "app3"], "allow_localhost": True,
-           "labels": {f"app{i}": {"k8s:id": f"app{i}", "k8s:zgroup": "testapp"} for i in (1, 2, 3)}}
+           "labels": {f"app{i}": dict({"k8s:id": f"app{i}", "k8s:zgroup": "testapp"},
+                                      **({"k8s:appSecond": "true"} if i == 2 else {})) for i in (1, 2, 3)}}
     """test/runtime/Policies.go:495-560 ("L7 Checks"): the two L7 policy files
     it imports (Policies-l7-simple.json, Policies-l7-multiple.json, copied as
     data) and every connectivity assertion.  `public` / `private` are curl
@@ -909,7 +910,10 @@ def policies_l7_kats() -> dict:
                  "asserts": [("app2", "app1", "public", True), ("app2", "app1", "private", False),
                              ("app3", "app1", "public", False), ("app3", "app1", "private", False)]},
                 {"name": "k8s L7 policy deleted", "src": "test/k8sT/Policies.go:330-342", "policy": [],
-                 "asserts": [("app3", "app1", "public", True), ("app2", "app1", "public", True)]})]}
+                 "asserts": [("app3", "app1", "public", True), ("app2", "app1", "public", True)]},
+                {"name": "k8s matchExpressions", "src": "test/k8sT/Policies.go:380-397",
+                 "policy": _k8s_manifest("cnp-matchexpressions.yaml"),
+                 "asserts": [("app2", "app1", "public", True), ("app3", "app1", "public", False)]})]}
 
 def kafka_runtime_kats() -> dict:
     """test/runtime/kafka.go:149-200 ("Kafka Policy Ingress", "Kafka Policy
