@@ -457,15 +457,31 @@ class PolicyMergeError(ValueError):
     (rule.go:52-96); the whole resolution fails, as the reference's does."""
 
 
-# EntitySelectorMapping (api/entity.go:71-84, :129-134)
+# EntitySelectorMapping (api/entity.go:71-84); "cluster" is filled in by
+# init_entities (InitEntities, :128-140)
 _ENTITY_SELECTORS = {
     "all": [EndpointSelector()],
     "world": [EndpointSelector.of({"reserved:world": ""})],
     "host": [EndpointSelector.of({"reserved:host": ""})],
     "init": [EndpointSelector.of({"reserved:init": ""})],
-    "cluster": [EndpointSelector.of({"reserved:host": ""}), EndpointSelector.of({"reserved:init": ""}),
-                EndpointSelector.of({"reserved:unmanaged": ""})],
+    "cluster": [],
 }
+POLICY_LABEL_CLUSTER = "io.cilium.k8s.policy.cluster"  # k8s/apis/cilium.io/const.go:35
+DEFAULT_CLUSTER_NAME = "default"                       # defaults/cluster.go:19
+
+
+def init_entities(cluster_name: str = DEFAULT_CLUSTER_NAME) -> None:
+    """InitEntities (api/entity.go:128-140): the cluster entity is the host,
+    init and unmanaged identities plus every workload labelled with this
+    cluster's name (k8s:io.cilium.k8s.policy.cluster, which the Kubernetes
+    workload labels carry: workloads/kubernetes.go:112)."""
+    _ENTITY_SELECTORS["cluster"] = [EndpointSelector.of({"reserved:host": ""}),
+                                    EndpointSelector.of({"reserved:init": ""}),
+                                    EndpointSelector.of({"reserved:unmanaged": ""}),
+                                    EndpointSelector.of({f"k8s:{POLICY_LABEL_CLUSTER}": cluster_name})]
+
+
+init_entities()  # the daemon calls it with option.Config.ClusterName at start-up
 
 
 def selector_from_json(d: Optional[dict]) -> EndpointSelector:

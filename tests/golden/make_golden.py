@@ -1036,6 +1036,38 @@ def cassandra_runtime_kats() -> dict:
             ]}
 
 
+def entities_kats() -> dict:
+    """test/k8sT/Policies.go:162-215,674-733 ("Validate to-entities
+    policies"): the four CNPs (cnp-to-entities-{all,world,cluster,host}.yaml,
+    copied as data) and validateConnectivity's probes from app2 and app3 —
+    HTTP to www.google.com and ICMP to 8.8.8.8 (world), DNS to kube-dns
+    (world || cluster: "kube-dns is always whitelisted"), HTTP to app1's
+    service (cluster) — with the (world, cluster) outcome each It asserts.
+    The destination addresses are resolved through the ipcache, as
+    bpf_lxc.c:509-527 does: pods and the node by their /32s, the internet
+    addresses by no entry (WORLD).  Pod IPs and the google address are
+    synthetic (the test reads the real ones from the cluster)."""
+    k8s = lambda d: dict(d, **{"k8s:io.cilium.k8s.policy.cluster": "default"})  # noqa: E731
+    pods = {"app1": k8s({"k8s:id": "app1", "k8s:zgroup": "testapp", "k8s:io.kubernetes.pod.namespace": "default"}),
+            "app2": k8s({"k8s:id": "app2", "k8s:zgroup": "testapp", "k8s:io.kubernetes.pod.namespace": "default"}),
+            "app3": k8s({"k8s:id": "app3", "k8s:zgroup": "testapp", "k8s:io.kubernetes.pod.namespace": "default"}),
+            "kube-dns": k8s({"k8s:k8s-app": "kube-dns", "k8s:io.kubernetes.pod.namespace": "kube-system"})}
+    addrs = {"app1": "10.10.0.11", "app2": "10.10.0.12", "app3": "10.10.0.13", "kube-dns": "10.10.1.53",
+             "google": "172.217.1.100", "8.8.8.8": "8.8.8.8"}
+    probes = [("google", 6, 80, "world"), ("8.8.8.8", 1, 0, "world"), ("kube-dns", 17, 53, "dns"),
+              ("app1", 6, 80, "cluster")]
+    its = [("all", True, True, "690-699"), ("world", True, False, "701-711"), ("cluster", False, True, "713-722"),
+           ("host", False, False, "724-732")]
+    return {"generator": "tests/golden/make_golden.py entities_kats()", "pods": pods, "addrs": addrs,
+            "node": "192.168.36.11",
+            "suites": [{"name": f"toEntities {e}", "src": f"test/k8sT/Policies.go:{ln}",
+                        "policy": _k8s_manifest(f"cnp-to-entities-{e}.yaml"),
+                        "asserts": [[c, dst, proto, dport,
+                                     (w or cl) if kind == "dns" else (w if kind == "world" else cl)]
+                                    for c in ("app2", "app3") for dst, proto, dport, kind in probes]}
+                       for e, w, cl, ln in its]}
+
+
 def _k8s_manifest(name: str) -> list:
     """A CiliumNetworkPolicy's rules (`specs`) from test/k8sT/manifests."""
     import yaml
@@ -1101,7 +1133,7 @@ def main():
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),
              "repository_kat.json": repository_kats(), "policies_l7_kat.json": policies_l7_kats(),
              "kafka_runtime_kat.json": kafka_runtime_kats(), "memcache_runtime_kat.json": memcache_runtime_kats(),
-             "cassandra_runtime_kat.json": cassandra_runtime_kats(),
+             "cassandra_runtime_kat.json": cassandra_runtime_kats(), "entities_kat.json": entities_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
