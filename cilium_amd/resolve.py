@@ -749,6 +749,7 @@ class PolicyConfig:
     AlwaysAllowLocalhost() and HostAllowsWorld (rule.go:166-172)."""
     always_allow_localhost: bool = True
     host_allows_world: bool = False
+    enforcement: str = "default"  # option.Config.EnablePolicy: default | always | never
 
 
 def resolve_rule_l4_ingress(r: Rule, to_labels, requirements: tuple, result: L4Policy,
@@ -934,6 +935,21 @@ class Repository:
                                 wildcard_l3l4_rule(pp.Protocol, parse_port(pp.Port), peers, r.Labels, l4map)
 
 
+def compute_policy_enforcement(repo: Repository, labels) -> tuple[bool, bool]:
+    """Endpoint.ComputePolicyEnforcement (pkg/endpoint/policy.go:616-639):
+    "always" enforces both directions, "never" neither; "default" enforces
+    both for an endpoint still labelled reserved:init, else the directions
+    some rule selecting it has rules for (GetRulesMatching)."""
+    mode = repo.cfg.enforcement
+    if mode == "always":
+        return True, True
+    if mode == "default":
+        if "reserved:init" in labels:
+            return True, True
+        return repo.get_rules_matching(labels)
+    return False, False
+
+
 def endpoint_policy_map_state(repo: Repository, labels, identity_cache: Mapping[int, Mapping[str, str]],
                               redirect_ports: Optional[Mapping[tuple, int]] = None) -> dict[PolicyKey, int]:
     """One endpoint's desired policy map state, as regeneratePolicy computes
@@ -942,7 +958,7 @@ def endpoint_policy_map_state(repo: Repository, labels, identity_cache: Mapping[
     enforced directions, then computeDesiredPolicyMapState — L4 entries,
     localhost, world, and L3 entries for every identity (an unenforced
     direction allows every identity)."""
-    ing_on, eg_on = repo.get_rules_matching(labels)
+    ing_on, eg_on = compute_policy_enforcement(repo, labels)
     l4 = L4Policy(Ingress=repo.resolve_l4_ingress_policy(labels) if ing_on else {},
                   Egress=repo.resolve_l4_egress_policy(labels) if eg_on else {})
     desired = compute_desired_l4_policymap_entries(l4, identity_cache, redirect_ports or {})

@@ -1068,6 +1068,45 @@ def entities_kats() -> dict:
                        for e, w, cl, ln in its]}
 
 
+def egress_world_kats() -> dict:
+    """test/runtime/Policies.go:1087-1190 ("Tests Egress To World") under
+    PolicyEnforcement=always: app1's egress to 8.8.8.8 (ping) and google.com
+    (HTTP) and its ping to app2, for the rule sets the test imports — none,
+    toEntities world, toEntities all, and world plus an in-cluster L7 rule to
+    app2 (the policy texts, copied as data).  The test's 0.0.0.0/0 toCIDR
+    variant is not carried: CIDR identities are outside this engine's scope
+    (DESIGN.md §7).  Destinations resolve through the ipcache (pods by /32,
+    the internet by no entry); a pod destination also passes the server's
+    ingress (bpf_lxc.c:948).  Addresses other than 8.8.8.8 are synthetic."""
+    app1 = {"endpointSelector": {"matchLabels": {"id.app1": ""}}}
+    world = dict(app1, egress=[{"toEntities": ["world"]}])
+    allent = dict(app1, egress=[{"toEntities": ["all"]}])
+    l7 = dict(app1, egress=[{"toEntities": ["world"]},
+                            {"toEndpoints": [{"matchLabels": {"id.app2": ""}}],
+                             "toPorts": [{"ports": [{"port": "80", "protocol": "tcp"}],
+                                          "rules": {"HTTP": [{"method": "GET", "path": "/nowhere"}]}}]}])
+    probes = [["8.8.8.8", 1, 0], ["app2", 1, 0], ["google", 6, 80]]
+    ok = [True, False, True]
+    # Policies.go:99-240: ExpectEndpointSummary for the one endpoint (id.app)
+    # per enforcement mode, without and with sample_policy.json
+    modes = {"policy": _manifest("sample_policy.json"), "src": "test/runtime/Policies.go:99-240",
+             "enabled": {"default": [False, True], "always": [True, True], "never": [False, False]}}
+    return {"generator": "tests/golden/make_golden.py egress_world_kats()", "enforcement_modes": modes,
+            "enforcement": "always",
+            "pods": ["app1", "app2"], "addrs": {"app1": "10.11.0.1", "app2": "10.11.0.2", "google": "172.217.1.100",
+                                               "8.8.8.8": "8.8.8.8"},
+            "suites": [
+                {"name": "always, no policy", "src": "test/runtime/Policies.go:1116-1119", "policy": [],
+                 "asserts": [["8.8.8.8", 1, 0, False]]},
+                {"name": "toEntities world", "src": "test/runtime/Policies.go:1121-1133", "policy": [world],
+                 "asserts": [p_ + [o] for p_, o in zip(probes, ok)]},
+                {"name": "toEntities all", "src": "test/runtime/Policies.go:1137-1148", "policy": [allent],
+                 "asserts": [p_ + [o] for p_, o in zip(probes, ok)]},
+                {"name": "world + in-cluster L7", "src": "test/runtime/Policies.go:1166-1189", "policy": [l7],
+                 "asserts": [p_ + [o] for p_, o in zip(probes, ok)]},
+            ]}
+
+
 def _k8s_manifest(name: str) -> list:
     """A CiliumNetworkPolicy's rules (`specs`) from test/k8sT/manifests."""
     import yaml
@@ -1134,6 +1173,7 @@ def main():
              "repository_kat.json": repository_kats(), "policies_l7_kat.json": policies_l7_kats(),
              "kafka_runtime_kat.json": kafka_runtime_kats(), "memcache_runtime_kat.json": memcache_runtime_kats(),
              "cassandra_runtime_kat.json": cassandra_runtime_kats(), "entities_kat.json": entities_kats(),
+             "egress_world_kat.json": egress_world_kats(),
              "go_regex_kat.json": go_regex_kats()}
     only = [a for a in sys.argv[1:] if a.endswith(".json")]
     for name, data in files.items():
