@@ -1091,7 +1091,15 @@ def egress_world_kats() -> dict:
     # per enforcement mode, without and with sample_policy.json
     modes = {"policy": _manifest("sample_policy.json"), "src": "test/runtime/Policies.go:99-240",
              "enabled": {"default": [False, True], "always": [True, True], "never": [False, False]}}
-    return {"generator": "tests/golden/make_golden.py egress_world_kats()", "enforcement_modes": modes,
+    # Policies.go:1395-1552 (enforcement always): a new endpoint is first
+    # reserved:init (identity 5), then gets its labels ("somelabel"); the
+    # host pings it (ingress) and it pings the host 10.0.2.15 (egress) —
+    # dropped with no policy, allowed with Policies-reserved-init.json
+    init = {"src": "test/runtime/Policies.go:1395-1552", "policy": _manifest("Policies-reserved-init.json"),
+            "host_ip": "10.0.2.15",
+            "endpoints": {"init": {"reserved:init": ""}, "somelabel": {"container:somelabel": ""}},
+            "asserts": [[ep, d, False, True] for ep in ("init", "somelabel") for d in ("ingress", "egress")]}
+    return {"generator": "tests/golden/make_golden.py egress_world_kats()", "enforcement_modes": modes, "init": init,
             "enforcement": "always",
             "pods": ["app1", "app2"], "addrs": {"app1": "10.11.0.1", "app2": "10.11.0.2", "google": "172.217.1.100",
                                                "8.8.8.8": "8.8.8.8"},

@@ -1,4 +1,5 @@
-"""test/runtime/Policies.go:1087-1190 ("Tests Egress To World") end to end
+"""test/runtime/Policies.go:1087-1190 ("Tests Egress To World"), :99-240
+(enforcement modes) and :1395-1552 (reserved:init policies) end to end
 (tests/golden/egress_world_kat.json) under PolicyEnforcement=always
 (ComputePolicyEnforcement, pkg/endpoint/policy.go:616-639): the destination
 through the ipcache, app1's egress map (policy_can_egress), and for a pod
@@ -121,3 +122,52 @@ def test_policy_enforcement_modes():
             assert any(R.compute_policy_enforcement(repo, lbl)) == want, (mode, bool(rules))
     # an endpoint still labelled reserved:init is enforced in default mode
     assert R.compute_policy_enforcement(R.Repository(), {"reserved:init": ""}) == (True, True)
+
+
+def _init_case(with_policy: bool):
+    """Policies.go:1395-1552 under enforcement always: (endpoint, direction,
+    tuple, remote address or None, expect) — ingress from the host identity,
+    egress to the host address through the ipcache."""
+    c = KAT["init"]
+    ids = {"init": R.RESERVED_INIT, "somelabel": 400}
+    cache = {ids[n]: lbl for n, lbl in c["endpoints"].items()}
+    cache.update({R.RESERVED_HOST: {"reserved:host": ""}, R.RESERVED_WORLD: {"reserved:world": ""}})
+    repo = R.Repository([R.Rule.from_json(r) for r in (c["policy"] if with_policy else [])],
+                        R.PolicyConfig(always_allow_localhost=False, enforcement="always"))
+    maps = {n: _keys_ports(R.endpoint_policy_map_state(repo, c["endpoints"][n], cache)) for n in ids}
+    host_a = np.array([int.from_bytes(ipaddress.ip_address(c["host_ip"]).packed, "little")], np.uint32)
+    ik = IPCache._keys([f"{c['host_ip']}/32"])
+    iv = np.array([[R.RESERVED_HOST, 0]], np.uint32)
+    out = []
+    for ep, d, no_pol, pol in c["asserts"]:
+        t = np.zeros(1, L4_TUPLE_DTYPE)
+        if d == "ingress":
+            t[0] = (R.RESERVED_HOST, 0, 1, N.CG_L4_F_INGRESS, 84)
+        else:
+            t[0] = (0, 0, 1, 0, 84)
+        out.append((ep, d, t, maps[ep], pol if with_policy else no_pol))
+    return out, ik, iv, host_a
+
+
+@pytest.mark.parametrize("with_policy", [False, True])
+def test_init_policy_oracle(with_policy):
+    probes, ik, iv, host_a = _init_case(with_policy)
+    for ep, d, t, kp, want in probes:
+        v = (oracle.l4(*kp, t, oracle.L4_INGRESS)[0][0] if d == "ingress" else
+             oracle.l4_egress_via_ipcache(*kp, ik, iv, host_a, t)[0][0])
+        assert (int(v) >= 0) == want, (ep, d, int(v))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_policy", [False, True])
+def test_gpu_init_policy(gpu, with_policy):
+    probes, ik, iv, host_a = _init_case(with_policy)
+    ic = gpu.ipcache()
+    ic.update(ik, iv)
+    for ep, d, t, kp, want in probes:
+        pm = gpu.policy_map()
+        pm.allow_keys(*kp)
+        v = pm.verdicts(t, mode=N.CG_L4_INGRESS)[0] if d == "ingress" else pm.verdicts_via_ipcache(ic, host_a, t)[0]
+        pm.destroy()
+        assert (int(v) >= 0) == want, (ep, d, int(v))
+    ic.destroy()
