@@ -1101,8 +1101,9 @@ def egress_world_kats() -> dict:
             "asserts": [[ep, d, False, True] for ep in ("init", "somelabel") for d in ("ingress", "egress")]}
     return {"generator": "tests/golden/make_golden.py egress_world_kats()", "enforcement_modes": modes, "init": init,
             "enforcement": "always",
-            "pods": ["app1", "app2"], "addrs": {"app1": "10.11.0.1", "app2": "10.11.0.2", "google": "172.217.1.100",
-                                               "8.8.8.8": "8.8.8.8"},
+            "pods": ["app1", "app2", "httpd2"], "host_ip": "10.0.2.15",
+            "addrs": {"app1": "10.11.0.1", "app2": "10.11.0.2", "httpd2": "10.11.0.3", "google": "172.217.1.100",
+                      "8.8.8.8": "8.8.8.8", "host": "10.0.2.15"},
             "suites": [
                 {"name": "always, no policy", "src": "test/runtime/Policies.go:1116-1119", "policy": [],
                  "asserts": [["8.8.8.8", 1, 0, False]]},
@@ -1112,6 +1113,11 @@ def egress_world_kats() -> dict:
                  "asserts": [p_ + [o] for p_, o in zip(probes, ok)]},
                 {"name": "world + in-cluster L7", "src": "test/runtime/Policies.go:1166-1189", "policy": [l7],
                  "asserts": [p_ + [o] for p_, o in zip(probes, ok)]},
+                # "Tests Egress To Host" (:1241-1270), default enforcement
+                {"name": "toEntities host", "src": "test/runtime/Policies.go:1241-1270", "enforcement": "default",
+                 "policy": [dict(app1, egress=[{"toEntities": ["host"]}])],
+                 "asserts": [["host", 1, 0, True], ["host", 6, 80, True], ["app2", 1, 0, False],
+                             ["httpd2", 6, 80, False]]},
             ]}
 
 

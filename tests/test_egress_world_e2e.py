@@ -28,14 +28,16 @@ CACHE.update({R.RESERVED_HOST: {"reserved:host": ""}, R.RESERVED_WORLD: {"reserv
 
 
 def _ipcache():
-    return (IPCache._keys([f"{KAT['addrs'][n]}/32" for n in PODS]),
-            np.array([[IDS[n], 0] for n in PODS], np.uint32))
+    """Pods by their /32s, the node by its address (the host identity)."""
+    return (IPCache._keys([f"{KAT['addrs'][n]}/32" for n in PODS] + [f"{KAT['host_ip']}/32"]),
+            np.array([[IDS[n], 0] for n in PODS] + [[R.RESERVED_HOST, 0]], np.uint32))
 
 
 def _probes(suite):
     """(remote address, egress tuple, ingress tuple or None, expect)"""
     repo = R.Repository([R.Rule.from_json(r) for r in suite["policy"]],
-                        R.PolicyConfig(always_allow_localhost=False, enforcement=KAT["enforcement"]))
+                        R.PolicyConfig(always_allow_localhost=False,
+                                       enforcement=suite.get("enforcement", KAT["enforcement"])))
     maps = {n: _keys_ports(R.endpoint_policy_map_state(repo, CACHE[IDS[n]], CACHE)) for n in PODS}
     out = []
     for dst, proto, dport, want in suite["asserts"]:
@@ -45,7 +47,7 @@ def _probes(suite):
         ing = None
         if dst in IDS:
             ing = np.zeros(1, L4_TUPLE_DTYPE)
-            ing[0] = (IDS["app1"], htons(dport), proto, N.CG_L4_F_INGRESS, 100)
+            ing[0] = (IDS["app1"], htons(dport), proto, N.CG_L4_F_INGRESS, 100)  # (the host has no map)
         out.append((dst, a, eg, ing, bool(want)))
     return maps, out
 
