@@ -858,7 +858,11 @@ def policies_e2e_kats() -> dict:
 
 def policies_l7_kats() -> dict:
     k8s = {"containers": ["app1", "app2", "app3"], "allow_localhost": True,
-           "labels": {f"app{i}": dict({"k8s:id": f"app{i}", "k8s:zgroup": "testapp"},
+           # the service account label workloads/kubernetes.go adds
+           # (demo.yaml: app1-account, app2-account, app3 the namespace default)
+           "labels": {f"app{i}": dict({"k8s:id": f"app{i}", "k8s:zgroup": "testapp",
+                                       "k8s:io.cilium.k8s.policy.serviceaccount":
+                                           f"app{i}-account" if i < 3 else "default"},
                                       **({"k8s:appSecond": "true"} if i == 2 else {})) for i in (1, 2, 3)}}
     """test/runtime/Policies.go:495-560 ("L7 Checks"): the two L7 policy files
     it imports (Policies-l7-simple.json, Policies-l7-multiple.json, copied as
@@ -913,6 +917,9 @@ def policies_l7_kats() -> dict:
                  "asserts": [("app3", "app1", "public", True), ("app2", "app1", "public", True)]},
                 {"name": "k8s matchExpressions", "src": "test/k8sT/Policies.go:380-397",
                  "policy": _k8s_manifest("cnp-matchexpressions.yaml"),
+                 "asserts": [("app2", "app1", "public", True), ("app3", "app1", "public", False)]},
+                {"name": "k8s ServiceAccount", "src": "test/k8sT/Policies.go:346-378",
+                 "policy": _k8s_manifest("service-account.yaml"),
                  "asserts": [("app2", "app1", "public", True), ("app3", "app1", "public", False)]})]}
 
 def kafka_runtime_kats() -> dict:
