@@ -648,14 +648,25 @@ class Rule:
                         pp.Protocol = parse_l4_proto(pp.Protocol)
                         if not _rules_empty(pr.Rules) and pp.Protocol != "TCP":
                             raise ValueError(f"L7 rules can only apply exclusively to TCP, not {pp.Protocol}")
-                    if not _rules_empty(pr.Rules):
-                        kinds = sum(bool(x) for x in (pr.Rules.HTTP, pr.Rules.Kafka, pr.Rules.L7))
+                    if not _rules_empty(pr.Rules):  # L7Rules.sanitize (:277-313)
+                        r, kinds = pr.Rules, 0
+                        if r.HTTP is not None:
+                            kinds += 1
+                            for h in r.HTTP:
+                                h.sanitize()
+                        if r.Kafka is not None:
+                            kinds += 1
+                            for k in r.Kafka:
+                                k.sanitize()
+                        if r.L7 is not None and not r.L7Proto:
+                            raise ValueError("'l7' may only be specified when a 'l7proto' is also specified")
+                        if r.L7Proto:
+                            kinds += 1
+                            for kv in r.L7 or []:  # PortRuleL7.Sanitize (l7.go:27-34)
+                                if "" in kv:
+                                    raise ValueError("Empty key not allowed")
                         if kinds > 1:
                             raise ValueError("multiple L7 protocol rule types specified in single rule")
-                        for h in pr.Rules.HTTP or []:
-                            h.sanitize()
-                        for k in pr.Rules.Kafka or []:
-                            k.sanitize()
 
 
 def _copy_l7(r: L7Rules) -> L7Rules:

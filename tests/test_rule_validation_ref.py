@@ -1,0 +1,40 @@
+"""Rule.Sanitize pinned to pkg/policy/api/rule_validation_test.go:28-352
+(TestL7RulesWithNonTCPProtocols, TestL7Rules): each rule of the test, in
+the policy JSON form, accepted or refused with the test's message."""
+import pytest
+
+from cilium_amd import resolve as R
+
+GET = {"http": [{"method": "GET", "path": "/"}]}
+
+
+def _rule(ports, rules):
+    return {"endpointSelector": {}, "ingress": [{"fromEndpoints": [{}], "toPorts": [
+        {"ports": [{"port": p, "protocol": pr} for p, pr in ports], **({"rules": rules} if rules else {})}]}]}
+
+
+CASES = [  # (source lines, rule, error message or None)
+    (":30-52", _rule([("80", "TCP"), ("81", "TCP")], GET), None),
+    (":54-75", _rule([("80", "UDP")], GET), "L7 rules can only apply exclusively to TCP, not UDP"),
+    (":77-99", _rule([("80", "ANY")], GET), "L7 rules can only apply exclusively to TCP, not ANY"),
+    (":101-124", _rule([("80", "TCP"), ("12345", "UDP")], GET), "L7 rules can only apply exclusively to TCP, not UDP"),
+    (":126-149", _rule([("80", "UDP"), ("12345", "TCP")], GET), "L7 rules can only apply exclusively to TCP, not UDP"),
+    (":280-303", _rule([("80", "TCP"), ("81", "TCP")],
+                       {"l7proto": "test.lineparser", "l7": [{"method": "PUT", "path": "/"},
+                                                            {"method": "GET", "path": "/"}]}), None),
+    (":305-325", _rule([("80", "TCP"), ("81", "TCP")], {"l7proto": "test.lineparser"}), None),
+    (":327-351", _rule([("80", "TCP"), ("81", "TCP")],
+                       {"l7proto": "test.lineparser", "l7": [{"method": "PUT", "": "Foo"}]}), "Empty key not allowed"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
+def test_rule_sanitize(case):
+    _, rule, err = case
+    r = R.Rule.from_json(rule)
+    if err is None:
+        r.sanitize()
+    else:
+        with pytest.raises(ValueError) as ei:
+            r.sanitize()
+        assert str(ei.value) == err
