@@ -45,3 +45,12 @@ def cluster1():
 def test_entity_matches(cluster1, case):
     entities, lbls, want = case
     assert _matches(entities, _labels(*lbls)) == want
+
+
+def test_selects_all_endpoints():
+    """selector_test.go:32-47 (EndpointSelectorSlice.SelectsAllEndpoints)."""
+    bar, foo = R.EndpointSelector.of({"bar": ""}), R.EndpointSelector.of({"foo": ""})
+    assert R.selects_all([])
+    assert R.selects_all([R.WILDCARD])
+    assert R.selects_all([R.WILDCARD, bar])
+    assert not R.selects_all([bar, foo])
