@@ -38,3 +38,13 @@ def test_rule_sanitize(case):
         with pytest.raises(ValueError) as ei:
             r.sanitize()
         assert str(ei.value) == err
+
+
+@pytest.mark.parametrize("sel", [R.WILDCARD, R.EndpointSelector.of({"bar": ""})], ids=["wildcard", "bar"])
+def test_create_l4_filter(sel):
+    """l4_test.go:58-83 (TestCreateL4Filter): one L7 rule entry whether the
+    selector is the wildcard or label-based, ingress and egress."""
+    from cilium_amd.policy import L7Rules, PortRuleHTTP
+    rules = L7Rules(HTTP=[PortRuleHTTP(Path="/public", Method="GET")])
+    assert len(R.create_l4_ingress_filter([sel], [], rules, 80, "TCP").L7RulesPerEp) == 1
+    assert len(R.create_l4_egress_filter([sel], rules, 80, "TCP").L7RulesPerEp) == 1
