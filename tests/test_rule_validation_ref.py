@@ -48,3 +48,22 @@ def test_create_l4_filter(sel):
     rules = L7Rules(HTTP=[PortRuleHTTP(Path="/public", Method="GET")])
     assert len(R.create_l4_ingress_filter([sel], [], rules, 80, "TCP").L7RulesPerEp) == 1
     assert len(R.create_l4_egress_filter([sel], rules, 80, "TCP").L7RulesPerEp) == 1
+
+
+def test_invalid_policies_runtime():
+    """test/runtime/Policies.go:1614-1657 ("Invalid Policies"): both imports
+    fail.  The truncated document is not JSON; the 50-port rule as the test
+    renders it (objects without commas) is not JSON either, and written as a
+    list it breaks the 40-port limit (rule_validation.go:317-319)."""
+    import json
+    with pytest.raises(json.JSONDecodeError):
+        json.loads('[{"endpointSelector": {"matchLabels":{"id.httpd1":""}},')
+    ports = "".join(f'{{"port": "{i}", "protocol": "tcp"}}' for i in range(50))
+    doc = ('[{"endpointSelector": {"matchLabels": {"foo": ""}}, "ingress": [{"fromEndpoints": '
+           '[{"matchLabels": {"reserved:host": ""}}, {"matchLabels": {"bar": ""}}], "toPorts": [{"ports": [%s]}]}]}]')
+    with pytest.raises(json.JSONDecodeError):
+        json.loads(doc % ports)
+    rules = json.loads(doc % ", ".join(f'{{"port": "{i}", "protocol": "tcp"}}' for i in range(50)))
+    with pytest.raises(ValueError) as ei:
+        R.Repository([R.Rule.from_json(r) for r in rules])
+    assert str(ei.value) == "too many ports, the max is 40"
