@@ -833,14 +833,44 @@ class Repository:
     def __init__(self, rules: Iterable[Rule] = (), cfg: Optional[PolicyConfig] = None):
         self.rules: list[Rule] = []
         self.cfg = cfg or PolicyConfig()
-        self.add_list(rules)
+        self.revision = 1  # NewPolicyRepository (repository.go:41-45)
+        rules = list(rules)
+        if rules:
+            self.add_list(rules)
 
-    def add_list(self, rules: Iterable[Rule]) -> None:
-        """AddListLocked after PolicyAdd's Sanitize (daemon/policy.go:171)."""
+    def add_list(self, rules: Iterable[Rule]) -> int:
+        """AddListLocked after PolicyAdd's Sanitize (daemon/policy.go:171):
+        all or nothing, one revision for the list."""
         rules = list(rules)
         for r in rules:
+            if r.EndpointSelector is None:  # Rule.Sanitize (rule_validation.go:39-41)
+                raise ValueError("rule cannot have nil EndpointSelector")
             r.sanitize()
         self.rules += rules
+        self.revision += 1
+        return self.revision
+
+    def add(self, rule: Rule) -> int:
+        """Add (repository.go:531-547): the new revision; a rule that does
+        not sanitize is refused and the revision stays."""
+        return self.add_list([rule])
+
+    def search(self, labels) -> list[Rule]:
+        """SearchRLocked (repository.go:495-505): the rules whose labels
+        contain every one of `labels`."""
+        need = set(labels)
+        return [r for r in self.rules if need <= set(r.Labels)]
+
+    def delete_by_labels(self, labels) -> tuple[int, int]:
+        """DeleteByLabelsLocked (repository.go:566-586): (revision, deleted);
+        the revision moves only when something was deleted."""
+        need = set(labels)
+        keep = [r for r in self.rules if not need <= set(r.Labels)]
+        n = len(self.rules) - len(keep)
+        if n:
+            self.rules = keep
+            self.revision += 1
+        return self.revision, n
 
     def get_rules_matching(self, labels) -> tuple[bool, bool]:
         """GetRulesMatching (:624-643): (ingress, egress) enforcement."""

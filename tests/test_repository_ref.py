@@ -165,3 +165,38 @@ def test_gpu_minikube_chain(gpu):
     pm.allow_keys(keys, ports)
     assert np.array_equal(pm.verdicts(t), exp_l4)
     pm.destroy()
+
+
+def test_add_search_delete():
+    """repository_test.go:29-112 (TestAddSearchDelete): revisions, search and
+    delete by rule labels."""
+    repo = R.Repository()
+    with pytest.raises(ValueError):
+        repo.add(R.Rule(EndpointSelector=None))
+    assert repo.revision == 1
+    lbls1, lbls2 = ("tag1", "tag2"), ("tag3",)
+    rule1 = R.Rule(R.EndpointSelector.of({"foo": ""}), Labels=lbls1)
+    rule2 = R.Rule(R.EndpointSelector.of({"bar": ""}), Labels=lbls1)
+    rule3 = R.Rule(R.EndpointSelector.of({"bar": ""}), Labels=lbls2)
+    assert repo.add(rule1) == 2 and repo.add(rule2) == 3
+    assert repo.search(lbls2) == []
+    assert repo.add(rule3) == 4
+    assert repo.search(lbls1) == [rule1, rule2] and repo.search(lbls2) == [rule3]
+    assert repo.delete_by_labels(lbls1) == (5, 2)
+    assert repo.delete_by_labels(lbls1) == (5, 0)
+    assert repo.search(lbls2) == [rule3]
+    assert repo.delete_by_labels(lbls2) == (6, 1)
+    assert repo.search(lbls2) == []
+
+
+def test_policy_command_labels():
+    """test/runtime/Policies.go:1658-1712 ("Policy command"): three rules
+    labelled key1..key3; each found by its label; deleting key2 leaves key1
+    and key3; deleting everything then succeeds with nothing left."""
+    doc = [{"endpointSelector": {"matchLabels": {"role": "frontend"}}, "labels": [k]} for k in ("key1", "key2", "key3")]
+    repo = R.Repository([R.Rule.from_json(r) for r in doc])
+    assert all(len(repo.search([k])) == 1 for k in ("key1", "key2", "key3"))
+    assert repo.delete_by_labels(["key2"])[1] == 1 and repo.search(["key2"]) == []
+    for k in ("key1", "key3"):
+        assert len(repo.search([k])) == 1 and repo.delete_by_labels([k])[1] == 1
+    assert repo.rules == [] and repo.delete_by_labels([])[1] == 0
