@@ -861,6 +861,11 @@ class Repository:
         need = set(labels)
         return [r for r in self.rules if need <= set(r.Labels)]
 
+    def contains_all(self, needed) -> bool:
+        """ContainsAllRLocked (repository.go:507-526): every label array of
+        `needed` contains the labels of some rule that has labels."""
+        return all(any(r.Labels and set(r.Labels) <= set(n) for r in self.rules) for n in needed)
+
     def delete_by_labels(self, labels) -> tuple[int, int]:
         """DeleteByLabelsLocked (repository.go:566-586): (revision, deleted);
         the revision moves only when something was deleted."""

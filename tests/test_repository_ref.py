@@ -200,3 +200,25 @@ def test_policy_command_labels():
     for k in ("key1", "key3"):
         assert len(repo.search([k])) == 1 and repo.delete_by_labels([k])[1] == 1
     assert repo.rules == [] and repo.delete_by_labels([])[1] == 0
+
+
+def test_contains_all():
+    """repository_test.go:114-191 (TestContainsAllRLocked); labels
+    NewLabel(key, value, source) written "source:key=value"."""
+    lab = lambda *ks: tuple(sorted(f"1:{k}={k}" for k in ks))  # noqa: E731
+    a = [lab("1", "2", "3"), lab("4", "5", "6"), lab("7", "8", "9")]
+    b = [lab("1", "2", "3"), lab("4", "5", "6")]
+    sel = lambda k: R.EndpointSelector.of({k: ""})  # noqa: E731
+    repo_a = R.Repository()
+    for lbls, k in zip(a, ("foo", "bar", "bar")):
+        repo_a.add(R.Rule(sel(k), Labels=lbls))
+    repo_b = R.Repository()
+    for lbls, k in zip(b, ("foo", "bar")):
+        repo_b.add(R.Rule(sel(k), Labels=lbls))
+    repo_empty = R.Repository()
+    repo_empty.add(R.Rule(sel("bar")))
+    assert repo_a.contains_all(b)
+    assert not repo_b.contains_all(a)
+    assert repo_a.contains_all([])
+    assert repo_empty.contains_all([])
+    assert not repo_empty.contains_all(a)
