@@ -222,3 +222,43 @@ def test_contains_all():
     assert repo_a.contains_all([])
     assert repo_empty.contains_all([])
     assert not repo_empty.contains_all(a)
+
+
+def _one(rule):
+    return R.Repository([R.Rule.from_json(rule)], CFG)
+
+
+def _L(*ks):
+    return {k.split("=")[0]: (k.split("=", 1)[1] if "=" in k else "") for k in ks}
+
+
+LOCAL_CLUSTER = f"k8s:{R.POLICY_LABEL_CLUSTER}=default"
+OTHER_CLUSTER = f"k8s:{R.POLICY_LABEL_CLUSTER}=non-local"  # rule_test.go:34-35
+
+
+def test_rule_can_reach():
+    """rule_test.go:38-115 (TestRuleCanReach): a FromEndpoints selector of two
+    labels, then FromRequires."""
+    r1 = _one({"endpointSelector": {"matchLabels": {"bar": ""}},
+               "ingress": [{"fromEndpoints": [{"matchLabels": {"foo": "", "foo2": ""}}]}]})
+    assert r1.can_reach_ingress(_L("foo", "foo2"), _L("bar")) == "allowed"
+    assert r1.can_reach_ingress(_L("foo"), _L("bar")) == "undecided"
+    r2 = _one({"endpointSelector": {"matchLabels": {"bar": ""}},
+               "ingress": [{"fromEndpoints": [{"matchLabels": {"foo": ""}}],
+                            "fromRequires": [{"matchLabels": {"baz": ""}}]}]})
+    assert r2.can_reach_ingress(_L("foo"), _L("bar")) == "denied"
+    assert r2.can_reach_ingress(_L("baz"), _L("bar")) == "undecided"
+    assert r2.can_reach_ingress(_L("foo", "baz"), _L("bar")) == "allowed"
+
+
+def test_rule_can_reach_entities():
+    """rule_test.go:1074-1166 (TestRuleCanReachFromEntity / ToEntity): world
+    and this cluster's workloads, not another cluster's."""
+    ing = _one({"endpointSelector": {"matchLabels": {"bar": ""}}, "ingress": [{"fromEntities": ["world", "cluster"]}]})
+    assert ing.can_reach_ingress(_L("reserved:world"), _L("bar")) == "allowed"
+    assert ing.can_reach_ingress(_L("foo", LOCAL_CLUSTER), _L("bar")) == "allowed"
+    assert ing.can_reach_ingress(_L("foo", OTHER_CLUSTER), _L("bar")) == "undecided"
+    eg = _one({"endpointSelector": {"matchLabels": {"bar": ""}}, "egress": [{"toEntities": ["world", "cluster"]}]})
+    assert eg.can_reach_egress(_L("bar"), _L("reserved:world")) == "allowed"
+    assert eg.can_reach_egress(_L("bar"), _L("foo", LOCAL_CLUSTER)) == "allowed"
+    assert eg.can_reach_egress(_L("bar"), _L("foo", OTHER_CLUSTER)) == "undecided"
