@@ -262,3 +262,37 @@ def test_rule_can_reach_entities():
     assert eg.can_reach_egress(_L("bar"), _L("reserved:world")) == "allowed"
     assert eg.can_reach_egress(_L("bar"), _L("foo", LOCAL_CLUSTER)) == "allowed"
     assert eg.can_reach_egress(_L("bar"), _L("foo", OTHER_CLUSTER)) == "undecided"
+
+
+ALLOW_ALL_CASES = [  # rule_test.go: (name, ingress rules of the rule selecting id=c, {dport: allowed from id=a})
+    ("IngressAllowAll:1504-1529", [{"fromEndpoints": [{}]}], {80: True, 90: True}),
+    ("IngressAllowAllL4Overlap:1531-1563", [{"fromEndpoints": [{}]},
+                                            {"toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}]}]}],
+     {80: True, 90: True}),
+    ("IngressL4AllowAll:1565-1599", [{"toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}]}]}],
+     {80: True, 90: False}),
+]
+
+
+@pytest.mark.parametrize("case", ALLOW_ALL_CASES, ids=lambda c: c[0])
+def test_ingress_allow_all_datapath(host, case):
+    """The checkIngress decisions for a → c (c selected) as c's policy map
+    decides them: the map state through the oracle and the compiled table."""
+    from test_policy_merge import _keys_ports
+    _, ingress, want = case
+    ids = {"a": 300, "c": 301}
+    cache = {300: {"id": "a"}, 301: {"id": "c"}}
+    repo = R.Repository([R.Rule.from_json({"endpointSelector": {"matchLabels": {"id": "c"}}, "ingress": ingress})],
+                        CFG)
+    keys, ports = _keys_ports(R.endpoint_policy_map_state(repo, cache[301], cache))
+    t = np.zeros(len(want), L4_TUPLE_DTYPE)
+    for i, dport in enumerate(want):
+        t[i] = (300, htons(dport), 6, N.CG_L4_F_INGRESS, 100)
+    exp = [want[d] for d in want]
+    assert [int(v) >= 0 for v in oracle.l4(keys, ports, t, oracle.L4_INGRESS)[0]] == exp
+    pm = host.policy_map()
+    pm.allow_keys(keys, ports)
+    assert [int(v) >= 0 for v in pm.eval_host_diag(t)] == exp
+    if case[0].startswith("IngressL4AllowAll"):  # :1589-1598
+        f = repo.resolve_l4_ingress_policy(cache[301])["80/TCP"]
+        assert (f.Port, f.Ingress, f.Endpoints) == (80, True, [R.WILDCARD])
