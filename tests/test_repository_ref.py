@@ -296,3 +296,38 @@ def test_ingress_allow_all_datapath(host, case):
     if case[0].startswith("IngressL4AllowAll"):  # :1589-1598
         f = repo.resolve_l4_ingress_policy(cache[301])["80/TCP"]
         assert (f.Port, f.Ingress, f.Endpoints) == (80, True, [R.WILDCARD])
+
+
+P80 = [{"ports": [{"port": "80", "protocol": "TCP"}]}]
+EGRESS_ALLOW_ALL_CASES = [  # rule_test.go: (name, egress rules of the id=a rule, {(dst, dport): allowed})
+    ("EgressAllowAll:1601-1622", [{"toEndpoints": [{}]}], {("c", 80): True, ("c", 90): True}),
+    ("EgressL4AllowAll:1623-1656", [{"toPorts": P80}], {("c", 80): True, ("c", 90): False}),
+    ("EgressL4AllowWorld:1657-1705", [{"toEntities": ["world"], "toPorts": P80}],
+     {("world", 80): True, ("world", 90): False, ("foo", 80): False, ("foo", 90): False}),
+    ("EgressL4AllowAllEntity:1706-1754", [{"toEntities": ["all"], "toPorts": P80}],
+     {("world", 80): True, ("world", 90): False, ("foo", 80): True, ("foo", 90): False}),
+    ("EgressL3AllowWorld:1755-1790", [{"toEntities": ["world"]}],
+     {("world", 80): True, ("world", 90): True, ("foo", 80): False, ("foo", 90): False}),
+    ("EgressL3AllowAllEntity:1791-1834", [{"toEntities": ["all"]}],
+     {("world", 80): True, ("world", 90): True, ("foo", 80): True, ("foo", 90): True}),
+]
+
+
+@pytest.mark.parametrize("case", EGRESS_ALLOW_ALL_CASES, ids=lambda c: c[0])
+def test_egress_allow_all_datapath(host, case):
+    """The checkEgress decisions from a as a's egress map decides them
+    (policy_can_egress: the oracle wrapper and the compiled table)."""
+    from test_policy_merge import _keys_ports
+    _, egress, want = case
+    ids = {"a": 300, "c": 301, "foo": 302, "world": R.RESERVED_WORLD}
+    cache = {300: {"id": "a"}, 301: {"id": "c"}, 302: {"foo": ""}, R.RESERVED_WORLD: {"reserved:world": ""}}
+    repo = R.Repository([R.Rule.from_json({"endpointSelector": {"matchLabels": {"id": "a"}}, "egress": egress})], CFG)
+    keys, ports = _keys_ports(R.endpoint_policy_map_state(repo, cache[300], cache))
+    t = np.zeros(len(want), L4_TUPLE_DTYPE)
+    for i, (dst, dport) in enumerate(want):
+        t[i] = (ids[dst], htons(dport), 6, 0, 100)
+    exp = list(want.values())
+    assert [int(v) >= 0 for v in oracle.l4(keys, ports, t, oracle.L4_EGRESS)[0]] == exp
+    pm = host.policy_map()
+    pm.allow_keys(keys, ports)
+    assert [int(v) >= 0 for v in pm.eval_host_diag(t)] == exp
