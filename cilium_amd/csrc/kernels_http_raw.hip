@@ -113,6 +113,48 @@ __device__ __forceinline__ bool tchar(uint32_t c) {
 }
 __device__ __forceinline__ uint32_t lower(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
+// http_parser.h HTTP_METHOD_MAP (v2.8): the methods s_req_method accepts
+// (case-sensitive; http_parse.cc known_method), in 64 slots of {bytes 0-3,
+// bytes 4-7, bytes 8-10 | length << 24, 0} under a perfect hash of (bytes
+// 0-3, length) — one 16-byte read and three compares per head.
+constexpr const char* kMethodNames[] = {
+    "DELETE", "GET",    "HEAD",     "POST",   "PUT",   "CONNECT",    "OPTIONS",    "TRACE",    "COPY",
+    "LOCK",   "MKCOL",  "MOVE",     "PROPFIND", "PROPPATCH", "SEARCH", "UNLOCK",   "BIND",     "REBIND",
+    "UNBIND", "ACL",    "REPORT",   "MKACTIVITY", "CHECKOUT", "MERGE", "M-SEARCH", "NOTIFY",   "SUBSCRIBE",
+    "UNSUBSCRIBE", "PATCH", "PURGE", "MKCALENDAR", "LINK",  "UNLINK"};
+constexpr uint32_t kMethodMaxLen = 11, kMethodSlots = 64;
+constexpr uint32_t method_slot(uint32_t w0, uint32_t len) { return ((w0 + len * 0x9E3779B1u) * 0x00C93D79u) >> 26; }
+struct MethodTab {
+  uint32_t e[kMethodSlots][4];
+  uint32_t collisions;
+};
+constexpr uint32_t cstr_len(const char* s) { return *s ? 1 + cstr_len(s + 1) : 0; }
+constexpr uint32_t cstr_word(const char* s, uint32_t len, uint32_t at) {
+  uint32_t w = 0;
+  for (uint32_t j = 0; j < 4; ++j)
+    if (at + j < len) w |= (uint32_t)(uint8_t)s[at + j] << (8 * j);
+  return w;
+}
+constexpr MethodTab make_method_tab() {
+  MethodTab t{};
+  for (const char* m : kMethodNames) {
+    const uint32_t n = cstr_len(m), w0 = cstr_word(m, n, 0);
+    uint32_t* e = t.e[method_slot(w0, n)];
+    t.collisions += e[2] != 0;
+    e[0] = w0;
+    e[1] = cstr_word(m, n, 4);
+    e[2] = cstr_word(m, n, 8) | n << 24;
+  }
+  return t;
+}
+constexpr MethodTab kMethodTabHost = make_method_tab();
+static_assert(kMethodTabHost.collisions == 0, "method_slot must place every method in its own slot");
+__device__ const MethodTab kMethodTab = make_method_tab();
+// the method's words (bytes past its length zero) against the table slot e
+__device__ __forceinline__ bool method_known(uint4 e, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t len) {
+  return len <= kMethodMaxLen && e.x == w0 && e.y == w1 && e.z == (w2 | len << 24);
+}
+
 // Four bytes that are all "plain": > 0x20 and not 0x7F (no control byte, no
 // SP / HTAB / CR): target and field-value bytes that need no decision.
 // hasless(q, 0x21) and haszero(q ^ 0x7F..) are exact presence tests.
@@ -215,9 +257,39 @@ __device__ __forceinline__ int field_of(const HttpRawDev& R, const Tabs& T, Head
   return -1;
 }
 
+// Content-Length (http_parser h_content_length) over the value's bytes from
+// its first non-OWS byte a to its line end e: digits, then SP only, the
+// value never past (ULLONG_MAX - 10) / 10 before a digit is appended.
+template <class Byte>
+__device__ __forceinline__ bool content_length_ok(uint32_t a, uint32_t e, Byte byte) {
+  uint64_t cl = 0;
+  uint32_t p = a;
+  for (; p < e; ++p) {
+    const uint32_t d = byte(p) - '0';
+    if (d > 9u) break;
+    if (cl > (~0ull - 10) / 10) return false;
+    cl = cl * 10 + d;
+  }
+  if (p == a) return false;
+  for (; p < e; ++p)
+    if (byte(p) != ' ') return false;
+  return true;
+}
+// "content-length" from a name's length and lowercased key words (first 8,
+// last 8 bytes: bytes 0-7 and 6-13 of the 14)
+__device__ __forceinline__ bool is_content_length(uint32_t nl, uint32_t lo0, uint32_t lo1, uint32_t hi0, uint32_t hi1) {
+  return nl == 14 && lo0 == 0x746E6F63u && lo1 == 0x2D746E65u && hi0 == 0x656C2D74u && hi1 == 0x6874676Eu;
+}
+// Four target bytes all in 0x21-0x7E (strict normal_url_char; '?' and '#'
+// are accepted as state changes)
+__device__ __forceinline__ bool all_url(uint32_t q) { return all_plain(q) && !(q & 0x80808080u); }
+
 // parse_head (http_parse.cc) for one head: the value span {start << 16 |
 // length} of every field it sets in sp[f * stride] (kAbsentSpan otherwise);
-// false = the codec rejects the head.
+// false = the codec or the connection manager stops the request before the
+// filter (http_parse.cc's rules: leading CR / LF skipped, http_parser's
+// methods, SP+, a '/' target of 0x21-0x7E bytes, HTTP/1.1, CR LF or a bare
+// LF at every line end, Content-Length digits, Host required).
 template <class Tabs>
 __device__ __forceinline__ bool parse_head(const HttpRawDev& R, const Tabs& T, HeadReader& hr, lds_u32* sp,
                                            uint32_t stride) {
@@ -225,35 +297,55 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, const Tabs& T, H
   const uint32_t n = hr.n;
   if (n > kRawMaxHead) return false;
   uint32_t k = 0;
+  while (k < n && (hr.at(k) == '\r' || hr.at(k) == '\n')) ++k;  // s_start_req
+  const uint32_t ms = k;
   while (k < n && tchar(hr.at(k))) ++k;  // method
-  if (k == 0 || k >= n || hr.at(k) != ' ') return false;
-  const uint32_t mlen = k++, t0 = k;
+  if (k == ms || k >= n || hr.at(k) != ' ') return false;
+  const uint32_t mlen = k - ms;
+  {
+    uint32_t w[3] = {0, 0, 0};
+    for (uint32_t j = 0; j < min(mlen, 12u); ++j) w[j >> 2] |= hr.at(ms + j) << (8 * (j & 3));
+    const uint32_t* e = kMethodTab.e[method_slot(w[0], mlen)];
+    if (!method_known(make_uint4(e[0], e[1], e[2], e[3]), w[0], w[1], w[2], mlen)) return false;
+  }
+  while (k < n && hr.at(k) == ' ') ++k;  // s_req_spaces_before_url
+  const uint32_t t0 = k;
   while (k < n) {  // request-target
-    if (k + 4 <= n && all_plain(hr.quad(k))) {
+    if (k + 4 <= n && all_url(hr.quad(k))) {
       k += 4;
       continue;
     }
     const uint32_t c = hr.at(k);
-    if (c <= 0x20 || c == 0x7F) break;
+    if (c <= 0x20 || c >= 0x7F) break;
     ++k;
   }
-  if (k == t0 || k >= n || hr.at(k) != ' ') return false;
+  if (k == t0 || hr.at(t0) != '/' || k >= n || hr.at(k) != ' ') return false;
   const uint32_t tlen = k - t0;
   ++k;
-  if (k + 10 > n) return false;  // "HTTP/" DIGIT "." DIGIT CRLF
-  {
-    const uint32_t d1 = hr.at(k + 5), d2 = hr.at(k + 7);
-    if (hr.at(k) != 'H' || hr.at(k + 1) != 'T' || hr.at(k + 2) != 'T' || hr.at(k + 3) != 'P' || hr.at(k + 4) != '/' ||
-        d1 < '0' || d1 > '9' || hr.at(k + 6) != '.' || d2 < '0' || d2 > '9' || hr.at(k + 8) != '\r' ||
-        hr.at(k + 9) != '\n')
-      return false;
+  if (k + 9 > n) return false;  // "HTTP/1.1" LF
+  if (hr.at(k) != 'H' || hr.at(k + 1) != 'T' || hr.at(k + 2) != 'T' || hr.at(k + 3) != 'P' || hr.at(k + 4) != '/' ||
+      hr.at(k + 5) != '1' || hr.at(k + 6) != '.' || hr.at(k + 7) != '1')
+    return false;
+  k += 8;
+  if (hr.at(k) == '\n') {
+    k += 1;
+  } else if (hr.at(k) == '\r' && k + 1 < n && hr.at(k + 1) == '\n') {
+    k += 2;
+  } else {
+    return false;
   }
-  k += 10;
-  bool have_host = false;
+  bool have_host = false, have_cl = false;
   uint32_t auth = kAbsentSpan;
   while (true) {
-    if (k + 1 >= n) return false;  // no CRLF left: incomplete head
-    if (hr.at(k) == '\r' && hr.at(k + 1) == '\n') break;  // empty line: end of head
+    if (k >= n) return false;  // no empty line: incomplete head
+    {
+      const uint32_t x0 = hr.at(k);
+      if (x0 == '\n') break;  // empty line: end of head
+      if (x0 == '\r') {
+        if (k + 1 < n && hr.at(k + 1) == '\n') break;
+        return false;
+      }
+    }
     uint32_t c = k, h = kRawFnvInit;
     for (bool more = true; more && c < n;) {  // a quad at a time
       const uint32_t q = hr.quad(c);
@@ -269,8 +361,8 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, const Tabs& T, H
     }
     if (c == k || c >= n || hr.at(c) != ':') return false;
     const uint32_t nl = c - k;
-    uint32_t v = c + 1, first = kAbsentSpan, lend = v;
-    while (true) {  // field-value up to CRLF: IS_HEADER_CHAR, OWS trimmed
+    uint32_t v = c + 1, first = kAbsentSpan, lend = v, nxt;
+    while (true) {  // field-value up to the line end: IS_HEADER_CHAR, OWS trimmed
       if (v + 4 <= n && all_plain(hr.quad(v))) {
         if (first == kAbsentSpan) first = v;
         v += 4;
@@ -279,8 +371,15 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, const Tabs& T, H
       }
       if (v >= n) return false;
       const uint32_t x = hr.at(v);
+      if (x == '\n') {  // a bare LF ends the line
+        nxt = v + 1;
+        break;
+      }
       if (x == '\r') {
-        if (v + 1 < n && hr.at(v + 1) == '\n') break;
+        if (v + 1 < n && hr.at(v + 1) == '\n') {
+          nxt = v + 2;
+          break;
+        }
         return false;
       }
       if (!(x == '\t' || (x >= 0x20 && x != 0x7F))) return false;
@@ -291,20 +390,27 @@ __device__ __forceinline__ bool parse_head(const HttpRawDev& R, const Tabs& T, H
       ++v;
     }
     const uint32_t span = first == kAbsentSpan ? (v << 16) : (first << 16 | (lend - first));
-    const bool is_host = nl == 4 && lower(hr.at(k)) == 'h' && lower(hr.at(k + 1)) == 'o' &&
-                         lower(hr.at(k + 2)) == 's' && lower(hr.at(k + 3)) == 't';
+    auto lw = [&](uint32_t at) { return lower(hr.at(at)); };
+    const bool is_host = nl == 4 && lw(k) == 'h' && lw(k + 1) == 'o' && lw(k + 2) == 's' && lw(k + 3) == 't';
     if (is_host) {
       if (!have_host) auth = span;  // the first value is the one the filter sees
       have_host = true;
     } else {
+      if (nl == 14 && first != kAbsentSpan) {  // h_content_length
+        bool cl = true;
+        for (uint32_t j = 0; j < 14 && cl; ++j) cl = lw(k + j) == (uint32_t)"content-length"[j];
+        if (cl && (have_cl || !content_length_ok(first, v, [&](uint32_t p) { return hr.at(p); }))) return false;
+        have_cl |= cl;
+      }
       const int f = field_of(R, T, hr, h, nl, k);
       if (f >= 0 && sp[f * stride] == kAbsentSpan) sp[f * stride] = span;  // first value wins
     }
-    k = v + 2;
+    k = nxt;
   }
-  if (R.f_method >= 0) sp[R.f_method * stride] = mlen;
+  if (!have_host) return false;  // the connection manager answers 400 without Host
+  if (R.f_method >= 0) sp[R.f_method * stride] = ms << 16 | mlen;
   if (R.f_path >= 0) sp[R.f_path * stride] = t0 << 16 | tlen;
-  if (R.f_authority >= 0 && have_host) sp[R.f_authority * stride] = auth;
+  if (R.f_authority >= 0) sp[R.f_authority * stride] = auth;
   return true;
 }
 
@@ -322,7 +428,7 @@ __device__ __forceinline__ uint32_t special4(uint32_t x) {
   const uint32_t lt = ~(((x & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | x) & 0x80808080u;  // byte < 0x21
   const uint32_t t = x ^ 0x7F7F7F7Fu;
   const uint32_t del = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;  // byte == 0x7F
-  return pack4(lt | del);
+  return pack4(lt | del | (x & 0x80808080u));  // bytes >= 0x80 end a target (strict URL bytes)
 }
 // 16 stage bytes per lane per round (rounds wave-uniform, so a lane's pair
 // partner is always active): the half-words of a mask word come from lanes
@@ -469,40 +575,54 @@ __device__ __forceinline__ uint32_t walked_len(const HttpRawDev& R, const Parsed
 
 // parse_head (http_parse.cc semantics) for a head inside the stage, bytes
 // [hs, he), over the structural masks.  Reads are issued in batches: the
-// request line's delimiter bytes and version in one round trip, then per
-// header line its first bytes, the name's end byte and key words and the
-// value's first two specials in one.
+// request line's delimiter bytes, method words and version in one round trip,
+// then per header line its first bytes, the name's end byte and key words and
+// the value's first two specials in one.  The leniencies of http_parser that
+// cost a loop (CR / LF before the request line, more than one SP before the
+// target) are found by bit tests on the masks and only then walked.
 template <class Tabs>
 __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
-                                                const lds_u32* msp, const lds_u32* mnt, uint32_t hs, uint32_t he,
-                                                lds_u32* sp, uint32_t stride, Parsed& P) {
+                                                const lds_u32* msp, const lds_u32* mnt, const lds_u32* mtab,
+                                                uint32_t hs, uint32_t he, lds_u32* sp, uint32_t stride, Parsed& P) {
   RAW_PSTART;
   P.present = P.vsum = 0;
   if (he - hs > kRawMaxHead) return false;
   const MaskWin W = load_win(msp, mnt, hs);
   auto nS = [&](uint32_t p) { return p >= he ? he : wnext(W.s, W.base, msp, p, he); };
   auto nN = [&](uint32_t p) { return p >= he ? he : wnext(W.n, W.base, mnt, p, he); };
-  const uint32_t m = nN(hs);  // method: a tchar run, then SP
-  const uint32_t t0 = m + 1;
-  const uint32_t te = nS(t0);  // request-target: plain bytes, then SP
-  {
-    // SP at m; " HTTP/" DIGIT "." DIGIT CRLF at te
-    const uint32_t bm = sbyte(st, m), q0 = squad(st, te), q1 = squad(st, te + 4), q2 = squad(st, te + 8);
-    if (m == hs || m >= he || te == t0 || te + 11 > he) return false;
-    if (bm != ' ' || q0 != 0x54544820u || (q1 & 0xFFFFu) != 0x2F50u || (q1 >> 24) != '.' ||
-        (q1 >> 16 & 0xFFu) - '0' > 9u || (q2 & 0xFFu) - '0' > 9u || (q2 >> 8 & 0xFFFFu) != 0x0A0Du)
-      return false;
+  uint32_t ms = hs;  // s_start_req: CR / LF before the method are skipped
+  if (hs < he && wbit(W.s, W.base, msp, hs))
+    while (ms < he && (sbyte(st, ms) == '\r' || sbyte(st, ms) == '\n')) ++ms;
+  const uint32_t m = nN(ms);  // method: a tchar run, then SP
+  uint32_t t0 = m + 1;
+  uint32_t te = nS(t0);  // request-target: plain bytes, then SP
+  if (te == t0 && t0 < he) {  // a special first: more SP (s_req_spaces_before_url) or a rejected head
+    while (t0 < he && sbyte(st, t0) == ' ') ++t0;
+    te = nS(t0);
   }
+  // SP at m; method words; '/' at t0; " HTTP/1.1" then CR LF or LF at te
+  const uint32_t bm = sbyte(st, m), bt = sbyte(st, t0), q0 = squad(st, te), q1 = squad(st, te + 4),
+                 q2 = squad(st, te + 8), a0 = squad(st, ms), a1 = squad(st, ms + 4), a2 = squad(st, ms + 8);
+  const uint32_t ml = m - ms;
+  const uint32_t w0 = keep_bytes(a0, ml), w1 = ml > 4 ? keep_bytes(a1, ml - 4) : 0u,
+                 w2 = ml > 8 ? keep_bytes(a2, ml - 8) : 0u;
+  const uint4 me = to_uint4(*(const lds_v4*)(mtab + 4 * method_slot(w0, ml)));
+  const bool lf_only = (q2 >> 8 & 0xFFu) == '\n';
+  uint32_t k = te + (lf_only ? 10u : 11u);
+  if (m == ms || m >= he || te == t0 || k > he) return false;
+  if (bm != ' ' || bt != '/' || q0 != 0x54544820u || q1 != 0x2E312F50u || (q2 & 0xFFu) != '1' ||
+      (!lf_only && (q2 >> 8 & 0xFFFFu) != 0x0A0Du))
+    return false;
   RAW_PMARK(0);  // window, request line
-  uint32_t k = te + 11;
-  bool have_host = false;
+  bool have_host = false, have_cl = false;
   uint32_t auth = kAbsentSpan;
   while (true) {
-    if (k + 1 >= he) return false;  // no CRLF left: incomplete head
-    // a line starting with a special byte is the empty line (CRLF) or a
-    // rejected head: one bit test, no searches
+    if (k >= he) return false;  // no empty line: incomplete head
+    // a line starting with a special byte is the empty line (CR LF or a
+    // bare LF) or a rejected head: one bit test, no searches
     if (wbit(W.s, W.base, msp, k)) {
-      if ((squad(st, k) & 0xFFFFu) == 0x0A0Du) break;  // empty line: end of head
+      const uint32_t q = squad(st, k);
+      if ((q & 0xFFu) == '\n' || ((q & 0xFFFFu) == 0x0A0Du && k + 1 < he)) break;  // empty line: end of head
       return false;
     }
     const uint32_t c = nN(k);       // name: a tchar run, then ':'
@@ -513,8 +633,9 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
     RAW_PMARK(1);  // a line's searches and reads
     if (c == k || c >= he || bc != ':') return false;
     const uint32_t nl = c - k;
-    // field-value to CRLF: IS_HEADER_CHAR, OWS trimmed
-    uint32_t v = c + 1, first = kAbsentSpan, lend = v, s = s1, q = q1;
+    // field-value to the line end: IS_HEADER_CHAR (bytes >= 0x80 are
+    // specials of the mask that belong to the value), OWS trimmed
+    uint32_t v = c + 1, first = kAbsentSpan, lend = v, s = s1, q = q1, nxt;
     for (uint32_t it = 0;; ++it) {
       if (s > v) {
         if (first == kAbsentSpan) first = v;
@@ -522,7 +643,11 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
       }
       if (s >= he) return false;
       const uint32_t x = q & 0xFFu;
-      if (x == ' ' || x == '\t') {
+      if (x == ' ' || x == '\t' || x >= 0x80) {
+        if (x >= 0x80) {
+          if (first == kAbsentSpan) first = s;
+          lend = s + 1;
+        }
         v = s + 1;
         if (it == 0) {
           s = s2;
@@ -533,7 +658,14 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
         }
         continue;
       }
-      if (x == '\r' && s + 1 < he && (q >> 8 & 0xFFu) == '\n') break;
+      if (x == '\n') {  // a bare LF ends the line
+        nxt = s + 1;
+        break;
+      }
+      if (x == '\r' && s + 1 < he && (q >> 8 & 0xFFu) == '\n') {
+        nxt = s + 2;
+        break;
+      }
       return false;
     }
     RAW_PMARK(2);  // value loop
@@ -547,16 +679,23 @@ __device__ __forceinline__ bool parse_head_fast(const HttpRawDev& R, const Tabs&
       const uint32_t lo0 = lower4(keep_bytes(qk, nl));
       const uint32_t lo1 = nl > 4 ? lower4(keep_bytes(r1, nl - 4)) : 0u;
       const uint32_t hi0 = nl > 8 ? lower4(r2) : 0u, hi1 = nl > 8 ? lower4(r3) : 0u;
+      if (is_content_length(nl, lo0, lo1, hi0, hi1) && first != kAbsentSpan) {  // h_content_length
+        if (have_cl || !content_length_ok(first, s, [&](uint32_t p) { return sbyte(st, p); })) return false;
+        have_cl = true;
+      }
       const int f = field_of_words(R, T, st, k, nl, lo0, lo1, hi0, hi1);
       if (f >= 0 && !(P.present >> f & 1u)) P.set(sp, stride, (uint32_t)f, span);  // first value wins
     }
-    k = s + 2;
+    k = nxt;
     RAW_PMARK(3);  // name key, span
   }
   RAW_PMARK(4);
-  if (R.f_method >= 0) P.set(sp, stride, (uint32_t)R.f_method, m - hs);
+  // the method (read above, under the header lines) and Host: the
+  // connection manager answers 400 without Host
+  if (!have_host || !method_known(me, w0, w1, w2, ml)) return false;
+  if (R.f_method >= 0) P.set(sp, stride, (uint32_t)R.f_method, (ms - hs) << 16 | ml);
   if (R.f_path >= 0) P.set(sp, stride, (uint32_t)R.f_path, (t0 - hs) << 16 | (te - t0));
-  if (R.f_authority >= 0 && have_host) P.set(sp, stride, (uint32_t)R.f_authority, auth);
+  if (R.f_authority >= 0) P.set(sp, stride, (uint32_t)R.f_authority, auth);
   return true;
 }
 
@@ -720,7 +859,8 @@ __device__ __forceinline__ uint32_t group_of(const HttpRawDev& R, uint32_t prog)
 
 // Dynamic LDS of the scan kernel: [spans: nfields × 256 u32][4 wave stages ×
 // kStage bytes][4 wave mask pairs × 2 × kStage bits][tchar table: 256 B]
-// [bucket counters: nkeys u32, when they fit (lds_keys)].
+// [method table: 64 × 16 B][bucket counters: nkeys u32, when they fit
+// (lds_keys)].
 __device__ __forceinline__ lds_u8* wave_stage(lds_u32* lds, uint32_t F, uint32_t wave) {
   return (lds_u8*)(lds + F * kRawThreads) + wave * kStage;
 }
@@ -728,7 +868,13 @@ __device__ __forceinline__ lds_u32* wave_masks(lds_u32* lds, uint32_t F, uint32_
   return (lds_u32*)((lds_u8*)(lds + F * kRawThreads) + kRawWaves * kStage) + wave * 2 * kMaskWords;
 }
 __device__ __forceinline__ lds_u8* tchar_table(lds_u32* lds, uint32_t F) { return (lds_u8*)wave_masks(lds, F, kRawWaves); }
-__device__ __forceinline__ lds_u32* key_counters(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + 256); }
+// the method table (kMethodTab) follows the 256-byte tchar table
+constexpr uint32_t kTctBytes = 256 + kMethodSlots * 16;
+__device__ __forceinline__ lds_u32* method_table(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + 256); }
+__device__ __forceinline__ void stage_methods(lds_u32* mt) {
+  for (uint32_t j = threadIdx.x; j < kMethodSlots * 4; j += blockDim.x) mt[j] = kMethodTab.e[j >> 2][j & 3];
+}
+__device__ __forceinline__ lds_u32* key_counters(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + kTctBytes); }
 // [name keys: 8 u32 per slot][field slots: 4 u32 per slot][names, u32
 // words][program hash keys][values] after the key counters, when they fit
 // (lds_tables): the lookups every header line and request makes, at LDS
@@ -986,6 +1132,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   if (lds_keys)
     for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) lk[k] = 0;
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = kLists ? list_stop(b, R.raw_values) : !tchar(b);
+  const lds_u32* mtab = method_table(lds, F);
+  if (!kLists) stage_methods(method_table(lds, F));
   // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
@@ -1052,7 +1200,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
         const uint32_t hs = (uint32_t)(ga - sbase);
         Parsed P;
         const bool ok = kLists ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
-                               : parse_head_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P);
+                               : parse_head_fast(R, T, stage, masks, masks + kMaskWords, mtab, hs, hs + hn, sp, kRawThreads, P);
         RAW_CLK(c3);
         if (!ok) {
           bad = 1;
@@ -1396,7 +1544,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_build_kernel(
 //                        walked one lane each over the tables in HBM
 // Dynamic LDS of raw_scan_dl_kernel: raw_scan_kernel's without the bucket
 // counters (the lookup tables follow the tchar table).
-__device__ __forceinline__ lds_u32* raw_tables(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + 256); }
+__device__ __forceinline__ lds_u32* raw_tables(lds_u32* lds, uint32_t F) { return (lds_u32*)(tchar_table(lds, F) + kTctBytes); }
 
 // ---- the walked string, class-coded, straight into its tile slot ---------
 // http_pack.cc's string: the values of the fields up to the last present
@@ -1551,6 +1699,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
   lds_u32* masks = wave_masks(lds, F, wave);
   lds_u8* tct = tchar_table(lds, F);
   for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) tct[b] = kLists ? list_stop(b, R.raw_values) : !tchar(b);
+  const lds_u32* mtab = method_table(lds, F);
+  if (!kLists) stage_methods(method_table(lds, F));
   // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
@@ -1600,7 +1750,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
     P.present = P.vsum = 0;
     if (live && !defer && prog != kProgDeny) {
       const bool ok = kLists ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
-                             : parse_head_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P);
+                             : parse_head_fast(R, T, stage, masks, masks + kMaskWords, mtab, hs, hs + hn, sp, kRawThreads, P);
       if (!ok) {
         flags |= CG_HTTP_F_MALFORMED;
       } else if (walked_t(R, T, prog)) {
@@ -1889,7 +2039,7 @@ unsigned grid_for(size_t n, int cus, unsigned per_cu) {
 bool lds_tables_fit(const HttpRawDev& R) { return raw_tables_lds_words(R) * 4 <= 8 * 1024; }
 size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
-  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + kRawWaves * (size_t)kStage + kRawWaves * 2 * (kStage / 8) + 256 +
+  return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + kRawWaves * (size_t)kStage + kRawWaves * 2 * (kStage / 8) + kTctBytes +
          (lds_keys ? nk * 4 : 0) + (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 : 0) +
          (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
 }

@@ -1186,8 +1186,117 @@ def go_regex_kats() -> dict:
             "matches": [{"pattern": p, "input": H(s), "match": m} for p, s, m in matches]}
 
 
+# ------------------------------------------------------ HTTP/1 codec KATs --
+def _hl(*pairs):
+    return [[k, v] for k, v in pairs]
+
+
+_NIGHTLY = ("GET /public HTTP/1.1\r\nhost: 10.10.0.5:8888\r\nuser-agent: curl/7.54.0\r\naccept: */*\r\n"
+            "UID: 5fa3c1d2\r\ncontent-length: 0\r\n")
+
+
+def http1_codec_kats() -> dict:
+    """Raw heads → the header list cilium.l7policy sees, or null when the
+    codec (http_parser) or the connection manager stops the request first.
+    Expected values are written by hand from the rules oracle/http1_ref.py
+    lists (http_parser's states and Envoy's checks), not computed.  The
+    first case is the reference's own traffic: test/k8sT/Nightly.go:247-254
+    sends this head through `echo -e "%s"` (:290), whose trailing newline
+    makes the head end CR LF, LF."""
+    ok = lambda *extra: _hl((":method", "GET"), (":path", "/x"), (":authority", "a"), *extra)
+    cases = [
+        ("nightly echo -e head (bare LF ends the head)", _NIGHTLY + "\n",
+         _hl((":method", "GET"), (":path", "/public"), (":authority", "10.10.0.5:8888"), ("user-agent", "curl/7.54.0"),
+             ("accept", "*/*"), ("UID", "5fa3c1d2"), ("content-length", "0")), "test/k8sT/Nightly.go:247-254,290"),
+        ("nightly head without the newline: incomplete", _NIGHTLY, None, "test/k8sT/Nightly.go:247-254"),
+        ("CRLF head", "GET /v1/ HTTP/1.1\r\nHost: deathstar\r\nX-Has-Force: true\r\n\r\n",
+         _hl((":method", "GET"), (":path", "/v1/"), (":authority", "deathstar"), ("X-Has-Force", "true")), "RFC 7230"),
+        ("bare LF everywhere", "GET /x HTTP/1.1\nHost: a\nA: 1\n\n", ok(("A", "1")), "s_req_http_minor, s_header_value LF"),
+        ("LF after the request line only", "GET /x HTTP/1.1\nHost: a\r\n\r\n", ok(), "s_req_http_minor LF"),
+        ("mixed line ends", "GET /x HTTP/1.1\r\nHost: a\nB: 2\r\n\n", ok(("B", "2")), "s_header_value LF"),
+        ("CRLF then LF empty line", "GET /x HTTP/1.1\r\nHost: a\r\n\n", ok(), "s_header_field_start LF"),
+        ("CR without LF in the request line", "GET /x HTTP/1.1\rHost: a\r\n\r\n", None, "s_req_line_almost_done"),
+        ("CR without LF ending a header", "GET /x HTTP/1.1\r\nHost: a\r\nX: 1\r\r\n\r\n", None, "s_header_almost_done"),
+        ("CR CR LF as the empty line", "GET /x HTTP/1.1\r\nHost: a\r\n\r\r\n", None, "s_headers_almost_done"),
+        ("CR inside a value", "GET /x HTTP/1.1\r\nHost: a\r\nX: 1\r2\r\n\r\n", None, "s_header_almost_done"),
+        ("CR LF before the request line", "\r\n\r\nGET /x HTTP/1.1\r\nHost: a\r\n\r\n", ok(), "s_start_req"),
+        ("LF and CR before the request line", "\n\r\rGET /x HTTP/1.1\r\nHost: a\r\n\r\n", ok(), "s_start_req"),
+        ("only line ends", "\r\n\r\n", None, "s_start_req"),
+        ("empty head", "", None, "s_start_req"),
+        ("two SP before the target", "GET   /x HTTP/1.1\r\nHost: a\r\n\r\n", ok(), "s_req_spaces_before_url"),
+        ("body after the head ignored", "GET /x HTTP/1.1\r\nHost: a\r\nEmpty:\r\n\r\nBODY\r\n\r\n", ok(("Empty", "")),
+         "on_headers_complete"),
+        ("OWS, repeated Host", "PUT /a?b=c HTTP/1.1\r\nhost:  h1 \r\nHOST: h2\r\nx:\t v \t\r\n\r\n",
+         _hl((":method", "PUT"), (":path", "/a?b=c"), (":authority", "h1"), ("x", "v")), "s_header_value_discard_ws"),
+        ("query and fragment", "GET /x?y=1&z#frag?# HTTP/1.1\r\nHost: a\r\n\r\n",
+         _hl((":method", "GET"), (":path", "/x?y=1&z#frag?#"), (":authority", "a")), "parse_url_char"),
+        ("lowercase method", "get /x HTTP/1.1\r\nHost: a\r\n\r\n", None, "s_start_req (IS_ALPHA, uppercase switch)"),
+        ("unknown method", "FOO /x HTTP/1.1\r\nHost: a\r\n\r\n", None, "s_req_method"),
+        ("method prefix", "POS /x HTTP/1.1\r\nHost: a\r\n\r\n", None, "s_req_method"),
+        ("method extended", "PUTX /x HTTP/1.1\r\nHost: a\r\n\r\n", None, "s_req_method"),
+        ("token method not in the table", "G@T /x HTTP/1.1\r\nHost: a\r\n\r\n", None, "s_req_method"),
+        ("M-SEARCH", "M-SEARCH /x HTTP/1.1\r\nHost: a\r\n\r\n",
+         _hl((":method", "M-SEARCH"), (":path", "/x"), (":authority", "a")), "HTTP_METHOD_MAP"),
+        ("UNSUBSCRIBE", "UNSUBSCRIBE /x HTTP/1.1\r\nHost: a\r\n\r\n",
+         _hl((":method", "UNSUBSCRIBE"), (":path", "/x"), (":authority", "a")), "HTTP_METHOD_MAP"),
+        ("MKCALENDAR", "MKCALENDAR /x HTTP/1.1\r\nHost: a\r\n\r\n",
+         _hl((":method", "MKCALENDAR"), (":path", "/x"), (":authority", "a")), "HTTP_METHOD_MAP"),
+        ("PROPPATCH", "PROPPATCH /x HTTP/1.1\r\nHost: a\r\n\r\n",
+         _hl((":method", "PROPPATCH"), (":path", "/x"), (":authority", "a")), "HTTP_METHOD_MAP"),
+        ("HTTP/1.0", "GET /x HTTP/1.0\r\nHost: a\r\n\r\n", None,
+         "accept_http_10 off: pkg/envoy/envoy/api/v2/core/protocol.pb.go:108-112, pkg/envoy/server.go:172-215"),
+        ("HTTP/0.9 request line", "GET /x\r\nHost: a\r\n\r\n", None, "protocol.pb.go:108-112"),
+        ("HTTP/2.0 in an HTTP/1 request line", "GET /x HTTP/2.0\r\nHost: a\r\n\r\n", None, "codec: not 1.1 is 1.0"),
+        ("version without a dot", "GET /x HTTP/11\r\nHost: a\r\n\r\n", None, "s_req_http_major"),
+        ("SP after the version", "GET /x HTTP/1.1 \r\nHost: a\r\n\r\n", None, "s_req_http_minor"),
+        ("lowercase http", "GET /x http/1.1\r\nHost: a\r\n\r\n", None, "s_req_http_start"),
+        ("no Host", "GET /x HTTP/1.1\r\n\r\n", None, "conn_manager_impl: 400 without Host"),
+        ("no Host, other headers", "GET /x HTTP/1.1\r\nX-Host: a\r\n\r\n", None, "conn_manager_impl"),
+        ("empty Host value", "GET /x HTTP/1.1\r\nHost:\r\n\r\n",
+         _hl((":method", "GET"), (":path", "/x"), (":authority", "")), "conn_manager_impl"),
+        ("asterisk-form", "OPTIONS * HTTP/1.1\r\nHost: a\r\n\r\n", None, "conn_manager_impl: 404 non-relative path"),
+        ("absolute-form", "GET http://a/x HTTP/1.1\r\nHost: a\r\n\r\n", None, "conn_manager_impl: 404"),
+        ("authority-form", "CONNECT a:443 HTTP/1.1\r\nHost: a\r\n\r\n", None, "conn_manager_impl: 404"),
+        ("UTF-8 in the target", "GET /caf\xc3\xa9 HTTP/1.1\r\nHost: a\r\n\r\n", None, "strict normal_url_char"),
+        ("HTAB in the target", "GET /x\ty HTTP/1.1\r\nHost: a\r\n\r\n", None, "strict parse_url_char"),
+        ("DEL in the target", "GET /x\x7fy HTTP/1.1\r\nHost: a\r\n\r\n", None, "normal_url_char"),
+        ("UTF-8 in a value", "GET /x HTTP/1.1\r\nHost: a\r\nX: caf\xc3\xa9 \xff\r\n\r\n", ok(("X", "caf\xc3\xa9 \xff")),
+         "IS_HEADER_CHAR"),
+        ("control byte in a value", "GET /x HTTP/1.1\r\nHost: a\r\nA: v\x01w\r\n\r\n", None, "IS_HEADER_CHAR"),
+        ("space in a name", "GET /x HTTP/1.1\r\nHost: a\r\nBad Name: v\r\n\r\n", None, "strict TOKEN"),
+        ("space before the colon", "GET /x HTTP/1.1\r\nHost: a\r\nX : v\r\n\r\n", None, "s_header_field"),
+        ("empty name", "GET /x HTTP/1.1\r\nHost: a\r\n: v\r\n\r\n", None, "s_header_field_start"),
+        ("obs-fold (unpinned: rejected here)", "GET /x HTTP/1.1\r\nHost: a\r\nX: 1\r\n 2\r\n\r\n", None,
+         "s_header_value_lws (joined by http_parser; see DESIGN §4)"),
+        ("Content-Length", "POST /x HTTP/1.1\r\nHost: a\r\nContent-Length: 12\r\n\r\n",
+         _hl((":method", "POST"), (":path", "/x"), (":authority", "a"), ("Content-Length", "12")), "h_content_length"),
+        ("Content-Length trailing SP", "GET /x HTTP/1.1\r\nHost: a\r\ncontent-LENGTH:  0012  \r\n\r\n",
+         ok(("content-LENGTH", "0012")), "h_content_length_ws"),
+        ("Content-Length trailing HTAB", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: 12\t\r\n\r\n", None,
+         "h_content_length_ws"),
+        ("Content-Length not a number", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: 1x\r\n\r\n", None,
+         "h_content_length"),
+        ("Content-Length inner SP", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: 1 2\r\n\r\n", None,
+         "h_content_length_ws"),
+        ("Content-Length twice", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: 1\r\nContent-Length: 1\r\n\r\n", None,
+         "HPE_UNEXPECTED_CONTENT_LENGTH"),
+        ("empty Content-Length, then one", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: \r\nContent-Length: 5\r\n\r\n",
+         ok(("Content-Length", ""), ("Content-Length", "5")), "s_header_value_discard_lws"),
+        ("Content-Length at the limit", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: 18446744073709551609\r\n\r\n",
+         ok(("Content-Length", "18446744073709551609")), "h_content_length overflow test"),
+        ("Content-Length past the limit", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Length: 18446744073709551610\r\n\r\n",
+         None, "h_content_length overflow test"),
+        ("Content-Lengths (other name)", "GET /x HTTP/1.1\r\nHost: a\r\nContent-Lengths: x\r\n\r\n",
+         ok(("Content-Lengths", "x")), "h_general"),
+        ("no empty line", "GET /x HTTP/1.1\r\nHost: a\r\nA: 1\r\n", None, "incomplete"),
+    ]
+    return {"source": "http_parser v2.8 states (strict) and Envoy conn_manager_impl checks, restated in "
+                      "oracle/http1_ref.py; expected values written by hand",
+            "cases": [{"name": n, "raw": raw, "expect": exp, "rule": rule} for n, raw, exp, rule in cases]}
+
+
 def main():
-    files = {"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
+    files = {"http1_codec_kat.json": http1_codec_kats(),"proxylib_kat.json": proxylib_kats(), "http_kat.json": http_kats(), "translation_kat.json": translation_kats(),
              "kafka_kat.json": kafka_kats(), "kafka_wire_kat.json": kafka_wire_kats(), "lpm_kat.json": lpm_kats(), "regex_vectors.json": regex_vectors(),
              "memcache_kat.json": memcache_kats(), "cassandra_kat.json": cassandra_kats(),
              "l4_merge_kat.json": l4_merge_kats(), "policies_e2e_kat.json": policies_e2e_kats(),

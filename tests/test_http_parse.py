@@ -1,9 +1,16 @@
 """HTTP/1.x request heads from raw bytes → the packer.
 
-The codec is Envoy's http_parser (external; parity unpinned): the cases are
-written from RFC 7230's request-line / header-field grammar.  The product
-parser (csrc/http_parse.cc) is checked against oracle/http1_ref.py, and the
-raw path's verdicts against the header-list path's on the same requests."""
+What stands before the filter is Envoy's http_parser plus the connection
+manager's checks (external, not vendored).  tests/golden/http1_codec_kat.json
+holds 60 hand-written vectors of their rules (bare LF line ends, the method
+table, HTTP/1.1 only, Host required, strict target bytes, Content-Length),
+led by the reference's own Nightly.go head with `echo -e`'s trailing LF.  The
+oracle (oracle/http1_ref.py) and the product parser (csrc/http_parse.cc) are
+checked against them and against each other on mutated heads; the raw path's
+verdicts against the header-list path's on the same requests."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -12,22 +19,16 @@ from cilium_amd import synth
 from cilium_amd.classifier import Classifier
 from oracle.http1_ref import parse_head
 
-CASES = [
-    (b"GET /v1/ HTTP/1.1\r\nHost: deathstar\r\nX-Has-Force: true\r\n\r\n",
-     [(b":method", b"GET"), (b":path", b"/v1/"), (b":authority", b"deathstar"), (b"X-Has-Force", b"true")]),
-    (b"PUT /a?b=c HTTP/1.0\r\nhost:  h1 \r\nHOST: h2\r\nx:\t v \t\r\n\r\n",
-     [(b":method", b"PUT"), (b":path", b"/a?b=c"), (b":authority", b"h1"), (b"x", b"v")]),
-    (b"DELETE * HTTP/1.1\r\n\r\n", [(b":method", b"DELETE"), (b":path", b"*")]),
-    (b"GET /x HTTP/1.1\r\nEmpty:\r\n\r\nBODY", [(b":method", b"GET"), (b":path", b"/x"), (b"Empty", b"")]),
-    (b"GET /x HTTP/1.1\r\nA: 1\r\n", None),            # no final CRLF
-    (b"GET /x HTTP/1.1\nA: 1\n\n", None),              # bare LF
-    (b"G@T /x HTTP/1.1\r\n\r\n", None),                 # method not a token
-    (b"GET  /x HTTP/1.1\r\n\r\n", None),                # empty target
-    (b"GET /x HTTP/11\r\n\r\n", None),                  # bad version
-    (b"GET /x HTTP/1.1\r\nBad Name: v\r\n\r\n", None),  # space in the name
-    (b"GET /x HTTP/1.1\r\nA: v\x01w\r\n\r\n", None),    # control byte in the value
-    (b"GET /x HTTP/1.1\r\n: v\r\n\r\n", None),          # empty name
-]
+_KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "http1_codec_kat.json")))
+
+
+def _kat_expect(e):
+    return None if e is None else [(k.encode("latin-1"), v.encode("latin-1")) for k, v in e]
+
+
+CASES = [(c["raw"].encode("latin-1"), _kat_expect(c["expect"])) for c in _KAT["cases"]]
+CASE_NAMES = [c["name"] for c in _KAT["cases"]]
+BAD_VALUE_HEAD = b"GET /x HTTP/1.1\r\nHost: a\r\nA: v\x01w\r\n\r\n"  # control byte in a value
 
 
 def _blob(raws):
@@ -48,13 +49,50 @@ def _lists(blob, off, ok):
 
 
 def test_oracle_cases():
-    for raw, exp in CASES:
-        assert parse_head(raw) == exp, raw
+    assert len(CASES) >= 60 and CASE_NAMES[0].startswith("nightly")
+    for (raw, exp), name in zip(CASES, CASE_NAMES):
+        assert parse_head(raw) == exp, name
 
 
 def test_library_parser_cases():
     blob, off, ok = Classifier.parse_http_heads(*_blob([r for r, _ in CASES]))
-    assert _lists(blob, off, ok) == [e for _, e in CASES]
+    got = _lists(blob, off, ok)
+    for g, (_, e), name in zip(got, CASES, CASE_NAMES):
+        assert g == e, name
+
+
+def _line_end_mix(raw: bytes, rng) -> bytes:
+    """Each CR LF of a head as CR LF or a bare LF, sometimes CR / LF bytes
+    in front, an extra SP before the target, a Content-Length line."""
+    parts = raw.split(b"\r\n")
+    out = parts[0]
+    for p in parts[1:]:
+        out += (b"\n" if rng.random() < 0.5 else b"\r\n") + p
+    if rng.random() < 0.1:
+        out = rng.choice([b"\r\n", b"\n", b"\r", b"\n\r\n"]) + out
+    if rng.random() < 0.1:
+        out = out.replace(b" ", b"  ", 1)
+    if rng.random() < 0.1:
+        cl = rng.choice([b"0", b"12", b"00", b"1x", b"1 ", b"2\t", b"", b"18446744073709551610"])
+        i = out.find(b"\n") + 1
+        out = out[:i] + b"Content-Length: " + cl + b"\r\n" + out[i:]
+    return out
+
+
+def test_line_end_mixes_vs_oracle():
+    """CR LF / bare LF mixes (and the other leniencies) of synth heads: the
+    product parser equals the oracle, and the mixes parse as the CR LF heads
+    do."""
+    rq = synth.starwars_requests(3000, seed=7)
+    base = _raw_requests(rq)
+    rng = np.random.default_rng(8)
+    raws = [_line_end_mix(r, rng) for r in base]
+    blob, off, ok = Classifier.parse_http_heads(*_blob(raws))
+    got = _lists(blob, off, ok)
+    assert got == [parse_head(r) for r in raws]
+    plain = [i for i, r in enumerate(raws) if b"Content-Length" not in r]
+    assert all(got[i] == parse_head(base[i]) for i in plain)
+    assert sum(g is not None for g in got) > 0.9 * len(raws)
 
 
 def _raw_requests(rq):
@@ -76,9 +114,9 @@ def test_random_heads_vs_oracle():
     rq = synth.starwars_requests(3000, seed=5)
     raws = _raw_requests(rq)
     rng = np.random.default_rng(3)
-    for i in rng.choice(len(raws), 300, replace=False):  # corrupt a tenth
+    for i in rng.choice(len(raws), 900, replace=False):  # corrupt a third
         r = bytearray(raws[i])
-        r[int(rng.integers(0, len(r)))] = int(rng.choice([0x01, 0x0a, 0x20, 0x3a, 0x7f]))
+        r[int(rng.integers(0, len(r)))] = int(rng.choice([0x01, 0x0a, 0x0d, 0x20, 0x3a, 0x7f, 0x80, 0xc3, 0x2f]))
         raws[i] = bytes(r)
     blob, off, ok = Classifier.parse_http_heads(*_blob(raws))
     assert _lists(blob, off, ok) == [parse_head(r) for r in raws]

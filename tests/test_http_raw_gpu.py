@@ -14,13 +14,14 @@ from cilium_amd import _native as N
 from cilium_amd import synth
 from cilium_amd.classifier import Classifier
 from oracle.http1_ref import MAX_HEAD, parse_head
-from test_http_parse import CASES, _blob, _raw_requests
+from test_http_parse import BAD_VALUE_HEAD, CASES, _blob, _line_end_mix, _raw_requests
 
 
 def _vary(raws, rng, frac=0.3):
     """Heads as clients send them: header-name case, OWS, repeated Host,
-    unknown headers, long values (strings past the 128-byte slot), and a few
-    corrupted bytes (heads the codec rejects)."""
+    unknown headers, long values (strings past the 128-byte slot), bare-LF /
+    CR LF mixes with the codec's other leniencies (test_http_parse
+    _line_end_mix), and a few corrupted bytes (heads the codec rejects)."""
     out = []
     for r in raws:
         if rng.random() >= frac:
@@ -29,7 +30,7 @@ def _vary(raws, rng, frac=0.3):
         head, _, _ = r.partition(b"\r\n\r\n")
         lines = head.split(b"\r\n")
         req, hdrs = lines[0], lines[1:]
-        k = int(rng.integers(0, 6))
+        k = int(rng.integers(0, 8))
         if k == 0:
             hdrs = [h.split(b":", 1)[0].upper() + b":" + h.split(b":", 1)[1] for h in hdrs]
         elif k == 1:
@@ -43,8 +44,10 @@ def _vary(raws, rng, frac=0.3):
         new = b"\r\n".join([req] + hdrs) + b"\r\n\r\n"
         if k == 5:
             b = bytearray(new)
-            b[int(rng.integers(0, len(b)))] = int(rng.choice([0x01, 0x0a, 0x20, 0x3a, 0x7f, 0x0d]))
+            b[int(rng.integers(0, len(b)))] = int(rng.choice([0x01, 0x0a, 0x20, 0x3a, 0x7f, 0x0d, 0x80, 0x2f]))
             new = bytes(b)
+        elif k >= 6:
+            new = _line_end_mix(new, rng)
         out.append(new)
     return out
 
@@ -109,7 +112,7 @@ def test_gpu_raw_reference_cases_and_limits(gpu):
     sw, op = gpu.http_policy_index(pols[0]["name"]), gpu.http_policy_index("open")
     ok_head = b"GET /v1/ HTTP/1.1\r\nHost: deathstar\r\n\r\n"
     big = b"GET /v1/ HTTP/1.1\r\nHost: deathstar\r\nX-Pad: " + b"a" * MAX_HEAD + b"\r\n\r\n"
-    raws = [r for r, _ in CASES] + [ok_head, CASES[10][0], ok_head, ok_head, big]
+    raws = [r for r, _ in CASES] + [ok_head, BAD_VALUE_HEAD, ok_head, ok_head, big]
     n = len(raws)
     pol = [sw] * len(CASES) + [op, op, sw, 0xFFFFFFFF, sw]
     ing = [0] * len(CASES) + [1, 1, 1, 0, 0]
@@ -173,8 +176,8 @@ def test_gpu_raw_proxylib_snapshot_unsupported():
 def test_head_size_limit_host_parser():
     """Heads over Envoy's default 60 KiB header limit are rejected by the
     host codec step and the oracle alike."""
-    ok = b"GET / HTTP/1.1\r\nX: " + b"a" * (MAX_HEAD - 40) + b"\r\n\r\n"
-    big = b"GET / HTTP/1.1\r\nX: " + b"a" * MAX_HEAD + b"\r\n\r\n"
+    ok = b"GET / HTTP/1.1\r\nHost: a\r\nX: " + b"a" * (MAX_HEAD - 50) + b"\r\n\r\n"
+    big = b"GET / HTTP/1.1\r\nHost: a\r\nX: " + b"a" * MAX_HEAD + b"\r\n\r\n"
     _, _, good = Classifier.parse_http_heads(*_blob([ok, big]))
     assert good.tolist() == [1, 0]
     assert parse_head(ok) is not None and parse_head(big) is None
@@ -280,7 +283,7 @@ def test_gpu_raw_header_name_keys(gpu):
             i = names.index(nm.lower()) if nm.lower() in names else 0
             val = "v%d" % (i if rng.random() < 0.7 else rng.randint(0, len(names)))
             hs.append(b"%s:%s%s" % (nm.encode(), rng.choice([b"", b" ", b"\t "]), val.encode()))
-        raws.append(b"GET /x HTTP/1.1\r\n" + b"".join(h + b"\r\n" for h in hs) + b"\r\n")
+        raws.append(b"GET /x HTTP/1.1\r\nHost: a\r\n" + b"".join(h + b"\r\n" for h in hs) + b"\r\n")
     n = len(raws)
     pol, ing, port, rem = [0] * n, [1] * n, [80] * n, [5] * n
     got = gpu.http_verdicts_raw(pol, ing, port, rem, *_blob(raws))
