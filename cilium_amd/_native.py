@@ -121,6 +121,7 @@ SIGNATURES = {
     "cg_ipcache_resolve_host": (C.c_int, [_u64, _u32, _p, _sz, _p, _p, _sz, _p]),
     "cg_proxylib_stats": (C.c_int, [_u64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "cg_kafka_decode_stats": (C.c_int, [_u64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "cg_kafka_inflate_stats": (C.c_int, [_u64, C.POINTER(C.c_uint64)]),
     "cg_proxylib_set_batching": (C.c_int, [_u64, _u32, _u32]),
     "cg_proxylib_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_proxylib_policy_update_npds": (C.c_int, [_u64, C.c_char_p, _sz]),

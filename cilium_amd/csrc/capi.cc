@@ -857,7 +857,7 @@ int cg_http_policy_stats(uint64_t h, uint64_t* out, size_t n) {
     for (const auto& pg : s->progs) {
       if (pg.flags & kProgAllowAll) continue;
       max_prog_cells = std::max<uint64_t>(max_prog_cells, pg.cell_count);
-      lds_progs += (pg.flags & kProgRebased) && pg.cell_count <= 40960;
+      lds_progs += (pg.flags & kProgRebased) && pg.cell_count <= kMaxLdsCells;
     }
     uint64_t v[12] = {s->progs.size(),
                      s->parts.size(),
@@ -1144,9 +1144,10 @@ static size_t kafka_decode_on(Engine& e, const KafkaSnapshot& s, StagingSlot& sl
                               hipStream_t st) {
   // counters: topic arena entries, requests the decode kernel deferred,
   // inflate bytes reserved, payloads inflated on the device, requests the
-  // inflate kernel deferred (to the host)
-  auto* ctr = (unsigned long long*)sl.dev_buf(7, 40);
-  hip_check(hipMemsetAsync(ctr, 0, 40, st), "hipMemsetAsync");
+  // inflate kernel deferred (to the host), payloads it deferred without a
+  // reservation (arena full, impossible size)
+  auto* ctr = (unsigned long long*)sl.dev_buf(7, 48);
+  hip_check(hipMemsetAsync(ctr, 0, 48, st), "hipMemsetAsync");
   // the decode kernel's deferred requests (compressed sets) and the
   // payloads' decoded bytes (grow-only; a payload past it goes to the host)
   auto* dlist = (uint32_t*)sl.dev_buf(28, n * 4);
@@ -1154,12 +1155,13 @@ static size_t kafka_decode_on(Engine& e, const KafkaSnapshot& s, StagingSlot& sl
   check_launch(launch_kafka_decode(s.ddict[0], s.ddict[1], d_raw, d_off, n, d_red, d_rem, d_reqs, d_arena,
                                    arena_cap, ctr, d_status, st, e.cus, dlist, zarena, kKafkaInflateArena),
                "kafka decode kernel launch");
-  auto* hc = (unsigned long long*)sl.host_buf(7, 40);
-  hip_check(hipMemcpyAsync(hc, ctr, 40, hipMemcpyDeviceToHost, st), "D2H");
+  auto* hc = (unsigned long long*)sl.host_buf(7, 48);
+  hip_check(hipMemcpyAsync(hc, ctr, 48, hipMemcpyDeviceToHost, st), "D2H");
   hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
   size_t used = (size_t)hc[0];
   e.kafka_inflated.fetch_add(hc[3]);
   e.kafka_deferred.fetch_add(hc[4]);
+  e.kafka_arena_full.fetch_add(hc[5]);
   if (hc[4] == 0) return used;
   std::vector<uint8_t> status(n);
   std::vector<uint64_t> off(n + 1);
@@ -1196,6 +1198,13 @@ int cg_kafka_decode_stats(uint64_t h, uint64_t* device_inflated, uint64_t* host_
     auto e = get(h);
     if (device_inflated) *device_inflated = e->kafka_inflated.load();
     if (host_deferred) *host_deferred = e->kafka_deferred.load();
+  });
+}
+
+int cg_kafka_inflate_stats(uint64_t h, uint64_t* unreserved) {
+  return guarded([&] {
+    auto e = get(h);
+    if (unreserved) *unreserved = e->kafka_arena_full.load();
   });
 }
 
@@ -1455,7 +1464,16 @@ int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint
                                  const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                                  const uint32_t* remote, uint8_t* out) {
   return guarded([&] {
-    if (n && n <= kSmallLists) {
+    // small calls, and any call on a snapshot the device packer does not
+    // take (more than kRawMaxFields header fields): the host packer, in
+    // pieces of kHostPackLists, so a snapshot works or fails the same way
+    // whatever the batch size
+    bool host_pack = n && n <= kSmallLists;
+    if (n && !host_pack) {
+      auto e = get(h);
+      host_pack = !http_snap(*e)->lists_ok;
+    }
+    if (host_pack) {
       auto e = get(h);
       e->require_gpu();
       (void)http_snap(*e);  // CG_NOT_FOUND first
@@ -1464,7 +1482,11 @@ int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint
         fail(CG_INVALID_ARGUMENT, "NULL hdr_blob/policy/ingress/port/remote/out");
       for (size_t i = 0; i < n; ++i)  // the packer's limit (16-bit value spans), before the batch is shared
         if (hdr_off[i + 1] - hdr_off[i] > 0xFFFFu) fail(CG_INVALID_ARGUMENT, "header list longer than 64 KiB");
-      small_lists_host(*e, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);
+      constexpr size_t kHostPackLists = (size_t)1 << 20;
+      for (size_t a = 0; a < n; a += kHostPackLists) {
+        const size_t m = std::min(kHostPackLists, n - a);
+        small_lists_host(*e, hdr_blob, hdr_off + a, m, policy + a, ingress + a, port + a, remote + a, out + a);
+      }
       return;
     }
     verdicts_raw_from_host(h, RawInput::Lists, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);

@@ -167,9 +167,11 @@ constexpr uint32_t kRdirMaxSpan = 8192;
 // Per-rule hit counters a workgroup keeps in LDS for its current program
 // (programs with more rules count straight into global memory).
 constexpr uint32_t kLdsRuleHits = 512;
-// 160 KiB less the static LDS (allowed/denied pair, per-rule hit counters):
-// the largest program table a workgroup stages (http.cc, http_pack.cc)
-constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits) / 4;
+// 160 KiB less the rest of http_kernel's LDS (allowed/denied pair and deal
+// ticket, per-rule hit counters, and the 64-word code map the raw-byte
+// instantiation stages after the block): the largest program table a
+// workgroup stages (http.cc, http_pack.cc)
+constexpr uint32_t kMaxLdsCells = (160 * 1024 - 64 - 4 * kLdsRuleHits - 4 * 64) / 4;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;  // empty remote-table slot
 // One DFA of a program as a comb-packed table (comb.h).  A state is its base
 // cell index relative to `walk_off`; `dead` is the dead state, states above it

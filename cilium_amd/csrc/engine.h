@@ -170,7 +170,7 @@ struct Engine {
   StagingPool staging;  // the "_host" entry points' buffers and streams
   // Kafka decode: compressed payloads decoded on the device / requests the
   // host decoder finished (cg_kafka_decode_stats)
-  std::atomic<uint64_t> kafka_inflated{0}, kafka_deferred{0};
+  std::atomic<uint64_t> kafka_inflated{0}, kafka_deferred{0}, kafka_arena_full{0};
 
   bool has_gpu() const { return device >= 0; }
   void require_gpu() const {

@@ -142,6 +142,14 @@ struct DevSink {
 struct DevDefer {
   __device__ uint8_t operator()(uint32_t, const uint8_t*, uint32_t, int16_t) const { return kKwDefer; }
 };
+// A second pass over a request whose first pass returned kKwOk (its inner
+// sets were decoded and validated then): the outer topic list is all it
+// needs, so compressed payloads are passed over — the set's next message
+// follows from the outer framing alone — and no arena space is reserved
+// again.
+struct DevValidated {
+  __device__ uint8_t operator()(uint32_t, const uint8_t*, uint32_t, int16_t) const { return kKwOk; }
+};
 
 // A compressed message's payload decoded on the device (kw_inflate.h) into a
 // reservation of the call's inflate arena, then its inner set parsed
@@ -155,6 +163,7 @@ struct DevInflate {
   unsigned long long cap;
   unsigned long long* used;  // bytes reserved (ctr[2])
   unsigned long long* done;  // payloads decoded on the device (ctr[3])
+  unsigned long long* full;  // payloads deferred unreserved: arena full or an impossible size (ctr[5])
   const LdsCrc* crc;
   __device__ uint8_t operator()(uint32_t codec, const uint8_t* p, uint32_t n, int16_t version) const {
     if (!arena) return kKwDefer;
@@ -165,8 +174,18 @@ struct DevInflate {
       return kKwDefer;
     }
     if (need > kKafkaMaxParseBuf) return kKwDefer;
+    // a size no payload of n bytes decodes to (DEFLATE expands at most
+    // 1032:1, a snappy copy op 64 bytes from 3): the host decoder decides,
+    // and the sender's claim reserves nothing
+    if (need > (uint64_t)n * (codec == 1 ? 1032u : 32u) + 64u) {
+      atomicAdd(full, 1ull);
+      return kKwDefer;
+    }
     const unsigned long long at = atomicAdd(used, (unsigned long long)need);
-    if (at + need > cap) return kKwDefer;
+    if (at + need > cap) {
+      atomicAdd(full, 1ull);
+      return kKwDefer;
+    }
     uint8_t* dst = arena + at;
     uint32_t got = 0;
     const int r = codec == 1 ? kwz::gunzip_one(p, n, dst, (uint32_t)need, &got, *crc)
@@ -202,7 +221,9 @@ __device__ __forceinline__ void decode_one(const KafkaDictDev& dt, const KafkaDi
     const bool fits = at + nt <= arena_cap;
     KwRequest r2;
     DevSink s2{&dt, p, arena + (fits ? at : 0), fits ? nt : 0u, 0xFFFFFFFFu};
-    kw_decode(p, len, crc, &r2, s2, inflate);
+    // the same outcome as pass 1 by construction; anything else would leave
+    // topic ids unwritten, so it goes to the host decoder
+    if (kw_decode(p, len, crc, &r2, s2, DevValidated{}) != kKwOk || s2.nt != nt) st = kKwDefer;
     t0 = (uint32_t)at;
     t1 = nt >= CG_KAFKA_TOPICS_IN_ARENA ? nt : 0;
   }
@@ -324,7 +345,7 @@ __global__ __launch_bounds__(kKwThreads) void kafka_inflate_kernel(
     __syncthreads();
   }
   const LdsCrc crc{s_crc};
-  const DevInflate inflate{zarena, zcap, ctr + 2, ctr + 3, &crc};
+  const DevInflate inflate{zarena, zcap, ctr + 2, ctr + 3, ctr + 5, &crc};
   for (unsigned long long j = (unsigned long long)blockIdx.x * kKwThreads + threadIdx.x; j < nd;
        j += (unsigned long long)gridDim.x * kKwThreads) {
     const uint32_t i = defer_list[j];

@@ -514,7 +514,9 @@ int cg_http_verdicts_fields_dev(uint64_t h, const uint8_t* d_hdr_blob, const uin
  * most 1024 lists (Envoy-sized: decodeHeaders decides one request,
  * envoy/cilium_l7policy.cc:127-182) is packed on the calling thread and
  * decided with one staged copy in, one launch and one copy out; larger ones
- * are grouped and packed on the GPU. */
+ * are grouped and packed on the GPU.  Any snapshot works at any size: when
+ * the device packer does not take it (more than 32 header fields walked),
+ * larger calls are packed on the calling thread too, 1M lists at a time. */
 int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
                                  const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                                  const uint32_t* remote, uint8_t* out);
@@ -611,6 +613,14 @@ int cg_kafka_decode_host(uint64_t h, const uint8_t* raw, const uint64_t* raw_off
  * compressed set, a second gzip member, a payload past the per-call inflate
  * arena).  Either pointer may be NULL. */
 int cg_kafka_decode_stats(uint64_t h, uint64_t* device_inflated, uint64_t* host_deferred);
+
+/* Compressed payloads the device handed to the host decoder without
+ * reserving inflate-arena space, cumulative: the per-call arena
+ * (kKafkaInflateArena) was full, or the size the payload declares (gzip
+ * ISIZE, snappy length) is more than its bytes can decode to (DEFLATE
+ * 1032:1, snappy 32:1), so a sender's claim cannot use up the arena.  The
+ * host decoder gives these requests their outcome either way. */
+int cg_kafka_inflate_stats(uint64_t h, uint64_t* unreserved);
 
 /* The same decode on the GPU (one lane per request, raw bytes in HBM),
  * records and statuses in device memory.  d_raw_off holds n + 1 offsets.

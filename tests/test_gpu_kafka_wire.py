@@ -183,3 +183,61 @@ def test_gpu_compressed_sets_decoded_on_device(gpu, host):
     inflated, deferred = i1.value - i0.value, d1.value - d0.value
     print(f"compressed payloads decoded on the device: {inflated}, requests finished by the host: {deferred}")
     assert inflated > 100 and deferred < inflated / 2, (inflated, deferred)
+
+
+def _produce_sets(version, client, topic_sets):
+    """A produce request with one partition per topic, each holding the
+    given message set."""
+    body = (K.string(b"") if version >= 3 else b"") + K.i16(-1) + K.i32(5000)
+    body += K.i32(len(topic_sets)) + b"".join(K.string(t) + K.i32(1) + K.i32(0) + K.i32(len(ms)) + ms
+                                              for t, ms in topic_sets)
+    return K._request(K.PRODUCE, version, client, body, 7)
+
+
+def test_gpu_wide_compressed_produce_with_full_arena(gpu, host):
+    """Compressed produce requests with 13-40 topics (their ids go to the
+    topic arena through a second decode pass) in one call with payloads
+    that fill the 64 MiB inflate arena (12 sets of 6 MB of zeros, gzip
+    and snappy) and payloads whose gzip ISIZE claims 6.5 MB from a few
+    bytes.  The second pass re-reads only the outer topic list (it reserves
+    nothing), so every record equals the host decoder's and the oracle's
+    whatever the arena holds; the unreserved deferrals are counted
+    (cg_kafka_inflate_stats)."""
+    import ctypes as C
+    import gzip
+    import struct
+    _, topics, clients, ids = _policy(gpu, host)
+    rng = np.random.default_rng(41)
+    reqs = []
+    for j in range(12):  # arena fillers
+        inner = bytes(6_000_000)
+        val = gzip.compress(inner, 9, mtime=0) if j % 2 == 0 else K.snappy_block(inner)
+        ms = K.message(None, val, K.CODEC_GZIP if j % 2 == 0 else K.CODEC_SNAPPY, 0, 0)
+        reqs.append(_produce_sets(2, clients[0], [(topics[j % len(topics)], ms)]))
+    for j in range(6):  # gzip ISIZE claiming 6.5 MB
+        z = bytearray(gzip.compress(K.message(None, b"v", 0, 0, 0), mtime=0))
+        z[-4:] = struct.pack("<I", 6_500_000)
+        reqs.append(_produce_sets(2, clients[1], [(topics[0], K.message(None, bytes(z), K.CODEC_GZIP, 0, 0))]))
+    for j in range(200):  # wide compressed produce requests
+        nt = int(rng.integers(13, 41))
+        sets = []
+        for t in range(nt):
+            plain = b"".join(K.message(None, b"m%d" % m, 0, m, 0) for m in range(int(rng.integers(1, 4))))
+            codec = K.CODEC_GZIP if rng.random() < 0.5 else K.CODEC_SNAPPY
+            val = gzip.compress(plain, mtime=0) if codec == K.CODEC_GZIP else K.snappy_block(plain)
+            sets.append((topics[int(rng.integers(0, len(topics)))], K.message(None, val, codec, 0, 0)))
+        reqs.append(_produce_sets(2, clients[j % len(clients)], sets))
+    order = rng.permutation(len(reqs))
+    reqs = [reqs[i] for i in order]
+    n = len(reqs)
+    raw, off = K.concat(reqs)
+    red = np.zeros(n, np.uint16)
+    rem = np.asarray(ids, np.uint32)[np.arange(n) % len(ids)]
+    u0, u1 = C.c_uint64(), C.c_uint64()
+    assert N.lib.cg_kafka_inflate_stats(gpu.h, C.byref(u0)) == N.CG_OK
+    g = gpu.kafka_decode(raw, off, red, rem)
+    assert N.lib.cg_kafka_inflate_stats(gpu.h, C.byref(u1)) == N.CG_OK
+    h = host.kafka_decode(raw, off, red, rem, diag_cpu=True)
+    assert records_view(*g) == records_view(*h)
+    assert records_view(*g) == oracle_view([R.decode(r) for r in reqs], red, rem, host.kafka_intern)
+    assert u1.value - u0.value >= 7, (u0.value, u1.value)  # the six claims and at least one full arena

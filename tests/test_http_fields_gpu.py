@@ -281,3 +281,37 @@ def test_gpu_fields_config5_full_size_oracle_subsample():
     assert 0.1 < float(exp.mean()) < 0.9
     del d_blob, d_off, d_out
     cl.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [200, 6000])
+def test_gpu_fields_host_many_fields_any_size(gpu, n):
+    """A snapshot walking 40 header fields (past the device packer's 32):
+    cg_http_verdicts_fields_host decides it at an Envoy-sized call and at a
+    call past the small-call limit alike (host packing for both), equal to
+    the host path and the oracle; the device entry refuses it."""
+    names = ["x-f%02d" % i for i in range(40)]
+    rules = [{"headers": [{"name": nm, "exact_match": "v%d" % i}]} for i, nm in enumerate(names)]
+    pols = [{"name": "p", "policy": 0, "ingress_per_port_policies": [
+        {"port": 80, "rules": [{"remote_policies": [], "http_rules": {"http_rules": rules}}]}]}]
+    gpu.update_http_policy(pols)
+    rng = np.random.default_rng(n)
+    lists = []
+    for _ in range(n):
+        ps = [(b":method", b"GET"), (b":path", b"/x")]
+        for _ in range(int(rng.integers(0, 3))):
+            i = int(rng.integers(0, len(names)))
+            ps.append((names[i].encode(), b"v%d" % (i if rng.random() < 0.6 else i + 1)))
+        lists.append(b"".join(a + b"\0" + b + b"\0" for a, b in ps))
+    args = (np.zeros(n, np.uint32), np.ones(n, np.uint8), np.full(n, 80, np.uint16), np.full(n, 5, np.uint32))
+    got = _check(gpu, pols, args, lists, n)
+    assert 0.2 < got.mean() < 0.9
+    import torch
+    blob, off = _join(lists)
+    d = torch.device("cuda:0")
+    with pytest.raises(N.CiliumGPUError):
+        gpu.http_verdicts_fields_dev(torch.from_numpy(blob).to(d), torch.from_numpy(off.astype(np.int64)).to(d), n,
+                                     torch.from_numpy(args[0].astype(np.int32)).to(d),
+                                     torch.from_numpy(args[1]).to(d), torch.from_numpy(args[2].astype(np.int16)).to(d),
+                                     torch.from_numpy(args[3].astype(np.int32)).to(d),
+                                     torch.zeros(n, dtype=torch.uint8, device=d))

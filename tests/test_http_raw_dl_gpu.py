@@ -228,3 +228,44 @@ def test_gpu_dl_policy_swap_after_async_call(dl):
     assert np.array_equal(got1[:8_000], _oracle(pols, *(np.asarray(a)[:8_000] for a in _args(rq)), raws[:8_000]))
     assert np.array_equal(out2.cpu().numpy(), _host_path(cl, *_args(rq), raws))
     cl.close()
+
+
+def _big_program_policy(n_rules: int, seed: int = 1):
+    """One program of n_rules random 12-character path prefixes: 732 rules
+    compile to 40,303 table cells, 734 to 40,407 — either side of the
+    largest block http_kernel stages in LDS next to the raw-byte path's code
+    map (kMaxLdsCells, dev_types.h)."""
+    import random
+    r = random.Random(seed)
+    al = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789"
+    words = ["".join(r.choice(al) for _ in range(12)) for _ in range(n_rules)]
+    rules = [{"headers": [{"name": ":path", "regex_match": "/" + w + ".*"}]} for w in words]
+    return [{"name": "big", "policy": 1, "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [7], "http_rules": {"http_rules": rules}}]}]}], words
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_rules", [732, 734])
+def test_gpu_dl_program_at_lds_limit(gpu, n_rules):
+    """A program at the LDS limit on the device-layout path (raw bytes coded
+    through the LDS code map): its block either fits beside the map or
+    walks from global memory; verdicts equal the host path's and the
+    oracle's."""
+    pols, words = _big_program_policy(n_rules)
+    gpu.update_http_policy(pols)
+    st = gpu.http_policy_stats()
+    assert 40192 < st["max_program_cells"] < 40432, st
+    assert st["lds_programs"] == (1 if n_rules == 732 else 0), st
+    rng = np.random.default_rng(n_rules)
+    raws = []
+    for j in range(4000):
+        w = words[int(rng.integers(0, len(words)))]
+        if rng.random() < 0.5:
+            w = w[:-1] + "_"
+        raws.append(b"GET /%s/%d HTTP/1.1\r\nHost: big\r\n\r\n" % (w.encode(), j))
+    n = len(raws)
+    pol, ing, port, rem = [0] * n, [1] * n, [80] * n, [7] * n
+    got = gpu.http_verdicts_raw(pol, ing, port, rem, *_blob(raws))
+    assert np.array_equal(got, _host_path(gpu, pol, ing, port, rem, raws))
+    assert np.array_equal(got, _oracle(pols, pol, ing, port, rem, raws))
+    assert 0.3 < got.mean() < 0.7
