@@ -54,6 +54,9 @@ def parse():
                          "on the device, no host round trip) or host (CILIUM_GPU_RAW_LAYOUT=host: the round-3 "
                          "sequence, bucket counts laid out on the host)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--sustain-seconds", type=float, default=3.0,
+                    help="after the timed steps, run steps back to back for this long and report the sustained "
+                         "rate (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--layout", default="tile", choices=["tile", "copy"],
@@ -112,7 +115,7 @@ def main():
     cl = Classifier(device=dev.index)
     pols, info = synth.http10k_rules()
     t0 = time.time()
-    share_policy(cl, pols, dist, rank, dev, torch)
+    bcast_s = share_policy(cl, pols, dist, rank, dev, torch)
     compile_s = time.time() - t0
     stats = cl.http_policy_stats()
 
@@ -129,8 +132,9 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.synchronize()
     kev = []  # (start, end) HIP events around each verdict-kernel launch, on its stream
+    aev = []  # (start, end) around each counter all-reduce (N > 1), on the same stream
 
-    def step(timed=False):
+    def step(timed=False, kev=kev, aev=aev):
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -142,8 +146,14 @@ def main():
             # the only collective: per-rule hits and per-program allowed/
             # denied counters, summed over ranks (RCCL over xGMI)
             cl.counters_copy_dev(d_ctr, n_ctr, stream=stream.cuda_stream)
+            if timed:
+                a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a0.record(stream)
             with torch.cuda.stream(stream):
                 dist.all_reduce(d_ctr)
+            if timed:
+                a1.record(stream)
+                aev.append((a0, a1))
 
     # parity spot-check of the resident batch (outside the timed region)
     check = None
@@ -175,7 +185,14 @@ def main():
     t_end = time.perf_counter()
     wall = t_end - t_start
     kernel_ms = sum(a.elapsed_time(z) for a, z in kev) / args.steps
+    allreduce_ms = sum(a.elapsed_time(z) for a, z in aev) / args.steps if aev else None
+    rank_wall = wall
     wall = max_over_ranks(wall, dist, dev, torch)
+    sustained = None
+    if args.sustain_seconds > 0:
+        sustained = sustain(step, args.sustain_seconds, B * world, dist, dev, torch)
+    ranks = gather_rank_stats({"kernel_ms": kernel_ms, "allreduce_ms": allreduce_ms, "broadcast_s": bcast_s,
+                               "wall_s": rank_wall}, dist, dev, torch)
 
     total_req = B * world * args.steps
     value = total_req / wall
@@ -244,6 +261,8 @@ def main():
                          "kernel": "http_kernel", "kernel_ms": kernel_ms,
                          "bytes_per_launch": per_launch_bytes, "traffic_bytes_per_launch": traffic_bytes,
                          "traffic_source": traffic_src},
+            "sustained": sustained,
+            "ranks": ranks,
             "distinct_262k": small,
             "end_to_end": e2e,
             "host_entry": host,
@@ -270,19 +289,75 @@ def max_over_ranks(sec: float, dist, dev, torch) -> float:
     return float(tt.item())
 
 
-def share_policy(cl, pols, dist, rank, dev, torch) -> None:
+def sustain(step, seconds: float, per_step: int, dist, dev, torch) -> dict:
+    """Steps back to back for `seconds` (the driver's timed region is ~30 ms
+    of launches): the sustained rate over the whole run and the mean of the
+    per-launch HIP events, so a clock drop past the short window would show
+    against the headline."""
+    kev, aev = [], []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for _ in range(16):
+            step(timed=True, kev=kev, aev=aev)
+        n += 16
+        torch.cuda.synchronize()
+        # every rank runs the same number of steps: rank 0's clock decides
+        done = torch.tensor([time.perf_counter() - t0 >= seconds], dtype=torch.int32, device=dev)
+        if dist is not None:
+            dist.broadcast(done, 0)
+        if int(done.item()):
+            break
+    wall = max_over_ranks(time.perf_counter() - t0, dist, dev, torch)
+    ms = [a.elapsed_time(z) for a, z in kev]
+    return {"seconds": wall, "steps": n, "value": per_step * n / wall, "unit": "verdicts/s",
+            "kernel_ms_mean": float(np.mean(ms)), "kernel_ms_first16": float(np.mean(ms[:16])),
+            "kernel_ms_last16": float(np.mean(ms[-16:])), "kernel_ms_max": float(np.max(ms)),
+            "allreduce_ms_mean": float(np.mean([a.elapsed_time(z) for a, z in aev])) if aev else None}
+
+
+RANK_KEYS = ("kernel_ms", "allreduce_ms", "broadcast_s", "wall_s")
+
+
+def gather_rank_stats(mine: dict, dist, dev, torch) -> list:
+    """Per-rank timings at rank 0 (all_gather of RANK_KEYS; None travels as
+    NaN): where an N-GPU run loses against linear scaling — the slowest
+    kernel, the counter all-reduce, the table image broadcast."""
+    vals = [float("nan") if mine.get(k) is None else float(mine[k]) for k in RANK_KEYS]
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    if dist is None or dist.get_world_size() == 1:
+        rows = [t]
+    else:
+        rows = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(rows, t)
+    out = []
+    for r, row in enumerate(rows):
+        d = {"rank": r}
+        for k, v in zip(RANK_KEYS, row.cpu().tolist()):
+            d[k] = None if v != v else v
+        out.append(d)
+    return out
+
+
+def share_policy(cl, pols, dist, rank, dev, torch) -> float:
     """Compile the rules once (rank 0) and give every rank the same compiled
     table image: broadcast over the process group, imported
-    without recompiling.  One rank: compile."""
+    without recompiling.  One rank: compile.  Returns the seconds spent on
+    the image's broadcast and import (0 for one rank)."""
     if dist is None or dist.get_world_size() == 1:
         cl.update_http_policy(pols)
-        return
+        return 0.0
     if rank == 0:
         cl.update_http_policy(pols)
         img = np.frombuffer(cl.export_http_policy(), np.uint8)
         size = torch.tensor([img.size], dtype=torch.int64, device=dev)
     else:
         size = torch.zeros(1, dtype=torch.int64, device=dev)
+    dist.barrier()  # rank 0's compile is not part of the broadcast
+    t0 = time.perf_counter()
     dist.broadcast(size, 0)
     buf = torch.empty(int(size.item()), dtype=torch.uint8, device=dev)
     if rank == 0:
@@ -290,6 +365,7 @@ def share_policy(cl, pols, dist, rank, dev, torch) -> None:
     dist.broadcast(buf, 0)
     if rank != 0:
         cl.import_http_policy(buf.cpu().numpy().tobytes())
+    return time.perf_counter() - t0
 
 
 def host_entry_fields(cl, rq, ref) -> dict:
@@ -438,25 +514,33 @@ def rehearse(args):
         dist.init_process_group("gloo")
     cl = Classifier(device=-1)
     pols, info = synth.http10k_rules(n_rules=2000, n_ports=16)
-    share_policy(cl, pols, dist if world > 1 else None, rank, torch.device("cpu"), torch)
+    bcast_s = share_policy(cl, pols, dist if world > 1 else None, rank, torch.device("cpu"), torch)
     D = max(64, min(args.requests_per_gpu, args.distinct))
     rq = synth.http10k_requests(D, info, seed=synth.SEED ^ (rank * 7919))
     b = cl.pack_http(**rq)
     nprog = int(cl.http_policy_stats()["programs"])
     ctr = torch.zeros(2 * nprog, dtype=torch.int64)
 
+    kt, at = [], []
+
     def step():
+        t0 = time.perf_counter()
         slot_v = cl.http_eval_host_diag_slots(b)
         ctr.add_(torch.from_numpy(program_counts(b, slot_v, nprog)))
+        kt.append(time.perf_counter() - t0)
         if world > 1:
             t = ctr.clone()
+            t1 = time.perf_counter()
             dist.all_reduce(t)
+            at.append(time.perf_counter() - t1)
             return t
         return ctr
 
     for _ in range(args.warmup):
         step()
     ctr.zero_()
+    kt.clear()
+    at.clear()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -464,7 +548,11 @@ def rehearse(args):
         total = step()
     if world > 1:
         dist.barrier()
-    wall = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None, torch.device("cpu"), torch)
+    rank_wall = time.perf_counter() - t0
+    wall = max_over_ranks(rank_wall, dist if world > 1 else None, torch.device("cpu"), torch)
+    ranks = gather_rank_stats({"kernel_ms": 1e3 * float(np.mean(kt)),
+                               "allreduce_ms": 1e3 * float(np.mean(at)) if at else None, "broadcast_s": bcast_s,
+                               "wall_s": rank_wall}, dist if world > 1 else None, torch.device("cpu"), torch)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": D * world * args.steps / wall, "unit": "verdicts/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -472,7 +560,7 @@ def rehearse(args):
                           "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                           "config": {"workload": "CPU rehearsal of the N-rank path (host table walker, gloo)",
                                      "requests_per_gpu": D, "parallelism": f"dp{world}"},
-                          "rehearsal": True,
+                          "rehearsal": True, "ranks": ranks,
                           "allreduced_requests": int(total.sum()), "expected_requests": D * world * args.steps}),
               flush=True)
     if world > 1:

@@ -104,6 +104,13 @@ def test_bench_spawns_two_ranks_cpu_rehearsal():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["rehearsal"] is True
     assert d["allreduced_requests"] == d["expected_requests"] == 2048 * 2 * 2
+    # per-rank diagnostics (bench.gather_rank_stats): one row per rank, every
+    # rank timed its shard, its counter all-reduce and the image broadcast
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    for r in d["ranks"]:
+        assert r["kernel_ms"] > 0 and r["allreduce_ms"] is not None and r["allreduce_ms"] >= 0
+        assert r["broadcast_s"] >= 0 and r["wall_s"] > 0
+    assert abs(max(r["wall_s"] for r in d["ranks"]) - d["ms_per_step"] * d["steps"] / 1e3) < 1e-6
 
 
 def _bench_collectives_worker(rank, world, port, q):
@@ -135,7 +142,11 @@ def _bench_collectives_worker(rank, world, port, q):
         same_verdicts = all(torch.equal(x, vs[0]) for x in vs)
         wall = bench.max_over_ranks(0.5 + rank, dist, torch.device("cpu"), torch)
         one = bench.max_over_ranks(0.25, None, torch.device("cpu"), torch)
-        q.put((rank, same_image, same_verdicts, wall, one))
+        rows = bench.gather_rank_stats({"kernel_ms": 1.0 + rank, "allreduce_ms": None if rank == 1 else 0.5,
+                                        "broadcast_s": 0.1 * rank, "wall_s": 2.0}, dist, torch.device("cpu"), torch)
+        rows_ok = rows == [{"rank": r, "kernel_ms": 1.0 + r, "allreduce_ms": None if r == 1 else 0.5,
+                            "broadcast_s": 0.1 * r, "wall_s": 2.0} for r in range(world)]
+        q.put((rank, same_image and rows_ok, same_verdicts, wall, one))
         cl.close()
     finally:
         dist.destroy_process_group()
@@ -144,8 +155,8 @@ def _bench_collectives_worker(rank, world, port, q):
 @pytest.mark.timeout(300)
 def test_bench_collectives_image_broadcast_and_max_time():
     """Every collective bench.py issues besides the counter all-reduce
-    (covered above): the compiled image broadcast and the max-over-ranks
-    time, on 3 gloo ranks."""
+    (covered above): the compiled image broadcast, the max-over-ranks time
+    and the per-rank timing gather, on 3 gloo ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
