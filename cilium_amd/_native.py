@@ -150,6 +150,10 @@ SIGNATURES = {
     "cg_http_verdicts_raw_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p]),
     "cg_http_verdicts_fields_dev": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p, _p]),
     "cg_http_verdicts_fields_host": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p]),
+    "cg_http_ring_open": (C.c_int, [_u64, C.c_uint32, C.c_uint32]),
+    "cg_http_ring_verdicts": (C.c_int, [_u64, _p, _p, _sz, _p, _p, _p, _p, _p]),
+    "cg_http_ring_stats": (C.c_int, [_u64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "cg_http_ring_close": (C.c_int, [_u64]),
     "cg_kafka_policy_update": (C.c_int, [_u64, C.c_char_p, _sz]),
     "cg_kafka_policy_index": (C.c_int, [_u64, C.c_char_p, C.POINTER(_u32)]),
     "cg_kafka_intern": (C.c_int, [_u64, _u32, C.c_char_p, _sz, C.POINTER(_u32)]),

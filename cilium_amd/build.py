@@ -19,7 +19,7 @@ BUILD = HERE / "_build"
 LIB = HERE / "libciliumgpu.so"
 ARCH = "gfx950"
 
-SOURCES = ["runtime.cc", "regex.cc", "regex_go.cc", "clsdfa.cc", "comb.cc", "http.cc", "l4.cc", "lpm.cc", "ipcache.cc", "kafka.cc", "http_pack.cc", "capi.cc", "proxylib_shim.cc", "proxylib_memcache.cc", "proxylib_cassandra.cc", "npds_pb.cc", "http_parse.cc", "http_raw.cc", "http_image.cc", "kafka_wire.cc",
+SOURCES = ["runtime.cc", "regex.cc", "regex_go.cc", "clsdfa.cc", "comb.cc", "http.cc", "l4.cc", "lpm.cc", "ipcache.cc", "kafka.cc", "http_pack.cc", "capi.cc", "proxylib_shim.cc", "proxylib_memcache.cc", "proxylib_cassandra.cc", "npds_pb.cc", "http_parse.cc", "http_raw.cc", "http_image.cc", "kafka_wire.cc", "ring.cc",
            "kernels.hip", "kernels_http.hip", "kernels_ipcache.hip", "kernels_kafka.hip", "kernels_http_raw.hip"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -205,6 +205,26 @@ class Classifier:
         return self._verdicts_from_host(N.lib.cg_http_verdicts_fields_host, policy, ingress, port, remote, hdr_blob,
                                         hdr_off)
 
+    def http_ring_open(self, workgroups: int = 16, slots: int = 32) -> None:
+        """cg_http_ring_open: start the persistent verdict ring (Envoy-sized
+        calls without a launch, copies or a stream synchronization)."""
+        N.check(N.lib.cg_http_ring_open(self.h, workgroups, slots))
+
+    def http_ring_verdicts(self, policy, ingress, port, remote, hdr_blob: np.ndarray,
+                           hdr_off: np.ndarray) -> np.ndarray:
+        """cg_http_ring_verdicts: header lists → verdicts through the ring
+        (request order; calls past a slot take cg_http_verdicts_fields_host)."""
+        return self._verdicts_from_host(N.lib.cg_http_ring_verdicts, policy, ingress, port, remote, hdr_blob,
+                                        hdr_off)
+
+    def http_ring_stats(self) -> dict:
+        served, launches = C.c_uint64(), C.c_uint64()
+        N.check(N.lib.cg_http_ring_stats(self.h, C.byref(served), C.byref(launches)))
+        return {"served": served.value, "launches": launches.value}
+
+    def http_ring_close(self) -> None:
+        N.check(N.lib.cg_http_ring_close(self.h))
+
     def _verdicts_from_host(self, fn, policy, ingress, port, remote, raw_blob, raw_off) -> np.ndarray:
         raw_blob = np.ascontiguousarray(raw_blob, np.uint8)
         raw_off = np.ascontiguousarray(raw_off, np.uint64)

@@ -22,6 +22,7 @@
 #include "ipcache.h"
 #include "lpm.h"
 #include "regex.h"
+#include "ring.h"
 
 using namespace cg;
 
@@ -158,6 +159,14 @@ void cg_close(uint64_t h) {
   }
   if (e->has_gpu()) {
     (void)hipSetDevice(e->device);
+    {
+      std::shared_ptr<HttpRing> r;
+      {
+        std::lock_guard<std::mutex> lk(e->ring_mu);
+        r = std::move(e->ring);
+      }
+      if (r) r->close();
+    }
     (void)hipStreamSynchronize((hipStream_t)e->stream);
     e->maps.clear();
     e->prefilters.clear();
@@ -1490,6 +1499,76 @@ int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint
       return;
     }
     verdicts_raw_from_host(h, RawInput::Lists, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);
+  });
+}
+
+// ------------------------------------------------------ verdict ring ----
+int cg_http_ring_open(uint64_t h, uint32_t workgroups, uint32_t slots) {
+  return guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    std::lock_guard<std::mutex> lk(e->ring_mu);
+    if (e->ring) fail(CG_INVALID_ARGUMENT, "the handle's ring is open");
+    auto r = std::make_shared<HttpRing>();
+    r->open(*e, workgroups, slots);
+    e->ring = std::move(r);
+  });
+}
+
+int cg_http_ring_verdicts(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
+                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                          const uint32_t* remote, uint8_t* out) {
+  bool other = false;
+  const int rc = guarded([&] {
+    auto e = get(h);
+    e->require_gpu();
+    std::shared_ptr<HttpRing> r;
+    {
+      std::lock_guard<std::mutex> lk(e->ring_mu);
+      r = e->ring;
+    }
+    if (!r) fail(CG_NOT_FOUND, "no ring open (cg_http_ring_open)");
+    auto s = http_snap(*e);
+    if (!n) return;
+    check_offsets(hdr_off, n);
+    if (!policy || !ingress || !port || !remote || !out || (hdr_off[n] != hdr_off[0] && !hdr_blob))
+      fail(CG_INVALID_ARGUMENT, "NULL hdr_blob/policy/ingress/port/remote/out");
+    for (size_t i = 0; i < n; ++i)  // the packer's limit (16-bit value spans)
+      if (hdr_off[i + 1] - hdr_off[i] > 0xFFFFu) fail(CG_INVALID_ARGUMENT, "header list longer than 64 KiB");
+    if (n > kRingReqs || hdr_off[n] - hdr_off[0] > kRingBlob || !s->lists_ok) {
+      other = true;  // past a slot: the staged entry
+      return;
+    }
+    r->verdicts(*e, s, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);
+  });
+  if (rc == CG_OK && other)
+    return cg_http_verdicts_fields_host(h, hdr_blob, hdr_off, n, policy, ingress, port, remote, out);
+  return rc;
+}
+
+int cg_http_ring_stats(uint64_t h, uint64_t* served, uint64_t* launches) {
+  return guarded([&] {
+    auto e = get(h);
+    std::shared_ptr<HttpRing> r;
+    {
+      std::lock_guard<std::mutex> lk(e->ring_mu);
+      r = e->ring;
+    }
+    if (!r) fail(CG_NOT_FOUND, "no ring open (cg_http_ring_open)");
+    r->stats(served, launches);
+  });
+}
+
+int cg_http_ring_close(uint64_t h) {
+  return guarded([&] {
+    auto e = get(h);
+    std::shared_ptr<HttpRing> r;
+    {
+      std::lock_guard<std::mutex> lk(e->ring_mu);
+      r = std::move(e->ring);
+    }
+    if (!r) fail(CG_NOT_FOUND, "no ring open (cg_http_ring_open)");
+    r->close();
   });
 }
 

@@ -312,6 +312,33 @@ CG_HD inline uint32_t raw_name_hash(uint32_t nl, uint32_t lo0, uint32_t lo1, uin
 // FNV-1a, 32 bit, over lowercase bytes
 CG_HD inline uint32_t raw_fnv(uint32_t h, uint8_t c) { return (h ^ c) * 16777619u; }
 constexpr uint32_t kRawFnvInit = 2166136261u;
+// ---- the persistent verdict ring (cg_http_ring_*, ring.cc): Envoy-sized
+// calls of header lists decided by a resident kernel that polls slots in
+// fine-grained pinned host memory — no launch, no copies, no stream
+// synchronization per call.  A slot holds one call: a 64-byte header
+// {seq (the host's doorbell), done (the device's completion word), n, bytes},
+// the per-request inputs, list offsets relative to the slot's blob, the
+// verdicts and the blob.
+constexpr uint32_t kRingReqs = 256;          // requests per slot (larger calls take the staged path)
+constexpr uint32_t kRingBlob = 32 * 1024;    // list bytes per slot
+constexpr size_t kRingPol = 64, kRingRem = kRingPol + 4 * kRingReqs, kRingPort = kRingRem + 4 * kRingReqs,
+                 kRingIng = kRingPort + 2 * kRingReqs, kRingOff = kRingIng + kRingReqs,
+                 kRingOut = kRingOff + 4 * (kRingReqs + 4), kRingBlobAt = kRingOut + kRingReqs,
+                 kRingSlotBytes = (kRingBlobAt + kRingBlob + 255) & ~(size_t)255;
+static_assert(kRingBlobAt % 16 == 0, "the blob is copied in 16-byte units");
+// ring control words (host memory, before the slots): the host's stop word
+// (the device only reads host memory with loads and writes it with plain
+// stores: no read-modify-write over the bus)
+constexpr uint32_t kRingStop = 0, kRingCtlBytes = 256;
+struct HttpRingDev {
+  uint8_t* slots;         // device view of the host slots (hipHostGetDevicePointer)
+  uint32_t* ctl;          // device view of the control words
+  uint32_t nslots, nwg;   // slot s is served by workgroup s % nwg
+  uint64_t idle_ticks;    // wall-clock ticks without a call before the kernel exits
+  uint64_t life_ticks;    // hard bound on one launch's life
+  uint32_t lds_cells;     // largest program block the kernel stages in LDS (0: none)
+};
+
 // A run of tiles of a raw batch with the same string units and program:
 // tiles [t0, next run's t0), tile t at granule base + (t - t0) * (1 + 2 * units).
 struct HttpRawRun {

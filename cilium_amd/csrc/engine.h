@@ -153,6 +153,7 @@ struct PrefilterState;
 struct IpcacheState;
 struct HttpSnapshot;
 struct KafkaSnapshot;
+class HttpRing;
 
 struct Engine {
   int device = -1;      // -1: host-only handle (compile/pack only)
@@ -171,6 +172,9 @@ struct Engine {
   // Kafka decode: compressed payloads decoded on the device / requests the
   // host decoder finished (cg_kafka_decode_stats)
   std::atomic<uint64_t> kafka_inflated{0}, kafka_deferred{0}, kafka_arena_full{0};
+  // the persistent verdict ring (cg_http_ring_open, ring.cc), or none
+  std::mutex ring_mu;
+  std::shared_ptr<HttpRing> ring;
 
   bool has_gpu() const { return device >= 0; }
   void require_gpu() const {

@@ -89,4 +89,11 @@ int launch_http_raw_walk(const HttpDev& T, const HttpRawDev& R, bool lists, cons
                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port, const uint32_t* remote,
                          const RawLayoutDev& L, uint8_t* out, void* stream, int cus);
 
+// The persistent verdict ring (ring.cc): nwg one-wave workgroups serving
+// the slots of G until its stop word, idle_ticks without a call or
+// life_ticks; `state` is http_ring_state_bytes() of zeroed device memory.
+size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells);
+size_t http_ring_state_bytes();
+int launch_http_ring(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream);
+
 }  // namespace cg

@@ -1952,13 +1952,13 @@ __global__ __launch_bounds__(kSealThreads) void raw_seal_kernel(HttpRawDev R, Ra
 // built on the fly through the program's code map and walked over the
 // program's tables in global memory; the verdict, its counters and rule hit
 // as http_kernel gives them (kernels_http.hip http_tiles).
-__device__ __forceinline__ uint32_t walk_request(const HttpDev& T, const HttpRawDev& R, const HttpProg& pg,
-                                                 uint32_t prog, HeadReader& hr, const lds_u32* sp, uint32_t stride,
-                                                 uint32_t remote) {
+// blk / lut: the program's block and code map (global memory, or LDS copies
+// for a rebased program: the persistent ring stages them).
+__device__ __forceinline__ uint32_t walk_request_at(const HttpDev& T, const HttpRawDev& R, const HttpProg& pg,
+                                                    const uint32_t* blk, const uint8_t* lut, HeadReader& hr,
+                                                    const lds_u32* sp, uint32_t stride, uint32_t remote) {
   using namespace walk;
-  const uint32_t* blk = T.cells + pg.cell_begin;
   const bool rebased = pg.flags & kProgRebased;
-  const uint8_t* lut = R.codes + (size_t)prog * 256;
   uint32_t last;
   (void)string_len(R, sp, stride, &last);
   const uint32_t row = remote_row(blk, pg, remote), W = pg.mask_words;
@@ -1990,6 +1990,32 @@ __device__ __forceinline__ uint32_t walk_request(const HttpDev& T, const HttpRaw
   return hit;
 }
 
+// One parsed request's verdict with its counters and rule hit, as
+// http_kernel gives them: no policy for the port → allowed when the codec
+// accepted it; unknown policy → denied; an allow-all scope → allowed
+// (counted); else the walk (cilium_network_policy.h:129-138,187-191).
+__device__ __forceinline__ uint32_t decide_request(const HttpDev& HT, const HttpRawDev& R, uint32_t prog, bool ok,
+                                                   const uint32_t* blk, const uint8_t* lut, HeadReader& hr,
+                                                   const lds_u32* sp, uint32_t stride, uint32_t remote) {
+  uint32_t v = 0;
+  if (prog == kProgAllow) {
+    v = ok;
+  } else if (prog < R.nprogs) {
+    const HttpProg pg = HT.progs[prog];
+    if (pg.flags & kProgAllowAll) {
+      v = ok;
+      if (ok) atomicAdd(&HT.counters[2 * prog], 1ull);
+    } else if (ok) {
+      const uint32_t hit = walk_request_at(HT, R, pg, blk ? blk : HT.cells + pg.cell_begin,
+                                           lut ? lut : R.codes + (size_t)prog * 256, hr, sp, stride, remote);
+      v = hit != walk::kNoHit;
+      atomicAdd(&HT.counters[2 * prog + (v ? 0 : 1)], 1ull);
+      if (v) atomicAdd(&HT.rule_hits[pg.rule_base + hit], 1ull);
+    }
+  }
+  return v;
+}
+
 template <bool kLists>
 __global__ __launch_bounds__(kRawThreads) void raw_walk_kernel(HttpDev HT, HttpRawDev R, const uint8_t* __restrict__ raw,
                                                                const uint64_t* __restrict__ off,
@@ -2012,24 +2038,157 @@ __global__ __launch_bounds__(kRawThreads) void raw_walk_kernel(HttpDev HT, HttpR
     const bool ok = prog == kProgDeny ? false
                     : kLists          ? hn <= kFieldsMaxList && parse_list_bytes(R, T, hr, sp, kRawThreads)
                                       : parse_head(R, T, hr, sp, kRawThreads);
-    uint32_t v = 0;
-    if (prog == kProgAllow) {
-      v = ok;  // no policy for the port
-    } else if (prog < R.nprogs) {
-      const HttpProg pg = HT.progs[prog];
-      if (pg.flags & kProgAllowAll) {
-        v = ok;
-        if (ok) atomicAdd(&HT.counters[2 * prog], 1ull);
-      } else if (ok) {
-        const uint32_t hit = walk_request(HT, R, pg, prog, hr, sp, kRawThreads, remote[i]);
-        v = hit != walk::kNoHit;
-        atomicAdd(&HT.counters[2 * prog + (v ? 0 : 1)], 1ull);
-        if (v) atomicAdd(&HT.rule_hits[pg.rule_base + hit], 1ull);
-      }
-    }
-    out[i] = (uint8_t)v;
+    out[i] = (uint8_t)decide_request(HT, R, prog, ok, nullptr, nullptr, hr, sp, kRawThreads, remote[i]);
   }
 }
+// ---- the persistent verdict ring (ring.cc; dev_types.h HttpRingDev) ------
+// One wave per workgroup, resident: lane j polls the doorbell of slot
+// blockIdx.x + j * nwg ({seq, done} in one system-scope acquire load over the
+// bus).  A ready slot's inputs and lists come into LDS with 16-byte loads;
+// each request is decided as raw_walk_kernel decides it (program lookup, the
+// list parse, decide_request), with the program's block and code map staged
+// in LDS when every request of the slot shares one rebased program that fits
+// (kept across slots: Envoy's calls on one listener repeat the program).
+// The verdicts go back into the slot and `done` is published with a
+// system-scope release after them.  Every wave exits: on the host's stop
+// word, or when workgroup 0 sees no call for idle_ticks or the launch pass
+// life_ticks (it raises the exit word in device memory; each wave serves
+// what is ready one last time and leaves) — ring.cc relaunches on the next
+// call.
+constexpr uint32_t kRingThreads = 64;
+// device memory of a launch: the exit word, the wall clock of the last call
+// served, slots served (read by cg_http_ring_stats)
+struct RingState {
+  uint32_t exit, pad;
+  unsigned long long last, served;
+};
+
+__device__ __forceinline__ uint32_t sys_load32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long sys_load64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, uint32_t s,
+                                           uint32_t seq, lds_u8* in, lds_u32* sp, uint32_t* cells, uint8_t* cmap,
+                                           uint32_t& staged, uint32_t lane) {
+  uint8_t* hs = G.slots + (size_t)s * kRingSlotBytes;
+  // (atomic loads: vector memory, never a cached scalar read of host memory)
+  uint32_t* hw = reinterpret_cast<uint32_t*>(hs);
+  const uint32_t n = min(__hip_atomic_load(hw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), kRingReqs);
+  const uint32_t bytes = min(__hip_atomic_load(hw + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), kRingBlob);
+  // the slot's inputs and lists: [kRingPol, kRingBlobAt + bytes) into LDS
+  const uint32_t total = (uint32_t)(kRingBlobAt - kRingPol) + ((bytes + 15) & ~15u);
+  for (uint32_t o = lane * 16; o < total; o += kRingThreads * 16)
+    *(lds_v4*)(in + o) = *(const glb_v4*)(hs + kRingPol + o);
+  wave_sync();
+  const lds_u32* pol = (const lds_u32*)(in + (kRingPol - kRingPol));
+  const lds_u32* rem = (const lds_u32*)(in + (kRingRem - kRingPol));
+  const CG_LDS uint16_t* prt = (const CG_LDS uint16_t*)(in + (kRingPort - kRingPol));
+  const lds_u8* ing = in + (kRingIng - kRingPol);
+  const lds_u32* off = (const lds_u32*)(in + (kRingOff - kRingPol));
+  const lds_u8* blob = in + (kRingBlobAt - kRingPol);
+  const GlbTabs T{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
+                  (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+  for (uint32_t b = 0; b < n; b += kRingThreads) {  // uniform
+    const uint32_t i = b + lane;
+    const bool live = i < n;
+    const uint32_t prog = live ? lookup_prog(R, T, pol[i], ing[i] != 0, prt[i]) : kProgDeny;
+    // one program for every live lane: stage its block (and code map) once
+    const uint32_t p0 = (uint32_t)__shfl((int)prog, 0, kRingThreads);
+    const bool same = !__ballot(live && prog != p0);
+    bool lds = false;
+    if (same && p0 < R.nprogs) {
+      const HttpProg pg = HT.progs[p0];
+      lds = !(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= G.lds_cells;
+      if (lds && staged != p0) {
+        wave_sync();
+        for (uint32_t c = lane; c < pg.cell_count; c += kRingThreads) cells[c] = HT.cells[pg.cell_begin + c];
+        for (uint32_t c = lane; c < 64; c += kRingThreads)
+          reinterpret_cast<uint32_t*>(cmap)[c] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)p0 * 256)[c];
+        staged = p0;
+        wave_sync();
+      }
+    }
+    uint32_t v = 0;
+    if (live) {
+      const uint32_t a = min(off[i], bytes), e = min(max(off[i + 1], a), bytes);
+      HeadReader hr((glb_u8*)0, e - a, blob + a, true);
+      const bool ok = prog != kProgDeny && e - a <= kFieldsMaxList && parse_list_bytes(R, T, hr, sp, kRingThreads);
+      v = decide_request(HT, R, prog, ok, lds ? cells : nullptr, lds ? cmap : nullptr, hr, sp, kRingThreads, rem[i]);
+      hs[kRingOut + i] = (uint8_t)v;
+    }
+  }
+  // the verdicts before `done` (every lane's stores, then one release)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  wave_sync();
+  if (lane == 0)
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(hs) + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, HttpRawDev R, HttpRingDev G,
+                                                                 RingState* __restrict__ st) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ring_[];
+  lds_u32* lds = (lds_u32*)lds_ring_;
+  const uint32_t F = max(R.nfields, 1u), lane = threadIdx.x;
+  lds_u8* in = (lds_u8*)lds;  // slot bytes from kRingPol
+  lds_u32* sp = lds + (kRingBlobAt - kRingPol + kRingBlob) / 4 + lane;
+  // the staged program (block, code map): walked through generic pointers
+  uint8_t* cmap = (uint8_t*)(lds + (kRingBlobAt - kRingPol + kRingBlob) / 4 + F * kRingThreads);
+  uint32_t* cells = reinterpret_cast<uint32_t*>(cmap + 256);
+  const uint32_t wg = blockIdx.x;
+  const uint32_t per = G.nslots > wg ? (G.nslots - wg + G.nwg - 1) / G.nwg : 0u;  // slots of this workgroup
+  const bool mine = lane < per;
+  const uint32_t my = wg + lane * G.nwg;
+  const unsigned long long* hdr =
+      reinterpret_cast<const unsigned long long*>(G.slots + (size_t)(mine ? my : 0) * kRingSlotBytes);
+  const uint64_t t0 = wall_clock64();
+  uint32_t staged = 0xFFFFFFFFu;
+  for (bool last_pass = false;;) {
+    const unsigned long long sd = mine ? sys_load64(hdr) : 0ull;
+    const uint32_t seq = (uint32_t)sd, done = (uint32_t)(sd >> 32);
+    unsigned long long m = __ballot(mine && seq != done);
+    const bool busy = m != 0;
+    if (busy && lane == 0)
+      __hip_atomic_store(&st->last, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      ring_serve(HT, R, G, wg + j * G.nwg, (uint32_t)__shfl((int)seq, (int)j, kRingThreads), in, sp, cells, cmap,
+                 staged, lane);
+      if (lane == 0) atomicAdd(&st->served, 1ull);
+    }
+    if (last_pass) break;
+    // every iteration, busy or not: the stop word, idle and life bounds
+    // (workgroup 0 decides for all), so a launch under steady load ends too
+    const uint64_t now = wall_clock64();
+    if (wg == 0 && lane == 0) {
+      const unsigned long long lw = __hip_atomic_load(&st->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t since = lw > t0 ? lw : t0;
+      if (sys_load32(&G.ctl[kRingStop]) || now - since > G.idle_ticks || now - t0 > G.life_ticks)
+        __hip_atomic_store(&st->exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t ex = __hip_atomic_load(&st->exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // past life + idle every wave leaves without the exit word (a bound
+    // that does not depend on workgroup 0)
+    const bool out = ex || now - t0 > G.life_ticks + G.idle_ticks;
+    if (__shfl((int)out, 0, kRingThreads)) {
+      last_pass = true;  // serve what is ready one more time, then leave
+      continue;
+    }
+    if (!busy) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+int launch_http_ring_impl(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream) {
+  const size_t lds = ring_lds_bytes(R, G.lds_cells);
+  (void)hipFuncSetAttribute((const void*)http_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(http_ring_kernel, dim3(G.nwg), dim3(kRingThreads), lds, (hipStream_t)stream, HT, R, G,
+                     (RingState*)state);
+  return (int)hipGetLastError();
+}
+
 unsigned grid_for(size_t n, int cus, unsigned per_cu) {
   const size_t want = (n + kRawThreads - 1) / kRawThreads;
   return (unsigned)std::max<size_t>(1, std::min<size_t>(want, (size_t)cus * per_cu));
@@ -2204,6 +2363,15 @@ int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch
   hipLaunchKernelGGL(raw_seal_kernel, dim3(1), dim3(kSealThreads), lds, (hipStream_t)stream, R, L, (uint8_t*)batch,
                      epoch, ttab_off, tiles_off, total_bytes, (uint32_t)sort);
   return (int)hipGetLastError();
+}
+
+size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells) {
+  return (size_t)(kRingBlobAt - kRingPol + kRingBlob) + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 +
+         (size_t)cells * 4;
+}
+size_t http_ring_state_bytes() { return sizeof(RingState); }
+int launch_http_ring(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream) {
+  return launch_http_ring_impl(HT, R, G, state, stream);
 }
 
 int launch_http_raw_walk(const HttpDev& T, const HttpRawDev& R, bool lists, const uint8_t* raw, const uint64_t* off,

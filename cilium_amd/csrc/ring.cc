@@ -1,0 +1,229 @@
+// ring.cc — the persistent verdict ring (include/cilium_gpu.h cg_http_ring_*).
+//
+// Envoy decides one request per AccessFilter::decodeHeaders
+// (envoy/cilium_l7policy.cc:127-182), from many worker threads.  Through
+// cg_http_verdicts_fields_host such a call pays a staged copy in, a launch, a
+// copy out and a stream synchronization (~30 us).  The ring removes all four:
+// a resident kernel (kernels_http_raw.hip http_ring_kernel) polls slots in
+// fine-grained pinned host memory; a call claims a slot, writes its header
+// lists and inputs there, stores the slot's doorbell and spins on the
+// completion word the kernel stores after the verdicts.
+//
+// Lifetime: the kernel runs with the tables of one HTTP snapshot (held here,
+// so they outlive it).  A call first makes sure a launch with the handle's
+// current snapshot is running — a policy update stops the old launch (stop
+// word, stream synchronize) and starts a new one — so a call that begins
+// after an update returns is decided by the new tables.  A launch also ends
+// by itself after kIdleMs without a call or kLifeMs in all; a caller whose
+// doorbell it missed sees the stream idle while it waits and relaunches.
+// cg_http_ring_close and cg_close stop it.  Calls that do not fit a slot
+// (more than kRingReqs lists, more than kRingBlob bytes) or a snapshot the
+// device list parser does not take (more than 32 header fields) are decided
+// by cg_http_verdicts_fields_host instead.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "engine.h"
+#include "http.h"
+#include "kernels.h"
+#include "ring.h"
+
+namespace cg {
+
+namespace {
+
+constexpr uint32_t kIdleMs = 50, kLifeMs = 2000;
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+}  // namespace
+
+HttpRing::~HttpRing() {
+  stop_locked_noexcept();
+  if (state_) (void)hipFree(state_);
+  if (host_) (void)hipHostFree(host_);
+  if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
+}
+
+void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
+  if (workgroups < 1 || workgroups > 256) fail(CG_INVALID_ARGUMENT, "ring workgroups must be 1..256");
+  if (slots < 1 || slots > 64 * workgroups) fail(CG_INVALID_ARGUMENT, "ring slots must be 1..64 * workgroups");
+  e.set_device();
+  device_ = e.device;
+  nwg_ = workgroups;
+  nslots_ = slots;
+  hip_check(hipStreamCreateWithFlags((hipStream_t*)&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  const size_t bytes = kRingCtlBytes + (size_t)slots * kRingSlotBytes;
+  hip_check(hipHostMalloc((void**)&host_, bytes, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
+  memset(host_, 0, bytes);
+  hip_check(hipHostGetDevicePointer((void**)&dev_view_, host_, 0), "hipHostGetDevicePointer");
+  hip_check(hipMalloc(&state_, http_ring_state_bytes()), "hipMalloc");
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0) khz = 100000;
+  clock_khz_ = (uint64_t)khz;
+  claimed_.reset(new std::atomic<uint32_t>[slots]);
+  for (uint32_t i = 0; i < slots; ++i) claimed_[i].store(0);
+  seq_.assign(slots, 0);
+}
+
+uint32_t* HttpRing::slot_words(uint32_t i) const {
+  return reinterpret_cast<uint32_t*>(host_ + kRingCtlBytes + (size_t)i * kRingSlotBytes);
+}
+
+bool HttpRing::stream_idle() const { return hipStreamQuery((hipStream_t)stream_) == hipSuccess; }
+
+// Stop the running launch (if any) and wait for it; mu_ held.
+void HttpRing::stop_locked() {
+  if (!launched_) return;
+  __atomic_store_n(reinterpret_cast<uint32_t*>(host_) + kRingStop, 1u, __ATOMIC_SEQ_CST);
+  hip_check(hipStreamSynchronize((hipStream_t)stream_), "ring stop");
+  __atomic_store_n(reinterpret_cast<uint32_t*>(host_) + kRingStop, 0u, __ATOMIC_SEQ_CST);
+  launched_ = false;
+  snap_.reset();
+}
+
+void HttpRing::stop_locked_noexcept() {
+  std::lock_guard<std::mutex> lk(mu_);
+  try {
+    if (host_ && stream_) stop_locked();
+  } catch (...) {
+  }
+}
+
+void HttpRing::launch_locked(const std::shared_ptr<HttpSnapshot>& s) {
+  // the previous launch has ended (stop_locked, or it left by itself)
+  hip_check(hipStreamSynchronize((hipStream_t)stream_), "ring launch");
+  if (launches_) {  // keep its served count
+    unsigned long long st[3] = {0, 0, 0};
+    hip_check(hipMemcpy(st, state_, sizeof(st), hipMemcpyDeviceToHost), "D2H");
+    served_before_ += st[2];
+  }
+  hip_check(hipMemsetAsync(state_, 0, http_ring_state_bytes(), (hipStream_t)stream_), "hipMemsetAsync");
+  HttpRingDev G{};
+  G.slots = dev_view_ + kRingCtlBytes;
+  G.ctl = reinterpret_cast<uint32_t*>(dev_view_);
+  G.nslots = nslots_;
+  G.nwg = nwg_;
+  G.idle_ticks = clock_khz_ * kIdleMs;
+  G.life_ticks = clock_khz_ * kLifeMs;
+  // the largest walked, rebased program that fits beside the slot and spans
+  uint32_t maxc = 0;
+  for (const auto& pg : s->progs)
+    if (!(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased)) maxc = std::max(maxc, pg.cell_count);
+  const size_t base = ring_lds_bytes(s->raw, 0);
+  const uint32_t room = base < 160 * 1024 ? (uint32_t)((160 * 1024 - base) / 4) : 0u;
+  G.lds_cells = std::min(maxc, room);
+  check_launch_rc(launch_http_ring(s->dev, s->raw, G, state_, stream_));
+  s->fence.record(stream_);
+  snap_ = s;
+  snap_ptr_.store(s.get(), std::memory_order_release);
+  launched_.store(true, std::memory_order_release);
+  launch_ns_.store(now_ns(), std::memory_order_relaxed);
+  ++launches_;
+}
+
+void HttpRing::check_launch_rc(int rc) { hip_check(rc, "ring kernel launch"); }
+
+// A launch with snapshot s is running (or about to) when this returns.
+void HttpRing::ensure(const std::shared_ptr<HttpSnapshot>& s) {
+  const uint64_t t = now_ns();
+  // fast path: the same tables, served a call recently enough that the
+  // launch cannot have idled out, and young enough not to have hit its life
+  if (launched_.load(std::memory_order_acquire) && snap_ptr_.load(std::memory_order_acquire) == s.get() &&
+      t - last_ns_.load(std::memory_order_relaxed) < (uint64_t)kIdleMs * 500000ull &&
+      t - launch_ns_.load(std::memory_order_relaxed) < (uint64_t)kLifeMs * 500000ull)
+    return;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (snap_ != s) {
+    stop_locked();
+    launch_locked(s);
+  } else if (!launched_ || stream_idle()) {
+    launched_ = false;
+    launch_locked(s);
+  }
+  snap_ptr_.store(s.get(), std::memory_order_release);
+}
+
+void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const uint8_t* blob, const uint64_t* off,
+                        size_t n, const uint32_t* pol, const uint8_t* ing, const uint16_t* port, const uint32_t* rem,
+                        uint8_t* out) {
+  (void)e;
+  ensure(s);
+  // a free slot (callers never hold more than one)
+  uint32_t i = next_.fetch_add(1, std::memory_order_relaxed) % nslots_;
+  for (uint32_t k = 1;; ++k) {
+    uint32_t z = 0;
+    if (claimed_[i].compare_exchange_strong(z, 1u, std::memory_order_acquire)) break;
+    i = (i + 1) % nslots_;
+    if (k % nslots_ == 0) std::this_thread::yield();
+  }
+  uint8_t* sl = host_ + kRingCtlBytes + (size_t)i * kRingSlotBytes;
+  const uint64_t a0 = off[0];
+  const uint32_t bytes = (uint32_t)(off[n] - a0);
+  memcpy(sl + kRingPol, pol, n * 4);
+  memcpy(sl + kRingRem, rem, n * 4);
+  memcpy(sl + kRingPort, port, n * 2);
+  memcpy(sl + kRingIng, ing, n);
+  uint32_t* o = reinterpret_cast<uint32_t*>(sl + kRingOff);
+  for (size_t k = 0; k <= n; ++k) o[k] = (uint32_t)(off[k] - a0);
+  if (bytes) memcpy(sl + kRingBlobAt, blob + a0, bytes);
+  uint32_t* w = slot_words(i);
+  w[2] = (uint32_t)n;
+  w[3] = bytes;
+  const uint32_t seq = ++seq_[i] ? seq_[i] : ++seq_[i];  // never 0 (the slot's initial done)
+  __atomic_store_n(&w[0], seq, __ATOMIC_RELEASE);         // the doorbell, after the slot's bytes
+  const uint64_t t0 = now_ns();
+  uint64_t checked = t0;
+  while (__atomic_load_n(&w[1], __ATOMIC_ACQUIRE) != seq) {
+    cpu_relax();
+    const uint64_t t = now_ns();
+    if (t - checked < 20000) continue;
+    checked = t;
+    // not served within 20 us: the launch may have left (idle or life)
+    // between ensure() and the doorbell — relaunch, the slot is still ready
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (__atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == seq) break;
+      if (stream_idle()) {
+        launched_ = false;
+        launch_locked(snap_ ? snap_ : s);
+      }
+    }
+    if (t - t0 > 5ull * 1000 * 1000 * 1000) {
+      claimed_[i].store(0, std::memory_order_release);
+      fail(CG_UNKNOWN_ERROR, "ring: a call was not served within 5 s");
+    }
+  }
+  memcpy(out, sl + kRingOut, n);
+  last_ns_.store(now_ns(), std::memory_order_relaxed);
+  claimed_[i].store(0, std::memory_order_release);
+}
+
+void HttpRing::stats(uint64_t* served, uint64_t* launches) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (launches) *launches = launches_;
+  if (served) {
+    // the running launch's count (its state is reset per launch) plus the
+    // finished ones'
+    unsigned long long st[3] = {0, 0, 0};
+    hip_check(hipMemcpy(st, state_, sizeof(st), hipMemcpyDeviceToHost), "D2H");
+    *served = served_before_ + st[2];
+  }
+}
+
+void HttpRing::close() {
+  std::lock_guard<std::mutex> lk(mu_);
+  stop_locked();
+}
+
+}  // namespace cg

@@ -1,0 +1,56 @@
+// ring.h — the persistent verdict ring of a handle (ring.cc).
+#pragma once
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "engine.h"
+
+namespace cg {
+
+struct HttpSnapshot;
+
+class HttpRing {
+ public:
+  HttpRing() = default;
+  HttpRing(const HttpRing&) = delete;
+  HttpRing& operator=(const HttpRing&) = delete;
+  ~HttpRing();
+  void open(Engine& e, uint32_t workgroups, uint32_t slots);
+  // n <= kRingReqs lists of at most kRingBlob bytes in all, on a snapshot
+  // with lists_ok (the caller checks)
+  void verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const uint8_t* blob, const uint64_t* off, size_t n,
+                const uint32_t* pol, const uint8_t* ing, const uint16_t* port, const uint32_t* rem, uint8_t* out);
+  void stats(uint64_t* served, uint64_t* launches);
+  void close();
+
+ private:
+  void ensure(const std::shared_ptr<HttpSnapshot>& s);
+  void launch_locked(const std::shared_ptr<HttpSnapshot>& s);
+  void stop_locked();
+  void stop_locked_noexcept();
+  bool stream_idle() const;
+  uint32_t* slot_words(uint32_t i) const;
+  static void check_launch_rc(int rc);
+
+  int device_ = 0;
+  uint32_t nwg_ = 0, nslots_ = 0;
+  uint8_t* host_ = nullptr;      // control words + slots (hipHostMalloc, coherent, mapped)
+  uint8_t* dev_view_ = nullptr;  // the same memory as the device addresses it
+  void* state_ = nullptr;        // the launch's RingState (device memory)
+  void* stream_ = nullptr;       // hipStream_t of the launches
+  uint64_t clock_khz_ = 100000;  // wall clock of the device (hipDeviceAttributeWallClockRate)
+  std::mutex mu_;                // launches, stops, stats
+  std::shared_ptr<HttpSnapshot> snap_;  // the running launch's tables
+  std::atomic<const HttpSnapshot*> snap_ptr_{nullptr};
+  std::atomic<bool> launched_{false};
+  std::atomic<uint64_t> launch_ns_{0}, last_ns_{0};
+  uint64_t launches_ = 0, served_before_ = 0;
+  std::unique_ptr<std::atomic<uint32_t>[]> claimed_;  // per slot: a call owns it
+  std::vector<uint32_t> seq_;                          // per slot, under its claim
+  std::atomic<uint32_t> next_{0};
+};
+
+}  // namespace cg

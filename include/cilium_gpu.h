@@ -521,6 +521,27 @@ int cg_http_verdicts_fields_host(uint64_t h, const uint8_t* hdr_blob, const uint
                                  const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                                  const uint32_t* remote, uint8_t* out);
 
+/* The persistent verdict ring: Envoy-sized calls (AccessFilter::decodeHeaders
+ * decides one request, envoy/cilium_l7policy.cc:127-182) without a launch,
+ * staged copies or a stream synchronization per call.  cg_http_ring_open
+ * starts `workgroups` one-wave workgroups (1..256) that poll `slots`
+ * (1..64 * workgroups) request slots in pinned host memory; a call of
+ * cg_http_ring_verdicts claims a slot, writes its header lists there, rings
+ * the slot's doorbell and spins until the kernel has written the verdicts.
+ * Same inputs, outputs and verdicts as cg_http_verdicts_fields_host (which
+ * decides calls past a slot: more than 256 lists or 32 KiB of list bytes,
+ * and snapshots walking more than 32 header fields).  The kernel serves the
+ * handle's current policy: a cg_http_policy_update restarts it before the
+ * next call; it leaves by itself after 50 ms without a call (the next call
+ * starts it again, ~20 us).  cg_http_ring_close (or cg_close) stops it. */
+int cg_http_ring_open(uint64_t h, uint32_t workgroups, uint32_t slots);
+int cg_http_ring_verdicts(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
+                          const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
+                          const uint32_t* remote, uint8_t* out);
+/* Calls served by the ring's kernels and launches made, cumulative. */
+int cg_http_ring_stats(uint64_t h, uint64_t* served, uint64_t* launches);
+int cg_http_ring_close(uint64_t h);
+
 /* NetworkPolicyMap::Allowed per slot (cilium_network_policy.h:223-237):
  * d_out[slot] = 1 allow, 0 deny (→ 403), in batch slot order.  d_arena may
  * be NULL when no record overflowed.  Per-(policy,direction,port) allowed/

@@ -1,0 +1,138 @@
+"""The persistent verdict ring (cg_http_ring_*, csrc/ring.cc + kernels_http_raw.hip
+http_ring_kernel): Envoy-sized calls (AccessFilter::decodeHeaders decides one
+request, envoy/cilium_l7policy.cc:127-182) decided by a resident kernel that
+polls request slots in pinned host memory.  Verdicts against the oracle and
+the staged entry; calls from many threads; a policy update between calls;
+the kernel's idle exit and relaunch; calls past a slot; open / close.  The
+test prints throughput and asserts no timing."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from cilium_amd import _native as N
+from cilium_amd import synth
+from cilium_amd.classifier import Classifier
+from test_http_fields_gpu import _join, _oracle, _split
+
+
+def test_ring_needs_a_gpu(host):
+    with pytest.raises(N.CiliumGPUError):
+        host.http_ring_open(2, 4)
+
+
+def _pool(n, seed):
+    pols, info = synth.http10k_rules()
+    rq = synth.http10k_requests(n, info, seed=seed)
+    lists = _split(rq["hdr_blob"], rq["hdr_off"])
+    args = (np.asarray(rq["policy"], np.uint32), np.asarray(rq["ingress"], np.uint8),
+            np.asarray(rq["port"], np.uint16), np.asarray(rq["remote"], np.uint32))
+    return pols, lists, args
+
+
+@pytest.mark.gpu
+def test_gpu_ring_calls():
+    cl = Classifier(device=0)
+    try:
+        pols, lists, args = _pool(4096, 71)
+        cl.update_http_policy(pols)
+        blob, off = _join(lists)
+        want = _oracle(pols, *args, blob, off)
+        assert np.array_equal(want, cl.http_verdicts_fields(*args, blob, off))
+        cl.http_ring_open(8, 16)
+        # single-request calls, the Envoy shape
+        t0 = time.perf_counter()
+        for i in range(1000):
+            b, o = _join(lists[i:i + 1])
+            got = cl.http_ring_verdicts(*(a[i:i + 1] for a in args), b, o)
+            assert got[0] == want[i], i
+        dt = time.perf_counter() - t0
+        print(f"ring, 1 thread, batch 1 (Python ctypes): {1000 / dt:.0f} calls/s, {dt / 1000 * 1e6:.1f} us per call")
+        # batches of 16 and 256 (a slot's limit), and 300 (past it: the staged entry)
+        for B in (16, 256, 300):
+            for a in range(0, 1200, B):
+                b, o = _join(lists[a:a + B])
+                got = cl.http_ring_verdicts(*(x[a:a + B] for x in args), b, o)
+                assert np.array_equal(got, want[a:a + B]), (B, a)
+        # an empty call
+        assert len(cl.http_ring_verdicts([], [], [], [], np.zeros(1, np.uint8), np.zeros(1, np.uint64))) == 0
+        # 16 threads at once, each with its own calls
+        errs = []
+
+        def worker(t):
+            try:
+                for k in range(150):
+                    i = (t * 257 + k * 13) % len(lists)
+                    b, o = _join(lists[i:i + 1])
+                    if cl.http_ring_verdicts(*(x[i:i + 1] for x in args), b, o)[0] != want[i]:
+                        errs.append((t, i))
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        dt = time.perf_counter() - t0
+        assert not errs, errs[:5]
+        print(f"ring, 16 threads, batch 1 (Python ctypes): {16 * 150 / dt:.0f} calls/s")
+        st = cl.http_ring_stats()
+        assert st["served"] >= 1000 + 16 * 150 and st["launches"] >= 1, st
+        # the kernel leaves after 50 ms without a call; the next call starts it again
+        time.sleep(0.3)
+        b, o = _join(lists[:64])
+        assert np.array_equal(cl.http_ring_verdicts(*(x[:64] for x in args), b, o), want[:64])
+        assert cl.http_ring_stats()["launches"] > st["launches"]
+        cl.http_ring_close()
+        with pytest.raises(N.CiliumGPUError):
+            cl.http_ring_verdicts(*(x[:1] for x in args), *_join(lists[:1]))
+    finally:
+        cl.close()
+
+
+@pytest.mark.gpu
+def test_gpu_ring_policy_update_and_fallbacks():
+    """A policy update between calls: the next call is decided by the new
+    tables (the ring restarts its kernel).  A snapshot walking more than 32
+    fields takes the staged entry.  cg_close stops a running ring."""
+    cl = Classifier(device=0)
+    try:
+        pols = synth.starwars_policy()
+        cl.update_http_policy(pols)
+        rq = synth.starwars_requests(2000, seed=72)
+        lists = _split(rq["hdr_blob"], rq["hdr_off"])
+        args = tuple(np.asarray(rq[k], dt) for k, dt in (("policy", np.uint32), ("ingress", np.uint8),
+                                                          ("port", np.uint16), ("remote", np.uint32)))
+        blob, off = _join(lists)
+        cl.http_ring_open(4, 8)
+        want = _oracle(pols, *args, blob, off)
+        got = np.concatenate([cl.http_ring_verdicts(*(x[a:a + 100] for x in args), *_join(lists[a:a + 100]))
+                              for a in range(0, 2000, 100)])
+        assert np.array_equal(got, want) and 0.05 < want.mean() < 0.95
+        # allow everything on the same policy names: every request is allowed now
+        open_pols = [{"name": p["name"], "policy": p.get("policy", 0),
+                      "egress_per_port_policies": [{"port": 80, "rules": [{"remote_policies": []}]}],
+                      "ingress_per_port_policies": [{"port": 80, "rules": [{"remote_policies": []}]}]}
+                     for p in pols]
+        cl.update_http_policy(open_pols)
+        want2 = _oracle(open_pols, *args, blob, off)
+        got2 = np.concatenate([cl.http_ring_verdicts(*(x[a:a + 100] for x in args), *_join(lists[a:a + 100]))
+                               for a in range(0, 2000, 100)])
+        assert np.array_equal(got2, want2) and not np.array_equal(want, want2)
+        # 40 walked fields: past the device list parser, decided by the staged entry
+        names = ["x-f%02d" % i for i in range(40)]
+        many = [{"name": "m", "policy": 0, "ingress_per_port_policies": [{"port": 80, "rules": [
+            {"remote_policies": [], "http_rules": {"http_rules": [
+                {"headers": [{"name": nm, "exact_match": "v"}]} for nm in names]}}]}]}]
+        cl.update_http_policy(many)
+        ml = [b":method\0GET\0x-f%02d\0%s\0" % (i % 40, b"v" if i % 3 else b"w") for i in range(200)]
+        mb, mo = _join(ml)
+        margs = (np.zeros(200, np.uint32), np.ones(200, np.uint8), np.full(200, 80, np.uint16), np.zeros(200, np.uint32))
+        assert np.array_equal(cl.http_ring_verdicts(*margs, mb, mo), _oracle(many, *margs, mb, mo))
+        cl.update_http_policy(pols)
+        assert cl.http_ring_verdicts(*(x[:1] for x in args), *_join(lists[:1]))[0] == want[0]
+    finally:
+        cl.close()  # stops the ring

@@ -5,8 +5,11 @@
 // (envoy/cilium_l7policy.cc:127-182 → NetworkPolicyMap::Allowed,
 // cilium_network_policy.h:223-237).  A drop-in hands the engine the header
 // lists it has (cg_http_pack's name\0value\0 input) in batches of B requests.
-// Two host entries are timed, each for B in {1, 16, 256, 4096, 65536} and 1
+// Three host entries are timed, each for B in {1, 16, 256, 4096, 65536} and 1
 // and 16 submitting threads:
+//   ring    cg_http_ring_verdicts: the persistent verdict ring (a resident
+//           kernel polls request slots in pinned host memory: no launch, no
+//           copies, no stream synchronization per call; B <= 256)
 //   fields  cg_http_verdicts_fields_host: calls of <= 1024 lists packed on
 //           the calling thread (one copy in, one launch, one copy out),
 //           larger ones: lists → pinned staging → H2D → grouping/packing on
@@ -23,7 +26,7 @@
 //
 // Build (in-tree, CPU): g++ -O2 -std=c++17 -I include tools/http_latency.cc
 //   -L cilium_amd -lciliumgpu -lpthread -Wl,-rpath,'$ORIGIN/../cilium_amd' -o tools/http_latency
-// Run (GPU box): tools/http_latency <dir> [seconds per point]
+// Run (GPU box): tools/http_latency <dir> [seconds per point] [entries: ring,fields,pack]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -63,7 +66,8 @@ struct Result {
 
 // One submitting thread: batches of B consecutive pool requests, starting at
 // a per-thread offset, until the deadline.
-void submit(uint64_t h, const Pool& p, bool pack, size_t B, size_t start, double seconds, Result* r) {
+void submit(uint64_t h, const Pool& p, int mode, size_t B, size_t start, double seconds, Result* r) {
+  const bool pack = mode == 2;
   std::vector<uint8_t> out(B);
   std::vector<uint8_t> batch;
   std::vector<uint32_t> order;
@@ -84,6 +88,9 @@ void submit(uint64_t h, const Pool& p, bool pack, size_t B, size_t start, double
                         batch.size(), order.data(), &nslots, arena.data(), arena.size(), &used);
       if (rc == CG_OK)
         rc = cg_http_verdicts_host(h, batch.data(), nslots, order.data(), B, arena.data(), used, out.data());
+    } else if (mode == 1) {
+      rc = cg_http_ring_verdicts(h, p.blob.data(), &p.off[a], B, &p.pol[a], &p.ing[a], &p.port[a], &p.rem[a],
+                                 out.data());
     } else {
       rc = cg_http_verdicts_fields_host(h, p.blob.data(), &p.off[a], B, &p.pol[a], &p.ing[a], &p.port[a], &p.rem[a],
                                         out.data());
@@ -113,6 +120,7 @@ int main(int argc, char** argv) {
   }
   const std::string d = argv[1];
   const double seconds = argc > 2 ? atof(argv[2]) : 1.0;
+  const std::string entries = argc > 3 ? argv[3] : "ring,fields,pack";
   Pool p;
   p.blob = load<uint8_t>(d + "/blob.bin");
   p.off = load<uint64_t>(d + "/off.bin");
@@ -141,21 +149,30 @@ int main(int argc, char** argv) {
     return 2;
   }
   int rc = 0;
-  // modes: 0 cg_http_verdicts_fields_host, 2 pack + host
-  for (const int mode : {0, 2}) {
+  const char* wg = getenv("CILIUM_RING_WORKGROUPS");
+  const char* sl = getenv("CILIUM_RING_SLOTS");
+  const uint32_t ring_wg = wg ? (uint32_t)atoi(wg) : 16, ring_slots = sl ? (uint32_t)atoi(sl) : 32;
+  // modes: 1 cg_http_ring_verdicts, 0 cg_http_verdicts_fields_host, 2 pack + host
+  for (const int mode : {1, 0, 2}) {
+    const char* name = mode == 1 ? "ring" : mode == 0 ? "fields" : "pack";
+    if (entries.find(name) == std::string::npos) continue;
     const bool pack = mode == 2;
+    if (mode == 1 && cg_http_ring_open(h, ring_wg, ring_slots) != CG_OK) {
+      fprintf(stderr, "cg_http_ring_open: %s\n", cg_last_error());
+      return 2;
+    }
     for (const size_t B : {(size_t)1, (size_t)16, (size_t)256, (size_t)4096, (size_t)65536}) {
-      if (B > p.n) continue;
+      if (B > p.n || (mode == 1 && B > 256)) continue;
       for (const int threads : {1, 16}) {
         {  // warm-up (pinned buffers, workers, launch caches) outside the clock
           Result w;
-          submit(h, p, pack, B, 0, 0.05, &w);
+          submit(h, p, mode, B, 0, 0.05, &w);
         }
         std::vector<Result> res(threads);
         std::vector<std::thread> th;
         const auto t0 = std::chrono::steady_clock::now();
         for (int t = 0; t < threads; ++t)
-          th.emplace_back(submit, h, std::cref(p), pack, B, (size_t)t * 7919 * B, seconds, &res[t]);
+          th.emplace_back(submit, h, std::cref(p), mode, B, (size_t)t * 7919 * B, seconds, &res[t]);
         for (auto& x : th) x.join();
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::vector<double> lat;
@@ -169,12 +186,20 @@ int main(int argc, char** argv) {
         printf("{\"metric\": \"HTTP verdicts through the host C ABI at Envoy batch sizes\", \"entry\": \"%s\", "
                "\"batch\": %zu, \"threads\": %d, \"calls\": %llu, \"requests_per_s\": %.1f, \"calls_per_s\": %.1f, "
                "\"p50_us\": %.1f, \"p99_us\": %.1f, \"bad_calls\": %llu}\n",
-               pack ? "cg_http_pack+cg_http_verdicts_host" : "cg_http_verdicts_fields_host", B, threads,
+               pack ? "cg_http_pack+cg_http_verdicts_host" : mode == 1 ? "cg_http_ring_verdicts"
+                                                            : "cg_http_verdicts_fields_host", B, threads,
                (unsigned long long)calls, (double)reqs / sec, (double)calls / sec, pct(lat, 0.5), pct(lat, 0.99),
                (unsigned long long)bad);
         fflush(stdout);
         if (bad) rc = 1;
       }
+    }
+    if (mode == 1) {
+      uint64_t served = 0, launches = 0;
+      cg_http_ring_stats(h, &served, &launches);
+      printf("{\"ring\": {\"workgroups\": %u, \"slots\": %u, \"served\": %llu, \"launches\": %llu}}\n", ring_wg,
+             ring_slots, (unsigned long long)served, (unsigned long long)launches);
+      cg_http_ring_close(h);
     }
   }
   cg_close(h);

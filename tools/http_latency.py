@@ -2,7 +2,8 @@
 config-5 header lists (the 10K-rule set) into a directory, computes the
 pool's verdicts through the engine in one batch, checks a subsample against
 the oracle (Envoy-faithful rule scan), then runs the C driver, which times
-cg_http_verdicts_fields_host and cg_http_pack + cg_http_verdicts_host at batch
+cg_http_ring_verdicts (the persistent ring), cg_http_verdicts_fields_host and
+cg_http_pack + cg_http_verdicts_host at batch
 sizes 1 … 64K from 1 and 16 threads (one JSON line per point).
 
     python tools/http_latency.py [--pool N] [--seconds S] [--out DIR]
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--pool", type=int, default=1 << 20)
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--entries", default="ring,fields,pack", help="entries to time (ring, fields, pack)")
     args = ap.parse_args()
     import oracle
     from cilium_amd import synth
@@ -55,7 +57,7 @@ def main():
     want.astype(np.uint8).tofile(os.path.join(d, "want.bin"))
     print(json.dumps({"pool": n, "dir": d, "oracle_checked": k, "allow_frac": float(want.mean())}), flush=True)
     exe = os.path.join(ROOT, "tools", "http_latency")
-    rc = subprocess.call([exe, d, str(args.seconds)])
+    rc = subprocess.call([exe, d, str(args.seconds), args.entries])
     sys.exit(rc)
 
 
