@@ -321,11 +321,27 @@ constexpr uint32_t kRawFnvInit = 2166136261u;
 // verdicts and the blob.
 constexpr uint32_t kRingReqs = 256;          // requests per slot (larger calls take the staged path)
 constexpr uint32_t kRingBlob = 32 * 1024;    // list bytes per slot
-constexpr size_t kRingPol = 64, kRingRem = kRingPol + 4 * kRingReqs, kRingPort = kRingRem + 4 * kRingReqs,
-                 kRingIng = kRingPort + 2 * kRingReqs, kRingOff = kRingIng + kRingReqs,
-                 kRingOut = kRingOff + 4 * (kRingReqs + 4), kRingBlobAt = kRingOut + kRingReqs,
-                 kRingSlotBytes = (kRingBlobAt + kRingBlob + 255) & ~(size_t)255;
-static_assert(kRingBlobAt % 16 == 0, "the blob is copied in 16-byte units");
+// A slot: [header: 64 B][verdicts: kRingReqs B][data], the data packed for
+// the call's n so a small call is a few hundred contiguous bytes (one round
+// of 16-byte loads over the bus): policy[n] u32, remote[n] u32, port[n] u16,
+// ingress[n] u8 (each padded to 4 bytes), list offsets[n + 1] u32 relative
+// to the blob, the blob from the next 16-byte boundary.
+constexpr size_t kRingOut = 64, kRingData = kRingOut + kRingReqs;
+struct RingLayout {
+  uint32_t rem, port, ing, off, blob;  // byte offsets in the data
+};
+CG_HD inline RingLayout ring_layout(uint32_t n) {
+  RingLayout L;
+  L.rem = 4 * n;
+  L.port = 8 * n;
+  L.ing = L.port + ((2 * n + 3) & ~3u);
+  L.off = L.ing + ((n + 3) & ~3u);
+  L.blob = (L.off + 4 * (n + 1) + 15) & ~15u;
+  return L;
+}
+constexpr size_t kRingDataMax = ((15 * kRingReqs + 4 + 16) & ~(size_t)15) + kRingBlob;
+constexpr size_t kRingSlotBytes = (kRingData + kRingDataMax + 255) & ~(size_t)255;
+static_assert(kRingData % 16 == 0, "the data is copied in 16-byte units");
 // ring control words (host memory, before the slots): the host's stop word
 // (the device only reads host memory with loads and writes it with plain
 // stores: no read-modify-write over the bus)

@@ -10,6 +10,8 @@
 #include "ipcache.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <tuple>
@@ -217,6 +219,15 @@ void IpcacheState::build_tables() {
   }
   if (ent6.empty()) ent6.assign(4, 0);
   if (crowd6.empty()) crowd6.assign(128, 0);
+  if (getenv("CILIUM_GPU_DEBUG")) {
+    size_t c24 = 0, direct = 0;
+    for (uint32_t q = 0; q < 65536; ++q)
+      if ((uint32_t)l16[q] == 0) ++c24, direct += (l16x[4 * q + 3] >> 16) & 1;
+    fprintf(stderr, "[cilium-gpu] ipcache: v4 chunks %zu (%zu /16s chunked, %zu direct), %.1f MB; v6 runs %zu (%.1f MB), "
+            "buckets 2^%u, set %zu (%.1f MB), crowd lines %zu\n", chunks.size() / 256, c24, direct,
+            chunks.size() * 8 / 1e6, runs6.size() / 4, runs6.size() * 8 / 1e6, v6_bits, ent6.size() / 4,
+            ent6.size() * 4 / 1e6, crowd6.size() / 128);
+  }
 }
 
 IpcacheDev IpcacheState::host_view() const {

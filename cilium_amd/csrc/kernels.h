@@ -95,5 +95,7 @@ int launch_http_raw_walk(const HttpDev& T, const HttpRawDev& R, bool lists, cons
 size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells);
 size_t http_ring_state_bytes();
 int launch_http_ring(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream);
+// the device's wall_clock64() into *d_out (ring.cc measures its rate)
+int ring_clock(unsigned long long* d_out, void* stream);
 
 }  // namespace cg

@@ -2056,6 +2056,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_walk_kernel(HttpDev HT, HttpR
 // what is ready one last time and leaves) — ring.cc relaunches on the next
 // call.
 constexpr uint32_t kRingThreads = 64;
+bool lds_tables_fit(const HttpRawDev& R);
 // device memory of a launch: the exit word, the wall clock of the last call
 // served, slots served (read by cg_http_ring_stats)
 struct RingState {
@@ -2070,32 +2071,64 @@ __device__ __forceinline__ unsigned long long sys_load64(const unsigned long lon
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, uint32_t s,
-                                           uint32_t seq, lds_u8* in, lds_u32* sp, uint32_t* cells, uint8_t* cmap,
-                                           uint32_t& staged, uint32_t lane) {
+// The program block (and code map) of p into LDS: 16-byte loads, eight in
+// flight per lane, so a 64-KB block takes a few round trips.
+__device__ __forceinline__ void ring_stage(const HttpDev& HT, const HttpRawDev& R, const HttpProg& pg, uint32_t p,
+                                           lds_u32* cells, lds_u32* cmap, uint32_t lane) {
+  const uint32_t* src = HT.cells + pg.cell_begin;
+  const uint32_t n = pg.cell_count;
+  uint32_t done = 0;
+  if ((((uintptr_t)src) & 15) == 0) {
+    const uint32_t n4 = n / 4;
+    for (uint32_t c0 = lane; c0 < n4; c0 += kRingThreads * 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const uint4*>(src)[min(c0 + u * kRingThreads, n4 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c0 + u * kRingThreads < n4) *(lds_v4*)(cells + 4 * (c0 + u * kRingThreads)) = to_v4(v[u]);
+    }
+    done = 4 * n4;
+  }
+  for (uint32_t c = done + lane; c < n; c += kRingThreads) cells[c] = src[c];
+  for (uint32_t c = lane; c < 64; c += kRingThreads) cmap[c] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)p * 256)[c];
+}
+
+template <class Tabs>
+__device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& R, const Tabs& T, const HttpRingDev& G,
+                                           uint32_t s, uint32_t seq, lds_u8* in, lds_u32* sp, lds_u32* cells,
+                                           lds_u32* cmap, uint32_t& staged, uint32_t lane) {
   uint8_t* hs = G.slots + (size_t)s * kRingSlotBytes;
   // (atomic loads: vector memory, never a cached scalar read of host memory)
   uint32_t* hw = reinterpret_cast<uint32_t*>(hs);
   const uint32_t n = min(__hip_atomic_load(hw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), kRingReqs);
   const uint32_t bytes = min(__hip_atomic_load(hw + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), kRingBlob);
-  // the slot's inputs and lists: [kRingPol, kRingBlobAt + bytes) into LDS
-  const uint32_t total = (uint32_t)(kRingBlobAt - kRingPol) + ((bytes + 15) & ~15u);
-  for (uint32_t o = lane * 16; o < total; o += kRingThreads * 16)
-    *(lds_v4*)(in + o) = *(const glb_v4*)(hs + kRingPol + o);
+  const RingLayout L = ring_layout(n);
+  // the call's data into LDS: every load issued before the stores (one
+  // round trip over the bus for a small call)
+  const uint32_t total = (L.blob + bytes + 15) & ~15u;
+  const uint8_t* src = hs + kRingData;
+  for (uint32_t o0 = lane * 16; o0 < total; o0 += kRingThreads * 16 * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      v[u] = to_uint4(*(const glb_v4*)(src + min(o0 + u * kRingThreads * 16, total - 16)));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (o0 + u * kRingThreads * 16 < total) *(lds_v4*)(in + o0 + u * kRingThreads * 16) = to_v4(v[u]);
+  }
   wave_sync();
-  const lds_u32* pol = (const lds_u32*)(in + (kRingPol - kRingPol));
-  const lds_u32* rem = (const lds_u32*)(in + (kRingRem - kRingPol));
-  const CG_LDS uint16_t* prt = (const CG_LDS uint16_t*)(in + (kRingPort - kRingPol));
-  const lds_u8* ing = in + (kRingIng - kRingPol);
-  const lds_u32* off = (const lds_u32*)(in + (kRingOff - kRingPol));
-  const lds_u8* blob = in + (kRingBlobAt - kRingPol);
-  const GlbTabs T{(glb_u32*)R.nkeys, (glb_u32*)R.fslots, (glb_u32*)R.phash_keys, (glb_u32*)R.phash_vals,
-                  (glb_u32*)R.walk_bits, (glb_u32*)R.dflt, (glb_u8*)R.fnames};
+  const lds_u32* pol = (const lds_u32*)in;
+  const lds_u32* rem = (const lds_u32*)(in + L.rem);
+  const CG_LDS uint16_t* prt = (const CG_LDS uint16_t*)(in + L.port);
+  const lds_u8* ing = in + L.ing;
+  const lds_u32* off = (const lds_u32*)(in + L.off);
+  const lds_u8* blob = in + L.blob;
   for (uint32_t b = 0; b < n; b += kRingThreads) {  // uniform
     const uint32_t i = b + lane;
     const bool live = i < n;
     const uint32_t prog = live ? lookup_prog(R, T, pol[i], ing[i] != 0, prt[i]) : kProgDeny;
-    // one program for every live lane: stage its block (and code map) once
+    // one program for every live lane: its block (and code map) in LDS
     const uint32_t p0 = (uint32_t)__shfl((int)prog, 0, kRingThreads);
     const bool same = !__ballot(live && prog != p0);
     bool lds = false;
@@ -2104,9 +2137,7 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
       lds = !(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= G.lds_cells;
       if (lds && staged != p0) {
         wave_sync();
-        for (uint32_t c = lane; c < pg.cell_count; c += kRingThreads) cells[c] = HT.cells[pg.cell_begin + c];
-        for (uint32_t c = lane; c < 64; c += kRingThreads)
-          reinterpret_cast<uint32_t*>(cmap)[c] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)p0 * 256)[c];
+        ring_stage(HT, R, pg, p0, cells, cmap, lane);
         staged = p0;
         wave_sync();
       }
@@ -2116,7 +2147,8 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
       const uint32_t a = min(off[i], bytes), e = min(max(off[i + 1], a), bytes);
       HeadReader hr((glb_u8*)0, e - a, blob + a, true);
       const bool ok = prog != kProgDeny && e - a <= kFieldsMaxList && parse_list_bytes(R, T, hr, sp, kRingThreads);
-      v = decide_request(HT, R, prog, ok, lds ? cells : nullptr, lds ? cmap : nullptr, hr, sp, kRingThreads, rem[i]);
+      v = decide_request(HT, R, prog, ok, lds ? (const uint32_t*)cells : nullptr, lds ? (const uint8_t*)cmap : nullptr,
+                         hr, sp, kRingThreads, rem[i]);
       hs[kRingOut + i] = (uint8_t)v;
     }
   }
@@ -2127,16 +2159,23 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
     __hip_atomic_store(reinterpret_cast<uint32_t*>(hs) + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+template <bool kLdsTabs>
 __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, HttpRawDev R, HttpRingDev G,
                                                                  RingState* __restrict__ st) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_ring_[];
   lds_u32* lds = (lds_u32*)lds_ring_;
   const uint32_t F = max(R.nfields, 1u), lane = threadIdx.x;
-  lds_u8* in = (lds_u8*)lds;  // slot bytes from kRingPol
-  lds_u32* sp = lds + (kRingBlobAt - kRingPol + kRingBlob) / 4 + lane;
-  // the staged program (block, code map): walked through generic pointers
-  uint8_t* cmap = (uint8_t*)(lds + (kRingBlobAt - kRingPol + kRingBlob) / 4 + F * kRingThreads);
-  uint32_t* cells = reinterpret_cast<uint32_t*>(cmap + 256);
+  // LDS: [call data: kRingDataMax][spans: F x 64][code map: 64 words]
+  // [lookup tables, kLdsTabs][program block: G.lds_cells]
+  lds_u8* in = (lds_u8*)lds;
+  lds_u32* sp = lds + kRingDataMax / 4 + lane;
+  lds_u32* cmap = lds + kRingDataMax / 4 + F * kRingThreads;
+  lds_u32* tabs = cmap + 64;
+  using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
+  Tabs T;
+  stage_tables(R, tabs, T);
+  lds_u32* cells = tabs + (kLdsTabs ? raw_tables_lds_words(R) : 0u);
+  wave_sync();
   const uint32_t wg = blockIdx.x;
   const uint32_t per = G.nslots > wg ? (G.nslots - wg + G.nwg - 1) / G.nwg : 0u;  // slots of this workgroup
   const bool mine = lane < per;
@@ -2145,7 +2184,7 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
       reinterpret_cast<const unsigned long long*>(G.slots + (size_t)(mine ? my : 0) * kRingSlotBytes);
   const uint64_t t0 = wall_clock64();
   uint32_t staged = 0xFFFFFFFFu;
-  for (bool last_pass = false;;) {
+  for (uint32_t it = 0, last_pass = 0;; ++it) {
     const unsigned long long sd = mine ? sys_load64(hdr) : 0ull;
     const uint32_t seq = (uint32_t)sd, done = (uint32_t)(sd >> 32);
     unsigned long long m = __ballot(mine && seq != done);
@@ -2155,13 +2194,14 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
     while (m) {
       const uint32_t j = (uint32_t)__builtin_ctzll(m);
       m &= m - 1;
-      ring_serve(HT, R, G, wg + j * G.nwg, (uint32_t)__shfl((int)seq, (int)j, kRingThreads), in, sp, cells, cmap,
+      ring_serve(HT, R, T, G, wg + j * G.nwg, (uint32_t)__shfl((int)seq, (int)j, kRingThreads), in, sp, cells, cmap,
                  staged, lane);
       if (lane == 0) atomicAdd(&st->served, 1ull);
     }
     if (last_pass) break;
-    // every iteration, busy or not: the stop word, idle and life bounds
+    // idle, or every 32nd busy pass: the stop word, idle and life bounds
     // (workgroup 0 decides for all), so a launch under steady load ends too
+    if (busy && (it & 31)) continue;
     const uint64_t now = wall_clock64();
     if (wg == 0 && lane == 0) {
       const unsigned long long lw = __hip_atomic_load(&st->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2174,18 +2214,23 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
     // that does not depend on workgroup 0)
     const bool out = ex || now - t0 > G.life_ticks + G.idle_ticks;
     if (__shfl((int)out, 0, kRingThreads)) {
-      last_pass = true;  // serve what is ready one more time, then leave
+      last_pass = 1;  // serve what is ready one more time, then leave
       continue;
     }
-    if (!busy) __builtin_amdgcn_s_sleep(8);
+    if (!busy) __builtin_amdgcn_s_sleep(4);
   }
+}
+
+// The device's constant-rate counter, for ring.cc to measure its rate.
+__global__ void ring_clock_kernel(unsigned long long* out) {
+  if (threadIdx.x == 0) *out = (unsigned long long)wall_clock64();
 }
 
 int launch_http_ring_impl(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream) {
   const size_t lds = ring_lds_bytes(R, G.lds_cells);
-  (void)hipFuncSetAttribute((const void*)http_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(http_ring_kernel, dim3(G.nwg), dim3(kRingThreads), lds, (hipStream_t)stream, HT, R, G,
-                     (RingState*)state);
+  const auto k = lds_tables_fit(R) ? http_ring_kernel<true> : http_ring_kernel<false>;
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipLaunchKernelGGL(k, dim3(G.nwg), dim3(kRingThreads), lds, (hipStream_t)stream, HT, R, G, (RingState*)state);
   return (int)hipGetLastError();
 }
 
@@ -2366,8 +2411,12 @@ int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch
 }
 
 size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells) {
-  return (size_t)(kRingBlobAt - kRingPol + kRingBlob) + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 +
-         (size_t)cells * 4;
+  return kRingDataMax + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 +
+         (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 : 0) + (size_t)cells * 4;
+}
+int ring_clock(unsigned long long* d_out, void* stream) {
+  hipLaunchKernelGGL(ring_clock_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_out);
+  return (int)hipGetLastError();
 }
 size_t http_ring_state_bytes() { return sizeof(RingState); }
 int launch_http_ring(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream) {

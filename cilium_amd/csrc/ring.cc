@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -68,9 +70,29 @@ void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
   memset(host_, 0, bytes);
   hip_check(hipHostGetDevicePointer((void**)&dev_view_, host_, 0), "hipHostGetDevicePointer");
   hip_check(hipMalloc(&state_, http_ring_state_bytes()), "hipMalloc");
-  int khz = 0;
-  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0) khz = 100000;
-  clock_khz_ = (uint64_t)khz;
+  // the rate of the kernel's wall_clock64(), measured (two reads 20 ms apart)
+  // rather than taken from hipDeviceAttributeWallClockRate
+  {
+    auto* d = static_cast<unsigned long long*>(state_);
+    unsigned long long c[2] = {0, 0};
+    uint64_t t[2] = {0, 0};
+    for (int k = 0; k < 2; ++k) {
+      if (k) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      hip_check(ring_clock(d, stream_), "ring clock");
+      hip_check(hipStreamSynchronize((hipStream_t)stream_), "ring clock");
+      t[k] = now_ns();
+      hip_check(hipMemcpy(&c[k], d, 8, hipMemcpyDeviceToHost), "D2H");
+    }
+    const double khz = (double)(c[1] - c[0]) / ((double)(t[1] - t[0]) * 1e-6);
+    clock_khz_ = khz > 1000.0 ? (uint64_t)khz : 100000;
+    if (e.debug || getenv("CILIUM_GPU_DEBUG"))
+      fprintf(stderr, "[cilium-gpu] ring: device wall clock %.0f kHz (attribute %d kHz)\n", khz,
+              [&] {
+                int a = 0;
+                (void)hipDeviceGetAttribute(&a, hipDeviceAttributeWallClockRate, device_);
+                return a;
+              }());
+  }
   claimed_.reset(new std::atomic<uint32_t>[slots]);
   for (uint32_t i = 0; i < slots; ++i) claimed_[i].store(0);
   seq_.assign(slots, 0);
@@ -168,15 +190,17 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     if (k % nslots_ == 0) std::this_thread::yield();
   }
   uint8_t* sl = host_ + kRingCtlBytes + (size_t)i * kRingSlotBytes;
+  uint8_t* d = sl + kRingData;
+  const RingLayout L = ring_layout((uint32_t)n);
   const uint64_t a0 = off[0];
   const uint32_t bytes = (uint32_t)(off[n] - a0);
-  memcpy(sl + kRingPol, pol, n * 4);
-  memcpy(sl + kRingRem, rem, n * 4);
-  memcpy(sl + kRingPort, port, n * 2);
-  memcpy(sl + kRingIng, ing, n);
-  uint32_t* o = reinterpret_cast<uint32_t*>(sl + kRingOff);
+  memcpy(d, pol, n * 4);
+  memcpy(d + L.rem, rem, n * 4);
+  memcpy(d + L.port, port, n * 2);
+  memcpy(d + L.ing, ing, n);
+  uint32_t* o = reinterpret_cast<uint32_t*>(d + L.off);
   for (size_t k = 0; k <= n; ++k) o[k] = (uint32_t)(off[k] - a0);
-  if (bytes) memcpy(sl + kRingBlobAt, blob + a0, bytes);
+  if (bytes) memcpy(d + L.blob, blob + a0, bytes);
   uint32_t* w = slot_words(i);
   w[2] = (uint32_t)n;
   w[3] = bytes;
