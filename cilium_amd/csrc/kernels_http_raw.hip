@@ -2174,7 +2174,15 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
   stage_tables(R, tabs, T);
-  lds_u32* cells = tabs + (kLdsTabs ? raw_tables_lds_words(R) : 0u);
+  lds_u32* cells = tabs;
+  if (kLdsTabs) {
+    // the list parser looks names up through the FNV field slots, which the
+    // scan's table set leaves in global memory: staged here after it
+    lds_u32* fs = tabs + raw_tables_lds_words(R);
+    for (uint32_t k = lane; k < 4 * (R.fmask + 1); k += kRingThreads) fs[k] = R.fslots[k];
+    T.fslots = reinterpret_cast<decltype(T.fslots)>(fs);
+    cells = fs + 4 * (R.fmask + 1);
+  }
   wave_sync();
   const uint32_t wg = blockIdx.x;
   const uint32_t per = G.nslots > wg ? (G.nslots - wg + G.nwg - 1) / G.nwg : 0u;  // slots of this workgroup
@@ -2412,7 +2420,8 @@ int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch
 
 size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells) {
   return kRingDataMax + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 +
-         (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 : 0) + (size_t)cells * 4;
+         (lds_tables_fit(R) ? ((size_t)raw_tables_lds_words(R) + 4 * ((size_t)R.fmask + 1)) * 4 : 0) +
+         (size_t)cells * 4;
 }
 int ring_clock(unsigned long long* d_out, void* stream) {
   hipLaunchKernelGGL(ring_clock_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_out);
