@@ -2175,12 +2175,12 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
   Tabs T;
   stage_tables(R, tabs, T);
   lds_u32* cells = tabs;
-  if (kLdsTabs) {
+  if constexpr (kLdsTabs) {
     // the list parser looks names up through the FNV field slots, which the
     // scan's table set leaves in global memory: staged here after it
     lds_u32* fs = tabs + raw_tables_lds_words(R);
     for (uint32_t k = lane; k < 4 * (R.fmask + 1); k += kRingThreads) fs[k] = R.fslots[k];
-    T.fslots = reinterpret_cast<decltype(T.fslots)>(fs);
+    T.fslots = fs;
     cells = fs + 4 * (R.fmask + 1);
   }
   wave_sync();
