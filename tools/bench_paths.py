@@ -186,34 +186,53 @@ def bench_kafka(torch, dev, stream, cl, args, threads):
                           "records_64b": {"value": n / sec, "ms": sec * 1e3, "bytes_per_item": 65}})
 
 
-def kafka_wire_pool(D: int, info: dict, seed: int = 0x4B):
-    """D distinct uncompressed wire requests of config 4's mix (apiKey /
-    version / topics / clientID as synth.kafka_requests draws them)."""
+def kafka_wire_pool(D: int, info: dict, seed: int = 0x4B, codec_frac: float = 0.0):
+    """D distinct wire requests of config 4's mix (apiKey / version / topics /
+    clientID as synth.kafka_requests draws them); codec_frac of the produce
+    requests carry their message sets compressed (gzip or snappy, one
+    member / block each: what the device inflates by itself)."""
     from cilium_amd import kafka_requests as K
     from cilium_amd import synth
     rq = synth.kafka_requests(D, info, seed=seed)
     rng = np.random.default_rng(seed)
-    reqs = [K.encode(int(rq["api_key"][i]), int(rq["api_version"][i]), rq["client_id"][i], rq["topics"][i], rng)
-            for i in range(D)]
-    return reqs, rq
+    reqs, codecs = [], []
+    for i in range(D):
+        codec = K.CODEC_NONE
+        if int(rq["api_key"][i]) == K.PRODUCE and rng.random() < codec_frac:
+            codec = K.CODEC_GZIP if rng.random() < 0.5 else K.CODEC_SNAPPY
+        codecs.append(codec)
+        reqs.append(K.encode(int(rq["api_key"][i]), int(rq["api_version"][i]), rq["client_id"][i], rq["topics"][i],
+                             rng, codec=codec))
+    return reqs, dict(rq, codec=codecs)
 
 
-def bench_kafka_wire(torch, dev, stream, cl, args, threads):
+def bench_kafka_wire(torch, dev, stream, cl, args, threads, codec_frac: float = 0.0):
     """Config 4's request mix as wire bytes: kafka_decode_kernel (ReadRequest
-    + the optiopay decoders, CRC-32 of every produce message) then
+    + the optiopay decoders, CRC-32 of every produce message), with
+    codec_frac > 0 kafka_inflate_kernel for the compressed sets (gzip /
+    snappy decoded on the device, their inner sets parsed), then
     kafka_kernel, per request."""
+    import ctypes as C
     from oracle import kafka_wire_ref as R
+    from cilium_amd import _native as N
     from cilium_amd import kafka_requests as K
     from cilium_amd import synth
     pols, info = synth.kafka_policy()
     cl.update_kafka_policy(pols)
     D, reps = 65_536, 256
-    pool, rq = kafka_wire_pool(D, info)
+    pool, rq = kafka_wire_pool(D, info, codec_frac=codec_frac)
+    if codec_frac:
+        # copies per call within the 64 MiB per-call inflate arena (each
+        # compressed set reserves its decoded size, at most its request's
+        # bytes here: a few short messages), so nothing waits for the host
+        # for want of room
+        zbytes = sum(len(r) for r, z in zip(pool, rq["codec"]) if z)
+        reps = max(1, min(256, int((48 << 20) / max(1, zbytes))))
     raw, off = K.concat(pool)
     red = np.zeros(D, np.uint16)
     rem = np.asarray(rq["remote"], np.uint32)
     v = cl.kafka_verdicts_raw(raw[: int(off[4096])], off[:4097], red[:4096], rem[:4096])
-    want = cl.kafka_verdicts(*cl.pack_kafka(**{k: x[:4096] for k, x in rq.items()}))
+    want = cl.kafka_verdicts(*cl.pack_kafka(**{k: x[:4096] for k, x in rq.items() if k != "codec"}))
     assert np.array_equal(v, want), "raw-bytes Kafka verdicts differ from the field-packed path"
     tot = int(off[-1])
     d_raw = tile_dev(torch, raw, reps, dev)
@@ -236,7 +255,13 @@ def bench_kafka_wire(torch, dev, stream, cl, args, threads):
     def both():
         decode()
         cl.kafka_verdicts_dev(d_reqs, n, d_a, d_o, stream=ss)
+    i0, d0 = C.c_uint64(), C.c_uint64()
+    N.check(N.lib.cg_kafka_decode_stats(cl.h, C.byref(i0), C.byref(d0)))
     sec = timed(torch, stream, decode, args.steps, 2)
+    i1, d1 = C.c_uint64(), C.c_uint64()
+    N.check(N.lib.cg_kafka_decode_stats(cl.h, C.byref(i1), C.byref(d1)))
+    calls = args.steps + 2
+    inflated, deferred = (i1.value - i0.value) / calls, (d1.value - d0.value) / calls
     sec2 = timed(torch, stream, both, args.steps, 1)
     # copies carry their original's verdict
     orig = d_o[:D].clone()
@@ -245,11 +270,15 @@ def bench_kafka_wire(torch, dev, stream, cl, args, threads):
     bpi = tot / D + 8 + 2 + 4 + 64 + 1
     sample = pool[:20_000]
     cpu = cpu_rate(lambda: [R.decode(r) for r in sample], len(sample), args.cpu_seconds)
-    out = line("Kafka wire decode requests/s (ReadRequest on raw bytes), config 4 mix", n, sec, bpi,
-               "kafka_decode_kernel", cpu, "20K requests of the same mix through oracle/kafka_wire_ref.decode, "
+    kern = "kafka_decode_kernel + kafka_inflate_kernel" if codec_frac else "kafka_decode_kernel"
+    mix = (f"{int(codec_frac * 100)}% of produce requests with gzip / snappy sets" if codec_frac
+           else "uncompressed wire bytes")
+    out = line(f"Kafka wire decode requests/s (ReadRequest on raw bytes), config 4 mix, {mix}", n, sec, bpi,
+               kern, cpu, "20K requests of the same mix through oracle/kafka_wire_ref.decode, "
                "1 thread (pure Python)", 1,
-               {"config": {"workload": "BASELINE config 4 request mix as uncompressed wire bytes "
+               {"config": {"workload": f"BASELINE config 4 request mix as wire bytes, {mix} "
                            f"({tot / D:.1f} B/request avg), 1K rules", "requests": n},
+                "per_call": {"payloads_inflated_on_device": inflated, "requests_finished_by_host": deferred},
                 "decode_plus_verdict": {"value": n / sec2, "ms_per_launch": sec2 * 1e3}})
     return out
 
@@ -568,6 +597,124 @@ def bench_proxylib(torch, dev, stream, cl, args, threads):
                             "requests": n, "allow_fraction": float(np.mean(exp))}})
 
 
+def _proxylib_fields_bench(torch, dev, stream, cl, pols, name, fields, remotes, ports, want, metric, workload, cpu,
+                           cpu_sample, reps):
+    """Requests given as their proxylib parser's fields (ProxylibPolicy.
+    pack_fields: the escaped values http_kernel walks), replicated to
+    `reps` copies of each program group on the device; verdicts of the
+    distinct requests equal `want` (the oracle's)."""
+    from bench import replicate_batch
+    from cilium_amd.proxylib import ProxylibPolicy
+    pl = ProxylibPolicy(cl)
+    pl.update(pols)
+    pidx = pl.index(name)
+    D = len(fields)
+    b = pl.pack_fields([pidx] * D, [1] * D, ports, remotes, fields)
+    got = cl.http_verdicts(b)
+    assert got.tolist() == list(want), f"{name}: verdicts differ from the oracle"
+    d_batch, nslots, _, data_bytes = replicate_batch(b, reps, dev, torch)
+    d_arena = torch.from_numpy(np.concatenate([b.arena.view(np.uint8), np.zeros(16, np.uint8)])).to(dev)
+    d_out = torch.zeros(nslots, dtype=torch.uint8, device=dev)
+    n = D * reps
+    sec = timed(torch, stream, lambda: cl.http_verdicts_dev(d_batch, nslots, d_arena, d_out,
+                                                            stream=stream.cuda_stream), 5, 2)
+    return line(metric, n, sec, data_bytes / n + 1, "http_kernel", cpu, cpu_sample, 1,
+                {"config": {"workload": workload, "requests": n, "allow_fraction": float(np.mean(want))}})
+
+
+def bench_memcache(torch, dev, stream, cl, args, threads):
+    """memcache (proxylib/memcached): 64 ports x 8 rules (a text command set
+    with keyExact / keyPrefix / keyRegex, or a binary opcode); requests are
+    the parser's MemcacheMeta (command or opcode, keys) as fields.  Oracle:
+    oracle/memcache_ref.py Rule.matches (parser.go:46-100), any rule of the
+    port (PolicyInstance.Matches)."""
+    from oracle.memcache_ref import Meta, Rule
+    from cilium_amd.proxylib import memcache_request
+    rng = np.random.default_rng(0x3CAC)
+    ports, rules_of = [], {}
+    for pi in range(64):
+        rules = []
+        for ri in range(8):
+            k = pi * 8 + ri
+            rule = [{"command": "get", "keyExact": f"user{k}"}, {"command": "set", "keyPrefix": f"cache{k}/"},
+                    {"command": "writeGroup", "keyRegex": f"^sess{k}-[0-9]+$"}, {"command": "delete"}][ri % 4]
+            rules.append(rule)
+        rules_of[7000 + pi] = [Rule(r) for r in rules]
+        ports.append({"port": 7000 + pi, "rules": [{"l7_proto": "memcache", "l7_rules": {"l7_rules": [
+            {"rule": r} for r in rules]}}]})
+    pols = [{"name": "memcache-bench", "ingress_per_port_policies": ports}]
+    D = 131_072
+    fields, prt, rem, want = [], [], [], []
+    for i in range(D):
+        pi = int(rng.integers(0, 64))
+        k = pi * 8 + int(rng.integers(0, 8))
+        cmd = [b"get", b"gets", b"set", b"add", b"delete", b"incr"][int(rng.integers(0, 6))]
+        nk = int(rng.integers(1, 4))
+        good = rng.random() < 0.5
+        keys = [(b"user%d" % k if cmd in (b"get", b"gets") else b"cache%d/x%d" % (k, j) if cmd in (b"set", b"add")
+                 else b"sess%d-%d" % (k, j)) if good else b"k%d" % int(rng.integers(0, 1000)) for j in range(nk)]
+        m = Meta(cmd, 0, keys)
+        fields.append(memcache_request(cmd, 0, keys))
+        prt.append(7000 + pi)
+        rem.append(1)
+        want.append(int(any(r.matches(m) for r in rules_of[7000 + pi])))
+    sample = list(zip(fields[:20_000], prt[:20_000]))
+
+    def cpu_fn():
+        for f, p in sample:
+            m = Meta(f[0][1][1:], 0, [x for x in bytes(f[1][1]).split(b"\x03\x14") if x])
+            any(r.matches(m) for r in rules_of[p])
+    cpu = cpu_rate(cpu_fn, len(sample), args.cpu_seconds)
+    return _proxylib_fields_bench(torch, dev, stream, cl, pols, "memcache-bench", fields, rem, prt, want,
+                                  "proxylib memcache verdicts/s (memcached Rule.Matches) on http_kernel",
+                                  "SURVEY 8(f) row 4: 512 memcache rules over 64 ports, requests as MemcacheMeta "
+                                  "fields", cpu, "20K requests, 1 thread (pure-Python oracle)", 400)
+
+
+def bench_cassandra(torch, dev, stream, cl, args, threads):
+    """cassandra (proxylib/cassandra): 64 ports x 8 rules (query_action /
+    query_table regexes); requests are the parser's paths
+    "/opcode/action/table" as fields.  Oracle: oracle/proxylib_ref.py
+    (CassandraRule.Matches, cassandraparser.go:73-89)."""
+    from oracle.proxylib_ref import ProxylibOracle
+    from cilium_amd.proxylib import cassandra_request
+    rng = np.random.default_rng(0xCA55)
+    ports = []
+    for pi in range(64):
+        rules = []
+        for ri in range(8):
+            k = pi * 8 + ri
+            rules.append([{"query_action": "select", "query_table": f"ks{k}\\.t[0-9]+"},
+                          {"query_action": "insert", "query_table": f"^ks{k}\\."},
+                          {"query_table": f"audit{k}$"}, {"query_action": "update"}][ri % 4])
+        ports.append({"port": 7000 + pi, "rules": [{"l7_proto": "cassandra", "l7_rules": {"l7_rules": [
+            {"rule": r} for r in rules]}}]})
+    pols = [{"name": "cassandra-bench", "ingress_per_port_policies": ports}]
+    o = ProxylibOracle(pols)
+    D = 131_072
+    fields, prt, rem, want, paths = [], [], [], [], []
+    for i in range(D):
+        pi = int(rng.integers(0, 64))
+        k = pi * 8 + int(rng.integers(0, 8))
+        act = [b"select", b"insert", b"update", b"delete", b"truncate"][int(rng.integers(0, 5))]
+        tab = [b"ks%d.t%d" % (k, int(rng.integers(0, 9))), b"ks%d.x" % k, b"audit%d" % k,
+               b"other%d.t" % int(rng.integers(0, 999))][int(rng.integers(0, 4))]
+        path = b"/query/" + act + b"/" + tab
+        paths.append(path)
+        fields.append(cassandra_request(path))
+        prt.append(7000 + pi)
+        rem.append(1)
+        want.append(int(o.matches_path("cassandra-bench", True, 7000 + pi, 1, path)))
+    sample = list(zip(paths[:20_000], prt[:20_000]))
+    cpu = cpu_rate(lambda: [o.matches_path("cassandra-bench", True, p, 1, x) for x, p in sample], len(sample),
+                   args.cpu_seconds)
+    return _proxylib_fields_bench(torch, dev, stream, cl, pols, "cassandra-bench", fields, rem, prt, want,
+                                  "proxylib cassandra verdicts/s (CassandraRule.Matches) on http_kernel",
+                                  "SURVEY 8(f) row 4: 512 cassandra rules over 64 ports, requests as "
+                                  "/opcode/action/table paths", cpu, "20K requests, 1 thread (pure-Python oracle)",
+                                  400)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--paths", default="l4,lpm,kafka,ipcache,proxylib,l4ipc")
@@ -582,7 +729,8 @@ def main():
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     fns = {"l4": bench_l4, "lpm": bench_lpm, "kafka": bench_kafka, "ipcache": bench_ipcache,
            "proxylib": bench_proxylib, "l4ipc": bench_l4ipc, "kafkawire": bench_kafka_wire, "httphost": bench_http_host, "httpraw": bench_http_raw,
-           "httpfields": bench_http_fields}
+           "httpfields": bench_http_fields, "memcache": bench_memcache, "cassandra": bench_cassandra,
+           "kafkawirez": lambda *a: bench_kafka_wire(*a, codec_frac=0.5)}
     for p in args.paths.split(","):
         print(json.dumps(fns[p](torch, dev, stream, cl, args, threads)), flush=True)
     cl.close()
