@@ -571,7 +571,7 @@ struct alignas(8) IpcVal {
 };
 struct IpcacheDev {
   const uint32_t* l16x;    // 4 words per /16 (16-B aligned)
-  const uint64_t* chunks;  // 256 entries per chunk
+  const uint64_t* chunks;  // encoded 256-entry chunks (ipc_chunk_get), 64-byte units
   const uint64_t* code6;   // (1 << v6_bits) / 32 words
   const uint32_t* ent6;    // {L, R, crowd, 0} per set bucket (at least one entry)
   const uint8_t* crowd6;   // 128 B per crowded bucket (kIpcNoCrowd: none)
@@ -580,19 +580,141 @@ struct IpcacheDev {
   uint32_t nruns6;
 };
 
-// The /16 summary word's range test; returns the chunk entry index to read
-// (UINT64_MAX: the background is the answer).
-CG_HD inline uint64_t ipc_v4_level2(uint32_t chunk, uint32_t r, uint32_t a) {
+// ---- IPv4: 256-entry chunks in one of three encodings (ipcache.cc) ------
+// An entry is a resolved {identity, tunnel} (identity != 0) or a pointer to
+// a /32-level chunk (low word 0, high word = a chunk reference).  A chunk
+// reference is kind << 30 | offset, the offset in 64-byte units of
+// IpcacheDev.chunks:
+//   DENSE   256 u64 entries (2 KiB)
+//   RUNS    one 64-byte line: word 0 = {run count n <= 7, the starts of runs
+//           1..n-1 as bytes 1..6}, words 1..7 the runs' entries — a chunk of
+//           a few prefixes (most /16s hold one or two CIDR prefixes)
+//   SPARSE  words 0-3 a 256-bit map of the keys whose entry is not the base,
+//           word 4 the base entry, word 5 the map's running popcounts (byte w
+//           = bits set in words < w), words 6.. those keys' entries in key
+//           order — a node's /24 of pod /32s (~60 of 256 set: 560 B, not 2 KiB)
+// so the hot part of the table (summaries, run lines, pod maps) is a few MB:
+// an XCD's L2, where the dense form was 139 MB at the bench's 512K entries.
+constexpr uint32_t kIpcDense = 0, kIpcRuns = 1, kIpcSparse = 2;
+CG_HD inline uint32_t ipc_runs_index(uint64_t w0, uint32_t key) {
+  const uint32_t n = (uint32_t)(w0 & 0xFF);
+  uint32_t idx = 0;
+  for (uint32_t i = 1; i < 7; ++i) idx += (uint32_t)(i < n) & (uint32_t)(((w0 >> (8 * i)) & 0xFF) <= key);
+  return idx;
+}
+// A chunk entry in two rounds of loads (the kernels issue each round for all
+// of a lane's addresses before the next): ipc_chunk_first gives the word
+// offsets of the two 16-byte loads of round 1 (a: the entry's pair, run word
+// 0 / the bitmap word pair; c: the sparse base and ranks), ipc_chunk_mid what
+// they settle and the word round 2 must read (or ~0u: settled).
+CG_HD inline void ipc_chunk_first(uint32_t ref, uint32_t key, size_t* a, size_t* c) {
+  const size_t b = (size_t)(ref & 0x3FFFFFFFu) * 8;
+  const uint32_t kind = ref >> 30;
+  *a = b + (kind == kIpcDense ? (key & ~1u) : kind == kIpcRuns ? 0u : ((key >> 6) & ~1u));
+  *c = kind == kIpcSparse ? b + 4 : *a;
+}
+CG_HD inline uint64_t ipc_chunk_mid(uint32_t ref, uint32_t key, uint64_t a0, uint64_t a1, uint64_t c0, uint64_t c1,
+                                    size_t* vword) {
+  const size_t b = (size_t)(ref & 0x3FFFFFFFu) * 8;
+  const uint32_t kind = ref >> 30;
+  *vword = ~(size_t)0;
+  if (kind == kIpcDense) return (key & 1) ? a1 : a0;
+  if (kind == kIpcRuns) {
+    const uint32_t idx = ipc_runs_index(a0, key);
+    if (idx) *vword = b + 1 + idx;
+    return a1;
+  }
+  const uint64_t w = ((key >> 6) & 1) ? a1 : a0;
+  const uint64_t below = w & ((1ull << (key & 63)) - 1);
+  if ((w >> (key & 63)) & 1) *vword = b + 6 + ((c1 >> (8 * (key >> 6))) & 0xFF) + (size_t)__builtin_popcountll(below);
+  return c0;
+}
+CG_HD inline uint64_t ipc_chunk_get(const uint64_t* ch, uint32_t ref, uint32_t key) {
+  size_t a, c, v;
+  ipc_chunk_first(ref, key, &a, &c);
+  const uint64_t r = ipc_chunk_mid(ref, key, ch[a], ch[a + 1], ch[c], ch[c + 1], &v);
+  return v == ~(size_t)0 ? r : ch[v];
+}
+// The /16 summary {background, chunk reference, lo | hi << 8 | direct << 16}:
+// an address whose /24 lies outside [lo, hi] has the background value; else
+// its entry is key (a >> 8) & 255 of the chunk, or — direct: the /16's only
+// non-background /24 points to a /32 chunk, named by the summary — key a & 255.
+CG_HD inline bool ipc_v4_in(uint32_t r, uint32_t a) {
   const uint32_t k = (a >> 8) & 255;
-  if (k < (r & 255) || k > ((r >> 8) & 255)) return ~0ULL;
-  return (uint64_t)chunk * 256 + ((r >> 16) ? (a & 255) : k);
+  return k >= (r & 255) && k <= ((r >> 8) & 255);
+}
+CG_HD inline uint32_t ipc_v4_key(uint32_t r, uint32_t a) { return (r >> 16) ? (a & 255) : ((a >> 8) & 255); }
+// K chunk reads at once, each round's loads issued for all K before the
+// next round (the kernels' form of ipc_chunk_get; every load unconditional,
+// its result selected after).
+template <uint32_t K>
+CG_HD inline void ipc_chunk_rounds(const uint64_t* __restrict__ ch, const uint32_t (&ref)[K],
+                                   const uint32_t (&key)[K], uint64_t (&out)[K]) {
+  size_t pa[K], pc[K], vw[K];
+  uint64_t a0[K], a1[K], c0[K], c1[K];
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) ipc_chunk_first(ref[u], key[u], &pa[u], &pc[u]);
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) {
+    a0[u] = ch[pa[u]];
+    a1[u] = ch[pa[u] + 1];
+    c0[u] = ch[pc[u]];
+    c1[u] = ch[pc[u] + 1];
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) out[u] = ipc_chunk_mid(ref[u], key[u], a0[u], a1[u], c0[u], c1[u], &vw[u]);
+  uint64_t v[K];
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) v[u] = ch[vw[u] != ~(size_t)0 ? vw[u] : pa[u]];
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u)
+    if (vw[u] != ~(size_t)0) out[u] = v[u];
+}
+// K IPv4 addresses (host order) → their resolved entries: the summaries, the
+// /24-level chunk (or the direct /32 chunk), then the /32-level chunk for
+// the addresses whose entry is a pointer.
+template <uint32_t K>
+CG_HD inline void ipc_v4_resolve(const IpcacheDev& t, const uint32_t (&a)[K], uint64_t (&e)[K]) {
+  uint32_t x0[K], x1[K], ref[K], key[K];
+  bool in[K];
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) {
+    const uint32_t* x = t.l16x + 4 * (size_t)(a[u] >> 16);
+    x0[u] = x[0];
+    x1[u] = x[1];
+    ref[u] = x[2];
+    key[u] = x[3];
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) {
+    in[u] = ipc_v4_in(key[u], a[u]);
+    e[u] = (uint64_t)x1[u] << 32 | x0[u];
+    ref[u] = in[u] ? ref[u] : 0u;
+    key[u] = ipc_v4_key(key[u], a[u]);
+  }
+  uint64_t r[K];
+  ipc_chunk_rounds<K>(t.chunks, ref, key, r);
+  bool ptr[K], any = false;
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) {
+    ptr[u] = in[u] && (uint32_t)r[u] == 0;
+    any |= ptr[u];
+    ref[u] = ptr[u] ? (uint32_t)(r[u] >> 32) : 0u;
+    key[u] = a[u] & 255;
+    if (in[u]) e[u] = r[u];
+  }
+  if (any) {
+    ipc_chunk_rounds<K>(t.chunks, ref, key, r);
+#pragma unroll
+    for (uint32_t u = 0; u < K; ++u)
+      if (ptr[u]) e[u] = r[u];
+  }
 }
 CG_HD inline uint64_t ipc_v4_value(const IpcacheDev& t, uint32_t a) {  // a in host order
   const uint32_t* x = t.l16x + 4 * (size_t)(a >> 16);
-  const uint64_t j = ipc_v4_level2(x[2], x[3], a);
-  if (j == ~0ULL) return (uint64_t)x[1] << 32 | x[0];
-  uint64_t e = t.chunks[j];
-  if ((uint32_t)e == 0) e = t.chunks[(size_t)(e >> 32) * 256 + (a & 255)];
+  if (!ipc_v4_in(x[3], a)) return (uint64_t)x[1] << 32 | x[0];
+  uint64_t e = ipc_chunk_get(t.chunks, x[2], ipc_v4_key(x[3], a));
+  if ((uint32_t)e == 0) e = ipc_chunk_get(t.chunks, (uint32_t)(e >> 32), a & 255);
   return e;
 }
 

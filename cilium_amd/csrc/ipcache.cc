@@ -89,13 +89,14 @@ void IpcacheState::build_tables() {
   }
   if (chunks.empty()) chunks.assign(256, kIpcMiss);
 
-  // /16 summaries: background = the most frequent value among the chunk's
-  // entries, [lo, hi] = the /24s holding anything else
-  l16x.assign(65536 * 4, 0);
+  // /16 summaries (on the dense chunks): background = the most frequent
+  // value among the chunk's entries, [lo, hi] = the /24s holding anything
+  // else, direct = that range is one /24 pointing to a /32 chunk
+  std::vector<uint32_t> sum_chunk(65536, 0), sum_range(65536, 1);
+  std::vector<uint64_t> sum_bg(65536);
   {
     std::vector<uint64_t> vals(256);
     for (uint32_t q = 0; q < 65536; ++q) {
-      uint32_t* x = &l16x[4 * (size_t)q];
       const uint64_t e = l16[q];
       uint64_t bg = e;
       uint32_t chunk = 0, lo = 1, hi = 0, direct = 0;
@@ -125,12 +126,105 @@ void IpcacheState::build_tables() {
           chunk = (uint32_t)(ent[lo] >> 32);
         }
       }
-      x[0] = (uint32_t)bg;
-      x[1] = (uint32_t)(bg >> 32);
-      x[2] = chunk;
-      x[3] = lo | hi << 8 | direct << 16;
+      sum_bg[q] = bg;
+      sum_chunk[q] = chunk;
+      sum_range[q] = lo | hi << 8 | direct << 16;
     }
   }
+
+  // Encode the dense chunks (dev_types.h ipc_chunk_get): /32-level chunks
+  // first, then the /24-level ones with their pointers rewritten to the
+  // encoded references.
+  const size_t ndense = chunks.size() / 256;
+  std::vector<uint8_t> level(ndense, 0);  // 1: /24-level, 2: /32-level
+  for (uint32_t q = 0; q < 65536; ++q)
+    if ((uint32_t)l16[q] == 0) level[(uint32_t)(l16[q] >> 32)] = 1;
+  for (size_t c = 0; c < ndense; ++c)
+    if (level[c] == 1)
+      for (uint32_t k = 0; k < 256; ++k)
+        if ((uint32_t)chunks[c * 256 + k] == 0) level[(uint32_t)(chunks[c * 256 + k] >> 32)] = 2;
+  std::vector<uint64_t> enc;
+  std::vector<uint32_t> ref(ndense, 0);
+  size_t n_runs = 0, n_sparse = 0, n_dense = 0;
+  auto encode = [&](const uint64_t* ent) -> uint32_t {
+    const size_t at = enc.size();
+    if (at / 8 >= (1u << 30)) fail(CG_MAP_FULL, "ipcache: encoded chunks past 64 GiB");
+    uint32_t nr = 1;
+    for (uint32_t k = 1; k < 256; ++k) nr += ent[k] != ent[k - 1];
+    if (nr <= 7) {
+      uint64_t w0 = nr;
+      uint32_t r = 0;
+      enc.resize(at + 8, 0);
+      enc[at + 1] = ent[0];
+      for (uint32_t k = 1; k < 256; ++k)
+        if (ent[k] != ent[k - 1]) {
+          ++r;
+          w0 |= (uint64_t)k << (8 * r);
+          enc[at + 1 + r] = ent[k];
+        }
+      enc[at] = w0;
+      ++n_runs;
+      return kIpcRuns << 30 | (uint32_t)(at / 8);
+    }
+    std::vector<uint64_t> v(ent, ent + 256);
+    std::sort(v.begin(), v.end());
+    uint64_t base = v[0];
+    size_t best = 0;
+    for (size_t i = 0; i < 256;) {
+      size_t j = i;
+      while (j < 256 && v[j] == v[i]) ++j;
+      if (j - i > best) best = j - i, base = v[i];
+      i = j;
+    }
+    const size_t k_set = 256 - best;
+    if (6 + k_set < 256) {
+      enc.resize(at + ((6 + k_set + 7) & ~(size_t)7), 0);
+      uint64_t bits[4] = {0, 0, 0, 0};
+      size_t r = 0;
+      for (uint32_t k = 0; k < 256; ++k)
+        if (ent[k] != base) {
+          bits[k >> 6] |= 1ull << (k & 63);
+          enc[at + 6 + r++] = ent[k];
+        }
+      uint64_t ranks = 0, run = 0;
+      for (int w = 0; w < 4; ++w) {
+        enc[at + w] = bits[w];
+        ranks |= run << (8 * w);
+        run += (uint64_t)__builtin_popcountll(bits[w]);
+      }
+      enc[at + 4] = base;
+      enc[at + 5] = ranks;
+      ++n_sparse;
+      return kIpcSparse << 30 | (uint32_t)(at / 8);
+    }
+    enc.insert(enc.end(), ent, ent + 256);
+    ++n_dense;
+    return kIpcDense << 30 | (uint32_t)(at / 8);
+  };
+  for (size_t c = 0; c < ndense; ++c)
+    if (level[c] == 2) ref[c] = encode(&chunks[c * 256]);
+  {
+    std::vector<uint64_t> tmp(256);
+    for (size_t c = 0; c < ndense; ++c) {
+      if (level[c] != 1) continue;
+      for (uint32_t k = 0; k < 256; ++k) {
+        const uint64_t e = chunks[c * 256 + k];
+        tmp[k] = (uint32_t)e == 0 ? (uint64_t)ref[(uint32_t)(e >> 32)] << 32 : e;
+      }
+      ref[c] = encode(tmp.data());
+    }
+  }
+  if (enc.empty()) enc.assign(8, 0);
+  l16x.assign(65536 * 4, 0);
+  for (uint32_t q = 0; q < 65536; ++q) {
+    uint32_t* x = &l16x[4 * (size_t)q];
+    x[0] = (uint32_t)sum_bg[q];
+    x[1] = (uint32_t)(sum_bg[q] >> 32);
+    x[2] = (sum_range[q] & 255) <= ((sum_range[q] >> 8) & 255) ? ref[sum_chunk[q]] : 0u;
+    x[3] = sum_range[q];
+  }
+  const size_t dense_bytes = chunks.size() * 8;
+  chunks.swap(enc);
 
   // ---- IPv6: sweep the nested prefix intervals into runs of one value.
   std::sort(v6.begin(), v6.end(), [](const auto& a, const auto& b) {
@@ -223,9 +317,10 @@ void IpcacheState::build_tables() {
     size_t c24 = 0, direct = 0;
     for (uint32_t q = 0; q < 65536; ++q)
       if ((uint32_t)l16[q] == 0) ++c24, direct += (l16x[4 * q + 3] >> 16) & 1;
-    fprintf(stderr, "[cilium-gpu] ipcache: v4 chunks %zu (%zu /16s chunked, %zu direct), %.1f MB; v6 runs %zu (%.1f MB), "
-            "buckets 2^%u, set %zu (%.1f MB), crowd lines %zu\n", chunks.size() / 256, c24, direct,
-            chunks.size() * 8 / 1e6, runs6.size() / 4, runs6.size() * 8 / 1e6, v6_bits, ent6.size() / 4,
+    fprintf(stderr, "[cilium-gpu] ipcache: v4 chunks %zu (%zu /16s chunked, %zu direct): %zu runs, %zu sparse, "
+            "%zu dense, %.1f MB (dense form %.1f MB); v6 runs %zu (%.1f MB), buckets 2^%u, set %zu (%.1f MB), "
+            "crowd lines %zu\n", ndense, c24, direct, n_runs, n_sparse, n_dense, chunks.size() * 8 / 1e6,
+            dense_bytes / 1e6, runs6.size() / 4, runs6.size() * 8 / 1e6, v6_bits, ent6.size() / 4,
             ent6.size() * 4 / 1e6, crowd6.size() / 128);
   }
 }

@@ -260,19 +260,10 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
     }
     if (kFam == 4) {  // the trie levels, each issued for all tuples of the lane
       uint64_t e[kL4Tuples];
-      uint4 x[kL4Tuples];
+      uint32_t a[kL4Tuples];
 #pragma unroll
-      for (uint32_t u = 0; u < kL4Tuples; ++u)
-        x[u] = *reinterpret_cast<const uint4*>(ipc.l16x + 4 * (size_t)(w[u][0] >> 16));
-#pragma unroll
-      for (uint32_t u = 0; u < kL4Tuples; ++u) {
-        const uint64_t j = ipc_v4_level2(x[u].z, x[u].w, w[u][0]);
-        e[u] = ((uint64_t)x[u].y << 32) | x[u].x;
-        if (j != ~0ULL) e[u] = ipc.chunks[j];
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kL4Tuples; ++u)
-        if ((uint32_t)e[u] == 0) e[u] = ipc.chunks[(size_t)(e[u] >> 32) * 256 + (w[u][0] & 255)];
+      for (uint32_t u = 0; u < kL4Tuples; ++u) a[u] = w[u][0];
+      ipc_v4_resolve<kL4Tuples>(ipc, a, e);
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u) w[u][0] = (uint32_t)e[u];
     }

@@ -3,7 +3,9 @@
 // address → {security identity, tunnel endpoint}.
 //
 // Integer work bound by the input/output stream plus dependent table loads
-// (IPv4: the /16 summary, then up to two 2-KiB chunks; IPv6: the bucket bit,
+// (IPv4: the /16 summary, then up to two encoded chunks — a run line, a
+// sparse map and its entry, or a dense entry: dev_types.h ipc_chunk_get;
+// IPv6: the bucket bit,
 // then for a bucket not spanned by one WORLD run its entry, its last 32-B run
 // record, and a short binary search when that run starts after the address).  Entries carry the resolved value inline, so
 // the last table load is the answer.  Each lane resolves
@@ -47,18 +49,7 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       i = i < n4 ? i : n4 - 1;  // unconditional loads: no vmcnt(0) under a branch
       a[u] = __builtin_bswap32(__builtin_nontemporal_load(v4 + i));
     }
-    uint4 x[kIpcV4];
-#pragma unroll
-    for (uint32_t u = 0; u < kIpcV4; ++u) x[u] = *reinterpret_cast<const uint4*>(t.l16x + 4 * (size_t)(a[u] >> 16));
-#pragma unroll
-    for (uint32_t u = 0; u < kIpcV4; ++u) {
-      const uint64_t j = ipc_v4_level2(x[u].z, x[u].w, a[u]);
-      e[u] = u64_of(x[u].x, x[u].y);
-      if (j != ~0ULL) e[u] = t.chunks[j];
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kIpcV4; ++u)
-      if ((uint32_t)e[u] == 0) e[u] = t.chunks[(size_t)(e[u] >> 32) * 256 + (a[u] & 255)];
+    ipc_v4_resolve<kIpcV4>(t, a, e);
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV4; ++u) {
       const size_t i = base + u * blockDim.x + threadIdx.x;
