@@ -353,7 +353,12 @@ struct HttpRingDev {
   uint64_t idle_ticks;    // wall-clock ticks without a call before the kernel exits
   uint64_t life_ticks;    // hard bound on one launch's life
   uint32_t lds_cells;     // largest program block the kernel stages in LDS (0: none)
+  uint32_t trace;         // write phase stamps into slot words 8..14 (CILIUM_GPU_RING_TRACE)
 };
+// phase stamps of a served call (low 32 bits of wall_clock64): polled,
+// data and list masks in LDS, program looked up / staged, request 0 parsed,
+// its string emitted, verdicts written, released
+constexpr uint32_t kRingStampAt = 8, kRingStamps = 7;
 
 // A run of tiles of a raw batch with the same string units and program:
 // tiles [t0, next run's t0), tile t at granule base + (t - t0) * (1 + 2 * units).
@@ -589,10 +594,10 @@ struct IpcacheDev {
 //   RUNS    one 64-byte line: word 0 = {run count n <= 7, the starts of runs
 //           1..n-1 as bytes 1..6}, words 1..7 the runs' entries — a chunk of
 //           a few prefixes (most /16s hold one or two CIDR prefixes)
-//   SPARSE  words 0-3 a 256-bit map of the keys whose entry is not the base,
-//           word 4 the base entry, word 5 the map's running popcounts (byte w
-//           = bits set in words < w), words 6.. those keys' entries in key
-//           order — a node's /24 of pod /32s (~60 of 256 set: 560 B, not 2 KiB)
+//   SPARSE  words 0-4: bits 0-55 of word w a map of keys 56w..56w+55 whose
+//           entry is not the base, bits 56-63 the keys set in words < w;
+//           word 5 the base entry, words 6.. the set keys' entries in key
+//           order — a node's /24 of pod /32s (~60 of 256 set: 530 B, not 2 KiB)
 // so the hot part of the table (summaries, run lines, pod maps) is a few MB:
 // an XCD's L2, where the dense form was 139 MB at the bench's 512K entries.
 constexpr uint32_t kIpcDense = 0, kIpcRuns = 1, kIpcSparse = 2;
@@ -603,37 +608,39 @@ CG_HD inline uint32_t ipc_runs_index(uint64_t w0, uint32_t key) {
   return idx;
 }
 // A chunk entry in two rounds of loads (the kernels issue each round for all
-// of a lane's addresses before the next): ipc_chunk_first gives the word
-// offsets of the two 16-byte loads of round 1 (a: the entry's pair, run word
-// 0 / the bitmap word pair; c: the sparse base and ranks), ipc_chunk_mid what
-// they settle and the word round 2 must read (or ~0u: settled).
-CG_HD inline void ipc_chunk_first(uint32_t ref, uint32_t key, size_t* a, size_t* c) {
-  const size_t b = (size_t)(ref & 0x3FFFFFFFu) * 8;
+// of a lane's addresses before the next): round 1 reads the aligned 16-byte
+// word pair at ipc_chunk_first (the entry's pair; run word 0 and the first
+// run's entry; the map word holding the key); ipc_chunk_mid settles the
+// entry from it or names the word round 2 reads (~0u: settled).  Word
+// offsets are 32-bit: the builder keeps the encoded table under 2^32 words.
+struct alignas(16) IpcPair {
+  uint64_t lo, hi;
+};
+CG_HD inline uint32_t ipc_chunk_first(uint32_t ref, uint32_t key) {
+  const uint32_t b = (ref & 0x3FFFFFFFu) * 8;
   const uint32_t kind = ref >> 30;
-  *a = b + (kind == kIpcDense ? (key & ~1u) : kind == kIpcRuns ? 0u : ((key >> 6) & ~1u));
-  *c = kind == kIpcSparse ? b + 4 : *a;
+  return b + (kind == kIpcDense ? (key & ~1u) : kind == kIpcRuns ? 0u : ((key / 56) & ~1u));
 }
-CG_HD inline uint64_t ipc_chunk_mid(uint32_t ref, uint32_t key, uint64_t a0, uint64_t a1, uint64_t c0, uint64_t c1,
-                                    size_t* vword) {
-  const size_t b = (size_t)(ref & 0x3FFFFFFFu) * 8;
+CG_HD inline uint64_t ipc_chunk_mid(uint32_t ref, uint32_t key, IpcPair A, uint32_t* vword) {
+  const uint32_t b = (ref & 0x3FFFFFFFu) * 8;
   const uint32_t kind = ref >> 30;
-  *vword = ~(size_t)0;
-  if (kind == kIpcDense) return (key & 1) ? a1 : a0;
+  *vword = ~0u;
+  if (kind == kIpcDense) return (key & 1) ? A.hi : A.lo;
   if (kind == kIpcRuns) {
-    const uint32_t idx = ipc_runs_index(a0, key);
+    const uint32_t idx = ipc_runs_index(A.lo, key);
     if (idx) *vword = b + 1 + idx;
-    return a1;
+    return A.hi;
   }
-  const uint64_t w = ((key >> 6) & 1) ? a1 : a0;
-  const uint64_t below = w & ((1ull << (key & 63)) - 1);
-  if ((w >> (key & 63)) & 1) *vword = b + 6 + ((c1 >> (8 * (key >> 6))) & 0xFF) + (size_t)__builtin_popcountll(below);
-  return c0;
+  const uint32_t wi = key / 56, bit = key - 56 * wi;
+  const uint64_t w = (wi & 1) ? A.hi : A.lo;
+  *vword = ((w >> bit) & 1) ? b + 6 + (uint32_t)(w >> 56) + (uint32_t)__builtin_popcountll(w & ((1ull << bit) - 1))
+                            : b + 5;
+  return 0;
 }
 CG_HD inline uint64_t ipc_chunk_get(const uint64_t* ch, uint32_t ref, uint32_t key) {
-  size_t a, c, v;
-  ipc_chunk_first(ref, key, &a, &c);
-  const uint64_t r = ipc_chunk_mid(ref, key, ch[a], ch[a + 1], ch[c], ch[c + 1], &v);
-  return v == ~(size_t)0 ? r : ch[v];
+  uint32_t v;
+  const uint64_t r = ipc_chunk_mid(ref, key, *reinterpret_cast<const IpcPair*>(ch + ipc_chunk_first(ref, key)), &v);
+  return v == ~0u ? r : ch[v];
 }
 // The /16 summary {background, chunk reference, lo | hi << 8 | direct << 16}:
 // an address whose /24 lies outside [lo, hi] has the background value; else
@@ -645,52 +652,38 @@ CG_HD inline bool ipc_v4_in(uint32_t r, uint32_t a) {
 }
 CG_HD inline uint32_t ipc_v4_key(uint32_t r, uint32_t a) { return (r >> 16) ? (a & 255) : ((a >> 8) & 255); }
 // K chunk reads at once, each round's loads issued for all K before the
-// next round (the kernels' form of ipc_chunk_get; every load unconditional,
-// its result selected after).
+// next round (the kernels' form of ipc_chunk_get); a lane reads the round-2
+// word only when its entry needs it.
 template <uint32_t K>
 CG_HD inline void ipc_chunk_rounds(const uint64_t* __restrict__ ch, const uint32_t (&ref)[K],
                                    const uint32_t (&key)[K], uint64_t (&out)[K]) {
-  size_t pa[K], pc[K], vw[K];
-  uint64_t a0[K], a1[K], c0[K], c1[K];
+  uint32_t vw[K];
+  IpcPair A[K];
 #pragma unroll
-  for (uint32_t u = 0; u < K; ++u) ipc_chunk_first(ref[u], key[u], &pa[u], &pc[u]);
+  for (uint32_t u = 0; u < K; ++u) A[u] = *reinterpret_cast<const IpcPair*>(ch + ipc_chunk_first(ref[u], key[u]));
 #pragma unroll
-  for (uint32_t u = 0; u < K; ++u) {
-    a0[u] = ch[pa[u]];
-    a1[u] = ch[pa[u] + 1];
-    c0[u] = ch[pc[u]];
-    c1[u] = ch[pc[u] + 1];
-  }
-#pragma unroll
-  for (uint32_t u = 0; u < K; ++u) out[u] = ipc_chunk_mid(ref[u], key[u], a0[u], a1[u], c0[u], c1[u], &vw[u]);
-  uint64_t v[K];
-#pragma unroll
-  for (uint32_t u = 0; u < K; ++u) v[u] = ch[vw[u] != ~(size_t)0 ? vw[u] : pa[u]];
+  for (uint32_t u = 0; u < K; ++u) out[u] = ipc_chunk_mid(ref[u], key[u], A[u], &vw[u]);
 #pragma unroll
   for (uint32_t u = 0; u < K; ++u)
-    if (vw[u] != ~(size_t)0) out[u] = v[u];
+    if (vw[u] != ~0u) out[u] = ch[vw[u]];
 }
 // K IPv4 addresses (host order) → their resolved entries: the summaries, the
 // /24-level chunk (or the direct /32 chunk), then the /32-level chunk for
 // the addresses whose entry is a pointer.
 template <uint32_t K>
 CG_HD inline void ipc_v4_resolve(const IpcacheDev& t, const uint32_t (&a)[K], uint64_t (&e)[K]) {
-  uint32_t x0[K], x1[K], ref[K], key[K];
+  uint32_t ref[K], key[K];
   bool in[K];
+  IpcPair x[K];
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) x[u] = *reinterpret_cast<const IpcPair*>(t.l16x + 4 * (size_t)(a[u] >> 16));
 #pragma unroll
   for (uint32_t u = 0; u < K; ++u) {
-    const uint32_t* x = t.l16x + 4 * (size_t)(a[u] >> 16);
-    x0[u] = x[0];
-    x1[u] = x[1];
-    ref[u] = x[2];
-    key[u] = x[3];
-  }
-#pragma unroll
-  for (uint32_t u = 0; u < K; ++u) {
-    in[u] = ipc_v4_in(key[u], a[u]);
-    e[u] = (uint64_t)x1[u] << 32 | x0[u];
-    ref[u] = in[u] ? ref[u] : 0u;
-    key[u] = ipc_v4_key(key[u], a[u]);
+    const uint32_t r = (uint32_t)(x[u].hi >> 32);
+    in[u] = ipc_v4_in(r, a[u]);
+    e[u] = x[u].lo;
+    ref[u] = in[u] ? (uint32_t)x[u].hi : 0u;
+    key[u] = ipc_v4_key(r, a[u]);
   }
   uint64_t r[K];
   ipc_chunk_rounds<K>(t.chunks, ref, key, r);

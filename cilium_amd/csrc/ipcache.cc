@@ -146,11 +146,14 @@ void IpcacheState::build_tables() {
   std::vector<uint64_t> enc;
   std::vector<uint32_t> ref(ndense, 0);
   size_t n_runs = 0, n_sparse = 0, n_dense = 0;
+  // CILIUM_GPU_IPC_DENSE: every chunk dense (the A/B of tools/ipcache_split.py)
+  const bool all_dense = getenv("CILIUM_GPU_IPC_DENSE") != nullptr;
   auto encode = [&](const uint64_t* ent) -> uint32_t {
     const size_t at = enc.size();
-    if (at / 8 >= (1u << 30)) fail(CG_MAP_FULL, "ipcache: encoded chunks past 64 GiB");
-    uint32_t nr = 1;
-    for (uint32_t k = 1; k < 256; ++k) nr += ent[k] != ent[k - 1];
+    // the kernels address words with 32-bit offsets (dev_types.h ipc_chunk_first)
+    if (at + 256 >= (1ull << 32)) fail(CG_MAP_FULL, "ipcache: encoded chunks past 32 GiB");
+    uint32_t nr = all_dense ? 256 : 1;
+    for (uint32_t k = 1; k < 256 && !all_dense; ++k) nr += ent[k] != ent[k - 1];
     if (nr <= 7) {
       uint64_t w0 = nr;
       uint32_t r = 0;
@@ -177,23 +180,17 @@ void IpcacheState::build_tables() {
       i = j;
     }
     const size_t k_set = 256 - best;
-    if (6 + k_set < 256) {
+    if (6 + k_set < 256 && !all_dense) {
       enc.resize(at + ((6 + k_set + 7) & ~(size_t)7), 0);
-      uint64_t bits[4] = {0, 0, 0, 0};
       size_t r = 0;
-      for (uint32_t k = 0; k < 256; ++k)
+      for (uint32_t k = 0; k < 256; ++k) {
+        if (k % 56 == 0) enc[at + k / 56] |= (uint64_t)r << 56;
         if (ent[k] != base) {
-          bits[k >> 6] |= 1ull << (k & 63);
+          enc[at + k / 56] |= 1ull << (k % 56);
           enc[at + 6 + r++] = ent[k];
         }
-      uint64_t ranks = 0, run = 0;
-      for (int w = 0; w < 4; ++w) {
-        enc[at + w] = bits[w];
-        ranks |= run << (8 * w);
-        run += (uint64_t)__builtin_popcountll(bits[w]);
       }
-      enc[at + 4] = base;
-      enc[at + 5] = ranks;
+      enc[at + 5] = base;
       ++n_sparse;
       return kIpcSparse << 30 | (uint32_t)(at / 8);
     }

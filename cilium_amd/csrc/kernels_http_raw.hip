@@ -536,19 +536,28 @@ __device__ __forceinline__ bool wbit(const uint32_t (&w)[4], uint32_t base, cons
 // lo1 / hi0 / hi1 zero where the name is shorter), or -1: R.nkeys
 // (raw_name_key), the bytes between the first and last 8 verified for longer
 // names.
+// A name-key slot's 8 words as two 16-byte loads (one round trip, not one
+// per compared word).
+__device__ __forceinline__ void key_slot(const lds_u32* p, uint4& a, uint4& b) {
+  a = to_uint4(*(const lds_v4*)p);
+  b = to_uint4(*(const lds_v4*)(p + 4));
+}
+__device__ __forceinline__ void key_slot(glb_u32* p, uint4& a, uint4& b) {
+  a = to_uint4(*(glb_v4*)p);
+  b = to_uint4(*(glb_v4*)(p + 4));
+}
 template <class Tabs>
 __device__ __forceinline__ int field_of_words(const HttpRawDev& R, const Tabs& T, const lds_u8* st, uint32_t k,
                                               uint32_t nl, uint32_t lo0, uint32_t lo1, uint32_t hi0, uint32_t hi1) {
   uint32_t sl = raw_name_hash(nl, lo0, lo1, hi0, hi1) & R.nkmask;
   for (uint32_t probe = 0; probe <= R.nkmask; ++probe) {
-    const uint32_t e0 = T.nkeys[8 * sl];
-    if (e0 == 0) return -1;
-    if (e0 == nl && T.nkeys[8 * sl + 1] == lo0 && T.nkeys[8 * sl + 2] == lo1 && T.nkeys[8 * sl + 3] == hi0 &&
-        T.nkeys[8 * sl + 4] == hi1) {
-      const uint32_t name_off = T.nkeys[8 * sl + 6];
+    uint4 a, b;  // {len, lo0, lo1, hi0}, {hi1, field, name offset, -}
+    key_slot(T.nkeys + 8 * sl, a, b);
+    if (a.x == 0) return -1;
+    if (a.x == nl && a.y == lo0 && a.z == lo1 && a.w == hi0 && b.x == hi1) {
       bool eq = true;
-      for (uint32_t j = 8; j + 8 < nl && eq; ++j) eq = lower(sbyte(st, k + j)) == T.fnames[name_off + j];
-      if (eq) return (int)T.nkeys[8 * sl + 5];
+      for (uint32_t j = 8; j + 8 < nl && eq; ++j) eq = lower(sbyte(st, k + j)) == T.fnames[b.z + j];
+      if (eq) return (int)b.y;
     }
     sl = (sl + 1) & R.nkmask;
   }
@@ -1137,7 +1146,7 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
   // the lookup tables: LDS copies when they fit (kLdsTabs), else HBM
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
-  stage_tables(R, lk + (lds_keys ? nk : 0u), T);
+  stage_tables(R, lk + (lds_keys ? (nk + 3u) & ~3u : 0u), T);  // 16-byte aligned (field_of_words' key slots)
   const uint64_t off0 = off[0];
   __syncthreads();
   // software pipeline per wave: iteration k parses stage k from LDS while the
@@ -2094,21 +2103,179 @@ __device__ __forceinline__ void ring_stage(const HttpDev& HT, const HttpRawDev& 
   for (uint32_t c = lane; c < 64; c += kRingThreads) cmap[c] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)p * 256)[c];
 }
 
+// The structural masks of a call's lists (list_stop / NUL, as the list
+// scan's build_masks_lists) over its blob in LDS: 16 bytes per lane per
+// round, mask m1 at kRingMaskWords past m0.
+constexpr uint32_t kRingMaskWords = kRingBlob / 32;
+__device__ __forceinline__ void ring_masks(const lds_u8* blob, uint32_t bytes, const lds_u8* tct, lds_u32* masks,
+                                           uint32_t lane) {
+  for (uint32_t r = 0; r * 1024 < bytes; ++r) {
+    const uint32_t u = r * 64 + lane;
+    const uint4 a = to_uint4(*(const lds_v4*)(blob + 16 * u));
+    const uint32_t d[4] = {a.x, a.y, a.z, a.w};
+    uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m1 |= zero4(d[k]) << (4 * k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m0 |= (uint32_t)tct[(d[k] >> (8 * j)) & 0xFFu] << (4 * k + j);
+    }
+    const uint32_t o0 = pair_swap(m0), o1 = pair_swap(m1);
+    if (!(lane & 1u) && (u >> 1) < kRingMaskWords) {  // (the last round's units past the blob: bits past it)
+      masks[u >> 1] = m0 | o0 << 16;
+      masks[kRingMaskWords + (u >> 1)] = m1 | o1 << 16;
+    }
+  }
+}
+// The walked string (http_pack.cc: the fields' values up to the last
+// present one, each SEP-terminated, ABSENT for a missing one, REST when a
+// later field is missing) walked straight from the parsed spans in the
+// call's LDS blob: four bytes per two LDS reads and a byte align (squad),
+// the next four bytes and their codes loaded ahead of this four's steps, so
+// only the cell load is on the chain.  Cells and codes are LDS pointers
+// when the program is staged (ds_read, not flat loads).
+__device__ __forceinline__ uint32_t ring_cell(const lds_u32* cells, uint32_t byte_off) {
+  return *(const lds_u32*)((const lds_u8*)cells + byte_off);
+}
+__device__ __forceinline__ uint32_t ring_cell(const uint32_t* cells, uint32_t byte_off) {
+  return *(const uint32_t*)((const uint8_t*)cells + byte_off);
+}
+template <bool kCls, class CellP>
+__device__ __forceinline__ uint32_t ring_step(CellP cells, uint32_t dead, uint32_t st, uint32_t x) {
+  // walk::comb_step / comb_step_cls on the typed pointer
+  const uint32_t e = ring_cell(cells, kCls ? st + x : (st << 2) + (x << 2));
+  const uint32_t dflt = max(st, dead);
+  uint32_t nx;
+  asm("v_cmp_eq_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_sdwa %0, %3, %1, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+      : "=v"(nx)
+      : "v"(e), "v"(st), "v"(dflt)
+      : "vcc");
+  return nx;
+}
+template <bool kCls, class CellP, class CodeP>
+__device__ __forceinline__ uint32_t ring_run(const HttpRawDev& R, CellP cells, uint32_t dead, uint32_t st, CodeP lut,
+                                             const lds_u8* blob, uint32_t hs, const lds_u32* sp, const Parsed& P,
+                                             uint32_t last) {
+  const uint32_t c_sep = lut[0], c_abs = lut[1];
+  uint32_t f = 0;
+  for (uint32_t rem = P.present; rem && st != dead; rem &= rem - 1) {
+    const uint32_t g = (uint32_t)__builtin_ctz(rem);
+    for (; f < g && st != dead; ++f) {
+      st = ring_step<kCls>(cells, dead, st, c_abs);
+      st = st == dead ? st : ring_step<kCls>(cells, dead, st, c_sep);
+    }
+    const uint32_t sv = sp[g * kRingThreads], a = hs + (sv >> 16), L = sv & 0xFFFFu;
+    uint32_t w = squad(blob, a);
+    for (uint32_t k = 0; k < L && st != dead; k += 4) {
+      const uint32_t wn = squad(blob, a + k + 4);  // (past the value: unused)
+      uint32_t x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = lut[(w >> (8 * j)) & 0xFFu];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t nx = ring_step<kCls>(cells, dead, st, x[j]);
+        st = k + j < L && st != dead ? nx : st;
+      }
+      w = wn;
+    }
+    st = st == dead ? st : ring_step<kCls>(cells, dead, st, c_sep);
+    f = g + 1;
+  }
+  if (last < R.nfields && st != dead) st = ring_step<kCls>(cells, dead, st, (uint32_t)lut[2]);  // REST
+  return st;
+}
+// walk::remote_row / state_label / first_meet over a typed block pointer
+// (LDS when staged: ds_read, not flat loads).
+__device__ __forceinline__ uint4 ring_q(const lds_u32* p) { return to_uint4(*(const lds_v4*)p); }
+__device__ __forceinline__ uint4 ring_q(const uint32_t* p) { return *(const uint4*)p; }
+__device__ __forceinline__ uint32_t ring_w(const lds_u32* p) { return *p; }
+__device__ __forceinline__ uint32_t ring_w(const uint32_t* p) { return *p; }
+__device__ __forceinline__ uint32_t ring_h(const lds_u32* p, uint32_t i) { return ((const CG_LDS uint16_t*)p)[i]; }
+__device__ __forceinline__ uint32_t ring_h(const uint32_t* p, uint32_t i) { return ((const uint16_t*)p)[i]; }
+template <class CellP>
+__device__ __forceinline__ uint32_t ring_remote_row(CellP blk, const HttpProg& pg, uint32_t remote) {
+  if (pg.flags & kProgRemoteDirect) {
+    const uint32_t d = remote - pg.rdir_base;
+    const bool in = d < pg.rdir_len;
+    const uint32_t v = ring_h(blk + pg.rdir_off, in ? d : 0);
+    return in ? v : pg.default_remote;
+  }
+  const uint32_t h = rtab_hash(remote);
+  const CellP b1 = blk + pg.rtab_off + kRtabBucketCells * rtab_b1h(h, pg.rtab_nb);
+  const CellP b2 = blk + pg.rtab_off + kRtabBucketCells * rtab_b2h(h, pg.rtab_nb);
+  const uint4 k1 = ring_q(b1), k2 = ring_q(b2), r1 = ring_q(b1 + 4), r2 = ring_q(b2 + 4);
+  uint32_t row = pg.default_remote;
+  row = k1.x == remote ? r1.x : row;
+  row = k1.y == remote ? r1.y : row;
+  row = k1.z == remote ? r1.z : row;
+  row = k1.w == remote ? r1.w : row;
+  row = k2.x == remote ? r2.x : row;
+  row = k2.y == remote ? r2.y : row;
+  row = k2.z == remote ? r2.z : row;
+  row = k2.w == remote ? r2.w : row;
+  return row;
+}
+template <class CellP>
+__device__ __forceinline__ uint32_t ring_first_meet(CellP blk, uint32_t a, uint32_t row, uint32_t W) {
+  for (uint32_t w = 0; w < W; ++w) {
+    const unsigned long long x = ((unsigned long long)ring_w(blk + a + 2 * w + 1) << 32 | ring_w(blk + a + 2 * w)) &
+                                 ((unsigned long long)ring_w(blk + row + 2 * w + 1) << 32 | ring_w(blk + row + 2 * w));
+    if (x) return w * 64 + (uint32_t)__builtin_ctzll(x);
+  }
+  return walk::kNoHit;
+}
+// walk_request_at from the parsed spans over the program's block and code
+// map at blk / lut (LDS, staged, or global memory); pt0: its first part.
+template <class CellP, class CodeP>
+__device__ __forceinline__ uint32_t walk_spans_at(const HttpDev& T, const HttpRawDev& R, const HttpProg& pg,
+                                                  const HttpPart& pt0, CellP blk, CodeP lut, const lds_u8* blob,
+                                                  uint32_t hs, const lds_u32* sp, const Parsed& P, uint32_t last,
+                                                  uint32_t remote) {
+  const uint32_t row = ring_remote_row(blk, pg, remote), W = pg.mask_words;
+  uint32_t hit = walk::kNoHit;
+  for (uint32_t pi = 0; pi < pg.part_count; ++pi) {
+    const HttpPart pt = pi ? T.parts[pg.part_begin + pi] : pt0;
+    const bool cls = pt.mode == kPartClass;
+    // (a program walked from global memory without a rebased block reads its
+    // cells at their place in the table)
+    CellP cells = blk;  // (staged programs are rebased)
+    if constexpr (std::is_same<CellP, const uint32_t*>::value)
+      if (!(pg.flags & kProgRebased)) cells = T.cells + pt.walk_off;
+    const uint32_t st = cls ? ring_run<true>(R, cells, pt.dead, pt.start, lut, blob, hs, sp, P, last)
+                            : ring_run<false>(R, cells, pt.dead, pt.start, lut, blob, hs, sp, P, last);
+    const uint32_t lab = (cls ? ring_cell(cells, st - 4) : ring_cell(cells, 4 * (st - 1))) >> 16;
+    if (lab != 0xFFFFu) hit = min(hit, ring_first_meet(blk, pt.acc_off + lab * 2 * W, row, W));
+  }
+  if (pg.flags & kProgHasAlways) hit = min(hit, ring_first_meet(blk, pg.always_off, row, W));
+  return hit;
+}
+
 template <class Tabs>
 __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& R, const Tabs& T, const HttpRingDev& G,
                                            uint32_t s, uint32_t seq, lds_u8* in, lds_u32* sp, lds_u32* cells,
-                                           lds_u32* cmap, uint32_t& staged, uint32_t lane) {
+                                           lds_u32* cmap, lds_u32* masks, const lds_u8* tct, uint32_t& staged,
+                                           HttpProg& spg, HttpPart& spt, uint32_t lane) {
   uint8_t* hs = G.slots + (size_t)s * kRingSlotBytes;
   // (atomic loads: vector memory, never a cached scalar read of host memory)
   uint32_t* hw = reinterpret_cast<uint32_t*>(hs);
+  uint32_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t cyc0 = 0;
+  if (G.trace) {
+    stamp[0] = (uint32_t)wall_clock64();
+    cyc0 = clock64();
+  }
+  // the call's first KiB is loaded with its size words, not after them (one
+  // round trip over the bus for a small call), the rest once they are known
+  const uint8_t* src = hs + kRingData;
+  const uint4 first = to_uint4(*(const glb_v4*)(src + lane * 16));
   const uint32_t n = min(__hip_atomic_load(hw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), kRingReqs);
   const uint32_t bytes = min(__hip_atomic_load(hw + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), kRingBlob);
   const RingLayout L = ring_layout(n);
-  // the call's data into LDS: every load issued before the stores (one
-  // round trip over the bus for a small call)
   const uint32_t total = (L.blob + bytes + 15) & ~15u;
-  const uint8_t* src = hs + kRingData;
-  for (uint32_t o0 = lane * 16; o0 < total; o0 += kRingThreads * 16 * 4) {
+  *(lds_v4*)(in + lane * 16) = to_v4(first);
+  for (uint32_t o0 = kRingThreads * 16 + lane * 16; o0 < total; o0 += kRingThreads * 16 * 4) {
     uint4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -2124,6 +2291,9 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
   const lds_u8* ing = in + L.ing;
   const lds_u32* off = (const lds_u32*)(in + L.off);
   const lds_u8* blob = in + L.blob;
+  ring_masks(blob, bytes, tct, masks, lane);
+  wave_sync();
+  if (G.trace) stamp[1] = (uint32_t)wall_clock64();
   for (uint32_t b = 0; b < n; b += kRingThreads) {  // uniform
     const uint32_t i = b + lane;
     const bool live = i < n;
@@ -2133,28 +2303,75 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
     const bool same = !__ballot(live && prog != p0);
     bool lds = false;
     if (same && p0 < R.nprogs) {
-      const HttpProg pg = HT.progs[p0];
+      // the staged program's record and first part stay in registers
+      const HttpProg pg = staged == p0 ? spg : HT.progs[p0];
       lds = !(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= G.lds_cells;
       if (lds && staged != p0) {
         wave_sync();
         ring_stage(HT, R, pg, p0, cells, cmap, lane);
+        spg = pg;
+        spt = HT.parts[pg.part_begin];
         staged = p0;
         wave_sync();
       }
     }
+    if (G.trace && b == 0) stamp[2] = (uint32_t)wall_clock64();
     uint32_t v = 0;
     if (live) {
       const uint32_t a = min(off[i], bytes), e = min(max(off[i + 1], a), bytes);
-      HeadReader hr((glb_u8*)0, e - a, blob + a, true);
-      const bool ok = prog != kProgDeny && e - a <= kFieldsMaxList && parse_list_bytes(R, T, hr, sp, kRingThreads);
-      v = decide_request(HT, R, prog, ok, lds ? (const uint32_t*)cells : nullptr, lds ? (const uint8_t*)cmap : nullptr,
-                         hr, sp, kRingThreads, rem[i]);
+      // the list over the call's masks (parse_list_fast), then decide_request
+      // with the walk over the emitted string
+      Parsed P;
+      const bool ok = prog != kProgDeny && e - a <= kFieldsMaxList &&
+                      parse_list_fast(R, T, blob, masks, masks + kRingMaskWords, a, e, sp, kRingThreads, P);
+      if (G.trace && i == 0) stamp[4] = stamp[5] = (uint32_t)wall_clock64();
+      const uint32_t* blk = lds ? (const uint32_t*)cells : nullptr;
+      const uint8_t* lut = lds ? (const uint8_t*)cmap : nullptr;
+      if (prog == kProgAllow) {
+        v = ok;
+      } else if (prog < R.nprogs) {
+        const HttpProg pg = lds ? spg : HT.progs[prog];
+        if (pg.flags & kProgAllowAll) {
+          v = ok;
+          if (ok) atomicAdd(&HT.counters[2 * prog], 1ull);
+        } else if (ok) {
+          uint32_t last;
+          (void)walked_len(R, P, &last);
+          const uint32_t* bk = blk ? blk : HT.cells + pg.cell_begin;
+          const uint8_t* lt = lut ? lut : R.codes + (size_t)prog * 256;
+          const HttpPart pt0 = lds ? spt : HT.parts[pg.part_begin];
+          const uint32_t hit = lds ? walk_spans_at(HT, R, pg, pt0, (const lds_u32*)cells, (const lds_u8*)cmap, blob, a,
+                                                   sp, P, last, rem[i])
+                                   : walk_spans_at(HT, R, pg, pt0, bk, lt, blob, a, sp, P, last, rem[i]);
+          v = hit != walk::kNoHit;
+          atomicAdd(&HT.counters[2 * prog + (v ? 0 : 1)], 1ull);
+          if (v) atomicAdd(&HT.rule_hits[pg.rule_base + hit], 1ull);
+        }
+      }
       hs[kRingOut + i] = (uint8_t)v;
     }
   }
+  if (G.trace) stamp[6] = (uint32_t)wall_clock64();
   // the verdicts before `done` (every lane's stores, then one release)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   wave_sync();
+  if (G.trace) {
+    stamp[7] = (uint32_t)wall_clock64();
+    // request 0's parse / emit stamps are lane 0's (0 when it took another way)
+    stamp[3] = (uint32_t)__shfl((int)stamp[4], 0, kRingThreads);
+    stamp[4] = (uint32_t)__shfl((int)stamp[5], 0, kRingThreads);
+    stamp[3] = stamp[3] ? stamp[3] : stamp[2];
+    stamp[4] = stamp[4] ? stamp[4] : stamp[3];
+    stamp[5] = stamp[6];
+    stamp[6] = stamp[7];
+    const uint32_t cyc = (uint32_t)(clock64() - cyc0);  // shader clock cycles over the serve
+    if (lane <= kRingStamps) {
+      uint32_t x = lane == kRingStamps ? cyc : stamp[0];
+      for (uint32_t j = 1; j < kRingStamps; ++j) x = lane == j ? stamp[j] : x;
+      hw[kRingStampAt + lane] = x;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
   if (lane == 0)
     __hip_atomic_store(reinterpret_cast<uint32_t*>(hs) + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2166,23 +2383,19 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
   lds_u32* lds = (lds_u32*)lds_ring_;
   const uint32_t F = max(R.nfields, 1u), lane = threadIdx.x;
   // LDS: [call data: kRingDataMax][spans: F x 64][code map: 64 words]
-  // [lookup tables, kLdsTabs][program block: G.lds_cells]
+  // [list masks: 2 x kRingMaskWords][stop table: 64 words][lookup tables,
+  // kLdsTabs][program block: G.lds_cells]
   lds_u8* in = (lds_u8*)lds;
   lds_u32* sp = lds + kRingDataMax / 4 + lane;
   lds_u32* cmap = lds + kRingDataMax / 4 + F * kRingThreads;
-  lds_u32* tabs = cmap + 64;
+  lds_u32* masks = cmap + 64;
+  lds_u8* tct = (lds_u8*)(masks + 2 * kRingMaskWords);
+  lds_u32* tabs = (lds_u32*)(tct + 256);
+  for (uint32_t b = lane; b < 256; b += kRingThreads) tct[b] = list_stop(b, R.raw_values);
   using Tabs = typename std::conditional<kLdsTabs, LdsTabs, GlbTabs>::type;
   Tabs T;
   stage_tables(R, tabs, T);
-  lds_u32* cells = tabs;
-  if constexpr (kLdsTabs) {
-    // the list parser looks names up through the FNV field slots, which the
-    // scan's table set leaves in global memory: staged here after it
-    lds_u32* fs = tabs + raw_tables_lds_words(R);
-    for (uint32_t k = lane; k < 4 * (R.fmask + 1); k += kRingThreads) fs[k] = R.fslots[k];
-    T.fslots = fs;
-    cells = fs + 4 * (R.fmask + 1);
-  }
+  lds_u32* cells = tabs + ((kLdsTabs ? raw_tables_lds_words(R) : 0u) + 3u & ~3u);  // 16-byte aligned
   wave_sync();
   const uint32_t wg = blockIdx.x;
   const uint32_t per = G.nslots > wg ? (G.nslots - wg + G.nwg - 1) / G.nwg : 0u;  // slots of this workgroup
@@ -2192,6 +2405,8 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
       reinterpret_cast<const unsigned long long*>(G.slots + (size_t)(mine ? my : 0) * kRingSlotBytes);
   const uint64_t t0 = wall_clock64();
   uint32_t staged = 0xFFFFFFFFu;
+  HttpProg spg{};
+  HttpPart spt{};
   for (uint32_t it = 0, last_pass = 0;; ++it) {
     const unsigned long long sd = mine ? sys_load64(hdr) : 0ull;
     const uint32_t seq = (uint32_t)sd, done = (uint32_t)(sd >> 32);
@@ -2203,7 +2418,7 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
       const uint32_t j = (uint32_t)__builtin_ctzll(m);
       m &= m - 1;
       ring_serve(HT, R, T, G, wg + j * G.nwg, (uint32_t)__shfl((int)seq, (int)j, kRingThreads), in, sp, cells, cmap,
-                 staged, lane);
+                 masks, tct, staged, spg, spt, lane);
       if (lane == 0) atomicAdd(&st->served, 1ull);
     }
     if (last_pass) break;
@@ -2253,7 +2468,7 @@ size_t raw_lds(const HttpRawDev& R, bool lds_keys, bool lds_codes) {
   const size_t nk = ((size_t)R.nprogs + 2) * kRawKeys;
   return (size_t)std::max(R.nfields, 1u) * kRawThreads * 4 + kRawWaves * (size_t)kStage + kRawWaves * 2 * (kStage / 8) + kTctBytes +
          (lds_keys ? nk * 4 : 0) + (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 : 0) +
-         (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16;  // + slack: a quad read may pass the last stage by 7 bytes
+         (lds_codes ? (size_t)R.nprogs * 256 : 0) + 16 + 12;  // + slack: a quad read may pass the last stage by 7 bytes; the tables' alignment
 }
 // code maps in LDS only while small: a larger table costs workgroups per CU
 // (occupancy) more than its global (L1-cached) lookups cost
@@ -2419,8 +2634,8 @@ int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch
 }
 
 size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells) {
-  return kRingDataMax + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 +
-         (lds_tables_fit(R) ? ((size_t)raw_tables_lds_words(R) + 4 * ((size_t)R.fmask + 1)) * 4 : 0) +
+  return kRingDataMax + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 + 8 * kRingMaskWords + 256 +
+         (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 + 12 : 0) +
          (size_t)cells * 4;
 }
 int ring_clock(unsigned long long* d_out, void* stream) {

@@ -24,7 +24,7 @@ namespace cg {
 
 namespace {
 
-constexpr uint32_t kIpcV4 = 8, kIpcV6 = 2;  // addresses per lane per iteration
+constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;  // addresses per lane per iteration
 constexpr int kIpcThreads = 256;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 

@@ -370,8 +370,9 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
                      raw, off, n, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap, ctr, status,
                      defer_list);
   // the deferred requests (their count stays on the device: a small grid
-  // that exits at once when there are none)
-  hipLaunchKernelGGL(kafka_inflate_kernel, dim3((unsigned)std::max(cus, 1)), dim3(kKwThreads), 0, (hipStream_t)stream,
+  // that exits at once when there are none) — two workgroups per CU, the
+  // inflater's occupancy (230 VGPRs: 2 waves per SIMD)
+  hipLaunchKernelGGL(kafka_inflate_kernel, dim3(2 * (unsigned)std::max(cus, 1)), dim3(kKwThreads), 0, (hipStream_t)stream,
                      topics, clients, raw, off, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap,
                      ctr, status, defer_list, zarena, (unsigned long long)zcap);
   return hipGetLastError();

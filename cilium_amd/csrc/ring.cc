@@ -95,7 +95,10 @@ void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
   }
   claimed_.reset(new std::atomic<uint32_t>[slots]);
   for (uint32_t i = 0; i < slots; ++i) claimed_[i].store(0);
+  busy_.reset(new std::atomic<uint32_t>[workgroups]);
+  for (uint32_t i = 0; i < workgroups; ++i) busy_[i].store(0);
   seq_.assign(slots, 0);
+  trace_ = getenv("CILIUM_GPU_RING_TRACE") != nullptr;
 }
 
 uint32_t* HttpRing::slot_words(uint32_t i) const {
@@ -145,6 +148,7 @@ void HttpRing::launch_locked(const std::shared_ptr<HttpSnapshot>& s) {
   const size_t base = ring_lds_bytes(s->raw, 0);
   const uint32_t room = base < 160 * 1024 ? (uint32_t)((160 * 1024 - base) / 4) : 0u;
   G.lds_cells = std::min(maxc, room);
+  G.trace = trace_;
   check_launch_rc(launch_http_ring(s->dev, s->raw, G, state_, stream_));
   s->fence.record(stream_);
   snap_ = s;
@@ -181,14 +185,36 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
                         uint8_t* out) {
   (void)e;
   ensure(s);
-  // a free slot (callers never hold more than one)
-  uint32_t i = next_.fetch_add(1, std::memory_order_relaxed) % nslots_;
-  for (uint32_t k = 1;; ++k) {
+  // a free slot (callers never hold more than one), preferably one of the
+  // home workgroup of the first request's program (its index modulo the
+  // workgroups): slot s is served by workgroup s % nwg, which keeps the last
+  // program it staged in LDS, so calls of one listener find theirs there
+  const uint32_t prog = n ? s->lookup_prog(pol[0], ing[0] != 0, port[0]) : 0u;
+  const uint32_t home = (prog < s->progs.size() ? prog : prog * 0x9E3779B1u >> 7) % nwg_;
+  const uint32_t r = next_.fetch_add(1, std::memory_order_relaxed);
+  uint32_t i = nslots_;
+  auto try_wg = [&](uint32_t wg) {  // a free slot of workgroup wg (slots wg, wg + nwg, ...)
+    const uint32_t mine = wg < nslots_ ? (nslots_ - wg + nwg_ - 1) / nwg_ : 0u;
+    for (uint32_t k = 0; k < mine && i == nslots_; ++k) {
+      const uint32_t c = wg + ((r + k) % mine) * nwg_;
+      uint32_t z = 0;
+      if (claimed_[c].compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
+    }
+  };
+  // the home workgroup when no call is in it, else the nearest idle one (a
+  // workgroup serves its slots one after another: a hot program spreads over
+  // the neighbours, which then hold it too), else home, else any slot
+  if (!busy_[home].load(std::memory_order_relaxed)) try_wg(home);
+  for (uint32_t d = 1; d < nwg_ && i == nslots_; ++d)
+    if (!busy_[(home + d) % nwg_].load(std::memory_order_relaxed)) try_wg((home + d) % nwg_);
+  if (i == nslots_) try_wg(home);
+  for (uint32_t k = 1; i == nslots_; ++k) {
+    const uint32_t c = (r + k) % nslots_;
     uint32_t z = 0;
-    if (claimed_[i].compare_exchange_strong(z, 1u, std::memory_order_acquire)) break;
-    i = (i + 1) % nslots_;
+    if (claimed_[c].compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
     if (k % nslots_ == 0) std::this_thread::yield();
   }
+  busy_[i % nwg_].fetch_add(1, std::memory_order_relaxed);
   uint8_t* sl = host_ + kRingCtlBytes + (size_t)i * kRingSlotBytes;
   uint8_t* d = sl + kRingData;
   const RingLayout L = ring_layout((uint32_t)n);
@@ -224,12 +250,27 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
       }
     }
     if (t - t0 > 5ull * 1000 * 1000 * 1000) {
+      busy_[i % nwg_].fetch_sub(1, std::memory_order_relaxed);
       claimed_[i].store(0, std::memory_order_release);
       fail(CG_UNKNOWN_ERROR, "ring: a call was not served within 5 s");
     }
   }
   memcpy(out, sl + kRingOut, n);
-  last_ns_.store(now_ns(), std::memory_order_relaxed);
+  const uint64_t t_done = now_ns();
+  last_ns_.store(t_done, std::memory_order_relaxed);
+  if (trace_) {  // device phases (10 ns ticks at 100 MHz) and the whole call
+    uint32_t st[kRingStamps + 1];
+    for (uint32_t j = 0; j <= kRingStamps; ++j) st[j] = __atomic_load_n(&w[kRingStampAt + j], __ATOMIC_ACQUIRE);
+    std::lock_guard<std::mutex> lk(trace_mu_);
+    const double ns_per_tick = 1e6 / (double)clock_khz_;
+    const int c = n == 1 ? 0 : n <= 16 ? 1 : 2;
+    for (uint32_t j = 1; j < kRingStamps; ++j)
+      trace_sum_[c][j - 1] += (double)(uint32_t)(st[j] - st[j - 1]) * ns_per_tick;
+    trace_sum_[c][kRingStamps - 1] += (double)(t_done - t0);
+    trace_sum_[c][kRingStamps] += (double)st[kRingStamps];
+    ++trace_n_[c];
+  }
+  busy_[i % nwg_].fetch_sub(1, std::memory_order_relaxed);
   claimed_[i].store(0, std::memory_order_release);
 }
 
@@ -248,6 +289,18 @@ void HttpRing::stats(uint64_t* served, uint64_t* launches) {
 void HttpRing::close() {
   std::lock_guard<std::mutex> lk(mu_);
   stop_locked();
+  static const char* const kClass[3] = {"1", "2-16", "17-256"};
+  for (int c = 0; c < 3 && trace_; ++c) {
+    if (!trace_n_[c]) continue;
+    const double k = 1e-3 / (double)trace_n_[c];
+    const double* t = trace_sum_[c];
+    fprintf(stderr,
+            "[cilium-gpu] ring trace, calls of %s requests (%llu), mean us: copy-in+masks %.2f, lookup+stage %.2f, "
+            "parse (request 0) %.2f, walk and the rest %.2f, release %.2f, whole call (host) %.2f; shader clock "
+            "%.0f MHz\n",
+            kClass[c], (unsigned long long)trace_n_[c], t[0] * k, t[1] * k, t[2] * k, t[3] * k + t[4] * k, t[5] * k,
+            t[6] * k, t[kRingStamps] * 1e3 / (t[0] + t[1] + t[2] + t[3] + t[4] + t[5]));
+  }
 }
 
 }  // namespace cg

@@ -49,8 +49,15 @@ class HttpRing {
   std::atomic<uint64_t> launch_ns_{0}, last_ns_{0};
   uint64_t launches_ = 0, served_before_ = 0;
   std::unique_ptr<std::atomic<uint32_t>[]> claimed_;  // per slot: a call owns it
+  std::unique_ptr<std::atomic<uint32_t>[]> busy_;     // per workgroup: calls in its slots
   std::vector<uint32_t> seq_;                          // per slot, under its claim
   std::atomic<uint32_t> next_{0};
+  // CILIUM_GPU_RING_TRACE: per-phase device stamps summed over calls
+  bool trace_ = false;
+  std::mutex trace_mu_;
+  // per call-size class (1, 2..16, 17..256 requests): phase sums, calls
+  double trace_sum_[3][kRingStamps + 1] = {};  // + shader clock cycles
+  uint64_t trace_n_[3] = {0, 0, 0};
 };
 
 }  // namespace cg

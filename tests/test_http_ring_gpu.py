@@ -14,7 +14,7 @@ import pytest
 from cilium_amd import _native as N
 from cilium_amd import synth
 from cilium_amd.classifier import Classifier
-from test_http_fields_gpu import _join, _oracle, _split
+from test_http_fields_gpu import _host_path, _join, _oracle, _split, _vary
 
 
 def test_ring_needs_a_gpu(host):
@@ -136,3 +136,83 @@ def test_gpu_ring_policy_update_and_fallbacks():
         assert cl.http_ring_verdicts(*(x[:1] for x in args), *_join(lists[:1]))[0] == want[0]
     finally:
         cl.close()  # stops the ring
+
+
+def _ring_batches(cl, args, lists, sizes):
+    """Verdicts of lists through the ring in calls of the given sizes (cycled)."""
+    out, a, k = [], 0, 0
+    while a < len(lists):
+        B = sizes[k % len(sizes)]
+        out.append(cl.http_ring_verdicts(*(x[a:a + B] for x in args), *_join(lists[a:a + B])))
+        a += B
+        k += 1
+    return np.concatenate(out)
+
+
+@pytest.mark.gpu
+def test_gpu_ring_varied_lists():
+    """Lists as a proxy hands them over (test_http_fields_gpu._vary: name case,
+    repeated names, unknown headers, values past the ring's 256-byte string
+    buffer, multi-KiB lists, control bytes, empty names, cut-short pairs,
+    empty lists), the hand-made edge cases, and a proxylib snapshot's escaped
+    values, through the ring at batch sizes 1, 3, 16 and 64 — against the
+    oracle and the host packer path."""
+    cl = Classifier(device=0)
+    try:
+        pols, info = synth.http10k_rules()
+        cl.update_http_policy(pols)
+        rq = synth.http10k_requests(3000, info, seed=73)
+        lists = _vary(_split(rq["hdr_blob"], rq["hdr_off"]), np.random.default_rng(74), frac=0.5)
+        args = tuple(np.asarray(rq[k], dt) for k, dt in (("policy", np.uint32), ("ingress", np.uint8),
+                                                          ("port", np.uint16), ("remote", np.uint32)))
+        blob, off = _join(lists)
+        want = _oracle(pols, *args, blob, off)
+        assert np.array_equal(want, _host_path(cl, *args, blob, off))
+        cl.http_ring_open(8, 32)
+        got = _ring_batches(cl, args, lists, (1, 3, 16, 64))
+        bad = np.nonzero(got != want)[0]
+        assert not len(bad), [(int(i), lists[i][:160], int(got[i]), int(want[i])) for i in bad[:4]]
+        assert 0.1 < want.mean() < 0.9
+        # the hand-made edge cases (test_gpu_fields_edge_cases, without the 20 KiB list)
+        sw_pols = synth.starwars_policy()
+        cl.update_http_policy(sw_pols)
+        sw = cl.http_policy_index(sw_pols[0]["name"])
+        ok = b":method\0POST\0:path\0/v1/request-landing/\0:authority\0deathstar\0"
+        upper = b":METHOD\0POST\0:Path\0/v1/request-landing/\0:AUTHORITY\0deathstar\0"
+        el = [b"", b"\0", ok[:-1], ok, upper, ok + b":method\0GET\0", b":method\0GET\0" + ok,
+              ok + b"x-a\0bad\x7fbyte\0", ok + b"x-a\0bad\nbyte\0", ok + b"x-a\0tab\there\0", ok + b"x-a\0\x80\xff\0",
+              b"\0v\0" + ok, ok + b"x-big\0" + b"z" * 9_000 + b"\0", ok.replace(b"POST", b"PO\x01ST"),
+              ok.replace(b"/v1/request-landing/", b"/v1/request-landing/" + b"q" * 400), ok, ok]
+        n = len(el)
+        eargs = (np.array([sw] * (n - 2) + [sw, 0xFFFFFFFF], np.uint32), np.zeros(n, np.uint8),
+                 np.array([80] * (n - 2) + [8080, 80], np.uint16), np.full(n, synth.SPACESHIP_ID, np.uint32))
+        eb, eo = _join(el)
+        ew = _oracle(sw_pols, *eargs, eb, eo)
+        for sizes in ((1,), (n,), (5,)):
+            assert np.array_equal(_ring_batches(cl, eargs, el, sizes), ew), sizes
+        # a proxylib snapshot (escaped values, raw_values lists)
+        rules = [{"headers": [{"name": "cmd", "exact_match": "READ"}, {"name": "file", "regex_match": "/pub/.*"}]},
+                 {"headers": [{"name": "cmd", "exact_match": "WR\x01TE"}]}]
+        ppol = [{"name": "p", "proxylib": True, "policy": 0, "ingress_per_port_policies": [
+            {"port": 80, "rules": [{"remote_policies": [1], "http_rules": {"http_rules": rules}}]}]}]
+        cl.update_http_policy(ppol)
+        rng = np.random.default_rng(75)
+        vals = [b"READ", b"WRITE", b"WR\x03\x11TE", b"WR\x01TE", b"RE\x03AD", b"READ\x03", b"\x03\x14x", b"/pub/a",
+                b"/pub/\x03\x10", b"/priv/x", b"\x02", b"\x03\x15"]
+        pl = []
+        for _ in range(600):
+            ps = [(b"cmd", vals[int(rng.integers(0, len(vals)))])]
+            if rng.random() < 0.7:
+                ps.append((b"File" if rng.random() < 0.3 else b"file", vals[int(rng.integers(0, len(vals)))]))
+            if rng.random() < 0.2:
+                ps.reverse()
+            pl.append(b"".join(nm + b"\0" + v + b"\0" for nm, v in ps))
+        m = len(pl)
+        pargs = (np.zeros(m, np.uint32), np.ones(m, np.uint8), np.full(m, 80, np.uint16),
+                 rng.integers(0, 3, m).astype(np.uint32))
+        pb, po = _join(pl)
+        pw = _host_path(cl, *pargs, pb, po)
+        assert np.array_equal(_ring_batches(cl, pargs, pl, (1, 7, 64)), pw)
+        assert 0.02 < pw.mean() < 0.9
+    finally:
+        cl.close()

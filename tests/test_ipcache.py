@@ -165,6 +165,54 @@ def test_tables_nested_dense(host):
     assert CIDR_DTYPE.itemsize == 20
 
 
+def v4_chunk_kinds_case():
+    """IPv4 chunks in every encoding (dev_types.h ipc_chunk_get): dense /32-
+    and /24-level chunks (every entry distinct), sparse maps whose set keys
+    sit on the 56-key map word edges, run lines of exactly 7 runs and sparse
+    ones of 8, with every address of those /24s probed."""
+    keys, vals, probe = [], [], []
+
+    def add(net, ident, tun=0):
+        keys.append(net)
+        vals.append([ident, tun])
+
+    for k in range(256):  # 10.9.9.0/24: 256 distinct /32s (dense /32 chunk)
+        add(f"10.9.9.{k}/32", 7000 + k, k)
+    for k in range(256):  # 10.8.0.0/16: 256 distinct /24s (dense /24 chunk)
+        add(f"10.8.{k}.0/24", 8000 + k)
+    edges = [0, 1, 54, 55, 56, 57, 111, 112, 113, 167, 168, 223, 224, 225, 254, 255]
+    for k in edges:  # sparse /32 chunk over a /24 background
+        add(f"10.7.7.{k}/32", 9000 + k, 1)
+    add("10.7.7.0/24", 9999)
+    for k in edges:  # sparse /24 chunk (/24s of one /16, alternating zero identities)
+        add(f"10.6.{k}.0/24", 0 if k % 3 == 0 else 6000 + k)
+    add("10.6.0.0/16", 6999)
+    for n, net in ((7, "10.5.5"), (8, "10.4.4")):  # 7 runs (a run line), 8 runs (sparse)
+        for r in range((n + 1) // 2):
+            add(f"{net}.{40 * r + 7}/32", 5000 + 10 * n + r)
+    for p in ("10.9.9", "10.7.7", "10.5.5", "10.4.4"):
+        probe += [f"{p}.{k}" for k in range(256)]
+    probe += [f"10.8.{k}.{(k * 37) & 255}" for k in range(256)] + [f"10.6.{k}.9" for k in range(256)]
+    a4 = np.array([int.from_bytes(ipaddress.ip_address(a).packed, "little") for a in probe], np.uint32)
+    return keys, np.array(vals, np.uint32), a4
+
+
+def _check_chunk_kinds(cl, lookup):
+    from cilium_amd.classifier import IPCache
+    keys, vals, a4 = v4_chunk_kinds_case()
+    ic = cl.ipcache()
+    ic.update(keys, vals)
+    a6 = np.zeros((0, 16), np.uint8)
+    g4, _ = lookup(ic, a4, a6)
+    o4, _ = oracle.ipcache(IPCache._keys(keys), vals, a4, a6)
+    assert np.array_equal(g4, o4)
+    assert len(np.unique(o4[:, 0])) > 500
+
+
+def test_tables_v4_chunk_kinds(host):
+    _check_chunk_kinds(host, lambda ic, a4, a6: ic.eval_host_diag(a4, a6))
+
+
 def v6_bucket_case(seed: int):
     """IPv6 top-bits buckets of every kind: spanned by one WORLD run (bit
     clear), spanned by one non-WORLD run (short prefixes), a few runs, and
@@ -221,6 +269,11 @@ def test_host_handle_refuses_resolve(host):
 
 
 # ------------------------------------------------------------------ GPU ----
+@pytest.mark.gpu
+def test_gpu_v4_chunk_kinds(gpu):
+    _check_chunk_kinds(gpu, lambda ic, a4, a6: ic.resolve(a4, a6))
+
+
 @pytest.mark.gpu
 def test_gpu_kat(gpu):
     ic = _kat_map(gpu)
