@@ -146,8 +146,12 @@ void IpcacheState::build_tables() {
   std::vector<uint64_t> enc;
   std::vector<uint32_t> ref(ndense, 0);
   size_t n_runs = 0, n_sparse = 0, n_dense = 0;
-  // CILIUM_GPU_IPC_DENSE: every chunk dense (the A/B of tools/ipcache_split.py)
-  const bool all_dense = getenv("CILIUM_GPU_IPC_DENSE") != nullptr;
+  // Dense chunks unless CILIUM_GPU_IPC_ENCODE is set: the run lines and
+  // sparse maps take ~20x less memory (7 MB, not 139 MB, at the bench's 512K
+  // entries) but a third of the IPv4 lookups a second dependent load, and
+  // measured slower (tools/ipcache_split.py: IPv4 59-66 vs 81 G lookups/s,
+  // profiles/r06j_*, r06p_*); both forms go through the same kernel.
+  const bool all_dense = getenv("CILIUM_GPU_IPC_ENCODE") == nullptr;
   auto encode = [&](const uint64_t* ent) -> uint32_t {
     const size_t at = enc.size();
     // the kernels address words with 32-bit offsets (dev_types.h ipc_chunk_first)

@@ -14,6 +14,7 @@
 // flight.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -24,7 +25,7 @@ namespace cg {
 
 namespace {
 
-constexpr uint32_t kIpcV4 = 4, kIpcV6 = 2;  // addresses per lane per iteration
+constexpr uint32_t kIpcV6 = 2;  // IPv6 addresses per lane per iteration (IPv4: the kernel's K)
 constexpr int kIpcThreads = 256;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -34,6 +35,7 @@ __device__ __forceinline__ void store_val(uint64_t v, IpcVal* out) {
   __builtin_nontemporal_store((unsigned long long)v, reinterpret_cast<unsigned long long*>(out));
 }
 
+template <uint32_t kIpcV4>
 __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, const uint32_t* __restrict__ v4,
                                                               size_t n4, IpcVal* __restrict__ out4,
                                                               const uint4* __restrict__ v6, size_t n6,
@@ -138,23 +140,34 @@ int resident_blocks(const void* fn, int threads) {
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus) {
   if (n4 + n6 == 0) return 0;
+  // IPv4 addresses per lane per iteration: 4 (CILIUM_GPU_IPC_K = 2..4 for
+  // the A/B of tools/ipcache_split.py)
+  const char* ke = getenv("CILIUM_GPU_IPC_K");
+  const uint32_t K = ke && atoi(ke) >= 2 && atoi(ke) <= 4 ? (uint32_t)atoi(ke) : 4u;
+  const void* fn = K == 2 ? (const void*)ipcache_kernel<2> : K == 3 ? (const void*)ipcache_kernel<3>
+                                                                    : (const void*)ipcache_kernel<4>;
   int dev = 0;
   (void)hipGetDevice(&dev);
   static std::mutex mu;
-  static std::map<int, int> occ_by_dev;  // per device ordinal
+  static std::map<std::pair<int, uint32_t>, int> occ_by_dev;  // per device ordinal and K
   int occ;
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = occ_by_dev.find(dev);
-    if (it == occ_by_dev.end()) it = occ_by_dev.emplace(dev, resident_blocks((const void*)ipcache_kernel, kIpcThreads)).first;
+    auto it = occ_by_dev.find({dev, K});
+    if (it == occ_by_dev.end()) it = occ_by_dev.emplace(std::make_pair(dev, K), resident_blocks(fn, kIpcThreads)).first;
     occ = it->second;
   }
-  size_t need = (n4 / kIpcV4 + n6 / kIpcV6 + kIpcThreads) / kIpcThreads;
+  size_t need = (n4 / K + n6 / kIpcV6 + kIpcThreads) / kIpcThreads;
   const size_t cap = (size_t)cus * occ;
   need = need < cap ? need : cap;
   need = need < 1 ? 1 : need;
-  hipLaunchKernelGGL(ipcache_kernel, dim3((unsigned)need), dim3(kIpcThreads), 0, (hipStream_t)stream, t, v4, n4,
-                     out4, (const uint4*)v6, n6, out6);
+  const dim3 g((unsigned)need), b(kIpcThreads);
+  if (K == 2)
+    hipLaunchKernelGGL(ipcache_kernel<2>, g, b, 0, (hipStream_t)stream, t, v4, n4, out4, (const uint4*)v6, n6, out6);
+  else if (K == 3)
+    hipLaunchKernelGGL(ipcache_kernel<3>, g, b, 0, (hipStream_t)stream, t, v4, n4, out4, (const uint4*)v6, n6, out6);
+  else
+    hipLaunchKernelGGL(ipcache_kernel<4>, g, b, 0, (hipStream_t)stream, t, v4, n4, out4, (const uint4*)v6, n6, out6);
   return (int)hipGetLastError();
 }
 

@@ -209,7 +209,10 @@ def _check_chunk_kinds(cl, lookup):
     assert len(np.unique(o4[:, 0])) > 500
 
 
-def test_tables_v4_chunk_kinds(host):
+@pytest.mark.parametrize("encode", [False, True])
+def test_tables_v4_chunk_kinds(host, monkeypatch, encode):
+    if encode:  # run lines and sparse maps (ipcache.cc; dense chunks by default)
+        monkeypatch.setenv("CILIUM_GPU_IPC_ENCODE", "1")
     _check_chunk_kinds(host, lambda ic, a4, a6: ic.eval_host_diag(a4, a6))
 
 
@@ -270,8 +273,24 @@ def test_host_handle_refuses_resolve(host):
 
 # ------------------------------------------------------------------ GPU ----
 @pytest.mark.gpu
-def test_gpu_v4_chunk_kinds(gpu):
+@pytest.mark.parametrize("encode", [False, True])
+def test_gpu_v4_chunk_kinds(gpu, monkeypatch, encode):
+    if encode:
+        monkeypatch.setenv("CILIUM_GPU_IPC_ENCODE", "1")
     _check_chunk_kinds(gpu, lambda ic, a4, a6: ic.resolve(a4, a6))
+
+
+@pytest.mark.gpu
+def test_gpu_encoded_tables_random_vs_oracle(gpu, monkeypatch):
+    """The encoded v4 chunks on the random workload of test_gpu_random."""
+    monkeypatch.setenv("CILIUM_GPU_IPC_ENCODE", "1")
+    k, v = synth.ipcache_entries(30000, n_nodes=200, seed=9)
+    a4, a6 = synth.ipcache_addresses(300_000, k, seed=9)
+    ic = gpu.ipcache()
+    ic.update(k, v)
+    g4, g6 = ic.resolve(a4, a6)
+    o4, o6 = oracle.ipcache(k, v, a4, a6, nthreads=8)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
 
 
 @pytest.mark.gpu

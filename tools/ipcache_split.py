@@ -2,8 +2,9 @@
 
 Times cg_ipcache_resolve_dev on the bench's 512K-entry table (synth) over
 100M addresses (70% v4) as bench_paths.py's ipcache line does, then the v4
-and v6 addresses alone; with --dense the builder writes every v4 chunk dense
-(CILIUM_GPU_IPC_DENSE, set before the library loads), the encoding A/B.
+and v6 addresses alone, and the v4 addresses at 3 and 2 per lane
+(CILIUM_GPU_IPC_K); with --encode the builder writes run lines and sparse
+maps (CILIUM_GPU_IPC_ENCODE, set before the library loads), the encoding A/B.
 One JSON line per leg."""
 import argparse
 import json
@@ -15,12 +16,12 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--dense", action="store_true")
+    ap.add_argument("--encode", action="store_true", help="run lines / sparse maps (CILIUM_GPU_IPC_ENCODE)")
     ap.add_argument("--addresses", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=5)
     args = ap.parse_args()
-    if args.dense:
-        os.environ["CILIUM_GPU_IPC_DENSE"] = "1"
+    if args.encode:
+        os.environ["CILIUM_GPU_IPC_ENCODE"] = "1"
     import numpy as np
     import torch
     from cilium_amd import synth
@@ -38,12 +39,15 @@ def main():
     n4, n6 = len(a4), len(a6)
     o4 = torch.empty(n4 * 2, dtype=torch.int32, device=dev)
     o6 = torch.empty(n6 * 2, dtype=torch.int32, device=dev)
-    for leg, m4, m6 in (("both", n4, n6), ("v4", n4, 0), ("v6", 0, n6)):
+    legs = [("both", n4, n6, "4"), ("v4", n4, 0, "4"), ("v6", 0, n6, "4"), ("v4", n4, 0, "3"), ("v4", n4, 0, "2")]
+    for leg, m4, m6, k4 in legs:
+        os.environ["CILIUM_GPU_IPC_K"] = k4  # read by the launcher on each call
         sec = timed(torch, stream, lambda: ic.resolve_dev(d4, m4, o4, d6, m6, o6, stream=stream.cuda_stream),
                     args.steps, 2)
-        print(json.dumps({"leg": leg, "encoding": "dense" if args.dense else "encoded", "v4": m4, "v6": m6,
-                          "ms": round(sec * 1e3, 3), "G_lookups_per_s": round((m4 + m6) / sec / 1e9, 2)}),
-              flush=True)
+        print(json.dumps({"leg": leg, "encoding": "encoded" if args.encode else "dense", "v4_per_lane": int(k4),
+                          "v4": m4, "v6": m6, "ms": round(sec * 1e3, 3),
+                          "G_lookups_per_s": round((m4 + m6) / sec / 1e9, 2)}), flush=True)
+    os.environ.pop("CILIUM_GPU_IPC_K")
     cl.close()
 
 
