@@ -789,6 +789,39 @@ __device__ __forceinline__ bool parse_list_fast(const HttpRawDev& R, const Tabs&
   return ok;
 }
 
+// parse_list_fast with the first 128 bits of both masks in registers
+// (MaskWin: s = stop, n = NUL): a short list's searches are register work,
+// and a stop byte is told from a NUL by the NUL window, not a byte read.
+// For header lists of HTTP snapshots (not raw_values).
+template <class Tabs>
+__device__ __forceinline__ bool parse_list_win(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
+                                               const lds_u32* mstop, const lds_u32* mzero, uint32_t hs, uint32_t he,
+                                               lds_u32* sp, uint32_t stride, Parsed& P) {
+  P.present = P.vsum = 0;
+  const MaskWin W = load_win(mstop, mzero, hs);
+  bool ok = true;
+  for (uint32_t k = hs; k < he;) {
+    const uint32_t ne = wnext(W.n, W.base, mzero, k, he), nl = ne - k;
+    const uint32_t v = ne < he ? ne + 1 : he;
+    const uint32_t s = v < he ? wnext(W.s, W.base, mstop, v, he) : he;
+    uint32_t e = s;
+    if (s < he && !wbit(W.n, W.base, mzero, s)) {  // a byte the codec rejects
+      ok = false;
+      e = wnext(W.n, W.base, mzero, s, he);
+    }
+    int f = R.f_empty;
+    if (nl) {
+      const uint32_t lo0 = lower4(keep_bytes(squad(st, k), nl));
+      const uint32_t lo1 = nl > 4 ? lower4(keep_bytes(squad(st, k + 4), nl - 4)) : 0u;
+      const uint32_t hi0 = nl > 8 ? lower4(squad(st, k + nl - 8)) : 0u, hi1 = nl > 8 ? lower4(squad(st, k + nl - 4)) : 0u;
+      f = field_of_words(R, T, st, k, nl, lo0, lo1, hi0, hi1);
+    }
+    if (f >= 0 && !(P.present >> f & 1u)) P.set(sp, stride, (uint32_t)f, (v - hs) << 16 | (e - v));  // first value wins
+    k = e < he ? e + 1 : he;
+  }
+  return ok;
+}
+
 // A list outside the stage, byte by byte.
 template <class Tabs>
 __device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, const Tabs& T, HeadReader& hr, lds_u32* sp,
@@ -2080,27 +2113,25 @@ __device__ __forceinline__ unsigned long long sys_load64(const unsigned long lon
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The program block (and code map) of p into LDS: 16-byte loads, eight in
-// flight per lane, so a 64-KB block takes a few round trips.
+// The program block (and code map) of p into LDS by LDS-DMA: every 1 KiB
+// piece's global_load_lds_dwordx4 issued back to back (no registers held),
+// then one wait — a 64-KB block in about one memory round trip, not eight.
 __device__ __forceinline__ void ring_stage(const HttpDev& HT, const HttpRawDev& R, const HttpProg& pg, uint32_t p,
                                            lds_u32* cells, lds_u32* cmap, uint32_t lane) {
   const uint32_t* src = HT.cells + pg.cell_begin;
   const uint32_t n = pg.cell_count;
   uint32_t done = 0;
   if ((((uintptr_t)src) & 15) == 0) {
-    const uint32_t n4 = n / 4;
-    for (uint32_t c0 = lane; c0 < n4; c0 += kRingThreads * 8) {
-      uint4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const uint4*>(src)[min(c0 + u * kRingThreads, n4 - 1)];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (c0 + u * kRingThreads < n4) *(lds_v4*)(cells + 4 * (c0 + u * kRingThreads)) = to_v4(v[u]);
-    }
+    const uint32_t n4 = n / 4;  // 16-byte units
+    for (uint32_t c0 = 0; c0 < n4; c0 += kRingThreads)
+      if (c0 + lane < n4)  // (the last piece's lanes past the block write nothing)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 4 * (c0 + lane)),
+                                         (__attribute__((address_space(3))) void*)(cells + 4 * c0), 16, 0, 0);
     done = 4 * n4;
   }
   for (uint32_t c = done + lane; c < n; c += kRingThreads) cells[c] = src[c];
   for (uint32_t c = lane; c < 64; c += kRingThreads) cmap[c] = reinterpret_cast<const uint32_t*>(R.codes + (size_t)p * 256)[c];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA'd pieces have landed
 }
 
 // The structural masks of a call's lists (list_stop / NUL, as the list
@@ -2323,7 +2354,9 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
       // with the walk over the emitted string
       Parsed P;
       const bool ok = prog != kProgDeny && e - a <= kFieldsMaxList &&
-                      parse_list_fast(R, T, blob, masks, masks + kRingMaskWords, a, e, sp, kRingThreads, P);
+                      (R.raw_values
+                           ? parse_list_fast(R, T, blob, masks, masks + kRingMaskWords, a, e, sp, kRingThreads, P)
+                           : parse_list_win(R, T, blob, masks, masks + kRingMaskWords, a, e, sp, kRingThreads, P));
       if (G.trace && i == 0) stamp[4] = stamp[5] = (uint32_t)wall_clock64();
       const uint32_t* blk = lds ? (const uint32_t*)cells : nullptr;
       const uint8_t* lut = lds ? (const uint8_t*)cmap : nullptr;

@@ -237,6 +237,9 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
   while (__atomic_load_n(&w[1], __ATOMIC_ACQUIRE) != seq) {
     cpu_relax();
     const uint64_t t = now_ns();
+    // past the device's usual time, spin yielding the core: callers on every
+    // core (Envoy's workers) must not keep one another's turn waiting
+    if (t - t0 > 6000) std::this_thread::yield();
     if (t - checked < 20000) continue;
     checked = t;
     // not served within 20 us: the launch may have left (idle or life)

@@ -6,7 +6,7 @@
 // cilium_network_policy.h:223-237).  A drop-in hands the engine the header
 // lists it has (cg_http_pack's name\0value\0 input) in batches of B requests.
 // Three host entries are timed, each for B in {1, 16, 256, 4096, 65536} and 1
-// and 16 submitting threads:
+// and 16 submitting threads (the ring also 4 and 8):
 //   ring    cg_http_ring_verdicts: the persistent verdict ring (a resident
 //           kernel polls request slots in pinned host memory: no launch, no
 //           copies, no stream synchronization per call; B <= 256)
@@ -163,7 +163,8 @@ int main(int argc, char** argv) {
     }
     for (const size_t B : {(size_t)1, (size_t)16, (size_t)256, (size_t)4096, (size_t)65536}) {
       if (B > p.n || (mode == 1 && B > 256)) continue;
-      for (const int threads : {1, 16}) {
+      for (const int threads : {1, 4, 8, 16}) {
+        if (mode != 1 && (threads == 4 || threads == 8)) continue;  // (the ring's scaling only)
         {  // warm-up (pinned buffers, workers, launch caches) outside the clock
           Result w;
           submit(h, p, mode, B, 0, 0.05, &w);
