@@ -55,6 +55,23 @@ struct Bits {
     cnt -= need;
     return v;
   }
+  // the next `need` (<= 16) bits without consuming them; bits past the input
+  // read as 0 (drop() then fails if a code needs them)
+  CG_HD uint32_t peek(uint32_t need) {
+    while (cnt < need && pos < n) {
+      buf |= (uint32_t)p[pos++] << cnt;
+      cnt += 8;
+    }
+    return buf & ((1u << need) - 1u);
+  }
+  CG_HD void drop(uint32_t k) {
+    if (k > cnt) {
+      err = true;
+      return;
+    }
+    buf >>= k;
+    cnt -= k;
+  }
 };
 
 // A canonical code: count[l] codes of length l, symbols in code order.
@@ -145,6 +162,50 @@ CG_HD inline int codes(Bits& b, const Huff& lit, const Huff& dist, uint8_t* dst,
   }
 }
 
+// A fixed-code block (RFC 1951 3.2.6) decoded arithmetically: the codes are
+// canonical over four ranges, so the next 9 bits, bit-reversed into code
+// order, name the symbol and its length with no table (small payloads —
+// Kafka's message sets — are compressed as fixed blocks: zlib picks them
+// below a few hundred bytes).  Same results as codes() over the built
+// fixed tables, errors included (literal/length 286-287, distance 30-31).
+CG_HD inline int codes_fixed(Bits& b, uint8_t* dst, uint32_t cap, uint32_t& d) {
+  for (;;) {
+    const uint32_t c9 = __builtin_bitreverse32(b.peek(9)) >> 23;
+    int s;
+    uint32_t l;
+    if ((c9 >> 2) <= 23) {  // 0000000-0010111: 256-279
+      s = 256 + (int)(c9 >> 2);
+      l = 7;
+    } else if ((c9 >> 1) <= 0xBF) {  // 00110000-10111111: 0-143
+      s = (int)(c9 >> 1) - 0x30;
+      l = 8;
+    } else if ((c9 >> 1) <= 0xC7) {  // 11000000-11000111: 280-287
+      s = 280 + (int)(c9 >> 1) - 0xC0;
+      l = 8;
+    } else {  // 110010000-111111111: 144-255
+      s = 144 + (int)c9 - 0x190;
+      l = 9;
+    }
+    b.drop(l);
+    if (b.err) return kKwzError;
+    if (s < 256) {
+      if (d >= cap) return kKwzMore;
+      dst[d++] = (uint8_t)s;
+      continue;
+    }
+    if (s == 256) return kKwzOk;
+    const int li = s - 257;
+    if (li >= 29) return kKwzError;  // 286, 287
+    const uint32_t len = kLenBase[li] + b.get(kLenExtra[li]);
+    const int ds = (int)(__builtin_bitreverse32(b.get(5)) >> 27);
+    if (ds >= 30 || b.err) return kKwzError;
+    const uint32_t off = kDistBase[ds] + b.get(kDistExtra[ds]);
+    if (b.err || off > d) return kKwzError;  // distance too far back
+    if (len > cap - d) return kKwzMore;
+    for (uint32_t k = 0; k < len; ++k, ++d) dst[d] = dst[d - off];
+  }
+}
+
 // RFC 1951 DEFLATE data at src[0, n) into dst[0, cap): *out = bytes
 // written, *used = input bytes consumed (through the byte holding the last
 // block's end).
@@ -158,6 +219,7 @@ CG_HD inline int inflate_raw(const uint8_t* src, uint32_t n, uint8_t* dst, uint3
     const uint32_t last = b.get(1), type = b.get(2);
     if (b.err) return kKwzError;
     if (type == 0) {  // stored: to the byte boundary, LEN, NLEN, the bytes
+      b.pos -= b.cnt / 8;  // (whole bytes a fixed block's peek loaded ahead)
       b.buf = 0;
       b.cnt = 0;
       if (b.pos + 4 > n) return kKwzError;
@@ -170,15 +232,7 @@ CG_HD inline int inflate_raw(const uint8_t* src, uint32_t n, uint8_t* dst, uint3
       for (uint32_t k = 0; k < l; ++k) dst[d++] = src[b.pos + k];
       b.pos += l;
     } else if (type == 1) {  // fixed codes (RFC 1951 3.2.6)
-      int s = 0;
-      for (; s < 144; ++s) len[s] = 8;
-      for (; s < 256; ++s) len[s] = 9;
-      for (; s < 280; ++s) len[s] = 7;
-      for (; s < 288; ++s) len[s] = 8;
-      huff_build(lit, len, 288);
-      for (s = 0; s < 30; ++s) len[s] = 5;
-      huff_build(dist, len, 30);
-      const int r = codes(b, lit, dist, dst, cap, d);
+      const int r = codes_fixed(b, dst, cap, d);
       if (r != kKwzOk) return r;
     } else if (type == 2) {  // dynamic codes (RFC 1951 3.2.7)
       const uint32_t nlen = b.get(5) + 257, ndist = b.get(5) + 1, ncode = b.get(4) + 4;
@@ -220,7 +274,7 @@ CG_HD inline int inflate_raw(const uint8_t* src, uint32_t n, uint8_t* dst, uint3
     }
     if (last) break;
   }
-  *used = b.pos;
+  *used = b.pos - b.cnt / 8;
   *out = d;
   return kKwzOk;
 }
