@@ -774,9 +774,14 @@ int cg_diag_ipcache_eval_host(uint64_t h, uint32_t ipc_id, const uint32_t* v4, s
         L = t.ent6[4 * (size_t)k];
         R = t.ent6[4 * (size_t)k + 1];
         const uint32_t crowd = t.ent6[4 * (size_t)k + 2];
-        v = t.runs6[4 * (size_t)R + 2];
-        if (!ipc_le128(t.runs6[4 * (size_t)R], t.runs6[4 * (size_t)R + 1], hi, lo))
-          v = ipc_v6_search_value(t, hi, lo, L, R, crowd);
+        uint64_t xv;
+        if (t.ent6[4 * (size_t)k + 3] && ipc_ex6_find(t, hi, lo, ipc_ex6_hash(hi, lo) & t.ex6_mask, &xv)) {
+          v = xv;  // a /128 entry
+        } else {
+          v = t.runs6[4 * (size_t)R + 2];
+          if (!ipc_le128(t.runs6[4 * (size_t)R], t.runs6[4 * (size_t)R + 1], hi, lo))
+            v = ipc_v6_search_value(t, hi, lo, L, R, crowd);
+        }
       }
       out6[i] = cg_remote_endpoint_info{(uint32_t)v, (uint32_t)(v >> 32)};
     }

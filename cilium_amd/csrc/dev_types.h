@@ -583,7 +583,53 @@ struct IpcacheDev {
   const uint64_t* runs6;   // 4 u64 per run
   uint32_t v6_bits;
   uint32_t nruns6;
+  // the /32 and /128 entries, by exact match (a full-length prefix is the
+  // longest one covering its address): open addressing, linear probing at
+  // load <= 1/2; a v4 slot {address, used, entry lo, entry hi}, a v6 slot
+  // {address hi, address lo, entry, used} (u64 words); ex*_probes bounds
+  // every search (the longest probe sequence the build made)
+  const uint32_t* ex4;
+  const uint64_t* ex6;
+  uint32_t ex4_mask, ex6_mask, ex4_probes, ex6_probes;
 };
+// summary flag (l16x word 3): the /16 holds exact /32 entries
+constexpr uint32_t kIpcExact = 1u << 17;
+CG_HD inline uint32_t ipc_ex4_hash(uint32_t a) {
+  a ^= a >> 16;
+  a *= 0x7FEB352Du;
+  a ^= a >> 15;
+  a *= 0x846CA68Bu;
+  return a ^ (a >> 16);
+}
+CG_HD inline uint32_t ipc_ex6_hash(uint64_t hi, uint64_t lo) {
+  uint64_t x = hi * 0x9E3779B97F4A7C15ull ^ lo;
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  return (uint32_t)(x >> 32);
+}
+// The exact /32 entry of a (host order): 1 found (*e), 0 not there.
+CG_HD inline int ipc_ex4_find(const IpcacheDev& t, uint32_t a, uint32_t h, uint64_t* e) {
+  for (uint32_t p = 0; p <= t.ex4_probes; ++p) {
+    const uint32_t* s = t.ex4 + 4 * (size_t)((h + p) & t.ex4_mask);
+    if (!s[1]) return 0;
+    if (s[0] == a) {
+      *e = (uint64_t)s[3] << 32 | s[2];
+      return 1;
+    }
+  }
+  return 0;
+}
+CG_HD inline int ipc_ex6_find(const IpcacheDev& t, uint64_t hi, uint64_t lo, uint32_t h, uint64_t* e) {
+  for (uint32_t p = 0; p <= t.ex6_probes; ++p) {
+    const uint64_t* s = t.ex6 + 4 * (size_t)((h + p) & t.ex6_mask);
+    if (!s[3]) return 0;
+    if (s[0] == hi && s[1] == lo) {
+      *e = s[2];
+      return 1;
+    }
+  }
+  return 0;
+}
 
 // ---- IPv4: 256-entry chunks in one of three encodings (ipcache.cc) ------
 // An entry is a resolved {identity, tunnel} (identity != 0) or a pointer to
@@ -650,7 +696,7 @@ CG_HD inline bool ipc_v4_in(uint32_t r, uint32_t a) {
   const uint32_t k = (a >> 8) & 255;
   return k >= (r & 255) && k <= ((r >> 8) & 255);
 }
-CG_HD inline uint32_t ipc_v4_key(uint32_t r, uint32_t a) { return (r >> 16) ? (a & 255) : ((a >> 8) & 255); }
+CG_HD inline uint32_t ipc_v4_key(uint32_t r, uint32_t a) { return ((r >> 16) & 1) ? (a & 255) : ((a >> 8) & 255); }
 // K chunk reads at once, each round's loads issued for all K before the
 // next round (the kernels' form of ipc_chunk_get); a lane reads the round-2
 // word only when its entry needs it.
@@ -673,7 +719,7 @@ CG_HD inline void ipc_chunk_rounds(const uint64_t* __restrict__ ch, const uint32
 template <uint32_t K>
 CG_HD inline void ipc_v4_resolve(const IpcacheDev& t, const uint32_t (&a)[K], uint64_t (&e)[K]) {
   uint32_t ref[K], key[K];
-  bool in[K];
+  bool in[K], ex[K];
   IpcPair x[K];
 #pragma unroll
   for (uint32_t u = 0; u < K; ++u) x[u] = *reinterpret_cast<const IpcPair*>(t.l16x + 4 * (size_t)(a[u] >> 16));
@@ -681,12 +727,33 @@ CG_HD inline void ipc_v4_resolve(const IpcacheDev& t, const uint32_t (&a)[K], ui
   for (uint32_t u = 0; u < K; ++u) {
     const uint32_t r = (uint32_t)(x[u].hi >> 32);
     in[u] = ipc_v4_in(r, a[u]);
+    ex[u] = (r & kIpcExact) != 0;
     e[u] = x[u].lo;
     ref[u] = in[u] ? (uint32_t)x[u].hi : 0u;
     key[u] = ipc_v4_key(r, a[u]);
   }
+  // a /16 holding /32 entries: the exact table's first slot, loaded in the
+  // chunk round (a hit is the answer; a used slot of another address
+  // continues the probe sequence)
+  uint32_t hx[K];
+  IpcPair sx[K];
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) {
+    hx[u] = ipc_ex4_hash(a[u]) & t.ex4_mask;
+    sx[u] = IpcPair{0, 0};
+    if (ex[u]) sx[u] = *reinterpret_cast<const IpcPair*>(t.ex4 + 4 * (size_t)hx[u]);
+  }
   uint64_t r[K];
   ipc_chunk_rounds<K>(t.chunks, ref, key, r);
+#pragma unroll
+  for (uint32_t u = 0; u < K; ++u) {
+    if (!ex[u] || (uint32_t)(sx[u].lo >> 32) == 0) continue;  // no exact entry here
+    uint64_t v;
+    if ((uint32_t)sx[u].lo == a[u] ? (v = sx[u].hi, true) : ipc_ex4_find(t, a[u], hx[u] + 1, &v)) {
+      e[u] = v;
+      in[u] = false;  // settled: the longest prefix
+    }
+  }
   bool ptr[K], any = false;
 #pragma unroll
   for (uint32_t u = 0; u < K; ++u) {
@@ -705,6 +772,8 @@ CG_HD inline void ipc_v4_resolve(const IpcacheDev& t, const uint32_t (&a)[K], ui
 }
 CG_HD inline uint64_t ipc_v4_value(const IpcacheDev& t, uint32_t a) {  // a in host order
   const uint32_t* x = t.l16x + 4 * (size_t)(a >> 16);
+  uint64_t ev;
+  if ((x[3] & kIpcExact) && ipc_ex4_find(t, a, ipc_ex4_hash(a) & t.ex4_mask, &ev)) return ev;
   if (!ipc_v4_in(x[3], a)) return (uint64_t)x[1] << 32 | x[0];
   uint64_t e = ipc_chunk_get(t.chunks, x[2], ipc_v4_key(x[3], a));
   if ((uint32_t)e == 0) e = ipc_chunk_get(t.chunks, (uint32_t)(e >> 32), a & 255);

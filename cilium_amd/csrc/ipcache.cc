@@ -50,13 +50,57 @@ void IpcacheState::build_tables() {
 
   // ---- IPv4: paint prefixes in increasing length, so a range being painted
   // never holds a pointer below the prefix's own level.
+  // Full-length prefixes (/32, /128: pod addresses, most of a cluster's
+  // ipcache) go to the exact tables; the trie and the runs hold the rest.
   std::vector<std::tuple<int, uint32_t, uint64_t>> v4;  // plen, net (host order), entry
   std::vector<std::tuple<U128, int, uint64_t>> v6;      // start, plen, entry
+  std::vector<std::pair<uint32_t, uint64_t>> x4;        // /32: address, entry
+  std::vector<std::pair<U128, uint64_t>> x6;            // /128
   for (const auto& [k, v] : entries) {
-    if (k.family == 4)
-      v4.emplace_back(k.plen, (uint32_t)k.net[0] << 24 | k.net[1] << 16 | k.net[2] << 8 | k.net[3], resolved(v));
-    else
-      v6.emplace_back(key128(k), k.plen, resolved(v));
+    if (k.family == 4) {
+      const uint32_t net = (uint32_t)k.net[0] << 24 | k.net[1] << 16 | k.net[2] << 8 | k.net[3];
+      if (k.plen == 32) x4.emplace_back(net, resolved(v));
+      else v4.emplace_back(k.plen, net, resolved(v));
+    } else {
+      if (k.plen == 128) x6.emplace_back(key128(k), resolved(v));
+      else v6.emplace_back(key128(k), k.plen, resolved(v));
+    }
+  }
+  // open addressing at load <= 1/4 (a lookup's first slot is nearly always
+  // the answer or empty), linear probing; the longest probe sequence bounds
+  // every lookup
+  {
+    uint32_t cap = 16;
+    while (cap < 4 * x4.size()) cap <<= 1;
+    ex4.assign(4 * (size_t)cap, 0);
+    ex4_mask = cap - 1;
+    ex4_probes = 0;
+    for (const auto& [a, e] : x4) {
+      uint32_t p = 0;
+      while (ex4[4 * (size_t)((ipc_ex4_hash(a) + p) & ex4_mask) + 1]) ++p;
+      uint32_t* sl = &ex4[4 * (size_t)((ipc_ex4_hash(a) + p) & ex4_mask)];
+      sl[0] = a;
+      sl[1] = 1;
+      sl[2] = (uint32_t)e;
+      sl[3] = (uint32_t)(e >> 32);
+      ex4_probes = std::max(ex4_probes, p);
+    }
+    cap = 16;
+    while (cap < 4 * x6.size()) cap <<= 1;
+    ex6.assign(4 * (size_t)cap, 0);
+    ex6_mask = cap - 1;
+    ex6_probes = 0;
+    for (const auto& [k, e] : x6) {
+      const uint32_t h = ipc_ex6_hash(k.first, k.second);
+      uint32_t p = 0;
+      while (ex6[4 * (size_t)((h + p) & ex6_mask) + 3]) ++p;
+      uint64_t* sl = &ex6[4 * (size_t)((h + p) & ex6_mask)];
+      sl[0] = k.first;
+      sl[1] = k.second;
+      sl[2] = e;
+      sl[3] = 1;
+      ex6_probes = std::max(ex6_probes, p);
+    }
   }
   std::sort(v4.begin(), v4.end());
   l16.assign(65536, kIpcMiss);
@@ -130,6 +174,7 @@ void IpcacheState::build_tables() {
       sum_chunk[q] = chunk;
       sum_range[q] = lo | hi << 8 | direct << 16;
     }
+    for (const auto& xa : x4) sum_range[xa.first >> 16] |= kIpcExact;
   }
 
   // Encode the dense chunks (dev_types.h ipc_chunk_get): /32-level chunks
@@ -268,6 +313,8 @@ void IpcacheState::build_tables() {
   while (bits < 22 && (1ull << bits) < 2 * runs.size()) ++bits;
   v6_bits = bits;
   const uint32_t nb = 1u << bits;
+  std::vector<uint8_t> has_exact(nb, 0);  // buckets holding /128 entries (set, flagged)
+  for (const auto& xk : x6) has_exact[(uint32_t)(xk.first.first >> (64 - bits))] = 1;
   code6.assign(nb / 32, 0);
   ent6.clear();
   crowd6.clear();
@@ -280,7 +327,7 @@ void IpcacheState::build_tables() {
     while (L + 1 < runs.size() && runs[L + 1].first <= start) ++L;
     size_t R = L;  // last run starting at or before the bucket end
     while (R + 1 < runs.size() && runs[R + 1].first <= end) ++R;
-    if (R == L && runs[L].second == kIpcMiss) continue;
+    if (R == L && runs[L].second == kIpcMiss && !has_exact[t]) continue;
     code6[t >> 5] |= 1ULL << (t & 31);
     ++nset;
     uint32_t crowd = kIpcNoCrowd;
@@ -310,7 +357,7 @@ void IpcacheState::build_tables() {
         d[24 + i] = (uint8_t)(r - L);
       }
     }
-    ent6.insert(ent6.end(), {(uint32_t)L, (uint32_t)R, crowd, 0});
+    ent6.insert(ent6.end(), {(uint32_t)L, (uint32_t)R, crowd, (uint32_t)has_exact[t]});
   }
   if (ent6.empty()) ent6.assign(4, 0);
   if (crowd6.empty()) crowd6.assign(128, 0);
@@ -320,9 +367,10 @@ void IpcacheState::build_tables() {
       if ((uint32_t)l16[q] == 0) ++c24, direct += (l16x[4 * q + 3] >> 16) & 1;
     fprintf(stderr, "[cilium-gpu] ipcache: v4 chunks %zu (%zu /16s chunked, %zu direct): %zu runs, %zu sparse, "
             "%zu dense, %.1f MB (dense form %.1f MB); v6 runs %zu (%.1f MB), buckets 2^%u, set %zu (%.1f MB), "
-            "crowd lines %zu\n", ndense, c24, direct, n_runs, n_sparse, n_dense, chunks.size() * 8 / 1e6,
-            dense_bytes / 1e6, runs6.size() / 4, runs6.size() * 8 / 1e6, v6_bits, ent6.size() / 4,
-            ent6.size() * 4 / 1e6, crowd6.size() / 128);
+            "crowd lines %zu; exact /32 %zu (%.1f MB, probes <= %u), /128 %zu (%.1f MB, probes <= %u)\n", ndense, c24,
+            direct, n_runs, n_sparse, n_dense, chunks.size() * 8 / 1e6, dense_bytes / 1e6, runs6.size() / 4,
+            runs6.size() * 8 / 1e6, v6_bits, ent6.size() / 4, ent6.size() * 4 / 1e6, crowd6.size() / 128, x4.size(),
+            ex4.size() * 4 / 1e6, ex4_probes + 1, x6.size(), ex6.size() * 8 / 1e6, ex6_probes + 1);
   }
 }
 
@@ -336,6 +384,12 @@ IpcacheDev IpcacheState::host_view() const {
   v.runs6 = runs6.data();
   v.v6_bits = v6_bits;
   v.nruns6 = (uint32_t)(runs6.size() / 4);
+  v.ex4 = ex4.data();
+  v.ex6 = ex6.data();
+  v.ex4_mask = ex4_mask;
+  v.ex6_mask = ex6_mask;
+  v.ex4_probes = ex4_probes;
+  v.ex6_probes = ex6_probes;
   return v;
 }
 
@@ -353,6 +407,12 @@ void IpcacheState::rebuild(Engine& e) {
     d.runs6 = t->add(runs6);
     d.v6_bits = v6_bits;
     d.nruns6 = (uint32_t)(runs6.size() / 4);
+    d.ex4 = t->add(ex4);
+    d.ex6 = t->add(ex6);
+    d.ex4_mask = ex4_mask;
+    d.ex6_mask = ex6_mask;
+    d.ex4_probes = ex4_probes;
+    d.ex6_probes = ex6_probes;
     tab = std::move(t);  // publish (the caller holds the handle lock)
     dev = d;
   }

@@ -23,6 +23,9 @@ struct IpcacheState {
   std::vector<uint64_t> l16, chunks, runs6, code6;  // l16: the /16 level while building
   std::vector<uint32_t> l16x, ent6;
   std::vector<uint8_t> crowd6;
+  std::vector<uint32_t> ex4;  // exact /32 slots (dev_types.h IpcacheDev)
+  std::vector<uint64_t> ex6;  // exact /128 slots
+  uint32_t ex4_mask = 0, ex6_mask = 0, ex4_probes = 0, ex6_probes = 0;
   uint32_t v6_bits = 16;
   std::shared_ptr<DevTables> tab;  // the published device tables (engine.h)
   IpcacheDev dev{};                // view of tab; copy it together with tab

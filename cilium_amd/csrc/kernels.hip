@@ -194,10 +194,12 @@ __device__ void l4_flush(const L4Dev& t, unsigned long long* lcnt) {
 // The remote identity of the egress flow (bpf_lxc.c:205-215 v6, :509-518 v4):
 // lookup_ip{4,6}_remote_endpoint resolved to sec_label, or WORLD_ID on a miss
 // or a zero sec_label (the tables store that resolution, dev_types.h).
-__device__ __forceinline__ uint32_t ipc_v6_identity(const IpcacheDev& ipc, uint64_t hi, uint64_t lo, uint32_t L,
-                                                    uint32_t R, uint32_t crowd, uint4 kr, uint32_t v) {
+__device__ __forceinline__ uint32_t ipc_v6_identity(const IpcacheDev& ipc, uint64_t hi, uint64_t lo, uint4 en,
+                                                    uint4 kr, uint32_t v) {
+  uint64_t xv;
+  if (en.w && ipc_ex6_find(ipc, hi, lo, ipc_ex6_hash(hi, lo) & ipc.ex6_mask, &xv)) return (uint32_t)xv;  // a /128
   if (!ipc_le128(((uint64_t)kr.y << 32) | kr.x, ((uint64_t)kr.w << 32) | kr.z, hi, lo))
-    v = (uint32_t)ipc_v6_search_value(ipc, hi, lo, L, R, crowd);
+    v = (uint32_t)ipc_v6_search_value(ipc, hi, lo, en.x, en.y, en.z);
   return v;
 }
 
@@ -295,8 +297,7 @@ __global__ __launch_bounds__(1024) void l4_fp_kernel(L4Dev t, IpcacheDev ipc, co
       }
 #pragma unroll
       for (uint32_t u = 0; u < kL4Tuples; ++u)
-        w[u][0] = set[u] ? ipc_v6_identity(ipc, hi[u], lo[u], L[u], R[u], ent[u].z, kr[u], vr[u].x)
-                         : (uint32_t)kIpcMiss;
+        w[u][0] = set[u] ? ipc_v6_identity(ipc, hi[u], lo[u], ent[u], kr[u], vr[u].x) : (uint32_t)kIpcMiss;
     }
     // candidates of every tuple, then every tuple's first slot load in
     // flight together, then the walks
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(256) void l4_kernel(L4Dev t, IpcacheDev ipc, const 
         L = en.x;
         R = en.y;
         const uint4* rec = reinterpret_cast<const uint4*>(ipc.runs6 + 4 * (size_t)R);
-        w0 = ipc_v6_identity(ipc, hi, lo, L, R, en.z, rec[0], rec[1].x);
+        w0 = ipc_v6_identity(ipc, hi, lo, en, rec[0], rec[1].x);
       }
     } else {
       w0 = tuples[i * 3 + 0];

@@ -10,7 +10,7 @@
 // record, and a short binary search when that run starts after the address).  Entries carry the resolved value inline, so
 // the last table load is the answer.  Each lane resolves
 // several addresses with every level's loads issued for all of them before
-// the next level, so a wave keeps 4 (v4) / 2 (v6) independent chains in
+// the next level, so a wave keeps 2-4 (v4) / 2 (v6) independent chains in
 // flight.
 #include <hip/hip_runtime.h>
 
@@ -87,8 +87,11 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
     // a plain set bucket: its last run (most buckets hold one run); a crowded
     // one: its crowd line's prefix and shift instead (the last run rarely
     // holds a pod address, so it is not read)
-    uint4 kr[kIpcV6], vr[kIpcV6], cp[kIpcV6], cs[kIpcV6];
-    bool crowd[kIpcV6];
+    // (a crowded bucket — many runs, now rare: the /128 pods are in the
+    // exact table — reads its crowd line in the last step)
+    uint4 kr[kIpcV6], vr[kIpcV6], x0[kIpcV6], x1[kIpcV6];
+    bool crowd[kIpcV6], ex[kIpcV6];
+    uint32_t hx[kIpcV6];
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
       L[u] = ent[u].x;
@@ -97,20 +100,33 @@ __global__ __launch_bounds__(kIpcThreads) void ipcache_kernel(IpcacheDev t, cons
       const uint4* rec = reinterpret_cast<const uint4*>(t.runs6 + 4 * (size_t)(set[u] && !crowd[u] ? R[u] : 0));
       kr[u] = rec[0];
       vr[u] = rec[1];
-      const uint4* cl = reinterpret_cast<const uint4*>(t.crowd6 + 128 * (size_t)(crowd[u] ? ent[u].z : 0));
-      cp[u] = cl[0];
-      cs[u] = cl[1];
+      // a bucket holding /128 entries: the exact table's first slot
+      ex[u] = set[u] && ent[u].w != 0;
+      hx[u] = ipc_ex6_hash(hi[u], lo[u]) & t.ex6_mask;
+      x0[u] = x1[u] = make_uint4(0, 0, 0, 0);
+      if (ex[u]) {
+        const uint4* xs = reinterpret_cast<const uint4*>(t.ex6 + 4 * (size_t)hx[u]);
+        x0[u] = xs[0];
+        x1[u] = xs[1];
+      }
     }
 #pragma unroll
     for (uint32_t u = 0; u < kIpcV6; ++u) {
       const size_t j = base + u * blockDim.x + threadIdx.x;
       if (j >= n6) continue;
-      uint64_t v = u64_of(vr[u].x, vr[u].y);
+      uint64_t v = u64_of(vr[u].x, vr[u].y), xv = 0;
+      const bool used = ex[u] && (x1[u].z | x1[u].w) != 0;
       if (!set[u]) {
         v = kIpcMiss;
+      } else if (used && u64_of(x0[u].x, x0[u].y) == hi[u] && u64_of(x0[u].z, x0[u].w) == lo[u]) {
+        v = u64_of(x1[u].x, x1[u].y);  // the /128 entry: the longest prefix
+      } else if (used && ipc_ex6_find(t, hi[u], lo[u], hx[u] + 1, &xv)) {
+        v = xv;
       } else if (crowd[u]) {
         uint32_t i = 0, l = L[u], r = R[u];
-        const uint32_t w = ipc_v6_window(u64_of(cp[u].x, cp[u].y), u64_of(cp[u].z, cp[u].w), cs[u].x, hi[u], lo[u], &i);
+        const uint4* cl = reinterpret_cast<const uint4*>(t.crowd6 + 128 * (size_t)ent[u].z);
+        const uint4 cp = cl[0], cs = cl[1];
+        const uint32_t w = ipc_v6_window(u64_of(cp.x, cp.y), u64_of(cp.z, cp.w), cs.x, hi[u], lo[u], &i);
         if (w == 0) {
           r = l;
         } else if (w == 1) {
@@ -140,10 +156,11 @@ int resident_blocks(const void* fn, int threads) {
 int launch_ipcache(const IpcacheDev& t, const uint32_t* v4, size_t n4, IpcVal* out4, const uint8_t* v6, size_t n6,
                    IpcVal* out6, void* stream, int cus) {
   if (n4 + n6 == 0) return 0;
-  // IPv4 addresses per lane per iteration: 4 (CILIUM_GPU_IPC_K = 2..4 for
-  // the A/B of tools/ipcache_split.py)
+  // IPv4 addresses per lane per iteration: 2 (the kernel's 62 VGPRs keep 8
+  // waves per SIMD for the IPv6 loop too; 2, 3 and 4 run the IPv4 half
+  // alike — CILIUM_GPU_IPC_K = 2..4 for the A/B of tools/ipcache_split.py)
   const char* ke = getenv("CILIUM_GPU_IPC_K");
-  const uint32_t K = ke && atoi(ke) >= 2 && atoi(ke) <= 4 ? (uint32_t)atoi(ke) : 4u;
+  const uint32_t K = ke && atoi(ke) >= 2 && atoi(ke) <= 4 ? (uint32_t)atoi(ke) : 2u;
   const void* fn = K == 2 ? (const void*)ipcache_kernel<2> : K == 3 ? (const void*)ipcache_kernel<3>
                                                                     : (const void*)ipcache_kernel<4>;
   int dev = 0;

@@ -2,7 +2,8 @@
 
 Times cg_ipcache_resolve_dev on the bench's 512K-entry table (synth) over
 100M addresses (70% v4) as bench_paths.py's ipcache line does, then the v4
-and v6 addresses alone, and the v4 addresses at 3 and 2 per lane
+and v6 addresses alone (2 v4 addresses per lane, the default), then the
+mix at 4 per lane and the v4 addresses at 3 and 4 per lane
 (CILIUM_GPU_IPC_K); with --encode the builder writes run lines and sparse
 maps (CILIUM_GPU_IPC_ENCODE, set before the library loads), the encoding A/B.
 One JSON line per leg."""
@@ -39,7 +40,8 @@ def main():
     n4, n6 = len(a4), len(a6)
     o4 = torch.empty(n4 * 2, dtype=torch.int32, device=dev)
     o6 = torch.empty(n6 * 2, dtype=torch.int32, device=dev)
-    legs = [("both", n4, n6, "4"), ("v4", n4, 0, "4"), ("v6", 0, n6, "4"), ("v4", n4, 0, "3"), ("v4", n4, 0, "2")]
+    legs = [("both", n4, n6, "2"), ("v4", n4, 0, "2"), ("v6", 0, n6, "2"), ("both", n4, n6, "4"), ("v4", n4, 0, "3"),
+            ("v4", n4, 0, "4")]
     for leg, m4, m6, k4 in legs:
         os.environ["CILIUM_GPU_IPC_K"] = k4  # read by the launcher on each call
         sec = timed(torch, stream, lambda: ic.resolve_dev(d4, m4, o4, d6, m6, o6, stream=stream.cuda_stream),
