@@ -2,16 +2,18 @@
 // (bpf/lib/eps.h:48-115) with the callers' resolution (bpf_lxc.c:509-518):
 // address → {security identity, tunnel endpoint}.
 //
-// Integer work bound by the input/output stream plus dependent table loads
-// (IPv4: the /16 summary, then up to two encoded chunks — a run line, a
-// sparse map and its entry, or a dense entry: dev_types.h ipc_chunk_get;
-// IPv6: the bucket bit,
-// then for a bucket not spanned by one WORLD run its entry, its last 32-B run
-// record, and a short binary search when that run starts after the address).  Entries carry the resolved value inline, so
-// the last table load is the answer.  Each lane resolves
-// several addresses with every level's loads issued for all of them before
-// the next level, so a wave keeps 2-4 (v4) / 2 (v6) independent chains in
-// flight.
+// Integer work bound by the input/output stream plus dependent table loads.
+// IPv4: the /16 summary; then, in one round, the /24-level chunk's entry
+// (dense, or an encoded run line / sparse map: dev_types.h ipc_chunk_get)
+// and — when the /16 holds /32 entries — the exact table's slot (a /32 is
+// the longest prefix: a hit is the answer); then the /32-level chunk for a
+// pointer entry.  IPv6: the bucket bit, then for a bucket not spanned by one
+// WORLD run its entry, then its last 32-B run record with — when the bucket
+// holds /128 entries — the exact table's slot, and a short search when the
+// run starts after the address.  Entries carry the resolved value inline,
+// so the last table load is the answer.  Each lane resolves several
+// addresses with every level's loads issued for all of them before the next
+// level, so a wave keeps 2-4 (v4) / 2 (v6) independent chains in flight.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
