@@ -2462,7 +2462,9 @@ __global__ __launch_bounds__(kRingThreads) void http_ring_kernel(HttpDev HT, Htt
     if (wg == 0 && lane == 0) {
       const unsigned long long lw = __hip_atomic_load(&st->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t since = lw > t0 ? lw : t0;
-      if (sys_load32(&G.ctl[kRingStop]) || now - since > G.idle_ticks || now - t0 > G.life_ticks)
+      // (another workgroup may have stamped a call after this one read `now`:
+      // since > now is not idle)
+      if (sys_load32(&G.ctl[kRingStop]) || (now > since && now - since > G.idle_ticks) || now - t0 > G.life_ticks)
         __hip_atomic_store(&st->exit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t ex = __hip_atomic_load(&st->exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
