@@ -1241,7 +1241,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_kernel(HttpRawDev R, con
       if (prog != kProgDeny) {
         const uint32_t hs = (uint32_t)(ga - sbase);
         Parsed P;
-        const bool ok = kLists ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
+        const bool ok = kLists ? (R.raw_values ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
+                                             : parse_list_win(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P))
                                : parse_head_fast(R, T, stage, masks, masks + kMaskWords, mtab, hs, hs + hn, sp, kRawThreads, P);
         RAW_CLK(c3);
         if (!ok) {
@@ -1791,7 +1792,8 @@ __global__ __launch_bounds__(kRawThreads) void raw_scan_dl_kernel(HttpRawDev R, 
     Parsed P;
     P.present = P.vsum = 0;
     if (live && !defer && prog != kProgDeny) {
-      const bool ok = kLists ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
+      const bool ok = kLists ? (R.raw_values ? parse_list_fast(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P)
+                                             : parse_list_win(R, T, stage, masks, masks + kMaskWords, hs, hs + hn, sp, kRawThreads, P))
                              : parse_head_fast(R, T, stage, masks, masks + kMaskWords, mtab, hs, hs + hn, sp, kRawThreads, P);
       if (!ok) {
         flags |= CG_HTTP_F_MALFORMED;

@@ -158,6 +158,13 @@ struct DevValidated {
 // device does not finish goes to the host decoder (kKwDefer): a payload it
 // cannot size, a full arena, a second gzip member, output past the sized
 // buffer, and compressed sets nested inside compressed sets.
+// A payload that decodes to at most kInfLds bytes (most of a Kafka produce
+// request's sets: a few small messages) is decoded into the lane's LDS
+// buffer instead: the inflater's back-references read what it just wrote,
+// and a byte written to HBM and read back costs an L2 round trip, in LDS a
+// few dozen cycles.  The inner set is only validated, never kept, so
+// nothing is copied out.
+constexpr uint32_t kInfLds = 256, kInfLdsStride = 260;  // (65 words: lanes at one offset hit distinct banks)
 struct DevInflate {
   uint8_t* arena;
   unsigned long long cap;
@@ -165,6 +172,7 @@ struct DevInflate {
   unsigned long long* done;  // payloads decoded on the device (ctr[3])
   unsigned long long* full;  // payloads deferred unreserved: arena full or an impossible size (ctr[5])
   const LdsCrc* crc;
+  uint8_t* lds_out;  // this lane's kInfLds bytes of LDS, or nullptr
   __device__ uint8_t operator()(uint32_t codec, const uint8_t* p, uint32_t n, int16_t version) const {
     if (!arena) return kKwDefer;
     uint64_t need = 0;
@@ -181,12 +189,15 @@ struct DevInflate {
       atomicAdd(full, 1ull);
       return kKwDefer;
     }
-    const unsigned long long at = atomicAdd(used, (unsigned long long)need);
-    if (at + need > cap) {
-      atomicAdd(full, 1ull);
-      return kKwDefer;
+    uint8_t* dst = lds_out;
+    if (!lds_out || need > kInfLds) {
+      const unsigned long long at = atomicAdd(used, (unsigned long long)need);
+      if (at + need > cap) {
+        atomicAdd(full, 1ull);
+        return kKwDefer;
+      }
+      dst = arena + at;
     }
-    uint8_t* dst = arena + at;
     uint32_t got = 0;
     const int r = codec == 1 ? kwz::gunzip_one(p, n, dst, (uint32_t)need, &got, *crc)
                              : kwz::snappy_go(p, n, dst, (uint32_t)need, &got);
@@ -329,6 +340,7 @@ __global__ __launch_bounds__(kKwThreads) void kafka_inflate_kernel(
     uint8_t* __restrict__ status, const uint32_t* __restrict__ defer_list, uint8_t* __restrict__ zarena,
     unsigned long long zcap) {
   __shared__ uint32_t s_crc[kKwSlices * 256];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kKwThreads * kInfLdsStride];
   const unsigned long long nd = ctr[1];
   if (nd == 0) return;  // uniform: the common case
   for (uint32_t i = threadIdx.x; i < 256; i += kKwThreads) {
@@ -345,7 +357,7 @@ __global__ __launch_bounds__(kKwThreads) void kafka_inflate_kernel(
     __syncthreads();
   }
   const LdsCrc crc{s_crc};
-  const DevInflate inflate{zarena, zcap, ctr + 2, ctr + 3, ctr + 5, &crc};
+  const DevInflate inflate{zarena, zcap, ctr + 2, ctr + 3, ctr + 5, &crc, s_out + threadIdx.x * kInfLdsStride};
   for (unsigned long long j = (unsigned long long)blockIdx.x * kKwThreads + threadIdx.x; j < nd;
        j += (unsigned long long)gridDim.x * kKwThreads) {
     const uint32_t i = defer_list[j];
