@@ -147,6 +147,22 @@ struct DevDefer {
 // needs, so compressed payloads are passed over — the set's next message
 // follows from the outer framing alone — and no arena space is reserved
 // again.
+// One atomic per wave for the active lanes that want a slot of a shared
+// counter (a returning atomic per lane on one address serializes at the L2:
+// hundreds of thousands of them per call), each lane's index by its rank
+// among them.  Called by every active lane together (divergence is fine: the
+// ballot is over the lanes active here).
+__device__ __forceinline__ unsigned long long wave_append(unsigned long long* ctr, bool want) {
+  const unsigned long long m = __ballot(want);
+  if (!m) return 0;
+  const uint32_t lane = __lane_id(), leader = (uint32_t)__builtin_ctzll(m);
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)base, (int)leader, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)leader, 64);
+  return ((unsigned long long)hi << 32 | lo) + (unsigned long long)__popcll(m & ((1ull << lane) - 1));
+}
+
 struct DevValidated {
   __device__ uint8_t operator()(uint32_t, const uint8_t*, uint32_t, int16_t) const { return kKwOk; }
 };
@@ -203,7 +219,7 @@ struct DevInflate {
                              : kwz::snappy_go(p, n, dst, (uint32_t)need, &got);
     if (r == kwz::kKwzMore) return kKwDefer;
     if (r != kwz::kKwzOk) return kKwError;
-    atomicAdd(done, 1ull);
+    (void)wave_append(done, true);
     KwStream inner{dst, got, 0};
     return kw_message_set(&inner, (int32_t)got, version, *crc, DevDefer{});
   }
@@ -238,9 +254,9 @@ __device__ __forceinline__ void decode_one(const KafkaDictDev& dt, const KafkaDi
     t0 = (uint32_t)at;
     t1 = nt >= CG_KAFKA_TOPICS_IN_ARENA ? nt : 0;
   }
-  if (st == kKwDefer) {
-    const unsigned long long j = atomicAdd(defer_ctr, 1ull);
-    if (defer_list) defer_list[j] = (uint32_t)i;
+  {
+    const unsigned long long j = wave_append(defer_ctr, st == kKwDefer);
+    if (st == kKwDefer && defer_list) defer_list[j] = (uint32_t)i;
   }
   uint4 h;
   if (st == kKwOk) {
