@@ -19,6 +19,8 @@
 // batch needs is bounded by its bytes / 2.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include "kafka_wire.h"
@@ -32,7 +34,10 @@ constexpr uint32_t kKwThreads = 256;
 constexpr uint32_t kKwWaves = kKwThreads / 64;
 // per-wave LDS stage of the wave's 64 requests (bytes; 0 = none): requests
 // reaching past it read HBM directly
-constexpr uint32_t kKwStage = 4096;
+// (a template parameter of the kernel: 4, 8 or 16 KiB, CILIUM_GPU_KAFKA_STAGE_KB
+// for the A/B; 4 KiB by default — measured 2.65 / 2.43 / 2.09 G requests/s:
+// the occupancy a larger stage costs outweighs the HBM reads it saves,
+// profiles/r06ze_kafka_stage_ab.txt)
 // CRC-32 tables (slicing-by-kKwSlices, kKwSlices KiB of LDS per block)
 constexpr uint32_t kKwSlices = 8;
 
@@ -278,6 +283,7 @@ __device__ __forceinline__ void decode_one(const KafkaDictDev& dt, const KafkaDi
   status[i] = st;
 }
 
+template <uint32_t kKwStage>
 __global__ __launch_bounds__(kKwThreads) void kafka_decode_kernel(
     KafkaDictDev dt, KafkaDictDev dc, const uint8_t* __restrict__ raw, const uint64_t* __restrict__ off, size_t n,
     const uint16_t* __restrict__ redirect, const uint32_t* __restrict__ remote, uint4* __restrict__ recs,
@@ -394,9 +400,11 @@ int launch_kafka_decode(const KafkaDictDev& topics, const KafkaDictDev& clients,
   if (n == 0) return hipSuccess;
   const size_t need = (n + kKwThreads - 1) / kKwThreads;  // one 64-request group per wave
   const int grid = (int)std::min<size_t>(need, (size_t)std::max(cus, 1) * (4096 / kKwThreads));
-  hipLaunchKernelGGL(kafka_decode_kernel, dim3(grid), dim3(kKwThreads), 0, (hipStream_t)stream, topics, clients,
-                     raw, off, n, redirect, remote, (uint4*)recs, arena, (unsigned long long)arena_cap, ctr, status,
-                     defer_list);
+  const char* sk = getenv("CILIUM_GPU_KAFKA_STAGE_KB");
+  const int kb = sk ? atoi(sk) : 4;
+  auto k = kb == 8 ? kafka_decode_kernel<8192> : kb == 16 ? kafka_decode_kernel<16384> : kafka_decode_kernel<4096>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kKwThreads), 0, (hipStream_t)stream, topics, clients, raw, off, n, redirect,
+                     remote, (uint4*)recs, arena, (unsigned long long)arena_cap, ctr, status, defer_list);
   // the deferred requests (their count stays on the device: a small grid
   // that exits at once when there are none) — two workgroups per CU, the
   // inflater's occupancy (230 VGPRs: 2 waves per SIMD)
