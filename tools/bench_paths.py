@@ -221,6 +221,12 @@ def bench_kafka_wire(torch, dev, stream, cl, args, threads, codec_frac: float = 
     cl.update_kafka_policy(pols)
     D, reps = 65_536, 256
     pool, rq = kafka_wire_pool(D, info, codec_frac=codec_frac)
+    if os.environ.get("CILIUM_BENCH_KAFKA_SORTED"):
+        # the same requests grouped by (apiKey, version): what a wave decodes
+        # when its lanes take one code path (the divergence A/B)
+        order = np.lexsort((np.asarray(rq["api_version"]), np.asarray(rq["api_key"])))
+        pool = [pool[i] for i in order]
+        rq = {k: (v[order] if isinstance(v, np.ndarray) else [v[i] for i in order]) for k, v in rq.items()}
     if codec_frac:
         # copies per call within the 64 MiB per-call inflate arena (each
         # compressed set reserves its decoded size, at most its request's
