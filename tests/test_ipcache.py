@@ -197,6 +197,44 @@ def v4_chunk_kinds_case():
     return keys, np.array(vals, np.uint32), a4
 
 
+def exact_shadow_case():
+    """Full-length entries (the exact tables) against shorter prefixes around
+    them: a /32 or /128 with identity 0 shadows its covering prefix (WORLD),
+    a /32 beside a /31, the first and last addresses of a family, a /16
+    holding only /32s, and a v6 bucket whose only entries are /128s."""
+    ents = [("10.20.0.0/16", 700, 0), ("10.20.5.7/32", 0, 0), ("10.20.5.8/32", 701, 3),
+            ("10.20.5.9/31", 702, 0), ("10.20.5.10/32", 703, 0), ("0.0.0.0/32", 704, 0),
+            ("255.255.255.255/32", 705, 0), ("10.21.1.1/32", 706, 0), ("10.21.200.3/32", 707, 0),
+            ("fd10::/32", 800, 0), ("fd10::7/128", 0, 0), ("fd10::8/128", 801, 5), ("fd10::9/127", 802, 0),
+            ("::/128", 803, 0), ("ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff/128", 804, 0),
+            ("fd77:1:2:3::1/128", 805, 0), ("fd77:1:2:3::2/128", 806, 0)]
+    a4 = ["10.20.5.%d" % k for k in range(4, 14)] + ["0.0.0.0", "0.0.0.1", "255.255.255.255", "255.255.255.254",
+                                                    "10.21.1.1", "10.21.1.2", "10.21.200.3", "10.21.0.0"]
+    a6 = ["fd10::%x" % k for k in range(4, 14)] + ["::", "::1", "ffff:ffff:ffff:ffff:ffff:ffff:ffff:ffff",
+                                                 "fd77:1:2:3::1", "fd77:1:2:3::2", "fd77:1:2:3::3", "fd77:1:2::"]
+    keys = [c for c, _, _ in ents]
+    vals = np.array([[i, t] for _, i, t in ents], np.uint32)
+    v4 = np.array([int.from_bytes(ipaddress.ip_address(x).packed, "little") for x in a4], np.uint32)
+    v6 = np.array([list(ipaddress.ip_address(x).packed) for x in a6], np.uint8)
+    return keys, vals, v4, v6
+
+
+def _check_exact_shadow(cl, lookup):
+    from cilium_amd.classifier import IPCache
+    keys, vals, v4, v6 = exact_shadow_case()
+    ic = cl.ipcache()
+    ic.update(keys, vals)
+    g4, g6 = lookup(ic, v4, v6)
+    o4, o6 = oracle.ipcache(IPCache._keys(keys), vals, v4, v6)
+    assert np.array_equal(g4, o4) and np.array_equal(g6, o6)
+    assert o4[3].tolist() == [WORLD, 0] and o4[4].tolist() == [701, 3]  # 10.20.5.7 (identity 0), .8
+    assert o6[3].tolist() == [WORLD, 0] and o6[4].tolist() == [801, 5]
+
+
+def test_tables_exact_shadow(host):
+    _check_exact_shadow(host, lambda ic, a4, a6: ic.eval_host_diag(a4, a6))
+
+
 def _check_chunk_kinds(cl, lookup):
     from cilium_amd.classifier import IPCache
     keys, vals, a4 = v4_chunk_kinds_case()
@@ -272,6 +310,11 @@ def test_host_handle_refuses_resolve(host):
 
 
 # ------------------------------------------------------------------ GPU ----
+@pytest.mark.gpu
+def test_gpu_exact_shadow(gpu):
+    _check_exact_shadow(gpu, lambda ic, a4, a6: ic.resolve(a4, a6))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("encode", [False, True])
 def test_gpu_v4_chunk_kinds(gpu, monkeypatch, encode):
