@@ -51,8 +51,8 @@ def test_gpu_ring_calls():
         print(f"ring, 1 thread, batch 1 (Python ctypes): {1000 / dt:.0f} calls/s, {dt / 1000 * 1e6:.1f} us per call")
         # one launch serves a steady stream of calls (it leaves only when idle
         # 50 ms or 2 s old)
-        if dt < 1.5:
-            assert cl.http_ring_stats()["launches"] <= 2, cl.http_ring_stats()
+        if dt < 1.5:  # (a pause of the test process past 50 ms may cost one relaunch)
+            assert cl.http_ring_stats()["launches"] <= 3, cl.http_ring_stats()
         # batches of 16 and 256 (a slot's limit), and 300 (past it: the staged entry)
         for B in (16, 256, 300):
             for a in range(0, 1200, B):
