@@ -354,6 +354,7 @@ struct HttpRingDev {
   uint64_t life_ticks;    // hard bound on one launch's life
   uint32_t lds_cells;     // largest program block the kernel stages in LDS (0: none)
   uint32_t trace;         // write phase stamps into slot words 8..14 (CILIUM_GPU_RING_TRACE)
+  uint32_t echo;          // transport experiments (CILIUM_GPU_RING_ECHO): 1 done at once, 2 after the data; 0 serve
 };
 // phase stamps of a served call (low 32 bits of wall_clock64): polled,
 // data and list masks in LDS, program looked up / staged, request 0 parsed,

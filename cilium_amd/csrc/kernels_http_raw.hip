@@ -2108,11 +2108,16 @@ struct RingState {
   unsigned long long last, served;
 };
 
+// Polls are relaxed system-scope loads (straight to host memory, no cache
+// maintenance): an acquire at system scope invalidates the L2 (buffer_inv
+// sc0 sc1), and 64 polling waves doing that without pause capped the ring
+// at ~0.6 M round trips/s for the whole chip.  A slot seen ready is followed
+// by one acquire fence before its data is read.
 __device__ __forceinline__ uint32_t sys_load32(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ unsigned long long sys_load64(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The program block (and code map) of p into LDS by LDS-DMA: every 1 KiB
@@ -2293,6 +2298,11 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
   uint8_t* hs = G.slots + (size_t)s * kRingSlotBytes;
   // (atomic loads: vector memory, never a cached scalar read of host memory)
   uint32_t* hw = reinterpret_cast<uint32_t*>(hs);
+  if (G.echo == 1) {  // transport experiment: no work at all
+    if (lane == 0) __hip_atomic_store(hw + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slot's data after its doorbell
   uint32_t stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t cyc0 = 0;
   if (G.trace) {
@@ -2327,6 +2337,11 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
   ring_masks(blob, bytes, tct, masks, lane);
   wave_sync();
   if (G.trace) stamp[1] = (uint32_t)wall_clock64();
+  if (G.echo == 2) {  // transport experiment: the data in, no decision
+    wave_sync();
+    if (lane == 0) __hip_atomic_store(hw + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   for (uint32_t b = 0; b < n; b += kRingThreads) {  // uniform
     const uint32_t i = b + lane;
     const bool live = i < n;
@@ -2387,8 +2402,6 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
     }
   }
   if (G.trace) stamp[6] = (uint32_t)wall_clock64();
-  // the verdicts before `done` (every lane's stores, then one release)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   wave_sync();
   if (G.trace) {
     stamp[7] = (uint32_t)wall_clock64();
@@ -2405,10 +2418,14 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
       for (uint32_t j = 1; j < kRingStamps; ++j) x = lane == j ? stamp[j] : x;
       hw[kRingStampAt + lane] = x;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
+  // the verdicts (and the counters, stamps) before `done`: one release, then
+  // a relaxed store of the word (a release store would write the L2 back a
+  // second time)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  wave_sync();
   if (lane == 0)
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(hs) + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(hs) + 1, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool kLdsTabs>

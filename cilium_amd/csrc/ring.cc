@@ -93,11 +93,9 @@ void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
                 return a;
               }());
   }
-  claimed_.reset(new std::atomic<uint32_t>[slots]);
-  for (uint32_t i = 0; i < slots; ++i) claimed_[i].store(0);
+  slot_st_.reset(new SlotState[slots]);
   busy_.reset(new std::atomic<uint32_t>[workgroups]);
   for (uint32_t i = 0; i < workgroups; ++i) busy_[i].store(0);
-  seq_.assign(slots, 0);
   trace_ = getenv("CILIUM_GPU_RING_TRACE") != nullptr;
 }
 
@@ -149,6 +147,10 @@ void HttpRing::launch_locked(const std::shared_ptr<HttpSnapshot>& s) {
   const uint32_t room = base < 160 * 1024 ? (uint32_t)((160 * 1024 - base) / 4) : 0u;
   G.lds_cells = std::min(maxc, room);
   G.trace = trace_;
+  {
+    const char* ec = getenv("CILIUM_GPU_RING_ECHO");  // (measuring only: no verdicts are decided)
+    G.echo = ec ? (uint32_t)atoi(ec) : 0u;
+  }
   check_launch_rc(launch_http_ring(s->dev, s->raw, G, state_, stream_));
   s->fence.record(stream_);
   snap_ = s;
@@ -191,14 +193,16 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
   // program it staged in LDS, so calls of one listener find theirs there
   const uint32_t prog = n ? s->lookup_prog(pol[0], ing[0] != 0, port[0]) : 0u;
   const uint32_t home = (prog < s->progs.size() ? prog : prog * 0x9E3779B1u >> 7) % nwg_;
-  const uint32_t r = next_.fetch_add(1, std::memory_order_relaxed);
+  // a rotating start per calling thread (no counter shared by the callers)
+  thread_local uint32_t next = 0;
+  const uint32_t r = next++;
   uint32_t i = nslots_;
   auto try_wg = [&](uint32_t wg) {  // a free slot of workgroup wg (slots wg, wg + nwg, ...)
     const uint32_t mine = wg < nslots_ ? (nslots_ - wg + nwg_ - 1) / nwg_ : 0u;
     for (uint32_t k = 0; k < mine && i == nslots_; ++k) {
       const uint32_t c = wg + ((r + k) % mine) * nwg_;
       uint32_t z = 0;
-      if (claimed_[c].compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
+      if (slot_st_[c].claimed.compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
     }
   };
   // the home workgroup when no call is in it, else the nearest idle one (a
@@ -211,7 +215,7 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
   for (uint32_t k = 1; i == nslots_; ++k) {
     const uint32_t c = (r + k) % nslots_;
     uint32_t z = 0;
-    if (claimed_[c].compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
+    if (slot_st_[c].claimed.compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
     if (k % nslots_ == 0) std::this_thread::yield();
   }
   busy_[i % nwg_].fetch_add(1, std::memory_order_relaxed);
@@ -230,7 +234,8 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
   uint32_t* w = slot_words(i);
   w[2] = (uint32_t)n;
   w[3] = bytes;
-  const uint32_t seq = ++seq_[i] ? seq_[i] : ++seq_[i];  // never 0 (the slot's initial done)
+  uint32_t& sq = slot_st_[i].seq;
+  const uint32_t seq = ++sq ? sq : ++sq;  // never 0 (the slot's initial done)
   __atomic_store_n(&w[0], seq, __ATOMIC_RELEASE);         // the doorbell, after the slot's bytes
   const uint64_t t0 = now_ns();
   uint64_t checked = t0;
@@ -254,13 +259,14 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     }
     if (t - t0 > 5ull * 1000 * 1000 * 1000) {
       busy_[i % nwg_].fetch_sub(1, std::memory_order_relaxed);
-      claimed_[i].store(0, std::memory_order_release);
+      slot_st_[i].claimed.store(0, std::memory_order_release);
       fail(CG_UNKNOWN_ERROR, "ring: a call was not served within 5 s");
     }
   }
   memcpy(out, sl + kRingOut, n);
   const uint64_t t_done = now_ns();
-  last_ns_.store(t_done, std::memory_order_relaxed);
+  // (written at most once a millisecond: every caller reads it)
+  if (t_done - last_ns_.load(std::memory_order_relaxed) > 1000000) last_ns_.store(t_done, std::memory_order_relaxed);
   if (trace_) {  // device phases (10 ns ticks at 100 MHz) and the whole call
     uint32_t st[kRingStamps + 1];
     for (uint32_t j = 0; j <= kRingStamps; ++j) st[j] = __atomic_load_n(&w[kRingStampAt + j], __ATOMIC_ACQUIRE);
@@ -274,7 +280,7 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     ++trace_n_[c];
   }
   busy_[i % nwg_].fetch_sub(1, std::memory_order_relaxed);
-  claimed_[i].store(0, std::memory_order_release);
+  slot_st_[i].claimed.store(0, std::memory_order_release);
 }
 
 void HttpRing::stats(uint64_t* served, uint64_t* launches) {

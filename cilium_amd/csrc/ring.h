@@ -48,10 +48,14 @@ class HttpRing {
   std::atomic<bool> launched_{false};
   std::atomic<uint64_t> launch_ns_{0}, last_ns_{0};
   uint64_t launches_ = 0, served_before_ = 0;
-  std::unique_ptr<std::atomic<uint32_t>[]> claimed_;  // per slot: a call owns it
-  std::unique_ptr<std::atomic<uint32_t>[]> busy_;     // per workgroup: calls in its slots
-  std::vector<uint32_t> seq_;                          // per slot, under its claim
-  std::atomic<uint32_t> next_{0};
+  // per slot, a cache line of its own (callers on many cores claim slots
+  // side by side): the claim and the slot's last doorbell value
+  struct alignas(64) SlotState {
+    std::atomic<uint32_t> claimed{0};  // a call owns the slot
+    uint32_t seq = 0;                  // under the claim
+  };
+  std::unique_ptr<SlotState[]> slot_st_;
+  std::unique_ptr<std::atomic<uint32_t>[]> busy_;  // per workgroup: calls in its slots (packed: scanned)
   // CILIUM_GPU_RING_TRACE: per-phase device stamps summed over calls
   bool trace_ = false;
   std::mutex trace_mu_;
