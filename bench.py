@@ -54,6 +54,9 @@ def parse():
                          "on the device, no host round trip) or host (CILIUM_GPU_RAW_LAYOUT=host: the round-3 "
                          "sequence, bucket counts laid out on the host)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--prewarm-seconds", type=float, default=0.5,
+                    help="before the --warmup steps, run untimed steps back to back for this long, so the timed "
+                         "steps start at the clocks the sustained leg holds (0: skip)")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
                     help="after the timed steps, run steps back to back for this long and report the sustained "
                          "rate (0: skip)")
@@ -171,6 +174,8 @@ def main():
         if not check:
             raise SystemExit(f"verdicts differ from the oracle on {int((got != exp).sum())} of {D} requests")
 
+    if args.prewarm_seconds > 0:
+        run_for(step, args.prewarm_seconds, dist, dev, torch)
     for _ in range(args.warmup):
         step()
     if dist is not None:
@@ -237,6 +242,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm_seconds": args.prewarm_seconds,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
@@ -289,12 +295,10 @@ def max_over_ranks(sec: float, dist, dev, torch) -> float:
     return float(tt.item())
 
 
-def sustain(step, seconds: float, per_step: int, dist, dev, torch) -> dict:
-    """Steps back to back for `seconds` (the driver's timed region is ~30 ms
-    of launches): the sustained rate over the whole run and the mean of the
-    per-launch HIP events, so a clock drop past the short window would show
-    against the headline."""
-    kev, aev = [], []
+def run_for(step, seconds: float, dist, dev, torch, **kw) -> tuple:
+    """Steps back to back in bursts of 16 until `seconds` have passed on rank
+    0's clock (every rank runs the same number: a step may hold a
+    collective).  Returns (steps, wall seconds, max over ranks)."""
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -302,16 +306,24 @@ def sustain(step, seconds: float, per_step: int, dist, dev, torch) -> dict:
     n = 0
     while True:
         for _ in range(16):
-            step(timed=True, kev=kev, aev=aev)
+            step(**kw)
         n += 16
         torch.cuda.synchronize()
-        # every rank runs the same number of steps: rank 0's clock decides
         done = torch.tensor([time.perf_counter() - t0 >= seconds], dtype=torch.int32, device=dev)
         if dist is not None:
             dist.broadcast(done, 0)
         if int(done.item()):
             break
-    wall = max_over_ranks(time.perf_counter() - t0, dist, dev, torch)
+    return n, max_over_ranks(time.perf_counter() - t0, dist, dev, torch)
+
+
+def sustain(step, seconds: float, per_step: int, dist, dev, torch) -> dict:
+    """Steps back to back for `seconds` (the driver's timed region is ~30 ms
+    of launches): the sustained rate over the whole run and the mean of the
+    per-launch HIP events, so a clock drop past the short window would show
+    against the headline."""
+    kev, aev = [], []
+    n, wall = run_for(step, seconds, dist, dev, torch, timed=True, kev=kev, aev=aev)
     ms = [a.elapsed_time(z) for a, z in kev]
     return {"seconds": wall, "steps": n, "value": per_step * n / wall, "unit": "verdicts/s",
             "kernel_ms_mean": float(np.mean(ms)), "kernel_ms_first16": float(np.mean(ms[:16])),
