@@ -179,6 +179,19 @@ VARIANTS.update({
                       "    const RawSlot sl = raw_slot(L, want, raw_vkey(L, group_of(R, prog) * kRawUnits + units, blockIdx.x), prog);",
                       "    const uint32_t tfake = (uint32_t)((i >> 6) % L.maxchunks);\n"
                       "    const RawSlot sl{L.tiles + (size_t)tfake * (kRawTileGran * 512), tfake, (uint32_t)(i & 63), want};")],
+    # the device-layout scan's string units stored nontemporal (verdicts
+    # valid), and as a measuring device without the unit stores (the units'
+    # bytes still gathered; verdicts meaningless, memory-safe)
+    "rawdl_ntunits": [("raw_emit.h", "    *dst = kCode ? make_uint4(code4(lut, w0), code4(lut, w1), code4(lut, w2), code4(lut, w3)) : make_uint4(w0, w1, w2, w3);",
+                       "    { typedef unsigned int v4u __attribute__((ext_vector_type(4))); __builtin_nontemporal_store(v4u{w0, w1, w2, w3}, reinterpret_cast<v4u*>(dst)); }"),
+                      ("raw_emit.h", "    *dst = make_uint4(keep(c(w0), 0), keep(c(w1), 4), keep(c(w2), 8), keep(c(w3), 12));",
+                       "    { typedef unsigned int v4u __attribute__((ext_vector_type(4))); __builtin_nontemporal_store(v4u{keep(c(w0), 0), keep(c(w1), 4), keep(c(w2), 8), keep(c(w3), 12)}, reinterpret_cast<v4u*>(dst)); }"),
+                      ("kernels_http_raw.hip", "#include <hip/hip_runtime.h>", "#include <hip/hip_runtime.h>")],
+    "rawdl_nounitst": [("raw_emit.h", "    *dst = kCode ? make_uint4(code4(lut, w0), code4(lut, w1), code4(lut, w2), code4(lut, w3)) : make_uint4(w0, w1, w2, w3);",
+                        "    asm volatile(\"\" ::\"v\"(w0), \"v\"(w1), \"v\"(w2), \"v\"(w3));"),
+                       ("raw_emit.h", "    *dst = make_uint4(keep(c(w0), 0), keep(c(w1), 4), keep(c(w2), 8), keep(c(w3), 12));",
+                        "    asm volatile(\"\" ::\"v\"(keep(c(w0), 0)), \"v\"(keep(c(w1), 4)), \"v\"(keep(c(w2), 8)), \"v\"(keep(c(w3), 12)));"),
+                       ("kernels_http_raw.hip", "#include <hip/hip_runtime.h>", "#include <hip/hip_runtime.h>")],
     # a wave issuing its tile's loads (window + next tile's head) at raised
     # priority, so the loads leave before other waves' walk steps
     "h_prio": [("  const uint2 meta = cur.meta;\n", "  __builtin_amdgcn_s_setprio(3);\n  const uint2 meta = cur.meta;\n"),
