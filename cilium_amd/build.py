@@ -58,7 +58,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(LIB),
-               "-lpthread", "-lz"]
+               "-lpthread", "-lz", "-lhsa-runtime64"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -313,12 +313,16 @@ CG_HD inline uint32_t raw_name_hash(uint32_t nl, uint32_t lo0, uint32_t lo1, uin
 CG_HD inline uint32_t raw_fnv(uint32_t h, uint8_t c) { return (h ^ c) * 16777619u; }
 constexpr uint32_t kRawFnvInit = 2166136261u;
 // ---- the persistent verdict ring (cg_http_ring_*, ring.cc): Envoy-sized
-// calls of header lists decided by a resident kernel that polls slots in
-// fine-grained pinned host memory — no launch, no copies, no stream
-// synchronization per call.  A slot holds one call: a 64-byte header
-// {seq (the host's doorbell), done (the device's completion word), n, bytes},
-// the per-request inputs, list offsets relative to the slot's blob, the
-// verdicts and the blob.
+// calls of header lists decided by a resident kernel that polls request
+// slots — no launch, no copies, no stream synchronization per call.  A
+// request slot holds one call: a 64-byte header {seq (the host's doorbell),
+// served (the last seq the device answered), n, bytes}, the per-request
+// inputs, list offsets relative to the slot's blob and the blob.  The request
+// slots live in fine-grained DEVICE memory the host writes through its
+// mapping (the kernel polls and reads them locally; the host's writes are
+// posted), the reply slots {done word 1, phase stamps, verdicts at kRingOut}
+// in pinned host memory the host polls; CILIUM_GPU_RING_SLOTS=host keeps both
+// in one pinned host slot (reply == request).
 constexpr uint32_t kRingReqs = 256;          // requests per slot (larger calls take the staged path)
 constexpr uint32_t kRingBlob = 32 * 1024;    // list bytes per slot
 // A slot: [header: 64 B][verdicts: kRingReqs B][data], the data packed for
@@ -346,8 +350,12 @@ static_assert(kRingData % 16 == 0, "the data is copied in 16-byte units");
 // (the device only reads host memory with loads and writes it with plain
 // stores: no read-modify-write over the bus)
 constexpr uint32_t kRingStop = 0, kRingCtlBytes = 256;
+constexpr size_t kRingReplyBytes = 512;       // [header: 64 B (done: word 1, stamps)][verdicts]
+static_assert(kRingOut + kRingReqs <= kRingReplyBytes, "reply slot");
 struct HttpRingDev {
-  uint8_t* slots;         // device view of the host slots (hipHostGetDevicePointer)
+  uint8_t* slots;         // request slots (device memory, or the device view of host slots), kRingSlotBytes apart
+  uint8_t* reply;         // reply slots (device view of pinned host memory), reply_stride apart
+  uint32_t reply_stride;  // kRingReplyBytes, or kRingSlotBytes when reply == slots
   uint32_t* ctl;          // device view of the control words
   uint32_t nslots, nwg;   // slot s is served by workgroup s % nwg
   uint64_t idle_ticks;    // wall-clock ticks without a call before the kernel exits

@@ -2295,11 +2295,16 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
                                            uint32_t s, uint32_t seq, lds_u8* in, lds_u32* sp, lds_u32* cells,
                                            lds_u32* cmap, lds_u32* masks, const lds_u8* tct, uint32_t& staged,
                                            HttpProg& spg, HttpPart& spt, uint32_t lane) {
-  uint8_t* hs = G.slots + (size_t)s * kRingSlotBytes;
-  // (atomic loads: vector memory, never a cached scalar read of host memory)
+  uint8_t* hs = G.slots + (size_t)s * kRingSlotBytes;     // the request
+  uint8_t* ho = G.reply + (size_t)s * G.reply_stride;      // the reply (host memory)
+  // (atomic loads: vector memory, never a cached scalar read of the slot)
   uint32_t* hw = reinterpret_cast<uint32_t*>(hs);
+  uint32_t* ow = reinterpret_cast<uint32_t*>(ho);
+  // the answered seq in the request slot (what the poll compares the
+  // doorbell with; the same word as `done` when the slots are one)
+  if (ho != hs && lane == 0) __hip_atomic_store(hw + 1, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (G.echo == 1) {  // transport experiment: no work at all
-    if (lane == 0) __hip_atomic_store(hw + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(ow + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slot's data after its doorbell
@@ -2339,7 +2344,7 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
   if (G.trace) stamp[1] = (uint32_t)wall_clock64();
   if (G.echo == 2) {  // transport experiment: the data in, no decision
     wave_sync();
-    if (lane == 0) __hip_atomic_store(hw + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(ow + 1, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   for (uint32_t b = 0; b < n; b += kRingThreads) {  // uniform
@@ -2398,7 +2403,7 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
           if (v) atomicAdd(&HT.rule_hits[pg.rule_base + hit], 1ull);
         }
       }
-      hs[kRingOut + i] = (uint8_t)v;
+      ho[kRingOut + i] = (uint8_t)v;
     }
   }
   if (G.trace) stamp[6] = (uint32_t)wall_clock64();
@@ -2416,7 +2421,7 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
     if (lane <= kRingStamps) {
       uint32_t x = lane == kRingStamps ? cyc : stamp[0];
       for (uint32_t j = 1; j < kRingStamps; ++j) x = lane == j ? stamp[j] : x;
-      hw[kRingStampAt + lane] = x;
+      ow[kRingStampAt + lane] = x;
     }
   }
   // the verdicts (and the counters, stamps) before `done`: one release, then
@@ -2424,8 +2429,7 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
   // second time)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   wave_sync();
-  if (lane == 0)
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(hs) + 1, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) __hip_atomic_store(ow + 1, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool kLdsTabs>

@@ -4,10 +4,13 @@
 // (envoy/cilium_l7policy.cc:127-182), from many worker threads.  Through
 // cg_http_verdicts_fields_host such a call pays a staged copy in, a launch, a
 // copy out and a stream synchronization (~30 us).  The ring removes all four:
-// a resident kernel (kernels_http_raw.hip http_ring_kernel) polls slots in
-// fine-grained pinned host memory; a call claims a slot, writes its header
-// lists and inputs there, stores the slot's doorbell and spins on the
-// completion word the kernel stores after the verdicts.
+// a resident kernel (kernels_http_raw.hip http_ring_kernel) polls request
+// slots; a call claims a slot, writes its header lists and inputs there,
+// stores the slot's doorbell and spins on the completion word the kernel
+// stores after the verdicts.  The request slots are fine-grained device
+// memory the host writes through its mapping (posted writes; the kernel
+// polls and reads them without crossing the bus), the replies pinned host
+// memory the host polls (dev_types.h kRingReplyBytes).
 //
 // Lifetime: the kernel runs with the tables of one HTTP snapshot (held here,
 // so they outlive it).  A call first makes sure a launch with the handle's
@@ -21,6 +24,8 @@
 // device list parser does not take (more than 32 header fields) are decided
 // by cg_http_verdicts_fields_host instead.
 #include <hip/hip_runtime_api.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -28,6 +33,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <vector>
 
 #include "engine.h"
 #include "http.h"
@@ -48,12 +54,46 @@ uint64_t now_ns() {
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 
+// Fine-grained device memory the host can store to (the same virtual address
+// on both sides), or nullptr: hipExtMallocWithFlags(hipDeviceMallocFinegrained)
+// and the CPU agents let in (hsa_amd_agents_allow_access), checked with one
+// store and load from the host.
+uint8_t* device_slots_for_host(size_t bytes) {
+  uint8_t* d = nullptr;
+  if (hipExtMallocWithFlags((void**)&d, bytes, hipDeviceMallocFinegrained) != hipSuccess) return nullptr;
+  std::vector<hsa_agent_t> cpus;
+  (void)hsa_iterate_agents(
+      [](hsa_agent_t ag, void* out) {
+        hsa_device_type_t t;
+        if (hsa_agent_get_info(ag, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU)
+          static_cast<std::vector<hsa_agent_t>*>(out)->push_back(ag);
+        return HSA_STATUS_SUCCESS;
+      },
+      &cpus);
+  hsa_amd_pointer_info_t pi{};
+  pi.size = sizeof(pi);
+  if (cpus.empty() || hsa_amd_agents_allow_access((uint32_t)cpus.size(), cpus.data(), nullptr, d) != HSA_STATUS_SUCCESS ||
+      hsa_amd_pointer_info(d, &pi, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS || pi.hostBaseAddress != d) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  volatile uint32_t* w = reinterpret_cast<volatile uint32_t*>(d);
+  *w = 0x5A5A5A5Au;
+  __builtin_ia32_mfence();
+  if (*w != 0x5A5A5A5Au) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  return d;
+}
+
 }  // namespace
 
 HttpRing::~HttpRing() {
   stop_locked_noexcept();
   if (state_) (void)hipFree(state_);
   if (host_) (void)hipHostFree(host_);
+  if (req_in_device_ && req_) (void)hipFree(req_);
   if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
 }
 
@@ -65,10 +105,26 @@ void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
   nwg_ = workgroups;
   nslots_ = slots;
   hip_check(hipStreamCreateWithFlags((hipStream_t*)&stream_, hipStreamNonBlocking), "hipStreamCreate");
-  const size_t bytes = kRingCtlBytes + (size_t)slots * kRingSlotBytes;
+  {
+    const char* w = getenv("CILIUM_GPU_RING_SLOTS");
+    if (!(w && !strcmp(w, "host"))) req_ = device_slots_for_host((size_t)slots * kRingSlotBytes);
+    req_in_device_ = req_ != nullptr;
+  }
+  rep_stride_ = req_in_device_ ? kRingReplyBytes : kRingSlotBytes;
+  const size_t bytes = kRingCtlBytes + (size_t)slots * rep_stride_;
   hip_check(hipHostMalloc((void**)&host_, bytes, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
   memset(host_, 0, bytes);
   hip_check(hipHostGetDevicePointer((void**)&dev_view_, host_, 0), "hipHostGetDevicePointer");
+  rep_ = host_ + kRingCtlBytes;
+  rep_dev_ = dev_view_ + kRingCtlBytes;
+  if (req_in_device_) {
+    hip_check(hipMemset(req_, 0, (size_t)slots * kRingSlotBytes), "hipMemset");
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    req_dev_ = req_;
+  } else {
+    req_ = rep_;
+    req_dev_ = rep_dev_;
+  }
   hip_check(hipMalloc(&state_, http_ring_state_bytes()), "hipMalloc");
   // the rate of the kernel's wall_clock64(), measured (two reads 20 ms apart)
   // rather than taken from hipDeviceAttributeWallClockRate
@@ -97,10 +153,9 @@ void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
   busy_.reset(new std::atomic<uint32_t>[workgroups]);
   for (uint32_t i = 0; i < workgroups; ++i) busy_[i].store(0);
   trace_ = getenv("CILIUM_GPU_RING_TRACE") != nullptr;
-}
-
-uint32_t* HttpRing::slot_words(uint32_t i) const {
-  return reinterpret_cast<uint32_t*>(host_ + kRingCtlBytes + (size_t)i * kRingSlotBytes);
+  if (e.debug || getenv("CILIUM_GPU_DEBUG"))
+    fprintf(stderr, "[cilium-gpu] ring: %u workgroups, %u slots, request slots in %s memory\n", nwg_, nslots_,
+            req_in_device_ ? "device" : "host");
 }
 
 bool HttpRing::stream_idle() const { return hipStreamQuery((hipStream_t)stream_) == hipSuccess; }
@@ -133,7 +188,9 @@ void HttpRing::launch_locked(const std::shared_ptr<HttpSnapshot>& s) {
   }
   hip_check(hipMemsetAsync(state_, 0, http_ring_state_bytes(), (hipStream_t)stream_), "hipMemsetAsync");
   HttpRingDev G{};
-  G.slots = dev_view_ + kRingCtlBytes;
+  G.slots = req_dev_;
+  G.reply = rep_dev_;
+  G.reply_stride = (uint32_t)rep_stride_;
   G.ctl = reinterpret_cast<uint32_t*>(dev_view_);
   G.nslots = nslots_;
   G.nwg = nwg_;
@@ -219,7 +276,8 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     if (k % nslots_ == 0) std::this_thread::yield();
   }
   busy_[i % nwg_].fetch_add(1, std::memory_order_relaxed);
-  uint8_t* sl = host_ + kRingCtlBytes + (size_t)i * kRingSlotBytes;
+  uint8_t* sl = req_slot(i);
+  uint8_t* rp = rep_slot(i);
   uint8_t* d = sl + kRingData;
   const RingLayout L = ring_layout((uint32_t)n);
   const uint64_t a0 = off[0];
@@ -231,15 +289,21 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
   uint32_t* o = reinterpret_cast<uint32_t*>(d + L.off);
   for (size_t k = 0; k <= n; ++k) o[k] = (uint32_t)(off[k] - a0);
   if (bytes) memcpy(d + L.blob, blob + a0, bytes);
-  uint32_t* w = slot_words(i);
+  uint32_t* w = reinterpret_cast<uint32_t*>(sl);   // request header
+  uint32_t* rw = reinterpret_cast<uint32_t*>(rp);  // reply header: done, stamps
   w[2] = (uint32_t)n;
   w[3] = bytes;
   uint32_t& sq = slot_st_[i].seq;
   const uint32_t seq = ++sq ? sq : ++sq;  // never 0 (the slot's initial done)
-  __atomic_store_n(&w[0], seq, __ATOMIC_RELEASE);         // the doorbell, after the slot's bytes
+  // the doorbell after the slot's bytes: stores to device memory through the
+  // mapping may be write-combined, which a release store does not order —
+  // fence them, store, and fence again so the doorbell leaves at once
+  __builtin_ia32_sfence();
+  __atomic_store_n(&w[0], seq, __ATOMIC_RELEASE);
+  __builtin_ia32_sfence();
   const uint64_t t0 = now_ns();
   uint64_t checked = t0;
-  while (__atomic_load_n(&w[1], __ATOMIC_ACQUIRE) != seq) {
+  while (__atomic_load_n(&rw[1], __ATOMIC_ACQUIRE) != seq) {
     cpu_relax();
     const uint64_t t = now_ns();
     // past the device's usual time, spin yielding the core: callers on every
@@ -251,7 +315,7 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     // between ensure() and the doorbell — relaunch, the slot is still ready
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (__atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == seq) break;
+      if (__atomic_load_n(&rw[1], __ATOMIC_ACQUIRE) == seq) break;
       if (stream_idle()) {
         launched_ = false;
         launch_locked(snap_ ? snap_ : s);
@@ -263,13 +327,13 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
       fail(CG_UNKNOWN_ERROR, "ring: a call was not served within 5 s");
     }
   }
-  memcpy(out, sl + kRingOut, n);
+  memcpy(out, rp + kRingOut, n);
   const uint64_t t_done = now_ns();
   // (written at most once a millisecond: every caller reads it)
   if (t_done - last_ns_.load(std::memory_order_relaxed) > 1000000) last_ns_.store(t_done, std::memory_order_relaxed);
   if (trace_) {  // device phases (10 ns ticks at 100 MHz) and the whole call
     uint32_t st[kRingStamps + 1];
-    for (uint32_t j = 0; j <= kRingStamps; ++j) st[j] = __atomic_load_n(&w[kRingStampAt + j], __ATOMIC_ACQUIRE);
+    for (uint32_t j = 0; j <= kRingStamps; ++j) st[j] = __atomic_load_n(&rw[kRingStampAt + j], __ATOMIC_ACQUIRE);
     std::lock_guard<std::mutex> lk(trace_mu_);
     const double ns_per_tick = 1e6 / (double)clock_khz_;
     const int c = n == 1 ? 0 : n <= 16 ? 1 : 2;

@@ -32,13 +32,21 @@ class HttpRing {
   void stop_locked();
   void stop_locked_noexcept();
   bool stream_idle() const;
-  uint32_t* slot_words(uint32_t i) const;
+  uint8_t* req_slot(uint32_t i) const { return req_ + (size_t)i * kRingSlotBytes; }
+  uint8_t* rep_slot(uint32_t i) const { return rep_ + (size_t)i * rep_stride_; }
   static void check_launch_rc(int rc);
 
   int device_ = 0;
   uint32_t nwg_ = 0, nslots_ = 0;
-  uint8_t* host_ = nullptr;      // control words + slots (hipHostMalloc, coherent, mapped)
+  uint8_t* host_ = nullptr;      // control words + reply slots (hipHostMalloc, coherent, mapped)
   uint8_t* dev_view_ = nullptr;  // the same memory as the device addresses it
+  uint8_t* req_ = nullptr;       // request slots: fine-grained device memory the host writes through its mapping
+                                 // (one address for both), or inside host_ (CILIUM_GPU_RING_SLOTS=host)
+  uint8_t* req_dev_ = nullptr;   // the request slots as the device addresses them
+  uint8_t* rep_ = nullptr;       // reply slots (host_), rep_stride_ apart
+  uint8_t* rep_dev_ = nullptr;
+  size_t rep_stride_ = 0;
+  bool req_in_device_ = false;
   void* state_ = nullptr;        // the launch's RingState (device memory)
   void* stream_ = nullptr;       // hipStream_t of the launches
   uint64_t clock_khz_ = 100000;  // wall clock of the device (hipDeviceAttributeWallClockRate)

@@ -1,7 +1,8 @@
 """The persistent verdict ring (cg_http_ring_*, csrc/ring.cc + kernels_http_raw.hip
 http_ring_kernel): Envoy-sized calls (AccessFilter::decodeHeaders decides one
 request, envoy/cilium_l7policy.cc:127-182) decided by a resident kernel that
-polls request slots in pinned host memory.  Verdicts against the oracle and
+polls request slots in fine-grained device memory the host writes through its
+mapping (or, CILIUM_GPU_RING_SLOTS=host, in pinned host memory).  Verdicts against the oracle and
 the staged entry; calls from many threads; a policy update between calls;
 the kernel's idle exit and relaunch; calls past a slot; open / close.  The
 test prints throughput and asserts no timing."""
@@ -32,7 +33,12 @@ def _pool(n, seed):
 
 
 @pytest.mark.gpu
-def test_gpu_ring_calls():
+@pytest.mark.parametrize("slots", ["device", "host"])
+def test_gpu_ring_calls(slots, monkeypatch):
+    if slots == "host":
+        monkeypatch.setenv("CILIUM_GPU_RING_SLOTS", "host")
+    else:
+        monkeypatch.delenv("CILIUM_GPU_RING_SLOTS", raising=False)
     cl = Classifier(device=0)
     try:
         pols, lists, args = _pool(4096, 71)

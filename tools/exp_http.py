@@ -265,7 +265,7 @@ def build_variant(name, subs):
     others = [B.BUILD / (s + ".o") for s in B.SOURCES if s not in files]
     lib = OUT / f"lib_{name}.so"
     subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *map(str, others), *map(str, objs),
-                    "-o", str(lib), "-lpthread", "-lz"], check=True)
+                    "-o", str(lib), "-lpthread", "-lz", "-lhsa-runtime64"], check=True)
     print("built", lib)
 
 
