@@ -363,6 +363,7 @@ struct HttpRingDev {
   uint32_t lds_cells;     // largest program block the kernel stages in LDS (0: none)
   uint32_t trace;         // write phase stamps into slot words 8..14 (CILIUM_GPU_RING_TRACE)
   uint32_t echo;          // transport experiments (CILIUM_GPU_RING_ECHO): 1 done at once, 2 after the data; 0 serve
+  uint32_t lds_tabs;      // the list parser's lookup tables staged in LDS (ring_lds_bytes)
 };
 // phase stamps of a served call (low 32 bits of wall_clock64): polled,
 // data and list masks in LDS, program looked up / staged, request 0 parsed,

@@ -92,7 +92,10 @@ int launch_http_raw_walk(const HttpDev& T, const HttpRawDev& R, bool lists, cons
 // The persistent verdict ring (ring.cc): nwg one-wave workgroups serving
 // the slots of G until its stop word, idle_ticks without a call or
 // life_ticks; `state` is http_ring_state_bytes() of zeroed device memory.
-size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells);
+// LDS of the ring kernel: `cells` of program block, the list parser's tables
+// when `tabs`; ring_tables_small: tables small enough to stage always
+size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells, bool tabs);
+bool ring_tables_small(const HttpRawDev& R);
 size_t http_ring_state_bytes();
 int launch_http_ring(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream);
 // the device's wall_clock64() into *d_out (ring.cc measures its rate)

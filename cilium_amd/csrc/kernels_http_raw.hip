@@ -822,6 +822,97 @@ __device__ __forceinline__ bool parse_list_win(const HttpRawDev& R, const Tabs& 
   return ok;
 }
 
+// parse_list_win's result for ONE list [hs, he) computed by the whole wave
+// (the ring's single-request calls, which would otherwise parse on one lane
+// while 63 wait).  The pairs follow from the NULs alone: pair j's name ends
+// at NUL 2j, its value [NUL 2j + 1, NUL 2j + 1) — the value's first stop byte
+// is either a byte the codec rejects or that NUL, so the list is malformed
+// iff a stop that is not a NUL lies where an odd number of NULs precede it.
+// Lanes take the mask words: NUL counts scanned over the wave, their
+// positions ranked into scr, the odd-parity regions by a prefix XOR of each
+// word; then lane j decides pair j, the first pair of each field wins (by
+// ballot, lowest lane first) and the spans go to sp0 (request 0's column).
+// Returns false, having written nothing, when the list holds more than 127
+// NULs (64+ pairs): the caller parses it on one lane.
+constexpr uint32_t kCoopNuls = 127;
+// (the ring's NUL ranks go after a single-request call's bytes in its data area)
+static_assert(64 + kRingBlob + 16 + 4 * kCoopNuls <= kRingDataMax, "ring scratch for parse_list_coop");
+template <class Tabs>
+__device__ __forceinline__ bool parse_list_coop(const HttpRawDev& R, const Tabs& T, const lds_u8* st,
+                                                const lds_u32* mstop, const lds_u32* mzero, uint32_t hs, uint32_t he,
+                                                lds_u32* sp0, uint32_t stride, lds_u32* scr, uint32_t lane, Parsed& P,
+                                                bool& ok) {
+  const uint32_t w_lo = hs >> 5, w_end = he > hs ? ((he - 1) >> 5) + 1 : w_lo;
+  uint32_t m = 0;       // NULs so far (wave-uniform)
+  bool bad = false;     // a rejected byte inside a value (this lane's words)
+  for (uint32_t w0 = w_lo; w0 < w_end; w0 += 64) {  // uniform
+    const uint32_t w = w0 + lane;
+    uint32_t z = 0, b = 0;
+    if (w < w_end) {
+      uint32_t keep = 0xFFFFFFFFu;
+      if (w == w_lo) keep &= 0xFFFFFFFFu << (hs & 31);
+      if (w == (he - 1) >> 5 && (he & 31)) keep &= (1u << (he & 31)) - 1u;
+      z = mzero[w] & keep;
+      b = mstop[w] & ~mzero[w] & keep;
+    }
+    // exclusive prefix of the NUL counts over the lanes
+    const uint32_t c = (uint32_t)__popc(z);
+    uint32_t inc = c;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    const uint32_t r0 = m + inc - c;
+    m += (uint32_t)__shfl((int)inc, 63, 64);
+    if (m > kCoopNuls) return false;  // uniform
+    // odd-parity positions: NULs before them in the word (exclusive prefix
+    // XOR of z) plus the parity carried in
+    uint32_t px = z;
+    px ^= px << 1;
+    px ^= px << 2;
+    px ^= px << 4;
+    px ^= px << 8;
+    px ^= px << 16;
+    const uint32_t inside = (px ^ z) ^ ((r0 & 1u) ? 0xFFFFFFFFu : 0u);
+    bad |= (b & inside) != 0;
+    for (uint32_t r = r0; z; z &= z - 1, ++r) scr[r] = 32 * w + (uint32_t)__builtin_ctz(z);
+  }
+  ok = !__ballot(bad);
+  wave_sync();  // the NUL positions
+  // pair j: name [k, ne), value [v, e)
+  const uint32_t j = lane;
+  const bool has = j == 0 ? hs < he : (2 * j - 1 < m && scr[2 * j - 1] + 1 < he);
+  int f = -1;
+  uint32_t span = 0;
+  if (has) {
+    const uint32_t k = j ? scr[2 * j - 1] + 1 : hs;
+    const uint32_t ne = 2 * j < m ? scr[2 * j] : he, nl = ne - k;
+    const uint32_t v = ne < he ? ne + 1 : he;
+    const uint32_t e = 2 * j + 1 < m ? scr[2 * j + 1] : he;
+    f = R.f_empty;
+    if (nl) {
+      const uint32_t lo0 = lower4(keep_bytes(squad(st, k), nl));
+      const uint32_t lo1 = nl > 4 ? lower4(keep_bytes(squad(st, k + 4), nl - 4)) : 0u;
+      const uint32_t hi0 = nl > 8 ? lower4(squad(st, k + nl - 8)) : 0u, hi1 = nl > 8 ? lower4(squad(st, k + nl - 4)) : 0u;
+      f = field_of_words(R, T, st, k, nl, lo0, lo1, hi0, hi1);
+    }
+    span = (v - hs) << 16 | (e - v);
+  }
+  // the first pair of each field wins: per field, the lowest lane naming it
+  P.present = P.vsum = 0;
+  for (unsigned long long left = __ballot(has && f >= 0); left;) {  // uniform
+    const uint32_t l = (uint32_t)__builtin_ctzll(left);
+    const int fl = __shfl(f, (int)l, 64);
+    const uint32_t sl = (uint32_t)__shfl((int)span, (int)l, 64);
+    left &= ~__ballot(has && f == fl);
+    if (lane == 0) sp0[(uint32_t)fl * stride] = sl;
+    P.present |= 1u << fl;
+    P.vsum += sl & 0xFFFFu;
+  }
+  wave_sync();  // request 0's spans for lane 0
+  return true;
+}
+
 // A list outside the stage, byte by byte.
 template <class Tabs>
 __device__ __forceinline__ bool parse_list_bytes(const HttpRawDev& R, const Tabs& T, HeadReader& hr, lds_u32* sp,
@@ -2205,19 +2296,20 @@ __device__ __forceinline__ uint32_t ring_run(const HttpRawDev& R, CellP cells, u
       st = st == dead ? st : ring_step<kCls>(cells, dead, st, c_sep);
     }
     const uint32_t sv = sp[g * kRingThreads], a = hs + (sv >> 16), L = sv & 0xFFFFu;
-    uint32_t w = squad(blob, a);
-    for (uint32_t k = 0; k < L && st != dead; k += 4) {
+    uint32_t w = squad(blob, a), k = 0;
+    // whole quads unguarded (the dead state is absorbing: a step from it
+    // stays there, as http_kernel's unguarded unit walk relies on), then the
+    // last 1-3 bytes
+    for (; k + 4 <= L && st != dead; k += 4) {
       const uint32_t wn = squad(blob, a + k + 4);  // (past the value: unused)
       uint32_t x[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) x[j] = lut[(w >> (8 * j)) & 0xFFu];
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t nx = ring_step<kCls>(cells, dead, st, x[j]);
-        st = k + j < L && st != dead ? nx : st;
-      }
+      for (uint32_t j = 0; j < 4; ++j) st = ring_step<kCls>(cells, dead, st, x[j]);
       w = wn;
     }
+    for (uint32_t j = 0; k + j < L && st != dead; ++j) st = ring_step<kCls>(cells, dead, st, (uint32_t)lut[(w >> (8 * j)) & 0xFFu]);
     st = st == dead ? st : ring_step<kCls>(cells, dead, st, c_sep);
     f = g + 1;
   }
@@ -2356,8 +2448,11 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
     const bool same = !__ballot(live && prog != p0);
     bool lds = false;
     if (same && p0 < R.nprogs) {
-      // the staged program's record and first part stay in registers
-      const HttpProg pg = staged == p0 ? spg : HT.progs[p0];
+      // the staged program's record and first part stay in registers (a
+      // copy and a uniform branch: `c ? spg : HT.progs[p0]` selects between
+      // two addresses, which put spg in scratch and cost a flat load per call)
+      HttpProg pg = spg;
+      if (staged != p0) pg = HT.progs[p0];
       lds = !(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased) && pg.cell_count <= G.lds_cells;
       if (lds && staged != p0) {
         wave_sync();
@@ -2369,23 +2464,35 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
       }
     }
     if (G.trace && b == 0) stamp[2] = (uint32_t)wall_clock64();
+    // a single-request call: its list parsed by the whole wave
+    Parsed P0{};
+    bool ok0 = false, coop = false;
+    if (n == 1 && !R.raw_values) {  // uniform
+      const uint32_t a0 = min(off[0], bytes), e0 = min(max(off[1], a0), bytes);
+      if (p0 != kProgDeny && e0 - a0 <= kFieldsMaxList)
+        coop = parse_list_coop(R, T, blob, masks, masks + kRingMaskWords, a0, e0, sp - lane, kRingThreads,
+                               (lds_u32*)(in + total), lane, P0, ok0);
+    }
     uint32_t v = 0;
     if (live) {
       const uint32_t a = min(off[i], bytes), e = min(max(off[i + 1], a), bytes);
       // the list over the call's masks (parse_list_fast), then decide_request
       // with the walk over the emitted string
-      Parsed P;
-      const bool ok = prog != kProgDeny && e - a <= kFieldsMaxList &&
-                      (R.raw_values
-                           ? parse_list_fast(R, T, blob, masks, masks + kRingMaskWords, a, e, sp, kRingThreads, P)
-                           : parse_list_win(R, T, blob, masks, masks + kRingMaskWords, a, e, sp, kRingThreads, P));
+      Parsed P = P0;
+      const bool ok = coop ? ok0
+                           : prog != kProgDeny && e - a <= kFieldsMaxList &&
+                                 (R.raw_values ? parse_list_fast(R, T, blob, masks, masks + kRingMaskWords, a, e, sp,
+                                                                 kRingThreads, P)
+                                               : parse_list_win(R, T, blob, masks, masks + kRingMaskWords, a, e, sp,
+                                                                kRingThreads, P));
       if (G.trace && i == 0) stamp[4] = stamp[5] = (uint32_t)wall_clock64();
       const uint32_t* blk = lds ? (const uint32_t*)cells : nullptr;
       const uint8_t* lut = lds ? (const uint8_t*)cmap : nullptr;
       if (prog == kProgAllow) {
         v = ok;
       } else if (prog < R.nprogs) {
-        const HttpProg pg = lds ? spg : HT.progs[prog];
+        HttpProg pg = spg;
+        if (!lds) pg = HT.progs[prog];
         if (pg.flags & kProgAllowAll) {
           v = ok;
           if (ok) atomicAdd(&HT.counters[2 * prog], 1ull);
@@ -2394,7 +2501,8 @@ __device__ __forceinline__ void ring_serve(const HttpDev& HT, const HttpRawDev& 
           (void)walked_len(R, P, &last);
           const uint32_t* bk = blk ? blk : HT.cells + pg.cell_begin;
           const uint8_t* lt = lut ? lut : R.codes + (size_t)prog * 256;
-          const HttpPart pt0 = lds ? spt : HT.parts[pg.part_begin];
+          HttpPart pt0 = spt;
+          if (!lds) pt0 = HT.parts[pg.part_begin];
           const uint32_t hit = lds ? walk_spans_at(HT, R, pg, pt0, (const lds_u32*)cells, (const lds_u8*)cmap, blob, a,
                                                    sp, P, last, rem[i])
                                    : walk_spans_at(HT, R, pg, pt0, bk, lt, blob, a, sp, P, last, rem[i]);
@@ -2508,8 +2616,8 @@ __global__ void ring_clock_kernel(unsigned long long* out) {
 }
 
 int launch_http_ring_impl(const HttpDev& HT, const HttpRawDev& R, const HttpRingDev& G, void* state, void* stream) {
-  const size_t lds = ring_lds_bytes(R, G.lds_cells);
-  const auto k = lds_tables_fit(R) ? http_ring_kernel<true> : http_ring_kernel<false>;
+  const size_t lds = ring_lds_bytes(R, G.lds_cells, G.lds_tabs != 0);
+  const auto k = G.lds_tabs ? http_ring_kernel<true> : http_ring_kernel<false>;
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(k, dim3(G.nwg), dim3(kRingThreads), lds, (hipStream_t)stream, HT, R, G, (RingState*)state);
   return (int)hipGetLastError();
@@ -2691,11 +2799,11 @@ int launch_http_raw_seal(const HttpRawDev& R, const RawLayoutDev& L, void* batch
   return (int)hipGetLastError();
 }
 
-size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells) {
+size_t ring_lds_bytes(const HttpRawDev& R, uint32_t cells, bool tabs) {
   return kRingDataMax + (size_t)std::max(R.nfields, 1u) * kRingThreads * 4 + 256 + 8 * kRingMaskWords + 256 +
-         (lds_tables_fit(R) ? (size_t)raw_tables_lds_words(R) * 4 + 12 : 0) +
-         (size_t)cells * 4;
+         (tabs ? (size_t)raw_tables_lds_words(R) * 4 + 12 : 0) + (size_t)cells * 4;
 }
+bool ring_tables_small(const HttpRawDev& R) { return lds_tables_fit(R); }
 int ring_clock(unsigned long long* d_out, void* stream) {
   hipLaunchKernelGGL(ring_clock_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_out);
   return (int)hipGetLastError();

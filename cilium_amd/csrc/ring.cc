@@ -200,9 +200,16 @@ void HttpRing::launch_locked(const std::shared_ptr<HttpSnapshot>& s) {
   uint32_t maxc = 0;
   for (const auto& pg : s->progs)
     if (!(pg.flags & kProgAllowAll) && (pg.flags & kProgRebased)) maxc = std::max(maxc, pg.cell_count);
-  const size_t base = ring_lds_bytes(s->raw, 0);
+  // the list parser's lookup tables (program lookup, name keys) go to LDS too
+  // when the largest program still fits beside them (a single-request call
+  // then reads no table from global memory), or when they are small anyway
+  G.lds_tabs = ring_tables_small(s->raw) || ring_lds_bytes(s->raw, maxc, true) <= 160 * 1024;
+  const size_t base = ring_lds_bytes(s->raw, 0, G.lds_tabs != 0);
   const uint32_t room = base < 160 * 1024 ? (uint32_t)((160 * 1024 - base) / 4) : 0u;
   G.lds_cells = std::min(maxc, room);
+  if (getenv("CILIUM_GPU_DEBUG"))
+    fprintf(stderr, "[cilium-gpu] ring launch: tables %s LDS, largest program %u cells, %u staged cells at most\n",
+            G.lds_tabs ? "in" : "not in", maxc, G.lds_cells);
   G.trace = trace_;
   {
     const char* ec = getenv("CILIUM_GPU_RING_ECHO");  // (measuring only: no verdicts are decided)
