@@ -192,7 +192,14 @@ def test_gpu_ring_varied_lists():
         el = [b"", b"\0", ok[:-1], ok, upper, ok + b":method\0GET\0", b":method\0GET\0" + ok,
               ok + b"x-a\0bad\x7fbyte\0", ok + b"x-a\0bad\nbyte\0", ok + b"x-a\0tab\there\0", ok + b"x-a\0\x80\xff\0",
               b"\0v\0" + ok, ok + b"x-big\0" + b"z" * 9_000 + b"\0", ok.replace(b"POST", b"PO\x01ST"),
-              ok.replace(b"/v1/request-landing/", b"/v1/request-landing/" + b"q" * 400), ok, ok]
+              ok.replace(b"/v1/request-landing/", b"/v1/request-landing/" + b"q" * 400),
+              # pair counts about the wave-cooperative parse's limit of 127 NULs
+              # (batch 1): 62 / 63 / 64 / 70 / 200 pairs, with the real fields
+              # last, a repeated name and a rejected byte late in the list
+              *[b"".join(b"x-p%d\0v%d\0" % (q, q) for q in range(m)) + ok for m in (59, 60, 61, 67, 197)],
+              b"".join(b"x-p%d\0v\0" % q for q in range(61)) + b":method\0GET\0" + ok,
+              b"".join(b"x-p%d\0v\0" % q for q in range(100)) + ok + b"x-late\0b\x01d\0",
+              ok, ok]
         n = len(el)
         eargs = (np.array([sw] * (n - 2) + [sw, 0xFFFFFFFF], np.uint32), np.zeros(n, np.uint8),
                  np.array([80] * (n - 2) + [8080, 80], np.uint16), np.full(n, synth.SPACESHIP_ID, np.uint32))
