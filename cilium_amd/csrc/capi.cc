@@ -31,6 +31,13 @@ namespace {
 std::mutex g_handles_mu;
 std::map<uint64_t, std::shared_ptr<Engine>> g_handles;
 uint64_t g_next_handle = 1;
+// Bumped (after the change is published) by everything that changes what a
+// ring call resolves to: cg_close, ring open / close, an HTTP policy publish.
+// cg_http_ring_verdicts keeps its handle, ring and snapshot per calling thread
+// while this is unchanged, so Envoy's workers take no lock and touch no
+// shared reference count per request.
+std::atomic<uint64_t> g_epoch{1};
+void bump_epoch() { g_epoch.fetch_add(1, std::memory_order_acq_rel); }
 
 std::shared_ptr<Engine> get(uint64_t h) {
   std::lock_guard<std::mutex> lk(g_handles_mu);
@@ -157,6 +164,7 @@ void cg_close(uint64_t h) {
     e = it->second;
     g_handles.erase(it);
   }
+  bump_epoch();
   if (e->has_gpu()) {
     (void)hipSetDevice(e->device);
     {
@@ -798,8 +806,11 @@ int cg_http_policy_update(uint64_t h, const char* json, size_t len) {
       e->set_device();
       snap->upload(*e);
     }
-    std::lock_guard<std::mutex> lk(e->mu);
-    e->http = snap;  // publish
+    {
+      std::lock_guard<std::mutex> lk(e->mu);
+      e->http = snap;  // publish
+    }
+    bump_epoch();
   });
 }
 
@@ -833,8 +844,11 @@ int cg_http_policy_import(uint64_t h, const void* buf, size_t len) {
       e->set_device();
       snap->upload(*e);
     }
-    std::lock_guard<std::mutex> lk(e->mu);
-    e->http = snap;  // publish
+    {
+      std::lock_guard<std::mutex> lk(e->mu);
+      e->http = snap;  // publish
+    }
+    bump_epoch();
   });
 }
 
@@ -1517,23 +1531,42 @@ int cg_http_ring_open(uint64_t h, uint32_t workgroups, uint32_t slots) {
     auto r = std::make_shared<HttpRing>();
     r->open(*e, workgroups, slots);
     e->ring = std::move(r);
+    bump_epoch();
   });
 }
+
+// A calling thread's handle, ring and snapshot as of epoch `epoch` (g_epoch).
+struct RingCallCache {
+  uint64_t h = 0, epoch = 0;
+  std::shared_ptr<Engine> e;
+  std::shared_ptr<HttpRing> r;
+  std::shared_ptr<HttpSnapshot> s;
+};
+thread_local RingCallCache t_ring_call;
 
 int cg_http_ring_verdicts(uint64_t h, const uint8_t* hdr_blob, const uint64_t* hdr_off, size_t n,
                           const uint32_t* policy, const uint8_t* ingress, const uint16_t* port,
                           const uint32_t* remote, uint8_t* out) {
   bool other = false;
   const int rc = guarded([&] {
-    auto e = get(h);
-    e->require_gpu();
-    std::shared_ptr<HttpRing> r;
-    {
-      std::lock_guard<std::mutex> lk(e->ring_mu);
-      r = e->ring;
+    RingCallCache& c = t_ring_call;
+    const uint64_t ep = g_epoch.load(std::memory_order_acquire);
+    if (c.h != h || c.epoch != ep || !c.e) {  // the locked lookups, once per thread and epoch
+      c = RingCallCache{};
+      auto e = get(h);
+      e->require_gpu();
+      std::shared_ptr<HttpRing> r;
+      {
+        std::lock_guard<std::mutex> lk(e->ring_mu);
+        r = e->ring;
+      }
+      if (!r) fail(CG_NOT_FOUND, "no ring open (cg_http_ring_open)");
+      auto s = http_snap(*e);
+      c = RingCallCache{h, ep, std::move(e), std::move(r), std::move(s)};
     }
-    if (!r) fail(CG_NOT_FOUND, "no ring open (cg_http_ring_open)");
-    auto s = http_snap(*e);
+    Engine* e = c.e.get();
+    HttpRing* r = c.r.get();
+    const std::shared_ptr<HttpSnapshot>& s = c.s;
     if (!n) return;
     check_offsets(hdr_off, n);
     if (!policy || !ingress || !port || !remote || !out || (hdr_off[n] != hdr_off[0] && !hdr_blob))
@@ -1572,6 +1605,7 @@ int cg_http_ring_close(uint64_t h) {
       std::lock_guard<std::mutex> lk(e->ring_mu);
       r = std::move(e->ring);
     }
+    bump_epoch();
     if (!r) fail(CG_NOT_FOUND, "no ring open (cg_http_ring_open)");
     r->close();
   });

@@ -8,7 +8,7 @@
 // Three host entries are timed, each for B in {1, 16, 256, 4096, 65536} and 1
 // and 16 submitting threads (the ring also 4 and 8):
 //   ring    cg_http_ring_verdicts: the persistent verdict ring (a resident
-//           kernel polls request slots in pinned host memory: no launch, no
+//           kernel polls request slots the host writes into device memory: no launch, no
 //           copies, no stream synchronization per call; B <= 256)
 //   fields  cg_http_verdicts_fields_host: calls of <= 1024 lists packed on
 //           the calling thread (one copy in, one launch, one copy out),
@@ -161,10 +161,17 @@ int main(int argc, char** argv) {
       fprintf(stderr, "cg_http_ring_open: %s\n", cg_last_error());
       return 2;
     }
+    // CILIUM_LAT_ONLY="B:T" times one point (e.g. a phase trace of 1:1 alone)
+    const char* only = getenv("CILIUM_LAT_ONLY");
+    size_t only_b = 0;
+    int only_t = 0;
+    if (only) sscanf(only, "%zu:%d", &only_b, &only_t);
     for (const size_t B : {(size_t)1, (size_t)16, (size_t)256, (size_t)4096, (size_t)65536}) {
       if (B > p.n || (mode == 1 && B > 256)) continue;
+      if (only && B != only_b) continue;
       for (const int threads : {1, 4, 8, 16}) {
         if (mode != 1 && (threads == 4 || threads == 8)) continue;  // (the ring's scaling only)
+        if (only && threads != only_t) continue;
         {  // warm-up (pinned buffers, workers, launch caches) outside the clock
           Result w;
           submit(h, p, mode, B, 0, 0.05, &w);
