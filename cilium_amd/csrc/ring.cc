@@ -150,8 +150,7 @@ void HttpRing::open(Engine& e, uint32_t workgroups, uint32_t slots) {
               }());
   }
   slot_st_.reset(new SlotState[slots]);
-  busy_.reset(new std::atomic<uint32_t>[workgroups]);
-  for (uint32_t i = 0; i < workgroups; ++i) busy_[i].store(0);
+  busy_.reset(new Busy[workgroups]);
   trace_ = getenv("CILIUM_GPU_RING_TRACE") != nullptr;
   if (e.debug || getenv("CILIUM_GPU_DEBUG"))
     fprintf(stderr, "[cilium-gpu] ring: %u workgroups, %u slots, request slots in %s memory\n", nwg_, nslots_,
@@ -272,9 +271,9 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
   // the home workgroup when no call is in it, else the nearest idle one (a
   // workgroup serves its slots one after another: a hot program spreads over
   // the neighbours, which then hold it too), else home, else any slot
-  if (!busy_[home].load(std::memory_order_relaxed)) try_wg(home);
+  if (!busy_[home].n.load(std::memory_order_relaxed)) try_wg(home);
   for (uint32_t d = 1; d < nwg_ && i == nslots_; ++d)
-    if (!busy_[(home + d) % nwg_].load(std::memory_order_relaxed)) try_wg((home + d) % nwg_);
+    if (!busy_[(home + d) % nwg_].n.load(std::memory_order_relaxed)) try_wg((home + d) % nwg_);
   if (i == nslots_) try_wg(home);
   for (uint32_t k = 1; i == nslots_; ++k) {
     const uint32_t c = (r + k) % nslots_;
@@ -282,7 +281,7 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     if (slot_st_[c].claimed.compare_exchange_strong(z, 1u, std::memory_order_acquire)) i = c;
     if (k % nslots_ == 0) std::this_thread::yield();
   }
-  busy_[i % nwg_].fetch_add(1, std::memory_order_relaxed);
+  busy_[i % nwg_].n.fetch_add(1, std::memory_order_relaxed);
   uint8_t* sl = req_slot(i);
   uint8_t* rp = rep_slot(i);
   uint8_t* d = sl + kRingData;
@@ -329,7 +328,7 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
       }
     }
     if (t - t0 > 5ull * 1000 * 1000 * 1000) {
-      busy_[i % nwg_].fetch_sub(1, std::memory_order_relaxed);
+      busy_[i % nwg_].n.fetch_sub(1, std::memory_order_relaxed);
       slot_st_[i].claimed.store(0, std::memory_order_release);
       fail(CG_UNKNOWN_ERROR, "ring: a call was not served within 5 s");
     }
@@ -350,7 +349,7 @@ void HttpRing::verdicts(Engine& e, const std::shared_ptr<HttpSnapshot>& s, const
     trace_sum_[c][kRingStamps] += (double)st[kRingStamps];
     ++trace_n_[c];
   }
-  busy_[i % nwg_].fetch_sub(1, std::memory_order_relaxed);
+  busy_[i % nwg_].n.fetch_sub(1, std::memory_order_relaxed);
   slot_st_[i].claimed.store(0, std::memory_order_release);
 }
 

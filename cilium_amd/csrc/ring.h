@@ -63,7 +63,13 @@ class HttpRing {
     uint32_t seq = 0;                  // under the claim
   };
   std::unique_ptr<SlotState[]> slot_st_;
-  std::unique_ptr<std::atomic<uint32_t>[]> busy_;  // per workgroup: calls in its slots (packed: scanned)
+  // per workgroup: calls in its slots, a cache line each (callers on many
+  // cores add and drop theirs on every call; a scan for an idle neighbour
+  // reads only as far as the first idle one)
+  struct alignas(64) Busy {
+    std::atomic<uint32_t> n{0};
+  };
+  std::unique_ptr<Busy[]> busy_;
   // CILIUM_GPU_RING_TRACE: per-phase device stamps summed over calls
   bool trace_ = false;
   std::mutex trace_mu_;
